@@ -1,0 +1,106 @@
+"""Seeded synthetic residue-PPI graphs.
+
+Each graph mimics one entry of a DeepRank2 residue-level PPI HDF5 file as
+``GraphDataset.load_one_graph`` sees it (reference ``deeprank2/dataset.py:883-1052``):
+
+* ``N ~ U{n_lo..n_hi}`` residues, two chains of Cα random walks (3.8 Å steps)
+  packed against each other;
+* one contact per residue pair closer than a per-graph cutoff chosen so the
+  graph has ``≈ mean_degree·N/2`` contacts (stored once, like ``_index``);
+* node features ``F = 30``: 20 one-hot residue types, 4 one-hot polarity
+  classes, 6 standard-normal continuous features;
+* edge features ``Fe = 3``: distance (Å), same_chain, covalent;
+* ``cluster0``: ``K0 ~ U{k_lo..k_hi}`` spatial clusters (k-means on positions,
+  relabelled to consecutive ids), ``cluster1 = zeros(K0)`` as in the fixtures;
+* ``y ~ U(0, 1)`` (regression) or Bernoulli (classification).
+
+Only numpy is used, so this runs anywhere ``bench.py`` runs.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+
+def _chain(rng, n, start, direction):
+    steps = rng.normal(size=(n, 3))
+    steps /= np.linalg.norm(steps, axis=1, keepdims=True)
+    # bias each chain along its own direction so the two chains face each other
+    steps = 0.55 * steps + 0.45 * direction
+    steps /= np.linalg.norm(steps, axis=1, keepdims=True)
+    return start + np.cumsum(3.8 * steps, axis=0)
+
+
+def _kmeans(rng, pos, k, iters=8):
+    n = pos.shape[0]
+    centers = pos[rng.choice(n, size=k, replace=False)]
+    lab = np.zeros(n, dtype=np.int64)
+    for _ in range(iters):
+        d = ((pos[:, None, :] - centers[None, :, :]) ** 2).sum(-1)
+        lab = d.argmin(1)
+        for c in range(k):
+            m = lab == c
+            if m.any():
+                centers[c] = pos[m].mean(0)
+    # consecutive ids in order of first appearance of each used label
+    _, lab = np.unique(lab, return_inverse=True)
+    return lab.astype(np.int64)
+
+
+def make_graph(rng, n_lo=180, n_hi=220, mean_degree=15.0, k_lo=2, k_hi=6, n_feat=30, task="regress"):
+    """One synthetic graph as a dict of numpy arrays (HDF5-entry layout)."""
+    n = int(rng.integers(n_lo, n_hi + 1))
+    na = n // 2
+    nb = n - na
+    pos_a = _chain(rng, na, np.zeros(3), np.array([1.0, 0.0, 0.0]))
+    pos_b = _chain(rng, nb, np.array([0.0, 9.0, 0.0]), np.array([1.0, 0.0, 0.0]))
+    pos = np.concatenate([pos_a, pos_b]).astype(np.float64)
+    chain = np.concatenate([np.zeros(na, np.int64), np.ones(nb, np.int64)])
+
+    iu, ju = np.triu_indices(n, k=1)
+    d = np.linalg.norm(pos[iu] - pos[ju], axis=1)
+    n_pairs = int(round(mean_degree * n / 2 * rng.uniform(0.9, 1.1)))
+    n_pairs = max(1, min(n_pairs, d.size))
+    sel = np.argpartition(d, n_pairs - 1)[:n_pairs]
+    sel.sort()
+    index = np.stack([iu[sel], ju[sel]], axis=1).astype(np.int64)
+    dist = d[sel]
+    same_chain = (chain[index[:, 0]] == chain[index[:, 1]]).astype(np.float64)
+    covalent = ((dist < 2.1) & (same_chain > 0)).astype(np.float64)
+
+    res_type = np.eye(20)[rng.integers(0, 20, size=n)]
+    polarity = np.eye(4)[rng.integers(0, 4, size=n)]
+    cont = rng.normal(size=(n, max(0, n_feat - 24)))
+    x = np.concatenate([res_type, polarity, cont], axis=1)[:, :n_feat]
+
+    k0 = int(rng.integers(k_lo, k_hi + 1))
+    k0 = min(k0, n)
+    cluster0 = _kmeans(rng, pos, k0)
+    k0u = int(cluster0.max()) + 1
+    cluster1 = np.zeros(k0u, dtype=np.int64)
+
+    y = float(rng.uniform()) if task == "regress" else float(rng.integers(0, 2))
+    return {
+        "x": x.astype(np.float32),
+        "index": index,  # [E/2, 2], each contact once (like edge_features/_index)
+        "edge_attr_half": np.stack([dist, same_chain, covalent], axis=1).astype(np.float32),
+        "pos": pos.astype(np.float32),
+        "cluster0": cluster0,
+        "cluster1": cluster1,
+        "y": np.float32(y),
+    }
+
+
+def make_dataset(n_graphs, seed=0, **kw):
+    rng = np.random.default_rng(seed)
+    return [make_graph(rng, **kw) for _ in range(n_graphs)]
+
+
+def doubled_edges(g):
+    """``edge_index`` [2, E] and ``edge_attr`` [E, Fe] exactly as
+    ``dataset.py:944-948,994-996`` build them: the stored pairs, then the same
+    pairs flipped; edge features duplicated in the same order."""
+    ind = g["index"]
+    ei = np.vstack((ind, np.flip(ind, 1))).T.copy()
+    ea = np.vstack((g["edge_attr_half"], g["edge_attr_half"]))
+    return ei, ea
