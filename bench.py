@@ -1,0 +1,222 @@
+"""Benchmark: GINet residue-PPI training step on MI355X (BASELINE.json configs[1]).
+
+One step = one mini-batch of 64 synthetic residue-PPI graphs (~200 nodes,
+~3k directed edges, 30 node features, 3 edge features) through forward,
+MSE loss, backward and Adam — the loop body of ``Trainer._epoch``
+(reference ``deeprank2/trainer.py:682-690``) — with the whole synthetic dataset
+already resident in HBM (a mini-batch is a list of graph ids).
+
+    python bench.py [--gpus N --steps K --warmup W]
+
+N>1 is launched by torch.distributed.run (one rank per GPU, RCCL): every rank
+trains on its own 64 graphs per step (weak scaling) and the gradients are
+all-reduced once per step.  Rank 0 prints one JSON line.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "deeprank-gnn-2_amd")]
+
+from deeprank2_amd.engine import GINetTrainStep  # noqa: E402
+from deeprank2_amd.neuralnets.gnn.ginet import GINet, BatchHandle  # noqa: E402
+from deeprank2_amd.store import GraphRecord, GraphStore, pack_graphs  # noqa: E402
+from deeprank2_amd.utils.synthetic import doubled_edges, make_dataset  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+B_PER_GPU = 64
+
+
+def records(graphs):
+    out = []
+    for i, g in enumerate(graphs):
+        ei, ea = doubled_edges(g)
+        out.append(GraphRecord(x=g["x"], edge_index=ei, edge_attr=ea, cluster0=g["cluster0"], cluster1=g["cluster1"], y=float(g["y"]), pos=g["pos"], name=f"syn{i}"))
+    return out
+
+
+def algorithmic_bytes(packed, gids):
+    """Bytes one graph pass must move for these graphs:
+    reads x (4NF), CSR (4(N+1)+4E), depth-0 members (4(K0+1)+4N), pooled CSR
+    (4(K0+1)+4P1), depth-1 members (4(K1+1)+4K0), y (4); writes the per-graph
+    weight-gradient slab 4(32F+1024) and head vectors 4*324."""
+    n, e, k0, p1, k1 = (a[gids] for a in packed.sizes())
+    f = packed.n_feat
+    per = 4 * n * f + 4 * (n + 1) + 4 * e + 4 * (k0 + 1) + 4 * n + 4 * (k0 + 1) + 4 * p1 + 4 * (k1 + 1) + 4 * k0 + 4
+    per = per + 4 * (32 * f + 1024) + 4 * 324
+    return int(per.sum())
+
+
+def cpu_baseline(graphs, budget_s=15.0, max_steps=60):
+    """The CPU oracle (op-for-op restatement of the reference, torch CPU) training
+    the same batch: forward, MSE, backward, Adam — on this host's cores."""
+    from oracle import data_ref, gnn_ref  # noqa: PLC0415
+    from oracle import pyg_ops as P  # noqa: PLC0415
+
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, 16))
+    torch.set_num_threads(cores)
+    datas = [data_ref.synthetic_to_data(g) for g in graphs]
+    torch.manual_seed(1234)
+    model = gnn_ref.GINet(30, 1, 3).train()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-5)
+
+    def one():
+        bat = P.Batch.from_data_list([d.clone() for d in datas])
+        opt.zero_grad()
+        out = model(bat)
+        loss = torch.nn.functional.mse_loss(out.reshape(-1), bat.y)
+        loss.backward()
+        opt.step()
+
+    for _ in range(2):
+        one()
+    t0 = time.perf_counter()
+    n = 0
+    while n < max_steps and time.perf_counter() - t0 < budget_s:
+        one()
+        n += 1
+    dt = (time.perf_counter() - t0) / n
+    return {"value": round(len(graphs) / dt, 2), "unit": "graphs/s", "cores": cores, "kind": "port", "sample": f"{n} GINet(30,1,3) train steps (fwd+MSE+bwd+Adam) on one batch of {len(graphs)} of the same synthetic graphs; oracle/gnn_ref.py on torch CPU, {cores} threads; {dt * 1e3:.1f} ms/step"}
+
+
+def main():  # noqa: PLR0915
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batches", type=int, default=16, help="resident mini-batches per rank (64 graphs each)")
+    ap.add_argument("--batch", type=int, default=B_PER_GPU)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    pg = None
+    if world > 1:
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        pg = torch.distributed.group.WORLD
+    dev = torch.device(f"cuda:{local}")
+
+    B = args.batch
+    graphs = make_dataset(B * args.batches, seed=1000 + rank)
+    packed = pack_graphs(records(graphs))
+    store = GraphStore(packed, dev)
+    order = np.random.default_rng(rank).permutation(packed.n_graphs).astype(np.int32)
+    handles = [BatchHandle(store, order[i * B:(i + 1) * B]) for i in range(args.batches)]
+
+    torch.manual_seed(1234)
+    model = GINet(30, 1, 3).to(dev).train()
+    if pg is not None:
+        for p in model.parameters():
+            torch.distributed.broadcast(p.data, 0)
+    step = GINetTrainStep(model, lr=1e-3, weight_decay=1e-5, loss="mse", process_group=pg)
+    gen = torch.Generator(device=dev).manual_seed(77 + rank)
+
+    def run(i):
+        h = handles[i % len(handles)]
+        mask = model.dropout_mask(h.B, dev, generator=gen)
+        return step.step(h, mask=mask, global_batch=B * world)
+
+    for i in range(args.warmup):
+        run(i)
+    torch.cuda.synchronize()
+    if pg is not None:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    step.kernel_events = []
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss, _ = run(args.warmup + i)
+    torch.cuda.synchronize()
+    if pg is not None:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kms = [a.elapsed_time(b) for a, b in step.kernel_events]
+    step.kernel_events = None
+    kernel_ms = float(np.mean(kms))
+    if pg is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+        km = torch.tensor([kernel_ms], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(km, op=torch.distributed.ReduceOp.MAX)
+        kernel_ms = float(km.item())
+
+    graphs_total = B * world * args.steps
+    edges_local = sum(store.edges_in(handles[(args.warmup + i) % len(handles)].gids_host) for i in range(args.steps))
+    et = torch.tensor([float(edges_local)], dtype=torch.float64, device=dev)
+    if pg is not None:
+        torch.distributed.all_reduce(et)
+    edges_total = float(et.item())
+    alg = np.mean([algorithmic_bytes(packed, h.gids_host) for h in handles])
+    achieved = alg / (kernel_ms * 1e-3) / 1e9
+
+    result = None
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(graphs[:B])
+        result = {
+            "metric": "graphs/sec per training step, GINet residue-PPI (fwd+MSE+bwd+Adam)",
+            "value": round(graphs_total / elapsed, 1),
+            "unit": "graphs/s",
+            "edges_per_sec": round(edges_total / elapsed, 1),
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded residue-PPI graphs per SURVEY §8(d); random-init GINet(30,1,3))",
+            "config": {
+                "workload": "GINet residue-PPI training step, BASELINE.json configs[1]",
+                "graphs_per_gpu": B,
+                "global_batch": B * world,
+                "mean_nodes_per_graph": round(float(np.diff(packed.node_off).mean()), 1),
+                "mean_edges_per_graph": round(float(np.diff(packed.edge_off).mean()), 1),
+                "node_features": 30,
+                "edge_features": 3,
+                "resident_graphs_per_gpu": packed.n_graphs,
+                "parallelism": f"dp{world}",
+            },
+            "roofline": {
+                "kernel": "ginet_graph_kernel (dr_ginet_graph_pass, fwd+loss+bwd, 1 workgroup/graph)",
+                "bound": "hbm",
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "traffic": None,
+                "algorithmic_bytes_per_launch": int(alg),
+                "kernel_ms_avg": round(kernel_ms, 5),
+            },
+            "cpu_baseline": cpu,
+            "final_loss": float(loss.item()),
+        }
+        print(json.dumps(result), flush=True)
+    if pg is not None:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+    return result
+
+
+if __name__ == "__main__":
+    main()

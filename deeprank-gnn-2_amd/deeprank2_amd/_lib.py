@@ -1,0 +1,163 @@
+"""ctypes binding of the C ABI declared in ``include/deeprank2_amd.h``.
+
+The shared library ``libdeeprank2_amd.so`` is built in-tree (``make -C
+deeprank-gnn-2_amd/csrc`` or ``__graft_entry__.build()``).  There is no CPU
+fallback: if the library is missing, or a compute entry is called with
+non-device tensors, an error is raised.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdeeprank2_amd.so")
+
+DR_PASS_FORWARD = 1
+DR_PASS_BACKWARD = 2
+DR_LOSS_NONE = 0
+DR_LOSS_MSE = 1
+DR_LOSS_CE = 2
+DR_MAX_OUT = 16
+DR_GINET_NPARAM = 16
+
+ERRORS = {-1: "bad argument", -2: "graph does not fit the per-graph LDS kernel", -3: "unsupported configuration"}
+
+_c_f = ctypes.POINTER(ctypes.c_float)
+_c_i32 = ctypes.POINTER(ctypes.c_int32)
+_c_i64 = ctypes.POINTER(ctypes.c_int64)
+_c_u8 = ctypes.POINTER(ctypes.c_uint8)
+VP = ctypes.c_void_p
+
+
+class GraphStoreC(ctypes.Structure):
+    _fields_ = [
+        ("n_graphs", ctypes.c_int32),
+        ("n_feat", ctypes.c_int32),
+        ("transpose_aliased", ctypes.c_int32),
+        ("pad0", ctypes.c_int32),
+        ("x", VP),
+        ("node_off", VP),
+        ("edge_off", VP),
+        ("rowptr", VP),
+        ("col", VP),
+        ("t_rowptr", VP),
+        ("t_col", VP),
+        ("k0_off", VP),
+        ("m0_ptr", VP),
+        ("m0_idx", VP),
+        ("p1_off", VP),
+        ("p1_rowptr", VP),
+        ("p1_col", VP),
+        ("p1t_rowptr", VP),
+        ("p1t_col", VP),
+        ("k1_off", VP),
+        ("m1_ptr", VP),
+        ("m1_idx", VP),
+        ("y", VP),
+    ]
+
+
+class GinetWeightsC(ctypes.Structure):
+    _fields_ = [(n, VP) for n in ("w1", "w1e", "w2", "w2e", "fc1w", "fc1b", "fc2w", "fc2b")]
+
+
+class GinetPassC(ctypes.Structure):
+    _fields_ = [
+        ("flags", ctypes.c_int32),
+        ("out_dim", ctypes.c_int32),
+        ("loss_kind", ctypes.c_int32),
+        ("use_dropout", ctypes.c_int32),
+        ("drop_scale", ctypes.c_float),
+        ("loss_scale", ctypes.c_float),
+        ("mask", VP),
+        ("class_w", VP),
+        ("out", VP),
+        ("dout", VP),
+        ("loss_per_graph", VP),
+        ("slab", VP),
+        ("head", VP),
+    ]
+
+
+class AdamC(ctypes.Structure):
+    _fields_ = [
+        ("lr", ctypes.c_float),
+        ("beta1", ctypes.c_float),
+        ("beta2", ctypes.c_float),
+        ("eps", ctypes.c_float),
+        ("weight_decay", ctypes.c_float),
+        ("bias_c1", ctypes.c_float),
+        ("bias_c2_sqrt", ctypes.c_float),
+        ("enabled", ctypes.c_int32),
+    ]
+
+
+class ParamTableC(ctypes.Structure):
+    _fields_ = [
+        ("param", VP * DR_GINET_NPARAM),
+        ("grad", VP * DR_GINET_NPARAM),
+        ("exp_avg", VP * DR_GINET_NPARAM),
+        ("exp_avg_sq", VP * DR_GINET_NPARAM),
+        ("numel", ctypes.c_int32 * DR_GINET_NPARAM),
+    ]
+
+
+# (name, restype, argtypes) for every entry of include/deeprank2_amd.h
+SIGNATURES = [
+    ("dr_ginet_graph_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(GinetWeightsC), ctypes.POINTER(GinetPassC), ctypes.c_int32, VP]),
+    ("dr_ginet_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 7),
+    ("dr_ginet_reduce_update", ctypes.c_int, [ctypes.POINTER(ParamTableC), ctypes.c_int32, ctypes.c_int32, VP, VP, ctypes.c_int32, ctypes.POINTER(AdamC), VP, ctypes.c_float, VP, VP]),
+    ("dr_csr_from_coo", ctypes.c_int, [VP, VP, ctypes.c_int64, ctypes.c_int32, VP, VP, VP, VP, VP]),
+    ("dr_spmm_csr", ctypes.c_int, [VP, VP, VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP, VP]),
+    ("dr_linear_xwT", ctypes.c_int, [VP, VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP, VP]),
+    ("dr_linear_xw", ctypes.c_int, [VP, VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP, VP]),
+    ("dr_linear_dw", ctypes.c_int, [VP, VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP, VP, ctypes.c_int32, VP]),
+    ("dr_version", ctypes.c_char_p, []),
+    ("dr_device_arch", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32]),
+]
+
+_LIB = None
+
+
+def load():
+    """Load the in-tree library (raises if it has not been built)."""
+    global _LIB  # noqa: PLW0603
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        msg = f"{LIB_PATH} is missing: build it with `make -C deeprank-gnn-2_amd/csrc` (or __graft_entry__.build()). There is no CPU fallback."
+        raise RuntimeError(msg)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = f"{what} failed: {ERRORS.get(rc, f'hip error {rc}')}"
+        raise RuntimeError(msg)
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_ptr(device) -> int:
+    import torch  # noqa: PLC0415
+
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_device(*tensors) -> None:
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            msg = "deeprank2_amd kernels run on the MI355X only: got a CPU tensor (no CPU fallback by design)"
+            raise RuntimeError(msg)

@@ -1,0 +1,75 @@
+"""Thin torch-facing wrappers over the C ABI (device tensors in, device tensors out).
+
+Each wrapper checks shapes/dtypes/devices, preallocates outputs with torch's
+caching allocator, launches on the current stream and converts a non-zero
+status into ``RuntimeError``.  No wrapper has a CPU path.
+"""
+
+from __future__ import annotations
+
+import torch
+
+from deeprank2_amd import _lib
+
+
+def _f32(t, name):
+    if t.dtype != torch.float32:
+        msg = f"{name} must be float32 (got {t.dtype})"
+        raise TypeError(msg)
+    return t.contiguous()
+
+
+def csr_from_coo(row: torch.Tensor, col: torch.Tensor, n_rows: int):
+    """Stable CSR of (row, col) sorted by row -> (rowptr int32 [n+1], perm int32 [E], col int32 [E])."""
+    _lib.require_device(row, col)
+    lib = _lib.load()
+    row = row.to(torch.int64).contiguous()
+    col = col.to(torch.int64).contiguous()
+    e = row.numel()
+    dev = row.device
+    rowptr = torch.empty(n_rows + 1, dtype=torch.int32, device=dev)
+    perm = torch.empty(max(e, 1), dtype=torch.int32, device=dev)
+    col_s = torch.empty(max(e, 1), dtype=torch.int32, device=dev)
+    scratch = torch.empty(n_rows + 1, dtype=torch.int32, device=dev)
+    _lib.check(lib.dr_csr_from_coo(row.data_ptr(), col.data_ptr(), e, n_rows, rowptr.data_ptr(), perm.data_ptr(), col_s.data_ptr(), scratch.data_ptr(), _lib.stream_ptr(dev)), "dr_csr_from_coo")
+    return rowptr, perm[:e], col_s[:e]
+
+
+def spmm_csr(rowptr, col, y, n_rows, relu=False):
+    _lib.require_device(rowptr, col, y)
+    y = _f32(y, "y")
+    out = torch.empty(n_rows, y.shape[1], dtype=torch.float32, device=y.device)
+    _lib.check(_lib.load().dr_spmm_csr(rowptr.data_ptr(), col.data_ptr(), y.data_ptr(), n_rows, y.shape[1], int(relu), out.data_ptr(), _lib.stream_ptr(y.device)), "dr_spmm_csr")
+    return out
+
+
+def linear_xwT(x, w):
+    _lib.require_device(x, w)
+    x, w = _f32(x, "x"), _f32(w, "weight")
+    m, k = x.shape
+    n = w.shape[0]
+    y = torch.empty(m, n, dtype=torch.float32, device=x.device)
+    _lib.check(_lib.load().dr_linear_xwT(x.data_ptr(), w.data_ptr(), m, k, n, y.data_ptr(), _lib.stream_ptr(x.device)), "dr_linear_xwT")
+    return y
+
+
+def linear_xw(dy, w):
+    _lib.require_device(dy, w)
+    dy, w = _f32(dy, "dy"), _f32(w, "weight")
+    m, n = dy.shape
+    k = w.shape[1]
+    dx = torch.empty(m, k, dtype=torch.float32, device=dy.device)
+    _lib.check(_lib.load().dr_linear_xw(dy.data_ptr(), w.data_ptr(), m, n, k, dx.data_ptr(), _lib.stream_ptr(dy.device)), "dr_linear_xw")
+    return dx
+
+
+def linear_dw(dy, x):
+    _lib.require_device(dy, x)
+    dy, x = _f32(dy, "dy"), _f32(x, "x")
+    m, n = dy.shape
+    k = x.shape[1]
+    n_split = max(1, min(64, m // 256))
+    dw = torch.empty(n, k, dtype=torch.float32, device=dy.device)
+    scratch = torch.empty(n_split * n * k, dtype=torch.float32, device=dy.device)
+    _lib.check(_lib.load().dr_linear_dw(dy.data_ptr(), x.data_ptr(), m, n, k, dw.data_ptr(), scratch.data_ptr(), n_split, _lib.stream_ptr(dy.device)), "dr_linear_dw")
+    return dw

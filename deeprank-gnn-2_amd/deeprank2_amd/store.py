@@ -1,0 +1,362 @@
+"""Packed, HBM-resident graph store: the data layout every kernel reads.
+
+A DeepRank2 batch goes through ``GraphDataset.load_one_graph`` (reference
+``deeprank2/dataset.py:883-1052``), the PyG ``Collater`` (``trainer.py:541``),
+then, inside every forward, ``get_preloaded_cluster`` + ``consecutive_cluster``
++ ``pool_edge`` (``community_pooling.py:23-27,205-212``) and PyG's
+``max_pool_x`` (``ginet.py:102-103``).  All of that index work is a pure
+function of each graph's static ``edge_index``/``cluster0``/``cluster1``, so it
+is done ONCE per graph here, and a mini-batch becomes a list of graph ids:
+
+* CSR by ``edge_index[0]`` (the scatter index of ``ginet.py:58``), stable, so
+  each row sums its edges in the same order as ``scatter_add_`` on the CPU;
+  its transpose (aliased when the graph is symmetric, which
+  ``load_one_graph``'s doubled edges always are);
+* depth-0 clusters relabelled densely per graph (what the per-batch offset +
+  ``consecutive_cluster`` produce, graph by graph) with member lists in
+  ascending node order (torch_scatter ``scatter_max`` keeps the first max);
+* the pooled graph of ``pool_edge`` (relabel, drop self loops, coalesce ->
+  unique pairs sorted by (row, col)) as a CSR, and its transpose;
+* depth-1 clusters relabelled densely with member lists.
+
+Per graph the index arrays use local int32 ids; offsets are int64.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+
+@dataclass
+class GraphRecord:
+    """One graph as ``load_one_graph`` returns it (numpy)."""
+
+    x: np.ndarray  # [N, F] float32
+    edge_index: np.ndarray  # [2, E] int64 (doubled: both directions)
+    edge_attr: np.ndarray | None = None  # [E, Fe] float32
+    cluster0: np.ndarray | None = None  # [N] int64
+    cluster1: np.ndarray | None = None  # [K0] int64
+    y: float | None = None
+    pos: np.ndarray | None = None
+    name: str = ""
+
+
+@dataclass
+class PackedGraphs:
+    n_feat: int
+    n_graphs: int
+    x: np.ndarray
+    node_off: np.ndarray
+    edge_off: np.ndarray
+    rowptr: np.ndarray
+    col: np.ndarray
+    eperm: np.ndarray  # CSR slot -> original edge position within the graph
+    t_rowptr: np.ndarray
+    t_col: np.ndarray
+    transpose_aliased: bool
+    k0_off: np.ndarray
+    m0_ptr: np.ndarray
+    m0_idx: np.ndarray
+    cl0: np.ndarray  # [N_all] dense depth-0 id per node
+    p1_off: np.ndarray
+    p1_rowptr: np.ndarray
+    p1_col: np.ndarray
+    p1t_rowptr: np.ndarray
+    p1t_col: np.ndarray
+    k1_off: np.ndarray
+    m1_ptr: np.ndarray
+    m1_idx: np.ndarray
+    cl1: np.ndarray
+    y: np.ndarray
+    edge_attr: np.ndarray | None  # [E_all, Fe] in CSR order
+    names: list = field(default_factory=list)
+
+    # per-graph sizes (host side, for launch geometry)
+    def sizes(self):
+        n = np.diff(self.node_off)
+        e = np.diff(self.edge_off)
+        k0 = np.diff(self.k0_off)
+        p1 = np.diff(self.p1_off)
+        k1 = np.diff(self.k1_off)
+        return n, e, k0, p1, k1
+
+
+def _csr(rows, cols, n):
+    perm = np.argsort(rows, kind="stable")
+    rowptr = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(np.bincount(rows, minlength=n), out=rowptr[1:])
+    return rowptr.astype(np.int32), cols[perm].astype(np.int32), perm.astype(np.int32)
+
+
+def _same_multiset(r1, c1, r2, c2, n):
+    if r1.size != r2.size:
+        return False
+    a = np.sort(r1.astype(np.int64) * n + c1)
+    b = np.sort(r2.astype(np.int64) * n + c2)
+    return bool(np.array_equal(a, b))
+
+
+def _dense(ids, what):
+    ids = np.asarray(ids, dtype=np.int64)
+    if ids.size and ids.min() < 0:
+        msg = f"{what} ids must be non-negative (get_preloaded_cluster offsets assume it)"
+        raise ValueError(msg)
+    uniq, inv = np.unique(ids, return_inverse=True)
+    return inv.astype(np.int64), int(uniq.size)
+
+
+def pack_graphs(records: list[GraphRecord], require_clusters: bool = True) -> PackedGraphs:  # noqa: PLR0915, C901
+    if not records:
+        msg = "empty graph list"
+        raise ValueError(msg)
+    F = int(records[0].x.shape[1])
+    xs, rps, cols, eperms, trps, tcols = [], [], [], [], [], []
+    m0ps, m0is, cl0s, p1rps, p1cs, p1trps, p1tcs, m1ps, m1is, cl1s, ys, eas = ([] for _ in range(12))
+    node_off = [0]
+    edge_off = [0]
+    k0_off = [0]
+    p1_off = [0]
+    k1_off = [0]
+    aliased = True
+    has_ea = records[0].edge_attr is not None
+    for gi, r in enumerate(records):
+        x = np.ascontiguousarray(r.x, dtype=np.float32)
+        if x.ndim != 2 or x.shape[1] != F:
+            msg = f"graph {gi}: x must be [N, {F}]"
+            raise ValueError(msg)
+        n = x.shape[0]
+        if n == 0:
+            msg = f"graph {gi} has no nodes (torch.max over an empty cluster would fail in the reference)"
+            raise ValueError(msg)
+        ei = np.asarray(r.edge_index, dtype=np.int64).reshape(2, -1)
+        e = ei.shape[1]
+        if e and (ei.min() < 0 or ei.max() >= n):
+            msg = f"graph {gi}: edge_index out of range [0, {n})"
+            raise ValueError(msg)
+        row, col = ei[0], ei[1]
+        rp, cs, perm = _csr(row, col, n)
+        trp, tcs, _ = _csr(col, row, n)
+        sym = _same_multiset(row, col, col, row, n)
+        aliased &= sym
+        xs.append(x)
+        rps.append(rp)
+        cols.append(cs)
+        eperms.append(perm)
+        trps.append(trp)
+        tcols.append(tcs)
+        if has_ea:
+            ea = np.asarray(r.edge_attr, dtype=np.float32).reshape(e, -1)
+            eas.append(ea[perm])
+
+        if r.cluster0 is None or r.cluster1 is None:
+            if require_clusters:
+                msg = f"graph {gi} ({r.name}) has no cluster0/cluster1 (set clustering_method when building the dataset)"
+                raise ValueError(msg)
+            c0 = np.zeros(n, dtype=np.int64)
+            c1 = np.zeros(1, dtype=np.int64)
+        else:
+            c0, c1 = r.cluster0, r.cluster1
+        if len(c0) != n:
+            msg = f"graph {gi}: cluster0 has {len(c0)} entries for {n} nodes"
+            raise ValueError(msg)
+        d0, k0 = _dense(c0, "cluster0")
+        m0i = np.argsort(d0, kind="stable").astype(np.int32)
+        m0p = np.zeros(k0 + 1, dtype=np.int32)
+        np.cumsum(np.bincount(d0, minlength=k0), out=m0p[1:])
+        # pool_edge: relabel, remove self loops, coalesce (unique, sorted by (row, col))
+        pr, pc = d0[row], d0[col]
+        keep = pr != pc
+        key = np.unique(pr[keep] * k0 + pc[keep])
+        prow, pcol = key // k0, key % k0
+        p1rp = np.zeros(k0 + 1, dtype=np.int32)
+        np.cumsum(np.bincount(prow, minlength=k0), out=p1rp[1:])
+        tkey = np.unique(pcol * k0 + prow)
+        p1trp = np.zeros(k0 + 1, dtype=np.int32)
+        np.cumsum(np.bincount(tkey // k0, minlength=k0), out=p1trp[1:])
+
+        c1 = np.asarray(c1, dtype=np.int64).reshape(-1)
+        if len(c1) != k0:
+            msg = f"graph {gi}: cluster1 has {len(c1)} entries but cluster0 defines {k0} clusters"
+            raise ValueError(msg)
+        d1, k1 = _dense(c1, "cluster1")
+        m1i = np.argsort(d1, kind="stable").astype(np.int32)
+        m1p = np.zeros(k1 + 1, dtype=np.int32)
+        np.cumsum(np.bincount(d1, minlength=k1), out=m1p[1:])
+
+        m0ps.append(m0p)
+        m0is.append(m0i)
+        cl0s.append(d0.astype(np.int32))
+        p1rps.append(p1rp)
+        p1cs.append(pcol.astype(np.int32))
+        p1trps.append(p1trp)
+        p1tcs.append((tkey % k0).astype(np.int32))
+        m1ps.append(m1p)
+        m1is.append(m1i)
+        cl1s.append(d1.astype(np.int32))
+        ys.append(np.nan if r.y is None else float(np.asarray(r.y).reshape(-1)[0]))
+        node_off.append(node_off[-1] + n)
+        edge_off.append(edge_off[-1] + e)
+        k0_off.append(k0_off[-1] + k0)
+        p1_off.append(p1_off[-1] + prow.size)
+        k1_off.append(k1_off[-1] + k1)
+
+    cat = np.concatenate
+    return PackedGraphs(
+        n_feat=F,
+        n_graphs=len(records),
+        x=cat(xs),
+        node_off=np.asarray(node_off, np.int64),
+        edge_off=np.asarray(edge_off, np.int64),
+        rowptr=cat(rps),
+        col=cat(cols),
+        eperm=cat(eperms),
+        t_rowptr=cat(trps),
+        t_col=cat(tcols),
+        transpose_aliased=bool(aliased),
+        k0_off=np.asarray(k0_off, np.int64),
+        m0_ptr=cat(m0ps),
+        m0_idx=cat(m0is),
+        cl0=cat(cl0s),
+        p1_off=np.asarray(p1_off, np.int64),
+        p1_rowptr=cat(p1rps),
+        p1_col=cat(p1cs) if p1cs else np.zeros(0, np.int32),
+        p1t_rowptr=cat(p1trps),
+        p1t_col=cat(p1tcs) if p1tcs else np.zeros(0, np.int32),
+        k1_off=np.asarray(k1_off, np.int64),
+        m1_ptr=cat(m1ps),
+        m1_idx=cat(m1is),
+        cl1=cat(cl1s),
+        y=np.asarray(ys, dtype=np.float32),
+        edge_attr=cat(eas) if has_ea else None,
+        names=[r.name for r in records],
+    )
+
+
+def records_from_batch(batch) -> list[GraphRecord]:
+    """Split a collated PyG-style batch (x, edge_index, batch/ptr, cluster0,
+    cluster1, edge_attr, y) back into per-graph records (host side)."""
+    import torch  # noqa: PLC0415
+
+    def np_(t):
+        return None if t is None else (t.detach().cpu().numpy() if isinstance(t, torch.Tensor) else np.asarray(t))
+
+    x = np_(batch.x)
+    ei = np_(batch.edge_index)
+    ea = np_(getattr(batch, "edge_attr", None))
+    bvec = np_(getattr(batch, "batch", None))
+    if bvec is None:
+        bvec = np.zeros(x.shape[0], dtype=np.int64)
+    n_graphs = int(bvec.max()) + 1 if bvec.size else 0
+    counts = np.bincount(bvec, minlength=n_graphs)
+    if not np.all(np.diff(bvec) >= 0):
+        msg = "batch vector must be sorted (PyG collate order)"
+        raise ValueError(msg)
+    ptr = np.concatenate([[0], np.cumsum(counts)])
+    c0 = np_(getattr(batch, "cluster0", None))
+    c1 = np_(getattr(batch, "cluster1", None))
+    y = np_(getattr(batch, "y", None))
+    names = getattr(batch, "entry_names", None)
+    eg = bvec[ei[0]] if ei.size else np.zeros(0, np.int64)
+    if ei.size and not np.array_equal(eg, bvec[ei[1]]):
+        msg = "edges must not cross graphs"
+        raise ValueError(msg)
+    eorder = np.argsort(eg, kind="stable")
+    ecount = np.bincount(eg, minlength=n_graphs)
+    eptr = np.concatenate([[0], np.cumsum(ecount)])
+    # cluster1 belongs to depth-0 clusters; split it by each graph's cluster count
+    k0s = [len(np.unique(c0[ptr[g]:ptr[g + 1]])) for g in range(n_graphs)] if c0 is not None else None
+    kptr = np.concatenate([[0], np.cumsum(k0s)]) if k0s is not None else None
+    recs = []
+    for g in range(n_graphs):
+        sl = slice(ptr[g], ptr[g + 1])
+        es = eorder[eptr[g]:eptr[g + 1]]
+        recs.append(
+            GraphRecord(
+                x=x[sl],
+                edge_index=ei[:, es] - ptr[g],
+                edge_attr=None if ea is None else ea[es],
+                cluster0=None if c0 is None else c0[sl],
+                cluster1=None if (c1 is None or kptr is None) else c1[kptr[g]:kptr[g + 1]],
+                y=None if y is None or y.size <= g else float(y.reshape(-1)[g]),
+                name=names[g] if isinstance(names, list) and g < len(names) else f"g{g}",
+            ),
+        )
+    return recs
+
+
+class GraphStore:
+    """Device copy of a :class:`PackedGraphs` (all arrays live in HBM)."""
+
+    def __init__(self, packed: PackedGraphs, device):
+        import torch  # noqa: PLC0415
+
+        self.packed = packed
+        self.device = torch.device(device)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(self.device)  # noqa: E731
+        p = packed
+        self.x = t(p.x)
+        self.node_off = t(p.node_off)
+        self.edge_off = t(p.edge_off)
+        self.rowptr = t(p.rowptr)
+        self.col = t(p.col)
+        if p.transpose_aliased:
+            self.t_rowptr, self.t_col = self.rowptr, self.col
+        else:
+            self.t_rowptr, self.t_col = t(p.t_rowptr), t(p.t_col)
+        self.k0_off = t(p.k0_off)
+        self.m0_ptr = t(p.m0_ptr)
+        self.m0_idx = t(p.m0_idx)
+        self.p1_off = t(p.p1_off)
+        self.p1_rowptr = t(p.p1_rowptr)
+        self.p1_col = t(p.p1_col if p.p1_col.size else np.zeros(1, np.int32))
+        if p.transpose_aliased:
+            self.p1t_rowptr, self.p1t_col = self.p1_rowptr, self.p1_col
+        else:
+            self.p1t_rowptr = t(p.p1t_rowptr)
+            self.p1t_col = t(p.p1t_col if p.p1t_col.size else np.zeros(1, np.int32))
+        self.k1_off = t(p.k1_off)
+        self.m1_ptr = t(p.m1_ptr)
+        self.m1_idx = t(p.m1_idx)
+        self.y = t(p.y)
+        self.edge_attr = None if p.edge_attr is None else t(p.edge_attr)
+        self._sizes = p.sizes()
+        self._c = None
+
+    @property
+    def n_graphs(self):
+        return self.packed.n_graphs
+
+    @property
+    def n_feat(self):
+        return self.packed.n_feat
+
+    def set_targets(self, y):
+        """Replace the per-graph targets (e.g. class indices for CE)."""
+        import torch  # noqa: PLC0415
+
+        self.y = torch.as_tensor(np.asarray(y, np.float32)).to(self.device)
+        self._c = None
+
+    def cstruct(self):
+        from deeprank2_amd import _lib  # noqa: PLC0415
+
+        if self._c is None:
+            s = _lib.GraphStoreC()
+            s.n_graphs = self.n_graphs
+            s.n_feat = self.n_feat
+            s.transpose_aliased = int(self.packed.transpose_aliased)
+            for name in ("x", "node_off", "edge_off", "rowptr", "col", "t_rowptr", "t_col", "k0_off", "m0_ptr", "m0_idx", "p1_off", "p1_rowptr", "p1_col", "p1t_rowptr", "p1t_col", "k1_off", "m1_ptr", "m1_idx", "y"):
+                setattr(s, name, getattr(self, name).data_ptr())
+            self._c = s
+        return self._c
+
+    def max_sizes(self, gids_host):
+        n, e, k0, p1, k1 = self._sizes
+        g = np.asarray(gids_host, dtype=np.int64)
+        return int(n[g].max()), int(e[g].max()), int(k0[g].max()), int(p1[g].max()), int(k1[g].max())
+
+    def edges_in(self, gids_host):
+        n, e, *_ = self._sizes
+        return int(e[np.asarray(gids_host, dtype=np.int64)].sum())

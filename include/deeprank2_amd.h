@@ -1,0 +1,191 @@
+/*
+ * deeprank2_amd — C ABI of the MI355X (gfx950) GNN hot path for DeepRank2.
+ *
+ * Everything here is plain C: device pointers, sizes, a hipStream_t passed as
+ * void*.  No torch types cross this boundary.  The library never allocates or
+ * frees caller memory; every output is preallocated by the caller.  Every
+ * entry returns 0 on success or a hipError_t / negative DR_E* code; no
+ * exception crosses the ABI.  Launches go on the caller's stream and no entry
+ * synchronises the host, so every call is capturable in a hipGraph.
+ *
+ * Reference interface each entry replaces (paths relative to the reference
+ * repo deeprank2 v3.1.0):
+ *
+ *   dr_ginet_graph_pass     GINet.forward + autograd backward
+ *                           (deeprank2/neuralnets/gnn/ginet.py:90-125, with the
+ *                           GINetConvLayer of ginet.py:40-60 and
+ *                           community_pooling / get_preloaded_cluster of
+ *                           deeprank2/utils/community_pooling.py:23-27,165-242),
+ *                           plus the loss gradient of Trainer._epoch
+ *                           (deeprank2/trainer.py:686-689)
+ *   dr_ginet_reduce_update  loss_.backward() parameter-gradient reduction and
+ *                           optimizer.step() of Trainer._epoch
+ *                           (trainer.py:689-690; torch.optim.Adam configured at
+ *                           trainer.py:419)
+ *   dr_spmm_csr             torch_scatter.scatter_sum(h, row, out=zeros) over
+ *                           gathered rows (ginet.py:45,55-58; vanilla_gnn.py:35)
+ *   dr_linear_xwT / dr_linear_xw / dr_linear_dw
+ *                           the node-side nn.Linear(bias=False) of
+ *                           GINetConvLayer.fc (ginet.py:45) and its backward
+ *   dr_csr_from_coo         the ordering torch_scatter's CPU scatter_add_
+ *                           implies for edge_index[0] (ginet.py:41,58): a stable
+ *                           row-sorted CSR, built on the device
+ */
+#ifndef DEEPRANK2_AMD_H
+#define DEEPRANK2_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DR_OK 0
+#define DR_E_ARG (-1)       /* bad argument (null pointer, negative size ...) */
+#define DR_E_LDS (-2)       /* a graph does not fit the per-graph LDS kernel  */
+#define DR_E_UNSUPPORTED (-3)
+
+/* ------------------------------------------------------------------------
+ * Packed graph store (HBM-resident).  "local" = index relative to the graph.
+ * G graphs; N_all nodes; E_all directed edges (edge_index columns); K0_all
+ * depth-0 (pooled) nodes; K1_all depth-1 clusters; P1_all pooled edges.
+ * Per graph g the CSR is sorted by edge_index[0] (the scatter index of
+ * ginet.py:58) and keeps the original edge order inside a row.
+ * ---------------------------------------------------------------------- */
+typedef struct dr_graph_store {
+  int32_t n_graphs;          /* G                                             */
+  int32_t n_feat;            /* F (row stride of x)                           */
+  int32_t transpose_aliased; /* 1: t_* arrays are the CSR arrays (symmetric)  */
+  int32_t pad0;
+  const float* x;            /* [N_all, F] fp32                               */
+  const int64_t* node_off;   /* [G+1]                                         */
+  const int64_t* edge_off;   /* [G+1]                                         */
+  const int32_t* rowptr;     /* [N_all+G] local CSR row pointers (g at node_off[g]+g) */
+  const int32_t* col;        /* [E_all]   local gathered node (edge_index[1]) */
+  const int32_t* t_rowptr;   /* transpose CSR (by edge_index[1])              */
+  const int32_t* t_col;
+  const int64_t* k0_off;     /* [G+1] depth-0 clusters per graph              */
+  const int32_t* m0_ptr;     /* [K0_all+G] members of each depth-0 cluster    */
+  const int32_t* m0_idx;     /* [N_all] local node ids, ascending per cluster  */
+  const int64_t* p1_off;     /* [G+1] pooled (coalesced) edges per graph      */
+  const int32_t* p1_rowptr;  /* [K0_all+G]                                    */
+  const int32_t* p1_col;     /* [P1_all]                                      */
+  const int32_t* p1t_rowptr; /* transpose of the pooled CSR                   */
+  const int32_t* p1t_col;
+  const int64_t* k1_off;     /* [G+1] depth-1 clusters per graph              */
+  const int32_t* m1_ptr;     /* [K1_all+G]                                    */
+  const int32_t* m1_idx;     /* [K0_all] local depth-0 ids, ascending          */
+  const float* y;            /* [G] target (class index as float for classif) */
+} dr_graph_store;
+
+/* GINet parameters (device pointers into the nn.Parameters, fp32).  */
+typedef struct dr_ginet_weights {
+  const float* w1;   /* conv1.fc.weight      [16, F]  */
+  const float* w1e;  /* conv1_ext.fc.weight  [16, F]  */
+  const float* w2;   /* conv2.fc.weight      [32, 16] */
+  const float* w2e;  /* conv2_ext.fc.weight  [32, 16] */
+  const float* fc1w; /* fc1.weight           [128, 64] */
+  const float* fc1b; /* fc1.bias             [128]     */
+  const float* fc2w; /* fc2.weight           [out, 128] */
+  const float* fc2b; /* fc2.bias             [out]      */
+} dr_ginet_weights;
+
+#define DR_PASS_FORWARD 1   /* write out[B,out]                                  */
+#define DR_PASS_BACKWARD 2  /* backprop dout (given, or from the loss) to slabs   */
+#define DR_LOSS_NONE 0      /* dout is an input (autograd)                       */
+#define DR_LOSS_MSE 1       /* nn.MSELoss(mean) on pred.reshape(-1)               */
+#define DR_LOSS_CE 2        /* nn.CrossEntropyLoss(mean, optional class weights)  */
+
+#define DR_SLAB_STRIDE(F) (32 * (F) + 1024)
+#define DR_HEAD_STRIDE(out) (320 + (((out) + 3) & ~3))
+#define DR_MAX_OUT 16
+
+typedef struct dr_ginet_pass {
+  int32_t flags;        /* DR_PASS_* bitmask                                   */
+  int32_t out_dim;      /* fc2 rows                                            */
+  int32_t loss_kind;    /* DR_LOSS_*                                           */
+  int32_t use_dropout;  /* 1: training-mode dropout with mask                  */
+  float drop_scale;     /* 1/(1-p)                                             */
+  float loss_scale;     /* 1/B (MSE) or 1/sum(w_y) (CE)                        */
+  const uint8_t* mask;  /* [B,128] keep mask (dropout), or NULL                */
+  const float* class_w; /* [out] CE class weights or NULL                      */
+  float* out;           /* [B,out] predictions (FORWARD)                       */
+  const float* dout;    /* [B,out] upstream gradient (BACKWARD, LOSS_NONE)     */
+  float* loss_per_graph;/* [B] weighted per-graph loss term (fused loss), or NULL */
+  float* slab;          /* [B, DR_SLAB_STRIDE(F)] per-graph conv weight-gradient partials */
+  float* head;          /* [B, DR_HEAD_STRIDE(out)] per-graph head vectors g, hd, dh, dout */
+} dr_ginet_pass;
+
+/* One workgroup per graph: conv1 -> depth-0 community pooling -> conv2 ->
+ * depth-1 max pooling -> per-graph mean -> fc1/relu/dropout/fc2, and (when
+ * DR_PASS_BACKWARD) the full backward of that graph, all in LDS.
+ * gids: [B] device int32 graph ids into the store.  lds_bytes: the dynamic
+ * LDS the largest graph of the batch needs (dr_ginet_lds_bytes).          */
+int dr_ginet_graph_pass(const dr_graph_store* store, const int32_t* gids, int32_t n_batch,
+                        const dr_ginet_weights* w, const dr_ginet_pass* pass,
+                        int32_t lds_bytes, void* stream);
+
+/* Dynamic LDS bytes dr_ginet_graph_pass needs for a graph of these sizes.  */
+int64_t dr_ginet_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_feat, int32_t k0,
+                           int32_t p1_edges, int32_t k1, int32_t transpose_aliased);
+
+/* Adam (torch.optim.Adam, L2 weight decay added to the gradient) settings.  */
+typedef struct dr_adam {
+  float lr, beta1, beta2, eps, weight_decay;
+  float bias_c1;      /* 1 - beta1^step                                        */
+  float bias_c2_sqrt; /* sqrt(1 - beta2^step)                                  */
+  int32_t enabled;    /* 0: only write gradients                              */
+} dr_adam;
+
+/* Parameter table in the order of GINet.named_parameters(): 16 tensors
+ * (4 x {fc, fc_edge_attr, fc_attention}.weight, fc1.{weight,bias},
+ * fc2.{weight,bias}).                                                      */
+#define DR_GINET_NPARAM 16
+typedef struct dr_param_table {
+  float* param[DR_GINET_NPARAM];
+  float* grad[DR_GINET_NPARAM];   /* may be NULL (grad not materialised)       */
+  float* exp_avg[DR_GINET_NPARAM];
+  float* exp_avg_sq[DR_GINET_NPARAM];
+  int32_t numel[DR_GINET_NPARAM];
+} dr_param_table;
+
+/* Sum the per-graph partials of dr_ginet_graph_pass over the batch into the
+ * 16 GINet gradients (dead attention weights get exact zeros), optionally
+ * apply Adam.  With slab == head == NULL the gradients are read from
+ * t->grad (e.g. after a data-parallel all-reduce) and only Adam runs.  Also
+ * write loss_scale * sum(loss_per_graph) to loss_out[0]
+ * when both are non-NULL.  */
+int dr_ginet_reduce_update(const dr_param_table* t, int32_t n_feat, int32_t out_dim,
+                           const float* slab, const float* head, int32_t n_batch,
+                           const dr_adam* adam, const float* loss_per_graph, float loss_scale,
+                           float* loss_out, void* stream);
+
+/* ---- generic layer kernels (arbitrary edge lists; GINetConvLayer API) ---- */
+
+/* Stable CSR of (row, col) pairs sorted by row: rowptr [n_rows+1], perm [E]
+ * (edge ids in CSR order), col_sorted [E].  scratch: n_rows+1 int32.      */
+int dr_csr_from_coo(const int64_t* row, const int64_t* col, int64_t n_edges, int32_t n_rows,
+                    int32_t* rowptr, int32_t* perm, int32_t* col_sorted, int32_t* scratch,
+                    void* stream);
+
+/* out[i,:] = sum_{e in row i} y[col[e],:]  (C channels, fp32), optional ReLU. */
+int dr_spmm_csr(const int32_t* rowptr, const int32_t* col, const float* y, int32_t n_rows,
+                int32_t n_chan, int32_t relu, float* out, void* stream);
+
+/* y[M,N] = x[M,K] w[N,K]^T            */
+int dr_linear_xwT(const float* x, const float* w, int32_t m, int32_t k, int32_t n, float* y, void* stream);
+/* dx[M,K] = dy[M,N] w[N,K]            */
+int dr_linear_xw(const float* dy, const float* w, int32_t m, int32_t n, int32_t k, float* dx, void* stream);
+/* dw[N,K] = dy[M,N]^T x[M,K]  (deterministic split over M into scratch[n_split,N,K]) */
+int dr_linear_dw(const float* dy, const float* x, int32_t m, int32_t n, int32_t k, float* dw,
+                 float* scratch, int32_t n_split, void* stream);
+
+/* Library / device info. */
+const char* dr_version(void);
+int dr_device_arch(char* buf, int32_t len); /* e.g. "gfx950"; 0 on success */
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DEEPRANK2_AMD_H */

@@ -1,0 +1,50 @@
+"""The C-ABI library loads on a CPU-only host and exports every symbol
+``include/deeprank2_amd.h`` declares (no compute calls without a GPU)."""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+from conftest import ROOT
+
+from deeprank2_amd import _lib
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "deeprank2_amd.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(dr_[A-Za-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_entry():
+    lib = _lib.load()
+    declared = _declared()
+    assert "dr_ginet_graph_pass" in declared
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert sorted(n for n, *_ in _lib.SIGNATURES) == declared
+
+
+def test_version_and_lds_query_are_host_only():
+    lib = _lib.load()
+    assert b"gfx950" in lib.dr_version()
+    small = lib.dr_ginet_lds_bytes(200, 3000, 30, 5, 20, 1, 1)
+    big = lib.dr_ginet_lds_bytes(200, 3000, 30, 5, 20, 1, 0)
+    assert 0 < small < big <= 200 * 1024
+    assert small % 16 == 0
+
+
+def test_struct_layouts_match_header():
+    # 4 int32 + 19 pointers; 8 pointers; 6 int32/float + 7 pointers
+    assert ctypes.sizeof(_lib.GraphStoreC) == 16 + 19 * 8
+    assert ctypes.sizeof(_lib.GinetWeightsC) == 8 * 8
+    assert ctypes.sizeof(_lib.GinetPassC) == 24 + 7 * 8
+    assert ctypes.sizeof(_lib.AdamC) == 32
+    assert ctypes.sizeof(_lib.ParamTableC) == 4 * 16 * 8 + 16 * 4
+
+
+def test_library_is_built_for_gfx950():
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob

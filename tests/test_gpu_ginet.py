@@ -1,0 +1,181 @@
+"""GPU parity of the MI355X GINet path (HIP kernels via the C ABI) against the
+reference goldens and the CPU oracle.  Tolerance: 1e-4 (north_star, fp32)."""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+from _util import fixed_dropout, golden_batch, golden_grads, golden_state_dict
+
+from deeprank2_amd.engine import GINetTrainStep
+from deeprank2_amd.neuralnets.gnn import ginet as amd
+from deeprank2_amd.store import GraphStore, pack_graphs, records_from_batch
+from oracle import data_ref, gnn_ref
+from oracle import pyg_ops as P
+
+pytestmark = pytest.mark.gpu
+TOL = dict(rtol=1e-4, atol=1e-4)
+DEV = "cuda:0"
+
+
+def _model(z, cls_args):
+    m = amd.GINet(*cls_args)
+    m.load_state_dict(golden_state_dict(z))
+    return m.to(DEV)
+
+
+@pytest.mark.parametrize("name,args", [("ginet_1atn", (50, 1, 1)), ("ginet_synth_regress", (30, 1, 3)), ("ginet_synth_classif", (30, 2, 3))])
+def test_ginet_module_vs_reference_golden(golden, name, args):
+    z = golden(name)
+    m = _model(z, args)
+    m.eval()
+    with torch.no_grad():
+        out = m(golden_batch(z)).cpu().numpy()
+    np.testing.assert_allclose(out, z["out/eval"], **TOL)
+
+    m.train()
+    m.zero_grad()
+    out = m(golden_batch(z), dropout_mask=torch.from_numpy(z["mask"]).to(torch.uint8))
+    y = torch.from_numpy(z["in/y"]).to(DEV)
+    loss = torch.nn.functional.mse_loss(out.reshape(-1), y) if str(z["meta/loss"]) == "mse" else torch.nn.functional.cross_entropy(out, y.long())
+    loss.backward()
+    np.testing.assert_allclose(out.detach().cpu().numpy(), z["out/train"], **TOL)
+    assert float(loss) == pytest.approx(float(z["loss"]), rel=1e-4)
+    ref = golden_grads(z)
+    for n, p in m.named_parameters():
+        assert p.grad is not None, n
+        np.testing.assert_allclose(p.grad.cpu().numpy(), ref[n], rtol=1e-4, atol=1e-5, err_msg=n)
+
+
+def test_ginet_batch1_vs_batch4(golden):
+    z = golden("ginet_1atn")
+    np.testing.assert_allclose(z["out/eval_b1"], z["out/eval"], rtol=1e-5, atol=1e-4)
+
+
+def test_conv_layer_arbitrary_edges_vs_golden(golden):
+    z = golden("ginet_conv_layer")
+    layer = amd.GINetConvLayer(12, 16, 2)
+    layer.load_state_dict(golden_state_dict(z))
+    layer = layer.to(DEV)
+    x = torch.from_numpy(z["in/x"]).to(DEV).requires_grad_(True)
+    out = layer(x, torch.from_numpy(z["in/edge_index"]).to(DEV), torch.from_numpy(z["in/edge_attr"]).to(DEV))
+    (out * torch.from_numpy(z["in/gz"]).to(DEV)).sum().backward()
+    np.testing.assert_allclose(out.detach().cpu().numpy(), z["out/z"], **TOL)
+    np.testing.assert_allclose(x.grad.cpu().numpy(), z["grad/x"], **TOL)
+    np.testing.assert_allclose(layer.fc.weight.grad.cpu().numpy(), z["grad/fc.weight"], **TOL)
+    assert torch.count_nonzero(layer.fc_attention.weight.grad) == 0
+
+
+def _synthetic(n, seed, **kw):
+    from deeprank2_amd.utils.synthetic import make_dataset
+
+    return [data_ref.synthetic_to_data(g, f"s{i}") for i, g in enumerate(make_dataset(n, seed=seed, **kw))]
+
+
+def _oracle_step(model_o, datas, mask):
+    model_o.train()
+    model_o.dropout_fn = fixed_dropout(mask)
+    model_o.zero_grad()
+    bat = P.Batch.from_data_list(datas)
+    out = model_o(bat)
+    loss = torch.nn.functional.mse_loss(out.reshape(-1), bat.y)
+    loss.backward()
+    return out.detach().numpy(), float(loss.detach())
+
+
+def test_fused_train_step_vs_oracle_config2_batch64():
+    """Config 2 shape (B=64 synthetic residue graphs, F=30, Fe=3): fused
+    fwd+loss+bwd kernel + reduce/Adam against the oracle + torch.optim.Adam."""
+    torch.manual_seed(1234)
+    datas = _synthetic(64, seed=0)
+    model_o = gnn_ref.GINet(30, 1, 3)
+    model = amd.GINet(30, 1, 3)
+    model.load_state_dict(model_o.state_dict())
+    model = model.to(DEV).train()
+    mask = (torch.rand(64, 128, generator=torch.Generator().manual_seed(3)) >= 0.4).float()
+    out_o, loss_o = _oracle_step(model_o, [d.clone() for d in datas], mask)
+
+    store = GraphStore(pack_graphs(records_from_batch(P.Batch.from_data_list(datas))), DEV)
+    h = amd.BatchHandle(store, np.arange(64))
+    step = GINetTrainStep(model)
+    before = [p.detach().clone() for p in step.params]
+    loss, out = step.step(h, mask=mask.to(torch.uint8).to(DEV))
+    np.testing.assert_allclose(out.cpu().numpy(), out_o, **TOL)
+    assert float(loss) == pytest.approx(loss_o, rel=1e-4)
+    grads = dict(zip(amd.PARAM_NAMES, step.grads))
+    for n, p in model_o.named_parameters():
+        np.testing.assert_allclose(grads[n].cpu().numpy(), p.grad.numpy(), rtol=1e-3, atol=1e-5, err_msg=n)
+    # the fused Adam against torch.optim.Adam fed the same (kernel) gradients
+    ref = [torch.nn.Parameter(b) for b in before]
+    for r, g in zip(ref, step.grads):
+        r.grad = g.detach().clone()
+    torch.optim.Adam(ref, lr=1e-3, weight_decay=1e-5).step()
+    for n, r, p in zip(amd.PARAM_NAMES, ref, step.params):
+        np.testing.assert_allclose(p.detach().cpu().numpy(), r.detach().cpu().numpy(), rtol=1e-5, atol=1e-7, err_msg=n)
+
+
+def test_module_autograd_vs_oracle_single_cluster_graphs():
+    """test.hdf5-like batches: one depth-0 cluster per graph -> conv2 sees no
+    edges; also a graph with several depth-1 clusters."""
+    datas = _synthetic(6, seed=11, n_lo=30, n_hi=60, mean_degree=8.0)
+    for d in datas[:3]:
+        d.cluster0 = torch.zeros_like(d.cluster0)
+        d.cluster1 = torch.zeros(1, dtype=torch.long)
+    torch.manual_seed(7)
+    model_o = gnn_ref.GINet(30, 1, 3).eval()
+    model = amd.GINet(30, 1, 3)
+    model.load_state_dict(model_o.state_dict())
+    model = model.to(DEV).eval()
+    out_o = model_o(P.Batch.from_data_list([d.clone() for d in datas]))
+    loss_o = out_o.square().sum()
+    loss_o.backward()
+    out = model(P.Batch.from_data_list(datas))
+    out.square().sum().backward()
+    np.testing.assert_allclose(out.detach().cpu().numpy(), out_o.detach().numpy(), **TOL)
+    ref = dict(model_o.named_parameters())
+    for n, p in model.named_parameters():
+        np.testing.assert_allclose(p.grad.cpu().numpy(), ref[n].grad.numpy(), rtol=1e-3, atol=1e-5, err_msg=n)
+
+
+def test_deterministic_bitwise():
+    datas = _synthetic(16, seed=4)
+    store = GraphStore(pack_graphs(records_from_batch(P.Batch.from_data_list(datas))), DEV)
+    h = amd.BatchHandle(store, np.arange(16))
+    torch.manual_seed(0)
+    model = amd.GINet(30, 1, 3).to(DEV)
+    params = model.ordered_params()
+    outs = []
+    for _ in range(3):
+        slab = torch.empty(16 * amd.slab_stride(30), device=DEV)
+        head = torch.empty(16 * amd.head_stride(1), device=DEV)
+        out = torch.empty(16, 1, device=DEV)
+        amd.graph_pass(h, params, 1, 3, loss_kind=1, loss_scale=1 / 16, out=out, loss_per_graph=torch.empty(16, device=DEV), slab=slab, head=head)
+        outs.append((out.cpu(), slab.cpu()))
+    for o, s in outs[1:]:
+        assert torch.equal(o, outs[0][0])
+        assert torch.equal(s, outs[0][1])
+
+
+def test_gids_subset_and_permutation():
+    """A mini-batch is a list of graph ids into the resident store: any order/subset."""
+    datas = _synthetic(10, seed=6)
+    store = GraphStore(pack_graphs(records_from_batch(P.Batch.from_data_list(datas))), DEV)
+    torch.manual_seed(1)
+    model_o = gnn_ref.GINet(30, 1, 3).eval()
+    model = amd.GINet(30, 1, 3)
+    model.load_state_dict(model_o.state_dict())
+    model = model.to(DEV).eval()
+    gids = np.array([7, 2, 9, 0])
+    b = P.Batch.from_data_list([datas[i].clone() for i in gids])
+    b._dr_handle = amd.BatchHandle(store, gids)
+    with torch.no_grad():
+        out = model(b).cpu().numpy()
+        ref = model_o(P.Batch.from_data_list([datas[i].clone() for i in gids])).numpy()
+    np.testing.assert_allclose(out, ref, **TOL)
+
+
+def test_cpu_model_raises():
+    m = amd.GINet(30, 1, 3)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        m(P.Batch.from_data_list(_synthetic(1, seed=1)))

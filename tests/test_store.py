@@ -1,0 +1,117 @@
+"""Host-side packing (GraphStore) and the fused kernel's algorithm, on CPU.
+
+``ginet_store_model`` walks the packed store exactly like ``ginet_fused.hip``;
+checking it against the reference goldens validates the packing and the
+algebra (alpha == 1, fused branches, precomputed pooling, tie-splitting and
+arg-member backward) without a GPU.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+from _util import golden_batch, golden_grads, golden_state_dict
+
+import ginet_store_model as M
+from deeprank2_amd.neuralnets.gnn.ginet import PARAM_NAMES
+from deeprank2_amd.store import pack_graphs, records_from_batch
+from oracle import gnn_ref
+
+
+def _packed(z, y_override=None):
+    recs = records_from_batch(golden_batch(z))
+    if y_override is not None:
+        for r, v in zip(recs, y_override):
+            r.y = v
+    return pack_graphs(recs)
+
+
+def _params(z):
+    sd = golden_state_dict(z)
+    return [sd[n].numpy() for n in PARAM_NAMES]
+
+
+@pytest.mark.parametrize("name", ["ginet_1atn", "ginet_synth_regress", "ginet_synth_classif"])
+def test_store_model_matches_reference(golden, name):
+    z = golden(name)
+    out_dim = int(z["meta/out"])
+    loss = str(z["meta/loss"])
+    packed = _packed(z)
+    params = _params(z)
+    out_eval, _, _ = M.run(packed, params, out_dim, loss=loss)
+    np.testing.assert_allclose(out_eval, z["out/eval"], rtol=1e-5, atol=1e-5)
+    out, grads, lval = M.run(packed, params, out_dim, mask=z["mask"], drop_scale=1 / 0.6, loss=loss)
+    np.testing.assert_allclose(out, z["out/train"], rtol=1e-5, atol=1e-5)
+    assert lval == pytest.approx(float(z["loss"]), rel=1e-5)
+    ref = golden_grads(z)
+    for i, n in enumerate(PARAM_NAMES):
+        np.testing.assert_allclose(grads[i], ref[n], rtol=1e-4, atol=2e-5, err_msg=n)
+
+
+def test_pooled_graph_matches_community_pooling(golden):
+    """The precomputed pooled CSR == pool_edge's coalesced edges (offset per graph)."""
+    z = golden("community_pooling_1atn")
+    packed = _packed(z)
+    rows, cols = [], []
+    for g in range(packed.n_graphs):
+        k0a, k0b = packed.k0_off[g], packed.k0_off[g + 1]
+        rp = packed.p1_rowptr[k0a + g:k0b + g + 1]
+        q0 = packed.p1_off[g]
+        for k in range(k0b - k0a):
+            for e in range(rp[k], rp[k + 1]):
+                rows.append(k0a + k)
+                cols.append(k0a + packed.p1_col[q0 + e])
+    np.testing.assert_array_equal(np.array([rows, cols]), z["out/edge_index"])
+    # depth-0 dense ids == consecutive_cluster of the offset ids
+    dense = np.concatenate([packed.cl0[packed.node_off[g]:packed.node_off[g + 1]] + packed.k0_off[g] for g in range(packed.n_graphs)])
+    np.testing.assert_array_equal(dense, np.unique(z["out/cluster_offset"], return_inverse=True)[1])
+
+
+def test_store_is_symmetric_for_doubled_edges(golden):
+    packed = _packed(golden("ginet_1atn"))
+    assert packed.transpose_aliased
+
+
+def test_store_asymmetric_keeps_transpose():
+    rec = records_from_batch(golden_batch({"in/x": np.zeros((4, 3), np.float32), "in/edge_index": np.array([[0, 1, 2], [1, 2, 3]]), "in/batch": np.zeros(4, np.int64), "in/cluster0": np.array([0, 0, 1, 1]), "in/cluster1": np.array([0, 0])}))
+    p = pack_graphs(rec)
+    assert not p.transpose_aliased
+    assert p.rowptr.tolist() == [0, 1, 2, 3, 3]
+    assert p.t_rowptr.tolist() == [0, 0, 1, 2, 3]
+    assert p.t_col.tolist() == [0, 1, 2]
+
+
+def test_pack_rejects_bad_clusters():
+    rec = records_from_batch(golden_batch({"in/x": np.zeros((3, 2), np.float32), "in/edge_index": np.array([[0, 1], [1, 0]]), "in/batch": np.zeros(3, np.int64), "in/cluster0": np.array([0, 0, 1]), "in/cluster1": np.array([0, 0])}))
+    rec[0].cluster1 = np.array([0, 0, 0])
+    with pytest.raises(ValueError, match="cluster1"):
+        pack_graphs(rec)
+
+
+def test_store_model_vs_oracle_random_ties():
+    """Integer-valued features force exact ties in both max-poolings."""
+    from deeprank2_amd.utils.synthetic import make_dataset
+    from oracle import data_ref
+    from oracle import pyg_ops as P
+
+    graphs = make_dataset(3, seed=5, n_lo=20, n_hi=30, mean_degree=6.0)
+    datas = [data_ref.synthetic_to_data(g) for g in graphs]
+    for d in datas:
+        d.x = torch.round(d.x * 2)
+        d.cluster1 = torch.tensor([i % 2 for i in range(len(d.cluster1))])
+    torch.manual_seed(0)
+    model = gnn_ref.GINet(30, 1, 3)
+    for p in model.parameters():
+        p.data = torch.round(p.data * 8) / 8
+    model.eval()
+    bat = P.Batch.from_data_list(datas)
+    out = model(bat.clone())
+    loss = torch.nn.functional.mse_loss(out.reshape(-1), bat.y)
+    loss.backward()
+    recs = records_from_batch(P.Batch.from_data_list(datas))
+    params = [dict(model.named_parameters())[n].detach().numpy() for n in PARAM_NAMES]
+    mout, grads, _ = M.run(pack_graphs(recs), params, 1, loss="mse")
+    np.testing.assert_allclose(mout, out.detach().numpy(), rtol=1e-5, atol=1e-5)
+    for i, n in enumerate(PARAM_NAMES):
+        np.testing.assert_allclose(grads[i], dict(model.named_parameters())[n].grad.numpy(), rtol=1e-4, atol=1e-5, err_msg=n)
