@@ -125,12 +125,10 @@ def main():  # noqa: PLR0915
         for p in model.parameters():
             torch.distributed.broadcast(p.data, 0)
     step = GINetTrainStep(model, lr=1e-3, weight_decay=1e-5, loss="mse", process_group=pg)
-    gen = torch.Generator(device=dev).manual_seed(77 + rank)
+    model._drop_seed = 77 + rank  # training-mode dropout drawn in-kernel (counter hash)
 
     def run(i):
-        h = handles[i % len(handles)]
-        mask = model.dropout_mask(h.B, dev, generator=gen)
-        return step.step(h, mask=mask, global_batch=B * world)
+        return step.step(handles[i % len(handles)], global_batch=B * world)
 
     for i in range(args.warmup):
         run(i)

@@ -32,3 +32,19 @@ inline int dr_allow_big_lds(const void* fn) {
   if (n_done < 64) done[n_done++] = fn;
   return 0;
 }
+
+// Counter-based uniform in [0,1) for dropout (splitmix64 finaliser, 24 bits):
+// u(seed, offset, idx) is a pure function, so the forward and the backward
+// pass regenerate the same keep mask without storing it.  The host replica
+// (dr_dropout_mask) calls the same code.
+__host__ __device__ inline uint64_t dr_mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+__host__ __device__ inline float dr_uniform(uint64_t seed, uint64_t offset, uint32_t idx) {
+  uint64_t z = dr_mix64(seed + 0x9E3779B97F4A7C15ULL * (offset + 1));
+  z = dr_mix64(z ^ (0xD1B54A32D192ED03ULL * ((uint64_t)idx + 1)));
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}

@@ -18,37 +18,53 @@
 //     dense relabelling of that graph's ids (precomputed into the store), and
 //     pool_edge's coalesced pooled graph is precomputed as a CSR too.
 //
-// LDS holds X, Y=XWᵀ, H=relu(AY), the CSR, cluster member lists, the pooled
-// graph and the head; the backward re-uses the Y/H regions for dY/dS.
-// Roofline: HBM-bound on the compulsory inputs (x, CSR, clusters) — see
-// DESIGN.md §Kernels for the algorithmic bytes per graph.
+// Execution: 1024 threads (16 waves) per graph so the LDS-latency-bound
+// gather phases have 4 waves per SIMD in flight; the two node GEMMs
+// (X·Wᵀ forward, dYᵀ·X for the weight gradient) run on the f32 MFMA
+// (v_mfma_f32_16x16x4_f32: an exact k-ordered fmaf chain, the same numerics as
+// the VALU loop).  X is stored with an odd row stride so MFMA column reads are
+// bank-conflict free.  The backward re-uses the Y/H regions for dY/dS.
+// Roofline: HBM-bound on the compulsory inputs (x, CSR, clusters) and the
+// per-graph partial writes — see DESIGN.md §Roofline.
 
 #include <hip/hip_runtime.h>
+
+#include <cstring>
 
 #include "../../include/deeprank2_amd.h"
 #include "dr_common.h"
 
 namespace {
 
-constexpr int NT = 256;      // 4 waves
+constexpr int NT = 1024;     // 16 waves
+constexpr int NW = NT / 64;
 constexpr int HEADW = 672;   // G64 hpre128 hh128 hd128 dh128 dG64 dout16 spare16
+constexpr float LOWEST = -3.402823466e+38f;
 
-struct Carve {
-  int wt, x, y, h, rp, col, trp, tcol, m0p, m0i, p1, a1, dp1, y2, h2, d2, p1rp, p1c, p1trp, p1tc, m1p, m1i, p2,
-      nt, head, red, total;
-};
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 __host__ __device__ inline int r4(int v) { return (v + 3) & ~3; }
+__host__ __device__ inline int r16(int v) { return (v + 15) & ~15; }
+__host__ __device__ inline int imax(int a, int b) { return a > b ? a : b; }
+
+struct Carve {
+  int KP, LDX, ntile, S;
+  int wt, x, y, h, rp, col, trp, tcol, m0p, m0i, p1, a1, dp1, y2, h2, d2, p1rp, p1c, p1trp, p1tc, m1p, m1i, p2,
+      nt, head, dgp, red, total;
+};
 
 __host__ __device__ inline Carve carve(int N, int E, int F, int K0, int P1, int K1, int alias) {
-  const int LDX = r4(F);
   Carve c;
+  c.KP = r16(F);          // K padded for 16-wide MFMA tiles (zeros)
+  c.LDX = c.KP + 1;       // odd stride: conflict-free MFMA column reads of X
+  c.ntile = 2 * (c.KP / 16);
+  c.S = imax(1, NW / c.ntile);
   int o = 0;
 #define TAKE(field, words) \
   c.field = o;             \
   o += r4(words);
-  TAKE(wt, LDX * 32)
-  TAKE(x, N * LDX)
+  TAKE(wt, c.KP * 32)
+  TAKE(x, N * c.LDX)
   TAKE(y, N * 32)
   TAKE(h, N * 32)
   TAKE(rp, N + 1)
@@ -82,7 +98,8 @@ __host__ __device__ inline Carve carve(int N, int E, int F, int K0, int P1, int 
   TAKE(p2, K1 * 64)
   TAKE(nt, K1 * 64)
   TAKE(head, HEADW)
-  TAKE(red, 4 * 32 * LDX)
+  TAKE(dgp, NW * 64)
+  TAKE(red, imax(c.S * 32 * c.KP, 2 * NT))
 #undef TAKE
   c.total = o;
   return c;
@@ -106,9 +123,40 @@ __device__ __forceinline__ void copy_in(T* dst, const T* __restrict__ src, int n
   for (int i = threadIdx.x; i < n; i += NT) dst[i] = src[i];
 }
 
+__device__ __forceinline__ bool keep_unit(const dr_ginet_pass& p, int b, int r) {
+  if (p.use_dropout == DR_DROPOUT_MASK) return p.mask[(int64_t)b * 128 + r] != 0;
+  return dr_uniform(p.drop_seed, p.drop_offset, (uint32_t)(b * 128 + r)) >= p.drop_p;
+}
+
+// dst[i,:32] = sum over CSR row i of src[col[e],:32]; 8 lanes per row, float4 each.
+__device__ __forceinline__ void csr_gather32(const int* rp, const int* col, const float* src, float* dst, int n,
+                                             bool relu) {
+  const int c4 = (threadIdx.x & 7) * 4;
+  for (int i = threadIdx.x >> 3; i < n; i += NT / 8) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int eb = rp[i], ee = rp[i + 1];
+    for (int e = eb; e < ee; ++e) {
+      const float4 v = *reinterpret_cast<const float4*>(&src[col[e] * 32 + c4]);
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+    if (relu) {
+      acc.x = relu_keepnan(acc.x);
+      acc.y = relu_keepnan(acc.y);
+      acc.z = relu_keepnan(acc.z);
+      acc.w = relu_keepnan(acc.w);
+    }
+    *reinterpret_cast<float4*>(&dst[i * 32 + c4]) = acc;
+  }
+}
+
 __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
   const int b = blockIdx.x;
   const dr_graph_store& s = a.s;
   const int g = a.gids[b];
@@ -123,9 +171,9 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   const int64_t k10 = s.k1_off[g];
   const int K1 = (int)(s.k1_off[g + 1] - k10);
   const int F = s.n_feat;
-  const int LDX = r4(F);
   const int alias = s.transpose_aliased;
   const Carve c = carve(N, E, F, K0, P1, K1, alias);
+  const int KP = c.KP, LDX = c.LDX;
   const int OUT = a.p.out_dim;
 
   float* sWT = lds + c.wt;
@@ -159,10 +207,11 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   float* sDh = sHd + 128;
   float* sDG = sDh + 128;
   float* sDout = sDG + 64;
+  float* sDGp = lds + c.dgp;
   float* sRed = lds + c.red;
 
   // ---------------- stage the graph into LDS --------------------------------
-  for (int p = tid; p < LDX * 32; p += NT) {
+  for (int p = tid; p < KP * 32; p += NT) {
     const int k = p >> 5, ch = p & 31;
     float v = 0.f;
     if (k < F) v = (ch < 16) ? a.w.w1[ch * F + k] : a.w.w1e[(ch - 16) * F + k];
@@ -172,10 +221,9 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
     const float* __restrict__ xg = s.x + n0 * (int64_t)F;
     for (int p = tid; p < N * F; p += NT) {
       const int i = p / F;
-      const int k = p - i * F;
-      sX[i * LDX + k] = xg[p];
+      sX[i * LDX + (p - i * F)] = xg[p];
     }
-    const int padw = LDX - F;
+    const int padw = KP - F;
     if (padw > 0)
       for (int p = tid; p < N * padw; p += NT) {
         const int i = p / padw;
@@ -200,68 +248,77 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   copy_in(sm1i, s.m1_idx + k00, K0);
   __syncthreads();
 
-  // ---------------- conv1 node GEMM: Y = X [W1;W1e]^T  (ginet.py:45) --------
+  // ---------------- conv1 node GEMM on MFMA: Y = X [W1;W1e]^T (ginet.py:45) -
   {
-    const int ch = tid & 31, rg = tid >> 5;
-    for (int base = 0; base < N; base += 32) {
-      const int r0 = base + rg * 4;
-      const int ra = min(r0, N - 1), rb = min(r0 + 1, N - 1), rc = min(r0 + 2, N - 1), rd = min(r0 + 3, N - 1);
-      float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
-      for (int k = 0; k < LDX; k += 4) {
-        const float w0 = sWT[(k + 0) * 32 + ch], w1 = sWT[(k + 1) * 32 + ch];
-        const float w2 = sWT[(k + 2) * 32 + ch], w3 = sWT[(k + 3) * 32 + ch];
-        const float4 xa = *reinterpret_cast<const float4*>(&sX[ra * LDX + k]);
-        const float4 xb = *reinterpret_cast<const float4*>(&sX[rb * LDX + k]);
-        const float4 xc = *reinterpret_cast<const float4*>(&sX[rc * LDX + k]);
-        const float4 xd = *reinterpret_cast<const float4*>(&sX[rd * LDX + k]);
-        acc0 = fmaf(xa.x, w0, acc0); acc0 = fmaf(xa.y, w1, acc0); acc0 = fmaf(xa.z, w2, acc0); acc0 = fmaf(xa.w, w3, acc0);
-        acc1 = fmaf(xb.x, w0, acc1); acc1 = fmaf(xb.y, w1, acc1); acc1 = fmaf(xb.z, w2, acc1); acc1 = fmaf(xb.w, w3, acc1);
-        acc2 = fmaf(xc.x, w0, acc2); acc2 = fmaf(xc.y, w1, acc2); acc2 = fmaf(xc.z, w2, acc2); acc2 = fmaf(xc.w, w3, acc2);
-        acc3 = fmaf(xd.x, w0, acc3); acc3 = fmaf(xd.y, w1, acc3); acc3 = fmaf(xd.z, w2, acc3); acc3 = fmaf(xd.w, w3, acc3);
+    const int li = lane & 15, kq = lane >> 4;
+    for (int t = wave; t * 16 < N; t += NW) {
+      const int r0 = t * 16;
+      const int ar = r0 + li;
+      floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < KP; k += 4) {
+        const float av = (ar < N) ? sX[ar * LDX + k + kq] : 0.f;
+        const float b0 = sWT[(k + kq) * 32 + li];
+        const float b1 = sWT[(k + kq) * 32 + 16 + li];
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b0, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b1, acc1, 0, 0, 0);
       }
-      if (r0 < N) sY[r0 * 32 + ch] = acc0;
-      if (r0 + 1 < N) sY[(r0 + 1) * 32 + ch] = acc1;
-      if (r0 + 2 < N) sY[(r0 + 2) * 32 + ch] = acc2;
-      if (r0 + 3 < N) sY[(r0 + 3) * 32 + ch] = acc3;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = r0 + kq * 4 + r;
+        if (row < N) {
+          sY[row * 32 + li] = acc0[r];
+          sY[row * 32 + 16 + li] = acc1[r];
+        }
+      }
     }
   }
   __syncthreads();
 
   // ---------------- conv1 aggregation + relu: H = relu(A Y)  (ginet.py:58,96)
-  {
-    const int c4 = (tid & 7) * 4;
-    for (int i = tid >> 3; i < N; i += NT / 8) {
-      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-      const int eb = srp[i], ee = srp[i + 1];
-      for (int e = eb; e < ee; ++e) {
-        const float4 v = *reinterpret_cast<const float4*>(&sY[scol[e] * 32 + c4]);
-        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-      }
-      float4 o;
-      o.x = relu_keepnan(acc.x); o.y = relu_keepnan(acc.y); o.z = relu_keepnan(acc.z); o.w = relu_keepnan(acc.w);
-      *reinterpret_cast<float4*>(&sH[i * 32 + c4]) = o;
-    }
-  }
+  csr_gather32(srp, scol, sY, sH, N, true);
   __syncthreads();
 
   // ---------------- depth-0 community pooling: torch_scatter scatter_max ----
   // (community_pooling.py:209): strict '>' from lowest(), members in node
   // order => first max wins, NaN never enters, empty -> 0 with no arg.
-  for (int p = tid; p < K0 * 32; p += NT) {
-    const int k = p >> 5, ch = p & 31;
-    float best = -3.402823466e+38f;
-    int arg = N;
-    for (int m = sm0p[k]; m < sm0p[k + 1]; ++m) {
-      const int i = sm0i[m];
-      const float v = sH[i * 32 + ch];
-      if (v > best) {
-        best = v;
-        arg = i;
+  // Members are split into S1 contiguous slices combined in slice order.
+  {
+    const int pairs = K0 * 32;
+    const int S1 = pairs > 0 ? max(1, min(8, NT / pairs)) : 1;
+    float* tb = sRed;
+    int* ta = reinterpret_cast<int*>(sRed + NT);
+    for (int p = tid; p < pairs * S1; p += NT) {
+      const int sl = p / pairs, pr = p - sl * pairs;
+      const int k = pr >> 5, ch = pr & 31;
+      const int mb = sm0p[k], cnt = sm0p[k + 1] - mb;
+      const int qb = mb + (cnt * sl) / S1, qe = mb + (cnt * (sl + 1)) / S1;
+      float best = LOWEST;
+      int arg = N;
+      for (int m = qb; m < qe; ++m) {
+        const int i = sm0i[m];
+        const float v = sH[i * 32 + ch];
+        if (v > best) {
+          best = v;
+          arg = i;
+        }
       }
+      tb[p] = best;
+      ta[p] = arg;
     }
-    if (best == -3.402823466e+38f) best = 0.f;
-    sP1[p] = best;
-    sA1[p] = arg;
+    __syncthreads();
+    for (int p = tid; p < pairs; p += NT) {
+      float best = LOWEST;
+      int arg = N;
+      for (int sl = 0; sl < S1; ++sl) {
+        const float v = tb[sl * pairs + p];
+        if (v > best) {
+          best = v;
+          arg = ta[sl * pairs + p];
+        }
+      }
+      sP1[p] = (best == LOWEST) ? 0.f : best;
+      sA1[p] = arg;
+    }
   }
   __syncthreads();
 
@@ -310,27 +367,31 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   __syncthreads();
 
   // ---------------- head: fc1 -> relu -> dropout -> fc2 (ginet.py:120-123) --
-  if (tid < 128) {
-    const float* __restrict__ wr = a.w.fc1w + tid * 64;
+  {
+    const int r = tid >> 3, part = tid & 7;  // 8 lanes per fc1 row
+    const float* __restrict__ wr = a.w.fc1w + r * 64 + part * 8;
     float acc = 0.f;
-    for (int o = 0; o < 64; ++o) acc = fmaf(sG[o], wr[o], acc);
-    acc += a.w.fc1b[tid];
-    sHpre[tid] = acc;
-    const float hh = relu_keepnan(acc);
-    sHh[tid] = hh;
-    float hd = hh;
-    if (a.p.use_dropout) hd = (a.p.mask[(int64_t)b * 128 + tid] ? hh : 0.f) * a.p.drop_scale;
-    sHd[tid] = hd;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc = fmaf(sG[part * 8 + j], wr[j], acc);
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    acc += __shfl_xor(acc, 4, 64);
+    if (part == 0) {
+      acc += a.w.fc1b[r];
+      sHpre[r] = acc;
+      const float hh = relu_keepnan(acc);
+      sHh[r] = hh;
+      float hd = hh;
+      if (a.p.use_dropout) hd = (keep_unit(a.p, b, r) ? hh : 0.f) * a.p.drop_scale;
+      sHd[r] = hd;
+    }
   }
   __syncthreads();
-  {
-    const int wave = tid >> 6, lane = tid & 63;
-    for (int q = wave; q < OUT; q += NT / 64) {
-      const float* __restrict__ wr = a.w.fc2w + q * 128;
-      float v = fmaf(sHd[lane], wr[lane], sHd[lane + 64] * wr[lane + 64]);
-      v = dr_wave_sum(v);
-      if (lane == 0) sDout[q] = v + a.w.fc2b[q];  // logits parked in sDout
-    }
+  for (int q = wave; q < OUT; q += NW) {
+    const float* __restrict__ wr = a.w.fc2w + q * 128;
+    float v = fmaf(sHd[lane], wr[lane], sHd[lane + 64] * wr[lane + 64]);
+    v = dr_wave_sum(v);
+    if (lane == 0) sDout[q] = v + a.w.fc2b[q];  // logits parked in sDout
   }
   __syncthreads();
   if ((a.p.flags & DR_PASS_FORWARD) && tid < OUT) a.p.out[(int64_t)b * OUT + tid] = sDout[tid];
@@ -339,13 +400,12 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
 
   // ---------------- loss gradient (trainer.py:688-689) ----------------------
   if (tid == 0) {
-    const int yrow = g;
     if (a.p.loss_kind == DR_LOSS_MSE) {
-      const float d = sDout[0] - s.y[yrow];
+      const float d = sDout[0] - s.y[g];
       if (a.p.loss_per_graph) a.p.loss_per_graph[b] = d * d;
       sDout[0] = 2.f * d * a.p.loss_scale;
     } else if (a.p.loss_kind == DR_LOSS_CE) {
-      const int yi = (int)s.y[yrow];
+      const int yi = (int)s.y[g];
       float mx = sDout[0];
       for (int q = 1; q < OUT; ++q) mx = fmaxf(mx, sDout[q]);
       float se = 0.f;
@@ -364,13 +424,21 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   if (tid < 128) {
     float acc = 0.f;
     for (int q = 0; q < OUT; ++q) acc = fmaf(a.w.fc2w[q * 128 + tid], sDout[q], acc);
-    if (a.p.use_dropout) acc = (a.p.mask[(int64_t)b * 128 + tid] ? acc : 0.f) * a.p.drop_scale;
+    if (a.p.use_dropout) acc = (keep_unit(a.p, b, tid) ? acc : 0.f) * a.p.drop_scale;
     sDh[tid] = relu_bwd(sHh[tid], acc);
+  }
+  __syncthreads();
+  {
+    const int o = tid & 63, rc = tid >> 6;  // 16 chunks of 8 fc1 rows
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc = fmaf(a.w.fc1w[(rc * 8 + j) * 64 + o], sDh[rc * 8 + j], acc);
+    sDGp[rc * 64 + o] = acc;
   }
   __syncthreads();
   if (tid < 64) {
     float acc = 0.f;
-    for (int r = 0; r < 128; ++r) acc = fmaf(a.w.fc1w[r * 64 + tid], sDh[r], acc);
+    for (int rc = 0; rc < NW; ++rc) acc += sDGp[rc * 64 + tid];
     sDG[tid] = acc;
   }
   {
@@ -438,63 +506,47 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   __syncthreads();
 
   // ---------------- conv1 backward: dY = A^T dS  -> reuse sY ---------------
-  {
-    const int c4 = (tid & 7) * 4;
-    for (int j = tid >> 3; j < N; j += NT / 8) {
-      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int e = strp[j]; e < strp[j + 1]; ++e) {
-        const float4 v = *reinterpret_cast<const float4*>(&sH[stcol[e] * 32 + c4]);
-        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-      }
-      *reinterpret_cast<float4*>(&sY[j * 32 + c4]) = acc;
-    }
-  }
+  csr_gather32(strp, stcol, sH, sY, N, false);
   __syncthreads();
 
-  // ---------------- dW1cat = dY^T X  (4 row-quarters, 4x4 register blocks) --
+  // ---------------- dW1cat = dY^T X on MFMA, node range split in S slices ---
   {
-    const int q = tid >> 6, t64 = tid & 63;
-    const int nblk = 8 * (LDX / 4);
-    const int ib = (q * N) / 4, ie = ((q + 1) * N) / 4;
-    for (int blk = t64; blk < nblk; blk += 64) {
-      const int cb = (blk & 7) * 4, kb = (blk >> 3) * 4;
-      float acc[4][4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) acc[u][v] = 0.f;
-      for (int i = ib; i < ie; ++i) {
-        const float4 dy = *reinterpret_cast<const float4*>(&sY[i * 32 + cb]);
-        const float4 xv = *reinterpret_cast<const float4*>(&sX[i * LDX + kb]);
-        const float dyv[4] = {dy.x, dy.y, dy.z, dy.w};
-        const float xvv[4] = {xv.x, xv.y, xv.z, xv.w};
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-          for (int v = 0; v < 4; ++v) acc[u][v] = fmaf(dyv[u], xvv[v], acc[u][v]);
+    const int li = lane & 15, kq = lane >> 4;
+    const int tile = wave % c.ntile, sl = wave / c.ntile;
+    if (sl < c.S) {
+      const int ct = tile & 1, kt = tile >> 1;
+      const int nb = (N * sl) / c.S, ne = (N * (sl + 1)) / c.S;
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int n = nb; n < ne; n += 4) {
+        const int node = n + kq;
+        const bool ok = node < ne;
+        const float av = ok ? sY[node * 32 + ct * 16 + li] : 0.f;
+        const float bv = ok ? sX[node * LDX + kt * 16 + li] : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
       }
-      float* red = sRed + q * 32 * LDX;
+      float* red = sRed + sl * 32 * KP;
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) red[(cb + u) * LDX + kb + v] = acc[u][v];
+      for (int r = 0; r < 4; ++r) red[(ct * 16 + kq * 4 + r) * KP + kt * 16 + li] = acc[r];
     }
   }
   __syncthreads();
   {
     const int SS = DR_SLAB_STRIDE(F);
     float* slab = a.p.slab + (int64_t)b * SS;
-    const int plane = 32 * LDX;
+    const int plane = 32 * KP;
     for (int p = tid; p < 32 * F; p += NT) {
       const int ch = p / F, k = p - ch * F;
-      const int o = ch * LDX + k;
-      slab[p] = (sRed[o] + sRed[plane + o]) + (sRed[2 * plane + o] + sRed[3 * plane + o]);
+      float acc = 0.f;
+      for (int sl = 0; sl < c.S; ++sl) acc += sRed[sl * plane + ch * KP + k];
+      slab[p] = acc;
     }
   }
 }
 
 // ---------------------------------------------------------------------------
 // Reduce the per-graph partials into the 16 GINet gradients, then Adam.
+// Block = 32 parameter elements x 8 batch chunks; the chunk partials are
+// combined in chunk order (deterministic).
 // ---------------------------------------------------------------------------
 struct ReduceArgs {
   dr_param_table t;
@@ -508,54 +560,77 @@ struct ReduceArgs {
   int32_t off[DR_GINET_NPARAM + 1];
 };
 
-__global__ void __launch_bounds__(256) ginet_reduce_kernel(ReduceArgs a) {
-  const int gi = blockIdx.x * 256 + threadIdx.x;
-  if (gi == 0 && a.lpg && a.loss_out) {
+constexpr int RP = 32;  // parameter elements per block
+constexpr int RC = 8;   // batch chunks per block
+
+__device__ float grad_partial(const ReduceArgs& a, int pi, int e, int b0, int b1) {
+  const int F = a.F;
+  const int64_t SS = DR_SLAB_STRIDE(F);
+  const int64_t HS = DR_HEAD_STRIDE(a.OUT);
+  float acc = 0.f;
+  switch (pi) {
+    case 0:  // conv1.fc.weight [16,F] = rows 0..15 of the slab's [32][F]
+      for (int b = b0; b < b1; ++b) acc += a.slab[b * SS + e];
+      break;
+    case 6:  // conv1_ext.fc.weight = rows 16..31
+      for (int b = b0; b < b1; ++b) acc += a.slab[b * SS + 16 * F + e];
+      break;
+    case 3:  // conv2.fc.weight [32,16]
+      for (int b = b0; b < b1; ++b) acc += a.slab[b * SS + 32 * F + e];
+      break;
+    case 9:  // conv2_ext.fc.weight
+      for (int b = b0; b < b1; ++b) acc += a.slab[b * SS + 32 * F + 512 + e];
+      break;
+    case 12: {  // fc1.weight [128,64] = sum_b dh ⊗ g
+      const int r = e >> 6, o = e & 63;
+      for (int b = b0; b < b1; ++b) acc = fmaf(a.head[b * HS + 192 + r], a.head[b * HS + o], acc);
+    } break;
+    case 13:  // fc1.bias
+      for (int b = b0; b < b1; ++b) acc += a.head[b * HS + 192 + e];
+      break;
+    case 14: {  // fc2.weight [out,128] = sum_b dout ⊗ hd
+      const int q = e >> 7, r = e & 127;
+      for (int b = b0; b < b1; ++b) acc = fmaf(a.head[b * HS + 320 + q], a.head[b * HS + 64 + r], acc);
+    } break;
+    case 15:
+      for (int b = b0; b < b1; ++b) acc += a.head[b * HS + 320 + e];
+      break;
+    default:  // fc_edge_attr / fc_attention: exact zeros (softmax over size-1 dim)
+      break;
+  }
+  return acc;
+}
+
+__global__ void __launch_bounds__(RP* RC) ginet_reduce_kernel(ReduceArgs a) {
+  __shared__ float part[RC][RP];
+  const int lp = threadIdx.x % RP, ch = threadIdx.x / RP;
+  const int gi = blockIdx.x * RP + lp;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && a.lpg && a.loss_out) {
     float acc = 0.f;
     for (int b = 0; b < a.B; ++b) acc += a.lpg[b];
     a.loss_out[0] = acc * a.loss_scale;
   }
-  if (gi >= a.off[DR_GINET_NPARAM]) return;
+  const bool live = gi < a.off[DR_GINET_NPARAM];
   int pi = 0;
-  while (gi >= a.off[pi + 1]) ++pi;
-  const int e = gi - a.off[pi];
-  const int F = a.F;
-  const int SS = DR_SLAB_STRIDE(F);
-  const int HS = DR_HEAD_STRIDE(a.OUT);
-  float gsum = 0.f;
-  if (!a.slab) {  // gradients supplied (e.g. after an RCCL all-reduce): Adam only
-    gsum = a.t.grad[pi] ? a.t.grad[pi][e] : 0.f;
-  } else switch (pi) {
-    case 0:  // conv1.fc.weight [16,F] = rows 0..15 of the slab's [32][F]
-      for (int b = 0; b < a.B; ++b) gsum += a.slab[(int64_t)b * SS + e];
-      break;
-    case 6:  // conv1_ext.fc.weight = rows 16..31
-      for (int b = 0; b < a.B; ++b) gsum += a.slab[(int64_t)b * SS + 16 * F + e];
-      break;
-    case 3:  // conv2.fc.weight [32,16]
-      for (int b = 0; b < a.B; ++b) gsum += a.slab[(int64_t)b * SS + 32 * F + e];
-      break;
-    case 9:  // conv2_ext.fc.weight
-      for (int b = 0; b < a.B; ++b) gsum += a.slab[(int64_t)b * SS + 32 * F + 512 + e];
-      break;
-    case 12: {  // fc1.weight [128,64] = sum_b dh ⊗ g
-      const int r = e >> 6, o = e & 63;
-      for (int b = 0; b < a.B; ++b) gsum = fmaf(a.head[(int64_t)b * HS + 192 + r], a.head[(int64_t)b * HS + o], gsum);
-    } break;
-    case 13:  // fc1.bias
-      for (int b = 0; b < a.B; ++b) gsum += a.head[(int64_t)b * HS + 192 + e];
-      break;
-    case 14: {  // fc2.weight [out,128] = sum_b dout ⊗ hd
-      const int q = e >> 7, r = e & 127;
-      for (int b = 0; b < a.B; ++b) gsum = fmaf(a.head[(int64_t)b * HS + 320 + q], a.head[(int64_t)b * HS + 64 + r], gsum);
-    } break;
-    case 15:
-      for (int b = 0; b < a.B; ++b) gsum += a.head[(int64_t)b * HS + 320 + e];
-      break;
-    default:  // fc_edge_attr / fc_attention: exact zeros (softmax over size-1 dim)
-      gsum = 0.f;
+  if (live)
+    while (gi >= a.off[pi + 1]) ++pi;
+  const int e = live ? gi - a.off[pi] : 0;
+  if (a.slab) {
+    float v = 0.f;
+    if (live) v = grad_partial(a, pi, e, (a.B * ch) / RC, (a.B * (ch + 1)) / RC);
+    part[ch][lp] = v;
   }
-  if (a.slab && a.t.grad[pi]) a.t.grad[pi][e] = gsum;
+  __syncthreads();
+  if (ch != 0 || !live) return;
+  float gsum;
+  if (a.slab) {
+    gsum = 0.f;
+#pragma unroll
+    for (int k = 0; k < RC; ++k) gsum += part[k][lp];
+    if (a.t.grad[pi]) a.t.grad[pi][e] = gsum;
+  } else {  // gradients supplied (e.g. after an RCCL all-reduce): Adam only
+    gsum = a.t.grad[pi] ? a.t.grad[pi][e] : 0.f;
+  }
   if (a.adam.enabled) {
     float* p = a.t.param[pi] + e;
     float* m = a.t.exp_avg[pi] + e;
@@ -588,7 +663,8 @@ extern "C" int dr_ginet_graph_pass(const dr_graph_store* store, const int32_t* g
   if ((pass->flags & DR_PASS_BACKWARD) && (!pass->slab || !pass->head)) return DR_E_ARG;
   if ((pass->flags & DR_PASS_BACKWARD) && pass->loss_kind == DR_LOSS_NONE && !pass->dout) return DR_E_ARG;
   if ((pass->flags & DR_PASS_FORWARD) && !pass->out) return DR_E_ARG;
-  if (pass->use_dropout && !pass->mask) return DR_E_ARG;
+  if (pass->use_dropout == DR_DROPOUT_MASK && !pass->mask) return DR_E_ARG;
+  if (pass->use_dropout < DR_DROPOUT_OFF || pass->use_dropout > DR_DROPOUT_HASH) return DR_E_ARG;
   if (n_batch == 0) return DR_OK;
   DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_graph_kernel)));
   GinetArgs args;
@@ -606,10 +682,8 @@ extern "C" int dr_ginet_reduce_update(const dr_param_table* t, int32_t n_feat, i
                                       const float* loss_per_graph, float loss_scale, float* loss_out, void* stream) {
   if (!t || !adam || n_batch < 0) return DR_E_ARG;
   if ((slab == nullptr) != (head == nullptr)) return DR_E_ARG;
-  if (!slab)
-    for (int i = 0; i < DR_GINET_NPARAM; ++i)
-      if (!t->grad[i]) return DR_E_ARG;
   ReduceArgs a;
+  std::memset(&a, 0, sizeof(a));
   a.t = *t;
   a.adam = *adam;
   a.slab = slab;
@@ -624,9 +698,16 @@ extern "C" int dr_ginet_reduce_update(const dr_param_table* t, int32_t n_feat, i
   for (int i = 0; i < DR_GINET_NPARAM; ++i) {
     if (t->numel[i] < 0 || !t->param[i]) return DR_E_ARG;
     if (adam->enabled && (!t->exp_avg[i] || !t->exp_avg_sq[i])) return DR_E_ARG;
+    if (!slab && !t->grad[i]) return DR_E_ARG;
     a.off[i + 1] = a.off[i] + t->numel[i];
   }
   const int total = a.off[DR_GINET_NPARAM];
-  hipLaunchKernelGGL(ginet_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(ginet_reduce_kernel, dim3((total + RP - 1) / RP), dim3(RP * RC), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
+}
+
+extern "C" int dr_dropout_mask(uint64_t seed, uint64_t offset, int32_t n, float p, uint8_t* keep_host) {
+  if (n < 0 || (n > 0 && !keep_host)) return DR_E_ARG;
+  for (int i = 0; i < n; ++i) keep_host[i] = dr_uniform(seed, offset, (uint32_t)i) >= p ? 1 : 0;
+  return DR_OK;
 }

@@ -19,6 +19,9 @@ DR_LOSS_NONE = 0
 DR_LOSS_MSE = 1
 DR_LOSS_CE = 2
 DR_MAX_OUT = 16
+DR_DROPOUT_OFF = 0
+DR_DROPOUT_MASK = 1
+DR_DROPOUT_HASH = 2
 DR_GINET_NPARAM = 16
 
 ERRORS = {-1: "bad argument", -2: "graph does not fit the per-graph LDS kernel", -3: "unsupported configuration"}
@@ -69,7 +72,11 @@ class GinetPassC(ctypes.Structure):
         ("loss_kind", ctypes.c_int32),
         ("use_dropout", ctypes.c_int32),
         ("drop_scale", ctypes.c_float),
+        ("drop_p", ctypes.c_float),
+        ("drop_seed", ctypes.c_uint64),
+        ("drop_offset", ctypes.c_uint64),
         ("loss_scale", ctypes.c_float),
+        ("pad0", ctypes.c_int32),
         ("mask", VP),
         ("class_w", VP),
         ("out", VP),
@@ -113,6 +120,7 @@ SIGNATURES = [
     ("dr_linear_xwT", ctypes.c_int, [VP, VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP, VP]),
     ("dr_linear_xw", ctypes.c_int, [VP, VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP, VP]),
     ("dr_linear_dw", ctypes.c_int, [VP, VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP, VP, ctypes.c_int32, VP]),
+    ("dr_dropout_mask", ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int32, ctypes.c_float, VP]),
     ("dr_version", ctypes.c_char_p, []),
     ("dr_device_arch", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32]),
 ]
@@ -161,3 +169,12 @@ def require_device(*tensors) -> None:
         if t is not None and not t.is_cuda:
             msg = "deeprank2_amd kernels run on the MI355X only: got a CPU tensor (no CPU fallback by design)"
             raise RuntimeError(msg)
+
+
+def dropout_keep_host(seed: int, offset: int, n: int, p: float):
+    """Host replica of the in-kernel dropout hash (DR_DROPOUT_HASH) -> numpy uint8 [n]."""
+    import numpy as np  # noqa: PLC0415
+
+    out = np.empty(n, dtype=np.uint8)
+    check(load().dr_dropout_mask(seed, offset, n, p, out.ctypes.data), "dr_dropout_mask")
+    return out

@@ -21,7 +21,7 @@ import math
 import torch
 
 from deeprank2_amd import _lib
-from deeprank2_amd.neuralnets.gnn.ginet import BatchHandle, GINet, graph_pass, head_stride, reduce_update, slab_stride
+from deeprank2_amd.neuralnets.gnn.ginet import BatchHandle, Dropout, GINet, graph_pass, head_stride, reduce_update, slab_stride
 
 
 class GINetTrainStep:
@@ -84,21 +84,28 @@ class GINetTrainStep:
         a.enabled = int(enabled)
         return a
 
-    def step(self, h: BatchHandle, mask=None, global_batch=None):
-        """One training step on the graphs of ``h``; returns (loss [1], out [B,out]) device views."""
+    def step(self, h: BatchHandle, mask=None, global_batch=None, dropout=True):
+        """One training step on the graphs of ``h``; returns (loss [1], out [B,out]) device views.
+
+        Dropout (ginet.py:122): ``mask`` (uint8 [B,128]) if given, else the
+        in-kernel hash RNG when ``dropout`` and the model's p > 0."""
         self._ensure(h.B)
         if global_batch is None:
             global_batch = h.B * self.world
         kind = _lib.DR_LOSS_MSE if self.loss == "mse" else _lib.DR_LOSS_CE
         scale = self.loss_scale(h, global_batch)
-        drop_scale = 1.0 / (1.0 - self.model.dropout) if mask is not None else 1.0
+        drop = None
+        if mask is not None:
+            drop = Dropout(self.model.dropout, mask=mask)
+        elif dropout and self.model.dropout > 0:
+            drop = self.model.next_dropout()
         ev = self.kernel_events
         if ev is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
         graph_pass(
             h, self.params, self.out_dim, _lib.DR_PASS_FORWARD | _lib.DR_PASS_BACKWARD,
-            mask=mask, drop_scale=drop_scale, loss_kind=kind, loss_scale=scale, class_w=self.class_weights,
+            dropout=drop, loss_kind=kind, loss_scale=scale, class_w=self.class_weights,
             out=self.out, loss_per_graph=self.lpg, slab=self.slab, head=self.head,
         )  # fmt: skip
         if ev is not None:

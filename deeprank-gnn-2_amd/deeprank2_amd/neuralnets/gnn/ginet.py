@@ -164,14 +164,40 @@ def weights_c(params):
     return w
 
 
-def graph_pass(h: BatchHandle, params, out_dim, flags, *, mask=None, drop_scale=1.0, dout=None, loss_kind=_lib.DR_LOSS_NONE, loss_scale=1.0, class_w=None, out=None, loss_per_graph=None, slab=None, head=None):
+class Dropout:
+    """How fc1's output is dropped: ``mask`` (uint8 [B,128] keep mask) or the
+    in-kernel counter hash ``(seed, offset)`` with probability ``p``."""
+
+    def __init__(self, p, mask=None, seed=None, offset=0):
+        self.p = float(p)
+        self.mask = mask
+        self.seed = seed
+        self.offset = int(offset)
+
+    @property
+    def scale(self):
+        return 1.0 / (1.0 - self.p)
+
+
+def graph_pass(h: BatchHandle, params, out_dim, flags, *, dropout: Dropout | None = None, dout=None, loss_kind=_lib.DR_LOSS_NONE, loss_scale=1.0, class_w=None, out=None, loss_per_graph=None, slab=None, head=None):
     dev = h.store.device
     p = _lib.GinetPassC()
     p.flags = flags
     p.out_dim = out_dim
     p.loss_kind = loss_kind
-    p.use_dropout = int(mask is not None)
-    p.drop_scale = drop_scale
+    mask = None
+    if dropout is None:
+        p.use_dropout = _lib.DR_DROPOUT_OFF
+    elif dropout.mask is not None:
+        mask = dropout.mask
+        p.use_dropout = _lib.DR_DROPOUT_MASK
+        p.drop_scale = dropout.scale
+    else:
+        p.use_dropout = _lib.DR_DROPOUT_HASH
+        p.drop_scale = dropout.scale
+        p.drop_p = dropout.p
+        p.drop_seed = dropout.seed
+        p.drop_offset = dropout.offset
     p.loss_scale = loss_scale
     p.mask = _lib.ptr(mask)
     p.class_w = _lib.ptr(class_w)
@@ -201,10 +227,10 @@ def reduce_update(h: BatchHandle, params, grads, out_dim, slab, head, adam=None,
 
 class _GINetFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, h, mask, drop_scale, out_dim, *params):
+    def forward(ctx, h, dropout, out_dim, *params):
         out = torch.empty(h.B, out_dim, dtype=torch.float32, device=h.store.device)
-        graph_pass(h, params, out_dim, _lib.DR_PASS_FORWARD, mask=mask, drop_scale=drop_scale, out=out)
-        ctx.h, ctx.mask, ctx.drop_scale, ctx.out_dim = h, mask, drop_scale, out_dim
+        graph_pass(h, params, out_dim, _lib.DR_PASS_FORWARD, dropout=dropout, out=out)
+        ctx.h, ctx.dropout, ctx.out_dim = h, dropout, out_dim
         ctx.save_for_backward(*params)
         return out
 
@@ -215,10 +241,10 @@ class _GINetFn(torch.autograd.Function):
         dev = h.store.device
         slab = torch.empty(h.B * slab_stride(h.store.n_feat), dtype=torch.float32, device=dev)
         head = torch.empty(h.B * head_stride(out_dim), dtype=torch.float32, device=dev)
-        graph_pass(h, params, out_dim, _lib.DR_PASS_BACKWARD, mask=ctx.mask, drop_scale=ctx.drop_scale, dout=dout.contiguous(), slab=slab, head=head)
+        graph_pass(h, params, out_dim, _lib.DR_PASS_BACKWARD, dropout=ctx.dropout, dout=dout.contiguous(), slab=slab, head=head)
         grads = [torch.empty_like(p) for p in params]
         reduce_update(h, params, grads, out_dim, slab, head)
-        return (None, None, None, None, *grads)
+        return (None, None, None, *grads)
 
 
 class GINet(nn.Module):
@@ -236,14 +262,20 @@ class GINet(nn.Module):
         self.dropout = 0.4
         self.input_shape = input_shape
         self.output_shape = output_shape
+        self._drop_seed = None
+        self._drop_calls = 0
 
     def ordered_params(self):
         named = dict(self.named_parameters())
         return [named[n] for n in PARAM_NAMES]
 
-    def dropout_mask(self, n_graphs, device, generator=None):
-        keep = torch.rand(n_graphs, 128, device=device, generator=generator) >= self.dropout
-        return keep.to(torch.uint8)
+    def next_dropout(self):
+        """Training-mode dropout of fc1's output (ginet.py:122) drawn by the
+        in-kernel counter hash: a fresh (seed, offset) per forward call."""
+        if self._drop_seed is None:
+            self._drop_seed = int(torch.randint(0, 2**62, (1,)).item())
+        self._drop_calls += 1
+        return Dropout(self.dropout, seed=self._drop_seed, offset=self._drop_calls)
 
     def forward(self, data, dropout_mask=None):
         params = [p.contiguous() for p in self.ordered_params()]
@@ -255,9 +287,10 @@ class GINet(nn.Module):
         if h.store.n_feat != self.input_shape:
             msg = f"batch has {h.store.n_feat} node features, model expects {self.input_shape}"
             raise ValueError(msg)
-        mask = None
+        dropout = None
         if self.training and self.dropout > 0:
-            mask = dropout_mask if dropout_mask is not None else self.dropout_mask(h.B, dev)
-            mask = mask.to(device=dev, dtype=torch.uint8).contiguous()
-        scale = 1.0 / (1.0 - self.dropout) if mask is not None else 1.0
-        return _GINetFn.apply(h, mask, scale, self.output_shape, *params)
+            if dropout_mask is not None:
+                dropout = Dropout(self.dropout, mask=dropout_mask.to(device=dev, dtype=torch.uint8).contiguous())
+            else:
+                dropout = self.next_dropout()
+        return _GINetFn.apply(h, dropout, self.output_shape, *params)

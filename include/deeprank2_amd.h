@@ -99,15 +99,22 @@ typedef struct dr_ginet_weights {
 #define DR_SLAB_STRIDE(F) (32 * (F) + 1024)
 #define DR_HEAD_STRIDE(out) (320 + (((out) + 3) & ~3))
 #define DR_MAX_OUT 16
+#define DR_DROPOUT_OFF 0
+#define DR_DROPOUT_MASK 1  /* keep mask given in pass->mask        */
+#define DR_DROPOUT_HASH 2  /* counter-based hash, see dr_dropout_mask */
 
 typedef struct dr_ginet_pass {
   int32_t flags;        /* DR_PASS_* bitmask                                   */
   int32_t out_dim;      /* fc2 rows                                            */
   int32_t loss_kind;    /* DR_LOSS_*                                           */
-  int32_t use_dropout;  /* 1: training-mode dropout with mask                  */
+  int32_t use_dropout;  /* DR_DROPOUT_*: training-mode dropout of fc1's output  */
   float drop_scale;     /* 1/(1-p)                                             */
+  float drop_p;         /* p (DR_DROPOUT_HASH)                                 */
+  uint64_t drop_seed;   /* DR_DROPOUT_HASH: keep[b,r] = u(seed, offset, 128b+r) >= p */
+  uint64_t drop_offset;
   float loss_scale;     /* 1/B (MSE) or 1/sum(w_y) (CE)                        */
-  const uint8_t* mask;  /* [B,128] keep mask (dropout), or NULL                */
+  int32_t pad0;
+  const uint8_t* mask;  /* [B,128] keep mask (DR_DROPOUT_MASK)                 */
   const float* class_w; /* [out] CE class weights or NULL                      */
   float* out;           /* [B,out] predictions (FORWARD)                       */
   const float* dout;    /* [B,out] upstream gradient (BACKWARD, LOSS_NONE)     */
@@ -179,6 +186,10 @@ int dr_linear_xw(const float* dy, const float* w, int32_t m, int32_t n, int32_t 
 /* dw[N,K] = dy[M,N]^T x[M,K]  (deterministic split over M into scratch[n_split,N,K]) */
 int dr_linear_dw(const float* dy, const float* x, int32_t m, int32_t n, int32_t k, float* dw,
                  float* scratch, int32_t n_split, void* stream);
+
+/* Host-side replica of the in-kernel dropout RNG (DR_DROPOUT_HASH): writes
+ * keep[i] for i in [0, n) (i = 128*b + r) into a host buffer.             */
+int dr_dropout_mask(uint64_t seed, uint64_t offset, int32_t n, float p, uint8_t* keep_host);
 
 /* Library / device info. */
 const char* dr_version(void);

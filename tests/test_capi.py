@@ -37,10 +37,10 @@ def test_version_and_lds_query_are_host_only():
 
 
 def test_struct_layouts_match_header():
-    # 4 int32 + 19 pointers; 8 pointers; 6 int32/float + 7 pointers
+    # 4 int32 + 19 pointers; 8 pointers; 4 int32 + 2 float + 2 uint64 + float/int32 + 7 pointers
     assert ctypes.sizeof(_lib.GraphStoreC) == 16 + 19 * 8
     assert ctypes.sizeof(_lib.GinetWeightsC) == 8 * 8
-    assert ctypes.sizeof(_lib.GinetPassC) == 24 + 7 * 8
+    assert ctypes.sizeof(_lib.GinetPassC) == 16 + 8 + 16 + 8 + 7 * 8
     assert ctypes.sizeof(_lib.AdamC) == 32
     assert ctypes.sizeof(_lib.ParamTableC) == 4 * 16 * 8 + 16 * 4
 
@@ -48,3 +48,12 @@ def test_struct_layouts_match_header():
 def test_library_is_built_for_gfx950():
     blob = open(_lib.LIB_PATH, "rb").read()
     assert b"gfx950" in blob
+
+
+def test_dropout_hash_host_replica_statistics():
+    keep = _lib.dropout_keep_host(1234, 7, 128 * 512, 0.4)
+    assert abs(keep.mean() - 0.6) < 0.01
+    again = _lib.dropout_keep_host(1234, 7, 128 * 512, 0.4)
+    other = _lib.dropout_keep_host(1234, 8, 128 * 512, 0.4)
+    assert (keep == again).all()
+    assert (keep != other).mean() > 0.3
