@@ -18,12 +18,13 @@
 //     dense relabelling of that graph's ids (precomputed into the store), and
 //     pool_edge's coalesced pooled graph is precomputed as a CSR too.
 //
-// Execution: 1024 threads (16 waves) per graph so the LDS-latency-bound
-// gather phases have 4 waves per SIMD in flight; the two node GEMMs
-// (X·Wᵀ forward, dYᵀ·X for the weight gradient) run on the f32 MFMA
-// (v_mfma_f32_16x16x4_f32: an exact k-ordered fmaf chain, the same numerics as
-// the VALU loop).  X is stored with an odd row stride so MFMA column reads are
-// bank-conflict free.  The backward re-uses the Y/H regions for dY/dS.
+// Execution: 1024 threads (16 waves) per graph; the graph and the weights are
+// staged by global->LDS DMA (16-byte lanes where the store layout allows);
+// conv1 aggregates first, Z = A·X, then H = relu(Z·Wᵀ) on the f32 MFMA
+// (v_mfma_f32_16x16x4_f32: an exact k-ordered fmaf chain).  Because the
+// depth-0 max pool routes each channel's gradient to one member per cluster,
+// the conv1 weight gradient is sum_k v_k·Z[arg_k] and the backward needs no
+// gather over the edges at all.
 // Roofline: HBM-bound on the compulsory inputs (x, CSR, clusters) and the
 // per-graph partial writes — see DESIGN.md §Roofline.
 
@@ -48,34 +49,32 @@ __host__ __device__ inline int r16(int v) { return (v + 15) & ~15; }
 __host__ __device__ inline int imax(int a, int b) { return a > b ? a : b; }
 
 struct Carve {
-  int KP, LDX, ntile, S;
-  int wt, x, y, h, rp, col, trp, tcol, m0p, m0i, p1, a1, dp1, y2, h2, d2, p1rp, p1c, p1trp, p1tc, m1p, m1i, p2,
+  int KP, LDW, XS;
+  int w1, w2, fc2, x, z, h, rp, col, m0p, m0i, p1, a1, dp1, y2, h2, d2, p1rp, p1c, p1trp, p1tc, m1p, m1i, p2,
       nt, head, dgp, red, total;
 };
 
-__host__ __device__ inline Carve carve(int N, int E, int F, int K0, int P1, int K1, int alias) {
+// LDS carve (4-byte words, every region 16-byte aligned).  X keeps the HBM
+// row stride XS = r4(F) (16-byte rows for the DMA and the float4 gather);
+// Z = A·X and W use the odd stride KP+1 so the MFMA column reads are
+// bank-conflict free.
+__host__ __device__ inline Carve carve(int N, int E, int F, int K0, int P1, int K1, int alias, int OUT) {
   Carve c;
-  c.KP = r16(F);          // K padded for 16-wide MFMA tiles (zeros)
-  c.LDX = c.KP + 1;       // odd stride: conflict-free MFMA column reads of X
-  c.ntile = 2 * (c.KP / 16);
-  c.S = imax(1, NW / c.ntile);
+  c.KP = r16(F);      // K padded for the 16x16x4 MFMA steps (zeros)
+  c.LDW = c.KP + 1;
+  c.XS = r4(F);
   int o = 0;
 #define TAKE(field, words) \
   c.field = o;             \
   o += r4(words);
-  TAKE(wt, c.KP * 32)
-  TAKE(x, N * c.LDX)
-  TAKE(y, N * 32)
+  TAKE(w1, 32 * c.LDW)       // [W1; W1e] row-major, zero-padded to KP
+  TAKE(w2, 1024)             // [W2 | W2e] (conv2 / conv2_ext .fc.weight)
+  TAKE(fc2, OUT * 128 + OUT) // fc2.weight rows, then fc2.bias
+  TAKE(x, N * c.XS)
+  TAKE(z, N * c.LDW)
   TAKE(h, N * 32)
   TAKE(rp, N + 1)
   TAKE(col, E)
-  if (alias) {
-    c.trp = c.rp;
-    c.tcol = c.col;
-  } else {
-    TAKE(trp, N + 1)
-    TAKE(tcol, E)
-  }
   TAKE(m0p, K0 + 1)
   TAKE(m0i, N)
   TAKE(p1, K0 * 32)
@@ -99,7 +98,7 @@ __host__ __device__ inline Carve carve(int N, int E, int F, int K0, int P1, int 
   TAKE(nt, K1 * 64)
   TAKE(head, HEADW)
   TAKE(dgp, NW * 64)
-  TAKE(red, imax(c.S * 32 * c.KP, 2 * NT))
+  TAKE(red, 2 * NT)
 #undef TAKE
   c.total = o;
   return c;
@@ -118,39 +117,93 @@ struct GinetArgs {
 __device__ __forceinline__ float relu_keepnan(float v) { return (v <= 0.f) ? 0.f : v; }
 __device__ __forceinline__ float relu_bwd(float out, float g) { return (out <= 0.f) ? 0.f : g; }
 
-template <typename T>
-__device__ __forceinline__ void copy_in(T* dst, const T* __restrict__ src, int n) {
-  for (int i = threadIdx.x; i < n; i += NT) dst[i] = src[i];
-}
-
-__device__ __forceinline__ bool keep_unit(const dr_ginet_pass& p, int b, int r) {
+__device__ __forceinline__ bool keep_unit(const dr_ginet_pass& p, uint64_t offset, int b, int r) {
   if (p.use_dropout == DR_DROPOUT_MASK) return p.mask[(int64_t)b * 128 + r] != 0;
-  return dr_uniform(p.drop_seed, p.drop_offset, (uint32_t)(b * 128 + r)) >= p.drop_p;
+  return dr_uniform(p.drop_seed, offset, (uint32_t)(b * 128 + r)) >= p.drop_p;
 }
 
-// dst[i,:32] = sum over CSR row i of src[col[e],:32]; 8 lanes per row, float4 each.
-__device__ __forceinline__ void csr_gather32(const int* rp, const int* col, const float* src, float* dst, int n,
-                                             bool relu) {
-  const int c4 = (threadIdx.x & 7) * 4;
-  for (int i = threadIdx.x >> 3; i < n; i += NT / 8) {
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#define AS1(p) ((const __attribute__((address_space(1))) void*)(p))
+#define AS3(p) ((__attribute__((address_space(3))) void*)(p))
+
+// Asynchronous global->LDS copy of n 4-byte words (global_load_lds_dword: one
+// wave instruction moves 256 contiguous bytes, no VGPR round trip).  The LDS
+// base handed to the instruction (M0) is wave-uniform; lane l lands at base+4l.
+__device__ __forceinline__ void dma_words(void* lds_dst, const void* gsrc, int n) {
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(gsrc);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(lds_dst);
+  for (int base = wave * 64; base < n; base += NT)
+    if (base + lane < n) __builtin_amdgcn_global_load_lds(AS1(src + base + lane), AS3(dst + base), 4, 0, 0);
+}
+
+// Same with 16-byte lanes (global_load_lds_dwordx4, 1 KiB per wave
+// instruction).  Source and destination 16-byte aligned; n4 = 16-byte units.
+__device__ __forceinline__ void dma_x4(void* lds_dst, const void* gsrc, int n4) {
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint4* src = reinterpret_cast<const uint4*>(gsrc);
+  uint4* dst = reinterpret_cast<uint4*>(lds_dst);
+  for (int base = wave * 64; base < n4; base += NT)
+    if (base + lane < n4) __builtin_amdgcn_global_load_lds(AS1(src + base + lane), AS3(dst + base), 16, 0, 0);
+}
+
+// Row-wise DMA of a [rows, width] global matrix into LDS rows of stride ld.
+__device__ __forceinline__ void dma_rows(float* lds_dst, int ld, const float* gsrc, int rows, int width) {
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (int r = wave; r < rows; r += NW)
+    for (int c0 = 0; c0 < width; c0 += 64)
+      if (c0 + lane < width)
+        __builtin_amdgcn_global_load_lds(AS1(gsrc + (int64_t)r * width + c0 + lane), AS3(lds_dst + r * ld + c0), 4, 0,
+                                         0);
+}
+
+__device__ __forceinline__ float4 f4add(float4 a, float4 v) {
+  return make_float4(a.x + v.x, a.y + v.y, a.z + v.z, a.w + v.w);
+}
+
+// Z[i, :XS] = sum over CSR row i of X[col[e], :XS] (edges in CSR order, i.e.
+// the order torch_scatter's CPU scatter_add_ visits them).  4 lanes per row,
+// float4 chunks c4 = lane&3, +4, ...; edges unrolled by 4 so 4 index reads and
+// then their row reads are in flight together.  Z rows have the odd stride ldz.
+__device__ __forceinline__ void gather_rows(const int* rp, const int* col, const float* X, int XS, float* Z, int ldz,
+                                            int n) {
+  const int nch = XS >> 2;
+  const int sub = threadIdx.x & 3;
+  for (int i = threadIdx.x >> 2; i < n; i += NT / 4) {
     const int eb = rp[i], ee = rp[i + 1];
-    for (int e = eb; e < ee; ++e) {
-      const float4 v = *reinterpret_cast<const float4*>(&src[col[e] * 32 + c4]);
-      acc.x += v.x;
-      acc.y += v.y;
-      acc.z += v.z;
-      acc.w += v.w;
+    for (int ch = sub; ch < nch; ch += 4) {
+      const int c4 = ch * 4;
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      int e = eb;
+      for (; e + 4 <= ee; e += 4) {
+        const int j0 = col[e], j1 = col[e + 1], j2 = col[e + 2], j3 = col[e + 3];
+        const float4 v0 = *reinterpret_cast<const float4*>(&X[j0 * XS + c4]);
+        const float4 v1 = *reinterpret_cast<const float4*>(&X[j1 * XS + c4]);
+        const float4 v2 = *reinterpret_cast<const float4*>(&X[j2 * XS + c4]);
+        const float4 v3 = *reinterpret_cast<const float4*>(&X[j3 * XS + c4]);
+        acc = f4add(f4add(f4add(f4add(acc, v0), v1), v2), v3);
+      }
+      for (; e < ee; ++e) acc = f4add(acc, *reinterpret_cast<const float4*>(&X[col[e] * XS + c4]));
+      float* zr = Z + i * ldz + c4;
+      zr[0] = acc.x;
+      zr[1] = acc.y;
+      zr[2] = acc.z;
+      zr[3] = acc.w;
     }
-    if (relu) {
-      acc.x = relu_keepnan(acc.x);
-      acc.y = relu_keepnan(acc.y);
-      acc.z = relu_keepnan(acc.z);
-      acc.w = relu_keepnan(acc.w);
-    }
-    *reinterpret_cast<float4*>(&dst[i * 32 + c4]) = acc;
   }
 }
+
+#ifdef DR_STAMPS
+#define STAMP(i)                                                                                  \
+  do {                                                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    if (tid == 0 && a.p.stamps) a.p.stamps[(int64_t)b * 32 + (i)] = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+  } while (0)
+#else
+#define STAMP(i) \
+  do {           \
+  } while (0)
+#endif
 
 __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -162,8 +215,8 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   const int g = a.gids[b];
   const int64_t n0 = s.node_off[g];
   const int N = (int)(s.node_off[g + 1] - n0);
-  const int64_t e0 = s.edge_off[g];
-  const int E = (int)(s.edge_off[g + 1] - e0);
+  const int E = (int)(s.edge_off[g + 1] - s.edge_off[g]);
+  const int64_t ec0 = s.col_off[g];
   const int64_t k00 = s.k0_off[g];
   const int K0 = (int)(s.k0_off[g + 1] - k00);
   const int64_t q0 = s.p1_off[g];
@@ -172,18 +225,18 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   const int K1 = (int)(s.k1_off[g + 1] - k10);
   const int F = s.n_feat;
   const int alias = s.transpose_aliased;
-  const Carve c = carve(N, E, F, K0, P1, K1, alias);
-  const int KP = c.KP, LDX = c.LDX;
   const int OUT = a.p.out_dim;
+  const Carve c = carve(N, E, F, K0, P1, K1, alias, OUT);
+  const int KP = c.KP, LDW = c.LDW, XS = c.XS;
 
-  float* sWT = lds + c.wt;
+  float* sW1 = lds + c.w1;
+  float* sW2 = lds + c.w2;
+  float* sFc2 = lds + c.fc2;
   float* sX = lds + c.x;
-  float* sY = lds + c.y;
+  float* sZ = lds + c.z;
   float* sH = lds + c.h;
   int* srp = reinterpret_cast<int*>(lds + c.rp);
   int* scol = reinterpret_cast<int*>(lds + c.col);
-  int* strp = reinterpret_cast<int*>(lds + c.trp);
-  int* stcol = reinterpret_cast<int*>(lds + c.tcol);
   int* sm0p = reinterpret_cast<int*>(lds + c.m0p);
   int* sm0i = reinterpret_cast<int*>(lds + c.m0i);
   float* sP1 = lds + c.p1;
@@ -210,74 +263,106 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   float* sDGp = lds + c.dgp;
   float* sRed = lds + c.red;
 
+  STAMP(0);
   // ---------------- stage the graph into LDS --------------------------------
-  for (int p = tid; p < KP * 32; p += NT) {
-    const int k = p >> 5, ch = p & 31;
-    float v = 0.f;
-    if (k < F) v = (ch < 16) ? a.w.w1[ch * F + k] : a.w.w1e[(ch - 16) * F + k];
-    sWT[p] = v;
-  }
+  // Head weights go to registers first (their latency hides under the DMA);
+  // the graph and the other weights are DMA'd straight into LDS.
+  float fc1_row[8], fc1_col[8], fc1_bias;
   {
-    const float* __restrict__ xg = s.x + n0 * (int64_t)F;
-    for (int p = tid; p < N * F; p += NT) {
-      const int i = p / F;
-      sX[i * LDX + (p - i * F)] = xg[p];
-    }
+    const int r = tid >> 3, part = tid & 7;
+    const float4 u0 = *reinterpret_cast<const float4*>(a.w.fc1w + r * 64 + part * 8);
+    const float4 u1 = *reinterpret_cast<const float4*>(a.w.fc1w + r * 64 + part * 8 + 4);
+    fc1_row[0] = u0.x; fc1_row[1] = u0.y; fc1_row[2] = u0.z; fc1_row[3] = u0.w;
+    fc1_row[4] = u1.x; fc1_row[5] = u1.y; fc1_row[6] = u1.z; fc1_row[7] = u1.w;
+    fc1_bias = a.w.fc1b[r];
+    const int o = tid & 63, rc = tid >> 6;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fc1_col[j] = a.w.fc1w[(rc * 8 + j) * 64 + o];
+  }
+  const float y_g = s.y[g];
+  uint64_t drop_offset = a.p.drop_offset;
+  if (a.p.step_counter) {
+    drop_offset = (uint64_t)a.p.step_counter[0];
+    if (b == 0 && tid == 0) a.p.step_counter[1] = (int64_t)drop_offset;  // snapshot for the update kernel
+  }
+  dma_x4(sX, s.x + n0 * (int64_t)XS, N * XS / 4);
+  dma_x4(scol, s.col + ec0, (E + 3) / 4);
+  dma_words(srp, s.rowptr + n0 + g, N + 1);
+  dma_rows(sW1, LDW, a.w.w1, 16, F);
+  dma_rows(sW1 + 16 * LDW, LDW, a.w.w1e, 16, F);
+  dma_words(sW2, a.w.w2, 512);
+  dma_words(sW2 + 512, a.w.w2e, 512);
+  dma_words(sFc2, a.w.fc2w, OUT * 128);
+  dma_words(sFc2 + OUT * 128, a.w.fc2b, OUT);
+  dma_words(sm0p, s.m0_ptr + k00 + g, K0 + 1);
+  dma_words(sm0i, s.m0_idx + n0, N);
+  dma_words(sp1rp, s.p1_rowptr + k00 + g, K0 + 1);
+  dma_words(sp1c, s.p1_col + q0, P1);
+  if (!alias) {
+    dma_words(sp1trp, s.p1t_rowptr + k00 + g, K0 + 1);
+    dma_words(sp1tc, s.p1t_col + q0, P1);
+  }
+  dma_words(sm1p, s.m1_ptr + k10 + g, K1 + 1);
+  dma_words(sm1i, s.m1_idx + k00, K0);
+  {  // zero the K padding of W (cols F..KP) and of Z (cols XS..KP; X's own pad is zero)
     const int padw = KP - F;
-    if (padw > 0)
-      for (int p = tid; p < N * padw; p += NT) {
-        const int i = p / padw;
-        sX[i * LDX + F + (p - i * padw)] = 0.f;
-      }
+    for (int p = tid; p < 32 * padw; p += NT) {
+      const int i = p / padw;
+      sW1[i * LDW + F + (p - i * padw)] = 0.f;
+    }
+    const int padz = KP - XS;
+    for (int p = tid; p < N * padz; p += NT) {
+      const int i = p / padz;
+      sZ[i * LDW + XS + (p - i * padz)] = 0.f;
+    }
   }
-  copy_in(srp, s.rowptr + n0 + g, N + 1);
-  copy_in(scol, s.col + e0, E);
-  if (!alias) {
-    copy_in(strp, s.t_rowptr + n0 + g, N + 1);
-    copy_in(stcol, s.t_col + e0, E);
-  }
-  copy_in(sm0p, s.m0_ptr + k00 + g, K0 + 1);
-  copy_in(sm0i, s.m0_idx + n0, N);
-  copy_in(sp1rp, s.p1_rowptr + k00 + g, K0 + 1);
-  copy_in(sp1c, s.p1_col + q0, P1);
-  if (!alias) {
-    copy_in(sp1trp, s.p1t_rowptr + k00 + g, K0 + 1);
-    copy_in(sp1tc, s.p1t_col + q0, P1);
-  }
-  copy_in(sm1p, s.m1_ptr + k10 + g, K1 + 1);
-  copy_in(sm1i, s.m1_idx + k00, K0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  // ---------------- conv1 node GEMM on MFMA: Y = X [W1;W1e]^T (ginet.py:45) -
+  STAMP(1);
+  // ---------------- conv1 aggregation first: Z = A X  (ginet.py:45,58) -----
+  // A (X W^T) = (A X) W^T: aggregating the F input features first lets the
+  // backward use dW1 = sum_k v_k (A X)[arg_k] (the depth-0 max pool routes
+  // each channel's gradient to one member per cluster) with no backward gather.
+  gather_rows(srp, scol, sX, XS, sZ, LDW, N);
+  __syncthreads();
+
+  STAMP(2);
+  // ---------------- conv1 node GEMM on MFMA + relu: H = relu(Z [W1;W1e]^T) --
   {
     const int li = lane & 15, kq = lane >> 4;
     for (int t = wave; t * 16 < N; t += NW) {
       const int r0 = t * 16;
-      const int ar = r0 + li;
+      const int ar = min(r0 + li, N - 1);  // rows past N compute garbage that is never stored
       floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-      for (int k = 0; k < KP; k += 4) {
-        const float av = (ar < N) ? sX[ar * LDX + k + kq] : 0.f;
-        const float b0 = sWT[(k + kq) * 32 + li];
-        const float b1 = sWT[(k + kq) * 32 + 16 + li];
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b0, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b1, acc1, 0, 0, 0);
+      for (int k = 0; k < KP; k += 16) {
+        float av[4], b0[4], b1[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int kk = k + 4 * u + kq;
+          av[u] = sZ[ar * LDW + kk];
+          b0[u] = sW1[li * LDW + kk];
+          b1[u] = sW1[(16 + li) * LDW + kk];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], b0[u], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], b1[u], acc1, 0, 0, 0);
+        }
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = r0 + kq * 4 + r;
         if (row < N) {
-          sY[row * 32 + li] = acc0[r];
-          sY[row * 32 + 16 + li] = acc1[r];
+          sH[row * 32 + li] = relu_keepnan(acc0[r]);
+          sH[row * 32 + 16 + li] = relu_keepnan(acc1[r]);
         }
       }
     }
   }
   __syncthreads();
 
-  // ---------------- conv1 aggregation + relu: H = relu(A Y)  (ginet.py:58,96)
-  csr_gather32(srp, scol, sY, sH, N, true);
-  __syncthreads();
-
+  STAMP(3);
   // ---------------- depth-0 community pooling: torch_scatter scatter_max ----
   // (community_pooling.py:209): strict '>' from lowest(), members in node
   // order => first max wins, NaN never enters, empty -> 0 with no arg.
@@ -294,7 +379,16 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
       const int qb = mb + (cnt * sl) / S1, qe = mb + (cnt * (sl + 1)) / S1;
       float best = LOWEST;
       int arg = N;
-      for (int m = qb; m < qe; ++m) {
+      int m = qb;
+      for (; m + 4 <= qe; m += 4) {
+        const int i0 = sm0i[m], i1 = sm0i[m + 1], i2 = sm0i[m + 2], i3 = sm0i[m + 3];
+        const float v0 = sH[i0 * 32 + ch], v1 = sH[i1 * 32 + ch], v2 = sH[i2 * 32 + ch], v3 = sH[i3 * 32 + ch];
+        if (v0 > best) { best = v0; arg = i0; }
+        if (v1 > best) { best = v1; arg = i1; }
+        if (v2 > best) { best = v2; arg = i2; }
+        if (v3 > best) { best = v3; arg = i3; }
+      }
+      for (; m < qe; ++m) {
         const int i = sm0i[m];
         const float v = sH[i * 32 + ch];
         if (v > best) {
@@ -322,10 +416,11 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   }
   __syncthreads();
 
+  STAMP(4);
   // ---------------- conv2 node GEMM on the pooled graph (ginet.py:101,112) --
   for (int p = tid; p < K0 * 64; p += NT) {
     const int k = p >> 6, o = p & 63, br = o >> 5;
-    const float* __restrict__ wr = br ? (a.w.w2e + (o - 32) * 16) : (a.w.w2 + o * 16);
+    const float* wr = sW2 + o * 16;  // rows 0..31 = W2, 32..63 = W2e
     const float* pr = sP1 + k * 32 + br * 16;
     float acc = 0.f;
 #pragma unroll
@@ -341,6 +436,7 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   }
   __syncthreads();
 
+  STAMP(5);
   // ---------------- depth-1 max_pool_x: scatter_reduce amax (ginet.py:103) --
   // NaN propagates; remember the tie count for the even-split backward.
   for (int p = tid; p < K1 * 64; p += NT) {
@@ -358,6 +454,7 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   }
   __syncthreads();
 
+  STAMP(6);
   // ---------------- per-graph mean (scatter_mean, ginet.py:117-118) ----------
   if (tid < 64) {
     float acc = 0.f;
@@ -366,46 +463,47 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   }
   __syncthreads();
 
+  STAMP(7);
   // ---------------- head: fc1 -> relu -> dropout -> fc2 (ginet.py:120-123) --
   {
     const int r = tid >> 3, part = tid & 7;  // 8 lanes per fc1 row
-    const float* __restrict__ wr = a.w.fc1w + r * 64 + part * 8;
     float acc = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc = fmaf(sG[part * 8 + j], wr[j], acc);
+    for (int j = 0; j < 8; ++j) acc = fmaf(sG[part * 8 + j], fc1_row[j], acc);
     acc += __shfl_xor(acc, 1, 64);
     acc += __shfl_xor(acc, 2, 64);
     acc += __shfl_xor(acc, 4, 64);
     if (part == 0) {
-      acc += a.w.fc1b[r];
+      acc += fc1_bias;
       sHpre[r] = acc;
       const float hh = relu_keepnan(acc);
       sHh[r] = hh;
       float hd = hh;
-      if (a.p.use_dropout) hd = (keep_unit(a.p, b, r) ? hh : 0.f) * a.p.drop_scale;
+      if (a.p.use_dropout) hd = (keep_unit(a.p, drop_offset, b, r) ? hh : 0.f) * a.p.drop_scale;
       sHd[r] = hd;
     }
   }
   __syncthreads();
   for (int q = wave; q < OUT; q += NW) {
-    const float* __restrict__ wr = a.w.fc2w + q * 128;
+    const float* wr = sFc2 + q * 128;
     float v = fmaf(sHd[lane], wr[lane], sHd[lane + 64] * wr[lane + 64]);
     v = dr_wave_sum(v);
-    if (lane == 0) sDout[q] = v + a.w.fc2b[q];  // logits parked in sDout
+    if (lane == 0) sDout[q] = v + sFc2[OUT * 128 + q];  // logits parked in sDout
   }
   __syncthreads();
   if ((a.p.flags & DR_PASS_FORWARD) && tid < OUT) a.p.out[(int64_t)b * OUT + tid] = sDout[tid];
   if (!(a.p.flags & DR_PASS_BACKWARD)) return;
   __syncthreads();
 
+  STAMP(8);
   // ---------------- loss gradient (trainer.py:688-689) ----------------------
   if (tid == 0) {
     if (a.p.loss_kind == DR_LOSS_MSE) {
-      const float d = sDout[0] - s.y[g];
+      const float d = sDout[0] - y_g;
       if (a.p.loss_per_graph) a.p.loss_per_graph[b] = d * d;
       sDout[0] = 2.f * d * a.p.loss_scale;
     } else if (a.p.loss_kind == DR_LOSS_CE) {
-      const int yi = (int)s.y[g];
+      const int yi = (int)y_g;
       float mx = sDout[0];
       for (int q = 1; q < OUT; ++q) mx = fmaxf(mx, sDout[q]);
       float se = 0.f;
@@ -420,11 +518,12 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   }
   __syncthreads();
 
+  STAMP(9);
   // ---------------- head backward -------------------------------------------
   if (tid < 128) {
     float acc = 0.f;
-    for (int q = 0; q < OUT; ++q) acc = fmaf(a.w.fc2w[q * 128 + tid], sDout[q], acc);
-    if (a.p.use_dropout) acc = (keep_unit(a.p, b, tid) ? acc : 0.f) * a.p.drop_scale;
+    for (int q = 0; q < OUT; ++q) acc = fmaf(sFc2[q * 128 + tid], sDout[q], acc);
+    if (a.p.use_dropout) acc = (keep_unit(a.p, drop_offset, b, tid) ? acc : 0.f) * a.p.drop_scale;
     sDh[tid] = relu_bwd(sHh[tid], acc);
   }
   __syncthreads();
@@ -432,7 +531,7 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
     const int o = tid & 63, rc = tid >> 6;  // 16 chunks of 8 fc1 rows
     float acc = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc = fmaf(a.w.fc1w[(rc * 8 + j) * 64 + o], sDh[rc * 8 + j], acc);
+    for (int j = 0; j < 8; ++j) acc = fmaf(fc1_col[j], sDh[rc * 8 + j], acc);
     sDGp[rc * 64 + o] = acc;
   }
   __syncthreads();
@@ -453,6 +552,7 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   }
   __syncthreads();
 
+  STAMP(10);
   // ---------------- depth-1 pooling + mean backward -------------------------
   // scatter_mean: grad/count; scatter_reduce amax: grad split evenly over the
   // members equal to the max ((src==max) * grad/ties, so NaN stays NaN).
@@ -467,6 +567,7 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
     }
   }
   __syncthreads();
+  STAMP(11);
   // dY2 = A1^T dS2 (pooled graph, transposed CSR)  -> reuse sY2
   for (int p = tid; p < K0 * 64; p += NT) {
     const int j = p >> 6, o = p & 63;
@@ -475,7 +576,9 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
     sY2[p] = acc;
   }
   __syncthreads();
-  // conv2 weight-gradient partials and dP1
+  STAMP(12);
+  // conv2 weight-gradient partials, and the gradient reaching each depth-0
+  // arg member through relu (v = relu'(H1[arg]) * dP1)
   {
     const int SS = DR_SLAB_STRIDE(F);
     float* slab = a.p.slab + (int64_t)b * SS + 32 * F;
@@ -488,59 +591,33 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   }
   for (int p = tid; p < K0 * 32; p += NT) {
     const int k = p >> 5, ch = p & 31, br = ch >> 4, j = ch & 15;
-    const float* __restrict__ wb = br ? a.w.w2e : a.w.w2;
+    const float* wb = sW2 + br * 512;
     float acc = 0.f;
+#pragma unroll 8
     for (int o = 0; o < 32; ++o) acc = fmaf(sY2[k * 64 + br * 32 + o], wb[o * 16 + j], acc);
-    // depth-0 scatter_max backward goes to the arg member only; fold the
-    // conv1 relu backward in here (needs H1 at that member).
     const int i = sA1[p];
     sdP1[p] = (i < N) ? relu_bwd(sH[i * 32 + ch], acc) : 0.f;
   }
   __syncthreads();
-  for (int p = tid; p < N * 32; p += NT) sH[p] = 0.f;
-  __syncthreads();
-  for (int p = tid; p < K0 * 32; p += NT) {
-    const int i = sA1[p];
-    if (i < N) sH[i * 32 + (p & 31)] = sdP1[p];
-  }
-  __syncthreads();
 
-  // ---------------- conv1 backward: dY = A^T dS  -> reuse sY ---------------
-  csr_gather32(strp, stcol, sH, sY, N, false);
-  __syncthreads();
-
-  // ---------------- dW1cat = dY^T X on MFMA, node range split in S slices ---
-  {
-    const int li = lane & 15, kq = lane >> 4;
-    const int tile = wave % c.ntile, sl = wave / c.ntile;
-    if (sl < c.S) {
-      const int ct = tile & 1, kt = tile >> 1;
-      const int nb = (N * sl) / c.S, ne = (N * (sl + 1)) / c.S;
-      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-      for (int n = nb; n < ne; n += 4) {
-        const int node = n + kq;
-        const bool ok = node < ne;
-        const float av = ok ? sY[node * 32 + ct * 16 + li] : 0.f;
-        const float bv = ok ? sX[node * LDX + kt * 16 + li] : 0.f;
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
-      }
-      float* red = sRed + sl * 32 * KP;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) red[(ct * 16 + kq * 4 + r) * KP + kt * 16 + li] = acc[r];
-    }
-  }
-  __syncthreads();
+  STAMP(13);
+  // ---------------- dW1cat[c, :] = sum_k v[k, c] * Z[arg(k, c), :] ---------
+  // (dH1 is non-zero only at the depth-0 arg members, so dS1^T (A X) needs
+  // K0 rows of Z per channel instead of a backward gather over all edges.)
   {
     const int SS = DR_SLAB_STRIDE(F);
     float* slab = a.p.slab + (int64_t)b * SS;
-    const int plane = 32 * KP;
     for (int p = tid; p < 32 * F; p += NT) {
-      const int ch = p / F, k = p - ch * F;
+      const int ch = p / F, kk = p - ch * F;
       float acc = 0.f;
-      for (int sl = 0; sl < c.S; ++sl) acc += sRed[sl * plane + ch * KP + k];
+      for (int k = 0; k < K0; ++k) {
+        const int i = sA1[k * 32 + ch];
+        if (i < N) acc = fmaf(sdP1[k * 32 + ch], sZ[i * LDW + kk], acc);
+      }
       slab[p] = acc;
     }
   }
+  STAMP(14);
 }
 
 // ---------------------------------------------------------------------------
@@ -560,43 +637,43 @@ struct ReduceArgs {
   int32_t off[DR_GINET_NPARAM + 1];
 };
 
-constexpr int RP = 32;  // parameter elements per block
+constexpr int RP = 64;  // parameter elements per block
 constexpr int RC = 8;   // batch chunks per block
+constexpr int RU = 8;   // batch rows per chunk issued together (predicated)
 
+// Sum over b in [b0, b1) of one gradient element; RU rows per group with all
+// their loads issued before the adds (the loads are independent; a serial
+// chain would pay one L2/MALL round trip per row).
 __device__ float grad_partial(const ReduceArgs& a, int pi, int e, int b0, int b1) {
   const int F = a.F;
   const int64_t SS = DR_SLAB_STRIDE(F);
   const int64_t HS = DR_HEAD_STRIDE(a.OUT);
-  float acc = 0.f;
+  const float* p1 = nullptr;  // first operand row 0, stride st1
+  const float* p2 = nullptr;  // optional second operand (outer products)
+  int64_t st = 0;
   switch (pi) {
-    case 0:  // conv1.fc.weight [16,F] = rows 0..15 of the slab's [32][F]
-      for (int b = b0; b < b1; ++b) acc += a.slab[b * SS + e];
-      break;
-    case 6:  // conv1_ext.fc.weight = rows 16..31
-      for (int b = b0; b < b1; ++b) acc += a.slab[b * SS + 16 * F + e];
-      break;
-    case 3:  // conv2.fc.weight [32,16]
-      for (int b = b0; b < b1; ++b) acc += a.slab[b * SS + 32 * F + e];
-      break;
-    case 9:  // conv2_ext.fc.weight
-      for (int b = b0; b < b1; ++b) acc += a.slab[b * SS + 32 * F + 512 + e];
-      break;
-    case 12: {  // fc1.weight [128,64] = sum_b dh ⊗ g
-      const int r = e >> 6, o = e & 63;
-      for (int b = b0; b < b1; ++b) acc = fmaf(a.head[b * HS + 192 + r], a.head[b * HS + o], acc);
-    } break;
-    case 13:  // fc1.bias
-      for (int b = b0; b < b1; ++b) acc += a.head[b * HS + 192 + e];
-      break;
-    case 14: {  // fc2.weight [out,128] = sum_b dout ⊗ hd
-      const int q = e >> 7, r = e & 127;
-      for (int b = b0; b < b1; ++b) acc = fmaf(a.head[b * HS + 320 + q], a.head[b * HS + 64 + r], acc);
-    } break;
-    case 15:
-      for (int b = b0; b < b1; ++b) acc += a.head[b * HS + 320 + e];
-      break;
-    default:  // fc_edge_attr / fc_attention: exact zeros (softmax over size-1 dim)
-      break;
+    case 0: p1 = a.slab + e; st = SS; break;                       // conv1.fc.weight: slab rows 0..15
+    case 6: p1 = a.slab + 16 * F + e; st = SS; break;              // conv1_ext.fc.weight: rows 16..31
+    case 3: p1 = a.slab + 32 * F + e; st = SS; break;              // conv2.fc.weight
+    case 9: p1 = a.slab + 32 * F + 512 + e; st = SS; break;        // conv2_ext.fc.weight
+    case 12: p1 = a.head + 192 + (e >> 6); p2 = a.head + (e & 63); st = HS; break;      // fc1.weight = sum dh (x) g
+    case 13: p1 = a.head + 192 + e; st = HS; break;                // fc1.bias
+    case 14: p1 = a.head + 320 + (e >> 7); p2 = a.head + 64 + (e & 127); st = HS; break;  // fc2.weight = sum dout (x) hd
+    case 15: p1 = a.head + 320 + e; st = HS; break;                // fc2.bias
+    default: return 0.f;  // fc_edge_attr / fc_attention: exact zeros (softmax over a size-1 dim)
+  }
+  float acc = 0.f;
+  for (int bb = b0; bb < b1; bb += RU) {
+    float u[RU], v[RU];
+#pragma unroll
+    for (int k = 0; k < RU; ++k) {
+      const bool ok = bb + k < b1;
+      const int64_t r = (int64_t)(ok ? bb + k : b0) * st;
+      u[k] = ok ? p1[r] : 0.f;
+      v[k] = (ok && p2) ? p2[r] : 1.f;
+    }
+#pragma unroll
+    for (int k = 0; k < RU; ++k) acc = p2 ? fmaf(u[k], v[k], acc) : acc + u[k];
   }
   return acc;
 }
@@ -605,10 +682,19 @@ __global__ void __launch_bounds__(RP* RC) ginet_reduce_kernel(ReduceArgs a) {
   __shared__ float part[RC][RP];
   const int lp = threadIdx.x % RP, ch = threadIdx.x / RP;
   const int gi = blockIdx.x * RP + lp;
-  if (blockIdx.x == 0 && threadIdx.x == 0 && a.lpg && a.loss_out) {
-    float acc = 0.f;
-    for (int b = 0; b < a.B; ++b) acc += a.lpg[b];
-    a.loss_out[0] = acc * a.loss_scale;
+  if (blockIdx.x == 0 && threadIdx.x < 64 && a.lpg && a.loss_out) {
+    float acc = 0.f;  // lane-strided partial sums, then a fixed-order wave reduction
+    for (int b = threadIdx.x; b < a.B; b += 64) acc += a.lpg[b];
+    acc = dr_wave_sum(acc);
+    if (threadIdx.x == 0) a.loss_out[0] = acc * a.loss_scale;
+  }
+  // Adam step number and bias corrections (host-given, or from the device counter)
+  float bc1 = a.adam.bias_c1, bc2s = a.adam.bias_c2_sqrt;
+  if (a.adam.step_counter) {
+    const int64_t t = a.adam.step_counter[1] + 1;
+    bc1 = 1.f - powf(a.adam.beta1, (float)t);
+    bc2s = sqrtf(1.f - powf(a.adam.beta2, (float)t));
+    if (a.adam.enabled && blockIdx.x == 0 && threadIdx.x == 0) a.adam.step_counter[0] = t;
   }
   const bool live = gi < a.off[DR_GINET_NPARAM];
   int pi = 0;
@@ -642,16 +728,16 @@ __global__ void __launch_bounds__(RP* RC) ginet_reduce_kernel(ReduceArgs a) {
     const float vv = fmaf((1.f - a.adam.beta2) * gr, gr, *v * a.adam.beta2);
     *m = mv;
     *v = vv;
-    const float denom = sqrtf(vv) / a.adam.bias_c2_sqrt + a.adam.eps;
-    *p = *p - (a.adam.lr / a.adam.bias_c1) * (mv / denom);
+    const float denom = sqrtf(vv) / bc2s + a.adam.eps;
+    *p = *p - (a.adam.lr / bc1) * (mv / denom);
   }
 }
 
 }  // namespace
 
 extern "C" int64_t dr_ginet_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_feat, int32_t k0, int32_t p1_edges,
-                                      int32_t k1, int32_t transpose_aliased) {
-  return 4LL * carve(n_nodes, n_edges, n_feat, k0, p1_edges, k1, transpose_aliased).total;
+                                      int32_t k1, int32_t transpose_aliased, int32_t out_dim) {
+  return 4LL * carve(n_nodes, n_edges, n_feat, k0, p1_edges, k1, transpose_aliased, out_dim).total;
 }
 
 extern "C" int dr_ginet_graph_pass(const dr_graph_store* store, const int32_t* gids, int32_t n_batch,

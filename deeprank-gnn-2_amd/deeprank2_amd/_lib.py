@@ -11,7 +11,7 @@ from __future__ import annotations
 import ctypes
 import os
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdeeprank2_amd.so")
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), os.environ.get("DR_LIB_NAME", "libdeeprank2_amd.so"))
 
 DR_PASS_FORWARD = 1
 DR_PASS_BACKWARD = 2
@@ -37,11 +37,12 @@ class GraphStoreC(ctypes.Structure):
     _fields_ = [
         ("n_graphs", ctypes.c_int32),
         ("n_feat", ctypes.c_int32),
+        ("x_stride", ctypes.c_int32),
         ("transpose_aliased", ctypes.c_int32),
-        ("pad0", ctypes.c_int32),
         ("x", VP),
         ("node_off", VP),
         ("edge_off", VP),
+        ("col_off", VP),
         ("rowptr", VP),
         ("col", VP),
         ("t_rowptr", VP),
@@ -84,6 +85,8 @@ class GinetPassC(ctypes.Structure):
         ("loss_per_graph", VP),
         ("slab", VP),
         ("head", VP),
+        ("stamps", VP),
+        ("step_counter", VP),
     ]
 
 
@@ -97,6 +100,7 @@ class AdamC(ctypes.Structure):
         ("bias_c1", ctypes.c_float),
         ("bias_c2_sqrt", ctypes.c_float),
         ("enabled", ctypes.c_int32),
+        ("step_counter", VP),
     ]
 
 
@@ -113,7 +117,7 @@ class ParamTableC(ctypes.Structure):
 # (name, restype, argtypes) for every entry of include/deeprank2_amd.h
 SIGNATURES = [
     ("dr_ginet_graph_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(GinetWeightsC), ctypes.POINTER(GinetPassC), ctypes.c_int32, VP]),
-    ("dr_ginet_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 7),
+    ("dr_ginet_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 8),
     ("dr_ginet_reduce_update", ctypes.c_int, [ctypes.POINTER(ParamTableC), ctypes.c_int32, ctypes.c_int32, VP, VP, ctypes.c_int32, ctypes.POINTER(AdamC), VP, ctypes.c_float, VP, VP]),
     ("dr_csr_from_coo", ctypes.c_int, [VP, VP, ctypes.c_int64, ctypes.c_int32, VP, VP, VP, VP, VP]),
     ("dr_spmm_csr", ctypes.c_int, [VP, VP, VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP, VP]),

@@ -8,6 +8,11 @@
    applies ``torch.optim.Adam`` (lr, betas, eps, L2 ``weight_decay`` as
    ``Trainer.configure_optimizers`` sets them, trainer.py:401-428).
 
+The dropout offset and Adam's step number live in a device counter that the
+two kernels advance themselves, so a step's launch arguments are constant and
+the whole step can be captured once per mini-batch and replayed as a HIP graph
+(``capture``).
+
 Data parallel (one process per GPU, RCCL over xGMI): every rank runs step 1 on
 its shard of the global batch with the loss scaled by 1/B_global, the 16
 gradients (one flat 42.7 KB buffer for GINet(30,1,3)) are SUM-all-reduced, then
@@ -16,16 +21,14 @@ step 2 runs Adam from the reduced gradients.  That is the only collective.
 
 from __future__ import annotations
 
-import math
-
 import torch
 
 from deeprank2_amd import _lib
-from deeprank2_amd.neuralnets.gnn.ginet import BatchHandle, Dropout, GINet, graph_pass, head_stride, reduce_update, slab_stride
+from deeprank2_amd.neuralnets.gnn.ginet import BatchHandle, GINet, head_stride, slab_stride, weights_c
 
 
 class GINetTrainStep:
-    def __init__(self, model: GINet, lr=1e-3, weight_decay=1e-5, betas=(0.9, 0.999), eps=1e-8, loss="mse", class_weights=None, process_group=None):
+    def __init__(self, model: GINet, lr=1e-3, weight_decay=1e-5, betas=(0.9, 0.999), eps=1e-8, loss="mse", class_weights=None, process_group=None, max_batch=64):
         self.model = model
         self.params = model.ordered_params()
         for p in self.params:
@@ -36,21 +39,27 @@ class GINetTrainStep:
         self.device = dev
         self.out_dim = model.output_shape
         self.lr, self.weight_decay, self.betas, self.eps = lr, weight_decay, betas, eps
+        if loss not in ("mse", "ce"):
+            msg = f"loss must be 'mse' or 'ce' (got {loss!r})"
+            raise ValueError(msg)
         self.loss = loss
         self.class_weights = None if class_weights is None else torch.as_tensor(class_weights, dtype=torch.float32, device=dev)
         self.pg = process_group
         self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
         numel = [p.numel() for p in self.params]
         self.flat_grad = torch.zeros(sum(numel), dtype=torch.float32, device=dev)
-        self.grads = list(torch.split(self.flat_grad, numel))
-        self.grads = [g.view_as(p) for g, p in zip(self.grads, self.params)]
+        self.grads = [g.view_as(p) for g, p in zip(torch.split(self.flat_grad, numel), self.params)]
         self.states = [(torch.zeros_like(p), torch.zeros_like(p)) for p in self.params]
+        self.counter = torch.zeros(2, dtype=torch.int64, device=dev)  # [steps done = dropout offset, snapshot]
         self.step_count = 0
         self.loss_out = torch.zeros(1, dtype=torch.float32, device=dev)
         self.kernel_events = None  # list -> (start, end) HIP events around each graph pass
+        if model._drop_seed is None:
+            model._drop_seed = int(torch.randint(0, 2**62, (1,)).item())
         self._cap = 0
-        self._ensure(64)
+        self._ensure(max_batch)
 
+    # ---- persistent C structs (built once; a step makes two ctypes calls) ----
     def _ensure(self, b):
         if b <= self._cap:
             return
@@ -61,6 +70,43 @@ class GINetTrainStep:
         self.lpg = torch.empty(b, dtype=torch.float32, device=dev)
         self.out = torch.empty(b, self.out_dim, dtype=torch.float32, device=dev)
         self._cap = b
+        self._build_structs()
+
+    def _build_structs(self):
+        p = _lib.GinetPassC()
+        p.flags = _lib.DR_PASS_FORWARD | _lib.DR_PASS_BACKWARD
+        p.out_dim = self.out_dim
+        p.loss_kind = _lib.DR_LOSS_MSE if self.loss == "mse" else _lib.DR_LOSS_CE
+        if self.model.dropout > 0:
+            p.use_dropout = _lib.DR_DROPOUT_HASH
+            p.drop_p = self.model.dropout
+            p.drop_scale = 1.0 / (1.0 - self.model.dropout)
+            p.drop_seed = self.model._drop_seed
+        p.class_w = _lib.ptr(self.class_weights)
+        p.out = self.out.data_ptr()
+        p.loss_per_graph = self.lpg.data_ptr()
+        p.slab = self.slab.data_ptr()
+        p.head = self.head.data_ptr()
+        p.step_counter = self.counter.data_ptr()
+        self._pass = p
+        self._pass_nodrop = _lib.GinetPassC.from_buffer_copy(p)
+        self._pass_nodrop.use_dropout = _lib.DR_DROPOUT_OFF
+        self._w = weights_c(self.params)
+        t = _lib.ParamTableC()
+        for i, prm in enumerate(self.params):
+            t.param[i] = prm.data_ptr()
+            t.grad[i] = self.grads[i].data_ptr()
+            t.exp_avg[i] = self.states[i][0].data_ptr()
+            t.exp_avg_sq[i] = self.states[i][1].data_ptr()
+            t.numel[i] = prm.numel()
+        self._table = t
+        a = _lib.AdamC()
+        a.lr, (a.beta1, a.beta2), a.eps, a.weight_decay = self.lr, self.betas, self.eps, self.weight_decay
+        a.enabled = 1
+        a.step_counter = self.counter.data_ptr()
+        self._adam = a
+        self._adam_off = _lib.AdamC.from_buffer_copy(a)
+        self._adam_off.enabled = 0
 
     def loss_scale(self, h: BatchHandle, global_batch):
         if self.loss == "mse":
@@ -75,48 +121,66 @@ class GINetTrainStep:
             wsum = float(t.item())
         return 1.0 / wsum
 
-    def adam_c(self, enabled=True):
-        a = _lib.AdamC()
-        t = self.step_count
-        a.lr, (a.beta1, a.beta2), a.eps, a.weight_decay = self.lr, self.betas, self.eps, self.weight_decay
-        a.bias_c1 = 1.0 - self.betas[0] ** t
-        a.bias_c2_sqrt = math.sqrt(1.0 - self.betas[1] ** t)
-        a.enabled = int(enabled)
-        return a
-
     def step(self, h: BatchHandle, mask=None, global_batch=None, dropout=True):
         """One training step on the graphs of ``h``; returns (loss [1], out [B,out]) device views.
 
         Dropout (ginet.py:122): ``mask`` (uint8 [B,128]) if given, else the
-        in-kernel hash RNG when ``dropout`` and the model's p > 0."""
+        in-kernel hash RNG (offset = the device step counter) when ``dropout``
+        and the model's p > 0."""
         self._ensure(h.B)
         if global_batch is None:
             global_batch = h.B * self.world
-        kind = _lib.DR_LOSS_MSE if self.loss == "mse" else _lib.DR_LOSS_CE
         scale = self.loss_scale(h, global_batch)
-        drop = None
+        lib = _lib.load()
+        stream = _lib.stream_ptr(self.device)
         if mask is not None:
-            drop = Dropout(self.model.dropout, mask=mask)
-        elif dropout and self.model.dropout > 0:
-            drop = self.model.next_dropout()
+            p = _lib.GinetPassC.from_buffer_copy(self._pass)
+            p.use_dropout = _lib.DR_DROPOUT_MASK
+            p.drop_scale = 1.0 / (1.0 - self.model.dropout)
+            p.mask = mask.data_ptr()
+        else:
+            p = self._pass if (dropout and self.model.dropout > 0) else self._pass_nodrop
+        p.loss_scale = scale
         ev = self.kernel_events
         if ev is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        graph_pass(
-            h, self.params, self.out_dim, _lib.DR_PASS_FORWARD | _lib.DR_PASS_BACKWARD,
-            dropout=drop, loss_kind=kind, loss_scale=scale, class_w=self.class_weights,
-            out=self.out, loss_per_graph=self.lpg, slab=self.slab, head=self.head,
-        )  # fmt: skip
+        _lib.check(lib.dr_ginet_graph_pass(h.store.cstruct(), h.gids.data_ptr(), h.B, self._w, p, h.lds(self.out_dim), stream), "dr_ginet_graph_pass")
         if ev is not None:
             e1.record()
             ev.append((e0, e1))
         self.step_count += 1
+        f = self.model.input_shape
+        slab, head, lpg, lout = self.slab.data_ptr(), self.head.data_ptr(), self.lpg.data_ptr(), self.loss_out.data_ptr()
         if self.world == 1:
-            reduce_update(h, self.params, self.grads, self.out_dim, self.slab, self.head, adam=self.adam_c(), states=self.states, loss_per_graph=self.lpg, loss_scale=scale, loss_out=self.loss_out)
+            _lib.check(lib.dr_ginet_reduce_update(self._table, f, self.out_dim, slab, head, h.B, self._adam, lpg, scale, lout, stream), "dr_ginet_reduce_update")
         else:
-            reduce_update(h, self.params, self.grads, self.out_dim, self.slab, self.head, adam=self.adam_c(False), loss_per_graph=self.lpg, loss_scale=scale, loss_out=self.loss_out)
+            _lib.check(lib.dr_ginet_reduce_update(self._table, f, self.out_dim, slab, head, h.B, self._adam_off, lpg, scale, lout, stream), "dr_ginet_reduce_update")
             torch.distributed.all_reduce(self.flat_grad, group=self.pg)
             torch.distributed.all_reduce(self.loss_out, group=self.pg)
-            reduce_update(h, self.params, self.grads, self.out_dim, None, None, adam=self.adam_c(), states=self.states)
+            _lib.check(lib.dr_ginet_reduce_update(self._table, f, self.out_dim, None, None, h.B, self._adam, None, 1.0, None, _lib.stream_ptr(self.device)), "dr_ginet_reduce_update")
         return self.loss_out, self.out[: h.B]
+
+    def _state_tensors(self):
+        return [*self.params, *[s for st in self.states for s in st], self.counter, self.flat_grad, self.loss_out]
+
+    def capture(self, h: BatchHandle, global_batch=None):
+        """Capture one training step on ``h`` into a HIP graph (``torch.cuda.CUDAGraph``).
+
+        Replaying it runs the same launches (plus the all-reduce for N>1) with
+        no host work; the device counter advances the dropout offset and
+        Adam's step on every replay.  Capturing does not change the training
+        state (the warm-up step it needs is rolled back)."""
+        self._ensure(h.B)
+        snap = [t.detach().clone() for t in self._state_tensors()]
+        n = self.step_count
+        self.step(h, global_batch=global_batch)  # warm-up: LDS attribute, allocator
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.step(h, global_batch=global_batch)
+        torch.cuda.synchronize(self.device)
+        for t, s in zip(self._state_tensors(), snap):
+            t.data.copy_(s)
+        self.step_count = n
+        return g

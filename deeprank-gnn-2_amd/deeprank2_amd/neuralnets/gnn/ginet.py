@@ -139,11 +139,19 @@ class BatchHandle:
         self.gids_host = np.ascontiguousarray(gids_host, dtype=np.int32)
         self.gids = torch.from_numpy(self.gids_host).to(store.device)
         self.B = int(self.gids_host.size)
-        n, e, k0, p1, k1 = store.max_sizes(self.gids_host)
-        self.lds = int(_lib.load().dr_ginet_lds_bytes(n, e, store.n_feat, k0, p1, k1, int(store.packed.transpose_aliased)))
-        if self.lds > 160 * 1024:
-            msg = f"largest graph of the batch needs {self.lds} B of LDS (> 160 KiB): the streamed large-graph path is not built yet"
-            raise RuntimeError(msg)
+        self.max_sizes = store.max_sizes(self.gids_host)
+        self._lds = {}
+
+    def lds(self, out_dim):
+        v = self._lds.get(out_dim)
+        if v is None:
+            n, e, k0, p1, k1 = self.max_sizes
+            v = int(_lib.load().dr_ginet_lds_bytes(n, e, self.store.n_feat, k0, p1, k1, int(self.store.packed.transpose_aliased), out_dim))
+            if v > 160 * 1024:
+                msg = f"largest graph of the batch needs {v} B of LDS (> 160 KiB): the streamed large-graph path is not built yet"
+                raise RuntimeError(msg)
+            self._lds[out_dim] = v
+        return v
 
 
 def resolve_batch(data, device) -> BatchHandle:
@@ -179,7 +187,7 @@ class Dropout:
         return 1.0 / (1.0 - self.p)
 
 
-def graph_pass(h: BatchHandle, params, out_dim, flags, *, dropout: Dropout | None = None, dout=None, loss_kind=_lib.DR_LOSS_NONE, loss_scale=1.0, class_w=None, out=None, loss_per_graph=None, slab=None, head=None):
+def graph_pass(h: BatchHandle, params, out_dim, flags, *, dropout: Dropout | None = None, dout=None, loss_kind=_lib.DR_LOSS_NONE, loss_scale=1.0, class_w=None, out=None, loss_per_graph=None, slab=None, head=None, stamps=None):
     dev = h.store.device
     p = _lib.GinetPassC()
     p.flags = flags
@@ -206,8 +214,9 @@ def graph_pass(h: BatchHandle, params, out_dim, flags, *, dropout: Dropout | Non
     p.loss_per_graph = _lib.ptr(loss_per_graph)
     p.slab = _lib.ptr(slab)
     p.head = _lib.ptr(head)
+    p.stamps = _lib.ptr(stamps)
     w = weights_c(params)
-    rc = _lib.load().dr_ginet_graph_pass(h.store.cstruct(), h.gids.data_ptr(), h.B, w, p, h.lds, _lib.stream_ptr(dev))
+    rc = _lib.load().dr_ginet_graph_pass(h.store.cstruct(), h.gids.data_ptr(), h.B, w, p, h.lds(out_dim), _lib.stream_ptr(dev))
     _lib.check(rc, "dr_ginet_graph_pass")
 
 

@@ -296,15 +296,33 @@ class GraphStore:
         self.device = torch.device(device)
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(self.device)  # noqa: E731
         p = packed
-        self.x = t(p.x)
+        # Device layout: x rows padded to a multiple of 4 floats (16-byte rows,
+        # zero pad) and each graph's col / t_col block 16-byte aligned, so the
+        # kernels stage them with 16-byte global->LDS DMA.
+        self.x_stride = (p.n_feat + 3) & ~3
+        xp = np.zeros((p.x.shape[0], self.x_stride), dtype=np.float32)
+        xp[:, : p.n_feat] = p.x
+        self.x = t(xp)
         self.node_off = t(p.node_off)
         self.edge_off = t(p.edge_off)
+        ecount = np.diff(p.edge_off)
+        col_off = np.zeros(p.n_graphs + 1, dtype=np.int64)
+        np.cumsum((ecount + 3) & ~3, out=col_off[1:])
+        self.col_off_host = col_off
+        self.col_off = t(col_off)
+
+        def spread(a):
+            out = np.zeros(max(int(col_off[-1]), 4), dtype=np.int32)
+            for gi in range(p.n_graphs):
+                out[col_off[gi]:col_off[gi] + ecount[gi]] = a[p.edge_off[gi]:p.edge_off[gi + 1]]
+            return out
+
         self.rowptr = t(p.rowptr)
-        self.col = t(p.col)
+        self.col = t(spread(p.col))
         if p.transpose_aliased:
             self.t_rowptr, self.t_col = self.rowptr, self.col
         else:
-            self.t_rowptr, self.t_col = t(p.t_rowptr), t(p.t_col)
+            self.t_rowptr, self.t_col = t(p.t_rowptr), t(spread(p.t_col))
         self.k0_off = t(p.k0_off)
         self.m0_ptr = t(p.m0_ptr)
         self.m0_idx = t(p.m0_idx)
@@ -346,8 +364,9 @@ class GraphStore:
             s = _lib.GraphStoreC()
             s.n_graphs = self.n_graphs
             s.n_feat = self.n_feat
+            s.x_stride = self.x_stride
             s.transpose_aliased = int(self.packed.transpose_aliased)
-            for name in ("x", "node_off", "edge_off", "rowptr", "col", "t_rowptr", "t_col", "k0_off", "m0_ptr", "m0_idx", "p1_off", "p1_rowptr", "p1_col", "p1t_rowptr", "p1t_col", "k1_off", "m1_ptr", "m1_idx", "y"):
+            for name in ("x", "node_off", "edge_off", "col_off", "rowptr", "col", "t_rowptr", "t_col", "k0_off", "m0_ptr", "m0_idx", "p1_off", "p1_rowptr", "p1_col", "p1t_rowptr", "p1t_col", "k1_off", "m1_ptr", "m1_idx", "y"):
                 setattr(s, name, getattr(self, name).data_ptr())
             self._c = s
         return self._c

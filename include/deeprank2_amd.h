@@ -54,14 +54,15 @@ extern "C" {
  * ---------------------------------------------------------------------- */
 typedef struct dr_graph_store {
   int32_t n_graphs;          /* G                                             */
-  int32_t n_feat;            /* F (row stride of x)                           */
-  int32_t transpose_aliased; /* 1: t_* arrays are the CSR arrays (symmetric)  */
-  int32_t pad0;
-  const float* x;            /* [N_all, F] fp32                               */
+  int32_t n_feat;            /* F                                             */
+  int32_t x_stride;          /* row stride of x in floats: multiple of 4, >= F, pad columns zero */
+  int32_t transpose_aliased; /* 1: t_* / p1t_* arrays are the CSR arrays (symmetric graphs) */
+  const float* x;            /* [N_all, x_stride] fp32 (16-byte aligned rows) */
   const int64_t* node_off;   /* [G+1]                                         */
-  const int64_t* edge_off;   /* [G+1]                                         */
+  const int64_t* edge_off;   /* [G+1] directed edges per graph (edge_attr rows, CSR order) */
+  const int64_t* col_off;    /* [G+1] 16-byte aligned start of each graph's col / t_col block */
   const int32_t* rowptr;     /* [N_all+G] local CSR row pointers (g at node_off[g]+g) */
-  const int32_t* col;        /* [E_all]   local gathered node (edge_index[1]) */
+  const int32_t* col;        /* local gathered node (edge_index[1]), graph g at col_off[g] */
   const int32_t* t_rowptr;   /* transpose CSR (by edge_index[1])              */
   const int32_t* t_col;
   const int64_t* k0_off;     /* [G+1] depth-0 clusters per graph              */
@@ -121,6 +122,11 @@ typedef struct dr_ginet_pass {
   float* loss_per_graph;/* [B] weighted per-graph loss term (fused loss), or NULL */
   float* slab;          /* [B, DR_SLAB_STRIDE(F)] per-graph conv weight-gradient partials */
   float* head;          /* [B, DR_HEAD_STRIDE(out)] per-graph head vectors g, hd, dh, dout */
+  int64_t* stamps;      /* diagnostic builds only (-DDR_STAMPS): [B, 32] s_memtime per phase; NULL */
+  int64_t* step_counter;/* optional device [2]: drop_offset := counter[0] (read by every
+                           workgroup); workgroup 0 snapshots counter[0] into counter[1] for
+                           dr_ginet_reduce_update, which advances counter[0].  Makes a
+                           step's launch arguments constant (hipGraph replay).            */
 } dr_ginet_pass;
 
 /* One workgroup per graph: conv1 -> depth-0 community pooling -> conv2 ->
@@ -134,7 +140,7 @@ int dr_ginet_graph_pass(const dr_graph_store* store, const int32_t* gids, int32_
 
 /* Dynamic LDS bytes dr_ginet_graph_pass needs for a graph of these sizes.  */
 int64_t dr_ginet_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_feat, int32_t k0,
-                           int32_t p1_edges, int32_t k1, int32_t transpose_aliased);
+                           int32_t p1_edges, int32_t k1, int32_t transpose_aliased, int32_t out_dim);
 
 /* Adam (torch.optim.Adam, L2 weight decay added to the gradient) settings.  */
 typedef struct dr_adam {
@@ -142,6 +148,9 @@ typedef struct dr_adam {
   float bias_c1;      /* 1 - beta1^step                                        */
   float bias_c2_sqrt; /* sqrt(1 - beta2^step)                                  */
   int32_t enabled;    /* 0: only write gradients                              */
+  int64_t* step_counter; /* optional device [2] (see dr_ginet_pass): step = counter[1]+1,
+                            bias corrections computed on the device, and (when enabled)
+                            counter[0] := step; overrides bias_c1 / bias_c2_sqrt    */
 } dr_adam;
 
 /* Parameter table in the order of GINet.named_parameters(): 16 tensors

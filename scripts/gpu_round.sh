@@ -10,6 +10,6 @@ ok $rc || exit $rc
 timeout -k 10 240 python bench.py --steps 100 --warmup 10 > gpurun_out/bench.log 2>&1; rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.log
 ok $rc || exit $rc
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/prof" -o run -- python3 "${GRAFT_REPO_ROOT:-/root/repo}/bench.py" --steps 100 --warmup 10 --no-cpu-baseline > "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/prof.log" 2>&1; rc=$?; echo "rocprof rc=$rc"
-find "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/prof" -name "*stats*" | head
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -f csv -d "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/prof" -o run -- python3 "${GRAFT_REPO_ROOT:-/root/repo}/bench.py" --steps 100 --warmup 10 --no-cpu-baseline > "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/prof.log" 2>&1; rc=$?; echo "rocprof rc=$rc"
+find "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/prof" -name "*stats*"
 exit $rc

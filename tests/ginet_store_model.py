@@ -42,8 +42,6 @@ def run(packed, params, out_dim, *, mask=None, drop_scale=1.0, loss="mse", y=Non
         e0 = packed.edge_off[g]
         rp = packed.rowptr[n0 + g:n1 + g + 1]
         col = packed.col[e0 + rp[0]:e0 + rp[-1]]
-        trp = packed.t_rowptr[n0 + g:n1 + g + 1]
-        tcol = packed.t_col[e0:e0 + trp[-1]]
         k0a, k0b = packed.k0_off[g], packed.k0_off[g + 1]
         K0 = k0b - k0a
         m0p = packed.m0_ptr[k0a + g:k0b + g + 1]
@@ -59,13 +57,13 @@ def run(packed, params, out_dim, *, mask=None, drop_scale=1.0, loss="mse", y=Non
         m1i = packed.m1_idx[k0a:k0b]
         X = packed.x[n0:n1]
 
-        Y = (X @ w1cat.T).astype(f32)
-        H = np.zeros((N, 32), f32)
+        Z = np.zeros((N, F), f32)  # aggregate first: A (X W^T) == (A X) W^T
         for i in range(N):
-            acc = np.zeros(32, f32)
+            acc = np.zeros(F, f32)
             for e in range(rp[i], rp[i + 1]):
-                acc = acc + Y[col[e]]
-            H[i] = relu(acc)
+                acc = acc + X[col[e]]
+            Z[i] = acc
+        H = relu((Z @ w1cat.T).astype(f32))
         P1 = np.zeros((K0, 32), f32)
         A1 = np.full((K0, 32), N, np.int64)
         for k in range(K0):
@@ -130,17 +128,13 @@ def run(packed, params, out_dim, *, mask=None, drop_scale=1.0, loss="mse", y=Non
         slab[g, 32 * F:32 * F + 512] = (dY2[:, :32].T @ P1[:, :16]).reshape(-1)
         slab[g, 32 * F + 512:] = (dY2[:, 32:].T @ P1[:, 16:]).reshape(-1)
         dP1 = np.concatenate([dY2[:, :32] @ w2, dY2[:, 32:] @ w2e], 1).astype(f32)
-        DS = np.zeros((N, 32), f32)
+        dW1 = np.zeros((32, F), f32)  # dS1 is non-zero only at the depth-0 arg members
         for k in range(K0):
             for c in range(32):
                 i = A1[k, c]
                 if i < N:
-                    DS[i, c] = relu_bwd(H[i, c], dP1[k, c])
-        dY = np.zeros((N, 32), f32)
-        for j in range(N):
-            for e in range(trp[j], trp[j + 1]):
-                dY[j] += DS[tcol[e]]
-        slab[g, :32 * F] = (dY.T @ X).reshape(-1)
+                    dW1[c] += relu_bwd(H[i, c], dP1[k, c]) * Z[i]
+        slab[g, :32 * F] = dW1.reshape(-1)
 
     grads = {}
     F32 = slab[:, :32 * F].sum(0).reshape(32, F)

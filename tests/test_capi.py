@@ -30,18 +30,18 @@ def test_library_exports_every_declared_entry():
 def test_version_and_lds_query_are_host_only():
     lib = _lib.load()
     assert b"gfx950" in lib.dr_version()
-    small = lib.dr_ginet_lds_bytes(200, 3000, 30, 5, 20, 1, 1)
-    big = lib.dr_ginet_lds_bytes(200, 3000, 30, 5, 20, 1, 0)
+    small = lib.dr_ginet_lds_bytes(200, 3000, 30, 5, 20, 1, 1, 1)
+    big = lib.dr_ginet_lds_bytes(200, 3000, 30, 5, 20, 1, 0, 1)
     assert 0 < small < big <= 200 * 1024
     assert small % 16 == 0
 
 
 def test_struct_layouts_match_header():
-    # 4 int32 + 19 pointers; 8 pointers; 4 int32 + 2 float + 2 uint64 + float/int32 + 7 pointers
-    assert ctypes.sizeof(_lib.GraphStoreC) == 16 + 19 * 8
+    # 4 int32 + 20 pointers; 8 pointers; 4 int32 + 2 float + 2 uint64 + float/int32 + 7 pointers
+    assert ctypes.sizeof(_lib.GraphStoreC) == 16 + 20 * 8
     assert ctypes.sizeof(_lib.GinetWeightsC) == 8 * 8
-    assert ctypes.sizeof(_lib.GinetPassC) == 16 + 8 + 16 + 8 + 7 * 8
-    assert ctypes.sizeof(_lib.AdamC) == 32
+    assert ctypes.sizeof(_lib.GinetPassC) == 16 + 8 + 16 + 8 + 9 * 8
+    assert ctypes.sizeof(_lib.AdamC) == 32 + 8
     assert ctypes.sizeof(_lib.ParamTableC) == 4 * 16 * 8 + 16 * 4
 
 

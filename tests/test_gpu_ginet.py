@@ -6,7 +6,7 @@ from __future__ import annotations
 import numpy as np
 import pytest
 import torch
-from _util import fixed_dropout, golden_batch, golden_grads, golden_state_dict
+from _util import assert_grad_close, fixed_dropout, golden_batch, golden_grads, golden_state_dict
 
 from deeprank2_amd.engine import GINetTrainStep
 from deeprank2_amd.neuralnets.gnn import ginet as amd
@@ -45,7 +45,7 @@ def test_ginet_module_vs_reference_golden(golden, name, args):
     ref = golden_grads(z)
     for n, p in m.named_parameters():
         assert p.grad is not None, n
-        np.testing.assert_allclose(p.grad.cpu().numpy(), ref[n], rtol=1e-4, atol=1e-5, err_msg=n)
+        assert_grad_close(p.grad.cpu().numpy(), ref[n], err_msg=n)
 
 
 def test_ginet_batch1_vs_batch4(golden):
@@ -105,7 +105,7 @@ def test_fused_train_step_vs_oracle_config2_batch64():
     assert float(loss) == pytest.approx(loss_o, rel=1e-4)
     grads = dict(zip(amd.PARAM_NAMES, step.grads))
     for n, p in model_o.named_parameters():
-        np.testing.assert_allclose(grads[n].cpu().numpy(), p.grad.numpy(), rtol=1e-3, atol=1e-5, err_msg=n)
+        assert_grad_close(grads[n].cpu().numpy(), p.grad.numpy(), err_msg=n)
     # the fused Adam against torch.optim.Adam fed the same (kernel) gradients
     ref = [torch.nn.Parameter(b) for b in before]
     for r, g in zip(ref, step.grads):
@@ -135,7 +135,7 @@ def test_module_autograd_vs_oracle_single_cluster_graphs():
     np.testing.assert_allclose(out.detach().cpu().numpy(), out_o.detach().numpy(), **TOL)
     ref = dict(model_o.named_parameters())
     for n, p in model.named_parameters():
-        np.testing.assert_allclose(p.grad.cpu().numpy(), ref[n].grad.numpy(), rtol=1e-3, atol=1e-5, err_msg=n)
+        assert_grad_close(p.grad.cpu().numpy(), ref[n].grad.numpy(), err_msg=n)
 
 
 def test_deterministic_bitwise():
@@ -196,8 +196,31 @@ def test_hash_dropout_matches_host_replica_mask():
     for drop in (amd.Dropout(0.4, seed=99, offset=5), amd.Dropout(0.4, mask=keep)):
         out = torch.empty(12, 1, device=DEV)
         slab = torch.empty(12 * amd.slab_stride(30), device=DEV)
-        head = torch.empty(12 * amd.head_stride(1), device=DEV)
+        head = torch.zeros(12 * amd.head_stride(1), device=DEV)
         amd.graph_pass(h, params, 1, 3, dropout=drop, loss_kind=1, loss_scale=1 / 12, out=out, loss_per_graph=torch.empty(12, device=DEV), slab=slab, head=head)
         outs.append((out.cpu(), slab.cpu(), head.cpu()))
     for x, y in zip(*outs):
         assert torch.equal(x, y)
+
+
+def test_captured_step_replay_matches_eager():
+    """hipGraph replay of the fused step == eager steps (device step counter
+    advances dropout offset and Adam's step on every replay)."""
+    datas = _synthetic(32, seed=12)
+    store = GraphStore(pack_graphs(records_from_batch(P.Batch.from_data_list(datas))), DEV)
+    hs = [amd.BatchHandle(store, np.arange(16)), amd.BatchHandle(store, np.arange(16, 32))]
+    torch.manual_seed(3)
+    m1 = amd.GINet(30, 1, 3).to(DEV).train()
+    m2 = amd.GINet(30, 1, 3).to(DEV).train()
+    m2.load_state_dict(m1.state_dict())
+    m1._drop_seed = m2._drop_seed = 1234
+    s1, s2 = GINetTrainStep(m1), GINetTrainStep(m2)
+    graphs = [s2.capture(h) for h in hs]
+    for i in range(6):
+        l1, _ = s1.step(hs[i % 2])
+        graphs[i % 2].replay()
+        torch.cuda.synchronize()
+        assert torch.equal(l1, s2.loss_out), i
+    for a, b in zip(s1.params, s2.params):
+        assert torch.equal(a, b)
+    assert int(s1.counter[0]) == int(s2.counter[0]) == 6
