@@ -61,7 +61,7 @@ struct Carve {
 __host__ __device__ inline Carve carve(int N, int E, int F, int K0, int P1, int K1, int alias, int OUT) {
   Carve c;
   c.KP = r16(F);      // K padded for the 16x16x4 MFMA steps (zeros)
-  c.LDW = c.KP + 1;
+  c.LDW = c.KP + 2;   // rows 2 words apart: lanes (row li, k+kq) hit 32 distinct banks
   c.XS = r4(F);
   int o = 0;
 #define TAKE(field, words) \
@@ -74,7 +74,7 @@ __host__ __device__ inline Carve carve(int N, int E, int F, int K0, int P1, int 
   TAKE(z, N * c.LDW)
   TAKE(h, N * 32)
   TAKE(rp, N + 1)
-  TAKE(col, E)
+  TAKE(col, (E + 1) / 2)     // uint16 column ids
   TAKE(m0p, K0 + 1)
   TAKE(m0i, N)
   TAKE(p1, K0 * 32)
@@ -108,7 +108,7 @@ struct GinetArgs {
   dr_graph_store s;
   dr_ginet_weights w;
   dr_ginet_pass p;
-  const int32_t* gids;
+  const dr_graph_desc* descs;
   int32_t B;
 };
 
@@ -161,28 +161,34 @@ __device__ __forceinline__ float4 f4add(float4 a, float4 v) {
 }
 
 // Z[i, :XS] = sum over CSR row i of X[col[e], :XS] (edges in CSR order, i.e.
-// the order torch_scatter's CPU scatter_add_ visits them).  4 lanes per row,
-// float4 chunks c4 = lane&3, +4, ...; edges unrolled by 4 so 4 index reads and
-// then their row reads are in flight together.  Z rows have the odd stride ldz.
-__device__ __forceinline__ void gather_rows(const int* rp, const int* col, const float* X, int XS, float* Z, int ldz,
-                                            int n) {
+// the order torch_scatter's CPU scatter_add_ visits them).  8 lanes per row,
+// one float4 chunk each (a 16-lane ds_read_b128 group then touches 2 rows, not
+// 4); edges unrolled by 4 so 4 index reads and then their row reads are in
+// flight together.  Z rows have the stride ldz of the MFMA operand layout.
+__device__ __forceinline__ void gather_rows(const int* rp, const uint16_t* col, const float* X, int XS, float* Z,
+                                            int ldz, int n) {
   const int nch = XS >> 2;
-  const int sub = threadIdx.x & 3;
-  for (int i = threadIdx.x >> 2; i < n; i += NT / 4) {
+  const int sub = threadIdx.x & 7;
+  for (int i = threadIdx.x >> 3; i < n; i += NT / 8) {
     const int eb = rp[i], ee = rp[i + 1];
-    for (int ch = sub; ch < nch; ch += 4) {
+    for (int ch = sub; ch < nch; ch += 8) {
       const int c4 = ch * 4;
       float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
       int e = eb;
       for (; e + 4 <= ee; e += 4) {
-        const int j0 = col[e], j1 = col[e + 1], j2 = col[e + 2], j3 = col[e + 3];
-        const float4 v0 = *reinterpret_cast<const float4*>(&X[j0 * XS + c4]);
-        const float4 v1 = *reinterpret_cast<const float4*>(&X[j1 * XS + c4]);
-        const float4 v2 = *reinterpret_cast<const float4*>(&X[j2 * XS + c4]);
-        const float4 v3 = *reinterpret_cast<const float4*>(&X[j3 * XS + c4]);
+        // Keep four separate 16-bit reads: hipcc would otherwise merge them
+        // into one ds_read_b64 that is misaligned for 3 of 4 row starts (LDS
+        // replays those at ~64 cycles).  The empty asm hides the contiguity.
+        int e1 = e + 1, e2 = e + 2, e3 = e + 3;
+        asm volatile("" : "+v"(e1), "+v"(e2), "+v"(e3));
+        const int j0 = col[e], j1 = col[e1], j2 = col[e2], j3 = col[e3];
+        const float4 v0 = *reinterpret_cast<const float4*>(&X[__umul24(j0, XS) + c4]);
+        const float4 v1 = *reinterpret_cast<const float4*>(&X[__umul24(j1, XS) + c4]);
+        const float4 v2 = *reinterpret_cast<const float4*>(&X[__umul24(j2, XS) + c4]);
+        const float4 v3 = *reinterpret_cast<const float4*>(&X[__umul24(j3, XS) + c4]);
         acc = f4add(f4add(f4add(f4add(acc, v0), v1), v2), v3);
       }
-      for (; e < ee; ++e) acc = f4add(acc, *reinterpret_cast<const float4*>(&X[col[e] * XS + c4]));
+      for (; e < ee; ++e) acc = f4add(acc, *reinterpret_cast<const float4*>(&X[__umul24((int)col[e], XS) + c4]));
       float* zr = Z + i * ldz + c4;
       zr[0] = acc.x;
       zr[1] = acc.y;
@@ -212,17 +218,10 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   const int wave = tid >> 6;
   const int b = blockIdx.x;
   const dr_graph_store& s = a.s;
-  const int g = a.gids[b];
-  const int64_t n0 = s.node_off[g];
-  const int N = (int)(s.node_off[g + 1] - n0);
-  const int E = (int)(s.edge_off[g + 1] - s.edge_off[g]);
-  const int64_t ec0 = s.col_off[g];
-  const int64_t k00 = s.k0_off[g];
-  const int K0 = (int)(s.k0_off[g + 1] - k00);
-  const int64_t q0 = s.p1_off[g];
-  const int P1 = (int)(s.p1_off[g + 1] - q0);
-  const int64_t k10 = s.k1_off[g];
-  const int K1 = (int)(s.k1_off[g + 1] - k10);
+  const dr_graph_desc d = a.descs[b];  // one 64-byte scalar load
+  const int g = d.gid;
+  const int64_t n0 = d.node0, ec0 = d.col0, k00 = d.k0, q0 = d.p1, k10 = d.k1;
+  const int N = d.n_nodes, E = d.n_edges, K0 = d.n_k0, P1 = d.n_p1, K1 = d.n_k1;
   const int F = s.n_feat;
   const int alias = s.transpose_aliased;
   const int OUT = a.p.out_dim;
@@ -236,7 +235,7 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   float* sZ = lds + c.z;
   float* sH = lds + c.h;
   int* srp = reinterpret_cast<int*>(lds + c.rp);
-  int* scol = reinterpret_cast<int*>(lds + c.col);
+  uint16_t* scol = reinterpret_cast<uint16_t*>(lds + c.col);
   int* sm0p = reinterpret_cast<int*>(lds + c.m0p);
   int* sm0i = reinterpret_cast<int*>(lds + c.m0i);
   float* sP1 = lds + c.p1;
@@ -286,14 +285,8 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
     if (b == 0 && tid == 0) a.p.step_counter[1] = (int64_t)drop_offset;  // snapshot for the update kernel
   }
   dma_x4(sX, s.x + n0 * (int64_t)XS, N * XS / 4);
-  dma_x4(scol, s.col + ec0, (E + 3) / 4);
+  dma_x4(scol, s.col + ec0, (E + 7) / 8);
   dma_words(srp, s.rowptr + n0 + g, N + 1);
-  dma_rows(sW1, LDW, a.w.w1, 16, F);
-  dma_rows(sW1 + 16 * LDW, LDW, a.w.w1e, 16, F);
-  dma_words(sW2, a.w.w2, 512);
-  dma_words(sW2 + 512, a.w.w2e, 512);
-  dma_words(sFc2, a.w.fc2w, OUT * 128);
-  dma_words(sFc2 + OUT * 128, a.w.fc2b, OUT);
   dma_words(sm0p, s.m0_ptr + k00 + g, K0 + 1);
   dma_words(sm0i, s.m0_idx + n0, N);
   dma_words(sp1rp, s.p1_rowptr + k00 + g, K0 + 1);
@@ -320,11 +313,49 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   __syncthreads();
 
   STAMP(1);
+  // The weights are not needed before the GEMM: load them into VGPRs now and
+  // store them to LDS after the gather, so their latency overlaps it.  (An
+  // LDS DMA here would make hipcc wait for it before every LDS read.)
+  float wv1[2], wv2, wfc[3];
+  {
+    const int n1 = 32 * F;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int p = tid + u * NT;
+      wv1[u] = 0.f;
+      if (p < n1) wv1[u] = (p < 16 * F) ? a.w.w1[p] : a.w.w1e[p - 16 * F];
+    }
+    wv2 = (tid < 512) ? a.w.w2[tid] : a.w.w2e[tid - 512];
+    const int nf = OUT * 128;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int p = tid + u * NT;
+      wfc[u] = 0.f;
+      if (p < nf) wfc[u] = a.w.fc2w[p];
+      else if (p < nf + OUT) wfc[u] = a.w.fc2b[p - nf];
+    }
+  }
   // ---------------- conv1 aggregation first: Z = A X  (ginet.py:45,58) -----
   // A (X W^T) = (A X) W^T: aggregating the F input features first lets the
   // backward use dW1 = sum_k v_k (A X)[arg_k] (the depth-0 max pool routes
   // each channel's gradient to one member per cluster) with no backward gather.
   gather_rows(srp, scol, sX, XS, sZ, LDW, N);
+  {
+    const int n1 = 32 * F;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int p = tid + u * NT;
+      if (p < n1) {
+        const int r = p / F;
+        sW1[r * LDW + (p - r * F)] = wv1[u];
+      }
+    }
+    sW2[tid] = wv2;
+    const int nf = OUT * 128 + OUT;
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+      if (tid + u * NT < nf) sFc2[tid + u * NT] = wfc[u];
+  }
   __syncthreads();
 
   STAMP(2);
@@ -369,14 +400,15 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   // Members are split into S1 contiguous slices combined in slice order.
   {
     const int pairs = K0 * 32;
-    const int S1 = pairs > 0 ? max(1, min(8, NT / pairs)) : 1;
+    const int LS = pairs <= NT / 8 ? 3 : pairs <= NT / 4 ? 2 : pairs <= NT / 2 ? 1 : 0;  // log2 slices
+    const int S1 = 1 << LS;
     float* tb = sRed;
     int* ta = reinterpret_cast<int*>(sRed + NT);
     for (int p = tid; p < pairs * S1; p += NT) {
-      const int sl = p / pairs, pr = p - sl * pairs;
+      const int sl = p & (S1 - 1), pr = p >> LS;  // p = pr * S1 + sl
       const int k = pr >> 5, ch = pr & 31;
       const int mb = sm0p[k], cnt = sm0p[k + 1] - mb;
-      const int qb = mb + (cnt * sl) / S1, qe = mb + (cnt * (sl + 1)) / S1;
+      const int qb = mb + ((cnt * sl) >> LS), qe = mb + ((cnt * (sl + 1)) >> LS);
       float best = LOWEST;
       int arg = N;
       int m = qb;
@@ -404,10 +436,10 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
       float best = LOWEST;
       int arg = N;
       for (int sl = 0; sl < S1; ++sl) {
-        const float v = tb[sl * pairs + p];
+        const float v = tb[(p << LS) + sl];
         if (v > best) {
           best = v;
-          arg = ta[sl * pairs + p];
+          arg = ta[(p << LS) + sl];
         }
       }
       sP1[p] = (best == LOWEST) ? 0.f : best;
@@ -740,11 +772,12 @@ extern "C" int64_t dr_ginet_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t 
   return 4LL * carve(n_nodes, n_edges, n_feat, k0, p1_edges, k1, transpose_aliased, out_dim).total;
 }
 
-extern "C" int dr_ginet_graph_pass(const dr_graph_store* store, const int32_t* gids, int32_t n_batch,
+extern "C" int dr_ginet_graph_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
                                    const dr_ginet_weights* w, const dr_ginet_pass* pass, int32_t lds_bytes,
                                    void* stream) {
-  if (!store || !gids || !w || !pass || n_batch < 0) return DR_E_ARG;
+  if (!store || !descs || !w || !pass || n_batch < 0) return DR_E_ARG;
   if (pass->out_dim < 1 || pass->out_dim > DR_MAX_OUT) return DR_E_UNSUPPORTED;
+  if (store->n_feat < 1 || 32 * store->n_feat > 2 * NT) return DR_E_UNSUPPORTED;  // F <= 64
   if (lds_bytes > 160 * 1024) return DR_E_LDS;
   if ((pass->flags & DR_PASS_BACKWARD) && (!pass->slab || !pass->head)) return DR_E_ARG;
   if ((pass->flags & DR_PASS_BACKWARD) && pass->loss_kind == DR_LOSS_NONE && !pass->dout) return DR_E_ARG;
@@ -757,7 +790,7 @@ extern "C" int dr_ginet_graph_pass(const dr_graph_store* store, const int32_t* g
   args.s = *store;
   args.w = *w;
   args.p = *pass;
-  args.gids = gids;
+  args.descs = descs;
   args.B = n_batch;
   hipLaunchKernelGGL(ginet_graph_kernel, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, args);
   return (int)hipGetLastError();

@@ -145,7 +145,7 @@ class GINetTrainStep:
         if ev is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        _lib.check(lib.dr_ginet_graph_pass(h.store.cstruct(), h.gids.data_ptr(), h.B, self._w, p, h.lds(self.out_dim), stream), "dr_ginet_graph_pass")
+        _lib.check(lib.dr_ginet_graph_pass(h.store.cstruct(), h.descs.data_ptr(), h.B, self._w, p, h.lds(self.out_dim), stream), "dr_ginet_graph_pass")
         if ev is not None:
             e1.record()
             ev.append((e0, e1))

@@ -138,6 +138,7 @@ class BatchHandle:
         self.store = store
         self.gids_host = np.ascontiguousarray(gids_host, dtype=np.int32)
         self.gids = torch.from_numpy(self.gids_host).to(store.device)
+        self.descs = store.descriptors(self.gids_host)
         self.B = int(self.gids_host.size)
         self.max_sizes = store.max_sizes(self.gids_host)
         self._lds = {}
@@ -216,7 +217,7 @@ def graph_pass(h: BatchHandle, params, out_dim, flags, *, dropout: Dropout | Non
     p.head = _lib.ptr(head)
     p.stamps = _lib.ptr(stamps)
     w = weights_c(params)
-    rc = _lib.load().dr_ginet_graph_pass(h.store.cstruct(), h.gids.data_ptr(), h.B, w, p, h.lds(out_dim), _lib.stream_ptr(dev))
+    rc = _lib.load().dr_ginet_graph_pass(h.store.cstruct(), h.descs.data_ptr(), h.B, w, p, h.lds(out_dim), _lib.stream_ptr(dev))
     _lib.check(rc, "dr_ginet_graph_pass")
 
 

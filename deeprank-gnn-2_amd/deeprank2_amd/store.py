@@ -286,6 +286,10 @@ def records_from_batch(batch) -> list[GraphRecord]:
     return recs
 
 
+DESC_DTYPE = np.dtype([("node0", "<i8"), ("col0", "<i8"), ("k0", "<i8"), ("p1", "<i8"), ("k1", "<i8"), ("n_nodes", "<i4"), ("n_edges", "<i4"), ("n_k0", "<i4"), ("n_p1", "<i4"), ("n_k1", "<i4"), ("gid", "<i4")])
+assert DESC_DTYPE.itemsize == 64  # dr_graph_desc
+
+
 class GraphStore:
     """Device copy of a :class:`PackedGraphs` (all arrays live in HBM)."""
 
@@ -305,16 +309,20 @@ class GraphStore:
         self.x = t(xp)
         self.node_off = t(p.node_off)
         self.edge_off = t(p.edge_off)
+        if np.diff(p.node_off).max() > 65535:
+            msg = "graphs with more than 65535 nodes are not supported (16-bit local column ids)"
+            raise ValueError(msg)
         ecount = np.diff(p.edge_off)
         col_off = np.zeros(p.n_graphs + 1, dtype=np.int64)
-        np.cumsum((ecount + 3) & ~3, out=col_off[1:])
+        np.cumsum((ecount + 7) & ~7, out=col_off[1:])  # 16-byte aligned uint16 blocks
         self.col_off_host = col_off
         self.col_off = t(col_off)
+        # gather index: graph g's CSR slot e lives at col_off[g] + e
+        slot = np.arange(int(p.edge_off[-1]), dtype=np.int64) - np.repeat(p.edge_off[:-1], ecount) + np.repeat(col_off[:-1], ecount)
 
         def spread(a):
-            out = np.zeros(max(int(col_off[-1]), 4), dtype=np.int32)
-            for gi in range(p.n_graphs):
-                out[col_off[gi]:col_off[gi] + ecount[gi]] = a[p.edge_off[gi]:p.edge_off[gi + 1]]
+            out = np.zeros(max(int(col_off[-1]), 8), dtype=np.uint16)
+            out[slot] = a
             return out
 
         self.rowptr = t(p.rowptr)
@@ -370,6 +378,23 @@ class GraphStore:
                 setattr(s, name, getattr(self, name).data_ptr())
             self._c = s
         return self._c
+
+    def descriptors(self, gids_host):
+        """dr_graph_desc records (64 bytes each) for these graph ids, as a device uint8 tensor."""
+        import torch  # noqa: PLC0415
+
+        p = self.packed
+        g = np.asarray(gids_host, dtype=np.int64)
+        d = np.zeros(g.size, dtype=DESC_DTYPE)
+        d["node0"] = p.node_off[g]
+        d["col0"] = self.col_off_host[g]
+        d["k0"] = p.k0_off[g]
+        d["p1"] = p.p1_off[g]
+        d["k1"] = p.k1_off[g]
+        n, e, k0, p1, k1 = self._sizes
+        d["n_nodes"], d["n_edges"], d["n_k0"], d["n_p1"], d["n_k1"] = n[g], e[g], k0[g], p1[g], k1[g]
+        d["gid"] = g
+        return torch.from_numpy(d.view(np.uint8)).to(self.device)
 
     def max_sizes(self, gids_host):
         n, e, k0, p1, k1 = self._sizes

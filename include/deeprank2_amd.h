@@ -62,9 +62,9 @@ typedef struct dr_graph_store {
   const int64_t* edge_off;   /* [G+1] directed edges per graph (edge_attr rows, CSR order) */
   const int64_t* col_off;    /* [G+1] 16-byte aligned start of each graph's col / t_col block */
   const int32_t* rowptr;     /* [N_all+G] local CSR row pointers (g at node_off[g]+g) */
-  const int32_t* col;        /* local gathered node (edge_index[1]), graph g at col_off[g] */
+  const uint16_t* col;       /* local gathered node (edge_index[1]), graph g at col_off[g] */
   const int32_t* t_rowptr;   /* transpose CSR (by edge_index[1])              */
-  const int32_t* t_col;
+  const uint16_t* t_col;
   const int64_t* k0_off;     /* [G+1] depth-0 clusters per graph              */
   const int32_t* m0_ptr;     /* [K0_all+G] members of each depth-0 cluster    */
   const int32_t* m0_idx;     /* [N_all] local node ids, ascending per cluster  */
@@ -78,6 +78,18 @@ typedef struct dr_graph_store {
   const int32_t* m1_idx;     /* [K0_all] local depth-0 ids, ascending          */
   const float* y;            /* [G] target (class index as float for classif) */
 } dr_graph_store;
+
+/* One mini-batch slot: where graph `gid` lives in the store (64 bytes, so a
+ * workgroup reads its whole descriptor with one scalar load).  Built from the
+ * graph ids on the host (the store keeps host copies of the offset tables).  */
+typedef struct dr_graph_desc {
+  int64_t node0;  /* node_off[gid]  (also indexes rowptr as node0 + gid)   */
+  int64_t col0;   /* col_off[gid]                                         */
+  int64_t k0;     /* k0_off[gid]    (m0_ptr / p1_rowptr at k0 + gid)      */
+  int64_t p1;     /* p1_off[gid]                                          */
+  int64_t k1;     /* k1_off[gid]    (m1_ptr at k1 + gid)                  */
+  int32_t n_nodes, n_edges, n_k0, n_p1, n_k1, gid;
+} dr_graph_desc;
 
 /* GINet parameters (device pointers into the nn.Parameters, fp32).  */
 typedef struct dr_ginet_weights {
@@ -132,9 +144,9 @@ typedef struct dr_ginet_pass {
 /* One workgroup per graph: conv1 -> depth-0 community pooling -> conv2 ->
  * depth-1 max pooling -> per-graph mean -> fc1/relu/dropout/fc2, and (when
  * DR_PASS_BACKWARD) the full backward of that graph, all in LDS.
- * gids: [B] device int32 graph ids into the store.  lds_bytes: the dynamic
- * LDS the largest graph of the batch needs (dr_ginet_lds_bytes).          */
-int dr_ginet_graph_pass(const dr_graph_store* store, const int32_t* gids, int32_t n_batch,
+ * descs: [B] device descriptors of the batch's graphs.  lds_bytes: the
+ * dynamic LDS the largest graph of the batch needs (dr_ginet_lds_bytes).  */
+int dr_ginet_graph_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
                         const dr_ginet_weights* w, const dr_ginet_pass* pass,
                         int32_t lds_bytes, void* stream);
 
