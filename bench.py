@@ -56,6 +56,27 @@ def algorithmic_bytes(packed, gids):
     return int(per.sum())
 
 
+def pmc_traffic_bytes():
+    """HBM bytes per graph-kernel launch from the committed PMC pass
+    (profiles/*/pmc_ginet_graph_kernel.txt, collected by scripts/gpu_pmc.sh with
+    FETCH_SIZE and WRITE_SIZE in separate passes).  gfx950 correction
+    (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts half the bytes of wide
+    coalesced reads, so bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024."""
+    import glob  # noqa: PLC0415
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_ginet_graph_kernel.txt")))
+    if not files:
+        return None, None
+    vals = {}
+    for line in open(files[-1]):
+        parts = line.split()
+        if len(parts) >= 2 and parts[0] in ("FETCH_SIZE", "WRITE_SIZE"):
+            vals[parts[0]] = float(parts[1])
+    if len(vals) != 2:
+        return None, None
+    return int((2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024), os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(graphs, budget_s=15.0, max_steps=60):
     """The CPU oracle (op-for-op restatement of the reference, torch CPU) training
     the same batch: forward, MSE, backward, Adam — on this host's cores."""
@@ -133,14 +154,14 @@ def main():  # noqa: PLR0915
 
     for i in range(args.warmup):
         run_eager(i)
-    graphs = None
+    captured = None
     if not args.eager:  # one captured step per resident mini-batch, replayed
-        graphs = [step.capture(h, global_batch=B * world) for h in handles]
+        captured = [step.capture(h, global_batch=B * world) for h in handles]
 
     def run(i):
-        if graphs is None:
+        if captured is None:
             return run_eager(i)
-        graphs[i % len(graphs)].replay()
+        captured[i % len(captured)].replay()
         return step.loss_out, None
 
     torch.cuda.synchronize()
@@ -182,6 +203,7 @@ def main():  # noqa: PLR0915
     edges_total = float(et.item())
     alg = np.mean([algorithmic_bytes(packed, h.gids_host) for h in handles])
     achieved = alg / (kernel_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic_bytes() if B == B_PER_GPU else (None, None)
 
     result = None
     if rank == 0:
@@ -220,12 +242,13 @@ def main():  # noqa: PLR0915
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": int(alg),
                 "kernel_ms_avg": round(kernel_ms, 5),
                 "kernel_timing": "HIP events around each dr_ginet_graph_pass launch over an eager region of the same step count",
             },
-            "launch": "eager" if graphs is None else "hipgraph-replay",
+            "launch": "eager" if captured is None else "hipgraph-replay",
             "cpu_baseline": cpu,
             "final_loss": float(loss.item()),
         }

@@ -673,41 +673,29 @@ constexpr int RP = 64;  // parameter elements per block
 constexpr int RC = 8;   // batch chunks per block
 constexpr int RU = 8;   // batch rows per chunk issued together (predicated)
 
-// Sum over b in [b0, b1) of one gradient element; RU rows per group with all
-// their loads issued before the adds (the loads are independent; a serial
-// chain would pay one L2/MALL round trip per row).
-__device__ float grad_partial(const ReduceArgs& a, int pi, int e, int b0, int b1) {
+// Where gradient element e of parameter pi comes from: rows b of p1 (stride st)
+// summed, or of p1*p2 (outer products of the per-graph head vectors).
+struct GradSrc {
+  const float* p1;
+  const float* p2;
+  int64_t st;
+};
+
+__device__ __forceinline__ GradSrc grad_src(const ReduceArgs& a, int pi, int e) {
   const int F = a.F;
   const int64_t SS = DR_SLAB_STRIDE(F);
   const int64_t HS = DR_HEAD_STRIDE(a.OUT);
-  const float* p1 = nullptr;  // first operand row 0, stride st1
-  const float* p2 = nullptr;  // optional second operand (outer products)
-  int64_t st = 0;
   switch (pi) {
-    case 0: p1 = a.slab + e; st = SS; break;                       // conv1.fc.weight: slab rows 0..15
-    case 6: p1 = a.slab + 16 * F + e; st = SS; break;              // conv1_ext.fc.weight: rows 16..31
-    case 3: p1 = a.slab + 32 * F + e; st = SS; break;              // conv2.fc.weight
-    case 9: p1 = a.slab + 32 * F + 512 + e; st = SS; break;        // conv2_ext.fc.weight
-    case 12: p1 = a.head + 192 + (e >> 6); p2 = a.head + (e & 63); st = HS; break;      // fc1.weight = sum dh (x) g
-    case 13: p1 = a.head + 192 + e; st = HS; break;                // fc1.bias
-    case 14: p1 = a.head + 320 + (e >> 7); p2 = a.head + 64 + (e & 127); st = HS; break;  // fc2.weight = sum dout (x) hd
-    case 15: p1 = a.head + 320 + e; st = HS; break;                // fc2.bias
-    default: return 0.f;  // fc_edge_attr / fc_attention: exact zeros (softmax over a size-1 dim)
+    case 0: return {a.slab + e, nullptr, SS};                                  // conv1.fc.weight: slab rows 0..15
+    case 6: return {a.slab + 16 * F + e, nullptr, SS};                         // conv1_ext.fc.weight: rows 16..31
+    case 3: return {a.slab + 32 * F + e, nullptr, SS};                         // conv2.fc.weight
+    case 9: return {a.slab + 32 * F + 512 + e, nullptr, SS};                   // conv2_ext.fc.weight
+    case 12: return {a.head + 192 + (e >> 6), a.head + (e & 63), HS};          // fc1.weight = sum dh (x) g
+    case 13: return {a.head + 192 + e, nullptr, HS};                           // fc1.bias
+    case 14: return {a.head + 320 + (e >> 7), a.head + 64 + (e & 127), HS};    // fc2.weight = sum dout (x) hd
+    case 15: return {a.head + 320 + e, nullptr, HS};                           // fc2.bias
+    default: return {nullptr, nullptr, 0};  // fc_edge_attr / fc_attention: exact zeros (softmax over a size-1 dim)
   }
-  float acc = 0.f;
-  for (int bb = b0; bb < b1; bb += RU) {
-    float u[RU], v[RU];
-#pragma unroll
-    for (int k = 0; k < RU; ++k) {
-      const bool ok = bb + k < b1;
-      const int64_t r = (int64_t)(ok ? bb + k : b0) * st;
-      u[k] = ok ? p1[r] : 0.f;
-      v[k] = (ok && p2) ? p2[r] : 1.f;
-    }
-#pragma unroll
-    for (int k = 0; k < RU; ++k) acc = p2 ? fmaf(u[k], v[k], acc) : acc + u[k];
-  }
-  return acc;
 }
 
 __global__ void __launch_bounds__(RP* RC) ginet_reduce_kernel(ReduceArgs a) {
@@ -720,23 +708,43 @@ __global__ void __launch_bounds__(RP* RC) ginet_reduce_kernel(ReduceArgs a) {
     acc = dr_wave_sum(acc);
     if (threadIdx.x == 0) a.loss_out[0] = acc * a.loss_scale;
   }
-  // Adam step number and bias corrections (host-given, or from the device counter)
-  float bc1 = a.adam.bias_c1, bc2s = a.adam.bias_c2_sqrt;
-  if (a.adam.step_counter) {
-    const int64_t t = a.adam.step_counter[1] + 1;
-    bc1 = 1.f - powf(a.adam.beta1, (float)t);
-    bc2s = sqrtf(1.f - powf(a.adam.beta2, (float)t));
-    if (a.adam.enabled && blockIdx.x == 0 && threadIdx.x == 0) a.adam.step_counter[0] = t;
-  }
   const bool live = gi < a.off[DR_GINET_NPARAM];
   int pi = 0;
   if (live)
     while (gi >= a.off[pi + 1]) ++pi;
   const int e = live ? gi - a.off[pi] : 0;
+  // Adam state loads are issued together with the partial-sum loads: one
+  // memory round trip per element instead of two.
+  const bool upd = live && ch == 0 && a.adam.enabled;
+  float p0 = 0.f, m0 = 0.f, v0 = 0.f, gin = 0.f;
+  if (upd) {
+    p0 = a.t.param[pi][e];
+    m0 = a.t.exp_avg[pi][e];
+    v0 = a.t.exp_avg_sq[pi][e];
+  }
+  if (live && ch == 0 && !a.slab && a.t.grad[pi]) gin = a.t.grad[pi][e];
   if (a.slab) {
-    float v = 0.f;
-    if (live) v = grad_partial(a, pi, e, (a.B * ch) / RC, (a.B * (ch + 1)) / RC);
-    part[ch][lp] = v;
+    float acc = 0.f;
+    const GradSrc src = live ? grad_src(a, pi, e) : GradSrc{nullptr, nullptr, 0};
+    if (src.p1) {
+      const int b0 = (a.B * ch) / RC, b1 = (a.B * (ch + 1)) / RC;
+      const float* q1 = src.p1 + (int64_t)b0 * src.st;
+      const float* q2 = src.p2 ? src.p2 + (int64_t)b0 * src.st : nullptr;
+      for (int bb = b0; bb < b1; bb += RU) {
+        float u[RU], v[RU];
+#pragma unroll
+        for (int k = 0; k < RU; ++k) {
+          const bool ok = bb + k < b1;
+          u[k] = ok ? q1[k * src.st] : 0.f;
+          v[k] = (ok && q2) ? q2[k * src.st] : 1.f;
+        }
+#pragma unroll
+        for (int k = 0; k < RU; ++k) acc = q2 ? fmaf(u[k], v[k], acc) : acc + u[k];
+        q1 += RU * src.st;
+        if (q2) q2 += RU * src.st;
+      }
+    }
+    part[ch][lp] = acc;
   }
   __syncthreads();
   if (ch != 0 || !live) return;
@@ -747,21 +755,25 @@ __global__ void __launch_bounds__(RP* RC) ginet_reduce_kernel(ReduceArgs a) {
     for (int k = 0; k < RC; ++k) gsum += part[k][lp];
     if (a.t.grad[pi]) a.t.grad[pi][e] = gsum;
   } else {  // gradients supplied (e.g. after an RCCL all-reduce): Adam only
-    gsum = a.t.grad[pi] ? a.t.grad[pi][e] : 0.f;
+    gsum = gin;
   }
-  if (a.adam.enabled) {
-    float* p = a.t.param[pi] + e;
-    float* m = a.t.exp_avg[pi] + e;
-    float* v = a.t.exp_avg_sq[pi] + e;
+  if (upd) {
+    float bc1 = a.adam.bias_c1, bc2s = a.adam.bias_c2_sqrt;
+    if (a.adam.step_counter) {  // step and bias corrections from the device counter
+      const int64_t t = a.adam.step_counter[1] + 1;
+      bc1 = 1.f - powf(a.adam.beta1, (float)t);
+      bc2s = sqrtf(1.f - powf(a.adam.beta2, (float)t));
+      if (gi == 0) a.adam.step_counter[0] = t;
+    }
     float gr = gsum;
-    if (a.adam.weight_decay != 0.f) gr = fmaf(a.adam.weight_decay, *p, gr);
+    if (a.adam.weight_decay != 0.f) gr = fmaf(a.adam.weight_decay, p0, gr);
     // torch.optim.Adam: exp_avg.lerp_(g, 1-b1); exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
-    const float mv = *m + (1.f - a.adam.beta1) * (gr - *m);
-    const float vv = fmaf((1.f - a.adam.beta2) * gr, gr, *v * a.adam.beta2);
-    *m = mv;
-    *v = vv;
+    const float mv = m0 + (1.f - a.adam.beta1) * (gr - m0);
+    const float vv = fmaf((1.f - a.adam.beta2) * gr, gr, v0 * a.adam.beta2);
+    a.t.exp_avg[pi][e] = mv;
+    a.t.exp_avg_sq[pi][e] = vv;
     const float denom = sqrtf(vv) / bc2s + a.adam.eps;
-    *p = *p - (a.adam.lr / bc1) * (mv / denom);
+    a.t.param[pi][e] = p0 - (a.adam.lr / bc1) * (mv / denom);
   }
 }
 
