@@ -107,7 +107,7 @@ __host__ __device__ inline Carve carve(int N, int E, int F, int K0, int P1, int 
 struct GinetArgs {
   dr_graph_store s;
   dr_ginet_weights w;
-  dr_ginet_pass p;
+  dr_pass p;
   const dr_graph_desc* descs;
   int32_t B;
 };
@@ -117,7 +117,7 @@ struct GinetArgs {
 __device__ __forceinline__ float relu_keepnan(float v) { return (v <= 0.f) ? 0.f : v; }
 __device__ __forceinline__ float relu_bwd(float out, float g) { return (out <= 0.f) ? 0.f : g; }
 
-__device__ __forceinline__ bool keep_unit(const dr_ginet_pass& p, uint64_t offset, int b, int r) {
+__device__ __forceinline__ bool keep_unit(const dr_pass& p, uint64_t offset, int b, int r) {
   if (p.use_dropout == DR_DROPOUT_MASK) return p.mask[(int64_t)b * 128 + r] != 0;
   return dr_uniform(p.drop_seed, offset, (uint32_t)(b * 128 + r)) >= p.drop_p;
 }
@@ -652,131 +652,6 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   STAMP(14);
 }
 
-// ---------------------------------------------------------------------------
-// Reduce the per-graph partials into the 16 GINet gradients, then Adam.
-// Block = 32 parameter elements x 8 batch chunks; the chunk partials are
-// combined in chunk order (deterministic).
-// ---------------------------------------------------------------------------
-struct ReduceArgs {
-  dr_param_table t;
-  dr_adam adam;
-  const float* slab;
-  const float* head;
-  const float* lpg;
-  float* loss_out;
-  float loss_scale;
-  int32_t F, OUT, B;
-  int32_t off[DR_GINET_NPARAM + 1];
-};
-
-constexpr int RP = 64;  // parameter elements per block
-constexpr int RC = 8;   // batch chunks per block
-constexpr int RU = 8;   // batch rows per chunk issued together (predicated)
-
-// Where gradient element e of parameter pi comes from: rows b of p1 (stride st)
-// summed, or of p1*p2 (outer products of the per-graph head vectors).
-struct GradSrc {
-  const float* p1;
-  const float* p2;
-  int64_t st;
-};
-
-__device__ __forceinline__ GradSrc grad_src(const ReduceArgs& a, int pi, int e) {
-  const int F = a.F;
-  const int64_t SS = DR_SLAB_STRIDE(F);
-  const int64_t HS = DR_HEAD_STRIDE(a.OUT);
-  switch (pi) {
-    case 0: return {a.slab + e, nullptr, SS};                                  // conv1.fc.weight: slab rows 0..15
-    case 6: return {a.slab + 16 * F + e, nullptr, SS};                         // conv1_ext.fc.weight: rows 16..31
-    case 3: return {a.slab + 32 * F + e, nullptr, SS};                         // conv2.fc.weight
-    case 9: return {a.slab + 32 * F + 512 + e, nullptr, SS};                   // conv2_ext.fc.weight
-    case 12: return {a.head + 192 + (e >> 6), a.head + (e & 63), HS};          // fc1.weight = sum dh (x) g
-    case 13: return {a.head + 192 + e, nullptr, HS};                           // fc1.bias
-    case 14: return {a.head + 320 + (e >> 7), a.head + 64 + (e & 127), HS};    // fc2.weight = sum dout (x) hd
-    case 15: return {a.head + 320 + e, nullptr, HS};                           // fc2.bias
-    default: return {nullptr, nullptr, 0};  // fc_edge_attr / fc_attention: exact zeros (softmax over a size-1 dim)
-  }
-}
-
-__global__ void __launch_bounds__(RP* RC) ginet_reduce_kernel(ReduceArgs a) {
-  __shared__ float part[RC][RP];
-  const int lp = threadIdx.x % RP, ch = threadIdx.x / RP;
-  const int gi = blockIdx.x * RP + lp;
-  if (blockIdx.x == 0 && threadIdx.x < 64 && a.lpg && a.loss_out) {
-    float acc = 0.f;  // lane-strided partial sums, then a fixed-order wave reduction
-    for (int b = threadIdx.x; b < a.B; b += 64) acc += a.lpg[b];
-    acc = dr_wave_sum(acc);
-    if (threadIdx.x == 0) a.loss_out[0] = acc * a.loss_scale;
-  }
-  const bool live = gi < a.off[DR_GINET_NPARAM];
-  int pi = 0;
-  if (live)
-    while (gi >= a.off[pi + 1]) ++pi;
-  const int e = live ? gi - a.off[pi] : 0;
-  // Adam state loads are issued together with the partial-sum loads: one
-  // memory round trip per element instead of two.
-  const bool upd = live && ch == 0 && a.adam.enabled;
-  float p0 = 0.f, m0 = 0.f, v0 = 0.f, gin = 0.f;
-  if (upd) {
-    p0 = a.t.param[pi][e];
-    m0 = a.t.exp_avg[pi][e];
-    v0 = a.t.exp_avg_sq[pi][e];
-  }
-  if (live && ch == 0 && !a.slab && a.t.grad[pi]) gin = a.t.grad[pi][e];
-  if (a.slab) {
-    float acc = 0.f;
-    const GradSrc src = live ? grad_src(a, pi, e) : GradSrc{nullptr, nullptr, 0};
-    if (src.p1) {
-      const int b0 = (a.B * ch) / RC, b1 = (a.B * (ch + 1)) / RC;
-      const float* q1 = src.p1 + (int64_t)b0 * src.st;
-      const float* q2 = src.p2 ? src.p2 + (int64_t)b0 * src.st : nullptr;
-      for (int bb = b0; bb < b1; bb += RU) {
-        float u[RU], v[RU];
-#pragma unroll
-        for (int k = 0; k < RU; ++k) {
-          const bool ok = bb + k < b1;
-          u[k] = ok ? q1[k * src.st] : 0.f;
-          v[k] = (ok && q2) ? q2[k * src.st] : 1.f;
-        }
-#pragma unroll
-        for (int k = 0; k < RU; ++k) acc = q2 ? fmaf(u[k], v[k], acc) : acc + u[k];
-        q1 += RU * src.st;
-        if (q2) q2 += RU * src.st;
-      }
-    }
-    part[ch][lp] = acc;
-  }
-  __syncthreads();
-  if (ch != 0 || !live) return;
-  float gsum;
-  if (a.slab) {
-    gsum = 0.f;
-#pragma unroll
-    for (int k = 0; k < RC; ++k) gsum += part[k][lp];
-    if (a.t.grad[pi]) a.t.grad[pi][e] = gsum;
-  } else {  // gradients supplied (e.g. after an RCCL all-reduce): Adam only
-    gsum = gin;
-  }
-  if (upd) {
-    float bc1 = a.adam.bias_c1, bc2s = a.adam.bias_c2_sqrt;
-    if (a.adam.step_counter) {  // step and bias corrections from the device counter
-      const int64_t t = a.adam.step_counter[1] + 1;
-      bc1 = 1.f - powf(a.adam.beta1, (float)t);
-      bc2s = sqrtf(1.f - powf(a.adam.beta2, (float)t));
-      if (gi == 0) a.adam.step_counter[0] = t;
-    }
-    float gr = gsum;
-    if (a.adam.weight_decay != 0.f) gr = fmaf(a.adam.weight_decay, p0, gr);
-    // torch.optim.Adam: exp_avg.lerp_(g, 1-b1); exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
-    const float mv = m0 + (1.f - a.adam.beta1) * (gr - m0);
-    const float vv = fmaf((1.f - a.adam.beta2) * gr, gr, v0 * a.adam.beta2);
-    a.t.exp_avg[pi][e] = mv;
-    a.t.exp_avg_sq[pi][e] = vv;
-    const float denom = sqrtf(vv) / bc2s + a.adam.eps;
-    a.t.param[pi][e] = p0 - (a.adam.lr / bc1) * (mv / denom);
-  }
-}
-
 }  // namespace
 
 extern "C" int64_t dr_ginet_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_feat, int32_t k0, int32_t p1_edges,
@@ -785,7 +660,7 @@ extern "C" int64_t dr_ginet_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t 
 }
 
 extern "C" int dr_ginet_graph_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
-                                   const dr_ginet_weights* w, const dr_ginet_pass* pass, int32_t lds_bytes,
+                                   const dr_ginet_weights* w, const dr_pass* pass, int32_t lds_bytes,
                                    void* stream) {
   if (!store || !descs || !w || !pass || n_batch < 0) return DR_E_ARG;
   if (pass->out_dim < 1 || pass->out_dim > DR_MAX_OUT) return DR_E_UNSUPPORTED;
@@ -805,35 +680,6 @@ extern "C" int dr_ginet_graph_pass(const dr_graph_store* store, const dr_graph_d
   args.descs = descs;
   args.B = n_batch;
   hipLaunchKernelGGL(ginet_graph_kernel, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, args);
-  return (int)hipGetLastError();
-}
-
-extern "C" int dr_ginet_reduce_update(const dr_param_table* t, int32_t n_feat, int32_t out_dim, const float* slab,
-                                      const float* head, int32_t n_batch, const dr_adam* adam,
-                                      const float* loss_per_graph, float loss_scale, float* loss_out, void* stream) {
-  if (!t || !adam || n_batch < 0) return DR_E_ARG;
-  if ((slab == nullptr) != (head == nullptr)) return DR_E_ARG;
-  ReduceArgs a;
-  std::memset(&a, 0, sizeof(a));
-  a.t = *t;
-  a.adam = *adam;
-  a.slab = slab;
-  a.head = head;
-  a.lpg = loss_per_graph;
-  a.loss_out = loss_out;
-  a.loss_scale = loss_scale;
-  a.F = n_feat;
-  a.OUT = out_dim;
-  a.B = n_batch;
-  a.off[0] = 0;
-  for (int i = 0; i < DR_GINET_NPARAM; ++i) {
-    if (t->numel[i] < 0 || !t->param[i]) return DR_E_ARG;
-    if (adam->enabled && (!t->exp_avg[i] || !t->exp_avg_sq[i])) return DR_E_ARG;
-    if (!slab && !t->grad[i]) return DR_E_ARG;
-    a.off[i + 1] = a.off[i] + t->numel[i];
-  }
-  const int total = a.off[DR_GINET_NPARAM];
-  hipLaunchKernelGGL(ginet_reduce_kernel, dim3((total + RP - 1) / RP), dim3(RP * RC), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
 

@@ -1,0 +1,90 @@
+// Device helpers shared by the per-graph fused kernels (gfx950, wave64).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/deeprank2_amd.h"
+#include "dr_common.h"
+
+namespace drk {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+constexpr float LOWEST = -3.402823466e+38f;
+
+__host__ __device__ inline int r4(int v) { return (v + 3) & ~3; }
+__host__ __device__ inline int r16(int v) { return (v + 15) & ~15; }
+__host__ __device__ inline int imax(int a, int b) { return a > b ? a : b; }
+
+// torch relu keeps NaN (clamp_min propagates it); its backward masks where the
+// output is <= 0 (threshold_backward), so a NaN output passes the gradient.
+__device__ __forceinline__ float relu_keepnan(float v) { return (v <= 0.f) ? 0.f : v; }
+__device__ __forceinline__ float relu_bwd(float out, float g) { return (out <= 0.f) ? 0.f : g; }
+
+#define DRK_AS1(p) ((const __attribute__((address_space(1))) void*)(p))
+#define DRK_AS3(p) ((__attribute__((address_space(3))) void*)(p))
+
+// Asynchronous global->LDS copy of n 4-byte words (global_load_lds_dword: one
+// wave instruction moves 256 contiguous bytes).  M0 (the LDS base) is
+// wave-uniform; lane l lands at base + 4l.
+template <int NT>
+__device__ __forceinline__ void dma_words(void* lds_dst, const void* gsrc, int n) {
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(gsrc);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(lds_dst);
+  for (int base = wave * 64; base < n; base += NT)
+    if (base + lane < n) __builtin_amdgcn_global_load_lds(DRK_AS1(src + base + lane), DRK_AS3(dst + base), 4, 0, 0);
+}
+
+// 16-byte lanes (global_load_lds_dwordx4, 1 KiB per wave instruction); source
+// and destination 16-byte aligned; n4 = number of 16-byte units.
+template <int NT>
+__device__ __forceinline__ void dma_x4(void* lds_dst, const void* gsrc, int n4) {
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint4* src = reinterpret_cast<const uint4*>(gsrc);
+  uint4* dst = reinterpret_cast<uint4*>(lds_dst);
+  for (int base = wave * 64; base < n4; base += NT)
+    if (base + lane < n4) __builtin_amdgcn_global_load_lds(DRK_AS1(src + base + lane), DRK_AS3(dst + base), 16, 0, 0);
+}
+
+__device__ __forceinline__ float4 f4add(float4 a, float4 v) {
+  return make_float4(a.x + v.x, a.y + v.y, a.z + v.z, a.w + v.w);
+}
+
+// acc = sum over CSR row [eb, ee) of X[col[e], c4..c4+3] in edge order (the
+// order torch_scatter's CPU scatter_add_ visits them).  Four index reads, then
+// four row reads in flight per step.  The empty asm keeps the four 16-bit
+// index reads separate: hipcc would otherwise merge them into a ds_read_b64
+// that is misaligned for 3 of 4 row starts (LDS replays those at ~64 cycles).
+__device__ __forceinline__ float4 gather_row_chunk(const uint16_t* col, int eb, int ee, const float* X, int XS,
+                                                   int c4) {
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  int e = eb;
+  for (; e + 4 <= ee; e += 4) {
+    int e1 = e + 1, e2 = e + 2, e3 = e + 3;
+    asm volatile("" : "+v"(e1), "+v"(e2), "+v"(e3));
+    const int j0 = col[e], j1 = col[e1], j2 = col[e2], j3 = col[e3];
+    const float4 v0 = *reinterpret_cast<const float4*>(&X[__umul24(j0, XS) + c4]);
+    const float4 v1 = *reinterpret_cast<const float4*>(&X[__umul24(j1, XS) + c4]);
+    const float4 v2 = *reinterpret_cast<const float4*>(&X[__umul24(j2, XS) + c4]);
+    const float4 v3 = *reinterpret_cast<const float4*>(&X[__umul24(j3, XS) + c4]);
+    acc = f4add(f4add(f4add(f4add(acc, v0), v1), v2), v3);
+  }
+  for (; e < ee; ++e) acc = f4add(acc, *reinterpret_cast<const float4*>(&X[__umul24((int)col[e], XS) + c4]));
+  return acc;
+}
+
+}  // namespace drk
+
+#ifdef DR_STAMPS
+#define DRK_STAMP(i)                                                                              \
+  do {                                                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    if (tid == 0 && a.p.stamps) a.p.stamps[(int64_t)b * 32 + (i)] = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+  } while (0)
+#else
+#define DRK_STAMP(i) \
+  do {               \
+  } while (0)
+#endif

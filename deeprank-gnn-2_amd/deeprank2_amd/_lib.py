@@ -22,7 +22,11 @@ DR_MAX_OUT = 16
 DR_DROPOUT_OFF = 0
 DR_DROPOUT_MASK = 1
 DR_DROPOUT_HASH = 2
-DR_GINET_NPARAM = 16
+DR_MAX_PARAMS = 24
+DR_GRAD_ZERO = 0
+DR_GRAD_SLAB = 1
+DR_GRAD_OUTER = 2
+DR_GRAD_HEAD = 3
 
 ERRORS = {-1: "bad argument", -2: "graph does not fit the per-graph LDS kernel", -3: "unsupported configuration"}
 
@@ -66,7 +70,7 @@ class GinetWeightsC(ctypes.Structure):
     _fields_ = [(n, VP) for n in ("w1", "w1e", "w2", "w2e", "fc1w", "fc1b", "fc2w", "fc2b")]
 
 
-class GinetPassC(ctypes.Structure):
+class PassC(ctypes.Structure):
     _fields_ = [
         ("flags", ctypes.c_int32),
         ("out_dim", ctypes.c_int32),
@@ -104,21 +108,30 @@ class AdamC(ctypes.Structure):
     ]
 
 
+class GradRecipeC(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("off1", ctypes.c_int32), ("off2", ctypes.c_int32), ("cols", ctypes.c_int32)]
+
+
 class ParamTableC(ctypes.Structure):
     _fields_ = [
-        ("param", VP * DR_GINET_NPARAM),
-        ("grad", VP * DR_GINET_NPARAM),
-        ("exp_avg", VP * DR_GINET_NPARAM),
-        ("exp_avg_sq", VP * DR_GINET_NPARAM),
-        ("numel", ctypes.c_int32 * DR_GINET_NPARAM),
+        ("param", VP * DR_MAX_PARAMS),
+        ("grad", VP * DR_MAX_PARAMS),
+        ("exp_avg", VP * DR_MAX_PARAMS),
+        ("exp_avg_sq", VP * DR_MAX_PARAMS),
+        ("numel", ctypes.c_int32 * DR_MAX_PARAMS),
+        ("recipe", GradRecipeC * DR_MAX_PARAMS),
+        ("n_params", ctypes.c_int32),
+        ("slab_stride", ctypes.c_int32),
+        ("head_stride", ctypes.c_int32),
+        ("pad0", ctypes.c_int32),
     ]
 
 
 # (name, restype, argtypes) for every entry of include/deeprank2_amd.h
 SIGNATURES = [
-    ("dr_ginet_graph_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(GinetWeightsC), ctypes.POINTER(GinetPassC), ctypes.c_int32, VP]),
+    ("dr_ginet_graph_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, VP]),
     ("dr_ginet_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 8),
-    ("dr_ginet_reduce_update", ctypes.c_int, [ctypes.POINTER(ParamTableC), ctypes.c_int32, ctypes.c_int32, VP, VP, ctypes.c_int32, ctypes.POINTER(AdamC), VP, ctypes.c_float, VP, VP]),
+    ("dr_reduce_update", ctypes.c_int, [ctypes.POINTER(ParamTableC), VP, VP, ctypes.c_int32, ctypes.POINTER(AdamC), VP, ctypes.c_float, VP, VP]),
     ("dr_csr_from_coo", ctypes.c_int, [VP, VP, ctypes.c_int64, ctypes.c_int32, VP, VP, VP, VP, VP]),
     ("dr_spmm_csr", ctypes.c_int, [VP, VP, VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP, VP]),
     ("dr_linear_xwT", ctypes.c_int, [VP, VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP, VP]),

@@ -1,10 +1,12 @@
-"""Fused GINet training step: the hot loop of ``Trainer._epoch``
-(reference ``deeprank2/trainer.py:682-690``) in two launches per mini-batch.
+"""Fused training step: the hot loop of ``Trainer._epoch``
+(reference ``deeprank2/trainer.py:682-690``) in two launches per mini-batch,
+for any model with a ``fused_spec`` (GINet, FoutNet).
 
-1. ``dr_ginet_graph_pass`` (FORWARD|BACKWARD, loss in-kernel): one workgroup
-   per graph computes the prediction, the loss term and the whole backward of
-   its graph, writing per-graph partials;
-2. ``dr_ginet_reduce_update``: sums the partials into the 16 gradients and
+1. the model's graph pass (``dr_ginet_graph_pass`` / ``dr_fout_graph_pass``;
+   FORWARD|BACKWARD, loss in-kernel): one workgroup per graph computes the
+   prediction, the loss term and the whole backward of its graph, writing
+   per-graph partials;
+2. ``dr_reduce_update``: sums the partials into every gradient and
    applies ``torch.optim.Adam`` (lr, betas, eps, L2 ``weight_decay`` as
    ``Trainer.configure_optimizers`` sets them, trainer.py:401-428).
 
@@ -24,12 +26,13 @@ from __future__ import annotations
 import torch
 
 from deeprank2_amd import _lib
-from deeprank2_amd.neuralnets.gnn.ginet import BatchHandle, GINet, head_stride, slab_stride, weights_c
+from deeprank2_amd.fused import BatchHandle, lds_for, param_table
 
 
-class GINetTrainStep:
-    def __init__(self, model: GINet, lr=1e-3, weight_decay=1e-5, betas=(0.9, 0.999), eps=1e-8, loss="mse", class_weights=None, process_group=None, max_batch=64):
+class FusedTrainStep:
+    def __init__(self, model, lr=1e-3, weight_decay=1e-5, betas=(0.9, 0.999), eps=1e-8, loss="mse", class_weights=None, process_group=None, max_batch=64):
         self.model = model
+        self.spec = model.fused_spec
         self.params = model.ordered_params()
         for p in self.params:
             if not p.is_cuda or not p.is_contiguous() or p.dtype != torch.float32:
@@ -54,7 +57,7 @@ class GINetTrainStep:
         self.step_count = 0
         self.loss_out = torch.zeros(1, dtype=torch.float32, device=dev)
         self.kernel_events = None  # list -> (start, end) HIP events around each graph pass
-        if model._drop_seed is None:
+        if getattr(model, "_drop_seed", 0) is None:
             model._drop_seed = int(torch.randint(0, 2**62, (1,)).item())
         self._cap = 0
         self._ensure(max_batch)
@@ -65,19 +68,19 @@ class GINetTrainStep:
             return
         f = self.model.input_shape
         dev = self.device
-        self.slab = torch.empty(b * slab_stride(f), dtype=torch.float32, device=dev)
-        self.head = torch.empty(b * head_stride(self.out_dim), dtype=torch.float32, device=dev)
+        self.slab = torch.empty(b * self.spec.slab_stride(f), dtype=torch.float32, device=dev)
+        self.head = torch.zeros(b * self.spec.head_stride(self.out_dim), dtype=torch.float32, device=dev)
         self.lpg = torch.empty(b, dtype=torch.float32, device=dev)
         self.out = torch.empty(b, self.out_dim, dtype=torch.float32, device=dev)
         self._cap = b
         self._build_structs()
 
     def _build_structs(self):
-        p = _lib.GinetPassC()
+        p = _lib.PassC()
         p.flags = _lib.DR_PASS_FORWARD | _lib.DR_PASS_BACKWARD
         p.out_dim = self.out_dim
         p.loss_kind = _lib.DR_LOSS_MSE if self.loss == "mse" else _lib.DR_LOSS_CE
-        if self.model.dropout > 0:
+        if self.spec.dropout > 0 and self.model.dropout > 0:
             p.use_dropout = _lib.DR_DROPOUT_HASH
             p.drop_p = self.model.dropout
             p.drop_scale = 1.0 / (1.0 - self.model.dropout)
@@ -89,17 +92,10 @@ class GINetTrainStep:
         p.head = self.head.data_ptr()
         p.step_counter = self.counter.data_ptr()
         self._pass = p
-        self._pass_nodrop = _lib.GinetPassC.from_buffer_copy(p)
+        self._pass_nodrop = _lib.PassC.from_buffer_copy(p)
         self._pass_nodrop.use_dropout = _lib.DR_DROPOUT_OFF
-        self._w = weights_c(self.params)
-        t = _lib.ParamTableC()
-        for i, prm in enumerate(self.params):
-            t.param[i] = prm.data_ptr()
-            t.grad[i] = self.grads[i].data_ptr()
-            t.exp_avg[i] = self.states[i][0].data_ptr()
-            t.exp_avg_sq[i] = self.states[i][1].data_ptr()
-            t.numel[i] = prm.numel()
-        self._table = t
+        self._w = self.spec.weights(self.params)
+        self._table = param_table(self.spec, self.params, self.grads, self.states, self.model.input_shape, self.out_dim)
         a = _lib.AdamC()
         a.lr, (a.beta1, a.beta2), a.eps, a.weight_decay = self.lr, self.betas, self.eps, self.weight_decay
         a.enabled = 1
@@ -134,31 +130,31 @@ class GINetTrainStep:
         lib = _lib.load()
         stream = _lib.stream_ptr(self.device)
         if mask is not None:
-            p = _lib.GinetPassC.from_buffer_copy(self._pass)
+            p = _lib.PassC.from_buffer_copy(self._pass)
             p.use_dropout = _lib.DR_DROPOUT_MASK
             p.drop_scale = 1.0 / (1.0 - self.model.dropout)
             p.mask = mask.data_ptr()
         else:
-            p = self._pass if (dropout and self.model.dropout > 0) else self._pass_nodrop
+            p = self._pass if (dropout and self.spec.dropout > 0 and self.model.dropout > 0) else self._pass_nodrop
         p.loss_scale = scale
         ev = self.kernel_events
         if ev is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        _lib.check(lib.dr_ginet_graph_pass(h.store.cstruct(), h.descs.data_ptr(), h.B, self._w, p, h.lds(self.out_dim), stream), "dr_ginet_graph_pass")
+        entry = getattr(lib, self.spec.entry)
+        _lib.check(entry(h.store.cstruct(), h.descs.data_ptr(), h.B, self._w, p, lds_for(self.spec, h, self.out_dim), stream), self.spec.entry)
         if ev is not None:
             e1.record()
             ev.append((e0, e1))
         self.step_count += 1
-        f = self.model.input_shape
         slab, head, lpg, lout = self.slab.data_ptr(), self.head.data_ptr(), self.lpg.data_ptr(), self.loss_out.data_ptr()
         if self.world == 1:
-            _lib.check(lib.dr_ginet_reduce_update(self._table, f, self.out_dim, slab, head, h.B, self._adam, lpg, scale, lout, stream), "dr_ginet_reduce_update")
+            _lib.check(lib.dr_reduce_update(self._table, slab, head, h.B, self._adam, lpg, scale, lout, stream), "dr_reduce_update")
         else:
-            _lib.check(lib.dr_ginet_reduce_update(self._table, f, self.out_dim, slab, head, h.B, self._adam_off, lpg, scale, lout, stream), "dr_ginet_reduce_update")
+            _lib.check(lib.dr_reduce_update(self._table, slab, head, h.B, self._adam_off, lpg, scale, lout, stream), "dr_reduce_update")
             torch.distributed.all_reduce(self.flat_grad, group=self.pg)
             torch.distributed.all_reduce(self.loss_out, group=self.pg)
-            _lib.check(lib.dr_ginet_reduce_update(self._table, f, self.out_dim, None, None, h.B, self._adam, None, 1.0, None, _lib.stream_ptr(self.device)), "dr_ginet_reduce_update")
+            _lib.check(lib.dr_reduce_update(self._table, None, None, h.B, self._adam, None, 1.0, None, _lib.stream_ptr(self.device)), "dr_reduce_update")
         return self.loss_out, self.out[: h.B]
 
     def _state_tensors(self):
@@ -184,3 +180,6 @@ class GINetTrainStep:
             t.data.copy_(s)
         self.step_count = n
         return g
+
+
+GINetTrainStep = FusedTrainStep  # GINet's fused spec drives it

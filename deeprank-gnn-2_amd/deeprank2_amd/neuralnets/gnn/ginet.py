@@ -29,12 +29,11 @@ from __future__ import annotations
 
 import math
 
-import numpy as np
 import torch
 from torch import nn
 
 from deeprank2_amd import _lib, ops
-from deeprank2_amd.store import GraphStore, pack_graphs, records_from_batch
+from deeprank2_amd.fused import BatchHandle, Dropout, FusedFn, FusedSpec, make_pass, resolve_batch, run_pass  # noqa: F401
 
 
 def _uniform(size, t):
@@ -111,7 +110,7 @@ class GINetConvLayer(nn.Module):
 
 
 # ---------------------------------------------------------------------------
-# Fused per-graph engine
+# Fused per-graph path (dr_ginet_graph_pass + dr_reduce_update)
 # ---------------------------------------------------------------------------
 
 PARAM_NAMES = [
@@ -124,44 +123,26 @@ PARAM_NAMES = [
 
 
 def slab_stride(f):
+    """Per-graph conv gradient partials: [W1;W1e] (32 x F), then [W2 | W2e] (1024)."""
     return 32 * f + 1024
 
 
 def head_stride(out):
+    """Per-graph head vectors: g (64), dropped fc1 output (128), its grad (128), dout."""
     return 320 + ((out + 3) & ~3)
 
 
-class BatchHandle:
-    """A mini-batch as the kernels see it: a store + graph ids (host and device)."""
-
-    def __init__(self, store: GraphStore, gids_host: np.ndarray):
-        self.store = store
-        self.gids_host = np.ascontiguousarray(gids_host, dtype=np.int32)
-        self.gids = torch.from_numpy(self.gids_host).to(store.device)
-        self.descs = store.descriptors(self.gids_host)
-        self.B = int(self.gids_host.size)
-        self.max_sizes = store.max_sizes(self.gids_host)
-        self._lds = {}
-
-    def lds(self, out_dim):
-        v = self._lds.get(out_dim)
-        if v is None:
-            n, e, k0, p1, k1 = self.max_sizes
-            v = int(_lib.load().dr_ginet_lds_bytes(n, e, self.store.n_feat, k0, p1, k1, int(self.store.packed.transpose_aliased), out_dim))
-            if v > 160 * 1024:
-                msg = f"largest graph of the batch needs {v} B of LDS (> 160 KiB): the streamed large-graph path is not built yet"
-                raise RuntimeError(msg)
-            self._lds[out_dim] = v
-        return v
-
-
-def resolve_batch(data, device) -> BatchHandle:
-    """Our DataLoader attaches a handle; any other PyG-style batch is packed here."""
-    h = getattr(data, "_dr_handle", None)
-    if h is not None:
-        return h
-    store = GraphStore(pack_graphs(records_from_batch(data)), device)
-    return BatchHandle(store, np.arange(store.n_graphs, dtype=np.int32))
+def recipe(f, out):
+    z = (_lib.DR_GRAD_ZERO, 0, 0, 0)  # attention weights: exact zeros (ginet.py:54)
+    slab = _lib.DR_GRAD_SLAB
+    return [
+        (slab, 0, 0, 0), z, z,
+        (slab, 32 * f, 0, 0), z, z,
+        (slab, 16 * f, 0, 0), z, z,
+        (slab, 32 * f + 512, 0, 0), z, z,
+        (_lib.DR_GRAD_OUTER, 192, 0, 64), (_lib.DR_GRAD_HEAD, 192, 0, 0),
+        (_lib.DR_GRAD_OUTER, 320, 64, 128), (_lib.DR_GRAD_HEAD, 320, 0, 0),
+    ]  # fmt: skip
 
 
 def weights_c(params):
@@ -173,88 +154,16 @@ def weights_c(params):
     return w
 
 
-class Dropout:
-    """How fc1's output is dropped: ``mask`` (uint8 [B,128] keep mask) or the
-    in-kernel counter hash ``(seed, offset)`` with probability ``p``."""
-
-    def __init__(self, p, mask=None, seed=None, offset=0):
-        self.p = float(p)
-        self.mask = mask
-        self.seed = seed
-        self.offset = int(offset)
-
-    @property
-    def scale(self):
-        return 1.0 / (1.0 - self.p)
+def _lds(n, e, k0, p1, k1, f, alias, out):
+    return _lib.load().dr_ginet_lds_bytes(n, e, f, k0, p1, k1, alias, out)
 
 
-def graph_pass(h: BatchHandle, params, out_dim, flags, *, dropout: Dropout | None = None, dout=None, loss_kind=_lib.DR_LOSS_NONE, loss_scale=1.0, class_w=None, out=None, loss_per_graph=None, slab=None, head=None, stamps=None):
-    dev = h.store.device
-    p = _lib.GinetPassC()
-    p.flags = flags
-    p.out_dim = out_dim
-    p.loss_kind = loss_kind
-    mask = None
-    if dropout is None:
-        p.use_dropout = _lib.DR_DROPOUT_OFF
-    elif dropout.mask is not None:
-        mask = dropout.mask
-        p.use_dropout = _lib.DR_DROPOUT_MASK
-        p.drop_scale = dropout.scale
-    else:
-        p.use_dropout = _lib.DR_DROPOUT_HASH
-        p.drop_scale = dropout.scale
-        p.drop_p = dropout.p
-        p.drop_seed = dropout.seed
-        p.drop_offset = dropout.offset
-    p.loss_scale = loss_scale
-    p.mask = _lib.ptr(mask)
-    p.class_w = _lib.ptr(class_w)
-    p.out = _lib.ptr(out)
-    p.dout = _lib.ptr(dout)
-    p.loss_per_graph = _lib.ptr(loss_per_graph)
-    p.slab = _lib.ptr(slab)
-    p.head = _lib.ptr(head)
-    p.stamps = _lib.ptr(stamps)
-    w = weights_c(params)
-    rc = _lib.load().dr_ginet_graph_pass(h.store.cstruct(), h.descs.data_ptr(), h.B, w, p, h.lds(out_dim), _lib.stream_ptr(dev))
-    _lib.check(rc, "dr_ginet_graph_pass")
+SPEC = FusedSpec(PARAM_NAMES, recipe, slab_stride, head_stride, "dr_ginet_graph_pass", weights_c, _lds, dropout=0.4)
 
 
-def reduce_update(h: BatchHandle, params, grads, out_dim, slab, head, adam=None, states=None, loss_per_graph=None, loss_scale=1.0, loss_out=None):
-    t = _lib.ParamTableC()
-    for i, prm in enumerate(params):
-        t.param[i] = prm.data_ptr()
-        t.grad[i] = None if grads is None or grads[i] is None else grads[i].data_ptr()
-        t.numel[i] = prm.numel()
-        if states is not None:
-            t.exp_avg[i] = states[i][0].data_ptr()
-            t.exp_avg_sq[i] = states[i][1].data_ptr()
-    a = adam if adam is not None else _lib.AdamC()
-    rc = _lib.load().dr_ginet_reduce_update(t, h.store.n_feat, out_dim, _lib.ptr(slab), _lib.ptr(head), h.B, a, _lib.ptr(loss_per_graph), loss_scale, _lib.ptr(loss_out), _lib.stream_ptr(h.store.device))
-    _lib.check(rc, "dr_ginet_reduce_update")
-
-
-class _GINetFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, h, dropout, out_dim, *params):
-        out = torch.empty(h.B, out_dim, dtype=torch.float32, device=h.store.device)
-        graph_pass(h, params, out_dim, _lib.DR_PASS_FORWARD, dropout=dropout, out=out)
-        ctx.h, ctx.dropout, ctx.out_dim = h, dropout, out_dim
-        ctx.save_for_backward(*params)
-        return out
-
-    @staticmethod
-    def backward(ctx, dout):
-        params = ctx.saved_tensors
-        h, out_dim = ctx.h, ctx.out_dim
-        dev = h.store.device
-        slab = torch.empty(h.B * slab_stride(h.store.n_feat), dtype=torch.float32, device=dev)
-        head = torch.empty(h.B * head_stride(out_dim), dtype=torch.float32, device=dev)
-        graph_pass(h, params, out_dim, _lib.DR_PASS_BACKWARD, dropout=ctx.dropout, dout=dout.contiguous(), slab=slab, head=head)
-        grads = [torch.empty_like(p) for p in params]
-        reduce_update(h, params, grads, out_dim, slab, head)
-        return (None, None, None, *grads)
+def graph_pass(h: BatchHandle, params, out_dim, flags, **kw):
+    """One dr_ginet_graph_pass launch (see fused.make_pass for the keywords)."""
+    run_pass(SPEC, h, params, make_pass(out_dim, flags, **kw))
 
 
 class GINet(nn.Module):
@@ -274,6 +183,8 @@ class GINet(nn.Module):
         self.output_shape = output_shape
         self._drop_seed = None
         self._drop_calls = 0
+
+    fused_spec = SPEC
 
     def ordered_params(self):
         named = dict(self.named_parameters())
@@ -303,4 +214,4 @@ class GINet(nn.Module):
                 dropout = Dropout(self.dropout, mask=dropout_mask.to(device=dev, dtype=torch.uint8).contiguous())
             else:
                 dropout = self.next_dropout()
-        return _GINetFn.apply(h, dropout, self.output_shape, *params)
+        return FusedFn.apply(SPEC, h, dropout, self.output_shape, *params)

@@ -18,7 +18,7 @@
  *                           deeprank2/utils/community_pooling.py:23-27,165-242),
  *                           plus the loss gradient of Trainer._epoch
  *                           (deeprank2/trainer.py:686-689)
- *   dr_ginet_reduce_update  loss_.backward() parameter-gradient reduction and
+ *   dr_reduce_update        loss_.backward() parameter-gradient reduction and
  *                           optimizer.step() of Trainer._epoch
  *                           (trainer.py:689-690; torch.optim.Adam configured at
  *                           trainer.py:419)
@@ -116,7 +116,7 @@ typedef struct dr_ginet_weights {
 #define DR_DROPOUT_MASK 1  /* keep mask given in pass->mask        */
 #define DR_DROPOUT_HASH 2  /* counter-based hash, see dr_dropout_mask */
 
-typedef struct dr_ginet_pass {
+typedef struct dr_pass {
   int32_t flags;        /* DR_PASS_* bitmask                                   */
   int32_t out_dim;      /* fc2 rows                                            */
   int32_t loss_kind;    /* DR_LOSS_*                                           */
@@ -137,9 +137,9 @@ typedef struct dr_ginet_pass {
   int64_t* stamps;      /* diagnostic builds only (-DDR_STAMPS): [B, 32] s_memtime per phase; NULL */
   int64_t* step_counter;/* optional device [2]: drop_offset := counter[0] (read by every
                            workgroup); workgroup 0 snapshots counter[0] into counter[1] for
-                           dr_ginet_reduce_update, which advances counter[0].  Makes a
+                           dr_reduce_update, which advances counter[0].  Makes a
                            step's launch arguments constant (hipGraph replay).            */
-} dr_ginet_pass;
+} dr_pass;
 
 /* One workgroup per graph: conv1 -> depth-0 community pooling -> conv2 ->
  * depth-1 max pooling -> per-graph mean -> fc1/relu/dropout/fc2, and (when
@@ -147,7 +147,7 @@ typedef struct dr_ginet_pass {
  * descs: [B] device descriptors of the batch's graphs.  lds_bytes: the
  * dynamic LDS the largest graph of the batch needs (dr_ginet_lds_bytes).  */
 int dr_ginet_graph_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
-                        const dr_ginet_weights* w, const dr_ginet_pass* pass,
+                        const dr_ginet_weights* w, const dr_pass* pass,
                         int32_t lds_bytes, void* stream);
 
 /* Dynamic LDS bytes dr_ginet_graph_pass needs for a graph of these sizes.  */
@@ -160,33 +160,45 @@ typedef struct dr_adam {
   float bias_c1;      /* 1 - beta1^step                                        */
   float bias_c2_sqrt; /* sqrt(1 - beta2^step)                                  */
   int32_t enabled;    /* 0: only write gradients                              */
-  int64_t* step_counter; /* optional device [2] (see dr_ginet_pass): step = counter[1]+1,
+  int64_t* step_counter; /* optional device [2] (see dr_pass): step = counter[1]+1,
                             bias corrections computed on the device, and (when enabled)
                             counter[0] := step; overrides bias_c1 / bias_c2_sqrt    */
 } dr_adam;
 
-/* Parameter table in the order of GINet.named_parameters(): 16 tensors
- * (4 x {fc, fc_edge_attr, fc_attention}.weight, fc1.{weight,bias},
- * fc2.{weight,bias}).                                                      */
-#define DR_GINET_NPARAM 16
+/* How one parameter's gradient is assembled from the per-graph partials the
+ * graph passes write ([B, slab_stride] slab and [B, head_stride] head rows).  */
+#define DR_GRAD_ZERO 0  /* exact zeros (GINet's attention weights, ginet.py:54)      */
+#define DR_GRAD_SLAB 1  /* sum_b slab[b, off1 + e]                                   */
+#define DR_GRAD_OUTER 2 /* sum_b head[b, off1 + e / cols] * head[b, off2 + e % cols]  */
+#define DR_GRAD_HEAD 3  /* sum_b head[b, off1 + e]                                   */
+typedef struct dr_grad_recipe {
+  int32_t kind, off1, off2, cols;
+} dr_grad_recipe;
+
+/* Parameter table, in the model's named_parameters() order.                 */
+#define DR_MAX_PARAMS 24
 typedef struct dr_param_table {
-  float* param[DR_GINET_NPARAM];
-  float* grad[DR_GINET_NPARAM];   /* may be NULL (grad not materialised)       */
-  float* exp_avg[DR_GINET_NPARAM];
-  float* exp_avg_sq[DR_GINET_NPARAM];
-  int32_t numel[DR_GINET_NPARAM];
+  float* param[DR_MAX_PARAMS];
+  float* grad[DR_MAX_PARAMS];       /* may be NULL (gradient not materialised) */
+  float* exp_avg[DR_MAX_PARAMS];
+  float* exp_avg_sq[DR_MAX_PARAMS];
+  int32_t numel[DR_MAX_PARAMS];
+  dr_grad_recipe recipe[DR_MAX_PARAMS];
+  int32_t n_params;
+  int32_t slab_stride;
+  int32_t head_stride;
+  int32_t pad0;
 } dr_param_table;
 
-/* Sum the per-graph partials of dr_ginet_graph_pass over the batch into the
- * 16 GINet gradients (dead attention weights get exact zeros), optionally
- * apply Adam.  With slab == head == NULL the gradients are read from
- * t->grad (e.g. after a data-parallel all-reduce) and only Adam runs.  Also
- * write loss_scale * sum(loss_per_graph) to loss_out[0]
- * when both are non-NULL.  */
-int dr_ginet_reduce_update(const dr_param_table* t, int32_t n_feat, int32_t out_dim,
-                           const float* slab, const float* head, int32_t n_batch,
-                           const dr_adam* adam, const float* loss_per_graph, float loss_scale,
-                           float* loss_out, void* stream);
+/* Sum the per-graph partials of a graph pass over the batch into every
+ * parameter's gradient in a fixed order (deterministic, no float atomics),
+ * optionally apply Adam (torch.optim.Adam semantics).  With slab == head ==
+ * NULL the gradients are read from t->grad (e.g. after a data-parallel
+ * all-reduce) and only Adam runs.  Also writes loss_scale * sum(loss_per_graph)
+ * to loss_out[0] when both are non-NULL.                                    */
+int dr_reduce_update(const dr_param_table* t, const float* slab, const float* head, int32_t n_batch,
+                     const dr_adam* adam, const float* loss_per_graph, float loss_scale, float* loss_out,
+                     void* stream);
 
 /* ---- generic layer kernels (arbitrary edge lists; GINetConvLayer API) ---- */
 

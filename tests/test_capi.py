@@ -40,9 +40,9 @@ def test_struct_layouts_match_header():
     # 4 int32 + 20 pointers; 8 pointers; 4 int32 + 2 float + 2 uint64 + float/int32 + 7 pointers
     assert ctypes.sizeof(_lib.GraphStoreC) == 16 + 20 * 8
     assert ctypes.sizeof(_lib.GinetWeightsC) == 8 * 8
-    assert ctypes.sizeof(_lib.GinetPassC) == 16 + 8 + 16 + 8 + 9 * 8
+    assert ctypes.sizeof(_lib.PassC) == 16 + 8 + 16 + 8 + 9 * 8
     assert ctypes.sizeof(_lib.AdamC) == 32 + 8
-    assert ctypes.sizeof(_lib.ParamTableC) == 4 * 16 * 8 + 16 * 4
+    assert ctypes.sizeof(_lib.ParamTableC) == 4 * 24 * 8 + 24 * 4 + 24 * 16 + 16
 
 
 def test_library_is_built_for_gfx950():
