@@ -1,0 +1,540 @@
+// FoutNet training step, one workgroup per graph, everything resident in LDS.
+//
+// Replaces (deeprank2 v3.1.0):
+//   FoutLayer.forward      deeprank2/neuralnets/gnn/foutnet.py:48-66
+//   FoutNet.forward        foutnet.py:99-118
+//   get_preloaded_cluster / community_pooling / max_pool_x / scatter_mean
+//                          (community_pooling.py:23-27,165-242; foutnet.py:105-114)
+//   autograd backward + loss (deeprank2/trainer.py:686-689)
+//
+// FoutLayer: out_i = x_i Wc + mean_{e=(i->j)} (x_j Wn) + b, NaN when node i has
+// no out-edge (mean over an empty set, foutnet.py:58).  By linearity this is
+// [x_i | mean_j x_j] [Wc; Wn] + b: the reference's O(N·E) Python loop becomes a
+// CSR gather of X (Zm = D^-1 A X, 0/0 = NaN on empty rows) and one MFMA GEMM
+// whose A operand reads X for k < F and Zm for F <= k < 2F.
+// Backward: the depth-0 max pool routes each channel's gradient to one
+// member per cluster, so dWc = sum_k v_k x[arg_k], dWn = sum_k v_k Zm[arg_k]
+// and db = sum_k v_k — no gather over the edges.  The pooled conv2 backward
+// scatters through the transposed pooled CSR.
+
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include "graph_common.h"
+
+namespace {
+
+using namespace drk;
+
+constexpr int NT = 1024;
+constexpr int NW = NT / 64;
+constexpr int HEADW = 512;  // G32 hpre64 hh64 dh64 dG32 dout16 spare
+
+struct Carve {
+  int KP, XS, LDZ;
+  int wc1, w2, fc1, fc2, x, zm, h1, rp, col, m0p, m0i, p1, a1, dp1, zm2, s2, h2, d2, dz2, p1rp, p1c, p1trp, p1tc,
+      m1p, m1i, p2, nt, head, dgp, red, total;
+};
+
+// X keeps the HBM row stride XS = r4(F) (16-byte rows: DMA + float4 gather);
+// Zm uses LDZ = r4(F)+2 (LDZ = 2 mod 32 or an odd multiple of 2 mod 32: the
+// MFMA column reads of lanes (row li, k+kq) hit distinct banks).
+__host__ __device__ inline Carve carve(int N, int E, int F, int K0, int P1, int K1, int alias, int OUT) {
+  Carve c;
+  c.KP = r16(2 * F);
+  c.XS = r4(F);
+  c.LDZ = c.XS + 2;
+  int o = 0;
+#define TAKE(field, words) \
+  c.field = o;             \
+  o += r4(words);
+  TAKE(wc1, c.KP * 16)                 // [Wc; Wn; 0] [KP, 16] (k-major, as stored)
+  TAKE(w2, 16 * 32 * 2 + 32 + 16)      // Wc2 [16,32], Wn2 [16,32], b2 [32], b1 [16]
+  TAKE(fc1, 64 * 32 + 64)              // fc1.weight [64,32], fc1.bias
+  TAKE(fc2, OUT * 64 + OUT)            // fc2.weight [out,64], fc2.bias
+  TAKE(x, N * c.XS)
+  TAKE(zm, N * c.LDZ)
+  TAKE(h1, N * 16)
+  TAKE(rp, N + 1)
+  TAKE(col, (E + 1) / 2)
+  TAKE(m0p, K0 + 1)
+  TAKE(m0i, N)
+  TAKE(p1, K0 * 16)
+  TAKE(a1, K0 * 16)
+  TAKE(dp1, K0 * 16)
+  TAKE(zm2, K0 * 16)
+  TAKE(s2, K0 * 32)
+  TAKE(h2, K0 * 32)
+  TAKE(d2, K0 * 32)
+  TAKE(dz2, K0 * 16)
+  TAKE(p1rp, K0 + 1)
+  TAKE(p1c, P1)
+  if (alias) {
+    c.p1trp = c.p1rp;
+    c.p1tc = c.p1c;
+  } else {
+    TAKE(p1trp, K0 + 1)
+    TAKE(p1tc, P1)
+  }
+  TAKE(m1p, K1 + 1)
+  TAKE(m1i, K0)
+  TAKE(p2, K1 * 32)
+  TAKE(nt, K1 * 32)
+  TAKE(head, HEADW)
+  TAKE(dgp, NW * 32)
+  TAKE(red, 2 * NT)
+#undef TAKE
+  c.total = o;
+  return c;
+}
+
+struct FoutArgs {
+  dr_graph_store s;
+  dr_fout_weights w;
+  dr_pass p;
+  const dr_graph_desc* descs;
+  int32_t B;
+};
+
+__global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int b = blockIdx.x;
+  const dr_graph_store& s = a.s;
+  const dr_graph_desc d = a.descs[b];
+  const int g = d.gid;
+  const int64_t n0 = d.node0, ec0 = d.col0, k00 = d.k0, q0 = d.p1, k10 = d.k1;
+  const int N = d.n_nodes, E = d.n_edges, K0 = d.n_k0, P1 = d.n_p1, K1 = d.n_k1;
+  const int F = s.n_feat;
+  const int alias = s.transpose_aliased;
+  const int OUT = a.p.out_dim;
+  const Carve c = carve(N, E, F, K0, P1, K1, alias, OUT);
+  const int KP = c.KP, XS = c.XS, LDZ = c.LDZ;
+
+  float* sWc1 = lds + c.wc1;
+  float* sWc2 = lds + c.w2;
+  float* sWn2 = sWc2 + 512;
+  float* sB2 = sWn2 + 512;
+  float* sB1 = sB2 + 32;
+  float* sFc1 = lds + c.fc1;
+  float* sFc1b = sFc1 + 2048;
+  float* sFc2 = lds + c.fc2;
+  float* sX = lds + c.x;
+  float* sZm = lds + c.zm;
+  float* sH1 = lds + c.h1;
+  int* srp = reinterpret_cast<int*>(lds + c.rp);
+  uint16_t* scol = reinterpret_cast<uint16_t*>(lds + c.col);
+  int* sm0p = reinterpret_cast<int*>(lds + c.m0p);
+  int* sm0i = reinterpret_cast<int*>(lds + c.m0i);
+  float* sP1 = lds + c.p1;
+  int* sA1 = reinterpret_cast<int*>(lds + c.a1);
+  float* sdP1 = lds + c.dp1;
+  float* sZm2 = lds + c.zm2;
+  float* sS2 = lds + c.s2;
+  float* sH2 = lds + c.h2;
+  float* sD2 = lds + c.d2;
+  float* sDz2 = lds + c.dz2;
+  int* sp1rp = reinterpret_cast<int*>(lds + c.p1rp);
+  int* sp1c = reinterpret_cast<int*>(lds + c.p1c);
+  int* sp1trp = reinterpret_cast<int*>(lds + c.p1trp);
+  int* sp1tc = reinterpret_cast<int*>(lds + c.p1tc);
+  int* sm1p = reinterpret_cast<int*>(lds + c.m1p);
+  int* sm1i = reinterpret_cast<int*>(lds + c.m1i);
+  float* sP2 = lds + c.p2;
+  float* sNT = lds + c.nt;
+  float* sG = lds + c.head;
+  float* sHpre = sG + 32;
+  float* sHh = sHpre + 64;
+  float* sDh = sHh + 64;
+  float* sDG = sDh + 64;
+  float* sDout = sDG + 32;
+  float* sDGp = lds + c.dgp;
+  float* sRed = lds + c.red;
+
+  DRK_STAMP(0);
+  // ---------------- stage: graph by DMA, weights through VGPRs --------------
+  const float y_g = s.y[g];
+  // no dropout here, but the step counter contract holds: snapshot for dr_reduce_update
+  if (a.p.step_counter && b == 0 && tid == 0) a.p.step_counter[1] = a.p.step_counter[0];
+  dma_x4<NT>(sX, s.x + n0 * (int64_t)XS, N * XS / 4);
+  dma_x4<NT>(scol, s.col + ec0, (E + 7) / 8);
+  dma_words<NT>(srp, s.rowptr + n0 + g, N + 1);
+  dma_words<NT>(sm0p, s.m0_ptr + k00 + g, K0 + 1);
+  dma_words<NT>(sm0i, s.m0_idx + n0, N);
+  dma_words<NT>(sp1rp, s.p1_rowptr + k00 + g, K0 + 1);
+  dma_words<NT>(sp1c, s.p1_col + q0, P1);
+  if (!alias) {
+    dma_words<NT>(sp1trp, s.p1t_rowptr + k00 + g, K0 + 1);
+    dma_words<NT>(sp1tc, s.p1t_col + q0, P1);
+  }
+  dma_words<NT>(sm1p, s.m1_ptr + k10 + g, K1 + 1);
+  dma_words<NT>(sm1i, s.m1_idx + k00, K0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  DRK_STAMP(1);
+  // Weights (needed after the gather) via VGPRs: their latency overlaps it.
+  // Flat weight image: [Wc;Wn] (2F*16) | Wc2 Wn2 b2 b1 (1072) | fc1 (2048+64) | fc2 (OUT*65)
+  constexpr int WREG = 6;
+  float wr[WREG];
+  const int nw1 = 2 * F * 16, nw2 = 1072, nf1 = 2048 + 64, nf2 = OUT * 64 + OUT;
+  const int ntot = nw1 + nw2 + nf1 + nf2;
+#pragma unroll
+  for (int u = 0; u < WREG; ++u) {
+    const int p = tid + u * NT;
+    float v = 0.f;
+    if (p < nw1) v = (p < F * 16) ? a.w.wc1[p] : a.w.wn1[p - F * 16];
+    else if (p < nw1 + nw2) {
+      const int q = p - nw1;
+      v = q < 512 ? a.w.wc2[q] : q < 1024 ? a.w.wn2[q - 512] : q < 1056 ? a.w.b2[q - 1024] : a.w.b1[q - 1056];
+    } else if (p < nw1 + nw2 + nf1) {
+      const int q = p - nw1 - nw2;
+      v = q < 2048 ? a.w.fc1w[q] : a.w.fc1b[q - 2048];
+    } else if (p < ntot) {
+      const int q = p - nw1 - nw2 - nf1;
+      v = q < OUT * 64 ? a.w.fc2w[q] : a.w.fc2b[q - OUT * 64];
+    }
+    wr[u] = v;
+  }
+  // ---------------- Zm = D^-1 A X (foutnet.py:55-58; NaN on empty rows) ----
+  {
+    const int nch = XS >> 2;
+    const int sub = tid & 7;
+    for (int i = tid >> 3; i < N; i += NT / 8) {
+      const int eb = srp[i], ee = srp[i + 1];
+      const float deg = (float)(ee - eb);
+      for (int ch = sub; ch < nch; ch += 8) {
+        const int c4 = ch * 4;
+        const float4 acc = gather_row_chunk(scol, eb, ee, sX, XS, c4);
+        float* zr = sZm + i * LDZ + c4;
+        // mean over the out-neighbours; 0/0 = NaN exactly as torch.mean(empty)
+        if (c4 + 0 < F) zr[0] = acc.x / deg;
+        if (c4 + 1 < F) zr[1] = acc.y / deg;
+        if (c4 + 2 < F) zr[2] = acc.z / deg;
+        if (c4 + 3 < F) zr[3] = acc.w / deg;
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < WREG; ++u) {
+    const int p = tid + u * NT;
+    if (p < nw1) sWc1[p] = wr[u];  // rows 0..F-1 = Wc, F..2F-1 = Wn
+    else if (p < nw1 + nw2) sWc2[p - nw1] = wr[u];
+    else if (p < nw1 + nw2 + nf1) sFc1[p - nw1 - nw2] = wr[u];
+    else if (p < ntot) sFc2[p - nw1 - nw2 - nf1] = wr[u];
+  }
+  for (int p = nw1 + tid; p < KP * 16; p += NT) sWc1[p] = 0.f;  // K padding rows
+  __syncthreads();
+
+  DRK_STAMP(2);
+  // ---------------- conv1 on MFMA: H1 = relu([X | Zm] [Wc; Wn] + b) -------
+  {
+    const int li = lane & 15, kq = lane >> 4;
+    for (int t = wave; t * 16 < N; t += NW) {
+      const int r0 = t * 16;
+      const int ar = min(r0 + li, N - 1);
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < KP; k += 16) {
+        float av[4], bv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int kk = k + 4 * u + kq;
+          av[u] = kk < F ? sX[ar * XS + kk] : (kk < 2 * F ? sZm[ar * LDZ + kk - F] : 0.f);
+          bv[u] = sWc1[kk * 16 + li];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = r0 + kq * 4 + r;
+        if (row < N) sH1[row * 16 + li] = relu_keepnan(acc[r] + sB1[li]);
+      }
+    }
+  }
+  __syncthreads();
+
+  DRK_STAMP(3);
+  // ---------------- depth-0 community pooling (torch_scatter scatter_max) ---
+  {
+    const int pairs = K0 * 16;
+    const int LS = pairs <= NT / 8 ? 3 : pairs <= NT / 4 ? 2 : pairs <= NT / 2 ? 1 : 0;
+    const int S1 = 1 << LS;
+    float* tb = sRed;
+    int* ta = reinterpret_cast<int*>(sRed + NT);
+    for (int p = tid; p < pairs * S1; p += NT) {
+      const int sl = p & (S1 - 1), pr = p >> LS;
+      const int k = pr >> 4, ch = pr & 15;
+      const int mb = sm0p[k], cnt = sm0p[k + 1] - mb;
+      const int qb = mb + ((cnt * sl) >> LS), qe = mb + ((cnt * (sl + 1)) >> LS);
+      float best = LOWEST;
+      int arg = N;
+      for (int m = qb; m < qe; ++m) {
+        const int i = sm0i[m];
+        const float v = sH1[i * 16 + ch];
+        if (v > best) {
+          best = v;
+          arg = i;
+        }
+      }
+      tb[p] = best;
+      ta[p] = arg;
+    }
+    __syncthreads();
+    for (int p = tid; p < pairs; p += NT) {
+      float best = LOWEST;
+      int arg = N;
+      for (int sl = 0; sl < S1; ++sl) {
+        const float v = tb[(p << LS) + sl];
+        if (v > best) {
+          best = v;
+          arg = ta[(p << LS) + sl];
+        }
+      }
+      sP1[p] = (best == LOWEST) ? 0.f : best;
+      sA1[p] = arg;
+    }
+  }
+  __syncthreads();
+
+  DRK_STAMP(4);
+  // ---------------- conv2 on the pooled graph: FoutLayer(16, 32) ----------
+  for (int p = tid; p < K0 * 16; p += NT) {  // Zm2 = mean over pooled out-neighbours
+    const int k = p >> 4, j = p & 15;
+    const int eb = sp1rp[k], ee = sp1rp[k + 1];
+    float acc = 0.f;
+    for (int e = eb; e < ee; ++e) acc += sP1[sp1c[e] * 16 + j];
+    sZm2[p] = acc / (float)(ee - eb);
+  }
+  __syncthreads();
+  for (int p = tid; p < K0 * 32; p += NT) {
+    const int k = p >> 5, o = p & 31;
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc = fmaf(sP1[k * 16 + j], sWc2[j * 32 + o], acc);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc = fmaf(sZm2[k * 16 + j], sWn2[j * 32 + o], acc);
+    const float sv = acc + sB2[o];
+    sS2[p] = sv;
+    sH2[p] = relu_keepnan(sv);
+  }
+  __syncthreads();
+
+  DRK_STAMP(5);
+  // ---------------- depth-1 max_pool_x (amax: NaN propagates) + mean -------
+  for (int p = tid; p < K1 * 32; p += NT) {
+    const int m = p >> 5, o = p & 31;
+    const int mb = sm1p[m], me = sm1p[m + 1];
+    float mx = sH2[sm1i[mb] * 32 + o];
+    for (int q = mb + 1; q < me; ++q) {
+      const float v = sH2[sm1i[q] * 32 + o];
+      mx = (mx != mx || v != v) ? __int_as_float(0x7fc00000) : fmaxf(mx, v);
+    }
+    float ties = 0.f;
+    for (int q = mb; q < me; ++q) ties += (sH2[sm1i[q] * 32 + o] == mx) ? 1.f : 0.f;
+    sP2[p] = mx;
+    sNT[p] = ties;
+  }
+  __syncthreads();
+  if (tid < 32) {
+    float acc = 0.f;
+    for (int m = 0; m < K1; ++m) acc += sP2[m * 32 + tid];
+    sG[tid] = acc / (float)K1;
+  }
+  __syncthreads();
+
+  DRK_STAMP(6);
+  // ---------------- head: fc1 (32->64) -> relu -> fc2 (foutnet.py:115-117) --
+  {
+    const int r = tid >> 3, part = tid & 7;  // 8 lanes per fc1 row, 4 inputs each
+    float acc = 0.f;
+    if (r < 64) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc = fmaf(sG[part * 4 + j], sFc1[r * 32 + part * 4 + j], acc);
+    }
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    acc += __shfl_xor(acc, 4, 64);
+    if (r < 64 && part == 0) {
+      acc += sFc1b[r];
+      sHpre[r] = acc;
+      sHh[r] = relu_keepnan(acc);
+    }
+  }
+  __syncthreads();
+  for (int q = wave; q < OUT; q += NW) {
+    float v = sHh[lane] * sFc2[q * 64 + lane];
+    v = dr_wave_sum(v);
+    if (lane == 0) sDout[q] = v + sFc2[OUT * 64 + q];
+  }
+  __syncthreads();
+  if ((a.p.flags & DR_PASS_FORWARD) && tid < OUT) a.p.out[(int64_t)b * OUT + tid] = sDout[tid];
+  if (!(a.p.flags & DR_PASS_BACKWARD)) return;
+  __syncthreads();
+
+  DRK_STAMP(7);
+  // ---------------- loss gradient (trainer.py:688-689) ----------------------
+  if (tid == 0) {
+    if (a.p.loss_kind == DR_LOSS_MSE) {
+      const float dlt = sDout[0] - y_g;
+      if (a.p.loss_per_graph) a.p.loss_per_graph[b] = dlt * dlt;
+      sDout[0] = 2.f * dlt * a.p.loss_scale;
+    } else if (a.p.loss_kind == DR_LOSS_CE) {
+      const int yi = (int)y_g;
+      float mx = sDout[0];
+      for (int q = 1; q < OUT; ++q) mx = fmaxf(mx, sDout[q]);
+      float se = 0.f;
+      for (int q = 0; q < OUT; ++q) se += expf(sDout[q] - mx);
+      const float lse = mx + logf(se);
+      const float wy = a.p.class_w ? a.p.class_w[yi] : 1.f;
+      if (a.p.loss_per_graph) a.p.loss_per_graph[b] = wy * (lse - sDout[yi]);
+      for (int q = 0; q < OUT; ++q) sDout[q] = wy * (expf(sDout[q] - lse) - (q == yi ? 1.f : 0.f)) * a.p.loss_scale;
+    } else {
+      for (int q = 0; q < OUT; ++q) sDout[q] = a.p.dout[(int64_t)b * OUT + q];
+    }
+  }
+  __syncthreads();
+
+  // ---------------- head backward -------------------------------------------
+  if (tid < 64) {
+    float acc = 0.f;
+    for (int q = 0; q < OUT; ++q) acc = fmaf(sFc2[q * 64 + tid], sDout[q], acc);
+    sDh[tid] = relu_bwd(sHh[tid], acc);
+  }
+  __syncthreads();
+  {
+    const int o = tid & 31, rc = tid >> 5;  // 32 chunks of 2 fc1 rows
+    float acc = fmaf(sFc1[(rc * 2) * 32 + o], sDh[rc * 2], sFc1[(rc * 2 + 1) * 32 + o] * sDh[rc * 2 + 1]);
+    sDGp[rc * 32 + o] = acc;
+  }
+  __syncthreads();
+  if (tid < 32) {
+    float acc = 0.f;
+    for (int rc = 0; rc < NT / 32; ++rc) acc += sDGp[rc * 32 + tid];
+    sDG[tid] = acc;
+  }
+  {
+    const int HS = DR_FOUT_HEAD_STRIDE(OUT);
+    float* hg = a.p.head + (int64_t)b * HS;
+    if (tid < 32) hg[tid] = sG[tid];
+    if (tid < 64) {
+      hg[32 + tid] = sHh[tid];
+      hg[96 + tid] = sDh[tid];
+    }
+    if (tid < OUT) hg[160 + tid] = sDout[tid];
+  }
+  __syncthreads();
+
+  DRK_STAMP(8);
+  // ---------------- depth-1 pooling + mean backward -------------------------
+  for (int p = tid; p < K1 * 32; p += NT) {
+    const int m = p >> 5, o = p & 31;
+    const float gm = (sDG[o] / (float)K1) / sNT[p];
+    const float mx = sP2[p];
+    for (int q = sm1p[m]; q < sm1p[m + 1]; ++q) {
+      const int k = sm1i[q];
+      const float h = sH2[k * 32 + o];
+      sD2[k * 32 + o] = relu_bwd(h, (h == mx ? 1.f : 0.f) * gm);
+    }
+  }
+  __syncthreads();
+  // conv2 weight partials; gradient into the mean term (dZm2 = dS2 Wn2^T)
+  {
+    const int SS = DR_FOUT_SLAB_STRIDE(F);
+    float* slab = a.p.slab + (int64_t)b * SS + 32 * F + 16;
+    for (int p = tid; p < 1024 + 32; p += NT) {
+      float acc = 0.f;
+      if (p < 512) {  // dWc2[j][o] = sum_k P1[k][j] dS2[k][o]
+        const int j = p >> 5, o = p & 31;
+        for (int k = 0; k < K0; ++k) acc = fmaf(sP1[k * 16 + j], sD2[k * 32 + o], acc);
+      } else if (p < 1024) {  // dWn2[j][o] = sum_{k: deg>0} Zm2[k][j] dS2[k][o]
+        const int q = p - 512, j = q >> 5, o = q & 31;
+        for (int k = 0; k < K0; ++k)
+          if (sp1rp[k + 1] > sp1rp[k]) acc = fmaf(sZm2[k * 16 + j], sD2[k * 32 + o], acc);
+      } else {  // db2[o]
+        const int o = p - 1024;
+        for (int k = 0; k < K0; ++k) acc += sD2[k * 32 + o];
+      }
+      slab[p] = acc;
+    }
+  }
+  for (int p = tid; p < K0 * 16; p += NT) {
+    const int k = p >> 4, j = p & 15;
+    float dz = 0.f, dp = 0.f;
+#pragma unroll 8
+    for (int o = 0; o < 32; ++o) {
+      const float ds = sD2[k * 32 + o];
+      dz = fmaf(ds, sWn2[j * 32 + o], dz);
+      dp = fmaf(ds, sWc2[j * 32 + o], dp);
+    }
+    const int deg = sp1rp[k + 1] - sp1rp[k];
+    sDz2[p] = deg > 0 ? dz / (float)deg : 0.f;
+    sdP1[p] = dp;
+  }
+  __syncthreads();
+  // dP1[j] += sum_{i: j in N(i)} dZm2[i] / deg_i  (transposed pooled CSR), then
+  // route to the depth-0 arg member through relu: v = relu'(H1[arg]) dP1
+  for (int p = tid; p < K0 * 16; p += NT) {
+    const int k = p >> 4, j = p & 15;
+    float acc = sdP1[p];
+    for (int e = sp1trp[k]; e < sp1trp[k + 1]; ++e) acc += sDz2[sp1tc[e] * 16 + j];
+    const int i = sA1[p];
+    sdP1[p] = (i < N) ? relu_bwd(sH1[i * 16 + j], acc) : 0.f;
+  }
+  __syncthreads();
+
+  DRK_STAMP(9);
+  // ---------------- conv1 weight partials: sum_k v_k [x | Zm][arg_k] -------
+  {
+    const int SS = DR_FOUT_SLAB_STRIDE(F);
+    float* slab = a.p.slab + (int64_t)b * SS;
+    for (int p = tid; p < 32 * F + 16; p += NT) {
+      float acc = 0.f;
+      if (p < 32 * F) {
+        const int half = p >= 16 * F;  // 0: dWc [F,16], 1: dWn [F,16]
+        const int q = p - half * 16 * F, kk = q >> 4, ch = q & 15;
+        for (int k = 0; k < K0; ++k) {
+          const int i = sA1[k * 16 + ch];
+          if (i < N) acc = fmaf(sdP1[k * 16 + ch], half ? sZm[i * LDZ + kk] : sX[i * XS + kk], acc);
+        }
+      } else {
+        const int ch = p - 32 * F;
+        for (int k = 0; k < K0; ++k) acc += sdP1[k * 16 + ch];
+      }
+      slab[p] = acc;
+    }
+  }
+  DRK_STAMP(10);
+}
+
+}  // namespace
+
+extern "C" int64_t dr_fout_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_feat, int32_t k0, int32_t p1_edges,
+                                     int32_t k1, int32_t transpose_aliased, int32_t out_dim) {
+  return 4LL * carve(n_nodes, n_edges, n_feat, k0, p1_edges, k1, transpose_aliased, out_dim).total;
+}
+
+extern "C" int dr_fout_graph_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                                  const dr_fout_weights* w, const dr_pass* pass, int32_t lds_bytes, void* stream) {
+  if (!store || !descs || !w || !pass || n_batch < 0) return DR_E_ARG;
+  if (pass->out_dim < 1 || pass->out_dim > DR_MAX_OUT) return DR_E_UNSUPPORTED;
+  if (store->n_feat < 1 || 2 * 16 * store->n_feat + 1072 + 2112 + 65 * pass->out_dim > 6 * NT) return DR_E_UNSUPPORTED;
+  if (lds_bytes > 160 * 1024) return DR_E_LDS;
+  if ((pass->flags & DR_PASS_BACKWARD) && (!pass->slab || !pass->head)) return DR_E_ARG;
+  if ((pass->flags & DR_PASS_BACKWARD) && pass->loss_kind == DR_LOSS_NONE && !pass->dout) return DR_E_ARG;
+  if ((pass->flags & DR_PASS_FORWARD) && !pass->out) return DR_E_ARG;
+  if (pass->use_dropout != DR_DROPOUT_OFF) return DR_E_UNSUPPORTED;  // FoutNet has no dropout
+  if (n_batch == 0) return DR_OK;
+  DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&fout_graph_kernel)));
+  FoutArgs args;
+  args.s = *store;
+  args.w = *w;
+  args.p = *pass;
+  args.descs = descs;
+  args.B = n_batch;
+  hipLaunchKernelGGL(fout_graph_kernel, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, args);
+  return (int)hipGetLastError();
+}

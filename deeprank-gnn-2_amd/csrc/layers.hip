@@ -7,6 +7,7 @@
 //   dr_csr_from_coo : stable CSR by row (the order torch_scatter's CPU
 //                     scatter_add_ visits edges in), fully on the device
 //   dr_spmm_csr     : out[i] = sum_{e in row i} y[col[e]]       (ginet.py:58)
+//                     or the row mean (foutnet.py:56-58; 0/0 = NaN on empty rows)
 //   dr_linear_*     : fc(x) = x W^T (ginet.py:45) and its two gradients
 //
 // All are HBM/L2-bound gathers; deterministic (no float atomics).
@@ -77,15 +78,17 @@ __global__ void sort_rows_kernel(const int32_t* __restrict__ rowptr, int32_t n_r
 }
 
 __global__ void spmm_kernel(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
-                            const float* __restrict__ y, int32_t n_rows, int32_t C, int32_t relu,
+                            const float* __restrict__ y, int32_t n_rows, int32_t C, int32_t mode,
                             float* __restrict__ out) {
   const int64_t total = (int64_t)n_rows * C;
   for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < total; p += (int64_t)gridDim.x * blockDim.x) {
     const int i = (int)(p / C);
     const int c = (int)(p - (int64_t)i * C);
     float acc = 0.f;
-    for (int e = rowptr[i]; e < rowptr[i + 1]; ++e) acc += y[(int64_t)col[e] * C + c];
-    out[p] = (relu && acc <= 0.f) ? 0.f : acc;
+    const int eb = rowptr[i], ee = rowptr[i + 1];
+    for (int e = eb; e < ee; ++e) acc += y[(int64_t)col[e] * C + c];
+    if (mode & DR_SPMM_MEAN) acc /= (float)(ee - eb);
+    out[p] = ((mode & DR_SPMM_RELU) && acc <= 0.f) ? 0.f : acc;
   }
 }
 
@@ -166,12 +169,12 @@ extern "C" int dr_csr_from_coo(const int64_t* row, const int64_t* col, int64_t n
 }
 
 extern "C" int dr_spmm_csr(const int32_t* rowptr, const int32_t* col, const float* y, int32_t n_rows, int32_t n_chan,
-                           int32_t relu, float* out, void* stream) {
+                           int32_t mode, float* out, void* stream) {
   if (!rowptr || !out || n_rows < 0 || n_chan < 0) return DR_E_ARG;
   const int64_t work = (int64_t)n_rows * n_chan;
   if (work == 0) return DR_OK;
   hipLaunchKernelGGL(spmm_kernel, dim3(grid_for(work)), dim3(256), 0, (hipStream_t)stream, rowptr, col, y, n_rows,
-                     n_chan, relu, out);
+                     n_chan, mode, out);
   return (int)hipGetLastError();
 }
 

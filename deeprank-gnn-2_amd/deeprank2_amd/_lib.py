@@ -27,6 +27,8 @@ DR_GRAD_ZERO = 0
 DR_GRAD_SLAB = 1
 DR_GRAD_OUTER = 2
 DR_GRAD_HEAD = 3
+DR_SPMM_RELU = 1
+DR_SPMM_MEAN = 2
 
 ERRORS = {-1: "bad argument", -2: "graph does not fit the per-graph LDS kernel", -3: "unsupported configuration"}
 
@@ -68,6 +70,10 @@ class GraphStoreC(ctypes.Structure):
 
 class GinetWeightsC(ctypes.Structure):
     _fields_ = [(n, VP) for n in ("w1", "w1e", "w2", "w2e", "fc1w", "fc1b", "fc2w", "fc2b")]
+
+
+class FoutWeightsC(ctypes.Structure):
+    _fields_ = [(n, VP) for n in ("wc1", "wn1", "b1", "wc2", "wn2", "b2", "fc1w", "fc1b", "fc2w", "fc2b")]
 
 
 class PassC(ctypes.Structure):
@@ -131,6 +137,8 @@ class ParamTableC(ctypes.Structure):
 SIGNATURES = [
     ("dr_ginet_graph_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, VP]),
     ("dr_ginet_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 8),
+    ("dr_fout_graph_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(FoutWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, VP]),
+    ("dr_fout_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 8),
     ("dr_reduce_update", ctypes.c_int, [ctypes.POINTER(ParamTableC), VP, VP, ctypes.c_int32, ctypes.POINTER(AdamC), VP, ctypes.c_float, VP, VP]),
     ("dr_csr_from_coo", ctypes.c_int, [VP, VP, ctypes.c_int64, ctypes.c_int32, VP, VP, VP, VP, VP]),
     ("dr_spmm_csr", ctypes.c_int, [VP, VP, VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP, VP]),

@@ -35,11 +35,12 @@ def csr_from_coo(row: torch.Tensor, col: torch.Tensor, n_rows: int):
     return rowptr, perm[:e], col_s[:e]
 
 
-def spmm_csr(rowptr, col, y, n_rows, relu=False):
+def spmm_csr(rowptr, col, y, n_rows, relu=False, mean=False):
+    """Row sum (or row mean, NaN on empty rows) of y over a CSR adjacency."""
     _lib.require_device(rowptr, col, y)
     y = _f32(y, "y")
     out = torch.empty(n_rows, y.shape[1], dtype=torch.float32, device=y.device)
-    _lib.check(_lib.load().dr_spmm_csr(rowptr.data_ptr(), col.data_ptr(), y.data_ptr(), n_rows, y.shape[1], int(relu), out.data_ptr(), _lib.stream_ptr(y.device)), "dr_spmm_csr")
+    _lib.check(_lib.load().dr_spmm_csr(rowptr.data_ptr(), col.data_ptr(), y.data_ptr(), n_rows, y.shape[1], int(relu) * _lib.DR_SPMM_RELU + int(mean) * _lib.DR_SPMM_MEAN, out.data_ptr(), _lib.stream_ptr(y.device)), "dr_spmm_csr")
     return out
 
 

@@ -18,6 +18,9 @@
  *                           deeprank2/utils/community_pooling.py:23-27,165-242),
  *                           plus the loss gradient of Trainer._epoch
  *                           (deeprank2/trainer.py:686-689)
+ *   dr_fout_graph_pass      FoutNet.forward + autograd backward
+ *                           (deeprank2/neuralnets/gnn/foutnet.py:48-66,99-118)
+ *                           plus the same loss gradient
  *   dr_reduce_update        loss_.backward() parameter-gradient reduction and
  *                           optimizer.step() of Trainer._epoch
  *                           (trainer.py:689-690; torch.optim.Adam configured at
@@ -154,6 +157,41 @@ int dr_ginet_graph_pass(const dr_graph_store* store, const dr_graph_desc* descs,
 int64_t dr_ginet_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_feat, int32_t k0,
                            int32_t p1_edges, int32_t k1, int32_t transpose_aliased, int32_t out_dim);
 
+/* ---- FoutNet (deeprank2/neuralnets/gnn/foutnet.py:72-118) ---------------- */
+
+/* FoutNet weights, all row-major as the torch parameters are stored.       */
+typedef struct dr_fout_weights {
+  const float* wc1;  /* conv1.wc    [F, 16]   (foutnet.py:32) */
+  const float* wn1;  /* conv1.wn    [F, 16]   (foutnet.py:33) */
+  const float* b1;   /* conv1.bias  [16]                      */
+  const float* wc2;  /* conv2.wc    [16, 32]                  */
+  const float* wn2;  /* conv2.wn    [16, 32]                  */
+  const float* b2;   /* conv2.bias  [32]                      */
+  const float* fc1w; /* fc1.weight  [64, 32]                  */
+  const float* fc1b; /* fc1.bias    [64]                      */
+  const float* fc2w; /* fc2.weight  [out, 64]                 */
+  const float* fc2b; /* fc2.bias    [out]                     */
+} dr_fout_weights;
+
+/* Per-graph partials of dr_fout_graph_pass:
+ *   slab: dWc1 [F,16] | dWn1 [F,16] | db1 [16] | dWc2 [16,32] | dWn2 [16,32] | db2 [32]
+ *   head: g [32] | relu(fc1) [64] | its grad [64] | dout [out]                 */
+#define DR_FOUT_SLAB_STRIDE(F) (32 * (F) + 1072)
+#define DR_FOUT_HEAD_STRIDE(out) (160 + (((out) + 3) & ~3))
+
+/* One workgroup per graph: FoutLayer(F,16) (foutnet.py:48-66; NaN where a node
+ * has no out-edge, as torch.mean over an empty set) -> relu -> depth-0
+ * community pooling -> FoutLayer(16,32) on the pooled graph -> relu -> depth-1
+ * max_pool_x -> per-graph mean -> fc1/relu/fc2, and its backward.  Same
+ * dr_pass contract as dr_ginet_graph_pass (no dropout: use_dropout must be
+ * DR_DROPOUT_OFF); partial layouts above.                                    */
+int dr_fout_graph_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                       const dr_fout_weights* w, const dr_pass* pass, int32_t lds_bytes, void* stream);
+
+/* Dynamic LDS bytes dr_fout_graph_pass needs for a graph of these sizes.   */
+int64_t dr_fout_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_feat, int32_t k0, int32_t p1_edges,
+                          int32_t k1, int32_t transpose_aliased, int32_t out_dim);
+
 /* Adam (torch.optim.Adam, L2 weight decay added to the gradient) settings.  */
 typedef struct dr_adam {
   float lr, beta1, beta2, eps, weight_decay;
@@ -208,9 +246,13 @@ int dr_csr_from_coo(const int64_t* row, const int64_t* col, int64_t n_edges, int
                     int32_t* rowptr, int32_t* perm, int32_t* col_sorted, int32_t* scratch,
                     void* stream);
 
-/* out[i,:] = sum_{e in row i} y[col[e],:]  (C channels, fp32), optional ReLU. */
+/* out[i,:] = sum_{e in row i} y[col[e],:]  (C channels, fp32)  (ginet.py:58);
+ * mode DR_SPMM_MEAN divides by the row length (foutnet.py:56-58: NaN on an
+ * empty row, as torch.mean over an empty set); DR_SPMM_RELU applies relu.  */
+#define DR_SPMM_RELU 1
+#define DR_SPMM_MEAN 2
 int dr_spmm_csr(const int32_t* rowptr, const int32_t* col, const float* y, int32_t n_rows,
-                int32_t n_chan, int32_t relu, float* out, void* stream);
+                int32_t n_chan, int32_t mode, float* out, void* stream);
 
 /* y[M,N] = x[M,K] w[N,K]^T            */
 int dr_linear_xwT(const float* x, const float* w, int32_t m, int32_t k, int32_t n, float* y, void* stream);
