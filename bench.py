@@ -122,15 +122,24 @@ def main():  # noqa: PLR0915
     ap.add_argument("--batch", type=int, default=B_PER_GPU)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch every step from Python instead of replaying captured HIP graphs")
+    ap.add_argument("--capture-ddp", action="store_true", help="N>1: also capture the RCCL all-reduce in the HIP graph (default: eager steps)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     pg = None
+    # DR_BENCH_SHARED_GPU=1 rehearses the N>1 code path on a one-GPU box (all
+    # ranks on cuda:0 over gloo); real multi-GPU runs use RCCL, one GPU per rank.
+    shared = os.environ.get("DR_BENCH_SHARED_GPU") == "1"
+    if shared:
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if shared:
+            torch.distributed.init_process_group("gloo")
+        else:
+            torch.distributed.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
         pg = torch.distributed.group.WORLD
     dev = torch.device(f"cuda:{local}")
 
@@ -155,7 +164,7 @@ def main():  # noqa: PLR0915
     for i in range(args.warmup):
         run_eager(i)
     captured = None
-    if not args.eager:  # one captured step per resident mini-batch, replayed
+    if not args.eager and (world == 1 or args.capture_ddp):  # one captured step per resident mini-batch, replayed
         captured = [step.capture(h, global_batch=B * world) for h in handles]
 
     def run(i):

@@ -1,0 +1,60 @@
+"""Data-parallel sharding of a global mini-batch over ranks (one process per GPU).
+
+Graphs are independent, so a global batch shards by graph with no data-path
+collective; the only exchange per step is the gradient + loss all-reduce
+inside ``FusedTrainStep.step``.
+
+* ``shard_contiguous``: rank r takes a contiguous slice of the global batch in
+  the global order.  With the loss scaled by 1/B_global on every rank the
+  summed gradients equal the single-GPU step on the whole batch (up to fp32
+  reordering) — no ``DistributedSampler`` re-shuffling.
+* ``shard_by_edges``: greedy longest-processing-time bin packing on the edge
+  counts for batches of very mixed graph sizes (config 5); the returned
+  permutation restores the global order of per-graph outputs.
+
+The reference's ``nn.DataParallel`` (trainer.py:387-389) replicates the model
+per step and gathers outputs on one device; there is no counterpart here.
+"""
+
+from __future__ import annotations
+
+import heapq
+
+import numpy as np
+
+
+def shard_contiguous(gids, rank: int, world: int) -> np.ndarray:
+    """Rank ``rank``'s share of the global batch ``gids``: sizes differ by at most one."""
+    gids = np.asarray(gids, dtype=np.int32)
+    if not 0 <= rank < world:
+        msg = f"rank {rank} outside world of {world}"
+        raise ValueError(msg)
+    b = gids.size
+    lo = (b * rank) // world
+    hi = (b * (rank + 1)) // world
+    return gids[lo:hi]
+
+
+def shard_by_edges(gids, edges, world: int):
+    """Assign graphs to ``world`` ranks balancing the summed edge counts.
+
+    Returns (shards, perm): ``shards[r]`` holds rank r's graph ids (in global
+    order within the rank); ``np.concatenate(shards)[perm]`` is ``gids`` again,
+    which puts gathered per-graph outputs back in the global order."""
+    gids = np.asarray(gids, dtype=np.int32)
+    edges = np.asarray(edges, dtype=np.int64)
+    if gids.shape != edges.shape:
+        msg = "gids and edges must have the same length"
+        raise ValueError(msg)
+    heap = [(0, r) for r in range(world)]
+    owner = np.empty(gids.size, dtype=np.int64)
+    for i in np.argsort(-edges, kind="stable"):
+        load, r = heapq.heappop(heap)
+        owner[i] = r
+        heapq.heappush(heap, (load + int(edges[i]), r))
+    idx = [np.flatnonzero(owner == r) for r in range(world)]
+    shards = [gids[ix] for ix in idx]
+    order = np.concatenate(idx) if idx else np.empty(0, np.int64)
+    perm = np.empty_like(order)
+    perm[order] = np.arange(order.size)
+    return shards, perm

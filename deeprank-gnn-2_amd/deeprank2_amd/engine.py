@@ -16,9 +16,10 @@ the whole step can be captured once per mini-batch and replayed as a HIP graph
 (``capture``).
 
 Data parallel (one process per GPU, RCCL over xGMI): every rank runs step 1 on
-its shard of the global batch with the loss scaled by 1/B_global, the 16
-gradients (one flat 42.7 KB buffer for GINet(30,1,3)) are SUM-all-reduced, then
-step 2 runs Adam from the reduced gradients.  That is the only collective.
+its shard of the global batch with the loss scaled by 1/B_global, the
+gradients and the loss term (one flat buffer: 42.7 KB for GINet(30,1,3),
+16.8 KB for FoutNet(30,1)) are SUM-all-reduced, then step 2 runs Adam from the
+reduced gradients.  That is the only collective (``distributed.py`` shards).
 """
 
 from __future__ import annotations
@@ -36,7 +37,7 @@ class FusedTrainStep:
         self.params = model.ordered_params()
         for p in self.params:
             if not p.is_cuda or not p.is_contiguous() or p.dtype != torch.float32:
-                msg = "GINetTrainStep needs contiguous fp32 cuda parameters"
+                msg = "FusedTrainStep needs contiguous fp32 cuda parameters"
                 raise ValueError(msg)
         dev = self.params[0].device
         self.device = dev
@@ -50,12 +51,14 @@ class FusedTrainStep:
         self.pg = process_group
         self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
         numel = [p.numel() for p in self.params]
-        self.flat_grad = torch.zeros(sum(numel), dtype=torch.float32, device=dev)
+        # gradients and the loss share one buffer: one all-reduce per step (N>1)
+        self.flat = torch.zeros(sum(numel) + 1, dtype=torch.float32, device=dev)
+        self.flat_grad = self.flat[:-1]
         self.grads = [g.view_as(p) for g, p in zip(torch.split(self.flat_grad, numel), self.params)]
         self.states = [(torch.zeros_like(p), torch.zeros_like(p)) for p in self.params]
         self.counter = torch.zeros(2, dtype=torch.int64, device=dev)  # [steps done = dropout offset, snapshot]
         self.step_count = 0
-        self.loss_out = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.loss_out = self.flat[-1:]
         self.kernel_events = None  # list -> (start, end) HIP events around each graph pass
         if getattr(model, "_drop_seed", 0) is None:
             model._drop_seed = int(torch.randint(0, 2**62, (1,)).item())
@@ -152,13 +155,12 @@ class FusedTrainStep:
             _lib.check(lib.dr_reduce_update(self._table, slab, head, h.B, self._adam, lpg, scale, lout, stream), "dr_reduce_update")
         else:
             _lib.check(lib.dr_reduce_update(self._table, slab, head, h.B, self._adam_off, lpg, scale, lout, stream), "dr_reduce_update")
-            torch.distributed.all_reduce(self.flat_grad, group=self.pg)
-            torch.distributed.all_reduce(self.loss_out, group=self.pg)
+            torch.distributed.all_reduce(self.flat, group=self.pg)
             _lib.check(lib.dr_reduce_update(self._table, None, None, h.B, self._adam, None, 1.0, None, _lib.stream_ptr(self.device)), "dr_reduce_update")
         return self.loss_out, self.out[: h.B]
 
     def _state_tensors(self):
-        return [*self.params, *[s for st in self.states for s in st], self.counter, self.flat_grad, self.loss_out]
+        return [*self.params, *[s for st in self.states for s in st], self.counter, self.flat]
 
     def capture(self, h: BatchHandle, global_batch=None):
         """Capture one training step on ``h`` into a HIP graph (``torch.cuda.CUDAGraph``).

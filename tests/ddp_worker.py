@@ -1,0 +1,58 @@
+"""One rank of the data-parallel parity test (tests/test_gpu_distributed.py).
+
+Launched as a child process per rank (RANK / WORLD_SIZE / MASTER_* in the
+environment); every rank uses the same GPU over the gloo backend, so the test
+fits a one-GPU box while exercising FusedTrainStep's sharded step and its
+single all-reduce.  Writes the final parameters (rank 0)."""
+
+from __future__ import annotations
+
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "deeprank-gnn-2_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from deeprank2_amd.distributed import shard_contiguous  # noqa: E402
+from deeprank2_amd.engine import FusedTrainStep  # noqa: E402
+from deeprank2_amd.fused import BatchHandle  # noqa: E402
+from deeprank2_amd.neuralnets.gnn.foutnet import FoutNet  # noqa: E402
+from deeprank2_amd.neuralnets.gnn.ginet import GINet  # noqa: E402
+from deeprank2_amd.store import GraphStore, pack_graphs, records_from_batch  # noqa: E402
+from deeprank2_amd.utils.synthetic import make_dataset  # noqa: E402
+from oracle import data_ref  # noqa: E402
+from oracle import pyg_ops as P  # noqa: E402
+
+B, STEPS = 24, 3
+
+
+def run(model_name, world, rank, out_path):
+    dev = torch.device("cuda:0")
+    pg = None
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        pg = dist.group.WORLD
+    datas = [data_ref.synthetic_to_data(g, f"s{i}") for i, g in enumerate(make_dataset(2 * B, seed=17, n_lo=30, n_hi=80, mean_degree=9.0))]
+    store = GraphStore(pack_graphs(records_from_batch(P.Batch.from_data_list(datas))), dev)
+    torch.manual_seed(42)
+    model = (GINet(30, 1, 3) if model_name == "ginet" else FoutNet(30, 1)).to(dev).train()
+    step = FusedTrainStep(model, process_group=pg)
+    losses = []
+    for s in range(STEPS):
+        gids = np.arange(B) + (s % 2) * B  # global batch, global order
+        h = BatchHandle(store, shard_contiguous(gids, rank, world))
+        loss, _ = step.step(h, global_batch=B, dropout=False)
+        losses.append(float(loss))
+    torch.cuda.synchronize()
+    if rank == 0:
+        np.savez(out_path, loss=np.array(losses), grad=step.flat_grad.cpu().numpy(), **{f"p{i}": p.detach().cpu().numpy() for i, p in enumerate(step.params)})
+    if pg is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    run(sys.argv[1], int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")), sys.argv[2])

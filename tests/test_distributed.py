@@ -1,0 +1,80 @@
+"""Data-parallel path on CPU (gloo, world size 2): sharding helpers and the
+gradient algebra FusedTrainStep relies on — per-rank loss scaled by
+1/B_global + SUM all-reduce == the single-process step on the whole batch."""
+
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from deeprank2_amd.distributed import shard_by_edges, shard_contiguous
+
+
+def test_shard_contiguous_covers_in_order():
+    g = np.arange(10, 27)
+    parts = [shard_contiguous(g, r, 4) for r in range(4)]
+    np.testing.assert_array_equal(np.concatenate(parts), g)
+    assert max(p.size for p in parts) - min(p.size for p in parts) <= 1
+    with pytest.raises(ValueError):
+        shard_contiguous(g, 4, 4)
+
+
+def test_shard_by_edges_balances_and_restores_order():
+    rng = np.random.default_rng(0)
+    gids = rng.permutation(200).astype(np.int32)
+    edges = np.where(rng.random(200) < 0.2, rng.integers(40000, 60000, 200), rng.integers(150, 3500, 200))
+    shards, perm = shard_by_edges(gids, edges, 8)
+    np.testing.assert_array_equal(np.concatenate(shards)[perm], gids)
+    e_of = dict(zip(gids.tolist(), edges.tolist()))
+    loads = [sum(e_of[int(x)] for x in s) for s in shards]
+    assert max(loads) - min(loads) <= edges.max()  # LPT bound
+    assert max(loads) / (sum(loads) / 8) < 1.1
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_main(rank, world, port, model_name, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    from deeprank2_amd.utils.synthetic import make_dataset
+    from oracle import data_ref, gnn_ref
+    from oracle import pyg_ops as P
+
+    datas = [data_ref.synthetic_to_data(g, f"s{i}") for i, g in enumerate(make_dataset(6, seed=2, n_lo=20, n_hi=40, mean_degree=6.0))]
+    torch.manual_seed(0)
+    model = gnn_ref.GINet(30, 1, 3) if model_name == "ginet" else gnn_ref.FoutNet(30, 1)
+    model.eval()  # dropout off: the shards see the same arithmetic as the full batch
+    mine = shard_contiguous(np.arange(6), rank, world)
+    bat = P.Batch.from_data_list([datas[i].clone() for i in mine])
+    out = model(bat)
+    loss = ((out.reshape(-1) - bat.y) ** 2).sum() / 6.0  # per-rank term of the global MSE mean
+    loss.backward()
+    flat = torch.cat([p.grad.reshape(-1) for p in model.parameters()] + [loss.detach().reshape(1)])
+    dist.all_reduce(flat)
+    if rank == 0:
+        full = P.Batch.from_data_list([d.clone() for d in datas])
+        model.zero_grad()
+        ref_loss = torch.nn.functional.mse_loss(model(full).reshape(-1), full.y)
+        ref_loss.backward()
+        ref = torch.cat([p.grad.reshape(-1) for p in model.parameters()] + [ref_loss.detach().reshape(1)])
+        np.savez(out_path, ddp=flat.numpy(), ref=ref.numpy())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("model_name", ["ginet", "foutnet"])
+def test_gloo_world2_allreduced_gradients_equal_global_batch(tmp_path, model_name):
+    out = str(tmp_path / "g.npz")
+    mp.spawn(_rank_main, args=(2, _free_port(), model_name, out), nprocs=2, join=True)
+    z = np.load(out)
+    np.testing.assert_allclose(z["ddp"], z["ref"], rtol=1e-5, atol=1e-6)
