@@ -1,0 +1,476 @@
+"""GraphDataset — drop-in for ``deeprank2.dataset.GraphDataset`` on the MI355X path.
+
+Same constructor, attributes (``hdf5_paths``, ``index_entries``,
+``node_features``, ``edge_features``, ``features_transform``, ``means``,
+``devs``, ``target``, ``task``, ``classes``, ``classes_to_index``,
+``inherited_params``, ``default_vars`` ...), ``train_source`` inheritance and
+``get``/``len``/``load_one_graph``/``hdf5_to_pandas`` semantics as the
+reference (``deeprank2/dataset.py:29-462,710-1122``).
+
+What changes is where the data lives: every file is read once
+(``io.hdf5``), each graph is turned into numpy arrays exactly as
+``load_one_graph`` builds its tensors, and ``batch_handle`` packs ALL graphs of
+the dataset once into an HBM-resident :class:`~deeprank2_amd.store.GraphStore`
+(CSR, cluster member lists, pooled graph).  A mini-batch is then a list of
+graph ids (``loader.DataLoader``): the per-step PyG collate of
+``trainer.py:541`` disappears.
+
+Deliberate differences (documented in DESIGN.md): ``target_filter``
+conditions are parsed (``">15"``, ``"<=0.5"`` ...) instead of ``eval``-ed;
+``classes`` passed explicitly for a classification task are honoured (the
+reference leaves ``self.classes`` unset in that case); pre-trained
+``train_source`` files are read with ``torch.load(weights_only=True)``.
+"""
+
+from __future__ import annotations
+
+import inspect
+import logging
+import re
+import warnings
+from typing import Literal
+
+import numpy as np
+import pandas as pd
+import torch
+
+from deeprank2_amd.data import Batch, Data
+from deeprank2_amd.io import hdf5
+
+_log = logging.getLogger(__name__)
+
+NODE = "node_features"
+EDGE = "edge_features"
+VALUES = "target_values"
+INDEX = "_index"
+POSITION = "_position"
+REGRESS, CLASSIF = "regress", "classif"
+_TARGET_TASK = {"irmsd": REGRESS, "lrmsd": REGRESS, "fnat": REGRESS, "dockq": REGRESS, "binary": CLASSIF, "capri_class": CLASSIF}
+_COND = re.compile(r"^\s*(>=|<=|==|!=|>|<)\s*([-+0-9.eE]+)\s*$")
+
+
+def _condition_holds(value, cond: str) -> bool:
+    m = _COND.match(cond)
+    if m is None:
+        msg = f"unsupported target_filter condition {cond!r} (use e.g. '>15', '<=0.5', '==1')"
+        raise ValueError(msg)
+    op, rhs = m.group(1), float(m.group(2))
+    v = float(value)
+    return {">": v > rhs, "<": v < rhs, ">=": v >= rhs, "<=": v <= rhs, "==": v == rhs, "!=": v != rhs}[op]
+
+
+class GraphDataset:
+    """HDF5 graphs -> ``Data`` items (``get``) and resident mini-batches (``batch_handle``)."""
+
+    def __init__(  # noqa: PLR0913, PLR0912, C901
+        self,
+        hdf5_path: str | list,
+        subset: list[str] | None = None,
+        train_source: str | GraphDataset | None = None,
+        node_features: list[str] | str | None = "all",
+        edge_features: list[str] | str | None = "all",
+        features_transform: dict | None = None,
+        clustering_method: str | None = None,
+        target: str | None = None,
+        target_transform: bool = False,
+        target_filter: dict[str, str] | None = None,
+        task: Literal["regress", "classif"] | None = None,
+        classes: list | None = None,
+        use_tqdm: bool = True,
+        root: str = "./",
+        check_integrity: bool = True,
+    ):
+        # ---- DeeprankDataset part (dataset.py:36-83) ----
+        if isinstance(hdf5_path, str):
+            self.hdf5_paths = [hdf5_path]
+        elif isinstance(hdf5_path, list):
+            self.hdf5_paths = list(hdf5_path)
+        else:
+            msg = f"hdf5_path: unexpected type: {type(hdf5_path)}"
+            raise TypeError(msg)
+        self.subset = subset
+        self.train_source = train_source
+        self.target = target
+        self.target_transform = target_transform
+        self.target_filter = target_filter
+        self.use_tqdm = use_tqdm
+        self.root = root
+        self._files = dict(zip(self.hdf5_paths, hdf5.read_files(self.hdf5_paths)))
+        if check_integrity:
+            self._check_hdf5_files()
+        self._check_task_and_classes(task, classes)
+        self._create_index_entries()
+        self.df = None
+        self.means = None
+        self.devs = None
+        self.train_means = None
+        self.train_devs = None
+        self.device = torch.device("cuda" if torch.cuda.is_available() else "cpu")
+
+        # ---- GraphDataset part (dataset.py:776-869) ----
+        self.default_vars = {k: v.default for k, v in inspect.signature(self.__init__).parameters.items() if v.default is not inspect.Parameter.empty}
+        self.default_vars["classes_to_index"] = None
+        self.node_features = node_features
+        self.edge_features = edge_features
+        self.clustering_method = clustering_method
+        self.features_transform = features_transform
+
+        if train_source is not None:
+            self.inherited_params = ["node_features", "edge_features", "features_transform", "target", "target_transform", "task", "classes", "classes_to_index"]
+            self._check_and_inherit_train(self.inherited_params)
+            self._check_features()
+        else:
+            self._check_features()
+            self.inherited_params = None
+            if not self.index_entries:
+                msg = "No entries found in the dataset. Please check the dataset parameters."
+                raise IndexError(msg)
+            fname, mol = self.index_entries[0]
+            possible = self._targets_in(self._entry(fname, mol))
+            if self.target is None:
+                msg = f"Please set the target during training dataset definition; targets present in the file/s are {possible}."
+                raise ValueError(msg)
+            if self.target not in possible:
+                msg = f"Target {self.target} not present in the file/s; targets present in the file/s are {possible}."
+                raise ValueError(msg)
+
+        self.features_dict = {NODE: self.node_features, EDGE: self.edge_features}
+        if self.target is not None:
+            self.features_dict[VALUES] = [self.target] if isinstance(self.target, str) else self.target
+
+        standardize = bool(self.features_transform) and any(v.get("standardize") for v in self.features_transform.values())
+        if standardize and train_source is None:
+            if self.df is None:
+                self.hdf5_to_pandas()
+            self._compute_mean_std()
+        elif standardize:
+            self.means = self.train_means
+            self.devs = self.train_devs
+
+        self._stores = {}
+        self._gid = None
+        self._y_cache = None
+
+    # ------------------------------------------------------------------ files
+    def _entry(self, fname, mol):
+        return self._files[fname][mol]
+
+    @staticmethod
+    def _targets_in(grp):
+        return [k.split("/", 1)[1] for k in grp if k.startswith(VALUES + "/")]
+
+    def _check_hdf5_files(self):
+        for p in list(self.hdf5_paths):
+            f = self._files.get(p)
+            if isinstance(f, Exception) or not f:
+                _log.info(f"    -> {p} is {'corrupted' if isinstance(f, Exception) else 'empty'} ")
+                self.hdf5_paths.remove(p)
+
+    def _check_task_and_classes(self, task, classes=None):
+        """dataset.py:156-190."""
+        if task is None:
+            self.task = _TARGET_TASK.get(self.target)
+        else:
+            self.task = task
+        if self.task not in (CLASSIF, REGRESS) and self.target is not None:
+            msg = f"User target detected: {self.target} -> The task argument must be 'classif' or 'regress', currently set as {self.task}"
+            raise ValueError(msg)
+        if task and task != self.task:
+            warnings.warn(f"Target {self.target} expects {self.task}, but was set to task {task} by user. User set task is ignored and {self.task} will be used.", stacklevel=2)
+        if self.task == CLASSIF:
+            if classes is None:
+                self.classes = [0, 1, 2, 3, 4, 5] if self.target == "capri_class" else [0, 1]
+            else:
+                self.classes = list(classes)
+            self.classes_to_index = {c: i for i, c in enumerate(self.classes)}
+        else:
+            self.classes = None
+            self.classes_to_index = None
+
+    def _create_index_entries(self):
+        """dataset.py:223-255 (entries in file order, or in ``subset`` order)."""
+        self.index_entries = []
+        for p in self.hdf5_paths:
+            f = self._files.get(p)
+            if isinstance(f, Exception) or f is None:
+                _log.error(f"on {p}: {f}")
+                continue
+            names = list(f) if self.subset is None else [e for e in self.subset if e in f]
+            if self.target_filter is None:
+                self.index_entries += [(p, e) for e in names]
+            else:
+                self.index_entries += [(p, e) for e in names if self._filter_targets(f[e])]
+
+    def _filter_targets(self, grp) -> bool:
+        """dataset.py:257-294."""
+        if self.target_filter is None:
+            return True
+        present = self._targets_in(grp)
+        for name, cond in self.target_filter.items():
+            if name in present:
+                if isinstance(cond, str):
+                    if not _condition_holds(grp[f"{VALUES}/{name}"], cond):
+                        return False
+                elif cond is not None:
+                    msg = "Conditions not supported"
+                    raise ValueError(msg, cond)
+            else:
+                _log.warning(f"   :Filter {name} not found for entry {grp}\n   :Filter options are: {present}")
+        return True
+
+    def _check_and_inherit_train(self, inherited_params):
+        """dataset.py:85-131 + 192-214."""
+        src = self.train_source
+        if isinstance(src, str):
+            try:
+                data = torch.load(src, map_location="cpu", weights_only=True)
+            except Exception as e:
+                msg = f"The path provided to `train_source` ({src}) is not a DeepRank2 model this package can read safely (weights_only load failed: {e})."
+                raise ValueError(msg) from e
+            if data.get("data_type") not in ("GraphDataset", GraphDataset):
+                msg = f"The pre-trained model has been trained with data of type {data.get('data_type')}; a GraphDataset needs a graph model."
+                raise TypeError(msg)
+            self.train_means = data["means"]
+            self.train_devs = data["devs"]
+            if data.get("features_transform"):
+                for v in data["features_transform"].values():
+                    if isinstance(v.get("transform"), str):
+                        v["transform"] = eval(v["transform"])  # noqa: S307  (a lambda source string, as the reference does)
+        elif isinstance(src, GraphDataset):
+            data = src
+            self.train_means = src.means
+            self.train_devs = src.devs
+        else:
+            msg = f"The train data provided is invalid: {type(src)}.\n\tPlease provide a valid training GraphDataset or the path to a valid DeepRank2 pre-trained model."
+            raise TypeError(msg)
+        mine = vars(self)
+        theirs = data if isinstance(data, dict) else vars(data)
+        for param in inherited_params:
+            if mine[param] != theirs[param]:
+                if mine[param] != self.default_vars[param]:
+                    _log.warning(f"The {param} parameter set here is: {mine[param]}, which is not equivalent to the one in the training phase: {theirs[param]}. Overwriting {param} parameter with the one used in the training phase.")
+                setattr(self, param, theirs[param])
+
+    def _check_features(self):
+        """dataset.py:1054-1122 (feature names from the first entry of the first file)."""
+        first = self._files[self.hdf5_paths[0]]
+        grp = first[next(iter(first))]
+
+        def names(group):
+            seen = []
+            for k in grp:
+                if k.startswith(group + "/"):
+                    n = k.split("/")[1]
+                    if n[0] != "_" and n not in seen:
+                        seen.append(n)
+            return seen
+
+        self.available_node_features = names(NODE)
+        self.available_edge_features = names(EDGE)
+        missing = []
+        for attr, avail in (("node_features", self.available_node_features), ("edge_features", self.available_edge_features)):
+            val = getattr(self, attr)
+            if val == "all":
+                setattr(self, attr, list(avail))
+                self.default_vars[attr] = list(avail)
+                continue
+            if not isinstance(val, list):
+                val = [] if val is None else [val]
+                setattr(self, attr, val)
+            missing += [f for f in val if f not in avail]
+        if missing:
+            msg = f"Not all features could be found in the file {self.hdf5_paths[0]}.\n\tMissing features: {missing}\n\tAvailable node features: {self.available_node_features}\n\tAvailable edge features: {self.available_edge_features}"
+            raise ValueError(msg)
+
+    # -------------------------------------------------------------- pandas/std
+    def _transform_of(self, feat):
+        """(transform, standardize) for a feature: the 'all' entry wins, then the feature's own."""
+        ft = self.features_transform
+        if ft is None:
+            return None, None
+        transform = ft.get("all", {}).get("transform")
+        standard = ft.get("all", {}).get("standardize")
+        if transform is None and feat in ft:
+            transform = ft.get(feat, {}).get("transform")
+        if standard is None and feat in ft:
+            standard = ft.get(feat, {}).get("standardize")
+        return transform, standard
+
+    def hdf5_to_pandas(self) -> pd.DataFrame:
+        """dataset.py:312-361.  As in the reference, the returned frame holds the
+        entries of the LAST file only (its concat never accumulates)."""
+        df = pd.DataFrame()
+        for fname in self.hdf5_paths:
+            f = self._files[fname]
+            first = f[next(iter(f))]
+            entries = [e for e in f if self.subset is None or e in self.subset]
+            cols = {"id": entries}
+            for group, feats in self.features_dict.items():
+                for feat in feats:
+                    transform = None
+                    if self.features_transform:
+                        transform = self.features_transform.get("all", {}).get("transform")
+                        if transform is None and feat in self.features_transform:
+                            transform = self.features_transform.get(feat, {}).get("transform")
+                    key = f"{group}/{feat}"
+                    if np.ndim(first[key]) == 2:  # noqa: PLR2004
+                        for i in range(first[key].shape[1]):
+                            col = [f[e][key][:, i] for e in entries]
+                            cols[f"{feat}_{i}"] = [transform(r) for r in col] if transform else col
+                    else:
+                        col = [f[e][key][()] if np.ndim(f[e][key]) == 0 else f[e][key][:] for e in entries]
+                        cols[feat] = [transform(r) for r in col] if transform else col
+            df = pd.DataFrame(data=cols).reset_index(drop=True)
+        self.df = df
+        return self.df
+
+    def _compute_mean_std(self):
+        """dataset.py:448-462 (rounded to one decimal, NaN-aware)."""
+
+        def arrays(col):
+            return isinstance(self.df[col].to_numpy()[0], np.ndarray)
+
+        self.means = {c: round(np.nanmean(np.concatenate(self.df[c].values)), 1) if arrays(c) else round(np.nanmean(self.df[c].to_numpy()), 1) for c in self.df.columns[1:]}
+        self.devs = {c: round(np.nanstd(np.concatenate(self.df[c].to_numpy())), 1) if arrays(c) else round(np.nanstd(self.df[c].to_numpy()), 1) for c in self.df.columns[1:]}
+
+    # ------------------------------------------------------------------ items
+    def len(self) -> int:
+        return len(self.index_entries)
+
+    def __len__(self) -> int:
+        return len(self.index_entries)
+
+    def __getitem__(self, idx):
+        return self.get(idx)
+
+    def get(self, idx: int) -> Data:
+        fname, mol = self.index_entries[idx]
+        return self.load_one_graph(fname, mol)
+
+    def _feature_block(self, grp, group, feats, fname, entry_name):
+        blocks = []
+        for feat in feats:
+            if feat[0] == "_":
+                continue
+            vals = grp[f"{group}/{feat}"][()]
+            transform, standard = self._transform_of(feat)
+            if transform:
+                with warnings.catch_warnings(record=True) as w:
+                    warnings.simplefilter("always")
+                    vals = transform(vals)
+                    if len(w) > 0:
+                        msg = f"Invalid value occurs in {entry_name}, file {fname}, when applying {transform} for feature {feat}.\n\tPlease change the transformation function for {feat}."
+                        raise ValueError(msg)
+            if np.ndim(vals) == 1:
+                vals = np.reshape(vals, (-1, 1))
+                if standard:
+                    vals = (vals - self.means[feat]) / self.devs[feat]
+            elif standard:  # multi-channel: every stats key containing the name (reference matching)
+                m = [v for k, v in self.means.items() if feat in k]
+                d = [v for k, v in self.devs.items() if feat in k]
+                vals = (vals - m) / d
+            blocks.append(vals)
+        return blocks
+
+    def graph_arrays(self, fname: str, entry_name: str) -> dict:
+        """``load_one_graph`` as numpy: x f32 [N,F], edge_index i64 [2,E],
+        edge_attr f32 [E,Fe], y (float or None), pos f32 [N,3], cluster0/1."""
+        grp = self._entry(fname, entry_name)
+        out = {}
+        nb = self._feature_block(grp, NODE, self.node_features, fname, entry_name) if self.node_features else []
+        out["x"] = np.hstack(nb).astype(np.float32) if nb else None
+        if f"{EDGE}/{INDEX}" in grp:
+            ind = grp[f"{EDGE}/{INDEX}"][()]
+            if ind.ndim == 2:  # noqa: PLR2004
+                ind = np.vstack((ind, np.flip(ind, 1))).T
+            out["edge_index"] = np.ascontiguousarray(ind, dtype=np.int64)
+        else:
+            out["edge_index"] = np.zeros((2, 0), dtype=np.int64)
+        eb = self._feature_block(grp, EDGE, self.edge_features, fname, entry_name) if self.edge_features else []
+        if eb:
+            ed = np.hstack(eb)
+            out["edge_attr"] = np.vstack((ed, ed)).astype(np.float32)
+        else:
+            out["edge_attr"] = np.zeros((out["edge_index"].shape[1], 0), dtype=np.float32)
+        y = None
+        if self.target is not None and f"{VALUES}/{self.target}" in grp:
+            y = float(np.float32(grp[f"{VALUES}/{self.target}"][()]))
+            if self.target_transform is True:
+                if self.task == REGRESS:
+                    y = float(torch.sigmoid(torch.log(torch.tensor([y], dtype=torch.float)))[0])
+                else:
+                    msg = f'Sigmoid transformation not possible for {self.task} tasks. Please change `task` to "regress" or set `target_transform` to `False`.'
+                    raise ValueError(msg)
+        elif self.target is not None and self.train_source is None:
+            msg = f"Target {self.target} missing in entry {entry_name} in file {fname}, possible targets are {self._targets_in(grp)}.\n\tUse the query class to add more target values to input data."
+            raise ValueError(msg)
+        out["y"] = y
+        out["pos"] = np.asarray(grp[f"{NODE}/{POSITION}"], dtype=np.float32)
+        out["cluster0"] = out["cluster1"] = None
+        if self.clustering_method is not None:
+            k0 = f"clustering/{self.clustering_method}/depth_0"
+            k1 = f"clustering/{self.clustering_method}/depth_1"
+            if k0 in grp and k1 in grp:
+                out["cluster0"] = np.asarray(grp[k0], dtype=np.int64)
+                out["cluster1"] = np.asarray(grp[k1], dtype=np.int64)
+            else:
+                _log.warning("no clusters detected")
+        return out
+
+    def load_one_graph(self, fname: str, entry_name: str) -> Data:
+        """dataset.py:883-1052 -> ``Data``."""
+        a = self.graph_arrays(fname, entry_name)
+        d = Data(
+            x=None if a["x"] is None else torch.from_numpy(a["x"]),
+            edge_index=torch.from_numpy(a["edge_index"]),
+            edge_attr=torch.from_numpy(a["edge_attr"]),
+            y=None if a["y"] is None else torch.tensor([a["y"]], dtype=torch.float),
+            pos=torch.from_numpy(a["pos"]),
+        )
+        d.cluster0 = None if a["cluster0"] is None else torch.from_numpy(a["cluster0"])
+        d.cluster1 = None if a["cluster1"] is None else torch.from_numpy(a["cluster1"])
+        d.entry_names = entry_name
+        return d
+
+    # ------------------------------------------------------ resident batches
+    def _targets_of(self, indices):
+        if self._y_cache is None:
+            ys = [self.graph_arrays(*e)["y"] for e in self.index_entries]
+            self._y_cache = None if any(v is None for v in ys) else torch.tensor(ys, dtype=torch.float)
+        if self._y_cache is None:
+            return None
+        return self._y_cache[torch.as_tensor(indices, dtype=torch.long)]
+
+    def graph_store(self, device):
+        """All graphs of the dataset packed once into HBM (cached per device)."""
+        from deeprank2_amd.store import GraphRecord, GraphStore, pack_graphs  # noqa: PLC0415
+
+        device = torch.device(device)
+        key = (str(device), tuple(self.index_entries))
+        st = self._stores.get(key)
+        if st is None:
+            recs = []
+            for fname, mol in self.index_entries:
+                a = self.graph_arrays(fname, mol)
+                recs.append(GraphRecord(x=a["x"], edge_index=a["edge_index"], edge_attr=a["edge_attr"], cluster0=a["cluster0"], cluster1=a["cluster1"], y=a["y"], pos=a["pos"], name=mol))
+            st = GraphStore(pack_graphs(recs), device)
+            self._stores = {key: st}
+        return st
+
+    def batch_handle(self, indices, device):
+        from deeprank2_amd.fused import BatchHandle  # noqa: PLC0415
+
+        return BatchHandle(self.graph_store(device), np.asarray(indices, dtype=np.int32))
+
+    def batch(self, indices) -> Batch:
+        return Batch(self, indices)
+
+    def subset_entries(self, positions):
+        """A copy of this dataset restricted to ``index_entries[positions]`` (shares the file cache)."""
+        import copy  # noqa: PLC0415
+
+        out = copy.copy(self)
+        out.index_entries = [self.index_entries[i] for i in positions]
+        out._stores = {}
+        out._y_cache = None
+        return out

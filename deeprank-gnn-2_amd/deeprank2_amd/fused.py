@@ -47,10 +47,16 @@ class BatchHandle:
 
 
 def resolve_batch(data, device) -> BatchHandle:
-    """Our DataLoader attaches a handle; any other PyG-style batch is packed here."""
+    """Our DataLoader's batches name their graphs in the dataset's resident
+    store; any other PyG-style batch is packed here (one upload per call)."""
     h = getattr(data, "_dr_handle", None)
     if h is not None:
         return h
+    fn = getattr(data, "dr_handle", None)
+    if callable(fn):
+        h = fn(device)
+        if h is not None:
+            return h
     store = GraphStore(pack_graphs(records_from_batch(data)), device)
     return BatchHandle(store, np.arange(store.n_graphs, dtype=np.int32))
 
