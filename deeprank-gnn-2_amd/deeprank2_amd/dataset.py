@@ -330,8 +330,9 @@ class GraphDataset:
         def arrays(col):
             return isinstance(self.df[col].to_numpy()[0], np.ndarray)
 
-        self.means = {c: round(np.nanmean(np.concatenate(self.df[c].values)), 1) if arrays(c) else round(np.nanmean(self.df[c].to_numpy()), 1) for c in self.df.columns[1:]}
-        self.devs = {c: round(np.nanstd(np.concatenate(self.df[c].to_numpy())), 1) if arrays(c) else round(np.nanstd(self.df[c].to_numpy()), 1) for c in self.df.columns[1:]}
+        # python floats (not numpy scalars) so checkpoints load with weights_only=True
+        self.means = {c: float(round(np.nanmean(np.concatenate(self.df[c].values)), 1) if arrays(c) else round(np.nanmean(self.df[c].to_numpy()), 1)) for c in self.df.columns[1:]}
+        self.devs = {c: float(round(np.nanstd(np.concatenate(self.df[c].to_numpy())), 1) if arrays(c) else round(np.nanstd(self.df[c].to_numpy()), 1)) for c in self.df.columns[1:]}
 
     # ------------------------------------------------------------------ items
     def len(self) -> int:

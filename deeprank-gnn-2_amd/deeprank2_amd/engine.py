@@ -159,6 +159,44 @@ class FusedTrainStep:
             _lib.check(lib.dr_reduce_update(self._table, None, None, h.B, self._adam, None, 1.0, None, _lib.stream_ptr(self.device)), "dr_reduce_update")
         return self.loss_out, self.out[: h.B]
 
+    # ---- torch.optim.Adam-compatible optimizer state (checkpoints) ----
+    def adam_state_dict(self):
+        """The fused optimizer state as ``torch.optim.Adam(model.parameters()).state_dict()``
+        would hold it (parameter order = the model's ``parameters()`` order)."""
+        opt = torch.optim.Adam(self.params, lr=self.lr, betas=self.betas, eps=self.eps, weight_decay=self.weight_decay)
+        t = int(self.counter[0].item())
+        if t > 0:
+            for p, (m, v) in zip(self.params, self.states):
+                opt.state[p] = {"step": torch.tensor(float(t)), "exp_avg": m.detach().clone(), "exp_avg_sq": v.detach().clone()}
+        return opt.state_dict()
+
+    def load_adam_state_dict(self, sd):
+        """Inverse of :meth:`adam_state_dict` (also accepts a torch Adam state_dict)."""
+        group = sd["param_groups"][0]
+        if len(group["params"]) != len(self.params) or group.get("amsgrad", False):
+            msg = "optimizer state does not match this model (or uses amsgrad)"
+            raise ValueError(msg)
+        states = sd.get("state", {})
+        steps = set()
+        for slot, (m, v) in zip(group["params"], self.states):
+            st = states.get(slot)
+            if st is None:
+                m.zero_()
+                v.zero_()
+                steps.add(0)
+                continue
+            m.copy_(st["exp_avg"])
+            v.copy_(st["exp_avg_sq"])
+            steps.add(int(float(st["step"])))
+        if len(steps) > 1:
+            msg = f"parameters are at different Adam steps {sorted(steps)}"
+            raise ValueError(msg)
+        t = steps.pop() if steps else 0
+        self.counter.fill_(t)
+        self.step_count = t
+        self.lr, self.betas, self.eps, self.weight_decay = group["lr"], tuple(group["betas"]), group["eps"], group["weight_decay"]
+        self._build_structs()
+
     def _state_tensors(self):
         return [*self.params, *[s for st in self.states for s in st], self.counter, self.flat]
 

@@ -1,0 +1,609 @@
+"""Trainer — drop-in for ``deeprank2.trainer.Trainer`` on the MI355X path.
+
+Same constructor, ``configure_optimizers`` / ``set_lossfunction`` /
+``train`` / ``test`` surface, epoch-0 evaluation, best-model selection,
+early stopping, output exporters and checkpoint keys as the reference
+(``deeprank2/trainer.py:31-1004``).
+
+The hot loop (``_epoch``, trainer.py:666-724) runs, for a model with a fused
+spec (GINet, FoutNet) under the default optimizer (Adam) and loss (MSELoss /
+CrossEntropyLoss, optional class weights), as two HIP launches per
+mini-batch through :class:`~deeprank2_amd.engine.FusedTrainStep` on graphs
+already resident in HBM; losses and outputs stay on the device until the
+epoch ends (one device->host copy per epoch instead of per-step ``.item()``).
+Any other optimizer or loss takes the generic path: the model's autograd
+forward/backward (still the HIP graph pass) + the torch optimizer.
+
+Multi-GPU: ``ngpu > 1`` expects one process per GPU started by
+``torch.distributed.run`` (``init_process_group`` done by the caller or here
+from the environment); each global mini-batch is split across ranks in order
+and the gradients are all-reduced once per step.  The reference's
+``nn.DataParallel`` (trainer.py:387-389) has no counterpart.
+
+Deliberate differences: the model always runs on the GPU (there is
+no CPU path; ``cuda=False`` is accepted and logged); a "best model"
+checkpoint is a snapshot (the reference keeps references to live tensors, so
+its in-memory best model follows later updates); checkpoints store the
+optimizer / loss / dataset types by name so that they load with
+``torch.load(weights_only=True)``; ``_precluster`` (MCL / Louvain, needs
+networkx / markov_clustering) is not provided: datasets must carry their
+stored ``clustering/<method>/depth_{0,1}``.
+"""
+
+from __future__ import annotations
+
+import copy
+import inspect
+import logging
+import re
+import warnings
+from time import time
+
+import numpy as np
+import torch
+from torch import nn
+from torch.nn.functional import softmax
+
+from deeprank2_amd.dataset import CLASSIF, REGRESS, GraphDataset
+from deeprank2_amd.distributed import shard_contiguous
+from deeprank2_amd.engine import FusedTrainStep
+from deeprank2_amd.exporters import HDF5OutputExporter, OutputExporterCollection
+from deeprank2_amd.loader import DataLoader
+from deeprank2_amd.utils.earlystopping import EarlyStopping
+
+_log = logging.getLogger(__name__)
+
+regression_losses = (nn.L1Loss, nn.SmoothL1Loss, nn.MSELoss, nn.HuberLoss)
+binary_classification_losses = (nn.SoftMarginLoss, nn.BCELoss, nn.BCEWithLogitsLoss)
+multi_classification_losses = (nn.CrossEntropyLoss, nn.NLLLoss, nn.PoissonNLLLoss, nn.GaussianNLLLoss, nn.KLDivLoss, nn.MultiLabelMarginLoss, nn.MultiLabelSoftMarginLoss)
+other_losses = (nn.HingeEmbeddingLoss, nn.CosineEmbeddingLoss, nn.MarginRankingLoss, nn.TripletMarginLoss, nn.CTCLoss)
+classification_losses = multi_classification_losses + binary_classification_losses
+classification_tested = (nn.CrossEntropyLoss, nn.NLLLoss, nn.BCELoss, nn.BCEWithLogitsLoss)
+
+_OPTIMIZERS = {c.__name__: c for c in (torch.optim.Adam, torch.optim.AdamW, torch.optim.SGD, torch.optim.RMSprop, torch.optim.Adagrad, torch.optim.Adadelta, torch.optim.Adamax, torch.optim.NAdam, torch.optim.RAdam)}
+_LOSSES = {c.__name__: c for c in regression_losses + classification_losses + other_losses}
+
+
+class Trainer:
+    def __init__(  # noqa: PLR0913, PLR0912, C901
+        self,
+        neuralnet: type[nn.Module] | None = None,
+        dataset_train: GraphDataset | None = None,
+        dataset_val: GraphDataset | None = None,
+        dataset_test: GraphDataset | None = None,
+        val_size: float | int | None = None,
+        test_size: float | int | None = None,
+        class_weights: bool = False,
+        pretrained_model: str | None = None,
+        cuda: bool = False,
+        ngpu: int = 0,
+        output_exporters: list | None = None,
+    ):
+        self.neuralnet = neuralnet
+        self.pretrained_model = pretrained_model
+        self._init_datasets(dataset_train, dataset_val, dataset_test, val_size, test_size)
+        self.cuda = cuda
+        self.ngpu = ngpu
+        if torch.cuda.is_available():
+            self.device = torch.device("cuda", torch.cuda.current_device())
+            if not cuda:
+                _log.info("deeprank2_amd has no CPU path: the model runs on the GPU although cuda=False was given.")
+            self.ngpu = max(1, ngpu)
+        else:
+            self.device = torch.device("cpu")
+            _log.warning("No GPU visible: models can be built and inspected but not trained or evaluated (no CPU fallback).")
+        self.process_group = None
+        if self.ngpu > 1:
+            if not torch.distributed.is_initialized():
+                msg = "ngpu > 1 runs one process per GPU: launch with torch.distributed.run (torchrun) and init_process_group first"
+                raise ValueError(msg)
+            self.process_group = torch.distributed.group.WORLD
+        self._init_output_exporters(output_exporters)
+
+        self.data_type = None
+        self.batch_size_train = None
+        self.batch_size_test = None
+        self.shuffle = None
+        self.model_load_state_dict = None
+        self._fused = None
+
+        if self.pretrained_model is None:
+            if self.dataset_train is None:
+                msg = "No training data specified. Training data is required if there is no pretrained model."
+                raise ValueError(msg)
+            if self.neuralnet is None:
+                msg = "No neural network specified. Specifying a model framework is required if there is no pretrained model."
+                raise ValueError(msg)
+            self._init_from_dataset(self.dataset_train)
+            self.optimizer = None
+            self.class_weights = class_weights
+            self.subset = self.dataset_train.subset
+            self.epoch_saved_model = None
+            if self.target is None:
+                msg = "No target set. You need to choose a target (set in the dataset) for training."
+                raise ValueError(msg)
+            self._load_model()
+            if self.clustering_method is not None:
+                if self.clustering_method not in ("mcl", "louvain"):
+                    msg = f"Invalid node clustering method: {self.clustering_method}. Please set clustering_method to 'mcl', 'louvain' or None."
+                    raise ValueError(msg)
+                if self.dataset_val is None:
+                    _log.warning("No validation dataset given. Randomly splitting training set in training set and validation set.")
+                    self.dataset_train, self.dataset_val = _divide_dataset(self.dataset_train, splitsize=self.val_size)
+        else:
+            if self.neuralnet is None:
+                msg = "No neural network class found. Please add it to complete loading the pretrained model."
+                raise ValueError(msg)
+            if self.dataset_test is None:
+                msg = "No dataset_test found. Please add it to evaluate the pretrained model."
+                raise ValueError(msg)
+            if self.dataset_train is not None:
+                self.dataset_train = None
+                _log.warning("Pretrained model loaded: dataset_train will be ignored.")
+            if self.dataset_val is not None:
+                self.dataset_val = None
+                _log.warning("Pretrained model loaded: dataset_val will be ignored.")
+            self._init_from_dataset(self.dataset_test)
+            self._load_params()
+            self._load_pretrained_model()
+
+    # ------------------------------------------------------------------ setup
+    def _init_output_exporters(self, output_exporters):
+        self._output_exporters = OutputExporterCollection(*output_exporters) if output_exporters is not None else OutputExporterCollection(HDF5OutputExporter("./output"))
+
+    def _init_datasets(self, dataset_train, dataset_val, dataset_test, val_size, test_size):
+        self._check_dataset_equivalence(dataset_train, dataset_val, dataset_test)
+        self.dataset_train = dataset_train
+        self.dataset_test = dataset_test
+        self.dataset_val = dataset_val
+        self.val_size = val_size
+        self.test_size = test_size
+        if test_size is not None:
+            if dataset_test is None:
+                self.dataset_train, self.dataset_test = _divide_dataset(dataset_train, test_size)
+            else:
+                _log.warning("Test dataset was provided to Trainer; test_size parameter is ignored.")
+        if val_size is not None:
+            if dataset_val is None:
+                self.dataset_train, self.dataset_val = _divide_dataset(dataset_train, val_size)
+            else:
+                _log.warning("Validation dataset was provided to Trainer; val_size parameter is ignored.")
+
+    def _check_dataset_equivalence(self, dataset_train, dataset_val, dataset_test):
+        if dataset_train is None:
+            if dataset_test is None:
+                msg = "Please provide at least a train or test dataset"
+                raise ValueError(msg)
+            return
+        if not isinstance(dataset_train, GraphDataset):
+            msg = f"train dataset is not the right type {type(dataset_train)}. Make sure it's a GraphDataset"
+            raise TypeError(msg)
+        for ds, kind in ((dataset_val, "valid"), (dataset_test, "test")):
+            if ds is None:
+                continue
+            if ds.train_source is None:
+                msg = f"{kind} dataset has train_source parameter set to None. Make sure to set it as a valid training data source."
+                raise ValueError(msg)
+            if ds.train_source is not dataset_train and ds.train_source != dataset_train:
+                msg = f"{kind} dataset has different train_source parameter from Trainer. Make sure to assign equivalent train_source in Trainer."
+                raise ValueError(msg)
+
+    def _init_from_dataset(self, dataset):
+        if not isinstance(dataset, GraphDataset):
+            msg = f"Incorrect `dataset` type provided: {type(dataset)}. Please provide a `GraphDataset` object instead."
+            raise TypeError(msg)
+        self.clustering_method = dataset.clustering_method
+        self.node_features = dataset.node_features
+        self.edge_features = dataset.edge_features
+        self.features = None
+        self.features_transform = dataset.features_transform
+        self.means = dataset.means
+        self.devs = dataset.devs
+        self.target = dataset.target
+        self.target_transform = dataset.target_transform
+        self.task = dataset.task
+        self.classes = dataset.classes
+        self.classes_to_index = dataset.classes_to_index
+
+    def _load_model(self):
+        self._put_model_to_device(self.dataset_train)
+        self.configure_optimizers()
+        self.set_lossfunction()
+
+    def _put_model_to_device(self, dataset):
+        if self.task == REGRESS:
+            self.output_shape = 1
+        elif self.task == CLASSIF:
+            self.output_shape = len(self.classes)
+        d0 = dataset.get(0)
+        target_shape = d0.y.shape[0] if d0.y is not None else None
+        self.model = self.neuralnet(d0.num_features, self.output_shape, len(dataset.edge_features)).to(self.device)
+        for e in self._output_exporters:
+            if not e.is_compatible_with(self.output_shape, target_shape):
+                msg = f"Output exporter of type {type(e)}\n\tis not compatible with output shape {self.output_shape}\n\tand target shape {target_shape}."
+                raise ValueError(msg)
+
+    def configure_optimizers(self, optimizer=None, lr: float = 0.001, weight_decay: float = 1e-05):
+        """trainer.py:401-426.  ``None`` -> Adam (the fused path)."""
+        self.lr = lr
+        self.weight_decay = weight_decay
+        cls = torch.optim.Adam if optimizer is None else optimizer
+        try:
+            self.optimizer = cls(self.model.parameters(), lr=lr, weight_decay=weight_decay)
+        except Exception as e:
+            _log.error(e)
+            _log.info("Invalid optimizer. Please use only optimizers classes from torch.optim package.")
+            raise
+        self._fused = None
+
+    def set_lossfunction(self, lossfunction=None, override_invalid: bool = False):  # noqa: C901
+        """trainer.py:428-501 (same validity rules per task)."""
+
+        def invalid():
+            text = f"The provided loss function ({lossfunction}) is not appropriate for {self.task} tasks."
+            if override_invalid:
+                _log.warning(text + " override_invalid is set: training continues with it.")
+            else:
+                raise ValueError(text + "\n\tIf you want to use this loss function anyway, set override_invalid to True.")
+
+        if lossfunction in other_losses:
+            invalid()
+            custom = False
+        else:
+            custom = lossfunction is not None and lossfunction not in (regression_losses + classification_losses)
+        if self.task == REGRESS:
+            if lossfunction is None:
+                lossfunction = nn.MSELoss
+            elif custom:
+                _log.warning(f"The provided loss function ({lossfunction}) is not part of the default list.")
+            elif lossfunction not in regression_losses:
+                invalid()
+            self.lossfunction = lossfunction()
+        elif self.task == CLASSIF:
+            if lossfunction is None:
+                lossfunction = nn.CrossEntropyLoss
+            elif custom:
+                _log.warning(f"The provided loss function ({lossfunction}) is not part of the default list.")
+            elif lossfunction not in classification_losses:
+                invalid()
+            self.lossfunction = lossfunction() if not self.class_weights else lossfunction
+        self._fused = None
+
+    # --------------------------------------------------------------- helpers
+    def _fused_step(self):
+        """FusedTrainStep when the configuration is exactly what the kernels compute."""
+        if self._fused is not None:
+            return self._fused or None
+        ok = hasattr(self.model, "fused_spec") and type(self.optimizer) is torch.optim.Adam
+        if ok:
+            g = self.optimizer.param_groups[0]
+            ok = len(self.optimizer.param_groups) == 1 and not g.get("amsgrad") and not g.get("maximize")
+        lf = self.lossfunction
+        loss = None
+        if ok and self.task == REGRESS and type(lf) is nn.MSELoss and lf.reduction == "mean":
+            loss = "mse"
+        elif ok and self.task == CLASSIF and type(lf) is nn.CrossEntropyLoss and lf.reduction == "mean" and lf.label_smoothing == 0 and lf.ignore_index == -100:
+            loss = "ce"
+        if loss is None or self.output_shape > 16 or self.device.type != "cuda":  # noqa: PLR2004
+            self._fused = False
+            return None
+        g = self.optimizer.param_groups[0]
+        w = lf.weight if loss == "ce" else None
+        step = FusedTrainStep(self.model, lr=g["lr"], weight_decay=g["weight_decay"], betas=tuple(g["betas"]), eps=g["eps"], loss=loss, class_weights=w, process_group=self.process_group)
+        if self.optimizer.state:
+            step.load_adam_state_dict(self.optimizer.state_dict())
+        self._fused = step
+        return step
+
+    def _targets_for_kernel(self, dataset, device):
+        """The in-kernel CE loss reads a class index per graph: map the stored
+        class values through ``classes_to_index`` once per store."""
+        store = dataset.graph_store(device)
+        if self.task != CLASSIF or getattr(store, "_dr_class_index", None) == self.classes_to_index:
+            return store
+        y = dataset._targets_of(list(range(len(dataset))))  # noqa: SLF001
+        if y is not None:
+            store.set_targets(np.array([self.classes_to_index[int(v)] for v in y.tolist()], dtype=np.float32))
+            store._dr_class_index = dict(self.classes_to_index)  # noqa: SLF001
+        return store
+
+    def _local(self, idx):
+        if self.process_group is None:
+            return idx
+        return shard_contiguous(idx, torch.distributed.get_rank(), torch.distributed.get_world_size())
+
+    def _format_output(self, pred, target=None):
+        """trainer.py:807-835."""
+        if self.task == CLASSIF and target is not None:
+            target = torch.tensor([self.classes_to_index[x] if isinstance(x, str) else self.classes_to_index[int(x)] for x in target])
+            if isinstance(self.lossfunction, nn.BCELoss | nn.BCEWithLogitsLoss):
+                msg = "BCELoss and BCEWithLogitsLoss are currently not supported."
+                raise ValueError(msg)
+            if isinstance(self.lossfunction, classification_losses) and not isinstance(self.lossfunction, classification_tested):
+                msg = f"{self.lossfunction} is currently not supported.\n\tSupported loss functions for classification: {classification_tested}."
+                raise ValueError(msg)
+        elif self.task == REGRESS:
+            pred = pred.reshape(-1)
+        if target is not None:
+            target = target.to(self.device)
+        return pred, target
+
+    def _export_pred(self, pred):
+        return softmax(pred.detach(), dim=1) if self.task == CLASSIF else pred.detach().reshape(-1)
+
+    # ---------------------------------------------------------------- train
+    def train(  # noqa: PLR0912, PLR0915, C901
+        self,
+        nepoch: int = 1,
+        batch_size: int = 32,
+        shuffle: bool = True,
+        earlystop_patience: int | None = None,
+        earlystop_maxgap: float | None = None,
+        min_epoch: int = 10,
+        validate: bool = False,
+        num_workers: int = 0,
+        best_model: bool = True,
+        filename: str | None = "model.pth.tar",
+    ):
+        """trainer.py:503-664."""
+        if self.dataset_train is None:
+            msg = "No training dataset provided."
+            raise ValueError(msg)
+        self.data_type = type(self.dataset_train)
+        self.batch_size_train = batch_size
+        self.shuffle = shuffle
+        self.train_loader = DataLoader(self.dataset_train, batch_size=batch_size, shuffle=shuffle, num_workers=num_workers, pin_memory=self.cuda)
+        self.valid_loader = DataLoader(self.dataset_val, batch_size=batch_size, shuffle=shuffle, num_workers=num_workers, pin_memory=self.cuda) if self.dataset_val is not None else None
+        if self.valid_loader is None:
+            _log.warning("Training data will be used both for learning and model selection, which may lead to overfitting.")
+
+        if self.task == CLASSIF and self.class_weights:
+            y = self.dataset_train._targets_of(list(range(len(self.dataset_train))))  # noqa: SLF001
+            counts = torch.tensor([float((y == c).sum()) for c in self.classes], dtype=torch.float32)
+            self.weights = 1.0 / counts
+            self.weights = self.weights / self.weights.sum()
+            try:
+                self.lossfunction = self.lossfunction(weight=self.weights.to(self.device))
+            except TypeError as e:
+                msg = f"Loss function {self.lossfunction} does not allow for weighted classes.\n\tPlease use a different loss function or set class_weights to False.\n"
+                raise ValueError(msg) from e
+            self._fused = None
+        else:
+            self.weights = None
+
+        train_losses, valid_losses = [], []
+        saved_model = False
+        checkpoint_model = None
+        early_stopping = EarlyStopping(patience=earlystop_patience, maxgap=earlystop_maxgap, min_epoch=min_epoch, trace_func=_log.info) if (earlystop_patience or earlystop_maxgap) else None
+        epoch = 0
+        with self._output_exporters:
+            self.nepoch = nepoch
+            self._eval(self.train_loader, 0, "training")
+            if validate:
+                if self.valid_loader is None:
+                    msg = "No validation dataset provided."
+                    raise ValueError(msg)
+                self._eval(self.valid_loader, 0, "validation")
+            for epoch in range(1, nepoch + 1):
+                self.model.train()
+                loss_ = self._epoch(epoch, "training")
+                train_losses.append(loss_)
+                if validate:
+                    loss_ = self._eval(self.valid_loader, epoch, "validation")
+                    valid_losses.append(loss_)
+                    if best_model and min(valid_losses) == loss_:
+                        checkpoint_model = self._save_model()
+                        saved_model = True
+                        self.epoch_saved_model = epoch
+                    if early_stopping:
+                        early_stopping(epoch, valid_losses[-1], train_losses[-1])
+                        if early_stopping.early_stop:
+                            break
+                elif best_model and min(train_losses) == loss_:
+                    checkpoint_model = self._save_model()
+                    saved_model = True
+                    self.epoch_saved_model = epoch
+            if best_model is False or not saved_model:
+                checkpoint_model = self._save_model()
+                self.epoch_saved_model = epoch
+                if not saved_model:
+                    warnings.warn("A model has been saved but the validation and/or the training losses were NaN;\n\ttry to increase the cutoff distance during the data processing or the number of data points during the training.", stacklevel=2)
+        if filename:
+            torch.save(checkpoint_model, filename)
+        self.opt_loaded_state_dict = checkpoint_model["optimizer_state"]
+        self.model_load_state_dict = checkpoint_model["model_state"]
+        self.optimizer.load_state_dict(self.opt_loaded_state_dict)
+        self.model.load_state_dict(self.model_load_state_dict)
+        if self._fused:
+            self._fused.load_adam_state_dict(self.opt_loaded_state_dict)
+
+    def _epoch(self, epoch_number: int, pass_name: str):
+        """trainer.py:666-724: one pass over the training loader."""
+        step = self._fused_step()
+        t0 = time()
+        dev = self.device
+        outputs, targets, names = [], [], []
+        loss_sum = torch.zeros((), dtype=torch.float64, device=dev)
+        count = 0
+        ds = self.dataset_train
+        if step is not None:
+            self._targets_for_kernel(ds, dev)
+        for idx in self.train_loader.batches():
+            b = len(idx)
+            if step is not None:
+                local = self._local(idx)
+                h = ds.batch_handle(local, dev)
+                loss, out = step.step(h, global_batch=b)
+                loss_sum += loss[0].double() * b
+                pred = out.clone()
+                if self.process_group is not None:
+                    pred = _gather_rows(pred, b, self.process_group)
+                pred, y = self._format_output(pred, ds._targets_of(idx))  # noqa: SLF001
+            else:
+                batch = ds.batch(idx).to(dev)
+                self.optimizer.zero_grad()
+                pred = self.model(batch)
+                pred, y = self._format_output(pred, batch.y)
+                loss = self.lossfunction(pred, y)
+                loss.backward()
+                self.optimizer.step()
+                loss_sum += loss.detach().double() * b
+            count += b
+            outputs.append(self._export_pred(pred))
+            targets.append(y.detach())
+            names += [ds.index_entries[i][1] for i in idx]
+        epoch_loss = float(loss_sum.item()) / count if count else None
+        out_l = torch.cat(outputs).cpu().numpy().tolist() if outputs else []
+        tgt_l = torch.cat(targets).cpu().numpy().tolist() if targets else []
+        dt = time() - t0
+        self._output_exporters.process(pass_name, epoch_number, names, out_l, tgt_l, epoch_loss)
+        _log.info(f"{pass_name} loss {epoch_loss} | time {dt}")
+        return epoch_loss
+
+    def _eval(self, loader: DataLoader, epoch_number: int, pass_name: str):
+        """trainer.py:726-795: forward passes, loss per batch on the device."""
+        self.model.eval()
+        dev = self.device
+        outputs, targets, names = [], [], []
+        loss_sum = torch.zeros((), dtype=torch.float64, device=dev)
+        count = 0
+        has_target = True
+        t0 = time()
+        with torch.no_grad():
+            for idx in loader.batches():
+                batch = loader.dataset.batch(idx).to(dev)
+                pred = self.model(batch)
+                pred, y = self._format_output(pred, batch.y)
+                if y is not None:
+                    loss = self.lossfunction(pred, y)
+                    loss_sum += loss.double() * pred.shape[0]
+                    count += pred.shape[0]
+                    targets.append(y)
+                else:
+                    has_target = False
+                outputs.append(self._export_pred(pred))
+                names += [loader.dataset.index_entries[i][1] for i in idx]
+        eval_loss = float(loss_sum.item()) / count if count else None
+        out_l = torch.cat(outputs).cpu().numpy().tolist() if outputs else []
+        tgt_l = torch.cat(targets).cpu().numpy().tolist() if (targets and has_target) else [None] * len(out_l)
+        dt = time() - t0
+        self._output_exporters.process(pass_name, epoch_number, names, out_l, tgt_l, eval_loss)
+        _log.info(f"{pass_name} loss {eval_loss} | time {dt}")
+        self.model.train()
+        return eval_loss
+
+    def test(self, batch_size: int = 32, num_workers: int = 0):
+        """trainer.py:837-871."""
+        if (not self.pretrained_model) and (not self.model_load_state_dict):
+            msg = "No pretrained model provided and no training performed. Please provide a pretrained model or train the model before testing."
+            raise ValueError(msg)
+        self.batch_size_test = batch_size
+        if self.dataset_test is None:
+            msg = "No test dataset provided."
+            raise ValueError(msg)
+        self.test_loader = DataLoader(self.dataset_test, batch_size=batch_size, num_workers=num_workers, pin_memory=self.cuda)
+        with self._output_exporters:
+            self._eval(self.test_loader, self.epoch_saved_model, "testing")
+
+    # ------------------------------------------------------------ checkpoints
+    def _optimizer_state(self):
+        if self._fused:
+            return self._fused.adam_state_dict()
+        return self.optimizer.state_dict()
+
+    def _save_model(self):
+        """trainer.py:910-956, with types stored by name (weights_only-loadable)
+        and tensors snapshotted."""
+        ft = copy.deepcopy(self.features_transform)
+        if ft:
+            for v in ft.values():
+                if v.get("transform") is None or isinstance(v["transform"], str):
+                    continue
+                src = inspect.getsource(v["transform"])
+                m = re.search(r"[\"|\']transform[\"|\']:.*(lambda.*).*,.*[\"|\']standardize[\"|\'].*", src)
+                v["transform"] = m.group(1) if m else None
+        lf = self.lossfunction
+        return {
+            "data_type": "GraphDataset",
+            "model_state": {k: t.detach().clone() for k, t in self.model.state_dict().items()},
+            "optimizer": type(self.optimizer).__name__,
+            "optimizer_state": copy.deepcopy(self._optimizer_state()),
+            "lossfunction": (lf if isinstance(lf, type) else type(lf)).__name__,
+            "target": self.target,
+            "target_transform": self.target_transform,
+            "task": self.task,
+            "classes": self.classes,
+            "classes_to_index": self.classes_to_index,
+            "class_weights": self.class_weights,
+            "batch_size_train": self.batch_size_train,
+            "batch_size_test": self.batch_size_test,
+            "val_size": self.val_size,
+            "test_size": self.test_size,
+            "lr": self.lr,
+            "weight_decay": self.weight_decay,
+            "epoch_saved_model": self.epoch_saved_model,
+            "subset": self.subset,
+            "shuffle": self.shuffle,
+            "clustering_method": self.clustering_method,
+            "node_features": self.node_features,
+            "edge_features": self.edge_features,
+            "features": self.features,
+            "features_transform": ft,
+            "means": self.means,
+            "devs": self.devs,
+            "cuda": self.cuda,
+            "ngpu": self.ngpu,
+        }
+
+    def _load_params(self):
+        """trainer.py:873-908 (weights_only load)."""
+        state = torch.load(self.pretrained_model, map_location="cpu", weights_only=True)
+        self.data_type = GraphDataset
+        self.model_load_state_dict = state["model_state"]
+        opt = state["optimizer"]
+        self.optimizer = _OPTIMIZERS[opt] if isinstance(opt, str) else type(opt)
+        self.opt_loaded_state_dict = state["optimizer_state"]
+        lf = state["lossfunction"]
+        self.lossfunction = _LOSSES[lf]() if isinstance(lf, str) else lf
+        for k in ("target", "target_transform", "task", "classes", "classes_to_index", "class_weights", "batch_size_train", "batch_size_test", "val_size", "test_size", "lr", "weight_decay", "epoch_saved_model", "subset", "shuffle", "clustering_method", "node_features", "edge_features", "features", "features_transform", "means", "devs", "cuda", "ngpu"):
+            setattr(self, k, state[k])
+        if torch.cuda.is_available():
+            self.ngpu = max(1, self.ngpu if self.process_group is not None else 1)
+
+    def _load_pretrained_model(self):
+        self.test_loader = DataLoader(self.dataset_test, pin_memory=self.cuda)
+        self._put_model_to_device(self.dataset_test)
+        self.optimizer = self.optimizer(self.model.parameters(), lr=self.lr, weight_decay=self.weight_decay)
+        self.optimizer.load_state_dict(self.opt_loaded_state_dict)
+        self.model.load_state_dict(self.model_load_state_dict)
+
+
+def _gather_rows(local, b, pg):
+    """All ranks' [b_r, out] predictions in global order (contiguous shards)."""
+    world = torch.distributed.get_world_size(pg)
+    sizes = [len(shard_contiguous(np.arange(b), r, world)) for r in range(world)]
+    bufs = [torch.empty(s, local.shape[1], dtype=local.dtype, device=local.device) for s in sizes]
+    torch.distributed.all_gather(bufs, local.contiguous(), group=pg)
+    return torch.cat(bufs)
+
+
+def _divide_dataset(dataset, splitsize=None):
+    """trainer.py:961-1004: random split into (main, split)."""
+    if splitsize is None:
+        splitsize = 0.25
+    full = len(dataset)
+    if isinstance(splitsize, float):
+        n_split = int(splitsize * full)
+    elif isinstance(splitsize, int):
+        n_split = splitsize
+    else:
+        msg = f"type(splitsize) must be float, int or None ({type(splitsize)} detected.)"
+        raise TypeError(msg)
+    if n_split >= full or n_split < 0:
+        msg = f"Invalid Split size: {n_split}.\nSplit size must be a float between 0 and 1 OR an int smaller than the size of the dataset ({full} datapoints)"
+        raise ValueError(msg)
+    if splitsize == 0:
+        return dataset, None
+    idx = np.arange(full)
+    np.random.default_rng().shuffle(idx)
+    return dataset.subset_entries(idx[n_split:]), dataset.subset_entries(idx[:n_split])
