@@ -34,6 +34,7 @@
 
 #include "../../include/deeprank2_amd.h"
 #include "dr_common.h"
+#include "graph_common.h"
 
 namespace {
 
@@ -46,7 +47,6 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 __host__ __device__ inline int r4(int v) { return (v + 3) & ~3; }
 __host__ __device__ inline int r16(int v) { return (v + 15) & ~15; }
-__host__ __device__ inline int imax(int a, int b) { return a > b ? a : b; }
 
 struct Carve {
   int KP, LDW, XS;
@@ -146,16 +146,6 @@ __device__ __forceinline__ void dma_x4(void* lds_dst, const void* gsrc, int n4) 
     if (base + lane < n4) __builtin_amdgcn_global_load_lds(AS1(src + base + lane), AS3(dst + base), 16, 0, 0);
 }
 
-// Row-wise DMA of a [rows, width] global matrix into LDS rows of stride ld.
-__device__ __forceinline__ void dma_rows(float* lds_dst, int ld, const float* gsrc, int rows, int width) {
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  for (int r = wave; r < rows; r += NW)
-    for (int c0 = 0; c0 < width; c0 += 64)
-      if (c0 + lane < width)
-        __builtin_amdgcn_global_load_lds(AS1(gsrc + (int64_t)r * width + c0 + lane), AS3(lds_dst + r * ld + c0), 4, 0,
-                                         0);
-}
-
 __device__ __forceinline__ float4 f4add(float4 a, float4 v) {
   return make_float4(a.x + v.x, a.y + v.y, a.z + v.z, a.w + v.w);
 }
@@ -211,6 +201,257 @@ __device__ __forceinline__ void gather_rows(const int* rp, const uint16_t* col, 
   } while (0)
 #endif
 
+// Everything after the depth-0 pooling (P1 / A1 in LDS): conv2 on the pooled
+// graph, depth-1 pooling, mean, head, loss and the whole backward.  Shared by
+// the single-workgroup kernel and the large-graph tail kernel; zat(i, kk)
+// reads Z = A·X at node i (LDS or the large path's HBM workspace).
+struct TailLds {
+  float *w2, *fc2, *p1, *dp1, *y2, *h2, *d2, *p2, *nt, *dgp;
+  float *g, *hpre, *hh, *hd, *dh, *dg, *dout;
+  int *a1, *p1rp, *p1c, *p1trp, *p1tc, *m1p, *m1i;
+};
+
+template <class C>
+__device__ __forceinline__ TailLds tail_lds(const C& c, float* lds) {
+  TailLds t;
+  t.w2 = lds + c.w2;
+  t.fc2 = lds + c.fc2;
+  t.p1 = lds + c.p1;
+  t.a1 = reinterpret_cast<int*>(lds + c.a1);
+  t.dp1 = lds + c.dp1;
+  t.y2 = lds + c.y2;
+  t.h2 = lds + c.h2;
+  t.d2 = lds + c.d2;
+  t.p1rp = reinterpret_cast<int*>(lds + c.p1rp);
+  t.p1c = reinterpret_cast<int*>(lds + c.p1c);
+  t.p1trp = reinterpret_cast<int*>(lds + c.p1trp);
+  t.p1tc = reinterpret_cast<int*>(lds + c.p1tc);
+  t.m1p = reinterpret_cast<int*>(lds + c.m1p);
+  t.m1i = reinterpret_cast<int*>(lds + c.m1i);
+  t.p2 = lds + c.p2;
+  t.nt = lds + c.nt;
+  t.g = lds + c.head;
+  t.hpre = t.g + 64;
+  t.hh = t.hpre + 128;
+  t.hd = t.hh + 128;
+  t.dh = t.hd + 128;
+  t.dg = t.dh + 128;
+  t.dout = t.dg + 64;
+  t.dgp = lds + c.dgp;
+  return t;
+}
+
+template <class ZAt>
+__device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t, const float (&fc1_row)[8],
+                                           const float (&fc1_col)[8], float fc1_bias, int b, int N, int K0, int K1,
+                                           int F, int OUT, float y_g, uint64_t drop_offset, ZAt zat) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  STAMP(4);
+  // ---------------- conv2 node GEMM on the pooled graph (ginet.py:101,112) --
+  for (int p = tid; p < K0 * 64; p += NT) {
+    const int k = p >> 6, o = p & 63, br = o >> 5;
+    const float* wr = t.w2 + o * 16;  // rows 0..31 = W2, 32..63 = W2e
+    const float* pr = t.p1 + k * 32 + br * 16;
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc = fmaf(pr[j], wr[j], acc);
+    t.y2[p] = acc;
+  }
+  __syncthreads();
+  for (int p = tid; p < K0 * 64; p += NT) {
+    const int k = p >> 6, o = p & 63;
+    float acc = 0.f;
+    for (int e = t.p1rp[k]; e < t.p1rp[k + 1]; ++e) acc += t.y2[t.p1c[e] * 64 + o];
+    t.h2[p] = relu_keepnan(acc);
+  }
+  __syncthreads();
+
+  STAMP(5);
+  // ---------------- depth-1 max_pool_x: scatter_reduce amax (ginet.py:103) --
+  // NaN propagates; remember the tie count for the even-split backward.
+  for (int p = tid; p < K1 * 64; p += NT) {
+    const int m = p >> 6, o = p & 63;
+    const int mb = t.m1p[m], me = t.m1p[m + 1];
+    float mx = t.h2[t.m1i[mb] * 64 + o];
+    for (int q = mb + 1; q < me; ++q) {
+      const float v = t.h2[t.m1i[q] * 64 + o];
+      mx = (mx != mx || v != v) ? __int_as_float(0x7fc00000) : fmaxf(mx, v);
+    }
+    float ties = 0.f;
+    for (int q = mb; q < me; ++q) ties += (t.h2[t.m1i[q] * 64 + o] == mx) ? 1.f : 0.f;
+    t.p2[p] = mx;
+    t.nt[p] = ties;
+  }
+  __syncthreads();
+
+  STAMP(6);
+  // ---------------- per-graph mean (scatter_mean, ginet.py:117-118) ----------
+  if (tid < 64) {
+    float acc = 0.f;
+    for (int m = 0; m < K1; ++m) acc += t.p2[m * 64 + tid];
+    t.g[tid] = acc / (float)K1;
+  }
+  __syncthreads();
+
+  STAMP(7);
+  // ---------------- head: fc1 -> relu -> dropout -> fc2 (ginet.py:120-123) --
+  {
+    const int r = tid >> 3, part = tid & 7;  // 8 lanes per fc1 row
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc = fmaf(t.g[part * 8 + j], fc1_row[j], acc);
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    acc += __shfl_xor(acc, 4, 64);
+    if (part == 0) {
+      acc += fc1_bias;
+      t.hpre[r] = acc;
+      const float hh = relu_keepnan(acc);
+      t.hh[r] = hh;
+      float hd = hh;
+      if (a.p.use_dropout) hd = (keep_unit(a.p, drop_offset, b, r) ? hh : 0.f) * a.p.drop_scale;
+      t.hd[r] = hd;
+    }
+  }
+  __syncthreads();
+  for (int q = wave; q < OUT; q += NW) {
+    const float* wr = t.fc2 + q * 128;
+    float v = fmaf(t.hd[lane], wr[lane], t.hd[lane + 64] * wr[lane + 64]);
+    v = dr_wave_sum(v);
+    if (lane == 0) t.dout[q] = v + t.fc2[OUT * 128 + q];  // logits parked in t.dout
+  }
+  __syncthreads();
+  if ((a.p.flags & DR_PASS_FORWARD) && tid < OUT) a.p.out[(int64_t)b * OUT + tid] = t.dout[tid];
+  if (!(a.p.flags & DR_PASS_BACKWARD)) return;
+  __syncthreads();
+
+  STAMP(8);
+  // ---------------- loss gradient (trainer.py:688-689) ----------------------
+  if (tid == 0) {
+    if (a.p.loss_kind == DR_LOSS_MSE) {
+      const float d = t.dout[0] - y_g;
+      if (a.p.loss_per_graph) a.p.loss_per_graph[b] = d * d;
+      t.dout[0] = 2.f * d * a.p.loss_scale;
+    } else if (a.p.loss_kind == DR_LOSS_CE) {
+      const int yi = (int)y_g;
+      float mx = t.dout[0];
+      for (int q = 1; q < OUT; ++q) mx = fmaxf(mx, t.dout[q]);
+      float se = 0.f;
+      for (int q = 0; q < OUT; ++q) se += expf(t.dout[q] - mx);
+      const float lse = mx + logf(se);
+      const float wy = a.p.class_w ? a.p.class_w[yi] : 1.f;
+      if (a.p.loss_per_graph) a.p.loss_per_graph[b] = wy * (lse - t.dout[yi]);
+      for (int q = 0; q < OUT; ++q) t.dout[q] = wy * (expf(t.dout[q] - lse) - (q == yi ? 1.f : 0.f)) * a.p.loss_scale;
+    } else {
+      for (int q = 0; q < OUT; ++q) t.dout[q] = a.p.dout[(int64_t)b * OUT + q];
+    }
+  }
+  __syncthreads();
+
+  STAMP(9);
+  // ---------------- head backward -------------------------------------------
+  if (tid < 128) {
+    float acc = 0.f;
+    for (int q = 0; q < OUT; ++q) acc = fmaf(t.fc2[q * 128 + tid], t.dout[q], acc);
+    if (a.p.use_dropout) acc = (keep_unit(a.p, drop_offset, b, tid) ? acc : 0.f) * a.p.drop_scale;
+    t.dh[tid] = relu_bwd(t.hh[tid], acc);
+  }
+  __syncthreads();
+  {
+    const int o = tid & 63, rc = tid >> 6;  // 16 chunks of 8 fc1 rows
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc = fmaf(fc1_col[j], t.dh[rc * 8 + j], acc);
+    t.dgp[rc * 64 + o] = acc;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    float acc = 0.f;
+    for (int rc = 0; rc < NW; ++rc) acc += t.dgp[rc * 64 + tid];
+    t.dg[tid] = acc;
+  }
+  {
+    const int HS = DR_HEAD_STRIDE(OUT);
+    float* hg = a.p.head + (int64_t)b * HS;
+    if (tid < 64) hg[tid] = t.g[tid];
+    if (tid < 128) {
+      hg[64 + tid] = t.hd[tid];
+      hg[192 + tid] = t.dh[tid];
+    }
+    if (tid < OUT) hg[320 + tid] = t.dout[tid];
+  }
+  __syncthreads();
+
+  STAMP(10);
+  // ---------------- depth-1 pooling + mean backward -------------------------
+  // scatter_mean: grad/count; scatter_reduce amax: grad split evenly over the
+  // members equal to the max ((src==max) * grad/ties, so NaN stays NaN).
+  for (int p = tid; p < K1 * 64; p += NT) {
+    const int m = p >> 6, o = p & 63;
+    const float gm = (t.dg[o] / (float)K1) / t.nt[p];
+    const float mx = t.p2[p];
+    for (int q = t.m1p[m]; q < t.m1p[m + 1]; ++q) {
+      const int k = t.m1i[q];
+      const float h = t.h2[k * 64 + o];
+      t.d2[k * 64 + o] = relu_bwd(h, (h == mx ? 1.f : 0.f) * gm);
+    }
+  }
+  __syncthreads();
+  STAMP(11);
+  // dY2 = A1^T dS2 (pooled graph, transposed CSR)  -> reuse t.y2
+  for (int p = tid; p < K0 * 64; p += NT) {
+    const int j = p >> 6, o = p & 63;
+    float acc = 0.f;
+    for (int e = t.p1trp[j]; e < t.p1trp[j + 1]; ++e) acc += t.d2[t.p1tc[e] * 64 + o];
+    t.y2[p] = acc;
+  }
+  __syncthreads();
+  STAMP(12);
+  // conv2 weight-gradient partials, and the gradient reaching each depth-0
+  // arg member through relu (v = relu'(H1[arg]) * dP1)
+  {
+    const int SS = DR_SLAB_STRIDE(F);
+    float* slab = a.p.slab + (int64_t)b * SS + 32 * F;
+    for (int p = tid; p < 1024; p += NT) {
+      const int br = p >> 9, o = ((p >> 4) & 31) + br * 32, j = p & 15;
+      float acc = 0.f;
+      for (int k = 0; k < K0; ++k) acc = fmaf(t.y2[k * 64 + o], t.p1[k * 32 + br * 16 + j], acc);
+      slab[p] = acc;
+    }
+  }
+  for (int p = tid; p < K0 * 32; p += NT) {
+    const int k = p >> 5, ch = p & 31, br = ch >> 4, j = ch & 15;
+    const float* wb = t.w2 + br * 512;
+    float acc = 0.f;
+#pragma unroll 8
+    for (int o = 0; o < 32; ++o) acc = fmaf(t.y2[k * 64 + br * 32 + o], wb[o * 16 + j], acc);
+    const int i = t.a1[p];
+    t.dp1[p] = (i < N) ? relu_bwd(t.p1[p], acc) : 0.f;  // P1 = H1[arg] exactly
+  }
+  __syncthreads();
+
+  STAMP(13);
+  // ---------------- dW1cat[c, :] = sum_k v[k, c] * Z[arg(k, c), :] ---------
+  // (dH1 is non-zero only at the depth-0 arg members, so dS1^T (A X) needs
+  // K0 rows of Z per channel instead of a backward gather over all edges.)
+  {
+    const int SS = DR_SLAB_STRIDE(F);
+    float* slab = a.p.slab + (int64_t)b * SS;
+    for (int p = tid; p < 32 * F; p += NT) {
+      const int ch = p / F, kk = p - ch * F;
+      float acc = 0.f;
+      for (int k = 0; k < K0; ++k) {
+        const int i = t.a1[k * 32 + ch];
+        if (i < N) acc = fmaf(t.dp1[k * 32 + ch], zat(i, kk), acc);
+      }
+      slab[p] = acc;
+    }
+  }
+  STAMP(14);
+}
+
 __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x;
@@ -240,26 +481,12 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   int* sm0i = reinterpret_cast<int*>(lds + c.m0i);
   float* sP1 = lds + c.p1;
   int* sA1 = reinterpret_cast<int*>(lds + c.a1);
-  float* sdP1 = lds + c.dp1;
-  float* sY2 = lds + c.y2;
-  float* sH2 = lds + c.h2;
-  float* sD2 = lds + c.d2;
   int* sp1rp = reinterpret_cast<int*>(lds + c.p1rp);
   int* sp1c = reinterpret_cast<int*>(lds + c.p1c);
   int* sp1trp = reinterpret_cast<int*>(lds + c.p1trp);
   int* sp1tc = reinterpret_cast<int*>(lds + c.p1tc);
   int* sm1p = reinterpret_cast<int*>(lds + c.m1p);
   int* sm1i = reinterpret_cast<int*>(lds + c.m1i);
-  float* sP2 = lds + c.p2;
-  float* sNT = lds + c.nt;
-  float* sG = lds + c.head;
-  float* sHpre = sG + 64;
-  float* sHh = sHpre + 128;
-  float* sHd = sHh + 128;
-  float* sDh = sHd + 128;
-  float* sDG = sDh + 128;
-  float* sDout = sDG + 64;
-  float* sDGp = lds + c.dgp;
   float* sRed = lds + c.red;
 
   STAMP(0);
@@ -448,208 +675,291 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   }
   __syncthreads();
 
-  STAMP(4);
-  // ---------------- conv2 node GEMM on the pooled graph (ginet.py:101,112) --
-  for (int p = tid; p < K0 * 64; p += NT) {
-    const int k = p >> 6, o = p & 63, br = o >> 5;
-    const float* wr = sW2 + o * 16;  // rows 0..31 = W2, 32..63 = W2e
-    const float* pr = sP1 + k * 32 + br * 16;
-    float acc = 0.f;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) acc = fmaf(pr[j], wr[j], acc);
-    sY2[p] = acc;
-  }
-  __syncthreads();
-  for (int p = tid; p < K0 * 64; p += NT) {
-    const int k = p >> 6, o = p & 63;
-    float acc = 0.f;
-    for (int e = sp1rp[k]; e < sp1rp[k + 1]; ++e) acc += sY2[sp1c[e] * 64 + o];
-    sH2[p] = relu_keepnan(acc);
-  }
-  __syncthreads();
+  const TailLds t = tail_lds(c, lds);
+  ginet_tail(a, t, fc1_row, fc1_col, fc1_bias, b, N, K0, K1, F, OUT, y_g, drop_offset,
+             [&](int i, int kk) { return sZ[i * LDW + kk]; });
+}
 
-  STAMP(5);
-  // ---------------- depth-1 max_pool_x: scatter_reduce amax (ginet.py:103) --
-  // NaN propagates; remember the tie count for the even-split backward.
-  for (int p = tid; p < K1 * 64; p += NT) {
-    const int m = p >> 6, o = p & 63;
-    const int mb = sm1p[m], me = sm1p[m + 1];
-    float mx = sH2[sm1i[mb] * 64 + o];
-    for (int q = mb + 1; q < me; ++q) {
-      const float v = sH2[sm1i[q] * 64 + o];
-      mx = (mx != mx || v != v) ? __int_as_float(0x7fc00000) : fmaxf(mx, v);
-    }
-    float ties = 0.f;
-    for (int q = mb; q < me; ++q) ties += (sH2[sm1i[q] * 64 + o] == mx) ? 1.f : 0.f;
-    sP2[p] = mx;
-    sNT[p] = ties;
-  }
-  __syncthreads();
 
-  STAMP(6);
-  // ---------------- per-graph mean (scatter_mean, ginet.py:117-118) ----------
-  if (tid < 64) {
-    float acc = 0.f;
-    for (int m = 0; m < K1; ++m) acc += sP2[m * 64 + tid];
-    sG[tid] = acc / (float)K1;
-  }
-  __syncthreads();
+// =========================================================================
+// Graphs larger than one workgroup's LDS (atom-level: N ~ 3e3, E ~ 5e4).
+// =========================================================================
 
-  STAMP(7);
-  // ---------------- head: fc1 -> relu -> dropout -> fc2 (ginet.py:120-123) --
+constexpr int NTA = 512;  // conv1 tile kernel: 8 waves
+constexpr int TR = DR_LARGE_TILE;
+
+struct LargeArgs {
+  GinetArgs g;
+  dr_large_plan plan;
+};
+
+struct ConvCarve {
+  int KP, LDW, XS, w1, z, h, m0i, m0p, rng, total;
+};
+
+__host__ __device__ inline ConvCarve conv_carve(int N, int F, int K0) {
+  ConvCarve c;
+  c.KP = r16(F);
+  c.LDW = c.KP + 2;
+  c.XS = r4(F);
+  int o = 0;
+  c.w1 = o;
+  o += r4(32 * c.LDW);
+  c.z = o;
+  o += r4(TR * c.LDW);
+  c.h = o;
+  o += TR * 32;
+  c.m0i = o;
+  o += r4(N);
+  c.m0p = o;
+  o += r4(K0 + 1);
+  c.rng = o;
+  o += r4(2 * K0);
+  c.total = o;
+  return c;
+}
+
+// first position in the ascending run v[lo, hi) whose value is >= key
+__device__ __forceinline__ int lower_bound_lds(const int* v, int lo, int hi, int key) {
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (v[mid] < key) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// One tile of TR nodes: Z rows (CSR gather over HBM/L2), H = relu(Z W^T) on
+// MFMA, and the tile's partial depth-0 max per (cluster, channel).
+__global__ void __launch_bounds__(NTA) ginet_large_conv1_kernel(LargeArgs la) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const GinetArgs& a = la.g;
+  const dr_large_plan& pl = la.plan;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tile = blockIdx.x;
+  const int b = pl.tile_slot[tile];
+  const int t = tile - pl.tile_first[b];
+  const dr_graph_desc d = a.descs[b];
+  const dr_graph_store& s = a.s;
+  const int g = d.gid;
+  const int64_t n0 = d.node0, ec0 = d.col0, k00 = d.k0;
+  const int N = d.n_nodes, K0 = d.n_k0, F = s.n_feat;
+  const int r0 = t * TR, nrows = min(TR, N - r0);
+  const ConvCarve c = conv_carve(N, F, K0);
+  const int KP = c.KP, LDW = c.LDW, XS = c.XS;
+  float* sW1 = lds + c.w1;
+  float* sZ = lds + c.z;
+  float* sH = lds + c.h;
+  int* sm0i = reinterpret_cast<int*>(lds + c.m0i);
+  int* sm0p = reinterpret_cast<int*>(lds + c.m0p);
+  int* srng = reinterpret_cast<int*>(lds + c.rng);
+
+  drk::dma_words<NTA>(sm0i, s.m0_idx + n0, N);
+  drk::dma_words<NTA>(sm0p, s.m0_ptr + k00 + g, K0 + 1);
+  for (int p = tid; p < 32 * KP; p += NTA) {  // [W1; W1e] zero-padded to KP
+    const int r = p / KP, k = p - r * KP;
+    float v = 0.f;
+    if (k < F) v = (r < 16) ? a.w.w1[r * F + k] : a.w.w1e[(r - 16) * F + k];
+    sW1[r * LDW + k] = v;
+  }
+  for (int p = tid; p < TR * (KP - XS); p += NTA) {  // Z pad columns
+    const int r = p / (KP - XS);
+    sZ[r * LDW + XS + (p - r * (KP - XS))] = 0.f;
+  }
+  // Z = A X for the tile's rows: 8 lanes per row, 16-byte chunks of X rows.
   {
-    const int r = tid >> 3, part = tid & 7;  // 8 lanes per fc1 row
-    float acc = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc = fmaf(sG[part * 8 + j], fc1_row[j], acc);
-    acc += __shfl_xor(acc, 1, 64);
-    acc += __shfl_xor(acc, 2, 64);
-    acc += __shfl_xor(acc, 4, 64);
-    if (part == 0) {
-      acc += fc1_bias;
-      sHpre[r] = acc;
-      const float hh = relu_keepnan(acc);
-      sHh[r] = hh;
-      float hd = hh;
-      if (a.p.use_dropout) hd = (keep_unit(a.p, drop_offset, b, r) ? hh : 0.f) * a.p.drop_scale;
-      sHd[r] = hd;
-    }
-  }
-  __syncthreads();
-  for (int q = wave; q < OUT; q += NW) {
-    const float* wr = sFc2 + q * 128;
-    float v = fmaf(sHd[lane], wr[lane], sHd[lane + 64] * wr[lane + 64]);
-    v = dr_wave_sum(v);
-    if (lane == 0) sDout[q] = v + sFc2[OUT * 128 + q];  // logits parked in sDout
-  }
-  __syncthreads();
-  if ((a.p.flags & DR_PASS_FORWARD) && tid < OUT) a.p.out[(int64_t)b * OUT + tid] = sDout[tid];
-  if (!(a.p.flags & DR_PASS_BACKWARD)) return;
-  __syncthreads();
-
-  STAMP(8);
-  // ---------------- loss gradient (trainer.py:688-689) ----------------------
-  if (tid == 0) {
-    if (a.p.loss_kind == DR_LOSS_MSE) {
-      const float d = sDout[0] - y_g;
-      if (a.p.loss_per_graph) a.p.loss_per_graph[b] = d * d;
-      sDout[0] = 2.f * d * a.p.loss_scale;
-    } else if (a.p.loss_kind == DR_LOSS_CE) {
-      const int yi = (int)y_g;
-      float mx = sDout[0];
-      for (int q = 1; q < OUT; ++q) mx = fmaxf(mx, sDout[q]);
-      float se = 0.f;
-      for (int q = 0; q < OUT; ++q) se += expf(sDout[q] - mx);
-      const float lse = mx + logf(se);
-      const float wy = a.p.class_w ? a.p.class_w[yi] : 1.f;
-      if (a.p.loss_per_graph) a.p.loss_per_graph[b] = wy * (lse - sDout[yi]);
-      for (int q = 0; q < OUT; ++q) sDout[q] = wy * (expf(sDout[q] - lse) - (q == yi ? 1.f : 0.f)) * a.p.loss_scale;
-    } else {
-      for (int q = 0; q < OUT; ++q) sDout[q] = a.p.dout[(int64_t)b * OUT + q];
-    }
-  }
-  __syncthreads();
-
-  STAMP(9);
-  // ---------------- head backward -------------------------------------------
-  if (tid < 128) {
-    float acc = 0.f;
-    for (int q = 0; q < OUT; ++q) acc = fmaf(sFc2[q * 128 + tid], sDout[q], acc);
-    if (a.p.use_dropout) acc = (keep_unit(a.p, drop_offset, b, tid) ? acc : 0.f) * a.p.drop_scale;
-    sDh[tid] = relu_bwd(sHh[tid], acc);
-  }
-  __syncthreads();
-  {
-    const int o = tid & 63, rc = tid >> 6;  // 16 chunks of 8 fc1 rows
-    float acc = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc = fmaf(fc1_col[j], sDh[rc * 8 + j], acc);
-    sDGp[rc * 64 + o] = acc;
-  }
-  __syncthreads();
-  if (tid < 64) {
-    float acc = 0.f;
-    for (int rc = 0; rc < NW; ++rc) acc += sDGp[rc * 64 + tid];
-    sDG[tid] = acc;
-  }
-  {
-    const int HS = DR_HEAD_STRIDE(OUT);
-    float* hg = a.p.head + (int64_t)b * HS;
-    if (tid < 64) hg[tid] = sG[tid];
-    if (tid < 128) {
-      hg[64 + tid] = sHd[tid];
-      hg[192 + tid] = sDh[tid];
-    }
-    if (tid < OUT) hg[320 + tid] = sDout[tid];
-  }
-  __syncthreads();
-
-  STAMP(10);
-  // ---------------- depth-1 pooling + mean backward -------------------------
-  // scatter_mean: grad/count; scatter_reduce amax: grad split evenly over the
-  // members equal to the max ((src==max) * grad/ties, so NaN stays NaN).
-  for (int p = tid; p < K1 * 64; p += NT) {
-    const int m = p >> 6, o = p & 63;
-    const float gm = (sDG[o] / (float)K1) / sNT[p];
-    const float mx = sP2[p];
-    for (int q = sm1p[m]; q < sm1p[m + 1]; ++q) {
-      const int k = sm1i[q];
-      const float h = sH2[k * 64 + o];
-      sD2[k * 64 + o] = relu_bwd(h, (h == mx ? 1.f : 0.f) * gm);
-    }
-  }
-  __syncthreads();
-  STAMP(11);
-  // dY2 = A1^T dS2 (pooled graph, transposed CSR)  -> reuse sY2
-  for (int p = tid; p < K0 * 64; p += NT) {
-    const int j = p >> 6, o = p & 63;
-    float acc = 0.f;
-    for (int e = sp1trp[j]; e < sp1trp[j + 1]; ++e) acc += sD2[sp1tc[e] * 64 + o];
-    sY2[p] = acc;
-  }
-  __syncthreads();
-  STAMP(12);
-  // conv2 weight-gradient partials, and the gradient reaching each depth-0
-  // arg member through relu (v = relu'(H1[arg]) * dP1)
-  {
-    const int SS = DR_SLAB_STRIDE(F);
-    float* slab = a.p.slab + (int64_t)b * SS + 32 * F;
-    for (int p = tid; p < 1024; p += NT) {
-      const int br = p >> 9, o = ((p >> 4) & 31) + br * 32, j = p & 15;
-      float acc = 0.f;
-      for (int k = 0; k < K0; ++k) acc = fmaf(sY2[k * 64 + o], sP1[k * 32 + br * 16 + j], acc);
-      slab[p] = acc;
-    }
-  }
-  for (int p = tid; p < K0 * 32; p += NT) {
-    const int k = p >> 5, ch = p & 31, br = ch >> 4, j = ch & 15;
-    const float* wb = sW2 + br * 512;
-    float acc = 0.f;
-#pragma unroll 8
-    for (int o = 0; o < 32; ++o) acc = fmaf(sY2[k * 64 + br * 32 + o], wb[o * 16 + j], acc);
-    const int i = sA1[p];
-    sdP1[p] = (i < N) ? relu_bwd(sH[i * 32 + ch], acc) : 0.f;
-  }
-  __syncthreads();
-
-  STAMP(13);
-  // ---------------- dW1cat[c, :] = sum_k v[k, c] * Z[arg(k, c), :] ---------
-  // (dH1 is non-zero only at the depth-0 arg members, so dS1^T (A X) needs
-  // K0 rows of Z per channel instead of a backward gather over all edges.)
-  {
-    const int SS = DR_SLAB_STRIDE(F);
-    float* slab = a.p.slab + (int64_t)b * SS;
-    for (int p = tid; p < 32 * F; p += NT) {
-      const int ch = p / F, kk = p - ch * F;
-      float acc = 0.f;
-      for (int k = 0; k < K0; ++k) {
-        const int i = sA1[k * 32 + ch];
-        if (i < N) acc = fmaf(sdP1[k * 32 + ch], sZ[i * LDW + kk], acc);
+    const int* rp = s.rowptr + n0 + g;
+    const uint16_t* col = s.col + ec0;
+    const float* X = s.x + n0 * (int64_t)XS;
+    float* zg = pl.z + (int64_t)pl.z_row0[b] * XS;
+    const int nch = XS >> 2, sub = tid & 7;
+    for (int r = tid >> 3; r < nrows; r += NTA / 8) {
+      const int i = r0 + r;
+      const int eb = rp[i], ee = rp[i + 1];
+      for (int ch = sub; ch < nch; ch += 8) {
+        const int c4 = ch * 4;
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        int e = eb;
+        for (; e + 4 <= ee; e += 4) {
+          const int j0 = col[e], j1 = col[e + 1], j2 = col[e + 2], j3 = col[e + 3];
+          const float4 v0 = *reinterpret_cast<const float4*>(X + (int64_t)j0 * XS + c4);
+          const float4 v1 = *reinterpret_cast<const float4*>(X + (int64_t)j1 * XS + c4);
+          const float4 v2 = *reinterpret_cast<const float4*>(X + (int64_t)j2 * XS + c4);
+          const float4 v3 = *reinterpret_cast<const float4*>(X + (int64_t)j3 * XS + c4);
+          acc = f4add(f4add(f4add(f4add(acc, v0), v1), v2), v3);
+        }
+        for (; e < ee; ++e) acc = f4add(acc, *reinterpret_cast<const float4*>(X + (int64_t)col[e] * XS + c4));
+        float* zr = sZ + r * LDW + c4;
+        zr[0] = acc.x;
+        zr[1] = acc.y;
+        zr[2] = acc.z;
+        zr[3] = acc.w;
+        *reinterpret_cast<float4*>(zg + (int64_t)i * XS + c4) = acc;
       }
-      slab[p] = acc;
     }
   }
-  STAMP(14);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // H = relu(Z [W1; W1e]^T), one 16-row MFMA tile per wave
+  {
+    const int li = lane & 15, kq = lane >> 4;
+    for (int tt = wave; tt * 16 < nrows; tt += NTA / 64) {
+      const int q0 = tt * 16;
+      const int ar = min(q0 + li, nrows - 1);
+      floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < KP; k += 16) {
+        float av[4], b0[4], b1[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int kk = k + 4 * u + kq;
+          av[u] = sZ[ar * LDW + kk];
+          b0[u] = sW1[li * LDW + kk];
+          b1[u] = sW1[(16 + li) * LDW + kk];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], b0[u], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], b1[u], acc1, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = q0 + kq * 4 + r;
+        if (row < nrows) {
+          sH[row * 32 + li] = relu_keepnan(acc0[r]);
+          sH[row * 32 + 16 + li] = relu_keepnan(acc1[r]);
+        }
+      }
+    }
+  }
+  // each cluster's members inside this tile: a sub-run of its ascending list
+  for (int k = tid; k < K0; k += NTA) {
+    const int mb = sm0p[k], me = sm0p[k + 1];
+    srng[2 * k] = lower_bound_lds(sm0i, mb, me, r0);
+    srng[2 * k + 1] = lower_bound_lds(sm0i, mb, me, r0 + nrows);
+  }
+  __syncthreads();
+  // partial scatter_max (strict '>', first max wins, NaN never enters)
+  for (int p = tid; p < K0 * 32; p += NTA) {
+    const int k = p >> 5, ch = p & 31;
+    float best = LOWEST;
+    int arg = N;
+    for (int m = srng[2 * k]; m < srng[2 * k + 1]; ++m) {
+      const int i = sm0i[m];
+      const float v = sH[(i - r0) * 32 + ch];
+      if (v > best) {
+        best = v;
+        arg = i;
+      }
+    }
+    const int64_t o = ((int64_t)tile * pl.k0_max + k) * 32 + ch;
+    pl.part_val[o] = best;
+    pl.part_arg[o] = arg;
+  }
+}
+
+struct TailCarve {
+  int w2, fc2, p1, a1, dp1, y2, h2, d2, p1rp, p1c, p1trp, p1tc, m1p, m1i, p2, nt, head, dgp, total;
+};
+
+__host__ __device__ inline TailCarve tail_carve(int K0, int P1, int K1, int alias, int OUT) {
+  TailCarve c;
+  int o = 0;
+#define TAKE(field, words) \
+  c.field = o;             \
+  o += r4(words);
+  TAKE(w2, 1024)
+  TAKE(fc2, OUT * 128 + OUT)
+  TAKE(p1, K0 * 32)
+  TAKE(a1, K0 * 32)
+  TAKE(dp1, K0 * 32)
+  TAKE(y2, K0 * 64)
+  TAKE(h2, K0 * 64)
+  TAKE(d2, K0 * 64)
+  TAKE(p1rp, K0 + 1)
+  TAKE(p1c, P1)
+  if (alias) {
+    c.p1trp = c.p1rp;
+    c.p1tc = c.p1c;
+  } else {
+    TAKE(p1trp, K0 + 1)
+    TAKE(p1tc, P1)
+  }
+  TAKE(m1p, K1 + 1)
+  TAKE(m1i, K0)
+  TAKE(p2, K1 * 64)
+  TAKE(nt, K1 * 64)
+  TAKE(head, HEADW)
+  TAKE(dgp, NW * 64)
+#undef TAKE
+  c.total = o;
+  return c;
+}
+
+// One workgroup per graph: combine the tiles' partial maxima, then the tail.
+__global__ void __launch_bounds__(NT) ginet_large_tail_kernel(LargeArgs la) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const GinetArgs& a = la.g;
+  const dr_large_plan& pl = la.plan;
+  const int tid = threadIdx.x;
+  const int b = blockIdx.x;
+  const dr_graph_store& s = a.s;
+  const dr_graph_desc d = a.descs[b];
+  const int g = d.gid;
+  const int64_t k00 = d.k0, q0 = d.p1, k10 = d.k1;
+  const int N = d.n_nodes, K0 = d.n_k0, P1 = d.n_p1, K1 = d.n_k1;
+  const int F = s.n_feat, alias = s.transpose_aliased, OUT = a.p.out_dim;
+  const TailCarve c = tail_carve(K0, P1, K1, alias, OUT);
+  const TailLds t = tail_lds(c, lds);
+
+  float fc1_row[8], fc1_col[8], fc1_bias;
+  {
+    const int r = tid >> 3, part = tid & 7;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fc1_row[j] = a.w.fc1w[r * 64 + part * 8 + j];
+    fc1_bias = a.w.fc1b[r];
+    const int o = tid & 63, rc = tid >> 6;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fc1_col[j] = a.w.fc1w[(rc * 8 + j) * 64 + o];
+  }
+  const float y_g = s.y[g];
+  uint64_t drop_offset = a.p.drop_offset;
+  if (a.p.step_counter) {
+    drop_offset = (uint64_t)a.p.step_counter[0];
+    if (b == 0 && tid == 0) a.p.step_counter[1] = (int64_t)drop_offset;
+  }
+  drk::dma_words<NT>(t.p1rp, s.p1_rowptr + k00 + g, K0 + 1);
+  drk::dma_words<NT>(t.p1c, s.p1_col + q0, P1);
+  if (!alias) {
+    drk::dma_words<NT>(t.p1trp, s.p1t_rowptr + k00 + g, K0 + 1);
+    drk::dma_words<NT>(t.p1tc, s.p1t_col + q0, P1);
+  }
+  drk::dma_words<NT>(t.m1p, s.m1_ptr + k10 + g, K1 + 1);
+  drk::dma_words<NT>(t.m1i, s.m1_idx + k00, K0);
+  t.w2[tid] = (tid < 512) ? a.w.w2[tid] : a.w.w2e[tid - 512];
+  for (int p = tid; p < OUT * 129; p += NT) t.fc2[p] = (p < OUT * 128) ? a.w.fc2w[p] : a.w.fc2b[p - OUT * 128];
+  // tiles in node order, strict '>': the first maximum over the whole graph
+  const int tb = pl.tile_first[b], te = pl.tile_first[b + 1];
+  for (int p = tid; p < K0 * 32; p += NT) {
+    float best = LOWEST;
+    int arg = N;
+    for (int tl = tb; tl < te; ++tl) {
+      const int64_t o = ((int64_t)tl * pl.k0_max) * 32 + p;
+      const float v = pl.part_val[o];
+      if (v > best) {
+        best = v;
+        arg = pl.part_arg[o];
+      }
+    }
+    t.p1[p] = (best == LOWEST) ? 0.f : best;
+    t.a1[p] = arg;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const float* z = pl.z + (int64_t)pl.z_row0[b] * r4(F);
+  const int XS = r4(F);
+  ginet_tail(a, t, fc1_row, fc1_col, fc1_bias, b, N, K0, K1, F, OUT, y_g, drop_offset,
+             [&](int i, int kk) { return z[(int64_t)i * XS + kk]; });
 }
 
 }  // namespace
@@ -680,6 +990,46 @@ extern "C" int dr_ginet_graph_pass(const dr_graph_store* store, const dr_graph_d
   args.descs = descs;
   args.B = n_batch;
   hipLaunchKernelGGL(ginet_graph_kernel, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, args);
+  return (int)hipGetLastError();
+}
+
+extern "C" int64_t dr_ginet_large_conv_lds_bytes(int32_t n_nodes, int32_t n_feat, int32_t k0) {
+  return 4LL * conv_carve(n_nodes, n_feat, k0).total;
+}
+
+extern "C" int64_t dr_ginet_tail_lds_bytes(int32_t k0, int32_t p1_edges, int32_t k1, int32_t transpose_aliased,
+                                           int32_t out_dim) {
+  return 4LL * tail_carve(k0, p1_edges, k1, transpose_aliased, out_dim).total;
+}
+
+extern "C" int dr_ginet_large_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                                   const dr_large_plan* plan, const dr_ginet_weights* w, const dr_pass* pass,
+                                   int32_t conv_lds_bytes, int32_t tail_lds_bytes, void* stream) {
+  if (!store || !descs || !w || !pass || !plan || n_batch < 0) return DR_E_ARG;
+  if (pass->out_dim < 1 || pass->out_dim > DR_MAX_OUT) return DR_E_UNSUPPORTED;
+  if (store->n_feat < 1 || store->n_feat > 64) return DR_E_UNSUPPORTED;
+  if (conv_lds_bytes > 160 * 1024 || tail_lds_bytes > 160 * 1024) return DR_E_LDS;
+  if (!plan->tile_first || !plan->z_row0 || !plan->tile_slot || !plan->z || !plan->part_val || !plan->part_arg)
+    return DR_E_ARG;
+  if (plan->n_tiles < n_batch || plan->k0_max < 1 || plan->k0_max > 64) return DR_E_ARG;
+  if ((pass->flags & DR_PASS_BACKWARD) && (!pass->slab || !pass->head)) return DR_E_ARG;
+  if ((pass->flags & DR_PASS_BACKWARD) && pass->loss_kind == DR_LOSS_NONE && !pass->dout) return DR_E_ARG;
+  if ((pass->flags & DR_PASS_FORWARD) && !pass->out) return DR_E_ARG;
+  if (pass->use_dropout == DR_DROPOUT_MASK && !pass->mask) return DR_E_ARG;
+  if (pass->use_dropout < DR_DROPOUT_OFF || pass->use_dropout > DR_DROPOUT_HASH) return DR_E_ARG;
+  if (n_batch == 0) return DR_OK;
+  DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_large_conv1_kernel)));
+  DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_large_tail_kernel)));
+  LargeArgs la;
+  la.g.s = *store;
+  la.g.w = *w;
+  la.g.p = *pass;
+  la.g.descs = descs;
+  la.g.B = n_batch;
+  la.plan = *plan;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(ginet_large_conv1_kernel, dim3(plan->n_tiles), dim3(NTA), conv_lds_bytes, st, la);
+  hipLaunchKernelGGL(ginet_large_tail_kernel, dim3(n_batch), dim3(NT), tail_lds_bytes, st, la);
   return (int)hipGetLastError();
 }
 

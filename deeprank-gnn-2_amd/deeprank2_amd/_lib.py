@@ -72,6 +72,19 @@ class GinetWeightsC(ctypes.Structure):
     _fields_ = [(n, VP) for n in ("w1", "w1e", "w2", "w2e", "fc1w", "fc1b", "fc2w", "fc2b")]
 
 
+class LargePlanC(ctypes.Structure):
+    _fields_ = [
+        ("tile_first", VP),
+        ("z_row0", VP),
+        ("tile_slot", VP),
+        ("n_tiles", ctypes.c_int32),
+        ("k0_max", ctypes.c_int32),
+        ("z", VP),
+        ("part_val", VP),
+        ("part_arg", VP),
+    ]
+
+
 class FoutWeightsC(ctypes.Structure):
     _fields_ = [(n, VP) for n in ("wc1", "wn1", "b1", "wc2", "wn2", "b2", "fc1w", "fc1b", "fc2w", "fc2b")]
 
@@ -137,6 +150,9 @@ class ParamTableC(ctypes.Structure):
 SIGNATURES = [
     ("dr_ginet_graph_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, VP]),
     ("dr_ginet_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 8),
+    ("dr_ginet_large_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(LargePlanC), ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, ctypes.c_int32, VP]),
+    ("dr_ginet_large_conv_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 3),
+    ("dr_ginet_tail_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 5),
     ("dr_fout_graph_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(FoutWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, VP]),
     ("dr_fout_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 8),
     ("dr_reduce_update", ctypes.c_int, [ctypes.POINTER(ParamTableC), VP, VP, ctypes.c_int32, ctypes.POINTER(AdamC), VP, ctypes.c_float, VP, VP]),

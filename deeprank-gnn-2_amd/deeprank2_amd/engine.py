@@ -27,7 +27,7 @@ from __future__ import annotations
 import torch
 
 from deeprank2_amd import _lib
-from deeprank2_amd.fused import BatchHandle, lds_for, param_table
+from deeprank2_amd.fused import BatchHandle, launch, param_table
 
 
 class FusedTrainStep:
@@ -144,8 +144,7 @@ class FusedTrainStep:
         if ev is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        entry = getattr(lib, self.spec.entry)
-        _lib.check(entry(h.store.cstruct(), h.descs.data_ptr(), h.B, self._w, p, lds_for(self.spec, h, self.out_dim), stream), self.spec.entry)
+        launch(self.spec, h, self._w, p)
         if ev is not None:
             e1.record()
             ev.append((e0, e1))

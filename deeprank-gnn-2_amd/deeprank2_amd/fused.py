@@ -33,17 +33,68 @@ class BatchHandle:
         self.B = int(self.gids_host.size)
         self.max_sizes = store.max_sizes(self.gids_host)
         self._lds = {}
+        self.force_large = False  # tests: run the large-graph path on small graphs too
 
     def lds(self, key, fn):
         """Dynamic LDS bytes for the largest graph of the batch (cached per model kind)."""
         v = self._lds.get(key)
         if v is None:
             v = int(fn(*self.max_sizes))
-            if v > 160 * 1024:
-                msg = f"largest graph of the batch needs {v} B of LDS (> 160 KiB): the streamed large-graph path is not built yet"
-                raise RuntimeError(msg)
             self._lds[key] = v
         return v
+
+    def large_plan(self, out_dim):
+        """Tiling + workspaces of the large-graph path (dr_large_plan), built once per batch."""
+        plan = self._lds.get(("large", out_dim))
+        if plan is None:
+            plan = LargePlan(self, out_dim)
+            self._lds[("large", out_dim)] = plan
+        return plan
+
+
+LDS_MAX = 160 * 1024
+
+
+class LargePlan:
+    """Host side of ``dr_large_plan``: tiles of DR_LARGE_TILE nodes per graph,
+    the Z workspace and the per-tile partial pooling buffers."""
+
+    TILE = 128
+
+    def __init__(self, h: BatchHandle, out_dim):
+        st = h.store
+        n, _e, k0, p1, k1 = (a[h.gids_host.astype(np.int64)] for a in st._sizes)  # noqa: SLF001
+        self.k0_max = int(k0.max())
+        if self.k0_max > 64:  # noqa: PLR2004
+            msg = f"a graph of the batch has {self.k0_max} depth-0 clusters (> 64): not supported by the large-graph path"
+            raise RuntimeError(msg)
+        tiles = (n + self.TILE - 1) // self.TILE
+        tile_first = np.concatenate([[0], np.cumsum(tiles)]).astype(np.int32)
+        z_row0 = np.concatenate([[0], np.cumsum(n)]).astype(np.int32)
+        tile_slot = np.repeat(np.arange(h.B, dtype=np.int32), tiles)
+        self.n_tiles = int(tile_first[-1])
+        dev = st.device
+        self.ints = torch.from_numpy(np.concatenate([tile_first, z_row0, tile_slot])).to(dev)
+        self.z = torch.empty(max(1, int(z_row0[-1])) * st.x_stride, dtype=torch.float32, device=dev)
+        self.part_val = torch.empty(self.n_tiles * self.k0_max * 32, dtype=torch.float32, device=dev)
+        self.part_arg = torch.empty(self.n_tiles * self.k0_max * 32, dtype=torch.int32, device=dev)
+        lib = _lib.load()
+        self.conv_lds = int(lib.dr_ginet_large_conv_lds_bytes(int(n.max()), st.n_feat, self.k0_max))
+        self.tail_lds = int(lib.dr_ginet_tail_lds_bytes(self.k0_max, int(p1.max()), int(k1.max()), int(st.packed.transpose_aliased), out_dim))
+        if max(self.conv_lds, self.tail_lds) > LDS_MAX:
+            msg = f"large-graph path needs {max(self.conv_lds, self.tail_lds)} B of LDS (> 160 KiB)"
+            raise RuntimeError(msg)
+        c = _lib.LargePlanC()
+        base = self.ints.data_ptr()
+        c.tile_first = base
+        c.z_row0 = base + 4 * (h.B + 1)
+        c.tile_slot = base + 8 * (h.B + 1)
+        c.n_tiles = self.n_tiles
+        c.k0_max = self.k0_max
+        c.z = self.z.data_ptr()
+        c.part_val = self.part_val.data_ptr()
+        c.part_arg = self.part_arg.data_ptr()
+        self.c = c
 
 
 def resolve_batch(data, device) -> BatchHandle:
@@ -85,6 +136,7 @@ class FusedSpec:
     weights: Callable  # params -> ctypes weights struct
     lds: Callable  # (n, e, k0, p1, k1, F, alias, out) -> bytes
     dropout: float = 0.0
+    large: Callable | None = None  # (handle, weights struct, pass struct) for graphs beyond one workgroup's LDS
 
 
 def make_pass(out_dim, flags, *, dropout: Dropout | None = None, dout=None, loss_kind=_lib.DR_LOSS_NONE, loss_scale=1.0, class_w=None, out=None, loss_per_graph=None, slab=None, head=None, stamps=None, step_counter=None):
@@ -122,13 +174,23 @@ def lds_for(spec: FusedSpec, h: BatchHandle, out_dim):
     return h.lds((spec.entry, out_dim), lambda n, e, k0, p1, k1: spec.lds(n, e, k0, p1, k1, f, alias, out_dim))
 
 
+def launch(spec: FusedSpec, h: BatchHandle, w, p):
+    """One graph pass on the current stream: the single-workgroup kernel when
+    the batch's largest graph fits in LDS, else the model's large-graph path."""
+    lds = lds_for(spec, h, p.out_dim)
+    if lds <= LDS_MAX and not (h.force_large and spec.large is not None):
+        fn = getattr(_lib.load(), spec.entry)
+        _lib.check(fn(h.store.cstruct(), h.descs.data_ptr(), h.B, w, p, lds, _lib.stream_ptr(h.store.device)), spec.entry)
+    elif spec.large is not None:
+        spec.large(h, w, p)
+    else:
+        msg = f"largest graph of the batch needs {lds} B of LDS (> 160 KiB) and {spec.entry} has no large-graph path"
+        raise RuntimeError(msg)
+
+
 def run_pass(spec: FusedSpec, h: BatchHandle, params, p, w=None):
     """Launch the model's graph pass on the current stream."""
-    if w is None:
-        w = spec.weights(params)
-    fn = getattr(_lib.load(), spec.entry)
-    rc = fn(h.store.cstruct(), h.descs.data_ptr(), h.B, w, p, lds_for(spec, h, p.out_dim), _lib.stream_ptr(h.store.device))
-    _lib.check(rc, spec.entry)
+    launch(spec, h, spec.weights(params) if w is None else w, p)
 
 
 def param_table(spec: FusedSpec, params, grads, states, n_feat, out_dim):

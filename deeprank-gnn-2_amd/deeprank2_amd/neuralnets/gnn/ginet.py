@@ -158,7 +158,15 @@ def _lds(n, e, k0, p1, k1, f, alias, out):
     return _lib.load().dr_ginet_lds_bytes(n, e, f, k0, p1, k1, alias, out)
 
 
-SPEC = FusedSpec(PARAM_NAMES, recipe, slab_stride, head_stride, "dr_ginet_graph_pass", weights_c, _lds, dropout=0.4)
+def _large(h, w, p):
+    """Graphs beyond one workgroup's LDS: tile conv1 kernel + per-graph tail (dr_ginet_large_pass)."""
+    plan = h.large_plan(p.out_dim)
+    lib = _lib.load()
+    rc = lib.dr_ginet_large_pass(h.store.cstruct(), h.descs.data_ptr(), h.B, plan.c, w, p, plan.conv_lds, plan.tail_lds, _lib.stream_ptr(h.store.device))
+    _lib.check(rc, "dr_ginet_large_pass")
+
+
+SPEC = FusedSpec(PARAM_NAMES, recipe, slab_stride, head_stride, "dr_ginet_graph_pass", weights_c, _lds, dropout=0.4, large=_large)
 
 
 def graph_pass(h: BatchHandle, params, out_dim, flags, **kw):

@@ -157,6 +157,38 @@ int dr_ginet_graph_pass(const dr_graph_store* store, const dr_graph_desc* descs,
 int64_t dr_ginet_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_feat, int32_t k0,
                            int32_t p1_edges, int32_t k1, int32_t transpose_aliased, int32_t out_dim);
 
+/* ---- GINet on graphs larger than one workgroup's LDS (atom-level graphs) ----
+ * Two launches with the same result as dr_ginet_graph_pass:
+ *   1. one workgroup per tile of DR_LARGE_TILE nodes: Z = A X for its rows
+ *      (CSR gather from HBM/L2), H = relu(Z [W1;W1e]^T) on MFMA, and the
+ *      tile's share of the depth-0 max pool (per cluster & channel: max and
+ *      first arg) -> plan->part_val / part_arg; Z rows -> plan->z;
+ *   2. one workgroup per graph: combine the tile partials in node order
+ *      (first max wins, as torch_scatter), then conv2 ... head, loss and the
+ *      backward exactly as the single-workgroup kernel; dW1 reads Z at the
+ *      pooling args from plan->z.
+ * The plan arrays are per batch (host-built, see deeprank2_amd.fused).      */
+#define DR_LARGE_TILE 128
+typedef struct dr_large_plan {
+  const int32_t* tile_first; /* [B+1] first tile of each batch slot             */
+  const int32_t* z_row0;     /* [B+1] first row of each slot's Z block          */
+  const int32_t* tile_slot;  /* [n_tiles] batch slot of each tile               */
+  int32_t n_tiles;
+  int32_t k0_max;            /* >= every n_k0 of the batch                      */
+  float* z;                  /* [z_row0[B], x_stride] workspace                 */
+  float* part_val;           /* [n_tiles, k0_max, 32] workspace                 */
+  int32_t* part_arg;         /* [n_tiles, k0_max, 32] workspace                 */
+} dr_large_plan;
+
+int dr_ginet_large_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                        const dr_large_plan* plan, const dr_ginet_weights* w, const dr_pass* pass,
+                        int32_t conv_lds_bytes, int32_t tail_lds_bytes, void* stream);
+
+/* Dynamic LDS of the two launches of dr_ginet_large_pass (largest graph).  */
+int64_t dr_ginet_large_conv_lds_bytes(int32_t n_nodes, int32_t n_feat, int32_t k0);
+int64_t dr_ginet_tail_lds_bytes(int32_t k0, int32_t p1_edges, int32_t k1, int32_t transpose_aliased,
+                                int32_t out_dim);
+
 /* ---- FoutNet (deeprank2/neuralnets/gnn/foutnet.py:72-118) ---------------- */
 
 /* FoutNet weights, all row-major as the torch parameters are stored.       */
