@@ -9,6 +9,7 @@
 //   dr_spmm_csr     : out[i] = sum_{e in row i} y[col[e]]       (ginet.py:58)
 //                     or the row mean (foutnet.py:56-58; 0/0 = NaN on empty rows)
 //   dr_linear_*     : fc(x) = x W^T (ginet.py:45) and its two gradients
+//   dr_edge_mlp_scatter[_bwd] : the vanilla edge MLP + scatter_sum (vanilla_gnn.py:29-35)
 //
 // All are HBM/L2-bound gathers; deterministic (no float atomics).
 
@@ -143,6 +144,68 @@ __global__ void dw_sum_kernel(const float* __restrict__ scratch, int64_t plane, 
   }
 }
 
+// Vanilla edge MLP fused into the CSR gather (vanilla_gnn.py:29-35), 32 channels:
+// S[i,c] = sum_{e in row i} relu(A[i,c] + B[col e, c] + Wc[c,:] ea_e + be[c]).
+__device__ __forceinline__ float edge_pre(const float* we, int ld_we, int c, const float* ea, int Fe, float base) {
+  float v = 0.f;
+  for (int f = 0; f < Fe; ++f) v = fmaf(we[c * ld_we + f], ea[f], v);
+  return base + v;
+}
+
+__global__ void edge_mlp_scatter_kernel(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                                        int32_t n_rows, const float* __restrict__ A, const float* __restrict__ B,
+                                        const float* __restrict__ ea, int32_t Fe, const float* __restrict__ wc,
+                                        int32_t ld_we, const float* __restrict__ be, float* __restrict__ S) {
+  const int64_t total = (int64_t)n_rows * 32;
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < total; p += (int64_t)gridDim.x * blockDim.x) {
+    const int i = (int)(p >> 5), c = (int)(p & 31);
+    const float a = A[p], bc = be[c];
+    float acc = 0.f;
+    for (int e = rowptr[i]; e < rowptr[i + 1]; ++e) {
+      const float pre = edge_pre(wc, ld_we, c, ea + (int64_t)e * Fe, Fe, a + B[(int64_t)col[e] * 32 + c]) + bc;
+      acc += (pre <= 0.f) ? 0.f : pre;
+    }
+    S[p] = acc;
+  }
+}
+
+// Its backward given ds = dL/dS: D[i] = sum_{e in row i} relu'(pre_e) ds_i,
+// D'[j] = sum_{e: dst j} relu'(pre_e) ds_src (transposed CSR + slot map),
+// EAP[i, c, f] = sum_{e in row i} relu'(pre_e) ds_i ea_e[f].
+__global__ void edge_mlp_scatter_bwd_kernel(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                                            const int32_t* __restrict__ trowptr, const int32_t* __restrict__ tcol,
+                                            const int32_t* __restrict__ teid, int32_t n_rows,
+                                            const float* __restrict__ A, const float* __restrict__ B,
+                                            const float* __restrict__ ea, int32_t Fe, const float* __restrict__ wc,
+                                            int32_t ld_we, const float* __restrict__ be, const float* __restrict__ DS,
+                                            float* __restrict__ D, float* __restrict__ DP, float* __restrict__ EAP) {
+  const int64_t total = (int64_t)n_rows * 32;
+  const int FeS = Fe > 0 ? Fe : 1;
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < total; p += (int64_t)gridDim.x * blockDim.x) {
+    const int i = (int)(p >> 5), c = (int)(p & 31);
+    const float a = A[p], bi = B[p], bc = be[c], dsi = DS[p];
+    int cnt = 0;
+    float eap[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int e = rowptr[i]; e < rowptr[i + 1]; ++e) {
+      const float* ev = ea + (int64_t)e * Fe;
+      const float pre = edge_pre(wc, ld_we, c, ev, Fe, a + B[(int64_t)col[e] * 32 + c]) + bc;
+      if (!(pre <= 0.f)) {
+        ++cnt;
+        for (int f = 0; f < Fe && f < 8; ++f) eap[f] += ev[f];
+      }
+    }
+    D[p] = cnt ? dsi * (float)cnt : 0.f;
+    for (int f = 0; f < Fe && f < 8; ++f) EAP[p * FeS + f] = cnt ? dsi * eap[f] : 0.f;
+    float acc = 0.f;
+    for (int q = trowptr[i]; q < trowptr[i + 1]; ++q) {
+      const int src = tcol[q], e = teid[q];
+      const float pre = edge_pre(wc, ld_we, c, ea + (int64_t)e * Fe, Fe, A[(int64_t)src * 32 + c] + bi) + bc;
+      if (!(pre <= 0.f)) acc += DS[(int64_t)src * 32 + c];
+    }
+    DP[p] = acc;
+  }
+}
+
 inline int grid_for(int64_t work, int block = 256) {
   int64_t g = (work + block - 1) / block;
   if (g < 1) g = 1;
@@ -202,5 +265,30 @@ extern "C" int dr_linear_dw(const float* dy, const float* x, int32_t m, int32_t 
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(dw_partial_kernel, dim3(grid_for(plane * n_split)), dim3(256), 0, st, dy, x, m, n, k, n_split, scratch);
   hipLaunchKernelGGL(dw_sum_kernel, dim3(grid_for(plane)), dim3(256), 0, st, scratch, plane, n_split, dw);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dr_edge_mlp_scatter(const int32_t* rowptr, const int32_t* col, int32_t n_rows, const float* A,
+                                   const float* B, const float* ea, int32_t n_edge_feat, const float* wc,
+                                   int32_t ld_we, const float* be, float* S, void* stream) {
+  if (!rowptr || !A || !B || !wc || !be || !S || n_rows < 0 || n_edge_feat < 0 || n_edge_feat > 8) return DR_E_ARG;
+  if (n_rows == 0) return DR_OK;
+  hipLaunchKernelGGL(edge_mlp_scatter_kernel, dim3(grid_for((int64_t)n_rows * 32)), dim3(256), 0, (hipStream_t)stream,
+                     rowptr, col, n_rows, A, B, ea, n_edge_feat, wc, ld_we, be, S);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dr_edge_mlp_scatter_bwd(const int32_t* rowptr, const int32_t* col, const int32_t* trowptr,
+                                       const int32_t* tcol, const int32_t* teid, int32_t n_rows, const float* A,
+                                       const float* B, const float* ea, int32_t n_edge_feat, const float* wc,
+                                       int32_t ld_we, const float* be, const float* DS, float* D, float* DP,
+                                       float* EAP, void* stream) {
+  if (!rowptr || !trowptr || !A || !B || !wc || !be || !DS || !D || !DP || !EAP || n_rows < 0 || n_edge_feat < 0 ||
+      n_edge_feat > 8)
+    return DR_E_ARG;
+  if (n_rows == 0) return DR_OK;
+  hipLaunchKernelGGL(edge_mlp_scatter_bwd_kernel, dim3(grid_for((int64_t)n_rows * 32)), dim3(256), 0,
+                     (hipStream_t)stream, rowptr, col, trowptr, tcol, teid, n_rows, A, B, ea, n_edge_feat, wc, ld_we,
+                     be, DS, D, DP, EAP);
   return (int)hipGetLastError();
 }

@@ -65,6 +65,10 @@ class GraphStoreC(ctypes.Structure):
         ("m1_ptr", VP),
         ("m1_idx", VP),
         ("y", VP),
+        ("ea", VP),
+        ("t_eid", VP),
+        ("n_edge_feat", ctypes.c_int32),
+        ("pad0", ctypes.c_int32),
     ]
 
 
@@ -87,6 +91,14 @@ class LargePlanC(ctypes.Structure):
 
 class FoutWeightsC(ctypes.Structure):
     _fields_ = [(n, VP) for n in ("wc1", "wn1", "b1", "wc2", "wn2", "b2", "fc1w", "fc1b", "fc2w", "fc2b")]
+
+
+class VanillaWeightsC(ctypes.Structure):
+    _fields_ = [(n, VP) for n in ("we1", "be1", "wn1", "bn1", "we2", "be2", "wn2", "bn2", "g1w", "g1b", "g2w", "g2b")]
+
+
+class VanillaScratchC(ctypes.Structure):
+    _fields_ = [("base", VP), ("row0", VP), ("n_rows", ctypes.c_int64)]
 
 
 class PassC(ctypes.Structure):
@@ -153,6 +165,9 @@ SIGNATURES = [
     ("dr_ginet_large_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(LargePlanC), ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, ctypes.c_int32, VP]),
     ("dr_ginet_large_conv_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 3),
     ("dr_ginet_tail_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 5),
+    ("dr_vanilla_graph_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(VanillaWeightsC), ctypes.POINTER(PassC), ctypes.POINTER(VanillaScratchC), ctypes.c_int32, VP]),
+    ("dr_vanilla_scratch_floats", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
+    ("dr_vanilla_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 3),
     ("dr_fout_graph_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(FoutWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, VP]),
     ("dr_fout_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 8),
     ("dr_reduce_update", ctypes.c_int, [ctypes.POINTER(ParamTableC), VP, VP, ctypes.c_int32, ctypes.POINTER(AdamC), VP, ctypes.c_float, VP, VP]),
@@ -161,6 +176,8 @@ SIGNATURES = [
     ("dr_linear_xwT", ctypes.c_int, [VP, VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP, VP]),
     ("dr_linear_xw", ctypes.c_int, [VP, VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP, VP]),
     ("dr_linear_dw", ctypes.c_int, [VP, VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP, VP, ctypes.c_int32, VP]),
+    ("dr_edge_mlp_scatter", ctypes.c_int, [VP, VP, ctypes.c_int32, VP, VP, VP, ctypes.c_int32, VP, ctypes.c_int32, VP, VP, VP]),
+    ("dr_edge_mlp_scatter_bwd", ctypes.c_int, [VP, VP, VP, VP, VP, ctypes.c_int32, VP, VP, VP, ctypes.c_int32, VP, ctypes.c_int32, VP, VP, VP, VP, VP, VP]),
     ("dr_dropout_mask", ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int32, ctypes.c_float, VP]),
     ("dr_version", ctypes.c_char_p, []),
     ("dr_device_arch", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32]),

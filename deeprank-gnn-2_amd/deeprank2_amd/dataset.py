@@ -454,7 +454,7 @@ class GraphDataset:
             for fname, mol in self.index_entries:
                 a = self.graph_arrays(fname, mol)
                 recs.append(GraphRecord(x=a["x"], edge_index=a["edge_index"], edge_attr=a["edge_attr"], cluster0=a["cluster0"], cluster1=a["cluster1"], y=a["y"], pos=a["pos"], name=mol))
-            st = GraphStore(pack_graphs(recs), device)
+            st = GraphStore(pack_graphs(recs, require_clusters=False), device)
             self._stores = {key: st}
         return st
 

@@ -43,6 +43,20 @@ class BatchHandle:
             self._lds[key] = v
         return v
 
+    def vanilla_scratch(self, n_feat, n_edge_feat):
+        """Node-level HBM scratch of dr_vanilla_graph_pass for this batch (row0 + buffer)."""
+        key = ("vanilla", n_feat, n_edge_feat)
+        sc = self._lds.get(key)
+        if sc is None:
+            n = self.store._sizes[0][self.gids_host.astype(np.int64)]  # noqa: SLF001
+            row0 = np.concatenate([[0], np.cumsum(n)]).astype(np.int32)
+            rows = int(row0[-1])
+            floats = int(_lib.load().dr_vanilla_scratch_floats(rows, n_feat, n_edge_feat))
+            dev = self.store.device
+            sc = (torch.from_numpy(row0).to(dev), torch.empty(floats, dtype=torch.float32, device=dev), rows)
+            self._lds[key] = sc
+        return sc
+
     def large_plan(self, out_dim):
         """Tiling + workspaces of the large-graph path (dr_large_plan), built once per batch."""
         plan = self._lds.get(("large", out_dim))
@@ -97,19 +111,22 @@ class LargePlan:
         self.c = c
 
 
-def resolve_batch(data, device) -> BatchHandle:
+def resolve_batch(data, device, require_clusters=True) -> BatchHandle:
     """Our DataLoader's batches name their graphs in the dataset's resident
-    store; any other PyG-style batch is packed here (one upload per call)."""
+    store; any other PyG-style batch is packed here (one upload per call).
+    Models that pool (GINet, FoutNet) need the stored clusters, as the
+    reference's get_preloaded_cluster does."""
     h = getattr(data, "_dr_handle", None)
-    if h is not None:
-        return h
-    fn = getattr(data, "dr_handle", None)
-    if callable(fn):
-        h = fn(device)
-        if h is not None:
-            return h
-    store = GraphStore(pack_graphs(records_from_batch(data)), device)
-    return BatchHandle(store, np.arange(store.n_graphs, dtype=np.int32))
+    if h is None:
+        fn = getattr(data, "dr_handle", None)
+        h = fn(device) if callable(fn) else None
+    if h is None:
+        store = GraphStore(pack_graphs(records_from_batch(data), require_clusters=require_clusters), device)
+        h = BatchHandle(store, np.arange(store.n_graphs, dtype=np.int32))
+    if require_clusters and not h.store.packed.has_clusters:
+        msg = "this model pools over the stored clusters: build the dataset with clustering_method set (cluster0/cluster1 are missing)"
+        raise ValueError(msg)
+    return h
 
 
 class Dropout:
@@ -137,6 +154,7 @@ class FusedSpec:
     lds: Callable  # (n, e, k0, p1, k1, F, alias, out) -> bytes
     dropout: float = 0.0
     large: Callable | None = None  # (handle, weights struct, pass struct) for graphs beyond one workgroup's LDS
+    run: Callable | None = None  # (handle, weights struct, pass struct): replaces the default entry call
 
 
 def make_pass(out_dim, flags, *, dropout: Dropout | None = None, dout=None, loss_kind=_lib.DR_LOSS_NONE, loss_scale=1.0, class_w=None, out=None, loss_per_graph=None, slab=None, head=None, stamps=None, step_counter=None):
@@ -177,6 +195,9 @@ def lds_for(spec: FusedSpec, h: BatchHandle, out_dim):
 def launch(spec: FusedSpec, h: BatchHandle, w, p):
     """One graph pass on the current stream: the single-workgroup kernel when
     the batch's largest graph fits in LDS, else the model's large-graph path."""
+    if spec.run is not None:
+        spec.run(h, w, p)
+        return
     lds = lds_for(spec, h, p.out_dim)
     if lds <= LDS_MAX and not (h.force_large and spec.large is not None):
         fn = getattr(_lib.load(), spec.entry)

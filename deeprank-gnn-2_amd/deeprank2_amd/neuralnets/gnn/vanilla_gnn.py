@@ -1,0 +1,166 @@
+"""VanillaConvolutionalLayer and VanillaNetwork on MI355X — drop-in for
+``deeprank2.neuralnets.gnn.vanilla_gnn``.
+
+Same constructor signatures, parameter names/shapes/initialisation order and
+``state_dict`` keys as the reference (``deeprank2/neuralnets/gnn/vanilla_gnn.py:10-65``).
+
+``VanillaNetwork.forward(batch)`` runs ``dr_vanilla_graph_pass``: one HIP
+workgroup per graph runs both layers with the edge MLP fused into the CSR
+gather (the E x 32 messages are never materialised), ``scatter_mean``, the
+graph MLP, the loss and the backward; node-level intermediates sit in a
+per-batch HBM scratch.  ``VanillaConvolutionalLayer.forward`` on an arbitrary
+edge list runs the same arithmetic through the layer-level C entries
+(``dr_edge_mlp_scatter`` / ``_bwd``).  There is no CPU path.
+"""
+
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from deeprank2_amd import _lib, ops
+from deeprank2_amd.fused import BatchHandle, FusedFn, FusedSpec, make_pass, resolve_batch, run_pass
+
+MESSAGE = 32
+
+
+def _r4(v):
+    return (v + 3) & ~3
+
+
+class _VanillaLayerFn(torch.autograd.Function):
+    """x' = relu(Wn [x | s] + bn),  s_i = sum_{e: src i} relu(We [x_i | x_j | ea_e] + be)."""
+
+    @staticmethod
+    def forward(ctx, x, edge_index, ea, we, be, wn, bn):
+        n, f = x.shape
+        fe = ea.shape[1]
+        g = ops.edge_graph(edge_index, n, ea)
+        wa, wb = we[:, :f].contiguous(), we[:, f:2 * f].contiguous()
+        a = ops.linear_xwT(x, wa)
+        b = ops.linear_xwT(x, wb)
+        s = ops.edge_mlp_scatter(g, a, b, we, be, f, fe)
+        u = ops.linear_xwT(torch.cat([x, s], 1), wn) + bn
+        out = torch.relu(u)
+        ctx.save_for_backward(x, we, be, wn, a, b, s, out)
+        ctx.g, ctx.f, ctx.fe = g, f, fe
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, we, be, wn, a, b, s, out = ctx.saved_tensors
+        g, f, fe = ctx.g, ctx.f, ctx.fe
+        du = torch.where(out <= 0, torch.zeros_like(dout), dout).contiguous()
+        dxs = ops.linear_xw(du, wn)  # [dx_direct | ds]
+        ds = dxs[:, f:].contiguous()
+        d, dp, eap = ops.edge_mlp_scatter_bwd(g, a, b, we, be, f, fe, ds)
+        dwa = ops.linear_dw(d, x)
+        dwb = ops.linear_dw(dp, x)
+        dwc = eap.reshape(-1, MESSAGE, max(fe, 1)).sum(0)[:, :fe]
+        dwe = torch.cat([dwa, dwb, dwc], 1)
+        dbe = d.sum(0)
+        dwn = ops.linear_dw(du, torch.cat([x, s], 1))
+        dbn = du.sum(0)
+        dx = dxs[:, :f] + ops.linear_xw(d, we[:, :f].contiguous()) + ops.linear_xw(dp, we[:, f:2 * f].contiguous())
+        return dx, None, None, dwe, dbe, dwn, dbn
+
+
+class VanillaConvolutionalLayer(nn.Module):
+    """vanilla_gnn.py:10-38."""
+
+    def __init__(self, count_node_features, count_edge_features):
+        super().__init__()
+        edge_input_size = 2 * count_node_features + count_edge_features
+        self._edge_mlp = nn.Sequential(nn.Linear(edge_input_size, MESSAGE), nn.ReLU())
+        self._node_mlp = nn.Sequential(nn.Linear(count_node_features + MESSAGE, count_node_features), nn.ReLU())
+
+    def forward(self, node_features, edge_node_indices, edge_features):
+        _lib.require_device(node_features, edge_node_indices, edge_features)
+        ea = edge_features.float().reshape(edge_node_indices.shape[1], -1).contiguous()
+        e, n = self._edge_mlp[0], self._node_mlp[0]
+        return _VanillaLayerFn.apply(node_features.float().contiguous(), edge_node_indices, ea, e.weight, e.bias, n.weight, n.bias)
+
+
+# ---------------------------------------------------------------------------
+# Fused per-graph path (dr_vanilla_graph_pass + dr_reduce_update)
+# ---------------------------------------------------------------------------
+
+PARAM_NAMES = [
+    "_external1._edge_mlp.0.weight", "_external1._edge_mlp.0.bias", "_external1._node_mlp.0.weight", "_external1._node_mlp.0.bias",
+    "_external2._edge_mlp.0.weight", "_external2._edge_mlp.0.bias", "_external2._node_mlp.0.weight", "_external2._node_mlp.0.bias",
+    "_graph_mlp.0.weight", "_graph_mlp.0.bias", "_graph_mlp.2.weight", "_graph_mlp.2.bias",
+]  # fmt: skip
+
+
+def make_spec(f, fe):
+    """The fused spec of a VanillaNetwork(f, out, fe) (partial layouts depend on F and Fe)."""
+    ke, kn = 2 * f + fe, f + MESSAGE
+    layer = 32 * ke + 32 + f * kn + f
+    xs = _r4(f)
+
+    def slab_stride(_f):
+        return 2 * layer
+
+    def head_stride(out):
+        return xs + 256 + _r4(out)
+
+    def recipe(_f, _out):
+        sl = _lib.DR_GRAD_SLAB
+        rec = []
+        for base in (0, layer):
+            rec += [(sl, base, 0, 0), (sl, base + 32 * ke, 0, 0), (sl, base + 32 * ke + 32, 0, 0), (sl, base + 32 * ke + 32 + f * kn, 0, 0)]
+        rec += [(_lib.DR_GRAD_OUTER, xs + 128, 0, f), (_lib.DR_GRAD_HEAD, xs + 128, 0, 0), (_lib.DR_GRAD_OUTER, xs + 256, xs, 128), (_lib.DR_GRAD_HEAD, xs + 256, 0, 0)]
+        return rec
+
+    def weights(params):
+        w = _lib.VanillaWeightsC()
+        (w.we1, w.be1, w.wn1, w.bn1, w.we2, w.be2, w.wn2, w.bn2, w.g1w, w.g1b, w.g2w, w.g2b) = (p.data_ptr() for p in params)
+        return w
+
+    def run(h, w, p):
+        st = h.store
+        if st.n_edge_feat != fe or st.n_feat != f:
+            msg = f"batch has F={st.n_feat}, Fe={st.n_edge_feat}; the model expects F={f}, Fe={fe}"
+            raise ValueError(msg)
+        row0, buf, rows = h.vanilla_scratch(f, fe)
+        sc = _lib.VanillaScratchC()
+        sc.base, sc.row0, sc.n_rows = buf.data_ptr(), row0.data_ptr(), rows
+        lib = _lib.load()
+        lds = int(lib.dr_vanilla_lds_bytes(f, fe, p.out_dim))
+        _lib.check(lib.dr_vanilla_graph_pass(st.cstruct(), h.descs.data_ptr(), h.B, w, p, sc, lds, _lib.stream_ptr(st.device)), "dr_vanilla_graph_pass")
+
+    return FusedSpec(PARAM_NAMES, recipe, slab_stride, head_stride, "dr_vanilla_graph_pass", weights, lambda *_: 0, dropout=0.0, run=run)
+
+
+def graph_pass(model, h: BatchHandle, params, out_dim, flags, **kw):
+    run_pass(model.fused_spec, h, params, make_pass(out_dim, flags, **kw))
+
+
+class VanillaNetwork(nn.Module):
+    """vanilla_gnn.py:41-65 (no clusters needed)."""
+
+    def __init__(self, input_shape: int, output_shape: int, input_shape_edge: int):
+        super().__init__()
+        self._external1 = VanillaConvolutionalLayer(input_shape, input_shape_edge)
+        self._external2 = VanillaConvolutionalLayer(input_shape, input_shape_edge)
+        hidden_size = 128
+        self._graph_mlp = nn.Sequential(nn.Linear(input_shape, hidden_size), nn.ReLU(), nn.Linear(hidden_size, output_shape))
+        self.input_shape = input_shape
+        self.output_shape = output_shape
+        self.input_shape_edge = input_shape_edge
+        self.fused_spec = make_spec(input_shape, input_shape_edge)
+
+    dropout = 0.0
+
+    def ordered_params(self):
+        named = dict(self.named_parameters())
+        return [named[n] for n in PARAM_NAMES]
+
+    def forward(self, data):
+        params = [p.contiguous() for p in self.ordered_params()]
+        dev = params[0].device
+        if dev.type != "cuda":
+            msg = "deeprank2_amd.VanillaNetwork runs on the MI355X only: move the model to a cuda device (no CPU fallback)"
+            raise RuntimeError(msg)
+        h = resolve_batch(data, dev, require_clusters=False)
+        return FusedFn.apply(self.fused_spec, h, None, self.output_shape, *params)

@@ -74,3 +74,41 @@ def linear_dw(dy, x):
     scratch = torch.empty(n_split * n * k, dtype=torch.float32, device=dy.device)
     _lib.check(_lib.load().dr_linear_dw(dy.data_ptr(), x.data_ptr(), m, n, k, dw.data_ptr(), scratch.data_ptr(), n_split, _lib.stream_ptr(dy.device)), "dr_linear_dw")
     return dw
+
+
+class EdgeGraph:
+    """CSR (by edge_index[0]) + transposed CSR + slot map + edge features in CSR order, on the device."""
+
+    def __init__(self, edge_index, n, ea):
+        row, col = edge_index[0], edge_index[1]
+        self.rowptr, perm, self.col = csr_from_coo(row, col, n)
+        self.trowptr, tperm, self.tcol = csr_from_coo(col, row, n)
+        e = perm.numel()
+        inv = torch.empty(max(e, 1), dtype=torch.int32, device=row.device)
+        inv[perm.long()] = torch.arange(e, dtype=torch.int32, device=row.device)
+        self.teid = inv[tperm.long()].contiguous() if e else inv
+        self.ea = ea[perm.long()].contiguous() if e else ea.new_zeros((1, max(ea.shape[1], 1)))
+        self.n = n
+
+
+def edge_graph(edge_index, n, ea):
+    _lib.require_device(edge_index, ea)
+    return EdgeGraph(edge_index, n, ea)
+
+
+def edge_mlp_scatter(g: EdgeGraph, a, b, we, be, f, fe):
+    """S = sum over CSR rows of relu(A_i + B_j + We[:, 2F:] ea_e + be) (32 channels)."""
+    s = torch.empty(g.n, 32, dtype=torch.float32, device=a.device)
+    wc = we[:, 2 * f:]
+    _lib.check(_lib.load().dr_edge_mlp_scatter(g.rowptr.data_ptr(), g.col.data_ptr(), g.n, a.data_ptr(), b.data_ptr(), g.ea.data_ptr(), fe, wc.data_ptr(), we.stride(0), be.data_ptr(), s.data_ptr(), _lib.stream_ptr(a.device)), "dr_edge_mlp_scatter")
+    return s
+
+
+def edge_mlp_scatter_bwd(g: EdgeGraph, a, b, we, be, f, fe, ds):
+    dev = a.device
+    d = torch.empty(g.n, 32, dtype=torch.float32, device=dev)
+    dp = torch.empty_like(d)
+    eap = torch.empty(g.n * 32 * max(fe, 1), dtype=torch.float32, device=dev)
+    wc = we[:, 2 * f:]
+    _lib.check(_lib.load().dr_edge_mlp_scatter_bwd(g.rowptr.data_ptr(), g.col.data_ptr(), g.trowptr.data_ptr(), g.tcol.data_ptr(), g.teid.data_ptr(), g.n, a.data_ptr(), b.data_ptr(), g.ea.data_ptr(), fe, wc.data_ptr(), we.stride(0), be.data_ptr(), ds.data_ptr(), d.data_ptr(), dp.data_ptr(), eap.data_ptr(), _lib.stream_ptr(dev)), "dr_edge_mlp_scatter_bwd")
+    return d, dp, eap

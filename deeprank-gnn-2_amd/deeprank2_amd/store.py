@@ -55,6 +55,7 @@ class PackedGraphs:
     eperm: np.ndarray  # CSR slot -> original edge position within the graph
     t_rowptr: np.ndarray
     t_col: np.ndarray
+    t_eid: np.ndarray  # transposed CSR slot -> CSR slot of the same edge (local)
     transpose_aliased: bool
     k0_off: np.ndarray
     m0_ptr: np.ndarray
@@ -72,6 +73,7 @@ class PackedGraphs:
     y: np.ndarray
     edge_attr: np.ndarray | None  # [E_all, Fe] in CSR order
     names: list = field(default_factory=list)
+    has_clusters: bool = True  # False: cluster0/1 were missing and filled with one cluster per graph
 
     # per-graph sizes (host side, for launch geometry)
     def sizes(self):
@@ -112,7 +114,7 @@ def pack_graphs(records: list[GraphRecord], require_clusters: bool = True) -> Pa
         msg = "empty graph list"
         raise ValueError(msg)
     F = int(records[0].x.shape[1])
-    xs, rps, cols, eperms, trps, tcols = [], [], [], [], [], []
+    xs, rps, cols, eperms, trps, tcols, teids = [], [], [], [], [], [], []
     m0ps, m0is, cl0s, p1rps, p1cs, p1trps, p1tcs, m1ps, m1is, cl1s, ys, eas = ([] for _ in range(12))
     node_off = [0]
     edge_off = [0]
@@ -120,6 +122,7 @@ def pack_graphs(records: list[GraphRecord], require_clusters: bool = True) -> Pa
     p1_off = [0]
     k1_off = [0]
     aliased = True
+    has_clusters = True
     has_ea = records[0].edge_attr is not None
     for gi, r in enumerate(records):
         x = np.ascontiguousarray(r.x, dtype=np.float32)
@@ -137,7 +140,10 @@ def pack_graphs(records: list[GraphRecord], require_clusters: bool = True) -> Pa
             raise ValueError(msg)
         row, col = ei[0], ei[1]
         rp, cs, perm = _csr(row, col, n)
-        trp, tcs, _ = _csr(col, row, n)
+        trp, tcs, tperm = _csr(col, row, n)
+        inv = np.empty(e, dtype=np.int32)
+        inv[perm] = np.arange(e, dtype=np.int32)
+        teids.append(inv[tperm])
         sym = _same_multiset(row, col, col, row, n)
         aliased &= sym
         xs.append(x)
@@ -156,6 +162,7 @@ def pack_graphs(records: list[GraphRecord], require_clusters: bool = True) -> Pa
                 raise ValueError(msg)
             c0 = np.zeros(n, dtype=np.int64)
             c1 = np.zeros(1, dtype=np.int64)
+            has_clusters = False
         else:
             c0, c1 = r.cluster0, r.cluster1
         if len(c0) != n:
@@ -214,6 +221,7 @@ def pack_graphs(records: list[GraphRecord], require_clusters: bool = True) -> Pa
         eperm=cat(eperms),
         t_rowptr=cat(trps),
         t_col=cat(tcols),
+        t_eid=cat(teids),
         transpose_aliased=bool(aliased),
         k0_off=np.asarray(k0_off, np.int64),
         m0_ptr=cat(m0ps),
@@ -231,6 +239,7 @@ def pack_graphs(records: list[GraphRecord], require_clusters: bool = True) -> Pa
         y=np.asarray(ys, dtype=np.float32),
         edge_attr=cat(eas) if has_ea else None,
         names=[r.name for r in records],
+        has_clusters=has_clusters,
     )
 
 
@@ -327,10 +336,17 @@ class GraphStore:
 
         self.rowptr = t(p.rowptr)
         self.col = t(spread(p.col))
-        if p.transpose_aliased:
-            self.t_rowptr, self.t_col = self.rowptr, self.col
-        else:
-            self.t_rowptr, self.t_col = t(p.t_rowptr), t(spread(p.t_col))
+        # level-0 transpose in true edge order (by edge_index[1], stable), with
+        # t_eid mapping each transposed slot to the CSR slot of the same edge
+        self.t_rowptr, self.t_col = t(p.t_rowptr), t(spread(p.t_col))
+        teid = np.zeros(max(int(col_off[-1]), 8), dtype=np.int32)
+        teid[slot] = p.t_eid
+        self.t_eid = t(teid)
+        self.n_edge_feat = 0 if p.edge_attr is None else int(p.edge_attr.shape[1])
+        ea = np.zeros((max(int(col_off[-1]), 8), max(self.n_edge_feat, 1)), dtype=np.float32)
+        if self.n_edge_feat:
+            ea[slot] = p.edge_attr
+        self.ea = t(ea)
         self.k0_off = t(p.k0_off)
         self.m0_ptr = t(p.m0_ptr)
         self.m0_idx = t(p.m0_idx)
@@ -374,8 +390,9 @@ class GraphStore:
             s.n_feat = self.n_feat
             s.x_stride = self.x_stride
             s.transpose_aliased = int(self.packed.transpose_aliased)
-            for name in ("x", "node_off", "edge_off", "col_off", "rowptr", "col", "t_rowptr", "t_col", "k0_off", "m0_ptr", "m0_idx", "p1_off", "p1_rowptr", "p1_col", "p1t_rowptr", "p1t_col", "k1_off", "m1_ptr", "m1_idx", "y"):
+            for name in ("x", "node_off", "edge_off", "col_off", "rowptr", "col", "t_rowptr", "t_col", "k0_off", "m0_ptr", "m0_idx", "p1_off", "p1_rowptr", "p1_col", "p1t_rowptr", "p1t_col", "k1_off", "m1_ptr", "m1_idx", "y", "ea", "t_eid"):
                 setattr(s, name, getattr(self, name).data_ptr())
+            s.n_edge_feat = self.n_edge_feat
             self._c = s
         return self._c
 

@@ -30,6 +30,10 @@
  *   dr_linear_xwT / dr_linear_xw / dr_linear_dw
  *                           the node-side nn.Linear(bias=False) of
  *                           GINetConvLayer.fc (ginet.py:45) and its backward
+ *   dr_vanilla_graph_pass   VanillaNetwork.forward + autograd backward
+ *                           (deeprank2/neuralnets/gnn/vanilla_gnn.py:26-65)
+ *   dr_edge_mlp_scatter[_bwd]  VanillaConvolutionalLayer edge MLP + scatter_sum
+ *                           (vanilla_gnn.py:29-35) on any edge list
  *   dr_csr_from_coo         the ordering torch_scatter's CPU scatter_add_
  *                           implies for edge_index[0] (ginet.py:41,58): a stable
  *                           row-sorted CSR, built on the device
@@ -59,14 +63,14 @@ typedef struct dr_graph_store {
   int32_t n_graphs;          /* G                                             */
   int32_t n_feat;            /* F                                             */
   int32_t x_stride;          /* row stride of x in floats: multiple of 4, >= F, pad columns zero */
-  int32_t transpose_aliased; /* 1: t_* / p1t_* arrays are the CSR arrays (symmetric graphs) */
+  int32_t transpose_aliased; /* 1: p1t_* arrays are the p1_* arrays (symmetric pooled graphs) */
   const float* x;            /* [N_all, x_stride] fp32 (16-byte aligned rows) */
   const int64_t* node_off;   /* [G+1]                                         */
   const int64_t* edge_off;   /* [G+1] directed edges per graph (edge_attr rows, CSR order) */
   const int64_t* col_off;    /* [G+1] 16-byte aligned start of each graph's col / t_col block */
   const int32_t* rowptr;     /* [N_all+G] local CSR row pointers (g at node_off[g]+g) */
   const uint16_t* col;       /* local gathered node (edge_index[1]), graph g at col_off[g] */
-  const int32_t* t_rowptr;   /* transpose CSR (by edge_index[1])              */
+  const int32_t* t_rowptr;   /* transpose CSR (by edge_index[1], stable: original edge order) */
   const uint16_t* t_col;
   const int64_t* k0_off;     /* [G+1] depth-0 clusters per graph              */
   const int32_t* m0_ptr;     /* [K0_all+G] members of each depth-0 cluster    */
@@ -80,6 +84,10 @@ typedef struct dr_graph_store {
   const int32_t* m1_ptr;     /* [K1_all+G]                                    */
   const int32_t* m1_idx;     /* [K0_all] local depth-0 ids, ascending          */
   const float* y;            /* [G] target (class index as float for classif) */
+  const float* ea;           /* edge_attr in CSR slot order: graph g's slot e at row col_off[g]+e, [*, max(Fe,1)] */
+  const int32_t* t_eid;      /* t_col slot -> CSR slot of the same edge (local), at col_off[g]+slot */
+  int32_t n_edge_feat;       /* Fe                                            */
+  int32_t pad0;
 } dr_graph_store;
 
 /* One mini-batch slot: where graph `gid` lives in the store (64 bytes, so a
@@ -224,6 +232,41 @@ int dr_fout_graph_pass(const dr_graph_store* store, const dr_graph_desc* descs, 
 int64_t dr_fout_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_feat, int32_t k0, int32_t p1_edges,
                           int32_t k1, int32_t transpose_aliased, int32_t out_dim);
 
+/* ---- VanillaNetwork (deeprank2/neuralnets/gnn/vanilla_gnn.py:10-65) ------- */
+
+typedef struct dr_vanilla_weights {
+  const float *we1, *be1; /* _external1._edge_mlp.0 weight [32, 2F+Fe], bias [32] */
+  const float *wn1, *bn1; /* _external1._node_mlp.0 weight [F, F+32],  bias [F]  */
+  const float *we2, *be2; /* _external2 ...                                        */
+  const float *wn2, *bn2;
+  const float *g1w, *g1b; /* _graph_mlp.0 weight [128, F], bias [128]             */
+  const float *g2w, *g2b; /* _graph_mlp.2 weight [out, 128], bias [out]           */
+} dr_vanilla_weights;
+
+/* Per-batch HBM scratch for the node-level intermediates (no per-edge storage):
+ * base: dr_vanilla_scratch_floats(n_rows, F, Fe) floats; row0[b]: first row of
+ * batch slot b (row0[B] = n_rows = total nodes of the batch).                */
+typedef struct dr_vanilla_scratch {
+  float* base;
+  const int32_t* row0;
+  int64_t n_rows;
+} dr_vanilla_scratch;
+
+/* slab: per layer [dWe (32 x (2F+Fe)) | dbe (32) | dWn (F x (F+32)) | dbn (F)], layer 1 then 2
+ * head: g [r4(F)] | relu(fc1) [128] | its grad [128] | dout [out]               */
+#define DR_VANILLA_SLAB_STRIDE(F, Fe) (2 * (32 * (2 * (F) + (Fe)) + 32 + (F) * ((F) + 32) + (F)))
+#define DR_VANILLA_HEAD_STRIDE(F, out) ((((F) + 3) & ~3) + 256 + (((out) + 3) & ~3))
+
+/* One workgroup per graph: both VanillaConvolutionalLayers (edge MLP fused
+ * into the CSR gather, scatter_sum, node MLP), scatter_mean, the graph MLP,
+ * the loss and the whole backward.  Same dr_pass contract as the other
+ * graph passes (no dropout).  Fe <= 8, F <= 64.                              */
+int dr_vanilla_graph_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                          const dr_vanilla_weights* w, const dr_pass* pass, const dr_vanilla_scratch* scratch,
+                          int32_t lds_bytes, void* stream);
+int64_t dr_vanilla_scratch_floats(int64_t n_rows, int32_t n_feat, int32_t n_edge_feat);
+int64_t dr_vanilla_lds_bytes(int32_t n_feat, int32_t n_edge_feat, int32_t out_dim);
+
 /* Adam (torch.optim.Adam, L2 weight decay added to the gradient) settings.  */
 typedef struct dr_adam {
   float lr, beta1, beta2, eps, weight_decay;
@@ -293,6 +336,22 @@ int dr_linear_xw(const float* dy, const float* w, int32_t m, int32_t n, int32_t 
 /* dw[N,K] = dy[M,N]^T x[M,K]  (deterministic split over M into scratch[n_split,N,K]) */
 int dr_linear_dw(const float* dy, const float* x, int32_t m, int32_t n, int32_t k, float* dw,
                  float* scratch, int32_t n_split, void* stream);
+
+/* VanillaConvolutionalLayer edge side (vanilla_gnn.py:29-35) on a CSR (int32,
+ * by edge_index[0]), 32 message channels, A/B = X Wa^T / X Wb^T [n_rows, 32],
+ * ea [E, Fe] in CSR slot order, wc = the edge-feature columns of the edge
+ * MLP weight (row stride ld_we), be its bias:
+ *   S[i,c] = sum_{e in row i} relu(A[i,c] + B[col e,c] + wc[c,:] ea_e + be[c]).  */
+int dr_edge_mlp_scatter(const int32_t* rowptr, const int32_t* col, int32_t n_rows, const float* A, const float* B,
+                        const float* ea, int32_t n_edge_feat, const float* wc, int32_t ld_we, const float* be,
+                        float* S, void* stream);
+/* Backward given DS = dL/dS: D (row sums of dpre), DP (dst sums of dpre, via
+ * the transposed CSR trowptr/tcol and teid = transposed slot -> CSR slot) and
+ * EAP [n_rows, 32, Fe] (per-row sums of dpre (x) ea).  Fe <= 8.               */
+int dr_edge_mlp_scatter_bwd(const int32_t* rowptr, const int32_t* col, const int32_t* trowptr, const int32_t* tcol,
+                            const int32_t* teid, int32_t n_rows, const float* A, const float* B, const float* ea,
+                            int32_t n_edge_feat, const float* wc, int32_t ld_we, const float* be, const float* DS,
+                            float* D, float* DP, float* EAP, void* stream);
 
 /* Host-side replica of the in-kernel dropout RNG (DR_DROPOUT_HASH): writes
  * keep[i] for i in [0, n) (i = 128*b + r) into a host buffer.             */

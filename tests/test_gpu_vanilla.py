@@ -1,0 +1,138 @@
+"""GPU parity of the MI355X VanillaNetwork path (dr_vanilla_graph_pass, the
+layer-level dr_edge_mlp_scatter entries) against the reference golden and the
+CPU oracle.  Tolerance: 1e-4 (north_star, fp32)."""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+from _util import assert_grad_close, golden_batch, golden_grads, golden_state_dict
+
+from deeprank2_amd.engine import FusedTrainStep
+from deeprank2_amd.fused import BatchHandle
+from deeprank2_amd.neuralnets.gnn import vanilla_gnn as amd
+from deeprank2_amd.store import GraphStore, pack_graphs, records_from_batch
+from deeprank2_amd.utils.synthetic import make_dataset
+from oracle import data_ref, gnn_ref
+from oracle import pyg_ops as P
+
+pytestmark = pytest.mark.gpu
+TOL = dict(rtol=1e-4, atol=1e-4)
+DEV = "cuda:0"
+
+
+def _datas(n, seed, **kw):
+    return [data_ref.synthetic_to_data(g, f"v{i}") for i, g in enumerate(make_dataset(n, seed=seed, **kw))]
+
+
+def _pair(f, out, fe, seed):
+    torch.manual_seed(seed)
+    mo = gnn_ref.VanillaNetwork(f, out, fe)
+    m = amd.VanillaNetwork(f, out, fe)
+    m.load_state_dict(mo.state_dict())
+    return mo, m.to(DEV)
+
+
+def test_vanilla_module_vs_reference_golden(golden):
+    z = golden("vanilla_synth")
+    m = amd.VanillaNetwork(30, 1, 3)
+    m.load_state_dict(golden_state_dict(z))
+    m = m.to(DEV).eval()
+    with torch.no_grad():
+        out = m(golden_batch(z)).cpu().numpy()
+    np.testing.assert_allclose(out, z["out/eval"], **TOL)
+    m.train()
+    out = m(golden_batch(z))
+    loss = torch.nn.functional.mse_loss(out.reshape(-1), torch.from_numpy(z["in/y"]).to(DEV))
+    loss.backward()
+    np.testing.assert_allclose(out.detach().cpu().numpy(), z["out/train"], **TOL)
+    assert float(loss.detach()) == pytest.approx(float(z["loss"]), rel=1e-4)
+    ref = golden_grads(z)
+    for n, p in m.named_parameters():
+        assert_grad_close(p.grad.cpu().numpy(), ref[n], err_msg=n)
+
+
+def test_vanilla_layer_arbitrary_edges_vs_oracle():
+    gen = torch.Generator().manual_seed(7)
+    x = torch.randn(45, 12, generator=gen)
+    ei = torch.randint(0, 45, (2, 300), generator=gen)
+    ei = ei[:, (ei[0] != 5) & (ei[1] != 5)]  # an isolated node
+    ei = torch.cat([ei, torch.tensor([[3, 3, 3, 9], [3, 3, 4, 9]])], 1)  # self loops, duplicates
+    ea = torch.randn(ei.shape[1], 2, generator=gen)
+    torch.manual_seed(3)
+    lo = gnn_ref.VanillaConvolutionalLayer(12, 2)
+    la = amd.VanillaConvolutionalLayer(12, 2)
+    la.load_state_dict(lo.state_dict())
+    la = la.to(DEV)
+    xo = x.clone().requires_grad_(True)
+    xa = x.to(DEV).requires_grad_(True)
+    zo = lo(xo, ei, ea)
+    za = la(xa, ei.to(DEV), ea.to(DEV))
+    gz = torch.randn(zo.shape, generator=gen)
+    (zo * gz).sum().backward()
+    (za * gz.to(DEV)).sum().backward()
+    np.testing.assert_allclose(za.detach().cpu().numpy(), zo.detach().numpy(), **TOL)
+    np.testing.assert_allclose(xa.grad.cpu().numpy(), xo.grad.numpy(), **TOL)
+    ref = dict(lo.named_parameters())
+    for n, p in la.named_parameters():
+        assert_grad_close(p.grad.cpu().numpy(), ref[n].grad.numpy(), err_msg=n)
+
+
+def test_vanilla_fused_train_step_vs_oracle():
+    datas = _datas(16, seed=41, n_lo=30, n_hi=80, mean_degree=10.0)
+    mo, m = _pair(30, 1, 3, seed=12)
+    bat = P.Batch.from_data_list([d.clone() for d in datas])
+    out_o = mo(bat)
+    loss_o = torch.nn.functional.mse_loss(out_o.reshape(-1), bat.y)
+    loss_o.backward()
+    store = GraphStore(pack_graphs(records_from_batch(P.Batch.from_data_list(datas))), DEV)
+    step = FusedTrainStep(m.train())
+    before = [p.detach().clone() for p in step.params]
+    loss, out = step.step(BatchHandle(store, np.arange(16)))
+    np.testing.assert_allclose(out.cpu().numpy(), out_o.detach().numpy(), **TOL)
+    assert float(loss) == pytest.approx(float(loss_o.detach()), rel=1e-4)
+    grads = dict(zip(amd.PARAM_NAMES, step.grads))
+    for n, p in mo.named_parameters():
+        assert_grad_close(grads[n].cpu().numpy(), p.grad.numpy(), err_msg=n)
+    ref = [torch.nn.Parameter(b) for b in before]
+    for r, g in zip(ref, step.grads):
+        r.grad = g.detach().clone()
+    torch.optim.Adam(ref, lr=1e-3, weight_decay=1e-5).step()
+    for n, r, p in zip(amd.PARAM_NAMES, ref, step.params):
+        np.testing.assert_allclose(p.detach().cpu().numpy(), r.detach().cpu().numpy(), rtol=1e-5, atol=1e-7, err_msg=n)
+
+
+def test_vanilla_classification_and_atom_graph_vs_oracle():
+    datas = _datas(2, seed=43, n_lo=2500, n_hi=3000, mean_degree=16.0) + _datas(3, seed=44, n_lo=20, n_hi=40)
+    for d in datas:
+        d.cluster0 = d.cluster1 = None  # VanillaNetwork needs no clusters
+    mo, m = _pair(30, 3, 3, seed=13)
+    y = torch.tensor([0, 2, 1, 1, 0])
+    out_o = mo(P.Batch.from_data_list([d.clone() for d in datas]))
+    torch.nn.functional.cross_entropy(out_o, y).backward()
+    out = m(P.Batch.from_data_list(datas))
+    torch.nn.functional.cross_entropy(out, y.to(DEV)).backward()
+    np.testing.assert_allclose(out.detach().cpu().numpy(), out_o.detach().numpy(), **TOL)
+    ref = dict(mo.named_parameters())
+    for n, p in m.named_parameters():
+        assert_grad_close(p.grad.cpu().numpy(), ref[n].grad.numpy(), err_msg=n)
+
+
+def test_vanilla_captured_replay_matches_eager():
+    datas = _datas(24, seed=45, n_lo=30, n_hi=60)
+    store = GraphStore(pack_graphs(records_from_batch(P.Batch.from_data_list(datas))), DEV)
+    hs = [BatchHandle(store, np.arange(12)), BatchHandle(store, np.arange(12, 24))]
+    torch.manual_seed(4)
+    m1 = amd.VanillaNetwork(30, 1, 3).to(DEV)
+    m2 = amd.VanillaNetwork(30, 1, 3).to(DEV)
+    m2.load_state_dict(m1.state_dict())
+    s1, s2 = FusedTrainStep(m1), FusedTrainStep(m2)
+    graphs = [s2.capture(h) for h in hs]
+    for i in range(4):
+        l1, _ = s1.step(hs[i % 2])
+        graphs[i % 2].replay()
+        torch.cuda.synchronize()
+        assert torch.equal(l1, s2.loss_out), i
+    for a, b in zip(s1.params, s2.params):
+        assert torch.equal(a, b)
