@@ -206,6 +206,85 @@ __global__ void edge_mlp_scatter_bwd_kernel(const int32_t* __restrict__ rowptr, 
   }
 }
 
+// Segment max over member lists (segptr/members: CSR of a cluster vector,
+// members ascending within a segment).
+//   mode 0 = torch_scatter.scatter_max (community_pooling.py:209): strict '>'
+//            from the lowest float, first max wins, NaN never enters, empty
+//            segment -> 0 with arg = n_rows;
+//   mode 1 = scatter_reduce('amax', include_self=False) as PyG's max_pool_x
+//            (ginet.py:103): NaN propagates, empty -> 0; arg = first max.
+__global__ void segment_max_kernel(const int32_t* __restrict__ segptr, const int32_t* __restrict__ members,
+                                   const float* __restrict__ x, int32_t n_seg, int32_t C, int32_t n_rows,
+                                   int32_t mode, float* __restrict__ out, int32_t* __restrict__ arg) {
+  const int64_t total = (int64_t)n_seg * C;
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < total; p += (int64_t)gridDim.x * blockDim.x) {
+    const int k = (int)(p / C), c = (int)(p - (int64_t)k * C);
+    const int mb = segptr[k], me = segptr[k + 1];
+    float best = -3.402823466e+38f, amax = -__builtin_inff();
+    int a = n_rows;
+    bool nan = false;
+    for (int m = mb; m < me; ++m) {
+      const int i = members[m];
+      const float v = x[(int64_t)i * C + c];
+      nan |= (v != v);
+      amax = fmaxf(amax, v);
+      if (v > best) {  // false for NaN: scatter_max never takes it
+        best = v;
+        a = i;
+      }
+    }
+    float r;
+    if (mode == 0) r = (a == n_rows) ? 0.f : best;
+    else r = (me == mb) ? 0.f : (nan ? __int_as_float(0x7fc00000) : amax);
+    out[p] = r;
+    if (arg) arg[p] = a;
+  }
+}
+
+// Backward: mode 0 routes dout to the arg member; mode 1 splits it evenly
+// over the members equal to the max ((x == max) * dout / ties).
+__global__ void segment_max_bwd_kernel(const int32_t* __restrict__ segptr, const int32_t* __restrict__ members,
+                                       const float* __restrict__ x, const float* __restrict__ out,
+                                       const int32_t* __restrict__ arg, const float* __restrict__ dout,
+                                       int32_t n_seg, int32_t C, int32_t n_rows, int32_t mode,
+                                       float* __restrict__ dx) {
+  const int64_t total = (int64_t)n_seg * C;
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < total; p += (int64_t)gridDim.x * blockDim.x) {
+    const int k = (int)(p / C), c = (int)(p - (int64_t)k * C);
+    const int mb = segptr[k], me = segptr[k + 1];
+    if (mode == 0) {
+      for (int m = mb; m < me; ++m) dx[(int64_t)members[m] * C + c] = 0.f;
+      const int a = arg[p];
+      if (a < n_rows) dx[(int64_t)a * C + c] = dout[p];
+    } else {
+      const float mx = out[p];
+      // torch's scatter_reduce amax backward counts the zero-initialised
+      // output as one more tie when the max is +-0, even with include_self=False
+      float ties = (mx == 0.f) ? 1.f : 0.f;
+      for (int m = mb; m < me; ++m) ties += (x[(int64_t)members[m] * C + c] == mx) ? 1.f : 0.f;
+      const float gsh = dout[p] / ties;
+      for (int m = mb; m < me; ++m) {
+        const int64_t q = (int64_t)members[m] * C + c;
+        dx[q] = (x[q] == mx ? 1.f : 0.f) * gsh;
+      }
+    }
+  }
+}
+
+// Segment mean (torch_scatter.scatter_mean: count clamped to 1), in member order.
+__global__ void segment_mean_kernel(const int32_t* __restrict__ segptr, const int32_t* __restrict__ members,
+                                    const float* __restrict__ x, int32_t n_seg, int32_t C,
+                                    float* __restrict__ out) {
+  const int64_t total = (int64_t)n_seg * C;
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < total; p += (int64_t)gridDim.x * blockDim.x) {
+    const int k = (int)(p / C), c = (int)(p - (int64_t)k * C);
+    const int mb = segptr[k], me = segptr[k + 1];
+    float acc = 0.f;
+    for (int m = mb; m < me; ++m) acc += x[(int64_t)members[m] * C + c];
+    out[p] = acc / (float)(me - mb > 0 ? me - mb : 1);
+  }
+}
+
 inline int grid_for(int64_t work, int block = 256) {
   int64_t g = (work + block - 1) / block;
   if (g < 1) g = 1;
@@ -290,5 +369,38 @@ extern "C" int dr_edge_mlp_scatter_bwd(const int32_t* rowptr, const int32_t* col
   hipLaunchKernelGGL(edge_mlp_scatter_bwd_kernel, dim3(grid_for((int64_t)n_rows * 32)), dim3(256), 0,
                      (hipStream_t)stream, rowptr, col, trowptr, tcol, teid, n_rows, A, B, ea, n_edge_feat, wc, ld_we,
                      be, DS, D, DP, EAP);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dr_segment_max(const int32_t* segptr, const int32_t* members, const float* x, int32_t n_seg,
+                              int32_t n_chan, int32_t n_rows, int32_t mode, float* out, int32_t* arg, void* stream) {
+  if (!segptr || !x || !out || n_seg < 0 || n_chan < 0 || n_rows < 0 || mode < 0 || mode > 1) return DR_E_ARG;
+  const int64_t work = (int64_t)n_seg * n_chan;
+  if (work == 0) return DR_OK;
+  hipLaunchKernelGGL(segment_max_kernel, dim3(grid_for(work)), dim3(256), 0, (hipStream_t)stream, segptr, members, x,
+                     n_seg, n_chan, n_rows, mode, out, arg);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dr_segment_max_bwd(const int32_t* segptr, const int32_t* members, const float* x, const float* out,
+                                  const int32_t* arg, const float* dout, int32_t n_seg, int32_t n_chan,
+                                  int32_t n_rows, int32_t mode, float* dx, void* stream) {
+  if (!segptr || !x || !dout || !dx || n_seg < 0 || n_chan < 0 || mode < 0 || mode > 1) return DR_E_ARG;
+  if (mode == 0 && !arg) return DR_E_ARG;
+  if (mode == 1 && !out) return DR_E_ARG;
+  const int64_t work = (int64_t)n_seg * n_chan;
+  if (work == 0) return DR_OK;
+  hipLaunchKernelGGL(segment_max_bwd_kernel, dim3(grid_for(work)), dim3(256), 0, (hipStream_t)stream, segptr, members,
+                     x, out, arg, dout, n_seg, n_chan, n_rows, mode, dx);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dr_segment_mean(const int32_t* segptr, const int32_t* members, const float* x, int32_t n_seg,
+                               int32_t n_chan, float* out, void* stream) {
+  if (!segptr || !x || !out || n_seg < 0 || n_chan < 0) return DR_E_ARG;
+  const int64_t work = (int64_t)n_seg * n_chan;
+  if (work == 0) return DR_OK;
+  hipLaunchKernelGGL(segment_mean_kernel, dim3(grid_for(work)), dim3(256), 0, (hipStream_t)stream, segptr, members, x,
+                     n_seg, n_chan, out);
   return (int)hipGetLastError();
 }

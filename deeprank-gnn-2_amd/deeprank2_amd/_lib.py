@@ -178,6 +178,9 @@ SIGNATURES = [
     ("dr_linear_dw", ctypes.c_int, [VP, VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP, VP, ctypes.c_int32, VP]),
     ("dr_edge_mlp_scatter", ctypes.c_int, [VP, VP, ctypes.c_int32, VP, VP, VP, ctypes.c_int32, VP, ctypes.c_int32, VP, VP, VP]),
     ("dr_edge_mlp_scatter_bwd", ctypes.c_int, [VP, VP, VP, VP, VP, ctypes.c_int32, VP, VP, VP, ctypes.c_int32, VP, ctypes.c_int32, VP, VP, VP, VP, VP, VP]),
+    ("dr_segment_max", ctypes.c_int, [VP, VP, VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP, VP, VP]),
+    ("dr_segment_max_bwd", ctypes.c_int, [VP, VP, VP, VP, VP, VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP, VP]),
+    ("dr_segment_mean", ctypes.c_int, [VP, VP, VP, ctypes.c_int32, ctypes.c_int32, VP, VP]),
     ("dr_dropout_mask", ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int32, ctypes.c_float, VP]),
     ("dr_version", ctypes.c_char_p, []),
     ("dr_device_arch", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32]),

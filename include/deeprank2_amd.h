@@ -34,6 +34,10 @@
  *                           (deeprank2/neuralnets/gnn/vanilla_gnn.py:26-65)
  *   dr_edge_mlp_scatter[_bwd]  VanillaConvolutionalLayer edge MLP + scatter_sum
  *                           (vanilla_gnn.py:29-35) on any edge list
+ *   dr_segment_max[_bwd] / dr_segment_mean
+ *                           torch_scatter scatter_max / scatter_mean and PyG
+ *                           max_pool_x behind community_pooling / max_pool_x
+ *                           (community_pooling.py:165-242; ginet.py:103)
  *   dr_csr_from_coo         the ordering torch_scatter's CPU scatter_add_
  *                           implies for edge_index[0] (ginet.py:41,58): a stable
  *                           row-sorted CSR, built on the device
@@ -352,6 +356,23 @@ int dr_edge_mlp_scatter_bwd(const int32_t* rowptr, const int32_t* col, const int
                             const int32_t* teid, int32_t n_rows, const float* A, const float* B, const float* ea,
                             int32_t n_edge_feat, const float* wc, int32_t ld_we, const float* be, const float* DS,
                             float* D, float* DP, float* EAP, void* stream);
+
+/* Segment max / mean over member lists (segptr [n_seg+1], members [n_rows]:
+ * the CSR of a cluster vector, members ascending in each segment), x/out
+ * [*, n_chan] fp32.  mode 0 = torch_scatter.scatter_max (community_pooling.py
+ * :209: NaN dropped, first max, empty -> 0 with arg = n_rows); mode 1 =
+ * scatter_reduce amax as PyG max_pool_x (ginet.py:103, foutnet.py:111: NaN
+ * propagates).  Backward: mode 0 routes dout to arg, mode 1 splits it over
+ * the members equal to the max (plus one when the max is +-0: torch counts
+ * its zero-initialised output as a tie).  dr_segment_mean: scatter_mean
+ * (community_pooling.py:216, count clamped to 1).                          */
+int dr_segment_max(const int32_t* segptr, const int32_t* members, const float* x, int32_t n_seg, int32_t n_chan,
+                   int32_t n_rows, int32_t mode, float* out, int32_t* arg, void* stream);
+int dr_segment_max_bwd(const int32_t* segptr, const int32_t* members, const float* x, const float* out,
+                       const int32_t* arg, const float* dout, int32_t n_seg, int32_t n_chan, int32_t n_rows,
+                       int32_t mode, float* dx, void* stream);
+int dr_segment_mean(const int32_t* segptr, const int32_t* members, const float* x, int32_t n_seg, int32_t n_chan,
+                    float* out, void* stream);
 
 /* Host-side replica of the in-kernel dropout RNG (DR_DROPOUT_HASH): writes
  * keep[i] for i in [0, n) (i = 128*b + r) into a host buffer.             */
