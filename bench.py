@@ -27,13 +27,38 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "deeprank-gnn-2_amd")]
 
-from deeprank2_amd.engine import GINetTrainStep  # noqa: E402
-from deeprank2_amd.neuralnets.gnn.ginet import GINet, BatchHandle  # noqa: E402
+from deeprank2_amd.engine import FusedTrainStep  # noqa: E402
+from deeprank2_amd.fused import BatchHandle  # noqa: E402
+from deeprank2_amd.neuralnets.gnn.foutnet import FoutNet  # noqa: E402
+from deeprank2_amd.neuralnets.gnn.ginet import GINet  # noqa: E402
+from deeprank2_amd.neuralnets.gnn.vanilla_gnn import VanillaNetwork  # noqa: E402
 from deeprank2_amd.store import GraphRecord, GraphStore, pack_graphs  # noqa: E402
 from deeprank2_amd.utils.synthetic import doubled_edges, make_dataset  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 B_PER_GPU = 64
+MODELS = {"ginet": GINet, "foutnet": FoutNet, "vanilla": VanillaNetwork}
+# graph families of SURVEY §8(d): residue-PPI (configs 2/3), atom-level (config 4), SRV-like
+FAMILIES = {
+    "residue": {},
+    "atom": {"n_lo": 2700, "n_hi": 3300, "mean_degree": 16.7, "k_lo": 8, "k_hi": 32},
+    "srv": {"n_lo": 26, "n_hi": 36, "mean_degree": 7.4, "k_lo": 2, "k_hi": 3},
+}
+WORKLOADS = {
+    ("ginet", "residue"): "GINet residue-PPI training step, BASELINE.json configs[1]",
+    ("foutnet", "residue"): "FoutNet residue-PPI training step, BASELINE.json configs[2]",
+    ("ginet", "atom"): "GINet atom-level training step (fp32), BASELINE.json configs[3] shape",
+    ("ginet", "mixed"): "GINet mixed residue/SRV/atom batch, BASELINE.json configs[4] shape",
+}
+
+
+def make_graphs(kind, n, seed):
+    """Synthetic dataset of one family, or config 5's 50/30/20 residue/SRV/atom mix."""
+    if kind != "mixed":
+        return make_dataset(n, seed=seed, **FAMILIES[kind])
+    rng = np.random.default_rng(seed)
+    fam = rng.choice(["residue", "srv", "atom"], size=n, p=[0.5, 0.3, 0.2])
+    return [make_dataset(1, seed=int(seed * 7919 + i), **FAMILIES[f])[0] for i, f in enumerate(fam)]
 
 
 def records(graphs):
@@ -44,15 +69,26 @@ def records(graphs):
     return out
 
 
-def algorithmic_bytes(packed, gids):
+def algorithmic_bytes(packed, gids, model="ginet", out_dim=1):
     """Bytes one graph pass must move for these graphs:
     reads x (4NF), CSR (4(N+1)+4E), depth-0 members (4(K0+1)+4N), pooled CSR
     (4(K0+1)+4P1), depth-1 members (4(K1+1)+4K0), y (4); writes the per-graph
-    weight-gradient slab 4(32F+1024) and head vectors 4*324."""
+    weight-gradient slab and head vectors (GINet: 4(32F+1024) + 4*324).
+    VanillaNetwork reads no clusters but the edge features (4*E*Fe) and the
+    transposed CSR with its slot map (4(N+1)+8E)."""
     n, e, k0, p1, k1 = (a[gids] for a in packed.sizes())
     f = packed.n_feat
+    r4 = lambda v: (v + 3) & ~3  # noqa: E731
+    if model == "vanilla":
+        fe = 0 if packed.edge_attr is None else packed.edge_attr.shape[1]
+        per = 4 * n * f + 2 * (4 * (n + 1) + 4 * e) + 4 * e + 4 * e * fe + 4
+        per = per + 4 * 2 * (32 * (2 * f + fe) + 32 + f * (f + 32) + f) + 4 * (r4(f) + 256 + r4(out_dim))
+        return int(per.sum())
     per = 4 * n * f + 4 * (n + 1) + 4 * e + 4 * (k0 + 1) + 4 * n + 4 * (k0 + 1) + 4 * p1 + 4 * (k1 + 1) + 4 * k0 + 4
-    per = per + 4 * (32 * f + 1024) + 4 * 324
+    if model == "foutnet":
+        per = per + 4 * (32 * f + 1072) + 4 * (160 + r4(out_dim))
+    else:
+        per = per + 4 * (32 * f + 1024) + 4 * (320 + r4(out_dim))
     return int(per.sum())
 
 
@@ -77,7 +113,7 @@ def pmc_traffic_bytes():
     return int((2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024), os.path.relpath(files[-1], ROOT)
 
 
-def cpu_baseline(graphs, budget_s=15.0, max_steps=60):
+def cpu_baseline(graphs, budget_s=15.0, max_steps=60, model_name="ginet"):
     """The CPU oracle (op-for-op restatement of the reference, torch CPU) training
     the same batch: forward, MSE, backward, Adam — on this host's cores."""
     from oracle import data_ref, gnn_ref  # noqa: PLC0415
@@ -91,7 +127,7 @@ def cpu_baseline(graphs, budget_s=15.0, max_steps=60):
     torch.set_num_threads(cores)
     datas = [data_ref.synthetic_to_data(g) for g in graphs]
     torch.manual_seed(1234)
-    model = gnn_ref.GINet(30, 1, 3).train()
+    model = {"ginet": gnn_ref.GINet, "foutnet": gnn_ref.FoutNet, "vanilla": gnn_ref.VanillaNetwork}[model_name](30, 1, 3).train()
     opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-5)
 
     def one():
@@ -110,7 +146,8 @@ def cpu_baseline(graphs, budget_s=15.0, max_steps=60):
         one()
         n += 1
     dt = (time.perf_counter() - t0) / n
-    return {"value": round(len(graphs) / dt, 2), "unit": "graphs/s", "cores": cores, "kind": "port", "sample": f"{n} GINet(30,1,3) train steps (fwd+MSE+bwd+Adam) on one batch of {len(graphs)} of the same synthetic graphs; oracle/gnn_ref.py on torch CPU, {cores} threads; {dt * 1e3:.1f} ms/step"}
+    name = {"ginet": "GINet", "foutnet": "FoutNet", "vanilla": "VanillaNetwork"}[model_name]
+    return {"value": round(len(graphs) / dt, 2), "unit": "graphs/s", "cores": cores, "kind": "port", "sample": f"{n} {name}(30,1,3) train steps (fwd+MSE+bwd+Adam) on one batch of {len(graphs)} of the same synthetic graphs; oracle/gnn_ref.py on torch CPU, {cores} threads; {dt * 1e3:.1f} ms/step"}
 
 
 def main():  # noqa: PLR0915
@@ -118,8 +155,10 @@ def main():  # noqa: PLR0915
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batches", type=int, default=16, help="resident mini-batches per rank (64 graphs each)")
-    ap.add_argument("--batch", type=int, default=B_PER_GPU)
+    ap.add_argument("--batches", type=int, default=16, help="resident mini-batches per rank")
+    ap.add_argument("--batch", type=int, default=None, help="graphs per GPU per step (default 64; 32 for atom-level graphs)")
+    ap.add_argument("--model", choices=sorted(MODELS), default="ginet")
+    ap.add_argument("--graphs", choices=["residue", "atom", "mixed", "srv"], default="residue")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch every step from Python instead of replaying captured HIP graphs")
     ap.add_argument("--capture-ddp", action="store_true", help="N>1: also capture the RCCL all-reduce in the HIP graph (default: eager steps)")
@@ -143,19 +182,21 @@ def main():  # noqa: PLR0915
         pg = torch.distributed.group.WORLD
     dev = torch.device(f"cuda:{local}")
 
-    B = args.batch
-    graphs = make_dataset(B * args.batches, seed=1000 + rank)
+    B = args.batch or (32 if args.graphs == "atom" else B_PER_GPU)
+    if args.graphs in ("atom", "mixed"):
+        args.batches = min(args.batches, 4)  # generation time of ~3k-node graphs
+    graphs = make_graphs(args.graphs, B * args.batches, seed=1000 + rank)
     packed = pack_graphs(records(graphs))
     store = GraphStore(packed, dev)
     order = np.random.default_rng(rank).permutation(packed.n_graphs).astype(np.int32)
     handles = [BatchHandle(store, order[i * B:(i + 1) * B]) for i in range(args.batches)]
 
     torch.manual_seed(1234)
-    model = GINet(30, 1, 3).to(dev).train()
+    model = MODELS[args.model](30, 1, 3).to(dev).train()
     if pg is not None:
         for p in model.parameters():
             torch.distributed.broadcast(p.data, 0)
-    step = GINetTrainStep(model, lr=1e-3, weight_decay=1e-5, loss="mse", process_group=pg)
+    step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5, loss="mse", process_group=pg)
     model._drop_seed = 77 + rank  # training-mode dropout drawn in-kernel (counter hash)
 
     def run_eager(i):
@@ -210,17 +251,21 @@ def main():  # noqa: PLR0915
     if pg is not None:
         torch.distributed.all_reduce(et)
     edges_total = float(et.item())
-    alg = np.mean([algorithmic_bytes(packed, h.gids_host) for h in handles])
+    alg = np.mean([algorithmic_bytes(packed, h.gids_host, args.model) for h in handles])
     achieved = alg / (kernel_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic_bytes() if B == B_PER_GPU else (None, None)
+    default_cfg = args.model == "ginet" and args.graphs == "residue" and B == B_PER_GPU
+    traffic, traffic_src = pmc_traffic_bytes() if default_cfg else (None, None)
+    large = any(h.lds((step.spec.entry, 1), lambda *sz: 0) > 160 * 1024 for h in handles) if args.model != "vanilla" else False
 
     result = None
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(graphs[:B])
+            cpu = cpu_baseline(graphs[:B], model_name=args.model)
+        workload = WORKLOADS.get((args.model, args.graphs), f"{args.model} on {args.graphs} graphs (diagnostic)")
+        kname = {"ginet": "ginet_large_conv1_kernel + ginet_large_tail_kernel (dr_ginet_large_pass)" if large else "ginet_graph_kernel (dr_ginet_graph_pass, fwd+loss+bwd, 1 workgroup/graph)", "foutnet": "fout_graph_kernel (dr_fout_graph_pass)", "vanilla": "vanilla_graph_kernel (dr_vanilla_graph_pass)"}[args.model]
         result = {
-            "metric": "graphs/sec per training step, GINet residue-PPI (fwd+MSE+bwd+Adam)",
+            "metric": "graphs/sec per training step, GINet residue-PPI (fwd+MSE+bwd+Adam)" if default_cfg else f"graphs/sec per training step, {workload} (fwd+MSE+bwd+Adam)",
             "value": round(graphs_total / elapsed, 1),
             "unit": "graphs/s",
             "edges_per_sec": round(edges_total / elapsed, 1),
@@ -232,9 +277,9 @@ def main():  # noqa: PLR0915
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (seeded residue-PPI graphs per SURVEY §8(d); random-init GINet(30,1,3))",
+            "data": f"synthetic (seeded {args.graphs} graphs per SURVEY §8(d); random-init {MODELS[args.model].__name__}(30,1,3))",
             "config": {
-                "workload": "GINet residue-PPI training step, BASELINE.json configs[1]",
+                "workload": workload,
                 "graphs_per_gpu": B,
                 "global_batch": B * world,
                 "mean_nodes_per_graph": round(float(np.diff(packed.node_off).mean()), 1),
@@ -245,7 +290,7 @@ def main():  # noqa: PLR0915
                 "parallelism": f"dp{world}",
             },
             "roofline": {
-                "kernel": "ginet_graph_kernel (dr_ginet_graph_pass, fwd+loss+bwd, 1 workgroup/graph)",
+                "kernel": kname,
                 "bound": "hbm",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
@@ -255,7 +300,7 @@ def main():  # noqa: PLR0915
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": int(alg),
                 "kernel_ms_avg": round(kernel_ms, 5),
-                "kernel_timing": "HIP events around each dr_ginet_graph_pass launch over an eager region of the same step count",
+                "kernel_timing": f"HIP events around each {step.spec.entry if not large else 'dr_ginet_large_pass'} launch over an eager region of the same step count",
             },
             "launch": "eager" if captured is None else "hipgraph-replay",
             "cpu_baseline": cpu,

@@ -1,4 +1,4 @@
-// VanillaNetwork training step, one workgroup per graph.
+// VanillaNetwork training step as a pipeline of batch-wide row-parallel kernels.
 //
 // Replaces (deeprank2 v3.1.0):
 //   VanillaConvolutionalLayer.forward  deeprank2/neuralnets/gnn/vanilla_gnn.py:26-38
@@ -9,13 +9,16 @@
 //             s_i = sum_{e: src i} m_e,   x'_i = relu(Wn [x_i | s_i] + bn).
 // The edge GEMM is never formed: We = [Wa | Wb | Wc] splits it into two node
 // GEMMs, A = X Wa^T and B = X Wb^T, and pre_e = A_i + B_j + Wc ea_e + be is
-// rebuilt on the fly in a CSR gather (the fused gather + edge MLP + scatter).
-// The backward needs no per-edge storage either: with dpre_e = relu'(pre_e) ds_i
+// rebuilt on the fly inside the CSR gather (the fused gather + edge MLP +
+// scatter).  The backward needs no per-edge storage either: with
+// dpre_e = relu'(pre_e) ds_i,
 //   D_i  = sum_{e: src i} dpre_e,   D'_j = sum_{e: dst j} dpre_e  (transposed CSR),
-//   dWa = D^T X,  dWb = D'^T X,  dWc = sum_e dpre_e ea_e^T,  dx = ... + D Wa + D' Wb,
-// all row-wise gathers and node-level products.
-// Node-level intermediates (E x 32 messages never exist) live in an HBM
-// scratch laid out per batch row (L2 / MALL resident); weights live in LDS.
+//   dWa = D^T X,  dWb = D'^T X,  dWc = sum_e dpre_e ea_e^T,  dx = ... + D Wa + D' Wb.
+// Unlike GINet/FoutNet, a residue graph's E x 32 edge work does not fit one
+// workgroup's LDS, so every node-level stage is a kernel over ALL rows of the
+// batch (every CU busy, latency hidden by occupancy), intermediates in an HBM
+// scratch (L2/MALL resident), weights staged in LDS per workgroup; only the
+// mean/graph-MLP and the weight-gradient reductions are per graph.
 
 #include <hip/hip_runtime.h>
 
@@ -25,20 +28,9 @@ namespace {
 
 using namespace drk;
 
-constexpr int NT = 1024;
-constexpr int NW = NT / 64;
 constexpr int MAXFE = 8;
+constexpr int RB = 256;  // row-kernel workgroup size
 
-struct VArgs {
-  dr_graph_store s;
-  dr_vanilla_weights w;
-  dr_pass p;
-  dr_vanilla_scratch ws;
-  const dr_graph_desc* descs;
-  int32_t B;
-};
-
-// scratch arrays (batch rows x width), array-major
 struct Scratch {
   int64_t x1, x2, du, dx1, s1, s2, a1, b1, a2, b2, ds, d, dp, eap, total;
 };
@@ -65,52 +57,69 @@ __host__ __device__ inline Scratch scratch_layout(int64_t rows, int F, int Fe) {
   return c;
 }
 
-struct VCarve {
-  int KE, KN, we1, be1, wn1, bn1, we2, be2, wn2, bn2, g1w, g1b, g2w, g2b, head, red, total;
+struct VA {
+  dr_graph_store s;
+  dr_vanilla_weights w;
+  dr_pass p;
+  dr_vanilla_scratch ws;
+  const dr_graph_desc* descs;
+  int32_t B, F, Fe, XS, KE, KN;
+  Scratch L;
 };
 
-__host__ __device__ inline VCarve vcarve(int F, int Fe, int OUT) {
-  VCarve c;
-  c.KE = 2 * F + Fe;
-  c.KN = F + 32;
-  int o = 0;
-#define TAKE(field, words) \
-  c.field = o;             \
-  o += r4(words);
-  TAKE(we1, 32 * c.KE)
-  TAKE(be1, 32)
-  TAKE(wn1, F * c.KN)
-  TAKE(bn1, F)
-  TAKE(we2, 32 * c.KE)
-  TAKE(be2, 32)
-  TAKE(wn2, F * c.KN)
-  TAKE(bn2, F)
-  TAKE(g1w, 128 * F)
-  TAKE(g1b, 128)
-  TAKE(g2w, OUT * 128)
-  TAKE(g2b, OUT)
-  TAKE(head, 2 * r4(F) + 3 * 128 + 16)
-  TAKE(red, NT)
-#undef TAKE
-  c.total = o;
-  return c;
-}
+struct Layer {
+  const float *we, *be, *wn, *bn;
+  const float* xin;  // scratch input rows (layer 2) or nullptr = the store's x (layer 1)
+  float *a, *bm, *s, *xout;
+};
 
-__device__ __forceinline__ void copy_w(float* dst, const float* src, int n) {
-  for (int p = threadIdx.x; p < n; p += NT) dst[p] = src[p];
-}
-
-// A = Xin Wa^T, B = Xin Wb^T (pre-activation halves of the edge MLP)
-__device__ __forceinline__ void edge_halves(const float* Xin, int ldx, int N, int F, const float* We, int KE, float* A,
-                                            float* Bm) {
-  for (int p = threadIdx.x; p < N * 64; p += NT) {
-    const int i = p >> 6, c = p & 63;
-    const float* w = We + (c & 31) * KE + (c < 32 ? 0 : F);
-    const float* x = Xin + (int64_t)i * ldx;
-    float acc = 0.f;
-    for (int k = 0; k < F; ++k) acc = fmaf(x[k], w[k], acc);
-    (c < 32 ? A : Bm)[(int64_t)i * 32 + (c & 31)] = acc;
+__host__ __device__ inline Layer layer_of(const VA& a, int l) {
+  Layer L;
+  float* ws = a.ws.base;
+  if (l == 1) {
+    L.we = a.w.we1; L.be = a.w.be1; L.wn = a.w.wn1; L.bn = a.w.bn1;
+    L.xin = nullptr;
+    L.a = ws + a.L.a1; L.bm = ws + a.L.b1; L.s = ws + a.L.s1; L.xout = ws + a.L.x1;
+  } else {
+    L.we = a.w.we2; L.be = a.w.be2; L.wn = a.w.wn2; L.bn = a.w.bn2;
+    L.xin = ws + a.L.x1;
+    L.a = ws + a.L.a2; L.bm = ws + a.L.b2; L.s = ws + a.L.s2; L.xout = ws + a.L.x2;
   }
+  return L;
+}
+
+// node row r's input features (layer 1 reads the HBM-resident store)
+__device__ __forceinline__ const float* xin_row(const VA& a, const Layer& L, int64_t r) {
+  if (L.xin) return L.xin + r * a.XS;
+  const int b = a.ws.row_slot[r];
+  const dr_graph_desc& d = a.descs[b];
+  return a.s.x + (d.node0 + (r - a.ws.row0[b])) * a.XS;
+}
+
+struct RowGraph {
+  const int* rp;
+  const uint16_t* col;
+  const int* trp;
+  const uint16_t* tcol;
+  const int* teid;
+  const float* ea;  // CSR slot order, row stride FeS
+  int i;            // local row
+  int64_t r0;       // batch row of local node 0
+};
+
+__device__ __forceinline__ RowGraph row_graph(const VA& a, int64_t r) {
+  const int b = a.ws.row_slot[r];
+  const dr_graph_desc& d = a.descs[b];
+  RowGraph g;
+  g.r0 = a.ws.row0[b];
+  g.i = (int)(r - g.r0);
+  g.rp = a.s.rowptr + d.node0 + d.gid;
+  g.col = a.s.col + d.col0;
+  g.trp = a.s.t_rowptr + d.node0 + d.gid;
+  g.tcol = a.s.t_col + d.col0;
+  g.teid = a.s.t_eid + d.col0;
+  g.ea = a.s.ea + d.col0 * (a.Fe > 0 ? a.Fe : 1);
+  return g;
 }
 
 __device__ __forceinline__ float edge_const(const float* wc, const float* ea, int Fe) {
@@ -122,199 +131,94 @@ __device__ __forceinline__ float edge_const(const float* wc, const float* ea, in
 // relu'(pre) as torch's threshold_backward on relu(pre): 0 where relu(pre) <= 0
 __device__ __forceinline__ bool active(float pre) { return !(pre <= 0.f); }
 
-struct Graph {
-  const int* rp;      // CSR (by edge_index[0]) row pointers, local
-  const uint16_t* col;
-  const int* trp;     // transposed CSR (by edge_index[1])
-  const uint16_t* tcol;
-  const int* teid;    // transposed slot -> CSR slot
-  const float* ea;    // [slot, FeS] in CSR slot order
-  int FeS;
-};
+// ---- forward ------------------------------------------------------------------
 
-// s_i = sum_{e in row i} relu(A_i + B_j + Wc ea_e + be)
-__device__ __forceinline__ void edge_forward(const Graph& G, int N, int Fe, const float* A, const float* Bm,
-                                             const float* We, int KE, int F, const float* be, float* S) {
-  for (int p = threadIdx.x; p < N * 32; p += NT) {
-    const int i = p >> 5, c = p & 31;
-    const float a = A[(int64_t)i * 32 + c], bc = be[c];
-    const float* wc = We + c * KE + 2 * F;
+// [A | B] = Xin [Wa; Wb]^T: 64 threads per row
+__global__ void __launch_bounds__(RB) vb_halves(VA a, int l) {
+  extern __shared__ float lds[];
+  const Layer L = layer_of(a, l);
+  const int F = a.F, KE = a.KE, LW = F + 1;
+  for (int p = threadIdx.x; p < 64 * F; p += RB) {  // [64][F+1]
+    const int c = p / F, k = p - c * F;
+    lds[c * LW + k] = L.we[(c & 31) * KE + (c < 32 ? 0 : F) + k];
+  }
+  __syncthreads();
+  const int c = threadIdx.x & 63;
+  const float* w = lds + c * LW;
+  for (int64_t r = blockIdx.x * (RB / 64) + (threadIdx.x >> 6); r < a.ws.n_rows; r += (int64_t)gridDim.x * (RB / 64)) {
+    const float* x = xin_row(a, L, r);
     float acc = 0.f;
-    for (int e = G.rp[i]; e < G.rp[i + 1]; ++e) {
-      const int j = G.col[e];
-      const float pre = a + Bm[(int64_t)j * 32 + c] + edge_const(wc, G.ea + (int64_t)e * G.FeS, Fe) + bc;
-      acc += relu_keepnan(pre);
-    }
-    S[(int64_t)i * 32 + c] = acc;
+    for (int k = 0; k < F; ++k) acc = fmaf(x[k], w[k], acc);
+    (c < 32 ? L.a : L.bm)[r * 32 + (c & 31)] = acc;
   }
 }
 
-// Xout = relu([Xin | S] Wn^T + bn)
-__device__ __forceinline__ void node_update(const float* Xin, int ldx, const float* S, int N, int F, const float* Wn,
-                                            int KN, const float* bn, float* Xout, int ldo) {
-  for (int p = threadIdx.x; p < N * F; p += NT) {
-    const int i = p / F, n = p - i * F;
-    const float* w = Wn + n * KN;
-    const float* x = Xin + (int64_t)i * ldx;
-    const float* sv = S + (int64_t)i * 32;
+// S_i = sum_{e in row i} relu(A_i + B_j + Wc ea_e + be): 32 threads per row
+__global__ void __launch_bounds__(RB) vb_edge_fwd(VA a, int l) {
+  __shared__ float swc[32 * MAXFE + 32];
+  const Layer L = layer_of(a, l);
+  const int F = a.F, Fe = a.Fe, KE = a.KE, FeS = Fe > 0 ? Fe : 1;
+  for (int p = threadIdx.x; p < 32 * Fe; p += RB) swc[p] = L.we[(p / Fe) * KE + 2 * F + p % Fe];
+  if (threadIdx.x < 32) swc[32 * MAXFE + threadIdx.x] = L.be[threadIdx.x];
+  __syncthreads();
+  const int c = threadIdx.x & 31;
+  const float* wc = swc + c * Fe;
+  const float bc = swc[32 * MAXFE + c];
+  for (int64_t r = blockIdx.x * (RB / 32) + (threadIdx.x >> 5); r < a.ws.n_rows; r += (int64_t)gridDim.x * (RB / 32)) {
+    const RowGraph g = row_graph(a, r);
+    const float ac = L.a[r * 32 + c];
+    const float* Bg = L.bm + g.r0 * 32 + c;
+    float acc = 0.f;
+    const int eb = g.rp[g.i], ee = g.rp[g.i + 1];
+    int e = eb;
+    for (; e + 4 <= ee; e += 4) {  // four independent gathers in flight, summed in edge order
+      const int j0 = g.col[e], j1 = g.col[e + 1], j2 = g.col[e + 2], j3 = g.col[e + 3];
+      const float q0 = Bg[(int64_t)j0 * 32], q1 = Bg[(int64_t)j1 * 32], q2 = Bg[(int64_t)j2 * 32], q3 = Bg[(int64_t)j3 * 32];
+      const float* ea = g.ea + (int64_t)e * FeS;
+      acc += relu_keepnan(ac + q0 + edge_const(wc, ea, Fe) + bc);
+      acc += relu_keepnan(ac + q1 + edge_const(wc, ea + FeS, Fe) + bc);
+      acc += relu_keepnan(ac + q2 + edge_const(wc, ea + 2 * FeS, Fe) + bc);
+      acc += relu_keepnan(ac + q3 + edge_const(wc, ea + 3 * FeS, Fe) + bc);
+    }
+    for (; e < ee; ++e) acc += relu_keepnan(ac + Bg[(int64_t)g.col[e] * 32] + edge_const(wc, g.ea + (int64_t)e * FeS, Fe) + bc);
+    L.s[r * 32 + c] = acc;
+  }
+}
+
+// Xout = relu([Xin | S] Wn^T + bn): 64 threads per row (F <= 64)
+__global__ void __launch_bounds__(RB) vb_node(VA a, int l) {
+  extern __shared__ float lds[];
+  const Layer L = layer_of(a, l);
+  const int F = a.F, KN = a.KN, XS = a.XS, LW = KN + 1;
+  for (int p = threadIdx.x; p < F * KN; p += RB) lds[(p / KN) * LW + p % KN] = L.wn[p];
+  for (int p = threadIdx.x; p < F; p += RB) lds[F * LW + p] = L.bn[p];
+  __syncthreads();
+  const int n = threadIdx.x & 63;
+  for (int64_t r = blockIdx.x * (RB / 64) + (threadIdx.x >> 6); r < a.ws.n_rows; r += (int64_t)gridDim.x * (RB / 64)) {
+    if (n >= F) continue;
+    const float* x = xin_row(a, L, r);
+    const float* sv = L.s + r * 32;
+    const float* w = lds + n * LW;
     float acc = 0.f;
     for (int k = 0; k < F; ++k) acc = fmaf(x[k], w[k], acc);
     for (int k = 0; k < 32; ++k) acc = fmaf(sv[k], w[F + k], acc);
-    Xout[(int64_t)i * ldo + n] = relu_keepnan(acc + bn[n]);
+    L.xout[r * XS + n] = relu_keepnan(acc + lds[F * LW + n]);
   }
 }
 
-// D, D' and the edge-attribute partials of one layer (see header comment)
-__device__ __forceinline__ void edge_backward(const Graph& G, int N, int Fe, const float* A, const float* Bm,
-                                              const float* We, int KE, int F, const float* be, const float* DS,
-                                              float* D, float* DP, float* EAP) {
-  for (int p = threadIdx.x; p < N * 32; p += NT) {
-    const int i = p >> 5, c = p & 31;
-    const float a = A[(int64_t)i * 32 + c], bi = Bm[(int64_t)i * 32 + c], bc = be[c];
-    const float dsi = DS[(int64_t)i * 32 + c];
-    const float* wc = We + c * KE + 2 * F;
-    int cnt = 0;
-    float eap[MAXFE];
-#pragma unroll
-    for (int f = 0; f < MAXFE; ++f) eap[f] = 0.f;
-    for (int e = G.rp[i]; e < G.rp[i + 1]; ++e) {
-      const int j = G.col[e];
-      const float* ea = G.ea + (int64_t)e * G.FeS;
-      const float pre = a + Bm[(int64_t)j * 32 + c] + edge_const(wc, ea, Fe) + bc;
-      if (active(pre)) {
-        ++cnt;
-#pragma unroll
-        for (int f = 0; f < MAXFE; ++f)
-          if (f < Fe) eap[f] += ea[f];
-      }
-    }
-    D[(int64_t)i * 32 + c] = cnt ? dsi * (float)cnt : 0.f;
-    float* ep = EAP + ((int64_t)i * 32 + c) * (Fe > 0 ? Fe : 1);
-    for (int f = 0; f < Fe; ++f) ep[f] = cnt ? dsi * eap[f] : 0.f;
-    // D'_i: edges e = (src -> i), pre_e = A_src + B_i + Wc ea_e + be
-    float acc = 0.f;
-    for (int q = G.trp[i]; q < G.trp[i + 1]; ++q) {
-      const int src = G.tcol[q], e = G.teid[q];
-      const float pre = A[(int64_t)src * 32 + c] + bi + edge_const(wc, G.ea + (int64_t)e * G.FeS, Fe) + bc;
-      if (active(pre)) acc += DS[(int64_t)src * 32 + c];
-    }
-    DP[(int64_t)i * 32 + c] = acc;
-  }
-}
-
-// per-graph weight-gradient partials of one layer into the slab
-__device__ __forceinline__ void layer_wgrad(int N, int F, int Fe, int KE, int KN, const float* Xin, int ldx,
-                                            const float* S, const float* DU, const float* D, const float* DP,
-                                            const float* EAP, float* slab) {
-  const int nwe = 32 * KE, nwn = F * KN;
-  const int total = nwe + 32 + nwn + F;
-  const int FeS = Fe > 0 ? Fe : 1;
-  for (int p = threadIdx.x; p < total; p += NT) {
-    float acc = 0.f;
-    if (p < nwe) {
-      const int c = p / KE, k = p - c * KE;
-      if (k < F) {
-        for (int i = 0; i < N; ++i) acc = fmaf(D[(int64_t)i * 32 + c], Xin[(int64_t)i * ldx + k], acc);
-      } else if (k < 2 * F) {
-        for (int i = 0; i < N; ++i) acc = fmaf(DP[(int64_t)i * 32 + c], Xin[(int64_t)i * ldx + k - F], acc);
-      } else {
-        for (int i = 0; i < N; ++i) acc += EAP[((int64_t)i * 32 + c) * FeS + (k - 2 * F)];
-      }
-    } else if (p < nwe + 32) {
-      const int c = p - nwe;
-      for (int i = 0; i < N; ++i) acc += D[(int64_t)i * 32 + c];
-    } else if (p < nwe + 32 + nwn) {
-      const int q = p - nwe - 32, n = q / KN, k = q - n * KN;
-      if (k < F) {
-        for (int i = 0; i < N; ++i) acc = fmaf(DU[(int64_t)i * r4(F) + n], Xin[(int64_t)i * ldx + k], acc);
-      } else {
-        for (int i = 0; i < N; ++i) acc = fmaf(DU[(int64_t)i * r4(F) + n], S[(int64_t)i * 32 + k - F], acc);
-      }
-    } else {
-      const int n = p - nwe - 32 - nwn;
-      for (int i = 0; i < N; ++i) acc += DU[(int64_t)i * r4(F) + n];
-    }
-    slab[p] = acc;
-  }
-}
-
-__global__ void __launch_bounds__(NT) vanilla_graph_kernel(VArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
+// per graph: scatter_mean -> graph MLP -> loss -> head backward (one workgroup)
+__global__ void __launch_bounds__(256) vb_head(VA a) {
+  __shared__ float sG[64], sH[128], sDh[128], sDout[16], sRed[256];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.x;
-  const dr_graph_store& s = a.s;
-  const dr_graph_desc d = a.descs[b];
-  const int g = d.gid;
-  const int64_t n0 = d.node0, ec0 = d.col0;
-  const int N = d.n_nodes, F = s.n_feat, Fe = s.n_edge_feat, OUT = a.p.out_dim;
-  const int XS = r4(F);
-  const VCarve c = vcarve(F, Fe, OUT);
-  const int KE = c.KE, KN = c.KN;
-  float *sWe1 = lds + c.we1, *sBe1 = lds + c.be1, *sWn1 = lds + c.wn1, *sBn1 = lds + c.bn1;
-  float *sWe2 = lds + c.we2, *sBe2 = lds + c.be2, *sWn2 = lds + c.wn2, *sBn2 = lds + c.bn2;
-  float *sG1w = lds + c.g1w, *sG1b = lds + c.g1b, *sG2w = lds + c.g2w, *sG2b = lds + c.g2b;
-  float* sG = lds + c.head;  // mean over nodes [XS]
-  float* sHh = sG + XS;      // relu(fc1)   [128]
-  float* sDh = sHh + 128;    // its grad    [128]
-  float* sDg = sDh + 128;    // d mean     [XS]
-  float* sDout = sDg + XS;   // logits / dout [16]
-  float* sHpre = sDout + 16; // [128]
-  float* sRed = lds + c.red;
-
-  const float y_g = s.y[g];
+  const int F = a.F, XS = a.XS, OUT = a.p.out_dim;
+  const int64_t r0 = a.ws.row0[b];
+  const int N = a.ws.row0[b + 1] - (int)r0;
+  const float* X2 = a.ws.base + a.L.x2 + r0 * XS;
+  const float y_g = a.s.y[a.descs[b].gid];
   if (a.p.step_counter && b == 0 && tid == 0) a.p.step_counter[1] = a.p.step_counter[0];
-  copy_w(sWe1, a.w.we1, 32 * KE);
-  copy_w(sBe1, a.w.be1, 32);
-  copy_w(sWn1, a.w.wn1, F * KN);
-  copy_w(sBn1, a.w.bn1, F);
-  copy_w(sWe2, a.w.we2, 32 * KE);
-  copy_w(sBe2, a.w.be2, 32);
-  copy_w(sWn2, a.w.wn2, F * KN);
-  copy_w(sBn2, a.w.bn2, F);
-  copy_w(sG1w, a.w.g1w, 128 * F);
-  copy_w(sG1b, a.w.g1b, 128);
-  copy_w(sG2w, a.w.g2w, OUT * 128);
-  copy_w(sG2b, a.w.g2b, OUT);
-
-  const Scratch L = scratch_layout(a.ws.n_rows, F, Fe);
-  const int64_t R0 = a.ws.row0[b];
-  float* ws = a.ws.base;
-  float *X1 = ws + L.x1 + R0 * XS, *X2 = ws + L.x2 + R0 * XS, *DU = ws + L.du + R0 * XS, *DX1 = ws + L.dx1 + R0 * XS;
-  float *S1 = ws + L.s1 + R0 * 32, *S2 = ws + L.s2 + R0 * 32, *A1 = ws + L.a1 + R0 * 32, *B1 = ws + L.b1 + R0 * 32;
-  float *A2 = ws + L.a2 + R0 * 32, *B2 = ws + L.b2 + R0 * 32, *DS = ws + L.ds + R0 * 32, *D = ws + L.d + R0 * 32;
-  float *DP = ws + L.dp + R0 * 32, *EAP = ws + L.eap + R0 * 32 * (Fe > 0 ? Fe : 1);
-  const float* X0 = s.x + n0 * XS;
-  Graph G;
-  G.rp = s.rowptr + n0 + g;
-  G.col = s.col + ec0;
-  G.trp = s.t_rowptr + n0 + g;
-  G.tcol = s.t_col + ec0;
-  G.teid = s.t_eid + ec0;
-  G.FeS = Fe > 0 ? Fe : 1;
-  G.ea = s.ea + ec0 * G.FeS;
-  __syncthreads();
-
-  DRK_STAMP(0);
-  // ---------------- layer 1 (vanilla_gnn.py:26-38) ----------------------------
-  edge_halves(X0, XS, N, F, sWe1, KE, A1, B1);
-  __syncthreads();
-  edge_forward(G, N, Fe, A1, B1, sWe1, KE, F, sBe1, S1);
-  __syncthreads();
-  node_update(X0, XS, S1, N, F, sWn1, KN, sBn1, X1, XS);
-  __syncthreads();
-  DRK_STAMP(1);
-  // ---------------- layer 2 ---------------------------------------------------
-  edge_halves(X1, XS, N, F, sWe2, KE, A2, B2);
-  __syncthreads();
-  edge_forward(G, N, Fe, A2, B2, sWe2, KE, F, sBe2, S2);
-  __syncthreads();
-  node_update(X1, XS, S2, N, F, sWn2, KN, sBn2, X2, XS);
-  __syncthreads();
-  DRK_STAMP(2);
-  // ---------------- scatter_mean over the graph (vanilla_gnn.py:62) ----------
-  {
-    const int CH = NT / XS;  // row chunks, combined in order
-    const int n = tid % XS, ch = tid / XS;
+  {  // column sums in row chunks, combined in chunk order
+    const int CH = 256 / XS, n = tid % XS, ch = tid / XS;
     float acc = 0.f;
     if (n < F && ch < CH) {
       const int i0 = (N * ch) / CH, i1 = (N * (ch + 1)) / CH;
@@ -329,27 +233,22 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VArgs a) {
     }
   }
   __syncthreads();
-  // ---------------- graph MLP: Linear(F,128) -> relu -> Linear(128,out) -------
   if (tid < 128) {
     float acc = 0.f;
-    for (int n = 0; n < F; ++n) acc = fmaf(sG[n], sG1w[tid * F + n], acc);
-    acc += sG1b[tid];
-    sHpre[tid] = acc;
-    sHh[tid] = relu_keepnan(acc);
+    for (int n = 0; n < F; ++n) acc = fmaf(sG[n], a.w.g1w[tid * F + n], acc);
+    sH[tid] = relu_keepnan(acc + a.w.g1b[tid]);
   }
   __syncthreads();
-  for (int q = wave; q < OUT; q += NW) {
-    float v = fmaf(sHh[lane], sG2w[q * 128 + lane], sHh[lane + 64] * sG2w[q * 128 + lane + 64]);
+  for (int q = wave; q < OUT; q += 4) {
+    float v = fmaf(sH[lane], a.w.g2w[q * 128 + lane], sH[lane + 64] * a.w.g2w[q * 128 + lane + 64]);
     v = dr_wave_sum(v);
-    if (lane == 0) sDout[q] = v + sG2b[q];
+    if (lane == 0) sDout[q] = v + a.w.g2b[q];
   }
   __syncthreads();
   if ((a.p.flags & DR_PASS_FORWARD) && tid < OUT) a.p.out[(int64_t)b * OUT + tid] = sDout[tid];
   if (!(a.p.flags & DR_PASS_BACKWARD)) return;
   __syncthreads();
-  DRK_STAMP(3);
-  // ---------------- loss gradient (trainer.py:688-689) ------------------------
-  if (tid == 0) {
+  if (tid == 0) {  // loss gradient (trainer.py:688-689)
     if (a.p.loss_kind == DR_LOSS_MSE) {
       const float dl = sDout[0] - y_g;
       if (a.p.loss_per_graph) a.p.loss_per_graph[b] = dl * dl;
@@ -371,73 +270,250 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VArgs a) {
   __syncthreads();
   if (tid < 128) {
     float acc = 0.f;
-    for (int q = 0; q < OUT; ++q) acc = fmaf(sG2w[q * 128 + tid], sDout[q], acc);
-    sDh[tid] = relu_bwd(sHh[tid], acc);
+    for (int q = 0; q < OUT; ++q) acc = fmaf(a.w.g2w[q * 128 + tid], sDout[q], acc);
+    sDh[tid] = relu_bwd(sH[tid], acc);
   }
   __syncthreads();
+  float* hg = a.p.head + (int64_t)b * DR_VANILLA_HEAD_STRIDE(F, OUT);
+  const int HD = XS + 256 + r4(OUT);  // d mean, consumed by vb_du2
   if (tid < F) {
     float acc = 0.f;
-    for (int r = 0; r < 128; ++r) acc = fmaf(sG1w[r * F + tid], sDh[r], acc);
-    sDg[tid] = acc / (float)N;  // scatter_mean backward: grad / count
+    for (int r = 0; r < 128; ++r) acc = fmaf(a.w.g1w[r * F + tid], sDh[r], acc);
+    hg[HD + tid] = acc / (float)N;  // scatter_mean backward: grad / count
   }
-  {
-    const int HS = DR_VANILLA_HEAD_STRIDE(F, OUT);
-    float* hg = a.p.head + (int64_t)b * HS;
-    if (tid < XS) hg[tid] = tid < F ? sG[tid] : 0.f;
-    if (tid < 128) {
-      hg[XS + tid] = sHh[tid];
-      hg[XS + 128 + tid] = sDh[tid];
+  if (tid < XS) hg[tid] = tid < F ? sG[tid] : 0.f;
+  if (tid < 128) {
+    hg[XS + tid] = sH[tid];
+    hg[XS + 128 + tid] = sDh[tid];
+  }
+  if (tid < OUT) hg[XS + 256 + tid] = sDout[tid];
+}
+
+// ---- backward -----------------------------------------------------------------
+
+// DU = relu'(X2) * dmean[graph]  (layer 2)   or   relu'(X1) * DX1  (layer 1)
+__global__ void __launch_bounds__(RB) vb_du(VA a, int l) {
+  const int F = a.F, XS = a.XS;
+  const float* xo = a.ws.base + (l == 2 ? a.L.x2 : a.L.x1);
+  const float* dx1 = a.ws.base + a.L.dx1;
+  float* du = a.ws.base + a.L.du;
+  const int HS = DR_VANILLA_HEAD_STRIDE(F, a.p.out_dim), HD = XS + 256 + r4(a.p.out_dim);
+  const int64_t total = a.ws.n_rows * XS;
+  for (int64_t p = blockIdx.x * (int64_t)RB + threadIdx.x; p < total; p += (int64_t)gridDim.x * RB) {
+    const int64_t r = p / XS;
+    const int n = (int)(p - r * XS);
+    float g = 0.f;
+    if (n < F) g = (l == 2) ? a.p.head[(int64_t)a.ws.row_slot[r] * HS + HD + n] : dx1[p];
+    du[p] = n < F ? relu_bwd(xo[p], g) : 0.f;
+  }
+}
+
+// [dX1_direct | DS] = DU Wn  (layer 2: both;  layer 1: DS only).  128 threads per row.
+__global__ void __launch_bounds__(RB) vb_dxs(VA a, int l) {
+  extern __shared__ float lds[];
+  const int F = a.F, KN = a.KN, XS = a.XS;
+  const float* wn = l == 2 ? a.w.wn2 : a.w.wn1;
+  for (int p = threadIdx.x; p < F * KN; p += RB) lds[p] = wn[p];
+  __syncthreads();
+  const float* du = a.ws.base + a.L.du;
+  float* dx1 = a.ws.base + a.L.dx1;
+  float* ds = a.ws.base + a.L.ds;
+  const int k = threadIdx.x & 127;
+  for (int64_t r = blockIdx.x * (RB / 128) + (threadIdx.x >> 7); r < a.ws.n_rows; r += (int64_t)gridDim.x * (RB / 128)) {
+    if (k >= KN || (l == 1 && k < F)) continue;
+    const float* u = du + r * XS;
+    float acc = 0.f;
+    for (int n = 0; n < F; ++n) acc = fmaf(u[n], lds[n * KN + k], acc);
+    if (k < F) dx1[r * XS + k] = acc;
+    else ds[r * 32 + k - F] = acc;
+  }
+}
+
+// D, D' and the edge-attribute partials of one layer: 32 threads per row
+__global__ void __launch_bounds__(RB) vb_edge_bwd(VA a, int l) {
+  __shared__ float swc[32 * MAXFE + 32];
+  const Layer L = layer_of(a, l);
+  const int F = a.F, Fe = a.Fe, KE = a.KE, FeS = Fe > 0 ? Fe : 1;
+  for (int p = threadIdx.x; p < 32 * Fe; p += RB) swc[p] = L.we[(p / Fe) * KE + 2 * F + p % Fe];
+  if (threadIdx.x < 32) swc[32 * MAXFE + threadIdx.x] = L.be[threadIdx.x];
+  __syncthreads();
+  float* ws = a.ws.base;
+  const float* DS = ws + a.L.ds;
+  float *D = ws + a.L.d, *DP = ws + a.L.dp, *EAP = ws + a.L.eap;
+  const int c = threadIdx.x & 31;
+  const float* wc = swc + c * Fe;
+  const float bc = swc[32 * MAXFE + c];
+  for (int64_t r = blockIdx.x * (RB / 32) + (threadIdx.x >> 5); r < a.ws.n_rows; r += (int64_t)gridDim.x * (RB / 32)) {
+    const RowGraph g = row_graph(a, r);
+    const float ac = L.a[r * 32 + c], bi = L.bm[r * 32 + c], dsi = DS[r * 32 + c];
+    const float* Bg = L.bm + g.r0 * 32 + c;
+    const float* Ag = L.a + g.r0 * 32 + c;
+    const float* DSg = DS + g.r0 * 32 + c;
+    int cnt = 0;
+    float eap[MAXFE];
+#pragma unroll
+    for (int f = 0; f < MAXFE; ++f) eap[f] = 0.f;
+    const int eb = g.rp[g.i], ee = g.rp[g.i + 1];
+    int e = eb;
+    for (; e + 4 <= ee; e += 4) {
+      const int j0 = g.col[e], j1 = g.col[e + 1], j2 = g.col[e + 2], j3 = g.col[e + 3];
+      const float q[4] = {Bg[(int64_t)j0 * 32], Bg[(int64_t)j1 * 32], Bg[(int64_t)j2 * 32], Bg[(int64_t)j3 * 32]};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float* ea = g.ea + (int64_t)(e + u) * FeS;
+        if (active(ac + q[u] + edge_const(wc, ea, Fe) + bc)) {
+          ++cnt;
+#pragma unroll
+          for (int f = 0; f < MAXFE; ++f)
+            if (f < Fe) eap[f] += ea[f];
+        }
+      }
     }
-    if (tid < OUT) hg[XS + 256 + tid] = sDout[tid];
+    for (; e < ee; ++e) {
+      const float* ea = g.ea + (int64_t)e * FeS;
+      if (active(ac + Bg[(int64_t)g.col[e] * 32] + edge_const(wc, ea, Fe) + bc)) {
+        ++cnt;
+#pragma unroll
+        for (int f = 0; f < MAXFE; ++f)
+          if (f < Fe) eap[f] += ea[f];
+      }
+    }
+    D[r * 32 + c] = cnt ? dsi * (float)cnt : 0.f;
+    for (int f = 0; f < Fe; ++f) EAP[(r * 32 + c) * FeS + f] = cnt ? dsi * eap[f] : 0.f;
+    float acc = 0.f;  // D'_i over edges (src -> i): pre = A_src + B_i + Wc ea_e + be
+    const int qb = g.trp[g.i], qe = g.trp[g.i + 1];
+    int q = qb;
+    for (; q + 4 <= qe; q += 4) {
+      int src[4], ed[4];
+      float av[4], dv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        src[u] = g.tcol[q + u];
+        ed[u] = g.teid[q + u];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        av[u] = Ag[(int64_t)src[u] * 32];
+        dv[u] = DSg[(int64_t)src[u] * 32];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (active(av[u] + bi + edge_const(wc, g.ea + (int64_t)ed[u] * FeS, Fe) + bc)) acc += dv[u];
+    }
+    for (; q < qe; ++q) {
+      const int src = g.tcol[q], e = g.teid[q];
+      if (active(Ag[(int64_t)src * 32] + bi + edge_const(wc, g.ea + (int64_t)e * FeS, Fe) + bc)) acc += DSg[(int64_t)src * 32];
+    }
+    DP[r * 32 + c] = acc;
+  }
+}
+
+// DX1 += D Wa2 + D' Wb2: 64 threads per row
+__global__ void __launch_bounds__(RB) vb_dx1(VA a) {
+  extern __shared__ float lds[];
+  const int F = a.F, KE = a.KE, XS = a.XS;
+  for (int p = threadIdx.x; p < 32 * 2 * F; p += RB) {  // [c][0..2F)
+    const int c = p / (2 * F), k = p - c * 2 * F;
+    lds[p] = a.w.we2[c * KE + k];
   }
   __syncthreads();
-  DRK_STAMP(4);
-  const int SS1 = 32 * KE + 32 + F * KN + F;
-  float* slab = a.p.slab + (int64_t)b * DR_VANILLA_SLAB_STRIDE(F, Fe);
-  // ---------------- layer 2 backward -------------------------------------------
-  for (int p = tid; p < N * F; p += NT) {
-    const int i = p / F, n = p - i * F;
-    DU[(int64_t)i * XS + n] = relu_bwd(X2[(int64_t)i * XS + n], sDg[n]);
+  float* ws = a.ws.base;
+  const float *D = ws + a.L.d, *DP = ws + a.L.dp;
+  float* dx1 = ws + a.L.dx1;
+  const int k = threadIdx.x & 63;
+  for (int64_t r = blockIdx.x * (RB / 64) + (threadIdx.x >> 6); r < a.ws.n_rows; r += (int64_t)gridDim.x * (RB / 64)) {
+    if (k >= F) continue;
+    float acc = dx1[r * XS + k];
+    for (int c = 0; c < 32; ++c) acc = fmaf(D[r * 32 + c], lds[c * 2 * F + k], acc);
+    for (int c = 0; c < 32; ++c) acc = fmaf(DP[r * 32 + c], lds[c * 2 * F + F + k], acc);
+    dx1[r * XS + k] = acc;
   }
-  __syncthreads();
-  for (int p = tid; p < N * KN; p += NT) {  // [dX1_direct | ds2] = du2 Wn2
-    const int i = p / KN, k = p - i * KN;
-    float acc = 0.f;
-    for (int n = 0; n < F; ++n) acc = fmaf(DU[(int64_t)i * XS + n], sWn2[n * KN + k], acc);
-    if (k < F) DX1[(int64_t)i * XS + k] = acc;
-    else DS[(int64_t)i * 32 + k - F] = acc;
+}
+
+// Weight-gradient partials of one layer per chunk of DR_VANILLA_CHUNK rows
+// (all CUs busy), rows staged through LDS; vb_wgrad_combine then sums each
+// graph's chunks in order into its slab (deterministic).
+constexpr int WR = DR_VANILLA_CHUNK;
+
+__host__ __device__ inline int layer_grad_size(int F, int Fe) { return 32 * (2 * F + Fe) + 32 + F * (F + 32) + F; }
+
+__global__ void __launch_bounds__(RB) vb_wgrad_part(VA a, int l) {
+  extern __shared__ float lds[];
+  const int ch = blockIdx.x;
+  const int b = a.ws.chunk_slot[ch];
+  const int F = a.F, Fe = a.Fe, KE = a.KE, KN = a.KN, XS = a.XS, FeS = Fe > 0 ? Fe : 1;
+  const Layer L = layer_of(a, l);
+  const int64_t r0 = a.ws.row0[b];
+  const int N = a.ws.row0[b + 1] - (int)r0;
+  const int i0 = (ch - a.ws.chunk_first[b]) * WR, nr = min(WR, N - i0);
+  const int64_t g0 = r0 + i0;  // first batch row of the chunk
+  float* ws = a.ws.base;
+  const float* X = L.xin ? L.xin + g0 * XS : a.s.x + (a.descs[b].node0 + i0) * XS;
+  // LDS chunk: X [WR][XS] | S [WR][32] | D [WR][32] | DP [WR][32] | DU [WR][XS] | EAP [WR][32*FeS]
+  float* cX = lds;
+  float* cS = cX + WR * XS;
+  float* cD = cS + WR * 32;
+  float* cDP = cD + WR * 32;
+  float* cDU = cDP + WR * 32;
+  float* cE = cDU + WR * XS;
+  for (int p = threadIdx.x; p < nr * XS; p += RB) {
+    cX[p] = X[p];
+    cDU[p] = ws[a.L.du + g0 * XS + p];
   }
-  __syncthreads();
-  edge_backward(G, N, Fe, A2, B2, sWe2, KE, F, sBe2, DS, D, DP, EAP);
-  __syncthreads();
-  DRK_STAMP(5);
-  for (int p = tid; p < N * F; p += NT) {  // dX1 += D Wa2 + D' Wb2
-    const int i = p / F, k = p - i * F;
-    float acc = DX1[(int64_t)i * XS + k];
-    for (int cc = 0; cc < 32; ++cc) acc = fmaf(D[(int64_t)i * 32 + cc], sWe2[cc * KE + k], acc);
-    for (int cc = 0; cc < 32; ++cc) acc = fmaf(DP[(int64_t)i * 32 + cc], sWe2[cc * KE + F + k], acc);
-    DX1[(int64_t)i * XS + k] = acc;
+  for (int p = threadIdx.x; p < nr * 32; p += RB) {
+    cS[p] = L.s[g0 * 32 + p];
+    cD[p] = ws[a.L.d + g0 * 32 + p];
+    cDP[p] = ws[a.L.dp + g0 * 32 + p];
   }
-  layer_wgrad(N, F, Fe, KE, KN, X1, XS, S2, DU, D, DP, EAP, slab + SS1);
+  for (int p = threadIdx.x; p < nr * 32 * FeS; p += RB) cE[p] = ws[a.L.eap + g0 * 32 * FeS + p];
   __syncthreads();
-  DRK_STAMP(6);
-  // ---------------- layer 1 backward -------------------------------------------
-  for (int p = tid; p < N * F; p += NT) {
-    const int i = p / F, n = p - i * F;
-    DU[(int64_t)i * XS + n] = relu_bwd(X1[(int64_t)i * XS + n], DX1[(int64_t)i * XS + n]);
+  const int nwe = 32 * KE, nwn = F * KN, total = nwe + 32 + nwn + F;
+  float* out = a.ws.part + (int64_t)ch * total;
+  for (int p = threadIdx.x; p < total; p += RB) {
+    float v = 0.f;
+    if (p < nwe) {
+      const int c = p / KE, k = p - c * KE;
+      if (k < F) {
+        for (int i = 0; i < nr; ++i) v = fmaf(cD[i * 32 + c], cX[i * XS + k], v);
+      } else if (k < 2 * F) {
+        for (int i = 0; i < nr; ++i) v = fmaf(cDP[i * 32 + c], cX[i * XS + k - F], v);
+      } else {
+        for (int i = 0; i < nr; ++i) v += cE[(i * 32 + c) * FeS + (k - 2 * F)];
+      }
+    } else if (p < nwe + 32) {
+      const int c = p - nwe;
+      for (int i = 0; i < nr; ++i) v += cD[i * 32 + c];
+    } else if (p < nwe + 32 + nwn) {
+      const int q = p - nwe - 32, n = q / KN, k = q - n * KN;
+      if (k < F) {
+        for (int i = 0; i < nr; ++i) v = fmaf(cDU[i * XS + n], cX[i * XS + k], v);
+      } else {
+        for (int i = 0; i < nr; ++i) v = fmaf(cDU[i * XS + n], cS[i * 32 + k - F], v);
+      }
+    } else {
+      const int n = p - nwe - 32 - nwn;
+      for (int i = 0; i < nr; ++i) v += cDU[i * XS + n];
+    }
+    out[p] = v;
   }
-  __syncthreads();
-  for (int p = tid; p < N * 32; p += NT) {  // ds1 = du1 Wn1[:, F:]
-    const int i = p >> 5, k = p & 31;
-    float acc = 0.f;
-    for (int n = 0; n < F; ++n) acc = fmaf(DU[(int64_t)i * XS + n], sWn1[n * KN + F + k], acc);
-    DS[(int64_t)i * 32 + k] = acc;
+}
+
+__global__ void __launch_bounds__(RB) vb_wgrad_combine(VA a, int l) {
+  const int total = layer_grad_size(a.F, a.Fe);
+  const int64_t work = (int64_t)a.B * total;
+  for (int64_t q = blockIdx.x * (int64_t)RB + threadIdx.x; q < work; q += (int64_t)gridDim.x * RB) {
+    const int b = (int)(q / total), p = (int)(q - (int64_t)b * total);
+    float v = 0.f;
+    for (int ch = a.ws.chunk_first[b]; ch < a.ws.chunk_first[b + 1]; ++ch) v += a.ws.part[(int64_t)ch * total + p];
+    a.p.slab[(int64_t)b * DR_VANILLA_SLAB_STRIDE(a.F, a.Fe) + (l == 2 ? total : 0) + p] = v;
   }
-  __syncthreads();
-  edge_backward(G, N, Fe, A1, B1, sWe1, KE, F, sBe1, DS, D, DP, EAP);
-  __syncthreads();
-  layer_wgrad(N, F, Fe, KE, KN, X0, XS, S1, DU, D, DP, EAP, slab);
-  DRK_STAMP(7);
+}
+
+inline int rows_grid(int64_t rows, int rows_per_block) {
+  int64_t g = (rows + rows_per_block - 1) / rows_per_block;
+  if (g < 1) g = 1;
+  if (g > 2048) g = 2048;  // grid-stride beyond 8 workgroups per CU
+  return (int)g;
 }
 
 }  // namespace
@@ -447,31 +523,66 @@ extern "C" int64_t dr_vanilla_scratch_floats(int64_t n_rows, int32_t n_feat, int
 }
 
 extern "C" int64_t dr_vanilla_lds_bytes(int32_t n_feat, int32_t n_edge_feat, int32_t out_dim) {
-  return 4LL * vcarve(n_feat, n_edge_feat, out_dim).total;
+  (void)out_dim;
+  const int XS = r4(n_feat), FeS = n_edge_feat > 0 ? n_edge_feat : 1;
+  return 4LL * WR * (2 * XS + 3 * 32 + 32 * FeS);  // the largest dynamic LDS of the pipeline (vb_wgrad_part)
+}
+
+extern "C" int64_t dr_vanilla_part_floats(int32_t n_feat, int32_t n_edge_feat) {
+  return layer_grad_size(n_feat, n_edge_feat);
 }
 
 extern "C" int dr_vanilla_graph_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
                                      const dr_vanilla_weights* w, const dr_pass* pass,
                                      const dr_vanilla_scratch* scratch, int32_t lds_bytes, void* stream) {
+  (void)lds_bytes;
   if (!store || !descs || !w || !pass || !scratch || n_batch < 0) return DR_E_ARG;
   if (pass->out_dim < 1 || pass->out_dim > DR_MAX_OUT) return DR_E_UNSUPPORTED;
-  if (store->n_feat < 1 || r4(store->n_feat) > NT / 16 || store->n_edge_feat < 0 || store->n_edge_feat > MAXFE)
+  if (store->n_feat < 1 || store->n_feat > 64 || store->n_edge_feat < 0 || store->n_edge_feat > MAXFE)
     return DR_E_UNSUPPORTED;
-  if (lds_bytes > 160 * 1024) return DR_E_LDS;
-  if (!scratch->base || !scratch->row0) return DR_E_ARG;
+  if (!scratch->base || !scratch->row0 || !scratch->row_slot) return DR_E_ARG;
   if ((pass->flags & DR_PASS_BACKWARD) && (!pass->slab || !pass->head)) return DR_E_ARG;
   if ((pass->flags & DR_PASS_BACKWARD) && pass->loss_kind == DR_LOSS_NONE && !pass->dout) return DR_E_ARG;
   if ((pass->flags & DR_PASS_FORWARD) && !pass->out) return DR_E_ARG;
+  if ((pass->flags & DR_PASS_BACKWARD) && (!scratch->part || !scratch->chunk_first || !scratch->chunk_slot))
+    return DR_E_ARG;
   if (pass->use_dropout != DR_DROPOUT_OFF) return DR_E_UNSUPPORTED;
   if (n_batch == 0) return DR_OK;
-  DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&vanilla_graph_kernel)));
-  VArgs args;
-  args.s = *store;
-  args.w = *w;
-  args.p = *pass;
-  args.ws = *scratch;
-  args.descs = descs;
-  args.B = n_batch;
-  hipLaunchKernelGGL(vanilla_graph_kernel, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, args);
+  VA a;
+  a.s = *store;
+  a.w = *w;
+  a.p = *pass;
+  a.ws = *scratch;
+  a.descs = descs;
+  a.B = n_batch;
+  a.F = store->n_feat;
+  a.Fe = store->n_edge_feat;
+  a.XS = r4(a.F);
+  a.KE = 2 * a.F + a.Fe;
+  a.KN = a.F + 32;
+  a.L = scratch_layout(scratch->n_rows, a.F, a.Fe);
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t R = scratch->n_rows;
+  const size_t lds_half = 4 * 64 * (a.F + 1), lds_node = 4 * (a.F * (a.KN + 1) + a.F), lds_dxs = 4 * a.F * a.KN,
+               lds_dx1 = 4 * 64 * a.F, lds_wg = (size_t)dr_vanilla_lds_bytes(a.F, a.Fe, pass->out_dim);
+  for (int l = 1; l <= 2; ++l) {
+    hipLaunchKernelGGL(vb_halves, dim3(rows_grid(R, RB / 64)), dim3(RB), lds_half, st, a, l);
+    hipLaunchKernelGGL(vb_edge_fwd, dim3(rows_grid(R, RB / 32)), dim3(RB), 0, st, a, l);
+    hipLaunchKernelGGL(vb_node, dim3(rows_grid(R, RB / 64)), dim3(RB), lds_node, st, a, l);
+  }
+  hipLaunchKernelGGL(vb_head, dim3(n_batch), dim3(256), 0, st, a);
+  if (pass->flags & DR_PASS_BACKWARD) {
+    hipLaunchKernelGGL(vb_du, dim3(rows_grid(R * a.XS, RB)), dim3(RB), 0, st, a, 2);
+    hipLaunchKernelGGL(vb_dxs, dim3(rows_grid(R, RB / 128)), dim3(RB), lds_dxs, st, a, 2);
+    hipLaunchKernelGGL(vb_edge_bwd, dim3(rows_grid(R, RB / 32)), dim3(RB), 0, st, a, 2);
+    hipLaunchKernelGGL(vb_dx1, dim3(rows_grid(R, RB / 64)), dim3(RB), lds_dx1, st, a);
+    hipLaunchKernelGGL(vb_wgrad_part, dim3(scratch->n_chunks), dim3(RB), lds_wg, st, a, 2);
+    hipLaunchKernelGGL(vb_wgrad_combine, dim3(rows_grid((int64_t)n_batch * layer_grad_size(a.F, a.Fe), RB)), dim3(RB), 0, st, a, 2);
+    hipLaunchKernelGGL(vb_du, dim3(rows_grid(R * a.XS, RB)), dim3(RB), 0, st, a, 1);
+    hipLaunchKernelGGL(vb_dxs, dim3(rows_grid(R, RB / 128)), dim3(RB), lds_dxs, st, a, 1);
+    hipLaunchKernelGGL(vb_edge_bwd, dim3(rows_grid(R, RB / 32)), dim3(RB), 0, st, a, 1);
+    hipLaunchKernelGGL(vb_wgrad_part, dim3(scratch->n_chunks), dim3(RB), lds_wg, st, a, 1);
+    hipLaunchKernelGGL(vb_wgrad_combine, dim3(rows_grid((int64_t)n_batch * layer_grad_size(a.F, a.Fe), RB)), dim3(RB), 0, st, a, 1);
+  }
   return (int)hipGetLastError();
 }

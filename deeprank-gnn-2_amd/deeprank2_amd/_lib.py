@@ -98,7 +98,7 @@ class VanillaWeightsC(ctypes.Structure):
 
 
 class VanillaScratchC(ctypes.Structure):
-    _fields_ = [("base", VP), ("row0", VP), ("n_rows", ctypes.c_int64)]
+    _fields_ = [("base", VP), ("row0", VP), ("row_slot", VP), ("n_rows", ctypes.c_int64), ("chunk_first", VP), ("chunk_slot", VP), ("n_chunks", ctypes.c_int32), ("pad0", ctypes.c_int32), ("part", VP)]
 
 
 class PassC(ctypes.Structure):
@@ -168,6 +168,7 @@ SIGNATURES = [
     ("dr_vanilla_graph_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(VanillaWeightsC), ctypes.POINTER(PassC), ctypes.POINTER(VanillaScratchC), ctypes.c_int32, VP]),
     ("dr_vanilla_scratch_floats", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
     ("dr_vanilla_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 3),
+    ("dr_vanilla_part_floats", ctypes.c_int64, [ctypes.c_int32] * 2),
     ("dr_fout_graph_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(FoutWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, VP]),
     ("dr_fout_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 8),
     ("dr_reduce_update", ctypes.c_int, [ctypes.POINTER(ParamTableC), VP, VP, ctypes.c_int32, ctypes.POINTER(AdamC), VP, ctypes.c_float, VP, VP]),

@@ -51,9 +51,25 @@ class BatchHandle:
             n = self.store._sizes[0][self.gids_host.astype(np.int64)]  # noqa: SLF001
             row0 = np.concatenate([[0], np.cumsum(n)]).astype(np.int32)
             rows = int(row0[-1])
-            floats = int(_lib.load().dr_vanilla_scratch_floats(rows, n_feat, n_edge_feat))
+            slot = np.repeat(np.arange(self.B, dtype=np.int32), n)
+            chunks = (n + 31) // 32  # DR_VANILLA_CHUNK
+            chunk_first = np.concatenate([[0], np.cumsum(chunks)]).astype(np.int32)
+            chunk_slot = np.repeat(np.arange(self.B, dtype=np.int32), chunks)
+            lib = _lib.load()
+            floats = int(lib.dr_vanilla_scratch_floats(rows, n_feat, n_edge_feat))
+            part = int(lib.dr_vanilla_part_floats(n_feat, n_edge_feat)) * int(chunk_first[-1])
             dev = self.store.device
-            sc = (torch.from_numpy(row0).to(dev), torch.empty(floats, dtype=torch.float32, device=dev), rows)
+            ints = torch.from_numpy(np.concatenate([row0, slot, chunk_first, chunk_slot])).to(dev)
+            c = _lib.VanillaScratchC()
+            buf = torch.empty(floats, dtype=torch.float32, device=dev)
+            pbuf = torch.empty(part, dtype=torch.float32, device=dev)
+            base = ints.data_ptr()
+            c.base, c.row0, c.row_slot, c.n_rows = buf.data_ptr(), base, base + 4 * (self.B + 1), rows
+            c.chunk_first = base + 4 * (self.B + 1 + rows)
+            c.chunk_slot = base + 4 * (2 * (self.B + 1) + rows)
+            c.n_chunks = int(chunk_first[-1])
+            c.part = pbuf.data_ptr()
+            sc = (c, (ints, buf, pbuf))
             self._lds[key] = sc
         return sc
 

@@ -4,11 +4,11 @@
 Same constructor signatures, parameter names/shapes/initialisation order and
 ``state_dict`` keys as the reference (``deeprank2/neuralnets/gnn/vanilla_gnn.py:10-65``).
 
-``VanillaNetwork.forward(batch)`` runs ``dr_vanilla_graph_pass``: one HIP
-workgroup per graph runs both layers with the edge MLP fused into the CSR
-gather (the E x 32 messages are never materialised), ``scatter_mean``, the
-graph MLP, the loss and the backward; node-level intermediates sit in a
-per-batch HBM scratch.  ``VanillaConvolutionalLayer.forward`` on an arbitrary
+``VanillaNetwork.forward(batch)`` runs ``dr_vanilla_graph_pass``: a pipeline
+of batch-wide row-parallel HIP kernels runs both layers with the edge MLP
+fused into the CSR gather (the E x 32 messages are never materialised),
+``scatter_mean``, the graph MLP, the loss and the backward; node-level
+intermediates sit in a per-batch HBM scratch.  ``VanillaConvolutionalLayer.forward`` on an arbitrary
 edge list runs the same arithmetic through the layer-level C entries
 (``dr_edge_mlp_scatter`` / ``_bwd``).  There is no CPU path.
 """
@@ -82,7 +82,7 @@ class VanillaConvolutionalLayer(nn.Module):
 
 
 # ---------------------------------------------------------------------------
-# Fused per-graph path (dr_vanilla_graph_pass + dr_reduce_update)
+# Fused path (dr_vanilla_graph_pass + dr_reduce_update)
 # ---------------------------------------------------------------------------
 
 PARAM_NAMES = [
@@ -102,7 +102,7 @@ def make_spec(f, fe):
         return 2 * layer
 
     def head_stride(out):
-        return xs + 256 + _r4(out)
+        return 2 * xs + 256 + _r4(out)  # g | h | dh | dout | d mean
 
     def recipe(_f, _out):
         sl = _lib.DR_GRAD_SLAB
@@ -122,9 +122,7 @@ def make_spec(f, fe):
         if st.n_edge_feat != fe or st.n_feat != f:
             msg = f"batch has F={st.n_feat}, Fe={st.n_edge_feat}; the model expects F={f}, Fe={fe}"
             raise ValueError(msg)
-        row0, buf, rows = h.vanilla_scratch(f, fe)
-        sc = _lib.VanillaScratchC()
-        sc.base, sc.row0, sc.n_rows = buf.data_ptr(), row0.data_ptr(), rows
+        sc, _keep = h.vanilla_scratch(f, fe)
         lib = _lib.load()
         lds = int(lib.dr_vanilla_lds_bytes(f, fe, p.out_dim))
         _lib.check(lib.dr_vanilla_graph_pass(st.cstruct(), h.descs.data_ptr(), h.B, w, p, sc, lds, _lib.stream_ptr(st.device)), "dr_vanilla_graph_pass")

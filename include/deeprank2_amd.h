@@ -252,23 +252,32 @@ typedef struct dr_vanilla_weights {
  * batch slot b (row0[B] = n_rows = total nodes of the batch).                */
 typedef struct dr_vanilla_scratch {
   float* base;
-  const int32_t* row0;
+  const int32_t* row0;        /* [B+1]                                          */
+  const int32_t* row_slot;    /* [n_rows] batch slot of each row                */
   int64_t n_rows;
+  const int32_t* chunk_first; /* [B+1] first row chunk (DR_VANILLA_CHUNK rows) of each slot */
+  const int32_t* chunk_slot;  /* [n_chunks]                                     */
+  int32_t n_chunks;
+  int32_t pad0;
+  float* part;                /* [n_chunks, dr_vanilla_part_floats(F, Fe)] weight-gradient partials */
 } dr_vanilla_scratch;
+#define DR_VANILLA_CHUNK 32
 
 /* slab: per layer [dWe (32 x (2F+Fe)) | dbe (32) | dWn (F x (F+32)) | dbn (F)], layer 1 then 2
- * head: g [r4(F)] | relu(fc1) [128] | its grad [128] | dout [out]               */
+ * head: g [r4(F)] | relu(fc1) [128] | its grad [128] | dout [r4(out)] | d mean [r4(F)] */
 #define DR_VANILLA_SLAB_STRIDE(F, Fe) (2 * (32 * (2 * (F) + (Fe)) + 32 + (F) * ((F) + 32) + (F)))
-#define DR_VANILLA_HEAD_STRIDE(F, out) ((((F) + 3) & ~3) + 256 + (((out) + 3) & ~3))
+#define DR_VANILLA_HEAD_STRIDE(F, out) (2 * (((F) + 3) & ~3) + 256 + (((out) + 3) & ~3))
 
-/* One workgroup per graph: both VanillaConvolutionalLayers (edge MLP fused
- * into the CSR gather, scatter_sum, node MLP), scatter_mean, the graph MLP,
- * the loss and the whole backward.  Same dr_pass contract as the other
- * graph passes (no dropout).  Fe <= 8, F <= 64.                              */
+/* Both VanillaConvolutionalLayers (edge MLP fused into the CSR gather,
+ * scatter_sum, node MLP), scatter_mean, the graph MLP, the loss and the whole
+ * backward, as a short pipeline of row-parallel kernels over every node of
+ * the batch (all CUs busy) plus per-graph reductions.  Same dr_pass contract
+ * as the other graph passes (no dropout).  Fe <= 8, F <= 64.                 */
 int dr_vanilla_graph_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
                           const dr_vanilla_weights* w, const dr_pass* pass, const dr_vanilla_scratch* scratch,
                           int32_t lds_bytes, void* stream);
 int64_t dr_vanilla_scratch_floats(int64_t n_rows, int32_t n_feat, int32_t n_edge_feat);
+int64_t dr_vanilla_part_floats(int32_t n_feat, int32_t n_edge_feat); /* one layer's gradient entries */
 int64_t dr_vanilla_lds_bytes(int32_t n_feat, int32_t n_edge_feat, int32_t out_dim);
 
 /* Adam (torch.optim.Adam, L2 weight decay added to the gradient) settings.  */
