@@ -204,23 +204,34 @@ def main():  # noqa: PLR0915
 
     for i in range(args.warmup):
         run_eager(i)
-    captured = None
-    if not args.eager and (world == 1 or args.capture_ddp):  # one captured step per resident mini-batch, replayed
+    captured = sweep = None
+    if not args.eager and (world == 1 or args.capture_ddp):
+        # one captured graph per resident mini-batch, plus one graph holding a
+        # whole sweep over them (one launch per len(handles) steps)
         captured = [step.capture(h, global_batch=B * world) for h in handles]
+        sweep = step.capture_sweep(handles, global_batch=B * world)
 
-    def run(i):
-        if captured is None:
-            return run_eager(i)
-        captured[i % len(captured)].replay()
-        return step.loss_out, None
+    def run_steps(i0, k):
+        """Steps i0 .. i0+k-1 (mini-batch i % len(handles)); whole sweeps replay the sweep graph."""
+        i = i0
+        while i < i0 + k:
+            if sweep is not None and i % len(handles) == 0 and i + len(handles) <= i0 + k:
+                sweep.replay()
+                i += len(handles)
+            elif captured is not None:
+                captured[i % len(captured)].replay()
+                i += 1
+            else:
+                run_eager(i)
+                i += 1
+        return step.loss_out
 
     torch.cuda.synchronize()
     if pg is not None:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        loss, _ = run(args.warmup + i)
+    loss = run_steps(args.warmup, args.steps)
     torch.cuda.synchronize()
     if pg is not None:
         torch.distributed.barrier()
@@ -302,7 +313,7 @@ def main():  # noqa: PLR0915
                 "kernel_ms_avg": round(kernel_ms, 5),
                 "kernel_timing": f"HIP events around each {step.spec.entry if not large else 'dr_ginet_large_pass'} launch over an eager region of the same step count",
             },
-            "launch": "eager" if captured is None else "hipgraph-replay",
+            "launch": "eager" if captured is None else f"hipgraph-replay ({len(handles)}-step sweep graphs + per-step graphs)",
             "cpu_baseline": cpu,
             "final_loss": float(loss.item()),
         }

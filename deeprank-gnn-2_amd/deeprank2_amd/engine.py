@@ -199,6 +199,28 @@ class FusedTrainStep:
     def _state_tensors(self):
         return [*self.params, *[s for st in self.states for s in st], self.counter, self.flat]
 
+    def capture_sweep(self, handles, global_batch=None):
+        """Capture one training step per handle, in order, into ONE HIP graph
+        (a sweep over the resident mini-batches): replaying it runs
+        len(handles) steps with a single graph launch.  Training state is
+        left as before the call."""
+        for h in handles:
+            self._ensure(h.B)
+        snap = [t.detach().clone() for t in self._state_tensors()]
+        n = self.step_count
+        for h in handles:  # warm-up: LDS attributes, plans, allocator
+            self.step(h, global_batch=global_batch)
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for h in handles:
+                self.step(h, global_batch=global_batch)
+        torch.cuda.synchronize(self.device)
+        for t, s in zip(self._state_tensors(), snap):
+            t.data.copy_(s)
+        self.step_count = n
+        return g
+
     def capture(self, h: BatchHandle, global_batch=None):
         """Capture one training step on ``h`` into a HIP graph (``torch.cuda.CUDAGraph``).
 

@@ -224,3 +224,26 @@ def test_captured_step_replay_matches_eager():
     for a, b in zip(s1.params, s2.params):
         assert torch.equal(a, b)
     assert int(s1.counter[0]) == int(s2.counter[0]) == 6
+
+
+def test_captured_sweep_matches_eager():
+    """One HIP graph holding a sweep of steps over several mini-batches == eager steps."""
+    datas = _synthetic(36, seed=13)
+    store = GraphStore(pack_graphs(records_from_batch(P.Batch.from_data_list(datas))), DEV)
+    hs = [amd.BatchHandle(store, np.arange(12 * k, 12 * k + 12)) for k in range(3)]
+    torch.manual_seed(5)
+    m1 = amd.GINet(30, 1, 3).to(DEV).train()
+    m2 = amd.GINet(30, 1, 3).to(DEV).train()
+    m2.load_state_dict(m1.state_dict())
+    m1._drop_seed = m2._drop_seed = 99
+    s1, s2 = GINetTrainStep(m1), GINetTrainStep(m2)
+    sweep = s2.capture_sweep(hs)
+    for _ in range(2):
+        for h in hs:
+            l1, _ = s1.step(h)
+        sweep.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(l1, s2.loss_out)
+    for a, b in zip(s1.params, s2.params):
+        assert torch.equal(a, b)
+    assert int(s2.counter[0]) == 6
