@@ -159,6 +159,7 @@ def main():  # noqa: PLR0915
     ap.add_argument("--batch", type=int, default=None, help="graphs per GPU per step (default 64; 32 for atom-level graphs)")
     ap.add_argument("--model", choices=sorted(MODELS), default="ginet")
     ap.add_argument("--graphs", choices=["residue", "atom", "mixed", "srv"], default="residue")
+    ap.add_argument("--force-large", type=int, default=0, help="GINet: run the split tile+tail path with this many nodes per tile (diagnostic)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch every step from Python instead of replaying captured HIP graphs")
     ap.add_argument("--capture-ddp", action="store_true", help="N>1: also capture the RCCL all-reduce in the HIP graph (default: eager steps)")
@@ -190,6 +191,9 @@ def main():  # noqa: PLR0915
     store = GraphStore(packed, dev)
     order = np.random.default_rng(rank).permutation(packed.n_graphs).astype(np.int32)
     handles = [BatchHandle(store, order[i * B:(i + 1) * B]) for i in range(args.batches)]
+    for h in handles:
+        h.force_large = bool(args.force_large)
+        h.large_tile = args.force_large or None
 
     torch.manual_seed(1234)
     model = MODELS[args.model](30, 1, 3).to(dev).train()
@@ -266,7 +270,7 @@ def main():  # noqa: PLR0915
     achieved = alg / (kernel_ms * 1e-3) / 1e9
     default_cfg = args.model == "ginet" and args.graphs == "residue" and B == B_PER_GPU
     traffic, traffic_src = pmc_traffic_bytes() if default_cfg else (None, None)
-    large = any(h.lds((step.spec.entry, 1), lambda *sz: 0) > 160 * 1024 for h in handles) if args.model != "vanilla" else False
+    large = args.model == "ginet" and (bool(args.force_large) or any(h.lds((step.spec.entry, 1), lambda *sz: 0) > 160 * 1024 for h in handles))
 
     result = None
     if rank == 0:

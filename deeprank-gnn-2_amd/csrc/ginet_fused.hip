@@ -744,7 +744,8 @@ __global__ void __launch_bounds__(NTA) ginet_large_conv1_kernel(LargeArgs la) {
   const int g = d.gid;
   const int64_t n0 = d.node0, ec0 = d.col0, k00 = d.k0;
   const int N = d.n_nodes, K0 = d.n_k0, F = s.n_feat;
-  const int r0 = t * TR, nrows = min(TR, N - r0);
+  const int TRr = pl.tile_rows;
+  const int r0 = t * TRr, nrows = min(TRr, N - r0);
   const ConvCarve c = conv_carve(N, F, K0);
   const int KP = c.KP, LDW = c.LDW, XS = c.XS;
   float* sW1 = lds + c.w1;
@@ -762,7 +763,7 @@ __global__ void __launch_bounds__(NTA) ginet_large_conv1_kernel(LargeArgs la) {
     if (k < F) v = (r < 16) ? a.w.w1[r * F + k] : a.w.w1e[(r - 16) * F + k];
     sW1[r * LDW + k] = v;
   }
-  for (int p = tid; p < TR * (KP - XS); p += NTA) {  // Z pad columns
+  for (int p = tid; p < TRr * (KP - XS); p += NTA) {  // Z pad columns
     const int r = p / (KP - XS);
     sZ[r * LDW + XS + (p - r * (KP - XS))] = 0.f;
   }
@@ -1012,6 +1013,7 @@ extern "C" int dr_ginet_large_pass(const dr_graph_store* store, const dr_graph_d
   if (!plan->tile_first || !plan->z_row0 || !plan->tile_slot || !plan->z || !plan->part_val || !plan->part_arg)
     return DR_E_ARG;
   if (plan->n_tiles < n_batch || plan->k0_max < 1 || plan->k0_max > 64) return DR_E_ARG;
+  if (plan->tile_rows < 16 || plan->tile_rows > TR || plan->tile_rows % 16) return DR_E_ARG;
   if ((pass->flags & DR_PASS_BACKWARD) && (!pass->slab || !pass->head)) return DR_E_ARG;
   if ((pass->flags & DR_PASS_BACKWARD) && pass->loss_kind == DR_LOSS_NONE && !pass->dout) return DR_E_ARG;
   if ((pass->flags & DR_PASS_FORWARD) && !pass->out) return DR_E_ARG;

@@ -83,6 +83,8 @@ class LargePlanC(ctypes.Structure):
         ("tile_slot", VP),
         ("n_tiles", ctypes.c_int32),
         ("k0_max", ctypes.c_int32),
+        ("tile_rows", ctypes.c_int32),
+        ("pad0", ctypes.c_int32),
         ("z", VP),
         ("part_val", VP),
         ("part_arg", VP),

@@ -33,7 +33,8 @@ class BatchHandle:
         self.B = int(self.gids_host.size)
         self.max_sizes = store.max_sizes(self.gids_host)
         self._lds = {}
-        self.force_large = False  # tests: run the large-graph path on small graphs too
+        self.force_large = False  # run the split (tile + tail) path on small graphs too
+        self.large_tile = None  # nodes per tile of the split path (default 128)
 
     def lds(self, key, fn):
         """Dynamic LDS bytes for the largest graph of the batch (cached per model kind)."""
@@ -91,8 +92,9 @@ class LargePlan:
 
     TILE = 128
 
-    def __init__(self, h: BatchHandle, out_dim):
+    def __init__(self, h: BatchHandle, out_dim, tile_rows=None):
         st = h.store
+        self.TILE = int(tile_rows or h.large_tile or self.TILE)
         n, _e, k0, p1, k1 = (a[h.gids_host.astype(np.int64)] for a in st._sizes)  # noqa: SLF001
         self.k0_max = int(k0.max())
         if self.k0_max > 64:  # noqa: PLR2004
@@ -121,6 +123,7 @@ class LargePlan:
         c.tile_slot = base + 8 * (h.B + 1)
         c.n_tiles = self.n_tiles
         c.k0_max = self.k0_max
+        c.tile_rows = self.TILE
         c.z = self.z.data_ptr()
         c.part_val = self.part_val.data_ptr()
         c.part_arg = self.part_arg.data_ptr()

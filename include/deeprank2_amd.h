@@ -171,7 +171,7 @@ int64_t dr_ginet_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_feat, int
 
 /* ---- GINet on graphs larger than one workgroup's LDS (atom-level graphs) ----
  * Two launches with the same result as dr_ginet_graph_pass:
- *   1. one workgroup per tile of DR_LARGE_TILE nodes: Z = A X for its rows
+ *   1. one workgroup per tile of plan->tile_rows nodes: Z = A X for its rows
  *      (CSR gather from HBM/L2), H = relu(Z [W1;W1e]^T) on MFMA, and the
  *      tile's share of the depth-0 max pool (per cluster & channel: max and
  *      first arg) -> plan->part_val / part_arg; Z rows -> plan->z;
@@ -187,6 +187,8 @@ typedef struct dr_large_plan {
   const int32_t* tile_slot;  /* [n_tiles] batch slot of each tile               */
   int32_t n_tiles;
   int32_t k0_max;            /* >= every n_k0 of the batch                      */
+  int32_t tile_rows;         /* nodes per tile: multiple of 16, <= DR_LARGE_TILE */
+  int32_t pad0;
   float* z;                  /* [z_row0[B], x_stride] workspace                 */
   float* part_val;           /* [n_tiles, k0_max, 32] workspace                 */
   int32_t* part_arg;         /* [n_tiles, k0_max, 32] workspace                 */
