@@ -103,6 +103,20 @@ class VanillaScratchC(ctypes.Structure):
     _fields_ = [("base", VP), ("row0", VP), ("row_slot", VP), ("n_rows", ctypes.c_int64), ("chunk_first", VP), ("chunk_slot", VP), ("n_chunks", ctypes.c_int32), ("pad0", ctypes.c_int32), ("part", VP)]
 
 
+class PackInputC(ctypes.Structure):
+    _fields_ = [
+        ("n_graphs", ctypes.c_int32), ("n_feat", ctypes.c_int32), ("n_edge_feat", ctypes.c_int32), ("require_clusters", ctypes.c_int32),
+        ("node_off", VP), ("edge_off", VP), ("c1_off", VP), ("edge_index", VP), ("edge_attr", VP), ("cluster0", VP), ("cluster1", VP),
+    ]  # fmt: skip
+
+
+class PackOutputC(ctypes.Structure):
+    _fields_ = [(n, VP) for n in (
+        "k0_off", "p1_off", "k1_off", "rowptr", "col", "eperm", "t_rowptr", "t_col", "t_eid", "m0_ptr", "m0_idx", "cl0",
+        "p1_rowptr", "p1_col", "p1t_rowptr", "p1t_col", "m1_ptr", "m1_idx", "cl1", "edge_attr",
+    )]  # fmt: skip
+
+
 class PassC(ctypes.Structure):
     _fields_ = [
         ("flags", ctypes.c_int32),
@@ -184,6 +198,8 @@ SIGNATURES = [
     ("dr_segment_max", ctypes.c_int, [VP, VP, VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP, VP, VP]),
     ("dr_segment_max_bwd", ctypes.c_int, [VP, VP, VP, VP, VP, VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP, VP]),
     ("dr_segment_mean", ctypes.c_int, [VP, VP, VP, ctypes.c_int32, ctypes.c_int32, VP, VP]),
+    ("dr_pack_sizes", ctypes.c_int, [ctypes.POINTER(PackInputC), VP, VP, VP, ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32]),
+    ("dr_pack_fill", ctypes.c_int, [ctypes.POINTER(PackInputC), ctypes.POINTER(PackOutputC), VP, ctypes.c_int32]),
     ("dr_dropout_mask", ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int32, ctypes.c_float, VP]),
     ("dr_version", ctypes.c_char_p, []),
     ("dr_device_arch", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32]),

@@ -109,137 +109,102 @@ def _dense(ids, what):
     return inv.astype(np.int64), int(uniq.size)
 
 
-def pack_graphs(records: list[GraphRecord], require_clusters: bool = True) -> PackedGraphs:  # noqa: PLR0915, C901
+def pack_graphs(records: list[GraphRecord], require_clusters: bool = True, threads: int = 0) -> PackedGraphs:
+    """Pack per-graph records into the store layout with the native host
+    packer (``dr_pack_sizes`` / ``dr_pack_fill``, threads over graphs)."""
+    import ctypes  # noqa: PLC0415
+
+    from deeprank2_amd import _lib  # noqa: PLC0415
+
     if not records:
         msg = "empty graph list"
         raise ValueError(msg)
-    F = int(records[0].x.shape[1])
-    xs, rps, cols, eperms, trps, tcols, teids = [], [], [], [], [], [], []
-    m0ps, m0is, cl0s, p1rps, p1cs, p1trps, p1tcs, m1ps, m1is, cl1s, ys, eas = ([] for _ in range(12))
-    node_off = [0]
-    edge_off = [0]
-    k0_off = [0]
-    p1_off = [0]
-    k1_off = [0]
-    aliased = True
-    has_clusters = True
+    G = len(records)
+    F = int(np.asarray(records[0].x).shape[1])
+    xs, eis, c0s, c1s, ys, eas = [], [], [], [], [], []
+    node_off = np.zeros(G + 1, np.int64)
+    edge_off = np.zeros(G + 1, np.int64)
+    c1_off = np.zeros(G + 1, np.int64)
     has_ea = records[0].edge_attr is not None
+    has_clusters = all(r.cluster0 is not None and r.cluster1 is not None for r in records)
+    if require_clusters and not has_clusters:
+        g = next(i for i, r in enumerate(records) if r.cluster0 is None or r.cluster1 is None)
+        msg = f"graph {g} ({records[g].name}) has no cluster0/cluster1 (set clustering_method when building the dataset)"
+        raise ValueError(msg)
     for gi, r in enumerate(records):
-        x = np.ascontiguousarray(r.x, dtype=np.float32)
+        x = np.asarray(r.x, dtype=np.float32)
         if x.ndim != 2 or x.shape[1] != F:
             msg = f"graph {gi}: x must be [N, {F}]"
             raise ValueError(msg)
         n = x.shape[0]
-        if n == 0:
-            msg = f"graph {gi} has no nodes (torch.max over an empty cluster would fail in the reference)"
-            raise ValueError(msg)
         ei = np.asarray(r.edge_index, dtype=np.int64).reshape(2, -1)
-        e = ei.shape[1]
-        if e and (ei.min() < 0 or ei.max() >= n):
-            msg = f"graph {gi}: edge_index out of range [0, {n})"
-            raise ValueError(msg)
-        row, col = ei[0], ei[1]
-        rp, cs, perm = _csr(row, col, n)
-        trp, tcs, tperm = _csr(col, row, n)
-        inv = np.empty(e, dtype=np.int32)
-        inv[perm] = np.arange(e, dtype=np.int32)
-        teids.append(inv[tperm])
-        sym = _same_multiset(row, col, col, row, n)
-        aliased &= sym
         xs.append(x)
-        rps.append(rp)
-        cols.append(cs)
-        eperms.append(perm)
-        trps.append(trp)
-        tcols.append(tcs)
-        if has_ea:
-            ea = np.asarray(r.edge_attr, dtype=np.float32).reshape(e, -1)
-            eas.append(ea[perm])
-
-        if r.cluster0 is None or r.cluster1 is None:
-            if require_clusters:
-                msg = f"graph {gi} ({r.name}) has no cluster0/cluster1 (set clustering_method when building the dataset)"
+        eis.append(ei)
+        node_off[gi + 1] = node_off[gi] + n
+        edge_off[gi + 1] = edge_off[gi] + ei.shape[1]
+        if has_clusters:
+            c0 = np.asarray(r.cluster0, dtype=np.int64).reshape(-1)
+            if len(c0) != n:
+                msg = f"graph {gi}: cluster0 has {len(c0)} entries for {n} nodes"
                 raise ValueError(msg)
-            c0 = np.zeros(n, dtype=np.int64)
-            c1 = np.zeros(1, dtype=np.int64)
-            has_clusters = False
-        else:
-            c0, c1 = r.cluster0, r.cluster1
-        if len(c0) != n:
-            msg = f"graph {gi}: cluster0 has {len(c0)} entries for {n} nodes"
-            raise ValueError(msg)
-        d0, k0 = _dense(c0, "cluster0")
-        m0i = np.argsort(d0, kind="stable").astype(np.int32)
-        m0p = np.zeros(k0 + 1, dtype=np.int32)
-        np.cumsum(np.bincount(d0, minlength=k0), out=m0p[1:])
-        # pool_edge: relabel, remove self loops, coalesce (unique, sorted by (row, col))
-        pr, pc = d0[row], d0[col]
-        keep = pr != pc
-        key = np.unique(pr[keep] * k0 + pc[keep])
-        prow, pcol = key // k0, key % k0
-        p1rp = np.zeros(k0 + 1, dtype=np.int32)
-        np.cumsum(np.bincount(prow, minlength=k0), out=p1rp[1:])
-        tkey = np.unique(pcol * k0 + prow)
-        p1trp = np.zeros(k0 + 1, dtype=np.int32)
-        np.cumsum(np.bincount(tkey // k0, minlength=k0), out=p1trp[1:])
-
-        c1 = np.asarray(c1, dtype=np.int64).reshape(-1)
-        if len(c1) != k0:
-            msg = f"graph {gi}: cluster1 has {len(c1)} entries but cluster0 defines {k0} clusters"
-            raise ValueError(msg)
-        d1, k1 = _dense(c1, "cluster1")
-        m1i = np.argsort(d1, kind="stable").astype(np.int32)
-        m1p = np.zeros(k1 + 1, dtype=np.int32)
-        np.cumsum(np.bincount(d1, minlength=k1), out=m1p[1:])
-
-        m0ps.append(m0p)
-        m0is.append(m0i)
-        cl0s.append(d0.astype(np.int32))
-        p1rps.append(p1rp)
-        p1cs.append(pcol.astype(np.int32))
-        p1trps.append(p1trp)
-        p1tcs.append((tkey % k0).astype(np.int32))
-        m1ps.append(m1p)
-        m1is.append(m1i)
-        cl1s.append(d1.astype(np.int32))
+            c1 = np.asarray(r.cluster1, dtype=np.int64).reshape(-1)
+            c0s.append(c0)
+            c1s.append(c1)
+            c1_off[gi + 1] = c1_off[gi] + len(c1)
         ys.append(np.nan if r.y is None else float(np.asarray(r.y).reshape(-1)[0]))
-        node_off.append(node_off[-1] + n)
-        edge_off.append(edge_off[-1] + e)
-        k0_off.append(k0_off[-1] + k0)
-        p1_off.append(p1_off[-1] + prow.size)
-        k1_off.append(k1_off[-1] + k1)
+        if has_ea:
+            eas.append(np.asarray(r.edge_attr, dtype=np.float32).reshape(ei.shape[1], -1))
+    x = np.concatenate(xs) if G else np.zeros((0, F), np.float32)
+    ei_all = np.ascontiguousarray(np.concatenate(eis, axis=1)) if G else np.zeros((2, 0), np.int64)
+    ea_all = np.ascontiguousarray(np.concatenate(eas)) if has_ea else None
+    fe = 0 if ea_all is None else ea_all.shape[1]
+    c0_all = np.ascontiguousarray(np.concatenate(c0s)) if has_clusters else None
+    c1_all = np.ascontiguousarray(np.concatenate(c1s)) if has_clusters else None
 
-    cat = np.concatenate
+    lib = _lib.load()
+    P = lambda a: None if a is None else a.ctypes.data  # noqa: E731
+    inp = _lib.PackInputC()
+    inp.n_graphs, inp.n_feat, inp.n_edge_feat, inp.require_clusters = G, F, fe, int(require_clusters)
+    inp.node_off, inp.edge_off, inp.c1_off = P(node_off), P(edge_off), P(c1_off)
+    inp.edge_index, inp.edge_attr, inp.cluster0, inp.cluster1 = P(ei_all), P(ea_all), P(c0_all), P(c1_all)
+    k0c, p1c, k1c = np.zeros(G, np.int64), np.zeros(G, np.int64), np.zeros(G, np.int64)
+    sym = ctypes.c_int32(0)
+    err = ctypes.create_string_buffer(256)
+    rc = lib.dr_pack_sizes(inp, P(k0c), P(p1c), P(k1c), threads, err, 256)
+    if rc != 0:
+        raise ValueError(err.value.decode() or "invalid graphs")
+    k0_off = np.concatenate([[0], np.cumsum(k0c)]).astype(np.int64)
+    p1_off = np.concatenate([[0], np.cumsum(p1c)]).astype(np.int64)
+    k1_off = np.concatenate([[0], np.cumsum(k1c)]).astype(np.int64)
+    N, E, K0, P1, K1 = int(node_off[-1]), int(edge_off[-1]), int(k0_off[-1]), int(p1_off[-1]), int(k1_off[-1])
+    i32 = lambda m: np.empty(max(m, 0), np.int32)  # noqa: E731
+    out = {
+        "rowptr": i32(N + G), "col": i32(E), "eperm": i32(E), "t_rowptr": i32(N + G), "t_col": i32(E), "t_eid": i32(E),
+        "m0_ptr": i32(K0 + G), "m0_idx": i32(N), "cl0": i32(N), "p1_rowptr": i32(K0 + G), "p1_col": i32(P1),
+        "p1t_rowptr": i32(K0 + G), "p1t_col": i32(P1), "m1_ptr": i32(K1 + G), "m1_idx": i32(K0), "cl1": i32(K0),
+    }  # fmt: skip
+    ea_csr = np.empty((E, fe), np.float32) if fe else None
+    o = _lib.PackOutputC()
+    o.k0_off, o.p1_off, o.k1_off = P(k0_off), P(p1_off), P(k1_off)
+    for name, arr in out.items():
+        setattr(o, name, P(arr))
+    o.edge_attr = P(ea_csr)
+    _lib.check(lib.dr_pack_fill(inp, o, ctypes.addressof(sym), threads), "dr_pack_fill")
     return PackedGraphs(
         n_feat=F,
-        n_graphs=len(records),
-        x=cat(xs),
-        node_off=np.asarray(node_off, np.int64),
-        edge_off=np.asarray(edge_off, np.int64),
-        rowptr=cat(rps),
-        col=cat(cols),
-        eperm=cat(eperms),
-        t_rowptr=cat(trps),
-        t_col=cat(tcols),
-        t_eid=cat(teids),
-        transpose_aliased=bool(aliased),
-        k0_off=np.asarray(k0_off, np.int64),
-        m0_ptr=cat(m0ps),
-        m0_idx=cat(m0is),
-        cl0=cat(cl0s),
-        p1_off=np.asarray(p1_off, np.int64),
-        p1_rowptr=cat(p1rps),
-        p1_col=cat(p1cs) if p1cs else np.zeros(0, np.int32),
-        p1t_rowptr=cat(p1trps),
-        p1t_col=cat(p1tcs) if p1tcs else np.zeros(0, np.int32),
-        k1_off=np.asarray(k1_off, np.int64),
-        m1_ptr=cat(m1ps),
-        m1_idx=cat(m1is),
-        cl1=cat(cl1s),
+        n_graphs=G,
+        x=x,
+        node_off=node_off,
+        edge_off=edge_off,
+        transpose_aliased=bool(sym.value),
+        k0_off=k0_off,
+        p1_off=p1_off,
+        k1_off=k1_off,
         y=np.asarray(ys, dtype=np.float32),
-        edge_attr=cat(eas) if has_ea else None,
+        edge_attr=ea_csr if has_ea else None,
         names=[r.name for r in records],
         has_clusters=has_clusters,
+        **out,
     )
 
 

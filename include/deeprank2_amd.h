@@ -38,6 +38,9 @@
  *                           torch_scatter scatter_max / scatter_mean and PyG
  *                           max_pool_x behind community_pooling / max_pool_x
  *                           (community_pooling.py:165-242; ginet.py:103)
+ *   dr_pack_sizes / dr_pack_fill   GraphDataset collate + per-graph pooling
+ *                           index work (host; dataset.py:883-1052, trainer.py:541,
+ *                           community_pooling.py:23-27,205-225)
  *   dr_csr_from_coo         the ordering torch_scatter's CPU scatter_add_
  *                           implies for edge_index[0] (ginet.py:41,58): a stable
  *                           row-sorted CSR, built on the device
@@ -384,6 +387,41 @@ int dr_segment_max_bwd(const int32_t* segptr, const int32_t* members, const floa
                        int32_t mode, float* dx, void* stream);
 int dr_segment_mean(const int32_t* segptr, const int32_t* members, const float* x, int32_t n_seg, int32_t n_chan,
                     float* out, void* stream);
+
+/* ---- host-side graph packer (deeprank2_amd/store.py) ----------------------
+ * Per-graph arrays as GraphDataset.load_one_graph returns them
+ * (dataset.py:883-1052) -> the packed store layout: stable CSR by
+ * edge_index[0] and its transpose with slot maps, dense depth-0 ids + member
+ * lists, the coalesced pooled graph of pool_edge (+ transpose), depth-1 member
+ * lists (the collate of trainer.py:541 plus community_pooling.py:23-27,205-225
+ * done once per graph).  Host memory only; threads over graphs.              */
+typedef struct dr_pack_input {
+  int32_t n_graphs, n_feat, n_edge_feat, require_clusters;
+  const int64_t* node_off;   /* [G+1]                                          */
+  const int64_t* edge_off;   /* [G+1]                                          */
+  const int64_t* c1_off;     /* [G+1] offsets into cluster1                    */
+  const int64_t* edge_index; /* [2, E_all] local ids: sources, then targets    */
+  const float* edge_attr;    /* [E_all, Fe] or NULL                            */
+  const int64_t* cluster0;   /* [N_all] or NULL                                */
+  const int64_t* cluster1;   /* [c1_off[G]] or NULL                            */
+} dr_pack_input;
+
+typedef struct dr_pack_output {
+  const int64_t *k0_off, *p1_off, *k1_off; /* [G+1] prefix sums of dr_pack_sizes' counts */
+  int32_t *rowptr, *col, *eperm, *t_rowptr, *t_col, *t_eid; /* rowptr/t_rowptr [N_all+G], others [E_all] */
+  int32_t *m0_ptr, *m0_idx, *cl0;         /* [K0_all+G], [N_all], [N_all]     */
+  int32_t *p1_rowptr, *p1_col, *p1t_rowptr, *p1t_col; /* [K0_all+G], [P1_all]  */
+  int32_t *m1_ptr, *m1_idx, *cl1;         /* [K1_all+G], [K0_all], [K0_all]   */
+  float* edge_attr;                       /* [E_all, Fe] in CSR order, or NULL */
+} dr_pack_output;
+
+/* Pass 1: per-graph K0, pooled-edge and K1 counts.  On invalid input returns
+ * DR_E_ARG with a message in err.  threads <= 0: min(16, hardware threads). */
+int dr_pack_sizes(const dr_pack_input* in, int64_t* k0_count, int64_t* p1_count, int64_t* k1_count,
+                  int32_t threads, char* err, int32_t err_len);
+/* Pass 2: fill the caller-allocated outputs; *symmetric = every graph's edge
+ * multiset is symmetric (then the pooled transposes equal the pooled CSRs). */
+int dr_pack_fill(const dr_pack_input* in, const dr_pack_output* out, int32_t* symmetric, int32_t threads);
 
 /* Host-side replica of the in-kernel dropout RNG (DR_DROPOUT_HASH): writes
  * keep[i] for i in [0, n) (i = 128*b + r) into a host buffer.             */

@@ -115,3 +115,56 @@ def test_store_model_vs_oracle_random_ties():
     np.testing.assert_allclose(mout, out.detach().numpy(), rtol=1e-5, atol=1e-5)
     for i, n in enumerate(PARAM_NAMES):
         np.testing.assert_allclose(grads[i], dict(model.named_parameters())[n].grad.numpy(), rtol=1e-4, atol=1e-5, err_msg=n)
+
+
+def _random_records(seed, n_graphs=12, asym=True):
+    from deeprank2_amd.store import GraphRecord
+
+    rng = np.random.default_rng(seed)
+    recs = []
+    for g in range(n_graphs):
+        n = int(rng.integers(1, 40))
+        e = int(rng.integers(0, 4 * n))
+        ei = rng.integers(0, n, size=(2, e))
+        if not asym:
+            ei = np.concatenate([ei, ei[::-1]], 1)
+        if g % 3 == 0 and n > 2:  # duplicates and self loops
+            ei = np.concatenate([ei, np.array([[0, 0, 1], [0, 1, 1]])], 1)
+        k = int(rng.integers(1, min(n, 6) + 1))
+        c0 = rng.integers(0, k, size=n) * (3 if g % 2 else 1)  # non-consecutive ids
+        k0 = len(np.unique(c0))
+        c1 = rng.integers(0, 2, size=k0)
+        recs.append(GraphRecord(x=rng.normal(size=(n, 7)).astype(np.float32), edge_index=ei, edge_attr=rng.normal(size=(ei.shape[1], 2)).astype(np.float32), cluster0=c0, cluster1=c1, y=float(g), name=f"r{g}"))
+    return recs
+
+
+@pytest.mark.parametrize("asym", [True, False])
+def test_native_packer_matches_numpy_model(asym):
+    from pack_model import pack_graphs_numpy
+
+    recs = _random_records(11 + asym, asym=asym)
+    a, b = pack_graphs(recs), pack_graphs_numpy(recs)
+    for f in ("node_off", "edge_off", "rowptr", "col", "eperm", "t_rowptr", "t_col", "t_eid", "k0_off", "m0_ptr", "m0_idx", "cl0", "p1_off", "p1_rowptr", "p1_col", "p1t_rowptr", "p1t_col", "k1_off", "m1_ptr", "m1_idx", "cl1", "edge_attr", "x", "y"):
+        np.testing.assert_array_equal(getattr(a, f), getattr(b, f), err_msg=f)
+    assert a.transpose_aliased == b.transpose_aliased
+
+
+def test_native_packer_errors_and_missing_clusters():
+    recs = _random_records(3, n_graphs=4)
+    recs[2].cluster1 = np.array([0])
+    recs[2].cluster0 = np.array([0, 5] * 50)[: len(recs[2].x)]
+    if len(np.unique(recs[2].cluster0)) != 1:
+        with pytest.raises(ValueError, match="cluster1"):
+            pack_graphs(recs)
+    recs = _random_records(4, n_graphs=3)
+    recs[1].edge_index = np.array([[0], [999]])
+    recs[1].edge_attr = np.zeros((1, 2), np.float32)
+    with pytest.raises(ValueError, match="out of range"):
+        pack_graphs(recs)
+    recs = _random_records(5, n_graphs=3)
+    for r in recs:
+        r.cluster0 = r.cluster1 = None
+    with pytest.raises(ValueError, match="cluster0/cluster1"):
+        pack_graphs(recs)
+    p = pack_graphs(recs, require_clusters=False)
+    assert not p.has_clusters and p.m1_ptr.tolist() == [0, 1] * 3
