@@ -117,6 +117,10 @@ class PackOutputC(ctypes.Structure):
     )]  # fmt: skip
 
 
+class MclGraphsC(ctypes.Structure):
+    _fields_ = [(n, VP) for n in ("node_off", "rowptr", "edge_off", "col", "weight", "ws_off", "ws", "pat_off", "pattern", "iters")]
+
+
 class PassC(ctypes.Structure):
     _fields_ = [
         ("flags", ctypes.c_int32),
@@ -200,6 +204,9 @@ SIGNATURES = [
     ("dr_segment_mean", ctypes.c_int, [VP, VP, VP, ctypes.c_int32, ctypes.c_int32, VP, VP]),
     ("dr_pack_sizes", ctypes.c_int, [ctypes.POINTER(PackInputC), VP, VP, VP, ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32]),
     ("dr_pack_fill", ctypes.c_int, [ctypes.POINTER(PackInputC), ctypes.POINTER(PackOutputC), VP, ctypes.c_int32]),
+    ("dr_mcl_workspace_doubles", ctypes.c_int64, [ctypes.c_int32]),
+    ("dr_mcl", ctypes.c_int, [ctypes.POINTER(MclGraphsC), ctypes.c_int32, ctypes.c_int32, ctypes.c_double, VP]),
+    ("dr_mcl_assign", ctypes.c_int, [VP, VP, VP, ctypes.c_int32, VP, VP]),
     ("dr_dropout_mask", ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int32, ctypes.c_float, VP]),
     ("dr_version", ctypes.c_char_p, []),
     ("dr_device_arch", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32]),

@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import inspect
 import logging
+import os
 import re
 import warnings
 from typing import Literal
@@ -46,6 +47,13 @@ INDEX = "_index"
 POSITION = "_position"
 REGRESS, CLASSIF = "regress", "classif"
 _TARGET_TASK = {"irmsd": REGRESS, "lrmsd": REGRESS, "fnat": REGRESS, "dockq": REGRESS, "binary": CLASSIF, "capri_class": CLASSIF}
+# Clusters computed by Trainer._precluster, keyed (abspath, entry, method).
+# The reference rewrites clustering/<method>/depth_{0,1} inside the HDF5 file
+# (trainer.py:334-346), so every dataset opened on that file afterwards sees
+# them; this registry gives the same view within the process without
+# modifying the user's files.
+_PRECLUSTERED: dict = {}
+_PRECLUSTER_VERSION = [0]  # bumped on every install: packed stores keyed on it
 _COND = re.compile(r"^\s*(>=|<=|==|!=|>|<)\s*([-+0-9.eE]+)\s*$")
 
 
@@ -408,7 +416,10 @@ class GraphDataset:
         out["y"] = y
         out["pos"] = np.asarray(grp[f"{NODE}/{POSITION}"], dtype=np.float32)
         out["cluster0"] = out["cluster1"] = None
-        if self.clustering_method is not None:
+        pre = _PRECLUSTERED.get((os.path.abspath(fname), entry_name, self.clustering_method)) if self.clustering_method is not None else None
+        if pre is not None:
+            out["cluster0"], out["cluster1"] = pre
+        elif self.clustering_method is not None:
             k0 = f"clustering/{self.clustering_method}/depth_0"
             k1 = f"clustering/{self.clustering_method}/depth_1"
             if k0 in grp and k1 in grp:
@@ -417,6 +428,16 @@ class GraphDataset:
             else:
                 _log.warning("no clusters detected")
         return out
+
+    def set_clusters(self, clusters: dict) -> None:
+        """Install ``{(fname, entry_name): (depth_0, depth_1)}`` for
+        ``clustering_method``: what ``Trainer._precluster`` writes into the
+        HDF5 file in the reference, kept in a process-wide registry here (every
+        dataset on that file sees it); drops packed stores."""
+        for (f, e), (a, b) in clusters.items():
+            _PRECLUSTERED[(os.path.abspath(f), e, self.clustering_method)] = (np.asarray(a, dtype=np.int64), np.asarray(b, dtype=np.int64))
+        _PRECLUSTER_VERSION[0] += 1
+        self._stores = {}
 
     def load_one_graph(self, fname: str, entry_name: str) -> Data:
         """dataset.py:883-1052 -> ``Data``."""
@@ -447,7 +468,7 @@ class GraphDataset:
         from deeprank2_amd.store import GraphRecord, GraphStore, pack_graphs  # noqa: PLC0415
 
         device = torch.device(device)
-        key = (str(device), tuple(self.index_entries))
+        key = (str(device), tuple(self.index_entries), _PRECLUSTER_VERSION[0])
         st = self._stores.get(key)
         if st is None:
             recs = []

@@ -25,9 +25,9 @@ no CPU path; ``cuda=False`` is accepted and logged); a "best model"
 checkpoint is a snapshot (the reference keeps references to live tensors, so
 its in-memory best model follows later updates); checkpoints store the
 optimizer / loss / dataset types by name so that they load with
-``torch.load(weights_only=True)``; ``_precluster`` (MCL / Louvain, needs
-networkx / markov_clustering) is not provided: datasets must carry their
-stored ``clustering/<method>/depth_{0,1}``.
+``torch.load(weights_only=True)``; ``_precluster`` runs MCL for all graphs
+on the GPU and keeps the clusters in memory (the reference rewrites the HDF5
+files); Louvain is not recomputed (stored clusters are used).
 """
 
 from __future__ import annotations
@@ -78,6 +78,7 @@ class Trainer:
         cuda: bool = False,
         ngpu: int = 0,
         output_exporters: list | None = None,
+        precluster: bool = True,
     ):
         self.neuralnet = neuralnet
         self.pretrained_model = pretrained_model
@@ -127,9 +128,15 @@ class Trainer:
                 if self.clustering_method not in ("mcl", "louvain"):
                     msg = f"Invalid node clustering method: {self.clustering_method}. Please set clustering_method to 'mcl', 'louvain' or None."
                     raise ValueError(msg)
+                if precluster:
+                    self._precluster(self.dataset_train)
                 if self.dataset_val is None:
                     _log.warning("No validation dataset given. Randomly splitting training set in training set and validation set.")
                     self.dataset_train, self.dataset_val = _divide_dataset(self.dataset_train, splitsize=self.val_size)
+                elif precluster:
+                    self._precluster(self.dataset_val)
+                if self.dataset_test is not None and precluster:
+                    self._precluster(self.dataset_test)
         else:
             if self.neuralnet is None:
                 msg = "No neural network class found. Please add it to complete loading the pretrained model."
@@ -209,6 +216,27 @@ class Trainer:
         self._put_model_to_device(self.dataset_train)
         self.configure_optimizers()
         self.set_lossfunction()
+
+    def _precluster(self, dataset):
+        """trainer.py:319-348: MCL depth_0 on every graph, depth_1 on the
+        pooled graph, for all graphs at once on the GPU (``dr_mcl``).  The
+        reference writes the result into the HDF5 files; here it is installed
+        in the dataset (``GraphDataset.set_clusters``).  Louvain is not
+        provided (randomised; stored clusters are used with a warning)."""
+        if self.clustering_method.lower() != "mcl":
+            _log.warning(f"{self.clustering_method} clustering is not recomputed by deeprank2_amd: the clusters stored in the HDF5 files are used.")
+            return
+        if self.device.type != "cuda":
+            _log.warning("No GPU visible: MCL pre-clustering skipped, the clusters stored in the HDF5 files are used.")
+            return
+        from deeprank2_amd import clustering  # noqa: PLC0415
+
+        graphs = []
+        for fname, mol in dataset.index_entries:
+            a = dataset.graph_arrays(fname, mol)
+            graphs.append((a["edge_index"], a["pos"].shape[0]))
+        c0, c1 = clustering.precluster_graphs(graphs, self.device)
+        dataset.set_clusters({e: (a, b) for e, a, b in zip(dataset.index_entries, c0, c1)})
 
     def _put_model_to_device(self, dataset):
         if self.task == REGRESS:

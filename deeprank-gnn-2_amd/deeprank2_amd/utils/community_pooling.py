@@ -10,8 +10,9 @@ backward; ``dr_segment_mean``); cluster relabelling and edge coalescing are
 integer bookkeeping done with device tensor ops.
 Reference: ``deeprank2/utils/community_pooling.py:23-27,165-242``; PyG 2.4
 ``consecutive_cluster`` / ``pool_edge`` / ``pool_batch`` / ``max_pool_x``.
-MCL / Louvain clustering (``community_detection``) is not provided: graphs
-carry their stored ``clustering/<method>/depth_{0,1}``.
+``community_detection(method="mcl")`` runs the batched fp64 MCL kernel
+(``deeprank2_amd.clustering``); Louvain (randomised ``python-louvain``) is not
+provided.
 """
 
 from __future__ import annotations
@@ -89,6 +90,29 @@ def segment_mean(x, dense, n_seg):
     out = torch.empty(n_seg, x.shape[1], dtype=torch.float32, device=x.device)
     _lib.check(_lib.load().dr_segment_mean(segptr.data_ptr(), members.data_ptr(), x.data_ptr(), n_seg, x.shape[1], out.data_ptr(), _lib.stream_ptr(x.device)), "dr_segment_mean")
     return out
+
+
+def community_detection(edge_index, num_nodes: int, edge_attr=None, method: str = "mcl"):
+    """community_pooling.py:96-162: cluster id per node (int64, on
+    ``edge_index``'s device).  MCL runs on the GPU (``dr_mcl``) with
+    markov_clustering's defaults; ``edge_attr`` (one weight per edge) gives the
+    weighted adjacency networkx builds (last weight of a repeated pair wins)."""
+    if method == "louvain":
+        msg = "Louvain clustering (python-louvain best_partition, randomised) is not provided by deeprank2_amd; use method='mcl'"
+        raise NotImplementedError(msg)
+    if method != "mcl":
+        msg = f"Clustering method {method} not supported"
+        raise ValueError(msg)
+    from deeprank2_amd import clustering  # noqa: PLC0415
+
+    dev = edge_index.device if edge_index.is_cuda else None
+    if dev is None and not torch.cuda.is_available():
+        msg = "community_detection runs on the MI355X only (no CPU fallback by design)"
+        raise RuntimeError(msg)
+    ei = edge_index.detach().cpu().numpy()
+    w = None if edge_attr is None else [torch.as_tensor(edge_attr).detach().cpu().double().reshape(-1).numpy()]
+    (c,) = clustering.mcl_clusters([(ei, int(num_nodes))], dev, weights=w)
+    return torch.from_numpy(c).to(edge_index.device)
 
 
 def pool_edge(cluster, edge_index, edge_attr=None):

@@ -41,6 +41,9 @@
  *   dr_pack_sizes / dr_pack_fill   GraphDataset collate + per-graph pooling
  *                           index work (host; dataset.py:883-1052, trainer.py:541,
  *                           community_pooling.py:23-27,205-225)
+ *   dr_mcl / dr_mcl_assign  community_detection(method="mcl") of
+ *                           Trainer._precluster (community_pooling.py:96-162,
+ *                           trainer.py:319-348)
  *   dr_csr_from_coo         the ordering torch_scatter's CPU scatter_add_
  *                           implies for edge_index[0] (ginet.py:41,58): a stable
  *                           row-sorted CSR, built on the device
@@ -422,6 +425,29 @@ int dr_pack_sizes(const dr_pack_input* in, int64_t* k0_count, int64_t* p1_count,
 /* Pass 2: fill the caller-allocated outputs; *symmetric = every graph's edge
  * multiset is symmetric (then the pooled transposes equal the pooled CSRs). */
 int dr_pack_fill(const dr_pack_input* in, const dr_pack_output* out, int32_t* symmetric, int32_t threads);
+
+/* ---- MCL community detection (community_pooling.py:96-162, as run by
+ * Trainer._precluster, trainer.py:319-348; markov_clustering 0.0.6 defaults) --
+ * One workgroup per graph, float64 like the reference.  All pointers in
+ * dr_mcl_graphs are device pointers.                                          */
+typedef struct dr_mcl_graphs {
+  const int64_t* node_off; /* [G+1]                                             */
+  const int32_t* rowptr;   /* local CSR, graph g's rows at node_off[g] + g      */
+  const int64_t* edge_off; /* [G+1]                                             */
+  const int32_t* col;      /* local columns, graph g's at edge_off[g]           */
+  const double* weight;    /* edge weights at edge_off (symmetric, coalesced), or NULL = 1 */
+  const int64_t* ws_off;   /* [G+1] workspace offsets in doubles (dr_mcl_workspace_doubles per graph) */
+  double* ws;
+  const int64_t* pat_off;  /* [G+1] offsets of each graph's N*N support pattern  */
+  uint8_t* pattern;        /* converged support, row-major 0/1                   */
+  int32_t* iters;          /* [G] iterations run, or NULL                        */
+} dr_mcl_graphs;
+int64_t dr_mcl_workspace_doubles(int32_t n_nodes);
+int dr_mcl(const dr_mcl_graphs* graphs, int32_t n_graphs, int32_t max_iter, double pruning_threshold, void* stream);
+/* Host: get_clusters + the reference's index assignment from the patterns
+ * (host copies): cluster_out [N_all] at node_off, n_clusters [G] or NULL.  */
+int dr_mcl_assign(const uint8_t* pattern, const int64_t* pat_off, const int64_t* node_off, int32_t n_graphs,
+                  int32_t* cluster_out, int32_t* n_clusters);
 
 /* Host-side replica of the in-kernel dropout RNG (DR_DROPOUT_HASH): writes
  * keep[i] for i in [0, n) (i = 128*b + r) into a host buffer.             */

@@ -45,3 +45,20 @@ def assert_grad_close(actual, ref, rtol=1e-4, ntol=1e-6, err_msg=""):
     ref = np.asarray(ref)
     scale = float(np.abs(ref).max()) if ref.size else 0.0
     np.testing.assert_allclose(np.asarray(actual), ref, rtol=rtol, atol=max(1e-6, ntol * scale), err_msg=err_msg)
+
+
+def golden_graphs(z):
+    """Per-graph (local edge_index, num_nodes, cluster0, cluster1) of a stored
+    collated batch (``in/ptr`` node offsets; cluster1 has one entry per
+    depth-0 cluster of each graph)."""
+    ptr, ei, c0, c1 = (np.asarray(z[f"in/{k}"]) for k in ("ptr", "edge_index", "cluster0", "cluster1"))
+    out, k1 = [], 0
+    for g in range(ptr.size - 1):
+        lo, hi = int(ptr[g]), int(ptr[g + 1])
+        m = (ei[0] >= lo) & (ei[0] < hi)
+        a = c0[lo:hi]
+        k = int(a.max()) + 1 if a.size else 0
+        out.append((ei[:, m] - lo, hi - lo, a, c1[k1 : k1 + k]))
+        k1 += k
+    assert k1 == c1.size
+    return out

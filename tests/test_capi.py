@@ -44,6 +44,7 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_lib.LargePlanC) == 3 * 8 + 16 + 3 * 8
     assert ctypes.sizeof(_lib.PassC) == 16 + 8 + 16 + 8 + 9 * 8
     assert ctypes.sizeof(_lib.AdamC) == 32 + 8
+    assert ctypes.sizeof(_lib.MclGraphsC) == 10 * 8
     assert ctypes.sizeof(_lib.ParamTableC) == 4 * 24 * 8 + 24 * 4 + 24 * 16 + 16
 
 

@@ -104,7 +104,7 @@ def test_foutnet_trainer_adam_matches_oracle_replay(files):
     tr, va = _sets(files[0], files[1])
     mem = MemoryOutputExporter()
     torch.manual_seed(4)
-    t = Trainer(FoutNet, tr, va, cuda=True, output_exporters=[mem])
+    t = Trainer(FoutNet, tr, va, cuda=True, output_exporters=[mem], precluster=False)  # keep the connected k-means clusters
     model_o = gnn_ref.FoutNet(30, 1)
     model_o.load_state_dict({k: v.cpu() for k, v in t.model.state_dict().items()})
     t.train(nepoch=3, batch_size=8, shuffle=False, validate=True, best_model=False, filename=None)
@@ -125,7 +125,7 @@ def test_foutnet_trainer_sgd_generic_path_matches_oracle(files):
     tr, va = _sets(files[0], files[1])
     mem = MemoryOutputExporter()
     torch.manual_seed(5)
-    t = Trainer(FoutNet, tr, va, cuda=True, output_exporters=[mem])
+    t = Trainer(FoutNet, tr, va, cuda=True, output_exporters=[mem], precluster=False)  # keep the connected k-means clusters
     t.configure_optimizers(torch.optim.SGD, lr=0.01, weight_decay=0.0)
     model_o = gnn_ref.FoutNet(30, 1)
     model_o.load_state_dict({k: v.cpu() for k, v in t.model.state_dict().items()})
