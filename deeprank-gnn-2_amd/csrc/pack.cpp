@@ -178,6 +178,24 @@ void fill(Ctx& c, const dr_pack_output& o, int g) {
     for (int k = 0; k < L.k0; ++k) cnt[k + 1] += cnt[k];
     std::memcpy(trp, cnt.data(), sizeof(int32_t) * (L.k0 + 1));
     for (int64_t q = 0; q < P; ++q) o.p1t_col[q0 + q] = (int32_t)(tk[q] % L.k0);
+    // transposed slot (b, a) -> pooled CSR slot of the edge a -> b
+    if (o.p1t_pid)
+      for (int64_t q = 0; q < P; ++q) {
+        const int64_t key = (tk[q] % L.k0) * L.k0 + tk[q] / L.k0;
+        o.p1t_pid[q0 + q] = (int32_t)(std::lower_bound(L.pkey.begin(), L.pkey.end(), key) - L.pkey.begin());
+      }
+    // pooled edge_attr: PyG coalesce sums the attributes of merged edges, in
+    // input edge order (community_pooling.py:212 -> pool_edge)
+    if (o.p1_ea && Fe > 0 && in.edge_attr) {
+      float* pe = o.p1_ea + q0 * Fe;
+      std::fill(pe, pe + P * Fe, 0.f);
+      for (int64_t e = 0; e < E; ++e) {
+        const int64_t pr = L.dense0[src[e]], pc = L.dense0[dst[e]];
+        if (pr == pc) continue;
+        const int64_t q = std::lower_bound(L.pkey.begin(), L.pkey.end(), pr * L.k0 + pc) - L.pkey.begin();
+        for (int f = 0; f < Fe; ++f) pe[q * Fe + f] += in.edge_attr[(e0 + e) * Fe + f];
+      }
+    }
   }
   // depth-1 members
   {

@@ -69,6 +69,8 @@ class GraphStoreC(ctypes.Structure):
         ("t_eid", VP),
         ("n_edge_feat", ctypes.c_int32),
         ("pad0", ctypes.c_int32),
+        ("p1_ea", VP),
+        ("p1t_pid", VP),
     ]
 
 
@@ -113,7 +115,7 @@ class PackInputC(ctypes.Structure):
 class PackOutputC(ctypes.Structure):
     _fields_ = [(n, VP) for n in (
         "k0_off", "p1_off", "k1_off", "rowptr", "col", "eperm", "t_rowptr", "t_col", "t_eid", "m0_ptr", "m0_idx", "cl0",
-        "p1_rowptr", "p1_col", "p1t_rowptr", "p1t_col", "m1_ptr", "m1_idx", "cl1", "edge_attr",
+        "p1_rowptr", "p1_col", "p1t_rowptr", "p1t_col", "m1_ptr", "m1_idx", "cl1", "edge_attr", "p1_ea", "p1t_pid",
     )]  # fmt: skip
 
 

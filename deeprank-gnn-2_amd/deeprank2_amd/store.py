@@ -66,12 +66,14 @@ class PackedGraphs:
     p1_col: np.ndarray
     p1t_rowptr: np.ndarray
     p1t_col: np.ndarray
+    p1t_pid: np.ndarray  # pooled transposed slot -> pooled CSR slot (local)
     k1_off: np.ndarray
     m1_ptr: np.ndarray
     m1_idx: np.ndarray
     cl1: np.ndarray
     y: np.ndarray
     edge_attr: np.ndarray | None  # [E_all, Fe] in CSR order
+    p1_ea: np.ndarray | None  # [P1_all, Fe] pooled edge_attr (PyG coalesce: sums of merged edges)
     names: list = field(default_factory=list)
     has_clusters: bool = True  # False: cluster0/1 were missing and filled with one cluster per graph
 
@@ -181,14 +183,16 @@ def pack_graphs(records: list[GraphRecord], require_clusters: bool = True, threa
     out = {
         "rowptr": i32(N + G), "col": i32(E), "eperm": i32(E), "t_rowptr": i32(N + G), "t_col": i32(E), "t_eid": i32(E),
         "m0_ptr": i32(K0 + G), "m0_idx": i32(N), "cl0": i32(N), "p1_rowptr": i32(K0 + G), "p1_col": i32(P1),
-        "p1t_rowptr": i32(K0 + G), "p1t_col": i32(P1), "m1_ptr": i32(K1 + G), "m1_idx": i32(K0), "cl1": i32(K0),
+        "p1t_rowptr": i32(K0 + G), "p1t_col": i32(P1), "p1t_pid": i32(P1), "m1_ptr": i32(K1 + G), "m1_idx": i32(K0), "cl1": i32(K0),
     }  # fmt: skip
     ea_csr = np.empty((E, fe), np.float32) if fe else None
+    p1_ea = np.empty((P1, fe), np.float32) if fe else None
     o = _lib.PackOutputC()
     o.k0_off, o.p1_off, o.k1_off = P(k0_off), P(p1_off), P(k1_off)
     for name, arr in out.items():
         setattr(o, name, P(arr))
     o.edge_attr = P(ea_csr)
+    o.p1_ea = P(p1_ea)
     _lib.check(lib.dr_pack_fill(inp, o, ctypes.addressof(sym), threads), "dr_pack_fill")
     return PackedGraphs(
         n_feat=F,
@@ -202,6 +206,7 @@ def pack_graphs(records: list[GraphRecord], require_clusters: bool = True, threa
         k1_off=k1_off,
         y=np.asarray(ys, dtype=np.float32),
         edge_attr=ea_csr if has_ea else None,
+        p1_ea=p1_ea if has_ea else None,
         names=[r.name for r in records],
         has_clusters=has_clusters,
         **out,
@@ -323,6 +328,11 @@ class GraphStore:
         else:
             self.p1t_rowptr = t(p.p1t_rowptr)
             self.p1t_col = t(p.p1t_col if p.p1t_col.size else np.zeros(1, np.int32))
+        self.p1t_pid = t(p.p1t_pid if p.p1t_pid.size else np.zeros(1, np.int32))
+        pea = np.zeros((max(int(p.p1_off[-1]), 1), max(self.n_edge_feat, 1)), dtype=np.float32)
+        if self.n_edge_feat and p.p1_ea is not None:
+            pea[: p.p1_ea.shape[0]] = p.p1_ea
+        self.p1_ea = t(pea)
         self.k1_off = t(p.k1_off)
         self.m1_ptr = t(p.m1_ptr)
         self.m1_idx = t(p.m1_idx)
@@ -355,7 +365,7 @@ class GraphStore:
             s.n_feat = self.n_feat
             s.x_stride = self.x_stride
             s.transpose_aliased = int(self.packed.transpose_aliased)
-            for name in ("x", "node_off", "edge_off", "col_off", "rowptr", "col", "t_rowptr", "t_col", "k0_off", "m0_ptr", "m0_idx", "p1_off", "p1_rowptr", "p1_col", "p1t_rowptr", "p1t_col", "k1_off", "m1_ptr", "m1_idx", "y", "ea", "t_eid"):
+            for name in ("x", "node_off", "edge_off", "col_off", "rowptr", "col", "t_rowptr", "t_col", "k0_off", "m0_ptr", "m0_idx", "p1_off", "p1_rowptr", "p1_col", "p1t_rowptr", "p1t_col", "k1_off", "m1_ptr", "m1_idx", "y", "ea", "t_eid", "p1_ea", "p1t_pid"):
                 setattr(s, name, getattr(self, name).data_ptr())
             s.n_edge_feat = self.n_edge_feat
             self._c = s

@@ -98,6 +98,8 @@ typedef struct dr_graph_store {
   const int32_t* t_eid;      /* t_col slot -> CSR slot of the same edge (local), at col_off[g]+slot */
   int32_t n_edge_feat;       /* Fe                                            */
   int32_t pad0;
+  const float* p1_ea;        /* [P1_all, max(Fe,1)] pooled edge_attr: sums over merged edges (PyG coalesce) */
+  const int32_t* p1t_pid;    /* [P1_all] pooled transposed slot -> pooled CSR slot (local) */
 } dr_graph_store;
 
 /* One mini-batch slot: where graph `gid` lives in the store (64 bytes, so a
@@ -416,6 +418,8 @@ typedef struct dr_pack_output {
   int32_t *p1_rowptr, *p1_col, *p1t_rowptr, *p1t_col; /* [K0_all+G], [P1_all]  */
   int32_t *m1_ptr, *m1_idx, *cl1;         /* [K1_all+G], [K0_all], [K0_all]   */
   float* edge_attr;                       /* [E_all, Fe] in CSR order, or NULL */
+  float* p1_ea;                           /* [P1_all, Fe] pooled edge_attr (coalesced sums), or NULL */
+  int32_t* p1t_pid;                       /* [P1_all] pooled transposed slot -> pooled CSR slot, or NULL */
 } dr_pack_output;
 
 /* Pass 1: per-graph K0, pooled-edge and K1 counts.  On invalid input returns

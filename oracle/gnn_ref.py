@@ -217,4 +217,92 @@ class VanillaNetwork(nn.Module):
         return self._graph_mlp(P.scatter_mean(h, data.batch, dim=0))
 
 
-MODELS = {"GINet": GINet, "FoutNet": FoutNet, "VanillaNetwork": VanillaNetwork}
+# --------------------------------------------------------------------------
+# sgat.py
+# --------------------------------------------------------------------------
+
+
+class SGraphAttentionLayer(nn.Module):
+    """sgat.py:13-84: ``z_i = mean_{e=(i->j)} a_e [x_i | x_j] W + b``
+    (torch_scatter ``scatter_mean`` into a zero ``out``: count clamped to 1);
+    ``undirected=False`` adds a second ``scatter_mean`` over ``col`` into the
+    same ``out`` (which also divides the first result by the col counts)."""
+
+    def __init__(self, in_channels, out_channels, bias=True, undirected=True):
+        super().__init__()
+        self.in_channels = in_channels
+        self.out_channels = out_channels
+        self.undirected = undirected
+        self.weight = nn.Parameter(torch.empty(2 * in_channels, out_channels))
+        if bias:
+            self.bias = nn.Parameter(torch.empty(out_channels))
+        else:
+            self.register_parameter("bias", None)
+        P.uniform(2 * in_channels, self.weight)
+        P.uniform(2 * in_channels, self.bias)
+
+    def forward(self, x, edge_index, edge_attr):
+        row, col = edge_index
+        if edge_attr.dim() == 1:
+            edge_attr = edge_attr.unsqueeze(-1)
+        alpha = edge_attr * torch.mm(torch.cat([x[row], x[col]], dim=-1), self.weight)
+        out = torch.zeros(len(x), self.out_channels)
+        out = P.scatter_mean(alpha, row, dim=0, out=out)
+        if not self.undirected:
+            out = P.scatter_mean(alpha, col, dim=0, out=out)
+        if self.bias is not None:
+            out = out + self.bias
+        return out
+
+
+class SGAT(nn.Module):
+    """sgat.py:87-133: conv1 / community pooling (edge_attr summed by
+    ``pool_edge``) / conv2 on the pooled graph / max_pool_x / mean / fc1 / fc2."""
+
+    def __init__(self, input_shape, output_shape=1, input_shape_edge=None):  # noqa: ARG002
+        super().__init__()
+        self.conv1 = SGraphAttentionLayer(input_shape, 16)
+        self.conv2 = SGraphAttentionLayer(16, 32)
+        self.fc1 = nn.Linear(32, 64)
+        self.fc2 = nn.Linear(64, output_shape)
+        self.clustering = "mcl"
+
+    def forward(self, data):
+        data.x = tf.relu(self.conv1(data.x, data.edge_index, data.edge_attr))
+        data = pool_communities(offset_clusters_inplace(data.cluster0, data.batch), data)
+        data.x = tf.relu(self.conv2(data.x, data.edge_index, data.edge_attr))
+        x, b = P.max_pool_x(offset_clusters_inplace(data.cluster1, data.batch), data.x, data.batch)
+        h = P.scatter_mean(x, b, dim=0)
+        return self.fc2(tf.relu(self.fc1(h)))
+
+
+# --------------------------------------------------------------------------
+# ginet_nocluster.py
+# --------------------------------------------------------------------------
+
+
+class GINetNoCluster(nn.Module):
+    """ginet_nocluster.py:66-111: two GINet conv branches (same layers as
+    ginet.py) on the full graph, no pooling; per-graph mean, fc1, dropout, fc2."""
+
+    def __init__(self, input_shape, output_shape=1, input_shape_edge=1):
+        super().__init__()
+        self.conv1 = GINetConvLayer(input_shape, 16, input_shape_edge)
+        self.conv2 = GINetConvLayer(16, 32, input_shape_edge)
+        self.conv1_ext = GINetConvLayer(input_shape, 16, input_shape_edge)
+        self.conv2_ext = GINetConvLayer(16, 32, input_shape_edge)
+        self.fc1 = nn.Linear(64, 128)
+        self.fc2 = nn.Linear(128, output_shape)
+        self.dropout = 0.4
+        self.dropout_fn = tf.dropout
+
+    def forward(self, data):
+        twin = data.clone()
+        h = tf.relu(self.conv2(tf.relu(self.conv1(data.x, data.edge_index, data.edge_attr)), data.edge_index, data.edge_attr))
+        he = tf.relu(self.conv2_ext(tf.relu(self.conv1_ext(twin.x, twin.edge_index, twin.edge_attr)), twin.edge_index, twin.edge_attr))
+        g = torch.cat([P.scatter_mean(h, data.batch, dim=0), P.scatter_mean(he, twin.batch, dim=0)], dim=1)
+        g = self.dropout_fn(tf.relu(self.fc1(g)), self.dropout, training=self.training)
+        return self.fc2(g)
+
+
+MODELS = {"GINet": GINet, "FoutNet": FoutNet, "VanillaNetwork": VanillaNetwork, "SGAT": SGAT, "GINetNoCluster": GINetNoCluster}

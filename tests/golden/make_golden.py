@@ -17,7 +17,8 @@ What it does:
    mask) and backward (MSE / CE losses) on seeded weights and stores inputs,
    weights, outputs, losses and every parameter gradient.
 
-Usage: ``python tests/golden/make_golden.py`` (from the repo root).
+Usage: ``python tests/golden/make_golden.py [siblings]`` (from the repo root;
+``siblings`` regenerates only the SGAT / ginet_nocluster fixtures).
 """
 
 from __future__ import annotations
@@ -37,6 +38,8 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "deeprank-gnn-2_amd"), os.path.join(HER
 
 from deeprank2.neuralnets.gnn import foutnet as ref_fout  # noqa: E402
 from deeprank2.neuralnets.gnn import ginet as ref_ginet  # noqa: E402
+from deeprank2.neuralnets.gnn import ginet_nocluster as ref_ginet_nc  # noqa: E402
+from deeprank2.neuralnets.gnn import sgat as ref_sgat  # noqa: E402
 from deeprank2.neuralnets.gnn import vanilla_gnn as ref_vanilla  # noqa: E402
 from deeprank2.utils import community_pooling as ref_cp  # noqa: E402
 
@@ -229,5 +232,79 @@ def main():  # noqa: PLR0915
     save("vanilla_synth", rec, {"F": 30, "Fe": 3, "out": 1, "loss": "mse"})
 
 
+def main_siblings():
+    """SGAT (sgat.py) and ginet_nocluster.GINet goldens."""
+    torch.set_num_threads(4)
+    dump = dump_hdf5("1ATN_ppi")
+    names = list(dump)
+    atn = [data_ref.load_one_graph(dump[n], n, DEFAULT_FEATURES, ["distance"], target="irmsd", clustering_method="mcl") for n in names[:4]]
+
+    # ---- SGAT on the reference fixture (Fe = 1: sgat.py:71 broadcasts edge_attr over the channels) ----
+    torch.manual_seed(4321)
+    model = ref_sgat.SGAT(50, 1)
+    bat = P.Batch.from_data_list([d.clone() for d in atn])
+    rec = batch_to_arrays(bat)
+    rec.update(run_model(model, bat, "mse"))
+    save("sgat_1atn", rec, {"F": 50, "Fe": 1, "out": 1, "loss": "mse", "source": "tests/data/hdf5/1ATN_ppi.hdf5 default_features+distance, mcl"})
+
+    # ---- SGAT, synthetic: twisted clusters, an isolated node (empty scatter_mean row), CE ----
+    torch.manual_seed(77)
+    datas = twist_clusters(synthetic_batch(5, seed=13, n_lo=40, n_hi=70, mean_degree=10.0))
+    for d in datas:
+        d.edge_attr = d.edge_attr[:, :1].contiguous()
+    isolate_node(datas[1], 5)
+    for i, d in enumerate(datas):
+        d.y = torch.tensor([float(i % 2)])
+    bat = P.Batch.from_data_list(datas)
+    model = ref_sgat.SGAT(30, 2)
+    rec = batch_to_arrays(bat)
+    rec.update(run_model(model, bat, "ce"))
+    save("sgat_synth", rec, {"F": 30, "Fe": 1, "out": 2, "loss": "ce", "source": "deeprank2_amd.utils.synthetic, edge_attr[:, :1], twisted clusters, node 5 of graph 1 isolated"})
+
+    # ---- SGraphAttentionLayer alone (arbitrary edges; undirected and directed forms) ----
+    for tag, undirected in (("", True), ("_directed", False)):
+        torch.manual_seed(6)
+        layer = ref_sgat.SGraphAttentionLayer(12, 16, undirected=undirected)
+        gen = torch.Generator().manual_seed(6)
+        x = torch.randn(41, 12, generator=gen, requires_grad=True)
+        ei = torch.randint(0, 40, (2, 260), generator=gen)  # node 40 has no edges
+        ei[:, :5] = torch.tensor([[3, 3, 3, 9, 9], [3, 3, 4, 9, 1]])
+        ea = torch.rand(260, generator=gen) + 0.5  # 1-D: sgat.py:65 unsqueezes
+        z = layer(x, ei, ea)
+        gz = torch.randn(z.shape, generator=gen)
+        (z * gz).sum().backward()
+        rec = {"in/x": x.detach().numpy(), "in/edge_index": ei.numpy(), "in/edge_attr": ea.numpy(), "in/gz": gz.numpy(), "out/z": z.detach().numpy(), "grad/x": x.grad.numpy()}
+        for n, p in layer.named_parameters():
+            rec["param/" + n] = p.detach().numpy().copy()
+            rec["grad/" + n] = p.grad.numpy().copy()
+        save(f"sgat_layer{tag}", rec, {"in": 12, "out": 16, "undirected": undirected})
+
+    # ---- ginet_nocluster.GINet: 1ATN (MSE, fixed dropout mask) and synthetic CE ----
+    torch.manual_seed(555)
+    model = ref_ginet_nc.GINet(50, 1, 1)
+    bat = P.Batch.from_data_list([d.clone() for d in atn])
+    mask = (torch.rand(4, 128, generator=torch.Generator().manual_seed(8)) >= 0.4).float()
+    rec = batch_to_arrays(bat)
+    rec.update(run_model(model, bat, "mse", mask, ref_ginet_nc))
+    rec["mask"] = mask.numpy()
+    save("ginet_nocluster_1atn", rec, {"F": 50, "Fe": 1, "out": 1, "loss": "mse", "source": "tests/data/hdf5/1ATN_ppi.hdf5 default_features+distance"})
+    torch.manual_seed(556)
+    datas = synthetic_batch(5, seed=17, n_lo=40, n_hi=70, mean_degree=10.0)
+    isolate_node(datas[2], 3)
+    for i, d in enumerate(datas):
+        d.y = torch.tensor([float(i % 3)])
+    bat = P.Batch.from_data_list(datas)
+    model = ref_ginet_nc.GINet(30, 3, 3)
+    mask = (torch.rand(5, 128, generator=torch.Generator().manual_seed(9)) >= 0.4).float()
+    rec = batch_to_arrays(bat)
+    rec.update(run_model(model, bat, "ce", mask, ref_ginet_nc))
+    rec["mask"] = mask.numpy()
+    save("ginet_nocluster_synth", rec, {"F": 30, "Fe": 3, "out": 3, "loss": "ce", "source": "deeprank2_amd.utils.synthetic, node 3 of graph 2 isolated"})
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["siblings"]:
+        main_siblings()
+    else:
+        main()
+        main_siblings()

@@ -16,6 +16,7 @@ def pack_graphs_numpy(records, require_clusters: bool = True) -> PackedGraphs:  
     F = int(records[0].x.shape[1])
     xs, rps, cols, eperms, trps, tcols, teids = [], [], [], [], [], [], []
     m0ps, m0is, cl0s, p1rps, p1cs, p1trps, p1tcs, m1ps, m1is, cl1s, ys, eas = ([] for _ in range(12))
+    p1tps, p1eas = [], []
     node_off = [0]
     edge_off = [0]
     k0_off = [0]
@@ -80,6 +81,12 @@ def pack_graphs_numpy(records, require_clusters: bool = True) -> PackedGraphs:  
         p1rp = np.zeros(k0 + 1, dtype=np.int32)
         np.cumsum(np.bincount(prow, minlength=k0), out=p1rp[1:])
         tkey = np.unique(pcol * k0 + prow)
+        p1tps.append(np.searchsorted(key, (tkey % k0) * k0 + tkey // k0).astype(np.int32))
+        if has_ea:  # PyG coalesce: attributes of merged edges summed in edge order
+            ea_in = np.asarray(r.edge_attr, dtype=np.float32).reshape(e, -1)
+            pe = np.zeros((key.size, ea_in.shape[1]), np.float32)
+            np.add.at(pe, np.searchsorted(key, pr[keep] * k0 + pc[keep]), ea_in[keep])
+            p1eas.append(pe)
         p1trp = np.zeros(k0 + 1, dtype=np.int32)
         np.cumsum(np.bincount(tkey // k0, minlength=k0), out=p1trp[1:])
 
@@ -132,6 +139,8 @@ def pack_graphs_numpy(records, require_clusters: bool = True) -> PackedGraphs:  
         p1_col=cat(p1cs) if p1cs else np.zeros(0, np.int32),
         p1t_rowptr=cat(p1trps),
         p1t_col=cat(p1tcs) if p1tcs else np.zeros(0, np.int32),
+        p1t_pid=cat(p1tps) if p1tps else np.zeros(0, np.int32),
+        p1_ea=cat(p1eas) if has_ea else None,
         k1_off=np.asarray(k1_off, np.int64),
         m1_ptr=cat(m1ps),
         m1_idx=cat(m1is),

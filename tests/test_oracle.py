@@ -41,6 +41,10 @@ def _run(model, z, loss_kind, mask=None):
     ("ginet_synth_classif", "GINet", (30, 2, 3)),
     ("foutnet_synth", "FoutNet", (30, 1)),
     ("vanilla_synth", "VanillaNetwork", (30, 1, 3)),
+    ("sgat_1atn", "SGAT", (50, 1)),
+    ("sgat_synth", "SGAT", (30, 2)),
+    ("ginet_nocluster_1atn", "GINetNoCluster", (50, 1, 1)),
+    ("ginet_nocluster_synth", "GINetNoCluster", (30, 3, 3)),
 ])
 def test_model_matches_reference(golden, name, cls, args):
     z = golden(name)
@@ -116,3 +120,17 @@ def test_scatter_max_semantics():
     assert arg.view(-1).tolist() == [0, 5, 3, 5]
     amax = P.pyg_scatter(src, idx, reduce="max")
     assert np.isnan(amax[0, 0].item())
+
+
+@pytest.mark.parametrize("name", ["sgat_layer", "sgat_layer_directed"])
+def test_sgat_layer_matches_reference(golden, name):
+    z = golden(name)
+    layer = gnn_ref.SGraphAttentionLayer(12, 16, undirected=bool(z["meta/undirected"]))
+    layer.load_state_dict({k[6:]: torch.from_numpy(v) for k, v in z.items() if k.startswith("param/")})
+    x = torch.from_numpy(z["in/x"]).requires_grad_(True)
+    out = layer(x, torch.from_numpy(z["in/edge_index"]), torch.from_numpy(z["in/edge_attr"]))
+    (out * torch.from_numpy(z["in/gz"])).sum().backward()
+    np.testing.assert_allclose(out.detach().numpy(), z["out/z"], **TOL)
+    np.testing.assert_allclose(x.grad.numpy(), z["grad/x"], rtol=1e-4, atol=1e-5)
+    for n, p in layer.named_parameters():
+        np.testing.assert_allclose(p.grad.numpy(), z["grad/" + n], rtol=1e-4, atol=1e-5, err_msg=n)

@@ -63,6 +63,19 @@ def test_pooled_graph_matches_community_pooling(golden):
                 rows.append(k0a + k)
                 cols.append(k0a + packed.p1_col[q0 + e])
     np.testing.assert_array_equal(np.array([rows, cols]), z["out/edge_index"])
+    # pooled edge_attr == pool_edge's coalesced sums (same slot order; the
+    # summation order of merged edges follows torch.sort, so ulp-level only)
+    np.testing.assert_allclose(packed.p1_ea, z["out/edge_attr"], rtol=1e-6)
+    # transposed pooled slot -> pooled slot of the reversed edge
+    for g in range(packed.n_graphs):
+        k0a, k0b = packed.k0_off[g], packed.k0_off[g + 1]
+        rp, trp = packed.p1_rowptr[k0a + g:k0b + g + 1], packed.p1t_rowptr[k0a + g:k0b + g + 1]
+        q0 = packed.p1_off[g]
+        row_of = np.repeat(np.arange(k0b - k0a), np.diff(rp))
+        for b in range(k0b - k0a):
+            for s in range(trp[b], trp[b + 1]):
+                q = packed.p1t_pid[q0 + s]
+                assert row_of[q] == packed.p1t_col[q0 + s] and packed.p1_col[q0 + q] == b
     # depth-0 dense ids == consecutive_cluster of the offset ids
     dense = np.concatenate([packed.cl0[packed.node_off[g]:packed.node_off[g + 1]] + packed.k0_off[g] for g in range(packed.n_graphs)])
     np.testing.assert_array_equal(dense, np.unique(z["out/cluster_offset"], return_inverse=True)[1])
@@ -144,7 +157,7 @@ def test_native_packer_matches_numpy_model(asym):
 
     recs = _random_records(11 + asym, asym=asym)
     a, b = pack_graphs(recs), pack_graphs_numpy(recs)
-    for f in ("node_off", "edge_off", "rowptr", "col", "eperm", "t_rowptr", "t_col", "t_eid", "k0_off", "m0_ptr", "m0_idx", "cl0", "p1_off", "p1_rowptr", "p1_col", "p1t_rowptr", "p1t_col", "k1_off", "m1_ptr", "m1_idx", "cl1", "edge_attr", "x", "y"):
+    for f in ("node_off", "edge_off", "rowptr", "col", "eperm", "t_rowptr", "t_col", "t_eid", "k0_off", "m0_ptr", "m0_idx", "cl0", "p1_off", "p1_rowptr", "p1_col", "p1t_rowptr", "p1t_col", "p1t_pid", "k1_off", "m1_ptr", "m1_idx", "cl1", "edge_attr", "p1_ea", "x", "y"):
         np.testing.assert_array_equal(getattr(a, f), getattr(b, f), err_msg=f)
     assert a.transpose_aliased == b.transpose_aliased
 
