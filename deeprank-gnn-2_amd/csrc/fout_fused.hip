@@ -1,4 +1,5 @@
-// FoutNet training step, one workgroup per graph, everything resident in LDS.
+// FoutNet and SGAT training steps, one workgroup per graph, everything
+// resident in LDS.
 //
 // Replaces (deeprank2 v3.1.0):
 //   FoutLayer.forward      deeprank2/neuralnets/gnn/foutnet.py:48-66
@@ -16,6 +17,15 @@
 // member per cluster, so dWc = sum_k v_k x[arg_k], dWn = sum_k v_k Zm[arg_k]
 // and db = sum_k v_k — no gather over the edges.  The pooled conv2 backward
 // scatters through the transposed pooled CSR.
+//
+// SGAT (template flag SG; deeprank2/neuralnets/gnn/sgat.py:56-133) has the same
+// shape: SGraphAttentionLayer is z_i = mean_{e=(i->j)} a_e [x_i | x_j] W + b
+// with torch_scatter's scatter_mean (count clamped to 1, so an edge-less row
+// is 0, not NaN), i.e. [c_i x_i | Zw_i] [W_top; W_bot] + b with
+// c_i = sum_e a_e / max(deg_i, 1) and Zw_i = sum_e a_e x_j / max(deg_i, 1).
+// conv2 runs on the pooled graph with the pooled edge_attr (PyG pool_edge
+// coalesce sums, precomputed in the store as p1_ea).  Needs Fe == 1 (sgat.py:71
+// broadcasts edge_attr [E, Fe] over the output channels).
 
 #include <hip/hip_runtime.h>
 
@@ -33,6 +43,7 @@ constexpr int HEADW = 512;  // G32 hpre64 hh64 dh64 dG32 dout16 spare
 
 struct Carve {
   int KP, XS, LDZ;
+  int ea, c1, p1w, p1tid, c2;  // SGAT only (0 words otherwise)
   int wc1, w2, fc1, fc2, x, zm, h1, rp, col, m0p, m0i, p1, a1, dp1, zm2, s2, h2, d2, dz2, p1rp, p1c, p1trp, p1tc,
       m1p, m1i, p2, nt, head, dgp, red, total;
 };
@@ -40,7 +51,7 @@ struct Carve {
 // X keeps the HBM row stride XS = r4(F) (16-byte rows: DMA + float4 gather);
 // Zm uses LDZ = r4(F)+2 (LDZ = 2 mod 32 or an odd multiple of 2 mod 32: the
 // MFMA column reads of lanes (row li, k+kq) hit distinct banks).
-__host__ __device__ inline Carve carve(int N, int E, int F, int K0, int P1, int K1, int alias, int OUT) {
+__host__ __device__ inline Carve carve(int N, int E, int F, int K0, int P1, int K1, int alias, int OUT, bool sg) {
   Carve c;
   c.KP = r16(2 * F);
   c.XS = r4(F);
@@ -84,6 +95,15 @@ __host__ __device__ inline Carve carve(int N, int E, int F, int K0, int P1, int 
   TAKE(head, HEADW)
   TAKE(dgp, NW * 32)
   TAKE(red, 2 * NT)
+  if (sg) {
+    TAKE(ea, E)
+    TAKE(c1, N)
+    TAKE(p1w, P1)
+    TAKE(p1tid, P1)
+    TAKE(c2, K0)
+  } else {
+    c.ea = c.c1 = c.p1w = c.p1tid = c.c2 = 0;
+  }
 #undef TAKE
   c.total = o;
   return c;
@@ -97,6 +117,19 @@ struct FoutArgs {
   int32_t B;
 };
 
+// gather_row_chunk with edge weights: acc = sum_e w[e] X[col[e], c4..c4+3]
+__device__ __forceinline__ float4 gather_row_chunk_w(const uint16_t* col, const float* w, int eb, int ee,
+                                                     const float* X, int XS, int c4) {
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int e = eb; e < ee; ++e) {
+    const float we = w[e];
+    const float4 v = *reinterpret_cast<const float4*>(&X[__umul24((int)col[e], XS) + c4]);
+    acc = make_float4(fmaf(we, v.x, acc.x), fmaf(we, v.y, acc.y), fmaf(we, v.z, acc.z), fmaf(we, v.w, acc.w));
+  }
+  return acc;
+}
+
+template <bool SG>
 __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x;
@@ -111,8 +144,13 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
   const int F = s.n_feat;
   const int alias = s.transpose_aliased;
   const int OUT = a.p.out_dim;
-  const Carve c = carve(N, E, F, K0, P1, K1, alias, OUT);
+  const Carve c = carve(N, E, F, K0, P1, K1, alias, OUT, SG);
   const int KP = c.KP, XS = c.XS, LDZ = c.LDZ;
+  float* sEa = lds + c.ea;
+  float* sC1 = lds + c.c1;
+  float* sP1w = lds + c.p1w;
+  int* sP1tid = reinterpret_cast<int*>(lds + c.p1tid);
+  float* sC2 = lds + c.c2;
 
   float* sWc1 = lds + c.wc1;
   float* sWc2 = lds + c.w2;
@@ -172,6 +210,11 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
   }
   dma_words<NT>(sm1p, s.m1_ptr + k10 + g, K1 + 1);
   dma_words<NT>(sm1i, s.m1_idx + k00, K0);
+  if (SG) {  // Fe == 1: edge weights are contiguous at col_off, pooled ones at p1_off
+    dma_words<NT>(sEa, s.ea + ec0, E);
+    dma_words<NT>(sP1w, s.p1_ea + q0, P1);
+    dma_words<NT>(sP1tid, s.p1t_pid + q0, P1);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -200,15 +243,21 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
     wr[u] = v;
   }
   // ---------------- Zm = D^-1 A X (foutnet.py:55-58; NaN on empty rows) ----
+  // SGAT: Zw = D^-1 A_w X and c = D^-1 A_w 1 with D clamped to 1 (sgat.py:74-76)
   {
     const int nch = XS >> 2;
     const int sub = tid & 7;
     for (int i = tid >> 3; i < N; i += NT / 8) {
       const int eb = srp[i], ee = srp[i + 1];
-      const float deg = (float)(ee - eb);
+      const float deg = SG ? (float)imax(ee - eb, 1) : (float)(ee - eb);
+      if (SG && sub == 0) {
+        float sw = 0.f;
+        for (int e = eb; e < ee; ++e) sw += sEa[e];
+        sC1[i] = sw / deg;
+      }
       for (int ch = sub; ch < nch; ch += 8) {
         const int c4 = ch * 4;
-        const float4 acc = gather_row_chunk(scol, eb, ee, sX, XS, c4);
+        const float4 acc = SG ? gather_row_chunk_w(scol, sEa, eb, ee, sX, XS, c4) : gather_row_chunk(scol, eb, ee, sX, XS, c4);
         float* zr = sZm + i * LDZ + c4;
         // mean over the out-neighbours; 0/0 = NaN exactly as torch.mean(empty)
         if (c4 + 0 < F) zr[0] = acc.x / deg;
@@ -236,13 +285,14 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
     for (int t = wave; t * 16 < N; t += NW) {
       const int r0 = t * 16;
       const int ar = min(r0 + li, N - 1);
+      const float cx = SG ? sC1[ar] : 1.f;
       floatx4 acc = {0.f, 0.f, 0.f, 0.f};
       for (int k = 0; k < KP; k += 16) {
         float av[4], bv[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int kk = k + 4 * u + kq;
-          av[u] = kk < F ? sX[ar * XS + kk] : (kk < 2 * F ? sZm[ar * LDZ + kk - F] : 0.f);
+          av[u] = kk < F ? cx * sX[ar * XS + kk] : (kk < 2 * F ? sZm[ar * LDZ + kk - F] : 0.f);
           bv[u] = sWc1[kk * 16 + li];
         }
 #pragma unroll
@@ -302,12 +352,24 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
 
   DRK_STAMP(4);
   // ---------------- conv2 on the pooled graph: FoutLayer(16, 32) ----------
+  // (SGAT: SGraphAttentionLayer(16, 32) with the pooled edge weights)
   for (int p = tid; p < K0 * 16; p += NT) {  // Zm2 = mean over pooled out-neighbours
     const int k = p >> 4, j = p & 15;
     const int eb = sp1rp[k], ee = sp1rp[k + 1];
     float acc = 0.f;
-    for (int e = eb; e < ee; ++e) acc += sP1[sp1c[e] * 16 + j];
-    sZm2[p] = acc / (float)(ee - eb);
+    if (SG) {
+      float sw = 0.f;
+      for (int e = eb; e < ee; ++e) {
+        acc = fmaf(sP1w[e], sP1[sp1c[e] * 16 + j], acc);
+        sw += sP1w[e];
+      }
+      const float deg = (float)imax(ee - eb, 1);
+      sZm2[p] = acc / deg;
+      if (j == 0) sC2[k] = sw / deg;
+    } else {
+      for (int e = eb; e < ee; ++e) acc += sP1[sp1c[e] * 16 + j];
+      sZm2[p] = acc / (float)(ee - eb);
+    }
   }
   __syncthreads();
   for (int p = tid; p < K0 * 32; p += NT) {
@@ -315,6 +377,7 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
     float acc = 0.f;
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc = fmaf(sP1[k * 16 + j], sWc2[j * 32 + o], acc);
+    if (SG) acc *= sC2[k];
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc = fmaf(sZm2[k * 16 + j], sWn2[j * 32 + o], acc);
     const float sv = acc + sB2[o];
@@ -447,13 +510,13 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
     float* slab = a.p.slab + (int64_t)b * SS + 32 * F + 16;
     for (int p = tid; p < 1024 + 32; p += NT) {
       float acc = 0.f;
-      if (p < 512) {  // dWc2[j][o] = sum_k P1[k][j] dS2[k][o]
+      if (p < 512) {  // dWc2[j][o] = sum_k (c2_k) P1[k][j] dS2[k][o]
         const int j = p >> 5, o = p & 31;
-        for (int k = 0; k < K0; ++k) acc = fmaf(sP1[k * 16 + j], sD2[k * 32 + o], acc);
+        for (int k = 0; k < K0; ++k) acc = fmaf((SG ? sC2[k] : 1.f) * sP1[k * 16 + j], sD2[k * 32 + o], acc);
       } else if (p < 1024) {  // dWn2[j][o] = sum_{k: deg>0} Zm2[k][j] dS2[k][o]
         const int q = p - 512, j = q >> 5, o = q & 31;
         for (int k = 0; k < K0; ++k)
-          if (sp1rp[k + 1] > sp1rp[k]) acc = fmaf(sZm2[k * 16 + j], sD2[k * 32 + o], acc);
+          if (SG || sp1rp[k + 1] > sp1rp[k]) acc = fmaf(sZm2[k * 16 + j], sD2[k * 32 + o], acc);
       } else {  // db2[o]
         const int o = p - 1024;
         for (int k = 0; k < K0; ++k) acc += sD2[k * 32 + o];
@@ -472,7 +535,7 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
     }
     const int deg = sp1rp[k + 1] - sp1rp[k];
     sDz2[p] = deg > 0 ? dz / (float)deg : 0.f;
-    sdP1[p] = dp;
+    sdP1[p] = SG ? sC2[k] * dp : dp;
   }
   __syncthreads();
   // dP1[j] += sum_{i: j in N(i)} dZm2[i] / deg_i  (transposed pooled CSR), then
@@ -480,7 +543,11 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
   for (int p = tid; p < K0 * 16; p += NT) {
     const int k = p >> 4, j = p & 15;
     float acc = sdP1[p];
-    for (int e = sp1trp[k]; e < sp1trp[k + 1]; ++e) acc += sDz2[sp1tc[e] * 16 + j];
+    if (SG) {
+      for (int e = sp1trp[k]; e < sp1trp[k + 1]; ++e) acc = fmaf(sP1w[sP1tid[e]], sDz2[sp1tc[e] * 16 + j], acc);
+    } else {
+      for (int e = sp1trp[k]; e < sp1trp[k + 1]; ++e) acc += sDz2[sp1tc[e] * 16 + j];
+    }
     const int i = sA1[p];
     sdP1[p] = (i < N) ? relu_bwd(sH1[i * 16 + j], acc) : 0.f;
   }
@@ -498,7 +565,7 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
         const int q = p - half * 16 * F, kk = q >> 4, ch = q & 15;
         for (int k = 0; k < K0; ++k) {
           const int i = sA1[k * 16 + ch];
-          if (i < N) acc = fmaf(sdP1[k * 16 + ch], half ? sZm[i * LDZ + kk] : sX[i * XS + kk], acc);
+          if (i < N) acc = fmaf(sdP1[k * 16 + ch], half ? sZm[i * LDZ + kk] : (SG ? sC1[i] : 1.f) * sX[i * XS + kk], acc);
         }
       } else {
         const int ch = p - 32 * F;
@@ -512,29 +579,54 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
 
 }  // namespace
 
-extern "C" int64_t dr_fout_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_feat, int32_t k0, int32_t p1_edges,
-                                     int32_t k1, int32_t transpose_aliased, int32_t out_dim) {
-  return 4LL * carve(n_nodes, n_edges, n_feat, k0, p1_edges, k1, transpose_aliased, out_dim).total;
-}
+namespace {
 
-extern "C" int dr_fout_graph_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
-                                  const dr_fout_weights* w, const dr_pass* pass, int32_t lds_bytes, void* stream) {
+int fout_family_pass(bool sg, const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                     const dr_fout_weights* w, const dr_pass* pass, int32_t lds_bytes, void* stream) {
   if (!store || !descs || !w || !pass || n_batch < 0) return DR_E_ARG;
+  if (sg && (store->n_edge_feat != 1 || !store->ea || !store->p1_ea || !store->p1t_pid)) return DR_E_UNSUPPORTED;
   if (pass->out_dim < 1 || pass->out_dim > DR_MAX_OUT) return DR_E_UNSUPPORTED;
   if (store->n_feat < 1 || 2 * 16 * store->n_feat + 1072 + 2112 + 65 * pass->out_dim > 6 * NT) return DR_E_UNSUPPORTED;
   if (lds_bytes > 160 * 1024) return DR_E_LDS;
   if ((pass->flags & DR_PASS_BACKWARD) && (!pass->slab || !pass->head)) return DR_E_ARG;
   if ((pass->flags & DR_PASS_BACKWARD) && pass->loss_kind == DR_LOSS_NONE && !pass->dout) return DR_E_ARG;
   if ((pass->flags & DR_PASS_FORWARD) && !pass->out) return DR_E_ARG;
-  if (pass->use_dropout != DR_DROPOUT_OFF) return DR_E_UNSUPPORTED;  // FoutNet has no dropout
+  if (pass->use_dropout != DR_DROPOUT_OFF) return DR_E_UNSUPPORTED;  // FoutNet / SGAT have no dropout
   if (n_batch == 0) return DR_OK;
-  DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&fout_graph_kernel)));
+  const void* fn = sg ? reinterpret_cast<const void*>(&fout_graph_kernel<true>)
+                      : reinterpret_cast<const void*>(&fout_graph_kernel<false>);
+  DR_CHECK(dr_allow_big_lds(fn));
   FoutArgs args;
   args.s = *store;
   args.w = *w;
   args.p = *pass;
   args.descs = descs;
   args.B = n_batch;
-  hipLaunchKernelGGL(fout_graph_kernel, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, args);
+  if (sg)
+    hipLaunchKernelGGL(fout_graph_kernel<true>, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, args);
+  else
+    hipLaunchKernelGGL(fout_graph_kernel<false>, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, args);
   return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" int64_t dr_fout_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_feat, int32_t k0, int32_t p1_edges,
+                                     int32_t k1, int32_t transpose_aliased, int32_t out_dim) {
+  return 4LL * carve(n_nodes, n_edges, n_feat, k0, p1_edges, k1, transpose_aliased, out_dim, false).total;
+}
+
+extern "C" int64_t dr_sgat_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_feat, int32_t k0, int32_t p1_edges,
+                                     int32_t k1, int32_t transpose_aliased, int32_t out_dim) {
+  return 4LL * carve(n_nodes, n_edges, n_feat, k0, p1_edges, k1, transpose_aliased, out_dim, true).total;
+}
+
+extern "C" int dr_fout_graph_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                                  const dr_fout_weights* w, const dr_pass* pass, int32_t lds_bytes, void* stream) {
+  return fout_family_pass(false, store, descs, n_batch, w, pass, lds_bytes, stream);
+}
+
+extern "C" int dr_sgat_graph_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                                  const dr_fout_weights* w, const dr_pass* pass, int32_t lds_bytes, void* stream) {
+  return fout_family_pass(true, store, descs, n_batch, w, pass, lds_bytes, stream);
 }

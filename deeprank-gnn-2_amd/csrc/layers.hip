@@ -7,7 +7,9 @@
 //   dr_csr_from_coo : stable CSR by row (the order torch_scatter's CPU
 //                     scatter_add_ visits edges in), fully on the device
 //   dr_spmm_csr     : out[i] = sum_{e in row i} y[col[e]]       (ginet.py:58)
-//                     or the row mean (foutnet.py:56-58; 0/0 = NaN on empty rows)
+//                     or the row mean (foutnet.py:56-58; 0/0 = NaN on empty rows);
+//                     dr_spmm_csr_w adds edge weights and scatter_mean's
+//                     clamped mean (sgat.py:74-80)
 //   dr_linear_*     : fc(x) = x W^T (ginet.py:45) and its two gradients
 //   dr_edge_mlp_scatter[_bwd] : the vanilla edge MLP + scatter_sum (vanilla_gnn.py:29-35)
 //
@@ -79,16 +81,20 @@ __global__ void sort_rows_kernel(const int32_t* __restrict__ rowptr, int32_t n_r
 }
 
 __global__ void spmm_kernel(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
-                            const float* __restrict__ y, int32_t n_rows, int32_t C, int32_t mode,
-                            float* __restrict__ out) {
+                            const float* __restrict__ w, const float* __restrict__ y, int32_t n_rows, int32_t C,
+                            int32_t mode, float* __restrict__ out) {
   const int64_t total = (int64_t)n_rows * C;
   for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < total; p += (int64_t)gridDim.x * blockDim.x) {
     const int i = (int)(p / C);
     const int c = (int)(p - (int64_t)i * C);
     float acc = 0.f;
     const int eb = rowptr[i], ee = rowptr[i + 1];
-    for (int e = eb; e < ee; ++e) acc += y[(int64_t)col[e] * C + c];
+    if (w)
+      for (int e = eb; e < ee; ++e) acc = fmaf(w[e], y[(int64_t)col[e] * C + c], acc);
+    else
+      for (int e = eb; e < ee; ++e) acc += y[(int64_t)col[e] * C + c];
     if (mode & DR_SPMM_MEAN) acc /= (float)(ee - eb);
+    if (mode & DR_SPMM_MEAN_CLAMP) acc /= (float)(ee > eb ? ee - eb : 1);
     out[p] = ((mode & DR_SPMM_RELU) && acc <= 0.f) ? 0.f : acc;
   }
 }
@@ -310,14 +316,20 @@ extern "C" int dr_csr_from_coo(const int64_t* row, const int64_t* col, int64_t n
   return (int)hipGetLastError();
 }
 
-extern "C" int dr_spmm_csr(const int32_t* rowptr, const int32_t* col, const float* y, int32_t n_rows, int32_t n_chan,
-                           int32_t mode, float* out, void* stream) {
+extern "C" int dr_spmm_csr_w(const int32_t* rowptr, const int32_t* col, const float* w, const float* y, int32_t n_rows,
+                             int32_t n_chan, int32_t mode, float* out, void* stream) {
   if (!rowptr || !out || n_rows < 0 || n_chan < 0) return DR_E_ARG;
+  if ((mode & DR_SPMM_MEAN) && (mode & DR_SPMM_MEAN_CLAMP)) return DR_E_ARG;
   const int64_t work = (int64_t)n_rows * n_chan;
   if (work == 0) return DR_OK;
-  hipLaunchKernelGGL(spmm_kernel, dim3(grid_for(work)), dim3(256), 0, (hipStream_t)stream, rowptr, col, y, n_rows,
+  hipLaunchKernelGGL(spmm_kernel, dim3(grid_for(work)), dim3(256), 0, (hipStream_t)stream, rowptr, col, w, y, n_rows,
                      n_chan, mode, out);
   return (int)hipGetLastError();
+}
+
+extern "C" int dr_spmm_csr(const int32_t* rowptr, const int32_t* col, const float* y, int32_t n_rows, int32_t n_chan,
+                           int32_t mode, float* out, void* stream) {
+  return dr_spmm_csr_w(rowptr, col, nullptr, y, n_rows, n_chan, mode, out, stream);
 }
 
 extern "C" int dr_linear_xwT(const float* x, const float* w, int32_t m, int32_t k, int32_t n, float* y, void* stream) {

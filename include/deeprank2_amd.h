@@ -27,6 +27,8 @@
  *                           trainer.py:419)
  *   dr_spmm_csr             torch_scatter.scatter_sum(h, row, out=zeros) over
  *                           gathered rows (ginet.py:45,55-58; vanilla_gnn.py:35)
+ *   dr_spmm_csr_w           the edge-weighted scatter_mean of
+ *                           SGraphAttentionLayer (sgat.py:71-80)
  *   dr_linear_xwT / dr_linear_xw / dr_linear_dw
  *                           the node-side nn.Linear(bias=False) of
  *                           GINetConvLayer.fc (ginet.py:45) and its backward
@@ -41,6 +43,7 @@
  *   dr_pack_sizes / dr_pack_fill   GraphDataset collate + per-graph pooling
  *                           index work (host; dataset.py:883-1052, trainer.py:541,
  *                           community_pooling.py:23-27,205-225)
+ *   dr_sgat_graph_pass      SGAT.forward + backward (sgat.py:56-133)
  *   dr_mcl / dr_mcl_assign  community_detection(method="mcl") of
  *                           Trainer._precluster (community_pooling.py:96-162,
  *                           trainer.py:319-348)
@@ -246,6 +249,22 @@ int dr_fout_graph_pass(const dr_graph_store* store, const dr_graph_desc* descs, 
 int64_t dr_fout_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_feat, int32_t k0, int32_t p1_edges,
                           int32_t k1, int32_t transpose_aliased, int32_t out_dim);
 
+/* ---- SGAT (deeprank2/neuralnets/gnn/sgat.py:13-133) -----------------------
+ * Same kernel family and partial layouts as FoutNet, with dr_fout_weights
+ * pointing into SGAT's parameters: wc1 = conv1.weight rows 0..F-1, wn1 = rows
+ * F..2F-1 (conv1.weight is [2F, 16]), b1 = conv1.bias, wc2/wn2 = conv2.weight
+ * rows 0..15 / 16..31, b2 = conv2.bias, fc1/fc2 as FoutNet.  The slab's
+ * dWc1|dWn1 and dWc2|dWn2 blocks are then d conv1.weight and d conv2.weight.
+ * Requires n_edge_feat == 1 (sgat.py:71 multiplies [E, Fe] into [E, out]).
+ * One workgroup per graph: SGraphAttentionLayer(F,16) (scatter_mean, edge-less
+ * rows give the bias) -> relu -> depth-0 community pooling (pooled edge_attr =
+ * sums, store p1_ea) -> SGraphAttentionLayer(16,32) -> relu -> depth-1
+ * max_pool_x -> mean -> fc1/relu/fc2, and its backward.                     */
+int dr_sgat_graph_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                       const dr_fout_weights* w, const dr_pass* pass, int32_t lds_bytes, void* stream);
+int64_t dr_sgat_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_feat, int32_t k0, int32_t p1_edges,
+                          int32_t k1, int32_t transpose_aliased, int32_t out_dim);
+
 /* ---- VanillaNetwork (deeprank2/neuralnets/gnn/vanilla_gnn.py:10-65) ------- */
 
 typedef struct dr_vanilla_weights {
@@ -349,8 +368,13 @@ int dr_csr_from_coo(const int64_t* row, const int64_t* col, int64_t n_edges, int
  * empty row, as torch.mean over an empty set); DR_SPMM_RELU applies relu.  */
 #define DR_SPMM_RELU 1
 #define DR_SPMM_MEAN 2
+#define DR_SPMM_MEAN_CLAMP 4 /* divide by max(row length, 1): torch_scatter scatter_mean */
 int dr_spmm_csr(const int32_t* rowptr, const int32_t* col, const float* y, int32_t n_rows,
                 int32_t n_chan, int32_t mode, float* out, void* stream);
+/* Weighted form: out[i,:] = sum_e w[e] y[col[e],:] (w in CSR order, NULL = 1);
+ * SGraphAttentionLayer's a_ij-weighted scatter_mean (sgat.py:71-80).      */
+int dr_spmm_csr_w(const int32_t* rowptr, const int32_t* col, const float* w, const float* y, int32_t n_rows,
+                  int32_t n_chan, int32_t mode, float* out, void* stream);
 
 /* y[M,N] = x[M,K] w[N,K]^T            */
 int dr_linear_xwT(const float* x, const float* w, int32_t m, int32_t k, int32_t n, float* y, void* stream);
