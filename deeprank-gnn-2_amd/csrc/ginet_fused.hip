@@ -35,6 +35,7 @@
 #include "../../include/deeprank2_amd.h"
 #include "dr_common.h"
 #include "graph_common.h"
+#include "ginet_head.h"
 
 namespace {
 
@@ -117,10 +118,6 @@ struct GinetArgs {
 __device__ __forceinline__ float relu_keepnan(float v) { return (v <= 0.f) ? 0.f : v; }
 __device__ __forceinline__ float relu_bwd(float out, float g) { return (out <= 0.f) ? 0.f : g; }
 
-__device__ __forceinline__ bool keep_unit(const dr_pass& p, uint64_t offset, int b, int r) {
-  if (p.use_dropout == DR_DROPOUT_MASK) return p.mask[(int64_t)b * 128 + r] != 0;
-  return dr_uniform(p.drop_seed, offset, (uint32_t)(b * 128 + r)) >= p.drop_p;
-}
 
 #define AS1(p) ((const __attribute__((address_space(1))) void*)(p))
 #define AS3(p) ((__attribute__((address_space(3))) void*)(p))
@@ -246,8 +243,6 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
                                            const float (&fc1_col)[8], float fc1_bias, int b, int N, int K0, int K1,
                                            int F, int OUT, float y_g, uint64_t drop_offset, ZAt zat) {
   const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
   STAMP(4);
   // ---------------- conv2 node GEMM on the pooled graph (ginet.py:101,112) --
   for (int p = tid; p < K0 * 64; p += NT) {
@@ -296,93 +291,19 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
   __syncthreads();
 
   STAMP(7);
-  // ---------------- head: fc1 -> relu -> dropout -> fc2 (ginet.py:120-123) --
   {
-    const int r = tid >> 3, part = tid & 7;  // 8 lanes per fc1 row
-    float acc = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc = fmaf(t.g[part * 8 + j], fc1_row[j], acc);
-    acc += __shfl_xor(acc, 1, 64);
-    acc += __shfl_xor(acc, 2, 64);
-    acc += __shfl_xor(acc, 4, 64);
-    if (part == 0) {
-      acc += fc1_bias;
-      t.hpre[r] = acc;
-      const float hh = relu_keepnan(acc);
-      t.hh[r] = hh;
-      float hd = hh;
-      if (a.p.use_dropout) hd = (keep_unit(a.p, drop_offset, b, r) ? hh : 0.f) * a.p.drop_scale;
-      t.hd[r] = hd;
-    }
+    drk::GinetHeadLds hl;
+    hl.fc2 = t.fc2;
+    hl.g = t.g;
+    hl.hpre = t.hpre;
+    hl.hh = t.hh;
+    hl.hd = t.hd;
+    hl.dh = t.dh;
+    hl.dg = t.dg;
+    hl.dout = t.dout;
+    hl.dgp = t.dgp;
+    if (!drk::ginet_head<NT>(a.p, hl, fc1_row, fc1_col, fc1_bias, b, OUT, y_g, drop_offset)) return;
   }
-  __syncthreads();
-  for (int q = wave; q < OUT; q += NW) {
-    const float* wr = t.fc2 + q * 128;
-    float v = fmaf(t.hd[lane], wr[lane], t.hd[lane + 64] * wr[lane + 64]);
-    v = dr_wave_sum(v);
-    if (lane == 0) t.dout[q] = v + t.fc2[OUT * 128 + q];  // logits parked in t.dout
-  }
-  __syncthreads();
-  if ((a.p.flags & DR_PASS_FORWARD) && tid < OUT) a.p.out[(int64_t)b * OUT + tid] = t.dout[tid];
-  if (!(a.p.flags & DR_PASS_BACKWARD)) return;
-  __syncthreads();
-
-  STAMP(8);
-  // ---------------- loss gradient (trainer.py:688-689) ----------------------
-  if (tid == 0) {
-    if (a.p.loss_kind == DR_LOSS_MSE) {
-      const float d = t.dout[0] - y_g;
-      if (a.p.loss_per_graph) a.p.loss_per_graph[b] = d * d;
-      t.dout[0] = 2.f * d * a.p.loss_scale;
-    } else if (a.p.loss_kind == DR_LOSS_CE) {
-      const int yi = (int)y_g;
-      float mx = t.dout[0];
-      for (int q = 1; q < OUT; ++q) mx = fmaxf(mx, t.dout[q]);
-      float se = 0.f;
-      for (int q = 0; q < OUT; ++q) se += expf(t.dout[q] - mx);
-      const float lse = mx + logf(se);
-      const float wy = a.p.class_w ? a.p.class_w[yi] : 1.f;
-      if (a.p.loss_per_graph) a.p.loss_per_graph[b] = wy * (lse - t.dout[yi]);
-      for (int q = 0; q < OUT; ++q) t.dout[q] = wy * (expf(t.dout[q] - lse) - (q == yi ? 1.f : 0.f)) * a.p.loss_scale;
-    } else {
-      for (int q = 0; q < OUT; ++q) t.dout[q] = a.p.dout[(int64_t)b * OUT + q];
-    }
-  }
-  __syncthreads();
-
-  STAMP(9);
-  // ---------------- head backward -------------------------------------------
-  if (tid < 128) {
-    float acc = 0.f;
-    for (int q = 0; q < OUT; ++q) acc = fmaf(t.fc2[q * 128 + tid], t.dout[q], acc);
-    if (a.p.use_dropout) acc = (keep_unit(a.p, drop_offset, b, tid) ? acc : 0.f) * a.p.drop_scale;
-    t.dh[tid] = relu_bwd(t.hh[tid], acc);
-  }
-  __syncthreads();
-  {
-    const int o = tid & 63, rc = tid >> 6;  // 16 chunks of 8 fc1 rows
-    float acc = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc = fmaf(fc1_col[j], t.dh[rc * 8 + j], acc);
-    t.dgp[rc * 64 + o] = acc;
-  }
-  __syncthreads();
-  if (tid < 64) {
-    float acc = 0.f;
-    for (int rc = 0; rc < NW; ++rc) acc += t.dgp[rc * 64 + tid];
-    t.dg[tid] = acc;
-  }
-  {
-    const int HS = DR_HEAD_STRIDE(OUT);
-    float* hg = a.p.head + (int64_t)b * HS;
-    if (tid < 64) hg[tid] = t.g[tid];
-    if (tid < 128) {
-      hg[64 + tid] = t.hd[tid];
-      hg[192 + tid] = t.dh[tid];
-    }
-    if (tid < OUT) hg[320 + tid] = t.dout[tid];
-  }
-  __syncthreads();
 
   STAMP(10);
   // ---------------- depth-1 pooling + mean backward -------------------------

@@ -1,0 +1,119 @@
+// The GINet head shared by the GINet kernels (ginet.py:117-123 and
+// ginet_nocluster.py:103-109): fc1 -> relu -> dropout -> fc2, the loss
+// gradient of Trainer._epoch (trainer.py:686-689) and the head backward down
+// to dG, with the per-graph head vectors (g, hd, dh, dout) for
+// dr_reduce_update.  Expects g [64] in LDS; returns false after a
+// forward-only pass.
+#pragma once
+
+#include "graph_common.h"
+
+namespace drk {
+
+__device__ __forceinline__ bool keep_unit(const dr_pass& p, uint64_t offset, int b, int r) {
+  if (p.use_dropout == DR_DROPOUT_MASK) return p.mask[(int64_t)b * 128 + r] != 0;
+  return dr_uniform(p.drop_seed, offset, (uint32_t)(b * 128 + r)) >= p.drop_p;
+}
+
+struct GinetHeadLds {
+  float *fc2, *g, *hpre, *hh, *hd, *dh, *dg, *dout, *dgp;
+};
+
+template <int NT>
+__device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds& t, const float (&fc1_row)[8],
+                                           const float (&fc1_col)[8], float fc1_bias, int b, int OUT, float y_g,
+                                           uint64_t drop_offset) {
+  constexpr int NW = NT / 64;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  // ---------------- head: fc1 -> relu -> dropout -> fc2 (ginet.py:120-123) --
+  {
+    const int r = tid >> 3, part = tid & 7;  // 8 lanes per fc1 row
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc = fmaf(t.g[part * 8 + j], fc1_row[j], acc);
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    acc += __shfl_xor(acc, 4, 64);
+    if (part == 0) {
+      acc += fc1_bias;
+      t.hpre[r] = acc;
+      const float hh = relu_keepnan(acc);
+      t.hh[r] = hh;
+      float hd = hh;
+      if (p.use_dropout) hd = (keep_unit(p, drop_offset, b, r) ? hh : 0.f) * p.drop_scale;
+      t.hd[r] = hd;
+    }
+  }
+  __syncthreads();
+  for (int q = wave; q < OUT; q += NW) {
+    const float* wr = t.fc2 + q * 128;
+    float v = fmaf(t.hd[lane], wr[lane], t.hd[lane + 64] * wr[lane + 64]);
+    v = dr_wave_sum(v);
+    if (lane == 0) t.dout[q] = v + t.fc2[OUT * 128 + q];  // logits parked in t.dout
+  }
+  __syncthreads();
+  if ((p.flags & DR_PASS_FORWARD) && tid < OUT) p.out[(int64_t)b * OUT + tid] = t.dout[tid];
+  if (!(p.flags & DR_PASS_BACKWARD)) return false;
+  __syncthreads();
+
+  // ---------------- loss gradient (trainer.py:688-689) ----------------------
+  if (tid == 0) {
+    if (p.loss_kind == DR_LOSS_MSE) {
+      const float d = t.dout[0] - y_g;
+      if (p.loss_per_graph) p.loss_per_graph[b] = d * d;
+      t.dout[0] = 2.f * d * p.loss_scale;
+    } else if (p.loss_kind == DR_LOSS_CE) {
+      const int yi = (int)y_g;
+      float mx = t.dout[0];
+      for (int q = 1; q < OUT; ++q) mx = fmaxf(mx, t.dout[q]);
+      float se = 0.f;
+      for (int q = 0; q < OUT; ++q) se += expf(t.dout[q] - mx);
+      const float lse = mx + logf(se);
+      const float wy = p.class_w ? p.class_w[yi] : 1.f;
+      if (p.loss_per_graph) p.loss_per_graph[b] = wy * (lse - t.dout[yi]);
+      for (int q = 0; q < OUT; ++q) t.dout[q] = wy * (expf(t.dout[q] - lse) - (q == yi ? 1.f : 0.f)) * p.loss_scale;
+    } else {
+      for (int q = 0; q < OUT; ++q) t.dout[q] = p.dout[(int64_t)b * OUT + q];
+    }
+  }
+  __syncthreads();
+
+  // ---------------- head backward -------------------------------------------
+  if (tid < 128) {
+    float acc = 0.f;
+    for (int q = 0; q < OUT; ++q) acc = fmaf(t.fc2[q * 128 + tid], t.dout[q], acc);
+    if (p.use_dropout) acc = (keep_unit(p, drop_offset, b, tid) ? acc : 0.f) * p.drop_scale;
+    t.dh[tid] = relu_bwd(t.hh[tid], acc);
+  }
+  __syncthreads();
+  {
+    const int o = tid & 63, rc = tid >> 6;  // 16 chunks of 8 fc1 rows
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc = fmaf(fc1_col[j], t.dh[rc * 8 + j], acc);
+    t.dgp[rc * 64 + o] = acc;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    float acc = 0.f;
+    for (int rc = 0; rc < NW; ++rc) acc += t.dgp[rc * 64 + tid];
+    t.dg[tid] = acc;
+  }
+  {
+    const int HS = DR_HEAD_STRIDE(OUT);
+    float* hg = p.head + (int64_t)b * HS;
+    if (tid < 64) hg[tid] = t.g[tid];
+    if (tid < 128) {
+      hg[64 + tid] = t.hd[tid];
+      hg[192 + tid] = t.dh[tid];
+    }
+    if (tid < OUT) hg[320 + tid] = t.dout[tid];
+  }
+  __syncthreads();
+
+  return true;
+}
+
+}  // namespace drk

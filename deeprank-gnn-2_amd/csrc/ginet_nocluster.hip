@@ -1,0 +1,393 @@
+// ginet_nocluster.GINet training step, one workgroup per graph, in LDS.
+//
+// Replaces (deeprank2 v3.1.0):
+//   GINet.forward (no clustering)   deeprank2/neuralnets/gnn/ginet_nocluster.py:84-111
+//   GINetConvLayer.forward          ginet_nocluster.py:39-60 (same layer as ginet.py)
+//   autograd backward + loss        deeprank2/trainer.py:686-689
+//
+// Both branches run conv1 -> relu -> conv2 -> relu on the full graph, then a
+// per-graph scatter_mean, fc1 -> relu -> dropout -> fc2.  As in the pooled
+// GINet the attention is identically 1, so conv(x) = A (x W^T) = (A x) W^T:
+//   Z1 = A X, H1 = relu(Z1 [W1; W1e]^T)                  (N x 32, one MFMA GEMM)
+//   Z2 = A H1, H2 = relu(Z2_b W2_b^T) per branch b       (N x 64, MFMA)
+//   g  = mean_i H2_i                                      (column sums in the GEMM epilogue)
+// H2 itself is never stored: the mean only needs its column sums, and the
+// backward only needs relu'(H2), kept as 64 mask bits per node.  Backward:
+//   dS2_i = relu'(H2_i) dG / N          (mean pooling: the same dG for every node)
+//   dW2_b = sum_i dS2_i (x) Z2_i,  dZ2 = dS2 W2_b,  dS1 = relu'(H1) (A^T dZ2),
+//   dW1   = sum_i dS1_i (x) Z1_i
+// The per-graph partials use the pooled GINet's slab/head layout, so the same
+// dr_reduce_update recipe turns them into gradients + Adam.
+// Roofline: HBM-bound on the compulsory graph bytes (x, CSR + transpose) and
+// the partial writes, like ginet_graph_kernel.
+
+#include <hip/hip_runtime.h>
+
+#include "ginet_head.h"
+
+namespace {
+
+using namespace drk;
+
+constexpr int NT = 1024;
+constexpr int NW = NT / 64;
+constexpr int HEADW = 672;  // g64 hpre128 hh128 hd128 dh128 dg64 dout16 spare16
+constexpr int LZ = 36;      // Z2 row stride: 16-byte rows (float4 gathers in the backward)
+
+struct NcCarve {
+  int KP, LDW, XS;
+  int w1, w2, fc2, xz2, z1, h1, mask, rp, trp, col, tcol, head, dgp, dgn, total;
+};
+
+__host__ __device__ inline NcCarve nc_carve(int N, int E, int F, int OUT) {
+  NcCarve c;
+  c.KP = r16(F);
+  c.LDW = c.KP + 2;
+  c.XS = r4(F);
+  int o = 0;
+#define TAKE(field, words) \
+  c.field = o;             \
+  o += r4(words);
+  TAKE(w1, 32 * c.LDW)             // [W1; W1e] row-major, zero-padded to KP
+  TAKE(w2, 1024)                   // [W2 | W2e] (conv2 / conv2_ext .fc.weight)
+  TAKE(fc2, OUT * 128 + OUT)
+  TAKE(xz2, N * imax(c.XS, LZ))    // X, then Z2 = A H1 (X is dead after the conv1 gather), then dZ2
+  TAKE(z1, N * c.LDW)              // Z1 = A X (kept for dW1)
+  TAKE(h1, N * 32)                 // H1, then dS1 in place
+  TAKE(mask, N * 2)                // relu'(H2) bits: word 2i+b, bit o of branch b
+  TAKE(rp, N + 1)
+  TAKE(trp, N + 1)
+  TAKE(col, (E + 1) / 2)
+  TAKE(tcol, (E + 1) / 2)
+  TAKE(head, HEADW)
+  TAKE(dgp, NW * 64)               // column-sum partials of H2, then the head's dG partials
+  TAKE(dgn, 64)                    // dG / N
+#undef TAKE
+  c.total = o;
+  return c;
+}
+
+struct NcArgs {
+  dr_graph_store s;
+  dr_ginet_weights w;
+  dr_pass p;
+  const dr_graph_desc* descs;
+  int32_t B;
+};
+
+// out[i, c4..c4+3] over rows [0, n): sum over CSR row i of Y[col[e], c4..]
+// (8 lanes per row, one float4 chunk each), written with row stride ldo.
+__device__ __forceinline__ void gather_rows(const int* rp, const uint16_t* col, const float* Y, int ys, int nch,
+                                            float* out, int ldo, int n) {
+  const int sub = threadIdx.x & 7;
+  for (int i = threadIdx.x >> 3; i < n; i += NT / 8) {
+    const int eb = rp[i], ee = rp[i + 1];
+    for (int ch = sub; ch < nch; ch += 8) {
+      const int c4 = ch * 4;
+      const float4 acc = gather_row_chunk(col, eb, ee, Y, ys, c4);
+      float* o = out + i * ldo + c4;
+      o[0] = acc.x;
+      o[1] = acc.y;
+      o[2] = acc.z;
+      o[3] = acc.w;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(NT) ginet_nocluster_kernel(NcArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int b = blockIdx.x;
+  const dr_graph_store& s = a.s;
+  const dr_graph_desc d = a.descs[b];
+  const int g = d.gid;
+  const int64_t n0 = d.node0, ec0 = d.col0;
+  const int N = d.n_nodes, E = d.n_edges;
+  const int F = s.n_feat;
+  const int OUT = a.p.out_dim;
+  const NcCarve c = nc_carve(N, E, F, OUT);
+  const int KP = c.KP, LDW = c.LDW, XS = c.XS;
+
+  float* sW1 = lds + c.w1;
+  float* sW2 = lds + c.w2;
+  float* sFc2 = lds + c.fc2;
+  float* sX = lds + c.xz2;
+  float* sZ2 = lds + c.xz2;
+  float* sZ1 = lds + c.z1;
+  float* sH1 = lds + c.h1;
+  uint32_t* sMask = reinterpret_cast<uint32_t*>(lds + c.mask);
+  int* srp = reinterpret_cast<int*>(lds + c.rp);
+  int* strp = reinterpret_cast<int*>(lds + c.trp);
+  uint16_t* scol = reinterpret_cast<uint16_t*>(lds + c.col);
+  uint16_t* stcol = reinterpret_cast<uint16_t*>(lds + c.tcol);
+  float* sDgp = lds + c.dgp;
+  float* sDgN = lds + c.dgn;
+  GinetHeadLds hl;
+  hl.fc2 = sFc2;
+  hl.g = lds + c.head;
+  hl.hpre = hl.g + 64;
+  hl.hh = hl.hpre + 128;
+  hl.hd = hl.hh + 128;
+  hl.dh = hl.hd + 128;
+  hl.dg = hl.dh + 128;
+  hl.dout = hl.dg + 64;
+  hl.dgp = sDgp;
+
+  // ---------------- stage ---------------------------------------------------
+  float fc1_row[8], fc1_col[8], fc1_bias;
+  {
+    const int r = tid >> 3, part = tid & 7;
+    const float4 u0 = *reinterpret_cast<const float4*>(a.w.fc1w + r * 64 + part * 8);
+    const float4 u1 = *reinterpret_cast<const float4*>(a.w.fc1w + r * 64 + part * 8 + 4);
+    fc1_row[0] = u0.x; fc1_row[1] = u0.y; fc1_row[2] = u0.z; fc1_row[3] = u0.w;
+    fc1_row[4] = u1.x; fc1_row[5] = u1.y; fc1_row[6] = u1.z; fc1_row[7] = u1.w;
+    fc1_bias = a.w.fc1b[r];
+    const int o = tid & 63, rc = tid >> 6;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fc1_col[j] = a.w.fc1w[(rc * 8 + j) * 64 + o];
+  }
+  const float y_g = s.y[g];
+  uint64_t drop_offset = a.p.drop_offset;
+  if (a.p.step_counter) {
+    drop_offset = (uint64_t)a.p.step_counter[0];
+    if (b == 0 && tid == 0) a.p.step_counter[1] = (int64_t)drop_offset;
+  }
+  dma_x4<NT>(sX, s.x + n0 * (int64_t)XS, N * XS / 4);
+  dma_x4<NT>(scol, s.col + ec0, (E + 7) / 8);
+  dma_x4<NT>(stcol, s.t_col + ec0, (E + 7) / 8);
+  dma_words<NT>(srp, s.rowptr + n0 + g, N + 1);
+  dma_words<NT>(strp, s.t_rowptr + n0 + g, N + 1);
+  {
+    const int padw = KP - F;
+    for (int p = tid; p < 32 * padw; p += NT) {
+      const int i = p / padw;
+      sW1[i * LDW + F + (p - i * padw)] = 0.f;
+    }
+    const int padz = KP - XS;
+    for (int p = tid; p < N * padz; p += NT) {
+      const int i = p / padz;
+      sZ1[i * LDW + XS + (p - i * padz)] = 0.f;
+    }
+    for (int p = tid; p < 2 * N; p += NT) sMask[p] = 0u;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  float wv1[2], wv2, wfc[3];
+  {
+    const int n1 = 32 * F;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int p = tid + u * NT;
+      wv1[u] = 0.f;
+      if (p < n1) wv1[u] = (p < 16 * F) ? a.w.w1[p] : a.w.w1e[p - 16 * F];
+    }
+    wv2 = (tid < 512) ? a.w.w2[tid] : a.w.w2e[tid - 512];
+    const int nf = OUT * 128;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int p = tid + u * NT;
+      wfc[u] = 0.f;
+      if (p < nf) wfc[u] = a.w.fc2w[p];
+      else if (p < nf + OUT) wfc[u] = a.w.fc2b[p - nf];
+    }
+  }
+  // ---------------- Z1 = A X (ginet_nocluster.py:45,58 reassociated) --------
+  gather_rows(srp, scol, sX, XS, XS >> 2, sZ1, LDW, N);
+  {
+    const int n1 = 32 * F;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int p = tid + u * NT;
+      if (p < n1) {
+        const int r = p / F;
+        sW1[r * LDW + (p - r * F)] = wv1[u];
+      }
+    }
+    sW2[tid] = wv2;
+    const int nf = OUT * 128 + OUT;
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+      if (tid + u * NT < nf) sFc2[tid + u * NT] = wfc[u];
+  }
+  __syncthreads();
+
+  // ---------------- H1 = relu(Z1 [W1; W1e]^T) on MFMA ----------------------
+  const int li = lane & 15, kq = lane >> 4;
+  for (int t = wave; t * 16 < N; t += NW) {
+    const int r0 = t * 16;
+    const int ar = min(r0 + li, N - 1);
+    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < KP; k += 16) {
+      float av[4], b0[4], b1[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int kk = k + 4 * u + kq;
+        av[u] = sZ1[ar * LDW + kk];
+        b0[u] = sW1[li * LDW + kk];
+        b1[u] = sW1[(16 + li) * LDW + kk];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], b0[u], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], b1[u], acc1, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = r0 + kq * 4 + r;
+      if (row < N) {
+        sH1[row * 32 + li] = relu_keepnan(acc0[r]);
+        sH1[row * 32 + 16 + li] = relu_keepnan(acc1[r]);
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---------------- Z2 = A H1 (X is dead: Z2 takes its place) ---------------
+  gather_rows(srp, scol, sH1, 32, 8, sZ2, LZ, N);
+  __syncthreads();
+
+  // ---------------- H2 = relu(Z2_b W2_b^T): column sums + relu' bits -------
+  {
+    float cs[4] = {0.f, 0.f, 0.f, 0.f};  // (branch, half) column partial sums of this lane
+    for (int t = wave; t * 16 < N; t += NW) {
+      const int r0 = t * 16;
+      const int ar = min(r0 + li, N - 1);
+#pragma unroll
+      for (int br = 0; br < 2; ++br) {
+        floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int kk = 4 * u + kq;
+          const float av = sZ2[ar * LZ + br * 16 + kk];
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, sW2[(br * 32 + li) * 16 + kk], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, sW2[(br * 32 + 16 + li) * 16 + kk], acc1, 0, 0, 0);
+        }
+        uint32_t bits[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = r0 + kq * 4 + r;
+          if (row < N) {
+            cs[br * 2] += relu_keepnan(acc0[r]);
+            cs[br * 2 + 1] += relu_keepnan(acc1[r]);
+            // relu_bwd passes the gradient unless the output is <= 0 (NaN passes)
+            bits[r] = (acc0[r] <= 0.f ? 0u : (1u << li)) | (acc1[r] <= 0.f ? 0u : (1u << (16 + li)));
+          }
+        }
+        // OR the 16 lanes (li) of each row group together, then one LDS write per row
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          uint32_t v = bits[r];
+          v |= __shfl_xor(v, 1, 64);
+          v |= __shfl_xor(v, 2, 64);
+          v |= __shfl_xor(v, 4, 64);
+          v |= __shfl_xor(v, 8, 64);
+          const int row = r0 + kq * 4 + r;
+          if (li == 0 && row < N) sMask[row * 2 + br] = v;
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // rows of a column live in lanes li, li+16, li+32, li+48
+      cs[q] += __shfl_xor(cs[q], 16, 64);
+      cs[q] += __shfl_xor(cs[q], 32, 64);
+    }
+    if (kq == 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sDgp[wave * 64 + (q >> 1) * 32 + (q & 1) * 16 + li] = cs[q];
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {  // per-graph scatter_mean (ginet_nocluster.py:103-104)
+    float acc = 0.f;
+    for (int w = 0; w < NW; ++w) acc += sDgp[w * 64 + tid];
+    hl.g[tid] = acc / (float)N;
+  }
+  __syncthreads();
+
+  // ---------------- head, loss, head backward (shared with GINet) -----------
+  if (!ginet_head<NT>(a.p, hl, fc1_row, fc1_col, fc1_bias, b, OUT, y_g, drop_offset)) return;
+
+  // ---------------- conv2 backward -----------------------------------------
+  if (tid < 64) sDgN[tid] = hl.dg[tid] / (float)N;
+  __syncthreads();
+  {
+    const int SS = DR_SLAB_STRIDE(F);
+    float* slab = a.p.slab + (int64_t)b * SS + 32 * F;
+    const int o = tid >> 4, j = tid & 15, br = o >> 5, bit = o & 31;  // 1024 = 64 outputs x 16 inputs
+    float acc = 0.f;
+    for (int i = 0; i < N; ++i)
+      if ((sMask[i * 2 + br] >> bit) & 1u) acc += sZ2[i * LZ + br * 16 + j];
+    slab[tid] = acc * sDgN[o];  // dW2cat[o][j] = sum_i dS2[i][o] Z2[i][br*16+j]
+  }
+  __syncthreads();
+  for (int p = tid; p < N * 32; p += NT) {  // dZ2 = dS2 W2_b (in place of Z2)
+    const int i = p >> 5, ch = p & 31, br = ch >> 4, j = ch & 15;
+    const uint32_t m = sMask[i * 2 + br];
+    float acc = 0.f;
+#pragma unroll 8
+    for (int ol = 0; ol < 32; ++ol)
+      if ((m >> ol) & 1u) acc = fmaf(sDgN[br * 32 + ol], sW2[(br * 32 + ol) * 16 + j], acc);
+    sZ2[i * LZ + ch] = acc;
+  }
+  __syncthreads();
+  // dS1 = relu'(H1) (A^T dZ2), in place of H1 (transposed CSR, true edge order)
+  {
+    const int sub = tid & 7;
+    for (int jn = tid >> 3; jn < N; jn += NT / 8) {
+      const int eb = strp[jn], ee = strp[jn + 1];
+      const int c4 = sub * 4;
+      const float4 acc = gather_row_chunk(stcol, eb, ee, sZ2, LZ, c4);
+      float* h = sH1 + jn * 32 + c4;
+      h[0] = relu_bwd(h[0], acc.x);
+      h[1] = relu_bwd(h[1], acc.y);
+      h[2] = relu_bwd(h[2], acc.z);
+      h[3] = relu_bwd(h[3], acc.w);
+    }
+  }
+  __syncthreads();
+  // dW1cat[ch][kk] = sum_i dS1[i][ch] Z1[i][kk]
+  {
+    const int SS = DR_SLAB_STRIDE(F);
+    float* slab = a.p.slab + (int64_t)b * SS;
+    for (int p = tid; p < 32 * F; p += NT) {
+      const int ch = p / F, kk = p - ch * F;
+      float acc = 0.f;
+      for (int i = 0; i < N; ++i) acc = fmaf(sH1[i * 32 + ch], sZ1[i * LDW + kk], acc);
+      slab[p] = acc;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int64_t dr_ginet_nocluster_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_feat, int32_t out_dim) {
+  return 4LL * nc_carve(n_nodes, n_edges, n_feat, out_dim).total;
+}
+
+extern "C" int dr_ginet_nocluster_graph_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                                             const dr_ginet_weights* w, const dr_pass* pass, int32_t lds_bytes,
+                                             void* stream) {
+  if (!store || !descs || !w || !pass || n_batch < 0) return DR_E_ARG;
+  if (pass->out_dim < 1 || pass->out_dim > DR_MAX_OUT) return DR_E_UNSUPPORTED;
+  if (store->n_feat < 1 || 32 * store->n_feat > 2 * NT) return DR_E_UNSUPPORTED;  // F <= 64
+  if (lds_bytes > 160 * 1024) return DR_E_LDS;
+  if ((pass->flags & DR_PASS_BACKWARD) && (!pass->slab || !pass->head)) return DR_E_ARG;
+  if ((pass->flags & DR_PASS_BACKWARD) && pass->loss_kind == DR_LOSS_NONE && !pass->dout) return DR_E_ARG;
+  if ((pass->flags & DR_PASS_FORWARD) && !pass->out) return DR_E_ARG;
+  if (pass->use_dropout == DR_DROPOUT_MASK && !pass->mask) return DR_E_ARG;
+  if (pass->use_dropout < DR_DROPOUT_OFF || pass->use_dropout > DR_DROPOUT_HASH) return DR_E_ARG;
+  if (n_batch == 0) return DR_OK;
+  DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_nocluster_kernel)));
+  NcArgs args;
+  args.s = *store;
+  args.w = *w;
+  args.p = *pass;
+  args.descs = descs;
+  args.B = n_batch;
+  hipLaunchKernelGGL(ginet_nocluster_kernel, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, args);
+  return (int)hipGetLastError();
+}

@@ -16,11 +16,15 @@ def install_as_deeprank2():
 
     names = [
         "neuralnets", "neuralnets.gnn", "neuralnets.gnn.ginet", "neuralnets.gnn.foutnet",
-        "neuralnets.gnn.vanilla_gnn", "utils", "utils.community_pooling",
+        "neuralnets.gnn.vanilla_gnn", "neuralnets.gnn.sgat", "neuralnets.gnn.ginet_nocluster",
+        "utils", "utils.community_pooling", "utils.earlystopping", "dataset", "trainer",
     ]  # fmt: skip
+    renamed = {"utils.exporters": "exporters"}  # deeprank2/utils/exporters.py
     sys.modules.setdefault("deeprank2", sys.modules[__name__])
     for n in names:
         try:
             sys.modules[f"deeprank2.{n}"] = importlib.import_module(f"{__name__}.{n}")
         except ModuleNotFoundError:
             pass
+    for ref_name, ours in renamed.items():
+        sys.modules[f"deeprank2.{ref_name}"] = importlib.import_module(f"{__name__}.{ours}")

@@ -194,6 +194,8 @@ SIGNATURES = [
     ("dr_vanilla_part_floats", ctypes.c_int64, [ctypes.c_int32] * 2),
     ("dr_fout_graph_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(FoutWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, VP]),
     ("dr_fout_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 8),
+    ("dr_ginet_nocluster_graph_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, VP]),
+    ("dr_ginet_nocluster_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 4),
     ("dr_sgat_graph_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(FoutWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, VP]),
     ("dr_sgat_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 8),
     ("dr_reduce_update", ctypes.c_int, [ctypes.POINTER(ParamTableC), VP, VP, ctypes.c_int32, ctypes.POINTER(AdamC), VP, ctypes.c_float, VP, VP]),

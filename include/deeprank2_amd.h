@@ -44,6 +44,9 @@
  *                           index work (host; dataset.py:883-1052, trainer.py:541,
  *                           community_pooling.py:23-27,205-225)
  *   dr_sgat_graph_pass      SGAT.forward + backward (sgat.py:56-133)
+ *   dr_ginet_nocluster_graph_pass
+ *                           ginet_nocluster.GINet.forward + backward
+ *                           (ginet_nocluster.py:84-111)
  *   dr_mcl / dr_mcl_assign  community_detection(method="mcl") of
  *                           Trainer._precluster (community_pooling.py:96-162,
  *                           trainer.py:319-348)
@@ -248,6 +251,17 @@ int dr_fout_graph_pass(const dr_graph_store* store, const dr_graph_desc* descs, 
 /* Dynamic LDS bytes dr_fout_graph_pass needs for a graph of these sizes.   */
 int64_t dr_fout_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_feat, int32_t k0, int32_t p1_edges,
                           int32_t k1, int32_t transpose_aliased, int32_t out_dim);
+
+/* ---- ginet_nocluster.GINet (deeprank2/neuralnets/gnn/ginet_nocluster.py:66-111)
+ * One workgroup per graph: both GINetConvLayer branches conv1 -> relu ->
+ * conv2 -> relu on the full graph (no pooling; needs the store's transposed
+ * CSR for the backward), per-graph mean, fc1/relu/dropout/fc2, loss and
+ * backward.  Same weights struct, dr_pass contract and slab/head layouts as
+ * dr_ginet_graph_pass (DR_SLAB_STRIDE / DR_HEAD_STRIDE), so dr_reduce_update
+ * uses the GINet recipe.  Clusters in the store are ignored.               */
+int dr_ginet_nocluster_graph_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                                  const dr_ginet_weights* w, const dr_pass* pass, int32_t lds_bytes, void* stream);
+int64_t dr_ginet_nocluster_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_feat, int32_t out_dim);
 
 /* ---- SGAT (deeprank2/neuralnets/gnn/sgat.py:13-133) -----------------------
  * Same kernel family and partial layouts as FoutNet, with dr_fout_weights

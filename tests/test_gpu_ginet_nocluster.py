@@ -1,0 +1,124 @@
+"""GPU parity of ginet_nocluster.GINet (dr_ginet_nocluster_graph_pass +
+dr_reduce_update) against goldens generated from the reference's
+ginet_nocluster.py and the CPU oracle.  Tolerance: 1e-4 (north_star, fp32)."""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+from _util import assert_grad_close, golden_batch, golden_grads, golden_state_dict
+
+from deeprank2_amd.engine import FusedTrainStep
+from deeprank2_amd.fused import BatchHandle
+from deeprank2_amd.neuralnets.gnn import ginet_nocluster as amd
+from deeprank2_amd.store import GraphStore, pack_graphs, records_from_batch
+from oracle import data_ref, gnn_ref
+from oracle import pyg_ops as P
+
+pytestmark = pytest.mark.gpu
+TOL = dict(rtol=1e-4, atol=1e-4)
+DEV = "cuda:0"
+
+
+def _synthetic(n, seed, **kw):
+    from deeprank2_amd.utils.synthetic import make_dataset
+
+    return [data_ref.synthetic_to_data(g, f"s{i}") for i, g in enumerate(make_dataset(n, seed=seed, **kw))]
+
+
+@pytest.mark.parametrize("name,args", [("ginet_nocluster_1atn", (50, 1, 1)), ("ginet_nocluster_synth", (30, 3, 3))])
+def test_nocluster_module_vs_reference_golden(golden, name, args):
+    z = golden(name)
+    m = amd.GINet(*args)
+    m.load_state_dict(golden_state_dict(z))
+    m = m.to(DEV).eval()
+    with torch.no_grad():
+        out = m(golden_batch(z)).cpu().numpy()
+    np.testing.assert_allclose(out, z["out/eval"], **TOL)
+    m.train()
+    out = m(golden_batch(z), dropout_mask=torch.from_numpy(z["mask"]).to(torch.uint8))
+    y = torch.from_numpy(z["in/y"]).to(DEV)
+    loss = torch.nn.functional.mse_loss(out.reshape(-1), y) if str(z["meta/loss"]) == "mse" else torch.nn.functional.cross_entropy(out, y.long())
+    loss.backward()
+    np.testing.assert_allclose(out.detach().cpu().numpy(), z["out/train"], **TOL)
+    assert float(loss.detach()) == pytest.approx(float(z["loss"]), rel=1e-4)
+    ref = golden_grads(z)
+    for n, p in m.named_parameters():
+        assert p.grad is not None, n
+        assert_grad_close(p.grad.cpu().numpy(), ref[n], err_msg=n)
+
+
+def test_nocluster_needs_no_clusters_and_matches_oracle():
+    """Graphs without cluster0/1, an isolated node, mixed sizes (1..3 MFMA row tiles and more)."""
+    datas = _synthetic(12, seed=31, n_lo=5, n_hi=120, mean_degree=8.0)
+    for i, d in enumerate(datas):
+        d.cluster0 = d.cluster1 = None
+        if i == 4:
+            keep = (d.edge_index[0] != 2) & (d.edge_index[1] != 2)
+            d.edge_index, d.edge_attr = d.edge_index[:, keep], d.edge_attr[keep]
+    torch.manual_seed(8)
+    model_o = gnn_ref.GINetNoCluster(30, 1, 3)
+    model = amd.GINet(30, 1, 3)
+    model.load_state_dict(model_o.state_dict())
+    model = model.to(DEV).eval()
+    model_o.eval()
+    bat_o = P.Batch.from_data_list([d.clone() for d in datas])
+    out_o = model_o(bat_o)
+    out_o.sum().backward()
+    out = model(P.Batch.from_data_list(datas))
+    out.sum().backward()
+    np.testing.assert_allclose(out.detach().cpu().numpy(), out_o.detach().numpy(), **TOL)
+    ref = dict(model_o.named_parameters())
+    for n, p in model.named_parameters():
+        assert_grad_close(p.grad.cpu().numpy(), ref[n].grad.numpy(), err_msg=n)
+
+
+def test_nocluster_fused_train_step_vs_oracle():
+    datas = _synthetic(32, seed=5, n_lo=30, n_hi=90, mean_degree=10.0)
+    torch.manual_seed(2)
+    model_o = gnn_ref.GINetNoCluster(30, 1, 3)
+    model = amd.GINet(30, 1, 3)
+    model.load_state_dict(model_o.state_dict())
+    model = model.to(DEV).train()
+    store = GraphStore(pack_graphs(records_from_batch(P.Batch.from_data_list(datas)), require_clusters=False), DEV)
+    h = BatchHandle(store, np.arange(32))
+    mask = (torch.rand(32, 128, generator=torch.Generator().manual_seed(3)) >= 0.4).to(torch.uint8)
+    model_o.dropout_fn = lambda x, p, training: x * mask.float() / (1 - p) if training else x
+    bat = P.Batch.from_data_list([d.clone() for d in datas])
+    out_o = model_o(bat)
+    loss_o = torch.nn.functional.mse_loss(out_o.reshape(-1), bat.y)
+    loss_o.backward()
+    step = FusedTrainStep(model)
+    before = [p.detach().clone() for p in step.params]
+    loss, out = step.step(h, mask=mask.to(DEV))
+    np.testing.assert_allclose(out.cpu().numpy(), out_o.detach().numpy(), **TOL)
+    assert float(loss) == pytest.approx(float(loss_o.detach()), rel=1e-4)
+    grads = dict(zip(amd.PARAM_NAMES, step.grads))
+    for n, p in model_o.named_parameters():
+        assert_grad_close(grads[n].cpu().numpy(), p.grad.numpy(), err_msg=n)
+    ref = [torch.nn.Parameter(b) for b in before]
+    for r, g in zip(ref, step.grads):
+        r.grad = g.detach().clone()
+    torch.optim.Adam(ref, lr=1e-3, weight_decay=1e-5).step()
+    for n, r, p in zip(amd.PARAM_NAMES, ref, step.params):
+        np.testing.assert_allclose(p.detach().cpu().numpy(), r.detach().cpu().numpy(), rtol=1e-5, atol=1e-7, err_msg=n)
+
+
+def test_nocluster_deterministic_bitwise():
+    datas = _synthetic(16, seed=9)
+    store = GraphStore(pack_graphs(records_from_batch(P.Batch.from_data_list(datas))), DEV)
+    h = BatchHandle(store, np.arange(16))
+    torch.manual_seed(1)
+    m = amd.GINet(30, 1, 3).to(DEV).eval()
+    outs = []
+    for _ in range(3):
+        m.zero_grad()
+        o = m(P.Batch.from_data_list(datas))
+        o.sum().backward()
+        outs.append((o.detach().clone(), [p.grad.clone() for p in m.parameters()]))
+    for o, gs in outs[1:]:
+        assert torch.equal(o, outs[0][0])
+        for a, b in zip(gs, outs[0][1]):
+            assert torch.equal(a, b)
+    del h
