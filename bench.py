@@ -31,13 +31,16 @@ from deeprank2_amd.engine import FusedTrainStep  # noqa: E402
 from deeprank2_amd.fused import BatchHandle  # noqa: E402
 from deeprank2_amd.neuralnets.gnn.foutnet import FoutNet  # noqa: E402
 from deeprank2_amd.neuralnets.gnn.ginet import GINet  # noqa: E402
+from deeprank2_amd.neuralnets.gnn.ginet_nocluster import GINet as GINetNoCluster  # noqa: E402
+from deeprank2_amd.neuralnets.gnn.sgat import SGAT  # noqa: E402
 from deeprank2_amd.neuralnets.gnn.vanilla_gnn import VanillaNetwork  # noqa: E402
 from deeprank2_amd.store import GraphRecord, GraphStore, pack_graphs  # noqa: E402
 from deeprank2_amd.utils.synthetic import doubled_edges, make_dataset  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 B_PER_GPU = 64
-MODELS = {"ginet": GINet, "foutnet": FoutNet, "vanilla": VanillaNetwork}
+MODELS = {"ginet": GINet, "foutnet": FoutNet, "vanilla": VanillaNetwork, "sgat": SGAT, "ginet_nocluster": GINetNoCluster}
+ORACLE_MODELS = {"ginet": "GINet", "foutnet": "FoutNet", "vanilla": "VanillaNetwork", "sgat": "SGAT", "ginet_nocluster": "GINetNoCluster"}
 # graph families of SURVEY §8(d): residue-PPI (configs 2/3), atom-level (config 4), SRV-like
 FAMILIES = {
     "residue": {},
@@ -49,6 +52,8 @@ WORKLOADS = {
     ("foutnet", "residue"): "FoutNet residue-PPI training step, BASELINE.json configs[2]",
     ("ginet", "atom"): "GINet atom-level training step (fp32), BASELINE.json configs[3] shape",
     ("ginet", "mixed"): "GINet mixed residue/SRV/atom batch, BASELINE.json configs[4] shape",
+    ("sgat", "residue"): "SGAT residue-PPI training step (1 edge feature), configs[1] graph shape",
+    ("ginet_nocluster", "residue"): "ginet_nocluster.GINet residue-PPI training step, configs[1] graph shape",
 }
 
 
@@ -61,10 +66,11 @@ def make_graphs(kind, n, seed):
     return [make_dataset(1, seed=int(seed * 7919 + i), **FAMILIES[f])[0] for i, f in enumerate(fam)]
 
 
-def records(graphs):
+def records(graphs, edge_features=3):
     out = []
     for i, g in enumerate(graphs):
         ei, ea = doubled_edges(g)
+        ea = ea[:, :edge_features]
         out.append(GraphRecord(x=g["x"], edge_index=ei, edge_attr=ea, cluster0=g["cluster0"], cluster1=g["cluster1"], y=float(g["y"]), pos=g["pos"], name=f"syn{i}"))
     return out
 
@@ -75,7 +81,9 @@ def algorithmic_bytes(packed, gids, model="ginet", out_dim=1):
     (4(K0+1)+4P1), depth-1 members (4(K1+1)+4K0), y (4); writes the per-graph
     weight-gradient slab and head vectors (GINet: 4(32F+1024) + 4*324).
     VanillaNetwork reads no clusters but the edge features (4*E*Fe) and the
-    transposed CSR with its slot map (4(N+1)+8E)."""
+    transposed CSR with its slot map (4(N+1)+8E).  SGAT adds the edge weights
+    (4E) and the pooled ones with their transposed slot map (8*P1) to FoutNet;
+    ginet_nocluster reads x, the CSR and its transpose and no clusters."""
     n, e, k0, p1, k1 = (a[gids] for a in packed.sizes())
     f = packed.n_feat
     r4 = lambda v: (v + 3) & ~3  # noqa: E731
@@ -84,8 +92,13 @@ def algorithmic_bytes(packed, gids, model="ginet", out_dim=1):
         per = 4 * n * f + 2 * (4 * (n + 1) + 4 * e) + 4 * e + 4 * e * fe + 4
         per = per + 4 * 2 * (32 * (2 * f + fe) + 32 + f * (f + 32) + f) + 4 * (r4(f) + 256 + r4(out_dim))
         return int(per.sum())
+    if model == "ginet_nocluster":
+        per = 4 * n * f + 2 * (4 * (n + 1) + 2 * e) + 4 + 4 * (32 * f + 1024) + 4 * (320 + r4(out_dim))
+        return int(per.sum())
     per = 4 * n * f + 4 * (n + 1) + 4 * e + 4 * (k0 + 1) + 4 * n + 4 * (k0 + 1) + 4 * p1 + 4 * (k1 + 1) + 4 * k0 + 4
-    if model == "foutnet":
+    if model == "sgat":
+        per = per + 4 * e + 8 * p1
+    if model in ("foutnet", "sgat"):
         per = per + 4 * (32 * f + 1072) + 4 * (160 + r4(out_dim))
     else:
         per = per + 4 * (32 * f + 1024) + 4 * (320 + r4(out_dim))
@@ -127,7 +140,10 @@ def cpu_baseline(graphs, budget_s=15.0, max_steps=60, model_name="ginet"):
     torch.set_num_threads(cores)
     datas = [data_ref.synthetic_to_data(g) for g in graphs]
     torch.manual_seed(1234)
-    model = {"ginet": gnn_ref.GINet, "foutnet": gnn_ref.FoutNet, "vanilla": gnn_ref.VanillaNetwork}[model_name](30, 1, 3).train()
+    if model_name == "sgat":
+        for d in datas:
+            d.edge_attr = d.edge_attr[:, :1].contiguous()
+    model = gnn_ref.MODELS[ORACLE_MODELS[model_name]](30, 1, 3).train()
     opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-5)
 
     def one():
@@ -146,7 +162,7 @@ def cpu_baseline(graphs, budget_s=15.0, max_steps=60, model_name="ginet"):
         one()
         n += 1
     dt = (time.perf_counter() - t0) / n
-    name = {"ginet": "GINet", "foutnet": "FoutNet", "vanilla": "VanillaNetwork"}[model_name]
+    name = ORACLE_MODELS[model_name]
     return {"value": round(len(graphs) / dt, 2), "unit": "graphs/s", "cores": cores, "kind": "port", "sample": f"{n} {name}(30,1,3) train steps (fwd+MSE+bwd+Adam) on one batch of {len(graphs)} of the same synthetic graphs; oracle/gnn_ref.py on torch CPU, {cores} threads; {dt * 1e3:.1f} ms/step"}
 
 
@@ -187,7 +203,7 @@ def main():  # noqa: PLR0915
     if args.graphs in ("atom", "mixed"):
         args.batches = min(args.batches, 4)  # generation time of ~3k-node graphs
     graphs = make_graphs(args.graphs, B * args.batches, seed=1000 + rank)
-    packed = pack_graphs(records(graphs))
+    packed = pack_graphs(records(graphs, 1 if args.model == "sgat" else 3), require_clusters=args.model != "ginet_nocluster")
     store = GraphStore(packed, dev)
     order = np.random.default_rng(rank).permutation(packed.n_graphs).astype(np.int32)
     handles = [BatchHandle(store, order[i * B:(i + 1) * B]) for i in range(args.batches)]
@@ -278,7 +294,7 @@ def main():  # noqa: PLR0915
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(graphs[:B], model_name=args.model)
         workload = WORKLOADS.get((args.model, args.graphs), f"{args.model} on {args.graphs} graphs (diagnostic)")
-        kname = {"ginet": "ginet_large_conv1_kernel + ginet_large_tail_kernel (dr_ginet_large_pass)" if large else "ginet_graph_kernel (dr_ginet_graph_pass, fwd+loss+bwd, 1 workgroup/graph)", "foutnet": "fout_graph_kernel (dr_fout_graph_pass)", "vanilla": "vanilla_graph_kernel (dr_vanilla_graph_pass)"}[args.model]
+        kname = {"ginet": "ginet_large_conv1_kernel + ginet_large_tail_kernel (dr_ginet_large_pass)" if large else "ginet_graph_kernel (dr_ginet_graph_pass, fwd+loss+bwd, 1 workgroup/graph)", "foutnet": "fout_graph_kernel<false> (dr_fout_graph_pass)", "vanilla": "vanilla_graph_kernel (dr_vanilla_graph_pass)", "sgat": "fout_graph_kernel<true> (dr_sgat_graph_pass)", "ginet_nocluster": "ginet_nocluster_kernel (dr_ginet_nocluster_graph_pass)"}[args.model]
         result = {
             "metric": "graphs/sec per training step, GINet residue-PPI (fwd+MSE+bwd+Adam)" if default_cfg else f"graphs/sec per training step, {workload} (fwd+MSE+bwd+Adam)",
             "value": round(graphs_total / elapsed, 1),
@@ -300,7 +316,7 @@ def main():  # noqa: PLR0915
                 "mean_nodes_per_graph": round(float(np.diff(packed.node_off).mean()), 1),
                 "mean_edges_per_graph": round(float(np.diff(packed.edge_off).mean()), 1),
                 "node_features": 30,
-                "edge_features": 3,
+                "edge_features": 1 if args.model == "sgat" else 3,
                 "resident_graphs_per_gpu": packed.n_graphs,
                 "parallelism": f"dp{world}",
             },
