@@ -304,6 +304,8 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
     hl.dgp = t.dgp;
     if (!drk::ginet_head<NT>(a.p, hl, fc1_row, fc1_col, fc1_bias, b, OUT, y_g, drop_offset)) return;
   }
+  STAMP(8);  // (stamps 8, 9 kept so the phase indices of the profile tool stay put)
+  STAMP(9);
 
   STAMP(10);
   // ---------------- depth-1 pooling + mean backward -------------------------

@@ -34,9 +34,11 @@ constexpr int NW = NT / 64;
 constexpr int HEADW = 672;  // g64 hpre128 hh128 hd128 dh128 dg64 dout16 spare16
 constexpr int LZ = 36;      // Z2 row stride: 16-byte rows (float4 gathers in the backward)
 
+constexpr int SCRATCH = 3 * 1024;  // K-split partial tiles of the backward reductions
+
 struct NcCarve {
   int KP, LDW, XS;
-  int w1, w2, fc2, xz2, z1, h1, mask, rp, trp, col, tcol, head, dgp, dgn, total;
+  int w1, dgp, w2, fc2, xz2, z1, h1, mask, rp, trp, col, tcol, head, dgn, total;
 };
 
 __host__ __device__ inline NcCarve nc_carve(int N, int E, int F, int OUT) {
@@ -48,7 +50,10 @@ __host__ __device__ inline NcCarve nc_carve(int N, int E, int F, int OUT) {
 #define TAKE(field, words) \
   c.field = o;             \
   o += r4(words);
+  // w1 and dgp are dead in the backward: together with the pad up to SCRATCH
+  // words they hold the K-split partial tiles of dW2 / dW1
   TAKE(w1, 32 * c.LDW)             // [W1; W1e] row-major, zero-padded to KP
+  TAKE(dgp, imax(NW * 64, SCRATCH - r4(32 * c.LDW)))  // column-sum partials of H2, then the head's dG partials
   TAKE(w2, 1024)                   // [W2 | W2e] (conv2 / conv2_ext .fc.weight)
   TAKE(fc2, OUT * 128 + OUT)
   TAKE(xz2, N * imax(c.XS, LZ))    // X, then Z2 = A H1 (X is dead after the conv1 gather), then dZ2
@@ -60,7 +65,6 @@ __host__ __device__ inline NcCarve nc_carve(int N, int E, int F, int OUT) {
   TAKE(col, (E + 1) / 2)
   TAKE(tcol, (E + 1) / 2)
   TAKE(head, HEADW)
-  TAKE(dgp, NW * 64)               // column-sum partials of H2, then the head's dG partials
   TAKE(dgn, 64)                    // dG / N
 #undef TAKE
   c.total = o;
@@ -123,6 +127,7 @@ __global__ void __launch_bounds__(NT) ginet_nocluster_kernel(NcArgs a) {
   uint16_t* scol = reinterpret_cast<uint16_t*>(lds + c.col);
   uint16_t* stcol = reinterpret_cast<uint16_t*>(lds + c.tcol);
   float* sDgp = lds + c.dgp;
+  float* sScr = lds + c.w1;  // backward scratch (w1 + dgp, >= SCRATCH words)
   float* sDgN = lds + c.dgn;
   GinetHeadLds hl;
   hl.fc2 = sFc2;
@@ -135,6 +140,7 @@ __global__ void __launch_bounds__(NT) ginet_nocluster_kernel(NcArgs a) {
   hl.dout = hl.dg + 64;
   hl.dgp = sDgp;
 
+  DRK_STAMP(0);
   // ---------------- stage ---------------------------------------------------
   float fc1_row[8], fc1_col[8], fc1_bias;
   {
@@ -174,6 +180,7 @@ __global__ void __launch_bounds__(NT) ginet_nocluster_kernel(NcArgs a) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  DRK_STAMP(1);
 
   float wv1[2], wv2, wfc[3];
   {
@@ -213,6 +220,7 @@ __global__ void __launch_bounds__(NT) ginet_nocluster_kernel(NcArgs a) {
       if (tid + u * NT < nf) sFc2[tid + u * NT] = wfc[u];
   }
   __syncthreads();
+  DRK_STAMP(2);
 
   // ---------------- H1 = relu(Z1 [W1; W1e]^T) on MFMA ----------------------
   const int li = lane & 15, kq = lane >> 4;
@@ -245,10 +253,12 @@ __global__ void __launch_bounds__(NT) ginet_nocluster_kernel(NcArgs a) {
     }
   }
   __syncthreads();
+  DRK_STAMP(3);
 
   // ---------------- Z2 = A H1 (X is dead: Z2 takes its place) ---------------
   gather_rows(srp, scol, sH1, 32, 8, sZ2, LZ, N);
   __syncthreads();
+  DRK_STAMP(4);
 
   // ---------------- H2 = relu(Z2_b W2_b^T): column sums + relu' bits -------
   {
@@ -266,27 +276,20 @@ __global__ void __launch_bounds__(NT) ginet_nocluster_kernel(NcArgs a) {
           acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, sW2[(br * 32 + li) * 16 + kk], acc0, 0, 0, 0);
           acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, sW2[(br * 32 + 16 + li) * 16 + kk], acc1, 0, 0, 0);
         }
-        uint32_t bits[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = r0 + kq * 4 + r;
-          if (row < N) {
+          const bool live = row < N;
+          if (live) {
             cs[br * 2] += relu_keepnan(acc0[r]);
             cs[br * 2 + 1] += relu_keepnan(acc1[r]);
-            // relu_bwd passes the gradient unless the output is <= 0 (NaN passes)
-            bits[r] = (acc0[r] <= 0.f ? 0u : (1u << li)) | (acc1[r] <= 0.f ? 0u : (1u << (16 + li)));
           }
-        }
-        // OR the 16 lanes (li) of each row group together, then one LDS write per row
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          uint32_t v = bits[r];
-          v |= __shfl_xor(v, 1, 64);
-          v |= __shfl_xor(v, 2, 64);
-          v |= __shfl_xor(v, 4, 64);
-          v |= __shfl_xor(v, 8, 64);
-          const int row = r0 + kq * 4 + r;
-          if (li == 0 && row < N) sMask[row * 2 + br] = v;
+          // relu_bwd passes the gradient unless the output is <= 0 (NaN passes).
+          // Lane kq*16+li holds channel li of row r0+kq*4+r: one ballot per half.
+          const uint64_t lo = __ballot(live && !(acc0[r] <= 0.f));
+          const uint64_t hi = __ballot(live && !(acc1[r] <= 0.f));
+          if (li == 0 && live)
+            sMask[row * 2 + br] = (uint32_t)((lo >> (kq * 16)) & 0xffffu) | ((uint32_t)((hi >> (kq * 16)) & 0xffffu) << 16);
         }
       }
     }
@@ -301,6 +304,7 @@ __global__ void __launch_bounds__(NT) ginet_nocluster_kernel(NcArgs a) {
     }
   }
   __syncthreads();
+  DRK_STAMP(5);
   if (tid < 64) {  // per-graph scatter_mean (ginet_nocluster.py:103-104)
     float acc = 0.f;
     for (int w = 0; w < NW; ++w) acc += sDgp[w * 64 + tid];
@@ -309,31 +313,67 @@ __global__ void __launch_bounds__(NT) ginet_nocluster_kernel(NcArgs a) {
   __syncthreads();
 
   // ---------------- head, loss, head backward (shared with GINet) -----------
+  DRK_STAMP(6);
   if (!ginet_head<NT>(a.p, hl, fc1_row, fc1_col, fc1_bias, b, OUT, y_g, drop_offset)) return;
+  DRK_STAMP(7);
 
   // ---------------- conv2 backward -----------------------------------------
   if (tid < 64) sDgN[tid] = hl.dg[tid] / (float)N;
   __syncthreads();
+  // dW2cat[o][j] = (dG[o]/N) sum_{i: bit(i,o)} Z2[i][br*16+j]: a [64 x N] x [N x 16]
+  // MFMA product with the 0/1 bit matrix as A; 4 output tiles x 4 node splits
+  // (one per wave), splits combined in fixed order (deterministic)
   {
-    const int SS = DR_SLAB_STRIDE(F);
-    float* slab = a.p.slab + (int64_t)b * SS + 32 * F;
-    const int o = tid >> 4, j = tid & 15, br = o >> 5, bit = o & 31;  // 1024 = 64 outputs x 16 inputs
-    float acc = 0.f;
-    for (int i = 0; i < N; ++i)
-      if ((sMask[i * 2 + br] >> bit) & 1u) acc += sZ2[i * LZ + br * 16 + j];
-    slab[tid] = acc * sDgN[o];  // dW2cat[o][j] = sum_i dS2[i][o] Z2[i][br*16+j]
+    const int ot = wave & 3, sp = wave >> 2, br = ot >> 1, sh = (ot & 1) * 16 + li;
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int i0 = sp * 4; i0 < N; i0 += 16) {
+      const int i = i0 + kq;
+      float av = 0.f, bv = 0.f;
+      if (i < N) {
+        av = ((sMask[i * 2 + br] >> sh) & 1u) ? 1.f : 0.f;
+        bv = sZ2[i * LZ + br * 16 + li];
+      }
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+    }
+    if (sp > 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sScr[((ot * 3 + sp - 1) * 16 + kq * 4 + r) * 16 + li] = acc[r];
+    }
+    __syncthreads();
+    if (sp == 0) {
+      float* slab = a.p.slab + (int64_t)b * DR_SLAB_STRIDE(F) + 32 * F;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = acc[r];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) v += sScr[((ot * 3 + q) * 16 + kq * 4 + r) * 16 + li];
+        const int o = ot * 16 + kq * 4 + r;
+        slab[o * 16 + li] = v * sDgN[o];
+      }
+    }
   }
   __syncthreads();
-  for (int p = tid; p < N * 32; p += NT) {  // dZ2 = dS2 W2_b (in place of Z2)
-    const int i = p >> 5, ch = p & 31, br = ch >> 4, j = ch & 15;
-    const uint32_t m = sMask[i * 2 + br];
-    float acc = 0.f;
-#pragma unroll 8
-    for (int ol = 0; ol < 32; ++ol)
-      if ((m >> ol) & 1u) acc = fmaf(sDgN[br * 32 + ol], sW2[(br * 32 + ol) * 16 + j], acc);
-    sZ2[i * LZ + ch] = acc;
+  DRK_STAMP(8);
+  // dZ2_b = dS2_b W2_b (N x 32 by 32 x 16 per branch, MFMA), in place of Z2:
+  // each (row tile, branch) job reads only bits and W2 and writes its own block
+  for (int job = wave; job < ((N + 15) >> 4) * 2; job += NW) {
+    const int r0 = (job >> 1) * 16, br = job & 1;
+    const uint32_t m = sMask[min(r0 + li, N - 1) * 2 + br];
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int ol = 4 * u + kq;
+      const float av = ((m >> ol) & 1u) ? sDgN[br * 32 + ol] : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, sW2[(br * 32 + ol) * 16 + li], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = r0 + kq * 4 + r;
+      if (row < N) sZ2[row * LZ + br * 16 + li] = acc[r];
+    }
   }
   __syncthreads();
+  DRK_STAMP(9);
   // dS1 = relu'(H1) (A^T dZ2), in place of H1 (transposed CSR, true edge order)
   {
     const int sub = tid & 7;
@@ -349,17 +389,44 @@ __global__ void __launch_bounds__(NT) ginet_nocluster_kernel(NcArgs a) {
     }
   }
   __syncthreads();
-  // dW1cat[ch][kk] = sum_i dS1[i][ch] Z1[i][kk]
+  DRK_STAMP(10);
+  // dW1cat[ch][kk] = sum_i dS1[i][ch] Z1[i][kk]: [32 x N] x [N x KP] on MFMA;
+  // T = 2*KP/16 output tiles (Z1's K padding columns are zero), NW/T node
+  // splits per tile (T <= 8 as F <= 64), splits combined in fixed order
   {
-    const int SS = DR_SLAB_STRIDE(F);
-    float* slab = a.p.slab + (int64_t)b * SS;
-    for (int p = tid; p < 32 * F; p += NT) {
-      const int ch = p / F, kk = p - ch * F;
-      float acc = 0.f;
-      for (int i = 0; i < N; ++i) acc = fmaf(sH1[i * 32 + ch], sZ1[i * LDW + kk], acc);
-      slab[p] = acc;
+    const int nkt = KP >> 4, T = 2 * nkt, S = min(NW / T, 4);  // (T-tiles x (S-1) partials fit SCRATCH)
+    const int tile = wave % T, sp = wave / T;
+    const int ct = tile / nkt, kt = tile - ct * nkt;
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (sp < S) {
+      for (int i0 = sp * 4; i0 < N; i0 += 4 * S) {
+        const int i = i0 + kq;
+        float av = 0.f, bv = 0.f;
+        if (i < N) {
+          av = sH1[i * 32 + ct * 16 + li];
+          bv = sZ1[i * LDW + kt * 16 + li];
+        }
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+      }
+      if (sp > 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sScr[((tile * (S - 1) + sp - 1) * 16 + kq * 4 + r) * 16 + li] = acc[r];
+      }
+    }
+    __syncthreads();
+    const int kk = kt * 16 + li;
+    if (sp == 0 && kk < F) {
+      float* slab = a.p.slab + (int64_t)b * DR_SLAB_STRIDE(F);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = acc[r];
+        for (int q = 0; q < S - 1; ++q) v += sScr[((tile * (S - 1) + q) * 16 + kq * 4 + r) * 16 + li];
+        slab[(ct * 16 + kq * 4 + r) * F + kk] = v;
+      }
     }
   }
+  __syncthreads();
+  DRK_STAMP(11);
 }
 
 }  // namespace

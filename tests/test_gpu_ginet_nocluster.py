@@ -122,3 +122,27 @@ def test_nocluster_deterministic_bitwise():
         for a, b in zip(gs, outs[0][1]):
             assert torch.equal(a, b)
     del h
+
+
+@pytest.mark.parametrize("f", [7, 16, 33])
+def test_nocluster_feature_widths_vs_oracle(f):
+    """Other K paddings of the conv1 GEMM / dW1 tiling (KP = 16, 16, 48)."""
+    rng = np.random.default_rng(f)
+    datas = _synthetic(6, seed=40 + f, n_lo=10, n_hi=90, mean_degree=6.0)
+    for d in datas:
+        d.x = torch.from_numpy(rng.normal(size=(d.x.shape[0], f)).astype(np.float32))
+    torch.manual_seed(f)
+    model_o = gnn_ref.GINetNoCluster(f, 2, 3)
+    model = amd.GINet(f, 2, 3)
+    model.load_state_dict(model_o.state_dict())
+    model = model.to(DEV).eval()
+    model_o.eval()
+    bat_o = P.Batch.from_data_list([d.clone() for d in datas])
+    out_o = model_o(bat_o)
+    out_o.square().sum().backward()
+    out = model(P.Batch.from_data_list(datas))
+    out.square().sum().backward()
+    np.testing.assert_allclose(out.detach().cpu().numpy(), out_o.detach().numpy(), **TOL)
+    ref = dict(model_o.named_parameters())
+    for n, p in model.named_parameters():
+        assert_grad_close(p.grad.cpu().numpy(), ref[n].grad.numpy(), err_msg=n)

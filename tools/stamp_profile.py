@@ -1,6 +1,7 @@
-"""Diagnostic: per-phase cycle shares of ginet_graph_kernel from the stamps build.
+"""Diagnostic: per-phase cycle shares of ginet_graph_kernel (or
+ginet_nocluster_kernel) from the stamps build.
 
-    DR_LIB_NAME=libdeeprank2_amd_stamps.so python tools/stamp_profile.py
+    DR_LIB_NAME=libdeeprank2_amd_stamps.so python tools/stamp_profile.py [B] [ginet|ginet_nocluster]
 
 Stamps (s_memtime, shader clock cycles) are taken by thread 0 right after each
 phase barrier; the build that takes them is never used for timing claims —
@@ -21,19 +22,23 @@ os.environ.setdefault("DR_LIB_NAME", "libdeeprank2_amd_stamps.so")
 
 from bench import records  # noqa: E402
 from deeprank2_amd.neuralnets.gnn import ginet as amd  # noqa: E402
+from deeprank2_amd.neuralnets.gnn import ginet_nocluster as amd_nc  # noqa: E402
 from deeprank2_amd.store import GraphStore, pack_graphs  # noqa: E402
 from deeprank2_amd.utils.synthetic import make_dataset  # noqa: E402
 
-PHASES = ["stage", "gather Z=AX", "gemm H=relu(ZW)", "pool0", "gemm2+spmm2", "pool1", "mean", "head-fwd", "loss", "head-bwd", "pool1-bwd", "spmm2T", "dW2+dP1", "dW1"]
+PHASES_NC = ["stage", "gather Z1=AX", "gemm H1", "gather Z2=AH1", "gemm2+bits+colsum", "mean", "head fwd+loss+bwd", "dW2", "dZ2", "spmmT dS1", "dW1"]
+PHASES = ["stage", "gather Z=AX", "gemm H=relu(ZW)", "pool0", "gemm2+spmm2", "pool1", "mean", "head fwd+loss+bwd", "-", "-", "pool1-bwd", "spmm2T", "dW2+dP1", "dW1"]
 
 
 def main():
     dev = torch.device("cuda:0")
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+    which = sys.argv[2] if len(sys.argv) > 2 else "ginet"
+    mod, phases = (amd_nc, PHASES_NC) if which == "ginet_nocluster" else (amd, PHASES)
     store = GraphStore(pack_graphs(records(make_dataset(B, seed=1000))), dev)
     h = amd.BatchHandle(store, np.arange(B))
     torch.manual_seed(0)
-    model = amd.GINet(30, 1, 3).to(dev)
+    model = mod.GINet(30, 1, 3).to(dev)
     params = model.ordered_params()
     st = torch.zeros(B * 32, dtype=torch.int64, device=dev)
     out = torch.empty(B, 1, device=dev)
@@ -42,16 +47,17 @@ def main():
     lpg = torch.empty(B, device=dev)
     rows = []
     for it in range(30):
-        amd.graph_pass(h, params, 1, 3, dropout=amd.Dropout(0.4, seed=1, offset=it), loss_kind=1, loss_scale=1 / B, out=out, loss_per_graph=lpg, slab=slab, head=head, stamps=st)
+        mod.graph_pass(h, params, 1, 3, dropout=amd.Dropout(0.4, seed=1, offset=it), loss_kind=1, loss_scale=1 / B, out=out, loss_per_graph=lpg, slab=slab, head=head, stamps=st)
         torch.cuda.synchronize()
         if it >= 5:
-            rows.append(st.view(B, 32)[:, :15].cpu().numpy().copy())
+            rows.append(st.view(B, 32)[:, : len(phases) + 1].cpu().numpy().copy())
     a = np.stack(rows)  # [iters, B, 16]
     d = np.diff(a, axis=2).astype(np.float64)  # phase i = stamp[i+1]-stamp[i]
     med = np.median(d.reshape(-1, d.shape[-1]), axis=0)
     tot = med.sum()
     print(f"B={B}  median cycles per graph-kernel workgroup: {tot:.0f}")
-    for name, v in zip(PHASES, med):
+    print(which)
+    for name, v in zip(phases, med):
         print(f"  {name:18s} {v:8.0f} cyc  {100 * v / tot:5.1f}%")
 
 
