@@ -302,10 +302,8 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
     hl.dg = t.dg;
     hl.dout = t.dout;
     hl.dgp = t.dgp;
-    if (!drk::ginet_head<NT>(a.p, hl, fc1_row, fc1_col, fc1_bias, b, OUT, y_g, drop_offset)) return;
-  }
-  STAMP(8);  // (stamps 8, 9 kept so the phase indices of the profile tool stay put)
-  STAMP(9);
+    if (!drk::ginet_head<NT>(a.p, hl, fc1_row, fc1_col, fc1_bias, b, OUT, y_g, drop_offset, 8)) return;
+  }  // stamps 8 (forward head done) and 9 (loss gradient done) are taken inside
 
   STAMP(10);
   // ---------------- depth-1 pooling + mean backward -------------------------

@@ -19,10 +19,23 @@ struct GinetHeadLds {
   float *fc2, *g, *hpre, *hh, *hd, *dh, *dg, *dout, *dgp;
 };
 
+// Diagnostic stamps (stamps build only): s_memtime at two points inside the head.
+__device__ __forceinline__ void head_stamp(int64_t* row, int i) {
+#ifdef DR_STAMPS
+  __builtin_amdgcn_sched_barrier(0);
+  if (threadIdx.x == 0 && row) row[i] = __builtin_amdgcn_s_memtime();
+  __builtin_amdgcn_sched_barrier(0);
+#else
+  (void)row;
+  (void)i;
+#endif
+}
+
 template <int NT>
 __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds& t, const float (&fc1_row)[8],
                                            const float (&fc1_col)[8], float fc1_bias, int b, int OUT, float y_g,
-                                           uint64_t drop_offset) {
+                                           uint64_t drop_offset, int stamp0 = -1) {
+  int64_t* srow = (stamp0 >= 0 && p.stamps) ? p.stamps + (int64_t)b * 32 : nullptr;
   constexpr int NW = NT / 64;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -57,6 +70,7 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
   if ((p.flags & DR_PASS_FORWARD) && tid < OUT) p.out[(int64_t)b * OUT + tid] = t.dout[tid];
   if (!(p.flags & DR_PASS_BACKWARD)) return false;
   __syncthreads();
+  head_stamp(srow, stamp0);
 
   // ---------------- loss gradient (trainer.py:688-689) ----------------------
   if (tid == 0) {
@@ -80,6 +94,7 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
   }
   __syncthreads();
 
+  head_stamp(srow, stamp0 + 1);
   // ---------------- head backward -------------------------------------------
   if (tid < 128) {
     float acc = 0.f;

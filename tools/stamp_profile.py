@@ -27,7 +27,7 @@ from deeprank2_amd.store import GraphStore, pack_graphs  # noqa: E402
 from deeprank2_amd.utils.synthetic import make_dataset  # noqa: E402
 
 PHASES_NC = ["stage", "gather Z1=AX", "gemm H1", "gather Z2=AH1", "gemm2+bits+colsum", "mean", "head fwd+loss+bwd", "dW2", "dZ2", "spmmT dS1", "dW1"]
-PHASES = ["stage", "gather Z=AX", "gemm H=relu(ZW)", "pool0", "gemm2+spmm2", "pool1", "mean", "head fwd+loss+bwd", "-", "-", "pool1-bwd", "spmm2T", "dW2+dP1", "dW1"]
+PHASES = ["stage", "gather Z=AX", "gemm H=relu(ZW)", "pool0", "gemm2+spmm2", "pool1", "mean", "head fwd (fc1,fc2)", "loss grad", "head bwd", "pool1-bwd", "spmm2T", "dW2+dP1", "dW1"]
 
 
 def main():
