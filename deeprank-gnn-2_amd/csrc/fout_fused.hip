@@ -195,8 +195,8 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
   DRK_STAMP(0);
   // ---------------- stage: graph by DMA, weights through VGPRs --------------
   const float y_g = s.y[g];
-  // no dropout here, but the step counter contract holds: snapshot for dr_reduce_update
-  if (a.p.step_counter && b == 0 && tid == 0) a.p.step_counter[1] = a.p.step_counter[0];
+  // no dropout here, but the step counter contract holds: snapshot for
+  // dr_reduce_update (stored after the staging wait below)
   dma_x4<NT>(sX, s.x + n0 * (int64_t)XS, N * XS / 4);
   dma_x4<NT>(scol, s.col + ec0, (E + 7) / 8);
   dma_words<NT>(srp, s.rowptr + n0 + g, N + 1);
@@ -215,7 +215,9 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
     dma_words<NT>(sP1w, s.p1_ea + q0, P1);
     dma_words<NT>(sP1tid, s.p1t_pid + q0, P1);
   }
+  const int64_t counter0 = (a.p.step_counter && b == 0) ? a.p.step_counter[0] : 0;  // loaded late: no early wait
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (a.p.step_counter && b == 0 && tid == 0) a.p.step_counter[1] = counter0;
   __syncthreads();
 
   DRK_STAMP(1);

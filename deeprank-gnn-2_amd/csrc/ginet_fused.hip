@@ -387,6 +387,13 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   const int F = s.n_feat;
   const int alias = s.transpose_aliased;
   const int OUT = a.p.out_dim;
+  // Fetch every kernel-argument field the staging needs, and the descriptor,
+  // in one scalar round trip each (hipcc would otherwise load them lazily
+  // with a wait before each DMA).
+  asm volatile("" ::"s"(s.x), "s"(s.col), "s"(s.rowptr), "s"(s.m0_ptr), "s"(s.m0_idx), "s"(s.p1_rowptr),
+               "s"(s.p1_col), "s"(s.p1t_rowptr), "s"(s.p1t_col), "s"(s.m1_ptr), "s"(s.m1_idx), "s"(s.y), "s"(F),
+               "s"(alias), "s"(OUT), "s"(n0), "s"(ec0), "s"(k00), "s"(q0), "s"(k10), "s"(N), "s"(E), "s"(K0),
+               "s"(P1), "s"(K1), "s"(g));
   const Carve c = carve(N, E, F, K0, P1, K1, alias, OUT);
   const int KP = c.KP, LDW = c.LDW, XS = c.XS;
 
@@ -428,10 +435,6 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   }
   const float y_g = s.y[g];
   uint64_t drop_offset = a.p.drop_offset;
-  if (a.p.step_counter) {
-    drop_offset = (uint64_t)a.p.step_counter[0];
-    if (b == 0 && tid == 0) a.p.step_counter[1] = (int64_t)drop_offset;  // snapshot for the update kernel
-  }
   dma_x4(sX, s.x + n0 * (int64_t)XS, N * XS / 4);
   dma_x4(scol, s.col + ec0, (E + 7) / 8);
   dma_words(srp, s.rowptr + n0 + g, N + 1);
@@ -457,7 +460,11 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
       sZ[i * LDW + XS + (p - i * padz)] = 0.f;
     }
   }
+  if (a.p.step_counter) drop_offset = (uint64_t)a.p.step_counter[0];  // loaded late: no early wait
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // snapshot for dr_reduce_update, stored only now so that no wait for the
+  // counter load sits between the descriptor and the graph DMA
+  if (a.p.step_counter && b == 0 && tid == 0) a.p.step_counter[1] = (int64_t)drop_offset;
   __syncthreads();
 
   STAMP(1);
@@ -846,10 +853,6 @@ __global__ void __launch_bounds__(NT) ginet_large_tail_kernel(LargeArgs la) {
   }
   const float y_g = s.y[g];
   uint64_t drop_offset = a.p.drop_offset;
-  if (a.p.step_counter) {
-    drop_offset = (uint64_t)a.p.step_counter[0];
-    if (b == 0 && tid == 0) a.p.step_counter[1] = (int64_t)drop_offset;
-  }
   drk::dma_words<NT>(t.p1rp, s.p1_rowptr + k00 + g, K0 + 1);
   drk::dma_words<NT>(t.p1c, s.p1_col + q0, P1);
   if (!alias) {
@@ -876,7 +879,11 @@ __global__ void __launch_bounds__(NT) ginet_large_tail_kernel(LargeArgs la) {
     t.p1[p] = (best == LOWEST) ? 0.f : best;
     t.a1[p] = arg;
   }
+  if (a.p.step_counter) drop_offset = (uint64_t)a.p.step_counter[0];  // loaded late: no early wait
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // snapshot for dr_reduce_update, stored only now so that no wait for the
+  // counter load sits between the descriptor and the graph DMA
+  if (a.p.step_counter && b == 0 && tid == 0) a.p.step_counter[1] = (int64_t)drop_offset;
   __syncthreads();
   const float* z = pl.z + (int64_t)pl.z_row0[b] * r4(F);
   const int XS = r4(F);

@@ -156,10 +156,6 @@ __global__ void __launch_bounds__(NT) ginet_nocluster_kernel(NcArgs a) {
   }
   const float y_g = s.y[g];
   uint64_t drop_offset = a.p.drop_offset;
-  if (a.p.step_counter) {
-    drop_offset = (uint64_t)a.p.step_counter[0];
-    if (b == 0 && tid == 0) a.p.step_counter[1] = (int64_t)drop_offset;
-  }
   dma_x4<NT>(sX, s.x + n0 * (int64_t)XS, N * XS / 4);
   dma_x4<NT>(scol, s.col + ec0, (E + 7) / 8);
   dma_x4<NT>(stcol, s.t_col + ec0, (E + 7) / 8);
@@ -178,7 +174,9 @@ __global__ void __launch_bounds__(NT) ginet_nocluster_kernel(NcArgs a) {
     }
     for (int p = tid; p < 2 * N; p += NT) sMask[p] = 0u;
   }
+  if (a.p.step_counter) drop_offset = (uint64_t)a.p.step_counter[0];  // loaded late: no early wait
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (a.p.step_counter && b == 0 && tid == 0) a.p.step_counter[1] = (int64_t)drop_offset;  // snapshot for dr_reduce_update
   __syncthreads();
   DRK_STAMP(1);
 
