@@ -363,7 +363,24 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
     for (int p = tid; p < 32 * F; p += NT) {
       const int ch = p / F, kk = p - ch * F;
       float acc = 0.f;
-      for (int k = 0; k < K0; ++k) {
+      int k = 0;
+      // 8 clusters at a time: the Z reads (HBM on the large path) are issued
+      // together, then accumulated in cluster order (same fmaf chain)
+      for (; k + 8 <= K0; k += 8) {
+        float zv[8], dv[8];
+        bool ok[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = t.a1[(k + u) * 32 + ch];
+          ok[u] = i < N;
+          dv[u] = t.dp1[(k + u) * 32 + ch];
+          zv[u] = zat(ok[u] ? i : 0, kk);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (ok[u]) acc = fmaf(dv[u], zv[u], acc);
+      }
+      for (; k < K0; ++k) {
         const int i = t.a1[k * 32 + ch];
         if (i < N) acc = fmaf(t.dp1[k * 32 + ch], zat(i, kk), acc);
       }
@@ -868,7 +885,24 @@ __global__ void __launch_bounds__(NT) ginet_large_tail_kernel(LargeArgs la) {
   for (int p = tid; p < K0 * 32; p += NT) {
     float best = LOWEST;
     int arg = N;
-    for (int tl = tb; tl < te; ++tl) {
+    int tl = tb;
+    for (; tl + 8 <= te; tl += 8) {  // 8 tiles' partials loaded together, combined in tile order
+      float v[8];
+      int ag[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int64_t o = ((int64_t)(tl + u) * pl.k0_max) * 32 + p;
+        v[u] = pl.part_val[o];
+        ag[u] = pl.part_arg[o];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (v[u] > best) {
+          best = v[u];
+          arg = ag[u];
+        }
+    }
+    for (; tl < te; ++tl) {
       const int64_t o = ((int64_t)tl * pl.k0_max) * 32 + p;
       const float v = pl.part_val[o];
       if (v > best) {
