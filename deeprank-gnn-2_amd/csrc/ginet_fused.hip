@@ -52,7 +52,7 @@ __host__ __device__ inline int r16(int v) { return (v + 15) & ~15; }
 struct Carve {
   int KP, LDW, XS;
   int w1, w2, fc2, x, z, h, rp, col, m0p, m0i, p1, a1, dp1, y2, h2, d2, p1rp, p1c, p1trp, p1tc, m1p, m1i, p2,
-      nt, head, dgp, red, total;
+      nt, cl1, head, dgp, red, total;
 };
 
 // LDS carve (4-byte words, every region 16-byte aligned).  X keeps the HBM
@@ -97,6 +97,7 @@ __host__ __device__ inline Carve carve(int N, int E, int F, int K0, int P1, int 
   TAKE(m1i, K0)
   TAKE(p2, K1 * 64)
   TAKE(nt, K1 * 64)
+  TAKE(cl1, K0)  // depth-1 cluster of each depth-0 cluster
   TAKE(head, HEADW)
   TAKE(dgp, NW * 64)
   TAKE(red, 2 * NT)
@@ -205,7 +206,7 @@ __device__ __forceinline__ void gather_rows(const int* rp, const uint16_t* col, 
 struct TailLds {
   float *w2, *fc2, *p1, *dp1, *y2, *h2, *d2, *p2, *nt, *dgp;
   float *g, *hpre, *hh, *hd, *dh, *dg, *dout;
-  int *a1, *p1rp, *p1c, *p1trp, *p1tc, *m1p, *m1i;
+  int *a1, *p1rp, *p1c, *p1trp, *p1tc, *m1p, *m1i, *cl1;
 };
 
 template <class C>
@@ -227,6 +228,7 @@ __device__ __forceinline__ TailLds tail_lds(const C& c, float* lds) {
   t.m1i = reinterpret_cast<int*>(lds + c.m1i);
   t.p2 = lds + c.p2;
   t.nt = lds + c.nt;
+  t.cl1 = reinterpret_cast<int*>(lds + c.cl1);
   t.g = lds + c.head;
   t.hpre = t.g + 64;
   t.hh = t.hpre + 128;
@@ -266,18 +268,66 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
   STAMP(5);
   // ---------------- depth-1 max_pool_x: scatter_reduce amax (ginet.py:103) --
   // NaN propagates; remember the tie count for the even-split backward.
-  for (int p = tid; p < K1 * 64; p += NT) {
-    const int m = p >> 6, o = p & 63;
-    const int mb = t.m1p[m], me = t.m1p[m + 1];
-    float mx = t.h2[t.m1i[mb] * 64 + o];
-    for (int q = mb + 1; q < me; ++q) {
-      const float v = t.h2[t.m1i[q] * 64 + o];
-      mx = (mx != mx || v != v) ? __int_as_float(0x7fc00000) : fmaxf(mx, v);
+  // Members are split into S slices per (cluster, channel): each slice's
+  // max (NaN-propagating) and its count of members equal to it, combined per
+  // pair (max is order-free here: H2 >= +0 or NaN).  Also record each
+  // depth-0 cluster's depth-1 cluster for the backward.
+  for (int q = tid; q < K0; q += NT) {
+    int m = 0;
+    while (q >= t.m1p[m + 1]) ++m;
+    t.cl1[t.m1i[q]] = m;
+  }
+  if (K0 < 16) {  // few members per pair: one pass
+    for (int p = tid; p < K1 * 64; p += NT) {
+      const int m = p >> 6, o = p & 63;
+      const int mb = t.m1p[m], me = t.m1p[m + 1];
+      float mx = t.h2[t.m1i[mb] * 64 + o];
+      for (int q = mb + 1; q < me; ++q) {
+        const float v = t.h2[t.m1i[q] * 64 + o];
+        mx = (mx != mx || v != v) ? __int_as_float(0x7fc00000) : fmaxf(mx, v);
+      }
+      float ties = 0.f;
+      for (int q = mb; q < me; ++q) ties += (t.h2[t.m1i[q] * 64 + o] == mx) ? 1.f : 0.f;
+      t.p2[p] = mx;
+      t.nt[p] = ties;
     }
-    float ties = 0.f;
-    for (int q = mb; q < me; ++q) ties += (t.h2[t.m1i[q] * 64 + o] == mx) ? 1.f : 0.f;
-    t.p2[p] = mx;
-    t.nt[p] = ties;
+  } else {
+    const int pairs = K1 * 64;
+    const int LS = pairs <= 32 ? 4 : pairs <= 64 ? 3 : pairs <= 128 ? 2 : pairs <= 256 ? 1 : 0;  // pairs*S <= 512
+    const int S = 1 << LS;
+    float* smx = t.dgp;            // [pairs*S] (dgp is free until the head)
+    float* scnt = t.dgp + 512;
+    const float NEG = -__builtin_inff();
+    for (int p = tid; p < pairs * S; p += NT) {
+      const int sl = p & (S - 1), pr = p >> LS, m = pr >> 6, o = pr & 63;
+      const int mb = t.m1p[m], cnt = t.m1p[m + 1] - mb;
+      const int qb = mb + ((cnt * sl) >> LS), qe = mb + ((cnt * (sl + 1)) >> LS);
+      float mx = NEG;
+      for (int q = qb; q < qe; ++q) {
+        const float v = t.h2[t.m1i[q] * 64 + o];
+        mx = (mx != mx || v != v) ? __int_as_float(0x7fc00000) : fmaxf(mx, v);
+      }
+      float ties = 0.f;
+      for (int q = qb; q < qe; ++q) ties += (t.h2[t.m1i[q] * 64 + o] == mx) ? 1.f : 0.f;
+      smx[p] = mx;
+      scnt[p] = ties;
+    }
+    __syncthreads();
+    for (int p = tid; p < pairs; p += NT) {
+      float mx = NEG;
+      bool nan = false;
+      for (int sl = 0; sl < S; ++sl) {
+        const float v = smx[(p << LS) + sl];
+        if (v != v) nan = true;
+        else mx = fmaxf(mx, v);
+      }
+      float ties = 0.f;
+      if (nan) mx = __int_as_float(0x7fc00000);
+      else
+        for (int sl = 0; sl < S; ++sl) ties += (smx[(p << LS) + sl] == mx) ? scnt[(p << LS) + sl] : 0.f;
+      t.p2[p] = mx;
+      t.nt[p] = ties;
+    }
   }
   __syncthreads();
 
@@ -309,15 +359,12 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
   // ---------------- depth-1 pooling + mean backward -------------------------
   // scatter_mean: grad/count; scatter_reduce amax: grad split evenly over the
   // members equal to the max ((src==max) * grad/ties, so NaN stays NaN).
-  for (int p = tid; p < K1 * 64; p += NT) {
-    const int m = p >> 6, o = p & 63;
-    const float gm = (t.dg[o] / (float)K1) / t.nt[p];
-    const float mx = t.p2[p];
-    for (int q = t.m1p[m]; q < t.m1p[m + 1]; ++q) {
-      const int k = t.m1i[q];
-      const float h = t.h2[k * 64 + o];
-      t.d2[k * 64 + o] = relu_bwd(h, (h == mx ? 1.f : 0.f) * gm);
-    }
+  for (int p = tid; p < K0 * 64; p += NT) {  // one (depth-0 cluster, channel) per thread
+    const int k = p >> 6, o = p & 63, mo = t.cl1[k] * 64 + o;
+    const float gm = (t.dg[o] / (float)K1) / t.nt[mo];
+    const float mx = t.p2[mo];
+    const float h = t.h2[p];
+    t.d2[p] = relu_bwd(h, (h == mx ? 1.f : 0.f) * gm);
   }
   __syncthreads();
   STAMP(11);
@@ -331,25 +378,63 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
   __syncthreads();
   STAMP(12);
   // conv2 weight-gradient partials, and the gradient reaching each depth-0
-  // arg member through relu (v = relu'(H1[arg]) * dP1)
-  {
-    const int SS = DR_SLAB_STRIDE(F);
-    float* slab = a.p.slab + (int64_t)b * SS + 32 * F;
+  // arg member through relu (v = relu'(H1[arg]) * dP1); with many clusters on MFMA:
+  // dW2 = dY2^T P1 per branch (4 tiles of 16 x 16, K = K0) and
+  // dP1 = dY2 W2 per branch (ceil(K0/16) row tiles, K = 32); one wave per tile
+  if (K0 < 12) {  // few clusters: direct loops
+    float* slab = a.p.slab + (int64_t)b * DR_SLAB_STRIDE(F) + 32 * F;
     for (int p = tid; p < 1024; p += NT) {
       const int br = p >> 9, o = ((p >> 4) & 31) + br * 32, j = p & 15;
       float acc = 0.f;
       for (int k = 0; k < K0; ++k) acc = fmaf(t.y2[k * 64 + o], t.p1[k * 32 + br * 16 + j], acc);
       slab[p] = acc;
     }
-  }
-  for (int p = tid; p < K0 * 32; p += NT) {
-    const int k = p >> 5, ch = p & 31, br = ch >> 4, j = ch & 15;
-    const float* wb = t.w2 + br * 512;
-    float acc = 0.f;
+    for (int p = tid; p < K0 * 32; p += NT) {
+      const int k = p >> 5, ch = p & 31, br = ch >> 4, j = ch & 15;
+      const float* wb = t.w2 + br * 512;
+      float acc = 0.f;
 #pragma unroll 8
-    for (int o = 0; o < 32; ++o) acc = fmaf(t.y2[k * 64 + br * 32 + o], wb[o * 16 + j], acc);
-    const int i = t.a1[p];
-    t.dp1[p] = (i < N) ? relu_bwd(t.p1[p], acc) : 0.f;  // P1 = H1[arg] exactly
+      for (int o = 0; o < 32; ++o) acc = fmaf(t.y2[k * 64 + br * 32 + o], wb[o * 16 + j], acc);
+      const int i = t.a1[p];
+      t.dp1[p] = (i < N) ? relu_bwd(t.p1[p], acc) : 0.f;  // P1 = H1[arg] exactly
+    }
+  } else
+  {
+    const int lane = tid & 63, wave = tid >> 6, li = lane & 15, kq = lane >> 4;
+    float* slab = a.p.slab + (int64_t)b * DR_SLAB_STRIDE(F) + 32 * F;
+    const int nrt = (K0 + 15) >> 4;
+    for (int job = wave; job < 4 + 2 * nrt; job += NW) {
+      if (job < 4) {
+        const int br = job >> 1, ot = job & 1;
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int k0 = 0; k0 < K0; k0 += 4) {
+          const int k = k0 + kq;
+          const float av = k < K0 ? t.y2[k * 64 + br * 32 + ot * 16 + li] : 0.f;
+          const float bv = k < K0 ? t.p1[k * 32 + br * 16 + li] : 0.f;
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) slab[br * 512 + (ot * 16 + kq * 4 + r) * 16 + li] = acc[r];
+      } else {
+        const int q = job - 4, br = q & 1, r0 = (q >> 1) * 16;
+        const int kr = min(r0 + li, K0 - 1);
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int o = 4 * u + kq;
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(t.y2[kr * 64 + br * 32 + o], t.w2[br * 512 + o * 16 + li], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int k = r0 + kq * 4 + r;
+          if (k < K0) {
+            const int p = k * 32 + br * 16 + li;
+            const int i = t.a1[p];
+            t.dp1[p] = (i < N) ? relu_bwd(t.p1[p], acc[r]) : 0.f;  // P1 = H1[arg] exactly
+          }
+        }
+      }
+    }
   }
   __syncthreads();
 
@@ -639,10 +724,11 @@ struct LargeArgs {
 };
 
 struct ConvCarve {
-  int KP, LDW, XS, w1, z, h, m0i, m0p, rng, total;
+  int KP, LDW, XS, w1, z, h, m0i, m0p, rng, xh, hid, lcol, trp, total;
 };
 
-__host__ __device__ inline ConvCarve conv_carve(int N, int F, int K0) {
+// HM / EM: halo rows and edges of the largest tile (0: no halo staging)
+__host__ __device__ inline ConvCarve conv_carve(int N, int F, int K0, int HM, int EM) {
   ConvCarve c;
   c.KP = r16(F);
   c.LDW = c.KP + 2;
@@ -652,14 +738,25 @@ __host__ __device__ inline ConvCarve conv_carve(int N, int F, int K0) {
   o += r4(32 * c.LDW);
   c.z = o;
   o += r4(TR * c.LDW);
+  // with halos (HM > 0): H lives in the halo-X region (dead after the
+  // gather) and the tile's own member lists replace the graph's
   c.h = o;
-  o += TR * 32;
+  o += HM ? 0 : TR * 32;
   c.m0i = o;
-  o += r4(N);
+  o += r4(HM ? TR : N);
   c.m0p = o;
   o += r4(K0 + 1);
   c.rng = o;
   o += r4(2 * K0);
+  c.xh = o;  // halo X rows (XS stride, 16-byte rows), then H
+  o += HM ? r4(drk::imax(HM * c.XS, TR * 32)) : 0;
+  if (HM) c.h = c.xh;
+  c.hid = o;
+  o += r4(HM);
+  c.trp = o;  // the tile's rowptr slice
+  o += HM ? r4(TR + 1) : 0;
+  c.lcol = o;  // the tile's edges as halo indices (uint16); last, so its size moves nothing
+  o += HM ? r4((EM + 8) / 2) : 0;
   c.total = o;
   return c;
 }
@@ -691,7 +788,7 @@ __global__ void __launch_bounds__(NTA) ginet_large_conv1_kernel(LargeArgs la) {
   const int N = d.n_nodes, K0 = d.n_k0, F = s.n_feat;
   const int TRr = pl.tile_rows;
   const int r0 = t * TRr, nrows = min(TRr, N - r0);
-  const ConvCarve c = conv_carve(N, F, K0);
+  const ConvCarve c = conv_carve(N, F, K0, pl.halo_max, 0);
   const int KP = c.KP, LDW = c.LDW, XS = c.XS;
   float* sW1 = lds + c.w1;
   float* sZ = lds + c.z;
@@ -700,8 +797,14 @@ __global__ void __launch_bounds__(NTA) ginet_large_conv1_kernel(LargeArgs la) {
   int* sm0p = reinterpret_cast<int*>(lds + c.m0p);
   int* srng = reinterpret_cast<int*>(lds + c.rng);
 
-  drk::dma_words<NTA>(sm0i, s.m0_idx + n0, N);
-  drk::dma_words<NTA>(sm0p, s.m0_ptr + k00 + g, K0 + 1);
+  const bool compact = pl.tile_members != nullptr;
+  if (compact) {  // this tile's members by cluster (host-built), runs from tile_mptr
+    drk::dma_words<NTA>(sm0i, pl.tile_members + (int64_t)tile * TRr, nrows);
+    drk::dma_words<NTA>(sm0p, pl.tile_mptr + (int64_t)tile * (pl.k0_max + 1), K0 + 1);
+  } else {
+    drk::dma_words<NTA>(sm0i, s.m0_idx + n0, N);
+    drk::dma_words<NTA>(sm0p, s.m0_ptr + k00 + g, K0 + 1);
+  }
   for (int p = tid; p < 32 * KP; p += NTA) {  // [W1; W1e] zero-padded to KP
     const int r = p / KP, k = p - r * KP;
     float v = 0.f;
@@ -712,6 +815,49 @@ __global__ void __launch_bounds__(NTA) ginet_large_conv1_kernel(LargeArgs la) {
     const int r = p / (KP - XS);
     sZ[r * LDW + XS + (p - r * (KP - XS))] = 0.f;
   }
+  if (pl.halo_ids) {
+    // Halo path: stage the tile's rowptr slice, its halo ids, then the halo X
+    // rows and the tile's edges (as halo indices) into LDS; gather from LDS.
+    int* strp = reinterpret_cast<int*>(lds + c.trp);
+    int* shid = reinterpret_cast<int*>(lds + c.hid);
+    uint16_t* slcol = reinterpret_cast<uint16_t*>(lds + c.lcol);
+    float* sXh = lds + c.xh;
+    const int h0 = pl.halo_off[tile], H = pl.halo_off[tile + 1] - h0;
+    const int l0 = pl.lcol_off[tile];
+    drk::dma_words<NTA>(strp, s.rowptr + n0 + g + r0, nrows + 1);
+    drk::dma_words<NTA>(shid, pl.halo_ids + h0, H);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int ebase = strp[0];
+    drk::dma_x4<NTA>(slcol, pl.lcol + l0, (strp[nrows] - ebase + 7) / 8);
+    {
+      const float* X = s.x + n0 * (int64_t)XS;
+      const int nch = XS >> 2, tot = H * nch;
+      const int wv = __builtin_amdgcn_readfirstlane(wave);
+      for (int base = wv * 64; base < tot; base += NTA)
+        if (base + lane < tot) {
+          const int hr = (base + lane) / nch, ch = base + lane - hr * nch;
+          __builtin_amdgcn_global_load_lds(DRK_AS1(X + (int64_t)shid[hr] * XS + ch * 4), DRK_AS3(sXh + base * 4), 16, 0, 0);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    float* zg = pl.z + (int64_t)pl.z_row0[b] * XS;
+    const int nch = XS >> 2, sub = tid & 7;
+    for (int r = tid >> 3; r < nrows; r += NTA / 8) {
+      const int eb = strp[r] - ebase, ee = strp[r + 1] - ebase;
+      for (int ch = sub; ch < nch; ch += 8) {
+        const int c4 = ch * 4;
+        const float4 acc = drk::gather_row_chunk(slcol, eb, ee, sXh, XS, c4);
+        float* zr = sZ + r * LDW + c4;
+        zr[0] = acc.x;
+        zr[1] = acc.y;
+        zr[2] = acc.z;
+        zr[3] = acc.w;
+        *reinterpret_cast<float4*>(zg + (int64_t)(r0 + r) * XS + c4) = acc;
+      }
+    }
+  } else {
   // Z = A X for the tile's rows: 8 lanes per row, 16-byte chunks of X rows.
   {
     const int* rp = s.rowptr + n0 + g;
@@ -743,6 +889,7 @@ __global__ void __launch_bounds__(NTA) ginet_large_conv1_kernel(LargeArgs la) {
         *reinterpret_cast<float4*>(zg + (int64_t)i * XS + c4) = acc;
       }
     }
+  }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -781,8 +928,8 @@ __global__ void __launch_bounds__(NTA) ginet_large_conv1_kernel(LargeArgs la) {
   // each cluster's members inside this tile: a sub-run of its ascending list
   for (int k = tid; k < K0; k += NTA) {
     const int mb = sm0p[k], me = sm0p[k + 1];
-    srng[2 * k] = lower_bound_lds(sm0i, mb, me, r0);
-    srng[2 * k + 1] = lower_bound_lds(sm0i, mb, me, r0 + nrows);
+    srng[2 * k] = compact ? mb : lower_bound_lds(sm0i, mb, me, r0);
+    srng[2 * k + 1] = compact ? me : lower_bound_lds(sm0i, mb, me, r0 + nrows);
   }
   __syncthreads();
   // partial scatter_max (strict '>', first max wins, NaN never enters)
@@ -805,7 +952,7 @@ __global__ void __launch_bounds__(NTA) ginet_large_conv1_kernel(LargeArgs la) {
 }
 
 struct TailCarve {
-  int w2, fc2, p1, a1, dp1, y2, h2, d2, p1rp, p1c, p1trp, p1tc, m1p, m1i, p2, nt, head, dgp, total;
+  int w2, fc2, p1, a1, dp1, y2, h2, d2, p1rp, p1c, p1trp, p1tc, m1p, m1i, p2, nt, cl1, head, dgp, total;
 };
 
 __host__ __device__ inline TailCarve tail_carve(int K0, int P1, int K1, int alias, int OUT) {
@@ -835,6 +982,7 @@ __host__ __device__ inline TailCarve tail_carve(int K0, int P1, int K1, int alia
   TAKE(m1i, K0)
   TAKE(p2, K1 * 64)
   TAKE(nt, K1 * 64)
+  TAKE(cl1, K0)  // depth-1 cluster of each depth-0 cluster
   TAKE(head, HEADW)
   TAKE(dgp, NW * 64)
 #undef TAKE
@@ -857,6 +1005,7 @@ __global__ void __launch_bounds__(NT) ginet_large_tail_kernel(LargeArgs la) {
   const int F = s.n_feat, alias = s.transpose_aliased, OUT = a.p.out_dim;
   const TailCarve c = tail_carve(K0, P1, K1, alias, OUT);
   const TailLds t = tail_lds(c, lds);
+  STAMP(0);
 
   float fc1_row[8], fc1_col[8], fc1_bias;
   {
@@ -880,6 +1029,7 @@ __global__ void __launch_bounds__(NT) ginet_large_tail_kernel(LargeArgs la) {
   drk::dma_words<NT>(t.m1i, s.m1_idx + k00, K0);
   t.w2[tid] = (tid < 512) ? a.w.w2[tid] : a.w.w2e[tid - 512];
   for (int p = tid; p < OUT * 129; p += NT) t.fc2[p] = (p < OUT * 128) ? a.w.fc2w[p] : a.w.fc2b[p - OUT * 128];
+  STAMP(1);
   // tiles in node order, strict '>': the first maximum over the whole graph
   const int tb = pl.tile_first[b], te = pl.tile_first[b + 1];
   for (int p = tid; p < K0 * 32; p += NT) {
@@ -919,6 +1069,8 @@ __global__ void __launch_bounds__(NT) ginet_large_tail_kernel(LargeArgs la) {
   // counter load sits between the descriptor and the graph DMA
   if (a.p.step_counter && b == 0 && tid == 0) a.p.step_counter[1] = (int64_t)drop_offset;
   __syncthreads();
+  STAMP(2);
+  STAMP(3);
   const float* z = pl.z + (int64_t)pl.z_row0[b] * r4(F);
   const int XS = r4(F);
   ginet_tail(a, t, fc1_row, fc1_col, fc1_bias, b, N, K0, K1, F, OUT, y_g, drop_offset,
@@ -956,8 +1108,9 @@ extern "C" int dr_ginet_graph_pass(const dr_graph_store* store, const dr_graph_d
   return (int)hipGetLastError();
 }
 
-extern "C" int64_t dr_ginet_large_conv_lds_bytes(int32_t n_nodes, int32_t n_feat, int32_t k0) {
-  return 4LL * conv_carve(n_nodes, n_feat, k0).total;
+extern "C" int64_t dr_ginet_large_conv_lds_bytes(int32_t n_nodes, int32_t n_feat, int32_t k0, int32_t halo_max,
+                                                 int32_t tile_edges_max) {
+  return 4LL * conv_carve(n_nodes, n_feat, k0, halo_max, tile_edges_max).total;
 }
 
 extern "C" int64_t dr_ginet_tail_lds_bytes(int32_t k0, int32_t p1_edges, int32_t k1, int32_t transpose_aliased,
@@ -976,6 +1129,10 @@ extern "C" int dr_ginet_large_pass(const dr_graph_store* store, const dr_graph_d
     return DR_E_ARG;
   if (plan->n_tiles < n_batch || plan->k0_max < 1 || plan->k0_max > 64) return DR_E_ARG;
   if (plan->tile_rows < 16 || plan->tile_rows > TR || plan->tile_rows % 16) return DR_E_ARG;
+  if (plan->halo_ids && (plan->halo_max < 1 || plan->halo_max > 65535 || !plan->halo_off || !plan->lcol_off ||
+                         !plan->lcol || !plan->tile_members || !plan->tile_mptr))
+    return DR_E_ARG;
+  if (!plan->halo_ids && plan->halo_max) return DR_E_ARG;
   if ((pass->flags & DR_PASS_BACKWARD) && (!pass->slab || !pass->head)) return DR_E_ARG;
   if ((pass->flags & DR_PASS_BACKWARD) && pass->loss_kind == DR_LOSS_NONE && !pass->dout) return DR_E_ARG;
   if ((pass->flags & DR_PASS_FORWARD) && !pass->out) return DR_E_ARG;

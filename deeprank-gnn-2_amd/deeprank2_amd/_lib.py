@@ -87,10 +87,16 @@ class LargePlanC(ctypes.Structure):
         ("n_tiles", ctypes.c_int32),
         ("k0_max", ctypes.c_int32),
         ("tile_rows", ctypes.c_int32),
-        ("pad0", ctypes.c_int32),
+        ("halo_max", ctypes.c_int32),
         ("z", VP),
         ("part_val", VP),
         ("part_arg", VP),
+        ("halo_off", VP),
+        ("halo_ids", VP),
+        ("lcol_off", VP),
+        ("lcol", VP),
+        ("tile_members", VP),
+        ("tile_mptr", VP),
     ]
 
 
@@ -186,7 +192,7 @@ SIGNATURES = [
     ("dr_ginet_graph_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, VP]),
     ("dr_ginet_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 8),
     ("dr_ginet_large_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(LargePlanC), ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, ctypes.c_int32, VP]),
-    ("dr_ginet_large_conv_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 3),
+    ("dr_ginet_large_conv_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 5),
     ("dr_ginet_tail_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 5),
     ("dr_vanilla_graph_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(VanillaWeightsC), ctypes.POINTER(PassC), ctypes.POINTER(VanillaScratchC), ctypes.c_int32, VP]),
     ("dr_vanilla_scratch_floats", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),

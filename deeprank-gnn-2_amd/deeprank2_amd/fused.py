@@ -35,6 +35,7 @@ class BatchHandle:
         self._lds = {}
         self.force_large = False  # run the split (tile + tail) path on small graphs too
         self.large_tile = None  # nodes per tile of the split path (default 128)
+        self.large_halos = True  # stage each tile's neighbour rows in LDS (False: per-edge HBM gather)
 
     def lds(self, key, fn):
         """Dynamic LDS bytes for the largest graph of the batch (cached per model kind)."""
@@ -78,7 +79,7 @@ class BatchHandle:
         """Tiling + workspaces of the large-graph path (dr_large_plan), built once per batch."""
         plan = self._lds.get(("large", out_dim))
         if plan is None:
-            plan = LargePlan(self, out_dim)
+            plan = LargePlan(self, out_dim, use_halos=self.large_halos)
             self._lds[("large", out_dim)] = plan
         return plan
 
@@ -92,7 +93,7 @@ class LargePlan:
 
     TILE = 128
 
-    def __init__(self, h: BatchHandle, out_dim, tile_rows=None):
+    def __init__(self, h: BatchHandle, out_dim, tile_rows=None, use_halos=True):
         st = h.store
         self.TILE = int(tile_rows or h.large_tile or self.TILE)
         n, _e, k0, p1, k1 = (a[h.gids_host.astype(np.int64)] for a in st._sizes)  # noqa: SLF001
@@ -111,7 +112,12 @@ class LargePlan:
         self.part_val = torch.empty(self.n_tiles * self.k0_max * 32, dtype=torch.float32, device=dev)
         self.part_arg = torch.empty(self.n_tiles * self.k0_max * 32, dtype=torch.int32, device=dev)
         lib = _lib.load()
-        self.conv_lds = int(lib.dr_ginet_large_conv_lds_bytes(int(n.max()), st.n_feat, self.k0_max))
+        halo = self._halos(h, n) if use_halos else None
+        hmax, emax = (halo[0], halo[1]) if halo is not None else (0, 0)
+        self.conv_lds = int(lib.dr_ginet_large_conv_lds_bytes(int(n.max()), st.n_feat, self.k0_max, hmax, emax))
+        if halo is not None and self.conv_lds > LDS_MAX:  # halos too wide for LDS: per-edge HBM gather
+            halo, hmax = None, 0
+            self.conv_lds = int(lib.dr_ginet_large_conv_lds_bytes(int(n.max()), st.n_feat, self.k0_max, 0, 0))
         self.tail_lds = int(lib.dr_ginet_tail_lds_bytes(self.k0_max, int(p1.max()), int(k1.max()), int(st.packed.transpose_aliased), out_dim))
         if max(self.conv_lds, self.tail_lds) > LDS_MAX:
             msg = f"large-graph path needs {max(self.conv_lds, self.tail_lds)} B of LDS (> 160 KiB)"
@@ -127,7 +133,47 @@ class LargePlan:
         c.z = self.z.data_ptr()
         c.part_val = self.part_val.data_ptr()
         c.part_arg = self.part_arg.data_ptr()
+        c.halo_max = hmax
+        self.halo_tensors = None
+        if halo is not None:
+            _, _, hoff, hids, loff, lcol, tmem, tmptr = halo
+            self.halo_tensors = [torch.from_numpy(a).to(dev) for a in (hoff, hids, loff, lcol.view(np.int16), tmem, tmptr)]
+            c.halo_off, c.halo_ids, c.lcol_off, c.lcol, c.tile_members, c.tile_mptr = (t.data_ptr() for t in self.halo_tensors)
         self.c = c
+
+    def _halos(self, h, n):
+        """Per tile: its neighbours (distinct local node ids, ascending) and its
+        edges re-indexed into that list (uint16), 8-aligned per tile."""
+        p = h.store.packed
+        hoff, hids, loff, lcols = [0], [], [0], []
+        tmem = np.zeros((self.n_tiles, self.TILE), np.int32)
+        tmptr = np.zeros((self.n_tiles, self.k0_max + 1), np.int32)
+        tile = 0
+        hmax = emax = 0
+        for slot, gid in enumerate(h.gids_host.astype(np.int64)):
+            n0, e0 = int(p.node_off[gid]), int(p.edge_off[gid])
+            rp = p.rowptr[n0 + gid : n0 + gid + int(n[slot]) + 1].astype(np.int64)
+            col = p.col[e0 : int(p.edge_off[gid + 1])]
+            cl0 = p.cl0[n0 : n0 + int(n[slot])]
+            k0 = int(p.k0_off[gid + 1] - p.k0_off[gid])
+            for r0 in range(0, int(n[slot]), self.TILE):
+                r1 = min(int(n[slot]), r0 + self.TILE)
+                order = np.argsort(cl0[r0:r1], kind="stable")  # by cluster, nodes ascending
+                tmem[tile, : r1 - r0] = r0 + order
+                np.cumsum(np.bincount(cl0[r0:r1], minlength=k0), out=tmptr[tile, 1 : k0 + 1])
+                tile += 1
+                cs = col[rp[r0] : rp[r1]]
+                uniq, inv = np.unique(cs, return_inverse=True)
+                hids.append(uniq.astype(np.int32))
+                hoff.append(hoff[-1] + uniq.size)
+                pad = (-cs.size) % 8
+                lcols.append(np.concatenate([inv.astype(np.uint16), np.zeros(pad, np.uint16)]))
+                loff.append(loff[-1] + cs.size + pad)
+                hmax, emax = max(hmax, uniq.size), max(emax, cs.size)
+        if hmax == 0 or hmax > 65535:
+            return None
+        lcol = np.concatenate([*lcols, np.zeros(8, np.uint16)])
+        return hmax, emax, np.asarray(hoff, np.int32), np.concatenate(hids), np.asarray(loff, np.int32), lcol, tmem.reshape(-1), tmptr.reshape(-1)
 
 
 def resolve_batch(data, device, require_clusters=True) -> BatchHandle:

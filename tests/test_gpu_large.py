@@ -53,9 +53,10 @@ def test_large_path_bit_identical_to_single_workgroup_kernel():
     model = amd.GINet(30, 2, 3).to(DEV)
     params = model.ordered_params()
     res = []
-    for force in (False, True):
+    for force, halos in ((False, True), (True, True), (True, False)):
         h = BatchHandle(store, np.arange(16))
         h.force_large = force
+        h.large_halos = halos
         out = torch.empty(16, 2, device=DEV)
         slab = torch.empty(16 * amd.slab_stride(30), device=DEV)
         head = torch.zeros(16 * amd.head_stride(2), device=DEV)
@@ -64,6 +65,27 @@ def test_large_path_bit_identical_to_single_workgroup_kernel():
         amd.graph_pass(h, params, 2, 3, loss_kind=_lib.DR_LOSS_CE, loss_scale=1 / 16, dropout=Dropout(0.4, seed=7, offset=3), out=out, loss_per_graph=lpg, slab=slab, head=head)
         torch.cuda.synchronize()
         res.append((out.cpu(), slab.cpu(), head.cpu(), lpg.cpu()))
+    for other in res[1:]:  # split path with tile halos in LDS, and with the per-edge HBM gather
+        for x, y in zip(res[0], other):
+            assert torch.equal(x, y)
+
+
+def test_atom_graphs_halo_and_hbm_gather_bit_identical():
+    store = _store(_atoms(3, seed=5))
+    torch.manual_seed(4)
+    model = amd.GINet(30, 1, 3).to(DEV)
+    params = model.ordered_params()
+    res = []
+    for halos in (True, False):
+        h = BatchHandle(store, np.arange(3))
+        h.large_halos = halos
+        assert (h.large_plan(1).halo_tensors is not None) == halos
+        out = torch.empty(3, 1, device=DEV)
+        slab = torch.empty(3 * amd.slab_stride(30), device=DEV)
+        head = torch.zeros(3 * amd.head_stride(1), device=DEV)
+        amd.graph_pass(h, params, 1, 3, loss_kind=_lib.DR_LOSS_MSE, loss_scale=1 / 3, out=out, slab=slab, head=head)
+        torch.cuda.synchronize()
+        res.append((out.cpu(), slab.cpu(), head.cpu()))
     for x, y in zip(*res):
         assert torch.equal(x, y)
 

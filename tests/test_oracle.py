@@ -9,7 +9,7 @@ from __future__ import annotations
 import numpy as np
 import pytest
 import torch
-from _util import fixed_dropout, golden_batch, golden_grads, golden_state_dict
+from _util import assert_grad_close, fixed_dropout, golden_batch, golden_grads, golden_state_dict
 
 from oracle import gnn_ref
 from oracle import pyg_ops as P
@@ -56,8 +56,8 @@ def test_model_matches_reference(golden, name, cls, args):
     assert loss == pytest.approx(float(z["loss"]), rel=1e-5, abs=1e-6)
     ref = golden_grads(z)
     assert set(ref) == set(grads)
-    for k in ref:
-        np.testing.assert_allclose(grads[k], ref[k], rtol=1e-4, atol=1e-5, err_msg=k)
+    for k in ref:  # rtol 1e-4 plus a normwise floor: CPU thread counts change summation order
+        assert_grad_close(grads[k], ref[k], err_msg=k)
 
 
 def test_ginet_dead_attention_grads_are_exactly_zero(golden):

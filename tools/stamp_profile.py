@@ -35,8 +35,14 @@ def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
     which = sys.argv[2] if len(sys.argv) > 2 else "ginet"
     mod, phases = (amd_nc, PHASES_NC) if which == "ginet_nocluster" else (amd, PHASES)
-    store = GraphStore(pack_graphs(records(make_dataset(B, seed=1000))), dev)
+    large = which == "ginet_large"
+    if large:  # tail kernel of the split path on atom-level graphs (stamps 0-3: staging, tile combine)
+        phases = ["stage", "tile combine", "-", *PHASES[4:]]
+    fam = {"n_lo": 2700, "n_hi": 3300, "mean_degree": 16.7, "k_lo": 8, "k_hi": 32} if large else {}
+    store = GraphStore(pack_graphs(records(make_dataset(B, seed=1000, **fam))), dev)
     h = amd.BatchHandle(store, np.arange(B))
+    if large:
+        h.large_tile = 64
     torch.manual_seed(0)
     model = mod.GINet(30, 1, 3).to(dev)
     params = model.ordered_params()
