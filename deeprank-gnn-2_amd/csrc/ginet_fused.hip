@@ -945,9 +945,15 @@ __global__ void __launch_bounds__(NTA) ginet_large_conv1_kernel(LargeArgs la) {
         arg = i;
       }
     }
-    const int64_t o = ((int64_t)tile * pl.k0_max + k) * 32 + ch;
-    pl.part_val[o] = best;
-    pl.part_arg[o] = arg;
+    if (pl.part_key) {  // order-free combine over the graph's tiles (see dr_large_plan.part_key)
+      if (best > LOWEST)
+        atomicMax(reinterpret_cast<unsigned long long*>(pl.part_key) + ((int64_t)b * pl.k0_max + k) * 32 + ch,
+                  ((unsigned long long)__float_as_uint(best) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)arg));
+    } else {
+      const int64_t o = ((int64_t)tile * pl.k0_max + k) * 32 + ch;
+      pl.part_val[o] = best;
+      pl.part_arg[o] = arg;
+    }
   }
 }
 
@@ -1032,6 +1038,15 @@ __global__ void __launch_bounds__(NT) ginet_large_tail_kernel(LargeArgs la) {
   STAMP(1);
   // tiles in node order, strict '>': the first maximum over the whole graph
   const int tb = pl.tile_first[b], te = pl.tile_first[b + 1];
+  if (pl.part_key) {
+    for (int p = tid; p < K0 * 32; p += NT) {
+      unsigned long long* kp = reinterpret_cast<unsigned long long*>(pl.part_key) + (int64_t)b * pl.k0_max * 32 + p;
+      const unsigned long long key = *kp;
+      *kp = 0ull;  // ready for the next pass
+      t.p1[p] = key ? __uint_as_float((uint32_t)(key >> 32)) : 0.f;
+      t.a1[p] = key ? (int)(0xffffffffu - (uint32_t)key) : N;
+    }
+  } else
   for (int p = tid; p < K0 * 32; p += NT) {
     float best = LOWEST;
     int arg = N;

@@ -97,6 +97,7 @@ class LargePlanC(ctypes.Structure):
         ("lcol", VP),
         ("tile_members", VP),
         ("tile_mptr", VP),
+        ("part_key", VP),
     ]
 
 

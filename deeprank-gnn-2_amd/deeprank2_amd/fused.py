@@ -36,6 +36,7 @@ class BatchHandle:
         self.force_large = False  # run the split (tile + tail) path on small graphs too
         self.large_tile = None  # nodes per tile of the split path (default 128)
         self.large_halos = True  # stage each tile's neighbour rows in LDS (False: per-edge HBM gather)
+        self.large_atomic_max = True  # depth-0 max over tiles by 64-bit atomic max (False: per-tile partials)
 
     def lds(self, key, fn):
         """Dynamic LDS bytes for the largest graph of the batch (cached per model kind)."""
@@ -79,7 +80,7 @@ class BatchHandle:
         """Tiling + workspaces of the large-graph path (dr_large_plan), built once per batch."""
         plan = self._lds.get(("large", out_dim))
         if plan is None:
-            plan = LargePlan(self, out_dim, use_halos=self.large_halos)
+            plan = LargePlan(self, out_dim, use_halos=self.large_halos, use_atomic_max=self.large_atomic_max)
             self._lds[("large", out_dim)] = plan
         return plan
 
@@ -91,9 +92,9 @@ class LargePlan:
     """Host side of ``dr_large_plan``: tiles of DR_LARGE_TILE nodes per graph,
     the Z workspace and the per-tile partial pooling buffers."""
 
-    TILE = 128
+    TILE = 64  # measured best for atom-level graphs with tile halos (tools/large_tiles.py)
 
-    def __init__(self, h: BatchHandle, out_dim, tile_rows=None, use_halos=True):
+    def __init__(self, h: BatchHandle, out_dim, tile_rows=None, use_halos=True, use_atomic_max=True):
         st = h.store
         self.TILE = int(tile_rows or h.large_tile or self.TILE)
         n, _e, k0, p1, k1 = (a[h.gids_host.astype(np.int64)] for a in st._sizes)  # noqa: SLF001
@@ -111,6 +112,7 @@ class LargePlan:
         self.z = torch.empty(max(1, int(z_row0[-1])) * st.x_stride, dtype=torch.float32, device=dev)
         self.part_val = torch.empty(self.n_tiles * self.k0_max * 32, dtype=torch.float32, device=dev)
         self.part_arg = torch.empty(self.n_tiles * self.k0_max * 32, dtype=torch.int32, device=dev)
+        self.part_key = torch.zeros(h.B * self.k0_max * 32, dtype=torch.int64, device=dev)  # kept zero between passes
         lib = _lib.load()
         halo = self._halos(h, n) if use_halos else None
         hmax, emax = (halo[0], halo[1]) if halo is not None else (0, 0)
@@ -134,6 +136,7 @@ class LargePlan:
         c.part_val = self.part_val.data_ptr()
         c.part_arg = self.part_arg.data_ptr()
         c.halo_max = hmax
+        c.part_key = self.part_key.data_ptr() if use_atomic_max else None
         self.halo_tensors = None
         if halo is not None:
             _, _, hoff, hids, loff, lcol, tmem, tmptr = halo

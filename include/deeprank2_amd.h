@@ -202,10 +202,25 @@ typedef struct dr_large_plan {
   int32_t n_tiles;
   int32_t k0_max;            /* >= every n_k0 of the batch                      */
   int32_t tile_rows;         /* nodes per tile: multiple of 16, <= DR_LARGE_TILE */
-  int32_t pad0;
+  int32_t halo_max;          /* >= every tile's halo size; 0 = no halos (gather X from HBM per edge) */
   float* z;                  /* [z_row0[B], x_stride] workspace                 */
   float* part_val;           /* [n_tiles, k0_max, 32] workspace                 */
   int32_t* part_arg;         /* [n_tiles, k0_max, 32] workspace                 */
+  /* Tile halos (optional): the distinct neighbours of a tile's rows are staged
+   * into LDS once, so the edge gather reads X from LDS instead of re-reading
+   * each neighbour row from L2/HBM once per edge.                             */
+  const int32_t* halo_off;   /* [n_tiles+1] offsets into halo_ids               */
+  const int32_t* halo_ids;   /* per tile: its neighbours' local node ids, ascending */
+  const int32_t* lcol_off;   /* [n_tiles+1] offsets into lcol, multiples of 8   */
+  const uint16_t* lcol;      /* per tile, per CSR edge of its rows: index into the tile's halo
+                                (array padded by 8 entries past the last tile)    */
+  const int32_t* tile_members; /* [n_tiles, tile_rows] with halos: the tile's nodes grouped by
+                                  depth-0 cluster, ascending within a cluster       */
+  const int32_t* tile_mptr;    /* [n_tiles, k0_max+1] with halos: cluster k's run in tile_members */
+  uint64_t* part_key;          /* optional [B, k0_max, 32], zero on entry and left zero: the depth-0
+                                  max over tiles by 64-bit atomic max of (H bits << 32 | ~node), i.e.
+                                  the largest value and, among equal values, the first node (H >= +0
+                                  after relu, NaN never enters); replaces part_val/part_arg */
 } dr_large_plan;
 
 int dr_ginet_large_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
@@ -213,7 +228,8 @@ int dr_ginet_large_pass(const dr_graph_store* store, const dr_graph_desc* descs,
                         int32_t conv_lds_bytes, int32_t tail_lds_bytes, void* stream);
 
 /* Dynamic LDS of the two launches of dr_ginet_large_pass (largest graph).  */
-int64_t dr_ginet_large_conv_lds_bytes(int32_t n_nodes, int32_t n_feat, int32_t k0);
+int64_t dr_ginet_large_conv_lds_bytes(int32_t n_nodes, int32_t n_feat, int32_t k0, int32_t halo_max,
+                                      int32_t tile_edges_max);
 int64_t dr_ginet_tail_lds_bytes(int32_t k0, int32_t p1_edges, int32_t k1, int32_t transpose_aliased,
                                 int32_t out_dim);
 

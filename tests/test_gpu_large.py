@@ -53,10 +53,11 @@ def test_large_path_bit_identical_to_single_workgroup_kernel():
     model = amd.GINet(30, 2, 3).to(DEV)
     params = model.ordered_params()
     res = []
-    for force, halos in ((False, True), (True, True), (True, False)):
+    for force, halos, amax in ((False, True, True), (True, True, True), (True, False, True), (True, True, False), (True, False, False)):
         h = BatchHandle(store, np.arange(16))
         h.force_large = force
         h.large_halos = halos
+        h.large_atomic_max = amax
         out = torch.empty(16, 2, device=DEV)
         slab = torch.empty(16 * amd.slab_stride(30), device=DEV)
         head = torch.zeros(16 * amd.head_stride(2), device=DEV)
@@ -76,9 +77,10 @@ def test_atom_graphs_halo_and_hbm_gather_bit_identical():
     model = amd.GINet(30, 1, 3).to(DEV)
     params = model.ordered_params()
     res = []
-    for halos in (True, False):
+    for halos, amax in ((True, True), (False, False), (True, False)):
         h = BatchHandle(store, np.arange(3))
         h.large_halos = halos
+        h.large_atomic_max = amax
         assert (h.large_plan(1).halo_tensors is not None) == halos
         out = torch.empty(3, 1, device=DEV)
         slab = torch.empty(3 * amd.slab_stride(30), device=DEV)
@@ -86,8 +88,9 @@ def test_atom_graphs_halo_and_hbm_gather_bit_identical():
         amd.graph_pass(h, params, 1, 3, loss_kind=_lib.DR_LOSS_MSE, loss_scale=1 / 3, out=out, slab=slab, head=head)
         torch.cuda.synchronize()
         res.append((out.cpu(), slab.cpu(), head.cpu()))
-    for x, y in zip(*res):
-        assert torch.equal(x, y)
+    for other in res[1:]:
+        for x, y in zip(res[0], other):
+            assert torch.equal(x, y)
 
 
 def test_atom_graphs_module_vs_oracle():
