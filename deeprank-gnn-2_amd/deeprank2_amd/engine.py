@@ -221,6 +221,42 @@ class FusedTrainStep:
         self.step_count = n
         return g
 
+    def time_graph_pass(self, handles, n_launches, global_batch=None):
+        """Mean duration (ms) of the model's graph pass alone: ``n_launches``
+        passes over ``handles`` (cycled) captured back to back into one HIP
+        graph, replayed between two HIP events on the launch stream.  Used for
+        ``roofline.achieved``; no host launch overhead enters the number (the
+        rocprofv3 kernel average is the cross-check).  State is restored."""
+        for h in handles:
+            self._ensure(h.B)
+        snap = [t.detach().clone() for t in self._state_tensors()]
+        n = self.step_count
+        p = self._pass if (self.spec.dropout > 0 and self.model.dropout > 0) else self._pass_nodrop
+
+        def passes(k):
+            for i in range(k):
+                h = handles[i % len(handles)]
+                p.loss_scale = self.loss_scale(h, global_batch or h.B * self.world)
+                launch(self.spec, h, self._w, p)
+
+        passes(len(handles))  # warm-up: LDS attributes, plans
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            passes(n_launches)
+        g.replay()  # untimed replay (first replay uploads the graph)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize(self.device)
+        ms = e0.elapsed_time(e1) / n_launches
+        del g
+        for t, s in zip(self._state_tensors(), snap):
+            t.data.copy_(s)
+        self.step_count = n
+        return ms
+
     def capture(self, h: BatchHandle, global_batch=None):
         """Capture one training step on ``h`` into a HIP graph (``torch.cuda.CUDAGraph``).
 
