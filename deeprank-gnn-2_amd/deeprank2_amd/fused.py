@@ -76,6 +76,23 @@ class BatchHandle:
             self._lds[key] = sc
         return sc
 
+    def vanilla_fused_scratch(self):
+        """Per-graph global scratch of dr_vanilla_fused_pass (S1, edge ReLU bit
+        words, transposed slot map) and each slot's float offset into it."""
+        sc = self._lds.get("vanilla_fused_scratch")
+        if sc is None:
+            idx = self.gids_host.astype(np.int64)
+            n, e = self.store._sizes[0][idx], self.store._sizes[1][idx]  # noqa: SLF001
+            r4 = lambda v: (v + 3) & ~3  # noqa: E731
+            per = r4(n * 32) + 5 * r4(e)  # dr_vanilla_fused_scratch_floats
+            off = np.concatenate([[0], np.cumsum(per)]).astype(np.int64)
+            dev = self.store.device
+            buf = torch.empty(max(1, int(off[-1])), dtype=torch.float32, device=dev)
+            offs = torch.from_numpy(off[:-1].copy()).to(dev)
+            sc = (buf, offs)
+            self._lds["vanilla_fused_scratch"] = sc
+        return sc
+
     def large_plan(self, out_dim):
         """Tiling + workspaces of the large-graph path (dr_large_plan), built once per batch."""
         plan = self._lds.get(("large", out_dim))

@@ -19,7 +19,7 @@ import torch
 from torch import nn
 
 from deeprank2_amd import _lib, ops
-from deeprank2_amd.fused import BatchHandle, FusedFn, FusedSpec, make_pass, resolve_batch, run_pass
+from deeprank2_amd.fused import LDS_MAX, BatchHandle, FusedFn, FusedSpec, make_pass, resolve_batch, run_pass
 
 MESSAGE = 32
 
@@ -122,12 +122,31 @@ def make_spec(f, fe):
         if st.n_edge_feat != fe or st.n_feat != f:
             msg = f"batch has F={st.n_feat}, Fe={st.n_edge_feat}; the model expects F={f}, Fe={fe}"
             raise ValueError(msg)
-        sc, _keep = h.vanilla_scratch(f, fe)
         lib = _lib.load()
+        if fused_fits(h, f, fe):  # one workgroup per graph, graph in LDS
+            buf, offs = h.vanilla_fused_scratch()
+            lds = h.lds("vanilla_fused", lambda n, e, *_: lib.dr_vanilla_fused_lds_bytes(n, e))
+            _lib.check(lib.dr_vanilla_fused_pass(st.cstruct(), h.descs.data_ptr(), h.B, w, p, buf.data_ptr(), offs.data_ptr(), lds, _lib.stream_ptr(st.device)), "dr_vanilla_fused_pass")
+            return
+        sc, _keep = h.vanilla_scratch(f, fe)
         lds = int(lib.dr_vanilla_lds_bytes(f, fe, p.out_dim))
         _lib.check(lib.dr_vanilla_graph_pass(st.cstruct(), h.descs.data_ptr(), h.B, w, p, sc, lds, _lib.stream_ptr(st.device)), "dr_vanilla_graph_pass")
 
     return FusedSpec(PARAM_NAMES, recipe, slab_stride, head_stride, "dr_vanilla_graph_pass", weights, lambda *_: 0, dropout=0.0, run=run)
+
+
+FUSED_MAX_FE = 4  # vanilla_graph.hip MAXFE
+
+
+def fused_fits(h: BatchHandle, f, fe):
+    """True when the batch runs on the per-graph fused kernel (dr_vanilla_fused_pass):
+    F <= 32, Fe <= 4 and the largest graph's CSR, transpose and node arrays fit
+    160 KiB of LDS; otherwise the batch-wide pipeline (dr_vanilla_graph_pass).
+    ``h.vanilla_pipeline = True`` forces the pipeline."""
+    if getattr(h, "vanilla_pipeline", False) or f > 32 or fe > FUSED_MAX_FE:  # noqa: PLR2004
+        return False
+    lib = _lib.load()
+    return h.lds("vanilla_fused", lambda n, e, *_: lib.dr_vanilla_fused_lds_bytes(n, e)) <= LDS_MAX
 
 
 def graph_pass(model, h: BatchHandle, params, out_dim, flags, **kw):

@@ -339,6 +339,19 @@ int64_t dr_vanilla_scratch_floats(int64_t n_rows, int32_t n_feat, int32_t n_edge
 int64_t dr_vanilla_part_floats(int32_t n_feat, int32_t n_edge_feat); /* one layer's gradient entries */
 int64_t dr_vanilla_lds_bytes(int32_t n_feat, int32_t n_edge_feat, int32_t out_dim);
 
+/* The same VanillaNetwork training pass (vanilla_gnn.py:26-65 + trainer.py:686-689)
+ * with ONE workgroup per graph and the graph in LDS (vanilla_graph.hip): for
+ * batches whose largest graph fits (dr_vanilla_fused_lds_bytes(max N, max E)
+ * <= 160 KiB), F <= 32, Fe <= 4.  Same slab/head partials as
+ * dr_vanilla_graph_pass, so dr_reduce_update is shared.  scratch: device
+ * floats, slot b owns dr_vanilla_fused_scratch_floats(N_b, E_b) of them from
+ * scratch_off[b] (device int64 [B]).  Needs the store's transpose + t_eid.  */
+int dr_vanilla_fused_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                          const dr_vanilla_weights* w, const dr_pass* pass, float* scratch,
+                          const int64_t* scratch_off, int32_t lds_bytes, void* stream);
+int64_t dr_vanilla_fused_lds_bytes(int32_t n_nodes, int32_t n_edges);
+int64_t dr_vanilla_fused_scratch_floats(int32_t n_nodes, int32_t n_edges);
+
 /* Adam (torch.optim.Adam, L2 weight decay added to the gradient) settings.  */
 typedef struct dr_adam {
   float lr, beta1, beta2, eps, weight_decay;
