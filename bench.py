@@ -178,7 +178,7 @@ def main():  # noqa: PLR0915
     ap.add_argument("--force-large", type=int, default=0, help="GINet: run the split tile+tail path with this many nodes per tile (diagnostic)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch every step from Python instead of replaying captured HIP graphs")
-    ap.add_argument("--capture-ddp", action="store_true", help="N>1: also capture the RCCL all-reduce in the HIP graph (default: eager steps)")
+    ap.add_argument("--eager-ddp", action="store_true", help="N>1: launch steps from Python (default: the RCCL all-reduce is captured in the HIP graph with the kernels)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -188,9 +188,13 @@ def main():  # noqa: PLR0915
     # DR_BENCH_SHARED_GPU=1 rehearses the N>1 code path on a one-GPU box (all
     # ranks on cuda:0 over gloo); real multi-GPU runs use RCCL, one GPU per rank.
     shared = os.environ.get("DR_BENCH_SHARED_GPU") == "1"
+    # DR_BENCH_PG=1 runs the data-parallel step (RCCL all-reduce between the
+    # graph pass and Adam) even at WORLD_SIZE=1: a one-GPU rehearsal of the
+    # N>1 launch path, captured all-reduce included.
+    force_pg = os.environ.get("DR_BENCH_PG") == "1"
     if shared:
         local = 0
-    if world > 1:
+    if world > 1 or force_pg:
         torch.cuda.set_device(local)
         if shared:
             torch.distributed.init_process_group("gloo")
@@ -225,11 +229,26 @@ def main():  # noqa: PLR0915
     for i in range(args.warmup):
         run_eager(i)
     captured = sweep = None
-    if not args.eager and (world == 1 or args.capture_ddp):
+    capture_note = ""
+    if not args.eager and (pg is None or (not shared and not args.eager_ddp)):
         # one captured graph per resident mini-batch, plus one graph holding a
-        # whole sweep over them (one launch per len(handles) steps)
-        captured = [step.capture(h, global_batch=B * world) for h in handles]
-        sweep = step.capture_sweep(handles, global_batch=B * world)
+        # whole sweep over them (one launch per len(handles) steps); N>1: the
+        # RCCL all-reduce is captured with the kernels
+        try:
+            captured = [step.capture(h, global_batch=B * world) for h in handles]
+            sweep = step.capture_sweep(handles, global_batch=B * world)
+        except RuntimeError as e:
+            if pg is None:
+                raise
+            captured = sweep = None  # fall back to eager steps
+            capture_note = f" (capture failed: {str(e)[:120]})"
+            print(f"[bench] rank {rank}: HIP graph capture of the DDP step failed, running eager steps: {e}", file=sys.stderr)
+        if pg is not None:  # every rank runs the same launch mode
+            ok = torch.tensor([0.0 if captured is None else 1.0], device=dev)
+            torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)
+            if float(ok.item()) < 1.0:
+                captured = sweep = None
+                capture_note = capture_note or " (capture failed on another rank)"
 
     def run_steps(i0, k):
         """Steps i0 .. i0+k-1 (mini-batch i % len(handles)); whole sweeps replay the sweep graph."""
@@ -328,7 +347,7 @@ def main():  # noqa: PLR0915
                 "kernel_ms_avg": round(kernel_ms, 5),
                 "kernel_timing": f"HIP events around one HIP graph of {args.steps} back-to-back {step.spec.entry if not large else 'dr_ginet_large_pass'} launches on the launch stream, divided by {args.steps}",
             },
-            "launch": "eager" if captured is None else f"hipgraph-replay ({len(handles)}-step sweep graphs + per-step graphs)",
+            "launch": ("eager" + capture_note) if captured is None else f"hipgraph-replay ({len(handles)}-step sweep graphs + per-step graphs{', RCCL all-reduce captured' if pg is not None else ''})",
             "cpu_baseline": cpu,
             "final_loss": float(loss.item()),
         }

@@ -150,7 +150,7 @@ class FusedTrainStep:
             ev.append((e0, e1))
         self.step_count += 1
         slab, head, lpg, lout = self.slab.data_ptr(), self.head.data_ptr(), self.lpg.data_ptr(), self.loss_out.data_ptr()
-        if self.world == 1:
+        if self.pg is None:
             _lib.check(lib.dr_reduce_update(self._table, slab, head, h.B, self._adam, lpg, scale, lout, stream), "dr_reduce_update")
         else:
             _lib.check(lib.dr_reduce_update(self._table, slab, head, h.B, self._adam_off, lpg, scale, lout, stream), "dr_reduce_update")

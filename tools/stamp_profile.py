@@ -27,6 +27,7 @@ from deeprank2_amd.store import GraphStore, pack_graphs  # noqa: E402
 from deeprank2_amd.utils.synthetic import make_dataset  # noqa: E402
 
 PHASES_NC = ["stage", "gather Z1=AX", "gemm H1", "gather Z2=AH1", "gemm2+bits+colsum", "mean", "head fwd+loss+bwd", "dW2", "dZ2", "spmmT dS1", "dW1"]
+PHASES_V = ["stage", "gemm [A|B]1", "row fwd 1", "gemm X1", "gemm [A|B]2", "row fwd 2", "gemm X2", "mean+bits", "head fwd/loss/bwd", "dWn2, dX1|dS2", "row bwd 2 + dWa2", "row T 2 + dWb2", "relu1, dS1, dWn1", "row bwd 1 + dWa1", "row T 1 + dWb1"]
 PHASES = ["stage", "gather Z=AX", "gemm H=relu(ZW)", "pool0", "gemm2+spmm2", "pool1", "mean", "head fwd (fc1,fc2)", "loss grad", "head bwd", "pool1-bwd", "spmm2T", "dW2+dP1", "dW1"]
 
 
@@ -34,6 +35,8 @@ def main():
     dev = torch.device("cuda:0")
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
     which = sys.argv[2] if len(sys.argv) > 2 else "ginet"
+    if which == "vanilla":
+        return vanilla(dev, B)
     mod, phases = (amd_nc, PHASES_NC) if which == "ginet_nocluster" else (amd, PHASES)
     large = which == "ginet_large"
     if large:  # tail kernel of the split path on atom-level graphs (stamps 0-3: staging, tile combine)
@@ -64,6 +67,39 @@ def main():
     print(f"B={B}  median cycles per graph-kernel workgroup: {tot:.0f}")
     print(which)
     for name, v in zip(phases, med):
+        print(f"  {name:18s} {v:8.0f} cyc  {100 * v / tot:5.1f}%")
+
+
+def vanilla(dev, B):
+    """vanilla_graph_kernel (dr_vanilla_fused_pass) phases on residue graphs."""
+    from deeprank2_amd import _lib  # noqa: PLC0415
+    from deeprank2_amd.fused import make_pass  # noqa: PLC0415
+    from deeprank2_amd.neuralnets.gnn import vanilla_gnn as van  # noqa: PLC0415
+
+    store = GraphStore(pack_graphs(records(make_dataset(B, seed=1000))), dev)
+    h = amd.BatchHandle(store, np.arange(B))
+    torch.manual_seed(0)
+    model = van.VanillaNetwork(30, 1, 3).to(dev)
+    spec = model.fused_spec
+    assert van.fused_fits(h, 30, 3)
+    st = torch.zeros(B * 32, dtype=torch.int64, device=dev)
+    out = torch.empty(B, 1, device=dev)
+    slab = torch.empty(B * spec.slab_stride(30), device=dev)
+    head = torch.empty(B * spec.head_stride(1), device=dev)
+    lpg = torch.empty(B, device=dev)
+    w = spec.weights(model.ordered_params())
+    rows = []
+    for it in range(30):
+        p = make_pass(1, _lib.DR_PASS_FORWARD | _lib.DR_PASS_BACKWARD, loss_kind=_lib.DR_LOSS_MSE, loss_scale=1 / B, out=out, loss_per_graph=lpg, slab=slab, head=head, stamps=st)
+        spec.run(h, w, p)
+        torch.cuda.synchronize()
+        if it >= 5:
+            rows.append(st.view(B, 32)[:, : len(PHASES_V) + 1].cpu().numpy().copy())
+    d = np.diff(np.stack(rows), axis=2).astype(np.float64)
+    med = np.median(d.reshape(-1, d.shape[-1]), axis=0)
+    tot = med.sum()
+    print(f"B={B}  median cycles per vanilla_graph_kernel workgroup: {tot:.0f}")
+    for name, v in zip(PHASES_V, med):
         print(f"  {name:18s} {v:8.0f} cyc  {100 * v / tot:5.1f}%")
 
 
