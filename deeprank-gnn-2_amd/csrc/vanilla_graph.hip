@@ -7,25 +7,32 @@
 //
 // Per layer:  m_e = relu(We [x_i | x_j | ea_e] + be)  for each edge e = (i -> j),
 //             s_i = sum_{e: src i} m_e,   x'_i = relu(Wn [x_i | s_i] + bn).
-// As in the batch-wide pipeline (vanilla_fused.hip) the edge GEMM is split,
-// We = [Wa | Wb | Wc]:  A = X Wa^T + be,  B = X Wb^T  (node GEMMs on MFMA) and
-// pre_e = A_i + B_j + Wc ea_e is rebuilt inside the CSR gather, so the E x 32
-// messages never exist.  Here the whole graph stays on one CU: A|B, S, X1 and
-// the CSR (+ transpose) live in LDS, the gather reads B_j from LDS, and the
-// forward records the ReLU pattern of every edge as one 32-bit word (bit c =
-// channel c active) in CSR order and in transposed order.  The backward then
-// needs neither A nor B again:
-//   D_i  = dS_i * #active(i, c)                       (CSR row pass on the bits)
-//   D'_j = sum_{e=(i->j) active} dS_i                 (transposed pass on the bits)
-//   dWc  = sum_i dS_i * sum_{e in row i, active} ea_e,  dbe = sum_i D_i
-//   dWa = D^T X, dWb = D'^T X, dX = DU Wn[:, :F] + D Wa + D' Wb   (MFMA)
+// The edge GEMM is split, We = [Wa | Wb | Wc]: B = X Wb^T is a node GEMM (MFMA),
+// A_i = Wa x_i + be is formed per CSR row inside the row pass, and
+// pre_e = A_i + B_j + Wc ea_e is rebuilt per edge, so the E x 32 messages never
+// exist.  While it sums s_i, the row pass also records, per (node i, channel c),
+//   cnt_i[c] = #{e in row i : pre_e[c] > 0}   and   eap_i[c][f] = sum of ea_e[f] over those edges,
+// and each edge's ReLU pattern (one 32-bit word, bit c = channel c active) in
+// TRANSPOSED order.  The backward then needs no pass over the CSR rows at all:
+//   D_i  = dS_i * cnt_i                  (elementwise)
+//   dWc  = sum_i dS_i * eap_i,  dbe = sum_i D_i
+//   D'_j = sum_{e=(i->j) active} dS_i     (transposed pass on the bits)
+//   dWa = D^T X, dWb = D'^T X, dX = [DU | D | D'] [Wn[:, :F]; Wa; Wb]   (MFMA)
 // and relu'(X2) is kept as one bit word per node, so dWn2 = dmean * (mask^T [X1|S2]).
-// Intermediates that are written once and read back much later by the same
-// workgroup (S1, the edge bit words, the transposed slot map) go to a per-graph
-// global scratch (L2-resident); everything gathered stays in LDS.
+//
+// Memory plan (LDS, 4-byte words; slots are N x 34, the stride that makes the
+// MFMA operand reads conflict free):
+//   forward : P = X0 -> B2 -> X2,  Q = B1 -> X1,  R = S1 -> S2,
+//             U = one 16-byte record per edge {B row byte offset | transposed slot, ea[0..2]} (+ ea[3])
+//   backward: P = dS2 -> dX1 -> DU1 -> D'1,  Q = X1 -> X0,  R = D2 -> S1 -> D1,
+//             U = T (D'2 -> dS1) | ReLU words (transposed) | transposed CSR
+// Written once, read back much later by the same workgroup, and too big to
+// keep: S1, cnt, eap and the transposed ReLU words go to a per-graph global
+// scratch (L2-resident) and come back by bulk loads.  GEMM weights (the MFMA B
+// operand) are loaded from global into registers once per phase and wave.
 // Bound: HBM on the compulsory inputs (x, CSR + transpose, edge_attr) and the
-// per-graph gradient partials; in practice the per-graph critical path (edge
-// passes on the VALU, ~5.7 M f32 MACs of node GEMMs on MFMA) — DESIGN.md §5.
+// per-graph gradient partials; in practice the per-graph critical path — see
+// DESIGN.md §5.
 
 #include <hip/hip_runtime.h>
 
@@ -38,38 +45,51 @@ using namespace drk;
 
 constexpr int NT = 1024;  // 16 waves
 constexpr int NW = NT / 64;
-constexpr int MAXFE = 4;   // edge features handled by this kernel (more: the pipeline)
-constexpr int LAB = 64;    // [A+be | B] per node; backward: [dS | D or D']
-constexpr int LS = 34;     // S / dX / X1 row stride (F <= 32, 2 words of skew for the MFMA reads)
-constexpr int REDW = 160;  // per-wave partials: 32 (dbe) + 32 * MAXFE (dWc)
+constexpr int MAXFE = 4;  // edge features handled by this kernel (more: the pipeline)
+constexpr int LS = 34;    // slot row stride
+constexpr int HEADW = 512;
 
 struct VCarve {
-  int rp, col, trp, tcol, x1, ab, s, xb, head, red, total;
+  int rp, xb, head, P, Q, R, U, ext, T, bt, trp, tcol, total;
 };
 
-__host__ __device__ inline VCarve vcarve(int N, int E) {
+__host__ __device__ inline int vslot(int N, int Fe) {
+  const int red = NW * 32 * (1 + Fe);  // the D pass partials live in P or T
+  return imax(r4(N * LS), imax(red, 1024));
+}
+
+__host__ __device__ inline VCarve vcarve(int N, int E, int Fe) {
   VCarve c;
   int o = 0;
 #define TAKE(field, words) \
   c.field = o;             \
   o += r4(words);
   TAKE(rp, N + 1)
-  TAKE(col, (E + 1) / 2)  // uint16 column ids (16-byte DMA units)
-  TAKE(trp, N + 1)
-  TAKE(tcol, (E + 1) / 2)
-  TAKE(x1, N * LS)
-  TAKE(ab, N * LAB)
-  TAKE(s, N * LS)
   TAKE(xb, N)
-  TAKE(head, 512)  // g 32 | h 128 | dh 128 | dout 16 | dmean 32 | spare
-  TAKE(red, NW * REDW)
+  TAKE(head, HEADW)
+  TAKE(P, vslot(N, Fe))
+  TAKE(Q, r4(N * LS))
+  TAKE(R, r4(N * LS))
 #undef TAKE
-  c.total = o;
+  c.U = o;
+  // 16 zero records past the last edge: a row pass may read up to 15 records
+  // beyond its row (masked), never beyond these
+  c.ext = c.U + 4 * (E + 16);  // ea[3] per edge behind the records (Fe == 4)
+  const int fwd = 4 * (E + 16) + (Fe > 3 ? E + 16 : 0);
+  c.T = c.U;
+  c.bt = c.T + vslot(N, Fe);
+  c.trp = c.bt + r4(E);
+  c.tcol = c.trp + r4(N + 1);
+  const int bwd = c.tcol + r4((E + 1) / 2) - c.U;
+  c.total = c.U + r4(imax(fwd, bwd));
   return c;
 }
 
-// per-graph global scratch (floats): S1 [N*32] | bits1 csr [E] | bits1 t [E] | bits2 csr [E] | bits2 t [E] | tpos [E]
-__host__ __device__ inline int64_t vscratch_floats(int N, int E) { return (int64_t)r4(N * 32) + 5LL * r4(E); }
+// per-graph global scratch (floats): S1 [32N] | cnt1 [32N] | cnt2 [32N] | eap1 [Fe][32N] | eap2 [Fe][32N] |
+// bt1 [E + 1] | bt2 [E + 1]  (slot E of bt takes the padding lanes' stores)
+__host__ __device__ inline int64_t vscratch_floats(int N, int E, int Fe) {
+  return (int64_t)(3 + 2 * Fe) * r4(32 * N) + 2LL * r4(E + 1);
+}
 
 struct VGArgs {
   dr_graph_store s;
@@ -81,11 +101,48 @@ struct VGArgs {
   int32_t B;
 };
 
-// C[m, n] = sum_k A(m, k) B(k, n) on v_mfma_f32_16x16x4_f32, 16x16 output tiles
-// spread over the 16 waves (job j on wave (start + j) % NW, so two GEMMs of a
-// phase can share the waves).  A / B must return 0 for k >= the true K
-// (K4 = K rounded up to 8 here: two accumulator chains).  epi(m, n, v) for
-// m < M, n < Nn.
+__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__device__ const float vg_zero_word = 0.f;
+
+// Branch-free global loads: p (nullptr = the value 0) is read unconditionally,
+// so a batch of them is issued back to back and waited for once.
+__device__ __forceinline__ float ld0(const float* p) { return *(p ? p : &vg_zero_word); }
+
+// C[M, 32] = A[M, K] W[K, 32], K = 32 * NK, on v_mfma_f32_16x16x4_f32.  Wave w
+// owns column tile w & 1 and row tiles w >> 1, (w >> 1) + 8, ...; its B
+// fragment (W(k, n): a pointer into the weights, nullptr = 0) and the column's
+// bias (Bp(n), nullptr = 0) are loaded into registers once, before the first
+// tile.  A returns the LDS operand; epi(m, n, v, bias).
+template <int NK, class AF, class WF, class BF, class EF>
+__device__ __forceinline__ void mm_w(int M, AF A, WF W, BF Bp, EF epi) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, kq = lane >> 4;
+  const int n = (wave & 1) * 16 + li;
+  float bw[8 * NK];
+#pragma unroll
+  for (int s = 0; s < 8 * NK; ++s) bw[s] = ld0(W(4 * s + kq, n));
+  const float bias = ld0(Bp(n));
+  const int nrt = (M + 15) >> 4;
+  for (int rt = wave >> 1; rt < nrt; rt += NW / 2) {
+    const int m0 = rt << 4, am = min(m0 + li, M - 1);
+    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 8 * NK; s += 2) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(A(am, 4 * s + kq), bw[s], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(A(am, 4 * s + 4 + kq), bw[s + 1], acc1, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = m0 + kq * 4 + r;
+      if (row < M) epi(row, n, acc0[r] + acc1[r], bias);
+    }
+  }
+}
+
+// C[M, Nn] = sum_k A(m, k) B(k, n), both operands in LDS (weight gradients,
+// K = the graph's node count), 16x16 tiles over the waves (job j on wave
+// (start + j) % NW, so two GEMMs of a phase can share the waves).  A / B must
+// return 0 for k >= the true K (K is rounded up to 8: two accumulator chains).
 template <class AF, class BF, class EF>
 __device__ __forceinline__ void mm16(int M, int Nn, int K, int start, AF A, BF Bf, EF epi) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, kq = lane >> 4;
@@ -108,141 +165,206 @@ __device__ __forceinline__ void mm16(int M, int Nn, int K, int start, AF A, BF B
   }
 }
 
-__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ float2 f2fma(float a, float2 w, float2 c) { return make_float2(fmaf(a, w.x, c.x), fmaf(a, w.y, c.y)); }
+__device__ __forceinline__ float2 f2add(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 f2shfl_xor(float2 v, int m) {
+  return make_float2(__shfl_xor(v.x, m, 64), __shfl_xor(v.y, m, 64));
+}
+// sum over the 4 edge slots of a wave (lanes l, l^16, l^32, l^48)
+__device__ __forceinline__ float2 f2slot_sum(float2 v) {
+  v = f2add(v, f2shfl_xor(v, 16));
+  return f2add(v, f2shfl_xor(v, 32));
+}
 
-// Forward CSR row pass of one layer: S_i = sum_{e in row i} relu(A_i + B_j + Wc ea_e)
-// (A already carries be), one wave per row, lane = (channel c, edge parity h).
-// The ReLU pattern of each edge (ballot over the 32 channel lanes) goes to
-// bc[e] (CSR order) and bt[tpos[e]] (transposed order).
-__device__ void row_fwd(const int* srp, const uint16_t* scol, const float* AB, float* S, float* S1g, const float* ea,
-                        int Fe, int FeS, const float* we, int KE, int F, const int* tpos, uint32_t* bc, uint32_t* bt,
-                        int N) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
-  float wc[MAXFE];
+// Edge ReLU words: bit b (b < 16) = channel 2b, bit 16 + b = channel 2b + 1
+// (the two ballots of the packed row pass side by side).
+
+// Forward CSR row pass of one layer, one wave per row.  Lane = (channel pair
+// cp = lane & 15: channels 2cp, 2cp+1 as a float2; edge slot sl = lane >> 4):
+// each 16-edge chunk of the row is 4 steps of 4 edges.
+//   S_i = sum_{e in row i} relu(A_i + B_j + Wc ea_e),   A_i = Wa x_i + be
+// (A_i: each slot sums 8 of the K = 32 (padded) inputs, then the slots combine).
+// Also cnt_i / eap_i (see the header) and each edge's ReLU word at its
+// transposed slot (global bt).  Edge records: {byte offset of B row col | tpos << 16, ea0, ea1, ea2}.
+template <int FE>
+__device__ __forceinline__ void row_fwd(const int* rp, const uint4* rec, const float* ext, const float* X,
+                                        const float* Bs, float* S, float* S1g, float* cntg, float* eapg,
+                                        uint32_t* btg, const float* we, const float* be, int KE, int F, int N,
+                                        int N_E) {
+  constexpr int FA = FE > 0 ? FE : 1;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, cp = lane & 15, sl = lane >> 4, c0 = 2 * cp;
+  float2 wa[8];
 #pragma unroll
-  for (int f = 0; f < MAXFE; ++f) wc[f] = f < Fe ? we[c * KE + 2 * F + f] : 0.f;
+  for (int m = 0; m < 8; ++m) {
+    const int k = 8 * sl + m;
+    const int kc = k < F ? k : 0;
+    const float w0 = we[c0 * KE + kc], w1 = we[(c0 + 1) * KE + kc];
+    wa[m] = k < F ? make_float2(w0, w1) : make_float2(0.f, 0.f);
+  }
+  float2 wc[FA];
+#pragma unroll
+  for (int f = 0; f < FE; ++f) wc[f] = make_float2(we[c0 * KE + 2 * F + f], we[(c0 + 1) * KE + 2 * F + f]);
+  const float2 be2 = make_float2(be[c0], be[c0 + 1]);
+  const int n32 = 32 * N;
   for (int i = wave; i < N; i += NW) {
-    const int eb = srp[i], ee = srp[i + 1];
-    const float ai = AB[i * LAB + c];
-    float acc = 0.f;
-    for (int e0 = eb; e0 < ee; e0 += 16) {
-      const int nch = min(16, ee - e0);
-      float ev[8][MAXFE];
-      int tp[8];
+    const int eb = rp[i], ee = rp[i + 1];
+    float2 a = make_float2(0.f, 0.f);
+    {
+      const float2* xr = reinterpret_cast<const float2*>(X + i * LS + 8 * sl);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int t = 2 * u + h;
-        const int e = e0 + (t < nch ? t : 0);
-#pragma unroll
-        for (int f = 0; f < MAXFE; ++f) ev[u][f] = f < Fe ? ea[(int64_t)e * FeS + f] : 0.f;
-        tp[u] = tpos[e];
-      }
-      float bj[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int t = 2 * u + h;
-        const int j = scol[e0 + (t < nch ? t : 0)];
-        bj[u] = AB[j * LAB + 32 + c];
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int t = 2 * u + h;
-        const bool ok = t < nch;
-        float ce = 0.f;
-#pragma unroll
-        for (int f = 0; f < MAXFE; ++f) ce = fmaf(wc[f], ev[u][f], ce);
-        const float pre = ai + bj[u] + ce;
-        if (ok) acc += relu_keepnan(pre);
-        const uint64_t m = __ballot(ok && !(pre <= 0.f));
-        if ((lane & 31) == 0 && ok) {
-          const uint32_t word = h ? (uint32_t)(m >> 32) : (uint32_t)m;
-          bc[e0 + t] = word;
-          bt[tp[u]] = word;
-        }
+      for (int m = 0; m < 4; ++m) {
+        const float2 v = xr[m];
+        a = f2fma(v.x, wa[2 * m], a);
+        a = f2fma(v.y, wa[2 * m + 1], a);
       }
     }
-    acc += __shfl_xor(acc, 32, 64);
-    if (h == 0) {
-      S[i * LS + c] = acc;
-      if (S1g) S1g[i * 32 + c] = acc;
+    a = f2add(f2slot_sum(a), be2);
+    float2 acc = make_float2(0.f, 0.f), cnt = make_float2(0.f, 0.f), eap[FA];
+#pragma unroll
+    for (int f = 0; f < FA; ++f) eap[f] = make_float2(0.f, 0.f);
+    for (int e0 = eb; e0 < ee; e0 += 16) {
+      const int nch = ee - e0;
+      uint4 r[4];
+      float e3[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        r[u] = rec[e0 + sl + 4 * u];  // past the row end: the next rows' / padding records (masked)
+        e3[u] = FE > 3 ? ext[e0 + sl + 4 * u] : 0.f;
+      }
+      float2 bj[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        bj[u] = *reinterpret_cast<const float2*>(reinterpret_cast<const char*>(Bs) + (r[u].x & 0xffffu) + 8 * cp);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bool ok = sl + 4 * u < nch;
+        const float ev[4] = {__uint_as_float(r[u].y), __uint_as_float(r[u].z), __uint_as_float(r[u].w), e3[u]};
+        float2 pre = f2add(a, bj[u]);
+#pragma unroll
+        for (int f = 0; f < FE; ++f) pre = f2fma(ev[f], wc[f], pre);
+        pre.x = ok ? pre.x : -1.f;  // slots past the row end: inactive, contribute 0
+        pre.y = ok ? pre.y : -1.f;
+        const bool al = !(pre.x <= 0.f), ah = !(pre.y <= 0.f);  // relu keeps NaN (active)
+        acc.x += al ? pre.x : 0.f;
+        acc.y += ah ? pre.y : 0.f;
+        const float2 af = make_float2(al ? 1.f : 0.f, ah ? 1.f : 0.f);
+        cnt = f2add(cnt, af);
+#pragma unroll
+        for (int f = 0; f < FE; ++f) eap[f] = make_float2(fmaf(af.x, ev[f], eap[f].x), fmaf(af.y, ev[f], eap[f].y));
+        const uint64_t blo = __ballot(al), bhi = __ballot(ah);
+#ifndef VG_NO_BT
+        // every lane of the slot stores its edge's word (same address); past the row end: slot E
+        btg[ok ? (int)(r[u].x >> 16) : N_E] =
+            (uint32_t)((blo >> (16 * sl)) & 0xffffu) | ((uint32_t)((bhi >> (16 * sl)) & 0xffffu) << 16);
+#endif
+      }
+    }
+    acc = f2slot_sum(acc);
+    cnt = f2slot_sum(cnt);
+#pragma unroll
+    for (int f = 0; f < FE; ++f) eap[f] = f2slot_sum(eap[f]);
+    if (sl == 0) {
+      *reinterpret_cast<float2*>(S + i * LS + c0) = acc;
+#ifndef VG_NO_CNT
+      if (S1g) *reinterpret_cast<float2*>(S1g + i * 32 + c0) = acc;
+      *reinterpret_cast<float2*>(cntg + i * 32 + c0) = cnt;
+#pragma unroll
+      for (int f = 0; f < FE; ++f) *reinterpret_cast<float2*>(eapg + f * n32 + i * 32 + c0) = eap[f];
+#endif
     }
   }
 }
 
-// Backward CSR row pass: D_i = dS_i * #active(i, c) (0 when none) into AB[:, 32:],
-// and per-wave partials of dbe = sum D and dWc[c][f] = sum_i dS_i * sum_{active} ea_e[f].
-__device__ void row_bwd(const int* srp, float* AB, const float* ea, int Fe, int FeS, const uint32_t* bc, float* red,
-                        int N) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
-  float pbe = 0.f, pwc[MAXFE];
+// D_i = dS_i * cnt_i (0 where no edge of row i is active) into D; per-wave
+// partials of dbe = sum_i D_i and dWc[c][f] = sum_i dS_i[c] eap_i[c][f] into red
+// [NW][32 * (1 + FE)].  Thread (slice sl = tid >> 5, channel c) takes rows sl, sl + 32, ...
+template <int FE>
+__device__ __forceinline__ void d_pass(const float* dS, float* D, const float* cntg, const float* eapg, float* red,
+                                       int N) {
+  constexpr int FA = FE > 0 ? FE : 1;
+  const int tid = threadIdx.x, c = tid & 31, sl = tid >> 5, wave = tid >> 6;
+  const int n32 = 32 * N;
+  float pbe = 0.f, pwc[FA];
 #pragma unroll
-  for (int f = 0; f < MAXFE; ++f) pwc[f] = 0.f;
-  for (int i = wave; i < N; i += NW) {
-    const int eb = srp[i], ee = srp[i + 1];
-    float cnt = 0.f, eap[MAXFE];
+  for (int f = 0; f < FA; ++f) pwc[f] = 0.f;
+  for (int i0 = sl; i0 < N; i0 += 128) {  // 4 rows per step, their loads issued together
+    float cn[4], ep[4][FA];
 #pragma unroll
-    for (int f = 0; f < MAXFE; ++f) eap[f] = 0.f;
-    for (int e0 = eb; e0 < ee; e0 += 16) {
-      const int nch = min(16, ee - e0);
-      uint32_t wd[8];
-      float ev[8][MAXFE];
+    for (int q = 0; q < 4; ++q) {
+      const int i = i0 + 32 * q;
+      const bool ok = i < N;
+      const int ii = ok ? i : 0;
+      cn[q] = cntg[ii * 32 + c];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int t = 2 * u + h;
-        const int e = e0 + (t < nch ? t : 0);
-        wd[u] = t < nch ? bc[e] : 0u;
+      for (int f = 0; f < FE; ++f) ep[q][f] = eapg[f * n32 + ii * 32 + c];
+    }
 #pragma unroll
-        for (int f = 0; f < MAXFE; ++f) ev[u][f] = f < Fe ? ea[(int64_t)e * FeS + f] : 0.f;
-      }
+    for (int q = 0; q < 4; ++q) {
+      const int i = i0 + 32 * q;
+      if (i < N) {  // (cn / ep of rows >= N are never used)
+        const float ds = dS[i * LS + c];
+        const float d = cn[q] != 0.f ? ds * cn[q] : 0.f;
+        D[i * LS + c] = d;
+        pbe += d;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if ((wd[u] >> c) & 1u) {
-          cnt += 1.f;
-#pragma unroll
-          for (int f = 0; f < MAXFE; ++f) eap[f] += ev[u][f];
-        }
+        for (int f = 0; f < FE; ++f) pwc[f] += cn[q] != 0.f ? ds * ep[q][f] : 0.f;
       }
     }
-    cnt += __shfl_xor(cnt, 32, 64);
-#pragma unroll
-    for (int f = 0; f < MAXFE; ++f) eap[f] += __shfl_xor(eap[f], 32, 64);
-    const float ds = AB[i * LAB + c];
-    const float D = cnt != 0.f ? ds * cnt : 0.f;
-    if (h == 0) AB[i * LAB + 32 + c] = D;
-    pbe += D;
-#pragma unroll
-    for (int f = 0; f < MAXFE; ++f) pwc[f] += cnt != 0.f ? ds * eap[f] : 0.f;
   }
-  if (h == 0) {
-    red[wave * REDW + c] = pbe;
+  pbe += __shfl_xor(pbe, 32, 64);
 #pragma unroll
-    for (int f = 0; f < MAXFE; ++f) red[wave * REDW + 32 + c * MAXFE + f] = pwc[f];
+  for (int f = 0; f < FE; ++f) pwc[f] += __shfl_xor(pwc[f], 32, 64);
+  constexpr int RW = 32 * (1 + FE);
+  if ((tid & 63) < 32) {
+    red[wave * RW + c] = pbe;
+#pragma unroll
+    for (int f = 0; f < FE; ++f) red[wave * RW + 32 + c * FE + f] = pwc[f];
   }
 }
 
-// Transposed pass: D'_j = sum over in-edges (i -> j) that are active in channel c of dS_i, into AB[:, 32:].
-__device__ void row_t(const int* strp, const uint16_t* stcol, float* AB, const uint32_t* bt, int N) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
+// dbe and dWc of one layer from the D pass partials (fixed wave order).
+template <int FE>
+__device__ __forceinline__ void d_pass_sum(const float* red, float* gw, int KE, int F) {
+  constexpr int RW = 32 * (1 + FE);
+  const int tid = threadIdx.x;
+  if (tid < RW) {
+    float t = 0.f;
+    for (int wv = 0; wv < NW; ++wv) t += red[wv * RW + tid];
+    if (tid < 32) gw[32 * KE + tid] = t;
+    else {
+      const int c = (tid - 32) / FE, f = (tid - 32) % FE;
+      gw[c * KE + 2 * F + f] = t;
+    }
+  }
+}
+
+// Transposed pass: D'_j = sum over in-edges (i -> j) active in channel c of dS_i
+// (lane layout of row_fwd: channel pair x edge slot).
+__device__ __forceinline__ void row_t(const int* trp, const uint16_t* tcol, const uint32_t* bt, const float* dS,
+                                      float* Dp, int N) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, cp = lane & 15, sl = lane >> 4, c0 = 2 * cp;
   for (int j = wave; j < N; j += NW) {
-    const int qb = strp[j], qe = strp[j + 1];
-    float acc = 0.f;
+    const int qb = trp[j], qe = trp[j + 1];
+    float2 acc = make_float2(0.f, 0.f);
     for (int q0 = qb; q0 < qe; q0 += 16) {
-      const int nch = min(16, qe - q0);
-      uint32_t wd[8];
-      float v[8];
+      const int nch = qe - q0;
+      uint32_t wd[4];
+      float2 v[4];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int t = 2 * u + h;
-        wd[u] = t < nch ? bt[q0 + t] : 0u;
-        const int src = stcol[q0 + (t < nch ? t : 0)];
-        v[u] = AB[src * LAB + c];
+      for (int u = 0; u < 4; ++u) {
+        const bool ok = sl + 4 * u < nch;
+        const int q = q0 + min(sl + 4 * u, nch - 1);
+        wd[u] = ok ? bt[q] : 0u;
+        v[u] = *reinterpret_cast<const float2*>(dS + (int)tcol[q] * LS + c0);
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if ((wd[u] >> c) & 1u) acc += v[u];
+      for (int u = 0; u < 4; ++u) {
+        acc.x += ((wd[u] >> cp) & 1u) ? v[u].x : 0.f;
+        acc.y += ((wd[u] >> (16 + cp)) & 1u) ? v[u].y : 0.f;
+      }
     }
-    acc += __shfl_xor(acc, 32, 64);
-    if (h == 0) AB[j * LAB + 32 + c] = acc;
+    acc = f2slot_sum(acc);
+    if (sl == 0) *reinterpret_cast<float2*>(Dp + j * LS + c0) = acc;
   }
 }
 
@@ -259,6 +381,7 @@ __device__ void row_t(const int* strp, const uint16_t* stcol, float* AB, const u
   } while (0)
 #endif
 
+template <int FE>
 __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -268,51 +391,82 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   const dr_pass& p = a.p;
   const dr_graph_desc d = a.descs[b];
   const int g = d.gid, N = d.n_nodes, E = d.n_edges;
-  const int F = s.n_feat, Fe = s.n_edge_feat, FeS = Fe > 0 ? Fe : 1, XS = s.x_stride;
+  const int F = s.n_feat, Fe = FE, FeS = Fe > 0 ? Fe : 1, XS = s.x_stride;
   const int KE = 2 * F + Fe, KN = F + 32, OUT = p.out_dim;
-  const int F4 = r4(F);
-  const VCarve cv = vcarve(N, E);
+  const VCarve cv = vcarve(N, E, Fe);
   int* srp = reinterpret_cast<int*>(lds + cv.rp);
-  uint16_t* scol = reinterpret_cast<uint16_t*>(lds + cv.col);
+  uint32_t* xb = reinterpret_cast<uint32_t*>(lds + cv.xb);
+  float* P = lds + cv.P;
+  float* Q = lds + cv.Q;
+  float* R = lds + cv.R;
+  uint4* rec = reinterpret_cast<uint4*>(lds + cv.U);
+  float* ext = lds + cv.ext;
+  float* T = lds + cv.T;
+  uint32_t* bt = reinterpret_cast<uint32_t*>(lds + cv.bt);
   int* strp = reinterpret_cast<int*>(lds + cv.trp);
   uint16_t* stcol = reinterpret_cast<uint16_t*>(lds + cv.tcol);
-  float* X1 = lds + cv.x1;
-  float* AB = lds + cv.ab;
-  float* S = lds + cv.s;
-  uint32_t* xb = reinterpret_cast<uint32_t*>(lds + cv.xb);
   float* sg = lds + cv.head;
   float* sh = sg + 32;
   float* sdh = sh + 128;
   float* sdout = sdh + 128;
   float* sdm = sdout + 16;
-  float* red = lds + cv.red;
 
   const float* X0 = s.x + d.node0 * (int64_t)XS;
   const float* ea = s.ea + d.col0 * (int64_t)FeS;
   float* scr = a.scr + a.scr_off[b];
+  const int n32 = r4(32 * N);
   float* S1g = scr;
-  uint32_t* b1c = reinterpret_cast<uint32_t*>(scr + r4(N * 32));
-  uint32_t* b1t = b1c + r4(E);
-  uint32_t* b2c = b1t + r4(E);
-  uint32_t* b2t = b2c + r4(E);
-  int* tpos = reinterpret_cast<int*>(b2t + r4(E));
+  float* cnt1 = S1g + n32;
+  float* cnt2 = cnt1 + n32;
+  float* eap1 = cnt2 + n32;
+  float* eap2 = eap1 + Fe * n32;
+  uint32_t* bt1g = reinterpret_cast<uint32_t*>(eap2 + Fe * n32);
+  uint32_t* bt2g = bt1g + r4(E + 1);
   const int LG = 32 * KE + 32 + F * KN + F;  // one layer's gradient entries in the slab
   float* slab = p.slab ? p.slab + (int64_t)b * DR_VANILLA_SLAB_STRIDE(F, Fe) : nullptr;
+  const bool bwd = (p.flags & DR_PASS_BACKWARD) != 0;
 
   VSTAMP(0);
-  // ---------------- stage: CSR + transpose into LDS, transposed slot map ----
+  // ---------------- stage: CSR rows, edge records, X0 into LDS ------------
   dma_words<NT>(srp, s.rowptr + d.node0 + g, N + 1);
-  dma_x4<NT>(scol, s.col + d.col0, (E + 7) / 8);
-  dma_words<NT>(strp, s.t_rowptr + d.node0 + g, N + 1);
-  dma_x4<NT>(stcol, s.t_col + d.col0, (E + 7) / 8);
   {
+    const uint16_t* gcol = s.col + d.col0;
     const int* teid = s.t_eid + d.col0;
-    for (int q = tid; q < E; q += NT) tpos[teid[q]] = q;  // CSR slot -> transposed slot
+    uint16_t* r16 = reinterpret_cast<uint16_t*>(rec);
+    float* rf = reinterpret_cast<float*>(rec);
+    for (int e0 = tid; e0 < E; e0 += 4 * NT) {  // 4 edges per thread and step, loads first
+      uint32_t cl[4];
+      int te[4];
+      float ev[4][MAXFE];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = e0 + u * NT;
+        const int ec = e < E ? e : 0;  // E >= 1 here (the loop runs only then)
+        cl[u] = gcol[ec];
+        te[u] = teid[ec];
+#pragma unroll
+        for (int f = 0; f < MAXFE; ++f) ev[u][f] = f < Fe ? ea[(int64_t)ec * FeS + f] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = e0 + u * NT;
+        if (e < E) {
+          r16[8 * e] = (uint16_t)(cl[u] * (LS * 4));  // byte offset of row col in a slot
+          r16[8 * te[u] + 1] = (uint16_t)e;  // transposed slot e holds CSR edge te[u]
+#pragma unroll
+          for (int f = 0; f < 3; ++f) rf[4 * e + 1 + f] = ev[u][f];
+          if (Fe > 3) ext[e] = ev[u][3];
+        }
+      }
+    }
+    for (int q = tid; q < 64; q += NT) reinterpret_cast<uint32_t*>(rec)[4 * E + q] = 0u;  // padding records
+    if (Fe > 3 && tid < 16) ext[E + tid] = 0.f;
   }
-  for (int p2 = tid; p2 < N * (LS - F); p2 += NT) {  // zero the pad columns of X1 and S (MFMA K padding)
-    const int i = p2 / (LS - F), k = F + p2 - i * (LS - F);
-    X1[i * LS + k] = 0.f;
-    S[i * LS + k] = 0.f;
+  for (int q = tid; q < N * 8; q += NT) {  // X0 -> P (stride LS), zero columns >= XS
+    const int i = q >> 3, c4 = (q & 7) * 4;
+    const float4 v = c4 < XS ? *reinterpret_cast<const float4*>(X0 + (int64_t)i * XS + c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    *reinterpret_cast<float2*>(P + i * LS + c4) = make_float2(v.x, v.y);
+    *reinterpret_cast<float2*>(P + i * LS + c4 + 2) = make_float2(v.z, v.w);
   }
   const float y_g = s.y[g];
   if (p.step_counter && b == 0 && tid == 0) p.step_counter[1] = p.step_counter[0];
@@ -320,69 +474,87 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   __syncthreads();
 
   VSTAMP(1);
-  // ---------------- layer 1: [A | B] = X0 [Wa; Wb]^T, A += be -------------
-  mm16(N, 64, F, 0, [&](int i, int k) { return k < F ? X0[(int64_t)i * XS + k] : 0.f; },
-       [&](int k, int n) { return k < F ? w.we1[(n & 31) * KE + (n < 32 ? 0 : F) + k] : 0.f; },
-       [&](int i, int n, float v) { AB[i * LAB + n] = v + (n < 32 ? w.be1[n] : 0.f); });
+  // ---------------- layer 1: B1 = X0 Wb1^T -> Q ----------------------------
+  mm_w<1>(N, [&](int i, int k) { return P[i * LS + k]; },
+          [&](int k, int n) -> const float* { return k < F ? w.we1 + n * KE + F + k : nullptr; }, [&](int) -> const float* { return nullptr; },
+          [&](int i, int n, float v, float) { Q[i * LS + n] = v; });
   __syncthreads();
   VSTAMP(2);
-  row_fwd(srp, scol, AB, S, S1g, ea, Fe, FeS, w.we1, KE, F, tpos, b1c, b1t, N);
-  wait_vm();
+  row_fwd<FE>(srp, rec, ext, P, Q, R, S1g, cnt1, eap1, bt1g, w.we1, w.be1, KE, F, N, E);
   __syncthreads();
   VSTAMP(3);
-  // X1 = relu([X0 | S1] Wn1^T + bn1)
-  mm16(N, F, F4 + 32, 0,
-       [&](int i, int k) { return k < F ? X0[(int64_t)i * XS + k] : (k < F4 ? 0.f : (k < F4 + 32 ? S[i * LS + k - F4] : 0.f)); },
-       [&](int k, int n) { return k < F ? w.wn1[n * KN + k] : (k < F4 ? 0.f : (k < F4 + 32 ? w.wn1[n * KN + F + k - F4] : 0.f)); },
-       [&](int i, int n, float v) { X1[i * LS + n] = relu_keepnan(v + w.bn1[n]); });
+  // X1 = relu([X0 | S1] Wn1^T + bn1) -> Q (pad columns 0)
+  mm_w<2>(N, [&](int i, int k) { return k < 32 ? P[i * LS + k] : R[i * LS + k - 32]; },
+          [&](int k, int n) -> const float* {
+            return n < F ? (k < F ? w.wn1 + n * KN + k : (k < 32 ? nullptr : w.wn1 + n * KN + F + k - 32)) : nullptr;
+          },
+          [&](int n) -> const float* { return n < F ? w.bn1 + n : nullptr; },
+          [&](int i, int n, float v, float bias) { Q[i * LS + n] = n < F ? relu_keepnan(v + bias) : 0.f; });
   __syncthreads();
   VSTAMP(4);
-  // ---------------- layer 2 ------------------------------------------------
-  mm16(N, 64, F, 0, [&](int i, int k) { return k < F ? X1[i * LS + k] : 0.f; },
-       [&](int k, int n) { return k < F ? w.we2[(n & 31) * KE + (n < 32 ? 0 : F) + k] : 0.f; },
-       [&](int i, int n, float v) { AB[i * LAB + n] = v + (n < 32 ? w.be2[n] : 0.f); });
+  // ---------------- layer 2: B2 = X1 Wb2^T -> P ----------------------------
+  mm_w<1>(N, [&](int i, int k) { return Q[i * LS + k]; },
+          [&](int k, int n) -> const float* { return k < F ? w.we2 + n * KE + F + k : nullptr; }, [&](int) -> const float* { return nullptr; },
+          [&](int i, int n, float v, float) { P[i * LS + n] = v; });
   __syncthreads();
   VSTAMP(5);
-  row_fwd(srp, scol, AB, S, nullptr, ea, Fe, FeS, w.we2, KE, F, tpos, b2c, b2t, N);
-  wait_vm();
+  row_fwd<FE>(srp, rec, ext, Q, P, R, nullptr, cnt2, eap2, bt2g, w.we2, w.be2, KE, F, N, E);
+  wait_vm();  // ReLU words, cnt, eap of both layers stored before anyone reads them back
   __syncthreads();
   VSTAMP(6);
-  // X2 = relu([X1 | S2] Wn2^T + bn2) into AB (A|B of layer 2 are dead)
-  mm16(N, F, F4 + 32, 0,
-       [&](int i, int k) { return k < F ? X1[i * LS + k] : (k < F4 ? 0.f : (k < F4 + 32 ? S[i * LS + k - F4] : 0.f)); },
-       [&](int k, int n) { return k < F ? w.wn2[n * KN + k] : (k < F4 ? 0.f : (k < F4 + 32 ? w.wn2[n * KN + F + k - F4] : 0.f)); },
-       [&](int i, int n, float v) { AB[i * LAB + n] = relu_keepnan(v + w.bn2[n]); });
+  // the records are dead: the backward's transposed CSR and layer-2 ReLU words
+  // land in U while the forward finishes
+  if (bwd) {
+    dma_words<NT>(bt, bt2g, E);
+    dma_words<NT>(strp, s.t_rowptr + d.node0 + g, N + 1);
+    dma_x4<NT>(stcol, s.t_col + d.col0, (E + 7) / 8);
+  }
+  // X2 = relu([X1 | S2] Wn2^T + bn2) -> P
+  mm_w<2>(N, [&](int i, int k) { return k < 32 ? Q[i * LS + k] : R[i * LS + k - 32]; },
+          [&](int k, int n) -> const float* {
+            return n < F ? (k < F ? w.wn2 + n * KN + k : (k < 32 ? nullptr : w.wn2 + n * KN + F + k - 32)) : nullptr;
+          },
+          [&](int n) -> const float* { return n < F ? w.bn2 + n : nullptr; },
+          [&](int i, int n, float v, float bias) { P[i * LS + n] = n < F ? relu_keepnan(v + bias) : 0.f; });
   __syncthreads();
   VSTAMP(7);
-  // per-graph mean (scatter_mean, vanilla_gnn.py:62): 32 row slices per column, combined in order;
-  // relu'(X2) as one bit word per node
+  // per-graph mean (scatter_mean, vanilla_gnn.py:62): 32 row slices per column
+  // (partials in T), combined in order; relu'(X2) as one bit word per node
   {
     const int n = tid & 31, sl = tid >> 5;
     float acc = 0.f;
-    if (n < F) {
-      const int i0 = (N * sl) >> 5, i1 = (N * (sl + 1)) >> 5;
-      for (int i = i0; i < i1; ++i) acc += AB[i * LAB + n];
-    }
-    red[sl * 32 + n] = acc;
+    const int i0 = (N * sl) >> 5, i1 = (N * (sl + 1)) >> 5;
+    for (int i = i0; i < i1; ++i) acc += P[i * LS + n];
+    T[sl * 32 + n] = acc;
     for (int i = wave * 2 + (lane >> 5); i < N; i += 2 * NW) {
       const int c = lane & 31;
-      const uint64_t m = __ballot(c < F && !(AB[i * LAB + c] <= 0.f));
+      const uint64_t m = __ballot(c < F && !(P[i * LS + c] <= 0.f));
       if (c == 0) xb[i] = (lane >> 5) ? (uint32_t)(m >> 32) : (uint32_t)m;
     }
   }
   __syncthreads();
   if (tid < 32) {
     float t = 0.f;
-    for (int sl = 0; sl < 32; ++sl) t += red[sl * 32 + tid];
+    for (int sl = 0; sl < 32; ++sl) t += T[sl * 32 + tid];
     sg[tid] = tid < F ? t / (float)N : 0.f;
   }
   __syncthreads();
   VSTAMP(8);
   // ---------------- graph MLP, loss, head backward (vanilla_gnn.py:63-64, trainer.py:686-689)
-  if (tid < 128) {
+  // fc1: 8 lanes per output (4 inputs each), reduced by shuffles
+  {
+    const int o = tid >> 3, part = tid & 7;
     float acc = 0.f;
-    for (int n = 0; n < F; ++n) acc = fmaf(sg[n], w.g1w[tid * F + n], acc);
-    sh[tid] = relu_keepnan(acc + w.g1b[tid]);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int n = 4 * part + m;
+      const float wv = w.g1w[o * F + (n < F ? n : 0)];
+      if (n < F) acc = fmaf(sg[n], wv, acc);
+    }
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    acc += __shfl_xor(acc, 4, 64);
+    if (part == 0) sh[o] = relu_keepnan(acc + w.g1b[o]);
   }
   __syncthreads();
   for (int q = wave; q < OUT; q += NW) {
@@ -392,8 +564,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   }
   __syncthreads();
   if ((p.flags & DR_PASS_FORWARD) && tid < OUT) p.out[(int64_t)b * OUT + tid] = sdout[tid];
-  if (!(p.flags & DR_PASS_BACKWARD)) return;
-  __syncthreads();
+  if (!bwd) return;
   if (tid == 0) {
     if (p.loss_kind == DR_LOSS_MSE) {
       const float dl = sdout[0] - y_g;
@@ -421,14 +592,28 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   }
   __syncthreads();
   {
+    // dmean[n] = sum_o fc1.w[o][n] dh[o] / N: 32 partial sums of 4 outputs per
+    // column (partials in T), combined in order
+    const int n = tid & 31, part = tid >> 5;
+    float acc = 0.f;
+    float wv[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) wv[m] = w.g1w[(4 * part + m) * F + (n < F ? n : 0)];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) acc = fmaf(wv[m], sdh[4 * part + m], acc);
+    if (n >= F) acc = 0.f;
+    T[part * 32 + n] = acc;
+  }
+  __syncthreads();
+  {
     float* hg = p.head + (int64_t)b * DR_VANILLA_HEAD_STRIDE(F, OUT);
     const int XSH = r4(F), HD = XSH + 256 + r4(OUT);
-    if (tid < F) {
+    if (tid < 32) {
       float acc = 0.f;
-      for (int r = 0; r < 128; ++r) acc = fmaf(w.g1w[r * F + tid], sdh[r], acc);
+      for (int part = 0; part < 32; ++part) acc += T[part * 32 + tid];
       const float dm = acc / (float)N;  // scatter_mean backward: grad / count
-      sdm[tid] = dm;
-      hg[HD + tid] = dm;
+      sdm[tid] = tid < F ? dm : 0.f;
+      if (tid < F) hg[HD + tid] = dm;
     }
     if (tid < XSH) hg[tid] = tid < F ? sg[tid] : 0.f;
     if (tid < 128) {
@@ -441,131 +626,110 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   VSTAMP(9);
 
   // ---------------- layer 2 backward ---------------------------------------
-  // DU2 = relu'(X2) * dmean (one bit word per node).  dWn2 = DU2^T [X1 | S2],
-  // dbn2 = sum DU2 (extra column of ones).
+  // DU2 = relu'(X2) * dmean (bit words).  dWn2 = DU2^T [X1 | S2], dbn2 = sum DU2
+  // (a column of ones); dS2 = DU2 Wn2[:, F:] -> P.
   {
     float* gw = slab + LG;  // layer 2
     mm16(F, KN + 1, N, 0, [&](int n, int i) { return (i < N && ((xb[i] >> n) & 1u)) ? 1.f : 0.f; },
-         [&](int i, int q) { return i < N ? (q < F ? X1[i * LS + q] : (q < KN ? S[i * LS + q - F] : 1.f)) : 0.f; },
+         [&](int i, int q) { return i < N ? (q < F ? Q[i * LS + q] : (q < KN ? R[i * LS + q - F] : 1.f)) : 0.f; },
          [&](int n, int q, float v) {
            if (q < KN) gw[32 * KE + 32 + n * KN + q] = sdm[n] * v;
            else gw[32 * KE + 32 + F * KN + n] = sdm[n] * v;
          });
+    mm_w<1>(N, [&](int i, int n) { return ((xb[i] >> n) & 1u) ? sdm[n] : 0.f; },
+            [&](int n, int c) -> const float* { return n < F ? w.wn2 + n * KN + F + c : nullptr; }, [&](int) -> const float* { return nullptr; },
+            [&](int i, int c, float v, float) { P[i * LS + c] = v; });
   }
-  __syncthreads();
-  // [dX1 | dS2] = DU2 [Wn2[:, :F] | Wn2[:, F:]]  -> dX1 into S's region, dS2 into AB[:, :32]
-  mm16(N, 64, F, 0, [&](int i, int n) { return (n < F && ((xb[i] >> n) & 1u)) ? sdm[n] : 0.f; },
-       [&](int n, int q) { return n < F ? (q < F ? w.wn2[n * KN + q] : (q >= 32 ? w.wn2[n * KN + F + q - 32] : 0.f)) : 0.f; },
-       [&](int i, int q, float v) {
-         if (q < 32) {
-           if (q < F) S[i * LS + q] = v;
-         } else {
-           AB[i * LAB + q - 32] = v;
-         }
-       });
   __syncthreads();
   VSTAMP(10);
-  row_bwd(srp, AB, ea, Fe, FeS, b2c, red, N);
+  // D2 = dS2 * cnt2 -> R (S2 is dead), dbe2 / dWc2 partials in T
+  d_pass<FE>(P, R, cnt2, eap2, T, N);
+  wait_vm();  // bt2 and the transposed CSR have landed in U
   __syncthreads();
-  {
-    float* gw = slab + LG;
-    if (tid < 32 * (1 + MAXFE)) {  // dbe2, dWc2 (fixed wave order)
-      float t = 0.f;
-      for (int wv = 0; wv < NW; ++wv) t += red[wv * REDW + tid];
-      if (tid < 32) gw[32 * KE + tid] = t;
-      else {
-        const int c = (tid - 32) / MAXFE, f = (tid - 32) % MAXFE;
-        if (f < Fe) gw[c * KE + 2 * F + f] = t;
-      }
-    }
-    // dWa2 = D2^T X1,  dX1 += D2 Wa2
-    mm16(32, F, N, 0, [&](int c, int i) { return i < N ? AB[i * LAB + 32 + c] : 0.f; },
-         [&](int i, int k) { return i < N && k < F ? X1[i * LS + k] : 0.f; },
-         [&](int c, int k, float v) { gw[c * KE + k] = v; });
-    mm16(N, F, 32, 4, [&](int i, int c) { return c < 32 ? AB[i * LAB + 32 + c] : 0.f; },
-         [&](int c, int k) { return c < 32 && k < F ? w.we2[c * KE + k] : 0.f; },
-         [&](int i, int k, float v) { S[i * LS + k] += v; });
-  }
+  d_pass_sum<FE>(T, slab + LG, KE, F);
   __syncthreads();
   VSTAMP(11);
-  row_t(strp, stcol, AB, b2t, N);
-  __syncthreads();
-  {
-    float* gw = slab + LG;
-    // dWb2 = D'2^T X1,  dX1 += D'2 Wb2
-    mm16(32, F, N, 0, [&](int c, int i) { return i < N ? AB[i * LAB + 32 + c] : 0.f; },
-         [&](int i, int k) { return i < N && k < F ? X1[i * LS + k] : 0.f; },
-         [&](int c, int k, float v) { gw[c * KE + F + k] = v; });
-    mm16(N, F, 32, 4, [&](int i, int c) { return c < 32 ? AB[i * LAB + 32 + c] : 0.f; },
-         [&](int c, int k) { return c < 32 && k < F ? w.we2[c * KE + F + k] : 0.f; },
-         [&](int i, int k, float v) { S[i * LS + k] += v; });
-  }
+  row_t(strp, stcol, bt, P, T, N);  // D'2 -> T
   __syncthreads();
   VSTAMP(12);
-  // ---------------- layer 1 backward ---------------------------------------
-  // DU1 = relu'(X1) * dX1 (in place)
-  for (int q = tid; q < N * 32; q += NT) {
-    const int i = q >> 5, n = q & 31;
-    if (n < F) S[i * LS + n] = relu_bwd(X1[i * LS + n], S[i * LS + n]);
+  {
+    float* gw = slab + LG;
+    // dWa2 = D2^T X1,  dWb2 = D'2^T X1
+    mm16(32, F, N, 0, [&](int c, int i) { return i < N ? R[i * LS + c] : 0.f; },
+         [&](int i, int k) { return i < N && k < F ? Q[i * LS + k] : 0.f; },
+         [&](int c, int k, float v) { gw[c * KE + k] = v; });
+    mm16(32, F, N, 4, [&](int c, int i) { return i < N ? T[i * LS + c] : 0.f; },
+         [&](int i, int k) { return i < N && k < F ? Q[i * LS + k] : 0.f; },
+         [&](int c, int k, float v) { gw[c * KE + F + k] = v; });
+    // dX1 = [DU2 | D2 | D'2] [Wn2[:, :F]; Wa2; Wb2], DU1 = relu'(X1) * dX1 -> P
+    mm_w<3>(N,
+            [&](int i, int k) {
+              return k < 32 ? (((xb[i] >> k) & 1u) ? sdm[k] : 0.f) : (k < 64 ? R[i * LS + k - 32] : T[i * LS + k - 64]);
+            },
+            [&](int k, int n) -> const float* {
+              return n < F ? (k < 32 ? (k < F ? w.wn2 + k * KN + n : nullptr)
+                                     : (k < 64 ? w.we2 + (k - 32) * KE + n : w.we2 + (k - 64) * KE + F + n))
+                           : nullptr;
+            },
+            [&](int) -> const float* { return nullptr; },
+            [&](int i, int n, float v, float) { P[i * LS + n] = n < F ? relu_bwd(Q[i * LS + n], v) : 0.f; });
   }
   __syncthreads();
+  VSTAMP(13);
+  // ---------------- layer 1 backward ---------------------------------------
+  // X0 (HBM row stride XS) -> Q, S1 -> R (stride 32), layer-1 ReLU words -> U:
+  // bulk DMA, landing while dS1 = DU1 Wn1[:, F:] -> T runs
+  dma_x4<NT>(Q, X0, N * XS / 4);
+  dma_x4<NT>(R, S1g, N * 8);
+  dma_words<NT>(bt, bt1g, E);
+  mm_w<1>(N, [&](int i, int n) { return P[i * LS + n]; },
+          [&](int n, int c) -> const float* { return n < F ? w.wn1 + n * KN + F + c : nullptr; }, [&](int) -> const float* { return nullptr; },
+          [&](int i, int c, float v, float) { T[i * LS + c] = v; });
+  wait_vm();
+  __syncthreads();
+  VSTAMP(14);
   {
     float* gw = slab;  // layer 1
-    // dS1 = DU1 Wn1[:, F:] into AB[:, :32];  dWn1 = DU1^T [X0 | S1], dbn1 = sum DU1
-    mm16(N, 32, F, 0, [&](int i, int n) { return n < F ? S[i * LS + n] : 0.f; },
-         [&](int n, int c) { return n < F ? w.wn1[n * KN + F + c] : 0.f; },
-         [&](int i, int c, float v) { AB[i * LAB + c] = v; });
-    mm16(F, KN + 1, N, 8, [&](int n, int i) { return i < N ? S[i * LS + n] : 0.f; },
-         [&](int i, int q) {
-           return i < N ? (q < F ? X0[(int64_t)i * XS + q] : (q < KN ? S1g[i * 32 + q - F] : 1.f)) : 0.f;
-         },
+    // dWn1 = DU1^T [X0 | S1], dbn1 = sum DU1
+    mm16(F, KN + 1, N, 0, [&](int n, int i) { return i < N ? P[i * LS + n] : 0.f; },
+         [&](int i, int q) { return i < N ? (q < F ? Q[i * XS + q] : (q < KN ? R[i * 32 + q - F] : 1.f)) : 0.f; },
          [&](int n, int q, float v) {
            if (q < KN) gw[32 * KE + 32 + n * KN + q] = v;
            else gw[32 * KE + 32 + F * KN + n] = v;
          });
   }
   __syncthreads();
-  VSTAMP(13);
-  row_bwd(srp, AB, ea, Fe, FeS, b1c, red, N);
+  VSTAMP(15);
+  // D1 = dS1 * cnt1 -> R (S1 is dead), partials in P (DU1 is dead)
+  d_pass<FE>(T, R, cnt1, eap1, P, N);
   __syncthreads();
+  d_pass_sum<FE>(P, slab, KE, F);
+  __syncthreads();
+  VSTAMP(16);
+  row_t(strp, stcol, bt, T, P, N);  // D'1 -> P
+  __syncthreads();
+  VSTAMP(17);
   {
     float* gw = slab;
-    if (tid < 32 * (1 + MAXFE)) {
-      float t = 0.f;
-      for (int wv = 0; wv < NW; ++wv) t += red[wv * REDW + tid];
-      if (tid < 32) gw[32 * KE + tid] = t;
-      else {
-        const int c = (tid - 32) / MAXFE, f = (tid - 32) % MAXFE;
-        if (f < Fe) gw[c * KE + 2 * F + f] = t;
-      }
-    }
-    // dWa1 = D1^T X0
-    mm16(32, F, N, 0, [&](int c, int i) { return i < N ? AB[i * LAB + 32 + c] : 0.f; },
-         [&](int i, int k) { return i < N && k < F ? X0[(int64_t)i * XS + k] : 0.f; },
+    // dWa1 = D1^T X0,  dWb1 = D'1^T X0
+    mm16(32, F, N, 0, [&](int c, int i) { return i < N ? R[i * LS + c] : 0.f; },
+         [&](int i, int k) { return i < N && k < F ? Q[i * XS + k] : 0.f; },
          [&](int c, int k, float v) { gw[c * KE + k] = v; });
-  }
-  __syncthreads();
-  VSTAMP(14);
-  row_t(strp, stcol, AB, b1t, N);
-  __syncthreads();
-  {
-    float* gw = slab;
-    // dWb1 = D'1^T X0
-    mm16(32, F, N, 0, [&](int c, int i) { return i < N ? AB[i * LAB + 32 + c] : 0.f; },
-         [&](int i, int k) { return i < N && k < F ? X0[(int64_t)i * XS + k] : 0.f; },
+    mm16(32, F, N, 4, [&](int c, int i) { return i < N ? P[i * LS + c] : 0.f; },
+         [&](int i, int k) { return i < N && k < F ? Q[i * XS + k] : 0.f; },
          [&](int c, int k, float v) { gw[c * KE + F + k] = v; });
   }
-  VSTAMP(15);
+  VSTAMP(18);
 }
 
 }  // namespace
 
-extern "C" int64_t dr_vanilla_fused_lds_bytes(int32_t n_nodes, int32_t n_edges) {
-  return 4LL * vcarve(n_nodes, n_edges).total;
+extern "C" int64_t dr_vanilla_fused_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_edge_feat) {
+  return 4LL * vcarve(n_nodes, n_edges, n_edge_feat).total;
 }
 
-extern "C" int64_t dr_vanilla_fused_scratch_floats(int32_t n_nodes, int32_t n_edges) {
-  return vscratch_floats(n_nodes, n_edges);
+extern "C" int64_t dr_vanilla_fused_scratch_floats(int32_t n_nodes, int32_t n_edges, int32_t n_edge_feat) {
+  return vscratch_floats(n_nodes, n_edges, n_edge_feat);
 }
 
 extern "C" int dr_vanilla_fused_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
@@ -584,7 +748,15 @@ extern "C" int dr_vanilla_fused_pass(const dr_graph_store* store, const dr_graph
   if ((pass->flags & DR_PASS_FORWARD) && !pass->out) return DR_E_ARG;
   if (pass->use_dropout != DR_DROPOUT_OFF) return DR_E_UNSUPPORTED;
   if (n_batch == 0) return DR_OK;
-  DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&vanilla_graph_kernel)));
+  const void* fn = nullptr;
+  switch (store->n_edge_feat) {
+    case 0: fn = reinterpret_cast<const void*>(&vanilla_graph_kernel<0>); break;
+    case 1: fn = reinterpret_cast<const void*>(&vanilla_graph_kernel<1>); break;
+    case 2: fn = reinterpret_cast<const void*>(&vanilla_graph_kernel<2>); break;
+    case 3: fn = reinterpret_cast<const void*>(&vanilla_graph_kernel<3>); break;
+    default: fn = reinterpret_cast<const void*>(&vanilla_graph_kernel<4>); break;
+  }
+  DR_CHECK(dr_allow_big_lds(fn));
   VGArgs a;
   a.s = *store;
   a.w = *w;
@@ -593,6 +765,12 @@ extern "C" int dr_vanilla_fused_pass(const dr_graph_store* store, const dr_graph
   a.scr = scratch;
   a.scr_off = scratch_off;
   a.B = n_batch;
-  hipLaunchKernelGGL(vanilla_graph_kernel, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, a);
+  switch (store->n_edge_feat) {
+    case 0: hipLaunchKernelGGL(vanilla_graph_kernel<0>, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, a); break;
+    case 1: hipLaunchKernelGGL(vanilla_graph_kernel<1>, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, a); break;
+    case 2: hipLaunchKernelGGL(vanilla_graph_kernel<2>, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, a); break;
+    case 3: hipLaunchKernelGGL(vanilla_graph_kernel<3>, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, a); break;
+    default: hipLaunchKernelGGL(vanilla_graph_kernel<4>, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, a); break;
+  }
   return (int)hipGetLastError();
 }

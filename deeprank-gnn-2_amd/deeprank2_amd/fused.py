@@ -77,14 +77,14 @@ class BatchHandle:
         return sc
 
     def vanilla_fused_scratch(self):
-        """Per-graph global scratch of dr_vanilla_fused_pass (S1, edge ReLU bit
-        words, transposed slot map) and each slot's float offset into it."""
+        """Per-graph global scratch of dr_vanilla_fused_pass (S1, per-(node,
+        channel) active-edge counts and edge-attribute sums of both layers, the
+        transposed edge ReLU words) and each slot's float offset into it."""
         sc = self._lds.get("vanilla_fused_scratch")
         if sc is None:
             idx = self.gids_host.astype(np.int64)
             n, e = self.store._sizes[0][idx], self.store._sizes[1][idx]  # noqa: SLF001
-            r4 = lambda v: (v + 3) & ~3  # noqa: E731
-            per = r4(n * 32) + 5 * r4(e)  # dr_vanilla_fused_scratch_floats
+            per = vanilla_fused_scratch_floats(n, e, self.store.n_edge_feat)
             off = np.concatenate([[0], np.cumsum(per)]).astype(np.int64)
             dev = self.store.device
             buf = torch.empty(max(1, int(off[-1])), dtype=torch.float32, device=dev)
@@ -240,6 +240,14 @@ class FusedSpec:
     dropout: float = 0.0
     large: Callable | None = None  # (handle, weights struct, pass struct) for graphs beyond one workgroup's LDS
     run: Callable | None = None  # (handle, weights struct, pass struct): replaces the default entry call
+
+
+def vanilla_fused_scratch_floats(n, e, fe):
+    """Mirror of dr_vanilla_fused_scratch_floats (vanilla_graph.hip), vectorised
+    over graphs: S1, cnt1, cnt2 (32N each), eap1, eap2 (32N*Fe each), two ReLU
+    word arrays (E + 1 each), every part rounded up to 16 bytes."""
+    r4 = lambda v: (np.asarray(v, dtype=np.int64) + 3) & ~3  # noqa: E731
+    return (3 + 2 * fe) * r4(32 * np.asarray(n, dtype=np.int64)) + 2 * r4(np.asarray(e, dtype=np.int64) + 1)
 
 
 def make_pass(out_dim, flags, *, dropout: Dropout | None = None, dout=None, loss_kind=_lib.DR_LOSS_NONE, loss_scale=1.0, class_w=None, out=None, loss_per_graph=None, slab=None, head=None, stamps=None, step_counter=None):

@@ -125,7 +125,7 @@ def make_spec(f, fe):
         lib = _lib.load()
         if fused_fits(h, f, fe):  # one workgroup per graph, graph in LDS
             buf, offs = h.vanilla_fused_scratch()
-            lds = h.lds("vanilla_fused", lambda n, e, *_: lib.dr_vanilla_fused_lds_bytes(n, e))
+            lds = h.lds(("vanilla_fused", fe), lambda n, e, *_: lib.dr_vanilla_fused_lds_bytes(n, e, fe))
             _lib.check(lib.dr_vanilla_fused_pass(st.cstruct(), h.descs.data_ptr(), h.B, w, p, buf.data_ptr(), offs.data_ptr(), lds, _lib.stream_ptr(st.device)), "dr_vanilla_fused_pass")
             return
         sc, _keep = h.vanilla_scratch(f, fe)
@@ -146,7 +146,7 @@ def fused_fits(h: BatchHandle, f, fe):
     if getattr(h, "vanilla_pipeline", False) or f > 32 or fe > FUSED_MAX_FE:  # noqa: PLR2004
         return False
     lib = _lib.load()
-    return h.lds("vanilla_fused", lambda n, e, *_: lib.dr_vanilla_fused_lds_bytes(n, e)) <= LDS_MAX
+    return h.lds(("vanilla_fused", fe), lambda n, e, *_: lib.dr_vanilla_fused_lds_bytes(n, e, fe)) <= LDS_MAX
 
 
 def graph_pass(model, h: BatchHandle, params, out_dim, flags, **kw):

@@ -349,8 +349,8 @@ int64_t dr_vanilla_lds_bytes(int32_t n_feat, int32_t n_edge_feat, int32_t out_di
 int dr_vanilla_fused_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
                           const dr_vanilla_weights* w, const dr_pass* pass, float* scratch,
                           const int64_t* scratch_off, int32_t lds_bytes, void* stream);
-int64_t dr_vanilla_fused_lds_bytes(int32_t n_nodes, int32_t n_edges);
-int64_t dr_vanilla_fused_scratch_floats(int32_t n_nodes, int32_t n_edges);
+int64_t dr_vanilla_fused_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_edge_feat);
+int64_t dr_vanilla_fused_scratch_floats(int32_t n_nodes, int32_t n_edges, int32_t n_edge_feat);
 
 /* Adam (torch.optim.Adam, L2 weight decay added to the gradient) settings.  */
 typedef struct dr_adam {
