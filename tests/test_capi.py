@@ -60,3 +60,19 @@ def test_dropout_hash_host_replica_statistics():
     other = _lib.dropout_keep_host(1234, 8, 128 * 512, 0.4)
     assert (keep == again).all()
     assert (keep != other).mean() > 0.3
+
+
+def test_vanilla_fused_sizes_host_mirror():
+    """The host's per-graph scratch sizing (fused.vanilla_fused_scratch_floats)
+    equals the library's, and residue graphs of SURVEY §8(d) up to N=220,
+    E=3606 fit one workgroup's 160 KiB of LDS for Fe <= 3."""
+    import numpy as np  # noqa: PLC0415
+
+    from deeprank2_amd.fused import vanilla_fused_scratch_floats  # noqa: PLC0415
+
+    lib = _lib.load()
+    for n, e, fe in [(1, 0, 0), (1, 1, 1), (33, 190, 2), (200, 3000, 3), (220, 3606, 4), (57, 342, 2)]:
+        assert int(vanilla_fused_scratch_floats(np.array([n]), np.array([e]), fe)[0]) == lib.dr_vanilla_fused_scratch_floats(n, e, fe)
+        assert lib.dr_vanilla_fused_lds_bytes(n, e, fe) % 16 == 0
+    for fe in (1, 2, 3):
+        assert lib.dr_vanilla_fused_lds_bytes(220, 3606, fe) <= 160 * 1024

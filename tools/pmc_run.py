@@ -1,6 +1,6 @@
 """Workload for rocprofv3 --pmc passes: eager GINet training steps (config 2).
 
-    rocprofv3 --pmc <counters> -f csv -d <dir> -- python3 tools/pmc_run.py [steps]
+    rocprofv3 --pmc <counters> -f csv -d <dir> -- python3 tools/pmc_run.py [steps] [ginet|vanilla]
 """
 
 from __future__ import annotations
@@ -17,6 +17,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "deeprank-gnn-2_amd")]
 from bench import records  # noqa: E402
 from deeprank2_amd.engine import GINetTrainStep  # noqa: E402
 from deeprank2_amd.neuralnets.gnn.ginet import BatchHandle, GINet  # noqa: E402
+from deeprank2_amd.neuralnets.gnn.vanilla_gnn import VanillaNetwork  # noqa: E402
 from deeprank2_amd.store import GraphStore, pack_graphs  # noqa: E402
 from deeprank2_amd.utils.synthetic import make_dataset  # noqa: E402
 
@@ -29,12 +30,13 @@ def main():
     order = np.random.default_rng(0).permutation(packed.n_graphs).astype(np.int32)
     hs = [BatchHandle(store, order[i * 64:(i + 1) * 64]) for i in range(16)]
     torch.manual_seed(1234)
-    model = GINet(30, 1, 3).to(dev).train()
+    which = sys.argv[2] if len(sys.argv) > 2 else "ginet"
+    model = (VanillaNetwork if which == "vanilla" else GINet)(30, 1, 3).to(dev).train()
     step = GINetTrainStep(model)
     for i in range(steps):
         step.step(hs[i % 16])
     torch.cuda.synchronize()
-    print("alg_bytes_per_launch", np.mean([__import__("bench").algorithmic_bytes(packed, h.gids_host) for h in hs]))
+    print("alg_bytes_per_launch", np.mean([__import__("bench").algorithmic_bytes(packed, h.gids_host, which) for h in hs]))
 
 
 if __name__ == "__main__":
