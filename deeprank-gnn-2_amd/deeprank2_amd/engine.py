@@ -257,7 +257,7 @@ class FusedTrainStep:
         self.step_count = n
         return ms
 
-    def capture(self, h: BatchHandle, global_batch=None):
+    def capture(self, h: BatchHandle, global_batch=None, dropout=True):
         """Capture one training step on ``h`` into a HIP graph (``torch.cuda.CUDAGraph``).
 
         Replaying it runs the same launches (plus the all-reduce for N>1) with
@@ -267,11 +267,11 @@ class FusedTrainStep:
         self._ensure(h.B)
         snap = [t.detach().clone() for t in self._state_tensors()]
         n = self.step_count
-        self.step(h, global_batch=global_batch)  # warm-up: LDS attribute, allocator
+        self.step(h, global_batch=global_batch, dropout=dropout)  # warm-up: LDS attribute, allocator
         torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self.step(h, global_batch=global_batch)
+            self.step(h, global_batch=global_batch, dropout=dropout)
         torch.cuda.synchronize(self.device)
         for t, s in zip(self._state_tensors(), snap):
             t.data.copy_(s)

@@ -3,7 +3,10 @@
 Launched as a child process per rank (RANK / WORLD_SIZE / MASTER_* in the
 environment); every rank uses the same GPU over the gloo backend, so the test
 fits a one-GPU box while exercising FusedTrainStep's sharded step and its
-single all-reduce.  Writes the final parameters (rank 0)."""
+single all-reduce.  DR_DDP_PG=nccl runs one rank over RCCL instead (the
+bench's N>1 launch path on one GPU) and DR_DDP_CAPTURE=1 replays every step
+from a captured HIP graph (all-reduce included).  Writes the final parameters
+(rank 0)."""
 
 from __future__ import annotations
 
@@ -33,9 +36,15 @@ B, STEPS = 24, 3
 def run(model_name, world, rank, out_path):
     dev = torch.device("cuda:0")
     pg = None
-    if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+    backend = os.environ.get("DR_DDP_PG", "gloo")
+    if world > 1 or backend == "nccl":
+        if backend == "nccl":
+            torch.cuda.set_device(dev)
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
         pg = dist.group.WORLD
+    capture = os.environ.get("DR_DDP_CAPTURE") == "1"
     datas = [data_ref.synthetic_to_data(g, f"s{i}") for i, g in enumerate(make_dataset(2 * B, seed=17, n_lo=30, n_hi=80, mean_degree=9.0))]
     store = GraphStore(pack_graphs(records_from_batch(P.Batch.from_data_list(datas))), dev)
     torch.manual_seed(42)
@@ -45,7 +54,12 @@ def run(model_name, world, rank, out_path):
     for s in range(STEPS):
         gids = np.arange(B) + (s % 2) * B  # global batch, global order
         h = BatchHandle(store, shard_contiguous(gids, rank, world))
-        loss, _ = step.step(h, global_batch=B, dropout=False)
+        if capture:
+            g = step.capture(h, global_batch=B, dropout=False)
+            g.replay()
+            loss = step.loss_out
+        else:
+            loss, _ = step.step(h, global_batch=B, dropout=False)
         losses.append(float(loss))
     torch.cuda.synchronize()
     if rank == 0:

@@ -22,11 +22,11 @@ def _port():
         return s.getsockname()[1]
 
 
-def _launch(model_name, world, out):
+def _launch(model_name, world, out, **extra_env):
     port = _port()
     procs = []
     for r in range(world):
-        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OMP_NUM_THREADS="2")
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OMP_NUM_THREADS="2", **extra_env)
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "ddp_worker.py"), model_name, out], env=env))
     rcs = []
     for p in procs:
@@ -53,3 +53,19 @@ def test_two_ranks_match_single_process(tmp_path, model_name):
         if k.startswith("p"):
             np.testing.assert_allclose(b[k], a[k], rtol=0, atol=3e-3, err_msg=k)
             assert np.mean(np.abs(b[k] - a[k]) < 1e-6) > 0.95, k
+
+
+def test_rccl_captured_ddp_step_matches_plain_step(tmp_path):
+    """bench.py's N>1 launch path on one GPU: a one-rank RCCL process group,
+    every step replayed from a captured HIP graph holding the graph pass, the
+    gradient reduce, the RCCL all-reduce and Adam — the same losses and
+    parameters as the plain single-process step."""
+    one, cap = str(tmp_path / "plain.npz"), str(tmp_path / "rccl.npz")
+    _launch("ginet", 1, one)
+    _launch("ginet", 1, cap, DR_DDP_PG="nccl", DR_DDP_CAPTURE="1")
+    a, b = np.load(one), np.load(cap)
+    np.testing.assert_allclose(b["loss"], a["loss"], rtol=1e-6)
+    np.testing.assert_allclose(b["grad"], a["grad"], rtol=1e-6, atol=1e-9)
+    for k in a.files:
+        if k.startswith("p"):
+            np.testing.assert_allclose(b[k], a[k], rtol=1e-6, atol=1e-8, err_msg=k)
