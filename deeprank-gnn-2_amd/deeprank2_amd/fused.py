@@ -37,6 +37,7 @@ class BatchHandle:
         self.large_tile = None  # nodes per tile of the split path (default 128)
         self.large_halos = True  # stage each tile's neighbour rows in LDS (False: per-edge HBM gather)
         self.large_atomic_max = True  # depth-0 max over tiles by 64-bit atomic max (False: per-tile partials)
+        self.force_layers = False  # run the layer-level path (layered.py) even when the graph pass fits (diagnostic)
 
     def lds(self, key, fn):
         """Dynamic LDS bytes for the largest graph of the batch (cached per model kind)."""
@@ -240,6 +241,7 @@ class FusedSpec:
     dropout: float = 0.0
     large: Callable | None = None  # (handle, weights struct, pass struct) for graphs beyond one workgroup's LDS
     run: Callable | None = None  # (handle, weights struct, pass struct): replaces the default entry call
+    layers: Callable | None = None  # (model, batch tensors, training) -> out: layer-level path (layered.py) for batches beyond LDS
 
 
 def vanilla_fused_scratch_floats(n, e, fe):

@@ -1,0 +1,144 @@
+"""Layer-level execution of FoutNet, SGAT and ``ginet_nocluster.GINet`` for
+batches their per-graph kernels cannot hold (a graph beyond one workgroup's
+160 KiB of LDS, e.g. atom-level graphs).  GINet and VanillaNetwork have
+split large-graph kernels of their own and never come here.
+
+The forward mirrors the reference line by line on the layer API — FoutLayer /
+SGraphAttentionLayer / GINetConvLayer on the CSR and linear HIP kernels,
+``get_preloaded_cluster`` / ``community_pooling`` / ``max_pool_x`` on the
+segment kernels (``deeprank2_amd.utils.community_pooling``), ``nn.Linear`` on
+rocBLAS — and torch autograd differentiates it:
+  * FoutNet.forward          deeprank2/neuralnets/gnn/foutnet.py:99-118
+  * SGAT.forward             deeprank2/neuralnets/gnn/sgat.py:113-133
+  * ginet_nocluster.GINet    deeprank2/neuralnets/gnn/ginet_nocluster.py:84-111
+The batch tensors come from the HBM store the batch handle points into
+(``batch_tensors``), in the reference's edge order (the store's CSR slot map
+``eperm``), so each scatter sums in the same order as the reference.
+"""
+
+from __future__ import annotations
+
+from types import SimpleNamespace
+
+import numpy as np
+import torch
+from torch.nn.functional import dropout, relu
+
+from deeprank2_amd.data import Data
+from deeprank2_amd.fused import LDS_MAX, BatchHandle, FusedSpec, lds_for
+from deeprank2_amd.utils.community_pooling import community_pooling, get_preloaded_cluster, max_pool_x
+
+
+def needs_layers(spec: FusedSpec, h: BatchHandle, out_dim) -> bool:
+    """True when ``spec``'s graph pass cannot run this batch: no split
+    large-graph path and the largest graph exceeds one workgroup's LDS (or the
+    handle asks for the layer path: ``h.force_layers``, a diagnostic)."""
+    if getattr(h, "force_layers", False):
+        return True
+    if spec.run is not None or spec.large is not None or spec.layers is None:
+        return False
+    return lds_for(spec, h, out_dim) > LDS_MAX
+
+
+def batch_tensors(h: BatchHandle):
+    """The batch as the reference's collated ``Batch`` holds it (x, edge_index
+    in the original edge order, edge_attr, batch vector, cluster0 / cluster1 as
+    dense per-graph ids, y), on the store's device; built once per handle."""
+    t = h._lds.get("layer_tensors")  # noqa: SLF001
+    if t is not None:
+        return t
+    p = h.store.packed
+    xs, eis, eas, bs, c0s, c1s = [], [], [], [], [], []
+    base = 0
+    for slot, gid in enumerate(h.gids_host.astype(np.int64)):
+        n0, n1 = int(p.node_off[gid]), int(p.node_off[gid + 1])
+        e0, e1 = int(p.edge_off[gid]), int(p.edge_off[gid + 1])
+        n, e = n1 - n0, e1 - e0
+        rp = p.rowptr[n0 + gid : n1 + gid + 1].astype(np.int64)
+        rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(rp))
+        cols = p.col[e0:e1].astype(np.int64)
+        pos = p.eperm[e0:e1].astype(np.int64)  # CSR slot -> original edge position
+        ei = np.empty((2, e), np.int64)
+        ei[0, pos], ei[1, pos] = rows, cols
+        eis.append(ei + base)
+        if p.edge_attr is not None:
+            ea = np.empty_like(p.edge_attr[e0:e1])
+            ea[pos] = p.edge_attr[e0:e1]
+            eas.append(ea)
+        xs.append(p.x[n0:n1])
+        bs.append(np.full(n, slot, np.int64))
+        c0s.append(p.cl0[n0:n1].astype(np.int64))
+        c1s.append(p.cl1[int(p.k0_off[gid]) : int(p.k0_off[gid + 1])].astype(np.int64))
+        base += n
+    dev = h.store.device
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    t = SimpleNamespace(
+        x=d(np.concatenate(xs)),
+        edge_index=d(np.concatenate(eis, axis=1)),
+        edge_attr=d(np.concatenate(eas)) if eas else None,
+        batch=d(np.concatenate(bs)),
+        cluster0=d(np.concatenate(c0s)),
+        cluster1=d(np.concatenate(c1s)),
+        y=d(p.y[h.gids_host.astype(np.int64)]),
+        n_graphs=h.B,
+    )
+    h._lds["layer_tensors"] = t  # noqa: SLF001
+    return t
+
+
+def scatter_mean(x, batch, n_seg):
+    """torch_scatter.scatter_mean over graphs (count clamped at 1), differentiable."""
+    s = torch.zeros(n_seg, x.shape[1], dtype=x.dtype, device=x.device).index_add(0, batch, x)
+    cnt = torch.zeros(n_seg, dtype=x.dtype, device=x.device).index_add(0, batch, torch.ones_like(batch, dtype=x.dtype))
+    return s / cnt.clamp_min(1).unsqueeze(1)
+
+
+def _pooled_head(model, data, with_edge_attr):
+    """conv2 block, depth-1 max_pool_x, per-graph mean and the MLP head
+    (foutnet.py:107-118, sgat.py:123-133)."""
+    if with_edge_attr:
+        x = relu(model.conv2(data.x, data.edge_index, data.edge_attr))
+    else:
+        x = relu(model.conv2(data.x, data.edge_index))
+    cluster = get_preloaded_cluster(data.cluster1.clone(), data.batch)
+    x, batch = max_pool_x(cluster, x, data.batch)
+    x = scatter_mean(x, batch, data.n_graphs)
+    x = relu(model.fc1(x))
+    return model.fc2(x)
+
+
+def _pooled_input(t, x):
+    d = Data(x=x, edge_index=t.edge_index, edge_attr=t.edge_attr, batch=t.batch, pos=None)
+    d.cluster0, d.cluster1 = t.cluster0, t.cluster1
+    return d
+
+
+def foutnet_forward(model, t, training=False):  # noqa: ARG001
+    """foutnet.py:99-118."""
+    x = relu(model.conv1(t.x, t.edge_index))
+    cluster = get_preloaded_cluster(t.cluster0.clone(), t.batch)
+    data = community_pooling(cluster, _pooled_input(t, x))
+    data.n_graphs = t.n_graphs
+    return _pooled_head(model, data, with_edge_attr=False)
+
+
+def sgat_forward(model, t, training=False):  # noqa: ARG001
+    """sgat.py:113-133 (pooled edge_attr = PyG coalesce sums, as community_pooling gives)."""
+    x = relu(model.conv1(t.x, t.edge_index, t.edge_attr))
+    cluster = get_preloaded_cluster(t.cluster0.clone(), t.batch)
+    data = community_pooling(cluster, _pooled_input(t, x))
+    data.n_graphs = t.n_graphs
+    return _pooled_head(model, data, with_edge_attr=True)
+
+
+def ginet_nocluster_forward(model, t, training=False):
+    """ginet_nocluster.py:84-111 (dropout from torch's RNG on this path)."""
+    ea = t.edge_attr
+    x = relu(model.conv1(t.x, t.edge_index, ea))
+    x = relu(model.conv2(x, t.edge_index, ea))
+    x_ext = relu(model.conv1_ext(t.x, t.edge_index, ea))
+    x_ext = relu(model.conv2_ext(x_ext, t.edge_index, ea))
+    g = torch.cat([scatter_mean(x, t.batch, t.n_graphs), scatter_mean(x_ext, t.batch, t.n_graphs)], dim=1)
+    g = relu(model.fc1(g))
+    g = dropout(g, model.dropout, training=training)
+    return model.fc2(g)

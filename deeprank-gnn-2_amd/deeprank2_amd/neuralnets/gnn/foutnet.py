@@ -25,7 +25,7 @@ import math
 import torch
 from torch import nn
 
-from deeprank2_amd import _lib, ops
+from deeprank2_amd import _lib, layered, ops
 from deeprank2_amd.fused import BatchHandle, FusedFn, FusedSpec, make_pass, resolve_batch, run_pass
 
 
@@ -142,7 +142,7 @@ def _lds(n, e, k0, p1, k1, f, alias, out):
     return _lib.load().dr_fout_lds_bytes(n, e, f, k0, p1, k1, alias, out)
 
 
-SPEC = FusedSpec(PARAM_NAMES, recipe, slab_stride, head_stride, "dr_fout_graph_pass", weights_c, _lds, dropout=0.0)
+SPEC = FusedSpec(PARAM_NAMES, recipe, slab_stride, head_stride, "dr_fout_graph_pass", weights_c, _lds, dropout=0.0, layers=layered.foutnet_forward)
 
 
 def graph_pass(h: BatchHandle, params, out_dim, flags, **kw):
@@ -180,4 +180,6 @@ class FoutNet(nn.Module):
         if h.store.n_feat != self.input_shape:
             msg = f"batch has {h.store.n_feat} node features, model expects {self.input_shape}"
             raise ValueError(msg)
+        if layered.needs_layers(SPEC, h, self.output_shape):  # a graph beyond one workgroup's LDS
+            return SPEC.layers(self, layered.batch_tensors(h), self.training)
         return FusedFn.apply(SPEC, h, None, self.output_shape, *params)

@@ -26,7 +26,7 @@ import math
 import torch
 from torch import nn
 
-from deeprank2_amd import _lib, ops
+from deeprank2_amd import _lib, layered, ops
 from deeprank2_amd.fused import BatchHandle, FusedFn, FusedSpec, make_pass, resolve_batch, run_pass
 from deeprank2_amd.neuralnets.gnn import foutnet
 
@@ -158,7 +158,7 @@ def _lds(n, e, k0, p1, k1, f, alias, out):
     return _lib.load().dr_sgat_lds_bytes(n, e, f, k0, p1, k1, alias, out)
 
 
-SPEC = FusedSpec(PARAM_NAMES, recipe, foutnet.slab_stride, foutnet.head_stride, "dr_sgat_graph_pass", weights_c, _lds, dropout=0.0)
+SPEC = FusedSpec(PARAM_NAMES, recipe, foutnet.slab_stride, foutnet.head_stride, "dr_sgat_graph_pass", weights_c, _lds, dropout=0.0, layers=layered.sgat_forward)
 
 
 def graph_pass(h: BatchHandle, params, out_dim, flags, **kw):
@@ -199,4 +199,6 @@ class SGAT(nn.Module):
         if h.store.n_edge_feat != 1:
             msg = f"SGAT needs exactly one edge feature (got {h.store.n_edge_feat}): sgat.py:71 multiplies edge_attr into every channel"
             raise ValueError(msg)
+        if layered.needs_layers(SPEC, h, self.output_shape):  # a graph beyond one workgroup's LDS
+            return SPEC.layers(self, layered.batch_tensors(h), self.training)
         return FusedFn.apply(SPEC, h, None, self.output_shape, *params)

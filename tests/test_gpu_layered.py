@@ -1,0 +1,116 @@
+"""GPU parity of the layer-level path (deeprank2_amd/layered.py) that FoutNet,
+SGAT and ginet_nocluster.GINet take for batches their per-graph kernels
+cannot hold: against the CPU oracle (oracle/gnn_ref.py, the op-for-op
+restatement of the reference networks), against the fused kernels on batches
+both can run (``h.force_layers``), and through the fused training step
+(autograd gradients -> the same Adam kernel).  Tolerance: 1e-4 (north_star,
+fp32) with the normwise gradient floor of tests/_util.py."""
+
+from __future__ import annotations
+
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+from _util import assert_grad_close
+
+from deeprank2_amd import layered
+from deeprank2_amd.engine import FusedTrainStep
+from deeprank2_amd.fused import BatchHandle
+from deeprank2_amd.neuralnets.gnn import foutnet, ginet_nocluster, sgat
+from deeprank2_amd.store import GraphStore, pack_graphs, records_from_batch
+from deeprank2_amd.utils.synthetic import make_dataset
+from oracle import data_ref, gnn_ref
+from oracle import pyg_ops as P
+
+pytestmark = pytest.mark.gpu
+TOL = dict(rtol=1e-4, atol=1e-4)
+DEV = "cuda:0"
+
+
+def _datas(n, seed, fe=3, **kw):
+    out = []
+    for i, g in enumerate(make_dataset(n, seed=seed, **kw)):
+        d = data_ref.synthetic_to_data(g, f"l{i}")
+        d.edge_attr = d.edge_attr[:, :fe].contiguous()
+        out.append(d)
+    return out
+
+
+def _handle(datas, force=False, clusters=True):
+    store = GraphStore(pack_graphs(records_from_batch(P.Batch.from_data_list(datas)), require_clusters=clusters), DEV)
+    h = BatchHandle(store, np.arange(len(datas), dtype=np.int32))
+    h.force_layers = force
+    return h
+
+
+def _oracle_grads(model_o, datas):
+    bat = P.Batch.from_data_list([d.clone() for d in datas])
+    out = model_o(bat)
+    loss = torch.nn.functional.mse_loss(out.reshape(-1), bat.y)
+    loss.backward()
+    return out.detach(), loss.detach(), {n: p.grad.numpy() for n, p in model_o.named_parameters()}
+
+
+@pytest.mark.parametrize("name", ["foutnet", "sgat", "ginet_nocluster"])
+def test_graph_beyond_lds_runs_layers_and_matches_oracle(name):
+    """Two ~1.1k-node graphs (too big for one workgroup's LDS): forward,
+    MSE loss and every parameter gradient vs the oracle (ginet_nocluster in
+    eval mode: its dropout draws from a different RNG than the oracle's)."""
+    fe = 1 if name == "sgat" else 3
+    datas = _datas(2, seed=5, fe=fe, n_lo=1000, n_hi=1200, mean_degree=12.0, k_lo=6, k_hi=9)
+    torch.manual_seed(3)
+    model_o = {"foutnet": gnn_ref.FoutNet, "sgat": gnn_ref.SGAT, "ginet_nocluster": gnn_ref.GINetNoCluster}[name](30, 1, fe)
+    m = {"foutnet": foutnet.FoutNet, "sgat": sgat.SGAT, "ginet_nocluster": ginet_nocluster.GINet}[name](30, 1, fe)
+    m.load_state_dict(model_o.state_dict())
+    m = m.to(DEV).train()
+    if name == "ginet_nocluster":
+        m.eval()
+        model_o.eval()
+    h = _handle(datas, clusters=name != "ginet_nocluster")
+    assert layered.needs_layers(m.fused_spec, h, 1)
+    out = m(SimpleNamespace(_dr_handle=h))
+    out_o, loss_o, g_o = _oracle_grads(model_o, datas)
+    np.testing.assert_allclose(out.detach().cpu().numpy(), out_o.numpy(), **TOL)
+    loss = torch.nn.functional.mse_loss(out.reshape(-1), torch.tensor([d.y.item() for d in datas], device=DEV))
+    assert float(loss.detach()) == pytest.approx(float(loss_o), rel=1e-4)
+    loss.backward()
+    for n, p in m.named_parameters():
+        assert_grad_close(p.grad.cpu().numpy(), g_o[n], err_msg=n)
+
+
+@pytest.mark.parametrize("name", ["foutnet", "sgat", "ginet_nocluster"])
+def test_layers_match_fused_kernel_on_residue_graphs(name):
+    fe = 1 if name == "sgat" else 3
+    datas = _datas(6, seed=21, fe=fe)
+    cls = {"foutnet": foutnet.FoutNet, "sgat": sgat.SGAT, "ginet_nocluster": ginet_nocluster.GINet}[name]
+    torch.manual_seed(4)
+    m = cls(30, 1, fe).to(DEV).eval()
+    hf, hl = _handle(datas, clusters=name != "ginet_nocluster"), _handle(datas, force=True, clusters=name != "ginet_nocluster")
+    with torch.no_grad():
+        of = m(SimpleNamespace(_dr_handle=hf))
+        ol = m(SimpleNamespace(_dr_handle=hl))
+    np.testing.assert_allclose(ol.cpu().numpy(), of.cpu().numpy(), **TOL)
+
+
+def test_fused_train_step_on_layers_matches_fused_kernel():
+    """Two Adam steps of FusedTrainStep: layer path (forced) vs graph pass —
+    same losses and parameters (fp32 reorder tolerance)."""
+    datas = _datas(8, seed=33)
+    torch.manual_seed(7)
+    m1 = foutnet.FoutNet(30, 1).to(DEV).train()
+    m2 = foutnet.FoutNet(30, 1).to(DEV).train()
+    m2.load_state_dict(m1.state_dict())
+    s1, s2 = FusedTrainStep(m1), FusedTrainStep(m2)
+    h1, h2 = _handle(datas), _handle(datas, force=True)
+    for _ in range(2):
+        l1, o1 = s1.step(h1)
+        l2, o2 = s2.step(h2)
+        np.testing.assert_allclose(o2.cpu().numpy(), o1.cpu().numpy(), **TOL)
+        assert float(l2) == pytest.approx(float(l1), rel=1e-4)
+    for a, b in zip(s1.grads, s2.grads):
+        assert_grad_close(b.cpu().numpy(), a.cpu().numpy())
+    for a, b in zip(s1.params, s2.params):
+        np.testing.assert_allclose(b.detach().cpu().numpy(), a.detach().cpu().numpy(), rtol=0, atol=5e-5)
+    assert int(s2.counter[0]) == 2
