@@ -332,7 +332,8 @@ __device__ __forceinline__ void d_pass_sum(const float* red, float* gw, int KE, 
     for (int wv = 0; wv < NW; ++wv) t += red[wv * RW + tid];
     if (tid < 32) gw[32 * KE + tid] = t;
     else {
-      const int c = (tid - 32) / FE, f = (tid - 32) % FE;
+      constexpr int FD = FE > 0 ? FE : 1;  // (FE == 0: this branch never runs)
+      const int c = (tid - 32) / FD, f = (tid - 32) % FD;
       gw[c * KE + 2 * F + f] = t;
     }
   }
