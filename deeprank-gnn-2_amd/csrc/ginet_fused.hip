@@ -157,31 +157,6 @@ __device__ __forceinline__ void gather_rows(const int* rp, const uint16_t* col, 
                                             int ldz, int n) {
   const int nch = XS >> 2;
   const int sub = threadIdx.x & 7;
-  if (n <= NT / 4 && nch <= 8) {
-    // up to 2 rows per 8-lane slot: rows i and i + half interleaved
-    // (drk::gather_row_pair), so one pass covers the graph
-    const int half = (n + 1) >> 1;
-    const int i = threadIdx.x >> 3;
-    if (i < half && sub < nch) {
-      const int c4 = sub * 4, i2 = i + half;
-      const bool two = i2 < n;
-      float4 acc, acc2;
-      drk::gather_row_pair(col, rp[i], rp[i + 1], two ? rp[i2] : 0, two ? rp[i2 + 1] : 0, X, XS, c4, acc, acc2);
-      float* zr = Z + i * ldz + c4;
-      zr[0] = acc.x;
-      zr[1] = acc.y;
-      zr[2] = acc.z;
-      zr[3] = acc.w;
-      if (two) {
-        float* zr2 = Z + i2 * ldz + c4;
-        zr2[0] = acc2.x;
-        zr2[1] = acc2.y;
-        zr2[2] = acc2.z;
-        zr2[3] = acc2.w;
-      }
-    }
-    return;
-  }
   for (int i = threadIdx.x >> 3; i < n; i += NT / 8) {
     const int eb = rp[i], ee = rp[i + 1];
     for (int ch = sub; ch < nch; ch += 8) {

@@ -84,29 +84,6 @@ struct NcArgs {
 __device__ __forceinline__ void gather_rows(const int* rp, const uint16_t* col, const float* Y, int ys, int nch,
                                             float* out, int ldo, int n) {
   const int sub = threadIdx.x & 7;
-  if (n <= NT / 4 && nch <= 8) {  // up to 2 rows per 8-lane slot, one pass (gather_row_pair)
-    const int half = (n + 1) >> 1;
-    const int i = threadIdx.x >> 3;
-    if (i < half && sub < nch) {
-      const int c4 = sub * 4, i2 = i + half;
-      const bool two = i2 < n;
-      float4 acc, acc2;
-      gather_row_pair(col, rp[i], rp[i + 1], two ? rp[i2] : 0, two ? rp[i2 + 1] : 0, Y, ys, c4, acc, acc2);
-      float* o = out + i * ldo + c4;
-      o[0] = acc.x;
-      o[1] = acc.y;
-      o[2] = acc.z;
-      o[3] = acc.w;
-      if (two) {
-        float* o2 = out + i2 * ldo + c4;
-        o2[0] = acc2.x;
-        o2[1] = acc2.y;
-        o2[2] = acc2.z;
-        o2[3] = acc2.w;
-      }
-    }
-    return;
-  }
   for (int i = threadIdx.x >> 3; i < n; i += NT / 8) {
     const int eb = rp[i], ee = rp[i + 1];
     for (int ch = sub; ch < nch; ch += 8) {

@@ -74,55 +74,6 @@ __device__ __forceinline__ float4 gather_row_chunk(const uint16_t* col, int eb, 
   return acc;
 }
 
-// Two CSR rows [eb, ee) and [fb, fe) by the same lanes: while both rows have
-// four edges left, both rows' index reads and then their eight row reads are
-// in flight together; each row still sums its own edges in CSR order, so acc
-// and acc2 are bit-identical to gather_row_chunk on each row.
-__device__ __forceinline__ void gather_row_pair(const uint16_t* col, int eb, int ee, int fb, int fe, const float* X,
-                                                int XS, int c4, float4& acc, float4& acc2) {
-  acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  acc2 = make_float4(0.f, 0.f, 0.f, 0.f);
-  int e = eb, f = fb;
-  for (; e + 4 <= ee && f + 4 <= fe; e += 4, f += 4) {
-    int e1 = e + 1, e2 = e + 2, e3 = e + 3, f1 = f + 1, f2 = f + 2, f3 = f + 3;
-    asm volatile("" : "+v"(e1), "+v"(e2), "+v"(e3), "+v"(f1), "+v"(f2), "+v"(f3));
-    const int j0 = col[e], j1 = col[e1], j2 = col[e2], j3 = col[e3];
-    const int k0 = col[f], k1 = col[f1], k2 = col[f2], k3 = col[f3];
-    const float4 v0 = *reinterpret_cast<const float4*>(&X[__umul24(j0, XS) + c4]);
-    const float4 v1 = *reinterpret_cast<const float4*>(&X[__umul24(j1, XS) + c4]);
-    const float4 v2 = *reinterpret_cast<const float4*>(&X[__umul24(j2, XS) + c4]);
-    const float4 v3 = *reinterpret_cast<const float4*>(&X[__umul24(j3, XS) + c4]);
-    const float4 w0 = *reinterpret_cast<const float4*>(&X[__umul24(k0, XS) + c4]);
-    const float4 w1 = *reinterpret_cast<const float4*>(&X[__umul24(k1, XS) + c4]);
-    const float4 w2 = *reinterpret_cast<const float4*>(&X[__umul24(k2, XS) + c4]);
-    const float4 w3 = *reinterpret_cast<const float4*>(&X[__umul24(k3, XS) + c4]);
-    acc = f4add(f4add(f4add(f4add(acc, v0), v1), v2), v3);
-    acc2 = f4add(f4add(f4add(f4add(acc2, w0), w1), w2), w3);
-  }
-  for (; e + 4 <= ee; e += 4) {
-    int e1 = e + 1, e2 = e + 2, e3 = e + 3;
-    asm volatile("" : "+v"(e1), "+v"(e2), "+v"(e3));
-    const int j0 = col[e], j1 = col[e1], j2 = col[e2], j3 = col[e3];
-    const float4 v0 = *reinterpret_cast<const float4*>(&X[__umul24(j0, XS) + c4]);
-    const float4 v1 = *reinterpret_cast<const float4*>(&X[__umul24(j1, XS) + c4]);
-    const float4 v2 = *reinterpret_cast<const float4*>(&X[__umul24(j2, XS) + c4]);
-    const float4 v3 = *reinterpret_cast<const float4*>(&X[__umul24(j3, XS) + c4]);
-    acc = f4add(f4add(f4add(f4add(acc, v0), v1), v2), v3);
-  }
-  for (; f + 4 <= fe; f += 4) {
-    int f1 = f + 1, f2 = f + 2, f3 = f + 3;
-    asm volatile("" : "+v"(f1), "+v"(f2), "+v"(f3));
-    const int k0 = col[f], k1 = col[f1], k2 = col[f2], k3 = col[f3];
-    const float4 w0 = *reinterpret_cast<const float4*>(&X[__umul24(k0, XS) + c4]);
-    const float4 w1 = *reinterpret_cast<const float4*>(&X[__umul24(k1, XS) + c4]);
-    const float4 w2 = *reinterpret_cast<const float4*>(&X[__umul24(k2, XS) + c4]);
-    const float4 w3 = *reinterpret_cast<const float4*>(&X[__umul24(k3, XS) + c4]);
-    acc2 = f4add(f4add(f4add(f4add(acc2, w0), w1), w2), w3);
-  }
-  for (; e < ee; ++e) acc = f4add(acc, *reinterpret_cast<const float4*>(&X[__umul24((int)col[e], XS) + c4]));
-  for (; f < fe; ++f) acc2 = f4add(acc2, *reinterpret_cast<const float4*>(&X[__umul24((int)col[f], XS) + c4]));
-}
-
 }  // namespace drk
 
 #ifdef DR_STAMPS
