@@ -37,6 +37,8 @@ def main():
     which = sys.argv[2] if len(sys.argv) > 2 else "ginet"
     if which == "vanilla":
         return vanilla(dev, B)
+    if which in ("foutnet", "sgat"):
+        return fout(dev, B, which)
     mod, phases = (amd_nc, PHASES_NC) if which == "ginet_nocluster" else (amd, PHASES)
     large = which == "ginet_large"
     if large:  # tail kernel of the split path on atom-level graphs (stamps 0-3: staging, tile combine)
@@ -68,6 +70,44 @@ def main():
     print(which)
     for name, v in zip(phases, med):
         print(f"  {name:18s} {v:8.0f} cyc  {100 * v / tot:5.1f}%")
+
+
+PHASES_F = ["stage", "gather rowmean(X)", "gemm conv1", "pool0", "conv2 (pooled)", "pool1+mean", "head fwd", "loss", "head/pool1/conv2 bwd", "dW1"]
+
+
+def fout(dev, B, which):
+    """fout_graph_kernel (FoutNet, or SGAT with one edge feature) phases on residue graphs."""
+    from deeprank2_amd import _lib  # noqa: PLC0415
+    from deeprank2_amd.fused import make_pass  # noqa: PLC0415
+    from deeprank2_amd.neuralnets.gnn import foutnet, sgat  # noqa: PLC0415
+
+    fe = 1 if which == "sgat" else 3
+    store = GraphStore(pack_graphs(records(make_dataset(B, seed=1000), fe)), dev)
+    h = amd.BatchHandle(store, np.arange(B))
+    torch.manual_seed(0)
+    model = (sgat.SGAT if which == "sgat" else foutnet.FoutNet)(30, 1, fe).to(dev)
+    spec = model.fused_spec
+    st = torch.zeros(B * 32, dtype=torch.int64, device=dev)
+    out = torch.empty(B, 1, device=dev)
+    slab = torch.empty(B * spec.slab_stride(30), device=dev)
+    head = torch.empty(B * spec.head_stride(1), device=dev)
+    lpg = torch.empty(B, device=dev)
+    params = model.ordered_params()
+    rows = []
+    for it in range(30):
+        p = make_pass(1, _lib.DR_PASS_FORWARD | _lib.DR_PASS_BACKWARD, loss_kind=_lib.DR_LOSS_MSE, loss_scale=1 / B, out=out, loss_per_graph=lpg, slab=slab, head=head, stamps=st)
+        from deeprank2_amd.fused import run_pass  # noqa: PLC0415
+
+        run_pass(spec, h, params, p)
+        torch.cuda.synchronize()
+        if it >= 5:
+            rows.append(st.view(B, 32)[:, : len(PHASES_F) + 1].cpu().numpy().copy())
+    d = np.diff(np.stack(rows), axis=2).astype(np.float64)
+    med = np.median(d.reshape(-1, d.shape[-1]), axis=0)
+    tot = med.sum()
+    print(f"B={B}  median cycles per fout_graph_kernel workgroup ({which}): {tot:.0f}")
+    for name, v in zip(PHASES_F, med):
+        print(f"  {name:22s} {v:8.0f} cyc  {100 * v / tot:5.1f}%")
 
 
 def vanilla(dev, B):
