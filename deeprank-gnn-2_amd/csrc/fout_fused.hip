@@ -43,19 +43,24 @@ constexpr int HEADW = 512;  // G32 hpre64 hh64 dh64 dG32 dout16 spare
 
 struct Carve {
   int KP, XS, LDZ;
+  bool wide;  // zm rows hold [x_i | Zm_i] (conv1 A operand at a conflict-free stride)
   int ea, c1, p1w, p1tid, c2;  // SGAT only (0 words otherwise)
   int wc1, w2, fc1, fc2, x, zm, h1, rp, col, m0p, m0i, p1, a1, dp1, zm2, s2, h2, d2, dz2, p1rp, p1c, p1trp, p1tc,
       m1p, m1i, p2, nt, head, dgp, red, total;
 };
 
 // X keeps the HBM row stride XS = r4(F) (16-byte rows: DMA + float4 gather);
-// Zm uses LDZ = r4(F)+2 (LDZ = 2 mod 32 or an odd multiple of 2 mod 32: the
-// MFMA column reads of lanes (row li, k+kq) hit distinct banks).
-__host__ __device__ inline Carve carve(int N, int E, int F, int K0, int P1, int K1, int alias, int OUT, bool sg) {
+// when the graph fits, the zm rows hold [x_i | Zm_i] (the own row copied in the
+// gather phase; SGAT: [x_i | Zw_i]) with stride LDZ = 2 r4(F) + 2, an odd
+// multiple of 2: the conv1 MFMA operand reads of lanes (row li, k+kq) hit
+// distinct banks (X's stride of 32 words puts 16 rows on one bank).  Otherwise
+// zm holds Zm alone (LDZ = r4(F) + 2) and conv1 reads x_i from X.
+__host__ __device__ inline Carve carve_at(int N, int E, int F, int K0, int P1, int K1, int alias, int OUT, bool sg, bool wide) {
   Carve c;
   c.KP = r16(2 * F);
   c.XS = r4(F);
-  c.LDZ = c.XS + 2;
+  c.wide = wide;
+  c.LDZ = wide ? 2 * c.XS + 2 : c.XS + 2;
   int o = 0;
 #define TAKE(field, words) \
   c.field = o;             \
@@ -109,6 +114,14 @@ __host__ __device__ inline Carve carve(int N, int E, int F, int K0, int P1, int 
   return c;
 }
 
+// The wide layout when it fits one workgroup's LDS, else the narrow one
+// (the conv1 A operand then reads x_i from the X rows; same sums either way).
+__host__ __device__ inline Carve carve(int N, int E, int F, int K0, int P1, int K1, int alias, int OUT, bool sg) {
+  const Carve w = carve_at(N, E, F, K0, P1, K1, alias, OUT, sg, true);
+  if (4LL * w.total <= 160 * 1024) return w;
+  return carve_at(N, E, F, K0, P1, K1, alias, OUT, sg, false);
+}
+
 struct FoutArgs {
   dr_graph_store s;
   dr_fout_weights w;
@@ -117,12 +130,15 @@ struct FoutArgs {
   int32_t B;
 };
 
-// gather_row_chunk with edge weights: acc = sum_e w[e] X[col[e], c4..c4+3]
+// gather_row_chunk with edge weights: acc = sum_e w[e] X[col[e], c4..c4+3];
+// sw = sum_e w[e] in edge order (the weights are loaded anyway)
 __device__ __forceinline__ float4 gather_row_chunk_w(const uint16_t* col, const float* w, int eb, int ee,
-                                                     const float* X, int XS, int c4) {
+                                                     const float* X, int XS, int c4, float& sw) {
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  sw = 0.f;
   for (int e = eb; e < ee; ++e) {
     const float we = w[e];
+    sw += we;
     const float4 v = *reinterpret_cast<const float4*>(&X[__umul24((int)col[e], XS) + c4]);
     acc = make_float4(fmaf(we, v.x, acc.x), fmaf(we, v.y, acc.y), fmaf(we, v.z, acc.z), fmaf(we, v.w, acc.w));
   }
@@ -146,6 +162,8 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
   const int OUT = a.p.out_dim;
   const Carve c = carve(N, E, F, K0, P1, K1, alias, OUT, SG);
   const int KP = c.KP, XS = c.XS, LDZ = c.LDZ;
+  const bool WIDE = c.wide;
+  const int ZO = WIDE ? XS : 0;  // column of Zm_0 in a zm row
   float* sEa = lds + c.ea;
   float* sC1 = lds + c.c1;
   float* sP1w = lds + c.p1w;
@@ -252,15 +270,20 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
     for (int i = tid >> 3; i < N; i += NT / 8) {
       const int eb = srp[i], ee = srp[i + 1];
       const float deg = SG ? (float)imax(ee - eb, 1) : (float)(ee - eb);
-      if (SG && sub == 0) {
-        float sw = 0.f;
-        for (int e = eb; e < ee; ++e) sw += sEa[e];
-        sC1[i] = sw / deg;
-      }
       for (int ch = sub; ch < nch; ch += 8) {
         const int c4 = ch * 4;
-        const float4 acc = SG ? gather_row_chunk_w(scol, sEa, eb, ee, sX, XS, c4) : gather_row_chunk(scol, eb, ee, sX, XS, c4);
-        float* zr = sZm + i * LDZ + c4;
+        float sw;
+        const float4 acc = SG ? gather_row_chunk_w(scol, sEa, eb, ee, sX, XS, c4, sw) : gather_row_chunk(scol, eb, ee, sX, XS, c4);
+        if (SG && ch == 0) sC1[i] = sw / deg;
+        if (WIDE) {  // own row x_i next to Zm_i (the conv1 A operand at a conflict-free stride)
+          float* xr = sZm + i * LDZ + c4;
+          const float4 xv = *reinterpret_cast<const float4*>(sX + i * XS + c4);
+          xr[0] = xv.x;
+          xr[1] = xv.y;
+          xr[2] = xv.z;
+          xr[3] = xv.w;
+        }
+        float* zr = sZm + i * LDZ + ZO + c4;
         // mean over the out-neighbours; 0/0 = NaN exactly as torch.mean(empty)
         if (c4 + 0 < F) zr[0] = acc.x / deg;
         if (c4 + 1 < F) zr[1] = acc.y / deg;
@@ -294,7 +317,8 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int kk = k + 4 * u + kq;
-          av[u] = kk < F ? cx * sX[ar * XS + kk] : (kk < 2 * F ? sZm[ar * LDZ + kk - F] : 0.f);
+          av[u] = kk < F ? cx * (WIDE ? sZm[ar * LDZ + kk] : sX[ar * XS + kk])
+                         : (kk < 2 * F ? sZm[ar * LDZ + ZO + kk - F] : 0.f);
           bv[u] = sWc1[kk * 16 + li];
         }
 #pragma unroll
@@ -567,7 +591,7 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
         const int q = p - half * 16 * F, kk = q >> 4, ch = q & 15;
         for (int k = 0; k < K0; ++k) {
           const int i = sA1[k * 16 + ch];
-          if (i < N) acc = fmaf(sdP1[k * 16 + ch], half ? sZm[i * LDZ + kk] : (SG ? sC1[i] : 1.f) * sX[i * XS + kk], acc);
+          if (i < N) acc = fmaf(sdP1[k * 16 + ch], half ? sZm[i * LDZ + ZO + kk] : (SG ? sC1[i] : 1.f) * (WIDE ? sZm[i * LDZ + kk] : sX[i * XS + kk]), acc);
         }
       } else {
         const int ch = p - 32 * F;

@@ -61,7 +61,9 @@ class _FoutLayerFn(torch.autograd.Function):
         deg = (rowptr[1:] - rowptr[:-1]).to(torch.float32).unsqueeze(1)
         has = deg > 0
         dwc = ops.linear_dw(dout, x).t().contiguous()
-        dwn = ops.linear_dw(dout, torch.where(has, zm, torch.zeros_like(zm))).t().contiguous()
+        # rows without out-edges contribute nothing: neither their (NaN) mean nor their dout
+        dout_has = torch.where(has, dout, torch.zeros_like(dout))
+        dwn = ops.linear_dw(dout_has, torch.where(has, zm, torch.zeros_like(zm))).t().contiguous()
         # d(neighbour term) / x_j = sum_{i: i->j} dout_i / deg_i  (transposed CSR)
         trowptr, _, tcol = ops.csr_from_coo(edge_index[1], edge_index[0], n)
         dbeta = ops.spmm_csr(trowptr, tcol, torch.where(has, dout / deg.clamp_min(1), torch.zeros_like(dout)), n)

@@ -86,6 +86,31 @@ def test_foutnet_nan_gradients_match_oracle(golden):
         np.testing.assert_allclose(g, r, equal_nan=True, rtol=1e-4, atol=1e-5, err_msg=n)
 
 
+@pytest.mark.parametrize("force_layers", [False, True])
+def test_foutnet_nan_gradients_match_oracle_both_paths(golden, force_layers):
+    """The NaN backward through the graph pass and through the layer-level path
+    (layered.py, FoutLayer autograd): a pooled node without out-edges adds
+    neither its NaN mean nor its gradient to conv2.wn (foutnet.py:56-58)."""
+    from types import SimpleNamespace
+
+    z = golden("foutnet_testhdf5")
+    model_o = gnn_ref.FoutNet(50, 2)
+    model_o.load_state_dict(golden_state_dict(z))
+    m = amd.FoutNet(50, 2)
+    m.load_state_dict(golden_state_dict(z))
+    m = m.to(DEV)
+    bat = golden_batch(z)
+    model_o(bat).sum().backward()
+    h = BatchHandle(GraphStore(pack_graphs(records_from_batch(golden_batch(z))), DEV), np.arange(4, dtype=np.int32))
+    h.force_layers = force_layers
+    m(SimpleNamespace(_dr_handle=h)).sum().backward()
+    ref = dict(model_o.named_parameters())
+    for n, p in m.named_parameters():
+        g, r = p.grad.cpu().numpy(), ref[n].grad.numpy()
+        np.testing.assert_array_equal(np.isnan(g), np.isnan(r), err_msg=n)
+        np.testing.assert_allclose(g, r, equal_nan=True, rtol=1e-4, atol=1e-5, err_msg=n)
+
+
 def test_foutnet_autograd_vs_oracle_mixed_clusters():
     """Isolated nodes (NaN rows dropped by the depth-0 scatter_max), several
     depth-1 clusters, CE loss over 3 classes."""
