@@ -116,9 +116,13 @@ __host__ __device__ inline Carve carve_at(int N, int E, int F, int K0, int P1, i
 
 // The wide layout when it fits one workgroup's LDS, else the narrow one
 // (the conv1 A operand then reads x_i from the X rows; same sums either way).
-__host__ __device__ inline Carve carve(int N, int E, int F, int K0, int P1, int K1, int alias, int OUT, bool sg) {
+// `limit` = the bytes of LDS available: 160 KiB when the host sizes a launch
+// (for the batch's elementwise-largest graph), the launch's dynamic LDS inside
+// the kernel, so a graph never takes a layout its launch did not reserve.
+__host__ __device__ inline Carve carve(int N, int E, int F, int K0, int P1, int K1, int alias, int OUT, bool sg,
+                                       int64_t limit = 160 * 1024) {
   const Carve w = carve_at(N, E, F, K0, P1, K1, alias, OUT, sg, true);
-  if (4LL * w.total <= 160 * 1024) return w;
+  if (4LL * w.total <= limit) return w;
   return carve_at(N, E, F, K0, P1, K1, alias, OUT, sg, false);
 }
 
@@ -128,6 +132,7 @@ struct FoutArgs {
   dr_pass p;
   const dr_graph_desc* descs;
   int32_t B;
+  int32_t lds_bytes;  // the launch's dynamic LDS: a graph takes the wide layout only if it fits this
 };
 
 // gather_row_chunk with edge weights: acc = sum_e w[e] X[col[e], c4..c4+3];
@@ -160,7 +165,7 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
   const int F = s.n_feat;
   const int alias = s.transpose_aliased;
   const int OUT = a.p.out_dim;
-  const Carve c = carve(N, E, F, K0, P1, K1, alias, OUT, SG);
+  const Carve c = carve(N, E, F, K0, P1, K1, alias, OUT, SG, a.lds_bytes);
   const int KP = c.KP, XS = c.XS, LDZ = c.LDZ;
   const bool WIDE = c.wide;
   const int ZO = WIDE ? XS : 0;  // column of Zm_0 in a zm row
@@ -628,6 +633,7 @@ int fout_family_pass(bool sg, const dr_graph_store* store, const dr_graph_desc* 
   args.p = *pass;
   args.descs = descs;
   args.B = n_batch;
+  args.lds_bytes = lds_bytes;
   if (sg)
     hipLaunchKernelGGL(fout_graph_kernel<true>, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, args);
   else
