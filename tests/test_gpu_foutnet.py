@@ -111,6 +111,32 @@ def test_foutnet_nan_gradients_match_oracle_both_paths(golden, force_layers):
         np.testing.assert_allclose(g, r, equal_nan=True, rtol=1e-4, atol=1e-5, err_msg=n)
 
 
+def test_foutnet_mixed_lds_layouts_vs_oracle():
+    """A batch whose largest graph (N~265) only fits the narrow LDS layout, so
+    the launch reserves the narrow size, and graphs (N~235) whose wide layout
+    fits 160 KiB but not that launch: every graph must take the layout its
+    launch reserved.  Forward + MSE gradients vs the oracle."""
+    from deeprank2_amd.utils.synthetic import make_dataset
+
+    gs = make_dataset(1, seed=6, n_lo=262, n_hi=268, mean_degree=15.0) + make_dataset(2, seed=3, n_lo=230, n_hi=238, mean_degree=15.0)
+    datas = [data_ref.synthetic_to_data(g, f"m{i}") for i, g in enumerate(gs)]
+    h = BatchHandle(GraphStore(pack_graphs(records_from_batch(P.Batch.from_data_list(datas))), DEV), np.arange(3, dtype=np.int32))
+    launch = amd.SPEC.lds(*h.max_sizes, 30, int(h.store.packed.transpose_aliased), 1)
+    assert launch <= 160 * 1024  # the fused kernel runs, not the layer path
+    model_o, model = _pair(30, 1, seed=8)
+    bat_o = P.Batch.from_data_list([d.clone() for d in datas])
+    out_o = model_o(bat_o)
+    torch.nn.functional.mse_loss(out_o.reshape(-1), bat_o.y).backward()
+    from types import SimpleNamespace
+
+    out = model(SimpleNamespace(_dr_handle=h))
+    torch.nn.functional.mse_loss(out.reshape(-1), bat_o.y.to(DEV)).backward()
+    np.testing.assert_allclose(out.detach().cpu().numpy(), out_o.detach().numpy(), equal_nan=True, **TOL)
+    ref = dict(model_o.named_parameters())
+    for n, p in model.named_parameters():
+        assert_grad_close(p.grad.cpu().numpy(), ref[n].grad.numpy(), err_msg=n)
+
+
 def test_foutnet_autograd_vs_oracle_mixed_clusters():
     """Isolated nodes (NaN rows dropped by the depth-0 scatter_max), several
     depth-1 clusters, CE loss over 3 classes."""
