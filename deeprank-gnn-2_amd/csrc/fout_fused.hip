@@ -280,20 +280,18 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
         float sw;
         const float4 acc = SG ? gather_row_chunk_w(scol, sEa, eb, ee, sX, XS, c4, sw) : gather_row_chunk(scol, eb, ee, sX, XS, c4);
         if (SG && ch == 0) sC1[i] = sw / deg;
+        // Rows are 8-byte aligned (LDZ even): two 64-bit stores per chunk; the
+        // pad columns F..XS-1 they also fill are never read.
         if (WIDE) {  // own row x_i next to Zm_i (the conv1 A operand at a conflict-free stride)
-          float* xr = sZm + i * LDZ + c4;
+          float2* xr = reinterpret_cast<float2*>(sZm + i * LDZ + c4);
           const float4 xv = *reinterpret_cast<const float4*>(sX + i * XS + c4);
-          xr[0] = xv.x;
-          xr[1] = xv.y;
-          xr[2] = xv.z;
-          xr[3] = xv.w;
+          xr[0] = make_float2(xv.x, xv.y);
+          xr[1] = make_float2(xv.z, xv.w);
         }
-        float* zr = sZm + i * LDZ + ZO + c4;
+        float2* zr = reinterpret_cast<float2*>(sZm + i * LDZ + ZO + c4);
         // mean over the out-neighbours; 0/0 = NaN exactly as torch.mean(empty)
-        if (c4 + 0 < F) zr[0] = acc.x / deg;
-        if (c4 + 1 < F) zr[1] = acc.y / deg;
-        if (c4 + 2 < F) zr[2] = acc.z / deg;
-        if (c4 + 3 < F) zr[3] = acc.w / deg;
+        zr[0] = make_float2(acc.x / deg, acc.y / deg);
+        zr[1] = make_float2(acc.z / deg, acc.w / deg);
       }
     }
   }
