@@ -105,15 +105,18 @@ def algorithmic_bytes(packed, gids, model="ginet", out_dim=1):
     return int(per.sum())
 
 
-def pmc_traffic_bytes():
+PMC_FILES = {"ginet": "pmc_ginet_graph_kernel.txt", "foutnet": "pmc_foutnet_graph_kernel.txt", "sgat": "pmc_sgat_graph_kernel.txt"}
+
+
+def pmc_traffic_bytes(model="ginet"):
     """HBM bytes per graph-kernel launch from the committed PMC pass
-    (profiles/*/pmc_ginet_graph_kernel.txt, collected by scripts/gpu_pmc.sh with
-    FETCH_SIZE and WRITE_SIZE in separate passes).  gfx950 correction
+    (profiles/*/pmc_<model>_graph_kernel.txt, collected by scripts/gpu_pmc.sh /
+    scripts/gpu_pmc_traffic.sh with FETCH_SIZE and WRITE_SIZE in separate passes).  gfx950 correction
     (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts half the bytes of wide
     coalesced reads, so bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024."""
     import glob  # noqa: PLC0415
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_ginet_graph_kernel.txt")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", PMC_FILES[model])))
     if not files:
         return None, None
     vals = {}
@@ -299,7 +302,8 @@ def main():  # noqa: PLR0915
     alg = np.mean([algorithmic_bytes(packed, h.gids_host, args.model) for h in handles])
     achieved = alg / (kernel_ms * 1e-3) / 1e9
     default_cfg = args.model == "ginet" and args.graphs == "residue" and B == B_PER_GPU
-    traffic, traffic_src = pmc_traffic_bytes() if default_cfg else (None, None)
+    pmc_cfg = default_cfg or (args.model in ("foutnet", "sgat") and args.graphs == "residue" and B == B_PER_GPU)
+    traffic, traffic_src = pmc_traffic_bytes(args.model) if pmc_cfg else (None, None)
     large = args.model == "ginet" and (bool(args.force_large) or any(h.lds((step.spec.entry, 1), lambda *sz: 0) > 160 * 1024 for h in handles))
 
     result = None

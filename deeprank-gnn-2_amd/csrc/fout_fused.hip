@@ -121,9 +121,10 @@ __host__ __device__ inline Carve carve_at(int N, int E, int F, int K0, int P1, i
 // the kernel, so a graph never takes a layout its launch did not reserve.
 __host__ __device__ inline Carve carve(int N, int E, int F, int K0, int P1, int K1, int alias, int OUT, bool sg,
                                        int64_t limit = 160 * 1024) {
-  const Carve w = carve_at(N, E, F, K0, P1, K1, alias, OUT, sg, true);
-  if (4LL * w.total <= limit) return w;
-  return carve_at(N, E, F, K0, P1, K1, alias, OUT, sg, false);
+  // decide first, then carve once: selecting between two Carve values makes
+  // hipcc build them in scratch (44 B per lane, ~3 MB of writes per launch)
+  const bool wide = 4LL * carve_at(N, E, F, K0, P1, K1, alias, OUT, sg, true).total <= limit;
+  return carve_at(N, E, F, K0, P1, K1, alias, OUT, sg, wide);
 }
 
 struct FoutArgs {

@@ -1,6 +1,6 @@
 """Workload for rocprofv3 --pmc passes: eager GINet training steps (config 2).
 
-    rocprofv3 --pmc <counters> -f csv -d <dir> -- python3 tools/pmc_run.py [steps] [ginet|vanilla]
+    rocprofv3 --pmc <counters> -f csv -d <dir> -- python3 tools/pmc_run.py [steps] [ginet|vanilla|foutnet|sgat]
 """
 
 from __future__ import annotations
@@ -25,13 +25,18 @@ from deeprank2_amd.utils.synthetic import make_dataset  # noqa: E402
 def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 40
     dev = torch.device("cuda:0")
-    packed = pack_graphs(records(make_dataset(64 * 16, seed=1000)))
+    which = sys.argv[2] if len(sys.argv) > 2 else "ginet"
+    packed = pack_graphs(records(make_dataset(64 * 16, seed=1000), 1 if which == "sgat" else 3))
     store = GraphStore(packed, dev)
     order = np.random.default_rng(0).permutation(packed.n_graphs).astype(np.int32)
     hs = [BatchHandle(store, order[i * 64:(i + 1) * 64]) for i in range(16)]
     torch.manual_seed(1234)
-    which = sys.argv[2] if len(sys.argv) > 2 else "ginet"
-    model = (VanillaNetwork if which == "vanilla" else GINet)(30, 1, 3).to(dev).train()
+    if which in ("foutnet", "sgat"):
+        from deeprank2_amd.neuralnets.gnn import foutnet, sgat  # noqa: PLC0415
+
+        model = (sgat.SGAT(30, 1, 1) if which == "sgat" else foutnet.FoutNet(30, 1, 3)).to(dev).train()
+    else:
+        model = (VanillaNetwork if which == "vanilla" else GINet)(30, 1, 3).to(dev).train()
     step = GINetTrainStep(model)
     for i in range(steps):
         step.step(hs[i % 16])
