@@ -8,9 +8,12 @@ already resident in HBM (a mini-batch is a list of graph ids).
 
     python bench.py [--gpus N --steps K --warmup W]
 
-N>1 is launched by torch.distributed.run (one rank per GPU, RCCL): every rank
-trains on its own 64 graphs per step (weak scaling) and the gradients are
-all-reduced once per step.  Rank 0 prints one JSON line.
+N>1: one rank per GPU over RCCL, every rank training on its own 64 graphs per
+step (weak scaling) with one gradient all-reduce per step.  Under
+torch.distributed.run (WORLD_SIZE set) this process is one rank; otherwise
+``--gpus N`` starts ``torch.distributed.run --nproc-per-node N bench.py ...`` as
+a child process before anything touches the GPU and relays its output.
+Rank 0 prints one JSON line.
 """
 
 from __future__ import annotations
@@ -18,28 +21,17 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
-
-import numpy as np
-import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "deeprank-gnn-2_amd")]
 
-from deeprank2_amd.engine import FusedTrainStep  # noqa: E402
-from deeprank2_amd.fused import BatchHandle  # noqa: E402
-from deeprank2_amd.neuralnets.gnn.foutnet import FoutNet  # noqa: E402
-from deeprank2_amd.neuralnets.gnn.ginet import GINet  # noqa: E402
-from deeprank2_amd.neuralnets.gnn.ginet_nocluster import GINet as GINetNoCluster  # noqa: E402
-from deeprank2_amd.neuralnets.gnn.sgat import SGAT  # noqa: E402
-from deeprank2_amd.neuralnets.gnn.vanilla_gnn import VanillaNetwork  # noqa: E402
-from deeprank2_amd.store import GraphRecord, GraphStore, pack_graphs  # noqa: E402
-from deeprank2_amd.utils.synthetic import doubled_edges, make_dataset  # noqa: E402
-
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 B_PER_GPU = 64
-MODELS = {"ginet": GINet, "foutnet": FoutNet, "vanilla": VanillaNetwork, "sgat": SGAT, "ginet_nocluster": GINetNoCluster}
+MODEL_NAMES = ("foutnet", "ginet", "ginet_nocluster", "sgat", "vanilla")
 ORACLE_MODELS = {"ginet": "GINet", "foutnet": "FoutNet", "vanilla": "VanillaNetwork", "sgat": "SGAT", "ginet_nocluster": "GINetNoCluster"}
 # graph families of SURVEY §8(d): residue-PPI (configs 2/3), atom-level (config 4), SRV-like
 FAMILIES = {
@@ -50,15 +42,43 @@ FAMILIES = {
 WORKLOADS = {
     ("ginet", "residue"): "GINet residue-PPI training step, BASELINE.json configs[1]",
     ("foutnet", "residue"): "FoutNet residue-PPI training step, BASELINE.json configs[2]",
-    ("ginet", "atom"): "GINet atom-level training step (fp32), BASELINE.json configs[3] shape",
+    ("ginet", "atom"): "GINet atom-level training step, BASELINE.json configs[3] (per-GPU share: 32 of 256)",
     ("ginet", "mixed"): "GINet mixed residue/SRV/atom batch, BASELINE.json configs[4] shape",
+    ("vanilla", "mixed"): "VanillaNetwork (fused gather+edge MLP+scatter) mixed residue/SRV/atom batch, BASELINE.json configs[4]",
+    ("vanilla", "residue"): "VanillaNetwork residue-PPI training step, configs[1] graph shape",
+    ("foutnet", "mixed"): "FoutNet mixed residue/SRV/atom batch, configs[4] graph mix",
     ("sgat", "residue"): "SGAT residue-PPI training step (1 edge feature), configs[1] graph shape",
     ("ginet_nocluster", "residue"): "ginet_nocluster.GINet residue-PPI training step, configs[1] graph shape",
 }
+HEADLINE_METRIC = "graphs/sec + edges/sec per training step, GINet residue-PPI, 1/2/4/8 MI355X"
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def relaunch(n, argv):
+    """``--gpus N`` outside torch.distributed.run: start N ranks as a child
+    process (nothing in this process has touched the GPU; only stdlib modules
+    are imported so far), stream its output through, exit with its code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    for line in proc.stdout:
+        sys.stdout.write(line)
+        sys.stdout.flush()
+    return proc.wait()
 
 
 def make_graphs(kind, n, seed):
     """Synthetic dataset of one family, or config 5's 50/30/20 residue/SRV/atom mix."""
+    import numpy as np  # noqa: PLC0415
+
+    from deeprank2_amd.utils.synthetic import make_dataset  # noqa: PLC0415
+
     if kind != "mixed":
         return make_dataset(n, seed=seed, **FAMILIES[kind])
     rng = np.random.default_rng(seed)
@@ -67,6 +87,9 @@ def make_graphs(kind, n, seed):
 
 
 def records(graphs, edge_features=3):
+    from deeprank2_amd.store import GraphRecord  # noqa: PLC0415
+    from deeprank2_amd.utils.synthetic import doubled_edges  # noqa: PLC0415
+
     out = []
     for i, g in enumerate(graphs):
         ei, ea = doubled_edges(g)
@@ -75,41 +98,59 @@ def records(graphs, edge_features=3):
     return out
 
 
-def algorithmic_bytes(packed, gids, model="ginet", out_dim=1):
-    """Bytes one graph pass must move for these graphs:
-    reads x (4NF), CSR (4(N+1)+4E), depth-0 members (4(K0+1)+4N), pooled CSR
-    (4(K0+1)+4P1), depth-1 members (4(K1+1)+4K0), y (4); writes the per-graph
-    weight-gradient slab and head vectors (GINet: 4(32F+1024) + 4*324).
-    VanillaNetwork reads no clusters but the edge features (4*E*Fe) and the
-    transposed CSR with its slot map (4(N+1)+8E).  SGAT adds the edge weights
-    (4E) and the pooled ones with their transposed slot map (8*P1) to FoutNet;
-    ginet_nocluster reads x, the CSR and its transpose and no clusters."""
+def algorithmic_bytes(packed, gids, model="ginet", s=4):
+    """SURVEY §8(d)'s compulsory bytes for one graph pass over these graphs:
+    B_alg(g) = s*N*F (x) + 4*E (int32 CSR sources) + 4*(N+1) (rowptr)
+    + 4*N (cluster0) + 4*K0 (cluster1) + 4 (y); s = 4 (fp32) or 2 (bf16).
+    VanillaNetwork adds its edge features (s*E*Fe) and reads no clusters;
+    SGAT adds its one edge feature (s*E); ginet_nocluster reads no clusters."""
+    n, e, k0, _p1, _k1 = (a[gids] for a in packed.sizes())
+    f = packed.n_feat
+    base = s * n * f + 4 * e + 4 * (n + 1) + 4
+    clusters = 4 * n + 4 * k0
+    if model == "vanilla":
+        fe = 0 if packed.edge_attr is None else packed.edge_attr.shape[1]
+        per = base + s * e * fe
+    elif model == "ginet_nocluster":
+        per = base
+    elif model == "sgat":
+        per = base + clusters + s * e
+    else:
+        per = base + clusters
+    return int(per.sum())
+
+
+def design_bytes(packed, gids, model="ginet", out_dim=1):
+    """Bytes this design moves beyond §8(d)'s compulsory ones, per graph pass:
+    the per-graph gradient slab and head vectors the graph pass writes and the
+    reduce kernel reads back (GINet: 4(32F+1024) + 4(320+r4(out)) per graph),
+    plus the precomputed pooling structures (depth-0 member lists, pooled CSR,
+    depth-1 members) and, for Vanilla, the transposed CSR."""
     n, e, k0, p1, k1 = (a[gids] for a in packed.sizes())
     f = packed.n_feat
     r4 = lambda v: (v + 3) & ~3  # noqa: E731
     if model == "vanilla":
         fe = 0 if packed.edge_attr is None else packed.edge_attr.shape[1]
-        per = 4 * n * f + 2 * (4 * (n + 1) + 4 * e) + 4 * e + 4 * e * fe + 4
-        per = per + 4 * 2 * (32 * (2 * f + fe) + 32 + f * (f + 32) + f) + 4 * (r4(f) + 256 + r4(out_dim))
-        return int(per.sum())
-    if model == "ginet_nocluster":
-        per = 4 * n * f + 2 * (4 * (n + 1) + 2 * e) + 4 + 4 * (32 * f + 1024) + 4 * (320 + r4(out_dim))
-        return int(per.sum())
-    per = 4 * n * f + 4 * (n + 1) + 4 * e + 4 * (k0 + 1) + 4 * n + 4 * (k0 + 1) + 4 * p1 + 4 * (k1 + 1) + 4 * k0 + 4
-    if model == "sgat":
-        per = per + 4 * e + 8 * p1
-    if model in ("foutnet", "sgat"):
-        per = per + 4 * (32 * f + 1072) + 4 * (160 + r4(out_dim))
+        part = 4 * 2 * (32 * (2 * f + fe) + 32 + f * (f + 32) + f) + 4 * (r4(f) + 256 + r4(out_dim))
+        extra = 4 * (n + 1) + 4 * e
+    elif model == "ginet_nocluster":
+        part = 4 * (32 * f + 1024) + 4 * (320 + r4(out_dim))
+        extra = 4 * (n + 1) + 2 * e
     else:
-        per = per + 4 * (32 * f + 1024) + 4 * (320 + r4(out_dim))
-    return int(per.sum())
+        pool = 4 * (k0 + 1) + 4 * (k0 + 1) + 4 * p1 + 4 * (k1 + 1)
+        if model in ("foutnet", "sgat"):
+            part = 4 * (32 * f + 1072) + 4 * (160 + r4(out_dim))
+        else:
+            part = 4 * (32 * f + 1024) + 4 * (320 + r4(out_dim))
+        extra = pool + (8 * p1 if model == "sgat" else 0)
+    return int((2 * part + extra).sum())
 
 
 PMC_FILES = {"ginet": "pmc_ginet_graph_kernel.txt", "foutnet": "pmc_foutnet_graph_kernel.txt", "sgat": "pmc_sgat_graph_kernel.txt"}
 
 
 def pmc_traffic_bytes(model="ginet"):
-    """HBM bytes per graph-kernel launch from the committed PMC pass
+    """HBM bytes per graph-kernel launch from the newest committed PMC pass
     (profiles/*/pmc_<model>_graph_kernel.txt, collected by scripts/gpu_pmc.sh /
     scripts/gpu_pmc_traffic.sh with FETCH_SIZE and WRITE_SIZE in separate passes).  gfx950 correction
     (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts half the bytes of wide
@@ -129,17 +170,49 @@ def pmc_traffic_bytes(model="ginet"):
     return int((2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024), os.path.relpath(files[-1], ROOT)
 
 
+def stream_copy_gbs(dev, mib=1024, reps=5):
+    """Achievable HBM bandwidth on this GPU: a device-to-device copy of ``mib``
+    MiB timed with HIP events (bytes read + written), best of ``reps``."""
+    import torch  # noqa: PLC0415
+
+    n = mib * (1 << 20) // 4
+    src = torch.ones(n, dtype=torch.float32, device=dev)
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    best = None
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        dst.copy_(src)
+        e1.record()
+        torch.cuda.synchronize(dev)
+        ms = e0.elapsed_time(e1)
+        best = ms if best is None else min(best, ms)
+    del src, dst
+    torch.cuda.empty_cache()
+    return 2 * n * 4 / (best * 1e-3) / 1e9
+
+
+def host_cores():
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    used = min(aff, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else aff
+    return used, aff
+
+
 def cpu_baseline(graphs, budget_s=15.0, max_steps=60, model_name="ginet"):
     """The CPU oracle (op-for-op restatement of the reference, torch CPU) training
-    the same batch: forward, MSE, backward, Adam — on this host's cores."""
+    the same batch: forward, MSE, backward, Adam — on this host's cores
+    (``len(os.sched_getaffinity(0))``, or the box's ``OMP_NUM_THREADS`` share)."""
+    import torch  # noqa: PLC0415
+
     from oracle import data_ref, gnn_ref  # noqa: PLC0415
     from oracle import pyg_ops as P  # noqa: PLC0415
 
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))
+    cores, affinity = host_cores()
     torch.set_num_threads(cores)
     datas = [data_ref.synthetic_to_data(g) for g in graphs]
     torch.manual_seed(1234)
@@ -166,23 +239,66 @@ def cpu_baseline(graphs, budget_s=15.0, max_steps=60, model_name="ginet"):
         n += 1
     dt = (time.perf_counter() - t0) / n
     name = ORACLE_MODELS[model_name]
-    return {"value": round(len(graphs) / dt, 2), "unit": "graphs/s", "cores": cores, "kind": "port", "sample": f"{n} {name}(30,1,3) train steps (fwd+MSE+bwd+Adam) on one batch of {len(graphs)} of the same synthetic graphs; oracle/gnn_ref.py on torch CPU, {cores} threads; {dt * 1e3:.1f} ms/step"}
+    return {"value": round(len(graphs) / dt, 2), "unit": "graphs/s", "cores": cores, "host_affinity_cores": affinity, "kind": "port", "sample": f"{n} {name}(30,1,3) train steps (fwd+MSE+bwd+Adam) on one batch of {len(graphs)} of the same synthetic graphs; oracle/gnn_ref.py on torch CPU, {cores} threads (host affinity {affinity}); {dt * 1e3:.1f} ms/step"}
 
 
-def main():  # noqa: PLR0915
+def parse_args(argv):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batches", type=int, default=16, help="resident mini-batches per rank")
     ap.add_argument("--batch", type=int, default=None, help="graphs per GPU per step (default 64; 32 for atom-level graphs)")
-    ap.add_argument("--model", choices=sorted(MODELS), default="ginet")
+    ap.add_argument("--model", choices=MODEL_NAMES, default="ginet")
     ap.add_argument("--graphs", choices=["residue", "atom", "mixed", "srv"], default="residue")
+    ap.add_argument("--dtype", choices=["f32", "bf16"], default="f32", help="compute dtype of the node GEMMs (bf16: GINet only; fp32 accumulate, fp32 master weights and Adam)")
     ap.add_argument("--force-large", type=int, default=0, help="GINet: run the split tile+tail path with this many nodes per tile (diagnostic)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-stream-copy", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch every step from Python instead of replaying captured HIP graphs")
     ap.add_argument("--eager-ddp", action="store_true", help="N>1: launch steps from Python (default: the RCCL all-reduce is captured in the HIP graph with the kernels)")
-    args = ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true", help="launcher check without a GPU: each rank joins a gloo group, rank 0 prints the JSON skeleton")
+    return ap.parse_args(argv)
+
+
+def dry_run(args):
+    """CPU-only rehearsal of the N-rank launch: the line carries the world size
+    and backend the ranks actually formed (tests/test_bench_launch.py)."""
+    import torch  # noqa: PLC0415
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    backend = None
+    if world > 1:
+        torch.distributed.init_process_group("gloo")
+        world = torch.distributed.get_world_size()
+        backend = torch.distributed.get_backend()
+        t = torch.ones(1)
+        torch.distributed.all_reduce(t)
+        assert int(t.item()) == world
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(json.dumps({"metric": HEADLINE_METRIC, "value": None, "unit": "graphs/s", "n_gpus": world, "world_size": world, "backend": backend, "dry_run": True, "config": {"parallelism": f"dp{world}"}}), flush=True)
+    if world > 1:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
+def main(args):  # noqa: PLR0915, PLR0912, C901
+    import numpy as np  # noqa: PLC0415
+    import torch  # noqa: PLC0415
+
+    from deeprank2_amd.engine import FusedTrainStep  # noqa: PLC0415
+    from deeprank2_amd.fused import BatchHandle  # noqa: PLC0415
+    from deeprank2_amd.neuralnets.gnn.foutnet import FoutNet  # noqa: PLC0415
+    from deeprank2_amd.neuralnets.gnn.ginet import GINet  # noqa: PLC0415
+    from deeprank2_amd.neuralnets.gnn.ginet_nocluster import GINet as GINetNoCluster  # noqa: PLC0415
+    from deeprank2_amd.neuralnets.gnn.sgat import SGAT  # noqa: PLC0415
+    from deeprank2_amd.neuralnets.gnn.vanilla_gnn import VanillaNetwork  # noqa: PLC0415
+    from deeprank2_amd.store import GraphStore, pack_graphs  # noqa: PLC0415
+
+    models = {"ginet": GINet, "foutnet": FoutNet, "vanilla": VanillaNetwork, "sgat": SGAT, "ginet_nocluster": GINetNoCluster}
+    if args.dtype == "bf16" and args.model != "ginet":
+        msg = "--dtype bf16 is implemented for GINet (BASELINE.json configs[3])"
+        raise SystemExit(msg)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -197,6 +313,7 @@ def main():  # noqa: PLR0915
     force_pg = os.environ.get("DR_BENCH_PG") == "1"
     if shared:
         local = 0
+    backend = None
     if world > 1 or force_pg:
         torch.cuda.set_device(local)
         if shared:
@@ -204,14 +321,16 @@ def main():  # noqa: PLR0915
         else:
             torch.distributed.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
         pg = torch.distributed.group.WORLD
+        world = torch.distributed.get_world_size()
+        backend = torch.distributed.get_backend()
     dev = torch.device(f"cuda:{local}")
 
     B = args.batch or (32 if args.graphs == "atom" else B_PER_GPU)
     if args.graphs in ("atom", "mixed"):
         args.batches = min(args.batches, 4)  # generation time of ~3k-node graphs
     graphs = make_graphs(args.graphs, B * args.batches, seed=1000 + rank)
-    packed = pack_graphs(records(graphs, 1 if args.model == "sgat" else 3), require_clusters=args.model != "ginet_nocluster")
-    store = GraphStore(packed, dev)
+    packed = pack_graphs(records(graphs, 1 if args.model == "sgat" else 3), require_clusters=args.model not in ("ginet_nocluster", "vanilla"))
+    store = GraphStore(packed, dev, dtype=args.dtype)
     order = np.random.default_rng(rank).permutation(packed.n_graphs).astype(np.int32)
     handles = [BatchHandle(store, order[i * B:(i + 1) * B]) for i in range(args.batches)]
     for h in handles:
@@ -219,11 +338,11 @@ def main():  # noqa: PLR0915
         h.large_tile = args.force_large or None
 
     torch.manual_seed(1234)
-    model = MODELS[args.model](30, 1, 3).to(dev).train()
+    model = models[args.model](30, 1, 3).to(dev).train()
     if pg is not None:
         for p in model.parameters():
             torch.distributed.broadcast(p.data, 0)
-    step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5, loss="mse", process_group=pg)
+    step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5, loss="mse", process_group=pg, compute_dtype=args.dtype)
     model._drop_seed = 77 + rank  # training-mode dropout drawn in-kernel (counter hash)
 
     def run_eager(i):
@@ -231,6 +350,11 @@ def main():  # noqa: PLR0915
 
     for i in range(args.warmup):
         run_eager(i)
+    # steps i0.. run in mini-batch order i % len(handles): the sweep graph is
+    # captured starting at the first timed mini-batch, so every timed step
+    # replays a captured graph whatever --steps / --warmup are
+    rot = args.warmup % len(handles)
+    sweep_handles = handles[rot:] + handles[:rot]
     captured = sweep = None
     capture_note = ""
     if not args.eager and (pg is None or (not shared and not args.eager_ddp)):
@@ -239,7 +363,7 @@ def main():  # noqa: PLR0915
         # RCCL all-reduce is captured with the kernels
         try:
             captured = [step.capture(h, global_batch=B * world) for h in handles]
-            sweep = step.capture_sweep(handles, global_batch=B * world)
+            sweep = step.capture_sweep(sweep_handles, global_batch=B * world)
         except RuntimeError as e:
             if pg is None:
                 raise
@@ -253,19 +377,20 @@ def main():  # noqa: PLR0915
                 captured = sweep = None
                 capture_note = capture_note or " (capture failed on another rank)"
 
+    n_sweeps = args.steps // len(handles) if sweep is not None else 0
+
     def run_steps(i0, k):
-        """Steps i0 .. i0+k-1 (mini-batch i % len(handles)); whole sweeps replay the sweep graph."""
+        """Steps i0 .. i0+k-1 (mini-batch i % len(handles)): whole sweeps first, then per-step graphs."""
         i = i0
+        for _ in range(n_sweeps):
+            sweep.replay()
+            i += len(handles)
         while i < i0 + k:
-            if sweep is not None and i % len(handles) == 0 and i + len(handles) <= i0 + k:
-                sweep.replay()
-                i += len(handles)
-            elif captured is not None:
+            if captured is not None:
                 captured[i % len(captured)].replay()
-                i += 1
             else:
                 run_eager(i)
-                i += 1
+            i += 1
         return step.loss_out
 
     torch.cuda.synchronize()
@@ -299,12 +424,19 @@ def main():  # noqa: PLR0915
     if pg is not None:
         torch.distributed.all_reduce(et)
     edges_total = float(et.item())
-    alg = np.mean([algorithmic_bytes(packed, h.gids_host, args.model) for h in handles])
+    s = 2 if args.dtype == "bf16" else 4
+    alg = float(np.mean([algorithmic_bytes(packed, h.gids_host, args.model, s) for h in handles]))
+    design = float(np.mean([design_bytes(packed, h.gids_host, args.model) for h in handles]))
+    n_params = sum(p.numel() for p in model.parameters())
+    adam_bytes = 28 * n_params  # Adam fp32: read param, grad, m, v; write param, m, v (§8(d))
     achieved = alg / (kernel_ms * 1e-3) / 1e9
-    default_cfg = args.model == "ginet" and args.graphs == "residue" and B == B_PER_GPU
+    ms_step = elapsed / args.steps * 1e3
+    wall_gbs = (alg + adam_bytes) / (ms_step * 1e-3) / 1e9
+    default_cfg = args.model == "ginet" and args.graphs == "residue" and B == B_PER_GPU and args.dtype == "f32"
     pmc_cfg = default_cfg or (args.model in ("foutnet", "sgat") and args.graphs == "residue" and B == B_PER_GPU)
     traffic, traffic_src = pmc_traffic_bytes(args.model) if pmc_cfg else (None, None)
-    large = args.model == "ginet" and (bool(args.force_large) or any(h.lds((step.spec.entry, 1), lambda *sz: 0) > 160 * 1024 for h in handles))
+    large = args.model == "ginet" and (bool(args.force_large) or args.dtype == "bf16" or any(h.lds((step.spec.entry, 1), lambda *sz: 0) > 160 * 1024 for h in handles))
+    copy_gbs = None if args.no_stream_copy else stream_copy_gbs(dev)
 
     result = None
     if rank == 0:
@@ -312,21 +444,23 @@ def main():  # noqa: PLR0915
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(graphs[:B], model_name=args.model)
         workload = WORKLOADS.get((args.model, args.graphs), f"{args.model} on {args.graphs} graphs (diagnostic)")
-        kname = {"ginet": "ginet_large_conv1_kernel + ginet_large_tail_kernel (dr_ginet_large_pass)" if large else "ginet_graph_kernel (dr_ginet_graph_pass, fwd+loss+bwd, 1 workgroup/graph)", "foutnet": "fout_graph_kernel<false> (dr_fout_graph_pass)", "vanilla": "vanilla_graph_kernel (dr_vanilla_graph_pass)", "sgat": "fout_graph_kernel<true> (dr_sgat_graph_pass)", "ginet_nocluster": "ginet_nocluster_kernel (dr_ginet_nocluster_graph_pass)"}[args.model]
+        kname = {"ginet": "ginet_large_conv1_kernel + ginet_large_tail_kernel (dr_ginet_large_pass)" if large else "ginet_graph_kernel (dr_ginet_graph_pass, fwd+loss+bwd, 1 workgroup/graph)", "foutnet": "fout_graph_kernel<false> (dr_fout_graph_pass)", "vanilla": "vanilla_graph_kernel (dr_vanilla_fused_pass) / vanilla pipeline (dr_vanilla_graph_pass)", "sgat": "fout_graph_kernel<true> (dr_sgat_graph_pass)", "ginet_nocluster": "ginet_nocluster_kernel (dr_ginet_nocluster_graph_pass)"}[args.model]
         result = {
-            "metric": "graphs/sec per training step, GINet residue-PPI (fwd+MSE+bwd+Adam)" if default_cfg else f"graphs/sec per training step, {workload} (fwd+MSE+bwd+Adam)",
+            "metric": HEADLINE_METRIC if default_cfg else f"graphs/sec per training step, {workload} (fwd+MSE+bwd+Adam)",
             "value": round(graphs_total / elapsed, 1),
             "unit": "graphs/s",
             "edges_per_sec": round(edges_total / elapsed, 1),
             "n_gpus": world,
+            "world_size": world,
+            "backend": backend,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "ms_per_step": round(ms_step, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
-            "data": f"synthetic (seeded {args.graphs} graphs per SURVEY §8(d); random-init {MODELS[args.model].__name__}(30,1,3))",
+            "dtype": args.dtype,
+            "data": f"synthetic (seeded {args.graphs} graphs per SURVEY §8(d); random-init {models[args.model].__name__}(30,1,3))",
             "config": {
                 "workload": workload,
                 "graphs_per_gpu": B,
@@ -348,10 +482,16 @@ def main():  # noqa: PLR0915
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": int(alg),
+                "algorithmic_definition": "SURVEY §8(d) B_alg: s*N*F + 4E + 4(N+1) + 4N + 4K0 + 4 per graph (s=2 bf16, 4 fp32; +s*E*Fe Vanilla, no clusters for Vanilla/ginet_nocluster)",
+                "design_bytes_per_launch": int(design),
+                "design_definition": "per-graph gradient slab + head vectors (written, then read by the reduce) and the precomputed pooling structures: intermediates of this design, not compulsory",
                 "kernel_ms_avg": round(kernel_ms, 5),
                 "kernel_timing": f"HIP events around one HIP graph of {args.steps} back-to-back {step.spec.entry if not large else 'dr_ginet_large_pass'} launches on the launch stream, divided by {args.steps}",
+                "stream_copy_GBs": None if copy_gbs is None else round(copy_gbs, 1),
+                "frac_of_stream_copy": None if copy_gbs is None else round(achieved / copy_gbs, 5),
+                "wallclock": {"bytes_per_step": int(alg + adam_bytes), "achieved": round(wall_gbs, 2), "frac": round(wall_gbs / HBM_PEAK_GBS, 5), "note": "B_alg(step) = sum_g B_alg(g) + 28*P (Adam fp32) over ms_per_step"},
             },
-            "launch": ("eager" + capture_note) if captured is None else f"hipgraph-replay ({len(handles)}-step sweep graphs + per-step graphs{', RCCL all-reduce captured' if pg is not None else ''})",
+            "launch": ("eager" + capture_note) if captured is None else f"hipgraph-replay ({n_sweeps} x {len(handles)}-step sweep graph + {args.steps - n_sweeps * len(handles)} per-step graphs{', RCCL all-reduce captured' if pg is not None else ''})",
             "cpu_baseline": cpu,
             "final_loss": float(loss.item()),
         }
@@ -363,4 +503,11 @@ def main():  # noqa: PLR0915
 
 
 if __name__ == "__main__":
-    main()
+    _argv = sys.argv[1:]
+    _args = parse_args(_argv)
+    if _args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch(_args.gpus, _argv))
+    if _args.dry_run:
+        dry_run(_args)
+    else:
+        main(_args)

@@ -40,11 +40,12 @@ struct alignas(64) ReduceArgs {
   const float* lpg;
   float* loss_out;
   int64_t* step_counter;
+  const float* grad_div;
   int32_t B, slab_stride, head_stride, adam_enabled;
   float loss_scale, pad0;
   float lr, beta1, beta2, eps, weight_decay, bias_c1, bias_c2_sqrt, pad1;
   float log2_beta1, log2_beta2;  // beta^t = exp2(t log2 beta): one v_exp_f32, not powf
-  int32_t pad2[14];
+  int32_t pad2[12];
   ParamRec rec[DR_MAX_PARAMS];
   // 1-D grid: block -> (parameter, first element); blocks never straddle two parameters
   uint8_t blk_param[DR_REDUCE_MAX_BLOCKS];
@@ -106,7 +107,11 @@ __global__ void __launch_bounds__(RP* RC) reduce_adam_kernel(ReduceArgs a) {
     v0 = r.v[ec];
     if (a.step_counter) tstep = a.step_counter[1] + 1;
   }
-  if (ch == 0 && !a.slab && r.grad) gin = r.grad[ec];
+  float div = 1.f;
+  if (ch == 0 && !a.slab && r.grad) {
+    gin = r.grad[ec];
+    if (a.grad_div) div = *a.grad_div;
+  }
   if (a.slab) {
     float acc = 0.f;
     if (has_src && b0 < b1) {
@@ -138,6 +143,11 @@ __global__ void __launch_bounds__(RP* RC) reduce_adam_kernel(ReduceArgs a) {
     if (r.grad) r.grad[e] = gsum;
   } else {  // gradients supplied (e.g. after an RCCL all-reduce): Adam only
     gsum = gin;
+    if (a.grad_div) {
+      gsum = gin / div;
+      r.grad[e] = gsum;
+      if (first && lp == 0 && a.loss_out) a.loss_out[0] = a.loss_out[0] / div;
+    }
   }
   if (upd) {
     float bc1 = a.bias_c1, bc2s = a.bias_c2_sqrt;
@@ -173,6 +183,7 @@ extern "C" int dr_reduce_update(const dr_param_table* t, const float* slab, cons
   a.lpg = loss_per_graph;
   a.loss_out = loss_out;
   a.step_counter = adam->step_counter;
+  a.grad_div = adam->grad_div;
   a.B = n_batch;
   a.slab_stride = t->slab_stride;
   a.head_stride = t->head_stride;

@@ -72,6 +72,9 @@ class GraphStoreC(ctypes.Structure):
         ("pad0", ctypes.c_int32),
         ("p1_ea", VP),
         ("p1t_pid", VP),
+        ("x_bf16", VP),
+        ("x_bf16_stride", ctypes.c_int32),
+        ("pad1", ctypes.c_int32),
     ]
 
 
@@ -131,6 +134,10 @@ class MclGraphsC(ctypes.Structure):
     _fields_ = [(n, VP) for n in ("node_off", "rowptr", "edge_off", "col", "weight", "ws_off", "ws", "pat_off", "pattern", "iters")]
 
 
+DR_DTYPE_F32 = 0
+DR_DTYPE_BF16 = 1
+
+
 class PassC(ctypes.Structure):
     _fields_ = [
         ("flags", ctypes.c_int32),
@@ -142,7 +149,7 @@ class PassC(ctypes.Structure):
         ("drop_seed", ctypes.c_uint64),
         ("drop_offset", ctypes.c_uint64),
         ("loss_scale", ctypes.c_float),
-        ("pad0", ctypes.c_int32),
+        ("compute_dtype", ctypes.c_int32),
         ("mask", VP),
         ("class_w", VP),
         ("out", VP),
@@ -166,6 +173,7 @@ class AdamC(ctypes.Structure):
         ("bias_c2_sqrt", ctypes.c_float),
         ("enabled", ctypes.c_int32),
         ("step_counter", VP),
+        ("grad_div", VP),
     ]
 
 

@@ -31,8 +31,15 @@ from deeprank2_amd.fused import BatchHandle, launch, param_table
 
 
 class FusedTrainStep:
-    def __init__(self, model, lr=1e-3, weight_decay=1e-5, betas=(0.9, 0.999), eps=1e-8, loss="mse", class_weights=None, process_group=None, max_batch=64):
+    def __init__(self, model, lr=1e-3, weight_decay=1e-5, betas=(0.9, 0.999), eps=1e-8, loss="mse", class_weights=None, process_group=None, max_batch=64, compute_dtype="f32"):
         self.model = model
+        if compute_dtype not in ("f32", "bf16"):
+            msg = f"compute_dtype must be 'f32' or 'bf16' (got {compute_dtype!r})"
+            raise ValueError(msg)
+        if compute_dtype == "bf16" and not getattr(model.fused_spec, "bf16", False):
+            msg = f"{type(model).__name__} has no bf16 compute path (GINet has: BASELINE.json configs[3])"
+            raise ValueError(msg)
+        self.compute_dtype = compute_dtype
         self.spec = model.fused_spec
         self.params = model.ordered_params()
         for p in self.params:
@@ -48,17 +55,24 @@ class FusedTrainStep:
             raise ValueError(msg)
         self.loss = loss
         self.class_weights = None if class_weights is None else torch.as_tensor(class_weights, dtype=torch.float32, device=dev)
+        # host copy, taken once: the per-batch weight sum never syncs with the device
+        self._cw_host = None if class_weights is None else torch.as_tensor(class_weights, dtype=torch.float32).detach().cpu().numpy()
         self.pg = process_group
         self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
         numel = [p.numel() for p in self.params]
-        # gradients and the loss share one buffer: one all-reduce per step (N>1)
-        self.flat = torch.zeros(sum(numel) + 1, dtype=torch.float32, device=dev)
-        self.flat_grad = self.flat[:-1]
+        # gradients, the loss and (weighted CE, N>1) the batch's class-weight sum
+        # share one buffer: one all-reduce per step (N>1)
+        self.flat = torch.zeros(sum(numel) + 2, dtype=torch.float32, device=dev)
+        self.flat_grad = self.flat[:-2]
         self.grads = [g.view_as(p) for g, p in zip(torch.split(self.flat_grad, numel), self.params)]
         self.states = [(torch.zeros_like(p), torch.zeros_like(p)) for p in self.params]
         self.counter = torch.zeros(2, dtype=torch.int64, device=dev)  # [steps done = dropout offset, snapshot]
         self.step_count = 0
-        self.loss_out = self.flat[-1:]
+        self.loss_out = self.flat[-2:-1]
+        self.wsum = self.flat[-1:]
+        # weighted CE with N>1: the graph pass runs unnormalised and Adam divides
+        # by the all-reduced weight sum (dr_adam.grad_div)
+        self.device_div = self.loss == "ce" and self.class_weights is not None and self.world > 1
         self.kernel_events = None  # list -> (start, end) HIP events around each graph pass
         if getattr(model, "_drop_seed", 0) is None:
             model._drop_seed = int(torch.randint(0, 2**62, (1,)).item())
@@ -94,6 +108,7 @@ class FusedTrainStep:
         p.slab = self.slab.data_ptr()
         p.head = self.head.data_ptr()
         p.step_counter = self.counter.data_ptr()
+        p.compute_dtype = _lib.DR_DTYPE_BF16 if self.compute_dtype == "bf16" else _lib.DR_DTYPE_F32
         self._pass = p
         self._pass_nodrop = _lib.PassC.from_buffer_copy(p)
         self._pass_nodrop.use_dropout = _lib.DR_DROPOUT_OFF
@@ -106,19 +121,35 @@ class FusedTrainStep:
         self._adam = a
         self._adam_off = _lib.AdamC.from_buffer_copy(a)
         self._adam_off.enabled = 0
+        self._adam_div = _lib.AdamC.from_buffer_copy(a)
+        self._adam_div.grad_div = self.wsum.data_ptr()
 
     def loss_scale(self, h: BatchHandle, global_batch):
+        """Factor of the per-graph loss terms: 1/B (MSE: 1/(B*out)), or for a
+        weighted CrossEntropyLoss 1/sum_b w[y_b] — computed on the host from the
+        stored targets.  With N>1 that sum spans all ranks: the pass then runs
+        with factor 1, the local sum goes into the all-reduced buffer and Adam
+        divides by the reduced one (``device_div``)."""
         if self.loss == "mse":
             return 1.0 / (global_batch * self.out_dim if self.out_dim > 1 else global_batch)
         if self.class_weights is None:
             return 1.0 / global_batch
+        if self.device_div:
+            return 1.0
         y = h.store.packed.y[h.gids_host].astype(int)
-        wsum = float(self.class_weights.cpu().numpy()[y].sum())
-        if self.world > 1:
-            t = torch.tensor([wsum], dtype=torch.float64)
-            torch.distributed.all_reduce(t, group=self.pg)
-            wsum = float(t.item())
-        return 1.0 / wsum
+        return 1.0 / float(self._cw_host[y].sum())
+
+    def _local_wsum(self, h: BatchHandle):
+        y = h.store.packed.y[h.gids_host].astype(int)
+        self.wsum.fill_(float(self._cw_host[y].sum()))
+
+    def _adam_after_allreduce(self):
+        lib = _lib.load()
+        stream = _lib.stream_ptr(self.device)
+        if self.device_div:
+            _lib.check(lib.dr_reduce_update(self._table, None, None, 0, self._adam_div, None, 1.0, self.loss_out.data_ptr(), stream), "dr_reduce_update")
+        else:
+            _lib.check(lib.dr_reduce_update(self._table, None, None, 0, self._adam, None, 1.0, None, stream), "dr_reduce_update")
 
     def step(self, h: BatchHandle, mask=None, global_batch=None, dropout=True):
         """One training step on the graphs of ``h``; returns (loss [1], out [B,out]) device views.
@@ -156,8 +187,10 @@ class FusedTrainStep:
             _lib.check(lib.dr_reduce_update(self._table, slab, head, h.B, self._adam, lpg, scale, lout, stream), "dr_reduce_update")
         else:
             _lib.check(lib.dr_reduce_update(self._table, slab, head, h.B, self._adam_off, lpg, scale, lout, stream), "dr_reduce_update")
+            if self.device_div:
+                self._local_wsum(h)
             torch.distributed.all_reduce(self.flat, group=self.pg)
-            _lib.check(lib.dr_reduce_update(self._table, None, None, h.B, self._adam, None, 1.0, None, _lib.stream_ptr(self.device)), "dr_reduce_update")
+            self._adam_after_allreduce()
         return self.loss_out, self.out[: h.B]
 
     def _layered_step(self, h: BatchHandle, scale, dropout):
@@ -187,8 +220,10 @@ class FusedTrainStep:
             self.counter[1].copy_(self.counter[0])  # the step snapshot the graph pass would have taken
         self.step_count += 1
         if self.pg is not None:
+            if self.device_div:
+                self._local_wsum(h)
             torch.distributed.all_reduce(self.flat, group=self.pg)
-        _lib.check(_lib.load().dr_reduce_update(self._table, None, None, h.B, self._adam, None, 1.0, None, _lib.stream_ptr(self.device)), "dr_reduce_update")
+        self._adam_after_allreduce()
         return self.loss_out, self.out[: h.B]
 
     # ---- torch.optim.Adam-compatible optimizer state (checkpoints) ----

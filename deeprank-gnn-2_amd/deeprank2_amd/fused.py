@@ -242,6 +242,7 @@ class FusedSpec:
     large: Callable | None = None  # (handle, weights struct, pass struct) for graphs beyond one workgroup's LDS
     run: Callable | None = None  # (handle, weights struct, pass struct): replaces the default entry call
     layers: Callable | None = None  # (model, batch tensors, training) -> out: layer-level path (layered.py) for batches beyond LDS
+    bf16: bool = False  # dr_pass.compute_dtype = DR_DTYPE_BF16 supported (runs on the large-graph path)
 
 
 def vanilla_fused_scratch_floats(n, e, fe):
@@ -292,6 +293,15 @@ def launch(spec: FusedSpec, h: BatchHandle, w, p):
     the batch's largest graph fits in LDS, else the model's large-graph path."""
     if spec.run is not None:
         spec.run(h, w, p)
+        return
+    if p.compute_dtype == _lib.DR_DTYPE_BF16:
+        if not spec.bf16 or spec.large is None:
+            msg = f"{spec.entry}: no bf16 compute path"
+            raise RuntimeError(msg)
+        if h.store.x_bf16 is None:
+            msg = "bf16 compute needs the store's bf16 copy of x: GraphStore(packed, device, dtype='bf16')"
+            raise RuntimeError(msg)
+        spec.large(h, w, p)  # the tile kernel holds the bf16 node GEMM, for every graph size
         return
     lds = lds_for(spec, h, p.out_dim)
     if lds <= LDS_MAX and not (h.force_large and spec.large is not None):

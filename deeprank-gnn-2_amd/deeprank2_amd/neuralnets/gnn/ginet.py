@@ -166,7 +166,7 @@ def _large(h, w, p):
     _lib.check(rc, "dr_ginet_large_pass")
 
 
-SPEC = FusedSpec(PARAM_NAMES, recipe, slab_stride, head_stride, "dr_ginet_graph_pass", weights_c, _lds, dropout=0.4, large=_large)
+SPEC = FusedSpec(PARAM_NAMES, recipe, slab_stride, head_stride, "dr_ginet_graph_pass", weights_c, _lds, dropout=0.4, large=_large, bf16=True)
 
 
 def graph_pass(h: BatchHandle, params, out_dim, flags, **kw):

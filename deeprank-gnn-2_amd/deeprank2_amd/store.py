@@ -272,8 +272,13 @@ assert DESC_DTYPE.itemsize == 64  # dr_graph_desc
 class GraphStore:
     """Device copy of a :class:`PackedGraphs` (all arrays live in HBM)."""
 
-    def __init__(self, packed: PackedGraphs, device):
+    def __init__(self, packed: PackedGraphs, device, dtype: str = "f32"):
         import torch  # noqa: PLC0415
+
+        if dtype not in ("f32", "bf16"):
+            msg = f"dtype must be 'f32' or 'bf16' (got {dtype!r})"
+            raise ValueError(msg)
+        self.dtype = dtype
 
         self.packed = packed
         self.device = torch.device(device)
@@ -286,6 +291,14 @@ class GraphStore:
         xp = np.zeros((p.x.shape[0], self.x_stride), dtype=np.float32)
         xp[:, : p.n_feat] = p.x
         self.x = t(xp)
+        # bf16 compute (dr_pass.compute_dtype): a bf16 copy of x, rows padded to
+        # 8 values (16 bytes), rounded to nearest even by torch
+        self.x_bf16_stride = (p.n_feat + 7) & ~7
+        self.x_bf16 = None
+        if dtype == "bf16":
+            xb = torch.zeros((p.x.shape[0], self.x_bf16_stride), dtype=torch.bfloat16)
+            xb[:, : p.n_feat] = torch.from_numpy(np.ascontiguousarray(p.x, dtype=np.float32)).to(torch.bfloat16)
+            self.x_bf16 = xb.to(self.device)
         self.node_off = t(p.node_off)
         self.edge_off = t(p.edge_off)
         if np.diff(p.node_off).max() > 65535:
@@ -368,6 +381,9 @@ class GraphStore:
             for name in ("x", "node_off", "edge_off", "col_off", "rowptr", "col", "t_rowptr", "t_col", "k0_off", "m0_ptr", "m0_idx", "p1_off", "p1_rowptr", "p1_col", "p1t_rowptr", "p1t_col", "k1_off", "m1_ptr", "m1_idx", "y", "ea", "t_eid", "p1_ea", "p1t_pid"):
                 setattr(s, name, getattr(self, name).data_ptr())
             s.n_edge_feat = self.n_edge_feat
+            if self.x_bf16 is not None:
+                s.x_bf16 = self.x_bf16.data_ptr()
+                s.x_bf16_stride = self.x_bf16_stride
             self._c = s
         return self._c
 

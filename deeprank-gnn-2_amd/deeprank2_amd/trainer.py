@@ -132,7 +132,7 @@ class Trainer:
                     self._precluster(self.dataset_train)
                 if self.dataset_val is None:
                     _log.warning("No validation dataset given. Randomly splitting training set in training set and validation set.")
-                    self.dataset_train, self.dataset_val = _divide_dataset(self.dataset_train, splitsize=self.val_size)
+                    self.dataset_train, self.dataset_val = _divide_dataset(self.dataset_train, splitsize=self.val_size, process_group=self.process_group)
                 elif precluster:
                     self._precluster(self.dataset_val)
                 if self.dataset_test is not None and precluster:
@@ -246,6 +246,11 @@ class Trainer:
         d0 = dataset.get(0)
         target_shape = d0.y.shape[0] if d0.y is not None else None
         self.model = self.neuralnet(d0.num_features, self.output_shape, len(dataset.edge_features)).to(self.device)
+        if self.process_group is not None:  # every replica starts from rank 0's initialisation
+            src_rank = torch.distributed.get_global_rank(self.process_group, 0)
+            with torch.no_grad():
+                for t in [*self.model.parameters(), *self.model.buffers()]:
+                    torch.distributed.broadcast(t.data, src_rank, group=self.process_group)
         for e in self._output_exporters:
             if not e.is_compatible_with(self.output_shape, target_shape):
                 msg = f"Output exporter of type {type(e)}\n\tis not compatible with output shape {self.output_shape}\n\tand target shape {target_shape}."
@@ -380,8 +385,9 @@ class Trainer:
         self.data_type = type(self.dataset_train)
         self.batch_size_train = batch_size
         self.shuffle = shuffle
-        self.train_loader = DataLoader(self.dataset_train, batch_size=batch_size, shuffle=shuffle, num_workers=num_workers, pin_memory=self.cuda)
-        self.valid_loader = DataLoader(self.dataset_val, batch_size=batch_size, shuffle=shuffle, num_workers=num_workers, pin_memory=self.cuda) if self.dataset_val is not None else None
+        pg = self.process_group
+        self.train_loader = DataLoader(self.dataset_train, batch_size=batch_size, shuffle=shuffle, num_workers=num_workers, pin_memory=self.cuda, process_group=pg)
+        self.valid_loader = DataLoader(self.dataset_val, batch_size=batch_size, shuffle=shuffle, num_workers=num_workers, pin_memory=self.cuda, process_group=pg) if self.dataset_val is not None else None
         if self.valid_loader is None:
             _log.warning("Training data will be used both for learning and model selection, which may lead to overfitting.")
 
@@ -467,6 +473,9 @@ class Trainer:
                 if self.process_group is not None:
                     pred = _gather_rows(pred, b, self.process_group)
                 pred, y = self._format_output(pred, ds._targets_of(idx))  # noqa: SLF001
+            elif self.process_group is not None:
+                pred, y, loss = self._generic_ddp_step(ds, idx)
+                loss_sum += loss.double() * b
             else:
                 batch = ds.batch(idx).to(dev)
                 self.optimizer.zero_grad()
@@ -487,6 +496,47 @@ class Trainer:
         self._output_exporters.process(pass_name, epoch_number, names, out_l, tgt_l, epoch_loss)
         _log.info(f"{pass_name} loss {epoch_loss} | time {dt}")
         return epoch_loss
+
+    def _generic_ddp_step(self, ds, idx):
+        """Any optimizer / loss outside the fused step, one process per GPU:
+        each rank runs the model on its contiguous shard, its mean loss is
+        weighted by the shard's share of the batch (graph count, or the
+        class-weight sum for a weighted CrossEntropyLoss), the gradients and
+        that loss are SUM-all-reduced in one flat buffer, then every rank
+        takes the same optimizer step.  Returns the global predictions,
+        targets and loss."""
+        pg = self.process_group
+        local = self._local(idx)
+        batch = ds.batch(local).to(self.device)
+        self.optimizer.zero_grad()
+        pred = self.model(batch)
+        pred_l, y_l = self._format_output(pred, batch.y)
+        y_all = ds._targets_of(idx)  # noqa: SLF001
+        w = getattr(self.lossfunction, "weight", None)
+        if w is not None and self.task == CLASSIF:
+            cls = torch.tensor([self.classes_to_index[int(v)] for v in y_all.tolist()])
+            wh = w.detach().cpu()
+            total = float(wh[cls].sum())  # the weighted mean's denominator over the global batch
+            local_pos = shard_contiguous(np.arange(len(idx)), torch.distributed.get_rank(pg), torch.distributed.get_world_size(pg))
+            frac = float(wh[cls[local_pos]].sum()) / total if total else 0.0
+        else:
+            frac = len(local) / len(idx)
+        loss = self.lossfunction(pred_l, y_l) * frac if len(local) else pred.sum() * 0.0
+        loss.backward()
+        params = [p for p in self.model.parameters() if p.requires_grad]
+        flat = torch.cat([*(p.grad.reshape(-1) if p.grad is not None else torch.zeros(p.numel(), device=p.device) for p in params), loss.detach().reshape(1)])
+        torch.distributed.all_reduce(flat, group=pg)
+        off = 0
+        for p in params:
+            n = p.numel()
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            p.grad.copy_(flat[off:off + n].view_as(p))
+            off += n
+        self.optimizer.step()
+        pred_all = _gather_rows(pred.detach().contiguous(), len(idx), pg)
+        pred_all, y = self._format_output(pred_all, y_all)
+        return pred_all, y, flat[-1]
 
     def _eval(self, loader: DataLoader, epoch_number: int, pass_name: str):
         """trainer.py:726-795: forward passes, loss per batch on the device."""
@@ -615,8 +665,9 @@ def _gather_rows(local, b, pg):
     return torch.cat(bufs)
 
 
-def _divide_dataset(dataset, splitsize=None):
-    """trainer.py:961-1004: random split into (main, split)."""
+def _divide_dataset(dataset, splitsize=None, process_group=None):
+    """trainer.py:961-1004: random split into (main, split).  With a process
+    group every rank takes rank 0's split."""
     if splitsize is None:
         splitsize = 0.25
     full = len(dataset)
@@ -634,4 +685,8 @@ def _divide_dataset(dataset, splitsize=None):
         return dataset, None
     idx = np.arange(full)
     np.random.default_rng().shuffle(idx)
+    if process_group is not None and torch.distributed.get_world_size(process_group) > 1:
+        box = [idx]
+        torch.distributed.broadcast_object_list(box, src=torch.distributed.get_global_rank(process_group, 0), group=process_group)
+        idx = np.asarray(box[0])
     return dataset.subset_entries(idx[n_split:]), dataset.subset_entries(idx[:n_split])

@@ -106,6 +106,11 @@ typedef struct dr_graph_store {
   int32_t pad0;
   const float* p1_ea;        /* [P1_all, max(Fe,1)] pooled edge_attr: sums over merged edges (PyG coalesce) */
   const int32_t* p1t_pid;    /* [P1_all] pooled transposed slot -> pooled CSR slot (local) */
+  const uint16_t* x_bf16;    /* optional [N_all, x_bf16_stride] bf16 copy of x (round to nearest even),
+                                16-byte rows, pad zero; read instead of x by passes with
+                                compute_dtype DR_DTYPE_BF16 (BASELINE configs[3])           */
+  int32_t x_bf16_stride;     /* multiple of 8, >= F                                */
+  int32_t pad1;
 } dr_graph_store;
 
 /* One mini-batch slot: where graph `gid` lives in the store (64 bytes, so a
@@ -145,6 +150,9 @@ typedef struct dr_ginet_weights {
 #define DR_DROPOUT_MASK 1  /* keep mask given in pass->mask        */
 #define DR_DROPOUT_HASH 2  /* counter-based hash, see dr_dropout_mask */
 
+#define DR_DTYPE_F32 0
+#define DR_DTYPE_BF16 1
+
 typedef struct dr_pass {
   int32_t flags;        /* DR_PASS_* bitmask                                   */
   int32_t out_dim;      /* fc2 rows                                            */
@@ -155,7 +163,10 @@ typedef struct dr_pass {
   uint64_t drop_seed;   /* DR_DROPOUT_HASH: keep[b,r] = u(seed, offset, 128b+r) >= p */
   uint64_t drop_offset;
   float loss_scale;     /* 1/B (MSE) or 1/sum(w_y) (CE)                        */
-  int32_t pad0;
+  int32_t compute_dtype;/* DR_DTYPE_F32, or DR_DTYPE_BF16: the conv1 node GEMM takes bf16
+                           operands (x from store->x_bf16, Z = A x rounded to bf16, W1
+                           rounded to bf16) on the bf16 MFMA with fp32 accumulate; all
+                           other arithmetic, the outputs and the gradients stay fp32 (GINet) */
   const uint8_t* mask;  /* [B,128] keep mask (DR_DROPOUT_MASK)                 */
   const float* class_w; /* [out] CE class weights or NULL                      */
   float* out;           /* [B,out] predictions (FORWARD)                       */
@@ -361,6 +372,12 @@ typedef struct dr_adam {
   int64_t* step_counter; /* optional device [2] (see dr_pass): step = counter[1]+1,
                             bias corrections computed on the device, and (when enabled)
                             counter[0] := step; overrides bias_c1 / bias_c2_sqrt    */
+  const float* grad_div; /* optional device scalar, Adam-only calls (slab NULL): every
+                            gradient is divided by it (and written back to grad) and so
+                            is loss_out[0].  Weighted CrossEntropyLoss under data
+                            parallelism: the weighted mean's denominator
+                            (trainer.py:688, nn.CrossEntropyLoss(weight)) is only known
+                            after the all-reduce, so it travels in the reduced buffer  */
 } dr_adam;
 
 /* How one parameter's gradient is assembled from the per-graph partials the

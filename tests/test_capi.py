@@ -38,12 +38,12 @@ def test_version_and_lds_query_are_host_only():
 
 def test_struct_layouts_match_header():
     # 4 int32 + 20 pointers; 8 pointers; 4 int32 + 2 float + 2 uint64 + float/int32 + 7 pointers
-    assert ctypes.sizeof(_lib.GraphStoreC) == 16 + 22 * 8 + 8 + 2 * 8
+    assert ctypes.sizeof(_lib.GraphStoreC) == 16 + 22 * 8 + 8 + 2 * 8 + 8 + 8  # ... x_bf16, x_bf16_stride + pad
     assert ctypes.sizeof(_lib.GinetWeightsC) == 8 * 8
     assert ctypes.sizeof(_lib.FoutWeightsC) == 10 * 8
     assert ctypes.sizeof(_lib.LargePlanC) == 3 * 8 + 16 + 3 * 8 + 7 * 8
     assert ctypes.sizeof(_lib.PassC) == 16 + 8 + 16 + 8 + 9 * 8
-    assert ctypes.sizeof(_lib.AdamC) == 32 + 8
+    assert ctypes.sizeof(_lib.AdamC) == 32 + 8 + 8  # + grad_div
     assert ctypes.sizeof(_lib.MclGraphsC) == 10 * 8
     assert ctypes.sizeof(_lib.ParamTableC) == 4 * 24 * 8 + 24 * 4 + 24 * 16 + 16
 

@@ -95,6 +95,31 @@ def test_shuffle_covers_every_graph_once(synth_file):
     assert len(DataLoader(ds, batch_size=2, drop_last=True)) == 3
 
 
+class _Range:
+    def __init__(self, n):
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+
+@pytest.mark.parametrize("shuffle", [True, False])
+@pytest.mark.parametrize(("n", "bs"), [(7, 2), (64, 8), (1, 4)])
+def test_loader_rng_consumption_matches_torch_dataloader(n, bs, shuffle):
+    """Same batches and the same torch RNG state afterwards as
+    torch.utils.data.DataLoader (which PyG's loader subclasses,
+    trainer.py:541-547) under one torch.manual_seed, two epochs in a row."""
+    torch.manual_seed(1234)
+    ref = torch.utils.data.DataLoader(list(range(n)), batch_size=bs, shuffle=shuffle)
+    want = [[b.tolist() for b in ref] for _ in range(2)]
+    state = torch.random.get_rng_state()
+    torch.manual_seed(1234)
+    dl = DataLoader(_Range(n), batch_size=bs, shuffle=shuffle)
+    got = [[list(map(int, b)) for b in dl.batches()] for _ in range(2)]
+    assert got == want
+    assert torch.equal(torch.random.get_rng_state(), state)
+
+
 def test_subset_order_and_target_filter(synth_file):
     path, graphs, names = synth_file
     ds = _ds(path, subset=[names[5], names[1], "missing"])

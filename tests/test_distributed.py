@@ -78,3 +78,57 @@ def test_gloo_world2_allreduced_gradients_equal_global_batch(tmp_path, model_nam
     mp.spawn(_rank_main, args=(2, _free_port(), model_name, out), nprocs=2, join=True)
     z = np.load(out)
     np.testing.assert_allclose(z["ddp"], z["ref"], rtol=1e-5, atol=1e-6)
+
+
+class _FakeDataset:
+    def __init__(self, n, entries=None):
+        self.entries = list(range(n)) if entries is None else entries
+
+    def __len__(self):
+        return len(self.entries)
+
+    def subset_entries(self, idx):
+        return _FakeDataset(0, [self.entries[i] for i in idx])
+
+
+def _trainer_rank_main(rank, world, port, out_path):
+    """Trainer's data-parallel bookkeeping on one rank: the validation split and
+    every epoch's order come from rank 0 (the ranks' RNGs are seeded apart on
+    purpose), and the contiguous shards of each global batch cover it once."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from deeprank2_amd.loader import DataLoader
+    from deeprank2_amd.trainer import _divide_dataset
+
+    pg = dist.group.WORLD
+    torch.manual_seed(100 + rank)
+    main, split = _divide_dataset(_FakeDataset(23), splitsize=0.25, process_group=pg)
+    dl = DataLoader(main, batch_size=4, shuffle=True, process_group=pg)
+    epochs = []
+    for _ in range(3):
+        seen = []
+        for idx in dl.batches():
+            seen.append(shard_contiguous(np.asarray(idx), rank, world).tolist())
+        epochs.append(seen)
+    box = [None] * world
+    dist.all_gather_object(box, {"main": main.entries, "split": split.entries, "epochs": epochs})
+    if rank == 0:
+        import json
+
+        with open(out_path, "w") as f:
+            json.dump(box, f)
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_trainer_split_and_epoch_order_from_rank0(tmp_path):
+    import json
+
+    out = str(tmp_path / "t.json")
+    mp.spawn(_trainer_rank_main, args=(2, _free_port(), out), nprocs=2, join=True)
+    r0, r1 = json.load(open(out))
+    assert r0["main"] == r1["main"] and r0["split"] == r1["split"]
+    assert sorted(r0["main"] + r0["split"]) == list(range(23))
+    for e0, e1 in zip(r0["epochs"], r1["epochs"]):
+        visited = [i for b0, b1 in zip(e0, e1) for i in b0 + b1]
+        assert sorted(visited) == list(range(len(r0["main"])))  # every graph once per epoch
+    assert r0["epochs"][0] != r0["epochs"][1]  # reshuffled per epoch

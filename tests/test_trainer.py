@@ -105,3 +105,22 @@ def test_early_stopping_rules():
     assert not es.early_stop
     es(2, 1.0, 0.5)
     assert es.early_stop
+
+
+def _stop_epoch(**kw):
+    """Known answers of the reference's tests/utils/test_earlystopping.py
+    (its loss sequences; min_epoch=0)."""
+    val = [3, 2, 1, 2, 0.5, 2, 3, 4, 5, 6, 7]
+    train = [3, 2, 1, 2, 0.5, 2, 3, 4, 5, 1, 7]
+    es = EarlyStopping(min_epoch=0, trace_func=lambda *_: None, **kw)
+    for ep, v in enumerate(val):
+        es(ep, v, train[ep])
+        if es.early_stop:
+            return ep
+    return None
+
+
+def test_early_stopping_reference_known_answers():
+    assert _stop_epoch(patience=3) == 7
+    assert _stop_epoch(patience=3, delta=1) == 5
+    assert _stop_epoch(maxgap=1) == 9
