@@ -771,6 +771,45 @@ __device__ __forceinline__ int lower_bound_lds(const int* v, int lo, int hi, int
   return lo;
 }
 
+// The tile's partial depth-0 max per (cluster, channel) of H (LDS, stride
+// 32, rows r0..r0+nrows-1): strict '>' in node order, first max wins, NaN never
+// enters (torch_scatter scatter_max, community_pooling.py:209).  Published by
+// 64-bit atomic max keys or per-tile partials (dr_large_plan).
+__device__ __forceinline__ void tile_partial_max(const dr_large_plan& pl, const float* sH, const int* sm0i,
+                                                 const int* sm0p, int* srng, bool compact, int tile, int b, int K0,
+                                                 int N, int r0, int nrows) {
+  const int tid = threadIdx.x;
+  // each cluster's members inside this tile: a sub-run of its ascending list
+  for (int k = tid; k < K0; k += NTA) {
+    const int mb = sm0p[k], me = sm0p[k + 1];
+    srng[2 * k] = compact ? mb : lower_bound_lds(sm0i, mb, me, r0);
+    srng[2 * k + 1] = compact ? me : lower_bound_lds(sm0i, mb, me, r0 + nrows);
+  }
+  __syncthreads();
+  for (int p = tid; p < K0 * 32; p += NTA) {
+    const int k = p >> 5, ch = p & 31;
+    float best = LOWEST;
+    int arg = N;
+    for (int m = srng[2 * k]; m < srng[2 * k + 1]; ++m) {
+      const int i = sm0i[m];
+      const float v = sH[(i - r0) * 32 + ch];
+      if (v > best) {
+        best = v;
+        arg = i;
+      }
+    }
+    if (pl.part_key) {  // order-free combine over the graph's tiles (see dr_large_plan.part_key)
+      if (best > LOWEST)
+        atomicMax(reinterpret_cast<unsigned long long*>(pl.part_key) + ((int64_t)b * pl.k0_max + k) * 32 + ch,
+                  ((unsigned long long)__float_as_uint(best) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)arg));
+    } else {
+      const int64_t o = ((int64_t)tile * pl.k0_max + k) * 32 + ch;
+      pl.part_val[o] = best;
+      pl.part_arg[o] = arg;
+    }
+  }
+}
+
 // One tile of TR nodes: Z rows (CSR gather over HBM/L2), H = relu(Z W^T) on
 // MFMA, and the tile's partial depth-0 max per (cluster, channel).
 __global__ void __launch_bounds__(NTA) ginet_large_conv1_kernel(LargeArgs la) {
@@ -925,36 +964,215 @@ __global__ void __launch_bounds__(NTA) ginet_large_conv1_kernel(LargeArgs la) {
       }
     }
   }
-  // each cluster's members inside this tile: a sub-run of its ascending list
-  for (int k = tid; k < K0; k += NTA) {
-    const int mb = sm0p[k], me = sm0p[k + 1];
-    srng[2 * k] = compact ? mb : lower_bound_lds(sm0i, mb, me, r0);
-    srng[2 * k + 1] = compact ? me : lower_bound_lds(sm0i, mb, me, r0 + nrows);
+  tile_partial_max(pl, sH, sm0i, sm0p, srng, compact, tile, b, K0, N, r0, nrows);
+}
+
+// ---- bf16 compute (dr_pass.compute_dtype == DR_DTYPE_BF16, BASELINE configs[3]) ----
+// Same tile as ginet_large_conv1_kernel with the node GEMM on bf16 operands:
+// X rows come from the store's bf16 copy (half the bytes of the halo staging
+// and of the gather's LDS reads), Z = A X is accumulated in fp32 and rounded
+// to bf16 (its LDS operand copy and the HBM workspace the tail reads for
+// dW1), W1 is rounded to bf16, and H = relu(Z W1^T) comes from
+// v_mfma_f32_16x16x32_bf16 with fp32 accumulation (one MFMA per 16x16 output
+// tile and 32 of K).  H, the pooling and everything after it stay fp32.
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) {  // round to nearest even (torch's .to(bfloat16))
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);  // quiet NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+__device__ __forceinline__ uint2 pack4bf(float a, float b, float c, float d) {
+  return make_uint2((uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16), (uint32_t)f2bf(c) | ((uint32_t)f2bf(d) << 16));
+}
+__device__ __forceinline__ float4 unpack4bf(uint2 v) {
+  return make_float4(__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u), __uint_as_float(v.y << 16),
+                     __uint_as_float(v.y & 0xffff0000u));
+}
+
+struct ConvCarveB {  // offsets in 4-byte words; bf16 row strides in bf16 elements
+  int KPB, ZSB, XSB, w1, z, h, m0i, m0p, rng, xh, hid, lcol, trp, total;
+};
+
+__host__ __device__ inline ConvCarveB conv_carve_bf16(int N, int F, int K0, int HM, int EM) {
+  ConvCarveB c;
+  c.KPB = (F + 31) & ~31;  // K padded to whole 32-deep MFMA steps (zeros)
+  c.ZSB = c.KPB + 8;       // 16-byte row shift: the 16 rows of an operand read start on distinct bank quads
+  c.XSB = (F + 7) & ~7;    // the store's x_bf16_stride (16-byte rows)
+  int o = 0;
+  c.w1 = o;
+  o += r4(32 * c.ZSB / 2);
+  c.z = o;
+  o += r4(TR * c.ZSB / 2);
+  c.h = o;
+  o += TR * 32;  // fp32 H
+  c.m0i = o;
+  o += r4(HM ? TR : N);
+  c.m0p = o;
+  o += r4(K0 + 1);
+  c.rng = o;
+  o += r4(2 * K0);
+  c.xh = o;  // halo X rows, bf16, XSB stride
+  o += HM ? r4(HM * c.XSB / 2) : 0;
+  c.hid = o;
+  o += r4(HM);
+  c.trp = o;
+  o += HM ? r4(TR + 1) : 0;
+  c.lcol = o;
+  o += HM ? r4((EM + 8) / 2) : 0;
+  c.total = o;
+  return c;
+}
+
+__global__ void __launch_bounds__(NTA) ginet_large_conv1_bf16_kernel(LargeArgs la) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const GinetArgs& a = la.g;
+  const dr_large_plan& pl = la.plan;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tile = blockIdx.x;
+  const int b = pl.tile_slot[tile];
+  const int t = tile - pl.tile_first[b];
+  const dr_graph_desc d = a.descs[b];
+  const dr_graph_store& s = a.s;
+  const int g = d.gid;
+  const int64_t n0 = d.node0, ec0 = d.col0, k00 = d.k0;
+  const int N = d.n_nodes, K0 = d.n_k0, F = s.n_feat;
+  const int TRr = pl.tile_rows;
+  const int r0 = t * TRr, nrows = min(TRr, N - r0);
+  const ConvCarveB c = conv_carve_bf16(N, F, K0, pl.halo_max, 0);
+  const int KPB = c.KPB, ZSB = c.ZSB, XSB = s.x_bf16_stride;
+  uint16_t* sW = reinterpret_cast<uint16_t*>(lds + c.w1);
+  uint16_t* sZ = reinterpret_cast<uint16_t*>(lds + c.z);
+  float* sH = lds + c.h;
+  int* sm0i = reinterpret_cast<int*>(lds + c.m0i);
+  int* sm0p = reinterpret_cast<int*>(lds + c.m0p);
+  int* srng = reinterpret_cast<int*>(lds + c.rng);
+  const uint16_t* X = s.x_bf16 + n0 * (int64_t)XSB;
+  uint16_t* zg = reinterpret_cast<uint16_t*>(pl.z) + (int64_t)pl.z_row0[b] * XSB;
+
+  const bool compact = pl.tile_members != nullptr;
+  if (compact) {
+    drk::dma_words<NTA>(sm0i, pl.tile_members + (int64_t)tile * TRr, nrows);
+    drk::dma_words<NTA>(sm0p, pl.tile_mptr + (int64_t)tile * (pl.k0_max + 1), K0 + 1);
+  } else {
+    drk::dma_words<NTA>(sm0i, s.m0_idx + n0, N);
+    drk::dma_words<NTA>(sm0p, s.m0_ptr + k00 + g, K0 + 1);
   }
-  __syncthreads();
-  // partial scatter_max (strict '>', first max wins, NaN never enters)
-  for (int p = tid; p < K0 * 32; p += NTA) {
-    const int k = p >> 5, ch = p & 31;
-    float best = LOWEST;
-    int arg = N;
-    for (int m = srng[2 * k]; m < srng[2 * k + 1]; ++m) {
-      const int i = sm0i[m];
-      const float v = sH[(i - r0) * 32 + ch];
-      if (v > best) {
-        best = v;
-        arg = i;
+  for (int p = tid; p < 32 * KPB; p += NTA) {  // [W1; W1e] in bf16, K zero-padded to KPB
+    const int r = p / KPB, k = p - r * KPB;
+    float v = 0.f;
+    if (k < F) v = (r < 16) ? a.w.w1[r * F + k] : a.w.w1e[(r - 16) * F + k];
+    sW[r * ZSB + k] = f2bf(v);
+  }
+  for (int p = tid; p < TRr * (KPB - XSB); p += NTA) {  // Z pad columns (X's own pad is zero)
+    const int r = p / (KPB - XSB);
+    sZ[r * ZSB + XSB + (p - r * (KPB - XSB))] = 0;
+  }
+  // Z = A X for the tile's rows: 8 lanes per row, 4 bf16 (8 bytes) per lane
+  // and edge, summed in fp32 in CSR order; rounded to bf16 once per row.
+  const int nch = XSB >> 2, sub = tid & 7;
+  if (pl.halo_ids) {
+    int* strp = reinterpret_cast<int*>(lds + c.trp);
+    int* shid = reinterpret_cast<int*>(lds + c.hid);
+    uint16_t* slcol = reinterpret_cast<uint16_t*>(lds + c.lcol);
+    uint16_t* sXh = reinterpret_cast<uint16_t*>(lds + c.xh);
+    const int h0 = pl.halo_off[tile], H = pl.halo_off[tile + 1] - h0;
+    const int l0 = pl.lcol_off[tile];
+    drk::dma_words<NTA>(strp, s.rowptr + n0 + g + r0, nrows + 1);
+    drk::dma_words<NTA>(shid, pl.halo_ids + h0, H);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int ebase = strp[0];
+    drk::dma_x4<NTA>(slcol, pl.lcol + l0, (strp[nrows] - ebase + 7) / 8);
+    {  // halo rows: 16-byte DMA lanes, XSB/8 per row
+      const int n16 = XSB >> 3, tot = H * n16;
+      const int wv = __builtin_amdgcn_readfirstlane(wave);
+      for (int base = wv * 64; base < tot; base += NTA)
+        if (base + lane < tot) {
+          const int hr = (base + lane) / n16, q = base + lane - hr * n16;
+          __builtin_amdgcn_global_load_lds(DRK_AS1(X + (int64_t)shid[hr] * XSB + q * 8), DRK_AS3(sXh + base * 8), 16, 0, 0);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int r = tid >> 3; r < nrows; r += NTA / 8) {
+      const int eb = strp[r] - ebase, ee = strp[r + 1] - ebase;
+      for (int ch = sub; ch < nch; ch += 8) {
+        const int c4 = ch * 4;
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        int e = eb;
+        for (; e + 4 <= ee; e += 4) {
+          int e1 = e + 1, e2 = e + 2, e3 = e + 3;
+          asm volatile("" : "+v"(e1), "+v"(e2), "+v"(e3));
+          const int j0 = slcol[e], j1 = slcol[e1], j2 = slcol[e2], j3 = slcol[e3];
+          const uint2 v0 = *reinterpret_cast<const uint2*>(&sXh[__umul24(j0, XSB) + c4]);
+          const uint2 v1 = *reinterpret_cast<const uint2*>(&sXh[__umul24(j1, XSB) + c4]);
+          const uint2 v2 = *reinterpret_cast<const uint2*>(&sXh[__umul24(j2, XSB) + c4]);
+          const uint2 v3 = *reinterpret_cast<const uint2*>(&sXh[__umul24(j3, XSB) + c4]);
+          acc = f4add(f4add(f4add(f4add(acc, unpack4bf(v0)), unpack4bf(v1)), unpack4bf(v2)), unpack4bf(v3));
+        }
+        for (; e < ee; ++e) acc = f4add(acc, unpack4bf(*reinterpret_cast<const uint2*>(&sXh[__umul24((int)slcol[e], XSB) + c4])));
+        const uint2 zb = pack4bf(acc.x, acc.y, acc.z, acc.w);
+        *reinterpret_cast<uint2*>(&sZ[r * ZSB + c4]) = zb;
+        *reinterpret_cast<uint2*>(zg + (int64_t)(r0 + r) * XSB + c4) = zb;
       }
     }
-    if (pl.part_key) {  // order-free combine over the graph's tiles (see dr_large_plan.part_key)
-      if (best > LOWEST)
-        atomicMax(reinterpret_cast<unsigned long long*>(pl.part_key) + ((int64_t)b * pl.k0_max + k) * 32 + ch,
-                  ((unsigned long long)__float_as_uint(best) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)arg));
-    } else {
-      const int64_t o = ((int64_t)tile * pl.k0_max + k) * 32 + ch;
-      pl.part_val[o] = best;
-      pl.part_arg[o] = arg;
+  } else {
+    const int* rp = s.rowptr + n0 + g;
+    const uint16_t* col = s.col + ec0;
+    for (int r = tid >> 3; r < nrows; r += NTA / 8) {
+      const int i = r0 + r;
+      const int eb = rp[i], ee = rp[i + 1];
+      for (int ch = sub; ch < nch; ch += 8) {
+        const int c4 = ch * 4;
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        int e = eb;
+        for (; e + 4 <= ee; e += 4) {
+          const int j0 = col[e], j1 = col[e + 1], j2 = col[e + 2], j3 = col[e + 3];
+          const uint2 v0 = *reinterpret_cast<const uint2*>(X + (int64_t)j0 * XSB + c4);
+          const uint2 v1 = *reinterpret_cast<const uint2*>(X + (int64_t)j1 * XSB + c4);
+          const uint2 v2 = *reinterpret_cast<const uint2*>(X + (int64_t)j2 * XSB + c4);
+          const uint2 v3 = *reinterpret_cast<const uint2*>(X + (int64_t)j3 * XSB + c4);
+          acc = f4add(f4add(f4add(f4add(acc, unpack4bf(v0)), unpack4bf(v1)), unpack4bf(v2)), unpack4bf(v3));
+        }
+        for (; e < ee; ++e) acc = f4add(acc, unpack4bf(*reinterpret_cast<const uint2*>(X + (int64_t)col[e] * XSB + c4)));
+        const uint2 zb = pack4bf(acc.x, acc.y, acc.z, acc.w);
+        *reinterpret_cast<uint2*>(&sZ[r * ZSB + c4]) = zb;
+        *reinterpret_cast<uint2*>(zg + (int64_t)i * XSB + c4) = zb;
+      }
     }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // H = relu(Z [W1; W1e]^T): lane l holds Z[row l&15][k 8(l>>4)..+7] and
+  // W[col l&15][same k] (16-byte LDS reads); C row (l>>4)*4+r, col l&15.
+  {
+    const int li = lane & 15, kq = lane >> 4;
+    for (int tt = wave; tt * 16 < nrows; tt += NTA / 64) {
+      const int q0 = tt * 16;
+      const int ar = min(q0 + li, nrows - 1);
+      floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < KPB; k += 32) {
+        const bf16x8 av = *reinterpret_cast<const bf16x8*>(&sZ[ar * ZSB + k + 8 * kq]);
+        const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(&sW[li * ZSB + k + 8 * kq]);
+        const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(&sW[(16 + li) * ZSB + k + 8 * kq]);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b0, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b1, acc1, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = q0 + kq * 4 + r;
+        if (row < nrows) {
+          sH[row * 32 + li] = relu_keepnan(acc0[r]);
+          sH[row * 32 + 16 + li] = relu_keepnan(acc1[r]);
+        }
+      }
+    }
+  }
+  tile_partial_max(pl, sH, sm0i, sm0p, srng, compact, tile, b, K0, N, r0, nrows);
 }
 
 struct TailCarve {
@@ -1086,6 +1304,13 @@ __global__ void __launch_bounds__(NT) ginet_large_tail_kernel(LargeArgs la) {
   __syncthreads();
   STAMP(2);
   STAMP(3);
+  if (a.p.compute_dtype == DR_DTYPE_BF16) {  // the bf16 Z the conv1 GEMM consumed
+    const int XSB = s.x_bf16_stride;
+    const uint16_t* zb = reinterpret_cast<const uint16_t*>(pl.z) + (int64_t)pl.z_row0[b] * XSB;
+    ginet_tail(a, t, fc1_row, fc1_col, fc1_bias, b, N, K0, K1, F, OUT, y_g, drop_offset,
+               [&](int i, int kk) { return bf2f(zb[(int64_t)i * XSB + kk]); });
+    return;
+  }
   const float* z = pl.z + (int64_t)pl.z_row0[b] * r4(F);
   const int XS = r4(F);
   ginet_tail(a, t, fc1_row, fc1_col, fc1_bias, b, N, K0, K1, F, OUT, y_g, drop_offset,
@@ -1106,6 +1331,7 @@ extern "C" int dr_ginet_graph_pass(const dr_graph_store* store, const dr_graph_d
   if (pass->out_dim < 1 || pass->out_dim > DR_MAX_OUT) return DR_E_UNSUPPORTED;
   if (store->n_feat < 1 || 32 * store->n_feat > 2 * NT) return DR_E_UNSUPPORTED;  // F <= 64
   if (lds_bytes > 160 * 1024) return DR_E_LDS;
+  if (pass->compute_dtype != DR_DTYPE_F32) return DR_E_UNSUPPORTED;  // bf16 runs dr_ginet_large_pass
   if ((pass->flags & DR_PASS_BACKWARD) && (!pass->slab || !pass->head)) return DR_E_ARG;
   if ((pass->flags & DR_PASS_BACKWARD) && pass->loss_kind == DR_LOSS_NONE && !pass->dout) return DR_E_ARG;
   if ((pass->flags & DR_PASS_FORWARD) && !pass->out) return DR_E_ARG;
@@ -1126,6 +1352,11 @@ extern "C" int dr_ginet_graph_pass(const dr_graph_store* store, const dr_graph_d
 extern "C" int64_t dr_ginet_large_conv_lds_bytes(int32_t n_nodes, int32_t n_feat, int32_t k0, int32_t halo_max,
                                                  int32_t tile_edges_max) {
   return 4LL * conv_carve(n_nodes, n_feat, k0, halo_max, tile_edges_max).total;
+}
+
+extern "C" int64_t dr_ginet_large_conv_lds_bytes_bf16(int32_t n_nodes, int32_t n_feat, int32_t k0, int32_t halo_max,
+                                                      int32_t tile_edges_max) {
+  return 4LL * conv_carve_bf16(n_nodes, n_feat, k0, halo_max, tile_edges_max).total;
 }
 
 extern "C" int64_t dr_ginet_tail_lds_bytes(int32_t k0, int32_t p1_edges, int32_t k1, int32_t transpose_aliased,
@@ -1153,8 +1384,12 @@ extern "C" int dr_ginet_large_pass(const dr_graph_store* store, const dr_graph_d
   if ((pass->flags & DR_PASS_FORWARD) && !pass->out) return DR_E_ARG;
   if (pass->use_dropout == DR_DROPOUT_MASK && !pass->mask) return DR_E_ARG;
   if (pass->use_dropout < DR_DROPOUT_OFF || pass->use_dropout > DR_DROPOUT_HASH) return DR_E_ARG;
+  const bool bf16 = pass->compute_dtype == DR_DTYPE_BF16;
+  if (pass->compute_dtype != DR_DTYPE_F32 && !bf16) return DR_E_ARG;
+  if (bf16 && (!store->x_bf16 || store->x_bf16_stride < store->n_feat || store->x_bf16_stride % 8)) return DR_E_ARG;
   if (n_batch == 0) return DR_OK;
   DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_large_conv1_kernel)));
+  DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_large_conv1_bf16_kernel)));
   DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_large_tail_kernel)));
   LargeArgs la;
   la.g.s = *store;
@@ -1164,7 +1399,10 @@ extern "C" int dr_ginet_large_pass(const dr_graph_store* store, const dr_graph_d
   la.g.B = n_batch;
   la.plan = *plan;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(ginet_large_conv1_kernel, dim3(plan->n_tiles), dim3(NTA), conv_lds_bytes, st, la);
+  if (bf16)
+    hipLaunchKernelGGL(ginet_large_conv1_bf16_kernel, dim3(plan->n_tiles), dim3(NTA), conv_lds_bytes, st, la);
+  else
+    hipLaunchKernelGGL(ginet_large_conv1_kernel, dim3(plan->n_tiles), dim3(NTA), conv_lds_bytes, st, la);
   hipLaunchKernelGGL(ginet_large_tail_kernel, dim3(n_batch), dim3(NT), tail_lds_bytes, st, la);
   return (int)hipGetLastError();
 }

@@ -94,12 +94,12 @@ class BatchHandle:
             self._lds["vanilla_fused_scratch"] = sc
         return sc
 
-    def large_plan(self, out_dim):
+    def large_plan(self, out_dim, bf16=False):
         """Tiling + workspaces of the large-graph path (dr_large_plan), built once per batch."""
-        plan = self._lds.get(("large", out_dim))
+        plan = self._lds.get(("large", out_dim, bf16))
         if plan is None:
-            plan = LargePlan(self, out_dim, use_halos=self.large_halos, use_atomic_max=self.large_atomic_max)
-            self._lds[("large", out_dim)] = plan
+            plan = LargePlan(self, out_dim, use_halos=self.large_halos, use_atomic_max=self.large_atomic_max, bf16=bf16)
+            self._lds[("large", out_dim, bf16)] = plan
         return plan
 
 
@@ -112,7 +112,7 @@ class LargePlan:
 
     TILE = 64  # measured best for atom-level graphs with tile halos (tools/large_tiles.py)
 
-    def __init__(self, h: BatchHandle, out_dim, tile_rows=None, use_halos=True, use_atomic_max=True):
+    def __init__(self, h: BatchHandle, out_dim, tile_rows=None, use_halos=True, use_atomic_max=True, bf16=False):
         st = h.store
         self.TILE = int(tile_rows or h.large_tile or self.TILE)
         n, _e, k0, p1, k1 = (a[h.gids_host.astype(np.int64)] for a in st._sizes)  # noqa: SLF001
@@ -134,10 +134,11 @@ class LargePlan:
         lib = _lib.load()
         halo = self._halos(h, n) if use_halos else None
         hmax, emax = (halo[0], halo[1]) if halo is not None else (0, 0)
-        self.conv_lds = int(lib.dr_ginet_large_conv_lds_bytes(int(n.max()), st.n_feat, self.k0_max, hmax, emax))
+        conv_lds = lib.dr_ginet_large_conv_lds_bytes_bf16 if bf16 else lib.dr_ginet_large_conv_lds_bytes
+        self.conv_lds = int(conv_lds(int(n.max()), st.n_feat, self.k0_max, hmax, emax))
         if halo is not None and self.conv_lds > LDS_MAX:  # halos too wide for LDS: per-edge HBM gather
             halo, hmax = None, 0
-            self.conv_lds = int(lib.dr_ginet_large_conv_lds_bytes(int(n.max()), st.n_feat, self.k0_max, 0, 0))
+            self.conv_lds = int(conv_lds(int(n.max()), st.n_feat, self.k0_max, 0, 0))
         self.tail_lds = int(lib.dr_ginet_tail_lds_bytes(self.k0_max, int(p1.max()), int(k1.max()), int(st.packed.transpose_aliased), out_dim))
         if max(self.conv_lds, self.tail_lds) > LDS_MAX:
             msg = f"large-graph path needs {max(self.conv_lds, self.tail_lds)} B of LDS (> 160 KiB)"

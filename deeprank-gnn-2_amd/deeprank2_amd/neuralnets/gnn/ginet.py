@@ -160,7 +160,7 @@ def _lds(n, e, k0, p1, k1, f, alias, out):
 
 def _large(h, w, p):
     """Graphs beyond one workgroup's LDS: tile conv1 kernel + per-graph tail (dr_ginet_large_pass)."""
-    plan = h.large_plan(p.out_dim)
+    plan = h.large_plan(p.out_dim, bf16=p.compute_dtype == _lib.DR_DTYPE_BF16)
     lib = _lib.load()
     rc = lib.dr_ginet_large_pass(h.store.cstruct(), h.descs.data_ptr(), h.B, plan.c, w, p, plan.conv_lds, plan.tail_lds, _lib.stream_ptr(h.store.device))
     _lib.check(rc, "dr_ginet_large_pass")

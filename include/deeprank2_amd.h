@@ -241,6 +241,9 @@ int dr_ginet_large_pass(const dr_graph_store* store, const dr_graph_desc* descs,
 /* Dynamic LDS of the two launches of dr_ginet_large_pass (largest graph).  */
 int64_t dr_ginet_large_conv_lds_bytes(int32_t n_nodes, int32_t n_feat, int32_t k0, int32_t halo_max,
                                       int32_t tile_edges_max);
+/* The same for passes with compute_dtype DR_DTYPE_BF16 (bf16 halo rows and Z operand).  */
+int64_t dr_ginet_large_conv_lds_bytes_bf16(int32_t n_nodes, int32_t n_feat, int32_t k0, int32_t halo_max,
+                                           int32_t tile_edges_max);
 int64_t dr_ginet_tail_lds_bytes(int32_t k0, int32_t p1_edges, int32_t k1, int32_t transpose_aliased,
                                 int32_t out_dim);
 
