@@ -253,6 +253,7 @@ def parse_args(argv):
     ap.add_argument("--graphs", choices=["residue", "atom", "mixed", "srv"], default="residue")
     ap.add_argument("--dtype", choices=["f32", "bf16"], default="f32", help="compute dtype of the node GEMMs (bf16: GINet only; fp32 accumulate, fp32 master weights and Adam)")
     ap.add_argument("--force-large", type=int, default=0, help="GINet: run the split tile+tail path with this many nodes per tile (diagnostic)")
+    ap.add_argument("--ginet-path", choices=["auto", "split", "onepass"], default="auto", help="GINet: auto = one workgroup per graph when the batch fits LDS, else the split path; split = tile kernel + tail kernel; onepass = tiles + in-launch tails (one launch)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stream-copy", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch every step from Python instead of replaying captured HIP graphs")
@@ -334,8 +335,9 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
     order = np.random.default_rng(rank).permutation(packed.n_graphs).astype(np.int32)
     handles = [BatchHandle(store, order[i * B:(i + 1) * B]) for i in range(args.batches)]
     for h in handles:
-        h.force_large = bool(args.force_large)
+        h.force_large = bool(args.force_large) or args.ginet_path != "auto"
         h.large_tile = args.force_large or None
+        h.large_onepass = args.ginet_path == "onepass"
 
     torch.manual_seed(1234)
     model = models[args.model](30, 1, 3).to(dev).train()
@@ -435,7 +437,7 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
     default_cfg = args.model == "ginet" and args.graphs == "residue" and B == B_PER_GPU and args.dtype == "f32"
     pmc_cfg = default_cfg or (args.model in ("foutnet", "sgat") and args.graphs == "residue" and B == B_PER_GPU)
     traffic, traffic_src = pmc_traffic_bytes(args.model) if pmc_cfg else (None, None)
-    large = args.model == "ginet" and (bool(args.force_large) or args.dtype == "bf16" or any(h.lds((step.spec.entry, 1), lambda *sz: 0) > 160 * 1024 for h in handles))
+    large = args.model == "ginet" and (bool(args.force_large) or args.ginet_path != "auto" or args.dtype == "bf16" or any(h.lds((step.spec.entry, 1), lambda *sz: 0) > 160 * 1024 for h in handles))
     copy_gbs = None if args.no_stream_copy else stream_copy_gbs(dev)
 
     result = None
@@ -444,7 +446,7 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(graphs[:B], model_name=args.model)
         workload = WORKLOADS.get((args.model, args.graphs), f"{args.model} on {args.graphs} graphs (diagnostic)")
-        kname = {"ginet": "ginet_large_conv1_kernel + ginet_large_tail_kernel (dr_ginet_large_pass)" if large else "ginet_graph_kernel (dr_ginet_graph_pass, fwd+loss+bwd, 1 workgroup/graph)", "foutnet": "fout_graph_kernel<false> (dr_fout_graph_pass)", "vanilla": "vanilla_graph_kernel (dr_vanilla_fused_pass) / vanilla pipeline (dr_vanilla_graph_pass)", "sgat": "fout_graph_kernel<true> (dr_sgat_graph_pass)", "ginet_nocluster": "ginet_nocluster_kernel (dr_ginet_nocluster_graph_pass)"}[args.model]
+        kname = {"ginet": ("ginet_onepass_kernel (dr_ginet_large_pass, one launch)" if args.ginet_path == "onepass" else "ginet_large_conv1_kernel + ginet_large_tail_kernel (dr_ginet_large_pass)") if large else "ginet_graph_kernel (dr_ginet_graph_pass, fwd+loss+bwd, 1 workgroup/graph)", "foutnet": "fout_graph_kernel<false> (dr_fout_graph_pass)", "vanilla": "vanilla_graph_kernel (dr_vanilla_fused_pass) / vanilla pipeline (dr_vanilla_graph_pass)", "sgat": "fout_graph_kernel<true> (dr_sgat_graph_pass)", "ginet_nocluster": "ginet_nocluster_kernel (dr_ginet_nocluster_graph_pass)"}[args.model]
         result = {
             "metric": HEADLINE_METRIC if default_cfg else f"graphs/sec per training step, {workload} (fwd+MSE+bwd+Adam)",
             "value": round(graphs_total / elapsed, 1),
@@ -463,6 +465,7 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
             "data": f"synthetic (seeded {args.graphs} graphs per SURVEY §8(d); random-init {models[args.model].__name__}(30,1,3))",
             "config": {
                 "workload": workload,
+                "ginet_path": args.ginet_path if args.model == "ginet" else None,
                 "graphs_per_gpu": B,
                 "global_batch": B * world,
                 "mean_nodes_per_graph": round(float(np.diff(packed.node_off).mean()), 1),

@@ -771,22 +771,50 @@ __device__ __forceinline__ int lower_bound_lds(const int* v, int lo, int hi, int
   return lo;
 }
 
+// Global-address-space views for in-launch hand-offs (MI355X_MICROARCH.md
+// §inter-workgroup visibility): agent-scope relaxed atomics lower to sc1
+// global loads/stores, which bypass the per-CU L1 and write through the
+// per-XCD L2, so a payload stored this way, drained (s_waitcnt vmcnt(0)) and
+// signalled by an agent-scope counter add is read correctly by the workgroup
+// whose add came last with sc1 loads, wherever the two sit.
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned int gu32;
+
+template <bool INL>
+__device__ __forceinline__ void store_u64(void* p, uint64_t v) {
+  if (INL) __hip_atomic_store((gu64*)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *reinterpret_cast<uint64_t*>(p) = v;
+}
+template <bool INL>
+__device__ __forceinline__ void store_z4(float* p, float4 v) {
+  if (INL) {
+    store_u64<true>(p, (uint64_t)__float_as_uint(v.x) | ((uint64_t)__float_as_uint(v.y) << 32));
+    store_u64<true>(p + 2, (uint64_t)__float_as_uint(v.z) | ((uint64_t)__float_as_uint(v.w) << 32));
+  } else {
+    *reinterpret_cast<float4*>(p) = v;
+  }
+}
+__device__ __forceinline__ uint32_t load_sc1_u32(const void* p) {
+  return __hip_atomic_load((const gu32*)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // The tile's partial depth-0 max per (cluster, channel) of H (LDS, stride
 // 32, rows r0..r0+nrows-1): strict '>' in node order, first max wins, NaN never
 // enters (torch_scatter scatter_max, community_pooling.py:209).  Published by
 // 64-bit atomic max keys or per-tile partials (dr_large_plan).
+template <int NTT, bool INL>
 __device__ __forceinline__ void tile_partial_max(const dr_large_plan& pl, const float* sH, const int* sm0i,
                                                  const int* sm0p, int* srng, bool compact, int tile, int b, int K0,
                                                  int N, int r0, int nrows) {
   const int tid = threadIdx.x;
   // each cluster's members inside this tile: a sub-run of its ascending list
-  for (int k = tid; k < K0; k += NTA) {
+  for (int k = tid; k < K0; k += NTT) {
     const int mb = sm0p[k], me = sm0p[k + 1];
     srng[2 * k] = compact ? mb : lower_bound_lds(sm0i, mb, me, r0);
     srng[2 * k + 1] = compact ? me : lower_bound_lds(sm0i, mb, me, r0 + nrows);
   }
   __syncthreads();
-  for (int p = tid; p < K0 * 32; p += NTA) {
+  for (int p = tid; p < K0 * 32; p += NTT) {
     const int k = p >> 5, ch = p & 31;
     float best = LOWEST;
     int arg = N;
@@ -800,8 +828,9 @@ __device__ __forceinline__ void tile_partial_max(const dr_large_plan& pl, const 
     }
     if (pl.part_key) {  // order-free combine over the graph's tiles (see dr_large_plan.part_key)
       if (best > LOWEST)
-        atomicMax(reinterpret_cast<unsigned long long*>(pl.part_key) + ((int64_t)b * pl.k0_max + k) * 32 + ch,
-                  ((unsigned long long)__float_as_uint(best) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)arg));
+        __hip_atomic_fetch_max((gu64*)(pl.part_key) + ((int64_t)b * pl.k0_max + k) * 32 + ch,
+                               ((unsigned long long)__float_as_uint(best) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)arg),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
       const int64_t o = ((int64_t)tile * pl.k0_max + k) * 32 + ch;
       pl.part_val[o] = best;
@@ -812,8 +841,8 @@ __device__ __forceinline__ void tile_partial_max(const dr_large_plan& pl, const 
 
 // One tile of TR nodes: Z rows (CSR gather over HBM/L2), H = relu(Z W^T) on
 // MFMA, and the tile's partial depth-0 max per (cluster, channel).
-__global__ void __launch_bounds__(NTA) ginet_large_conv1_kernel(LargeArgs la) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
+template <int NTT, bool INL>
+__device__ __forceinline__ void conv_tile_f32(const LargeArgs& la, float* lds) {
   const GinetArgs& a = la.g;
   const dr_large_plan& pl = la.plan;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -838,19 +867,19 @@ __global__ void __launch_bounds__(NTA) ginet_large_conv1_kernel(LargeArgs la) {
 
   const bool compact = pl.tile_members != nullptr;
   if (compact) {  // this tile's members by cluster (host-built), runs from tile_mptr
-    drk::dma_words<NTA>(sm0i, pl.tile_members + (int64_t)tile * TRr, nrows);
-    drk::dma_words<NTA>(sm0p, pl.tile_mptr + (int64_t)tile * (pl.k0_max + 1), K0 + 1);
+    drk::dma_words<NTT>(sm0i, pl.tile_members + (int64_t)tile * TRr, nrows);
+    drk::dma_words<NTT>(sm0p, pl.tile_mptr + (int64_t)tile * (pl.k0_max + 1), K0 + 1);
   } else {
-    drk::dma_words<NTA>(sm0i, s.m0_idx + n0, N);
-    drk::dma_words<NTA>(sm0p, s.m0_ptr + k00 + g, K0 + 1);
+    drk::dma_words<NTT>(sm0i, s.m0_idx + n0, N);
+    drk::dma_words<NTT>(sm0p, s.m0_ptr + k00 + g, K0 + 1);
   }
-  for (int p = tid; p < 32 * KP; p += NTA) {  // [W1; W1e] zero-padded to KP
+  for (int p = tid; p < 32 * KP; p += NTT) {  // [W1; W1e] zero-padded to KP
     const int r = p / KP, k = p - r * KP;
     float v = 0.f;
     if (k < F) v = (r < 16) ? a.w.w1[r * F + k] : a.w.w1e[(r - 16) * F + k];
     sW1[r * LDW + k] = v;
   }
-  for (int p = tid; p < TRr * (KP - XS); p += NTA) {  // Z pad columns
+  for (int p = tid; p < TRr * (KP - XS); p += NTT) {  // Z pad columns
     const int r = p / (KP - XS);
     sZ[r * LDW + XS + (p - r * (KP - XS))] = 0.f;
   }
@@ -863,17 +892,17 @@ __global__ void __launch_bounds__(NTA) ginet_large_conv1_kernel(LargeArgs la) {
     float* sXh = lds + c.xh;
     const int h0 = pl.halo_off[tile], H = pl.halo_off[tile + 1] - h0;
     const int l0 = pl.lcol_off[tile];
-    drk::dma_words<NTA>(strp, s.rowptr + n0 + g + r0, nrows + 1);
-    drk::dma_words<NTA>(shid, pl.halo_ids + h0, H);
+    drk::dma_words<NTT>(strp, s.rowptr + n0 + g + r0, nrows + 1);
+    drk::dma_words<NTT>(shid, pl.halo_ids + h0, H);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const int ebase = strp[0];
-    drk::dma_x4<NTA>(slcol, pl.lcol + l0, (strp[nrows] - ebase + 7) / 8);
+    drk::dma_x4<NTT>(slcol, pl.lcol + l0, (strp[nrows] - ebase + 7) / 8);
     {
       const float* X = s.x + n0 * (int64_t)XS;
       const int nch = XS >> 2, tot = H * nch;
       const int wv = __builtin_amdgcn_readfirstlane(wave);
-      for (int base = wv * 64; base < tot; base += NTA)
+      for (int base = wv * 64; base < tot; base += NTT)
         if (base + lane < tot) {
           const int hr = (base + lane) / nch, ch = base + lane - hr * nch;
           __builtin_amdgcn_global_load_lds(DRK_AS1(X + (int64_t)shid[hr] * XS + ch * 4), DRK_AS3(sXh + base * 4), 16, 0, 0);
@@ -883,7 +912,7 @@ __global__ void __launch_bounds__(NTA) ginet_large_conv1_kernel(LargeArgs la) {
     __syncthreads();
     float* zg = pl.z + (int64_t)pl.z_row0[b] * XS;
     const int nch = XS >> 2, sub = tid & 7;
-    for (int r = tid >> 3; r < nrows; r += NTA / 8) {
+    for (int r = tid >> 3; r < nrows; r += NTT / 8) {
       const int eb = strp[r] - ebase, ee = strp[r + 1] - ebase;
       for (int ch = sub; ch < nch; ch += 8) {
         const int c4 = ch * 4;
@@ -893,7 +922,7 @@ __global__ void __launch_bounds__(NTA) ginet_large_conv1_kernel(LargeArgs la) {
         zr[1] = acc.y;
         zr[2] = acc.z;
         zr[3] = acc.w;
-        *reinterpret_cast<float4*>(zg + (int64_t)(r0 + r) * XS + c4) = acc;
+        store_z4<INL>(zg + (int64_t)(r0 + r) * XS + c4, acc);
       }
     }
   } else {
@@ -904,7 +933,7 @@ __global__ void __launch_bounds__(NTA) ginet_large_conv1_kernel(LargeArgs la) {
     const float* X = s.x + n0 * (int64_t)XS;
     float* zg = pl.z + (int64_t)pl.z_row0[b] * XS;
     const int nch = XS >> 2, sub = tid & 7;
-    for (int r = tid >> 3; r < nrows; r += NTA / 8) {
+    for (int r = tid >> 3; r < nrows; r += NTT / 8) {
       const int i = r0 + r;
       const int eb = rp[i], ee = rp[i + 1];
       for (int ch = sub; ch < nch; ch += 8) {
@@ -925,7 +954,7 @@ __global__ void __launch_bounds__(NTA) ginet_large_conv1_kernel(LargeArgs la) {
         zr[1] = acc.y;
         zr[2] = acc.z;
         zr[3] = acc.w;
-        *reinterpret_cast<float4*>(zg + (int64_t)i * XS + c4) = acc;
+        store_z4<INL>(zg + (int64_t)i * XS + c4, acc);
       }
     }
   }
@@ -935,7 +964,7 @@ __global__ void __launch_bounds__(NTA) ginet_large_conv1_kernel(LargeArgs la) {
   // H = relu(Z [W1; W1e]^T), one 16-row MFMA tile per wave
   {
     const int li = lane & 15, kq = lane >> 4;
-    for (int tt = wave; tt * 16 < nrows; tt += NTA / 64) {
+    for (int tt = wave; tt * 16 < nrows; tt += NTT / 64) {
       const int q0 = tt * 16;
       const int ar = min(q0 + li, nrows - 1);
       floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -964,7 +993,12 @@ __global__ void __launch_bounds__(NTA) ginet_large_conv1_kernel(LargeArgs la) {
       }
     }
   }
-  tile_partial_max(pl, sH, sm0i, sm0p, srng, compact, tile, b, K0, N, r0, nrows);
+  tile_partial_max<NTT, INL>(pl, sH, sm0i, sm0p, srng, compact, tile, b, K0, N, r0, nrows);
+}
+
+__global__ void __launch_bounds__(NTA) ginet_large_conv1_kernel(LargeArgs la) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  conv_tile_f32<NTA, false>(la, lds);
 }
 
 // ---- bf16 compute (dr_pass.compute_dtype == DR_DTYPE_BF16, BASELINE configs[3]) ----
@@ -1027,8 +1061,8 @@ __host__ __device__ inline ConvCarveB conv_carve_bf16(int N, int F, int K0, int 
   return c;
 }
 
-__global__ void __launch_bounds__(NTA) ginet_large_conv1_bf16_kernel(LargeArgs la) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
+template <int NTT, bool INL>
+__device__ __forceinline__ void conv_tile_bf16(const LargeArgs& la, float* lds) {
   const GinetArgs& a = la.g;
   const dr_large_plan& pl = la.plan;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1055,19 +1089,19 @@ __global__ void __launch_bounds__(NTA) ginet_large_conv1_bf16_kernel(LargeArgs l
 
   const bool compact = pl.tile_members != nullptr;
   if (compact) {
-    drk::dma_words<NTA>(sm0i, pl.tile_members + (int64_t)tile * TRr, nrows);
-    drk::dma_words<NTA>(sm0p, pl.tile_mptr + (int64_t)tile * (pl.k0_max + 1), K0 + 1);
+    drk::dma_words<NTT>(sm0i, pl.tile_members + (int64_t)tile * TRr, nrows);
+    drk::dma_words<NTT>(sm0p, pl.tile_mptr + (int64_t)tile * (pl.k0_max + 1), K0 + 1);
   } else {
-    drk::dma_words<NTA>(sm0i, s.m0_idx + n0, N);
-    drk::dma_words<NTA>(sm0p, s.m0_ptr + k00 + g, K0 + 1);
+    drk::dma_words<NTT>(sm0i, s.m0_idx + n0, N);
+    drk::dma_words<NTT>(sm0p, s.m0_ptr + k00 + g, K0 + 1);
   }
-  for (int p = tid; p < 32 * KPB; p += NTA) {  // [W1; W1e] in bf16, K zero-padded to KPB
+  for (int p = tid; p < 32 * KPB; p += NTT) {  // [W1; W1e] in bf16, K zero-padded to KPB
     const int r = p / KPB, k = p - r * KPB;
     float v = 0.f;
     if (k < F) v = (r < 16) ? a.w.w1[r * F + k] : a.w.w1e[(r - 16) * F + k];
     sW[r * ZSB + k] = f2bf(v);
   }
-  for (int p = tid; p < TRr * (KPB - XSB); p += NTA) {  // Z pad columns (X's own pad is zero)
+  for (int p = tid; p < TRr * (KPB - XSB); p += NTT) {  // Z pad columns (X's own pad is zero)
     const int r = p / (KPB - XSB);
     sZ[r * ZSB + XSB + (p - r * (KPB - XSB))] = 0;
   }
@@ -1081,16 +1115,16 @@ __global__ void __launch_bounds__(NTA) ginet_large_conv1_bf16_kernel(LargeArgs l
     uint16_t* sXh = reinterpret_cast<uint16_t*>(lds + c.xh);
     const int h0 = pl.halo_off[tile], H = pl.halo_off[tile + 1] - h0;
     const int l0 = pl.lcol_off[tile];
-    drk::dma_words<NTA>(strp, s.rowptr + n0 + g + r0, nrows + 1);
-    drk::dma_words<NTA>(shid, pl.halo_ids + h0, H);
+    drk::dma_words<NTT>(strp, s.rowptr + n0 + g + r0, nrows + 1);
+    drk::dma_words<NTT>(shid, pl.halo_ids + h0, H);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const int ebase = strp[0];
-    drk::dma_x4<NTA>(slcol, pl.lcol + l0, (strp[nrows] - ebase + 7) / 8);
+    drk::dma_x4<NTT>(slcol, pl.lcol + l0, (strp[nrows] - ebase + 7) / 8);
     {  // halo rows: 16-byte DMA lanes, XSB/8 per row
       const int n16 = XSB >> 3, tot = H * n16;
       const int wv = __builtin_amdgcn_readfirstlane(wave);
-      for (int base = wv * 64; base < tot; base += NTA)
+      for (int base = wv * 64; base < tot; base += NTT)
         if (base + lane < tot) {
           const int hr = (base + lane) / n16, q = base + lane - hr * n16;
           __builtin_amdgcn_global_load_lds(DRK_AS1(X + (int64_t)shid[hr] * XSB + q * 8), DRK_AS3(sXh + base * 8), 16, 0, 0);
@@ -1098,7 +1132,7 @@ __global__ void __launch_bounds__(NTA) ginet_large_conv1_bf16_kernel(LargeArgs l
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int r = tid >> 3; r < nrows; r += NTA / 8) {
+    for (int r = tid >> 3; r < nrows; r += NTT / 8) {
       const int eb = strp[r] - ebase, ee = strp[r + 1] - ebase;
       for (int ch = sub; ch < nch; ch += 8) {
         const int c4 = ch * 4;
@@ -1117,13 +1151,13 @@ __global__ void __launch_bounds__(NTA) ginet_large_conv1_bf16_kernel(LargeArgs l
         for (; e < ee; ++e) acc = f4add(acc, unpack4bf(*reinterpret_cast<const uint2*>(&sXh[__umul24((int)slcol[e], XSB) + c4])));
         const uint2 zb = pack4bf(acc.x, acc.y, acc.z, acc.w);
         *reinterpret_cast<uint2*>(&sZ[r * ZSB + c4]) = zb;
-        *reinterpret_cast<uint2*>(zg + (int64_t)(r0 + r) * XSB + c4) = zb;
+        store_u64<INL>(zg + (int64_t)(r0 + r) * XSB + c4, (uint64_t)zb.x | ((uint64_t)zb.y << 32));
       }
     }
   } else {
     const int* rp = s.rowptr + n0 + g;
     const uint16_t* col = s.col + ec0;
-    for (int r = tid >> 3; r < nrows; r += NTA / 8) {
+    for (int r = tid >> 3; r < nrows; r += NTT / 8) {
       const int i = r0 + r;
       const int eb = rp[i], ee = rp[i + 1];
       for (int ch = sub; ch < nch; ch += 8) {
@@ -1141,7 +1175,7 @@ __global__ void __launch_bounds__(NTA) ginet_large_conv1_bf16_kernel(LargeArgs l
         for (; e < ee; ++e) acc = f4add(acc, unpack4bf(*reinterpret_cast<const uint2*>(X + (int64_t)col[e] * XSB + c4)));
         const uint2 zb = pack4bf(acc.x, acc.y, acc.z, acc.w);
         *reinterpret_cast<uint2*>(&sZ[r * ZSB + c4]) = zb;
-        *reinterpret_cast<uint2*>(zg + (int64_t)i * XSB + c4) = zb;
+        store_u64<INL>(zg + (int64_t)i * XSB + c4, (uint64_t)zb.x | ((uint64_t)zb.y << 32));
       }
     }
   }
@@ -1151,7 +1185,7 @@ __global__ void __launch_bounds__(NTA) ginet_large_conv1_bf16_kernel(LargeArgs l
   // W[col l&15][same k] (16-byte LDS reads); C row (l>>4)*4+r, col l&15.
   {
     const int li = lane & 15, kq = lane >> 4;
-    for (int tt = wave; tt * 16 < nrows; tt += NTA / 64) {
+    for (int tt = wave; tt * 16 < nrows; tt += NTT / 64) {
       const int q0 = tt * 16;
       const int ar = min(q0 + li, nrows - 1);
       floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -1172,7 +1206,12 @@ __global__ void __launch_bounds__(NTA) ginet_large_conv1_bf16_kernel(LargeArgs l
       }
     }
   }
-  tile_partial_max(pl, sH, sm0i, sm0p, srng, compact, tile, b, K0, N, r0, nrows);
+  tile_partial_max<NTT, INL>(pl, sH, sm0i, sm0p, srng, compact, tile, b, K0, N, r0, nrows);
+}
+
+__global__ void __launch_bounds__(NTA) ginet_large_conv1_bf16_kernel(LargeArgs la) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  conv_tile_bf16<NTA, false>(la, lds);
 }
 
 struct TailCarve {
@@ -1215,12 +1254,15 @@ __host__ __device__ inline TailCarve tail_carve(int K0, int P1, int K1, int alia
 }
 
 // One workgroup per graph: combine the tiles' partial maxima, then the tail.
-__global__ void __launch_bounds__(NT) ginet_large_tail_kernel(LargeArgs la) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
+// The per-graph tail of the large path: combine the tiles' partial maxima,
+// then ginet_tail.  INL: run by the last-arriving tile workgroup of graph b
+// inside the one-launch kernel, so the tiles' hand-off (part_key atomics, Z
+// rows) is read with agent-scope (sc1) loads.
+template <bool INL>
+__device__ __forceinline__ void tail_body(const LargeArgs& la, int b, float* lds) {
   const GinetArgs& a = la.g;
   const dr_large_plan& pl = la.plan;
   const int tid = threadIdx.x;
-  const int b = blockIdx.x;
   const dr_graph_store& s = a.s;
   const dr_graph_desc d = a.descs[b];
   const int g = d.gid;
@@ -1259,8 +1301,14 @@ __global__ void __launch_bounds__(NT) ginet_large_tail_kernel(LargeArgs la) {
   if (pl.part_key) {
     for (int p = tid; p < K0 * 32; p += NT) {
       unsigned long long* kp = reinterpret_cast<unsigned long long*>(pl.part_key) + (int64_t)b * pl.k0_max * 32 + p;
-      const unsigned long long key = *kp;
-      *kp = 0ull;  // ready for the next pass
+      unsigned long long key;
+      if (INL) {
+        key = __hip_atomic_load((gu64*)(kp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((gu64*)(kp), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        key = *kp;
+        *kp = 0ull;  // ready for the next pass
+      }
       t.p1[p] = key ? __uint_as_float((uint32_t)(key >> 32)) : 0.f;
       t.a1[p] = key ? (int)(0xffffffffu - (uint32_t)key) : N;
     }
@@ -1307,14 +1355,65 @@ __global__ void __launch_bounds__(NT) ginet_large_tail_kernel(LargeArgs la) {
   if (a.p.compute_dtype == DR_DTYPE_BF16) {  // the bf16 Z the conv1 GEMM consumed
     const int XSB = s.x_bf16_stride;
     const uint16_t* zb = reinterpret_cast<const uint16_t*>(pl.z) + (int64_t)pl.z_row0[b] * XSB;
-    ginet_tail(a, t, fc1_row, fc1_col, fc1_bias, b, N, K0, K1, F, OUT, y_g, drop_offset,
-               [&](int i, int kk) { return bf2f(zb[(int64_t)i * XSB + kk]); });
+    if (INL)
+      ginet_tail(a, t, fc1_row, fc1_col, fc1_bias, b, N, K0, K1, F, OUT, y_g, drop_offset, [&](int i, int kk) {
+        const int64_t o = (int64_t)i * XSB + kk;  // the 4-byte word holding the bf16 value
+        const uint32_t w = load_sc1_u32(zb + (o & ~(int64_t)1));
+        return __uint_as_float((o & 1) ? (w & 0xffff0000u) : (w << 16));
+      });
+    else
+      ginet_tail(a, t, fc1_row, fc1_col, fc1_bias, b, N, K0, K1, F, OUT, y_g, drop_offset,
+                 [&](int i, int kk) { return bf2f(zb[(int64_t)i * XSB + kk]); });
     return;
   }
   const float* z = pl.z + (int64_t)pl.z_row0[b] * r4(F);
   const int XS = r4(F);
-  ginet_tail(a, t, fc1_row, fc1_col, fc1_bias, b, N, K0, K1, F, OUT, y_g, drop_offset,
-             [&](int i, int kk) { return z[(int64_t)i * XS + kk]; });
+  if (INL)
+    ginet_tail(a, t, fc1_row, fc1_col, fc1_bias, b, N, K0, K1, F, OUT, y_g, drop_offset,
+               [&](int i, int kk) { return __uint_as_float(load_sc1_u32(z + (int64_t)i * XS + kk)); });
+  else
+    ginet_tail(a, t, fc1_row, fc1_col, fc1_bias, b, N, K0, K1, F, OUT, y_g, drop_offset,
+               [&](int i, int kk) { return z[(int64_t)i * XS + kk]; });
+}
+
+__global__ void __launch_bounds__(NT) ginet_large_tail_kernel(LargeArgs la) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  tail_body<false>(la, blockIdx.x, lds);
+}
+
+// One launch for the whole pass (dr_large_plan.arrive set): every workgroup
+// runs one tile (conv_tile_*), publishes its Z rows (sc1 stores) and its
+// partial maxima (agent-scope atomic max), drains them, and takes a ticket on
+// its graph's arrival counter; the workgroup that draws the last ticket runs
+// the graph's tail (tail_body<true>) right away — no second launch, and a
+// graph's tail starts as soon as its own tiles are done.  Nothing waits on
+// another workgroup, so any dispatch order or placement completes.
+template <bool BF16>
+__global__ void __launch_bounds__(NT) ginet_onepass_kernel(LargeArgs la) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const dr_large_plan& pl = la.plan;
+  if (BF16)
+    conv_tile_bf16<NT, true>(la, lds);
+  else
+    conv_tile_f32<NT, true>(la, lds);
+  const int tile = blockIdx.x, b = pl.tile_slot[tile];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave drains its Z stores and key atomics
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(lds);
+  if (threadIdx.x == 0) {
+    const uint32_t tiles = (uint32_t)(pl.tile_first[b + 1] - pl.tile_first[b]);
+    gu32* cnt = (gu32*)(pl.arrive + b);
+    const uint32_t ticket = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = ticket == tiles - 1;
+    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next pass
+    flag[0] = last ? 1 : 0;
+  }
+  __syncthreads();
+  const bool last = flag[0] != 0;
+  __syncthreads();  // flag read by every wave before the tail reuses the LDS
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the hand-off loads below the ticket
+  tail_body<true>(la, b, lds);
 }
 
 }  // namespace
@@ -1379,6 +1478,7 @@ extern "C" int dr_ginet_large_pass(const dr_graph_store* store, const dr_graph_d
                          !plan->lcol || !plan->tile_members || !plan->tile_mptr))
     return DR_E_ARG;
   if (!plan->halo_ids && plan->halo_max) return DR_E_ARG;
+  if (plan->arrive && !plan->part_key) return DR_E_ARG;  // the one-launch form combines tiles by atomic max
   if ((pass->flags & DR_PASS_BACKWARD) && (!pass->slab || !pass->head)) return DR_E_ARG;
   if ((pass->flags & DR_PASS_BACKWARD) && pass->loss_kind == DR_LOSS_NONE && !pass->dout) return DR_E_ARG;
   if ((pass->flags & DR_PASS_FORWARD) && !pass->out) return DR_E_ARG;
@@ -1399,6 +1499,17 @@ extern "C" int dr_ginet_large_pass(const dr_graph_store* store, const dr_graph_d
   la.g.B = n_batch;
   la.plan = *plan;
   hipStream_t st = (hipStream_t)stream;
+  if (plan->arrive) {  // one launch: tiles + in-launch tail by each graph's last-arriving tile
+    const int lds = conv_lds_bytes > tail_lds_bytes ? conv_lds_bytes : tail_lds_bytes;
+    if (bf16) {
+      DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_onepass_kernel<true>)));
+      hipLaunchKernelGGL(ginet_onepass_kernel<true>, dim3(plan->n_tiles), dim3(NT), lds, st, la);
+    } else {
+      DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_onepass_kernel<false>)));
+      hipLaunchKernelGGL(ginet_onepass_kernel<false>, dim3(plan->n_tiles), dim3(NT), lds, st, la);
+    }
+    return (int)hipGetLastError();
+  }
   if (bf16)
     hipLaunchKernelGGL(ginet_large_conv1_bf16_kernel, dim3(plan->n_tiles), dim3(NTA), conv_lds_bytes, st, la);
   else

@@ -101,6 +101,7 @@ class LargePlanC(ctypes.Structure):
         ("tile_members", VP),
         ("tile_mptr", VP),
         ("part_key", VP),
+        ("arrive", VP),
     ]
 
 

@@ -37,6 +37,7 @@ class BatchHandle:
         self.large_tile = None  # nodes per tile of the split path (default 128)
         self.large_halos = True  # stage each tile's neighbour rows in LDS (False: per-edge HBM gather)
         self.large_atomic_max = True  # depth-0 max over tiles by 64-bit atomic max (False: per-tile partials)
+        self.large_onepass = False  # split path in ONE launch: each graph's last-arriving tile runs its tail (dr_large_plan.arrive)
         self.force_layers = False  # run the layer-level path (layered.py) even when the graph pass fits (diagnostic)
 
     def lds(self, key, fn):
@@ -98,7 +99,7 @@ class BatchHandle:
         """Tiling + workspaces of the large-graph path (dr_large_plan), built once per batch."""
         plan = self._lds.get(("large", out_dim, bf16))
         if plan is None:
-            plan = LargePlan(self, out_dim, use_halos=self.large_halos, use_atomic_max=self.large_atomic_max, bf16=bf16)
+            plan = LargePlan(self, out_dim, use_halos=self.large_halos, use_atomic_max=self.large_atomic_max or self.large_onepass, bf16=bf16, onepass=self.large_onepass)
             self._lds[("large", out_dim, bf16)] = plan
         return plan
 
@@ -112,7 +113,7 @@ class LargePlan:
 
     TILE = 64  # measured best for atom-level graphs with tile halos (tools/large_tiles.py)
 
-    def __init__(self, h: BatchHandle, out_dim, tile_rows=None, use_halos=True, use_atomic_max=True, bf16=False):
+    def __init__(self, h: BatchHandle, out_dim, tile_rows=None, use_halos=True, use_atomic_max=True, bf16=False, onepass=False):
         st = h.store
         self.TILE = int(tile_rows or h.large_tile or self.TILE)
         n, _e, k0, p1, k1 = (a[h.gids_host.astype(np.int64)] for a in st._sizes)  # noqa: SLF001
@@ -121,6 +122,8 @@ class LargePlan:
             msg = f"a graph of the batch has {self.k0_max} depth-0 clusters (> 64): not supported by the large-graph path"
             raise RuntimeError(msg)
         tiles = (n + self.TILE - 1) // self.TILE
+        if onepass:  # every graph needs a tile workgroup to run its tail (an empty graph gets an empty tile)
+            tiles = np.maximum(tiles, 1)
         tile_first = np.concatenate([[0], np.cumsum(tiles)]).astype(np.int32)
         z_row0 = np.concatenate([[0], np.cumsum(n)]).astype(np.int32)
         tile_slot = np.repeat(np.arange(h.B, dtype=np.int32), tiles)
@@ -156,6 +159,8 @@ class LargePlan:
         c.part_arg = self.part_arg.data_ptr()
         c.halo_max = hmax
         c.part_key = self.part_key.data_ptr() if use_atomic_max else None
+        self.arrive = torch.zeros(h.B, dtype=torch.int32, device=dev) if onepass else None  # kept zero between passes
+        c.arrive = None if self.arrive is None else self.arrive.data_ptr()
         self.halo_tensors = None
         if halo is not None:
             _, _, hoff, hids, loff, lcol, tmem, tmptr = halo

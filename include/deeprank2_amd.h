@@ -232,6 +232,10 @@ typedef struct dr_large_plan {
                                   max over tiles by 64-bit atomic max of (H bits << 32 | ~node), i.e.
                                   the largest value and, among equal values, the first node (H >= +0
                                   after relu, NaN never enters); replaces part_val/part_arg */
+  uint32_t* arrive;            /* optional [B], zero on entry and left zero: one launch instead of
+                                  two — each tile workgroup publishes its Z rows and partial maxima
+                                  (agent-scope stores / atomics), takes a ticket here, and the
+                                  graph's last-arriving tile runs its tail; needs part_key    */
 } dr_large_plan;
 
 int dr_ginet_large_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,

@@ -41,7 +41,7 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_lib.GraphStoreC) == 16 + 22 * 8 + 8 + 2 * 8 + 8 + 8  # ... x_bf16, x_bf16_stride + pad
     assert ctypes.sizeof(_lib.GinetWeightsC) == 8 * 8
     assert ctypes.sizeof(_lib.FoutWeightsC) == 10 * 8
-    assert ctypes.sizeof(_lib.LargePlanC) == 3 * 8 + 16 + 3 * 8 + 7 * 8
+    assert ctypes.sizeof(_lib.LargePlanC) == 3 * 8 + 16 + 3 * 8 + 7 * 8 + 8  # ... part_key, arrive
     assert ctypes.sizeof(_lib.PassC) == 16 + 8 + 16 + 8 + 9 * 8
     assert ctypes.sizeof(_lib.AdamC) == 32 + 8 + 8  # + grad_div
     assert ctypes.sizeof(_lib.MclGraphsC) == 10 * 8
