@@ -51,14 +51,14 @@ __host__ __device__ inline int r16(int v) { return (v + 15) & ~15; }
 
 struct Carve {
   int KP, LDW, XS;
-  int w1, w2, fc2, x, z, h, rp, col, m0p, m0i, p1, a1, dp1, y2, h2, d2, p1rp, p1c, p1trp, p1tc, m1p, m1i, p2,
-      nt, cl1, head, dgp, red, total;
+  int w1, w2, fc2, x, z, rp, col, cl0, key, p1, a1, dp1, y2, h2, d2, p1rp, p1c, p1trp, p1tc, m1p, m1i, p2, nt, cl1,
+      head, dgp, keep, total;
 };
 
 // LDS carve (4-byte words, every region 16-byte aligned).  X keeps the HBM
 // row stride XS = r4(F) (16-byte rows for the DMA and the float4 gather);
-// Z = A·X and W use the odd stride KP+1 so the MFMA column reads are
-// bank-conflict free.
+// Z = A·X uses the stride KP+2 so the MFMA column reads are bank-conflict
+// free.
 __host__ __device__ inline Carve carve(int N, int E, int F, int K0, int P1, int K1, int alias, int OUT) {
   Carve c;
   c.KP = r16(F);      // K padded for the 16x16x4 MFMA steps (zeros)
@@ -68,16 +68,15 @@ __host__ __device__ inline Carve carve(int N, int E, int F, int K0, int P1, int 
 #define TAKE(field, words) \
   c.field = o;             \
   o += r4(words);
-  TAKE(w1, 32 * c.LDW)       // [W1; W1e] row-major, zero-padded to KP
+  TAKE(w1, 32 * F)           // [W1; W1e] (conv1 / conv1_ext .fc.weight), rows of F
   TAKE(w2, 1024)             // [W2 | W2e] (conv2 / conv2_ext .fc.weight)
   TAKE(fc2, OUT * 128 + OUT) // fc2.weight rows, then fc2.bias
   TAKE(x, N * c.XS)
   TAKE(z, N * c.LDW)
-  TAKE(h, N * 32)
   TAKE(rp, N + 1)
   TAKE(col, (E + 1) / 2)     // uint16 column ids
-  TAKE(m0p, K0 + 1)
-  TAKE(m0i, N)
+  TAKE(cl0, N)               // depth-0 cluster of each node
+  TAKE(key, 2 * K0 * 32)     // depth-0 pooling keys (uint64)
   TAKE(p1, K0 * 32)
   TAKE(a1, K0 * 32)
   TAKE(dp1, K0 * 32)
@@ -100,7 +99,7 @@ __host__ __device__ inline Carve carve(int N, int E, int F, int K0, int P1, int 
   TAKE(cl1, K0)  // depth-1 cluster of each depth-0 cluster
   TAKE(head, HEADW)
   TAKE(dgp, NW * 64)
-  TAKE(red, 2 * NT)
+  TAKE(keep, 32)  // 128 dropout keep bytes
 #undef TAKE
   c.total = o;
   return c;
@@ -199,6 +198,21 @@ __device__ __forceinline__ void gather_rows(const int* rp, const uint16_t* col, 
   } while (0)
 #endif
 
+// sum over a pooled CSR row [eb, ee) of v[col[e] * 64 + o], in edge order;
+// four index reads, then four value reads in flight per step (same sum order
+// as the plain loop).
+__device__ __forceinline__ float pooled_row_sum(const int* col, int eb, int ee, const float* v, int o) {
+  float acc = 0.f;
+  int e = eb;
+  for (; e + 4 <= ee; e += 4) {
+    const int c0 = col[e], c1 = col[e + 1], c2 = col[e + 2], c3 = col[e + 3];
+    const float v0 = v[c0 * 64 + o], v1 = v[c1 * 64 + o], v2 = v[c2 * 64 + o], v3 = v[c3 * 64 + o];
+    acc = (((acc + v0) + v1) + v2) + v3;
+  }
+  for (; e < ee; ++e) acc += v[col[e] * 64 + o];
+  return acc;
+}
+
 // Everything after the depth-0 pooling (P1 / A1 in LDS): conv2 on the pooled
 // graph, depth-1 pooling, mean, head, loss and the whole backward.  Shared by
 // the single-workgroup kernel and the large-graph tail kernel; zat(i, kk)
@@ -207,6 +221,7 @@ struct TailLds {
   float *w2, *fc2, *p1, *dp1, *y2, *h2, *d2, *p2, *nt, *dgp;
   float *g, *hpre, *hh, *hd, *dh, *dg, *dout;
   int *a1, *p1rp, *p1c, *p1trp, *p1tc, *m1p, *m1i, *cl1;
+  const uint8_t* keep = nullptr;  // prefetched dropout keep flags, or null (hash in the head)
 };
 
 template <class C>
@@ -259,9 +274,7 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
   __syncthreads();
   for (int p = tid; p < K0 * 64; p += NT) {
     const int k = p >> 6, o = p & 63;
-    float acc = 0.f;
-    for (int e = t.p1rp[k]; e < t.p1rp[k + 1]; ++e) acc += t.y2[t.p1c[e] * 64 + o];
-    t.h2[p] = relu_keepnan(acc);
+    t.h2[p] = relu_keepnan(pooled_row_sum(t.p1c, t.p1rp[k], t.p1rp[k + 1], t.y2, o));
   }
   __syncthreads();
 
@@ -281,13 +294,22 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
     for (int p = tid; p < K1 * 64; p += NT) {
       const int m = p >> 6, o = p & 63;
       const int mb = t.m1p[m], me = t.m1p[m + 1];
-      float mx = t.h2[t.m1i[mb] * 64 + o];
-      for (int q = mb + 1; q < me; ++q) {
-        const float v = t.h2[t.m1i[q] * 64 + o];
-        mx = (mx != mx || v != v) ? __int_as_float(0x7fc00000) : fmaxf(mx, v);
-      }
+      // members' values gathered once (<= 15): all index reads, then all
+      // value reads in flight (predicated); max and tie count are order-free
+      float v[16];
+      int q[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) q[u] = t.m1i[(mb + u < me) ? mb + u : mb];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = t.h2[q[u] * 64 + o];
+      float mx = v[0];
+#pragma unroll
+      for (int u = 1; u < 16; ++u)
+        if (mb + u < me) mx = (mx != mx || v[u] != v[u]) ? __int_as_float(0x7fc00000) : fmaxf(mx, v[u]);
       float ties = 0.f;
-      for (int q = mb; q < me; ++q) ties += (t.h2[t.m1i[q] * 64 + o] == mx) ? 1.f : 0.f;
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (mb + u < me) ties += (v[u] == mx) ? 1.f : 0.f;
       t.p2[p] = mx;
       t.nt[p] = ties;
     }
@@ -352,6 +374,7 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
     hl.dg = t.dg;
     hl.dout = t.dout;
     hl.dgp = t.dgp;
+    hl.keep = t.keep;
     if (!drk::ginet_head<NT>(a.p, hl, fc1_row, fc1_col, fc1_bias, b, OUT, y_g, drop_offset, 8)) return;
   }  // stamps 8 (forward head done) and 9 (loss gradient done) are taken inside
 
@@ -371,9 +394,7 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
   // dY2 = A1^T dS2 (pooled graph, transposed CSR)  -> reuse t.y2
   for (int p = tid; p < K0 * 64; p += NT) {
     const int j = p >> 6, o = p & 63;
-    float acc = 0.f;
-    for (int e = t.p1trp[j]; e < t.p1trp[j + 1]; ++e) acc += t.d2[t.p1tc[e] * 64 + o];
-    t.y2[p] = acc;
+    t.y2[p] = pooled_row_sum(t.p1tc, t.p1trp[j], t.p1trp[j + 1], t.d2, o);
   }
   __syncthreads();
   STAMP(12);
@@ -386,7 +407,18 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
     for (int p = tid; p < 1024; p += NT) {
       const int br = p >> 9, o = ((p >> 4) & 31) + br * 32, j = p & 15;
       float acc = 0.f;
-      for (int k = 0; k < K0; ++k) acc = fmaf(t.y2[k * 64 + o], t.p1[k * 32 + br * 16 + j], acc);
+      int k = 0;
+      for (; k + 4 <= K0; k += 4) {  // 8 independent reads, then the fmaf chain in k order
+        float yv[4], pv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          yv[u] = t.y2[(k + u) * 64 + o];
+          pv[u] = t.p1[(k + u) * 32 + br * 16 + j];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc = fmaf(yv[u], pv[u], acc);
+      }
+      for (; k < K0; ++k) acc = fmaf(t.y2[k * 64 + o], t.p1[k * 32 + br * 16 + j], acc);
       slab[p] = acc;
     }
     for (int p = tid; p < K0 * 32; p += NT) {
@@ -451,23 +483,22 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
       int k = 0;
       // 8 clusters at a time: the Z reads (HBM on the large path) are issued
       // together, then accumulated in cluster order (same fmaf chain)
-      for (; k + 8 <= K0; k += 8) {
+      // 8 clusters at a time, the last group predicated (clusters past K0 and
+      // empty ones contribute nothing): every Z read of a group in flight
+      for (; k < K0; k += 8) {
         float zv[8], dv[8];
         bool ok[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const int i = t.a1[(k + u) * 32 + ch];
+          const bool in = k + u < K0;
+          const int i = in ? t.a1[(k + u) * 32 + ch] : N;
           ok[u] = i < N;
-          dv[u] = t.dp1[(k + u) * 32 + ch];
+          dv[u] = in ? t.dp1[(k + u) * 32 + ch] : 0.f;
           zv[u] = zat(ok[u] ? i : 0, kk);
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u)
           if (ok[u]) acc = fmaf(dv[u], zv[u], acc);
-      }
-      for (; k < K0; ++k) {
-        const int i = t.a1[k * 32 + ch];
-        if (i < N) acc = fmaf(t.dp1[k * 32 + ch], zat(i, kk), acc);
       }
       slab[p] = acc;
     }
@@ -475,6 +506,8 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
   STAMP(14);
 }
 
+// KPT: conv1's K (F) padded to whole 16-deep MFMA steps, 32 (F <= 32) or 64.
+template <int KPT>
 __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x;
@@ -492,23 +525,22 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   // Fetch every kernel-argument field the staging needs, and the descriptor,
   // in one scalar round trip each (hipcc would otherwise load them lazily
   // with a wait before each DMA).
-  asm volatile("" ::"s"(s.x), "s"(s.col), "s"(s.rowptr), "s"(s.m0_ptr), "s"(s.m0_idx), "s"(s.p1_rowptr),
-               "s"(s.p1_col), "s"(s.p1t_rowptr), "s"(s.p1t_col), "s"(s.m1_ptr), "s"(s.m1_idx), "s"(s.y), "s"(F),
-               "s"(alias), "s"(OUT), "s"(n0), "s"(ec0), "s"(k00), "s"(q0), "s"(k10), "s"(N), "s"(E), "s"(K0),
-               "s"(P1), "s"(K1), "s"(g));
+  asm volatile("" ::"s"(s.x), "s"(s.col), "s"(s.rowptr), "s"(s.cl0), "s"(s.p1_rowptr), "s"(s.p1_col),
+               "s"(s.p1t_rowptr), "s"(s.p1t_col), "s"(s.m1_ptr), "s"(s.m1_idx), "s"(s.y), "s"(F), "s"(alias),
+               "s"(OUT), "s"(n0), "s"(ec0), "s"(k00), "s"(q0), "s"(k10), "s"(N), "s"(E), "s"(K0), "s"(P1), "s"(K1),
+               "s"(g));
   const Carve c = carve(N, E, F, K0, P1, K1, alias, OUT);
-  const int KP = c.KP, LDW = c.LDW, XS = c.XS;
+  const int LDW = c.LDW, XS = c.XS;
 
   float* sW1 = lds + c.w1;
   float* sW2 = lds + c.w2;
   float* sFc2 = lds + c.fc2;
   float* sX = lds + c.x;
   float* sZ = lds + c.z;
-  float* sH = lds + c.h;
   int* srp = reinterpret_cast<int*>(lds + c.rp);
   uint16_t* scol = reinterpret_cast<uint16_t*>(lds + c.col);
-  int* sm0p = reinterpret_cast<int*>(lds + c.m0p);
-  int* sm0i = reinterpret_cast<int*>(lds + c.m0i);
+  int* scl0 = reinterpret_cast<int*>(lds + c.cl0);
+  unsigned long long* skey = reinterpret_cast<unsigned long long*>(lds + c.key);
   float* sP1 = lds + c.p1;
   int* sA1 = reinterpret_cast<int*>(lds + c.a1);
   int* sp1rp = reinterpret_cast<int*>(lds + c.p1rp);
@@ -517,12 +549,12 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   int* sp1tc = reinterpret_cast<int*>(lds + c.p1tc);
   int* sm1p = reinterpret_cast<int*>(lds + c.m1p);
   int* sm1i = reinterpret_cast<int*>(lds + c.m1i);
-  float* sRed = lds + c.red;
+  uint8_t* skeep = reinterpret_cast<uint8_t*>(lds + c.keep);
 
   STAMP(0);
   // ---------------- stage the graph into LDS --------------------------------
   // Head weights go to registers first (their latency hides under the DMA);
-  // the graph and the other weights are DMA'd straight into LDS.
+  // the graph and conv1's weights are DMA'd straight into LDS.
   float fc1_row[8], fc1_col[8], fc1_bias;
   {
     const int r = tid >> 3, part = tid & 7;
@@ -540,8 +572,7 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   dma_x4(sX, s.x + n0 * (int64_t)XS, N * XS / 4);
   dma_x4(scol, s.col + ec0, (E + 7) / 8);
   dma_words(srp, s.rowptr + n0 + g, N + 1);
-  dma_words(sm0p, s.m0_ptr + k00 + g, K0 + 1);
-  dma_words(sm0i, s.m0_idx + n0, N);
+  dma_words(scl0, s.cl0 + n0, N);
   dma_words(sp1rp, s.p1_rowptr + k00 + g, K0 + 1);
   dma_words(sp1c, s.p1_col + q0, P1);
   if (!alias) {
@@ -550,17 +581,15 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   }
   dma_words(sm1p, s.m1_ptr + k10 + g, K1 + 1);
   dma_words(sm1i, s.m1_idx + k00, K0);
-  {  // zero the K padding of W (cols F..KP) and of Z (cols XS..KP; X's own pad is zero)
-    const int padw = KP - F;
-    for (int p = tid; p < 32 * padw; p += NT) {
-      const int i = p / padw;
-      sW1[i * LDW + F + (p - i * padw)] = 0.f;
-    }
-    const int padz = KP - XS;
+  dma_words(sW1, a.w.w1, 16 * F);  // [W1; W1e] rows of F, packed
+  dma_words(sW1 + 16 * F, a.w.w1e, 16 * F);
+  {  // zero Z's K padding (cols XS..KPT; X's own pad is zero) and the pooling keys
+    const int padz = KPT - XS;
     for (int p = tid; p < N * padz; p += NT) {
       const int i = p / padz;
       sZ[i * LDW + XS + (p - i * padz)] = 0.f;
     }
+    for (int p = tid; p < K0 * 32; p += NT) skey[p] = 0ull;
   }
   if (a.p.step_counter) drop_offset = (uint64_t)a.p.step_counter[0];  // loaded late: no early wait
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -570,18 +599,12 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   __syncthreads();
 
   STAMP(1);
-  // The weights are not needed before the GEMM: load them into VGPRs now and
-  // store them to LDS after the gather, so their latency overlaps it.  (An
-  // LDS DMA here would make hipcc wait for it before every LDS read.)
-  float wv1[2], wv2, wfc[3];
+  // The conv2 / head weights are not needed before the tail: load them into
+  // VGPRs now and store them to LDS after the front half, so their latency
+  // overlaps it.  (An LDS DMA here would make hipcc wait for it before every
+  // LDS read.)
+  float wv2, wfc[3];
   {
-    const int n1 = 32 * F;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int p = tid + u * NT;
-      wv1[u] = 0.f;
-      if (p < n1) wv1[u] = (p < 16 * F) ? a.w.w1[p] : a.w.w1e[p - 16 * F];
-    }
     wv2 = (tid < 512) ? a.w.w2[tid] : a.w.w2e[tid - 512];
     const int nf = OUT * 128;
 #pragma unroll
@@ -592,120 +615,116 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
       else if (p < nf + OUT) wfc[u] = a.w.fc2b[p - nf];
     }
   }
-  // ---------------- conv1 aggregation first: Z = A X  (ginet.py:45,58) -----
-  // A (X W^T) = (A X) W^T: aggregating the F input features first lets the
-  // backward use dW1 = sum_k v_k (A X)[arg_k] (the depth-0 max pool routes
-  // each channel's gradient to one member per cluster) with no backward gather.
-  gather_rows(srp, scol, sX, XS, sZ, LDW, N);
-  {
-    const int n1 = 32 * F;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int p = tid + u * NT;
-      if (p < n1) {
-        const int r = p / F;
-        sW1[r * LDW + (p - r * F)] = wv1[u];
-      }
-    }
-    sW2[tid] = wv2;
-    const int nf = OUT * 128 + OUT;
-#pragma unroll
-    for (int u = 0; u < 3; ++u)
-      if (tid + u * NT < nf) sFc2[tid + u * NT] = wfc[u];
-  }
-  __syncthreads();
-
-  STAMP(2);
-  // ---------------- conv1 node GEMM on MFMA + relu: H = relu(Z [W1;W1e]^T) --
+  // ---------------- conv1 + depth-0 pooling, one 16-row tile per wave -------
+  // Each wave runs its rows through the whole front half with no workgroup
+  // barrier in between:
+  //   Z = A X  (ginet.py:45,58 aggregated first: A (X W^T) = (A X) W^T), 8
+  //     lanes per row, edges in CSR order (torch_scatter's scatter_add_ order),
+  //     two rows per lane in flight;
+  //   H = relu(Z [W1;W1e]^T) on v_mfma_f32_16x16x4_f32 (exact k-ordered fmaf
+  //     chain), B operands in registers;
+  //   depth-0 max pool (torch_scatter scatter_max, community_pooling.py:209):
+  //     a 64-bit LDS atomic max of (H bits << 32 | ~node) per (cluster,
+  //     channel): H >= +0 after relu so the bit order is the value order, and
+  //     among equal values the smallest node wins — the first max of the
+  //     reference's node-ordered strict '>' scan; NaN never enters; an empty
+  //     (cluster, channel) keeps key 0 -> value 0, no arg.  H itself is never
+  //     stored: the backward needs only P1 = H[arg] and Z[arg].
   {
     const int li = lane & 15, kq = lane >> 4;
-    for (int t = wave; t * 16 < N; t += NW) {
-      const int r0 = t * 16;
-      const int ar = min(r0 + li, N - 1);  // rows past N compute garbage that is never stored
-      floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-      for (int k = 0; k < KP; k += 16) {
-        float av[4], b0[4], b1[4];
+    const int slot = lane >> 3, sub = lane & 7, nch = XS >> 2;
+    // conv1 B operand of v_mfma_f32_16x16x4_f32: lane (li, kq) holds
+    // W[li][k + 4u + kq] (wa: conv1 rows, wb: conv1_ext rows), zero past F
+    constexpr int NKV = KPT / 4;
+    float wa[NKV], wb[NKV];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int kk = k + 4 * u + kq;
-          av[u] = sZ[ar * LDW + kk];
-          b0[u] = sW1[li * LDW + kk];
-          b1[u] = sW1[(16 + li) * LDW + kk];
+    for (int j = 0; j < NKV; ++j) {
+      const int kk = 16 * (j >> 2) + 4 * (j & 3) + kq;
+      wa[j] = kk < F ? sW1[li * F + kk] : 0.f;
+      wb[j] = kk < F ? sW1[(16 + li) * F + kk] : 0.f;
+    }
+    for (int tt = wave; tt * 16 < N; tt += NW) {
+      const int r0 = tt * 16;
+      {  // rows r0+slot and r0+8+slot together: two independent edge chains per lane
+        const int i0 = r0 + slot, i1 = r0 + 8 + slot;
+        const int eb0 = i0 < N ? srp[i0] : 0, ee0 = i0 < N ? srp[i0 + 1] : 0;
+        const int eb1 = i1 < N ? srp[i1] : 0, ee1 = i1 < N ? srp[i1 + 1] : 0;
+        for (int ch = sub; ch < nch; ch += 8) {
+          float4 z0, z1;
+          drk::gather_two_row_chunks(scol, eb0, ee0, eb1, ee1, sX, XS, ch * 4, z0, z1);
+          if (i0 < N) {
+            float* zr = sZ + i0 * LDW + ch * 4;
+            zr[0] = z0.x;
+            zr[1] = z0.y;
+            zr[2] = z0.z;
+            zr[3] = z0.w;
+          }
+          if (i1 < N) {
+            float* zr = sZ + i1 * LDW + ch * 4;
+            zr[0] = z1.x;
+            zr[1] = z1.y;
+            zr[2] = z1.z;
+            zr[3] = z1.w;
+          }
         }
+      }
+      // this wave's Z rows are complete in LDS before its own MFMA reads them
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const int ar = min(r0 + li, N - 1);  // rows past N compute garbage that is never pooled
+      floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KPT / 16; ++ks) {
+        float av[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) av[u] = sZ[ar * LDW + ks * 16 + 4 * u + kq];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], b0[u], acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], b1[u], acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], wa[4 * ks + u], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], wb[4 * ks + u], acc1, 0, 0, 0);
         }
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = r0 + kq * 4 + r;
         if (row < N) {
-          sH[row * 32 + li] = relu_keepnan(acc0[r]);
-          sH[row * 32 + 16 + li] = relu_keepnan(acc1[r]);
+          const int k = scl0[row];
+          const unsigned long long low = 0xffffffffull - (unsigned long long)(uint32_t)row;
+          const float v0 = relu_keepnan(acc0[r]), v1 = relu_keepnan(acc1[r]);
+          if (v0 == v0)
+            __hip_atomic_fetch_max(skey + k * 32 + li, ((unsigned long long)__float_as_uint(v0) << 32) | low,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (v1 == v1)
+            __hip_atomic_fetch_max(skey + k * 32 + 16 + li, ((unsigned long long)__float_as_uint(v1) << 32) | low,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
       }
     }
   }
-  __syncthreads();
-
-  STAMP(3);
-  // ---------------- depth-0 community pooling: torch_scatter scatter_max ----
-  // (community_pooling.py:209): strict '>' from lowest(), members in node
-  // order => first max wins, NaN never enters, empty -> 0 with no arg.
-  // Members are split into S1 contiguous slices combined in slice order.
+  // the head's dropout keep flags, by the last two waves (idle in the front
+  // half up to N = 224): off the tail's critical path
+  if (tid >= NT - 128) {
+    const int r = tid - (NT - 128);
+    if (a.p.use_dropout) skeep[r] = drk::keep_unit(a.p, drop_offset, b, r) ? 1 : 0;
+  }
+  sW2[tid] = wv2;
   {
-    const int pairs = K0 * 32;
-    const int LS = pairs <= NT / 8 ? 3 : pairs <= NT / 4 ? 2 : pairs <= NT / 2 ? 1 : 0;  // log2 slices
-    const int S1 = 1 << LS;
-    float* tb = sRed;
-    int* ta = reinterpret_cast<int*>(sRed + NT);
-    for (int p = tid; p < pairs * S1; p += NT) {
-      const int sl = p & (S1 - 1), pr = p >> LS;  // p = pr * S1 + sl
-      const int k = pr >> 5, ch = pr & 31;
-      const int mb = sm0p[k], cnt = sm0p[k + 1] - mb;
-      const int qb = mb + ((cnt * sl) >> LS), qe = mb + ((cnt * (sl + 1)) >> LS);
-      float best = LOWEST;
-      int arg = N;
-      int m = qb;
-      for (; m + 4 <= qe; m += 4) {
-        const int i0 = sm0i[m], i1 = sm0i[m + 1], i2 = sm0i[m + 2], i3 = sm0i[m + 3];
-        const float v0 = sH[i0 * 32 + ch], v1 = sH[i1 * 32 + ch], v2 = sH[i2 * 32 + ch], v3 = sH[i3 * 32 + ch];
-        if (v0 > best) { best = v0; arg = i0; }
-        if (v1 > best) { best = v1; arg = i1; }
-        if (v2 > best) { best = v2; arg = i2; }
-        if (v3 > best) { best = v3; arg = i3; }
-      }
-      for (; m < qe; ++m) {
-        const int i = sm0i[m];
-        const float v = sH[i * 32 + ch];
-        if (v > best) {
-          best = v;
-          arg = i;
-        }
-      }
-      tb[p] = best;
-      ta[p] = arg;
-    }
-    __syncthreads();
-    for (int p = tid; p < pairs; p += NT) {
-      float best = LOWEST;
-      int arg = N;
-      for (int sl = 0; sl < S1; ++sl) {
-        const float v = tb[(p << LS) + sl];
-        if (v > best) {
-          best = v;
-          arg = ta[(p << LS) + sl];
-        }
-      }
-      sP1[p] = (best == LOWEST) ? 0.f : best;
-      sA1[p] = arg;
-    }
+    const int nf = OUT * 128 + OUT;
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+      if (tid + u * NT < nf) sFc2[tid + u * NT] = wfc[u];
+  }
+  STAMP(2);
+  __syncthreads();
+  STAMP(3);
+  for (int p = tid; p < K0 * 32; p += NT) {
+    const unsigned long long key = skey[p];
+    sP1[p] = key ? __uint_as_float((uint32_t)(key >> 32)) : 0.f;
+    sA1[p] = key ? (int)(0xffffffffu - (uint32_t)key) : N;
   }
   __syncthreads();
 
-  const TailLds t = tail_lds(c, lds);
+  TailLds t = tail_lds(c, lds);
+  t.keep = skeep;
   ginet_tail(a, t, fc1_row, fc1_col, fc1_bias, b, N, K0, K1, F, OUT, y_g, drop_offset,
              [&](int i, int kk) { return sZ[i * LDW + kk]; });
 }
@@ -1437,14 +1456,20 @@ extern "C" int dr_ginet_graph_pass(const dr_graph_store* store, const dr_graph_d
   if (pass->use_dropout == DR_DROPOUT_MASK && !pass->mask) return DR_E_ARG;
   if (pass->use_dropout < DR_DROPOUT_OFF || pass->use_dropout > DR_DROPOUT_HASH) return DR_E_ARG;
   if (n_batch == 0) return DR_OK;
-  DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_graph_kernel)));
+  if (!store->cl0) return DR_E_ARG;
   GinetArgs args;
   args.s = *store;
   args.w = *w;
   args.p = *pass;
   args.descs = descs;
   args.B = n_batch;
-  hipLaunchKernelGGL(ginet_graph_kernel, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, args);
+  if (store->n_feat <= 32) {
+    DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_graph_kernel<32>)));
+    hipLaunchKernelGGL(ginet_graph_kernel<32>, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, args);
+  } else {
+    DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_graph_kernel<64>)));
+    hipLaunchKernelGGL(ginet_graph_kernel<64>, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, args);
+  }
   return (int)hipGetLastError();
 }
 

@@ -17,7 +17,16 @@ __device__ __forceinline__ bool keep_unit(const dr_pass& p, uint64_t offset, int
 
 struct GinetHeadLds {
   float *fc2, *g, *hpre, *hh, *hd, *dh, *dg, *dout, *dgp;
+  const uint8_t* keep = nullptr;  // optional [128] dropout keep flags computed ahead (head_keep_prefetch)
 };
+
+// The fc1-output dropout keep flags of graph b, written to LDS by the first
+// 128 threads while the graph is still being staged: the counter hash (or the
+// mask read) leaves the head's critical path.
+__device__ __forceinline__ void head_keep_prefetch(const dr_pass& p, uint64_t offset, int b, uint8_t* keep) {
+  const int r = threadIdx.x;
+  if (r < 128 && p.use_dropout) keep[r] = keep_unit(p, offset, b, r) ? 1 : 0;
+}
 
 // Diagnostic stamps (stamps build only): s_memtime at two points inside the head.
 __device__ __forceinline__ void head_stamp(int64_t* row, int i) {
@@ -55,7 +64,7 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
       const float hh = relu_keepnan(acc);
       t.hh[r] = hh;
       float hd = hh;
-      if (p.use_dropout) hd = (keep_unit(p, drop_offset, b, r) ? hh : 0.f) * p.drop_scale;
+      if (p.use_dropout) hd = ((t.keep ? t.keep[r] != 0 : keep_unit(p, drop_offset, b, r)) ? hh : 0.f) * p.drop_scale;
       t.hd[r] = hd;
     }
   }
@@ -99,7 +108,7 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
   if (tid < 128) {
     float acc = 0.f;
     for (int q = 0; q < OUT; ++q) acc = fmaf(t.fc2[q * 128 + tid], t.dout[q], acc);
-    if (p.use_dropout) acc = (keep_unit(p, drop_offset, b, tid) ? acc : 0.f) * p.drop_scale;
+    if (p.use_dropout) acc = ((t.keep ? t.keep[tid] != 0 : keep_unit(p, drop_offset, b, tid)) ? acc : 0.f) * p.drop_scale;
     t.dh[tid] = relu_bwd(t.hh[tid], acc);
   }
   __syncthreads();

@@ -75,6 +75,7 @@ class GraphStoreC(ctypes.Structure):
         ("x_bf16", VP),
         ("x_bf16_stride", ctypes.c_int32),
         ("pad1", ctypes.c_int32),
+        ("cl0", VP),
     ]
 
 

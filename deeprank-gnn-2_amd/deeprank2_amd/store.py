@@ -333,6 +333,7 @@ class GraphStore:
         self.k0_off = t(p.k0_off)
         self.m0_ptr = t(p.m0_ptr)
         self.m0_idx = t(p.m0_idx)
+        self.cl0 = t(np.ascontiguousarray(p.cl0, dtype=np.int32))
         self.p1_off = t(p.p1_off)
         self.p1_rowptr = t(p.p1_rowptr)
         self.p1_col = t(p.p1_col if p.p1_col.size else np.zeros(1, np.int32))
@@ -378,7 +379,7 @@ class GraphStore:
             s.n_feat = self.n_feat
             s.x_stride = self.x_stride
             s.transpose_aliased = int(self.packed.transpose_aliased)
-            for name in ("x", "node_off", "edge_off", "col_off", "rowptr", "col", "t_rowptr", "t_col", "k0_off", "m0_ptr", "m0_idx", "p1_off", "p1_rowptr", "p1_col", "p1t_rowptr", "p1t_col", "k1_off", "m1_ptr", "m1_idx", "y", "ea", "t_eid", "p1_ea", "p1t_pid"):
+            for name in ("x", "node_off", "edge_off", "col_off", "rowptr", "col", "t_rowptr", "t_col", "k0_off", "m0_ptr", "m0_idx", "p1_off", "p1_rowptr", "p1_col", "p1t_rowptr", "p1t_col", "k1_off", "m1_ptr", "m1_idx", "y", "ea", "t_eid", "p1_ea", "p1t_pid", "cl0"):
                 setattr(s, name, getattr(self, name).data_ptr())
             s.n_edge_feat = self.n_edge_feat
             if self.x_bf16 is not None:

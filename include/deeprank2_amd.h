@@ -111,6 +111,8 @@ typedef struct dr_graph_store {
                                 compute_dtype DR_DTYPE_BF16 (BASELINE configs[3])           */
   int32_t x_bf16_stride;     /* multiple of 8, >= F                                */
   int32_t pad1;
+  const int32_t* cl0;        /* [N_all] dense depth-0 cluster id of each node (local), the
+                                inverse of m0_ptr/m0_idx                               */
 } dr_graph_store;
 
 /* One mini-batch slot: where graph `gid` lives in the store (64 bytes, so a

@@ -38,7 +38,7 @@ def test_version_and_lds_query_are_host_only():
 
 def test_struct_layouts_match_header():
     # 4 int32 + 20 pointers; 8 pointers; 4 int32 + 2 float + 2 uint64 + float/int32 + 7 pointers
-    assert ctypes.sizeof(_lib.GraphStoreC) == 16 + 22 * 8 + 8 + 2 * 8 + 8 + 8  # ... x_bf16, x_bf16_stride + pad
+    assert ctypes.sizeof(_lib.GraphStoreC) == 16 + 22 * 8 + 8 + 2 * 8 + 8 + 8 + 8  # ... x_bf16, x_bf16_stride + pad, cl0
     assert ctypes.sizeof(_lib.GinetWeightsC) == 8 * 8
     assert ctypes.sizeof(_lib.FoutWeightsC) == 10 * 8
     assert ctypes.sizeof(_lib.LargePlanC) == 3 * 8 + 16 + 3 * 8 + 7 * 8 + 8  # ... part_key, arrive

@@ -28,7 +28,7 @@ from deeprank2_amd.utils.synthetic import make_dataset  # noqa: E402
 
 PHASES_NC = ["stage", "gather Z1=AX", "gemm H1", "gather Z2=AH1", "gemm2+bits+colsum", "mean", "head fwd+loss+bwd", "dW2", "dZ2", "spmmT dS1", "dW1"]
 PHASES_V = ["stage", "gemm B1", "row fwd 1", "gemm X1", "gemm B2", "row fwd 2", "gemm X2", "mean+bits", "head fwd/loss/bwd", "dWn2, dS2", "D2 pass", "row T 2", "dWa2 dWb2 dX1", "DMA X0/S1, dS1", "dWn1", "D1 pass", "row T 1", "dWa1 dWb1"]
-PHASES = ["stage", "gather Z=AX", "gemm H=relu(ZW)", "pool0", "gemm2+spmm2", "pool1", "mean", "head fwd (fc1,fc2)", "loss grad", "head bwd", "pool1-bwd", "spmm2T", "dW2+dP1", "dW1"]
+PHASES = ["stage", "front: gather+MFMA+pool0 (per wave)", "front barrier wait", "pool0 key decode", "gemm2+spmm2", "pool1", "mean", "head fwd (fc1,fc2)", "loss grad", "head bwd", "pool1-bwd", "spmm2T", "dW2+dP1", "dW1"]
 
 
 def main():
