@@ -6,7 +6,7 @@ from __future__ import annotations
 import numpy as np
 import pytest
 import torch
-from _util import assert_grad_close, fixed_dropout, golden_batch, golden_grads, golden_state_dict
+from _util import assert_grad_close, fixed_dropout, golden_batch, golden_graphs, golden_grads, golden_state_dict
 
 from deeprank2_amd.engine import GINetTrainStep
 from deeprank2_amd.neuralnets.gnn import ginet as amd
@@ -48,9 +48,30 @@ def test_ginet_module_vs_reference_golden(golden, name, args):
         assert_grad_close(p.grad.cpu().numpy(), ref[n], err_msg=n)
 
 
-def test_ginet_batch1_vs_batch4(golden):
+def test_ginet_batch1_hip_vs_reference_golden(golden):
+    """configs[0]: the reference's 1ATN fixture, one graph per batch (the
+    reference CPU Trainer's batch_size=1), each graph through the HIP pass
+    against the reference's own batch-1 outputs (``out/eval_b1``)."""
     z = golden("ginet_1atn")
-    np.testing.assert_allclose(z["out/eval_b1"], z["out/eval"], rtol=1e-5, atol=1e-4)
+    m = _model(z, (50, 1, 1)).eval()
+    ptr = np.asarray(z["in/ptr"])
+    ei = np.asarray(z["in/edge_index"])
+    ref_b1 = np.asarray(z["out/eval_b1"]).reshape(ptr.size - 1, -1)
+    for g, (_, n, c0, c1) in enumerate(golden_graphs(z)):
+        lo, hi = int(ptr[g]), int(ptr[g + 1])
+        em = (ei[0] >= lo) & (ei[0] < hi)
+        d = P.Data(
+            x=torch.from_numpy(np.array(z["in/x"][lo:hi])),
+            edge_index=torch.from_numpy(ei[:, em] - lo),
+            edge_attr=torch.from_numpy(np.array(z["in/edge_attr"])[em]),
+            cluster0=torch.from_numpy(np.array(c0)),
+            cluster1=torch.from_numpy(np.array(c1)),
+            y=torch.from_numpy(np.array(z["in/y"])[g : g + 1]),
+        )
+        assert d.x.shape[0] == n
+        with torch.no_grad():
+            out = m(P.Batch.from_data_list([d])).cpu().numpy()
+        np.testing.assert_allclose(out.reshape(-1), ref_b1[g], **TOL, err_msg=f"graph {g}")
 
 
 def test_conv_layer_arbitrary_edges_vs_golden(golden):
