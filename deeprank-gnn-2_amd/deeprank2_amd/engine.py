@@ -162,7 +162,7 @@ class FusedTrainStep:
             global_batch = h.B * self.world
         scale = self.loss_scale(h, global_batch)
         if self.spec.layers is not None and layered.needs_layers(self.spec, h, self.out_dim):
-            return self._layered_step(h, scale, dropout)
+            return self._layered_step(h, scale, dropout, mask)
         lib = _lib.load()
         stream = _lib.stream_ptr(self.device)
         if mask is not None:
@@ -193,13 +193,14 @@ class FusedTrainStep:
             self._adam_after_allreduce()
         return self.loss_out, self.out[: h.B]
 
-    def _layered_step(self, h: BatchHandle, scale, dropout):
-        """A batch the model's graph pass cannot hold (``layered.py``): the
+    def _layered_step(self, h: BatchHandle, scale, dropout, mask=None):
+        """A batch the model's graph pass cannot hold, or (GINet) one with
+        non-finite inputs (``layered.py``): the
         layer-level forward (reference forward on the layer kernels), the loss
         of the fused path, autograd gradients into the flat buffer, then the
         same all-reduce (N>1) and Adam kernel as the fused step."""
         t = layered.batch_tensors(h)
-        out = self.spec.layers(self.model, t, dropout and self.model.training)
+        out = self.spec.layers(self.model, t, (dropout or mask is not None) and self.model.training, mask=mask)
         if self.loss == "mse":
             lpg = (out[:, 0] - t.y) ** 2
         else:

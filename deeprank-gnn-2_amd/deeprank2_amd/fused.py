@@ -32,6 +32,8 @@ class BatchHandle:
         self.descs = store.descriptors(self.gids_host)
         self.B = int(self.gids_host.size)
         self.max_sizes = store.max_sizes(self.gids_host)
+        nf = store.packed.nonfinite
+        self.nonfinite = bool(nf is not None and nf[self.gids_host.astype(np.int64)].any())
         self._lds = {}
         self.force_large = False  # run the split (tile + tail) path on small graphs too
         self.large_tile = None  # nodes per tile of the split path (default 128)
@@ -249,6 +251,7 @@ class FusedSpec:
     run: Callable | None = None  # (handle, weights struct, pass struct): replaces the default entry call
     layers: Callable | None = None  # (model, batch tensors, training) -> out: layer-level path (layered.py) for batches beyond LDS
     bf16: bool = False  # dr_pass.compute_dtype = DR_DTYPE_BF16 supported (runs on the large-graph path)
+    attention: bool = False  # GINetConvLayer model: batches with non-finite inputs need the layer path
 
 
 def vanilla_fused_scratch_floats(n, e, fe):

@@ -1,7 +1,10 @@
 """Layer-level execution of FoutNet, SGAT and ``ginet_nocluster.GINet`` for
 batches their per-graph kernels cannot hold (a graph beyond one workgroup's
 160 KiB of LDS, e.g. atom-level graphs).  GINet and VanillaNetwork have
-split large-graph kernels of their own and never come here.
+split large-graph kernels of their own for that.  GINet and
+``ginet_nocluster.GINet`` also come here for batches holding a non-finite
+``x`` / ``edge_attr`` entry: their kernels take the attention as identically 1,
+which holds only for finite logits (ginet.py:48-54).
 
 The forward mirrors the reference line by line on the layer API — FoutLayer /
 SGraphAttentionLayer / GINetConvLayer on the CSR and linear HIP kernels,
@@ -11,6 +14,7 @@ rocBLAS — and torch autograd differentiates it:
   * FoutNet.forward          deeprank2/neuralnets/gnn/foutnet.py:99-118
   * SGAT.forward             deeprank2/neuralnets/gnn/sgat.py:113-133
   * ginet_nocluster.GINet    deeprank2/neuralnets/gnn/ginet_nocluster.py:84-111
+  * GINet.forward            deeprank2/neuralnets/gnn/ginet.py:90-125
 The batch tensors come from the HBM store the batch handle points into
 (``batch_tensors``), in the reference's edge order (the store's CSR slot map
 ``eperm``), so each scatter sums in the same order as the reference.
@@ -35,7 +39,11 @@ def needs_layers(spec: FusedSpec, h: BatchHandle, out_dim) -> bool:
     handle asks for the layer path: ``h.force_layers``, a diagnostic)."""
     if getattr(h, "force_layers", False):
         return True
-    if spec.run is not None or spec.large is not None or spec.layers is None:
+    if spec.layers is None:
+        return False
+    if spec.attention and getattr(h, "nonfinite", False):
+        return True
+    if spec.run is not None or spec.large is not None:
         return False
     return lds_for(spec, h, out_dim) > LDS_MAX
 
@@ -113,7 +121,35 @@ def _pooled_input(t, x):
     return d
 
 
-def foutnet_forward(model, t, training=False):  # noqa: ARG001
+def _dropout(model, g, training, mask):
+    """Dropout of the head (ginet.py:122): the explicit uint8 keep mask
+    [B, 128] if given (tests, as the fused kernels take it), else torch's RNG."""
+    if not training or model.dropout <= 0:
+        return g
+    if mask is not None:
+        return g * mask.to(device=g.device, dtype=g.dtype) * (1.0 / (1.0 - model.dropout))
+    return dropout(g, model.dropout, training=True)
+
+
+def ginet_forward(model, t, training=False, mask=None):
+    """ginet.py:90-125, both branches, with GINetConvLayer's attention computed
+    whenever its inputs are non-finite (``ginet._attention_conv``)."""
+
+    def branch(conv_a, conv_b):
+        x = relu(conv_a(t.x, t.edge_index, t.edge_attr))
+        cluster = get_preloaded_cluster(t.cluster0.clone(), t.batch)
+        data = community_pooling(cluster, _pooled_input(t, x))
+        x = relu(conv_b(data.x, data.edge_index, data.edge_attr))
+        cluster = get_preloaded_cluster(data.cluster1.clone(), data.batch)
+        x, batch = max_pool_x(cluster, x, data.batch)
+        return scatter_mean(x, batch, t.n_graphs)
+
+    g = torch.cat([branch(model.conv1, model.conv2), branch(model.conv1_ext, model.conv2_ext)], dim=1)
+    g = _dropout(model, relu(model.fc1(g)), training, mask)
+    return model.fc2(g)
+
+
+def foutnet_forward(model, t, training=False, mask=None):  # noqa: ARG001
     """foutnet.py:99-118."""
     x = relu(model.conv1(t.x, t.edge_index))
     cluster = get_preloaded_cluster(t.cluster0.clone(), t.batch)
@@ -122,7 +158,7 @@ def foutnet_forward(model, t, training=False):  # noqa: ARG001
     return _pooled_head(model, data, with_edge_attr=False)
 
 
-def sgat_forward(model, t, training=False):  # noqa: ARG001
+def sgat_forward(model, t, training=False, mask=None):  # noqa: ARG001
     """sgat.py:113-133 (pooled edge_attr = PyG coalesce sums, as community_pooling gives)."""
     x = relu(model.conv1(t.x, t.edge_index, t.edge_attr))
     cluster = get_preloaded_cluster(t.cluster0.clone(), t.batch)
@@ -131,14 +167,13 @@ def sgat_forward(model, t, training=False):  # noqa: ARG001
     return _pooled_head(model, data, with_edge_attr=True)
 
 
-def ginet_nocluster_forward(model, t, training=False):
-    """ginet_nocluster.py:84-111 (dropout from torch's RNG on this path)."""
+def ginet_nocluster_forward(model, t, training=False, mask=None):
+    """ginet_nocluster.py:84-111 (dropout: the keep mask if given, else torch's RNG)."""
     ea = t.edge_attr
     x = relu(model.conv1(t.x, t.edge_index, ea))
     x = relu(model.conv2(x, t.edge_index, ea))
     x_ext = relu(model.conv1_ext(t.x, t.edge_index, ea))
     x_ext = relu(model.conv2_ext(x_ext, t.edge_index, ea))
     g = torch.cat([scatter_mean(x, t.batch, t.n_graphs), scatter_mean(x_ext, t.batch, t.n_graphs)], dim=1)
-    g = relu(model.fc1(g))
-    g = dropout(g, model.dropout, training=training)
+    g = _dropout(model, relu(model.fc1(g)), training, mask)
     return model.fc2(g)

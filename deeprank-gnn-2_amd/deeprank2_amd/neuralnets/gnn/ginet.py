@@ -16,13 +16,18 @@ so reference checkpoints load unchanged and ``Trainer`` builds it with
   over a size-1 dimension, ginet.py:54).
 * ``GINetConvLayer.forward(x, edge_index, edge_attr)`` works on any edge list
   (asymmetric, self loops, duplicates) with the generic CSR kernels.
+* Batches holding a non-finite ``x`` or ``edge_attr`` entry (flagged per graph
+  when the store is packed) run the reference forward on the layer API with
+  the attention computed (``layered.ginet_forward``): the reference's softmax
+  turns a non-finite logit into NaN (ginet.py:48-54), and those NaN rows,
+  dropped by the depth-0 ``scatter_max`` and propagated by ``max_pool_x``,
+  decide which outputs and gradients are NaN.
 
 Differences from the reference, by design: the input batch is not mutated
 (the reference overwrites ``data.x`` and offsets ``data.cluster0/1`` in
-place); the dropout mask comes from torch's device RNG, not the CPU RNG; with
-non-finite node features the set of NaN outputs can differ (the reference's
-attention turns a non-finite logit into NaN, ginet.py:54).  There is no CPU
-path: the model must live on the GPU.
+place); the dropout mask comes from a device counter hash, not the CPU RNG; a
+logit that overflows to inf from finite inputs is not detected.  There is no
+CPU path: the model must live on the GPU.
 """
 
 from __future__ import annotations
@@ -32,7 +37,7 @@ import math
 import torch
 from torch import nn
 
-from deeprank2_amd import _lib, ops
+from deeprank2_amd import _lib, layered, ops
 from deeprank2_amd.fused import BatchHandle, Dropout, FusedFn, FusedSpec, make_pass, resolve_batch, run_pass  # noqa: F401
 
 
@@ -71,10 +76,29 @@ class _ConvFn(torch.autograd.Function):
         return dx, None, dw, torch.zeros_like(w_ea), torch.zeros_like(w_att)
 
 
+def _attention_conv(layer, x, edge_index, ea):
+    """ginet.py:40-60 op for op on the device, attention included: a
+    non-finite logit makes ``softmax(dim=1)`` NaN, so its row of ``z`` is NaN
+    and the attention weights get NaN (not zero) gradients, as in the
+    reference.  Used only when ``x`` or ``edge_attr`` holds a non-finite
+    value; for finite inputs the attention is identically 1 and ``_ConvFn``
+    runs."""
+    row, col = edge_index[0], edge_index[1]
+    xcol = nn.functional.linear(x[col], layer.fc.weight)
+    xrow = nn.functional.linear(x[row], layer.fc.weight)
+    ed = nn.functional.linear(ea, layer.fc_edge_attr.weight)
+    logit = nn.functional.leaky_relu(nn.functional.linear(torch.cat([xrow, xcol, ed], dim=1), layer.fc_attention.weight))
+    alpha = torch.softmax(logit, dim=1)
+    z = torch.zeros(x.shape[0], layer.out_channels, dtype=alpha.dtype, device=alpha.device)
+    return z.index_add(0, row, alpha * xcol)
+
+
 class GINetConvLayer(nn.Module):
     """ginet.py:13-63: ``z_i = sum_{e=(i->j)} softmax_1(att_e) * W x_j``, with
-    ``softmax_1 == 1``; ``fc_edge_attr``/``fc_attention`` exist (and are
-    trained with zero gradients) exactly as in the reference."""
+    ``softmax_1 == 1`` for finite logits; ``fc_edge_attr``/``fc_attention``
+    exist (and are trained with zero gradients) exactly as in the reference.
+    Non-finite inputs take ``_attention_conv`` (NaN rows where the reference
+    has them)."""
 
     def __init__(self, in_channels, out_channels, number_edge_features=1, bias=False):
         super().__init__()
@@ -103,6 +127,8 @@ class GINetConvLayer(nn.Module):
         if ea.shape[0] != edge_index.shape[1] or ea.shape[1] != self.fc_edge_attr.in_features:
             msg = f"edge_attr must be [E, {self.fc_edge_attr.in_features}]"
             raise ValueError(msg)
+        if not bool(torch.isfinite(x).all()) or not bool(torch.isfinite(ea).all()):
+            return _attention_conv(self, x, edge_index, ea)
         return _ConvFn.apply(x, edge_index, self.fc.weight, self.fc_edge_attr.weight, self.fc_attention.weight)
 
     def __repr__(self):
@@ -166,7 +192,7 @@ def _large(h, w, p):
     _lib.check(rc, "dr_ginet_large_pass")
 
 
-SPEC = FusedSpec(PARAM_NAMES, recipe, slab_stride, head_stride, "dr_ginet_graph_pass", weights_c, _lds, dropout=0.4, large=_large, bf16=True)
+SPEC = FusedSpec(PARAM_NAMES, recipe, slab_stride, head_stride, "dr_ginet_graph_pass", weights_c, _lds, dropout=0.4, large=_large, bf16=True, layers=layered.ginet_forward, attention=True)
 
 
 def graph_pass(h: BatchHandle, params, out_dim, flags, **kw):
@@ -216,6 +242,8 @@ class GINet(nn.Module):
         if h.store.n_feat != self.input_shape:
             msg = f"batch has {h.store.n_feat} node features, model expects {self.input_shape}"
             raise ValueError(msg)
+        if layered.needs_layers(SPEC, h, self.output_shape):  # non-finite x / edge_attr: the attention matters
+            return SPEC.layers(self, layered.batch_tensors(h), self.training, mask=dropout_mask)
         dropout = None
         if self.training and self.dropout > 0:
             if dropout_mask is not None:

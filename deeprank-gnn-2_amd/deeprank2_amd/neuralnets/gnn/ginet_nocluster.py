@@ -31,7 +31,7 @@ def _lds(n, e, k0, p1, k1, f, alias, out):  # noqa: ARG001
     return _lib.load().dr_ginet_nocluster_lds_bytes(n, e, f, out)
 
 
-SPEC = FusedSpec(PARAM_NAMES, _ginet.recipe, _ginet.slab_stride, _ginet.head_stride, "dr_ginet_nocluster_graph_pass", _ginet.weights_c, _lds, dropout=0.4, layers=layered.ginet_nocluster_forward)
+SPEC = FusedSpec(PARAM_NAMES, _ginet.recipe, _ginet.slab_stride, _ginet.head_stride, "dr_ginet_nocluster_graph_pass", _ginet.weights_c, _lds, dropout=0.4, layers=layered.ginet_nocluster_forward, attention=True)
 
 
 def graph_pass(h: BatchHandle, params, out_dim, flags, **kw):
@@ -79,8 +79,8 @@ class GINet(nn.Module):
         if h.store.n_feat != self.input_shape:
             msg = f"batch has {h.store.n_feat} node features, model expects {self.input_shape}"
             raise ValueError(msg)
-        if layered.needs_layers(SPEC, h, self.output_shape):  # a graph beyond one workgroup's LDS
-            return SPEC.layers(self, layered.batch_tensors(h), self.training)
+        if layered.needs_layers(SPEC, h, self.output_shape):  # a graph beyond LDS, or non-finite inputs
+            return SPEC.layers(self, layered.batch_tensors(h), self.training, mask=dropout_mask)
         dropout = None
         if self.training and self.dropout > 0:
             if dropout_mask is not None:

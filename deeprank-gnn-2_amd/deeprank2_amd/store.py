@@ -76,6 +76,10 @@ class PackedGraphs:
     p1_ea: np.ndarray | None  # [P1_all, Fe] pooled edge_attr (PyG coalesce: sums of merged edges)
     names: list = field(default_factory=list)
     has_clusters: bool = True  # False: cluster0/1 were missing and filled with one cluster per graph
+    # per graph: a non-finite x or edge_attr entry.  GINet's attention
+    # (ginet.py:48-54) is identically 1 only for finite logits; such graphs
+    # take the layer path, which computes it (layered.ginet_forward)
+    nonfinite: np.ndarray | None = None
 
     # per-graph sizes (host side, for launch geometry)
     def sizes(self):
@@ -195,6 +199,7 @@ def pack_graphs(records: list[GraphRecord], require_clusters: bool = True, threa
     o.p1_ea = P(p1_ea)
     _lib.check(lib.dr_pack_fill(inp, o, ctypes.addressof(sym), threads), "dr_pack_fill")
     return PackedGraphs(
+        nonfinite=nonfinite_graphs(x, node_off, ea_all, edge_off),
         n_feat=F,
         n_graphs=G,
         x=x,
@@ -211,6 +216,19 @@ def pack_graphs(records: list[GraphRecord], require_clusters: bool = True, threa
         has_clusters=has_clusters,
         **out,
     )
+
+
+def nonfinite_graphs(x, node_off, edge_attr=None, edge_off=None) -> np.ndarray:
+    """bool [G]: graph g holds a non-finite node feature or edge attribute."""
+    G = node_off.size - 1
+    bad = np.zeros(G, bool)
+    for a, off in ((x, node_off), (edge_attr, edge_off)):
+        if a is None or a.size == 0:
+            continue
+        rows = np.flatnonzero(~np.isfinite(a.reshape(a.shape[0], -1)).all(axis=1))
+        if rows.size:
+            bad[np.searchsorted(off, rows, side="right") - 1] = True
+    return bad
 
 
 def records_from_batch(batch) -> list[GraphRecord]:

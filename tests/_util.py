@@ -43,7 +43,8 @@ def assert_grad_close(actual, ref, rtol=1e-4, ntol=1e-6, err_msg=""):
     that scale with the tensor's largest entries (~1e3 on the 1ATN fixture),
     so tiny entries of a large gradient need the normwise floor."""
     ref = np.asarray(ref)
-    scale = float(np.abs(ref).max()) if ref.size else 0.0
+    fin = np.abs(ref[np.isfinite(ref)])
+    scale = float(fin.max()) if fin.size else 0.0  # NaN entries must match NaN (assert_allclose equal_nan)
     np.testing.assert_allclose(np.asarray(actual), ref, rtol=rtol, atol=max(1e-6, ntol * scale), err_msg=err_msg)
 
 

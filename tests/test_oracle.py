@@ -60,6 +60,34 @@ def test_model_matches_reference(golden, name, cls, args):
         assert_grad_close(grads[k], ref[k], err_msg=k)
 
 
+@pytest.mark.parametrize("name,cls", [("ginet_nonfinite_all", "GINet"), ("ginet_nonfinite_conv1", "GINet"), ("ginet_nocluster_nonfinite", "GINetNoCluster")])
+def test_model_matches_reference_nonfinite_inputs(golden, name, cls):
+    """inf edge attributes / NaN node features: the reference's singleton
+    softmax gives NaN for a non-finite logit (ginet.py:48-54); NaN outputs and
+    gradients must sit exactly where the reference's are."""
+    z = golden(name)
+    out_eval, out_train, loss, grads = _run(gnn_ref.MODELS[cls](30, 1, 3), z, "mse", z["mask"])
+    np.testing.assert_allclose(out_eval, z["out/eval"], **TOL)
+    np.testing.assert_allclose(out_train, z["out/train"], **TOL)
+    np.testing.assert_allclose(loss, float(z["loss"]), rtol=1e-5)
+    ref = golden_grads(z)
+    for k in ref:
+        assert_grad_close(grads[k], ref[k], err_msg=k)
+
+
+def test_conv_layer_nonfinite_edge_attr(golden):
+    z = golden("ginet_conv_layer_nonfinite")
+    layer = gnn_ref.GINetConvLayer(12, 16, 2)
+    layer.load_state_dict(golden_state_dict(z))
+    x = torch.from_numpy(z["in/x"]).requires_grad_(True)
+    out = layer(x, torch.from_numpy(z["in/edge_index"]), torch.from_numpy(z["in/edge_attr"]))
+    (out * torch.from_numpy(z["in/gz"])).sum().backward()
+    np.testing.assert_allclose(out.detach().numpy(), z["out/z"], **TOL)
+    np.testing.assert_allclose(x.grad.numpy(), z["grad/x"], **TOL)
+    for n, p in layer.named_parameters():
+        np.testing.assert_allclose(p.grad.numpy(), z["grad/" + n], **TOL, err_msg=n)
+
+
 def test_ginet_dead_attention_grads_are_exactly_zero(golden):
     """softmax over the singleton dim makes the attention constant."""
     z = golden("ginet_1atn")

@@ -181,3 +181,21 @@ def test_native_packer_errors_and_missing_clusters():
         pack_graphs(recs)
     p = pack_graphs(recs, require_clusters=False)
     assert not p.has_clusters and p.m1_ptr.tolist() == [0, 1] * 3
+
+
+def test_nonfinite_flag_per_graph(golden):
+    """The packer flags each graph holding a non-finite x / edge_attr entry
+    (GINet routes those batches to the layer path that computes the attention)."""
+    from _util import golden_batch
+
+    from deeprank2_amd.store import nonfinite_graphs
+
+    z = golden("ginet_nonfinite_all")
+    p = pack_graphs(records_from_batch(golden_batch(z)))
+    assert p.nonfinite.tolist() == [True, True, True, False, False]
+    x = np.zeros((6, 2), np.float32)
+    x[4, 1] = np.inf
+    ea = np.zeros((5, 1), np.float32)
+    ea[0, 0] = np.nan
+    assert nonfinite_graphs(x, np.array([0, 2, 4, 6]), ea, np.array([0, 1, 3, 5])).tolist() == [True, False, True]
+    assert nonfinite_graphs(x[:0], np.array([0])).tolist() == []
