@@ -254,6 +254,7 @@ def parse_args(argv):
     ap.add_argument("--dtype", choices=["f32", "bf16"], default="f32", help="compute dtype of the node GEMMs (bf16: GINet only; fp32 accumulate, fp32 master weights and Adam)")
     ap.add_argument("--force-large", type=int, default=0, help="GINet: run the split tile+tail path with this many nodes per tile (diagnostic)")
     ap.add_argument("--ginet-path", choices=["auto", "split", "onepass"], default="auto", help="GINet: auto = one workgroup per graph when the batch fits LDS, else the split path; split = tile kernel + tail kernel; onepass = tiles + in-launch tails (one launch)")
+    ap.add_argument("--one-launch", action="store_true", help="GINet, N=1: graph pass + gradient reduce + Adam in one launch (dr_ginet_train_step; opt-in, measured slower at B=64)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stream-copy", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch every step from Python instead of replaying captured HIP graphs")
@@ -346,6 +347,7 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
             torch.distributed.broadcast(p.data, 0)
     step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5, loss="mse", process_group=pg, compute_dtype=args.dtype)
     model._drop_seed = 77 + rank  # training-mode dropout drawn in-kernel (counter hash)
+    step.fuse_update = bool(args.one_launch)
 
     def run_eager(i):
         return step.step(handles[i % len(handles)], global_batch=B * world)
@@ -437,11 +439,13 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
         torch.distributed.all_reduce(et)
     edges_total = float(et.item())
     s = 2 if args.dtype == "bf16" else 4
+    one = all(step.one_launch(h) for h in handles)  # graph pass + reduce + Adam in one kernel
     alg = float(np.mean([algorithmic_bytes(packed, h.gids_host, args.model, s) for h in handles]))
     design = float(np.mean([design_bytes(packed, h.gids_host, args.model) for h in handles]))
     n_params = sum(p.numel() for p in model.parameters())
     adam_bytes = 28 * n_params  # Adam fp32: read param, grad, m, v; write param, m, v (§8(d))
-    achieved = alg / (kernel_ms * 1e-3) / 1e9
+    kernel_alg = alg + (adam_bytes if one else 0)
+    achieved = kernel_alg / (kernel_ms * 1e-3) / 1e9
     ms_step = elapsed / args.steps * 1e3
     wall_gbs = (alg + adam_bytes) / (ms_step * 1e-3) / 1e9
     default_cfg = args.model == "ginet" and args.graphs == "residue" and B == B_PER_GPU and args.dtype == "f32"
@@ -456,7 +460,7 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(graphs[:B], model_name=args.model)
         workload = WORKLOADS.get((args.model, args.graphs), f"{args.model} on {args.graphs} graphs (diagnostic)")
-        kname = "layer-level path (FoutLayer/SGAT/GINetConvLayer + pooling kernels, torch autograd): whole-step wall clock" if layer_path else {"ginet": ("ginet_onepass_kernel (dr_ginet_large_pass, one launch)" if args.ginet_path == "onepass" else "ginet_large_conv1_kernel + ginet_large_tail_kernel (dr_ginet_large_pass)") if large else "ginet_graph_kernel (dr_ginet_graph_pass, fwd+loss+bwd, 1 workgroup/graph)", "foutnet": "fout_graph_kernel<false> (dr_fout_graph_pass)", "vanilla": "vanilla_graph_kernel (dr_vanilla_fused_pass) / vanilla pipeline (dr_vanilla_graph_pass)", "sgat": "fout_graph_kernel<true> (dr_sgat_graph_pass)", "ginet_nocluster": "ginet_nocluster_kernel (dr_ginet_nocluster_graph_pass)"}[args.model]
+        kname = "layer-level path (FoutLayer/SGAT/GINetConvLayer + pooling kernels, torch autograd): whole-step wall clock" if layer_path else {"ginet": ("ginet_onepass_kernel (dr_ginet_large_pass, one launch)" if args.ginet_path == "onepass" else "ginet_large_conv1_kernel + ginet_large_tail_kernel (dr_ginet_large_pass)") if large else ("ginet_step_kernel (dr_ginet_train_step: fwd+loss+bwd, 1 workgroup/graph, then gradient reduce + Adam by the last 64 workgroups)" if one else "ginet_graph_kernel (dr_ginet_graph_pass, fwd+loss+bwd, 1 workgroup/graph)"), "foutnet": "fout_graph_kernel<false> (dr_fout_graph_pass)", "vanilla": "vanilla_graph_kernel (dr_vanilla_fused_pass) / vanilla pipeline (dr_vanilla_graph_pass)", "sgat": "fout_graph_kernel<true> (dr_sgat_graph_pass)", "ginet_nocluster": "ginet_nocluster_kernel (dr_ginet_nocluster_graph_pass)"}[args.model]
         result = {
             "metric": HEADLINE_METRIC if default_cfg else f"graphs/sec per training step, {workload} (fwd+MSE+bwd+Adam)",
             "value": round(graphs_total / elapsed, 1),
@@ -494,12 +498,12 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "algorithmic_bytes_per_launch": int(alg),
-                "algorithmic_definition": "SURVEY §8(d) B_alg: s*N*F + 4E + 4(N+1) + 4N + 4K0 + 4 per graph (s=2 bf16, 4 fp32; +s*E*Fe Vanilla, no clusters for Vanilla/ginet_nocluster)",
+                "algorithmic_bytes_per_launch": int(kernel_alg),
+                "algorithmic_definition": "SURVEY §8(d) B_alg: s*N*F + 4E + 4(N+1) + 4N + 4K0 + 4 per graph (s=2 bf16, 4 fp32; +s*E*Fe Vanilla, no clusters for Vanilla/ginet_nocluster)" + (" + 28*P Adam bytes (the kernel runs the optimizer step)" if one else ""),
                 "design_bytes_per_launch": int(design),
                 "design_definition": "per-graph gradient slab + head vectors (written, then read by the reduce) and the precomputed pooling structures: intermediates of this design, not compulsory",
                 "kernel_ms_avg": round(kernel_ms, 5),
-                "kernel_timing": "wall clock per eager step (layer-level path)" if layer_path else f"HIP events around one HIP graph of {args.steps} back-to-back {step.spec.entry if not large else 'dr_ginet_large_pass'} launches on the launch stream, divided by {args.steps}",
+                "kernel_timing": "wall clock per eager step (layer-level path)" if layer_path else f"HIP events around one HIP graph of {args.steps} back-to-back {('dr_ginet_train_step' if one else step.spec.entry) if not large else 'dr_ginet_large_pass'} launches on the launch stream, divided by {args.steps}",
                 "stream_copy_GBs": None if copy_gbs is None else round(copy_gbs, 1),
                 "frac_of_stream_copy": None if copy_gbs is None else round(achieved / copy_gbs, 5),
                 "wallclock": {"bytes_per_step": int(alg + adam_bytes), "achieved": round(wall_gbs, 2), "frac": round(wall_gbs / HBM_PEAK_GBS, 5), "note": "B_alg(step) = sum_g B_alg(g) + 28*P (Adam fp32) over ms_per_step"},

@@ -30,12 +30,15 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/deeprank2_amd.h"
 #include "dr_common.h"
 #include "graph_common.h"
 #include "ginet_head.h"
+#include "reduce_common.h"
 
 namespace {
 
@@ -45,6 +48,8 @@ constexpr int HEADW = 672;   // G64 hpre128 hh128 hd128 dh128 dG64 dout16 spare1
 constexpr float LOWEST = -3.402823466e+38f;
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned int gu32;
 
 __host__ __device__ inline int r4(int v) { return (v + 3) & ~3; }
 __host__ __device__ inline int r16(int v) { return (v + 15) & ~15; }
@@ -192,9 +197,18 @@ __device__ __forceinline__ void gather_rows(const int* rp, const uint16_t* col, 
     if (tid == 0 && a.p.stamps) a.p.stamps[(int64_t)b * 32 + (i)] = __builtin_amdgcn_s_memtime(); \
     __builtin_amdgcn_sched_barrier(0);                                                            \
   } while (0)
+#define SSTAMP(i)                                                                                   \
+  do {                                                                                              \
+    __builtin_amdgcn_sched_barrier(0);                                                              \
+    if (tid == 0 && ga.p.stamps) ga.p.stamps[(int64_t)b * 32 + (i)] = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0);                                                              \
+  } while (0)
 #else
 #define STAMP(i) \
   do {           \
+  } while (0)
+#define SSTAMP(i) \
+  do {            \
   } while (0)
 #endif
 
@@ -255,7 +269,7 @@ __device__ __forceinline__ TailLds tail_lds(const C& c, float* lds) {
   return t;
 }
 
-template <class ZAt>
+template <class ZAt, bool WT = false>
 __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t, const float (&fc1_row)[8],
                                            const float (&fc1_col)[8], float fc1_bias, int b, int N, int K0, int K1,
                                            int F, int OUT, float y_g, uint64_t drop_offset, ZAt zat) {
@@ -375,7 +389,7 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
     hl.dout = t.dout;
     hl.dgp = t.dgp;
     hl.keep = t.keep;
-    if (!drk::ginet_head<NT>(a.p, hl, fc1_row, fc1_col, fc1_bias, b, OUT, y_g, drop_offset, 8)) return;
+    if (!drk::ginet_head<NT, WT>(a.p, hl, fc1_row, fc1_col, fc1_bias, b, OUT, y_g, drop_offset, 8)) return;
   }  // stamps 8 (forward head done) and 9 (loss gradient done) are taken inside
 
   STAMP(10);
@@ -419,7 +433,7 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
         for (int u = 0; u < 4; ++u) acc = fmaf(yv[u], pv[u], acc);
       }
       for (; k < K0; ++k) acc = fmaf(t.y2[k * 64 + o], t.p1[k * 32 + br * 16 + j], acc);
-      slab[p] = acc;
+      drk::st_part<WT>(slab + p, acc);
     }
     for (int p = tid; p < K0 * 32; p += NT) {
       const int k = p >> 5, ch = p & 31, br = ch >> 4, j = ch & 15;
@@ -446,7 +460,7 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
           acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) slab[br * 512 + (ot * 16 + kq * 4 + r) * 16 + li] = acc[r];
+        for (int r = 0; r < 4; ++r) drk::st_part<WT>(slab + br * 512 + (ot * 16 + kq * 4 + r) * 16 + li, acc[r]);
       } else {
         const int q = job - 4, br = q & 1, r0 = (q >> 1) * 16;
         const int kr = min(r0 + li, K0 - 1);
@@ -500,15 +514,18 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
         for (int u = 0; u < 8; ++u)
           if (ok[u]) acc = fmaf(dv[u], zv[u], acc);
       }
-      slab[p] = acc;
+      drk::st_part<WT>(slab + p, acc);
     }
   }
   STAMP(14);
 }
 
 // KPT: conv1's K (F) padded to whole 16-deep MFMA steps, 32 (F <= 32) or 64.
-template <int KPT>
-__global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
+// WT: the per-graph partials are stored write-through (read back inside the
+// same launch by dr_ginet_train_step's reducers).  Returns the step counter
+// value the pass used (its dropout offset).
+template <int KPT, bool WT>
+__device__ __forceinline__ uint64_t graph_body(const GinetArgs& a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -725,10 +742,134 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
 
   TailLds t = tail_lds(c, lds);
   t.keep = skeep;
-  ginet_tail(a, t, fc1_row, fc1_col, fc1_bias, b, N, K0, K1, F, OUT, y_g, drop_offset,
-             [&](int i, int kk) { return sZ[i * LDW + kk]; });
+  auto zat = [&](int i, int kk) { return sZ[i * LDW + kk]; };
+  ginet_tail<decltype(zat), WT>(a, t, fc1_row, fc1_col, fc1_bias, b, N, K0, K1, F, OUT, y_g, drop_offset, zat);
+  return drop_offset;
 }
 
+template <int KPT>
+__global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
+  graph_body<KPT, false>(a);
+}
+
+// ---------------------------------------------------------------------------
+// One-launch training step (dr_ginet_train_step): B graph workgroups run the
+// graph pass; NR more workgroups of the same grid (blockIdx >= B) are the
+// reducers: they wait for the B arrivals, then sum the partials over the batch
+// and apply Adam (reduce_common.h: the same fixed-order arithmetic as
+// dr_reduce_update, so parameters are bit-identical to the two-launch step).
+//
+// Hand-off (MI355X_MICROARCH.md §inter-workgroup visibility, table row 1):
+// every graph workgroup stores its partials (slab, head vectors, loss term)
+// write-through (sc1), every wave drains them (s_waitcnt vmcnt(0)), and after
+// a workgroup barrier one lane adds to the arrival counter (agent atomic).  A
+// reducer polls the counter (sc1 loads, s_sleep, bounded) until all B have
+// arrived; its waves then read the partials with sc1 loads only.  Graph
+// workgroups never wait, and at most NR <= 128 reducers (of 256 CUs) ever do,
+// so any dispatch order completes.  Each reducer reads the step counter before
+// it counts itself past the poll; the last one past it writes the new step
+// and returns the counters to zero for the next launch.
+// ---------------------------------------------------------------------------
+constexpr int STEP_PARAMS = 16;
+constexpr int STEP_NR_MAX = 128;
+
+struct GinetStepArgs {
+  GinetArgs g;
+  drr::ReduceHdr h;
+  drr::ParamRec rec[STEP_PARAMS];
+  uint32_t* sync;  // [4]: arrivals, reducers past the poll, timeout flag, spare
+  int32_t NR;      // reducer workgroups (blockIdx B .. B+NR-1)
+  int32_t diag;    // DR_STEP_DIAG=1: reducers skip the reduction (times the pass + hand-off alone)
+};
+
+template <int KPT>
+__global__ void __launch_bounds__(NT) ginet_step_kernel(GinetStepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  gu32* arrive = (gu32*)(a.sync);
+  gu32* passed = (gu32*)(a.sync + 1);
+  const int B = a.g.B;
+  if ((int)blockIdx.x < B) {
+    graph_body<KPT, true>(a.g);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave drains its write-through partials
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  const int role = blockIdx.x - B;
+  const int tid = threadIdx.x, b = blockIdx.x;
+  const GinetArgs& ga = a.g;
+  (void)tid;
+  (void)b;
+  (void)ga;
+  SSTAMP(0);
+  int64_t* sw = reinterpret_cast<int64_t*>(lds);
+  if (threadIdx.x == 0) {
+    // Adam's step: the counter every graph workgroup read (nothing writes it
+    // before every reducer is past the poll)
+    const int64_t t = (int64_t)__hip_atomic_load((__attribute__((address_space(1))) unsigned long long*)(a.g.p.step_counter),
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    uint32_t polls = 0;
+    int ok = 1;
+    while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)B) {
+      __builtin_amdgcn_s_sleep(20);  // ~1.3 K cycles between polls: little traffic beside the graph pass
+      if (++polls == (1u << 22)) {  // seconds: never expected; flag it and finish the launch
+        __hip_atomic_store((gu32*)(a.sync + 2), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+    }
+    const uint32_t d = __hip_atomic_fetch_add(passed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == (uint32_t)a.NR - 1) {  // the last reducer past the poll: new step, counters back to zero
+      a.g.p.step_counter[0] = t;
+      __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(passed, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    sw[0] = ok && !a.diag ? t : -1;
+  }
+  __syncthreads();
+  SSTAMP(1);
+  const int64_t tstep = sw[0];
+  if (tstep < 0) return;
+  // reduce blocks: two per workgroup pass (2 x 512 threads), slot = 2 role +
+  // half, blocks slot, slot + 2 NR, ...; every thread runs the same number of
+  // calls (reduce_block holds a workgroup barrier), past the end on an empty
+  // record
+  const int half = threadIdx.x / drr::RT, t = threadIdx.x % drr::RT;
+  float(*part)[drr::RP] = reinterpret_cast<float(*)[drr::RP]>(lds + 64) + half * drr::RC;
+  const int nb = a.h.n_blocks, stride = 2 * a.NR;
+  // the records, read in place from the kernel-argument segment (a dynamic
+  // index into the by-value argument would copy it to scratch)
+  typedef const __attribute__((address_space(4))) drr::ParamRec ConstRec;
+  ConstRec* recs = (ConstRec*)((const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() +
+                               offsetof(GinetStepArgs, rec));
+  for (int j0 = 0; j0 < nb; j0 += stride) {
+    const int j = j0 + 2 * role + half;  // block j -> (parameter, element block): no dependent loads
+    int pi = 0;
+#pragma unroll
+    for (int q = 1; q <= STEP_PARAMS; ++q) pi += (a.h.blk0[q] <= j) ? 1 : 0;
+    pi = j < nb ? pi : a.h.n_params;
+    int eb = pi < a.h.n_params ? j - a.h.blk0[pi] : 0;
+    drr::ParamRec r;
+    memset(&r, 0, sizeof(r));
+    if (pi < a.h.n_params) {  // field by field: scalar loads from the argument segment
+      ConstRec& q = recs[pi];
+      r.param = q.param;
+      r.grad = q.grad;
+      r.m = q.m;
+      r.v = q.v;
+      r.numel = q.numel;
+      r.kind = q.kind;
+      r.off1 = q.off1;
+      r.off2 = q.off2;
+      r.cols = q.cols;
+    } else {
+      eb = 0;
+    }
+    drr::reduce_block<1, true>(a.h, r, eb, j == 0, t, part, tstep);
+    __syncthreads();  // part reused by the next pass
+  }
+  SSTAMP(2);
+}
 
 // =========================================================================
 // Graphs larger than one workgroup's LDS (atom-level: N ~ 3e3, E ~ 5e4).
@@ -796,8 +937,6 @@ __device__ __forceinline__ int lower_bound_lds(const int* v, int lo, int hi, int
 // per-XCD L2, so a payload stored this way, drained (s_waitcnt vmcnt(0)) and
 // signalled by an agent-scope counter add is read correctly by the workgroup
 // whose add came last with sc1 loads, wherever the two sit.
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-typedef __attribute__((address_space(1))) unsigned int gu32;
 
 template <bool INL>
 __device__ __forceinline__ void store_u64(void* p, uint64_t v) {
@@ -1469,6 +1608,54 @@ extern "C" int dr_ginet_graph_pass(const dr_graph_store* store, const dr_graph_d
   } else {
     DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_graph_kernel<64>)));
     hipLaunchKernelGGL(ginet_graph_kernel<64>, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, args);
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int dr_ginet_train_step(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                                   const dr_ginet_weights* w, const dr_pass* pass, int32_t lds_bytes,
+                                   const dr_param_table* table, const dr_adam* adam, float* loss_out, uint32_t* sync,
+                                   void* stream) {
+  if (!store || !descs || !w || !pass || !table || !adam || !sync || n_batch < 0) return DR_E_ARG;
+  if (pass->out_dim < 1 || pass->out_dim > DR_MAX_OUT) return DR_E_UNSUPPORTED;
+  if (store->n_feat < 1 || 32 * store->n_feat > 2 * NT) return DR_E_UNSUPPORTED;  // F <= 64
+  if (lds_bytes > 160 * 1024) return DR_E_LDS;
+  if (pass->compute_dtype != DR_DTYPE_F32) return DR_E_UNSUPPORTED;
+  if (pass->flags != (DR_PASS_FORWARD | DR_PASS_BACKWARD) || pass->loss_kind == DR_LOSS_NONE) return DR_E_ARG;
+  if (!pass->out || !pass->slab || !pass->head || !pass->loss_per_graph || !pass->step_counter) return DR_E_ARG;
+  if (pass->use_dropout == DR_DROPOUT_MASK && !pass->mask) return DR_E_ARG;
+  if (pass->use_dropout < DR_DROPOUT_OFF || pass->use_dropout > DR_DROPOUT_HASH) return DR_E_ARG;
+  if (!adam->enabled || adam->step_counter != pass->step_counter || adam->grad_div) return DR_E_ARG;
+  if (table->n_params > STEP_PARAMS || table->slab_stride != DR_SLAB_STRIDE(store->n_feat) ||
+      table->head_stride != DR_HEAD_STRIDE(pass->out_dim))
+    return DR_E_ARG;
+  if (n_batch == 0) return DR_OK;
+  if (!store->cl0) return DR_E_ARG;
+  GinetStepArgs a;
+  std::memset(&a, 0, sizeof(a));
+  const int blocks = drr::build_reduce(table, pass->slab, pass->head, n_batch, adam, pass->loss_per_graph,
+                                       pass->loss_scale, loss_out, a.h, a.rec);
+  if (blocks < 0) return blocks;
+  a.g.s = *store;
+  a.g.w = *w;
+  a.g.p = *pass;
+  a.g.descs = descs;
+  a.g.B = n_batch;
+  a.sync = sync;
+  a.NR = (blocks + 1) / 2 < STEP_NR_MAX ? (blocks + 1) / 2 : STEP_NR_MAX;
+  if (a.NR < 1) return DR_E_ARG;
+  {
+    static const char* env = std::getenv("DR_STEP_DIAG");  // diagnostic: skip the reduction
+    a.diag = env ? std::atoi(env) : 0;
+  }
+  const int lds = lds_bytes > (64 + 2 * drr::RT) * 4 ? lds_bytes : (64 + 2 * drr::RT) * 4;
+  const dim3 grid(n_batch + a.NR);
+  if (store->n_feat <= 32) {
+    DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_step_kernel<32>)));
+    hipLaunchKernelGGL(ginet_step_kernel<32>, grid, dim3(NT), lds, (hipStream_t)stream, a);
+  } else {
+    DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_step_kernel<64>)));
+    hipLaunchKernelGGL(ginet_step_kernel<64>, grid, dim3(NT), lds, (hipStream_t)stream, a);
   }
   return (int)hipGetLastError();
 }

@@ -40,7 +40,20 @@ __device__ __forceinline__ void head_stamp(int64_t* row, int i) {
 #endif
 }
 
-template <int NT>
+// Per-graph partial stores: plain, or write-through (sc1: agent-scope relaxed
+// atomic stores) when other workgroups of the same launch read them
+// (dr_ginet_train_step's in-launch reduction; MI355X_MICROARCH.md
+// §inter-workgroup visibility).
+template <bool WT>
+__device__ __forceinline__ void st_part(float* p, float v) {
+  if (WT)
+    __hip_atomic_store((__attribute__((address_space(1))) unsigned int*)(p), __float_as_uint(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  else
+    *p = v;
+}
+
+template <int NT, bool WT = false>
 __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds& t, const float (&fc1_row)[8],
                                            const float (&fc1_col)[8], float fc1_bias, int b, int OUT, float y_g,
                                            uint64_t drop_offset, int stamp0 = -1) {
@@ -85,7 +98,7 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
   if (tid == 0) {
     if (p.loss_kind == DR_LOSS_MSE) {
       const float d = t.dout[0] - y_g;
-      if (p.loss_per_graph) p.loss_per_graph[b] = d * d;
+      if (p.loss_per_graph) st_part<WT>(p.loss_per_graph + b, d * d);
       t.dout[0] = 2.f * d * p.loss_scale;
     } else if (p.loss_kind == DR_LOSS_CE) {
       const int yi = (int)y_g;
@@ -95,7 +108,7 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
       for (int q = 0; q < OUT; ++q) se += expf(t.dout[q] - mx);
       const float lse = mx + logf(se);
       const float wy = p.class_w ? p.class_w[yi] : 1.f;
-      if (p.loss_per_graph) p.loss_per_graph[b] = wy * (lse - t.dout[yi]);
+      if (p.loss_per_graph) st_part<WT>(p.loss_per_graph + b, wy * (lse - t.dout[yi]));
       for (int q = 0; q < OUT; ++q) t.dout[q] = wy * (expf(t.dout[q] - lse) - (q == yi ? 1.f : 0.f)) * p.loss_scale;
     } else {
       for (int q = 0; q < OUT; ++q) t.dout[q] = p.dout[(int64_t)b * OUT + q];
@@ -128,12 +141,12 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
   {
     const int HS = DR_HEAD_STRIDE(OUT);
     float* hg = p.head + (int64_t)b * HS;
-    if (tid < 64) hg[tid] = t.g[tid];
+    if (tid < 64) st_part<WT>(hg + tid, t.g[tid]);
     if (tid < 128) {
-      hg[64 + tid] = t.hd[tid];
-      hg[192 + tid] = t.dh[tid];
+      st_part<WT>(hg + 64 + tid, t.hd[tid]);
+      st_part<WT>(hg + 192 + tid, t.dh[tid]);
     }
-    if (tid < OUT) hg[320 + tid] = t.dout[tid];
+    if (tid < OUT) st_part<WT>(hg + 320 + tid, t.dout[tid]);
   }
   __syncthreads();
 

@@ -1,0 +1,233 @@
+// Gradient reduction over the batch + Adam for one block of parameter
+// elements: shared by the stand-alone reduce kernel (reduce_adam.hip) and the
+// one-launch GINet training step (ginet_fused.hip), so both sum the per-graph
+// partials in the same fixed order and give bit-identical parameters.
+//
+// Replaces loss_.backward()'s accumulation over the batch and
+// optimizer.step() of Trainer._epoch (deeprank2/trainer.py:689-690; Adam
+// configured at trainer.py:419).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+
+#include "../../include/deeprank2_amd.h"
+#include "dr_common.h"
+
+namespace drr {
+
+constexpr int RP = 64;  // parameter elements per block
+constexpr int RC = 8;   // batch chunks per block
+constexpr int RU = 8;   // batch rows per chunk issued together (predicated)
+constexpr int RT = RP * RC;  // threads per block
+
+// One 64-byte kernel-argument line per parameter: a block fetches everything
+// it needs about its parameter with one scalar load.
+struct alignas(64) ParamRec {
+  float* param;
+  float* grad;
+  float* m;
+  float* v;
+  int32_t numel, kind, off1, off2;
+  int32_t cols, pad0, pad1, pad2;
+};
+
+struct alignas(64) ReduceHdr {
+  const float* slab;
+  const float* head;
+  const float* lpg;
+  float* loss_out;
+  int64_t* step_counter;
+  const float* grad_div;
+  int32_t B, slab_stride, head_stride, adam_enabled;
+  float loss_scale, pad0;
+  float lr, beta1, beta2, eps, weight_decay, bias_c1, bias_c2_sqrt, pad1;
+  float log2_beta1, log2_beta2;  // beta^t = exp2(t log2 beta): one v_exp_f32, not powf
+  int32_t n_params, n_blocks;
+  int16_t blk0[18];  // first block of each parameter (prefix sums of ceil(numel / RP)), blk0[n_params] = n_blocks
+  int32_t pad2;
+};
+
+typedef __attribute__((address_space(1))) unsigned int gu32r;
+
+// LD: how the partials are read.  0: plain loads (written by an earlier
+// launch).  1: agent-scope relaxed atomic loads (sc1: past this CU's L1) and
+// 2: system-scope ones, for partials published inside the same launch by
+// write-through stores of other workgroups (MI355X_MICROARCH.md
+// §inter-workgroup visibility).
+template <int LD>
+__device__ __forceinline__ float ld_part(const float* p) {
+  if (LD == 1) return __uint_as_float(__hip_atomic_load((const gu32r*)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (LD == 2) return __uint_as_float(__hip_atomic_load((const gu32r*)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+  return *p;
+}
+
+// One block = RP consecutive elements (from elem_block * RP) of parameter r,
+// RC batch chunks per element; t = thread index within the block's RT
+// threads, part = the block's [RC][RP] LDS scratch.  first: the block that
+// also sums the loss and advances the step counter.  tstep: the Adam step
+// (counter[1] + 1) when h.step_counter is set.  Every load of the block is
+// issued in one straight-line group (clamped indices, zero weights past the
+// batch), so one wait covers the partials and the Adam state.  The caller
+// synchronises the workgroup between two calls that share `part`.
+template <int LD, bool LEAN = false>
+__device__ __forceinline__ void reduce_block(const ReduceHdr& h, const ParamRec& r, int elem_block, bool first, int t,
+                                             float (*part)[RP], int64_t tstep) {
+  // LEAN: partials always given, Adam always on (the one-launch step): the
+  // gradients-supplied path is compiled out (less code to fetch cold)
+  const int lp = t % RP, ch = t / RP;
+  const int e = elem_block * RP + lp;
+  const bool live = e < r.numel;
+  if (first && t < 64 && h.lpg && h.loss_out) {
+    float acc = 0.f;  // lane-strided partial sums, then a fixed-order wave reduction
+    for (int b = t; b < h.B; b += 64) acc += ld_part<LD>(h.lpg + b);
+    acc = dr_wave_sum(acc);
+    if (t == 0) h.loss_out[0] = acc * h.loss_scale;
+  }
+  const int ec = live ? e : 0;
+  const bool slab_kind = r.kind == DR_GRAD_SLAB, outer = r.kind == DR_GRAD_OUTER;
+  const bool has_src = h.slab && (slab_kind || outer || r.kind == DR_GRAD_HEAD);
+  const float* base = slab_kind ? h.slab : h.head;
+  const int64_t st = slab_kind ? h.slab_stride : h.head_stride;
+  const int col1 = outer ? r.off1 + ec / r.cols : r.off1 + ec;
+  const int col2 = outer ? r.off2 + ec % r.cols : 0;
+  const int b0 = (h.B * ch) / RC, b1 = (h.B * (ch + 1)) / RC;
+  float u[RU], w[RU];
+  if (has_src && b0 < b1) {
+#pragma unroll
+    for (int k = 0; k < RU; ++k) {
+      const int64_t row = min(b0 + k, b1 - 1);
+      u[k] = ld_part<LD>(base + row * st + col1);
+      w[k] = outer ? ld_part<LD>(base + row * st + col2) : 1.f;
+    }
+  }
+  const bool upd = live && ch == 0 && (LEAN || h.adam_enabled);
+  float p0 = 0.f, m0 = 0.f, v0 = 0.f, gin = 0.f;
+  if (ch == 0 && (LEAN || h.adam_enabled) && r.numel > 0) {  // numel 0: an empty record (no pointers)
+    p0 = r.param[ec];
+    m0 = r.m[ec];
+    v0 = r.v[ec];
+  }
+  float div = 1.f;
+  if (!LEAN && ch == 0 && !h.slab && r.grad) {
+    gin = r.grad[ec];
+    if (h.grad_div) div = *h.grad_div;
+  }
+  if (h.slab) {
+    float acc = 0.f;
+    if (has_src && b0 < b1) {
+#pragma unroll
+      for (int k = 0; k < RU; ++k)
+        if (b0 + k < b1) acc = outer ? fmaf(u[k], w[k], acc) : acc + u[k];
+      // batches larger than RC*RU rows per block: the rest, RU rows at a time
+      for (int bb = b0 + RU; bb < b1; bb += RU) {
+#pragma unroll
+        for (int k = 0; k < RU; ++k) {
+          const int64_t row = min(bb + k, b1 - 1);
+          u[k] = ld_part<LD>(base + row * st + col1);
+          w[k] = outer ? ld_part<LD>(base + row * st + col2) : 1.f;
+        }
+#pragma unroll
+        for (int k = 0; k < RU; ++k)
+          if (bb + k < b1) acc = outer ? fmaf(u[k], w[k], acc) : acc + u[k];
+      }
+    }
+    part[ch][lp] = acc;
+  }
+  __syncthreads();
+  if (ch != 0 || !live) return;
+  float gsum;
+  if (LEAN || h.slab) {
+    gsum = 0.f;
+#pragma unroll
+    for (int k = 0; k < RC; ++k) gsum += part[k][lp];
+    if (r.grad) r.grad[e] = gsum;
+  } else {  // gradients supplied (e.g. after an RCCL all-reduce): Adam only
+    gsum = gin;
+    if (h.grad_div) {
+      gsum = gin / div;
+      r.grad[e] = gsum;
+      if (first && lp == 0 && h.loss_out) h.loss_out[0] = h.loss_out[0] / div;
+    }
+  }
+  if (upd) {
+    float bc1 = h.bias_c1, bc2s = h.bias_c2_sqrt;
+    if (h.step_counter) {  // step and bias corrections from the device counter
+      bc1 = 1.f - exp2f((float)tstep * h.log2_beta1);
+      bc2s = sqrtf(1.f - exp2f((float)tstep * h.log2_beta2));
+      if (!LEAN && first && lp == 0) h.step_counter[0] = tstep;  // LEAN: the caller advances it
+    }
+    float gr = gsum;
+    if (h.weight_decay != 0.f) gr = fmaf(h.weight_decay, p0, gr);
+    // torch.optim.Adam: exp_avg.lerp_(g, 1-b1); exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
+    // every product-sum spelled out (fmaf / __fmul_rn / __fadd_rn): contraction
+    // is then the same in every kernel that inlines this block
+    const float mv = fmaf(1.f - h.beta1, __fsub_rn(gr, m0), m0);
+    const float vv = fmaf(__fmul_rn(1.f - h.beta2, gr), gr, __fmul_rn(v0, h.beta2));
+    r.m[e] = mv;
+    r.v[e] = vv;
+    const float denom = __fadd_rn(__fdiv_rn(sqrtf(vv), bc2s), h.eps);
+    r.param[e] = fmaf(-(h.lr / bc1), __fdiv_rn(mv, denom), p0);
+  }
+}
+
+// Host: header + records from the C-ABI table and Adam settings; returns the
+// number of RP-element blocks, or a negative DR_E_* code.
+inline int build_reduce(const dr_param_table* t, const float* slab, const float* head, int32_t n_batch,
+                        const dr_adam* adam, const float* loss_per_graph, float loss_scale, float* loss_out,
+                        ReduceHdr& h, ParamRec* rec) {
+  if (!t || !adam || n_batch < 0) return DR_E_ARG;
+  if ((slab == nullptr) != (head == nullptr)) return DR_E_ARG;
+  if (t->n_params < 1 || t->n_params > DR_MAX_PARAMS) return DR_E_ARG;
+  std::memset(&h, 0, sizeof(h));
+  h.slab = slab;
+  h.head = head;
+  h.lpg = loss_per_graph;
+  h.loss_out = loss_out;
+  h.step_counter = adam->step_counter;
+  h.grad_div = adam->grad_div;
+  h.B = n_batch;
+  h.slab_stride = t->slab_stride;
+  h.head_stride = t->head_stride;
+  h.adam_enabled = adam->enabled;
+  h.loss_scale = loss_scale;
+  h.lr = adam->lr;
+  h.beta1 = adam->beta1;
+  h.beta2 = adam->beta2;
+  h.eps = adam->eps;
+  h.weight_decay = adam->weight_decay;
+  h.bias_c1 = adam->bias_c1;
+  h.bias_c2_sqrt = adam->bias_c2_sqrt;
+  h.log2_beta1 = (float)std::log2((double)adam->beta1);
+  h.log2_beta2 = (float)std::log2((double)adam->beta2);
+  int blocks = 0;
+  for (int i = 0; i < t->n_params; ++i) {
+    if (t->numel[i] < 0 || !t->param[i]) return DR_E_ARG;
+    if (adam->enabled && (!t->exp_avg[i] || !t->exp_avg_sq[i])) return DR_E_ARG;
+    if (!slab && !t->grad[i]) return DR_E_ARG;
+    const dr_grad_recipe r = t->recipe[i];
+    if (r.kind < DR_GRAD_ZERO || r.kind > DR_GRAD_HEAD || (r.kind == DR_GRAD_OUTER && r.cols <= 0)) return DR_E_ARG;
+    ParamRec& pr = rec[i];
+    std::memset(&pr, 0, sizeof(pr));
+    pr.param = t->param[i];
+    pr.grad = t->grad[i];
+    pr.m = t->exp_avg[i];
+    pr.v = t->exp_avg_sq[i];
+    pr.numel = t->numel[i];
+    pr.kind = r.kind;
+    pr.off1 = r.off1;
+    pr.off2 = r.off2;
+    pr.cols = r.cols;
+    h.blk0[i] = (int16_t)blocks;
+    blocks += (t->numel[i] + RP - 1) / RP;
+  }
+  if (blocks > 32767) return DR_E_UNSUPPORTED;
+  for (int i = t->n_params; i < 18; ++i) h.blk0[i] = (int16_t)blocks;
+  h.n_params = t->n_params;
+  h.n_blocks = blocks;
+  return blocks;
+}
+
+}  // namespace drr

@@ -2,6 +2,10 @@
 (reference ``deeprank2/trainer.py:682-690``) in two launches per mini-batch,
 for any model with a ``fused_spec`` (GINet, FoutNet).
 
+(GINet in a world of one, opt-in ``fuse_update``: both in ONE launch,
+``dr_ginet_train_step`` — extra reducer workgroups of the same grid wait for
+the graph workgroups, then reduce the partials and run Adam.)
+
 1. the model's graph pass (``dr_ginet_graph_pass`` / ``dr_fout_graph_pass``;
    FORWARD|BACKWARD, loss in-kernel): one workgroup per graph computes the
    prediction, the loss term and the whole backward of its graph, writing
@@ -27,7 +31,7 @@ from __future__ import annotations
 import torch
 
 from deeprank2_amd import _lib, layered
-from deeprank2_amd.fused import BatchHandle, launch, param_table
+from deeprank2_amd.fused import BatchHandle, launch, launch_step, param_table, step_fits
 
 
 class FusedTrainStep:
@@ -74,6 +78,11 @@ class FusedTrainStep:
         # by the all-reduced weight sum (dr_adam.grad_div)
         self.device_div = self.loss == "ce" and self.class_weights is not None and self.world > 1
         self.kernel_events = None  # list -> (start, end) HIP events around each graph pass
+        # world of one: graph pass + reduce + Adam in ONE launch where the model
+        # has it (GINet: dr_ginet_train_step; bit-identical to the two launches).
+        # Off by default: measured slower at B=64 (24.7 vs 20.6 us/step)
+        self.fuse_update = False
+        self.sync = torch.zeros(4, dtype=torch.int32, device=dev)  # its arrival counters, left zero
         if getattr(model, "_drop_seed", 0) is None:
             model._drop_seed = int(torch.randint(0, 2**62, (1,)).item())
         self._cap = 0
@@ -177,6 +186,12 @@ class FusedTrainStep:
         if ev is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
+        if self.pg is None and self.fuse_update and launch_step(self.spec, h, self._w, p, self._table, self._adam, self.loss_out, self.sync):
+            if ev is not None:
+                e1.record()
+                ev.append((e0, e1))
+            self.step_count += 1
+            return self.loss_out, self.out[: h.B]
         launch(self.spec, h, self._w, p)
         if ev is not None:
             e1.record()
@@ -290,8 +305,14 @@ class FusedTrainStep:
         self.step_count = n
         return g
 
+    def one_launch(self, h: BatchHandle) -> bool:
+        """True when ``step(h)`` is a single kernel launch (``dr_ginet_train_step``)."""
+        cd = _lib.DR_DTYPE_BF16 if self.compute_dtype == "bf16" else _lib.DR_DTYPE_F32
+        return self.pg is None and self.fuse_update and not h.nonfinite and step_fits(self.spec, h, cd, self.out_dim)
+
     def time_graph_pass(self, handles, n_launches, global_batch=None):
-        """Mean duration (ms) of the model's graph pass alone: ``n_launches``
+        """Mean duration (ms) of the model's graph pass alone (or of the whole
+        step where ``one_launch``: graph pass + reduce + Adam): ``n_launches``
         passes over ``handles`` (cycled) captured back to back into one HIP
         graph, replayed between two HIP events on the launch stream.  Used for
         ``roofline.achieved``; no host launch overhead enters the number (the
@@ -301,10 +322,14 @@ class FusedTrainStep:
         snap = [t.detach().clone() for t in self._state_tensors()]
         n = self.step_count
         p = self._pass if (self.spec.dropout > 0 and self.model.dropout > 0) else self._pass_nodrop
+        one = all(self.one_launch(h) for h in handles)
 
         def passes(k):
             for i in range(k):
                 h = handles[i % len(handles)]
+                if one:  # the step IS one kernel: time it whole (reduce + Adam included)
+                    self.step(h, global_batch=global_batch)
+                    continue
                 p.loss_scale = self.loss_scale(h, global_batch or h.B * self.world)
                 launch(self.spec, h, self._w, p)
 

@@ -252,6 +252,7 @@ class FusedSpec:
     layers: Callable | None = None  # (model, batch tensors, training) -> out: layer-level path (layered.py) for batches beyond LDS
     bf16: bool = False  # dr_pass.compute_dtype = DR_DTYPE_BF16 supported (runs on the large-graph path)
     attention: bool = False  # GINetConvLayer model: batches with non-finite inputs need the layer path
+    step_entry: str | None = None  # one-launch training step (graph pass + reduce + Adam), world of one
 
 
 def vanilla_fused_scratch_floats(n, e, fe):
@@ -321,6 +322,26 @@ def launch(spec: FusedSpec, h: BatchHandle, w, p):
     else:
         msg = f"largest graph of the batch needs {lds} B of LDS (> 160 KiB) and {spec.entry} has no large-graph path"
         raise RuntimeError(msg)
+
+
+def step_fits(spec: FusedSpec, h: BatchHandle, compute_dtype, out_dim) -> bool:
+    """True when ``launch_step`` runs this batch in one launch."""
+    if spec.step_entry is None or spec.run is not None or compute_dtype != _lib.DR_DTYPE_F32 or h.force_large:
+        return False
+    return lds_for(spec, h, out_dim) <= LDS_MAX
+
+
+def launch_step(spec: FusedSpec, h: BatchHandle, w, p, table, adam, loss_out, sync) -> bool:
+    """The model's one-launch training step (graph pass, gradient reduction
+    and Adam; ``spec.step_entry``) when it has one and the batch runs on its
+    per-graph kernel; False (nothing launched) otherwise."""
+    if not step_fits(spec, h, p.compute_dtype, p.out_dim):
+        return False
+    lds = lds_for(spec, h, p.out_dim)
+    fn = getattr(_lib.load(), spec.step_entry)
+    rc = fn(h.store.cstruct(), h.descs.data_ptr(), h.B, w, p, lds, table, adam, loss_out.data_ptr(), sync.data_ptr(), _lib.stream_ptr(h.store.device))
+    _lib.check(rc, spec.step_entry)
+    return True
 
 
 def run_pass(spec: FusedSpec, h: BatchHandle, params, p, w=None):

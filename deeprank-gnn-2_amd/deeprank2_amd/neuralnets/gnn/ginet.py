@@ -192,7 +192,7 @@ def _large(h, w, p):
     _lib.check(rc, "dr_ginet_large_pass")
 
 
-SPEC = FusedSpec(PARAM_NAMES, recipe, slab_stride, head_stride, "dr_ginet_graph_pass", weights_c, _lds, dropout=0.4, large=_large, bf16=True, layers=layered.ginet_forward, attention=True)
+SPEC = FusedSpec(PARAM_NAMES, recipe, slab_stride, head_stride, "dr_ginet_graph_pass", weights_c, _lds, dropout=0.4, large=_large, bf16=True, layers=layered.ginet_forward, attention=True, step_entry="dr_ginet_train_step")
 
 
 def graph_pass(h: BatchHandle, params, out_dim, flags, **kw):

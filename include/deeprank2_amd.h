@@ -424,6 +424,24 @@ int dr_reduce_update(const dr_param_table* t, const float* slab, const float* he
                      const dr_adam* adam, const float* loss_per_graph, float loss_scale, float* loss_out,
                      void* stream);
 
+/* One-launch GINet training step (data-parallel world of one): the graph pass
+ * above (FORWARD|BACKWARD with the fused loss), then the gradient reduction
+ * over the batch and Adam, by the last min(B, 64) workgroups to finish their
+ * graph inside the same launch.  Replaces the forward, loss.backward() and
+ * optimizer.step() of one Trainer._epoch iteration (deeprank2/trainer.py:686-690;
+ * Adam as configured at trainer.py:419) -- what dr_ginet_graph_pass followed by
+ * dr_reduce_update does in two launches, with bit-identical results.
+ * table / adam / loss_out: as for dr_reduce_update (adam->enabled, no grad_div,
+ * adam->step_counter == pass->step_counter, at most 16 parameters, GINet's
+ * slab/head strides).  sync: device uint32 [4], zero before the first call and
+ * left zero by every call; sync[2] is set to 1 if a reducer ever gave up
+ * waiting (never expected; the step's update is then incomplete).  */
+int dr_ginet_train_step(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                        const dr_ginet_weights* w, const dr_pass* pass, int32_t lds_bytes,
+                        const dr_param_table* table, const dr_adam* adam, float* loss_out, uint32_t* sync,
+                        void* stream);
+
+
 /* ---- generic layer kernels (arbitrary edge lists; GINetConvLayer API) ---- */
 
 /* Stable CSR of (row, col) pairs sorted by row: rowptr [n_rows+1], perm [E]

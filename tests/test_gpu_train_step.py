@@ -1,0 +1,93 @@
+"""The one-launch GINet training step (``dr_ginet_train_step``: graph pass,
+then the gradient reduction and Adam by the last workgroups to finish, in
+the same launch, opt-in ``FusedTrainStep.fuse_update``) against the two-launch step (``dr_ginet_graph_pass`` +
+``dr_reduce_update``).  Both run the same fixed-order arithmetic
+(``csrc/reduce_common.h``), so parameters, Adam moments, gradients, loss and
+outputs must agree bit for bit — over batch sizes below, at and above the
+64 in-launch reducers, with hash dropout, and replayed from a HIP graph.  The
+two-launch step itself is checked against the oracle in test_gpu_trainer /
+test_gpu_ginet."""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from deeprank2_amd.engine import FusedTrainStep
+from deeprank2_amd.fused import BatchHandle
+from deeprank2_amd.neuralnets.gnn import ginet as amd
+from deeprank2_amd.store import GraphStore, pack_graphs
+from deeprank2_amd.utils.synthetic import make_dataset
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _records(n, seed):
+    from bench import records
+
+    return records(make_dataset(n, seed=seed))
+
+
+def _pair(loss="mse", out=1):
+    torch.manual_seed(3)
+    m1 = amd.GINet(30, out, 3).to(DEV).train()
+    m2 = amd.GINet(30, out, 3).to(DEV).train()
+    m2.load_state_dict(m1.state_dict())
+    m2._drop_seed = m1._drop_seed = 12345  # noqa: SLF001
+    one = FusedTrainStep(m1, lr=1e-3, weight_decay=1e-5, loss=loss, max_batch=256)
+    two = FusedTrainStep(m2, lr=1e-3, weight_decay=1e-5, loss=loss, max_batch=256)
+    one.fuse_update, two.fuse_update = True, False
+    return one, two
+
+
+def _assert_same(one, two, what):
+    bad = []
+    for k, (a, b) in enumerate(zip(one._state_tensors(), two._state_tensors())):  # noqa: SLF001 - params, moments, counter, grads+loss
+        if not torch.equal(a, b):
+            bad.append((k, a.numel(), int((a != b).sum()), float((a.double() - b.double()).abs().max())))
+    assert not bad, f"{what}: (tensor, numel, n_diff, max|diff|) {bad}; sync {one.sync.tolist()}"
+    assert one.sync.tolist() == [0, 0, 0, 0], "arrival counters must be left zero"
+
+
+@pytest.mark.parametrize("sizes", [(64, 64, 64), (7, 1, 130, 64, 200)])
+def test_one_launch_step_bit_identical_to_two_launches(sizes):
+    store = GraphStore(pack_graphs(_records(256, 31)), DEV)
+    one, two = _pair()
+    rng = np.random.default_rng(0)
+    for i, b in enumerate(sizes):
+        h = BatchHandle(store, rng.permutation(256)[:b].astype(np.int32))
+        l1, o1 = one.step(h)
+        l2, o2 = two.step(h)
+        torch.cuda.synchronize()
+        assert torch.equal(o1, o2), f"outputs step {i} (B={b})"
+        assert torch.equal(l1, l2), f"loss step {i}"
+        _assert_same(one, two, f"state after step {i} (B={b})")
+
+
+def test_one_launch_step_cross_entropy_bit_identical():
+    recs = _records(96, 32)
+    for i, r in enumerate(recs):
+        r.y = float(i % 3)
+    store = GraphStore(pack_graphs(recs), DEV)
+    one, two = _pair(loss="ce", out=3)
+    for s in range(3):
+        h = BatchHandle(store, np.arange(s * 32, s * 32 + 32, dtype=np.int32))
+        one.step(h)
+        two.step(h)
+    torch.cuda.synchronize()
+    _assert_same(one, two, "CE steps")
+
+
+def test_one_launch_step_replays_from_hip_graph():
+    store = GraphStore(pack_graphs(_records(128, 33)), DEV)
+    one, two = _pair()
+    hs = [BatchHandle(store, np.arange(k * 64, k * 64 + 64, dtype=np.int32)) for k in range(2)]
+    g = one.capture_sweep(hs)
+    for _ in range(3):
+        g.replay()
+        for h in hs:
+            two.step(h)
+    torch.cuda.synchronize()
+    _assert_same(one, two, "captured one-launch steps vs eager two-launch steps")
