@@ -164,23 +164,40 @@ __global__ void __launch_bounds__(RB) vb_edge_fwd(VA a, int l) {
   const int c = threadIdx.x & 31;
   const float* wc = swc + c * Fe;
   const float bc = swc[32 * MAXFE + c];
+  // per-edge ReLU words for the backward (a 64-lane ballot holds the two rows
+  // of the wave: lanes 0-31 and 32-63)
+  uint32_t* words = a.ws.relu_words ? a.ws.relu_words + (int64_t)(l - 1) * a.ws.edge0[a.B] : nullptr;
+  const int hs = threadIdx.x & 32;
   for (int64_t r = blockIdx.x * (RB / 32) + (threadIdx.x >> 5); r < a.ws.n_rows; r += (int64_t)gridDim.x * (RB / 32)) {
     const RowGraph g = row_graph(a, r);
     const float ac = L.a[r * 32 + c];
     const float* Bg = L.bm + g.r0 * 32 + c;
+    uint32_t* wr = words ? words + a.ws.edge0[a.ws.row_slot[r]] : nullptr;
     float acc = 0.f;
     const int eb = g.rp[g.i], ee = g.rp[g.i + 1];
     int e = eb;
     for (; e + 4 <= ee; e += 4) {  // four independent gathers in flight, summed in edge order
       const int j0 = g.col[e], j1 = g.col[e + 1], j2 = g.col[e + 2], j3 = g.col[e + 3];
-      const float q0 = Bg[(int64_t)j0 * 32], q1 = Bg[(int64_t)j1 * 32], q2 = Bg[(int64_t)j2 * 32], q3 = Bg[(int64_t)j3 * 32];
+      const float q[4] = {Bg[(int64_t)j0 * 32], Bg[(int64_t)j1 * 32], Bg[(int64_t)j2 * 32], Bg[(int64_t)j3 * 32]};
       const float* ea = g.ea + (int64_t)e * FeS;
-      acc += relu_keepnan(ac + q0 + edge_const(wc, ea, Fe) + bc);
-      acc += relu_keepnan(ac + q1 + edge_const(wc, ea + FeS, Fe) + bc);
-      acc += relu_keepnan(ac + q2 + edge_const(wc, ea + 2 * FeS, Fe) + bc);
-      acc += relu_keepnan(ac + q3 + edge_const(wc, ea + 3 * FeS, Fe) + bc);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float pre = ac + q[u] + edge_const(wc, ea + u * FeS, Fe) + bc;
+        acc += relu_keepnan(pre);
+        if (wr) {
+          const uint64_t m = __ballot(active(pre));
+          if (c == 0) wr[e + u] = (uint32_t)(m >> hs);
+        }
+      }
     }
-    for (; e < ee; ++e) acc += relu_keepnan(ac + Bg[(int64_t)g.col[e] * 32] + edge_const(wc, g.ea + (int64_t)e * FeS, Fe) + bc);
+    for (; e < ee; ++e) {
+      const float pre = ac + Bg[(int64_t)g.col[e] * 32] + edge_const(wc, g.ea + (int64_t)e * FeS, Fe) + bc;
+      acc += relu_keepnan(pre);
+      if (wr) {
+        const uint64_t m = __ballot(active(pre));
+        if (c == 0) wr[e] = (uint32_t)(m >> hs);
+      }
+    }
     L.s[r * 32 + c] = acc;
   }
 }
@@ -222,7 +239,15 @@ __global__ void __launch_bounds__(256) vb_head(VA a) {
     float acc = 0.f;
     if (n < F && ch < CH) {
       const int i0 = (N * ch) / CH, i1 = (N * (ch + 1)) / CH;
-      for (int i = i0; i < i1; ++i) acc += X2[(int64_t)i * XS + n];
+      int i = i0;
+      for (; i + 8 <= i1; i += 8) {  // 8 rows' loads in flight, summed in row order
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = X2[(int64_t)(i + u) * XS + n];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += v[u];
+      }
+      for (; i < i1; ++i) acc += X2[(int64_t)i * XS + n];
     }
     sRed[tid] = acc;
     __syncthreads();
@@ -343,6 +368,73 @@ __global__ void __launch_bounds__(RB) vb_edge_bwd(VA a, int l) {
   const int c = threadIdx.x & 31;
   const float* wc = swc + c * Fe;
   const float bc = swc[32 * MAXFE + c];
+  const uint32_t* words = a.ws.relu_words ? a.ws.relu_words + (int64_t)(l - 1) * a.ws.edge0[a.B] : nullptr;
+  if (words) {  // the forward's ReLU words: no B_j / A_i gathers, no edge_attr for the transposed sum
+    for (int64_t r = blockIdx.x * (RB / 32) + (threadIdx.x >> 5); r < a.ws.n_rows; r += (int64_t)gridDim.x * (RB / 32)) {
+      const RowGraph g = row_graph(a, r);
+      const uint32_t* wr = words + a.ws.edge0[a.ws.row_slot[r]];
+      const float dsi = DS[r * 32 + c];
+      const float* DSg = DS + g.r0 * 32 + c;
+      int cnt = 0;
+      float eap[MAXFE];
+#pragma unroll
+      for (int f = 0; f < MAXFE; ++f) eap[f] = 0.f;
+      const int eb = g.rp[g.i], ee = g.rp[g.i + 1];
+      int e = eb;
+      for (; e + 4 <= ee; e += 4) {
+        uint32_t wv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) wv[u] = wr[e + u];
+        float ev[4][MAXFE];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int f = 0; f < MAXFE; ++f) ev[u][f] = f < Fe ? g.ea[(int64_t)(e + u) * FeS + f] : 0.f;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if ((wv[u] >> c) & 1u) {
+            ++cnt;
+#pragma unroll
+            for (int f = 0; f < MAXFE; ++f)
+              if (f < Fe) eap[f] += ev[u][f];
+          }
+      }
+      for (; e < ee; ++e)
+        if ((wr[e] >> c) & 1u) {
+          ++cnt;
+#pragma unroll
+          for (int f = 0; f < MAXFE; ++f)
+            if (f < Fe) eap[f] += g.ea[(int64_t)e * FeS + f];
+        }
+      D[r * 32 + c] = cnt ? dsi * (float)cnt : 0.f;
+      for (int f = 0; f < Fe; ++f) EAP[(r * 32 + c) * FeS + f] = cnt ? dsi * eap[f] : 0.f;
+      float acc = 0.f;  // D'_i over edges (src -> i), in transposed (original edge) order
+      const int qb = g.trp[g.i], qe = g.trp[g.i + 1];
+      int q = qb;
+      for (; q + 4 <= qe; q += 4) {
+        int src[4], ed[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          src[u] = g.tcol[q + u];
+          ed[u] = g.teid[q + u];
+        }
+        uint32_t wv[4];
+        float dv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          wv[u] = wr[ed[u]];
+          dv[u] = DSg[(int64_t)src[u] * 32];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if ((wv[u] >> c) & 1u) acc += dv[u];
+      }
+      for (; q < qe; ++q)
+        if ((wr[g.teid[q]] >> c) & 1u) acc += DSg[(int64_t)g.tcol[q] * 32];
+      DP[r * 32 + c] = acc;
+    }
+    return;
+  }
   for (int64_t r = blockIdx.x * (RB / 32) + (threadIdx.x >> 5); r < a.ws.n_rows; r += (int64_t)gridDim.x * (RB / 32)) {
     const RowGraph g = row_graph(a, r);
     const float ac = L.a[r * 32 + c], bi = L.bm[r * 32 + c], dsi = DS[r * 32 + c];

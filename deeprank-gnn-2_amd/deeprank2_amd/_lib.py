@@ -115,7 +115,7 @@ class VanillaWeightsC(ctypes.Structure):
 
 
 class VanillaScratchC(ctypes.Structure):
-    _fields_ = [("base", VP), ("row0", VP), ("row_slot", VP), ("n_rows", ctypes.c_int64), ("chunk_first", VP), ("chunk_slot", VP), ("n_chunks", ctypes.c_int32), ("pad0", ctypes.c_int32), ("part", VP)]
+    _fields_ = [("base", VP), ("row0", VP), ("row_slot", VP), ("n_rows", ctypes.c_int64), ("chunk_first", VP), ("chunk_slot", VP), ("n_chunks", ctypes.c_int32), ("pad0", ctypes.c_int32), ("part", VP), ("edge0", VP), ("relu_words", VP)]
 
 
 class PackInputC(ctypes.Structure):

@@ -76,7 +76,12 @@ class BatchHandle:
             c.chunk_slot = base + 4 * (2 * (self.B + 1) + rows)
             c.n_chunks = int(chunk_first[-1])
             c.part = pbuf.data_ptr()
-            sc = (c, (ints, buf, pbuf))
+            # per-edge ReLU words of both layers (forward -> backward)
+            ne = self.store._sizes[1][self.gids_host.astype(np.int64)]  # noqa: SLF001
+            e0 = torch.from_numpy(np.concatenate([[0], np.cumsum(ne)]).astype(np.int32)).to(dev)
+            words = torch.empty(max(1, 2 * int(ne.sum())), dtype=torch.int32, device=dev)
+            c.edge0, c.relu_words = e0.data_ptr(), words.data_ptr()
+            sc = (c, (ints, buf, pbuf, e0, words))
             self._lds[key] = sc
         return sc
 

@@ -339,6 +339,10 @@ typedef struct dr_vanilla_scratch {
   int32_t n_chunks;
   int32_t pad0;
   float* part;                /* [n_chunks, dr_vanilla_part_floats(F, Fe)] weight-gradient partials */
+  const int32_t* edge0;       /* optional [B+1] first edge of each slot in relu_words (prefix sums of n_edges) */
+  uint32_t* relu_words;       /* optional [2, edge0[B]]: per layer and edge (CSR order) bit c = channel c of
+                                 the edge MLP active, written by the forward and read by the backward (which
+                                 then neither re-gathers B_j nor re-reads edge_attr for the transposed sum) */
 } dr_vanilla_scratch;
 #define DR_VANILLA_CHUNK 32
 
