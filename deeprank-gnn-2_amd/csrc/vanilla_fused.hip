@@ -522,6 +522,106 @@ __global__ void __launch_bounds__(RB) vb_dx1(VA a) {
   }
 }
 
+// ---- node GEMMs on MFMA -----------------------------------------------------
+// out(r, n) = init(r, n) + sum_{k < K} A(r, k) W(k, n) for every batch row r,
+// n < NO, on v_mfma_f32_16x16x4_f32 (k in order: the same fmaf chain as a
+// scalar loop).  A workgroup (4 waves) stages W [KP][NOP] in LDS once, then
+// takes 64-row tiles: the A tile [64][KP] is loaded coalesced into LDS
+// (stride KP + 1: the 16 rows of an operand read hit distinct banks), each
+// wave runs 16 rows x all NO columns.  Modes (vanilla_gnn.py:29-37 and their
+// gradients):
+//   GM_HALVES: [A | B] = Xin [Wa; Wb]^T            (K = F,      NO = 64)
+//   GM_NODE:   Xout = relu([Xin | S] Wn^T + bn)    (K = F + 32, NO = F)
+//   GM_DXS:    [dX1 | DS] = DU Wn                  (K = F,      NO = F + 32)
+//   GM_DX1:    dX1 += [D | D'] [Wa2; Wb2]          (K = 64,     NO = F)
+enum GemmMode { GM_HALVES = 0, GM_NODE = 1, GM_DXS = 2, GM_DX1 = 3 };
+constexpr int GT = 64;  // rows per tile
+
+__host__ __device__ inline void gemm_dims(int mode, int F, int& K, int& NO) {
+  K = mode == GM_NODE ? F + 32 : (mode == GM_DX1 ? 64 : F);
+  NO = mode == GM_HALVES ? 64 : (mode == GM_DXS ? F + 32 : F);
+}
+__host__ __device__ inline int gemm_lds_floats(int mode, int F) {
+  int K, NO;
+  gemm_dims(mode, F, K, NO);
+  const int KP = r4(K), NOP = (NO + 15) & ~15;
+  return KP * NOP + GT * (KP + 1);
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(RB) vb_gemm(VA a, int l) {
+  extern __shared__ float lds[];
+  const Layer L = layer_of(a, l);
+  const int F = a.F, KE = a.KE, KN = a.KN, XS = a.XS;
+  int K, NO;
+  gemm_dims(MODE, F, K, NO);
+  const int KP = r4(K), NOP = (NO + 15) & ~15, LA = KP + 1;
+  float* Ws = lds;              // [KP][NOP]
+  float* As = lds + KP * NOP;   // [GT][LA]
+  const float* wn = l == 2 ? a.w.wn2 : a.w.wn1;
+  for (int p = threadIdx.x; p < KP * NOP; p += RB) {
+    const int k = p / NOP, n = p - k * NOP;
+    float v = 0.f;
+    if (k < K && n < NO) {
+      if (MODE == GM_HALVES) v = L.we[(n & 31) * KE + (n < 32 ? 0 : F) + k];
+      else if (MODE == GM_NODE) v = L.wn[n * KN + k];
+      else if (MODE == GM_DXS) v = wn[k * KN + n];
+      else v = a.w.we2[(k & 31) * KE + (k < 32 ? 0 : F) + n];
+    }
+    Ws[p] = v;
+  }
+  float* ws = a.ws.base;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, kq = lane >> 4;
+  const int64_t R = a.ws.n_rows;
+  for (int64_t t0 = (int64_t)blockIdx.x * GT; t0 < R; t0 += (int64_t)gridDim.x * GT) {
+    __syncthreads();  // W staged / the previous tile's A reads done
+    for (int p = threadIdx.x; p < GT * KP; p += RB) {
+      const int i = p / KP, k = p - i * KP;
+      const int64_t r = t0 + i;
+      float v = 0.f;
+      if (r < R && k < K) {
+        if (MODE == GM_HALVES) v = xin_row(a, L, r)[k];
+        else if (MODE == GM_NODE) v = k < F ? xin_row(a, L, r)[k] : L.s[r * 32 + k - F];
+        else if (MODE == GM_DXS) v = ws[a.L.du + r * XS + k];
+        else v = k < 32 ? ws[a.L.d + r * 32 + k] : ws[a.L.dp + r * 32 + k - 32];
+      }
+      As[i * LA + k] = v;
+    }
+    __syncthreads();
+    const int i0 = wave * 16;
+    for (int n0 = 0; n0 < NO; n0 += 16) {
+      const int n = n0 + li;
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+      if (MODE == GM_DX1) {  // the accumulation starts from dX1 (vb_dxs's direct part)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int64_t r = t0 + i0 + kq * 4 + q;
+          acc[q] = (r < R && n < NO) ? ws[a.L.dx1 + r * XS + n] : 0.f;
+        }
+      }
+      for (int k0 = 0; k0 < KP; k0 += 4)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(As[(i0 + li) * LA + k0 + kq], Ws[(k0 + kq) * NOP + n], acc, 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t r = t0 + i0 + kq * 4 + q;
+        if (r >= R || n >= NO) continue;
+        const float v = acc[q];
+        if (MODE == GM_HALVES) (n < 32 ? L.a : L.bm)[r * 32 + (n & 31)] = v;
+        else if (MODE == GM_NODE) L.xout[r * XS + n] = relu_keepnan(v + L.bn[n]);
+        else if (MODE == GM_DXS) {
+          if (n < F) {
+            if (l == 2) ws[a.L.dx1 + r * XS + n] = v;
+          } else {
+            ws[a.L.ds + r * 32 + n - F] = v;
+          }
+        } else {
+          ws[a.L.dx1 + r * XS + n] = v;
+        }
+      }
+    }
+  }
+}
+
 // Weight-gradient partials of one layer per chunk of DR_VANILLA_CHUNK rows
 // (all CUs busy), rows staged through LDS; vb_wgrad_combine then sums each
 // graph's chunks in order into its slab (deterministic).
@@ -657,21 +757,29 @@ extern "C" int dr_vanilla_graph_pass(const dr_graph_store* store, const dr_graph
   const int64_t R = scratch->n_rows;
   const size_t lds_half = 4 * 64 * (a.F + 1), lds_node = 4 * (a.F * (a.KN + 1) + a.F), lds_dxs = 4 * a.F * a.KN,
                lds_dx1 = 4 * 64 * a.F, lds_wg = (size_t)dr_vanilla_lds_bytes(a.F, a.Fe, pass->out_dim);
+  const bool mf = a.F <= 64;  // node GEMMs on MFMA (vb_gemm); the scalar kernels stay as the reference form
+  const int gg = rows_grid(R, GT) < 1024 ? rows_grid(R, GT) : 1024;
+  auto glds = [&](int mode) { return (size_t)4 * gemm_lds_floats(mode, a.F); };
   for (int l = 1; l <= 2; ++l) {
-    hipLaunchKernelGGL(vb_halves, dim3(rows_grid(R, RB / 64)), dim3(RB), lds_half, st, a, l);
+    if (mf) hipLaunchKernelGGL(vb_gemm<GM_HALVES>, dim3(gg), dim3(RB), glds(GM_HALVES), st, a, l);
+    else hipLaunchKernelGGL(vb_halves, dim3(rows_grid(R, RB / 64)), dim3(RB), lds_half, st, a, l);
     hipLaunchKernelGGL(vb_edge_fwd, dim3(rows_grid(R, RB / 32)), dim3(RB), 0, st, a, l);
-    hipLaunchKernelGGL(vb_node, dim3(rows_grid(R, RB / 64)), dim3(RB), lds_node, st, a, l);
+    if (mf) hipLaunchKernelGGL(vb_gemm<GM_NODE>, dim3(gg), dim3(RB), glds(GM_NODE), st, a, l);
+    else hipLaunchKernelGGL(vb_node, dim3(rows_grid(R, RB / 64)), dim3(RB), lds_node, st, a, l);
   }
   hipLaunchKernelGGL(vb_head, dim3(n_batch), dim3(256), 0, st, a);
   if (pass->flags & DR_PASS_BACKWARD) {
     hipLaunchKernelGGL(vb_du, dim3(rows_grid(R * a.XS, RB)), dim3(RB), 0, st, a, 2);
-    hipLaunchKernelGGL(vb_dxs, dim3(rows_grid(R, RB / 128)), dim3(RB), lds_dxs, st, a, 2);
+    if (mf) hipLaunchKernelGGL(vb_gemm<GM_DXS>, dim3(gg), dim3(RB), glds(GM_DXS), st, a, 2);
+    else hipLaunchKernelGGL(vb_dxs, dim3(rows_grid(R, RB / 128)), dim3(RB), lds_dxs, st, a, 2);
     hipLaunchKernelGGL(vb_edge_bwd, dim3(rows_grid(R, RB / 32)), dim3(RB), 0, st, a, 2);
-    hipLaunchKernelGGL(vb_dx1, dim3(rows_grid(R, RB / 64)), dim3(RB), lds_dx1, st, a);
+    if (mf) hipLaunchKernelGGL(vb_gemm<GM_DX1>, dim3(gg), dim3(RB), glds(GM_DX1), st, a, 2);
+    else hipLaunchKernelGGL(vb_dx1, dim3(rows_grid(R, RB / 64)), dim3(RB), lds_dx1, st, a);
     hipLaunchKernelGGL(vb_wgrad_part, dim3(scratch->n_chunks), dim3(RB), lds_wg, st, a, 2);
     hipLaunchKernelGGL(vb_wgrad_combine, dim3(rows_grid((int64_t)n_batch * layer_grad_size(a.F, a.Fe), RB)), dim3(RB), 0, st, a, 2);
     hipLaunchKernelGGL(vb_du, dim3(rows_grid(R * a.XS, RB)), dim3(RB), 0, st, a, 1);
-    hipLaunchKernelGGL(vb_dxs, dim3(rows_grid(R, RB / 128)), dim3(RB), lds_dxs, st, a, 1);
+    if (mf) hipLaunchKernelGGL(vb_gemm<GM_DXS>, dim3(gg), dim3(RB), glds(GM_DXS), st, a, 1);
+    else hipLaunchKernelGGL(vb_dxs, dim3(rows_grid(R, RB / 128)), dim3(RB), lds_dxs, st, a, 1);
     hipLaunchKernelGGL(vb_edge_bwd, dim3(rows_grid(R, RB / 32)), dim3(RB), 0, st, a, 1);
     hipLaunchKernelGGL(vb_wgrad_part, dim3(scratch->n_chunks), dim3(RB), lds_wg, st, a, 1);
     hipLaunchKernelGGL(vb_wgrad_combine, dim3(rows_grid((int64_t)n_batch * layer_grad_size(a.F, a.Fe), RB)), dim3(RB), 0, st, a, 1);
