@@ -690,6 +690,94 @@ __global__ void __launch_bounds__(RB) vb_wgrad_part(VA a, int l) {
   }
 }
 
+// The same partials with the three GEMMs on MFMA (dWa = D^T X, dWb = D'^T X,
+// dWn = DU^T [X | S]: K = the chunk's rows, zero-padded to WR; one 16x16
+// output tile per job, jobs over the 4 waves); the bias / edge-attribute sums
+// stay scalar.
+__global__ void __launch_bounds__(RB) vb_wgrad_mfma(VA a, int l) {
+  extern __shared__ float lds[];
+  const int ch = blockIdx.x;
+  const int b = a.ws.chunk_slot[ch];
+  const int F = a.F, Fe = a.Fe, KE = a.KE, KN = a.KN, XS = a.XS, FeS = Fe > 0 ? Fe : 1;
+  const Layer L = layer_of(a, l);
+  const int64_t r0 = a.ws.row0[b];
+  const int N = a.ws.row0[b + 1] - (int)r0;
+  const int i0 = (ch - a.ws.chunk_first[b]) * WR, nr = min(WR, N - i0);
+  const int64_t g0 = r0 + i0;
+  float* ws = a.ws.base;
+  const float* X = L.xin ? L.xin + g0 * XS : a.s.x + (a.descs[b].node0 + i0) * XS;
+  float* cX = lds;
+  float* cS = cX + WR * XS;
+  float* cD = cS + WR * 32;
+  float* cDP = cD + WR * 32;
+  float* cDU = cDP + WR * 32;
+  float* cE = cDU + WR * XS;
+  for (int p = threadIdx.x; p < WR * XS; p += RB) {  // rows past the chunk: zeros
+    const bool in = p < nr * XS;
+    cX[p] = in ? X[p] : 0.f;
+    cDU[p] = in ? ws[a.L.du + g0 * XS + p] : 0.f;
+  }
+  for (int p = threadIdx.x; p < WR * 32; p += RB) {
+    const bool in = p < nr * 32;
+    cS[p] = in ? L.s[g0 * 32 + p] : 0.f;
+    cD[p] = in ? ws[a.L.d + g0 * 32 + p] : 0.f;
+    cDP[p] = in ? ws[a.L.dp + g0 * 32 + p] : 0.f;
+  }
+  for (int p = threadIdx.x; p < nr * 32 * FeS; p += RB) cE[p] = ws[a.L.eap + g0 * 32 * FeS + p];
+  __syncthreads();
+  const int nwe = 32 * KE, nwn = F * KN, total = nwe + 32 + nwn + F;
+  float* out = a.ws.part + (int64_t)ch * total;
+  // scalar sums: dWc (edge-attribute partials), dbe, dbn
+  for (int p = threadIdx.x; p < 32 * Fe + 32 + F; p += RB) {
+    float v = 0.f;
+    if (p < 32 * Fe) {
+      const int c = p / Fe, f = p - c * Fe;
+      for (int i = 0; i < nr; ++i) v += cE[(i * 32 + c) * FeS + f];
+      out[c * KE + 2 * F + f] = v;
+    } else if (p < 32 * Fe + 32) {
+      const int c = p - 32 * Fe;
+      for (int i = 0; i < nr; ++i) v += cD[i * 32 + c];
+      out[nwe + c] = v;
+    } else {
+      const int n = p - 32 * Fe - 32;
+      for (int i = 0; i < nr; ++i) v += cDU[i * XS + n];
+      out[nwe + 32 + nwn + n] = v;
+    }
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, kq = lane >> 4;
+  const int KT = (F + 15) >> 4, QT = (KN + 15) >> 4;
+  const int jw = 2 * 2 * KT, jobs = jw + KT * QT;
+  for (int job = wave; job < jobs; job += RB / 64) {
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (job < jw) {  // dWa (w = 0) / dWb (w = 1): rows c of the tile, columns k
+      const int w = job / (2 * KT), rem = job - w * 2 * KT, ct = rem / KT, kt = rem - ct * KT;
+      const float* Dm = w ? cDP : cD;
+      const int cc = ct * 16 + li, kc = kt * 16 + li;
+      for (int i = 0; i < WR; i += 4)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Dm[(i + kq) * 32 + cc], kc < XS ? cX[(i + kq) * XS + kc] : 0.f, acc, 0, 0, 0);
+      if (kc < F) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) out[(ct * 16 + kq * 4 + q) * KE + w * F + kc] = acc[q];
+      }
+    } else {  // dWn: rows n, columns q of [X | S]
+      const int jj = job - jw, nt = jj / QT, qt = jj - nt * QT;
+      const int nn = nt * 16 + li, qc = qt * 16 + li;
+      for (int i = 0; i < WR; i += 4) {
+        const float av = nn < XS ? cDU[(i + kq) * XS + nn] : 0.f;
+        const float bv = qc < F ? cX[(i + kq) * XS + qc] : (qc < KN ? cS[(i + kq) * 32 + qc - F] : 0.f);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+      }
+      if (qc < KN) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int n = nt * 16 + kq * 4 + q;
+          if (n < F) out[nwe + 32 + n * KN + qc] = acc[q];
+        }
+      }
+    }
+  }
+}
+
 __global__ void __launch_bounds__(RB) vb_wgrad_combine(VA a, int l) {
   const int total = layer_grad_size(a.F, a.Fe);
   const int64_t work = (int64_t)a.B * total;
@@ -775,13 +863,15 @@ extern "C" int dr_vanilla_graph_pass(const dr_graph_store* store, const dr_graph
     hipLaunchKernelGGL(vb_edge_bwd, dim3(rows_grid(R, RB / 32)), dim3(RB), 0, st, a, 2);
     if (mf) hipLaunchKernelGGL(vb_gemm<GM_DX1>, dim3(gg), dim3(RB), glds(GM_DX1), st, a, 2);
     else hipLaunchKernelGGL(vb_dx1, dim3(rows_grid(R, RB / 64)), dim3(RB), lds_dx1, st, a);
-    hipLaunchKernelGGL(vb_wgrad_part, dim3(scratch->n_chunks), dim3(RB), lds_wg, st, a, 2);
+    if (mf) hipLaunchKernelGGL(vb_wgrad_mfma, dim3(scratch->n_chunks), dim3(RB), lds_wg, st, a, 2);
+    else hipLaunchKernelGGL(vb_wgrad_part, dim3(scratch->n_chunks), dim3(RB), lds_wg, st, a, 2);
     hipLaunchKernelGGL(vb_wgrad_combine, dim3(rows_grid((int64_t)n_batch * layer_grad_size(a.F, a.Fe), RB)), dim3(RB), 0, st, a, 2);
     hipLaunchKernelGGL(vb_du, dim3(rows_grid(R * a.XS, RB)), dim3(RB), 0, st, a, 1);
     if (mf) hipLaunchKernelGGL(vb_gemm<GM_DXS>, dim3(gg), dim3(RB), glds(GM_DXS), st, a, 1);
     else hipLaunchKernelGGL(vb_dxs, dim3(rows_grid(R, RB / 128)), dim3(RB), lds_dxs, st, a, 1);
     hipLaunchKernelGGL(vb_edge_bwd, dim3(rows_grid(R, RB / 32)), dim3(RB), 0, st, a, 1);
-    hipLaunchKernelGGL(vb_wgrad_part, dim3(scratch->n_chunks), dim3(RB), lds_wg, st, a, 1);
+    if (mf) hipLaunchKernelGGL(vb_wgrad_mfma, dim3(scratch->n_chunks), dim3(RB), lds_wg, st, a, 1);
+    else hipLaunchKernelGGL(vb_wgrad_part, dim3(scratch->n_chunks), dim3(RB), lds_wg, st, a, 1);
     hipLaunchKernelGGL(vb_wgrad_combine, dim3(rows_grid((int64_t)n_batch * layer_grad_size(a.F, a.Fe), RB)), dim3(RB), 0, st, a, 1);
   }
   return (int)hipGetLastError();
