@@ -202,6 +202,139 @@ __global__ void __launch_bounds__(RB) vb_edge_fwd(VA a, int l) {
   }
 }
 
+// vb_edge_fwd with the edge-attribute width FE fixed at compile time and 8
+// edges in flight per row (the column ids, edge attributes and B rows of a
+// group are all requested before the first is used); same sums, same order.
+template <int FE, int U>
+__device__ __forceinline__ void fwd_group(const RowGraph& g, int e, const float* Bg, const float (&wcr)[FE > 0 ? FE : 1],
+                                          float ac, float bc, int FeS, int c, int hs, uint32_t* wr, float& acc) {
+  constexpr int FA = FE > 0 ? FE : 1;
+  int j[U];
+  float ev[U][FA], q[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) j[u] = g.col[e + u];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int f = 0; f < FE; ++f) ev[u][f] = g.ea[(int64_t)(e + u) * FeS + f];
+#pragma unroll
+  for (int u = 0; u < U; ++u) q[u] = Bg[(int64_t)j[u] * 32];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    float ec = 0.f;
+#pragma unroll
+    for (int f = 0; f < FE; ++f) ec = fmaf(wcr[f], ev[u][f], ec);
+    const float pre = ac + q[u] + ec + bc;
+    acc += relu_keepnan(pre);
+    if (wr) {
+      const uint64_t m = __ballot(active(pre));
+      if (c == 0) wr[e + u] = (uint32_t)(m >> hs);
+    }
+  }
+}
+
+template <int FE>
+__global__ void __launch_bounds__(RB) vb_edge_fwd8(VA a, int l) {
+  constexpr int FA = FE > 0 ? FE : 1;
+  const Layer L = layer_of(a, l);
+  const int F = a.F, KE = a.KE, FeS = FE > 0 ? FE : 1;
+  const int c = threadIdx.x & 31;
+  float wcr[FA];
+#pragma unroll
+  for (int f = 0; f < FE; ++f) wcr[f] = L.we[c * KE + 2 * F + f];
+  const float bc = L.be[c];
+  uint32_t* words = a.ws.relu_words ? a.ws.relu_words + (int64_t)(l - 1) * a.ws.edge0[a.B] : nullptr;
+  const int hs = threadIdx.x & 32;
+  for (int64_t r = blockIdx.x * (RB / 32) + (threadIdx.x >> 5); r < a.ws.n_rows; r += (int64_t)gridDim.x * (RB / 32)) {
+    const RowGraph g = row_graph(a, r);
+    const float ac = L.a[r * 32 + c];
+    const float* Bg = L.bm + g.r0 * 32 + c;
+    uint32_t* wr = words ? words + a.ws.edge0[a.ws.row_slot[r]] : nullptr;
+    float acc = 0.f;
+    const int eb = g.rp[g.i], ee = g.rp[g.i + 1];
+    int e = eb;
+    for (; e + 8 <= ee; e += 8) fwd_group<FE, 8>(g, e, Bg, wcr, ac, bc, FeS, c, hs, wr, acc);
+    for (; e + 4 <= ee; e += 4) fwd_group<FE, 4>(g, e, Bg, wcr, ac, bc, FeS, c, hs, wr, acc);
+    for (; e < ee; ++e) fwd_group<FE, 1>(g, e, Bg, wcr, ac, bc, FeS, c, hs, wr, acc);
+    L.s[r * 32 + c] = acc;
+  }
+}
+
+// vb_edge_bwd's ReLU-word form with FE fixed and 8 edges in flight (same
+// counts, sums and order).
+template <int FE>
+__global__ void __launch_bounds__(RB) vb_edge_bwd8(VA a, int l) {
+  constexpr int FA = FE > 0 ? FE : 1;
+  const int FeS = FE > 0 ? FE : 1;
+  float* ws = a.ws.base;
+  const float* DS = ws + a.L.ds;
+  float *D = ws + a.L.d, *DP = ws + a.L.dp, *EAP = ws + a.L.eap;
+  const int c = threadIdx.x & 31;
+  const uint32_t* words = a.ws.relu_words + (int64_t)(l - 1) * a.ws.edge0[a.B];
+  for (int64_t r = blockIdx.x * (RB / 32) + (threadIdx.x >> 5); r < a.ws.n_rows; r += (int64_t)gridDim.x * (RB / 32)) {
+    const RowGraph g = row_graph(a, r);
+    const uint32_t* wr = words + a.ws.edge0[a.ws.row_slot[r]];
+    const float dsi = DS[r * 32 + c];
+    const float* DSg = DS + g.r0 * 32 + c;
+    int cnt = 0;
+    float eap[FA];
+#pragma unroll
+    for (int f = 0; f < FA; ++f) eap[f] = 0.f;
+    const int eb = g.rp[g.i], ee = g.rp[g.i + 1];
+    int e = eb;
+    for (; e + 8 <= ee; e += 8) {
+      uint32_t wv[8];
+      float ev[8][FA];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) wv[u] = wr[e + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int f = 0; f < FE; ++f) ev[u][f] = g.ea[(int64_t)(e + u) * FeS + f];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if ((wv[u] >> c) & 1u) {
+          ++cnt;
+#pragma unroll
+          for (int f = 0; f < FE; ++f) eap[f] += ev[u][f];
+        }
+    }
+    for (; e < ee; ++e)
+      if ((wr[e] >> c) & 1u) {
+        ++cnt;
+#pragma unroll
+        for (int f = 0; f < FE; ++f) eap[f] += g.ea[(int64_t)e * FeS + f];
+      }
+    D[r * 32 + c] = cnt ? dsi * (float)cnt : 0.f;
+#pragma unroll
+    for (int f = 0; f < FE; ++f) EAP[(r * 32 + c) * FeS + f] = cnt ? dsi * eap[f] : 0.f;
+    float acc = 0.f;
+    const int qb = g.trp[g.i], qe = g.trp[g.i + 1];
+    int q = qb;
+    for (; q + 8 <= qe; q += 8) {
+      int src[8], ed[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        src[u] = g.tcol[q + u];
+        ed[u] = g.teid[q + u];
+      }
+      uint32_t wv[8];
+      float dv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        wv[u] = wr[ed[u]];
+        dv[u] = DSg[(int64_t)src[u] * 32];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if ((wv[u] >> c) & 1u) acc += dv[u];
+    }
+    for (; q < qe; ++q)
+      if ((wr[g.teid[q]] >> c) & 1u) acc += DSg[(int64_t)g.tcol[q] * 32];
+    DP[r * 32 + c] = acc;
+  }
+}
+
 // Xout = relu([Xin | S] Wn^T + bn): 64 threads per row (F <= 64)
 __global__ void __launch_bounds__(RB) vb_node(VA a, int l) {
   extern __shared__ float lds[];
@@ -789,6 +922,24 @@ __global__ void __launch_bounds__(RB) vb_wgrad_combine(VA a, int l) {
   }
 }
 
+// the FE-specialised 8-in-flight edge kernels (Fe <= 4; the backward needs the
+// forward's ReLU words); false: not launched
+inline bool launch_edge8(bool fwd, const VA& a, int l, dim3 grid, hipStream_t st) {
+  if (a.Fe > 4 || (!fwd && !a.ws.relu_words)) return false;
+#define DR_E8(FE)                                                                   \
+  if (fwd) hipLaunchKernelGGL(vb_edge_fwd8<FE>, grid, dim3(RB), 0, st, a, l);      \
+  else hipLaunchKernelGGL(vb_edge_bwd8<FE>, grid, dim3(RB), 0, st, a, l);
+  switch (a.Fe) {
+    case 0: DR_E8(0) break;
+    case 1: DR_E8(1) break;
+    case 2: DR_E8(2) break;
+    case 3: DR_E8(3) break;
+    default: DR_E8(4) break;
+  }
+#undef DR_E8
+  return true;
+}
+
 inline int rows_grid(int64_t rows, int rows_per_block) {
   int64_t g = (rows + rows_per_block - 1) / rows_per_block;
   if (g < 1) g = 1;
@@ -851,7 +1002,8 @@ extern "C" int dr_vanilla_graph_pass(const dr_graph_store* store, const dr_graph
   for (int l = 1; l <= 2; ++l) {
     if (mf) hipLaunchKernelGGL(vb_gemm<GM_HALVES>, dim3(gg), dim3(RB), glds(GM_HALVES), st, a, l);
     else hipLaunchKernelGGL(vb_halves, dim3(rows_grid(R, RB / 64)), dim3(RB), lds_half, st, a, l);
-    hipLaunchKernelGGL(vb_edge_fwd, dim3(rows_grid(R, RB / 32)), dim3(RB), 0, st, a, l);
+    if (!launch_edge8(true, a, l, dim3(rows_grid(R, RB / 32)), st))
+      hipLaunchKernelGGL(vb_edge_fwd, dim3(rows_grid(R, RB / 32)), dim3(RB), 0, st, a, l);
     if (mf) hipLaunchKernelGGL(vb_gemm<GM_NODE>, dim3(gg), dim3(RB), glds(GM_NODE), st, a, l);
     else hipLaunchKernelGGL(vb_node, dim3(rows_grid(R, RB / 64)), dim3(RB), lds_node, st, a, l);
   }
@@ -860,7 +1012,8 @@ extern "C" int dr_vanilla_graph_pass(const dr_graph_store* store, const dr_graph
     hipLaunchKernelGGL(vb_du, dim3(rows_grid(R * a.XS, RB)), dim3(RB), 0, st, a, 2);
     if (mf) hipLaunchKernelGGL(vb_gemm<GM_DXS>, dim3(gg), dim3(RB), glds(GM_DXS), st, a, 2);
     else hipLaunchKernelGGL(vb_dxs, dim3(rows_grid(R, RB / 128)), dim3(RB), lds_dxs, st, a, 2);
-    hipLaunchKernelGGL(vb_edge_bwd, dim3(rows_grid(R, RB / 32)), dim3(RB), 0, st, a, 2);
+    if (!launch_edge8(false, a, 2, dim3(rows_grid(R, RB / 32)), st))
+      hipLaunchKernelGGL(vb_edge_bwd, dim3(rows_grid(R, RB / 32)), dim3(RB), 0, st, a, 2);
     if (mf) hipLaunchKernelGGL(vb_gemm<GM_DX1>, dim3(gg), dim3(RB), glds(GM_DX1), st, a, 2);
     else hipLaunchKernelGGL(vb_dx1, dim3(rows_grid(R, RB / 64)), dim3(RB), lds_dx1, st, a);
     if (mf) hipLaunchKernelGGL(vb_wgrad_mfma, dim3(scratch->n_chunks), dim3(RB), lds_wg, st, a, 2);
@@ -869,7 +1022,8 @@ extern "C" int dr_vanilla_graph_pass(const dr_graph_store* store, const dr_graph
     hipLaunchKernelGGL(vb_du, dim3(rows_grid(R * a.XS, RB)), dim3(RB), 0, st, a, 1);
     if (mf) hipLaunchKernelGGL(vb_gemm<GM_DXS>, dim3(gg), dim3(RB), glds(GM_DXS), st, a, 1);
     else hipLaunchKernelGGL(vb_dxs, dim3(rows_grid(R, RB / 128)), dim3(RB), lds_dxs, st, a, 1);
-    hipLaunchKernelGGL(vb_edge_bwd, dim3(rows_grid(R, RB / 32)), dim3(RB), 0, st, a, 1);
+    if (!launch_edge8(false, a, 1, dim3(rows_grid(R, RB / 32)), st))
+      hipLaunchKernelGGL(vb_edge_bwd, dim3(rows_grid(R, RB / 32)), dim3(RB), 0, st, a, 1);
     if (mf) hipLaunchKernelGGL(vb_wgrad_mfma, dim3(scratch->n_chunks), dim3(RB), lds_wg, st, a, 1);
     else hipLaunchKernelGGL(vb_wgrad_part, dim3(scratch->n_chunks), dim3(RB), lds_wg, st, a, 1);
     hipLaunchKernelGGL(vb_wgrad_combine, dim3(rows_grid((int64_t)n_batch * layer_grad_size(a.F, a.Fe), RB)), dim3(RB), 0, st, a, 1);
