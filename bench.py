@@ -254,6 +254,7 @@ def parse_args(argv):
     ap.add_argument("--dtype", choices=["f32", "bf16"], default="f32", help="compute dtype of the node GEMMs (bf16: GINet only; fp32 accumulate, fp32 master weights and Adam)")
     ap.add_argument("--force-large", type=int, default=0, help="GINet: run the split tile+tail path with this many nodes per tile (diagnostic)")
     ap.add_argument("--ginet-path", choices=["auto", "split", "onepass"], default="auto", help="GINet: auto = one workgroup per graph when the batch fits LDS, else the split path; split = tile kernel + tail kernel; onepass = tiles + in-launch tails (one launch)")
+    ap.add_argument("--vanilla-pipeline", action="store_true", help="VanillaNetwork: the batch-wide kernel pipeline even when the per-graph kernel fits (diagnostic)")
     ap.add_argument("--one-launch", action="store_true", help="GINet, N=1: graph pass + gradient reduce + Adam in one launch (dr_ginet_train_step; opt-in, measured slower at B=64)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stream-copy", action="store_true")
@@ -339,6 +340,7 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
         h.force_large = bool(args.force_large) or args.ginet_path != "auto"
         h.large_tile = args.force_large or None
         h.large_onepass = args.ginet_path == "onepass"
+        h.vanilla_pipeline = bool(args.vanilla_pipeline)
 
     torch.manual_seed(1234)
     model = models[args.model](30, 1, 3).to(dev).train()
