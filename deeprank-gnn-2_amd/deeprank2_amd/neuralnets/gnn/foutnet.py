@@ -44,7 +44,7 @@ class _FoutLayerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, edge_index, wc, wn, bias):
         n = x.shape[0]
-        rowptr, _, col = ops.csr_from_coo(edge_index[0], edge_index[1], n)
+        rowptr, _, col = ops.graph_csr(edge_index, n)
         zm = ops.spmm_csr(rowptr, col, x, n, mean=True)
         out = ops.linear_xwT(x, wc.t().contiguous()) + ops.linear_xwT(zm, wn.t().contiguous())
         if bias is not None:
@@ -65,7 +65,7 @@ class _FoutLayerFn(torch.autograd.Function):
         dout_has = torch.where(has, dout, torch.zeros_like(dout))
         dwn = ops.linear_dw(dout_has, torch.where(has, zm, torch.zeros_like(zm))).t().contiguous()
         # d(neighbour term) / x_j = sum_{i: i->j} dout_i / deg_i  (transposed CSR)
-        trowptr, _, tcol = ops.csr_from_coo(edge_index[1], edge_index[0], n)
+        trowptr, _, tcol = ops.graph_csr(edge_index, n, transpose=True)
         dbeta = ops.spmm_csr(trowptr, tcol, torch.where(has, dout / deg.clamp_min(1), torch.zeros_like(dout)), n)
         dx = ops.linear_xwT(dout, wc) + ops.linear_xwT(dbeta, wn)
         db = dout.sum(0) if ctx.has_bias else None
@@ -95,9 +95,7 @@ class FoutLayer(nn.Module):
 
     def forward(self, x, edge_index):
         _lib.require_device(x, edge_index)
-        if edge_index.numel() and (int(edge_index.min()) < 0 or int(edge_index.max()) >= x.shape[0]):
-            msg = "edge_index refers to a node outside x"
-            raise IndexError(msg)
+        ops.check_edge_range(edge_index, x.shape[0])
         return _FoutLayerFn.apply(x.float(), edge_index, self.wc, self.wn, self.bias)
 
     def __repr__(self):

@@ -57,8 +57,7 @@ class _ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, edge_index, w, w_ea, w_att):
         n = x.shape[0]
-        row, col = edge_index[0], edge_index[1]
-        rowptr, _, col_s = ops.csr_from_coo(row, col, n)
+        rowptr, _, col_s = ops.graph_csr(edge_index, n)
         z = ops.spmm_csr(rowptr, col_s, ops.linear_xwT(x, w), n)
         ctx.save_for_backward(x, edge_index, w)
         ctx.dead = (w_ea, w_att)
@@ -68,7 +67,7 @@ class _ConvFn(torch.autograd.Function):
     def backward(ctx, dz):
         x, edge_index, w = ctx.saved_tensors
         n = x.shape[0]
-        trowptr, _, tcol = ops.csr_from_coo(edge_index[1], edge_index[0], n)
+        trowptr, _, tcol = ops.graph_csr(edge_index, n, transpose=True)
         dy = ops.spmm_csr(trowptr, tcol, dz.contiguous(), n)
         dx = ops.linear_xw(dy, w) if ctx.needs_input_grad[0] else None
         dw = ops.linear_dw(dy, x) if ctx.needs_input_grad[2] else None
@@ -118,11 +117,7 @@ class GINetConvLayer(nn.Module):
             msg = "GINetConvLayer(bias=True) is not supported on the MI355X path"
             raise NotImplementedError(msg)
         _lib.require_device(x, edge_index)
-        if edge_index.numel():
-            lo, hi = int(edge_index.min()), int(edge_index.max())
-            if lo < 0 or hi >= x.shape[0]:
-                msg = f"edge_index out of range [0, {x.shape[0]})"
-                raise IndexError(msg)
+        ops.check_edge_range(edge_index, x.shape[0])
         ea = edge_attr.unsqueeze(-1) if edge_attr.dim() == 1 else edge_attr
         if ea.shape[0] != edge_index.shape[1] or ea.shape[1] != self.fc_edge_attr.in_features:
             msg = f"edge_attr must be [E, {self.fc_edge_attr.in_features}]"

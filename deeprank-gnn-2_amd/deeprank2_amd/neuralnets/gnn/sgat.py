@@ -95,9 +95,7 @@ class SGraphAttentionLayer(nn.Module):
     def forward(self, x, edge_index, edge_attr):
         _lib.require_device(x, edge_index, edge_attr)
         n = x.shape[0]
-        if edge_index.numel() and (int(edge_index.min()) < 0 or int(edge_index.max()) >= n):
-            msg = "edge_index refers to a node outside x"
-            raise IndexError(msg)
+        ops.check_edge_range(edge_index, n)
         ea = edge_attr.unsqueeze(-1) if edge_attr.dim() == 1 else edge_attr
         if ea.shape[1] != 1:
             msg = f"SGraphAttentionLayer needs one edge feature (edge_attr [E] or [E, 1], got {tuple(edge_attr.shape)}): sgat.py:71 multiplies it into every output channel"

@@ -7,9 +7,50 @@ status into ``RuntimeError``.  No wrapper has a CPU path.
 
 from __future__ import annotations
 
+import weakref
+
 import torch
 
 from deeprank2_amd import _lib
+
+# Per edge_index tensor (held weakly; dropped when the tensor dies or is
+# modified in place): its CSR, transposed CSR and range check.  A batch's
+# edge_index is static across the layers and steps that reuse it (the layer
+# path of layered.py), so those CSR builds and the host-syncing range check
+# run once per tensor instead of once per call.
+_GRAPHS: dict = {}
+
+
+def _graph_entry(edge_index, n_rows):
+    key = id(edge_index)
+    ent = _GRAPHS.get(key)
+    if ent is not None and (ent["ref"]() is not edge_index or ent["version"] != edge_index._version or ent["n"] != n_rows):
+        ent = None
+    if ent is None:
+        ent = {"ref": weakref.ref(edge_index, lambda _r, k=key: _GRAPHS.pop(k, None)), "version": edge_index._version, "n": n_rows}
+        _GRAPHS[key] = ent
+    return ent
+
+
+def check_edge_range(edge_index, n_rows):
+    """IndexError if edge_index refers to a node outside [0, n_rows) (one host sync per tensor)."""
+    ent = _graph_entry(edge_index, n_rows)
+    if not ent.get("checked"):
+        if edge_index.numel() and (int(edge_index.min()) < 0 or int(edge_index.max()) >= n_rows):
+            msg = f"edge_index refers to a node outside [0, {n_rows})"
+            raise IndexError(msg)
+        ent["checked"] = True
+
+
+def graph_csr(edge_index, n_rows, transpose=False):
+    """(rowptr, perm, col) of edge_index by edge_index[0] (transpose: by
+    edge_index[1]), stable; cached per tensor."""
+    ent = _graph_entry(edge_index, n_rows)
+    k = "tcsr" if transpose else "csr"
+    if k not in ent:
+        r, c = (edge_index[1], edge_index[0]) if transpose else (edge_index[0], edge_index[1])
+        ent[k] = csr_from_coo(r, c, n_rows)
+    return ent[k]
 
 
 def _f32(t, name):
