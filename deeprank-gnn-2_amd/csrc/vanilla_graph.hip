@@ -151,9 +151,20 @@ __device__ __forceinline__ void mm16(int M, int Nn, int K, int start, AF A, BF B
     const int m0 = (job / ntl) << 4, n0 = (job % ntl) << 4;
     const int am = min(m0 + li, M - 1), bn = min(n0 + li, Nn - 1);
     floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < K; k += 8) {
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(A(am, k + kq), Bf(k + kq, bn), acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(A(am, k + 4 + kq), Bf(k + 4 + kq, bn), acc1, 0, 0, 0);
+    // four 8-deep k-steps per iteration, their operand reads issued together
+    // (A / B return 0 for k >= K, so the last group may run past K)
+    for (int k = 0; k < K; k += 32) {
+      float av[8], bv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        av[u] = A(am, k + 4 * u + kq);
+        bv[u] = Bf(k + 4 * u + kq, bn);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u + 1], bv[u + 1], acc1, 0, 0, 0);
+      }
     }
     if (n0 + li < Nn) {
 #pragma unroll
