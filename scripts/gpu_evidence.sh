@@ -13,6 +13,9 @@ echo "smoke rc=$rc"; tail -1 gpurun_out/smoke.log
 timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1; rc=$?
 echo "bench rc=$rc"; grep '^{' gpurun_out/bench.log | cut -c1-300
 [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_driver.log 2>&1; rc=$?
+echo "bench (driver step counts) rc=$rc"; grep '^{' gpurun_out/bench_driver.log | cut -c1-300
+[ $rc -eq 0 ] || exit $rc
 bash scripts/gpu_configs.sh || exit $?
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/prof -o run -- python3 $R/bench.py --steps 100 --warmup 10 --no-cpu-baseline > $R/gpurun_out/prof.log 2>&1; rc=$?
