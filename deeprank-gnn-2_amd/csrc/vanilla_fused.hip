@@ -133,26 +133,6 @@ __device__ __forceinline__ bool active(float pre) { return !(pre <= 0.f); }
 
 // ---- forward ------------------------------------------------------------------
 
-// [A | B] = Xin [Wa; Wb]^T: 64 threads per row
-__global__ void __launch_bounds__(RB) vb_halves(VA a, int l) {
-  extern __shared__ float lds[];
-  const Layer L = layer_of(a, l);
-  const int F = a.F, KE = a.KE, LW = F + 1;
-  for (int p = threadIdx.x; p < 64 * F; p += RB) {  // [64][F+1]
-    const int c = p / F, k = p - c * F;
-    lds[c * LW + k] = L.we[(c & 31) * KE + (c < 32 ? 0 : F) + k];
-  }
-  __syncthreads();
-  const int c = threadIdx.x & 63;
-  const float* w = lds + c * LW;
-  for (int64_t r = blockIdx.x * (RB / 64) + (threadIdx.x >> 6); r < a.ws.n_rows; r += (int64_t)gridDim.x * (RB / 64)) {
-    const float* x = xin_row(a, L, r);
-    float acc = 0.f;
-    for (int k = 0; k < F; ++k) acc = fmaf(x[k], w[k], acc);
-    (c < 32 ? L.a : L.bm)[r * 32 + (c & 31)] = acc;
-  }
-}
-
 // S_i = sum_{e in row i} relu(A_i + B_j + Wc ea_e + be): 32 threads per row
 __global__ void __launch_bounds__(RB) vb_edge_fwd(VA a, int l) {
   __shared__ float swc[32 * MAXFE + 32];
@@ -335,27 +315,6 @@ __global__ void __launch_bounds__(RB) vb_edge_bwd8(VA a, int l) {
   }
 }
 
-// Xout = relu([Xin | S] Wn^T + bn): 64 threads per row (F <= 64)
-__global__ void __launch_bounds__(RB) vb_node(VA a, int l) {
-  extern __shared__ float lds[];
-  const Layer L = layer_of(a, l);
-  const int F = a.F, KN = a.KN, XS = a.XS, LW = KN + 1;
-  for (int p = threadIdx.x; p < F * KN; p += RB) lds[(p / KN) * LW + p % KN] = L.wn[p];
-  for (int p = threadIdx.x; p < F; p += RB) lds[F * LW + p] = L.bn[p];
-  __syncthreads();
-  const int n = threadIdx.x & 63;
-  for (int64_t r = blockIdx.x * (RB / 64) + (threadIdx.x >> 6); r < a.ws.n_rows; r += (int64_t)gridDim.x * (RB / 64)) {
-    if (n >= F) continue;
-    const float* x = xin_row(a, L, r);
-    const float* sv = L.s + r * 32;
-    const float* w = lds + n * LW;
-    float acc = 0.f;
-    for (int k = 0; k < F; ++k) acc = fmaf(x[k], w[k], acc);
-    for (int k = 0; k < 32; ++k) acc = fmaf(sv[k], w[F + k], acc);
-    L.xout[r * XS + n] = relu_keepnan(acc + lds[F * LW + n]);
-  }
-}
-
 // per graph: scatter_mean -> graph MLP -> loss -> head backward (one workgroup)
 __global__ void __launch_bounds__(256) vb_head(VA a) {
   __shared__ float sG[64], sH[128], sDh[128], sDout[16], sRed[256];
@@ -463,27 +422,6 @@ __global__ void __launch_bounds__(RB) vb_du(VA a, int l) {
     float g = 0.f;
     if (n < F) g = (l == 2) ? a.p.head[(int64_t)a.ws.row_slot[r] * HS + HD + n] : dx1[p];
     du[p] = n < F ? relu_bwd(xo[p], g) : 0.f;
-  }
-}
-
-// [dX1_direct | DS] = DU Wn  (layer 2: both;  layer 1: DS only).  128 threads per row.
-__global__ void __launch_bounds__(RB) vb_dxs(VA a, int l) {
-  extern __shared__ float lds[];
-  const int F = a.F, KN = a.KN, XS = a.XS;
-  const float* wn = l == 2 ? a.w.wn2 : a.w.wn1;
-  for (int p = threadIdx.x; p < F * KN; p += RB) lds[p] = wn[p];
-  __syncthreads();
-  const float* du = a.ws.base + a.L.du;
-  float* dx1 = a.ws.base + a.L.dx1;
-  float* ds = a.ws.base + a.L.ds;
-  const int k = threadIdx.x & 127;
-  for (int64_t r = blockIdx.x * (RB / 128) + (threadIdx.x >> 7); r < a.ws.n_rows; r += (int64_t)gridDim.x * (RB / 128)) {
-    if (k >= KN || (l == 1 && k < F)) continue;
-    const float* u = du + r * XS;
-    float acc = 0.f;
-    for (int n = 0; n < F; ++n) acc = fmaf(u[n], lds[n * KN + k], acc);
-    if (k < F) dx1[r * XS + k] = acc;
-    else ds[r * 32 + k - F] = acc;
   }
 }
 
@@ -633,28 +571,6 @@ __global__ void __launch_bounds__(RB) vb_edge_bwd(VA a, int l) {
   }
 }
 
-// DX1 += D Wa2 + D' Wb2: 64 threads per row
-__global__ void __launch_bounds__(RB) vb_dx1(VA a) {
-  extern __shared__ float lds[];
-  const int F = a.F, KE = a.KE, XS = a.XS;
-  for (int p = threadIdx.x; p < 32 * 2 * F; p += RB) {  // [c][0..2F)
-    const int c = p / (2 * F), k = p - c * 2 * F;
-    lds[p] = a.w.we2[c * KE + k];
-  }
-  __syncthreads();
-  float* ws = a.ws.base;
-  const float *D = ws + a.L.d, *DP = ws + a.L.dp;
-  float* dx1 = ws + a.L.dx1;
-  const int k = threadIdx.x & 63;
-  for (int64_t r = blockIdx.x * (RB / 64) + (threadIdx.x >> 6); r < a.ws.n_rows; r += (int64_t)gridDim.x * (RB / 64)) {
-    if (k >= F) continue;
-    float acc = dx1[r * XS + k];
-    for (int c = 0; c < 32; ++c) acc = fmaf(D[r * 32 + c], lds[c * 2 * F + k], acc);
-    for (int c = 0; c < 32; ++c) acc = fmaf(DP[r * 32 + c], lds[c * 2 * F + F + k], acc);
-    dx1[r * XS + k] = acc;
-  }
-}
-
 // ---- node GEMMs on MFMA -----------------------------------------------------
 // out(r, n) = init(r, n) + sum_{k < K} A(r, k) W(k, n) for every batch row r,
 // n < NO, on v_mfma_f32_16x16x4_f32 (k in order: the same fmaf chain as a
@@ -725,7 +641,7 @@ __global__ void __launch_bounds__(RB) vb_gemm(VA a, int l) {
     for (int n0 = 0; n0 < NO; n0 += 16) {
       const int n = n0 + li;
       floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-      if (MODE == GM_DX1) {  // the accumulation starts from dX1 (vb_dxs's direct part)
+      if (MODE == GM_DX1) {  // the accumulation starts from dX1 (the DU Wn part, GM_DXS)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int64_t r = t0 + i0 + kq * 4 + q;
@@ -757,76 +673,14 @@ __global__ void __launch_bounds__(RB) vb_gemm(VA a, int l) {
 
 // Weight-gradient partials of one layer per chunk of DR_VANILLA_CHUNK rows
 // (all CUs busy), rows staged through LDS; vb_wgrad_combine then sums each
-// graph's chunks in order into its slab (deterministic).
+// graph's chunks in order into its slab (deterministic).  The three GEMMs
+// (dWa = D^T X, dWb = D'^T X, dWn = DU^T [X | S]: K = the chunk's rows,
+// zero-padded to WR) run on MFMA, one 16x16 output tile per job, jobs over
+// the 4 waves; the bias / edge-attribute sums stay scalar.
 constexpr int WR = DR_VANILLA_CHUNK;
 
 __host__ __device__ inline int layer_grad_size(int F, int Fe) { return 32 * (2 * F + Fe) + 32 + F * (F + 32) + F; }
 
-__global__ void __launch_bounds__(RB) vb_wgrad_part(VA a, int l) {
-  extern __shared__ float lds[];
-  const int ch = blockIdx.x;
-  const int b = a.ws.chunk_slot[ch];
-  const int F = a.F, Fe = a.Fe, KE = a.KE, KN = a.KN, XS = a.XS, FeS = Fe > 0 ? Fe : 1;
-  const Layer L = layer_of(a, l);
-  const int64_t r0 = a.ws.row0[b];
-  const int N = a.ws.row0[b + 1] - (int)r0;
-  const int i0 = (ch - a.ws.chunk_first[b]) * WR, nr = min(WR, N - i0);
-  const int64_t g0 = r0 + i0;  // first batch row of the chunk
-  float* ws = a.ws.base;
-  const float* X = L.xin ? L.xin + g0 * XS : a.s.x + (a.descs[b].node0 + i0) * XS;
-  // LDS chunk: X [WR][XS] | S [WR][32] | D [WR][32] | DP [WR][32] | DU [WR][XS] | EAP [WR][32*FeS]
-  float* cX = lds;
-  float* cS = cX + WR * XS;
-  float* cD = cS + WR * 32;
-  float* cDP = cD + WR * 32;
-  float* cDU = cDP + WR * 32;
-  float* cE = cDU + WR * XS;
-  for (int p = threadIdx.x; p < nr * XS; p += RB) {
-    cX[p] = X[p];
-    cDU[p] = ws[a.L.du + g0 * XS + p];
-  }
-  for (int p = threadIdx.x; p < nr * 32; p += RB) {
-    cS[p] = L.s[g0 * 32 + p];
-    cD[p] = ws[a.L.d + g0 * 32 + p];
-    cDP[p] = ws[a.L.dp + g0 * 32 + p];
-  }
-  for (int p = threadIdx.x; p < nr * 32 * FeS; p += RB) cE[p] = ws[a.L.eap + g0 * 32 * FeS + p];
-  __syncthreads();
-  const int nwe = 32 * KE, nwn = F * KN, total = nwe + 32 + nwn + F;
-  float* out = a.ws.part + (int64_t)ch * total;
-  for (int p = threadIdx.x; p < total; p += RB) {
-    float v = 0.f;
-    if (p < nwe) {
-      const int c = p / KE, k = p - c * KE;
-      if (k < F) {
-        for (int i = 0; i < nr; ++i) v = fmaf(cD[i * 32 + c], cX[i * XS + k], v);
-      } else if (k < 2 * F) {
-        for (int i = 0; i < nr; ++i) v = fmaf(cDP[i * 32 + c], cX[i * XS + k - F], v);
-      } else {
-        for (int i = 0; i < nr; ++i) v += cE[(i * 32 + c) * FeS + (k - 2 * F)];
-      }
-    } else if (p < nwe + 32) {
-      const int c = p - nwe;
-      for (int i = 0; i < nr; ++i) v += cD[i * 32 + c];
-    } else if (p < nwe + 32 + nwn) {
-      const int q = p - nwe - 32, n = q / KN, k = q - n * KN;
-      if (k < F) {
-        for (int i = 0; i < nr; ++i) v = fmaf(cDU[i * XS + n], cX[i * XS + k], v);
-      } else {
-        for (int i = 0; i < nr; ++i) v = fmaf(cDU[i * XS + n], cS[i * 32 + k - F], v);
-      }
-    } else {
-      const int n = p - nwe - 32 - nwn;
-      for (int i = 0; i < nr; ++i) v += cDU[i * XS + n];
-    }
-    out[p] = v;
-  }
-}
-
-// The same partials with the three GEMMs on MFMA (dWa = D^T X, dWb = D'^T X,
-// dWn = DU^T [X | S]: K = the chunk's rows, zero-padded to WR; one 16x16
-// output tile per job, jobs over the 4 waves); the bias / edge-attribute sums
-// stay scalar.
 __global__ void __launch_bounds__(RB) vb_wgrad_mfma(VA a, int l) {
   extern __shared__ float lds[];
   const int ch = blockIdx.x;
@@ -956,7 +810,7 @@ extern "C" int64_t dr_vanilla_scratch_floats(int64_t n_rows, int32_t n_feat, int
 extern "C" int64_t dr_vanilla_lds_bytes(int32_t n_feat, int32_t n_edge_feat, int32_t out_dim) {
   (void)out_dim;
   const int XS = r4(n_feat), FeS = n_edge_feat > 0 ? n_edge_feat : 1;
-  return 4LL * WR * (2 * XS + 3 * 32 + 32 * FeS);  // the largest dynamic LDS of the pipeline (vb_wgrad_part)
+  return 4LL * WR * (2 * XS + 3 * 32 + 32 * FeS);  // the largest dynamic LDS of the pipeline (vb_wgrad_mfma)
 }
 
 extern "C" int64_t dr_vanilla_part_floats(int32_t n_feat, int32_t n_edge_feat) {
@@ -994,38 +848,29 @@ extern "C" int dr_vanilla_graph_pass(const dr_graph_store* store, const dr_graph
   a.L = scratch_layout(scratch->n_rows, a.F, a.Fe);
   hipStream_t st = (hipStream_t)stream;
   const int64_t R = scratch->n_rows;
-  const size_t lds_half = 4 * 64 * (a.F + 1), lds_node = 4 * (a.F * (a.KN + 1) + a.F), lds_dxs = 4 * a.F * a.KN,
-               lds_dx1 = 4 * 64 * a.F, lds_wg = (size_t)dr_vanilla_lds_bytes(a.F, a.Fe, pass->out_dim);
-  const bool mf = a.F <= 64;  // node GEMMs on MFMA (vb_gemm); the scalar kernels stay as the reference form
+  const size_t lds_wg = (size_t)dr_vanilla_lds_bytes(a.F, a.Fe, pass->out_dim);
   const int gg = rows_grid(R, GT) < 1024 ? rows_grid(R, GT) : 1024;
   auto glds = [&](int mode) { return (size_t)4 * gemm_lds_floats(mode, a.F); };
   for (int l = 1; l <= 2; ++l) {
-    if (mf) hipLaunchKernelGGL(vb_gemm<GM_HALVES>, dim3(gg), dim3(RB), glds(GM_HALVES), st, a, l);
-    else hipLaunchKernelGGL(vb_halves, dim3(rows_grid(R, RB / 64)), dim3(RB), lds_half, st, a, l);
+    hipLaunchKernelGGL(vb_gemm<GM_HALVES>, dim3(gg), dim3(RB), glds(GM_HALVES), st, a, l);
     if (!launch_edge8(true, a, l, dim3(rows_grid(R, RB / 32)), st))
       hipLaunchKernelGGL(vb_edge_fwd, dim3(rows_grid(R, RB / 32)), dim3(RB), 0, st, a, l);
-    if (mf) hipLaunchKernelGGL(vb_gemm<GM_NODE>, dim3(gg), dim3(RB), glds(GM_NODE), st, a, l);
-    else hipLaunchKernelGGL(vb_node, dim3(rows_grid(R, RB / 64)), dim3(RB), lds_node, st, a, l);
+    hipLaunchKernelGGL(vb_gemm<GM_NODE>, dim3(gg), dim3(RB), glds(GM_NODE), st, a, l);
   }
   hipLaunchKernelGGL(vb_head, dim3(n_batch), dim3(256), 0, st, a);
   if (pass->flags & DR_PASS_BACKWARD) {
     hipLaunchKernelGGL(vb_du, dim3(rows_grid(R * a.XS, RB)), dim3(RB), 0, st, a, 2);
-    if (mf) hipLaunchKernelGGL(vb_gemm<GM_DXS>, dim3(gg), dim3(RB), glds(GM_DXS), st, a, 2);
-    else hipLaunchKernelGGL(vb_dxs, dim3(rows_grid(R, RB / 128)), dim3(RB), lds_dxs, st, a, 2);
+    hipLaunchKernelGGL(vb_gemm<GM_DXS>, dim3(gg), dim3(RB), glds(GM_DXS), st, a, 2);
     if (!launch_edge8(false, a, 2, dim3(rows_grid(R, RB / 32)), st))
       hipLaunchKernelGGL(vb_edge_bwd, dim3(rows_grid(R, RB / 32)), dim3(RB), 0, st, a, 2);
-    if (mf) hipLaunchKernelGGL(vb_gemm<GM_DX1>, dim3(gg), dim3(RB), glds(GM_DX1), st, a, 2);
-    else hipLaunchKernelGGL(vb_dx1, dim3(rows_grid(R, RB / 64)), dim3(RB), lds_dx1, st, a);
-    if (mf) hipLaunchKernelGGL(vb_wgrad_mfma, dim3(scratch->n_chunks), dim3(RB), lds_wg, st, a, 2);
-    else hipLaunchKernelGGL(vb_wgrad_part, dim3(scratch->n_chunks), dim3(RB), lds_wg, st, a, 2);
+    hipLaunchKernelGGL(vb_gemm<GM_DX1>, dim3(gg), dim3(RB), glds(GM_DX1), st, a, 2);
+    hipLaunchKernelGGL(vb_wgrad_mfma, dim3(scratch->n_chunks), dim3(RB), lds_wg, st, a, 2);
     hipLaunchKernelGGL(vb_wgrad_combine, dim3(rows_grid((int64_t)n_batch * layer_grad_size(a.F, a.Fe), RB)), dim3(RB), 0, st, a, 2);
     hipLaunchKernelGGL(vb_du, dim3(rows_grid(R * a.XS, RB)), dim3(RB), 0, st, a, 1);
-    if (mf) hipLaunchKernelGGL(vb_gemm<GM_DXS>, dim3(gg), dim3(RB), glds(GM_DXS), st, a, 1);
-    else hipLaunchKernelGGL(vb_dxs, dim3(rows_grid(R, RB / 128)), dim3(RB), lds_dxs, st, a, 1);
+    hipLaunchKernelGGL(vb_gemm<GM_DXS>, dim3(gg), dim3(RB), glds(GM_DXS), st, a, 1);
     if (!launch_edge8(false, a, 1, dim3(rows_grid(R, RB / 32)), st))
       hipLaunchKernelGGL(vb_edge_bwd, dim3(rows_grid(R, RB / 32)), dim3(RB), 0, st, a, 1);
-    if (mf) hipLaunchKernelGGL(vb_wgrad_mfma, dim3(scratch->n_chunks), dim3(RB), lds_wg, st, a, 1);
-    else hipLaunchKernelGGL(vb_wgrad_part, dim3(scratch->n_chunks), dim3(RB), lds_wg, st, a, 1);
+    hipLaunchKernelGGL(vb_wgrad_mfma, dim3(scratch->n_chunks), dim3(RB), lds_wg, st, a, 1);
     hipLaunchKernelGGL(vb_wgrad_combine, dim3(rows_grid((int64_t)n_batch * layer_grad_size(a.F, a.Fe), RB)), dim3(RB), 0, st, a, 1);
   }
   return (int)hipGetLastError();

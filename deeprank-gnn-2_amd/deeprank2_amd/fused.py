@@ -41,6 +41,7 @@ class BatchHandle:
         self.large_atomic_max = True  # depth-0 max over tiles by 64-bit atomic max (False: per-tile partials)
         self.large_onepass = False  # split path in ONE launch: each graph's last-arriving tile runs its tail (dr_large_plan.arrive)
         self.force_layers = False  # run the layer-level path (layered.py) even when the graph pass fits (diagnostic)
+        self.vanilla_words = True  # Vanilla pipeline: forward ReLU words feed the backward (False: recomputed)
 
     def lds(self, key, fn):
         """Dynamic LDS bytes for the largest graph of the batch (cached per model kind)."""
@@ -76,11 +77,13 @@ class BatchHandle:
             c.chunk_slot = base + 4 * (2 * (self.B + 1) + rows)
             c.n_chunks = int(chunk_first[-1])
             c.part = pbuf.data_ptr()
-            # per-edge ReLU words of both layers (forward -> backward)
+            # per-edge ReLU words of both layers (forward -> backward);
+            # vanilla_words = False: the backward recomputes them (diagnostic)
             ne = self.store._sizes[1][self.gids_host.astype(np.int64)]  # noqa: SLF001
             e0 = torch.from_numpy(np.concatenate([[0], np.cumsum(ne)]).astype(np.int32)).to(dev)
             words = torch.empty(max(1, 2 * int(ne.sum())), dtype=torch.int32, device=dev)
-            c.edge0, c.relu_words = e0.data_ptr(), words.data_ptr()
+            if self.vanilla_words:
+                c.edge0, c.relu_words = e0.data_ptr(), words.data_ptr()
             sc = (c, (ints, buf, pbuf, e0, words))
             self._lds[key] = sc
         return sc

@@ -114,3 +114,20 @@ def test_fused_train_step_on_layers_matches_fused_kernel():
     for a, b in zip(s1.params, s2.params):
         np.testing.assert_allclose(b.detach().cpu().numpy(), a.detach().cpu().numpy(), rtol=0, atol=5e-5)
     assert int(s2.counter[0]) == 2
+
+
+def test_edge_index_csr_cache_follows_in_place_changes():
+    """ops.graph_csr caches per edge_index tensor; an in-place change of the
+    tensor (version bump) or another node count rebuilds it."""
+    from deeprank2_amd import ops
+
+    ei = torch.tensor([[0, 0, 1, 2], [1, 2, 2, 0]], device="cuda:0")
+    rp, _, col = ops.graph_csr(ei, 3)
+    assert rp.tolist() == [0, 2, 3, 4] and col.tolist() == [1, 2, 2, 0]
+    assert ops.graph_csr(ei, 3)[0] is rp  # cached
+    ei[0, 3] = 1  # edge (2 -> 0) becomes (1 -> 0)
+    rp2, _, col2 = ops.graph_csr(ei, 3)
+    assert rp2.tolist() == [0, 2, 4, 4] and col2.tolist() == [1, 2, 2, 0]
+    assert ops.graph_csr(ei, 4)[0].tolist() == [0, 2, 4, 4, 4]
+    with pytest.raises(IndexError):
+        ops.check_edge_range(torch.tensor([[0, 3], [1, 0]], device="cuda:0"), 3)

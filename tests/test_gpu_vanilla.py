@@ -136,3 +136,35 @@ def test_vanilla_captured_replay_matches_eager():
         assert torch.equal(l1, s2.loss_out), i
     for a, b in zip(s1.params, s2.params):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("fe", [3, 6])
+def test_vanilla_pipeline_relu_words_bit_identical_to_recomputed(fe):
+    """The pipeline's backward reading the forward's per-edge ReLU words
+    (vb_edge_bwd8 for Fe <= 4, vb_edge_bwd for more) gives exactly the
+    outputs, slabs and head vectors of the backward that recomputes every
+    activation (same decisions, same sums, same order)."""
+    import itertools
+
+    from deeprank2_amd import _lib
+
+    datas = _datas(3, seed=46, n_lo=600, n_hi=900, mean_degree=14.0)
+    gen = np.random.default_rng(5)
+    for d in datas:
+        d.cluster0 = d.cluster1 = None
+        d.edge_attr = torch.from_numpy(gen.normal(size=(d.edge_index.shape[1], fe)).astype(np.float32))
+    store = GraphStore(pack_graphs(records_from_batch(P.Batch.from_data_list(datas)), require_clusters=False), DEV)
+    torch.manual_seed(17)
+    m = amd.VanillaNetwork(30, 1, fe).to(DEV)
+    res = []
+    for words in (True, False):
+        h = BatchHandle(store, np.arange(len(datas)))
+        h.vanilla_pipeline, h.vanilla_words = True, words
+        out = torch.empty(len(datas), 1, device=DEV)
+        slab = torch.empty(len(datas) * m.fused_spec.slab_stride(30), device=DEV)
+        head = torch.zeros(len(datas) * m.fused_spec.head_stride(1), device=DEV)
+        amd.graph_pass(m, h, m.ordered_params(), 1, _lib.DR_PASS_FORWARD | _lib.DR_PASS_BACKWARD, loss_kind=_lib.DR_LOSS_MSE, loss_scale=0.3, out=out, slab=slab, head=head)
+        torch.cuda.synchronize()
+        res.append((out.cpu(), slab.cpu(), head.cpu()))
+    for a, b in itertools.zip_longest(*res):
+        assert torch.equal(a, b)
