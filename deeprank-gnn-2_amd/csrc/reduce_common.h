@@ -47,7 +47,7 @@ struct alignas(64) ReduceHdr {
   float log2_beta1, log2_beta2;  // beta^t = exp2(t log2 beta): one v_exp_f32, not powf
   int32_t n_params, n_blocks;
   int16_t blk0[18];  // first block of each parameter (prefix sums of ceil(numel / RP)), blk0[n_params] = n_blocks
-  int32_t pad2;
+  int32_t slab_rows;  // slab rows per graph (>= 1): a slab-kind gradient sums B * slab_rows rows
 };
 
 typedef __attribute__((address_space(1))) unsigned int gu32r;
@@ -93,7 +93,8 @@ __device__ __forceinline__ void reduce_block(const ReduceHdr& h, const ParamRec&
   const int64_t st = slab_kind ? h.slab_stride : h.head_stride;
   const int col1 = outer ? r.off1 + ec / r.cols : r.off1 + ec;
   const int col2 = outer ? r.off2 + ec % r.cols : 0;
-  const int b0 = (h.B * ch) / RC, b1 = (h.B * (ch + 1)) / RC;
+  const int nb = slab_kind ? h.B * h.slab_rows : h.B;  // rows of this gradient's partials
+  const int b0 = (nb * ch) / RC, b1 = (nb * (ch + 1)) / RC;
   float u[RU], w[RU];
   if (has_src && b0 < b1) {
 #pragma unroll
@@ -227,6 +228,8 @@ inline int build_reduce(const dr_param_table* t, const float* slab, const float*
   for (int i = t->n_params; i < 18; ++i) h.blk0[i] = (int16_t)blocks;
   h.n_params = t->n_params;
   h.n_blocks = blocks;
+  if (t->slab_rows < 0 || t->slab_rows > 64) return DR_E_ARG;
+  h.slab_rows = t->slab_rows > 0 ? t->slab_rows : 1;
   return blocks;
 }
 

@@ -30,6 +30,20 @@
 // keep: S1, cnt, eap and the transposed ReLU words go to a per-graph global
 // scratch (L2-resident) and come back by bulk loads.  GEMM weights (the MFMA B
 // operand) are loaded from global into registers once per phase and wave.
+//
+// Split (k = 2..4 workgroups per graph, so a small batch fills the chip):
+// workgroup r owns the CSR rows [r0, r1) (edge-balanced bounds every sibling
+// computes alike) and runs every row-parallel phase on them; the weight
+// gradients are per-workgroup partials (slab row b*k + r, summed by
+// dr_reduce_update).  What crosses rows is exchanged through the scratch,
+// in-launch (MI355X_MICROARCH.md hand-off row 1: sc1 stores drained by every
+// wave, one agent-scope arrival per workgroup, an sc1 poll, sc1 loads):
+//   1. B2 rows (B1 is recomputed by every sibling from X0),
+//   2. the per-workgroup column sums of X2 (then every sibling runs the head),
+//   3. dS2 rows and 4. dS1 rows (the transposed passes gather them by source);
+// the edge ReLU words cross with them (stored sc1 in the forward row passes).
+// Siblings sit 8 blocks apart (one XCD under round-robin dispatch; placement
+// only affects speed) within a window of 8k consecutive blocks.
 // Bound: HBM on the compulsory inputs (x, CSR + transpose, edge_attr) and the
 // per-graph gradient partials; in practice the per-graph critical path — see
 // DESIGN.md §5.
@@ -86,9 +100,11 @@ __host__ __device__ inline VCarve vcarve(int N, int E, int Fe) {
 }
 
 // per-graph global scratch (floats): S1 [32N] | cnt1 [32N] | cnt2 [32N] | eap1 [Fe][32N] | eap2 [Fe][32N] |
-// bt1 [E + 1] | bt2 [E + 1]  (slot E of bt takes the padding lanes' stores)
+// bt1 [E + 1] | bt2 [E + 1] (slot E of bt takes the padding lanes' stores) |
+// split exchange: XA [32N] (B2, then dS1) | XB [32N] (dS2) | column sums [MAX_SPLIT][32]
+constexpr int MAXK = DR_VANILLA_MAX_SPLIT;
 __host__ __device__ inline int64_t vscratch_floats(int N, int E, int Fe) {
-  return (int64_t)(3 + 2 * Fe) * r4(32 * N) + 2LL * r4(E + 1);
+  return (int64_t)(5 + 2 * Fe) * r4(32 * N) + 2LL * r4(E + 1) + 32 * MAXK;
 }
 
 struct VGArgs {
@@ -98,8 +114,105 @@ struct VGArgs {
   const dr_graph_desc* descs;
   float* scr;
   const int64_t* scr_off;
-  int32_t B;
+  uint32_t* sync;  // [2B + 1]: per graph {arrivals, exits}; [2B]: hand-off timeout flag
+  int32_t B, k;
 };
+
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) uint64_t gu64;
+
+// write-through (sc1) stores and L1-bypassing (sc1) loads of handed-off bytes
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store((gu32*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1_u32(uint32_t* p, uint32_t v) {
+  __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1_f2(float* p, float a, float b) {
+  const uint64_t v = (uint64_t)__float_as_uint(a) | ((uint64_t)__float_as_uint(b) << 32);
+  __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __uint_as_float(__hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ uint32_t ld_sc1_u32(const uint32_t* p) {
+  return __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_sc1_u64(const float* p) {
+  return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Hand-off among the k workgroups of a graph.  Every wave drains its (sc1)
+// stores, then one lane arrives on the graph's counter and polls it (sc1)
+// until all k siblings have arrived at this hand-off; the counter only grows
+// within a launch (the h-th hand-off completes at h*k), so arrival v waits for
+// (v / k + 1) * k.  Bounded: a wait that gives up sets the timeout flag and
+// goes on (wrong results, reported by the host; never a hung launch).
+__device__ __forceinline__ void sib_handoff(uint32_t* ctr, uint32_t* flag, int k) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t v = __hip_atomic_fetch_add((gu32*)ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t target = (v / (uint32_t)k + 1u) * (uint32_t)k;
+    for (int spin = 0; ld_sc1_u32(ctr) < target; ++spin) {
+      if (spin > (1 << 22)) {
+        __hip_atomic_store((gu32*)flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+}
+
+// After a workgroup's last hand-off wait: the last sibling out resets the
+// graph's counters for the next launch (every sibling has stopped polling).
+__device__ __forceinline__ void sib_exit(uint32_t* ctr, int k) {
+  if (threadIdx.x == 0) {
+    const uint32_t v = __hip_atomic_fetch_add((gu32*)(ctr + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v == (uint32_t)k - 1u) {
+      __hip_atomic_store((gu32*)ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store((gu32*)(ctr + 1), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Rows [r0, r1) of an N x 34 LDS slot -> global rows (stride 32), 8-byte sc1 stores.
+__device__ __forceinline__ void publish_rows(const float* slot, float* g, int r0, int r1) {
+  for (int q = r0 * 16 + (int)threadIdx.x; q < r1 * 16; q += NT) {
+    const int i = q >> 4, c = (q & 15) * 2;
+    st_sc1_f2(g + i * 32 + c, slot[i * LS + c], slot[i * LS + c + 1]);
+  }
+}
+// The other siblings' rows (all of [0, N) but [r0, r1)) of global rows -> LDS slot, 8-byte sc1 loads.
+__device__ __forceinline__ void gather_rows(float* slot, const float* g, int N, int r0, int r1) {
+  const int own = r1 - r0;
+  for (int q = (int)threadIdx.x; q < (N - own) * 16; q += NT) {
+    int i = q >> 4;
+    i = i < r0 ? i : i + own;
+    const int c = (q & 15) * 2;
+    const uint64_t v = ld_sc1_u64(g + i * 32 + c);
+    *reinterpret_cast<float2*>(slot + i * LS + c) = make_float2(__uint_as_float((uint32_t)v), __uint_as_float((uint32_t)(v >> 32)));
+  }
+}
+// ReLU words of the transposed slots [q0, q1) (stored sc1 by other siblings) -> LDS.
+__device__ __forceinline__ void gather_words(uint32_t* dst, const uint32_t* g, int q0, int q1) {
+  for (int q = q0 + (int)threadIdx.x; q < q1; q += NT) dst[q] = ld_sc1_u32(g + q);
+}
+
+// Edge-balanced row bound of sibling r: the first row i with rp[i] + 2i >= r (E + 2N) / k.
+__device__ __forceinline__ int row_bound(const int* rp, int N, int r, int k) {
+  if (r <= 0) return 0;
+  if (r >= k) return N;
+  const int64_t t = ((int64_t)(rp[N] + 2 * N) * r + k - 1) / k;
+  int lo = 0, hi = N;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if ((int64_t)rp[mid] + 2 * mid >= t) hi = mid;
+    else lo = mid + 1;
+  }
+  return lo;
+}
 
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
@@ -201,7 +314,7 @@ template <int FE>
 __device__ __forceinline__ void row_fwd(const int* rp, const uint4* rec, const float* ext, const float* X,
                                         const float* Bs, float* S, float* S1g, float* cntg, float* eapg,
                                         uint32_t* btg, const float* we, const float* be, int KE, int F, int N,
-                                        int N_E) {
+                                        int N_E, int r0, int r1) {
   constexpr int FA = FE > 0 ? FE : 1;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, cp = lane & 15, sl = lane >> 4, c0 = 2 * cp;
   float2 wa[8];
@@ -217,7 +330,7 @@ __device__ __forceinline__ void row_fwd(const int* rp, const uint4* rec, const f
   for (int f = 0; f < FE; ++f) wc[f] = make_float2(we[c0 * KE + 2 * F + f], we[(c0 + 1) * KE + 2 * F + f]);
   const float2 be2 = make_float2(be[c0], be[c0 + 1]);
   const int n32 = 32 * N;
-  for (int i = wave; i < N; i += NW) {
+  for (int i = r0 + wave; i < r1; i += NW) {
     const int eb = rp[i], ee = rp[i + 1];
     float2 a = make_float2(0.f, 0.f);
     {
@@ -263,11 +376,11 @@ __device__ __forceinline__ void row_fwd(const int* rp, const uint4* rec, const f
 #pragma unroll
         for (int f = 0; f < FE; ++f) eap[f] = make_float2(fmaf(af.x, ev[f], eap[f].x), fmaf(af.y, ev[f], eap[f].y));
         const uint64_t blo = __ballot(al), bhi = __ballot(ah);
-#ifndef VG_NO_BT
-        // every lane of the slot stores its edge's word (same address); past the row end: slot E
-        btg[ok ? (int)(r[u].x >> 16) : N_E] =
-            (uint32_t)((blo >> (16 * sl)) & 0xffffu) | ((uint32_t)((bhi >> (16 * sl)) & 0xffffu) << 16);
-#endif
+        // lane 0 of the slot stores its edge's word (write-through: a sibling
+        // workgroup may read it); past the row end: slot E
+        if (cp == 0)
+          st_sc1_u32(btg + (ok ? (int)(r[u].x >> 16) : N_E),
+                     (uint32_t)((blo >> (16 * sl)) & 0xffffu) | ((uint32_t)((bhi >> (16 * sl)) & 0xffffu) << 16));
       }
     }
     acc = f2slot_sum(acc);
@@ -276,12 +389,10 @@ __device__ __forceinline__ void row_fwd(const int* rp, const uint4* rec, const f
     for (int f = 0; f < FE; ++f) eap[f] = f2slot_sum(eap[f]);
     if (sl == 0) {
       *reinterpret_cast<float2*>(S + i * LS + c0) = acc;
-#ifndef VG_NO_CNT
       if (S1g) *reinterpret_cast<float2*>(S1g + i * 32 + c0) = acc;
       *reinterpret_cast<float2*>(cntg + i * 32 + c0) = cnt;
 #pragma unroll
       for (int f = 0; f < FE; ++f) *reinterpret_cast<float2*>(eapg + f * n32 + i * 32 + c0) = eap[f];
-#endif
     }
   }
 }
@@ -291,20 +402,20 @@ __device__ __forceinline__ void row_fwd(const int* rp, const uint4* rec, const f
 // [NW][32 * (1 + FE)].  Thread (slice sl = tid >> 5, channel c) takes rows sl, sl + 32, ...
 template <int FE>
 __device__ __forceinline__ void d_pass(const float* dS, float* D, const float* cntg, const float* eapg, float* red,
-                                       int N) {
+                                       int N, int r0, int r1) {
   constexpr int FA = FE > 0 ? FE : 1;
   const int tid = threadIdx.x, c = tid & 31, sl = tid >> 5, wave = tid >> 6;
   const int n32 = 32 * N;
   float pbe = 0.f, pwc[FA];
 #pragma unroll
   for (int f = 0; f < FA; ++f) pwc[f] = 0.f;
-  for (int i0 = sl; i0 < N; i0 += 128) {  // 4 rows per step, their loads issued together
+  for (int i0 = r0 + sl; i0 < r1; i0 += 128) {  // 4 rows per step, their loads issued together
     float cn[4], ep[4][FA];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int i = i0 + 32 * q;
-      const bool ok = i < N;
-      const int ii = ok ? i : 0;
+      const bool ok = i < r1;
+      const int ii = ok ? i : r0;
       cn[q] = cntg[ii * 32 + c];
 #pragma unroll
       for (int f = 0; f < FE; ++f) ep[q][f] = eapg[f * n32 + ii * 32 + c];
@@ -312,7 +423,7 @@ __device__ __forceinline__ void d_pass(const float* dS, float* D, const float* c
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int i = i0 + 32 * q;
-      if (i < N) {  // (cn / ep of rows >= N are never used)
+      if (i < r1) {  // (cn / ep of rows >= r1 are never used)
         const float ds = dS[i * LS + c];
         const float d = cn[q] != 0.f ? ds * cn[q] : 0.f;
         D[i * LS + c] = d;
@@ -353,9 +464,9 @@ __device__ __forceinline__ void d_pass_sum(const float* red, float* gw, int KE, 
 // Transposed pass: D'_j = sum over in-edges (i -> j) active in channel c of dS_i
 // (lane layout of row_fwd: channel pair x edge slot).
 __device__ __forceinline__ void row_t(const int* trp, const uint16_t* tcol, const uint32_t* bt, const float* dS,
-                                      float* Dp, int N) {
+                                      float* Dp, int r0, int r1) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, cp = lane & 15, sl = lane >> 4, c0 = 2 * cp;
-  for (int j = wave; j < N; j += NW) {
+  for (int j = r0 + wave; j < r1; j += NW) {
     const int qb = trp[j], qe = trp[j + 1];
     float2 acc = make_float2(0.f, 0.f);
     for (int q0 = qb; q0 < qe; q0 += 16) {
@@ -381,11 +492,11 @@ __device__ __forceinline__ void row_t(const int* trp, const uint16_t* tcol, cons
 }
 
 #ifdef DR_STAMPS
-#define VSTAMP(i)                                                                                 \
-  do {                                                                                            \
-    __builtin_amdgcn_sched_barrier(0);                                                            \
-    if (tid == 0 && a.p.stamps) a.p.stamps[(int64_t)b * 32 + (i)] = __builtin_amdgcn_s_memtime(); \
-    __builtin_amdgcn_sched_barrier(0);                                                            \
+#define VSTAMP(i)                                                                                           \
+  do {                                                                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                                                      \
+    if (tid == 0 && rk == 0 && a.p.stamps) a.p.stamps[(int64_t)b * 32 + (i)] = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0);                                                                      \
   } while (0)
 #else
 #define VSTAMP(i) \
@@ -397,7 +508,11 @@ template <int FE>
 __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int b = blockIdx.x;
+  // block -> (graph slot b, sibling rk): siblings 8 blocks apart, 8 graphs per 8k blocks
+  const int k = a.k;
+  const int bx = blockIdx.x, hi = bx >> 3;
+  const int rk = hi % k, b = (hi / k) * 8 + (bx & 7);
+  if (b >= a.B) return;
   const dr_graph_store& s = a.s;
   const dr_vanilla_weights& w = a.w;
   const dr_pass& p = a.p;
@@ -434,9 +549,16 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   float* eap2 = eap1 + Fe * n32;
   uint32_t* bt1g = reinterpret_cast<uint32_t*>(eap2 + Fe * n32);
   uint32_t* bt2g = bt1g + r4(E + 1);
+  float* XA = reinterpret_cast<float*>(bt2g + r4(E + 1));  // B2, then dS1 rows (split)
+  float* XB = XA + n32;                                    // dS2 rows (split)
+  float* csum = XB + n32;                                  // [k][32] column sums of X2 (split)
+  uint32_t* ctr = a.sync + 2 * b;
+  uint32_t* tflag = a.sync + 2 * a.B;
+  const bool split = k > 1;
   const int LG = 32 * KE + 32 + F * KN + F;  // one layer's gradient entries in the slab
-  float* slab = p.slab ? p.slab + (int64_t)b * DR_VANILLA_SLAB_STRIDE(F, Fe) : nullptr;
+  float* slab = p.slab ? p.slab + ((int64_t)b * k + rk) * DR_VANILLA_SLAB_STRIDE(F, Fe) : nullptr;
   const bool bwd = (p.flags & DR_PASS_BACKWARD) != 0;
+  const bool lead = rk == 0;  // writes the graph's outputs, loss and head vectors
 
   VSTAMP(0);
   // ---------------- stage: CSR rows, edge records, X0 into LDS ------------
@@ -481,64 +603,73 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
     *reinterpret_cast<float2*>(P + i * LS + c4 + 2) = make_float2(v.z, v.w);
   }
   const float y_g = s.y[g];
-  if (p.step_counter && b == 0 && tid == 0) p.step_counter[1] = p.step_counter[0];
+  if (p.step_counter && b == 0 && lead && tid == 0) p.step_counter[1] = p.step_counter[0];
   wait_vm();
   __syncthreads();
+  // this workgroup's rows (the transposed passes take the same range of target rows)
+  const int r0 = row_bound(srp, N, rk, k), r1 = row_bound(srp, N, rk + 1, k), nown = r1 - r0;
 
   VSTAMP(1);
-  // ---------------- layer 1: B1 = X0 Wb1^T -> Q ----------------------------
+  // ---------------- layer 1: B1 = X0 Wb1^T -> Q (every row: the row pass gathers any) --
   mm_w<1>(N, [&](int i, int k) { return P[i * LS + k]; },
           [&](int k, int n) -> const float* { return k < F ? w.we1 + n * KE + F + k : nullptr; }, [&](int) -> const float* { return nullptr; },
           [&](int i, int n, float v, float) { Q[i * LS + n] = v; });
   __syncthreads();
   VSTAMP(2);
-  row_fwd<FE>(srp, rec, ext, P, Q, R, S1g, cnt1, eap1, bt1g, w.we1, w.be1, KE, F, N, E);
+  row_fwd<FE>(srp, rec, ext, P, Q, R, S1g, cnt1, eap1, bt1g, w.we1, w.be1, KE, F, N, E, r0, r1);
   __syncthreads();
   VSTAMP(3);
-  // X1 = relu([X0 | S1] Wn1^T + bn1) -> Q (pad columns 0)
-  mm_w<2>(N, [&](int i, int k) { return k < 32 ? P[i * LS + k] : R[i * LS + k - 32]; },
+  // X1 = relu([X0 | S1] Wn1^T + bn1) -> Q (pad columns 0), own rows
+  mm_w<2>(nown, [&](int i, int k) { return k < 32 ? P[(r0 + i) * LS + k] : R[(r0 + i) * LS + k - 32]; },
           [&](int k, int n) -> const float* {
             return n < F ? (k < F ? w.wn1 + n * KN + k : (k < 32 ? nullptr : w.wn1 + n * KN + F + k - 32)) : nullptr;
           },
           [&](int n) -> const float* { return n < F ? w.bn1 + n : nullptr; },
-          [&](int i, int n, float v, float bias) { Q[i * LS + n] = n < F ? relu_keepnan(v + bias) : 0.f; });
+          [&](int i, int n, float v, float bias) { Q[(r0 + i) * LS + n] = n < F ? relu_keepnan(v + bias) : 0.f; });
   __syncthreads();
   VSTAMP(4);
-  // ---------------- layer 2: B2 = X1 Wb2^T -> P ----------------------------
-  mm_w<1>(N, [&](int i, int k) { return Q[i * LS + k]; },
+  // ---------------- layer 2: B2 = X1 Wb2^T -> P, own rows ---------------------
+  mm_w<1>(nown, [&](int i, int k) { return Q[(r0 + i) * LS + k]; },
           [&](int k, int n) -> const float* { return k < F ? w.we2 + n * KE + F + k : nullptr; }, [&](int) -> const float* { return nullptr; },
-          [&](int i, int n, float v, float) { P[i * LS + n] = v; });
+          [&](int i, int n, float v, float) { P[(r0 + i) * LS + n] = v; });
   __syncthreads();
+  if (split) {  // hand-off 1: every sibling's B2 rows (and the layer-1 ReLU words)
+    publish_rows(P, XA, r0, r1);
+    sib_handoff(ctr, tflag, k);
+    gather_rows(P, XA, N, r0, r1);
+    __syncthreads();
+  }
   VSTAMP(5);
-  row_fwd<FE>(srp, rec, ext, Q, P, R, nullptr, cnt2, eap2, bt2g, w.we2, w.be2, KE, F, N, E);
+  row_fwd<FE>(srp, rec, ext, Q, P, R, nullptr, cnt2, eap2, bt2g, w.we2, w.be2, KE, F, N, E, r0, r1);
   wait_vm();  // ReLU words, cnt, eap of both layers stored before anyone reads them back
   __syncthreads();
   VSTAMP(6);
   // the records are dead: the backward's transposed CSR and layer-2 ReLU words
   // land in U while the forward finishes
   if (bwd) {
-    dma_words<NT>(bt, bt2g, E);
+    if (!split) dma_words<NT>(bt, bt2g, E);  // (split: after hand-off 2, sc1)
     dma_words<NT>(strp, s.t_rowptr + d.node0 + g, N + 1);
     dma_x4<NT>(stcol, s.t_col + d.col0, (E + 7) / 8);
   }
-  // X2 = relu([X1 | S2] Wn2^T + bn2) -> P
-  mm_w<2>(N, [&](int i, int k) { return k < 32 ? Q[i * LS + k] : R[i * LS + k - 32]; },
+  // X2 = relu([X1 | S2] Wn2^T + bn2) -> P, own rows
+  mm_w<2>(nown, [&](int i, int k) { return k < 32 ? Q[(r0 + i) * LS + k] : R[(r0 + i) * LS + k - 32]; },
           [&](int k, int n) -> const float* {
             return n < F ? (k < F ? w.wn2 + n * KN + k : (k < 32 ? nullptr : w.wn2 + n * KN + F + k - 32)) : nullptr;
           },
           [&](int n) -> const float* { return n < F ? w.bn2 + n : nullptr; },
-          [&](int i, int n, float v, float bias) { P[i * LS + n] = n < F ? relu_keepnan(v + bias) : 0.f; });
+          [&](int i, int n, float v, float bias) { P[(r0 + i) * LS + n] = n < F ? relu_keepnan(v + bias) : 0.f; });
   __syncthreads();
   VSTAMP(7);
   // per-graph mean (scatter_mean, vanilla_gnn.py:62): 32 row slices per column
-  // (partials in T), combined in order; relu'(X2) as one bit word per node
+  // (partials in T), combined in order (split: then the siblings' sums, in
+  // sibling order); relu'(X2) as one bit word per node
   {
     const int n = tid & 31, sl = tid >> 5;
     float acc = 0.f;
-    const int i0 = (N * sl) >> 5, i1 = (N * (sl + 1)) >> 5;
+    const int i0 = r0 + ((nown * sl) >> 5), i1 = r0 + ((nown * (sl + 1)) >> 5);
     for (int i = i0; i < i1; ++i) acc += P[i * LS + n];
     T[sl * 32 + n] = acc;
-    for (int i = wave * 2 + (lane >> 5); i < N; i += 2 * NW) {
+    for (int i = r0 + wave * 2 + (lane >> 5); i < r1; i += 2 * NW) {
       const int c = lane & 31;
       const uint64_t m = __ballot(c < F && !(P[i * LS + c] <= 0.f));
       if (c == 0) xb[i] = (lane >> 5) ? (uint32_t)(m >> 32) : (uint32_t)m;
@@ -548,11 +679,23 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   if (tid < 32) {
     float t = 0.f;
     for (int sl = 0; sl < 32; ++sl) t += T[sl * 32 + tid];
-    sg[tid] = tid < F ? t / (float)N : 0.f;
+    if (split) st_sc1(csum + rk * 32 + tid, t);
+    else sg[tid] = tid < F ? t / (float)N : 0.f;
+  }
+  if (split) {  // hand-off 2: the siblings' column sums (and the layer-2 ReLU words)
+    sib_handoff(ctr, tflag, k);
+    if (tid < 32) {
+      float t = ld_sc1(csum + tid);
+      for (int q = 1; q < k; ++q) t += ld_sc1(csum + q * 32 + tid);
+      sg[tid] = tid < F ? t / (float)N : 0.f;
+    }
+    if (bwd) gather_words(bt, bt2g, strp[r0], strp[r1]);  // (strp landed: waited at the hand-off)
+    if (!bwd) sib_exit(ctr, k);
   }
   __syncthreads();
   VSTAMP(8);
   // ---------------- graph MLP, loss, head backward (vanilla_gnn.py:63-64, trainer.py:686-689)
+  // (every sibling runs it on the same inputs; the lead writes the outputs)
   // fc1: 8 lanes per output (4 inputs each), reduced by shuffles
   {
     const int o = tid >> 3, part = tid & 7;
@@ -575,12 +718,12 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
     if (lane == 0) sdout[q] = v + w.g2b[q];
   }
   __syncthreads();
-  if ((p.flags & DR_PASS_FORWARD) && tid < OUT) p.out[(int64_t)b * OUT + tid] = sdout[tid];
+  if ((p.flags & DR_PASS_FORWARD) && lead && tid < OUT) p.out[(int64_t)b * OUT + tid] = sdout[tid];
   if (!bwd) return;
   if (tid == 0) {
     if (p.loss_kind == DR_LOSS_MSE) {
       const float dl = sdout[0] - y_g;
-      if (p.loss_per_graph) p.loss_per_graph[b] = dl * dl;
+      if (p.loss_per_graph && lead) p.loss_per_graph[b] = dl * dl;
       sdout[0] = 2.f * dl * p.loss_scale;
     } else if (p.loss_kind == DR_LOSS_CE) {
       const int yi = (int)y_g;
@@ -590,7 +733,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
       for (int q = 0; q < OUT; ++q) se += expf(sdout[q] - mx);
       const float lse = mx + logf(se);
       const float wy = p.class_w ? p.class_w[yi] : 1.f;
-      if (p.loss_per_graph) p.loss_per_graph[b] = wy * (lse - sdout[yi]);
+      if (p.loss_per_graph && lead) p.loss_per_graph[b] = wy * (lse - sdout[yi]);
       for (int q = 0; q < OUT; ++q) sdout[q] = wy * (expf(sdout[q] - lse) - (q == yi ? 1.f : 0.f)) * p.loss_scale;
     } else {
       for (int q = 0; q < OUT; ++q) sdout[q] = p.dout[(int64_t)b * OUT + q];
@@ -625,58 +768,68 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
       for (int part = 0; part < 32; ++part) acc += T[part * 32 + tid];
       const float dm = acc / (float)N;  // scatter_mean backward: grad / count
       sdm[tid] = tid < F ? dm : 0.f;
-      if (tid < F) hg[HD + tid] = dm;
+      if (tid < F && lead) hg[HD + tid] = dm;
     }
-    if (tid < XSH) hg[tid] = tid < F ? sg[tid] : 0.f;
-    if (tid < 128) {
-      hg[XSH + tid] = sh[tid];
-      hg[XSH + 128 + tid] = sdh[tid];
+    if (lead) {
+      if (tid < XSH) hg[tid] = tid < F ? sg[tid] : 0.f;
+      if (tid < 128) {
+        hg[XSH + tid] = sh[tid];
+        hg[XSH + 128 + tid] = sdh[tid];
+      }
+      if (tid < OUT) hg[XSH + 256 + tid] = sdout[tid];
     }
-    if (tid < OUT) hg[XSH + 256 + tid] = sdout[tid];
   }
   __syncthreads();
   VSTAMP(9);
 
-  // ---------------- layer 2 backward ---------------------------------------
+  // ---------------- layer 2 backward (own rows; weight gradients = this workgroup's partials)
   // DU2 = relu'(X2) * dmean (bit words).  dWn2 = DU2^T [X1 | S2], dbn2 = sum DU2
   // (a column of ones); dS2 = DU2 Wn2[:, F:] -> P.
   {
     float* gw = slab + LG;  // layer 2
-    mm16(F, KN + 1, N, 0, [&](int n, int i) { return (i < N && ((xb[i] >> n) & 1u)) ? 1.f : 0.f; },
-         [&](int i, int q) { return i < N ? (q < F ? Q[i * LS + q] : (q < KN ? R[i * LS + q - F] : 1.f)) : 0.f; },
+    mm16(F, KN + 1, nown, 0, [&](int n, int i) { return (i < nown && ((xb[r0 + i] >> n) & 1u)) ? 1.f : 0.f; },
+         [&](int i, int q) {
+           return i < nown ? (q < F ? Q[(r0 + i) * LS + q] : (q < KN ? R[(r0 + i) * LS + q - F] : 1.f)) : 0.f;
+         },
          [&](int n, int q, float v) {
            if (q < KN) gw[32 * KE + 32 + n * KN + q] = sdm[n] * v;
            else gw[32 * KE + 32 + F * KN + n] = sdm[n] * v;
          });
-    mm_w<1>(N, [&](int i, int n) { return ((xb[i] >> n) & 1u) ? sdm[n] : 0.f; },
+    mm_w<1>(nown, [&](int i, int n) { return ((xb[r0 + i] >> n) & 1u) ? sdm[n] : 0.f; },
             [&](int n, int c) -> const float* { return n < F ? w.wn2 + n * KN + F + c : nullptr; }, [&](int) -> const float* { return nullptr; },
-            [&](int i, int c, float v, float) { P[i * LS + c] = v; });
+            [&](int i, int c, float v, float) { P[(r0 + i) * LS + c] = v; });
   }
   __syncthreads();
+  if (split) {  // hand-off 3: every sibling's dS2 rows (the transposed pass gathers them by source)
+    publish_rows(P, XB, r0, r1);
+    sib_handoff(ctr, tflag, k);
+    gather_rows(P, XB, N, r0, r1);
+  }
   VSTAMP(10);
   // D2 = dS2 * cnt2 -> R (S2 is dead), dbe2 / dWc2 partials in T
-  d_pass<FE>(P, R, cnt2, eap2, T, N);
+  d_pass<FE>(P, R, cnt2, eap2, T, N, r0, r1);
   wait_vm();  // bt2 and the transposed CSR have landed in U
   __syncthreads();
   d_pass_sum<FE>(T, slab + LG, KE, F);
   __syncthreads();
   VSTAMP(11);
-  row_t(strp, stcol, bt, P, T, N);  // D'2 -> T
+  row_t(strp, stcol, bt, P, T, r0, r1);  // D'2 -> T
   __syncthreads();
   VSTAMP(12);
   {
     float* gw = slab + LG;
     // dWa2 = D2^T X1,  dWb2 = D'2^T X1
-    mm16(32, F, N, 0, [&](int c, int i) { return i < N ? R[i * LS + c] : 0.f; },
-         [&](int i, int k) { return i < N && k < F ? Q[i * LS + k] : 0.f; },
+    mm16(32, F, nown, 0, [&](int c, int i) { return i < nown ? R[(r0 + i) * LS + c] : 0.f; },
+         [&](int i, int k) { return i < nown && k < F ? Q[(r0 + i) * LS + k] : 0.f; },
          [&](int c, int k, float v) { gw[c * KE + k] = v; });
-    mm16(32, F, N, 4, [&](int c, int i) { return i < N ? T[i * LS + c] : 0.f; },
-         [&](int i, int k) { return i < N && k < F ? Q[i * LS + k] : 0.f; },
+    mm16(32, F, nown, 4, [&](int c, int i) { return i < nown ? T[(r0 + i) * LS + c] : 0.f; },
+         [&](int i, int k) { return i < nown && k < F ? Q[(r0 + i) * LS + k] : 0.f; },
          [&](int c, int k, float v) { gw[c * KE + F + k] = v; });
     // dX1 = [DU2 | D2 | D'2] [Wn2[:, :F]; Wa2; Wb2], DU1 = relu'(X1) * dX1 -> P
-    mm_w<3>(N,
+    mm_w<3>(nown,
             [&](int i, int k) {
-              return k < 32 ? (((xb[i] >> k) & 1u) ? sdm[k] : 0.f) : (k < 64 ? R[i * LS + k - 32] : T[i * LS + k - 64]);
+              const int ii = r0 + i;
+              return k < 32 ? (((xb[ii] >> k) & 1u) ? sdm[k] : 0.f) : (k < 64 ? R[ii * LS + k - 32] : T[ii * LS + k - 64]);
             },
             [&](int k, int n) -> const float* {
               return n < F ? (k < 32 ? (k < F ? w.wn2 + k * KN + n : nullptr)
@@ -684,27 +837,37 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
                            : nullptr;
             },
             [&](int) -> const float* { return nullptr; },
-            [&](int i, int n, float v, float) { P[i * LS + n] = n < F ? relu_bwd(Q[i * LS + n], v) : 0.f; });
+            [&](int i, int n, float v, float) { P[(r0 + i) * LS + n] = n < F ? relu_bwd(Q[(r0 + i) * LS + n], v) : 0.f; });
   }
   __syncthreads();
   VSTAMP(13);
   // ---------------- layer 1 backward ---------------------------------------
   // X0 (HBM row stride XS) -> Q, S1 -> R (stride 32), layer-1 ReLU words -> U:
-  // bulk DMA, landing while dS1 = DU1 Wn1[:, F:] -> T runs
-  dma_x4<NT>(Q, X0, N * XS / 4);
-  dma_x4<NT>(R, S1g, N * 8);
-  dma_words<NT>(bt, bt1g, E);
-  mm_w<1>(N, [&](int i, int n) { return P[i * LS + n]; },
+  // bulk DMA (own rows), landing while dS1 = DU1 Wn1[:, F:] -> T runs
+  dma_x4<NT>(Q + r0 * XS, X0 + (int64_t)r0 * XS, nown * XS / 4);
+  dma_x4<NT>(R + r0 * 32, S1g + r0 * 32, nown * 8);
+  if (split) gather_words(bt, bt1g, strp[r0], strp[r1]);
+  else dma_words<NT>(bt, bt1g, E);
+  mm_w<1>(nown, [&](int i, int n) { return P[(r0 + i) * LS + n]; },
           [&](int n, int c) -> const float* { return n < F ? w.wn1 + n * KN + F + c : nullptr; }, [&](int) -> const float* { return nullptr; },
-          [&](int i, int c, float v, float) { T[i * LS + c] = v; });
+          [&](int i, int c, float v, float) { T[(r0 + i) * LS + c] = v; });
   wait_vm();
   __syncthreads();
+  if (split) {  // hand-off 4: every sibling's dS1 rows
+    publish_rows(T, XA, r0, r1);
+    sib_handoff(ctr, tflag, k);
+    sib_exit(ctr, k);
+    gather_rows(T, XA, N, r0, r1);
+  }
   VSTAMP(14);
   {
     float* gw = slab;  // layer 1
     // dWn1 = DU1^T [X0 | S1], dbn1 = sum DU1
-    mm16(F, KN + 1, N, 0, [&](int n, int i) { return i < N ? P[i * LS + n] : 0.f; },
-         [&](int i, int q) { return i < N ? (q < F ? Q[i * XS + q] : (q < KN ? R[i * 32 + q - F] : 1.f)) : 0.f; },
+    mm16(F, KN + 1, nown, 0, [&](int n, int i) { return i < nown ? P[(r0 + i) * LS + n] : 0.f; },
+         [&](int i, int q) {
+           const int ii = r0 + i;
+           return i < nown ? (q < F ? Q[ii * XS + q] : (q < KN ? R[ii * 32 + q - F] : 1.f)) : 0.f;
+         },
          [&](int n, int q, float v) {
            if (q < KN) gw[32 * KE + 32 + n * KN + q] = v;
            else gw[32 * KE + 32 + F * KN + n] = v;
@@ -713,22 +876,22 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   __syncthreads();
   VSTAMP(15);
   // D1 = dS1 * cnt1 -> R (S1 is dead), partials in P (DU1 is dead)
-  d_pass<FE>(T, R, cnt1, eap1, P, N);
+  d_pass<FE>(T, R, cnt1, eap1, P, N, r0, r1);
   __syncthreads();
   d_pass_sum<FE>(P, slab, KE, F);
   __syncthreads();
   VSTAMP(16);
-  row_t(strp, stcol, bt, T, P, N);  // D'1 -> P
+  row_t(strp, stcol, bt, T, P, r0, r1);  // D'1 -> P
   __syncthreads();
   VSTAMP(17);
   {
     float* gw = slab;
     // dWa1 = D1^T X0,  dWb1 = D'1^T X0
-    mm16(32, F, N, 0, [&](int c, int i) { return i < N ? R[i * LS + c] : 0.f; },
-         [&](int i, int k) { return i < N && k < F ? Q[i * XS + k] : 0.f; },
+    mm16(32, F, nown, 0, [&](int c, int i) { return i < nown ? R[(r0 + i) * LS + c] : 0.f; },
+         [&](int i, int k) { return i < nown && k < F ? Q[(r0 + i) * XS + k] : 0.f; },
          [&](int c, int k, float v) { gw[c * KE + k] = v; });
-    mm16(32, F, N, 4, [&](int c, int i) { return i < N ? P[i * LS + c] : 0.f; },
-         [&](int i, int k) { return i < N && k < F ? Q[i * XS + k] : 0.f; },
+    mm16(32, F, nown, 4, [&](int c, int i) { return i < nown ? P[(r0 + i) * LS + c] : 0.f; },
+         [&](int i, int k) { return i < nown && k < F ? Q[(r0 + i) * XS + k] : 0.f; },
          [&](int c, int k, float v) { gw[c * KE + F + k] = v; });
   }
   VSTAMP(18);
@@ -746,8 +909,10 @@ extern "C" int64_t dr_vanilla_fused_scratch_floats(int32_t n_nodes, int32_t n_ed
 
 extern "C" int dr_vanilla_fused_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
                                      const dr_vanilla_weights* w, const dr_pass* pass, float* scratch,
-                                     const int64_t* scratch_off, int32_t lds_bytes, void* stream) {
+                                     const int64_t* scratch_off, int32_t split, uint32_t* sync, int32_t lds_bytes,
+                                     void* stream) {
   if (!store || !descs || !w || !pass || n_batch < 0) return DR_E_ARG;
+  if (split < 1 || split > MAXK || (split > 1 && !sync)) return DR_E_ARG;
   if (pass->out_dim < 1 || pass->out_dim > DR_MAX_OUT) return DR_E_UNSUPPORTED;
   if (store->n_feat < 1 || store->n_feat > 32 || store->x_stride > 32 || store->n_edge_feat < 0 ||
       store->n_edge_feat > MAXFE)
@@ -776,13 +941,17 @@ extern "C" int dr_vanilla_fused_pass(const dr_graph_store* store, const dr_graph
   a.descs = descs;
   a.scr = scratch;
   a.scr_off = scratch_off;
+  a.sync = sync;
   a.B = n_batch;
+  a.k = split;
+  // graph b's siblings are blocks 8 apart (see the kernel); grid padded to 8 graphs
+  const dim3 grid((unsigned)(((n_batch + 7) / 8) * 8 * split));
   switch (store->n_edge_feat) {
-    case 0: hipLaunchKernelGGL(vanilla_graph_kernel<0>, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, a); break;
-    case 1: hipLaunchKernelGGL(vanilla_graph_kernel<1>, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, a); break;
-    case 2: hipLaunchKernelGGL(vanilla_graph_kernel<2>, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, a); break;
-    case 3: hipLaunchKernelGGL(vanilla_graph_kernel<3>, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, a); break;
-    default: hipLaunchKernelGGL(vanilla_graph_kernel<4>, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, a); break;
+    case 0: hipLaunchKernelGGL(vanilla_graph_kernel<0>, grid, dim3(NT), lds_bytes, (hipStream_t)stream, a); break;
+    case 1: hipLaunchKernelGGL(vanilla_graph_kernel<1>, grid, dim3(NT), lds_bytes, (hipStream_t)stream, a); break;
+    case 2: hipLaunchKernelGGL(vanilla_graph_kernel<2>, grid, dim3(NT), lds_bytes, (hipStream_t)stream, a); break;
+    case 3: hipLaunchKernelGGL(vanilla_graph_kernel<3>, grid, dim3(NT), lds_bytes, (hipStream_t)stream, a); break;
+    default: hipLaunchKernelGGL(vanilla_graph_kernel<4>, grid, dim3(NT), lds_bytes, (hipStream_t)stream, a); break;
   }
   return (int)hipGetLastError();
 }

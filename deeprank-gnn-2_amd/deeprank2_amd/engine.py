@@ -31,7 +31,7 @@ from __future__ import annotations
 import torch
 
 from deeprank2_amd import _lib, layered
-from deeprank2_amd.fused import BatchHandle, launch, launch_step, param_table, step_fits
+from deeprank2_amd.fused import BatchHandle, launch, launch_step, param_table, slab_rows_for, step_fits
 
 
 class FusedTrainStep:
@@ -198,6 +198,7 @@ class FusedTrainStep:
             ev.append((e0, e1))
         self.step_count += 1
         slab, head, lpg, lout = self.slab.data_ptr(), self.head.data_ptr(), self.lpg.data_ptr(), self.loss_out.data_ptr()
+        self._table.slab_rows = slab_rows_for(self.spec, h)
         if self.pg is None:
             _lib.check(lib.dr_reduce_update(self._table, slab, head, h.B, self._adam, lpg, scale, lout, stream), "dr_reduce_update")
         else:

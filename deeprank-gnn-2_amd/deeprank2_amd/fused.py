@@ -42,6 +42,7 @@ class BatchHandle:
         self.large_onepass = False  # split path in ONE launch: each graph's last-arriving tile runs its tail (dr_large_plan.arrive)
         self.force_layers = False  # run the layer-level path (layered.py) even when the graph pass fits (diagnostic)
         self.vanilla_words = True  # Vanilla pipeline: forward ReLU words feed the backward (False: recomputed)
+        self.vanilla_split = None  # Vanilla per-graph kernel: workgroups per graph (None: by batch size)
 
     def lds(self, key, fn):
         """Dynamic LDS bytes for the largest graph of the batch (cached per model kind)."""
@@ -91,7 +92,8 @@ class BatchHandle:
     def vanilla_fused_scratch(self):
         """Per-graph global scratch of dr_vanilla_fused_pass (S1, per-(node,
         channel) active-edge counts and edge-attribute sums of both layers, the
-        transposed edge ReLU words) and each slot's float offset into it."""
+        transposed edge ReLU words, the split's exchange rows), each slot's
+        float offset into it, and the split's arrival counters."""
         sc = self._lds.get("vanilla_fused_scratch")
         if sc is None:
             idx = self.gids_host.astype(np.int64)
@@ -101,7 +103,8 @@ class BatchHandle:
             dev = self.store.device
             buf = torch.empty(max(1, int(off[-1])), dtype=torch.float32, device=dev)
             offs = torch.from_numpy(off[:-1].copy()).to(dev)
-            sc = (buf, offs)
+            sync = torch.zeros(2 * self.B + 1, dtype=torch.int32, device=dev)  # arrival counters, left zero by every launch
+            sc = (buf, offs, sync)
             self._lds["vanilla_fused_scratch"] = sc
         return sc
 
@@ -255,6 +258,8 @@ class FusedSpec:
     weights: Callable  # params -> ctypes weights struct
     lds: Callable  # (n, e, k0, p1, k1, F, alias, out) -> bytes
     dropout: float = 0.0
+    slab_rows: int = 1  # most slab rows a graph's pass writes (slab_stride(F) covers them all)
+    slab_k: Callable | None = None  # handle -> slab rows per graph of that batch's pass (default 1)
     large: Callable | None = None  # (handle, weights struct, pass struct) for graphs beyond one workgroup's LDS
     run: Callable | None = None  # (handle, weights struct, pass struct): replaces the default entry call
     layers: Callable | None = None  # (model, batch tensors, training) -> out: layer-level path (layered.py) for batches beyond LDS
@@ -266,9 +271,10 @@ class FusedSpec:
 def vanilla_fused_scratch_floats(n, e, fe):
     """Mirror of dr_vanilla_fused_scratch_floats (vanilla_graph.hip), vectorised
     over graphs: S1, cnt1, cnt2 (32N each), eap1, eap2 (32N*Fe each), two ReLU
-    word arrays (E + 1 each), every part rounded up to 16 bytes."""
+    word arrays (E + 1 each), the split's exchange rows XA, XB (32N each) and
+    column sums (4 x 32), every part rounded up to 16 bytes."""
     r4 = lambda v: (np.asarray(v, dtype=np.int64) + 3) & ~3  # noqa: E731
-    return (3 + 2 * fe) * r4(32 * np.asarray(n, dtype=np.int64)) + 2 * r4(np.asarray(e, dtype=np.int64) + 1)
+    return (5 + 2 * fe) * r4(32 * np.asarray(n, dtype=np.int64)) + 2 * r4(np.asarray(e, dtype=np.int64) + 1) + 32 * 4
 
 
 def make_pass(out_dim, flags, *, dropout: Dropout | None = None, dout=None, loss_kind=_lib.DR_LOSS_NONE, loss_scale=1.0, class_w=None, out=None, loss_per_graph=None, slab=None, head=None, stamps=None, step_counter=None):
@@ -373,9 +379,15 @@ def param_table(spec: FusedSpec, params, grads, states, n_feat, out_dim):
         kind, off1, off2, cols = recipe[i]
         t.recipe[i].kind, t.recipe[i].off1, t.recipe[i].off2, t.recipe[i].cols = kind, off1, off2, cols
     t.n_params = len(params)
-    t.slab_stride = spec.slab_stride(n_feat)
+    t.slab_stride = spec.slab_stride(n_feat) // spec.slab_rows  # floats per slab row
     t.head_stride = spec.head_stride(out_dim)
+    t.slab_rows = 1  # set per batch (slab_rows_for) before each reduce
     return t
+
+
+def slab_rows_for(spec: FusedSpec, h: BatchHandle) -> int:
+    """Slab rows per graph the model's pass writes for this batch."""
+    return 1 if spec.slab_k is None else int(spec.slab_k(h))
 
 
 def reduce_update(table, B, slab, head, device, adam=None, loss_per_graph=None, loss_scale=1.0, loss_out=None):
@@ -406,5 +418,7 @@ class FusedFn(torch.autograd.Function):
         head = torch.zeros(h.B * spec.head_stride(out_dim), dtype=torch.float32, device=dev)
         run_pass(spec, h, params, make_pass(out_dim, _lib.DR_PASS_BACKWARD, dropout=ctx.dropout, dout=dout.contiguous(), slab=slab, head=head))
         grads = [torch.empty_like(p) for p in params]
-        reduce_update(param_table(spec, params, grads, None, f, out_dim), h.B, slab, head, dev)
+        t = param_table(spec, params, grads, None, f, out_dim)
+        t.slab_rows = slab_rows_for(spec, h)
+        reduce_update(t, h.B, slab, head, dev)
         return (None, None, None, None, *grads)

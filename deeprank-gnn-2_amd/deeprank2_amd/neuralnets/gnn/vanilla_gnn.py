@@ -99,7 +99,7 @@ def make_spec(f, fe):
     xs = _r4(f)
 
     def slab_stride(_f):
-        return 2 * layer
+        return MAX_SPLIT * 2 * layer  # room for one partial row per workgroup of a split graph
 
     def head_stride(out):
         return 2 * xs + 256 + _r4(out)  # g | h | dh | dout | d mean
@@ -123,19 +123,32 @@ def make_spec(f, fe):
             msg = f"batch has F={st.n_feat}, Fe={st.n_edge_feat}; the model expects F={f}, Fe={fe}"
             raise ValueError(msg)
         lib = _lib.load()
-        if fused_fits(h, f, fe):  # one workgroup per graph, graph in LDS
-            buf, offs = h.vanilla_fused_scratch()
+        if fused_fits(h, f, fe):  # split_k(h) workgroups per graph, graph in LDS
+            buf, offs, sync = h.vanilla_fused_scratch()
             lds = h.lds(("vanilla_fused", fe), lambda n, e, *_: lib.dr_vanilla_fused_lds_bytes(n, e, fe))
-            _lib.check(lib.dr_vanilla_fused_pass(st.cstruct(), h.descs.data_ptr(), h.B, w, p, buf.data_ptr(), offs.data_ptr(), lds, _lib.stream_ptr(st.device)), "dr_vanilla_fused_pass")
+            _lib.check(lib.dr_vanilla_fused_pass(st.cstruct(), h.descs.data_ptr(), h.B, w, p, buf.data_ptr(), offs.data_ptr(), split_k(h, f, fe), sync.data_ptr(), lds, _lib.stream_ptr(st.device)), "dr_vanilla_fused_pass")
             return
         sc, _keep = h.vanilla_scratch(f, fe)
         lds = int(lib.dr_vanilla_lds_bytes(f, fe, p.out_dim))
         _lib.check(lib.dr_vanilla_graph_pass(st.cstruct(), h.descs.data_ptr(), h.B, w, p, sc, lds, _lib.stream_ptr(st.device)), "dr_vanilla_graph_pass")
 
-    return FusedSpec(PARAM_NAMES, recipe, slab_stride, head_stride, "dr_vanilla_graph_pass", weights, lambda *_: 0, dropout=0.0, run=run)
+    return FusedSpec(PARAM_NAMES, recipe, slab_stride, head_stride, "dr_vanilla_graph_pass", weights, lambda *_: 0, dropout=0.0, run=run, slab_rows=MAX_SPLIT, slab_k=lambda h: split_k(h, f, fe))
 
 
 FUSED_MAX_FE = 4  # vanilla_graph.hip MAXFE
+MAX_SPLIT = 4  # DR_VANILLA_MAX_SPLIT
+CUS = 256  # MI355X compute units: one 1024-thread workgroup per CU
+
+
+def split_k(h: BatchHandle, f, fe):
+    """Workgroups per graph of the per-graph kernel for this batch (1 on the
+    pipeline): as many as keep the grid within one workgroup per CU (a batch of
+    64 graphs: 4), ``h.vanilla_split`` if set."""
+    if not fused_fits(h, f, fe):
+        return 1
+    if h.vanilla_split is not None:
+        return int(h.vanilla_split)
+    return max(1, min(MAX_SPLIT, CUS // max(1, ((h.B + 7) // 8) * 8)))
 
 
 def fused_fits(h: BatchHandle, f, fe):

@@ -364,15 +364,24 @@ int64_t dr_vanilla_part_floats(int32_t n_feat, int32_t n_edge_feat); /* one laye
 int64_t dr_vanilla_lds_bytes(int32_t n_feat, int32_t n_edge_feat, int32_t out_dim);
 
 /* The same VanillaNetwork training pass (vanilla_gnn.py:26-65 + trainer.py:686-689)
- * with ONE workgroup per graph and the graph in LDS (vanilla_graph.hip): for
- * batches whose largest graph fits (dr_vanilla_fused_lds_bytes(max N, max E)
- * <= 160 KiB), F <= 32, Fe <= 4.  Same slab/head partials as
- * dr_vanilla_graph_pass, so dr_reduce_update is shared.  scratch: device
- * floats, slot b owns dr_vanilla_fused_scratch_floats(N_b, E_b) of them from
- * scratch_off[b] (device int64 [B]).  Needs the store's transpose + t_eid.  */
+ * with the graph in LDS (vanilla_graph.hip): for batches whose largest graph
+ * fits (dr_vanilla_fused_lds_bytes(max N, max E) <= 160 KiB), F <= 32, Fe <= 4.
+ * split (1..DR_VANILLA_MAX_SPLIT) workgroups per graph, each owning a
+ * contiguous, edge-balanced range of CSR rows; they exchange B2 rows, the
+ * mean's column sums and dS2 / dS1 rows through the scratch in-launch.  The
+ * slab then holds `split` partial rows per graph (slab row b*split + r; set
+ * dr_param_table.slab_rows = split), each graph's head vectors one row.
+ * Otherwise the slab/head partials of dr_vanilla_graph_pass, so
+ * dr_reduce_update is shared.  scratch: device floats, slot b owns
+ * dr_vanilla_fused_scratch_floats(N_b, E_b) of them from scratch_off[b]
+ * (device int64 [B]).  sync: device uint32 [2B + 1], zero when allocated and
+ * left zero by every launch (arrival counters; sync[2B] = nonzero after a
+ * hand-off wait gave up).  Needs the store's transpose + t_eid.             */
+#define DR_VANILLA_MAX_SPLIT 4
 int dr_vanilla_fused_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
                           const dr_vanilla_weights* w, const dr_pass* pass, float* scratch,
-                          const int64_t* scratch_off, int32_t lds_bytes, void* stream);
+                          const int64_t* scratch_off, int32_t split, uint32_t* sync, int32_t lds_bytes,
+                          void* stream);
 int64_t dr_vanilla_fused_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_edge_feat);
 int64_t dr_vanilla_fused_scratch_floats(int32_t n_nodes, int32_t n_edges, int32_t n_edge_feat);
 
@@ -413,9 +422,11 @@ typedef struct dr_param_table {
   int32_t numel[DR_MAX_PARAMS];
   dr_grad_recipe recipe[DR_MAX_PARAMS];
   int32_t n_params;
-  int32_t slab_stride;
+  int32_t slab_stride;   /* floats per slab row                                 */
   int32_t head_stride;
-  int32_t pad0;
+  int32_t slab_rows;     /* slab rows per graph (0 or 1: one): graph b's partials are
+                            rows b*slab_rows .. b*slab_rows + slab_rows-1, summed with
+                            the rest (dr_vanilla_fused_pass with split > 1)       */
 } dr_param_table;
 
 /* Sum the per-graph partials of a graph pass over the batch into every

@@ -185,8 +185,9 @@ def test_vanilla_residue_srv_fused_equals_pipeline():
     for pipeline in (False, True):
         h = BatchHandle(store, np.arange(len(datas)))
         h.vanilla_pipeline = pipeline
+        h.vanilla_split = 1  # one partial row per graph on both paths: the slabs compare entry for entry
         out = torch.empty(len(datas), 1, device=DEV)
-        slab = torch.empty(len(datas) * model.fused_spec.slab_stride(30), device=DEV)
+        slab = torch.zeros(len(datas) * model.fused_spec.slab_stride(30), device=DEV)
         head = torch.zeros(len(datas) * model.fused_spec.head_stride(1), device=DEV)
         van_amd.graph_pass(model, h, model.ordered_params(), 1, _lib.DR_PASS_FORWARD | _lib.DR_PASS_BACKWARD, loss_kind=_lib.DR_LOSS_MSE, loss_scale=0.1, out=out, slab=slab, head=head)
         torch.cuda.synchronize()

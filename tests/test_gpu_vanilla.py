@@ -161,7 +161,7 @@ def test_vanilla_pipeline_relu_words_bit_identical_to_recomputed(fe):
         h = BatchHandle(store, np.arange(len(datas)))
         h.vanilla_pipeline, h.vanilla_words = True, words
         out = torch.empty(len(datas), 1, device=DEV)
-        slab = torch.empty(len(datas) * m.fused_spec.slab_stride(30), device=DEV)
+        slab = torch.zeros(len(datas) * m.fused_spec.slab_stride(30), device=DEV)
         head = torch.zeros(len(datas) * m.fused_spec.head_stride(1), device=DEV)
         amd.graph_pass(m, h, m.ordered_params(), 1, _lib.DR_PASS_FORWARD | _lib.DR_PASS_BACKWARD, loss_kind=_lib.DR_LOSS_MSE, loss_scale=0.3, out=out, slab=slab, head=head)
         torch.cuda.synchronize()
