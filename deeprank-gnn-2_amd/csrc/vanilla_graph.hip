@@ -220,7 +220,10 @@ __device__ const float vg_zero_word = 0.f;
 
 // Branch-free global loads: p (nullptr = the value 0) is read unconditionally,
 // so a batch of them is issued back to back and waited for once.
-__device__ __forceinline__ float ld0(const float* p) { return *(p ? p : &vg_zero_word); }
+__device__ __forceinline__ float ld0(const float* p) {
+  // a global (not flat) load: a flat one would also hold every later LDS wait
+  return *(const __attribute__((address_space(1))) float*)(p ? p : &vg_zero_word);
+}
 
 // C[M, 32] = A[M, K] W[K, 32], K = 32 * NK, on v_mfma_f32_16x16x4_f32.  Wave w
 // owns column tile w & 1 and row tiles w >> 1, (w >> 1) + 8, ...; its B
@@ -495,7 +498,7 @@ __device__ __forceinline__ void row_t(const int* trp, const uint16_t* tcol, cons
 #define VSTAMP(i)                                                                                           \
   do {                                                                                                      \
     __builtin_amdgcn_sched_barrier(0);                                                                      \
-    if (tid == 0 && rk == 0 && a.p.stamps) a.p.stamps[(int64_t)b * 32 + (i)] = __builtin_amdgcn_s_memtime(); \
+    if (tid == 0 && a.p.stamps) a.p.stamps[((int64_t)b * a.k + rk) * 32 + (i)] = __builtin_amdgcn_s_memtime(); \
     __builtin_amdgcn_sched_barrier(0);                                                                      \
   } while (0)
 #else
@@ -635,6 +638,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   __syncthreads();
   if (split) {  // hand-off 1: every sibling's B2 rows (and the layer-1 ReLU words)
     publish_rows(P, XA, r0, r1);
+    VSTAMP(19);
     sib_handoff(ctr, tflag, k);
     gather_rows(P, XA, N, r0, r1);
     __syncthreads();
@@ -683,6 +687,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
     else sg[tid] = tid < F ? t / (float)N : 0.f;
   }
   if (split) {  // hand-off 2: the siblings' column sums (and the layer-2 ReLU words)
+    VSTAMP(20);
     sib_handoff(ctr, tflag, k);
     if (tid < 32) {
       float t = ld_sc1(csum + tid);
@@ -802,6 +807,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   __syncthreads();
   if (split) {  // hand-off 3: every sibling's dS2 rows (the transposed pass gathers them by source)
     publish_rows(P, XB, r0, r1);
+    VSTAMP(21);
     sib_handoff(ctr, tflag, k);
     gather_rows(P, XB, N, r0, r1);
   }
@@ -855,6 +861,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   __syncthreads();
   if (split) {  // hand-off 4: every sibling's dS1 rows
     publish_rows(T, XA, r0, r1);
+    VSTAMP(22);
     sib_handoff(ctr, tflag, k);
     sib_exit(ctr, k);
     gather_rows(T, XA, N, r0, r1);

@@ -27,7 +27,7 @@ from deeprank2_amd.store import GraphStore, pack_graphs  # noqa: E402
 from deeprank2_amd.utils.synthetic import make_dataset  # noqa: E402
 
 PHASES_NC = ["stage", "gather Z1=AX", "gemm H1", "gather Z2=AH1", "gemm2+bits+colsum", "mean", "head fwd+loss+bwd", "dW2", "dZ2", "spmmT dS1", "dW1"]
-PHASES_V = ["stage", "gemm B1", "row fwd 1", "gemm X1", "gemm B2", "row fwd 2", "gemm X2", "mean+bits", "head fwd/loss/bwd", "dWn2, dS2", "D2 pass", "row T 2", "dWa2 dWb2 dX1", "DMA X0/S1, dS1", "dWn1", "D1 pass", "row T 1", "dWa1 dWb1"]
+PHASES_V = ["stage", "gemm B1", "row fwd 1", "gemm X1", "gemm B2 + hand-off 1", "row fwd 2", "gemm X2", "mean+bits + hand-off 2", "head fwd/loss/bwd", "dWn2, dS2 + hand-off 3", "D2 pass", "row T 2", "dWa2 dWb2 dX1", "DMA X0/S1, dS1 + h-o 4", "dWn1", "D1 pass", "row T 1", "dWa1 dWb1"]
 PHASES = ["stage", "front: gather+MFMA+pool0 (per wave)", "front barrier wait", "pool0 key decode", "gemm2+spmm2", "pool1", "mean", "head fwd (fc1,fc2)", "loss grad", "head bwd", "pool1-bwd", "spmm2T", "dW2+dP1", "dW1"]
 
 
@@ -111,18 +111,23 @@ def fout(dev, B, which):
 
 
 def vanilla(dev, B):
-    """vanilla_graph_kernel (dr_vanilla_fused_pass) phases on residue graphs."""
+    """vanilla_graph_kernel (dr_vanilla_fused_pass) phases on residue graphs,
+    per workgroup (DR_SPLIT workgroups per graph, default by batch size); the
+    hand-off phases include their waits, reported separately (entry -> done)."""
     from deeprank2_amd import _lib  # noqa: PLC0415
     from deeprank2_amd.fused import make_pass  # noqa: PLC0415
     from deeprank2_amd.neuralnets.gnn import vanilla_gnn as van  # noqa: PLC0415
 
     store = GraphStore(pack_graphs(records(make_dataset(B, seed=1000))), dev)
     h = amd.BatchHandle(store, np.arange(B))
+    if os.environ.get("DR_SPLIT"):
+        h.vanilla_split = int(os.environ["DR_SPLIT"])
+    k = van.split_k(h, 30, 3)
     torch.manual_seed(0)
     model = van.VanillaNetwork(30, 1, 3).to(dev)
     spec = model.fused_spec
     assert van.fused_fits(h, 30, 3)
-    st = torch.zeros(B * 32, dtype=torch.int64, device=dev)
+    st = torch.zeros(B * k * 32, dtype=torch.int64, device=dev)
     out = torch.empty(B, 1, device=dev)
     slab = torch.empty(B * spec.slab_stride(30), device=dev)
     head = torch.empty(B * spec.head_stride(1), device=dev)
@@ -134,13 +139,19 @@ def vanilla(dev, B):
         spec.run(h, w, p)
         torch.cuda.synchronize()
         if it >= 5:
-            rows.append(st.view(B, 32)[:, : len(PHASES_V) + 1].cpu().numpy().copy())
-    d = np.diff(np.stack(rows), axis=2).astype(np.float64)
+            rows.append(st.view(B * k, 32).cpu().numpy().copy())
+    a = np.stack(rows).astype(np.float64)  # [iters, B*k, 32]
+    d = np.diff(a[:, :, : len(PHASES_V) + 1], axis=2)
     med = np.median(d.reshape(-1, d.shape[-1]), axis=0)
     tot = med.sum()
-    print(f"B={B}  median cycles per vanilla_graph_kernel workgroup: {tot:.0f}")
+    print(f"B={B} split={k}  median cycles per vanilla_graph_kernel workgroup: {tot:.0f}")
     for name, v in zip(PHASES_V, med):
         print(f"  {name:18s} {v:8.0f} cyc  {100 * v / tot:5.1f}%")
+    if k > 1:  # hand-off waits: entry stamp (19..22) -> the next phase stamp
+        for name, e, x in (("hand-off 1 (B2)", 19, 5), ("hand-off 2 (col sums)", 20, 8), ("hand-off 3 (dS2)", 21, 10), ("hand-off 4 (dS1)", 22, 14)):
+            print(f"  {name:22s} {np.median(a[:, :, x] - a[:, :, e]):8.0f} cyc (wait + gather)")
+        span = a[:, :, len(PHASES_V)] - a[:, :, 0]
+        print(f"  workgroup span min/median/max {span.min():.0f} / {np.median(span):.0f} / {span.max():.0f} cyc")
 
 
 if __name__ == "__main__":
