@@ -6,7 +6,10 @@ fits a one-GPU box while exercising FusedTrainStep's sharded step and its
 single all-reduce.  DR_DDP_PG=nccl runs one rank over RCCL instead (the
 bench's N>1 launch path on one GPU) and DR_DDP_CAPTURE=1 replays every step
 from a captured HIP graph (all-reduce included).  Writes the final parameters
-(rank 0)."""
+(rank 0).  DR_DDP_EMULATE=n (one process, no group): each global batch's n
+shards run one after another, their gradient buffers summed in rank order
+(what the all-reduce computes), then one Adam update; for n = 2 the same
+bits as two ranks, since a two-operand sum does not depend on the order."""
 
 from __future__ import annotations
 
@@ -25,6 +28,7 @@ from deeprank2_amd.engine import FusedTrainStep  # noqa: E402
 from deeprank2_amd.fused import BatchHandle  # noqa: E402
 from deeprank2_amd.neuralnets.gnn.foutnet import FoutNet  # noqa: E402
 from deeprank2_amd.neuralnets.gnn.ginet import GINet  # noqa: E402
+from deeprank2_amd.neuralnets.gnn.vanilla_gnn import VanillaNetwork  # noqa: E402
 from deeprank2_amd.store import GraphStore, pack_graphs, records_from_batch  # noqa: E402
 from deeprank2_amd.utils.synthetic import make_dataset  # noqa: E402
 from oracle import data_ref  # noqa: E402
@@ -48,11 +52,29 @@ def run(model_name, world, rank, out_path):
     datas = [data_ref.synthetic_to_data(g, f"s{i}") for i, g in enumerate(make_dataset(2 * B, seed=17, n_lo=30, n_hi=80, mean_degree=9.0))]
     store = GraphStore(pack_graphs(records_from_batch(P.Batch.from_data_list(datas))), dev)
     torch.manual_seed(42)
-    model = (GINet(30, 1, 3) if model_name == "ginet" else FoutNet(30, 1)).to(dev).train()
+    model = {"ginet": lambda: GINet(30, 1, 3), "foutnet": lambda: FoutNet(30, 1), "vanilla": lambda: VanillaNetwork(30, 1, 3)}[model_name]().to(dev).train()
     step = FusedTrainStep(model, process_group=pg)
+    emulate = int(os.environ.get("DR_DDP_EMULATE", "0"))
+    if emulate:
+        step.pg, step.world = "emulated", emulate
+        acc = []
+
+        def all_reduce(t, group=None):  # noqa: ARG001
+            acc.append(t.clone() if not acc else acc[-1] + t)
+            t.copy_(acc[-1])
+
+        dist.all_reduce = all_reduce
+        adam = step._adam_after_allreduce  # noqa: SLF001
     losses = []
     for s in range(STEPS):
         gids = np.arange(B) + (s % 2) * B  # global batch, global order
+        if emulate:
+            acc.clear()
+            for r in range(emulate):
+                step._adam_after_allreduce = adam if r == emulate - 1 else (lambda: None)  # noqa: SLF001
+                loss, _ = step.step(BatchHandle(store, shard_contiguous(gids, r, emulate)), global_batch=B, dropout=False)
+            losses.append(float(loss))
+            continue
         h = BatchHandle(store, shard_contiguous(gids, rank, world))
         if capture:
             g = step.capture(h, global_batch=B, dropout=False)

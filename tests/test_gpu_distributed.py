@@ -55,6 +55,21 @@ def test_two_ranks_match_single_process(tmp_path, model_name):
             assert np.mean(np.abs(b[k] - a[k]) < 1e-6) > 0.95, k
 
 
+@pytest.mark.parametrize("model_name", ["ginet", "vanilla"])
+def test_two_ranks_bit_identical_to_summed_shards(tmp_path, model_name):
+    """Two gloo ranks against one process that runs the same two shards one
+    after another and sums their gradient buffers (the all-reduce's sum of two
+    operands, order-free) before one Adam update: losses, all-reduced gradients
+    and parameters after 3 steps agree bit for bit.  VanillaNetwork runs its
+    shards of 12 graphs on 4 workgroups per graph (split partial rows)."""
+    emu, two = str(tmp_path / "emu.npz"), str(tmp_path / "w2.npz")
+    _launch(model_name, 1, emu, DR_DDP_EMULATE="2")
+    _launch(model_name, 2, two)
+    a, b = np.load(emu), np.load(two)
+    for k in a.files:
+        np.testing.assert_array_equal(b[k], a[k], err_msg=k)
+
+
 def test_rccl_captured_ddp_step_matches_plain_step(tmp_path):
     """bench.py's N>1 launch path on one GPU: a one-rank RCCL process group,
     every step replayed from a captured HIP graph holding the graph pass, the
