@@ -146,8 +146,9 @@ __device__ __forceinline__ uint64_t ld_sc1_u64(const float* p) {
 // stores, then one lane arrives on the graph's counter and polls it (sc1)
 // until all k siblings have arrived at this hand-off; the counter only grows
 // within a launch (the h-th hand-off completes at h*k), so arrival v waits for
-// (v / k + 1) * k.  Bounded: a wait that gives up sets the timeout flag and
-// goes on (wrong results, reported by the host; never a hung launch).
+// (v / k + 1) * k.  Bounded: a wait that gives up sets the timeout flag
+// (sync[2B], read by the host through BatchHandle.vanilla_sync_ok()) and goes
+// on with wrong results rather than hanging the launch.
 __device__ __forceinline__ void sib_handoff(uint32_t* ctr, uint32_t* flag, int k) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();

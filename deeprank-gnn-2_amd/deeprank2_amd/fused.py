@@ -108,6 +108,12 @@ class BatchHandle:
             self._lds["vanilla_fused_scratch"] = sc
         return sc
 
+    def vanilla_sync_ok(self):
+        """False if a VanillaNetwork split launch on this batch gave up waiting
+        for a sibling workgroup (its timeout flag; one device read)."""
+        sc = self._lds.get("vanilla_fused_scratch")
+        return sc is None or int(sc[2][-1].item()) == 0
+
     def large_plan(self, out_dim, bf16=False):
         """Tiling + workspaces of the large-graph path (dr_large_plan), built once per batch."""
         plan = self._lds.get(("large", out_dim, bf16))
