@@ -16,7 +16,7 @@ echo "bench rc=$rc"; grep '^{' gpurun_out/bench.log | cut -c1-300
 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_driver.log 2>&1; rc=$?
 echo "bench (driver step counts) rc=$rc"; grep '^{' gpurun_out/bench_driver.log | cut -c1-300
 [ $rc -eq 0 ] || exit $rc
-bash scripts/gpu_configs.sh || exit $?
+[ -n "$SKIP_CONFIGS" ] || bash scripts/gpu_configs.sh || exit $?
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/prof -o run -- python3 $R/bench.py --steps 100 --warmup 10 --no-cpu-baseline > $R/gpurun_out/prof.log 2>&1; rc=$?
 echo "rocprof bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
