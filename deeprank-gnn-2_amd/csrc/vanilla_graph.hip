@@ -115,6 +115,7 @@ struct VGArgs {
   float* scr;
   const int64_t* scr_off;
   uint32_t* sync;  // [2B + 1]: per graph {arrivals, exits}; [2B]: hand-off timeout flag
+  const float* wpack;  // [WPACK_FLOATS]: the weights in fragment order (vanilla_pack_kernel)
   int32_t B, k;
 };
 
@@ -226,18 +227,84 @@ __device__ __forceinline__ float ld0(const float* p) {
   return *(const __attribute__((address_space(1))) float*)(p ? p : &vg_zero_word);
 }
 
+// Weights in MFMA-fragment order, packed once per launch by vanilla_pack_kernel
+// (the parameters change every step): every fragment load of a GEMM phase is
+// then one coalesced 256-byte wave read instead of 64 lanes touching 16 rows.
+// GEMM operand o (NK_o 32-deep k blocks): element ((ct * 8 NK_o + s) * 64 + lane)
+// = W_o(k = 4s + lane / 16, n = 16 ct + lane % 16), zero outside W_o.
+enum { OP_B1, OP_X1, OP_B2, OP_X2, OP_DS2, OP_DX1, OP_DS1, N_OPS };
+__host__ __device__ constexpr int op_nk(int o) { return (o == OP_X1 || o == OP_X2) ? 2 : (o == OP_DX1 ? 3 : 1); }
+__host__ __device__ constexpr int op_base(int o) { return o == 0 ? 0 : op_base(o - 1) + 1024 * op_nk(o - 1); }
+// row-pass weights of layer l at ROW_BASE + l * ROWPACK: float2 per lane (channels
+// 2cp, 2cp+1 of the lane's pair cp = lane % 16): Wa[k = 8 (lane / 16) + m] for m < 8,
+// then Wc[f] for f < 4, then be
+constexpr int ROW_BASE = op_base(N_OPS), ROWPACK = 2 * 64 * (8 + 4 + 1), WPACK_FLOATS = ROW_BASE + 2 * ROWPACK;
+
+struct PackArgs {
+  dr_vanilla_weights w;
+  float* out;
+  int32_t F, Fe;
+};
+
+__device__ float pack_value(const PackArgs& a, int e) {
+  const int F = a.F, Fe = a.Fe, KE = 2 * F + Fe, KN = F + 32;
+  if (e >= ROW_BASE) {  // row-pass block
+    const int l = (e - ROW_BASE) / ROWPACK, q = (e - ROW_BASE) % ROWPACK;
+    const float* we = l ? a.w.we2 : a.w.we1;
+    const float* be = l ? a.w.be2 : a.w.be1;
+    const int part = q >> 1, hi = q & 1;  // float2 index, which channel of the pair
+    const int lane = part & 63, blk = part >> 6, c = 2 * (lane & 15) + hi;
+    if (blk < 8) {
+      const int k = 8 * (lane >> 4) + blk;
+      return k < F ? we[c * KE + k] : 0.f;
+    }
+    if (blk < 12) return blk - 8 < Fe ? we[c * KE + 2 * F + blk - 8] : 0.f;
+    return be[c];
+  }
+  int o = 0;
+  while (o + 1 < N_OPS && e >= op_base(o + 1)) ++o;
+  const int q = e - op_base(o), nk = op_nk(o), lane = q & 63, s = (q >> 6) % (8 * nk), ct = (q >> 6) / (8 * nk);
+  const int k = 4 * s + (lane >> 4), n = 16 * ct + (lane & 15);
+  switch (o) {
+    case OP_B1: return k < F ? a.w.we1[n * KE + F + k] : 0.f;
+    case OP_B2: return k < F ? a.w.we2[n * KE + F + k] : 0.f;
+    case OP_X1:
+    case OP_X2: {
+      const float* wn = o == OP_X1 ? a.w.wn1 : a.w.wn2;
+      return n < F ? (k < F ? wn[n * KN + k] : (k < 32 ? 0.f : wn[n * KN + F + k - 32])) : 0.f;
+    }
+    case OP_DS1:
+    case OP_DS2: {  // W(k, c) = Wn[k][F + c], k < F (the rows of dS = DU Wn[:, F:])
+      const float* wn = o == OP_DS1 ? a.w.wn1 : a.w.wn2;
+      return k < F ? wn[k * KN + F + n] : 0.f;
+    }
+    default:  // OP_DX1: [Wn2[:, :F]; Wa2; Wb2]
+      return n < F ? (k < 32 ? (k < F ? a.w.wn2[k * KN + n] : 0.f)
+                             : (k < 64 ? a.w.we2[(k - 32) * KE + n] : a.w.we2[(k - 64) * KE + F + n]))
+                   : 0.f;
+  }
+}
+
+__global__ void __launch_bounds__(256) vanilla_pack_kernel(PackArgs a) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e < WPACK_FLOATS) a.out[e] = pack_value(a, e);
+}
+
 // C[M, 32] = A[M, K] W[K, 32], K = 32 * NK, on v_mfma_f32_16x16x4_f32.  Wave w
 // owns column tile w & 1 and row tiles w >> 1, (w >> 1) + 8, ...; its B
-// fragment (W(k, n): a pointer into the weights, nullptr = 0) and the column's
-// bias (Bp(n), nullptr = 0) are loaded into registers once, before the first
-// tile.  A returns the LDS operand; epi(m, n, v, bias).
-template <int NK, class AF, class WF, class BF, class EF>
-__device__ __forceinline__ void mm_w(int M, AF A, WF W, BF Bp, EF epi) {
+// fragment (packed operand frag, coalesced) and the column's bias (Bp(n),
+// nullptr = 0) are loaded into registers once, before the first tile; waves
+// without a row tile load nothing.  A returns the LDS operand; epi(m, n, v, bias).
+template <int NK, class AF, class BF, class EF>
+__device__ __forceinline__ void mm_w(int M, AF A, const float* frag, BF Bp, EF epi) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, kq = lane >> 4;
   const int n = (wave & 1) * 16 + li;
+  if ((wave >> 1) * 16 >= M) return;
+  const __attribute__((address_space(1))) float* fr =
+      (const __attribute__((address_space(1))) float*)(frag + (wave & 1) * 8 * NK * 64 + lane);
   float bw[8 * NK];
 #pragma unroll
-  for (int s = 0; s < 8 * NK; ++s) bw[s] = ld0(W(4 * s + kq, n));
+  for (int s = 0; s < 8 * NK; ++s) bw[s] = fr[s * 64];
   const float bias = ld0(Bp(n));
   const int nrt = (M + 15) >> 4;
   for (int rt = wave >> 1; rt < nrt; rt += NW / 2) {
@@ -317,22 +384,26 @@ __device__ __forceinline__ float2 f2slot_sum(float2 v) {
 template <int FE>
 __device__ __forceinline__ void row_fwd(const int* rp, const uint4* rec, const float* ext, const float* X,
                                         const float* Bs, float* S, float* S1g, float* cntg, float* eapg,
-                                        uint32_t* btg, const float* we, const float* be, int KE, int F, int N,
-                                        int N_E, int r0, int r1) {
+                                        uint32_t* btg, const float* rpack, int N, int N_E, int r0, int r1) {
   constexpr int FA = FE > 0 ? FE : 1;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, cp = lane & 15, sl = lane >> 4, c0 = 2 * cp;
+  // this layer's Wa / Wc / be pairs, packed per lane (vanilla_pack_kernel): coalesced float2 loads
+  typedef float fl2 __attribute__((ext_vector_type(2)));
+  const __attribute__((address_space(1))) fl2* rp2 = (const __attribute__((address_space(1))) fl2*)(rpack) + lane;
   float2 wa[8];
 #pragma unroll
   for (int m = 0; m < 8; ++m) {
-    const int k = 8 * sl + m;
-    const int kc = k < F ? k : 0;
-    const float w0 = we[c0 * KE + kc], w1 = we[(c0 + 1) * KE + kc];
-    wa[m] = k < F ? make_float2(w0, w1) : make_float2(0.f, 0.f);
+    const fl2 v = rp2[m * 64];
+    wa[m] = make_float2(v.x, v.y);
   }
   float2 wc[FA];
 #pragma unroll
-  for (int f = 0; f < FE; ++f) wc[f] = make_float2(we[c0 * KE + 2 * F + f], we[(c0 + 1) * KE + 2 * F + f]);
-  const float2 be2 = make_float2(be[c0], be[c0 + 1]);
+  for (int f = 0; f < FE; ++f) {
+    const fl2 v = rp2[(8 + f) * 64];
+    wc[f] = make_float2(v.x, v.y);
+  }
+  const fl2 bev = rp2[12 * 64];
+  const float2 be2 = make_float2(bev.x, bev.y);
   const int n32 = 32 * N;
   for (int i = r0 + wave; i < r1; i += NW) {
     const int eb = rp[i], ee = rp[i + 1];
@@ -616,25 +687,22 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   VSTAMP(1);
   // ---------------- layer 1: B1 = X0 Wb1^T -> Q (every row: the row pass gathers any) --
   mm_w<1>(N, [&](int i, int k) { return P[i * LS + k]; },
-          [&](int k, int n) -> const float* { return k < F ? w.we1 + n * KE + F + k : nullptr; }, [&](int) -> const float* { return nullptr; },
+          a.wpack + op_base(OP_B1), [&](int) -> const float* { return nullptr; },
           [&](int i, int n, float v, float) { Q[i * LS + n] = v; });
   __syncthreads();
   VSTAMP(2);
-  row_fwd<FE>(srp, rec, ext, P, Q, R, S1g, cnt1, eap1, bt1g, w.we1, w.be1, KE, F, N, E, r0, r1);
+  row_fwd<FE>(srp, rec, ext, P, Q, R, S1g, cnt1, eap1, bt1g, a.wpack + ROW_BASE, N, E, r0, r1);
   __syncthreads();
   VSTAMP(3);
   // X1 = relu([X0 | S1] Wn1^T + bn1) -> Q (pad columns 0), own rows
   mm_w<2>(nown, [&](int i, int k) { return k < 32 ? P[(r0 + i) * LS + k] : R[(r0 + i) * LS + k - 32]; },
-          [&](int k, int n) -> const float* {
-            return n < F ? (k < F ? w.wn1 + n * KN + k : (k < 32 ? nullptr : w.wn1 + n * KN + F + k - 32)) : nullptr;
-          },
-          [&](int n) -> const float* { return n < F ? w.bn1 + n : nullptr; },
+          a.wpack + op_base(OP_X1), [&](int n) -> const float* { return n < F ? w.bn1 + n : nullptr; },
           [&](int i, int n, float v, float bias) { Q[(r0 + i) * LS + n] = n < F ? relu_keepnan(v + bias) : 0.f; });
   __syncthreads();
   VSTAMP(4);
   // ---------------- layer 2: B2 = X1 Wb2^T -> P, own rows ---------------------
   mm_w<1>(nown, [&](int i, int k) { return Q[(r0 + i) * LS + k]; },
-          [&](int k, int n) -> const float* { return k < F ? w.we2 + n * KE + F + k : nullptr; }, [&](int) -> const float* { return nullptr; },
+          a.wpack + op_base(OP_B2), [&](int) -> const float* { return nullptr; },
           [&](int i, int n, float v, float) { P[(r0 + i) * LS + n] = v; });
   __syncthreads();
   if (split) {  // hand-off 1: every sibling's B2 rows (and the layer-1 ReLU words)
@@ -645,7 +713,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
     __syncthreads();
   }
   VSTAMP(5);
-  row_fwd<FE>(srp, rec, ext, Q, P, R, nullptr, cnt2, eap2, bt2g, w.we2, w.be2, KE, F, N, E, r0, r1);
+  row_fwd<FE>(srp, rec, ext, Q, P, R, nullptr, cnt2, eap2, bt2g, a.wpack + ROW_BASE + ROWPACK, N, E, r0, r1);
   wait_vm();  // ReLU words, cnt, eap of both layers stored before anyone reads them back
   __syncthreads();
   VSTAMP(6);
@@ -658,10 +726,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   }
   // X2 = relu([X1 | S2] Wn2^T + bn2) -> P, own rows
   mm_w<2>(nown, [&](int i, int k) { return k < 32 ? Q[(r0 + i) * LS + k] : R[(r0 + i) * LS + k - 32]; },
-          [&](int k, int n) -> const float* {
-            return n < F ? (k < F ? w.wn2 + n * KN + k : (k < 32 ? nullptr : w.wn2 + n * KN + F + k - 32)) : nullptr;
-          },
-          [&](int n) -> const float* { return n < F ? w.bn2 + n : nullptr; },
+          a.wpack + op_base(OP_X2), [&](int n) -> const float* { return n < F ? w.bn2 + n : nullptr; },
           [&](int i, int n, float v, float bias) { P[(r0 + i) * LS + n] = n < F ? relu_keepnan(v + bias) : 0.f; });
   __syncthreads();
   VSTAMP(7);
@@ -802,7 +867,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
            else gw[32 * KE + 32 + F * KN + n] = sdm[n] * v;
          });
     mm_w<1>(nown, [&](int i, int n) { return ((xb[r0 + i] >> n) & 1u) ? sdm[n] : 0.f; },
-            [&](int n, int c) -> const float* { return n < F ? w.wn2 + n * KN + F + c : nullptr; }, [&](int) -> const float* { return nullptr; },
+            a.wpack + op_base(OP_DS2), [&](int) -> const float* { return nullptr; },
             [&](int i, int c, float v, float) { P[(r0 + i) * LS + c] = v; });
   }
   __syncthreads();
@@ -838,12 +903,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
               const int ii = r0 + i;
               return k < 32 ? (((xb[ii] >> k) & 1u) ? sdm[k] : 0.f) : (k < 64 ? R[ii * LS + k - 32] : T[ii * LS + k - 64]);
             },
-            [&](int k, int n) -> const float* {
-              return n < F ? (k < 32 ? (k < F ? w.wn2 + k * KN + n : nullptr)
-                                     : (k < 64 ? w.we2 + (k - 32) * KE + n : w.we2 + (k - 64) * KE + F + n))
-                           : nullptr;
-            },
-            [&](int) -> const float* { return nullptr; },
+            a.wpack + op_base(OP_DX1), [&](int) -> const float* { return nullptr; },
             [&](int i, int n, float v, float) { P[(r0 + i) * LS + n] = n < F ? relu_bwd(Q[(r0 + i) * LS + n], v) : 0.f; });
   }
   __syncthreads();
@@ -856,7 +916,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   if (split) gather_words(bt, bt1g, strp[r0], strp[r1]);
   else dma_words<NT>(bt, bt1g, E);
   mm_w<1>(nown, [&](int i, int n) { return P[(r0 + i) * LS + n]; },
-          [&](int n, int c) -> const float* { return n < F ? w.wn1 + n * KN + F + c : nullptr; }, [&](int) -> const float* { return nullptr; },
+          a.wpack + op_base(OP_DS1), [&](int) -> const float* { return nullptr; },
           [&](int i, int c, float v, float) { T[(r0 + i) * LS + c] = v; });
   wait_vm();
   __syncthreads();
@@ -915,11 +975,13 @@ extern "C" int64_t dr_vanilla_fused_scratch_floats(int32_t n_nodes, int32_t n_ed
   return vscratch_floats(n_nodes, n_edges, n_edge_feat);
 }
 
+extern "C" int64_t dr_vanilla_wpack_floats(void) { return WPACK_FLOATS; }
+
 extern "C" int dr_vanilla_fused_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
                                      const dr_vanilla_weights* w, const dr_pass* pass, float* scratch,
-                                     const int64_t* scratch_off, int32_t split, uint32_t* sync, int32_t lds_bytes,
-                                     void* stream) {
-  if (!store || !descs || !w || !pass || n_batch < 0) return DR_E_ARG;
+                                     const int64_t* scratch_off, int32_t split, uint32_t* sync, float* wpack,
+                                     int32_t lds_bytes, void* stream) {
+  if (!store || !descs || !w || !pass || n_batch < 0 || !wpack) return DR_E_ARG;
   if (split < 1 || split > MAXK || (split > 1 && !sync)) return DR_E_ARG;
   if (pass->out_dim < 1 || pass->out_dim > DR_MAX_OUT) return DR_E_UNSUPPORTED;
   if (store->n_feat < 1 || store->n_feat > 32 || store->x_stride > 32 || store->n_edge_feat < 0 ||
@@ -950,8 +1012,17 @@ extern "C" int dr_vanilla_fused_pass(const dr_graph_store* store, const dr_graph
   a.scr = scratch;
   a.scr_off = scratch_off;
   a.sync = sync;
+  a.wpack = wpack;
   a.B = n_batch;
   a.k = split;
+  {
+    PackArgs pa;
+    pa.w = *w;
+    pa.out = wpack;
+    pa.F = store->n_feat;
+    pa.Fe = store->n_edge_feat;
+    hipLaunchKernelGGL(vanilla_pack_kernel, dim3((WPACK_FLOATS + 255) / 256), dim3(256), 0, (hipStream_t)stream, pa);
+  }
   // graph b's siblings are blocks 8 apart (see the kernel); grid padded to 8 graphs
   const dim3 grid((unsigned)(((n_batch + 7) / 8) * 8 * split));
   switch (store->n_edge_feat) {

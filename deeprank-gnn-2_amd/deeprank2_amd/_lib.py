@@ -210,7 +210,8 @@ SIGNATURES = [
     ("dr_vanilla_scratch_floats", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
     ("dr_vanilla_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 3),
     ("dr_vanilla_part_floats", ctypes.c_int64, [ctypes.c_int32] * 2),
-    ("dr_vanilla_fused_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(VanillaWeightsC), ctypes.POINTER(PassC), VP, VP, ctypes.c_int32, VP, ctypes.c_int32, VP]),
+    ("dr_vanilla_fused_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(VanillaWeightsC), ctypes.POINTER(PassC), VP, VP, ctypes.c_int32, VP, VP, ctypes.c_int32, VP]),
+    ("dr_vanilla_wpack_floats", ctypes.c_int64, []),
     ("dr_vanilla_fused_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 3),
     ("dr_vanilla_fused_scratch_floats", ctypes.c_int64, [ctypes.c_int32] * 3),
     ("dr_fout_graph_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(FoutWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, VP]),

@@ -104,7 +104,8 @@ class BatchHandle:
             buf = torch.empty(max(1, int(off[-1])), dtype=torch.float32, device=dev)
             offs = torch.from_numpy(off[:-1].copy()).to(dev)
             sync = torch.zeros(2 * self.B + 1, dtype=torch.int32, device=dev)  # arrival counters, left zero by every launch
-            sc = (buf, offs, sync)
+            wpack = torch.empty(int(_lib.load().dr_vanilla_wpack_floats()), dtype=torch.float32, device=dev)  # weights in fragment order
+            sc = (buf, offs, sync, wpack)
             self._lds["vanilla_fused_scratch"] = sc
         return sc
 

@@ -124,9 +124,9 @@ def make_spec(f, fe):
             raise ValueError(msg)
         lib = _lib.load()
         if fused_fits(h, f, fe):  # split_k(h) workgroups per graph, graph in LDS
-            buf, offs, sync = h.vanilla_fused_scratch()
+            buf, offs, sync, wpack = h.vanilla_fused_scratch()
             lds = h.lds(("vanilla_fused", fe), lambda n, e, *_: lib.dr_vanilla_fused_lds_bytes(n, e, fe))
-            _lib.check(lib.dr_vanilla_fused_pass(st.cstruct(), h.descs.data_ptr(), h.B, w, p, buf.data_ptr(), offs.data_ptr(), split_k(h, f, fe), sync.data_ptr(), lds, _lib.stream_ptr(st.device)), "dr_vanilla_fused_pass")
+            _lib.check(lib.dr_vanilla_fused_pass(st.cstruct(), h.descs.data_ptr(), h.B, w, p, buf.data_ptr(), offs.data_ptr(), split_k(h, f, fe), sync.data_ptr(), wpack.data_ptr(), lds, _lib.stream_ptr(st.device)), "dr_vanilla_fused_pass")
             return
         sc, _keep = h.vanilla_scratch(f, fe)
         lds = int(lib.dr_vanilla_lds_bytes(f, fe, p.out_dim))

@@ -376,12 +376,15 @@ int64_t dr_vanilla_lds_bytes(int32_t n_feat, int32_t n_edge_feat, int32_t out_di
  * dr_vanilla_fused_scratch_floats(N_b, E_b) of them from scratch_off[b]
  * (device int64 [B]).  sync: device uint32 [2B + 1], zero when allocated and
  * left zero by every launch (arrival counters; sync[2B] = nonzero after a
- * hand-off wait gave up).  Needs the store's transpose + t_eid.             */
+ * hand-off wait gave up).  wpack: device floats [dr_vanilla_wpack_floats()],
+ * rewritten by every call (the weights in MFMA-fragment order, packed by a
+ * first small launch).  Needs the store's transpose + t_eid.               */
 #define DR_VANILLA_MAX_SPLIT 4
 int dr_vanilla_fused_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
                           const dr_vanilla_weights* w, const dr_pass* pass, float* scratch,
-                          const int64_t* scratch_off, int32_t split, uint32_t* sync, int32_t lds_bytes,
-                          void* stream);
+                          const int64_t* scratch_off, int32_t split, uint32_t* sync, float* wpack,
+                          int32_t lds_bytes, void* stream);
+int64_t dr_vanilla_wpack_floats(void);
 int64_t dr_vanilla_fused_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_edge_feat);
 int64_t dr_vanilla_fused_scratch_floats(int32_t n_nodes, int32_t n_edges, int32_t n_edge_feat);
 

@@ -171,7 +171,7 @@ def _split_step(datas, store, fe, split, state, loss="mse", out_dim=1):
     assert amd.split_k(h, 30, fe) == split
     loss_v, out = step.step(h)
     torch.cuda.synchronize()
-    _buf, _offs, sync = h.vanilla_fused_scratch()
+    _buf, _offs, sync, _wpack = h.vanilla_fused_scratch()
     assert h.vanilla_sync_ok(), "a hand-off wait gave up"
     assert int(sync.abs().sum()) == 0, "arrival counters not left zero"
     return m, step, loss_v.clone(), out.clone(), [g.clone() for g in step.grads], [p.detach().clone() for p in step.params]
