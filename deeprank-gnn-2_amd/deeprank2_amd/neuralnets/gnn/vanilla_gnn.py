@@ -137,18 +137,30 @@ def make_spec(f, fe):
 
 FUSED_MAX_FE = 4  # vanilla_graph.hip MAXFE
 MAX_SPLIT = 4  # DR_VANILLA_MAX_SPLIT
-CUS = 256  # MI355X compute units: one 1024-thread workgroup per CU
+_CUS = {}
+
+
+def _cus(device):
+    """Compute units of the device (256 on a whole MI355X; fewer in a partition
+    mode): the per-graph kernel holds one 1024-thread workgroup per CU."""
+    key = str(device)
+    if key not in _CUS:
+        try:
+            _CUS[key] = int(torch.cuda.get_device_properties(torch.device(device)).multi_processor_count)
+        except (RuntimeError, AssertionError, ValueError):
+            _CUS[key] = 256
+    return _CUS[key]
 
 
 def split_k(h: BatchHandle, f, fe):
     """Workgroups per graph of the per-graph kernel for this batch (1 on the
     pipeline): as many as keep the grid within one workgroup per CU (a batch of
-    64 graphs: 4), ``h.vanilla_split`` if set."""
+    64 graphs on 256 CUs: 4), ``h.vanilla_split`` if set."""
     if not fused_fits(h, f, fe):
         return 1
     if h.vanilla_split is not None:
         return int(h.vanilla_split)
-    return max(1, min(MAX_SPLIT, CUS // max(1, ((h.B + 7) // 8) * 8)))
+    return max(1, min(MAX_SPLIT, _cus(h.store.device) // max(1, ((h.B + 7) // 8) * 8)))
 
 
 def fused_fits(h: BatchHandle, f, fe):
