@@ -21,6 +21,7 @@ namespace drr {
 constexpr int RP = 64;  // parameter elements per block
 constexpr int RC = 8;   // batch chunks per block
 constexpr int RU = 8;   // batch rows per chunk issued together (predicated)
+constexpr int RU2 = 24; // then the rest of a chunk, this many at a time
 constexpr int RT = RP * RC;  // threads per block
 
 // One 64-byte kernel-argument line per parameter: a block fetches everything
@@ -122,17 +123,19 @@ __device__ __forceinline__ void reduce_block(const ReduceHdr& h, const ParamRec&
 #pragma unroll
       for (int k = 0; k < RU; ++k)
         if (b0 + k < b1) acc = outer ? fmaf(u[k], w[k], acc) : acc + u[k];
-      // batches larger than RC*RU rows per block: the rest, RU rows at a time
-      for (int bb = b0 + RU; bb < b1; bb += RU) {
+      // more than RU rows per chunk (e.g. split partial rows): the rest, RU2
+      // rows' loads in flight at a time (same rows, same order)
+      for (int bb = b0 + RU; bb < b1; bb += RU2) {
+        float u2[RU2], w2[RU2];
 #pragma unroll
-        for (int k = 0; k < RU; ++k) {
+        for (int k = 0; k < RU2; ++k) {
           const int64_t row = min(bb + k, b1 - 1);
-          u[k] = ld_part<LD>(base + row * st + col1);
-          w[k] = outer ? ld_part<LD>(base + row * st + col2) : 1.f;
+          u2[k] = ld_part<LD>(base + row * st + col1);
+          w2[k] = outer ? ld_part<LD>(base + row * st + col2) : 1.f;
         }
 #pragma unroll
-        for (int k = 0; k < RU; ++k)
-          if (bb + k < b1) acc = outer ? fmaf(u[k], w[k], acc) : acc + u[k];
+        for (int k = 0; k < RU2; ++k)
+          if (bb + k < b1) acc = outer ? fmaf(u2[k], w2[k], acc) : acc + u2[k];
       }
     }
     part[ch][lp] = acc;
