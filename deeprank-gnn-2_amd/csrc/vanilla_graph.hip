@@ -239,9 +239,9 @@ enum { OP_B1, OP_X1, OP_B2, OP_X2, OP_DS2, OP_DX1, OP_DS1, N_OPS };
 __host__ __device__ constexpr int op_nk(int o) { return (o == OP_X1 || o == OP_X2) ? 2 : (o == OP_DX1 ? 3 : 1); }
 __host__ __device__ constexpr int op_base(int o) { return o == 0 ? 0 : op_base(o - 1) + 1024 * op_nk(o - 1); }
 // row-pass weights of layer l at ROW_BASE + l * ROWPACK: float2 per lane (channels
-// 2cp, 2cp+1 of the lane's pair cp = lane % 16): Wa[k = 8 (lane / 16) + m] for m < 8,
-// then Wc[f] for f < 4, then be
-constexpr int ROW_BASE = op_base(N_OPS), ROWPACK = 2 * 64 * (8 + 4 + 1), WPACK_FLOATS = ROW_BASE + 2 * ROWPACK;
+// 2cp, 2cp+1 of the lane's pair cp = lane % 16): Wa[k = 16 (lane / 16 % 2) + m] for
+// m < 16, then Wc[f] for f < 4, then be
+constexpr int ROW_BASE = op_base(N_OPS), ROWPACK = 2 * 64 * (16 + 4 + 1), WPACK_FLOATS = ROW_BASE + 2 * ROWPACK;
 
 struct PackArgs {
   dr_vanilla_weights w;
@@ -257,11 +257,11 @@ __device__ float pack_value(const PackArgs& a, int e) {
     const float* be = l ? a.w.be2 : a.w.be1;
     const int part = q >> 1, hi = q & 1;  // float2 index, which channel of the pair
     const int lane = part & 63, blk = part >> 6, c = 2 * (lane & 15) + hi;
-    if (blk < 8) {
-      const int k = 8 * (lane >> 4) + blk;
+    if (blk < 16) {
+      const int k = 16 * ((lane >> 4) & 1) + blk;
       return k < F ? we[c * KE + k] : 0.f;
     }
-    if (blk < 12) return blk - 8 < Fe ? we[c * KE + 2 * F + blk - 8] : 0.f;
+    if (blk < 20) return blk - 16 < Fe ? we[c * KE + 2 * F + blk - 16] : 0.f;
     return be[c];
   }
   int o = 0;
@@ -377,61 +377,71 @@ __device__ __forceinline__ float2 f2slot_sum(float2 v) {
 // Edge ReLU words: bit b (b < 16) = channel 2b, bit 16 + b = channel 2b + 1
 // (the two ballots of the packed row pass side by side).
 
-// Forward CSR row pass of one layer, one wave per row.  Lane = (channel pair
-// cp = lane & 15: channels 2cp, 2cp+1 as a float2; edge slot sl = lane >> 4):
-// each 16-edge chunk of the row is 4 steps of 4 edges.
+// Forward CSR row pass of one layer, two rows per wave.  Lane = (channel pair
+// cp = lane & 15: channels 2cp, 2cp+1 as a float2; edge slot es = (lane >> 4) & 1;
+// row hr = lane >> 5 of the wave's pair): each 8-edge chunk of a row is 4 steps
+// of 2 edges, the pair's shorter row idling (masked) past its end.
 //   S_i = sum_{e in row i} relu(A_i + B_j + Wc ea_e),   A_i = Wa x_i + be
-// (A_i: each slot sums 8 of the K = 32 (padded) inputs, then the slots combine).
+// (A_i: each slot sums 16 of the K = 32 (padded) inputs, then the slots combine).
 // Also cnt_i / eap_i (see the header) and each edge's ReLU word at its
 // transposed slot (global bt).  Edge records: {byte offset of B row col | tpos << 16, ea0, ea1, ea2}.
+__device__ __forceinline__ float2 f2half_sum(float2 v) { return f2add(v, f2shfl_xor(v, 16)); }
+
 template <int FE>
 __device__ __forceinline__ void row_fwd(const int* rp, const uint4* rec, const float* ext, const float* X,
                                         const float* Bs, float* S, float* S1g, float* cntg, float* eapg,
                                         uint32_t* btg, const float* rpack, int N, int N_E, int r0, int r1) {
   constexpr int FA = FE > 0 ? FE : 1;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, cp = lane & 15, sl = lane >> 4, c0 = 2 * cp;
+  const int es = sl & 1, hr = sl >> 1;
   // this layer's Wa / Wc / be pairs, packed per lane (vanilla_pack_kernel): coalesced float2 loads
   typedef float fl2 __attribute__((ext_vector_type(2)));
   const __attribute__((address_space(1))) fl2* rp2 = (const __attribute__((address_space(1))) fl2*)(rpack) + lane;
-  float2 wa[8];
+  float2 wa[16];
 #pragma unroll
-  for (int m = 0; m < 8; ++m) {
+  for (int m = 0; m < 16; ++m) {
     const fl2 v = rp2[m * 64];
     wa[m] = make_float2(v.x, v.y);
   }
   float2 wc[FA];
 #pragma unroll
   for (int f = 0; f < FE; ++f) {
-    const fl2 v = rp2[(8 + f) * 64];
+    const fl2 v = rp2[(16 + f) * 64];
     wc[f] = make_float2(v.x, v.y);
   }
-  const fl2 bev = rp2[12 * 64];
+  const fl2 bev = rp2[20 * 64];
   const float2 be2 = make_float2(bev.x, bev.y);
   const int n32 = 32 * N;
-  for (int i = r0 + wave; i < r1; i += NW) {
-    const int eb = rp[i], ee = rp[i + 1];
+  for (int i0 = r0 + 2 * wave; i0 < r1; i0 += 2 * NW) {
+    const int i = i0 + hr;
+    const bool rowok = i < r1;
+    const int ii = rowok ? i : i0;
+    const int eb = rp[ii], len = rowok ? rp[ii + 1] - eb : 0;
+    const int lmax = max(len, __shfl_xor(len, 32, 64));
     float2 a = make_float2(0.f, 0.f);
     {
-      const float2* xr = reinterpret_cast<const float2*>(X + i * LS + 8 * sl);
+      const float2* xr = reinterpret_cast<const float2*>(X + ii * LS + 16 * es);
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
+      for (int m = 0; m < 8; ++m) {
         const float2 v = xr[m];
         a = f2fma(v.x, wa[2 * m], a);
         a = f2fma(v.y, wa[2 * m + 1], a);
       }
     }
-    a = f2add(f2slot_sum(a), be2);
+    a = f2add(f2half_sum(a), be2);
     float2 acc = make_float2(0.f, 0.f), cnt = make_float2(0.f, 0.f), eap[FA];
 #pragma unroll
     for (int f = 0; f < FA; ++f) eap[f] = make_float2(0.f, 0.f);
-    for (int e0 = eb; e0 < ee; e0 += 16) {
-      const int nch = ee - e0;
+    for (int off = 0; off < lmax; off += 8) {
+      const int nch = len - off;
+      // past this row's end (the pair's other row is longer): the zero padding records
+      const int base = nch > 0 ? eb + off : N_E;
       uint4 r[4];
       float e3[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        r[u] = rec[e0 + sl + 4 * u];  // past the row end: the next rows' / padding records (masked)
-        e3[u] = FE > 3 ? ext[e0 + sl + 4 * u] : 0.f;
+        r[u] = rec[base + es + 2 * u];  // past the row end: the next rows' / padding records (masked)
+        e3[u] = FE > 3 ? ext[base + es + 2 * u] : 0.f;
       }
       float2 bj[4];
 #pragma unroll
@@ -439,7 +449,7 @@ __device__ __forceinline__ void row_fwd(const int* rp, const uint4* rec, const f
         bj[u] = *reinterpret_cast<const float2*>(reinterpret_cast<const char*>(Bs) + (r[u].x & 0xffffu) + 8 * cp);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const bool ok = sl + 4 * u < nch;
+        const bool ok = es + 2 * u < nch;
         const float ev[4] = {__uint_as_float(r[u].y), __uint_as_float(r[u].z), __uint_as_float(r[u].w), e3[u]};
         float2 pre = f2add(a, bj[u]);
 #pragma unroll
@@ -461,11 +471,11 @@ __device__ __forceinline__ void row_fwd(const int* rp, const uint4* rec, const f
                      (uint32_t)((blo >> (16 * sl)) & 0xffffu) | ((uint32_t)((bhi >> (16 * sl)) & 0xffffu) << 16));
       }
     }
-    acc = f2slot_sum(acc);
-    cnt = f2slot_sum(cnt);
+    acc = f2half_sum(acc);
+    cnt = f2half_sum(cnt);
 #pragma unroll
-    for (int f = 0; f < FE; ++f) eap[f] = f2slot_sum(eap[f]);
-    if (sl == 0) {
+    for (int f = 0; f < FE; ++f) eap[f] = f2half_sum(eap[f]);
+    if (es == 0 && rowok) {
       *reinterpret_cast<float2*>(S + i * LS + c0) = acc;
       if (S1g) *reinterpret_cast<float2*>(S1g + i * 32 + c0) = acc;
       *reinterpret_cast<float2*>(cntg + i * 32 + c0) = cnt;
