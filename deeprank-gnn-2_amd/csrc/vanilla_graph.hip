@@ -550,23 +550,29 @@ __device__ __forceinline__ void d_pass_sum(const float* red, float* gw, int KE, 
 }
 
 // Transposed pass: D'_j = sum over in-edges (i -> j) active in channel c of dS_i
-// (lane layout of row_fwd: channel pair x edge slot).
+// (lane layout of row_fwd: channel pair x edge slot x row of the wave's pair).
 __device__ __forceinline__ void row_t(const int* trp, const uint16_t* tcol, const uint32_t* bt, const float* dS,
                                       float* Dp, int r0, int r1) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, cp = lane & 15, sl = lane >> 4, c0 = 2 * cp;
-  for (int j = r0 + wave; j < r1; j += NW) {
-    const int qb = trp[j], qe = trp[j + 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, cp = lane & 15, c0 = 2 * cp;
+  const int es = (lane >> 4) & 1, hr = lane >> 5;
+  for (int j0 = r0 + 2 * wave; j0 < r1; j0 += 2 * NW) {
+    const int j = j0 + hr;
+    const bool rowok = j < r1;
+    const int jj = rowok ? j : j0;
+    const int qb = trp[jj], len = rowok ? trp[jj + 1] - qb : 0;
+    const int lmax = max(len, __shfl_xor(len, 32, 64));
     float2 acc = make_float2(0.f, 0.f);
-    for (int q0 = qb; q0 < qe; q0 += 16) {
-      const int nch = qe - q0;
+    for (int off = 0; off < lmax; off += 8) {
+      const int nch = len - off;
       uint32_t wd[4];
       float2 v[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const bool ok = sl + 4 * u < nch;
-        const int q = q0 + min(sl + 4 * u, nch - 1);
+        const bool ok = es + 2 * u < nch;
+        const int q = qb + off + es + 2 * u;
         wd[u] = ok ? bt[q] : 0u;
-        v[u] = *reinterpret_cast<const float2*>(dS + (int)tcol[q] * LS + c0);
+        // masked slots (past the row end, or an empty row) read node 0's row
+        v[u] = *reinterpret_cast<const float2*>(dS + (ok ? (int)tcol[q] : 0) * LS + c0);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -574,8 +580,8 @@ __device__ __forceinline__ void row_t(const int* trp, const uint16_t* tcol, cons
         acc.y += ((wd[u] >> (16 + cp)) & 1u) ? v[u].y : 0.f;
       }
     }
-    acc = f2slot_sum(acc);
-    if (sl == 0) *reinterpret_cast<float2*>(Dp + j * LS + c0) = acc;
+    acc = f2half_sum(acc);
+    if (es == 0 && rowok) *reinterpret_cast<float2*>(Dp + j * LS + c0) = acc;
   }
 }
 
