@@ -146,7 +146,7 @@ def design_bytes(packed, gids, model="ginet", out_dim=1):
     return int((2 * part + extra).sum())
 
 
-PMC_FILES = {"ginet": "pmc_ginet_graph_kernel.txt", "foutnet": "pmc_foutnet_graph_kernel.txt", "sgat": "pmc_sgat_graph_kernel.txt"}
+PMC_FILES = {"ginet": "pmc_ginet_graph_kernel.txt", "foutnet": "pmc_foutnet_graph_kernel.txt", "sgat": "pmc_sgat_graph_kernel.txt", "vanilla": "pmc_vanilla_graph_kernel.txt"}
 
 
 def pmc_traffic_bytes(model="ginet"):
