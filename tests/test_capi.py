@@ -76,3 +76,21 @@ def test_vanilla_fused_sizes_host_mirror():
         assert lib.dr_vanilla_fused_lds_bytes(n, e, fe) % 16 == 0
     for fe in (1, 2, 3):
         assert lib.dr_vanilla_fused_lds_bytes(220, 3606, fe) <= 160 * 1024
+
+
+def test_vanilla_fused_pass_argument_checks_are_host_only():
+    """dr_vanilla_fused_pass refuses a split outside 1..DR_VANILLA_MAX_SPLIT and
+    missing sync / wpack buffers before touching the GPU; the fragment-order
+    weight buffer has a fixed size; dr_param_table.slab_rows is the field the
+    split's partial rows are summed by."""
+    lib = _lib.load()
+    wpack = int(lib.dr_vanilla_wpack_floats())
+    assert wpack > 0 and wpack % 64 == 0
+    st, w, p = _lib.GraphStoreC(), _lib.VanillaWeightsC(), _lib.PassC()
+    p.out_dim = 1
+    st.n_feat, st.x_stride, st.n_edge_feat = 30, 32, 3
+    dummy = ctypes.c_void_p(16)  # never dereferenced: the checks return first
+    for split, sync, wp in [(0, dummy, dummy), (5, dummy, dummy), (4, None, dummy), (4, dummy, None)]:
+        rc = lib.dr_vanilla_fused_pass(ctypes.byref(st), dummy, 8, ctypes.byref(w), ctypes.byref(p), dummy, dummy, split, sync, wp, 1024, None)
+        assert rc == -1, (split, sync, wp, rc)  # DR_E_ARG
+    assert [f for f, _ in _lib.ParamTableC._fields_][-1] == "slab_rows"
