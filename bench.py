@@ -475,7 +475,7 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
     ms_step = elapsed / args.steps * 1e3
     wall_gbs = (alg + adam_bytes) / (ms_step * 1e-3) / 1e9
     default_cfg = args.model == "ginet" and args.graphs == "residue" and B == B_PER_GPU and args.dtype == "f32"
-    pmc_cfg = default_cfg or (args.model in ("foutnet", "sgat") and args.graphs == "residue" and B == B_PER_GPU)
+    pmc_cfg = default_cfg or (args.model in ("foutnet", "sgat", "vanilla") and args.graphs == "residue" and B == B_PER_GPU and args.dtype == "f32")
     traffic, traffic_src = pmc_traffic_bytes(args.model) if pmc_cfg else (None, None)
     large = args.model == "ginet" and (bool(args.force_large) or args.ginet_path != "auto" or args.dtype == "bf16" or any(h.lds((step.spec.entry, 1), lambda *sz: 0) > 160 * 1024 for h in handles))
     copy_gbs = None if args.no_stream_copy else stream_copy_gbs(dev)
