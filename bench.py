@@ -146,6 +146,82 @@ def design_bytes(packed, gids, model="ginet", out_dim=1):
     return int((2 * part + extra).sum())
 
 
+MFMA_PEAK_TFLOPS = {"f32": 157.3, "bf16": 2500.0}  # dense MFMA peaks (MI355X_MICROARCH.md, chip-level parameters)
+MFMA_FLOP_PER_INST = 16 * 16 * 4 * 2  # v_mfma_f32_16x16x4_f32, the only MFMA shape of the fp32 graph kernels
+N_SIMDS = 256 * 4
+
+
+def algorithmic_flops(packed, gids, model="ginet"):
+    """Algorithmic FLOPs of one graph pass (fwd + bwd) over these graphs.
+    GINet: SURVEY §8(d)'s formula per graph, 3*(2*N*F*32) + 2*E*32 (the conv1
+    node GEMM forward and its two backward GEMMs, plus the edge aggregation;
+    §8(d) quotes ~0.96 MFLOP/graph, but the formula it states evaluates to
+    1.34 MFLOP at N=200, E=3000, F=30 — the formula is what is used here).
+    The other models by the same recipe (their dense node GEMMs x3 + one
+    multiply-add per aggregated element):
+    FoutNet/SGAT 3*(2*N*2F*16) + 2*E*F; ginet_nocluster adds conv2 on the
+    full graph, 3*(2*N*32*64) + 2*E*32; VanillaNetwork per layer
+    3*(2*N*F*64 + 2*N*(F+32)*F) + 2*E*32*(Fe+2)."""
+    n, e, *_ = (a[gids] for a in packed.sizes())
+    f = packed.n_feat
+    if model == "ginet":
+        per = 3 * (2 * n * f * 32) + 2 * e * 32
+    elif model in ("foutnet", "sgat"):
+        per = 3 * (2 * n * 2 * f * 16) + 2 * e * f
+    elif model == "ginet_nocluster":
+        per = 3 * (2 * n * f * 32) + 2 * e * 32 + 3 * (2 * n * 32 * 64) + 2 * e * 32
+    else:  # vanilla
+        fe = 0 if packed.edge_attr is None else packed.edge_attr.shape[1]
+        per = 2 * (3 * (2 * n * f * 64 + 2 * n * (f + 32) * f) + 2 * e * 32 * (fe + 2))
+    return int(per.sum())
+
+
+def pmc_mfma(model, kernel_ms, n_wg):
+    """MFMA utilisation of the dominant kernel from the newest committed PMC pass
+    (profiles/*/pmc_mfma_<model>.txt, scripts/gpu_pmc_mfma.sh: one rocprofv3
+    --pmc run of SQ_VALU_MFMA_BUSY_CYCLES, SQ_INSTS_MFMA, SQ_BUSY_CU_CYCLES,
+    GRBM_GUI_ACTIVE, median over dispatches).
+    * executed MFMA FLOPs = SQ_INSTS_MFMA x 2048 (16x16x4 f32), priced against
+      this run's kernel time and the fp32 MFMA peak;
+    * busy fractions: SQ_VALU_MFMA_BUSY_CYCLES (matrix-pipe busy cycles summed
+      over SIMDs) / (kernel cycles x SIMDs), kernel cycles = GRBM_GUI_ACTIVE / 8
+      (summed over the 8 XCDs; reads high on short dispatches, so the
+      fractions are lower bounds), over the whole chip (1024 SIMDs) and over
+      the SIMDs of the CUs the launch occupies (one workgroup per CU)."""
+    import glob  # noqa: PLC0415
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"pmc_mfma_{model}.txt")))
+    if not files:
+        return None
+    vals = {}
+    for line in open(files[-1]):
+        parts = line.split()
+        if len(parts) >= 2:
+            try:
+                vals[parts[0]] = float(parts[1])
+            except ValueError:
+                pass
+    need = ("SQ_INSTS_MFMA", "SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE")
+    if any(k not in vals for k in need):
+        return None
+    cyc = vals["GRBM_GUI_ACTIVE"] / 8.0
+    busy = vals["SQ_VALU_MFMA_BUSY_CYCLES"]
+    exec_flops = vals["SQ_INSTS_MFMA"] * MFMA_FLOP_PER_INST
+    tf = exec_flops / (kernel_ms * 1e-3) / 1e12
+    return {
+        "source": os.path.relpath(files[-1], ROOT),
+        "insts_per_launch": vals["SQ_INSTS_MFMA"],
+        "executed_flops_per_launch": exec_flops,
+        "executed_tflops": round(tf, 4),
+        "executed_frac_of_peak": round(tf / MFMA_PEAK_TFLOPS["f32"], 6),
+        "busy_cycles": busy,
+        "kernel_cycles_grbm": cyc,
+        "mfma_busy_frac": round(busy / (cyc * N_SIMDS), 6),
+        "mfma_busy_frac_active_simds": round(busy / (cyc * 4 * min(256, n_wg)), 6),
+        "active_cus": min(256, n_wg),
+    }
+
+
 PMC_FILES = {"ginet": "pmc_ginet_graph_kernel.txt", "foutnet": "pmc_foutnet_graph_kernel.txt", "sgat": "pmc_sgat_graph_kernel.txt", "vanilla": "pmc_vanilla_graph_kernel.txt"}
 
 
@@ -479,6 +555,16 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
     traffic, traffic_src = pmc_traffic_bytes(args.model) if pmc_cfg else (None, None)
     large = args.model == "ginet" and (bool(args.force_large) or args.ginet_path != "auto" or args.dtype == "bf16" or any(h.lds((step.spec.entry, 1), lambda *sz: 0) > 160 * 1024 for h in handles))
     copy_gbs = None if args.no_stream_copy else stream_copy_gbs(dev)
+    # §8(d) FLOP side: algorithmic FLOPs per launch against the dense MFMA peak
+    # of the compute dtype, and MFMA utilisation from the committed PMC pass
+    flops = float(np.mean([algorithmic_flops(packed, h.gids_host, args.model) for h in handles]))
+    tflops = flops / (kernel_ms * 1e-3) / 1e12
+    n_wg = B
+    if args.model == "vanilla" and not layer_path:
+        from deeprank2_amd.neuralnets.gnn.vanilla_gnn import split_k  # noqa: PLC0415
+
+        n_wg = B * split_k(handles[0], 30, 3)
+    mfma = pmc_mfma(args.model, kernel_ms, n_wg) if pmc_cfg else None
 
     result = None
     if rank == 0:
@@ -532,6 +618,12 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
                 "kernel_timing": "wall clock per eager step (layer-level path)" if layer_path else f"HIP events around one HIP graph of {args.steps} back-to-back {('dr_ginet_train_step' if one else step.spec.entry) if not large else 'dr_ginet_large_pass'} launches on the launch stream, divided by {args.steps}",
                 "stream_copy_GBs": None if copy_gbs is None else round(copy_gbs, 1),
                 "frac_of_stream_copy": None if copy_gbs is None else round(achieved / copy_gbs, 5),
+                "flops_per_launch": int(flops),
+                "flops_definition": "algorithmic FLOPs of one graph pass (fwd+bwd), bench.algorithmic_flops: GINet 3*(2*N*F*32) + 2*E*32 per graph (SURVEY §8(d) formula)",
+                "achieved_tflops": round(tflops, 4),
+                "mfma_peak_tflops": MFMA_PEAK_TFLOPS[args.dtype],
+                "flop_frac": round(tflops / MFMA_PEAK_TFLOPS[args.dtype], 6),
+                "mfma": mfma,
                 "wallclock": {"bytes_per_step": int(alg + adam_bytes), "achieved": round(wall_gbs, 2), "frac": round(wall_gbs / HBM_PEAK_GBS, 5), "note": "B_alg(step) = sum_g B_alg(g) + 28*P (Adam fp32) over ms_per_step"},
             },
             "launch": ("eager" + capture_note) if captured is None else f"hipgraph-replay ({n_sweeps} x {len(handles)}-step sweep graph + " + (f"one {n_rest}-step graph" if rest is not None else f"{n_rest} per-step graphs") + f"{', RCCL all-reduce captured' if pg is not None else ''})",

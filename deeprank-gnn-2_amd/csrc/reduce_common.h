@@ -47,7 +47,7 @@ struct alignas(64) ReduceHdr {
   float lr, beta1, beta2, eps, weight_decay, bias_c1, bias_c2_sqrt, pad1;
   float log2_beta1, log2_beta2;  // beta^t = exp2(t log2 beta): one v_exp_f32, not powf
   int32_t n_params, n_blocks;
-  int16_t blk0[18];  // first block of each parameter (prefix sums of ceil(numel / RP)), blk0[n_params] = n_blocks
+  int16_t blk0[DR_MAX_PARAMS + 1];  // first block of each parameter (prefix sums of ceil(numel / RP)), blk0[n_params] = n_blocks
   int32_t slab_rows;  // slab rows per graph (>= 1): a slab-kind gradient sums B * slab_rows rows
 };
 
@@ -228,7 +228,7 @@ inline int build_reduce(const dr_param_table* t, const float* slab, const float*
     blocks += (t->numel[i] + RP - 1) / RP;
   }
   if (blocks > 32767) return DR_E_UNSUPPORTED;
-  for (int i = t->n_params; i < 18; ++i) h.blk0[i] = (int16_t)blocks;
+  for (int i = t->n_params; i <= DR_MAX_PARAMS; ++i) h.blk0[i] = (int16_t)blocks;
   h.n_params = t->n_params;
   h.n_blocks = blocks;
   if (t->slab_rows < 0 || t->slab_rows > 64) return DR_E_ARG;

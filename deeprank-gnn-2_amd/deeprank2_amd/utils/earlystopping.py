@@ -6,10 +6,12 @@ reference's ``tests/utils/test_earlystopping.py`` cases, restated in
 Two independent triggers, evaluated once per epoch:
 
 * stall: an epoch whose validation loss is above ``best - delta`` is a
-  stalled epoch (equal counts as progress); ``patience`` stalled epochs in a row stop training.  A
-  non-stalled epoch resets the run.  ``best`` is the lowest validation loss
-  seen so far (it also moves down on a stalled epoch whose loss is below it
-  by less than ``delta``).
+  stalled epoch (equal counts as progress); ``patience`` stalled epochs in a
+  row stop training.  A non-stalled epoch resets the run.  ``best`` is the
+  lowest validation loss seen so far (it also moves down on a stalled epoch
+  whose loss is below it by less than ``delta``); a NaN validation loss
+  resets the run and makes the next epoch count as progress, as in the
+  reference.
 * overfitting: after ``min_epoch``, a validation loss above the training loss
   by more than ``maxgap`` stops training at once.
 """
@@ -29,34 +31,34 @@ class EarlyStopping:
         self.trace_func = trace_func
         self.early_stop = False
         self.counter = 0  # stalled epochs in the current run
-        self.val_loss_min = None  # lowest validation loss so far
+        self.best_score = None  # the negated best validation loss (NaN after a NaN epoch, as the reference)
+        self.val_loss_min = None  # the validation loss that set best_score
 
-    @property
-    def best_score(self):
-        """The reference keeps the negated best loss under this name."""
-        return None if self.val_loss_min is None else -self.val_loss_min
-
-    def _stalled(self, val_loss: float) -> bool:
-        return val_loss > self.val_loss_min - self.delta
+    def _stall(self, epoch, val_loss):
+        self.counter += 1
+        if self.verbose:
+            margin = f"by more than {self.delta} " if self.delta else ""
+            self.trace_func(f"Validation loss did not decrease {margin}({self.val_loss_min:.6f} --> {val_loss:.6f}); stalled epochs: {self.counter} of {self.patience}")
+        if self.counter >= self.patience:
+            self.trace_func(f"EarlyStopping activated at epoch # {epoch}: no improvement for {self.patience} epochs (patience reached).")
+            self.early_stop = True
 
     def __call__(self, epoch: int, val_loss: float, train_loss: float | None = None):
-        first = self.val_loss_min is None
-        if not first:
-            previous = self.val_loss_min
-            if self._stalled(val_loss):
-                self.counter += 1
-                if self.verbose:
-                    margin = f"by more than {self.delta} " if self.delta else ""
-                    self.trace_func(f"Validation loss did not decrease {margin}({previous:.6f} --> {val_loss:.6f}); stalled epochs: {self.counter} of {self.patience}")
-                if self.counter >= self.patience:
-                    self.trace_func(f"EarlyStopping activated at epoch # {epoch}: no improvement for {self.patience} epochs (patience reached).")
-                    self.early_stop = True
-            else:
-                self.counter = 0
-                if self.verbose:
-                    self.trace_func(f"Validation loss decreased ({previous:.6f} --> {val_loss:.6f}).")
-        if first or val_loss <= self.val_loss_min:
-            self.val_loss_min = val_loss
+        # The comparisons run on the negated loss exactly as the reference's
+        # (earlystopping.py:47-70), so a NaN loss behaves the same: it is
+        # never "stalled" (NaN < x is False), it resets the run and leaves
+        # best_score NaN, and the next finite epoch then always counts as progress.
+        score = -val_loss
+        if self.best_score is None:
+            self.best_score, self.val_loss_min = score, val_loss
+        elif score < self.best_score + self.delta:
+            self._stall(epoch, val_loss)
+        else:
+            if self.verbose:
+                self.trace_func(f"Validation loss decreased ({self.val_loss_min:.6f} --> {val_loss:.6f}).")
+            self.best_score, self.counter = score, 0
+        if score >= self.best_score:
+            self.best_score, self.val_loss_min = score, val_loss
         self._check_gap(epoch, val_loss, train_loss)
 
     def _check_gap(self, epoch, val_loss, train_loss):

@@ -124,3 +124,24 @@ def test_early_stopping_reference_known_answers():
     assert _stop_epoch(patience=3) == 7
     assert _stop_epoch(patience=3, delta=1) == 5
     assert _stop_epoch(maxgap=1) == 9
+
+
+def test_early_stopping_nan_loss_as_reference():
+    """A NaN validation loss (reference earlystopping.py:47-70 on the negated
+    score): not a stall, resets the run, best_score becomes NaN, and the next
+    finite epoch counts as progress whatever its value."""
+    es = EarlyStopping(patience=2, verbose=False, trace_func=lambda *_: None)
+    es(1, 1.0)
+    es(2, 2.0)
+    assert es.counter == 1
+    es(3, float("nan"))
+    assert es.counter == 0 and es.best_score != es.best_score and es.val_loss_min == 1.0
+    es(4, 5.0)  # worse than 1.0, still progress after the NaN epoch
+    assert es.counter == 0 and es.best_score == -5.0 and es.val_loss_min == 5.0
+    es(5, 6.0)
+    es(6, 7.0)
+    assert es.early_stop
+    es = EarlyStopping(patience=2, verbose=False, trace_func=lambda *_: None)
+    es(1, float("nan"))  # a NaN first epoch
+    es(2, 3.0)
+    assert es.counter == 0 and es.val_loss_min == 3.0
