@@ -821,7 +821,9 @@ __global__ void __launch_bounds__(NT) ginet_step_kernel(GinetStepArgs a) {
     const uint32_t d = __hip_atomic_fetch_add(passed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (d == (uint32_t)a.NR - 1) {  // the last reducer past the poll: new step, counters back to zero
       a.g.p.step_counter[0] = t;
-      __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // minus B, not := 0: after a give-up, graph workgroups still arriving in
+      // this launch bring it back to exactly 0 by the launch's end
+      __hip_atomic_fetch_sub(arrive, (uint32_t)B, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(passed, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     sw[0] = ok && !a.diag ? t : -1;

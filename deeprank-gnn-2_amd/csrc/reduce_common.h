@@ -42,6 +42,7 @@ struct alignas(64) ReduceHdr {
   float* loss_out;
   int64_t* step_counter;
   const float* grad_div;
+  const uint32_t* fault;  // dr_adam.fault: nonzero -> NaN loss / gradients, no update
   int32_t B, slab_stride, head_stride, adam_enabled;
   float loss_scale, pad0;
   float lr, beta1, beta2, eps, weight_decay, bias_c1, bias_c2_sqrt, pad1;
@@ -81,11 +82,16 @@ __device__ __forceinline__ void reduce_block(const ReduceHdr& h, const ParamRec&
   const int lp = t % RP, ch = t / RP;
   const int e = elem_block * RP + lp;
   const bool live = e < r.numel;
+  // a graph pass whose in-launch hand-off gave up (dr_pass.fault): its
+  // partials are wrong, so the step reports NaN and changes no state
+  const bool bad = !LEAN && h.fault && *h.fault != 0u;
   if (first && t < 64 && h.lpg && h.loss_out) {
     float acc = 0.f;  // lane-strided partial sums, then a fixed-order wave reduction
     for (int b = t; b < h.B; b += 64) acc += ld_part<LD>(h.lpg + b);
     acc = dr_wave_sum(acc);
-    if (t == 0) h.loss_out[0] = acc * h.loss_scale;
+    if (t == 0) h.loss_out[0] = bad ? __builtin_nanf("") : acc * h.loss_scale;
+  } else if (bad && first && t == 0 && h.loss_out) {
+    h.loss_out[0] = __builtin_nanf("");
   }
   const int ec = live ? e : 0;
   const bool slab_kind = r.kind == DR_GRAD_SLAB, outer = r.kind == DR_GRAD_OUTER;
@@ -105,7 +111,7 @@ __device__ __forceinline__ void reduce_block(const ReduceHdr& h, const ParamRec&
       w[k] = outer ? ld_part<LD>(base + row * st + col2) : 1.f;
     }
   }
-  const bool upd = live && ch == 0 && (LEAN || h.adam_enabled);
+  const bool upd = live && ch == 0 && (LEAN || h.adam_enabled) && !bad;
   float p0 = 0.f, m0 = 0.f, v0 = 0.f, gin = 0.f;
   if (ch == 0 && (LEAN || h.adam_enabled) && r.numel > 0) {  // numel 0: an empty record (no pointers)
     p0 = r.param[ec];
@@ -147,6 +153,7 @@ __device__ __forceinline__ void reduce_block(const ReduceHdr& h, const ParamRec&
     gsum = 0.f;
 #pragma unroll
     for (int k = 0; k < RC; ++k) gsum += part[k][lp];
+    if (bad) gsum = __builtin_nanf("");
     if (r.grad) r.grad[e] = gsum;
   } else {  // gradients supplied (e.g. after an RCCL all-reduce): Adam only
     gsum = gin;
@@ -155,6 +162,7 @@ __device__ __forceinline__ void reduce_block(const ReduceHdr& h, const ParamRec&
       r.grad[e] = gsum;
       if (first && lp == 0 && h.loss_out) h.loss_out[0] = h.loss_out[0] / div;
     }
+    if (bad) r.grad[e] = __builtin_nanf("");
   }
   if (upd) {
     float bc1 = h.bias_c1, bc2s = h.bias_c2_sqrt;
@@ -192,6 +200,7 @@ inline int build_reduce(const dr_param_table* t, const float* slab, const float*
   h.loss_out = loss_out;
   h.step_counter = adam->step_counter;
   h.grad_div = adam->grad_div;
+  h.fault = adam->fault;
   h.B = n_batch;
   h.slab_stride = t->slab_stride;
   h.head_stride = t->head_stride;

@@ -832,6 +832,9 @@ extern "C" int dr_vanilla_graph_pass(const dr_graph_store* store, const dr_graph
   if ((pass->flags & DR_PASS_BACKWARD) && (!scratch->part || !scratch->chunk_first || !scratch->chunk_slot))
     return DR_E_ARG;
   if (pass->use_dropout != DR_DROPOUT_OFF) return DR_E_UNSUPPORTED;
+  // no in-launch hand-offs here: the pass never faults, but it clears the
+  // caller's per-launch flag like every pass that takes one (dr_pass.fault)
+  if (pass->fault) DR_CHECK(hipMemsetAsync(pass->fault, 0, sizeof(uint32_t), (hipStream_t)stream));
   if (n_batch == 0) return DR_OK;
   VA a;
   a.s = *store;

@@ -147,18 +147,25 @@ __device__ __forceinline__ uint64_t ld_sc1_u64(const float* p) {
 // stores, then one lane arrives on the graph's counter and polls it (sc1)
 // until all k siblings have arrived at this hand-off; the counter only grows
 // within a launch (the h-th hand-off completes at h*k), so arrival v waits for
-// (v / k + 1) * k.  Bounded: a wait that gives up sets the timeout flag
-// (sync[2B], read by the host through BatchHandle.vanilla_sync_ok()) and goes
-// on with wrong results rather than hanging the launch.
-__device__ __forceinline__ void sib_handoff(uint32_t* ctr, uint32_t* flag, int k) {
+// (v / k + 1) * k.  Bounded (limit polls): a wait that gives up goes on with
+// wrong results rather than hanging the launch, and says so: the batch's
+// sticky flag sync[2B] (BatchHandle.vanilla_sync_ok), and when the caller
+// passed dr_pass.fault, fault[0] = 1 for this launch (the reduce then
+// withholds the update and reports a NaN loss) and fault[1] += 1 (read by the
+// host once per epoch, FusedTrainStep.check_faults).
+__device__ __forceinline__ void sib_handoff(uint32_t* ctr, uint32_t* flag, uint32_t* fault, int limit, int k) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t v = __hip_atomic_fetch_add((gu32*)ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t target = (v / (uint32_t)k + 1u) * (uint32_t)k;
     for (int spin = 0; ld_sc1_u32(ctr) < target; ++spin) {
-      if (spin > (1 << 22)) {
+      if (spin >= limit) {
         __hip_atomic_store((gu32*)flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (fault) {
+          __hip_atomic_store((gu32*)fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add((gu32*)(fault + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -246,6 +253,7 @@ constexpr int ROW_BASE = op_base(N_OPS), ROWPACK = 2 * 64 * (16 + 4 + 1), WPACK_
 struct PackArgs {
   dr_vanilla_weights w;
   float* out;
+  uint32_t* fault;  // dr_pass.fault: [0] cleared for the graph launch that follows
   int32_t F, Fe;
 };
 
@@ -291,6 +299,7 @@ __device__ float pack_value(const PackArgs& a, int e) {
 __global__ void __launch_bounds__(256) vanilla_pack_kernel(PackArgs a) {
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (e < WPACK_FLOATS) a.out[e] = pack_value(a, e);
+  if (e == 0 && a.fault) a.fault[0] = 0u;  // stream order: cleared before the graph launch starts
 }
 
 // C[M, 32] = A[M, K] W[K, 32], K = 32 * NK, on v_mfma_f32_16x16x4_f32.  Wave w
@@ -649,6 +658,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   uint32_t* ctr = a.sync + 2 * b;
   uint32_t* tflag = a.sync + 2 * a.B;
   const bool split = k > 1;
+  const int spin_limit = a.p.spin_limit > 0 ? a.p.spin_limit : (1 << 22);
   const int LG = 32 * KE + 32 + F * KN + F;  // one layer's gradient entries in the slab
   float* slab = p.slab ? p.slab + ((int64_t)b * k + rk) * DR_VANILLA_SLAB_STRIDE(F, Fe) : nullptr;
   const bool bwd = (p.flags & DR_PASS_BACKWARD) != 0;
@@ -727,7 +737,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   if (split) {  // hand-off 1: every sibling's B2 rows (and the layer-1 ReLU words)
     publish_rows(P, XA, r0, r1);
     VSTAMP(19);
-    sib_handoff(ctr, tflag, k);
+    sib_handoff(ctr, tflag, a.p.fault, spin_limit, k);
     gather_rows(P, XA, N, r0, r1);
     __syncthreads();
   }
@@ -773,7 +783,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   }
   if (split) {  // hand-off 2: the siblings' column sums (and the layer-2 ReLU words)
     VSTAMP(20);
-    sib_handoff(ctr, tflag, k);
+    sib_handoff(ctr, tflag, a.p.fault, spin_limit, k);
     if (tid < 32) {
       float t = ld_sc1(csum + tid);
       for (int q = 1; q < k; ++q) t += ld_sc1(csum + q * 32 + tid);
@@ -893,7 +903,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   if (split) {  // hand-off 3: every sibling's dS2 rows (the transposed pass gathers them by source)
     publish_rows(P, XB, r0, r1);
     VSTAMP(21);
-    sib_handoff(ctr, tflag, k);
+    sib_handoff(ctr, tflag, a.p.fault, spin_limit, k);
     gather_rows(P, XB, N, r0, r1);
   }
   VSTAMP(10);
@@ -942,7 +952,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   if (split) {  // hand-off 4: every sibling's dS1 rows
     publish_rows(T, XA, r0, r1);
     VSTAMP(22);
-    sib_handoff(ctr, tflag, k);
+    sib_handoff(ctr, tflag, a.p.fault, spin_limit, k);
     sib_exit(ctr, k);
     gather_rows(T, XA, N, r0, r1);
   }
@@ -1038,6 +1048,7 @@ extern "C" int dr_vanilla_fused_pass(const dr_graph_store* store, const dr_graph
     PackArgs pa;
     pa.w = *w;
     pa.out = wpack;
+    pa.fault = pass->fault;
     pa.F = store->n_feat;
     pa.Fe = store->n_edge_feat;
     hipLaunchKernelGGL(vanilla_pack_kernel, dim3((WPACK_FLOATS + 255) / 256), dim3(256), 0, (hipStream_t)stream, pa);

@@ -161,6 +161,9 @@ class PassC(ctypes.Structure):
         ("head", VP),
         ("stamps", VP),
         ("step_counter", VP),
+        ("fault", VP),
+        ("spin_limit", ctypes.c_int32),
+        ("pad0", ctypes.c_int32),
     ]
 
 
@@ -176,6 +179,7 @@ class AdamC(ctypes.Structure):
         ("enabled", ctypes.c_int32),
         ("step_counter", VP),
         ("grad_div", VP),
+        ("fault", VP),
     ]
 
 

@@ -19,7 +19,10 @@ Deliberate differences (documented in DESIGN.md): ``target_filter``
 conditions are parsed (``">15"``, ``"<=0.5"`` ...) instead of ``eval``-ed;
 ``classes`` passed explicitly for a classification task are honoured (the
 reference leaves ``self.classes`` unset in that case); pre-trained
-``train_source`` files are read with ``torch.load(weights_only=True)``.
+``train_source`` files are read with ``torch.load(weights_only=True)``, or
+(reference checkpoints, which pickle optimizer classes with dill) by the
+inert opcode reader of ``io.checkpoint``; stored transform lambdas are parsed,
+not ``eval``-ed.
 """
 
 from __future__ import annotations
@@ -37,6 +40,7 @@ import torch
 
 from deeprank2_amd.data import Batch, Data
 from deeprank2_amd.io import hdf5
+from deeprank2_amd.io.checkpoint import load_checkpoint, transform_from_source
 
 _log = logging.getLogger(__name__)
 
@@ -231,9 +235,9 @@ class GraphDataset:
         src = self.train_source
         if isinstance(src, str):
             try:
-                data = torch.load(src, map_location="cpu", weights_only=True)
+                data = load_checkpoint(src)
             except Exception as e:
-                msg = f"The path provided to `train_source` ({src}) is not a DeepRank2 model this package can read safely (weights_only load failed: {e})."
+                msg = f"The path provided to `train_source` ({src}) is not a DeepRank2 model this package can read ({e})."
                 raise ValueError(msg) from e
             if data.get("data_type") not in ("GraphDataset", GraphDataset):
                 msg = f"The pre-trained model has been trained with data of type {data.get('data_type')}; a GraphDataset needs a graph model."
@@ -243,7 +247,7 @@ class GraphDataset:
             if data.get("features_transform"):
                 for v in data["features_transform"].values():
                     if isinstance(v.get("transform"), str):
-                        v["transform"] = eval(v["transform"])  # noqa: S307  (a lambda source string, as the reference does)
+                        v["transform"] = transform_from_source(v["transform"])  # the reference eval()s it; parsed here
         elif isinstance(src, GraphDataset):
             data = src
             self.train_means = src.means

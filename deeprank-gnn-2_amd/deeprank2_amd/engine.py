@@ -66,14 +66,24 @@ class FusedTrainStep:
         numel = [p.numel() for p in self.params]
         # gradients, the loss and (weighted CE, N>1) the batch's class-weight sum
         # share one buffer: one all-reduce per step (N>1)
-        self.flat = torch.zeros(sum(numel) + 2, dtype=torch.float32, device=dev)
-        self.flat_grad = self.flat[:-2]
+        # (models whose graph pass has in-launch hand-offs: + the pass's fault flag,
+        # so a give-up on any rank withholds the update on every rank)
+        self.handoffs = bool(getattr(self.spec, "handoffs", False))
+        extra = 3 if self.handoffs else 2
+        self.flat = torch.zeros(sum(numel) + extra, dtype=torch.float32, device=dev)
+        self.flat_grad = self.flat[: sum(numel)]
         self.grads = [g.view_as(p) for g, p in zip(torch.split(self.flat_grad, numel), self.params)]
         self.states = [(torch.zeros_like(p), torch.zeros_like(p)) for p in self.params]
         self.counter = torch.zeros(2, dtype=torch.int64, device=dev)  # [steps done = dropout offset, snapshot]
         self.step_count = 0
-        self.loss_out = self.flat[-2:-1]
-        self.wsum = self.flat[-1:]
+        self.loss_out = self.flat[sum(numel) : sum(numel) + 1]
+        self.wsum = self.flat[sum(numel) + 1 : sum(numel) + 2]
+        self.flat_fault = self.flat[sum(numel) + 2 :]  # (handoffs) fault[0] of this rank, summed over ranks
+        # dr_pass.fault: [0] = this step's graph pass gave up a hand-off (cleared
+        # by every launch), [1] = such launches since the last check_faults();
+        # fault_red: [0] after the all-reduce (N>1)
+        self.fault = torch.zeros(2, dtype=torch.int32, device=dev)
+        self.fault_red = torch.zeros(1, dtype=torch.int32, device=dev)
         # weighted CE with N>1: the graph pass runs unnormalised and Adam divides
         # by the all-reduced weight sum (dr_adam.grad_div)
         self.device_div = self.loss == "ce" and self.class_weights is not None and self.world > 1
@@ -118,6 +128,7 @@ class FusedTrainStep:
         p.head = self.head.data_ptr()
         p.step_counter = self.counter.data_ptr()
         p.compute_dtype = _lib.DR_DTYPE_BF16 if self.compute_dtype == "bf16" else _lib.DR_DTYPE_F32
+        p.fault = self.fault.data_ptr()
         self._pass = p
         self._pass_nodrop = _lib.PassC.from_buffer_copy(p)
         self._pass_nodrop.use_dropout = _lib.DR_DROPOUT_OFF
@@ -127,9 +138,13 @@ class FusedTrainStep:
         a.lr, (a.beta1, a.beta2), a.eps, a.weight_decay = self.lr, self.betas, self.eps, self.weight_decay
         a.enabled = 1
         a.step_counter = self.counter.data_ptr()
+        # world of one: this step's own flag; N>1: the all-reduced one (the
+        # partial reduce before the all-reduce NaNs the rank's gradients)
+        a.fault = (self.fault if self.pg is None else self.fault_red).data_ptr()
         self._adam = a
         self._adam_off = _lib.AdamC.from_buffer_copy(a)
         self._adam_off.enabled = 0
+        self._adam_off.fault = self.fault.data_ptr()
         self._adam_div = _lib.AdamC.from_buffer_copy(a)
         self._adam_div.grad_div = self.wsum.data_ptr()
 
@@ -205,9 +220,52 @@ class FusedTrainStep:
             _lib.check(lib.dr_reduce_update(self._table, slab, head, h.B, self._adam_off, lpg, scale, lout, stream), "dr_reduce_update")
             if self.device_div:
                 self._local_wsum(h)
+            if self.handoffs:
+                self.flat_fault.copy_(self.fault[:1])
             torch.distributed.all_reduce(self.flat, group=self.pg)
+            if self.handoffs:
+                self.fault_red.copy_(self.flat_fault)
             self._adam_after_allreduce()
         return self.loss_out, self.out[: h.B]
+
+    def step_empty(self):
+        """A rank whose shard of the global batch is empty (global batch smaller
+        than the world): zero gradients and loss into the all-reduce, then the
+        same Adam step as every other rank."""
+        if self.pg is None:
+            msg = "an empty batch only occurs as a data-parallel shard"
+            raise ValueError(msg)
+        with torch.no_grad():
+            self.flat.zero_()
+            self.fault[0].zero_()
+            self.counter[1].copy_(self.counter[0])  # the snapshot a graph pass would take
+        self.step_count += 1
+        torch.distributed.all_reduce(self.flat, group=self.pg)
+        if self.handoffs:
+            self.fault_red.copy_(self.flat_fault)
+        self._adam_after_allreduce()
+        return self.loss_out, self.out[:0]
+
+    def check_faults(self, reset=True):
+        """Raise RuntimeError if any graph pass since the last check gave up an
+        in-launch hand-off (VanillaNetwork split over workgroups whose siblings
+        were not co-resident): those steps reported a NaN loss and were not
+        applied.  One device read; ``Trainer`` calls it once per epoch."""
+        if self.fuse_update and int(self.sync[2].item()):
+            if reset:
+                self.sync[2].zero_()
+            msg = "a one-launch training step's reducer gave up waiting for the graph workgroups: that step's update was skipped"
+            raise RuntimeError(msg)
+        if not self.handoffs:
+            return
+        n = int(self.fault[1].item())
+        if reset:
+            self.fault[1].zero_()
+        if n:
+            msg = (f"{n} graph pass(es) of {type(self.model).__name__} gave up waiting for a sibling workgroup "
+                   "(in-launch hand-off timed out): those steps were skipped (NaN loss, no update). "
+                   "Run with BatchHandle.vanilla_split = 1, or keep other work off the GPU during training.")
+            raise RuntimeError(msg)
 
     def _layered_step(self, h: BatchHandle, scale, dropout, mask=None):
         """A batch the model's graph pass cannot hold, or (GINet) one with
@@ -282,7 +340,7 @@ class FusedTrainStep:
         self._build_structs()
 
     def _state_tensors(self):
-        return [*self.params, *[s for st in self.states for s in st], self.counter, self.flat]
+        return [*self.params, *[s for st in self.states for s in st], self.counter, self.flat, self.fault]
 
     def capture_sweep(self, handles, global_batch=None):
         """Capture one training step per handle, in order, into ONE HIP graph

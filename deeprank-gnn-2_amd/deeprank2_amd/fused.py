@@ -43,6 +43,7 @@ class BatchHandle:
         self.force_layers = False  # run the layer-level path (layered.py) even when the graph pass fits (diagnostic)
         self.vanilla_words = True  # Vanilla pipeline: forward ReLU words feed the backward (False: recomputed)
         self.vanilla_split = None  # Vanilla per-graph kernel: workgroups per graph (None: by batch size)
+        self.fault = None  # device uint32 [2] (dr_pass.fault) of the autograd path's passes, made on first use
 
     def lds(self, key, fn):
         """Dynamic LDS bytes for the largest graph of the batch (cached per model kind)."""
@@ -273,6 +274,7 @@ class FusedSpec:
     bf16: bool = False  # dr_pass.compute_dtype = DR_DTYPE_BF16 supported (runs on the large-graph path)
     attention: bool = False  # GINetConvLayer model: batches with non-finite inputs need the layer path
     step_entry: str | None = None  # one-launch training step (graph pass + reduce + Adam), world of one
+    handoffs: bool = False  # the graph pass hands rows between workgroups in-launch (dr_pass.fault can be set)
 
 
 def vanilla_fused_scratch_floats(n, e, fe):
@@ -284,7 +286,7 @@ def vanilla_fused_scratch_floats(n, e, fe):
     return (5 + 2 * fe) * r4(32 * np.asarray(n, dtype=np.int64)) + 2 * r4(np.asarray(e, dtype=np.int64) + 1) + 32 * 4
 
 
-def make_pass(out_dim, flags, *, dropout: Dropout | None = None, dout=None, loss_kind=_lib.DR_LOSS_NONE, loss_scale=1.0, class_w=None, out=None, loss_per_graph=None, slab=None, head=None, stamps=None, step_counter=None):
+def make_pass(out_dim, flags, *, dropout: Dropout | None = None, dout=None, loss_kind=_lib.DR_LOSS_NONE, loss_scale=1.0, class_w=None, out=None, loss_per_graph=None, slab=None, head=None, stamps=None, step_counter=None, fault=None, spin_limit=0):
     p = _lib.PassC()
     p.flags = flags
     p.out_dim = out_dim
@@ -310,6 +312,8 @@ def make_pass(out_dim, flags, *, dropout: Dropout | None = None, dout=None, loss
     p.head = _lib.ptr(head)
     p.stamps = _lib.ptr(stamps)
     p.step_counter = _lib.ptr(step_counter)
+    p.fault = _lib.ptr(fault)
+    p.spin_limit = int(spin_limit)
     return p
 
 
@@ -397,8 +401,10 @@ def slab_rows_for(spec: FusedSpec, h: BatchHandle) -> int:
     return 1 if spec.slab_k is None else int(spec.slab_k(h))
 
 
-def reduce_update(table, B, slab, head, device, adam=None, loss_per_graph=None, loss_scale=1.0, loss_out=None):
+def reduce_update(table, B, slab, head, device, adam=None, loss_per_graph=None, loss_scale=1.0, loss_out=None, fault=None):
     a = adam if adam is not None else _lib.AdamC()
+    if fault is not None:
+        a.fault = fault.data_ptr()
     rc = _lib.load().dr_reduce_update(table, _lib.ptr(slab), _lib.ptr(head), B, a, _lib.ptr(loss_per_graph), loss_scale, _lib.ptr(loss_out), _lib.stream_ptr(device))
     _lib.check(rc, "dr_reduce_update")
 
@@ -423,9 +429,14 @@ class FusedFn(torch.autograd.Function):
         f = h.store.n_feat
         slab = torch.empty(h.B * spec.slab_stride(f), dtype=torch.float32, device=dev)
         head = torch.zeros(h.B * spec.head_stride(out_dim), dtype=torch.float32, device=dev)
-        run_pass(spec, h, params, make_pass(out_dim, _lib.DR_PASS_BACKWARD, dropout=ctx.dropout, dout=dout.contiguous(), slab=slab, head=head))
+        fault = None
+        if spec.handoffs:  # a hand-off that gave up: NaN gradients rather than wrong ones
+            if h.fault is None:
+                h.fault = torch.zeros(2, dtype=torch.int32, device=dev)
+            fault = h.fault
+        run_pass(spec, h, params, make_pass(out_dim, _lib.DR_PASS_BACKWARD, dropout=ctx.dropout, dout=dout.contiguous(), slab=slab, head=head, fault=fault))
         grads = [torch.empty_like(p) for p in params]
         t = param_table(spec, params, grads, None, f, out_dim)
         t.slab_rows = slab_rows_for(spec, h)
-        reduce_update(t, h.B, slab, head, dev)
+        reduce_update(t, h.B, slab, head, dev, fault=fault)
         return (None, None, None, None, *grads)

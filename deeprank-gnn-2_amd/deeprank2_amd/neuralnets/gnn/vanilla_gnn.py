@@ -132,7 +132,7 @@ def make_spec(f, fe):
         lds = int(lib.dr_vanilla_lds_bytes(f, fe, p.out_dim))
         _lib.check(lib.dr_vanilla_graph_pass(st.cstruct(), h.descs.data_ptr(), h.B, w, p, sc, lds, _lib.stream_ptr(st.device)), "dr_vanilla_graph_pass")
 
-    return FusedSpec(PARAM_NAMES, recipe, slab_stride, head_stride, "dr_vanilla_graph_pass", weights, lambda *_: 0, dropout=0.0, run=run, slab_rows=MAX_SPLIT, slab_k=lambda h: split_k(h, f, fe))
+    return FusedSpec(PARAM_NAMES, recipe, slab_stride, head_stride, "dr_vanilla_graph_pass", weights, lambda *_: 0, dropout=0.0, run=run, slab_rows=MAX_SPLIT, slab_k=lambda h: split_k(h, f, fe), handoffs=True)
 
 
 FUSED_MAX_FE = 4  # vanilla_graph.hip MAXFE
@@ -159,7 +159,11 @@ def split_k(h: BatchHandle, f, fe):
     if not fused_fits(h, f, fe):
         return 1
     if h.vanilla_split is not None:
-        return int(h.vanilla_split)
+        k = int(h.vanilla_split)
+        if not 1 <= k <= MAX_SPLIT:
+            msg = f"vanilla_split must be in 1..{MAX_SPLIT} (got {k})"
+            raise ValueError(msg)
+        return k
     return max(1, min(MAX_SPLIT, _cus(h.store.device) // max(1, ((h.B + 7) // 8) * 8)))
 
 

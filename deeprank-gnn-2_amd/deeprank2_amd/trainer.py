@@ -47,6 +47,7 @@ from torch.nn.functional import softmax
 from deeprank2_amd.dataset import CLASSIF, REGRESS, GraphDataset
 from deeprank2_amd.distributed import shard_contiguous
 from deeprank2_amd.engine import FusedTrainStep
+from deeprank2_amd.io.checkpoint import load_checkpoint
 from deeprank2_amd.exporters import HDF5OutputExporter, OutputExporterCollection
 from deeprank2_amd.loader import DataLoader
 from deeprank2_amd.utils.earlystopping import EarlyStopping
@@ -343,7 +344,8 @@ class Trainer:
     def _local(self, idx):
         if self.process_group is None:
             return idx
-        return shard_contiguous(idx, torch.distributed.get_rank(), torch.distributed.get_world_size())
+        pg = self.process_group  # the group's own rank / size (a subgroup need not start at global rank 0)
+        return shard_contiguous(idx, torch.distributed.get_rank(pg), torch.distributed.get_world_size(pg))
 
     def _format_output(self, pred, target=None):
         """trainer.py:807-835."""
@@ -466,8 +468,10 @@ class Trainer:
             b = len(idx)
             if step is not None:
                 local = self._local(idx)
-                h = ds.batch_handle(local, dev)
-                loss, out = step.step(h, global_batch=b)
+                if len(local):
+                    loss, out = step.step(ds.batch_handle(local, dev), global_batch=b)
+                else:  # global batch smaller than the world
+                    loss, out = step.step_empty()
                 loss_sum += loss[0].double() * b
                 pred = out.clone()
                 if self.process_group is not None:
@@ -490,6 +494,8 @@ class Trainer:
             targets.append(y.detach())
             names += [ds.index_entries[i][1] for i in idx]
         epoch_loss = float(loss_sum.item()) / count if count else None
+        if step is not None:
+            step.check_faults()  # a skipped step (hand-off gave up) is an error, once per epoch
         out_l = torch.cat(outputs).cpu().numpy().tolist() if outputs else []
         tgt_l = torch.cat(targets).cpu().numpy().tolist() if targets else []
         dt = time() - t0
@@ -507,10 +513,14 @@ class Trainer:
         targets and loss."""
         pg = self.process_group
         local = self._local(idx)
-        batch = ds.batch(local).to(self.device)
         self.optimizer.zero_grad()
-        pred = self.model(batch)
-        pred_l, y_l = self._format_output(pred, batch.y)
+        if len(local):
+            batch = ds.batch(local).to(self.device)
+            pred = self.model(batch)
+            pred_l, y_l = self._format_output(pred, batch.y)
+        else:  # a global batch smaller than the world: this rank contributes zeros
+            pred = torch.zeros((0, self.output_shape), dtype=torch.float32, device=self.device)
+            pred_l = y_l = None
         y_all = ds._targets_of(idx)  # noqa: SLF001
         w = getattr(self.lossfunction, "weight", None)
         if w is not None and self.task == CLASSIF:
@@ -521,8 +531,11 @@ class Trainer:
             frac = float(wh[cls[local_pos]].sum()) / total if total else 0.0
         else:
             frac = len(local) / len(idx)
-        loss = self.lossfunction(pred_l, y_l) * frac if len(local) else pred.sum() * 0.0
-        loss.backward()
+        if len(local):
+            loss = self.lossfunction(pred_l, y_l) * frac
+            loss.backward()
+        else:
+            loss = torch.zeros((), dtype=torch.float32, device=self.device)
         params = [p for p in self.model.parameters() if p.requires_grad]
         flat = torch.cat([*(p.grad.reshape(-1) if p.grad is not None else torch.zeros(p.numel(), device=p.device) for p in params), loss.detach().reshape(1)])
         torch.distributed.all_reduce(flat, group=pg)
@@ -634,8 +647,8 @@ class Trainer:
         }
 
     def _load_params(self):
-        """trainer.py:873-908 (weights_only load)."""
-        state = torch.load(self.pretrained_model, map_location="cpu", weights_only=True)
+        """trainer.py:873-908 (weights_only load, or the inert reader for reference checkpoints)."""
+        state = load_checkpoint(self.pretrained_model)
         self.data_type = GraphDataset
         self.model_load_state_dict = state["model_state"]
         opt = state["optimizer"]

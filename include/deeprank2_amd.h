@@ -181,6 +181,15 @@ typedef struct dr_pass {
                            workgroup); workgroup 0 snapshots counter[0] into counter[1] for
                            dr_reduce_update, which advances counter[0].  Makes a
                            step's launch arguments constant (hipGraph replay).            */
+  uint32_t* fault;      /* optional device [2], passes with in-launch hand-offs between
+                           workgroups (dr_vanilla_fused_pass, split > 1): fault[0] is cleared
+                           at the start of every launch and set to 1 when one of its
+                           hand-off waits gave up (its partials are then wrong); fault[1]
+                           counts such launches and is only ever cleared by the caller.
+                           Hand the same pointer to dr_adam.fault so the step's update
+                           is withheld and its loss reads NaN.                            */
+  int32_t spin_limit;   /* polls before a hand-off wait gives up (<= 0: 1 << 22)        */
+  int32_t pad0;
 } dr_pass;
 
 /* One workgroup per graph: conv1 -> depth-0 community pooling -> conv2 ->
@@ -376,7 +385,8 @@ int64_t dr_vanilla_lds_bytes(int32_t n_feat, int32_t n_edge_feat, int32_t out_di
  * dr_vanilla_fused_scratch_floats(N_b, E_b) of them from scratch_off[b]
  * (device int64 [B]).  sync: device uint32 [2B + 1], zero when allocated and
  * left zero by every launch (arrival counters; sync[2B] = nonzero after a
- * hand-off wait gave up).  wpack: device floats [dr_vanilla_wpack_floats()],
+ * hand-off wait of any launch on this batch gave up; pass->fault reports it
+ * per launch, pass->spin_limit bounds the waits).  wpack: device floats [dr_vanilla_wpack_floats()],
  * rewritten by every call (the weights in MFMA-fragment order, packed by a
  * first small launch).  Needs the store's transpose + t_eid.               */
 #define DR_VANILLA_MAX_SPLIT 4
@@ -403,6 +413,10 @@ typedef struct dr_adam {
                             parallelism: the weighted mean's denominator
                             (trainer.py:688, nn.CrossEntropyLoss(weight)) is only known
                             after the all-reduce, so it travels in the reduced buffer  */
+  const uint32_t* fault; /* optional device flag (dr_pass.fault[0] of the graph pass whose
+                            partials this call reduces): when nonzero, loss_out[0] and every
+                            gradient written are NaN, and Adam leaves parameters, moments
+                            and the step counter unchanged                           */
 } dr_adam;
 
 /* How one parameter's gradient is assembled from the per-graph partials the

@@ -17,9 +17,10 @@ What it does:
    mask) and backward (MSE / CE losses) on seeded weights and stores inputs,
    weights, outputs, losses and every parameter gradient.
 
-Usage: ``python tests/golden/make_golden.py [siblings|nonfinite]`` (from the
-repo root; ``siblings`` regenerates only the SGAT / ginet_nocluster fixtures,
-``nonfinite`` only the non-finite-input GINet fixtures).
+Usage: ``python tests/golden/make_golden.py [siblings|nonfinite|pretrained]``
+(from the repo root; ``siblings`` regenerates only the SGAT / ginet_nocluster
+fixtures, ``nonfinite`` only the non-finite-input GINet fixtures,
+``pretrained`` only the reference's pre-trained VanillaNetwork on test.hdf5).
 """
 
 from __future__ import annotations
@@ -233,6 +234,36 @@ def main():  # noqa: PLR0915
     save("vanilla_synth", rec, {"F": 30, "Fe": 3, "out": 1, "loss": "mse"})
 
 
+PRETRAINED = f"{REF}/tests/data/pretrained/testing_graph_model.pth.tar"
+
+
+def main_pretrained():
+    """The reference's pre-trained VanillaNetwork (tests/data/pretrained/
+    testing_graph_model.pth.tar, read with the inert opcode reader of
+    deeprank2_amd.io.checkpoint: nothing from the file runs) on the reference's
+    test.hdf5, the graphs loaded as GraphDataset(test.hdf5, train_source=<that
+    checkpoint>) loads them (dataset.py:85-131 inheritance: its node / edge
+    features, transforms and the stored means / devs; load_one_graph restated in
+    oracle/data_ref): eval outputs as Trainer.test() computes them
+    (trainer.py:836-872), plus a CE loss and every gradient."""
+    from deeprank2_amd.io.checkpoint import load_checkpoint, transform_from_source  # noqa: PLC0415
+
+    st = load_checkpoint(PRETRAINED)
+    ft = {k: {"transform": transform_from_source(v["transform"]) if isinstance(v.get("transform"), str) else v.get("transform"), "standardize": v.get("standardize")} for k, v in st["features_transform"].items()}
+    means = {k: float(v) for k, v in st["means"].items()}
+    devs = {k: float(v) for k, v in st["devs"].items()}
+    dump_t = dump_hdf5("test")
+    tn = list(dump_t)
+    datas = [data_ref.load_one_graph(dump_t[n], n, st["node_features"], st["edge_features"], target=st["target"], features_transform=ft, means=means, devs=devs, task=st["task"]) for n in tn]
+    bat = P.Batch.from_data_list(datas)
+    f, fe = bat.x.shape[1], bat.edge_attr.shape[1]
+    model = ref_vanilla.VanillaNetwork(f, len(st["classes"]), fe)
+    model.load_state_dict(st["model_state"])
+    rec = batch_to_arrays(bat)
+    rec.update(run_model(model, bat, "ce"))
+    save("vanilla_pretrained_testhdf5", rec, {"F": f, "Fe": fe, "out": len(st["classes"]), "loss": "ce", "source": "tests/data/pretrained/testing_graph_model.pth.tar on tests/data/hdf5/test.hdf5 (train_source inheritance)", "node_features": st["node_features"], "edge_features": st["edge_features"]})
+
+
 def main_siblings():
     """SGAT (sgat.py) and ginet_nocluster.GINet goldens."""
     torch.set_num_threads(4)
@@ -364,6 +395,8 @@ def main_nonfinite():
 if __name__ == "__main__":
     if sys.argv[1:] == ["siblings"]:
         main_siblings()
+    elif sys.argv[1:] == ["pretrained"]:
+        main_pretrained()
     elif sys.argv[1:] == ["nonfinite"]:
         main_nonfinite()
     else:

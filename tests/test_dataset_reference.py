@@ -190,3 +190,68 @@ def test_invalid_train_source():
         GraphDataset(H5, train_source=H5)
     with pytest.raises(TypeError):
         GraphDataset(H5, train_source=3.0)
+
+
+PRETRAINED = "/root/reference/tests/data/pretrained/testing_graph_model.pth.tar"
+
+
+def test_reference_checkpoint_read_inert():
+    """The reference's pre-trained VanillaNetwork checkpoint (it pickles the
+    optimizer class with dill) read by the opcode reader: nothing from the
+    file runs; weights, optimizer state, standardisation and settings come out
+    as data (reference tests/test_trainer.py:661-700 load it with torch.load)."""
+    from deeprank2_amd.io.checkpoint import load_checkpoint, transform_from_source  # noqa: PLC0415
+    from deeprank2_amd.neuralnets.gnn.vanilla_gnn import VanillaNetwork  # noqa: PLC0415
+
+    st = load_checkpoint(PRETRAINED)
+    assert st["data_type"] == "GraphDataset" and st["optimizer"] == "Adam" and st["lossfunction"] == "CrossEntropyLoss"
+    assert st["task"] == "classif" and st["classes"] == [0, 1] and st["target"] == "binary"
+    assert st["node_features"] == ["bsa", "res_depth", "hse", "info_content", "pssm"] and st["edge_features"] == ["distance"]
+    assert float(st["means"]["bsa"]) == 0.8 and float(st["devs"]["pssm_18"]) == 3.0
+    m = VanillaNetwork(26, 2, 1)  # 26 node feature channels, 1 edge feature, 2 classes
+    m.load_state_dict(st["model_state"])  # every key and shape of the reference module
+    assert int(st["optimizer_state"]["state"][0]["step"]) == 50
+    torch_opt = __import__("torch").optim.Adam(m.parameters())
+    torch_opt.load_state_dict(st["optimizer_state"])
+    f = transform_from_source(st["features_transform"]["bsa"]["transform"])
+    x = np.array([0.0, 1.5, 7.0])
+    np.testing.assert_array_equal(f(x), np.log(x + 1))
+    for bad in ("lambda t: __import__('os')", "lambda t: t.__class__", "lambda t, u: t", "print(1)"):
+        with pytest.raises(ValueError):
+            transform_from_source(bad)
+
+
+def test_inherit_info_pretrained_model_graphdataset():
+    """reference tests/test_dataset.py:1191-1236: every inherited parameter comes
+    from the pre-trained model, also over explicitly conflicting arguments."""
+    from deeprank2_amd.io.checkpoint import load_checkpoint  # noqa: PLC0415
+
+    data = load_checkpoint(PRETRAINED)
+    for kw in ({}, dict(node_features="all", edge_features="all", features_transform=None, target="BA", target_transform=True, task="regress", classes=None)):
+        ds = GraphDataset(hdf5_path=H5, train_source=PRETRAINED, **kw)
+        mine = vars(ds)
+        for param in ds.inherited_params:
+            if param == "features_transform":
+                for item, key in data[param].items():
+                    assert mine[param][item]["transform"].source == key["transform"]
+                    assert mine[param][item]["standardize"] == key["standardize"]
+            else:
+                assert mine[param] == data[param], param
+        assert ds.means == data["means"] and ds.devs == data["devs"]
+
+
+def test_pretrained_inputs_match_golden():
+    """GraphDataset(test.hdf5, train_source=<the reference's pre-trained model>)
+    yields exactly the batch the golden ``vanilla_pretrained_testhdf5`` was made
+    from (its features, transforms and stored means / devs, applied as the
+    reference's load_one_graph does): with test_gpu_vanilla's check of the model
+    on that golden, the pre-trained path is pinned end to end."""
+    import os as _os  # noqa: PLC0415
+
+    z = np.load(_os.path.join(_os.path.dirname(__file__), "golden", "vanilla_pretrained_testhdf5.npz"))
+    ds = GraphDataset(hdf5_path=H5, train_source=PRETRAINED)
+    b = ds.batch(list(range(len(ds))))
+    np.testing.assert_array_equal(b.x.numpy(), z["in/x"])
+    np.testing.assert_array_equal(b.edge_index.numpy(), z["in/edge_index"])
+    np.testing.assert_array_equal(b.edge_attr.numpy(), z["in/edge_attr"])
+    np.testing.assert_array_equal(b.y.numpy(), z["in/y"])

@@ -10,7 +10,7 @@ import torch
 from _util import assert_grad_close, golden_batch, golden_grads, golden_state_dict
 
 from deeprank2_amd.engine import FusedTrainStep
-from deeprank2_amd.fused import BatchHandle
+from deeprank2_amd.fused import BatchHandle, resolve_batch
 from deeprank2_amd.neuralnets.gnn import vanilla_gnn as amd
 from deeprank2_amd.store import GraphStore, pack_graphs, records_from_batch
 from deeprank2_amd.utils.synthetic import make_dataset
@@ -51,6 +51,36 @@ def test_vanilla_module_vs_reference_golden(golden):
     ref = golden_grads(z)
     for n, p in m.named_parameters():
         assert_grad_close(p.grad.cpu().numpy(), ref[n], err_msg=n)
+
+
+def test_vanilla_pretrained_reference_weights_golden(golden):
+    """The reference's pre-trained VanillaNetwork (tests/data/pretrained/
+    testing_graph_model.pth.tar: F = 26 node channels, Fe = 1, 2 classes, CE)
+    on its test.hdf5 graphs (~11.7k directed edges each: the batch-wide
+    pipeline): Trainer.test()'s eval outputs, and a training step's CE loss and
+    gradients, against the reference run with the same weights."""
+    z = golden("vanilla_pretrained_testhdf5")
+    m = amd.VanillaNetwork(26, 2, 1)
+    m.load_state_dict(golden_state_dict(z))
+    m = m.to(DEV).eval()
+    with torch.no_grad():
+        out = m(golden_batch(z)).cpu().numpy()
+    np.testing.assert_allclose(out, z["out/eval"], **TOL)
+    m.train()
+    out = m(golden_batch(z))
+    loss = torch.nn.functional.cross_entropy(out, torch.from_numpy(z["in/y"]).to(DEV).long())
+    loss.backward()
+    assert float(loss.detach()) == pytest.approx(float(z["loss"]), rel=1e-4)
+    ref = golden_grads(z)
+    for n, p in m.named_parameters():
+        assert_grad_close(p.grad.cpu().numpy(), ref[n], err_msg=n)
+    # the fused training step on the same batch: same loss and gradients
+    step = FusedTrainStep(m, loss="ce")
+    h = resolve_batch(golden_batch(z), DEV, require_clusters=False)
+    lf, _ = step.step(h)
+    assert float(lf) == pytest.approx(float(z["loss"]), rel=1e-4)
+    for n, g in zip(amd.PARAM_NAMES, step.grads):
+        assert_grad_close(g.cpu().numpy(), ref[n], err_msg=n)
 
 
 def test_vanilla_layer_arbitrary_edges_vs_oracle():

@@ -216,3 +216,39 @@ def test_split_irregular_graphs_and_determinism():
             for a, b in zip(runs[split], grads + params):
                 assert torch.equal(a, b)
         runs[split] = grads + params
+
+
+def test_handoff_timeout_is_loud_and_not_sticky():
+    """A hand-off wait that gives up (forced here: dr_pass.spin_limit = 1 poll)
+    withholds the step: NaN loss, parameters / moments / step counter unchanged,
+    the arrival counters still left zero; the next launch clears the per-launch
+    flag and trains normally; check_faults() raises once for the epoch."""
+    datas = _datas(64, seed=91)  # 64 graphs: 4 workgroups per graph
+    store = _store(datas)
+    torch.manual_seed(3)
+    m = amd.VanillaNetwork(30, 1, 3).to(DEV)
+    step = FusedTrainStep(m.train())
+    h = BatchHandle(store, np.arange(64))
+    h.vanilla_split = 4
+    before = [p.detach().clone() for p in step.params]
+    step._pass.spin_limit = step._pass_nodrop.spin_limit = 1  # noqa: SLF001
+    loss, _ = step.step(h)
+    torch.cuda.synchronize()
+    assert int(step.fault[0]) == 1 and int(step.fault[1]) >= 1
+    assert torch.isnan(loss).all()
+    assert all(torch.isnan(g).all() for g in step.grads)
+    for a, b in zip(before, step.params):
+        assert torch.equal(a, b)
+    assert all(int(t.abs().sum()) == 0 for st in step.states for t in st)
+    assert int(step.counter[0]) == 0
+    _buf, _offs, sync, _wpack = h.vanilla_fused_scratch()
+    assert int(sync[:-1].abs().sum()) == 0, "arrival counters not left zero"
+    step._pass.spin_limit = step._pass_nodrop.spin_limit = 0  # noqa: SLF001
+    loss2, _ = step.step(h)
+    torch.cuda.synchronize()
+    assert int(step.fault[0]) == 0 and bool(torch.isfinite(loss2).all())
+    assert int(step.counter[0]) == 1
+    assert not all(torch.equal(a, b) for a, b in zip(before, step.params))
+    with pytest.raises(RuntimeError, match="gave up"):
+        step.check_faults()
+    step.check_faults()  # the count was reset: no error

@@ -41,6 +41,7 @@ def _run(model, z, loss_kind, mask=None):
     ("ginet_synth_classif", "GINet", (30, 2, 3)),
     ("foutnet_synth", "FoutNet", (30, 1)),
     ("vanilla_synth", "VanillaNetwork", (30, 1, 3)),
+    ("vanilla_pretrained_testhdf5", "VanillaNetwork", (26, 2, 1)),  # the reference's pre-trained weights on test.hdf5
     ("sgat_1atn", "SGAT", (50, 1)),
     ("sgat_synth", "SGAT", (30, 2)),
     ("ginet_nocluster_1atn", "GINetNoCluster", (50, 1, 1)),
