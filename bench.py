@@ -417,6 +417,8 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
         h.large_tile = args.force_large or None
         h.large_onepass = args.ginet_path == "onepass"
         h.vanilla_pipeline = bool(args.vanilla_pipeline)
+        if os.environ.get("DR_VANILLA_TILE") is not None:  # diagnostic: rows per pipeline edge tile (0: untiled)
+            h.vanilla_tile_rows = int(os.environ["DR_VANILLA_TILE"])
 
     torch.manual_seed(1234)
     model = models[args.model](30, 1, 3).to(dev).train()

@@ -151,6 +151,258 @@ __device__ __forceinline__ float4 gather_row_chunk_w(const uint16_t* col, const 
   return acc;
 }
 
+// The per-graph tail shared by fout_graph_kernel and the large-graph tail
+// kernel: conv2 on the pooled graph, depth-1 max pool, mean, head, loss and
+// the whole backward down to the conv1 weight partials.  Needs the depth-0
+// pool (P1, A1: value and first arg per (cluster, channel)) and the pooled
+// graph / weights in LDS (FoutTail); xarg(i, k) = [c1 x]_{i,k} (SGAT: c1_i x_ik)
+// and zarg(i, k) = Zm_{i,k} at the pooling args, wherever they live.
+struct FoutTail {
+  float *P1, *dP1, *Zm2, *S2, *H2, *D2, *Dz2, *P2, *NTie, *G, *Hpre, *Hh, *Dh, *DG, *Dout, *DGp, *P1w, *C2;
+  int *A1, *p1rp, *p1c, *p1trp, *p1tc, *m1p, *m1i, *P1tid;
+  const float *Wc2, *Wn2, *B2, *Fc1, *Fc1b, *Fc2;
+};
+
+#define FT_STAMP(i)                                                                             \
+  do {                                                                                          \
+    if (DR_STAMPS_ON && tid == 0 && p.stamps) p.stamps[(int64_t)b * 32 + (i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#ifdef DR_STAMPS
+#define DR_STAMPS_ON 1
+#else
+#define DR_STAMPS_ON 0
+#endif
+
+template <bool SG, class XF, class ZF>
+__device__ __forceinline__ void fout_tail(const dr_pass& p, const FoutTail t, int b, int N, int K0, int K1, int F, int OUT,
+                                          float y_g, XF xarg, ZF zarg) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  FT_STAMP(4);
+  // ---------------- conv2 on the pooled graph: FoutLayer(16, 32) ----------
+  // (SGAT: SGraphAttentionLayer(16, 32) with the pooled edge weights)
+  for (int p = tid; p < K0 * 16; p += NT) {  // Zm2 = mean over pooled out-neighbours
+    const int k = p >> 4, j = p & 15;
+    const int eb = t.p1rp[k], ee = t.p1rp[k + 1];
+    float acc = 0.f;
+    if (SG) {
+      float sw = 0.f;
+      for (int e = eb; e < ee; ++e) {
+        acc = fmaf(t.P1w[e], t.P1[t.p1c[e] * 16 + j], acc);
+        sw += t.P1w[e];
+      }
+      const float deg = (float)imax(ee - eb, 1);
+      t.Zm2[p] = acc / deg;
+      if (j == 0) t.C2[k] = sw / deg;
+    } else {
+      for (int e = eb; e < ee; ++e) acc += t.P1[t.p1c[e] * 16 + j];
+      t.Zm2[p] = acc / (float)(ee - eb);
+    }
+  }
+  __syncthreads();
+  for (int p = tid; p < K0 * 32; p += NT) {
+    const int k = p >> 5, o = p & 31;
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc = fmaf(t.P1[k * 16 + j], t.Wc2[j * 32 + o], acc);
+    if (SG) acc *= t.C2[k];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc = fmaf(t.Zm2[k * 16 + j], t.Wn2[j * 32 + o], acc);
+    const float sv = acc + t.B2[o];
+    t.S2[p] = sv;
+    t.H2[p] = relu_keepnan(sv);
+  }
+  __syncthreads();
+
+  FT_STAMP(5);
+  // ---------------- depth-1 max_pool_x (amax: NaN propagates) + mean -------
+  for (int p = tid; p < K1 * 32; p += NT) {
+    const int m = p >> 5, o = p & 31;
+    const int mb = t.m1p[m], me = t.m1p[m + 1];
+    float mx = t.H2[t.m1i[mb] * 32 + o];
+    for (int q = mb + 1; q < me; ++q) {
+      const float v = t.H2[t.m1i[q] * 32 + o];
+      mx = (mx != mx || v != v) ? __int_as_float(0x7fc00000) : fmaxf(mx, v);
+    }
+    float ties = 0.f;
+    for (int q = mb; q < me; ++q) ties += (t.H2[t.m1i[q] * 32 + o] == mx) ? 1.f : 0.f;
+    t.P2[p] = mx;
+    t.NTie[p] = ties;
+  }
+  __syncthreads();
+  if (tid < 32) {
+    float acc = 0.f;
+    for (int m = 0; m < K1; ++m) acc += t.P2[m * 32 + tid];
+    t.G[tid] = acc / (float)K1;
+  }
+  __syncthreads();
+
+  FT_STAMP(6);
+  // ---------------- head: fc1 (32->64) -> relu -> fc2 (foutnet.py:115-117) --
+  {
+    const int r = tid >> 3, part = tid & 7;  // 8 lanes per fc1 row, 4 inputs each
+    float acc = 0.f;
+    if (r < 64) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc = fmaf(t.G[part * 4 + j], t.Fc1[r * 32 + part * 4 + j], acc);
+    }
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    acc += __shfl_xor(acc, 4, 64);
+    if (r < 64 && part == 0) {
+      acc += t.Fc1b[r];
+      t.Hpre[r] = acc;
+      t.Hh[r] = relu_keepnan(acc);
+    }
+  }
+  __syncthreads();
+  for (int q = wave; q < OUT; q += NW) {
+    float v = t.Hh[lane] * t.Fc2[q * 64 + lane];
+    v = dr_wave_sum(v);
+    if (lane == 0) t.Dout[q] = v + t.Fc2[OUT * 64 + q];
+  }
+  __syncthreads();
+  if ((p.flags & DR_PASS_FORWARD) && tid < OUT) p.out[(int64_t)b * OUT + tid] = t.Dout[tid];
+  if (!(p.flags & DR_PASS_BACKWARD)) return;
+  __syncthreads();
+
+  FT_STAMP(7);
+  // ---------------- loss gradient (trainer.py:688-689) ----------------------
+  if (tid == 0) {
+    if (p.loss_kind == DR_LOSS_MSE) {
+      const float dlt = t.Dout[0] - y_g;
+      if (p.loss_per_graph) p.loss_per_graph[b] = dlt * dlt;
+      t.Dout[0] = 2.f * dlt * p.loss_scale;
+    } else if (p.loss_kind == DR_LOSS_CE) {
+      const int yi = (int)y_g;
+      float mx = t.Dout[0];
+      for (int q = 1; q < OUT; ++q) mx = fmaxf(mx, t.Dout[q]);
+      float se = 0.f;
+      for (int q = 0; q < OUT; ++q) se += expf(t.Dout[q] - mx);
+      const float lse = mx + logf(se);
+      const float wy = p.class_w ? p.class_w[yi] : 1.f;
+      if (p.loss_per_graph) p.loss_per_graph[b] = wy * (lse - t.Dout[yi]);
+      for (int q = 0; q < OUT; ++q) t.Dout[q] = wy * (expf(t.Dout[q] - lse) - (q == yi ? 1.f : 0.f)) * p.loss_scale;
+    } else {
+      for (int q = 0; q < OUT; ++q) t.Dout[q] = p.dout[(int64_t)b * OUT + q];
+    }
+  }
+  __syncthreads();
+
+  // ---------------- head backward -------------------------------------------
+  if (tid < 64) {
+    float acc = 0.f;
+    for (int q = 0; q < OUT; ++q) acc = fmaf(t.Fc2[q * 64 + tid], t.Dout[q], acc);
+    t.Dh[tid] = relu_bwd(t.Hh[tid], acc);
+  }
+  __syncthreads();
+  {
+    const int o = tid & 31, rc = tid >> 5;  // 32 chunks of 2 fc1 rows
+    float acc = fmaf(t.Fc1[(rc * 2) * 32 + o], t.Dh[rc * 2], t.Fc1[(rc * 2 + 1) * 32 + o] * t.Dh[rc * 2 + 1]);
+    t.DGp[rc * 32 + o] = acc;
+  }
+  __syncthreads();
+  if (tid < 32) {
+    float acc = 0.f;
+    for (int rc = 0; rc < NT / 32; ++rc) acc += t.DGp[rc * 32 + tid];
+    t.DG[tid] = acc;
+  }
+  {
+    const int HS = DR_FOUT_HEAD_STRIDE(OUT);
+    float* hg = p.head + (int64_t)b * HS;
+    if (tid < 32) hg[tid] = t.G[tid];
+    if (tid < 64) {
+      hg[32 + tid] = t.Hh[tid];
+      hg[96 + tid] = t.Dh[tid];
+    }
+    if (tid < OUT) hg[160 + tid] = t.Dout[tid];
+  }
+  __syncthreads();
+
+  FT_STAMP(8);
+  // ---------------- depth-1 pooling + mean backward -------------------------
+  for (int p = tid; p < K1 * 32; p += NT) {
+    const int m = p >> 5, o = p & 31;
+    const float gm = (t.DG[o] / (float)K1) / t.NTie[p];
+    const float mx = t.P2[p];
+    for (int q = t.m1p[m]; q < t.m1p[m + 1]; ++q) {
+      const int k = t.m1i[q];
+      const float h = t.H2[k * 32 + o];
+      t.D2[k * 32 + o] = relu_bwd(h, (h == mx ? 1.f : 0.f) * gm);
+    }
+  }
+  __syncthreads();
+  // conv2 weight partials; gradient into the mean term (dZm2 = dS2 Wn2^T)
+  {
+    const int SS = DR_FOUT_SLAB_STRIDE(F);
+    float* slab = p.slab + (int64_t)b * SS + 32 * F + 16;
+    for (int p = tid; p < 1024 + 32; p += NT) {
+      float acc = 0.f;
+      if (p < 512) {  // dWc2[j][o] = sum_k (c2_k) P1[k][j] dS2[k][o]
+        const int j = p >> 5, o = p & 31;
+        for (int k = 0; k < K0; ++k) acc = fmaf((SG ? t.C2[k] : 1.f) * t.P1[k * 16 + j], t.D2[k * 32 + o], acc);
+      } else if (p < 1024) {  // dWn2[j][o] = sum_{k: deg>0} Zm2[k][j] dS2[k][o]
+        const int q = p - 512, j = q >> 5, o = q & 31;
+        for (int k = 0; k < K0; ++k)
+          if (SG || t.p1rp[k + 1] > t.p1rp[k]) acc = fmaf(t.Zm2[k * 16 + j], t.D2[k * 32 + o], acc);
+      } else {  // db2[o]
+        const int o = p - 1024;
+        for (int k = 0; k < K0; ++k) acc += t.D2[k * 32 + o];
+      }
+      slab[p] = acc;
+    }
+  }
+  for (int p = tid; p < K0 * 16; p += NT) {
+    const int k = p >> 4, j = p & 15;
+    float dz = 0.f, dp = 0.f;
+#pragma unroll 8
+    for (int o = 0; o < 32; ++o) {
+      const float ds = t.D2[k * 32 + o];
+      dz = fmaf(ds, t.Wn2[j * 32 + o], dz);
+      dp = fmaf(ds, t.Wc2[j * 32 + o], dp);
+    }
+    const int deg = t.p1rp[k + 1] - t.p1rp[k];
+    t.Dz2[p] = deg > 0 ? dz / (float)deg : 0.f;
+    t.dP1[p] = SG ? t.C2[k] * dp : dp;
+  }
+  __syncthreads();
+  // dP1[j] += sum_{i: j in N(i)} dZm2[i] / deg_i  (transposed pooled CSR), then
+  // route to the depth-0 arg member through relu: v = relu'(H1[arg]) dP1
+  for (int p = tid; p < K0 * 16; p += NT) {
+    const int k = p >> 4, j = p & 15;
+    float acc = t.dP1[p];
+    if (SG) {
+      for (int e = t.p1trp[k]; e < t.p1trp[k + 1]; ++e) acc = fmaf(t.P1w[t.P1tid[e]], t.Dz2[t.p1tc[e] * 16 + j], acc);
+    } else {
+      for (int e = t.p1trp[k]; e < t.p1trp[k + 1]; ++e) acc += t.Dz2[t.p1tc[e] * 16 + j];
+    }
+    const int i = t.A1[p];
+    t.dP1[p] = (i < N) ? relu_bwd(t.P1[p], acc) : 0.f;  // H1[arg] is the pooled value itself
+  }
+  __syncthreads();
+
+  FT_STAMP(9);
+  // ---------------- conv1 weight partials: sum_k v_k [x | Zm][arg_k] -------
+  {
+    const int SS = DR_FOUT_SLAB_STRIDE(F);
+    float* slab = p.slab + (int64_t)b * SS;
+    for (int p = tid; p < 32 * F + 16; p += NT) {
+      float acc = 0.f;
+      if (p < 32 * F) {
+        const int half = p >= 16 * F;  // 0: dWc [F,16], 1: dWn [F,16]
+        const int q = p - half * 16 * F, kk = q >> 4, ch = q & 15;
+        for (int k = 0; k < K0; ++k) {
+          const int i = t.A1[k * 16 + ch];
+          if (i < N) acc = fmaf(t.dP1[k * 16 + ch], half ? zarg(i, kk) : xarg(i, kk), acc);
+        }
+      } else {
+        const int ch = p - 32 * F;
+        for (int k = 0; k < K0; ++k) acc += t.dP1[k * 16 + ch];
+      }
+      slab[p] = acc;
+    }
+  }
+}
+
 template <bool SG>
 __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -380,230 +632,16 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
   }
   __syncthreads();
 
-  DRK_STAMP(4);
-  // ---------------- conv2 on the pooled graph: FoutLayer(16, 32) ----------
-  // (SGAT: SGraphAttentionLayer(16, 32) with the pooled edge weights)
-  for (int p = tid; p < K0 * 16; p += NT) {  // Zm2 = mean over pooled out-neighbours
-    const int k = p >> 4, j = p & 15;
-    const int eb = sp1rp[k], ee = sp1rp[k + 1];
-    float acc = 0.f;
-    if (SG) {
-      float sw = 0.f;
-      for (int e = eb; e < ee; ++e) {
-        acc = fmaf(sP1w[e], sP1[sp1c[e] * 16 + j], acc);
-        sw += sP1w[e];
-      }
-      const float deg = (float)imax(ee - eb, 1);
-      sZm2[p] = acc / deg;
-      if (j == 0) sC2[k] = sw / deg;
-    } else {
-      for (int e = eb; e < ee; ++e) acc += sP1[sp1c[e] * 16 + j];
-      sZm2[p] = acc / (float)(ee - eb);
-    }
-  }
-  __syncthreads();
-  for (int p = tid; p < K0 * 32; p += NT) {
-    const int k = p >> 5, o = p & 31;
-    float acc = 0.f;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) acc = fmaf(sP1[k * 16 + j], sWc2[j * 32 + o], acc);
-    if (SG) acc *= sC2[k];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) acc = fmaf(sZm2[k * 16 + j], sWn2[j * 32 + o], acc);
-    const float sv = acc + sB2[o];
-    sS2[p] = sv;
-    sH2[p] = relu_keepnan(sv);
-  }
-  __syncthreads();
-
-  DRK_STAMP(5);
-  // ---------------- depth-1 max_pool_x (amax: NaN propagates) + mean -------
-  for (int p = tid; p < K1 * 32; p += NT) {
-    const int m = p >> 5, o = p & 31;
-    const int mb = sm1p[m], me = sm1p[m + 1];
-    float mx = sH2[sm1i[mb] * 32 + o];
-    for (int q = mb + 1; q < me; ++q) {
-      const float v = sH2[sm1i[q] * 32 + o];
-      mx = (mx != mx || v != v) ? __int_as_float(0x7fc00000) : fmaxf(mx, v);
-    }
-    float ties = 0.f;
-    for (int q = mb; q < me; ++q) ties += (sH2[sm1i[q] * 32 + o] == mx) ? 1.f : 0.f;
-    sP2[p] = mx;
-    sNT[p] = ties;
-  }
-  __syncthreads();
-  if (tid < 32) {
-    float acc = 0.f;
-    for (int m = 0; m < K1; ++m) acc += sP2[m * 32 + tid];
-    sG[tid] = acc / (float)K1;
-  }
-  __syncthreads();
-
-  DRK_STAMP(6);
-  // ---------------- head: fc1 (32->64) -> relu -> fc2 (foutnet.py:115-117) --
-  {
-    const int r = tid >> 3, part = tid & 7;  // 8 lanes per fc1 row, 4 inputs each
-    float acc = 0.f;
-    if (r < 64) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc = fmaf(sG[part * 4 + j], sFc1[r * 32 + part * 4 + j], acc);
-    }
-    acc += __shfl_xor(acc, 1, 64);
-    acc += __shfl_xor(acc, 2, 64);
-    acc += __shfl_xor(acc, 4, 64);
-    if (r < 64 && part == 0) {
-      acc += sFc1b[r];
-      sHpre[r] = acc;
-      sHh[r] = relu_keepnan(acc);
-    }
-  }
-  __syncthreads();
-  for (int q = wave; q < OUT; q += NW) {
-    float v = sHh[lane] * sFc2[q * 64 + lane];
-    v = dr_wave_sum(v);
-    if (lane == 0) sDout[q] = v + sFc2[OUT * 64 + q];
-  }
-  __syncthreads();
-  if ((a.p.flags & DR_PASS_FORWARD) && tid < OUT) a.p.out[(int64_t)b * OUT + tid] = sDout[tid];
-  if (!(a.p.flags & DR_PASS_BACKWARD)) return;
-  __syncthreads();
-
-  DRK_STAMP(7);
-  // ---------------- loss gradient (trainer.py:688-689) ----------------------
-  if (tid == 0) {
-    if (a.p.loss_kind == DR_LOSS_MSE) {
-      const float dlt = sDout[0] - y_g;
-      if (a.p.loss_per_graph) a.p.loss_per_graph[b] = dlt * dlt;
-      sDout[0] = 2.f * dlt * a.p.loss_scale;
-    } else if (a.p.loss_kind == DR_LOSS_CE) {
-      const int yi = (int)y_g;
-      float mx = sDout[0];
-      for (int q = 1; q < OUT; ++q) mx = fmaxf(mx, sDout[q]);
-      float se = 0.f;
-      for (int q = 0; q < OUT; ++q) se += expf(sDout[q] - mx);
-      const float lse = mx + logf(se);
-      const float wy = a.p.class_w ? a.p.class_w[yi] : 1.f;
-      if (a.p.loss_per_graph) a.p.loss_per_graph[b] = wy * (lse - sDout[yi]);
-      for (int q = 0; q < OUT; ++q) sDout[q] = wy * (expf(sDout[q] - lse) - (q == yi ? 1.f : 0.f)) * a.p.loss_scale;
-    } else {
-      for (int q = 0; q < OUT; ++q) sDout[q] = a.p.dout[(int64_t)b * OUT + q];
-    }
-  }
-  __syncthreads();
-
-  // ---------------- head backward -------------------------------------------
-  if (tid < 64) {
-    float acc = 0.f;
-    for (int q = 0; q < OUT; ++q) acc = fmaf(sFc2[q * 64 + tid], sDout[q], acc);
-    sDh[tid] = relu_bwd(sHh[tid], acc);
-  }
-  __syncthreads();
-  {
-    const int o = tid & 31, rc = tid >> 5;  // 32 chunks of 2 fc1 rows
-    float acc = fmaf(sFc1[(rc * 2) * 32 + o], sDh[rc * 2], sFc1[(rc * 2 + 1) * 32 + o] * sDh[rc * 2 + 1]);
-    sDGp[rc * 32 + o] = acc;
-  }
-  __syncthreads();
-  if (tid < 32) {
-    float acc = 0.f;
-    for (int rc = 0; rc < NT / 32; ++rc) acc += sDGp[rc * 32 + tid];
-    sDG[tid] = acc;
-  }
-  {
-    const int HS = DR_FOUT_HEAD_STRIDE(OUT);
-    float* hg = a.p.head + (int64_t)b * HS;
-    if (tid < 32) hg[tid] = sG[tid];
-    if (tid < 64) {
-      hg[32 + tid] = sHh[tid];
-      hg[96 + tid] = sDh[tid];
-    }
-    if (tid < OUT) hg[160 + tid] = sDout[tid];
-  }
-  __syncthreads();
-
-  DRK_STAMP(8);
-  // ---------------- depth-1 pooling + mean backward -------------------------
-  for (int p = tid; p < K1 * 32; p += NT) {
-    const int m = p >> 5, o = p & 31;
-    const float gm = (sDG[o] / (float)K1) / sNT[p];
-    const float mx = sP2[p];
-    for (int q = sm1p[m]; q < sm1p[m + 1]; ++q) {
-      const int k = sm1i[q];
-      const float h = sH2[k * 32 + o];
-      sD2[k * 32 + o] = relu_bwd(h, (h == mx ? 1.f : 0.f) * gm);
-    }
-  }
-  __syncthreads();
-  // conv2 weight partials; gradient into the mean term (dZm2 = dS2 Wn2^T)
-  {
-    const int SS = DR_FOUT_SLAB_STRIDE(F);
-    float* slab = a.p.slab + (int64_t)b * SS + 32 * F + 16;
-    for (int p = tid; p < 1024 + 32; p += NT) {
-      float acc = 0.f;
-      if (p < 512) {  // dWc2[j][o] = sum_k (c2_k) P1[k][j] dS2[k][o]
-        const int j = p >> 5, o = p & 31;
-        for (int k = 0; k < K0; ++k) acc = fmaf((SG ? sC2[k] : 1.f) * sP1[k * 16 + j], sD2[k * 32 + o], acc);
-      } else if (p < 1024) {  // dWn2[j][o] = sum_{k: deg>0} Zm2[k][j] dS2[k][o]
-        const int q = p - 512, j = q >> 5, o = q & 31;
-        for (int k = 0; k < K0; ++k)
-          if (SG || sp1rp[k + 1] > sp1rp[k]) acc = fmaf(sZm2[k * 16 + j], sD2[k * 32 + o], acc);
-      } else {  // db2[o]
-        const int o = p - 1024;
-        for (int k = 0; k < K0; ++k) acc += sD2[k * 32 + o];
-      }
-      slab[p] = acc;
-    }
-  }
-  for (int p = tid; p < K0 * 16; p += NT) {
-    const int k = p >> 4, j = p & 15;
-    float dz = 0.f, dp = 0.f;
-#pragma unroll 8
-    for (int o = 0; o < 32; ++o) {
-      const float ds = sD2[k * 32 + o];
-      dz = fmaf(ds, sWn2[j * 32 + o], dz);
-      dp = fmaf(ds, sWc2[j * 32 + o], dp);
-    }
-    const int deg = sp1rp[k + 1] - sp1rp[k];
-    sDz2[p] = deg > 0 ? dz / (float)deg : 0.f;
-    sdP1[p] = SG ? sC2[k] * dp : dp;
-  }
-  __syncthreads();
-  // dP1[j] += sum_{i: j in N(i)} dZm2[i] / deg_i  (transposed pooled CSR), then
-  // route to the depth-0 arg member through relu: v = relu'(H1[arg]) dP1
-  for (int p = tid; p < K0 * 16; p += NT) {
-    const int k = p >> 4, j = p & 15;
-    float acc = sdP1[p];
-    if (SG) {
-      for (int e = sp1trp[k]; e < sp1trp[k + 1]; ++e) acc = fmaf(sP1w[sP1tid[e]], sDz2[sp1tc[e] * 16 + j], acc);
-    } else {
-      for (int e = sp1trp[k]; e < sp1trp[k + 1]; ++e) acc += sDz2[sp1tc[e] * 16 + j];
-    }
-    const int i = sA1[p];
-    sdP1[p] = (i < N) ? relu_bwd(sH1[i * 16 + j], acc) : 0.f;
-  }
-  __syncthreads();
-
-  DRK_STAMP(9);
-  // ---------------- conv1 weight partials: sum_k v_k [x | Zm][arg_k] -------
-  {
-    const int SS = DR_FOUT_SLAB_STRIDE(F);
-    float* slab = a.p.slab + (int64_t)b * SS;
-    for (int p = tid; p < 32 * F + 16; p += NT) {
-      float acc = 0.f;
-      if (p < 32 * F) {
-        const int half = p >= 16 * F;  // 0: dWc [F,16], 1: dWn [F,16]
-        const int q = p - half * 16 * F, kk = q >> 4, ch = q & 15;
-        for (int k = 0; k < K0; ++k) {
-          const int i = sA1[k * 16 + ch];
-          if (i < N) acc = fmaf(sdP1[k * 16 + ch], half ? sZm[i * LDZ + ZO + kk] : (SG ? sC1[i] : 1.f) * (WIDE ? sZm[i * LDZ + kk] : sX[i * XS + kk]), acc);
-        }
-      } else {
-        const int ch = p - 32 * F;
-        for (int k = 0; k < K0; ++k) acc += sdP1[k * 16 + ch];
-      }
-      slab[p] = acc;
-    }
-  }
+  FoutTail t;
+  t.P1 = sP1; t.A1 = sA1; t.dP1 = sdP1; t.Zm2 = sZm2; t.S2 = sS2; t.H2 = sH2; t.D2 = sD2; t.Dz2 = sDz2;
+  t.p1rp = sp1rp; t.p1c = sp1c; t.p1trp = sp1trp; t.p1tc = sp1tc; t.m1p = sm1p; t.m1i = sm1i;
+  t.P2 = sP2; t.NTie = sNT; t.G = sG; t.Hpre = sHpre; t.Hh = sHh; t.Dh = sDh; t.DG = sDG; t.Dout = sDout; t.DGp = sDGp;
+  t.Wc2 = sWc2; t.Wn2 = sWn2; t.B2 = sB2; t.Fc1 = sFc1; t.Fc1b = sFc1b; t.Fc2 = sFc2;
+  t.P1w = sP1w; t.P1tid = sP1tid; t.C2 = sC2;
+  // conv1 weight partials read [c1 x | Zm] at the pooling args from LDS
+  fout_tail<SG>(a.p, t, b, N, K0, K1, F, OUT, y_g,
+                [=](int i, int kk) { return (SG ? sC1[i] : 1.f) * (WIDE ? sZm[i * LDZ + kk] : sX[i * XS + kk]); },
+                [=](int i, int kk) { return sZm[i * LDZ + ZO + kk]; });
   DRK_STAMP(10);
 }
 

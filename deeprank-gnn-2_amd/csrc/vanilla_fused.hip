@@ -22,6 +22,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "graph_common.h"
 
 namespace {
@@ -311,6 +313,220 @@ __global__ void __launch_bounds__(RB) vb_edge_bwd8(VA a, int l) {
     }
     for (; q < qe; ++q)
       if ((wr[g.teid[q]] >> c) & 1u) acc += DSg[(int64_t)g.tcol[q] * 32];
+    DP[r * 32 + c] = acc;
+  }
+}
+
+// ---- tiled edge kernels (dr_vanilla_scratch tile plan) -----------------------
+// One workgroup per tile of consecutive rows of one graph.  The tile's halo --
+// the distinct neighbours of its rows, out- and in-edges -- is staged in LDS
+// once (B rows in the forward, dS rows in the backward: one 128-byte row each,
+// coalesced), together with the tile's edge attributes, halo-local column ids
+// and (backward) ReLU words, so the per-edge work of vb_edge_fwd8 / vb_edge_bwd8
+// reads LDS instead of gathering a 128-byte row from L2/HBM per edge.  Rows are
+// taken in the same lane layout (32 channels per row, two rows per wave) and
+// every sum runs in the same order: results are bit-identical to the untiled
+// kernels.  LDS (floats): halo rows [halo_max][32] | edge attributes
+// [edges][FeS] | words [edges] | column ids (uint16) [edges] (+ transposed).
+struct TileCarve {
+  int rows, ea, words, wt, lc, ltc, tp, total;
+};
+__host__ __device__ inline TileCarve tile_carve(int hmax, int emax, int tmax, int FeS, bool bwd) {
+  TileCarve c;
+  int o = 0;
+  c.rows = o;
+  o += hmax * 32;
+  c.ea = o;
+  o += r4(emax * FeS);
+  c.words = o;  // backward: the tile's CSR-order words
+  o += bwd ? r4(emax) : 0;
+  c.wt = o;  // backward: the tile's transposed-order words
+  o += bwd ? r4(tmax) : 0;
+  c.tp = o;  // forward: each CSR edge's transposed slot
+  o += bwd ? 0 : r4(emax);
+  c.lc = o;
+  o += bwd ? 0 : r4((emax + 1) / 2);
+  c.ltc = o;
+  o += bwd ? r4((tmax + 1) / 2) : 0;
+  c.total = o;
+  return c;
+}
+
+// the tile's halo rows of a node-level [rows][32] array (graph block at g32) -> LDS
+__device__ __forceinline__ void stage_halo(float* dst, const float* g32, const int* ids, int H) {
+  for (int p = threadIdx.x; p < H * 8; p += RB) {
+    const int h = p >> 3, q = (p & 7) * 4;
+    *reinterpret_cast<float4*>(dst + h * 32 + q) = *reinterpret_cast<const float4*>(g32 + (int64_t)ids[h] * 32 + q);
+  }
+}
+
+template <int FE>
+__global__ void __launch_bounds__(RB) vb_edge_fwd_tile(VA a, int l) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int FA = FE > 0 ? FE : 1, FeS = FA;
+  const Layer L = layer_of(a, l);
+  const int F = a.F, KE = a.KE;
+  const int t = blockIdx.x, tid = threadIdx.x, c = tid & 31, hs = tid & 32;
+  const int64_t rt0 = a.ws.tile_row0[t], rt1 = a.ws.tile_row0[t + 1];
+  const int b = a.ws.row_slot[rt0];
+  const dr_graph_desc& d = a.descs[b];
+  const int64_t g0 = a.ws.row0[b];
+  const int* rp = a.s.rowptr + d.node0 + d.gid;
+  const int i0 = (int)(rt0 - g0), e0 = rp[i0], ne = rp[(int)(rt1 - g0)] - e0;
+  const int h0 = a.ws.halo_off[t], H = a.ws.halo_off[t + 1] - h0;
+  const TileCarve tc = tile_carve(a.ws.halo_max, a.ws.tile_edges_max, 0, FeS, false);
+  float* sB = lds + tc.rows;
+  float* sE = lds + tc.ea;
+  uint16_t* sC = reinterpret_cast<uint16_t*>(lds + tc.lc);
+  int* sTp = reinterpret_cast<int*>(lds + tc.tp);
+  stage_halo(sB, L.bm + g0 * 32, a.ws.halo_ids + h0, H);
+  {
+    const float* ea = a.s.ea + (d.col0 + e0) * FeS;
+    for (int p = tid; p < ne * FeS; p += RB) sE[p] = ea[p];
+    const uint16_t* lc = a.ws.lcol + a.ws.lcol_off[t];
+    const int* tp = a.ws.tpos + a.ws.lcol_off[t];
+    for (int p = tid; p < ne; p += RB) {
+      sC[p] = lc[p];
+      sTp[p] = tp[p];
+    }
+  }
+  float wcr[FA];
+#pragma unroll
+  for (int f = 0; f < FE; ++f) wcr[f] = L.we[c * KE + 2 * F + f];
+  const float bc = L.be[c];
+  uint32_t* wr = a.ws.relu_words + (int64_t)(l - 1) * a.ws.edge0[a.B] + a.ws.edge0[b] + e0;
+  uint32_t* wt = a.ws.relu_words_t + (int64_t)(l - 1) * a.ws.edge0[a.B] + a.ws.edge0[b];
+  __syncthreads();
+  for (int64_t r = rt0 + (tid >> 5); r < rt1; r += RB / 32) {
+    const int i = (int)(r - g0);
+    const float ac = L.a[r * 32 + c];
+    float acc = 0.f;
+    const int eb = rp[i] - e0, ee = rp[i + 1] - e0;
+    int e = eb;
+    auto group = [&](auto un) {
+      constexpr int U = decltype(un)::value;
+      int j[U];
+      float ev[U][FA], q[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) j[u] = sC[e + u];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int f = 0; f < FE; ++f) ev[u][f] = sE[(e + u) * FeS + f];
+#pragma unroll
+      for (int u = 0; u < U; ++u) q[u] = sB[j[u] * 32 + c];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        float ec = 0.f;
+#pragma unroll
+        for (int f = 0; f < FE; ++f) ec = fmaf(wcr[f], ev[u][f], ec);
+        const float pre = ac + q[u] + ec + bc;
+        acc += relu_keepnan(pre);
+        const uint64_t m = __ballot(active(pre));
+        const uint32_t word = (uint32_t)(m >> hs);
+        if (c == 0) wr[e + u] = word;
+        if (c == 1) wt[sTp[e + u]] = word;  // the backward's transposed pass reads this copy
+      }
+    };
+    for (; e + 8 <= ee; e += 8) group(std::integral_constant<int, 8>());
+    for (; e + 4 <= ee; e += 4) group(std::integral_constant<int, 4>());
+    for (; e < ee; ++e) group(std::integral_constant<int, 1>());
+    L.s[r * 32 + c] = acc;
+  }
+}
+
+template <int FE>
+__global__ void __launch_bounds__(RB) vb_edge_bwd_tile(VA a, int l) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int FA = FE > 0 ? FE : 1, FeS = FA;
+  float* ws = a.ws.base;
+  const float* DS = ws + a.L.ds;
+  float *D = ws + a.L.d, *DP = ws + a.L.dp, *EAP = ws + a.L.eap;
+  const int t = blockIdx.x, tid = threadIdx.x, c = tid & 31;
+  const int64_t rt0 = a.ws.tile_row0[t], rt1 = a.ws.tile_row0[t + 1];
+  const int b = a.ws.row_slot[rt0];
+  const dr_graph_desc& d = a.descs[b];
+  const int64_t g0 = a.ws.row0[b];
+  const int* rp = a.s.rowptr + d.node0 + d.gid;
+  const int* trp = a.s.t_rowptr + d.node0 + d.gid;
+  const int i0 = (int)(rt0 - g0), i1 = (int)(rt1 - g0);
+  const int e0 = rp[i0], ne = rp[i1] - e0, q0 = trp[i0], nq = trp[i1] - q0;
+  const int h0 = a.ws.halo_off[t], H = a.ws.halo_off[t + 1] - h0;
+  const TileCarve tc = tile_carve(a.ws.halo_max, a.ws.tile_edges_max, a.ws.tile_tedges_max, FeS, true);
+  float* sD = lds + tc.rows;
+  float* sE = lds + tc.ea;
+  uint32_t* sW = reinterpret_cast<uint32_t*>(lds + tc.words);
+  uint32_t* sWt = reinterpret_cast<uint32_t*>(lds + tc.wt);
+  uint16_t* sT = reinterpret_cast<uint16_t*>(lds + tc.ltc);
+  const uint32_t* words = a.ws.relu_words + (int64_t)(l - 1) * a.ws.edge0[a.B] + a.ws.edge0[b];
+  const uint32_t* words_t = a.ws.relu_words_t + (int64_t)(l - 1) * a.ws.edge0[a.B] + a.ws.edge0[b];
+  stage_halo(sD, DS + g0 * 32, a.ws.halo_ids + h0, H);
+  {
+    const float* ea = a.s.ea + (d.col0 + e0) * FeS;
+    for (int p = tid; p < ne * FeS; p += RB) sE[p] = ea[p];
+    for (int p = tid; p < ne; p += RB) sW[p] = words[e0 + p];
+    const uint16_t* lt = a.ws.ltcol + a.ws.ltcol_off[t];
+    for (int p = tid; p < nq; p += RB) {
+      sT[p] = lt[p];
+      sWt[p] = words_t[q0 + p];
+    }
+  }
+  __syncthreads();
+  for (int64_t r = rt0 + (tid >> 5); r < rt1; r += RB / 32) {
+    const int i = (int)(r - g0);
+    const float dsi = DS[r * 32 + c];
+    int cnt = 0;
+    float eap[FA];
+#pragma unroll
+    for (int f = 0; f < FA; ++f) eap[f] = 0.f;
+    const int eb = rp[i] - e0, ee = rp[i + 1] - e0;
+    int e = eb;
+    for (; e + 8 <= ee; e += 8) {
+      uint32_t wv[8];
+      float ev[8][FA];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) wv[u] = sW[e + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int f = 0; f < FE; ++f) ev[u][f] = sE[(e + u) * FeS + f];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if ((wv[u] >> c) & 1u) {
+          ++cnt;
+#pragma unroll
+          for (int f = 0; f < FE; ++f) eap[f] += ev[u][f];
+        }
+    }
+    for (; e < ee; ++e)
+      if ((sW[e] >> c) & 1u) {
+        ++cnt;
+#pragma unroll
+        for (int f = 0; f < FE; ++f) eap[f] += sE[e * FeS + f];
+      }
+    D[r * 32 + c] = cnt ? dsi * (float)cnt : 0.f;
+#pragma unroll
+    for (int f = 0; f < FE; ++f) EAP[(r * 32 + c) * FeS + f] = cnt ? dsi * eap[f] : 0.f;
+    float acc = 0.f;
+    const int qb = trp[i] - q0, qe = trp[i + 1] - q0;
+    int q = qb;
+    for (; q + 8 <= qe; q += 8) {
+      int src[8];
+      uint32_t wv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        src[u] = sT[q + u];
+        wv[u] = sWt[q + u];
+      }
+      float dv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) dv[u] = sD[src[u] * 32 + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if ((wv[u] >> c) & 1u) acc += dv[u];
+    }
+    for (; q < qe; ++q)
+      if ((sWt[q] >> c) & 1u) acc += sD[sT[q] * 32 + c];
     DP[r * 32 + c] = acc;
   }
 }
@@ -777,9 +993,31 @@ __global__ void __launch_bounds__(RB) vb_wgrad_combine(VA a, int l) {
 }
 
 // the FE-specialised 8-in-flight edge kernels (Fe <= 4; the backward needs the
-// forward's ReLU words); false: not launched
+// forward's ReLU words), tiled when the scratch carries a tile plan; false: not launched
 inline bool launch_edge8(bool fwd, const VA& a, int l, dim3 grid, hipStream_t st) {
   if (a.Fe > 4 || (!fwd && !a.ws.relu_words)) return false;
+  if (a.ws.tile_row0 && a.ws.relu_words && a.ws.n_tiles > 0) {
+    const int FeS = a.Fe > 0 ? a.Fe : 1;
+    const size_t lds = 4 * (size_t)tile_carve(a.ws.halo_max, a.ws.tile_edges_max, a.ws.tile_tedges_max, FeS, !fwd).total;
+    const dim3 tg((unsigned)a.ws.n_tiles);
+#define DR_ET(FE)                                                                              \
+  if (fwd) {                                                                                   \
+    if (dr_allow_big_lds(reinterpret_cast<const void*>(&vb_edge_fwd_tile<FE>))) return false;  \
+    hipLaunchKernelGGL(vb_edge_fwd_tile<FE>, tg, dim3(RB), lds, st, a, l);                     \
+  } else {                                                                                     \
+    if (dr_allow_big_lds(reinterpret_cast<const void*>(&vb_edge_bwd_tile<FE>))) return false;  \
+    hipLaunchKernelGGL(vb_edge_bwd_tile<FE>, tg, dim3(RB), lds, st, a, l);                     \
+  }
+    switch (a.Fe) {
+      case 0: DR_ET(0) break;
+      case 1: DR_ET(1) break;
+      case 2: DR_ET(2) break;
+      case 3: DR_ET(3) break;
+      default: DR_ET(4) break;
+    }
+#undef DR_ET
+    return true;
+  }
 #define DR_E8(FE)                                                                   \
   if (fwd) hipLaunchKernelGGL(vb_edge_fwd8<FE>, grid, dim3(RB), 0, st, a, l);      \
   else hipLaunchKernelGGL(vb_edge_bwd8<FE>, grid, dim3(RB), 0, st, a, l);
@@ -831,6 +1069,16 @@ extern "C" int dr_vanilla_graph_pass(const dr_graph_store* store, const dr_graph
   if ((pass->flags & DR_PASS_FORWARD) && !pass->out) return DR_E_ARG;
   if ((pass->flags & DR_PASS_BACKWARD) && (!scratch->part || !scratch->chunk_first || !scratch->chunk_slot))
     return DR_E_ARG;
+  if (scratch->tile_row0) {  // the tile plan: complete, and its LDS within one workgroup's 160 KiB
+    if (!scratch->relu_words || !scratch->halo_off || !scratch->halo_ids || !scratch->lcol_off || !scratch->lcol ||
+        !scratch->ltcol_off || !scratch->ltcol || !scratch->tpos || !scratch->relu_words_t || scratch->n_tiles < 1 || scratch->halo_max < 1 ||
+        scratch->halo_max > 65535 || scratch->tile_edges_max < 0 || scratch->tile_tedges_max < 0)
+      return DR_E_ARG;
+    const int FeS = store->n_edge_feat > 0 ? store->n_edge_feat : 1;
+    if (4LL * tile_carve(scratch->halo_max, scratch->tile_edges_max, scratch->tile_tedges_max, FeS, true).total > 160 * 1024 ||
+        4LL * tile_carve(scratch->halo_max, scratch->tile_edges_max, scratch->tile_tedges_max, FeS, false).total > 160 * 1024)
+      return DR_E_LDS;
+  }
   if (pass->use_dropout != DR_DROPOUT_OFF) return DR_E_UNSUPPORTED;
   // no in-launch hand-offs here: the pass never faults, but it clears the
   // caller's per-launch flag like every pass that takes one (dr_pass.fault)

@@ -43,6 +43,7 @@ class BatchHandle:
         self.force_layers = False  # run the layer-level path (layered.py) even when the graph pass fits (diagnostic)
         self.vanilla_words = True  # Vanilla pipeline: forward ReLU words feed the backward (False: recomputed)
         self.vanilla_split = None  # Vanilla per-graph kernel: workgroups per graph (None: by batch size)
+        self.vanilla_tile_rows = 16  # Vanilla pipeline edge kernels: rows per halo-staged tile (0: untiled gathers)
         self.fault = None  # device uint32 [2] (dr_pass.fault) of the autograd path's passes, made on first use
 
     def lds(self, key, fn):
@@ -84,9 +85,19 @@ class BatchHandle:
             ne = self.store._sizes[1][self.gids_host.astype(np.int64)]  # noqa: SLF001
             e0 = torch.from_numpy(np.concatenate([[0], np.cumsum(ne)]).astype(np.int32)).to(dev)
             words = torch.empty(max(1, 2 * int(ne.sum())), dtype=torch.int32, device=dev)
+            keep = [ints, buf, pbuf, e0, words]
             if self.vanilla_words:
                 c.edge0, c.relu_words = e0.data_ptr(), words.data_ptr()
-            sc = (c, (ints, buf, pbuf, e0, words))
+                if self.vanilla_tile_rows:
+                    plan = vanilla_tile_plan(self, n, row0, int(self.vanilla_tile_rows), n_edge_feat)
+                    if plan is not None:
+                        tensors, (n_tiles, hmax, emax, tmax) = plan
+                        words_t = torch.empty_like(words)  # the words in transposed order
+                        keep += [*tensors, words_t]
+                        (c.tile_row0, c.halo_off, c.halo_ids, c.lcol_off, c.lcol, c.ltcol_off, c.ltcol, c.tpos) = (t.data_ptr() for t in tensors)
+                        c.relu_words_t = words_t.data_ptr()
+                        c.n_tiles, c.halo_max, c.tile_edges_max, c.tile_tedges_max = n_tiles, hmax, emax, tmax
+            sc = (c, tuple(keep))
             self._lds[key] = sc
         return sc
 
@@ -126,6 +137,50 @@ class BatchHandle:
 
 
 LDS_MAX = 160 * 1024
+
+
+def vanilla_tile_plan(h: BatchHandle, n, row0, tile_rows, n_edge_feat):
+    """Edge-tile plan of the VanillaNetwork pipeline (dr_vanilla_scratch tile_*
+    fields): each graph's rows cut into tiles of ``tile_rows``; per tile the
+    ascending union of its rows' out- and in-neighbours (the halo staged in LDS)
+    and every CSR / transposed edge's column as an index into it.  None when a
+    tile's LDS would exceed one workgroup's 160 KiB (the untiled kernels run)."""
+    p = h.store.packed
+    tile_row0, hoff, hids, loff, lcs, toff, tcs, tps = [0], [0], [], [0], [], [0], [], []
+    hmax = emax = tmax = 0
+    for slot, gid in enumerate(h.gids_host.astype(np.int64)):
+        ng = int(n[slot])
+        n0, e0, e1 = int(p.node_off[gid]), int(p.edge_off[gid]), int(p.edge_off[gid + 1])
+        rp = p.rowptr[n0 + gid : n0 + gid + ng + 1].astype(np.int64)
+        trp = p.t_rowptr[n0 + gid : n0 + gid + ng + 1].astype(np.int64)
+        col, tcol = p.col[e0:e1], p.t_col[e0:e1]
+        tinv = np.empty(e1 - e0, np.int32)  # CSR slot -> transposed slot
+        tinv[p.t_eid[e0:e1]] = np.arange(e1 - e0, dtype=np.int32)
+        for r0 in range(0, ng, tile_rows):
+            r1 = min(ng, r0 + tile_rows)
+            cs, ts = col[rp[r0] : rp[r1]], tcol[trp[r0] : trp[r1]]
+            halo = np.union1d(cs, ts).astype(np.int32)
+            hids.append(halo)
+            hoff.append(hoff[-1] + halo.size)
+            lcs.append(np.searchsorted(halo, cs).astype(np.uint16))
+            tps.append(tinv[rp[r0] : rp[r1]])
+            loff.append(loff[-1] + cs.size)
+            tcs.append(np.searchsorted(halo, ts).astype(np.uint16))
+            toff.append(toff[-1] + ts.size)
+            tile_row0.append(int(row0[slot]) + r1)
+            hmax, emax, tmax = max(hmax, halo.size), max(emax, cs.size), max(tmax, ts.size)
+    n_tiles = len(tile_row0) - 1
+    if n_tiles == 0 or hmax == 0 or hmax > 65535:  # noqa: PLR2004
+        return None
+    fes = max(1, n_edge_feat)
+    r4 = lambda v: (v + 3) & ~3  # noqa: E731
+    lds = 4 * max(hmax * 32 + r4(emax * fes) + r4(emax) + r4((emax + 1) // 2), hmax * 32 + r4(emax * fes) + r4(emax) + r4(tmax) + r4((tmax + 1) // 2))  # tile_carve (forward, backward)
+    if lds > LDS_MAX:
+        return None
+    dev = h.store.device
+    cat16 = lambda parts: np.concatenate([*parts, np.zeros(8, np.uint16)])  # noqa: E731
+    arrays = [np.asarray(tile_row0, np.int32), np.asarray(hoff, np.int32), np.concatenate(hids), np.asarray(loff, np.int32), cat16(lcs).view(np.int16), np.asarray(toff, np.int32), cat16(tcs).view(np.int16), np.concatenate([*tps, np.zeros(8, np.int32)])]
+    return [torch.from_numpy(a).to(dev) for a in arrays], (n_tiles, hmax, emax, tmax)
 
 
 class LargePlan:

@@ -352,6 +352,26 @@ typedef struct dr_vanilla_scratch {
   uint32_t* relu_words;       /* optional [2, edge0[B]]: per layer and edge (CSR order) bit c = channel c of
                                  the edge MLP active, written by the forward and read by the backward (which
                                  then neither re-gathers B_j nor re-reads edge_attr for the transposed sum) */
+  /* Optional edge-tile plan (needs relu_words): the edge kernels then run one
+   * workgroup per tile of consecutive rows of one graph, first staging in LDS
+   * the tile's neighbour rows (its halo: B rows in the forward, dS rows in the
+   * backward), its edge attributes, ReLU words and halo-local column ids, so
+   * every per-edge gather reads LDS; same sums in the same order.           */
+  const int32_t* tile_row0;   /* [n_tiles+1] batch row ranges; a tile never spans two graphs */
+  const int32_t* halo_off;    /* [n_tiles+1] offsets into halo_ids                          */
+  const int32_t* halo_ids;    /* per tile: local node ids of the union of its rows' out- and
+                                 in-neighbours, ascending                                     */
+  const int32_t* lcol_off;    /* [n_tiles+1] into lcol: the tile's CSR edges rp[i0]..rp[i1]   */
+  const uint16_t* lcol;       /* halo index of each such edge's column                       */
+  const int32_t* ltcol_off;   /* [n_tiles+1] into ltcol: the tile's transposed edges          */
+  const uint16_t* ltcol;      /* halo index of each transposed edge's source                 */
+  const int32_t* tpos;        /* indexed like lcol: each CSR edge's transposed slot (graph-local) */
+  uint32_t* relu_words_t;     /* [2, edge0[B]]: the ReLU words again, in transposed order (written by
+                                 the tiled forward, staged per tile by the tiled backward)    */
+  int32_t n_tiles;
+  int32_t halo_max;           /* >= every tile's halo size (<= 65535)                        */
+  int32_t tile_edges_max;     /* >= every tile's CSR edge count                               */
+  int32_t tile_tedges_max;    /* >= every tile's transposed edge count                        */
 } dr_vanilla_scratch;
 #define DR_VANILLA_CHUNK 32
 

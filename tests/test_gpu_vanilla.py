@@ -72,15 +72,18 @@ def test_vanilla_pretrained_reference_weights_golden(golden):
     loss.backward()
     assert float(loss.detach()) == pytest.approx(float(z["loss"]), rel=1e-4)
     ref = golden_grads(z)
+    # ~11.7k directed edges per graph summed in another order than the
+    # reference's per-edge [x_i | x_j | e] W^T: normwise floor 1e-5 max|ref|
+    # (measured: 5e-6 on the largest edge-MLP weight gradient)
     for n, p in m.named_parameters():
-        assert_grad_close(p.grad.cpu().numpy(), ref[n], err_msg=n)
+        assert_grad_close(p.grad.cpu().numpy(), ref[n], ntol=1e-5, err_msg=n)
     # the fused training step on the same batch: same loss and gradients
     step = FusedTrainStep(m, loss="ce")
     h = resolve_batch(golden_batch(z), DEV, require_clusters=False)
     lf, _ = step.step(h)
     assert float(lf) == pytest.approx(float(z["loss"]), rel=1e-4)
     for n, g in zip(amd.PARAM_NAMES, step.grads):
-        assert_grad_close(g.cpu().numpy(), ref[n], err_msg=n)
+        assert_grad_close(g.cpu().numpy(), ref[n], ntol=1e-5, err_msg=n)
 
 
 def test_vanilla_layer_arbitrary_edges_vs_oracle():
@@ -196,5 +199,43 @@ def test_vanilla_pipeline_relu_words_bit_identical_to_recomputed(fe):
         amd.graph_pass(m, h, m.ordered_params(), 1, _lib.DR_PASS_FORWARD | _lib.DR_PASS_BACKWARD, loss_kind=_lib.DR_LOSS_MSE, loss_scale=0.3, out=out, slab=slab, head=head)
         torch.cuda.synchronize()
         res.append((out.cpu(), slab.cpu(), head.cpu()))
+    for a, b in itertools.zip_longest(*res):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("fe,tile", [(3, 64), (1, 32), (4, 128)])
+def test_vanilla_pipeline_halo_tiles_bit_identical(fe, tile):
+    """The tiled edge kernels (each tile's halo rows, edge attributes, words and
+    halo-local columns staged in LDS) give exactly the outputs, slabs, head
+    vectors and ReLU words of the untiled 8-in-flight kernels, on atom-size
+    graphs, a small graph, a node without edges and a hub row."""
+    import itertools
+
+    from deeprank2_amd import _lib
+
+    datas = _datas(2, seed=47, n_lo=900, n_hi=1300, mean_degree=15.0) + _datas(1, seed=48, n_lo=20, n_hi=30)
+    gen = np.random.default_rng(6)
+    for d in datas:
+        d.cluster0 = d.cluster1 = None
+    ei = datas[0].edge_index
+    hub = torch.stack([torch.full((90,), 5, dtype=torch.long), torch.arange(100, 190)])
+    datas[0].edge_index = torch.cat([ei[:, (ei[0] != 7) & (ei[1] != 7)], hub, hub.flip(0)], 1)  # node 7 isolated, node 5 a hub
+    for d in datas:
+        d.edge_attr = torch.from_numpy(gen.normal(size=(d.edge_index.shape[1], fe)).astype(np.float32))
+    store = GraphStore(pack_graphs(records_from_batch(P.Batch.from_data_list(datas)), require_clusters=False), DEV)
+    torch.manual_seed(18)
+    m = amd.VanillaNetwork(30, 2, fe).to(DEV)
+    res = []
+    for t in (tile, 0):
+        h = BatchHandle(store, np.arange(len(datas)))
+        h.vanilla_pipeline, h.vanilla_tile_rows = True, t
+        out = torch.empty(len(datas), 2, device=DEV)
+        slab = torch.zeros(len(datas) * m.fused_spec.slab_stride(30), device=DEV)
+        head = torch.zeros(len(datas) * m.fused_spec.head_stride(2), device=DEV)
+        amd.graph_pass(m, h, m.ordered_params(), 2, _lib.DR_PASS_FORWARD | _lib.DR_PASS_BACKWARD, loss_kind=_lib.DR_LOSS_CE, loss_scale=0.3, out=out, slab=slab, head=head)
+        torch.cuda.synchronize()
+        c, keep = h.vanilla_scratch(30, fe)
+        assert (c.n_tiles > 0) == (t > 0)
+        res.append((out.cpu(), slab.cpu(), head.cpu(), keep[4].cpu()))
     for a, b in itertools.zip_longest(*res):
         assert torch.equal(a, b)
