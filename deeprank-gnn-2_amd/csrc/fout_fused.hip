@@ -645,6 +645,353 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
   DRK_STAMP(10);
 }
 
+// ---- graphs beyond one workgroup's LDS (atom-level): tile kernel + tail kernel ----
+// Same arithmetic as fout_graph_kernel, split like dr_ginet_large_pass and on
+// its plan (dr_large_plan: tiles of tile_rows nodes, optional LDS halos, the
+// depth-0 pool combined over tiles by 64-bit atomic max keys):
+//   1. one 512-thread workgroup per tile: the tile's Zm rows (the mean over
+//      out-neighbours, from halo-staged X rows), conv1 on MFMA with the same
+//      operand order and bias add, relu, and the tile's share of the depth-0
+//      max per (cluster, channel) as key (H bits << 32 | ~node) -- first max in
+//      node order, NaN never enters, exactly the strict '>' scan; the Zm rows
+//      (and SGAT's c1 in column XS) go to plan->z for the tail;
+//   2. one 1024-thread workgroup per graph: decode the keys into P1 / A1 and
+//      run fout_tail, reading x at the pooling args from the store and Zm / c1
+//      from plan->z.  Bit-identical to fout_graph_kernel on graphs both run.
+constexpr int NTA = 512;
+constexpr int TRF = DR_LARGE_TILE;
+
+struct FoutLargeArgs {
+  FoutArgs f;
+  dr_large_plan plan;
+  int32_t zs;  // plan->z row stride: r4(F) (FoutNet) or r4(F) + 4 (SGAT: c1 in column r4(F))
+};
+
+struct FConvCarve {
+  int KP, LDA, XS, w, b1, a, h, c1, m0i, m0p, xh, hid, trp, ew, lcol, total;
+};
+__host__ __device__ inline FConvCarve fconv_carve(int N, int F, int K0, int HM, int EM, bool sg) {
+  FConvCarve c;
+  c.KP = r16(2 * F);
+  c.LDA = c.KP + 4;  // lanes (row li, k + kq) of an operand read: banks 4 li + kq, distinct
+  c.XS = r4(F);
+  int o = 0;
+#define TAKE(field, words) \
+  c.field = o;             \
+  o += r4(words);
+  TAKE(w, c.KP * 16)
+  TAKE(b1, 16)
+  TAKE(a, TRF * c.LDA)  // [x_i | Zm_i | 0] per tile row
+  TAKE(h, TRF * 16)
+  TAKE(c1, sg ? TRF : 0)
+  TAKE(m0i, HM ? TRF : N)
+  TAKE(m0p, K0 + 1)
+  TAKE(xh, HM * c.XS)
+  TAKE(hid, HM)
+  TAKE(trp, HM ? TRF + 1 : 0)
+  // last: the tile's edges as halo indices (uint16), then (SGAT) their weights
+  // at lcol + r4((ne + 8) / 2) for the tile's ne edges -- so the kernel, which
+  // carves with EM = 0, places them by its own tile's edge count
+  TAKE(lcol, HM ? (EM + 8) / 2 : 0)
+  TAKE(ew, (HM && sg) ? EM + 8 : 0)
+#undef TAKE
+  c.total = o;
+  return c;
+}
+
+template <bool SG>
+__global__ void __launch_bounds__(NTA) fout_large_conv1_kernel(FoutLargeArgs la) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const FoutArgs& a = la.f;
+  const dr_large_plan& pl = la.plan;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tile = blockIdx.x;
+  const int b = pl.tile_slot[tile];
+  const int t = tile - pl.tile_first[b];
+  const dr_graph_desc d = a.descs[b];
+  const dr_graph_store& s = a.s;
+  const int g = d.gid;
+  const int64_t n0 = d.node0, ec0 = d.col0, k00 = d.k0;
+  const int N = d.n_nodes, K0 = d.n_k0, F = s.n_feat;
+  const int TRr = pl.tile_rows;
+  const int r0 = t * TRr, nrows = min(TRr, N - r0);
+  const FConvCarve c = fconv_carve(N, F, K0, pl.halo_max, 0, SG);
+  const int KP = c.KP, LDA = c.LDA, XS = c.XS, ZS = la.zs;
+  float* sW = lds + c.w;
+  float* sB1 = lds + c.b1;
+  float* sA = lds + c.a;
+  float* sH = lds + c.h;
+  float* sC1 = lds + c.c1;
+  int* sm0i = reinterpret_cast<int*>(lds + c.m0i);
+  int* sm0p = reinterpret_cast<int*>(lds + c.m0p);
+  const bool compact = pl.tile_members != nullptr;
+  if (compact) {  // this tile's members by cluster (host-built), runs from tile_mptr
+    dma_words<NTA>(sm0i, pl.tile_members + (int64_t)tile * TRr, nrows);
+    dma_words<NTA>(sm0p, pl.tile_mptr + (int64_t)tile * (pl.k0_max + 1), K0 + 1);
+  } else {
+    dma_words<NTA>(sm0i, s.m0_idx + n0, N);
+    dma_words<NTA>(sm0p, s.m0_ptr + k00 + g, K0 + 1);
+  }
+  for (int p = tid; p < KP * 16; p += NTA) {  // [Wc; Wn; 0], k-major as stored
+    const int k = p >> 4, o = p & 15;
+    sW[p] = k < F ? a.w.wc1[k * 16 + o] : (k < 2 * F ? a.w.wn1[(k - F) * 16 + o] : 0.f);
+  }
+  if (tid < 16) sB1[tid] = a.w.b1[tid];
+  // own rows x_i into the A tile (columns 0..F-1); pad columns past 2F: 0
+  const float* X = s.x + n0 * (int64_t)XS;
+  for (int p = tid; p < nrows * LDA; p += NTA) {
+    const int r = p / LDA, k = p - r * LDA;
+    if (k < F) sA[p] = X[(int64_t)(r0 + r) * XS + k];
+    else if (k >= 2 * F) sA[p] = 0.f;
+  }
+  float* zg = pl.z + (int64_t)pl.z_row0[b] * ZS;
+  // Zm = D^-1 A X for the tile's rows (SGAT: Zw, c1): 8 lanes per row, 16-byte chunks
+  auto gather_rows = [&](const uint16_t* col, const float* ew, const float* Xs, const int* rowp, int ebase) {
+    const int nch = XS >> 2, sub = tid & 7;
+    for (int r = tid >> 3; r < nrows; r += NTA / 8) {
+      const int eb = rowp[r] - ebase, ee = rowp[r + 1] - ebase;
+      const float deg = SG ? (float)imax(ee - eb, 1) : (float)(ee - eb);
+      for (int ch = sub; ch < nch; ch += 8) {
+        const int c4 = ch * 4;
+        float sw = 0.f;
+        const float4 acc = SG ? gather_row_chunk_w(col, ew, eb, ee, Xs, XS, c4, sw) : gather_row_chunk(col, eb, ee, Xs, XS, c4);
+        const float4 zm = make_float4(acc.x / deg, acc.y / deg, acc.z / deg, acc.w / deg);  // 0/0 = NaN (torch.mean(empty))
+        const float zv[4] = {zm.x, zm.y, zm.z, zm.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (c4 + q < F) sA[r * LDA + F + c4 + q] = zv[q];
+        *reinterpret_cast<float4*>(zg + (int64_t)(r0 + r) * ZS + c4) = zm;
+        if (SG && ch == 0) {
+          sC1[r] = sw / deg;
+          zg[(int64_t)(r0 + r) * ZS + XS] = sw / deg;
+        }
+      }
+    }
+  };
+  if (pl.halo_ids) {  // halo path: the tile's neighbour X rows, edges and (SGAT) weights in LDS
+    int* strp = reinterpret_cast<int*>(lds + c.trp);
+    int* shid = reinterpret_cast<int*>(lds + c.hid);
+    uint16_t* slcol = reinterpret_cast<uint16_t*>(lds + c.lcol);
+    float* sXh = lds + c.xh;
+    float* sEw;
+    const int h0 = pl.halo_off[tile], H = pl.halo_off[tile + 1] - h0;
+    dma_words<NTA>(strp, s.rowptr + n0 + g + r0, nrows + 1);
+    dma_words<NTA>(shid, pl.halo_ids + h0, H);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int ebase = strp[0], ne = strp[nrows] - ebase;
+    sEw = lds + c.lcol + r4((ne + 8) / 2);
+    dma_x4<NTA>(slcol, pl.lcol + pl.lcol_off[tile], (ne + 7) / 8);
+    if (SG) dma_words<NTA>(sEw, s.ea + ec0 + ebase, ne);  // Fe == 1: weights contiguous in CSR order
+    {
+      const int nch = XS >> 2, tot = H * nch;
+      const int wv = __builtin_amdgcn_readfirstlane(wave);
+      for (int base = wv * 64; base < tot; base += NTA)
+        if (base + lane < tot) {
+          const int hr = (base + lane) / nch, ch = base + lane - hr * nch;
+          __builtin_amdgcn_global_load_lds(DRK_AS1(X + (int64_t)shid[hr] * XS + ch * 4), DRK_AS3(sXh + base * 4), 16, 0, 0);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    gather_rows(slcol, sEw, sXh, strp, ebase);
+  } else {  // per-edge gather of X rows from HBM / L2
+    gather_rows(s.col + ec0, SG ? s.ea + ec0 : nullptr, X, s.rowptr + n0 + g + r0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // conv1 on MFMA: H1 = relu([c1 x | Zm] [Wc; Wn] + b) -- fout_graph_kernel's operand order
+  {
+    const int li = lane & 15, kq = lane >> 4;
+    for (int tt = wave; tt * 16 < nrows; tt += NTA / 64) {
+      const int q0 = tt * 16;
+      const int ar = min(q0 + li, nrows - 1);
+      const float cx = SG ? sC1[ar] : 1.f;
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < KP; k += 16) {
+        float av[4], bv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int kk = k + 4 * u + kq;
+          av[u] = kk < F ? cx * sA[ar * LDA + kk] : sA[ar * LDA + kk];
+          bv[u] = sW[kk * 16 + li];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = q0 + kq * 4 + r;
+        if (row < nrows) sH[row * 16 + li] = relu_keepnan(acc[r] + sB1[li]);
+      }
+    }
+  }
+  __syncthreads();
+  // the tile's share of the depth-0 max: members of each cluster inside the tile (a sub-run of its ascending list)
+  for (int p = tid; p < K0 * 16; p += NTA) {
+    const int k = p >> 4, ch = p & 15;
+    int mb = sm0p[k], me = sm0p[k + 1];
+    if (!compact) {
+      int lo = mb, hi = me;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (sm0i[mid] < r0) lo = mid + 1;
+        else hi = mid;
+      }
+      mb = lo;
+      hi = me;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (sm0i[mid] < r0 + nrows) lo = mid + 1;
+        else hi = mid;
+      }
+      me = lo;
+    }
+    float best = LOWEST;
+    int arg = N;
+    for (int m = mb; m < me; ++m) {
+      const int i = sm0i[m];
+      const float v = sH[(i - r0) * 16 + ch];
+      if (v > best) {
+        best = v;
+        arg = i;
+      }
+    }
+    if (best > LOWEST)
+      __hip_atomic_fetch_max((__attribute__((address_space(1))) unsigned long long*)(pl.part_key) + ((int64_t)b * pl.k0_max + k) * 32 + ch,
+                             ((unsigned long long)__float_as_uint(best) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)arg),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+struct FTailCarve {
+  int w2, fc1, fc2, p1, a1, dp1, zm2, s2, h2, d2, dz2, p1rp, p1c, p1trp, p1tc, m1p, m1i, p2, nt, head, dgp, p1w, p1tid, c2, total;
+};
+__host__ __device__ inline FTailCarve ftail_carve(int K0, int P1, int K1, int alias, int OUT, bool sg) {
+  FTailCarve c;
+  int o = 0;
+#define TAKE(field, words) \
+  c.field = o;             \
+  o += r4(words);
+  TAKE(w2, 16 * 32 * 2 + 32 + 16)
+  TAKE(fc1, 64 * 32 + 64)
+  TAKE(fc2, OUT * 64 + OUT)
+  TAKE(p1, K0 * 16)
+  TAKE(a1, K0 * 16)
+  TAKE(dp1, K0 * 16)
+  TAKE(zm2, K0 * 16)
+  TAKE(s2, K0 * 32)
+  TAKE(h2, K0 * 32)
+  TAKE(d2, K0 * 32)
+  TAKE(dz2, K0 * 16)
+  TAKE(p1rp, K0 + 1)
+  TAKE(p1c, P1)
+  if (alias) {
+    c.p1trp = c.p1rp;
+    c.p1tc = c.p1c;
+  } else {
+    TAKE(p1trp, K0 + 1)
+    TAKE(p1tc, P1)
+  }
+  TAKE(m1p, K1 + 1)
+  TAKE(m1i, K0)
+  TAKE(p2, K1 * 32)
+  TAKE(nt, K1 * 32)
+  TAKE(head, HEADW)
+  TAKE(dgp, NW * 64)
+  TAKE(p1w, sg ? P1 : 0)
+  TAKE(p1tid, sg ? P1 : 0)
+  TAKE(c2, sg ? K0 : 0)
+#undef TAKE
+  c.total = o;
+  return c;
+}
+
+template <bool SG>
+__global__ void __launch_bounds__(NT) fout_large_tail_kernel(FoutLargeArgs la) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const FoutArgs& a = la.f;
+  const dr_large_plan& pl = la.plan;
+  const int tid = threadIdx.x;
+  const int b = blockIdx.x;
+  const dr_graph_store& s = a.s;
+  const dr_graph_desc d = a.descs[b];
+  const int g = d.gid;
+  const int64_t n0 = d.node0, k00 = d.k0, q0 = d.p1, k10 = d.k1;
+  const int N = d.n_nodes, K0 = d.n_k0, P1 = d.n_p1, K1 = d.n_k1;
+  const int F = s.n_feat, alias = s.transpose_aliased, OUT = a.p.out_dim, XS = r4(F), ZS = la.zs;
+  const FTailCarve c = ftail_carve(K0, P1, K1, alias, OUT, SG);
+  FoutTail t;
+  float* w2 = lds + c.w2;
+  t.Wc2 = w2;
+  t.Wn2 = w2 + 512;
+  t.B2 = w2 + 1024;
+  t.Fc1 = lds + c.fc1;
+  t.Fc1b = lds + c.fc1 + 2048;
+  t.Fc2 = lds + c.fc2;
+  t.P1 = lds + c.p1;
+  t.A1 = reinterpret_cast<int*>(lds + c.a1);
+  t.dP1 = lds + c.dp1;
+  t.Zm2 = lds + c.zm2;
+  t.S2 = lds + c.s2;
+  t.H2 = lds + c.h2;
+  t.D2 = lds + c.d2;
+  t.Dz2 = lds + c.dz2;
+  t.p1rp = reinterpret_cast<int*>(lds + c.p1rp);
+  t.p1c = reinterpret_cast<int*>(lds + c.p1c);
+  t.p1trp = reinterpret_cast<int*>(lds + c.p1trp);
+  t.p1tc = reinterpret_cast<int*>(lds + c.p1tc);
+  t.m1p = reinterpret_cast<int*>(lds + c.m1p);
+  t.m1i = reinterpret_cast<int*>(lds + c.m1i);
+  t.P2 = lds + c.p2;
+  t.NTie = lds + c.nt;
+  t.G = lds + c.head;
+  t.Hpre = t.G + 32;
+  t.Hh = t.Hpre + 64;
+  t.Dh = t.Hh + 64;
+  t.DG = t.Dh + 64;
+  t.Dout = t.DG + 32;
+  t.DGp = lds + c.dgp;
+  t.P1w = lds + c.p1w;
+  t.P1tid = reinterpret_cast<int*>(lds + c.p1tid);
+  t.C2 = lds + c.c2;
+  const float y_g = s.y[g];
+  dma_words<NT>(t.p1rp, s.p1_rowptr + k00 + g, K0 + 1);
+  dma_words<NT>(t.p1c, s.p1_col + q0, P1);
+  if (!alias) {
+    dma_words<NT>(t.p1trp, s.p1t_rowptr + k00 + g, K0 + 1);
+    dma_words<NT>(t.p1tc, s.p1t_col + q0, P1);
+  }
+  dma_words<NT>(t.m1p, s.m1_ptr + k10 + g, K1 + 1);
+  dma_words<NT>(t.m1i, s.m1_idx + k00, K0);
+  if (SG) {
+    dma_words<NT>(t.P1w, s.p1_ea + q0, P1);
+    dma_words<NT>(t.P1tid, s.p1t_pid + q0, P1);
+  }
+  for (int p = tid; p < 1072; p += NT) {
+    const int q = p;
+    w2[p] = q < 512 ? a.w.wc2[q] : q < 1024 ? a.w.wn2[q - 512] : q < 1056 ? a.w.b2[q - 1024] : a.w.b1[q - 1056];
+  }
+  for (int p = tid; p < 2048 + 64; p += NT) lds[c.fc1 + p] = p < 2048 ? a.w.fc1w[p] : a.w.fc1b[p - 2048];
+  for (int p = tid; p < OUT * 65; p += NT) lds[c.fc2 + p] = p < OUT * 64 ? a.w.fc2w[p] : a.w.fc2b[p - OUT * 64];
+  for (int p = tid; p < K0 * 16; p += NT) {  // the depth-0 pool from the tiles' keys (and the keys back to zero)
+    unsigned long long* kp = reinterpret_cast<unsigned long long*>(pl.part_key) + ((int64_t)b * pl.k0_max + (p >> 4)) * 32 + (p & 15);
+    const unsigned long long key = *kp;
+    *kp = 0ull;
+    t.P1[p] = key ? __uint_as_float((uint32_t)(key >> 32)) : 0.f;
+    t.A1[p] = key ? (int)(0xffffffffu - (uint32_t)key) : N;
+  }
+  const int64_t counter0 = (a.p.step_counter && b == 0) ? a.p.step_counter[0] : 0;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (a.p.step_counter && b == 0 && tid == 0) a.p.step_counter[1] = counter0;  // snapshot for dr_reduce_update
+  __syncthreads();
+  const float* X = s.x + n0 * (int64_t)XS;
+  const float* z = pl.z + (int64_t)pl.z_row0[b] * ZS;
+  fout_tail<SG>(a.p, t, b, N, K0, K1, F, OUT, y_g,
+                [=](int i, int kk) { return (SG ? z[(int64_t)i * ZS + XS] : 1.f) * X[(int64_t)i * XS + kk]; },
+                [=](int i, int kk) { return z[(int64_t)i * ZS + kk]; });
+}
+
 }  // namespace
 
 namespace {
@@ -698,4 +1045,74 @@ extern "C" int dr_fout_graph_pass(const dr_graph_store* store, const dr_graph_de
 extern "C" int dr_sgat_graph_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
                                   const dr_fout_weights* w, const dr_pass* pass, int32_t lds_bytes, void* stream) {
   return fout_family_pass(true, store, descs, n_batch, w, pass, lds_bytes, stream);
+}
+
+extern "C" int64_t dr_fout_large_conv_lds_bytes(int32_t n_nodes, int32_t n_feat, int32_t k0, int32_t halo_max,
+                                                int32_t tile_edges_max, int32_t sgat) {
+  return 4LL * fconv_carve(n_nodes, n_feat, k0, halo_max, tile_edges_max, sgat != 0).total;
+}
+
+extern "C" int64_t dr_fout_tail_lds_bytes(int32_t k0, int32_t p1_edges, int32_t k1, int32_t transpose_aliased,
+                                          int32_t out_dim, int32_t sgat) {
+  return 4LL * ftail_carve(k0, p1_edges, k1, transpose_aliased, out_dim, sgat != 0).total;
+}
+
+namespace {
+int fout_large_family(bool sg, const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                      const dr_large_plan* plan, const dr_fout_weights* w, const dr_pass* pass, int32_t z_stride,
+                      int32_t conv_lds_bytes, int32_t tail_lds_bytes, void* stream) {
+  if (!store || !descs || !w || !pass || !plan || n_batch < 0) return DR_E_ARG;
+  if (sg && (store->n_edge_feat != 1 || !store->ea || !store->p1_ea || !store->p1t_pid)) return DR_E_UNSUPPORTED;
+  if (pass->out_dim < 1 || pass->out_dim > DR_MAX_OUT) return DR_E_UNSUPPORTED;
+  if (store->n_feat < 1 || store->n_feat > 64) return DR_E_UNSUPPORTED;
+  const int XS = (store->n_feat + 3) & ~3;
+  if (z_stride != (sg ? XS + 4 : XS)) return DR_E_ARG;
+  if (conv_lds_bytes > 160 * 1024 || tail_lds_bytes > 160 * 1024) return DR_E_LDS;
+  if (!plan->tile_first || !plan->z_row0 || !plan->tile_slot || !plan->z || !plan->part_key) return DR_E_ARG;
+  if (plan->n_tiles < n_batch || plan->k0_max < 1 || plan->k0_max > 64 || plan->arrive) return DR_E_ARG;
+  if (plan->tile_rows < 16 || plan->tile_rows > TRF || plan->tile_rows % 16) return DR_E_ARG;
+  if (plan->halo_ids && (plan->halo_max < 1 || plan->halo_max > 65535 || !plan->halo_off || !plan->lcol_off ||
+                         !plan->lcol || !plan->tile_members || !plan->tile_mptr))
+    return DR_E_ARG;
+  if (!plan->halo_ids && plan->halo_max) return DR_E_ARG;
+  if ((pass->flags & DR_PASS_BACKWARD) && (!pass->slab || !pass->head)) return DR_E_ARG;
+  if ((pass->flags & DR_PASS_BACKWARD) && pass->loss_kind == DR_LOSS_NONE && !pass->dout) return DR_E_ARG;
+  if ((pass->flags & DR_PASS_FORWARD) && !pass->out) return DR_E_ARG;
+  if (pass->use_dropout != DR_DROPOUT_OFF || pass->compute_dtype != DR_DTYPE_F32) return DR_E_UNSUPPORTED;
+  if (n_batch == 0) return DR_OK;
+  const void* conv = sg ? reinterpret_cast<const void*>(&fout_large_conv1_kernel<true>) : reinterpret_cast<const void*>(&fout_large_conv1_kernel<false>);
+  const void* tail = sg ? reinterpret_cast<const void*>(&fout_large_tail_kernel<true>) : reinterpret_cast<const void*>(&fout_large_tail_kernel<false>);
+  DR_CHECK(dr_allow_big_lds(conv));
+  DR_CHECK(dr_allow_big_lds(tail));
+  FoutLargeArgs la;
+  la.f.s = *store;
+  la.f.w = *w;
+  la.f.p = *pass;
+  la.f.descs = descs;
+  la.f.B = n_batch;
+  la.f.lds_bytes = tail_lds_bytes;
+  la.plan = *plan;
+  la.zs = z_stride;
+  hipStream_t st = (hipStream_t)stream;
+  if (sg) {
+    hipLaunchKernelGGL(fout_large_conv1_kernel<true>, dim3(plan->n_tiles), dim3(NTA), conv_lds_bytes, st, la);
+    hipLaunchKernelGGL(fout_large_tail_kernel<true>, dim3(n_batch), dim3(NT), tail_lds_bytes, st, la);
+  } else {
+    hipLaunchKernelGGL(fout_large_conv1_kernel<false>, dim3(plan->n_tiles), dim3(NTA), conv_lds_bytes, st, la);
+    hipLaunchKernelGGL(fout_large_tail_kernel<false>, dim3(n_batch), dim3(NT), tail_lds_bytes, st, la);
+  }
+  return (int)hipGetLastError();
+}
+}  // namespace
+
+extern "C" int dr_fout_large_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                                  const dr_large_plan* plan, const dr_fout_weights* w, const dr_pass* pass,
+                                  int32_t z_stride, int32_t conv_lds_bytes, int32_t tail_lds_bytes, void* stream) {
+  return fout_large_family(false, store, descs, n_batch, plan, w, pass, z_stride, conv_lds_bytes, tail_lds_bytes, stream);
+}
+
+extern "C" int dr_sgat_large_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                                  const dr_large_plan* plan, const dr_fout_weights* w, const dr_pass* pass,
+                                  int32_t z_stride, int32_t conv_lds_bytes, int32_t tail_lds_bytes, void* stream) {
+  return fout_large_family(true, store, descs, n_batch, plan, w, pass, z_stride, conv_lds_bytes, tail_lds_bytes, stream);
 }

@@ -210,6 +210,10 @@ SIGNATURES = [
     ("dr_ginet_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 8),
     ("dr_ginet_large_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(LargePlanC), ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, ctypes.c_int32, VP]),
     ("dr_ginet_large_conv_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 5),
+    ("dr_fout_large_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(LargePlanC), ctypes.POINTER(FoutWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP]),
+    ("dr_sgat_large_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(LargePlanC), ctypes.POINTER(FoutWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP]),
+    ("dr_fout_large_conv_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 6),
+    ("dr_fout_tail_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 6),
     ("dr_ginet_large_conv_lds_bytes_bf16", ctypes.c_int64, [ctypes.c_int32] * 5),
     ("dr_ginet_tail_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 5),
     ("dr_vanilla_graph_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(VanillaWeightsC), ctypes.POINTER(PassC), ctypes.POINTER(VanillaScratchC), ctypes.c_int32, VP]),

@@ -127,12 +127,16 @@ class BatchHandle:
         sc = self._lds.get("vanilla_fused_scratch")
         return sc is None or int(sc[2][-1].item()) == 0
 
-    def large_plan(self, out_dim, bf16=False):
-        """Tiling + workspaces of the large-graph path (dr_large_plan), built once per batch."""
-        plan = self._lds.get(("large", out_dim, bf16))
+    def large_plan(self, out_dim, bf16=False, kind="ginet"):
+        """Tiling + workspaces of the large-graph path (dr_large_plan), built once per batch
+        (kind: "ginet", or "fout" / "sgat" for dr_fout_large_pass / dr_sgat_large_pass)."""
+        plan = self._lds.get(("large", out_dim, bf16, kind))
         if plan is None:
-            plan = LargePlan(self, out_dim, use_halos=self.large_halos, use_atomic_max=self.large_atomic_max or self.large_onepass, bf16=bf16, onepass=self.large_onepass)
-            self._lds[("large", out_dim, bf16)] = plan
+            if kind == "ginet":
+                plan = LargePlan(self, out_dim, use_halos=self.large_halos, use_atomic_max=self.large_atomic_max or self.large_onepass, bf16=bf16, onepass=self.large_onepass)
+            else:
+                plan = LargePlan(self, out_dim, use_halos=self.large_halos, use_atomic_max=True, kind=kind)
+            self._lds[("large", out_dim, bf16, kind)] = plan
         return plan
 
 
@@ -189,8 +193,9 @@ class LargePlan:
 
     TILE = 64  # measured best for atom-level graphs with tile halos (tools/large_tiles.py)
 
-    def __init__(self, h: BatchHandle, out_dim, tile_rows=None, use_halos=True, use_atomic_max=True, bf16=False, onepass=False):
+    def __init__(self, h: BatchHandle, out_dim, tile_rows=None, use_halos=True, use_atomic_max=True, bf16=False, onepass=False, kind="ginet"):
         st = h.store
+        self.kind = kind
         self.TILE = int(tile_rows or h.large_tile or self.TILE)
         n, _e, k0, p1, k1 = (a[h.gids_host.astype(np.int64)] for a in st._sizes)  # noqa: SLF001
         self.k0_max = int(k0.max())
@@ -206,19 +211,26 @@ class LargePlan:
         self.n_tiles = int(tile_first[-1])
         dev = st.device
         self.ints = torch.from_numpy(np.concatenate([tile_first, z_row0, tile_slot])).to(dev)
-        self.z = torch.empty(max(1, int(z_row0[-1])) * st.x_stride, dtype=torch.float32, device=dev)
+        # z rows: GINet's Z = A X; FoutNet's Zm (stride r4(F)); SGAT's Zw + c1 (r4(F) + 4)
+        self.zs = st.x_stride + (4 if kind == "sgat" else 0)
+        self.z = torch.empty(max(1, int(z_row0[-1])) * self.zs, dtype=torch.float32, device=dev)
         self.part_val = torch.empty(self.n_tiles * self.k0_max * 32, dtype=torch.float32, device=dev)
         self.part_arg = torch.empty(self.n_tiles * self.k0_max * 32, dtype=torch.int32, device=dev)
         self.part_key = torch.zeros(h.B * self.k0_max * 32, dtype=torch.int64, device=dev)  # kept zero between passes
         lib = _lib.load()
         halo = self._halos(h, n) if use_halos else None
         hmax, emax = (halo[0], halo[1]) if halo is not None else (0, 0)
-        conv_lds = lib.dr_ginet_large_conv_lds_bytes_bf16 if bf16 else lib.dr_ginet_large_conv_lds_bytes
+        if kind == "ginet":
+            conv_lds = lib.dr_ginet_large_conv_lds_bytes_bf16 if bf16 else lib.dr_ginet_large_conv_lds_bytes
+        else:
+            sg = int(kind == "sgat")
+            conv_lds = lambda *a: lib.dr_fout_large_conv_lds_bytes(*a, sg)  # noqa: E731
         self.conv_lds = int(conv_lds(int(n.max()), st.n_feat, self.k0_max, hmax, emax))
         if halo is not None and self.conv_lds > LDS_MAX:  # halos too wide for LDS: per-edge HBM gather
             halo, hmax = None, 0
             self.conv_lds = int(conv_lds(int(n.max()), st.n_feat, self.k0_max, 0, 0))
-        self.tail_lds = int(lib.dr_ginet_tail_lds_bytes(self.k0_max, int(p1.max()), int(k1.max()), int(st.packed.transpose_aliased), out_dim))
+        tail_args = (self.k0_max, int(p1.max()), int(k1.max()), int(st.packed.transpose_aliased), out_dim)
+        self.tail_lds = int(lib.dr_ginet_tail_lds_bytes(*tail_args) if kind == "ginet" else lib.dr_fout_tail_lds_bytes(*tail_args, int(kind == "sgat")))
         if max(self.conv_lds, self.tail_lds) > LDS_MAX:
             msg = f"large-graph path needs {max(self.conv_lds, self.tail_lds)} B of LDS (> 160 KiB)"
             raise RuntimeError(msg)

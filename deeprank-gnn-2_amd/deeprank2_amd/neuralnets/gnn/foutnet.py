@@ -142,7 +142,14 @@ def _lds(n, e, k0, p1, k1, f, alias, out):
     return _lib.load().dr_fout_lds_bytes(n, e, f, k0, p1, k1, alias, out)
 
 
-SPEC = FusedSpec(PARAM_NAMES, recipe, slab_stride, head_stride, "dr_fout_graph_pass", weights_c, _lds, dropout=0.0, layers=layered.foutnet_forward)
+def _large(h, w, p):
+    """Graphs beyond one workgroup's LDS: tile conv1 kernel + per-graph tail (dr_fout_large_pass)."""
+    plan = h.large_plan(p.out_dim, kind="fout")
+    rc = _lib.load().dr_fout_large_pass(h.store.cstruct(), h.descs.data_ptr(), h.B, plan.c, w, p, plan.zs, plan.conv_lds, plan.tail_lds, _lib.stream_ptr(h.store.device))
+    _lib.check(rc, "dr_fout_large_pass")
+
+
+SPEC = FusedSpec(PARAM_NAMES, recipe, slab_stride, head_stride, "dr_fout_graph_pass", weights_c, _lds, dropout=0.0, large=_large, layers=layered.foutnet_forward)
 
 
 def graph_pass(h: BatchHandle, params, out_dim, flags, **kw):

@@ -156,7 +156,14 @@ def _lds(n, e, k0, p1, k1, f, alias, out):
     return _lib.load().dr_sgat_lds_bytes(n, e, f, k0, p1, k1, alias, out)
 
 
-SPEC = FusedSpec(PARAM_NAMES, recipe, foutnet.slab_stride, foutnet.head_stride, "dr_sgat_graph_pass", weights_c, _lds, dropout=0.0, layers=layered.sgat_forward)
+def _large(h, w, p):
+    """Graphs beyond one workgroup's LDS: tile conv1 kernel + per-graph tail (dr_sgat_large_pass)."""
+    plan = h.large_plan(p.out_dim, kind="sgat")
+    rc = _lib.load().dr_sgat_large_pass(h.store.cstruct(), h.descs.data_ptr(), h.B, plan.c, w, p, plan.zs, plan.conv_lds, plan.tail_lds, _lib.stream_ptr(h.store.device))
+    _lib.check(rc, "dr_sgat_large_pass")
+
+
+SPEC = FusedSpec(PARAM_NAMES, recipe, foutnet.slab_stride, foutnet.head_stride, "dr_sgat_graph_pass", weights_c, _lds, dropout=0.0, large=_large, layers=layered.sgat_forward)
 
 
 def graph_pass(h: BatchHandle, params, out_dim, flags, **kw):

@@ -324,6 +324,29 @@ int dr_sgat_graph_pass(const dr_graph_store* store, const dr_graph_desc* descs, 
 int64_t dr_sgat_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_feat, int32_t k0, int32_t p1_edges,
                           int32_t k1, int32_t transpose_aliased, int32_t out_dim);
 
+/* ---- FoutNet / SGAT on graphs beyond one workgroup's LDS (atom level) -----
+ * Replaces FoutNet.forward / SGAT.forward + backward (foutnet.py:48-66,99-118,
+ * sgat.py:56-133) where dr_fout_graph_pass / dr_sgat_graph_pass cannot hold
+ * the graph; same result bit for bit on graphs both can run.  Two launches on
+ * dr_large_plan (tiles, optional halos; part_key required, arrive unsupported):
+ *   1. one workgroup per tile: the mean over out-neighbours (SGAT: weighted,
+ *      count clamped to 1, and c1), conv1 on MFMA, relu, the tile's share of
+ *      the depth-0 max per (cluster, channel) as 64-bit atomic max keys; the
+ *      Zm rows (SGAT: and c1 in column r4(F)) -> plan->z with row stride
+ *      z_stride = r4(F) (FoutNet) or r4(F) + 4 (SGAT);
+ *   2. one workgroup per graph: the pool from the keys (keys left zero), then
+ *      conv2 ... head, loss and backward as the single-workgroup kernel.    */
+int dr_fout_large_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                       const dr_large_plan* plan, const dr_fout_weights* w, const dr_pass* pass, int32_t z_stride,
+                       int32_t conv_lds_bytes, int32_t tail_lds_bytes, void* stream);
+int dr_sgat_large_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                       const dr_large_plan* plan, const dr_fout_weights* w, const dr_pass* pass, int32_t z_stride,
+                       int32_t conv_lds_bytes, int32_t tail_lds_bytes, void* stream);
+int64_t dr_fout_large_conv_lds_bytes(int32_t n_nodes, int32_t n_feat, int32_t k0, int32_t halo_max,
+                                     int32_t tile_edges_max, int32_t sgat);
+int64_t dr_fout_tail_lds_bytes(int32_t k0, int32_t p1_edges, int32_t k1, int32_t transpose_aliased, int32_t out_dim,
+                               int32_t sgat);
+
 /* ---- VanillaNetwork (deeprank2/neuralnets/gnn/vanilla_gnn.py:10-65) ------- */
 
 typedef struct dr_vanilla_weights {
