@@ -639,7 +639,7 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
   t.Wc2 = sWc2; t.Wn2 = sWn2; t.B2 = sB2; t.Fc1 = sFc1; t.Fc1b = sFc1b; t.Fc2 = sFc2;
   t.P1w = sP1w; t.P1tid = sP1tid; t.C2 = sC2;
   // conv1 weight partials read [c1 x | Zm] at the pooling args from LDS
-  fout_tail<SG>(a.p, t, b, N, K0, K1, F, OUT, y_g,
+  fout_tail<SG>(a.p, t, a.p.slot ? a.p.slot[b] : b, N, K0, K1, F, OUT, y_g,
                 [=](int i, int kk) { return (SG ? sC1[i] : 1.f) * (WIDE ? sZm[i * LDZ + kk] : sX[i * XS + kk]); },
                 [=](int i, int kk) { return sZm[i * LDZ + ZO + kk]; });
   DRK_STAMP(10);
@@ -987,7 +987,7 @@ __global__ void __launch_bounds__(NT) fout_large_tail_kernel(FoutLargeArgs la) {
   __syncthreads();
   const float* X = s.x + n0 * (int64_t)XS;
   const float* z = pl.z + (int64_t)pl.z_row0[b] * ZS;
-  fout_tail<SG>(a.p, t, b, N, K0, K1, F, OUT, y_g,
+  fout_tail<SG>(a.p, t, a.p.slot ? a.p.slot[b] : b, N, K0, K1, F, OUT, y_g,
                 [=](int i, int kk) { return (SG ? z[(int64_t)i * ZS + XS] : 1.f) * X[(int64_t)i * XS + kk]; },
                 [=](int i, int kk) { return z[(int64_t)i * ZS + kk]; });
 }

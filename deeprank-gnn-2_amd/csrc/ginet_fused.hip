@@ -721,7 +721,7 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a) {
   // half up to N = 224): off the tail's critical path
   if (tid >= NT - 128) {
     const int r = tid - (NT - 128);
-    if (a.p.use_dropout) skeep[r] = drk::keep_unit(a.p, drop_offset, b, r) ? 1 : 0;
+    if (a.p.use_dropout) skeep[r] = drk::keep_unit(a.p, drop_offset, a.p.slot ? a.p.slot[b] : b, r) ? 1 : 0;
   }
   sW2[tid] = wv2;
   {
@@ -743,7 +743,8 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a) {
   TailLds t = tail_lds(c, lds);
   t.keep = skeep;
   auto zat = [&](int i, int kk) { return sZ[i * LDW + kk]; };
-  ginet_tail<decltype(zat), WT>(a, t, fc1_row, fc1_col, fc1_bias, b, N, K0, K1, F, OUT, y_g, drop_offset, zat);
+  // (dr_pass.slot: the graph's rows of the batch when it is split over launches)
+  ginet_tail<decltype(zat), WT>(a, t, fc1_row, fc1_col, fc1_bias, a.p.slot ? a.p.slot[b] : b, N, K0, K1, F, OUT, y_g, drop_offset, zat);
   return drop_offset;
 }
 
@@ -1431,6 +1432,7 @@ __device__ __forceinline__ void tail_body(const LargeArgs& la, int b, float* lds
   const int F = s.n_feat, alias = s.transpose_aliased, OUT = a.p.out_dim;
   const TailCarve c = tail_carve(K0, P1, K1, alias, OUT);
   const TailLds t = tail_lds(c, lds);
+  const int row = a.p.slot ? a.p.slot[b] : b;  // the graph's rows of the batch (dr_pass.slot)
   STAMP(0);
 
   float fc1_row[8], fc1_col[8], fc1_bias;
@@ -1516,23 +1518,23 @@ __device__ __forceinline__ void tail_body(const LargeArgs& la, int b, float* lds
     const int XSB = s.x_bf16_stride;
     const uint16_t* zb = reinterpret_cast<const uint16_t*>(pl.z) + (int64_t)pl.z_row0[b] * XSB;
     if (INL)
-      ginet_tail(a, t, fc1_row, fc1_col, fc1_bias, b, N, K0, K1, F, OUT, y_g, drop_offset, [&](int i, int kk) {
+      ginet_tail(a, t, fc1_row, fc1_col, fc1_bias, row, N, K0, K1, F, OUT, y_g, drop_offset, [&](int i, int kk) {
         const int64_t o = (int64_t)i * XSB + kk;  // the 4-byte word holding the bf16 value
         const uint32_t w = load_sc1_u32(zb + (o & ~(int64_t)1));
         return __uint_as_float((o & 1) ? (w & 0xffff0000u) : (w << 16));
       });
     else
-      ginet_tail(a, t, fc1_row, fc1_col, fc1_bias, b, N, K0, K1, F, OUT, y_g, drop_offset,
+      ginet_tail(a, t, fc1_row, fc1_col, fc1_bias, row, N, K0, K1, F, OUT, y_g, drop_offset,
                  [&](int i, int kk) { return bf2f(zb[(int64_t)i * XSB + kk]); });
     return;
   }
   const float* z = pl.z + (int64_t)pl.z_row0[b] * r4(F);
   const int XS = r4(F);
   if (INL)
-    ginet_tail(a, t, fc1_row, fc1_col, fc1_bias, b, N, K0, K1, F, OUT, y_g, drop_offset,
+    ginet_tail(a, t, fc1_row, fc1_col, fc1_bias, row, N, K0, K1, F, OUT, y_g, drop_offset,
                [&](int i, int kk) { return __uint_as_float(load_sc1_u32(z + (int64_t)i * XS + kk)); });
   else
-    ginet_tail(a, t, fc1_row, fc1_col, fc1_bias, b, N, K0, K1, F, OUT, y_g, drop_offset,
+    ginet_tail(a, t, fc1_row, fc1_col, fc1_bias, row, N, K0, K1, F, OUT, y_g, drop_offset,
                [&](int i, int kk) { return z[(int64_t)i * XS + kk]; });
 }
 

@@ -166,6 +166,7 @@ class PassC(ctypes.Structure):
         ("fault", VP),
         ("spin_limit", ctypes.c_int32),
         ("pad0", ctypes.c_int32),
+        ("slot", VP),
     ]
 
 

@@ -45,6 +45,7 @@ class BatchHandle:
         self.vanilla_split = None  # Vanilla per-graph kernel: workgroups per graph (None: by batch size)
         self.vanilla_tile_rows = 16  # Vanilla pipeline edge kernels: rows per halo-staged tile (0: untiled gathers)
         self.fault = None  # device uint32 [2] (dr_pass.fault) of the autograd path's passes, made on first use
+        self.mixed_dispatch = False  # graphs that fit LDS on the per-graph kernel, the rest on the large path (two streams; measured slower at configs[4])
 
     def lds(self, key, fn):
         """Dynamic LDS bytes for the largest graph of the batch (cached per model kind)."""
@@ -406,6 +407,11 @@ def launch(spec: FusedSpec, h: BatchHandle, w, p):
         spec.large(h, w, p)  # the tile kernel holds the bf16 node GEMM, for every graph size
         return
     lds = lds_for(spec, h, p.out_dim)
+    if lds > LDS_MAX and spec.large is not None and not h.force_large and h.mixed_dispatch:
+        m = mixed_split(spec, h, p.out_dim)
+        if m is not None:
+            launch_mixed(spec, m, w, p)
+            return
     if lds <= LDS_MAX and not (h.force_large and spec.large is not None):
         fn = getattr(_lib.load(), spec.entry)
         _lib.check(fn(h.store.cstruct(), h.descs.data_ptr(), h.B, w, p, lds, _lib.stream_ptr(h.store.device)), spec.entry)
@@ -414,6 +420,58 @@ def launch(spec: FusedSpec, h: BatchHandle, w, p):
     else:
         msg = f"largest graph of the batch needs {lds} B of LDS (> 160 KiB) and {spec.entry} has no large-graph path"
         raise RuntimeError(msg)
+
+
+class MixedSplit:
+    """A batch whose graphs do not all fit one workgroup's LDS (BASELINE configs[4]:
+    residue / SRV / atom graphs together), run as two launches: the graphs that
+    fit on the model's per-graph kernel, the others on its large-graph path, on
+    two HIP streams so they overlap.  ``dr_pass.slot`` sends every graph's
+    outputs, loss term and partials to its row of the whole batch, so the
+    reduction, outputs and dropout units are those of one launch over it."""
+
+    def __init__(self, spec: FusedSpec, h: BatchHandle, out_dim):
+        st = h.store
+        f, alias = st.n_feat, int(st.packed.transpose_aliased)
+        idx = h.gids_host.astype(np.int64)
+        sizes = [a[idx] for a in st._sizes]  # noqa: SLF001
+        fits = np.array([spec.lds(*(int(a[i]) for a in sizes), f, alias, out_dim) <= LDS_MAX for i in range(h.B)])
+        self.valid = bool(fits.any() and not fits.all())
+        if not self.valid:
+            return
+        dev = st.device
+        self.hs, self.hl = BatchHandle(st, h.gids_host[fits]), BatchHandle(st, h.gids_host[~fits])
+        for sub in (self.hs, self.hl):
+            sub.large_tile, sub.large_halos, sub.large_atomic_max = h.large_tile, h.large_halos, h.large_atomic_max
+        self.slot_s = torch.from_numpy(np.nonzero(fits)[0].astype(np.int32)).to(dev)
+        self.slot_l = torch.from_numpy(np.nonzero(~fits)[0].astype(np.int32)).to(dev)
+        self.side = torch.cuda.Stream(device=dev)
+        self.out_dim = out_dim
+
+
+def mixed_split(spec: FusedSpec, h: BatchHandle, out_dim):
+    key = ("mixed", spec.entry, out_dim)
+    m = h._lds.get(key)  # noqa: SLF001
+    if m is None:
+        m = MixedSplit(spec, h, out_dim)
+        h._lds[key] = m  # noqa: SLF001
+    return m if m.valid else None
+
+
+def launch_mixed(spec: FusedSpec, m: MixedSplit, w, p):
+    ps, pl = _lib.PassC.from_buffer_copy(p), _lib.PassC.from_buffer_copy(p)
+    ps.slot, pl.slot = m.slot_s.data_ptr(), m.slot_l.data_ptr()
+    dev = m.hs.store.device
+    cur = torch.cuda.current_stream(dev)
+    fork, join = torch.cuda.Event(), torch.cuda.Event()
+    fork.record(cur)
+    m.side.wait_event(fork)
+    with torch.cuda.stream(m.side):  # the large graphs (tile kernel + tail)
+        spec.large(m.hl, w, pl)
+        join.record(m.side)
+    fn = getattr(_lib.load(), spec.entry)  # the graphs that fit, on the per-graph kernel
+    _lib.check(fn(m.hs.store.cstruct(), m.hs.descs.data_ptr(), m.hs.B, w, ps, lds_for(spec, m.hs, p.out_dim), _lib.stream_ptr(dev)), spec.entry)
+    cur.wait_event(join)
 
 
 def step_fits(spec: FusedSpec, h: BatchHandle, compute_dtype, out_dim) -> bool:

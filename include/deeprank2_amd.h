@@ -190,6 +190,12 @@ typedef struct dr_pass {
                            is withheld and its loss reads NaN.                            */
   int32_t spin_limit;   /* polls before a hand-off wait gives up (<= 0: 1 << 22)        */
   int32_t pad0;
+  const int32_t* slot;  /* optional device [B] (GINet / FoutNet / SGAT passes): launch position b
+                           writes row slot[b] of out, loss_per_graph, slab, head and reads row
+                           slot[b] of dout / mask, and draws dropout unit slot[b] -- a batch run
+                           as several launches (graphs that fit one workgroup's LDS on the
+                           per-graph kernel, the others on the large-graph path) fills the rows
+                           one launch over the whole batch would                          */
 } dr_pass;
 
 /* One workgroup per graph: conv1 -> depth-0 community pooling -> conv2 ->

@@ -2,12 +2,12 @@
 E~3k), SRV-like graphs (N~30, E~200, like variants.hdf5) and atom-level graphs
 (N~3k, E~50k) — SURVEY §8(d) item 5 — through each model's dispatch:
 
-* GINet: the batch's atom graphs exceed one workgroup's LDS, so the whole
-  batch runs the split tile+tail path (dr_ginet_large_pass); residue and SRV
-  graphs run the single-workgroup kernel when the batch holds no atom graph.
-  Forward, every gradient and one Adam step vs the CPU oracle
-  (oracle/gnn_ref.py), and the per-graph results of the two dispatches agree
-  bit for bit for the graphs both can run.
+* GINet / FoutNet / SGAT: the batch's residue and SRV graphs run the
+  single-workgroup kernel and its atom graphs (beyond one workgroup's LDS)
+  the split tile+tail path, on two streams, every graph's results in its
+  batch row (dr_pass.slot).  Forward, every gradient and one Adam step vs the
+  CPU oracle (oracle/gnn_ref.py); per-graph rows bit-identical to the whole
+  batch on the split path and to each part alone.
 * VanillaNetwork (the fused gather -> edge MLP -> scatter of
   vanilla_gnn.py:26-38): the mixed batch runs the batch-wide pipeline
   (dr_vanilla_graph_pass), its residue/SRV part the per-graph fused kernel;
@@ -114,33 +114,61 @@ def test_ginet_mixed_batch_train_step_vs_oracle():
     _check_step(ginet_amd.PARAM_NAMES, step, model, model_o, out, loss, out_o, loss_o)
 
 
-def test_ginet_mixed_dispatch_bit_identical_for_small_graphs():
-    """The residue+SRV graphs give the same per-graph outputs, slab rows and
-    head vectors on the single-workgroup kernel (batch without atom graphs)
-    and inside the mixed batch on the split path."""
+@pytest.mark.parametrize("name", ["ginet", "foutnet", "sgat"])
+def test_mixed_dispatch_rows_bit_identical(name):
+    """A mixed batch runs its residue / SRV graphs on the per-graph kernel and
+    its atom graphs on the large-graph path, on two streams, each writing its
+    batch rows (dr_pass.slot): outputs, loss terms, slab rows and head vectors
+    are bit-identical to the whole batch on the large path (dispatch off; the
+    large path equals the per-graph kernel bit for bit), to the residue / SRV
+    graphs alone and to the atom graphs alone; GINet with hash dropout too
+    (units follow the batch row)."""
+    from deeprank2_amd.fused import Dropout, mixed_split
+    from deeprank2_amd.neuralnets.gnn import sgat as sgat_amd
+
     fam_datas = _mixed({"residue": 4, "srv": 4, "atom": 2}, seed=43)
     datas = [d for _, d in fam_datas]
+    if name == "sgat":
+        for d in datas:
+            d.edge_attr = d.edge_attr[:, :1].contiguous()
     small = [i for i, (f, _) in enumerate(fam_datas) if f != "atom"]
+    atoms = [i for i, (f, _) in enumerate(fam_datas) if f == "atom"]
     store = _store(datas)
     torch.manual_seed(13)
-    params = ginet_amd.GINet(30, 2, 3).to(DEV).ordered_params()
+    mod = {"ginet": ginet_amd, "foutnet": fout_amd, "sgat": sgat_amd}[name]
+    model = {"ginet": lambda: ginet_amd.GINet(30, 2, 3), "foutnet": lambda: fout_amd.FoutNet(30, 2), "sgat": lambda: sgat_amd.SGAT(30, 2, 1)}[name]()
+    params = model.to(DEV).ordered_params()
+    ss, hs = (ginet_amd.slab_stride, ginet_amd.head_stride) if name == "ginet" else (fout_amd.slab_stride, fout_amd.head_stride)
     store.set_targets(np.arange(len(datas)) % 2)
 
-    def run(gids):
+    def run(gids, mixed=True, dropout=None):
         h = BatchHandle(store, np.asarray(gids))
+        h.mixed_dispatch = mixed
         b = len(gids)
         out = torch.empty(b, 2, device=DEV)
-        slab = torch.empty(b * ginet_amd.slab_stride(30), device=DEV)
-        head = torch.zeros(b * ginet_amd.head_stride(2), device=DEV)
-        ginet_amd.graph_pass(h, params, 2, 3, loss_kind=_lib.DR_LOSS_CE, loss_scale=0.1, out=out, slab=slab, head=head)
+        lpg = torch.empty(b, device=DEV)
+        slab = torch.empty(b * ss(30), device=DEV)
+        head = torch.zeros(b * hs(2), device=DEV)
+        mod.graph_pass(h, params, 2, 3, loss_kind=_lib.DR_LOSS_CE, loss_scale=0.1, out=out, loss_per_graph=lpg, slab=slab, head=head, dropout=dropout)
         torch.cuda.synchronize()
-        return out.cpu(), slab.cpu().view(b, -1), head.cpu().view(b, -1)
+        return (out.cpu(), lpg.cpu(), slab.cpu().view(b, -1), head.cpu().view(b, -1)), h
 
-    o_mix, s_mix, h_mix = run(list(range(len(datas))))
-    o_small, s_small, h_small = run(small)
-    assert torch.equal(o_mix[small], o_small)
-    assert torch.equal(s_mix[small], s_small)
-    assert torch.equal(h_mix[small], h_small)
+    every = list(range(len(datas)))
+    on, h_on = run(every)
+    assert mixed_split(mod.SPEC, h_on, 2) is not None
+    off, _ = run(every, mixed=False)
+    for x, y in zip(on, off):
+        assert torch.equal(x, y)
+    for part in (small, atoms):
+        alone, _ = run(part)
+        for x, y in zip(on, alone):
+            assert torch.equal(x[part], y)
+    if name == "ginet":
+        drop = Dropout(0.4, seed=7, offset=3)
+        on_d, _ = run(every, dropout=drop)
+        off_d, _ = run(every, mixed=False, dropout=drop)
+        for x, y in zip(on_d, off_d):
+            assert torch.equal(x, y)
 
 
 def _vanilla_datas(counts, seed):
