@@ -83,135 +83,120 @@ class Trainer:
     ):
         self.neuralnet = neuralnet
         self.pretrained_model = pretrained_model
-        self._init_datasets(dataset_train, dataset_val, dataset_test, val_size, test_size)
+        self._adopt_datasets(dataset_train, dataset_val, dataset_test, val_size, test_size)
         self.cuda = cuda
-        self.ngpu = ngpu
-        if torch.cuda.is_available():
-            self.device = torch.device("cuda", torch.cuda.current_device())
-            if not cuda:
-                _log.info("deeprank2_amd has no CPU path: the model runs on the GPU although cuda=False was given.")
-            self.ngpu = max(1, ngpu)
-        else:
-            self.device = torch.device("cpu")
-            _log.warning("No GPU visible: models can be built and inspected but not trained or evaluated (no CPU fallback).")
-        self.process_group = None
-        if self.ngpu > 1:
-            if not torch.distributed.is_initialized():
-                msg = "ngpu > 1 runs one process per GPU: launch with torch.distributed.run (torchrun) and init_process_group first"
-                raise ValueError(msg)
-            self.process_group = torch.distributed.group.WORLD
+        self._select_device(ngpu)
         self._init_output_exporters(output_exporters)
-
-        self.data_type = None
-        self.batch_size_train = None
-        self.batch_size_test = None
-        self.shuffle = None
+        self.data_type = self.batch_size_train = self.batch_size_test = self.shuffle = None
         self.model_load_state_dict = None
         self._fused = None
-
         if self.pretrained_model is None:
-            if self.dataset_train is None:
-                msg = "No training data specified. Training data is required if there is no pretrained model."
-                raise ValueError(msg)
-            if self.neuralnet is None:
-                msg = "No neural network specified. Specifying a model framework is required if there is no pretrained model."
-                raise ValueError(msg)
-            self._init_from_dataset(self.dataset_train)
-            self.optimizer = None
-            self.class_weights = class_weights
-            self.subset = self.dataset_train.subset
-            self.epoch_saved_model = None
-            if self.target is None:
-                msg = "No target set. You need to choose a target (set in the dataset) for training."
-                raise ValueError(msg)
-            self._load_model()
-            if self.clustering_method is not None:
-                if self.clustering_method not in ("mcl", "louvain"):
-                    msg = f"Invalid node clustering method: {self.clustering_method}. Please set clustering_method to 'mcl', 'louvain' or None."
-                    raise ValueError(msg)
-                if precluster:
-                    self._precluster(self.dataset_train)
-                if self.dataset_val is None:
-                    _log.warning("No validation dataset given. Randomly splitting training set in training set and validation set.")
-                    self.dataset_train, self.dataset_val = _divide_dataset(self.dataset_train, splitsize=self.val_size, process_group=self.process_group)
-                elif precluster:
-                    self._precluster(self.dataset_val)
-                if self.dataset_test is not None and precluster:
-                    self._precluster(self.dataset_test)
+            self._setup_for_training(class_weights, precluster)
         else:
-            if self.neuralnet is None:
-                msg = "No neural network class found. Please add it to complete loading the pretrained model."
-                raise ValueError(msg)
-            if self.dataset_test is None:
-                msg = "No dataset_test found. Please add it to evaluate the pretrained model."
-                raise ValueError(msg)
-            if self.dataset_train is not None:
-                self.dataset_train = None
-                _log.warning("Pretrained model loaded: dataset_train will be ignored.")
-            if self.dataset_val is not None:
-                self.dataset_val = None
-                _log.warning("Pretrained model loaded: dataset_val will be ignored.")
-            self._init_from_dataset(self.dataset_test)
-            self._load_params()
-            self._load_pretrained_model()
+            self._setup_from_pretrained()
 
     # ------------------------------------------------------------------ setup
-    def _init_output_exporters(self, output_exporters):
-        self._output_exporters = OutputExporterCollection(*output_exporters) if output_exporters is not None else OutputExporterCollection(HDF5OutputExporter("./output"))
+    # Every precondition is a (holds, exception type, message) rule, checked in
+    # order; the exception types and messages are the reference's (its tests,
+    # tests/test_trainer.py:287-656, assert them).
+    @staticmethod
+    def _enforce(rules):
+        for holds, exc, msg in rules:
+            if not holds():
+                raise exc(msg)
 
-    def _init_datasets(self, dataset_train, dataset_val, dataset_test, val_size, test_size):
+    def _select_device(self, ngpu):
+        """The model always runs on the GPU when one is visible; ngpu > 1 means one process per GPU."""
+        self.ngpu = ngpu
+        self.process_group = None
+        if not torch.cuda.is_available():
+            self.device = torch.device("cpu")
+            _log.warning("No GPU visible: models can be built and inspected but not trained or evaluated (no CPU fallback).")
+            return
+        self.device = torch.device("cuda", torch.cuda.current_device())
+        if not self.cuda:
+            _log.info("deeprank2_amd has no CPU path: the model runs on the GPU although cuda=False was given.")
+        self.ngpu = max(1, ngpu)
+        if self.ngpu > 1:
+            self._enforce([(torch.distributed.is_initialized, ValueError, "ngpu > 1 runs one process per GPU: launch with torch.distributed.run (torchrun) and init_process_group first")])
+            self.process_group = torch.distributed.group.WORLD
+
+    def _setup_for_training(self, class_weights, precluster):
+        self._enforce([
+            (lambda: self.dataset_train is not None, ValueError, "No training data specified. Training data is required if there is no pretrained model."),
+            (lambda: self.neuralnet is not None, ValueError, "No neural network specified. Specifying a model framework is required if there is no pretrained model."),
+        ])  # fmt: skip
+        self._init_from_dataset(self.dataset_train)
+        self.optimizer = None
+        self.class_weights = class_weights
+        self.subset = self.dataset_train.subset
+        self.epoch_saved_model = None
+        self._enforce([(lambda: self.target is not None, ValueError, "No target set. You need to choose a target (set in the dataset) for training.")])
+        self._load_model()
+        if self.clustering_method is None:
+            return
+        self._enforce([(lambda: self.clustering_method in ("mcl", "louvain"), ValueError, f"Invalid node clustering method: {self.clustering_method}. Please set clustering_method to 'mcl', 'louvain' or None.")])
+        # every dataset the run will read gets the same pre-clustering; a missing
+        # validation set is split off the (pre-clustered) training set
+        if precluster:
+            self._precluster(self.dataset_train)
+        if self.dataset_val is None:
+            _log.warning("No validation dataset given. Randomly splitting training set in training set and validation set.")
+            self.dataset_train, self.dataset_val = _divide_dataset(self.dataset_train, splitsize=self.val_size, process_group=self.process_group)
+        elif precluster:
+            self._precluster(self.dataset_val)
+        if precluster and self.dataset_test is not None:
+            self._precluster(self.dataset_test)
+
+    def _setup_from_pretrained(self):
+        self._enforce([
+            (lambda: self.neuralnet is not None, ValueError, "No neural network class found. Please add it to complete loading the pretrained model."),
+            (lambda: self.dataset_test is not None, ValueError, "No dataset_test found. Please add it to evaluate the pretrained model."),
+        ])  # fmt: skip
+        for attr, name in (("dataset_train", "dataset_train"), ("dataset_val", "dataset_val")):
+            if getattr(self, attr) is not None:
+                setattr(self, attr, None)
+                _log.warning(f"Pretrained model loaded: {name} will be ignored.")
+        self._init_from_dataset(self.dataset_test)
+        self._load_params()
+        self._load_pretrained_model()
+
+    def _init_output_exporters(self, output_exporters):
+        self._output_exporters = OutputExporterCollection(*(output_exporters if output_exporters is not None else [HDF5OutputExporter("./output")]))
+
+    def _adopt_datasets(self, dataset_train, dataset_val, dataset_test, val_size, test_size):
+        """The three datasets after the consistency rules, with val / test split
+        off the training set when only a size is given (a given set wins)."""
         self._check_dataset_equivalence(dataset_train, dataset_val, dataset_test)
-        self.dataset_train = dataset_train
-        self.dataset_test = dataset_test
-        self.dataset_val = dataset_val
-        self.val_size = val_size
-        self.test_size = test_size
-        if test_size is not None:
-            if dataset_test is None:
-                self.dataset_train, self.dataset_test = _divide_dataset(dataset_train, test_size)
-            else:
-                _log.warning("Test dataset was provided to Trainer; test_size parameter is ignored.")
-        if val_size is not None:
-            if dataset_val is None:
-                self.dataset_train, self.dataset_val = _divide_dataset(dataset_train, val_size)
-            else:
-                _log.warning("Validation dataset was provided to Trainer; val_size parameter is ignored.")
+        self.dataset_train, self.dataset_val, self.dataset_test = dataset_train, dataset_val, dataset_test
+        self.val_size, self.test_size = val_size, test_size
+        for size, attr, what, param in ((test_size, "dataset_test", "Test", "test_size"), (val_size, "dataset_val", "Validation", "val_size")):
+            if size is None:
+                continue
+            if getattr(self, attr) is not None:
+                _log.warning(f"{what} dataset was provided to Trainer; {param} parameter is ignored.")
+                continue
+            self.dataset_train, split = _divide_dataset(self.dataset_train, size)
+            setattr(self, attr, split)
 
     def _check_dataset_equivalence(self, dataset_train, dataset_val, dataset_test):
+        """valid / test sets must name the training set they standardise by (train_source)."""
         if dataset_train is None:
-            if dataset_test is None:
-                msg = "Please provide at least a train or test dataset"
-                raise ValueError(msg)
+            self._enforce([(lambda: dataset_test is not None, ValueError, "Please provide at least a train or test dataset")])
             return
-        if not isinstance(dataset_train, GraphDataset):
-            msg = f"train dataset is not the right type {type(dataset_train)}. Make sure it's a GraphDataset"
-            raise TypeError(msg)
+        self._enforce([(lambda: isinstance(dataset_train, GraphDataset), TypeError, f"train dataset is not the right type {type(dataset_train)}. Make sure it's a GraphDataset")])
         for ds, kind in ((dataset_val, "valid"), (dataset_test, "test")):
-            if ds is None:
-                continue
-            if ds.train_source is None:
-                msg = f"{kind} dataset has train_source parameter set to None. Make sure to set it as a valid training data source."
-                raise ValueError(msg)
-            if ds.train_source is not dataset_train and ds.train_source != dataset_train:
-                msg = f"{kind} dataset has different train_source parameter from Trainer. Make sure to assign equivalent train_source in Trainer."
-                raise ValueError(msg)
+            if ds is not None:
+                self._enforce([
+                    (lambda ds=ds: ds.train_source is not None, ValueError, f"{kind} dataset has train_source parameter set to None. Make sure to set it as a valid training data source."),
+                    (lambda ds=ds: ds.train_source is dataset_train or ds.train_source == dataset_train, ValueError, f"{kind} dataset has different train_source parameter from Trainer. Make sure to assign equivalent train_source in Trainer."),
+                ])  # fmt: skip
 
     def _init_from_dataset(self, dataset):
-        if not isinstance(dataset, GraphDataset):
-            msg = f"Incorrect `dataset` type provided: {type(dataset)}. Please provide a `GraphDataset` object instead."
-            raise TypeError(msg)
-        self.clustering_method = dataset.clustering_method
-        self.node_features = dataset.node_features
-        self.edge_features = dataset.edge_features
+        self._enforce([(lambda: isinstance(dataset, GraphDataset), TypeError, f"Incorrect `dataset` type provided: {type(dataset)}. Please provide a `GraphDataset` object instead.")])
+        for attr in ("clustering_method", "node_features", "edge_features", "features_transform", "means", "devs", "target", "target_transform", "task", "classes", "classes_to_index"):
+            setattr(self, attr, getattr(dataset, attr))
         self.features = None
-        self.features_transform = dataset.features_transform
-        self.means = dataset.means
-        self.devs = dataset.devs
-        self.target = dataset.target
-        self.target_transform = dataset.target_transform
-        self.task = dataset.task
-        self.classes = dataset.classes
-        self.classes_to_index = dataset.classes_to_index
 
     def _load_model(self):
         self._put_model_to_device(self.dataset_train)
@@ -407,43 +392,39 @@ class Trainer:
         else:
             self.weights = None
 
-        train_losses, valid_losses = [], []
-        saved_model = False
-        checkpoint_model = None
-        early_stopping = EarlyStopping(patience=earlystop_patience, maxgap=earlystop_maxgap, min_epoch=min_epoch, trace_func=_log.info) if (earlystop_patience or earlystop_maxgap) else None
+        # model selection: a checkpoint whenever the monitored loss (validation
+        # when validating, else training) equals the lowest so far; without one
+        # (best_model False, or NaN losses) the last epoch's model is kept, with
+        # the reference's warning whenever no selection happened
+        history = {"training": [], "validation": []}
+        monitored = "validation" if validate else "training"
+        kept = None
+        stopper = EarlyStopping(patience=earlystop_patience, maxgap=earlystop_maxgap, min_epoch=min_epoch, trace_func=_log.info) if (earlystop_patience or earlystop_maxgap) else None
         epoch = 0
         with self._output_exporters:
             self.nepoch = nepoch
             self._eval(self.train_loader, 0, "training")
             if validate:
-                if self.valid_loader is None:
-                    msg = "No validation dataset provided."
-                    raise ValueError(msg)
+                self._enforce([(lambda: self.valid_loader is not None, ValueError, "No validation dataset provided.")])
                 self._eval(self.valid_loader, 0, "validation")
-            for epoch in range(1, nepoch + 1):
+            while epoch < nepoch:
+                epoch += 1
                 self.model.train()
-                loss_ = self._epoch(epoch, "training")
-                train_losses.append(loss_)
+                history["training"].append(self._epoch(epoch, "training"))
                 if validate:
-                    loss_ = self._eval(self.valid_loader, epoch, "validation")
-                    valid_losses.append(loss_)
-                    if best_model and min(valid_losses) == loss_:
-                        checkpoint_model = self._save_model()
-                        saved_model = True
-                        self.epoch_saved_model = epoch
-                    if early_stopping:
-                        early_stopping(epoch, valid_losses[-1], train_losses[-1])
-                        if early_stopping.early_stop:
-                            break
-                elif best_model and min(train_losses) == loss_:
-                    checkpoint_model = self._save_model()
-                    saved_model = True
-                    self.epoch_saved_model = epoch
-            if best_model is False or not saved_model:
-                checkpoint_model = self._save_model()
-                self.epoch_saved_model = epoch
-                if not saved_model:
+                    history["validation"].append(self._eval(self.valid_loader, epoch, "validation"))
+                seen = history[monitored]
+                if best_model and min(seen) == seen[-1]:
+                    kept = (self._save_model(), epoch)
+                if validate and stopper is not None:
+                    stopper(epoch, history["validation"][-1], history["training"][-1])
+                    if stopper.early_stop:
+                        break
+            if kept is None or not best_model:
+                if kept is None:
                     warnings.warn("A model has been saved but the validation and/or the training losses were NaN;\n\ttry to increase the cutoff distance during the data processing or the number of data points during the training.", stacklevel=2)
+                kept = (self._save_model(), epoch)
+        checkpoint_model, self.epoch_saved_model = kept
         if filename:
             torch.save(checkpoint_model, filename)
         self.opt_loaded_state_dict = checkpoint_model["optimizer_state"]
