@@ -329,7 +329,7 @@ __global__ void __launch_bounds__(RB) vb_edge_bwd8(VA a, int l) {
 // kernels.  LDS (floats): halo rows [halo_max][32] | edge attributes
 // [edges][FeS] | words [edges] | column ids (uint16) [edges] (+ transposed).
 struct TileCarve {
-  int rows, ea, words, wt, lc, ltc, tp, total;
+  int rows, ea, words, wt, lc, ltc, total;
 };
 __host__ __device__ inline TileCarve tile_carve(int hmax, int emax, int tmax, int FeS, bool bwd) {
   TileCarve c;
@@ -342,8 +342,6 @@ __host__ __device__ inline TileCarve tile_carve(int hmax, int emax, int tmax, in
   o += bwd ? r4(emax) : 0;
   c.wt = o;  // backward: the tile's transposed-order words
   o += bwd ? r4(tmax) : 0;
-  c.tp = o;  // forward: each CSR edge's transposed slot
-  o += bwd ? 0 : r4(emax);
   c.lc = o;
   o += bwd ? 0 : r4((emax + 1) / 2);
   c.ltc = o;
@@ -378,24 +376,18 @@ __global__ void __launch_bounds__(RB) vb_edge_fwd_tile(VA a, int l) {
   float* sB = lds + tc.rows;
   float* sE = lds + tc.ea;
   uint16_t* sC = reinterpret_cast<uint16_t*>(lds + tc.lc);
-  int* sTp = reinterpret_cast<int*>(lds + tc.tp);
   stage_halo(sB, L.bm + g0 * 32, a.ws.halo_ids + h0, H);
   {
     const float* ea = a.s.ea + (d.col0 + e0) * FeS;
     for (int p = tid; p < ne * FeS; p += RB) sE[p] = ea[p];
     const uint16_t* lc = a.ws.lcol + a.ws.lcol_off[t];
-    const int* tp = a.ws.tpos + a.ws.lcol_off[t];
-    for (int p = tid; p < ne; p += RB) {
-      sC[p] = lc[p];
-      sTp[p] = tp[p];
-    }
+    for (int p = tid; p < ne; p += RB) sC[p] = lc[p];
   }
   float wcr[FA];
 #pragma unroll
   for (int f = 0; f < FE; ++f) wcr[f] = L.we[c * KE + 2 * F + f];
   const float bc = L.be[c];
   uint32_t* wr = a.ws.relu_words + (int64_t)(l - 1) * a.ws.edge0[a.B] + a.ws.edge0[b] + e0;
-  uint32_t* wt = a.ws.relu_words_t + (int64_t)(l - 1) * a.ws.edge0[a.B] + a.ws.edge0[b];
   __syncthreads();
   for (int64_t r = rt0 + (tid >> 5); r < rt1; r += RB / 32) {
     const int i = (int)(r - g0);
@@ -415,6 +407,7 @@ __global__ void __launch_bounds__(RB) vb_edge_fwd_tile(VA a, int l) {
         for (int f = 0; f < FE; ++f) ev[u][f] = sE[(e + u) * FeS + f];
 #pragma unroll
       for (int u = 0; u < U; ++u) q[u] = sB[j[u] * 32 + c];
+      uint32_t mine = 0u;  // lane c < U keeps word c: one contiguous store per group
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         float ec = 0.f;
@@ -423,10 +416,9 @@ __global__ void __launch_bounds__(RB) vb_edge_fwd_tile(VA a, int l) {
         const float pre = ac + q[u] + ec + bc;
         acc += relu_keepnan(pre);
         const uint64_t m = __ballot(active(pre));
-        const uint32_t word = (uint32_t)(m >> hs);
-        if (c == 0) wr[e + u] = word;
-        if (c == 1) wt[sTp[e + u]] = word;  // the backward's transposed pass reads this copy
+        if (c == u) mine = (uint32_t)(m >> hs);
       }
+      if (c < U) wr[e + c] = mine;
     };
     for (; e + 8 <= ee; e += 8) group(std::integral_constant<int, 8>());
     for (; e + 4 <= ee; e += 4) group(std::integral_constant<int, 4>());
@@ -459,16 +451,16 @@ __global__ void __launch_bounds__(RB) vb_edge_bwd_tile(VA a, int l) {
   uint32_t* sWt = reinterpret_cast<uint32_t*>(lds + tc.wt);
   uint16_t* sT = reinterpret_cast<uint16_t*>(lds + tc.ltc);
   const uint32_t* words = a.ws.relu_words + (int64_t)(l - 1) * a.ws.edge0[a.B] + a.ws.edge0[b];
-  const uint32_t* words_t = a.ws.relu_words_t + (int64_t)(l - 1) * a.ws.edge0[a.B] + a.ws.edge0[b];
   stage_halo(sD, DS + g0 * 32, a.ws.halo_ids + h0, H);
   {
     const float* ea = a.s.ea + (d.col0 + e0) * FeS;
     for (int p = tid; p < ne * FeS; p += RB) sE[p] = ea[p];
     for (int p = tid; p < ne; p += RB) sW[p] = words[e0 + p];
     const uint16_t* lt = a.ws.ltcol + a.ws.ltcol_off[t];
+    const int* teid = a.s.t_eid + d.col0;  // transposed slot -> CSR slot
     for (int p = tid; p < nq; p += RB) {
       sT[p] = lt[p];
-      sWt[p] = words_t[q0 + p];
+      sWt[p] = words[teid[q0 + p]];  // gathered while staging: no dependent loads in the row loop
     }
   }
   __syncthreads();
@@ -532,8 +524,9 @@ __global__ void __launch_bounds__(RB) vb_edge_bwd_tile(VA a, int l) {
 }
 
 // per graph: scatter_mean -> graph MLP -> loss -> head backward (one workgroup)
-__global__ void __launch_bounds__(256) vb_head(VA a) {
-  __shared__ float sG[64], sH[128], sDh[128], sDout[16], sRed[256];
+constexpr int HT = 1024;  // vb_head threads: 32 row chunks per column for the mean over ~3k-node graphs
+__global__ void __launch_bounds__(HT) vb_head(VA a) {
+  __shared__ float sG[64], sH[128], sDh[128], sDout[16], sRed[HT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.x;
   const int F = a.F, XS = a.XS, OUT = a.p.out_dim;
@@ -543,7 +536,7 @@ __global__ void __launch_bounds__(256) vb_head(VA a) {
   const float y_g = a.s.y[a.descs[b].gid];
   if (a.p.step_counter && b == 0 && tid == 0) a.p.step_counter[1] = a.p.step_counter[0];
   {  // column sums in row chunks, combined in chunk order
-    const int CH = 256 / XS, n = tid % XS, ch = tid / XS;
+    const int CH = HT / XS, n = tid % XS, ch = tid / XS;
     float acc = 0.f;
     if (n < F && ch < CH) {
       const int i0 = (N * ch) / CH, i1 = (N * (ch + 1)) / CH;
@@ -572,19 +565,20 @@ __global__ void __launch_bounds__(256) vb_head(VA a) {
     sH[tid] = relu_keepnan(acc + a.w.g1b[tid]);
   }
   __syncthreads();
-  for (int q = wave; q < OUT; q += 4) {
+  for (int q = wave; q < OUT; q += HT / 64) {
     float v = fmaf(sH[lane], a.w.g2w[q * 128 + lane], sH[lane + 64] * a.w.g2w[q * 128 + lane + 64]);
     v = dr_wave_sum(v);
     if (lane == 0) sDout[q] = v + a.w.g2b[q];
   }
   __syncthreads();
-  if ((a.p.flags & DR_PASS_FORWARD) && tid < OUT) a.p.out[(int64_t)b * OUT + tid] = sDout[tid];
+  const int row = a.p.slot ? a.p.slot[b] : b;  // the graph's rows of the batch (dr_pass.slot)
+  if ((a.p.flags & DR_PASS_FORWARD) && tid < OUT) a.p.out[(int64_t)row * OUT + tid] = sDout[tid];
   if (!(a.p.flags & DR_PASS_BACKWARD)) return;
   __syncthreads();
   if (tid == 0) {  // loss gradient (trainer.py:688-689)
     if (a.p.loss_kind == DR_LOSS_MSE) {
       const float dl = sDout[0] - y_g;
-      if (a.p.loss_per_graph) a.p.loss_per_graph[b] = dl * dl;
+      if (a.p.loss_per_graph) a.p.loss_per_graph[row] = dl * dl;
       sDout[0] = 2.f * dl * a.p.loss_scale;
     } else if (a.p.loss_kind == DR_LOSS_CE) {
       const int yi = (int)y_g;
@@ -594,10 +588,10 @@ __global__ void __launch_bounds__(256) vb_head(VA a) {
       for (int q = 0; q < OUT; ++q) se += expf(sDout[q] - mx);
       const float lse = mx + logf(se);
       const float wy = a.p.class_w ? a.p.class_w[yi] : 1.f;
-      if (a.p.loss_per_graph) a.p.loss_per_graph[b] = wy * (lse - sDout[yi]);
+      if (a.p.loss_per_graph) a.p.loss_per_graph[row] = wy * (lse - sDout[yi]);
       for (int q = 0; q < OUT; ++q) sDout[q] = wy * (expf(sDout[q] - lse) - (q == yi ? 1.f : 0.f)) * a.p.loss_scale;
     } else {
-      for (int q = 0; q < OUT; ++q) sDout[q] = a.p.dout[(int64_t)b * OUT + q];
+      for (int q = 0; q < OUT; ++q) sDout[q] = a.p.dout[(int64_t)row * OUT + q];
     }
   }
   __syncthreads();
@@ -607,7 +601,7 @@ __global__ void __launch_bounds__(256) vb_head(VA a) {
     sDh[tid] = relu_bwd(sH[tid], acc);
   }
   __syncthreads();
-  float* hg = a.p.head + (int64_t)b * DR_VANILLA_HEAD_STRIDE(F, OUT);
+  float* hg = a.p.head + (int64_t)row * DR_VANILLA_HEAD_STRIDE(F, OUT);
   const int HD = XS + 256 + r4(OUT);  // d mean, consumed by vb_du2
   if (tid < F) {
     float acc = 0.f;
@@ -636,7 +630,7 @@ __global__ void __launch_bounds__(RB) vb_du(VA a, int l) {
     const int64_t r = p / XS;
     const int n = (int)(p - r * XS);
     float g = 0.f;
-    if (n < F) g = (l == 2) ? a.p.head[(int64_t)a.ws.row_slot[r] * HS + HD + n] : dx1[p];
+    if (n < F) g = (l == 2) ? a.p.head[(int64_t)(a.p.slot ? a.p.slot[a.ws.row_slot[r]] : a.ws.row_slot[r]) * HS + HD + n] : dx1[p];
     du[p] = n < F ? relu_bwd(xo[p], g) : 0.f;
   }
 }
@@ -789,48 +783,52 @@ __global__ void __launch_bounds__(RB) vb_edge_bwd(VA a, int l) {
 
 // ---- node GEMMs on MFMA -----------------------------------------------------
 // out(r, n) = init(r, n) + sum_{k < K} A(r, k) W(k, n) for every batch row r,
-// n < NO, on v_mfma_f32_16x16x4_f32 (k in order: the same fmaf chain as a
-// scalar loop).  A workgroup (4 waves) stages W [KP][NOP] in LDS once, then
-// takes 64-row tiles: the A tile [64][KP] is loaded coalesced into LDS
-// (stride KP + 1: the 16 rows of an operand read hit distinct banks), each
-// wave runs 16 rows x all NO columns.  Modes (vanilla_gnn.py:29-37 and their
-// gradients):
-//   GM_HALVES: [A | B] = Xin [Wa; Wb]^T            (K = F,      NO = 64)
-//   GM_NODE:   Xout = relu([Xin | S] Wn^T + bn)    (K = F + 32, NO = F)
-//   GM_DXS:    [dX1 | DS] = DU Wn                  (K = F,      NO = F + 32)
-//   GM_DX1:    dX1 += [D | D'] [Wa2; Wb2]          (K = 64,     NO = F)
+// n < NO, on v_mfma_f32_16x16x4_f32 (k in order).  A workgroup (4 waves)
+// stages W [KP][NOP] in LDS once, then takes 64-row tiles: the A tile
+// [64][KP] comes in as 16-byte loads (one row base per tile row, looked up
+// once) into LDS at stride KP + 4 (the 16 rows of an operand read hit
+// distinct banks), each wave runs 16 rows x all NO columns.  A's k axis is
+// 16-byte aligned pieces: a feature row takes XS = r4(F) columns (its pad
+// columns read as 0, W rows there are 0).  Modes (vanilla_gnn.py:29-37 and
+// their gradients):
+//   GM_HALVES: [A | B] = Xin [Wa; Wb]^T            (K = XS,      NO = 64)
+//   GM_NODE:   Xout = relu([Xin | S] Wn^T + bn)    (K = XS + 32, NO = F)
+//   GM_DXS:    [dX1 | DS] = DU Wn                  (K = XS,      NO = F + 32)
+//   GM_DX1:    dX1 += [D | D'] [Wa2; Wb2]          (K = 64,      NO = F)
 enum GemmMode { GM_HALVES = 0, GM_NODE = 1, GM_DXS = 2, GM_DX1 = 3 };
 constexpr int GT = 64;  // rows per tile
 
 __host__ __device__ inline void gemm_dims(int mode, int F, int& K, int& NO) {
-  K = mode == GM_NODE ? F + 32 : (mode == GM_DX1 ? 64 : F);
+  const int XS = r4(F);
+  K = mode == GM_NODE ? XS + 32 : (mode == GM_DX1 ? 64 : XS);
   NO = mode == GM_HALVES ? 64 : (mode == GM_DXS ? F + 32 : F);
 }
 __host__ __device__ inline int gemm_lds_floats(int mode, int F) {
   int K, NO;
   gemm_dims(mode, F, K, NO);
-  const int KP = r4(K), NOP = (NO + 15) & ~15;
-  return KP * NOP + GT * (KP + 1);
+  const int NOP = (NO + 15) & ~15;
+  return K * NOP + GT * (K + 4) + GT * 2;  // W | A tile | row bases (64-bit)
 }
 
 template <int MODE>
 __global__ void __launch_bounds__(RB) vb_gemm(VA a, int l) {
-  extern __shared__ float lds[];
+  extern __shared__ __attribute__((aligned(16))) float lds[];
   const Layer L = layer_of(a, l);
   const int F = a.F, KE = a.KE, KN = a.KN, XS = a.XS;
-  int K, NO;
-  gemm_dims(MODE, F, K, NO);
-  const int KP = r4(K), NOP = (NO + 15) & ~15, LA = KP + 1;
+  int KP, NO;
+  gemm_dims(MODE, F, KP, NO);
+  const int NOP = (NO + 15) & ~15, LA = KP + 4, CH = KP / 4;
   float* Ws = lds;              // [KP][NOP]
   float* As = lds + KP * NOP;   // [GT][LA]
+  const float** rowp = reinterpret_cast<const float**>(As + GT * LA);  // [GT] feature-row bases
   const float* wn = l == 2 ? a.w.wn2 : a.w.wn1;
   for (int p = threadIdx.x; p < KP * NOP; p += RB) {
     const int k = p / NOP, n = p - k * NOP;
     float v = 0.f;
-    if (k < K && n < NO) {
-      if (MODE == GM_HALVES) v = L.we[(n & 31) * KE + (n < 32 ? 0 : F) + k];
-      else if (MODE == GM_NODE) v = L.wn[n * KN + k];
-      else if (MODE == GM_DXS) v = wn[k * KN + n];
+    if (n < NO) {
+      if (MODE == GM_HALVES) v = k < F ? L.we[(n & 31) * KE + (n < 32 ? 0 : F) + k] : 0.f;
+      else if (MODE == GM_NODE) v = k < F ? L.wn[n * KN + k] : (k < XS ? 0.f : L.wn[n * KN + F + k - XS]);
+      else if (MODE == GM_DXS) v = k < F ? wn[k * KN + n] : 0.f;
       else v = a.w.we2[(k & 31) * KE + (k < 32 ? 0 : F) + n];
     }
     Ws[p] = v;
@@ -840,17 +838,35 @@ __global__ void __launch_bounds__(RB) vb_gemm(VA a, int l) {
   const int64_t R = a.ws.n_rows;
   for (int64_t t0 = (int64_t)blockIdx.x * GT; t0 < R; t0 += (int64_t)gridDim.x * GT) {
     __syncthreads();  // W staged / the previous tile's A reads done
-    for (int p = threadIdx.x; p < GT * KP; p += RB) {
-      const int i = p / KP, k = p - i * KP;
+    if ((MODE == GM_HALVES || MODE == GM_NODE) && threadIdx.x < GT) {
+      const int64_t r = t0 + threadIdx.x;
+      rowp[threadIdx.x] = r < R ? xin_row(a, L, r) : nullptr;
+    }
+    if (MODE == GM_HALVES || MODE == GM_NODE) __syncthreads();
+    for (int p = threadIdx.x; p < GT * CH; p += RB) {
+      const int i = p / CH, c4 = (p - i * CH) * 4;
       const int64_t r = t0 + i;
-      float v = 0.f;
-      if (r < R && k < K) {
-        if (MODE == GM_HALVES) v = xin_row(a, L, r)[k];
-        else if (MODE == GM_NODE) v = k < F ? xin_row(a, L, r)[k] : L.s[r * 32 + k - F];
-        else if (MODE == GM_DXS) v = ws[a.L.du + r * XS + k];
-        else v = k < 32 ? ws[a.L.d + r * 32 + k] : ws[a.L.dp + r * 32 + k - 32];
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r < R) {
+        if (MODE == GM_HALVES || MODE == GM_NODE) {
+          if (c4 < XS) {
+            v = *reinterpret_cast<const float4*>(rowp[i] + c4);
+            if (c4 + 4 > F) {  // the row's pad columns (scratch rows leave them unwritten)
+              v.y = c4 + 1 < F ? v.y : 0.f;
+              v.z = c4 + 2 < F ? v.z : 0.f;
+              v.w = c4 + 3 < F ? v.w : 0.f;
+              v.x = c4 < F ? v.x : 0.f;
+            }
+          } else {
+            v = *reinterpret_cast<const float4*>(L.s + r * 32 + c4 - XS);
+          }
+        } else if (MODE == GM_DXS) {
+          v = *reinterpret_cast<const float4*>(ws + a.L.du + r * XS + c4);
+        } else {
+          v = *reinterpret_cast<const float4*>(c4 < 32 ? ws + a.L.d + r * 32 + c4 : ws + a.L.dp + r * 32 + c4 - 32);
+        }
       }
-      As[i * LA + k] = v;
+      *reinterpret_cast<float4*>(As + i * LA + c4) = v;
     }
     __syncthreads();
     const int i0 = wave * 16;
@@ -898,7 +914,7 @@ constexpr int WR = DR_VANILLA_CHUNK;
 __host__ __device__ inline int layer_grad_size(int F, int Fe) { return 32 * (2 * F + Fe) + 32 + F * (F + 32) + F; }
 
 __global__ void __launch_bounds__(RB) vb_wgrad_mfma(VA a, int l) {
-  extern __shared__ float lds[];
+  extern __shared__ __attribute__((aligned(16))) float lds[];
   const int ch = blockIdx.x;
   const int b = a.ws.chunk_slot[ch];
   const int F = a.F, Fe = a.Fe, KE = a.KE, KN = a.KN, XS = a.XS, FeS = Fe > 0 ? Fe : 1;
@@ -915,18 +931,17 @@ __global__ void __launch_bounds__(RB) vb_wgrad_mfma(VA a, int l) {
   float* cDP = cD + WR * 32;
   float* cDU = cDP + WR * 32;
   float* cE = cDU + WR * XS;
-  for (int p = threadIdx.x; p < WR * XS; p += RB) {  // rows past the chunk: zeros
-    const bool in = p < nr * XS;
-    cX[p] = in ? X[p] : 0.f;
-    cDU[p] = in ? ws[a.L.du + g0 * XS + p] : 0.f;
-  }
-  for (int p = threadIdx.x; p < WR * 32; p += RB) {
-    const bool in = p < nr * 32;
-    cS[p] = in ? L.s[g0 * 32 + p] : 0.f;
-    cD[p] = in ? ws[a.L.d + g0 * 32 + p] : 0.f;
-    cDP[p] = in ? ws[a.L.dp + g0 * 32 + p] : 0.f;
-  }
-  for (int p = threadIdx.x; p < nr * 32 * FeS; p += RB) cE[p] = ws[a.L.eap + g0 * 32 * FeS + p];
+  // the chunk's rows (contiguous in every array) by 16-byte loads; rows past the chunk: zeros
+  auto stage4 = [&](float* dst, const float* src, int n4, int valid4) {
+    for (int p = threadIdx.x; p < n4; p += RB)
+      reinterpret_cast<float4*>(dst)[p] = p < valid4 ? reinterpret_cast<const float4*>(src)[p] : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  stage4(cX, X, WR * XS / 4, nr * XS / 4);
+  stage4(cDU, ws + a.L.du + g0 * XS, WR * XS / 4, nr * XS / 4);
+  stage4(cS, L.s + g0 * 32, WR * 8, nr * 8);
+  stage4(cD, ws + a.L.d + g0 * 32, WR * 8, nr * 8);
+  stage4(cDP, ws + a.L.dp + g0 * 32, WR * 8, nr * 8);
+  stage4(cE, ws + a.L.eap + g0 * 32 * FeS, nr * 8 * FeS, nr * 8 * FeS);
   __syncthreads();
   const int nwe = 32 * KE, nwn = F * KN, total = nwe + 32 + nwn + F;
   float* out = a.ws.part + (int64_t)ch * total;
@@ -988,7 +1003,7 @@ __global__ void __launch_bounds__(RB) vb_wgrad_combine(VA a, int l) {
     const int b = (int)(q / total), p = (int)(q - (int64_t)b * total);
     float v = 0.f;
     for (int ch = a.ws.chunk_first[b]; ch < a.ws.chunk_first[b + 1]; ++ch) v += a.ws.part[(int64_t)ch * total + p];
-    a.p.slab[(int64_t)b * DR_VANILLA_SLAB_STRIDE(a.F, a.Fe) + (l == 2 ? total : 0) + p] = v;
+    a.p.slab[(int64_t)(a.p.slot ? a.p.slot[b] : b) * DR_VANILLA_SLAB_STRIDE(a.F, a.Fe) + (l == 2 ? total : 0) + p] = v;
   }
 }
 
@@ -1071,7 +1086,7 @@ extern "C" int dr_vanilla_graph_pass(const dr_graph_store* store, const dr_graph
     return DR_E_ARG;
   if (scratch->tile_row0) {  // the tile plan: complete, and its LDS within one workgroup's 160 KiB
     if (!scratch->relu_words || !scratch->halo_off || !scratch->halo_ids || !scratch->lcol_off || !scratch->lcol ||
-        !scratch->ltcol_off || !scratch->ltcol || !scratch->tpos || !scratch->relu_words_t || scratch->n_tiles < 1 || scratch->halo_max < 1 ||
+        !scratch->ltcol_off || !scratch->ltcol || scratch->n_tiles < 1 || scratch->halo_max < 1 ||
         scratch->halo_max > 65535 || scratch->tile_edges_max < 0 || scratch->tile_tedges_max < 0)
       return DR_E_ARG;
     const int FeS = store->n_edge_feat > 0 ? store->n_edge_feat : 1;
@@ -1108,7 +1123,7 @@ extern "C" int dr_vanilla_graph_pass(const dr_graph_store* store, const dr_graph
       hipLaunchKernelGGL(vb_edge_fwd, dim3(rows_grid(R, RB / 32)), dim3(RB), 0, st, a, l);
     hipLaunchKernelGGL(vb_gemm<GM_NODE>, dim3(gg), dim3(RB), glds(GM_NODE), st, a, l);
   }
-  hipLaunchKernelGGL(vb_head, dim3(n_batch), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(vb_head, dim3(n_batch), dim3(HT), 0, st, a);
   if (pass->flags & DR_PASS_BACKWARD) {
     hipLaunchKernelGGL(vb_du, dim3(rows_grid(R * a.XS, RB)), dim3(RB), 0, st, a, 2);
     hipLaunchKernelGGL(vb_gemm<GM_DXS>, dim3(gg), dim3(RB), glds(GM_DXS), st, a, 2);

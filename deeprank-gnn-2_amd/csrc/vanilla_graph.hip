@@ -660,7 +660,8 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   const bool split = k > 1;
   const int spin_limit = a.p.spin_limit > 0 ? a.p.spin_limit : (1 << 22);
   const int LG = 32 * KE + 32 + F * KN + F;  // one layer's gradient entries in the slab
-  float* slab = p.slab ? p.slab + ((int64_t)b * k + rk) * DR_VANILLA_SLAB_STRIDE(F, Fe) : nullptr;
+  const int row = p.slot ? p.slot[b] : b;  // the graph's rows of the batch (dr_pass.slot)
+  float* slab = p.slab ? p.slab + ((int64_t)row * k + rk) * DR_VANILLA_SLAB_STRIDE(F, Fe) : nullptr;
   const bool bwd = (p.flags & DR_PASS_BACKWARD) != 0;
   const bool lead = rk == 0;  // writes the graph's outputs, loss and head vectors
 
@@ -818,12 +819,12 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
     if (lane == 0) sdout[q] = v + w.g2b[q];
   }
   __syncthreads();
-  if ((p.flags & DR_PASS_FORWARD) && lead && tid < OUT) p.out[(int64_t)b * OUT + tid] = sdout[tid];
+  if ((p.flags & DR_PASS_FORWARD) && lead && tid < OUT) p.out[(int64_t)row * OUT + tid] = sdout[tid];
   if (!bwd) return;
   if (tid == 0) {
     if (p.loss_kind == DR_LOSS_MSE) {
       const float dl = sdout[0] - y_g;
-      if (p.loss_per_graph && lead) p.loss_per_graph[b] = dl * dl;
+      if (p.loss_per_graph && lead) p.loss_per_graph[row] = dl * dl;
       sdout[0] = 2.f * dl * p.loss_scale;
     } else if (p.loss_kind == DR_LOSS_CE) {
       const int yi = (int)y_g;
@@ -833,10 +834,10 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
       for (int q = 0; q < OUT; ++q) se += expf(sdout[q] - mx);
       const float lse = mx + logf(se);
       const float wy = p.class_w ? p.class_w[yi] : 1.f;
-      if (p.loss_per_graph && lead) p.loss_per_graph[b] = wy * (lse - sdout[yi]);
+      if (p.loss_per_graph && lead) p.loss_per_graph[row] = wy * (lse - sdout[yi]);
       for (int q = 0; q < OUT; ++q) sdout[q] = wy * (expf(sdout[q] - lse) - (q == yi ? 1.f : 0.f)) * p.loss_scale;
     } else {
-      for (int q = 0; q < OUT; ++q) sdout[q] = p.dout[(int64_t)b * OUT + q];
+      for (int q = 0; q < OUT; ++q) sdout[q] = p.dout[(int64_t)row * OUT + q];
     }
   }
   __syncthreads();
@@ -861,7 +862,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   }
   __syncthreads();
   {
-    float* hg = p.head + (int64_t)b * DR_VANILLA_HEAD_STRIDE(F, OUT);
+    float* hg = p.head + (int64_t)row * DR_VANILLA_HEAD_STRIDE(F, OUT);
     const int XSH = r4(F), HD = XSH + 256 + r4(OUT);
     if (tid < 32) {
       float acc = 0.f;

@@ -64,7 +64,7 @@ class BatchHandle:
             row0 = np.concatenate([[0], np.cumsum(n)]).astype(np.int32)
             rows = int(row0[-1])
             slot = np.repeat(np.arange(self.B, dtype=np.int32), n)
-            chunks = (n + 31) // 32  # DR_VANILLA_CHUNK
+            chunks = (n + VANILLA_CHUNK - 1) // VANILLA_CHUNK
             chunk_first = np.concatenate([[0], np.cumsum(chunks)]).astype(np.int32)
             chunk_slot = np.repeat(np.arange(self.B, dtype=np.int32), chunks)
             lib = _lib.load()
@@ -93,10 +93,8 @@ class BatchHandle:
                     plan = vanilla_tile_plan(self, n, row0, int(self.vanilla_tile_rows), n_edge_feat)
                     if plan is not None:
                         tensors, (n_tiles, hmax, emax, tmax) = plan
-                        words_t = torch.empty_like(words)  # the words in transposed order
-                        keep += [*tensors, words_t]
-                        (c.tile_row0, c.halo_off, c.halo_ids, c.lcol_off, c.lcol, c.ltcol_off, c.ltcol, c.tpos) = (t.data_ptr() for t in tensors)
-                        c.relu_words_t = words_t.data_ptr()
+                        keep += tensors
+                        (c.tile_row0, c.halo_off, c.halo_ids, c.lcol_off, c.lcol, c.ltcol_off, c.ltcol) = (t.data_ptr() for t in tensors)
                         c.n_tiles, c.halo_max, c.tile_edges_max, c.tile_tedges_max = n_tiles, hmax, emax, tmax
             sc = (c, tuple(keep))
             self._lds[key] = sc
@@ -142,6 +140,7 @@ class BatchHandle:
 
 
 LDS_MAX = 160 * 1024
+VANILLA_CHUNK = 64  # DR_VANILLA_CHUNK: rows per weight-gradient partial of the Vanilla pipeline
 
 
 def vanilla_tile_plan(h: BatchHandle, n, row0, tile_rows, n_edge_feat):
@@ -151,7 +150,7 @@ def vanilla_tile_plan(h: BatchHandle, n, row0, tile_rows, n_edge_feat):
     and every CSR / transposed edge's column as an index into it.  None when a
     tile's LDS would exceed one workgroup's 160 KiB (the untiled kernels run)."""
     p = h.store.packed
-    tile_row0, hoff, hids, loff, lcs, toff, tcs, tps = [0], [0], [], [0], [], [0], [], []
+    tile_row0, hoff, hids, loff, lcs, toff, tcs = [0], [0], [], [0], [], [0], []
     hmax = emax = tmax = 0
     for slot, gid in enumerate(h.gids_host.astype(np.int64)):
         ng = int(n[slot])
@@ -159,8 +158,6 @@ def vanilla_tile_plan(h: BatchHandle, n, row0, tile_rows, n_edge_feat):
         rp = p.rowptr[n0 + gid : n0 + gid + ng + 1].astype(np.int64)
         trp = p.t_rowptr[n0 + gid : n0 + gid + ng + 1].astype(np.int64)
         col, tcol = p.col[e0:e1], p.t_col[e0:e1]
-        tinv = np.empty(e1 - e0, np.int32)  # CSR slot -> transposed slot
-        tinv[p.t_eid[e0:e1]] = np.arange(e1 - e0, dtype=np.int32)
         for r0 in range(0, ng, tile_rows):
             r1 = min(ng, r0 + tile_rows)
             cs, ts = col[rp[r0] : rp[r1]], tcol[trp[r0] : trp[r1]]
@@ -168,7 +165,6 @@ def vanilla_tile_plan(h: BatchHandle, n, row0, tile_rows, n_edge_feat):
             hids.append(halo)
             hoff.append(hoff[-1] + halo.size)
             lcs.append(np.searchsorted(halo, cs).astype(np.uint16))
-            tps.append(tinv[rp[r0] : rp[r1]])
             loff.append(loff[-1] + cs.size)
             tcs.append(np.searchsorted(halo, ts).astype(np.uint16))
             toff.append(toff[-1] + ts.size)
@@ -179,12 +175,12 @@ def vanilla_tile_plan(h: BatchHandle, n, row0, tile_rows, n_edge_feat):
         return None
     fes = max(1, n_edge_feat)
     r4 = lambda v: (v + 3) & ~3  # noqa: E731
-    lds = 4 * max(hmax * 32 + r4(emax * fes) + r4(emax) + r4((emax + 1) // 2), hmax * 32 + r4(emax * fes) + r4(emax) + r4(tmax) + r4((tmax + 1) // 2))  # tile_carve (forward, backward)
+    lds = 4 * (hmax * 32 + r4(emax * fes) + r4(emax) + r4(tmax) + r4((tmax + 1) // 2))  # tile_carve (backward, the larger)
     if lds > LDS_MAX:
         return None
     dev = h.store.device
     cat16 = lambda parts: np.concatenate([*parts, np.zeros(8, np.uint16)])  # noqa: E731
-    arrays = [np.asarray(tile_row0, np.int32), np.asarray(hoff, np.int32), np.concatenate(hids), np.asarray(loff, np.int32), cat16(lcs).view(np.int16), np.asarray(toff, np.int32), cat16(tcs).view(np.int16), np.concatenate([*tps, np.zeros(8, np.int32)])]
+    arrays = [np.asarray(tile_row0, np.int32), np.asarray(hoff, np.int32), np.concatenate(hids), np.asarray(loff, np.int32), cat16(lcs).view(np.int16), np.asarray(toff, np.int32), cat16(tcs).view(np.int16)]
     return [torch.from_numpy(a).to(dev) for a in arrays], (n_tiles, hmax, emax, tmax)
 
 
@@ -430,12 +426,13 @@ class MixedSplit:
     outputs, loss term and partials to its row of the whole batch, so the
     reduction, outputs and dropout units are those of one launch over it."""
 
-    def __init__(self, spec: FusedSpec, h: BatchHandle, out_dim):
+    def __init__(self, spec: FusedSpec, h: BatchHandle, out_dim, fits=None):
         st = h.store
-        f, alias = st.n_feat, int(st.packed.transpose_aliased)
-        idx = h.gids_host.astype(np.int64)
-        sizes = [a[idx] for a in st._sizes]  # noqa: SLF001
-        fits = np.array([spec.lds(*(int(a[i]) for a in sizes), f, alias, out_dim) <= LDS_MAX for i in range(h.B)])
+        if fits is None:  # per graph: does the model's per-graph kernel hold it
+            f, alias = st.n_feat, int(st.packed.transpose_aliased)
+            idx = h.gids_host.astype(np.int64)
+            sizes = [a[idx] for a in st._sizes]  # noqa: SLF001
+            fits = np.array([spec.lds(*(int(a[i]) for a in sizes), f, alias, out_dim) <= LDS_MAX for i in range(h.B)])
         self.valid = bool(fits.any() and not fits.all())
         if not self.valid:
             return

@@ -394,15 +394,12 @@ typedef struct dr_vanilla_scratch {
   const uint16_t* lcol;       /* halo index of each such edge's column                       */
   const int32_t* ltcol_off;   /* [n_tiles+1] into ltcol: the tile's transposed edges          */
   const uint16_t* ltcol;      /* halo index of each transposed edge's source                 */
-  const int32_t* tpos;        /* indexed like lcol: each CSR edge's transposed slot (graph-local) */
-  uint32_t* relu_words_t;     /* [2, edge0[B]]: the ReLU words again, in transposed order (written by
-                                 the tiled forward, staged per tile by the tiled backward)    */
   int32_t n_tiles;
   int32_t halo_max;           /* >= every tile's halo size (<= 65535)                        */
   int32_t tile_edges_max;     /* >= every tile's CSR edge count                               */
   int32_t tile_tedges_max;    /* >= every tile's transposed edge count                        */
 } dr_vanilla_scratch;
-#define DR_VANILLA_CHUNK 32
+#define DR_VANILLA_CHUNK 64
 
 /* slab: per layer [dWe (32 x (2F+Fe)) | dbe (32) | dWn (F x (F+32)) | dbn (F)], layer 1 then 2
  * head: g [r4(F)] | relu(fc1) [128] | its grad [128] | dout [r4(out)] | d mean [r4(F)] */

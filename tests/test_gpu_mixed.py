@@ -179,8 +179,10 @@ def _vanilla_datas(counts, seed):
     return out
 
 
-@pytest.mark.parametrize("with_atoms", [True, False])
-def test_vanilla_mixed_batch_train_step_vs_oracle(with_atoms):
+@pytest.mark.parametrize("with_atoms,dispatch", [(True, False), (True, True), (False, False)])
+def test_vanilla_mixed_batch_train_step_vs_oracle(with_atoms, dispatch):
+    """dispatch: the residue / SRV graphs on the per-graph kernel, the atom
+    graphs on the pipeline, two streams, rows by dr_pass.slot."""
     counts = {"residue": 5, "srv": 3, "atom": 2} if with_atoms else {"residue": 6, "srv": 4}
     datas = [d for _, d in _vanilla_datas(counts, seed=47)]
     torch.manual_seed(21)
@@ -193,7 +195,9 @@ def test_vanilla_mixed_batch_train_step_vs_oracle(with_atoms):
     model.load_state_dict(model_o.state_dict())
     model = model.to(DEV).train()
     h = BatchHandle(_store(datas, clusters=False), np.arange(len(datas)))
+    h.mixed_dispatch = dispatch
     assert van_amd.fused_fits(h, 30, 3) == (not with_atoms)  # per-graph kernel only without atom graphs
+    assert (van_amd._mixed_split(h, 30, 3, 1) is not None) == with_atoms  # noqa: SLF001
     step = FusedTrainStep(model)
     loss, out = step.step(h)
     torch.cuda.synchronize()
