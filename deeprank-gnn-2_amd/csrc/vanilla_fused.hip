@@ -930,7 +930,6 @@ __global__ void __launch_bounds__(RB) vb_wgrad_mfma(VA a, int l) {
   float* cD = cS + WR * 32;
   float* cDP = cD + WR * 32;
   float* cDU = cDP + WR * 32;
-  float* cE = cDU + WR * XS;
   // the chunk's rows (contiguous in every array) by 16-byte loads; rows past the chunk: zeros
   auto stage4 = [&](float* dst, const float* src, int n4, int valid4) {
     for (int p = threadIdx.x; p < n4; p += RB)
@@ -941,25 +940,37 @@ __global__ void __launch_bounds__(RB) vb_wgrad_mfma(VA a, int l) {
   stage4(cS, L.s + g0 * 32, WR * 8, nr * 8);
   stage4(cD, ws + a.L.d + g0 * 32, WR * 8, nr * 8);
   stage4(cDP, ws + a.L.dp + g0 * 32, WR * 8, nr * 8);
-  stage4(cE, ws + a.L.eap + g0 * 32 * FeS, nr * 8 * FeS, nr * 8 * FeS);
   __syncthreads();
   const int nwe = 32 * KE, nwn = F * KN, total = nwe + 32 + nwn + F;
   float* out = a.ws.part + (int64_t)ch * total;
-  // scalar sums: dWc (edge-attribute partials), dbe, dbn
-  for (int p = threadIdx.x; p < 32 * Fe + 32 + F; p += RB) {
+  // scalar sums: dWc (edge-attribute partials, read from HBM), dbe, dbn: four
+  // lanes per output (16 rows each, loads issued together), combined in order
+  const float* eap = ws + a.L.eap + g0 * 32 * FeS;
+  for (int p0 = threadIdx.x; p0 < 4 * (32 * Fe + 32 + F); p0 += RB) {
+    const int p = p0 >> 2, qr = p0 & 3, ib = qr * (WR / 4);
     float v = 0.f;
     if (p < 32 * Fe) {
       const int c = p / Fe, f = p - c * Fe;
-      for (int i = 0; i < nr; ++i) v += cE[(i * 32 + c) * FeS + f];
-      out[c * KE + 2 * F + f] = v;
+      float t[WR / 4];
+#pragma unroll
+      for (int u = 0; u < WR / 4; ++u) t[u] = ib + u < nr ? eap[((ib + u) * 32 + c) * FeS + f] : 0.f;
+#pragma unroll
+      for (int u = 0; u < WR / 4; ++u) v += t[u];
     } else if (p < 32 * Fe + 32) {
       const int c = p - 32 * Fe;
-      for (int i = 0; i < nr; ++i) v += cD[i * 32 + c];
-      out[nwe + c] = v;
+#pragma unroll
+      for (int u = 0; u < WR / 4; ++u) v += cD[(ib + u) * 32 + c];  // rows past the chunk are 0
     } else {
       const int n = p - 32 * Fe - 32;
-      for (int i = 0; i < nr; ++i) v += cDU[i * XS + n];
-      out[nwe + 32 + nwn + n] = v;
+#pragma unroll
+      for (int u = 0; u < WR / 4; ++u) v += cDU[(ib + u) * XS + n];
+    }
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    if (qr == 0) {
+      if (p < 32 * Fe) out[(p / Fe) * KE + 2 * F + p % Fe] = v;
+      else if (p < 32 * Fe + 32) out[nwe + p - 32 * Fe] = v;
+      else out[nwe + 32 + nwn + p - 32 * Fe - 32] = v;
     }
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, kq = lane >> 4;
@@ -1063,7 +1074,8 @@ extern "C" int64_t dr_vanilla_scratch_floats(int64_t n_rows, int32_t n_feat, int
 extern "C" int64_t dr_vanilla_lds_bytes(int32_t n_feat, int32_t n_edge_feat, int32_t out_dim) {
   (void)out_dim;
   const int XS = r4(n_feat), FeS = n_edge_feat > 0 ? n_edge_feat : 1;
-  return 4LL * WR * (2 * XS + 3 * 32 + 32 * FeS);  // the largest dynamic LDS of the pipeline (vb_wgrad_mfma)
+  (void)FeS;
+  return 4LL * WR * (2 * XS + 3 * 32);  // the largest dynamic LDS of the pipeline (vb_wgrad_mfma)
 }
 
 extern "C" int64_t dr_vanilla_part_floats(int32_t n_feat, int32_t n_edge_feat) {
