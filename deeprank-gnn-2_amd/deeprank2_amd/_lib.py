@@ -120,6 +120,12 @@ class VanillaScratchC(ctypes.Structure):
                 ("n_tiles", ctypes.c_int32), ("halo_max", ctypes.c_int32), ("tile_edges_max", ctypes.c_int32), ("tile_tedges_max", ctypes.c_int32)]
 
 
+class NcPlanC(ctypes.Structure):
+    _fields_ = [("base", VP), ("row0", VP), ("row_slot", VP), ("n_rows", ctypes.c_int64), ("tile_row0", VP), ("tile_first", VP),
+                ("halo_off", VP), ("halo_ids", VP), ("lcol_off", VP), ("lcol", VP), ("ltcol_off", VP), ("ltcol", VP),
+                ("n_tiles", ctypes.c_int32), ("halo_max", ctypes.c_int32), ("tile_edges_max", ctypes.c_int32), ("tile_tedges_max", ctypes.c_int32)]
+
+
 class PackInputC(ctypes.Structure):
     _fields_ = [
         ("n_graphs", ctypes.c_int32), ("n_feat", ctypes.c_int32), ("n_edge_feat", ctypes.c_int32), ("require_clusters", ctypes.c_int32),
@@ -211,6 +217,9 @@ SIGNATURES = [
     ("dr_ginet_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 8),
     ("dr_ginet_large_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(LargePlanC), ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, ctypes.c_int32, VP]),
     ("dr_ginet_large_conv_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 5),
+    ("dr_ginet_nocluster_large_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(NcPlanC), ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), VP]),
+    ("dr_nc_large_scratch_floats", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
+    ("dr_nc_large_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 5),
     ("dr_fout_large_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(LargePlanC), ctypes.POINTER(FoutWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP]),
     ("dr_sgat_large_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(LargePlanC), ctypes.POINTER(FoutWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP]),
     ("dr_fout_large_conv_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 6),

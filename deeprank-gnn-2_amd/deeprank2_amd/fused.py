@@ -143,9 +143,9 @@ LDS_MAX = 160 * 1024
 VANILLA_CHUNK = 64  # DR_VANILLA_CHUNK: rows per weight-gradient partial of the Vanilla pipeline
 
 
-def vanilla_tile_plan(h: BatchHandle, n, row0, tile_rows, n_edge_feat):
+def vanilla_tile_plan(h: BatchHandle, n, row0, tile_rows, n_edge_feat, lds_check=True):
     """Edge-tile plan of the VanillaNetwork pipeline (dr_vanilla_scratch tile_*
-    fields): each graph's rows cut into tiles of ``tile_rows``; per tile the
+    fields; also ginet_nocluster's large-graph pipeline, dr_nc_plan): each graph's rows cut into tiles of ``tile_rows``; per tile the
     ascending union of its rows' out- and in-neighbours (the halo staged in LDS)
     and every CSR / transposed edge's column as an index into it.  None when a
     tile's LDS would exceed one workgroup's 160 KiB (the untiled kernels run)."""
@@ -176,7 +176,7 @@ def vanilla_tile_plan(h: BatchHandle, n, row0, tile_rows, n_edge_feat):
     fes = max(1, n_edge_feat)
     r4 = lambda v: (v + 3) & ~3  # noqa: E731
     lds = 4 * (hmax * 32 + r4(emax * fes) + r4(emax) + r4(tmax) + r4((tmax + 1) // 2))  # tile_carve (backward, the larger)
-    if lds > LDS_MAX:
+    if lds_check and lds > LDS_MAX:
         return None
     dev = h.store.device
     cat16 = lambda parts: np.concatenate([*parts, np.zeros(8, np.uint16)])  # noqa: E731

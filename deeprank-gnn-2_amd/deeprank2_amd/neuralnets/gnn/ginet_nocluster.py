@@ -14,11 +14,12 @@ GINet's recipe.  No clusters are needed.  There is no CPU path.
 
 from __future__ import annotations
 
+import numpy as np
 import torch
 from torch import nn
 
 from deeprank2_amd import _lib, layered
-from deeprank2_amd.fused import BatchHandle, Dropout, FusedFn, FusedSpec, make_pass, resolve_batch, run_pass
+from deeprank2_amd.fused import LDS_MAX, BatchHandle, Dropout, FusedFn, FusedSpec, make_pass, resolve_batch, run_pass, vanilla_tile_plan
 from deeprank2_amd.neuralnets.gnn import ginet as _ginet
 from deeprank2_amd.neuralnets.gnn.ginet import GINetConvLayer
 
@@ -31,7 +32,52 @@ def _lds(n, e, k0, p1, k1, f, alias, out):  # noqa: ARG001
     return _lib.load().dr_ginet_nocluster_lds_bytes(n, e, f, out)
 
 
-SPEC = FusedSpec(PARAM_NAMES, _ginet.recipe, _ginet.slab_stride, _ginet.head_stride, "dr_ginet_nocluster_graph_pass", _ginet.weights_c, _lds, dropout=0.4, layers=layered.ginet_nocluster_forward, attention=True)
+NC_TILE = 64  # rows per tile of the large-graph pipeline (its kernels hold at most 64)
+
+
+class _NcPlan:
+    """Host side of dr_nc_plan for one batch: node rows, the edge-tile plan
+    (halos of out- and in-neighbours, as the Vanilla pipeline's) and the scratch."""
+
+    def __init__(self, h: BatchHandle):
+        st = h.store
+        idx = h.gids_host.astype(np.int64)
+        n = st._sizes[0][idx]  # noqa: SLF001
+        row0 = np.concatenate([[0], np.cumsum(n)]).astype(np.int32)
+        plan = vanilla_tile_plan(h, n, row0, NC_TILE, st.n_edge_feat, lds_check=False)
+        if plan is None:
+            msg = "ginet_nocluster large-graph path: no tile plan for this batch (a tile's halo exceeds 65535 nodes)"
+            raise RuntimeError(msg)
+        tensors, (n_tiles, hmax, emax, tmax) = plan
+        lib = _lib.load()
+        self.lds = int(lib.dr_nc_large_lds_bytes(st.n_feat, hmax, emax, tmax, 16))
+        if self.lds > LDS_MAX:
+            msg = f"ginet_nocluster large-graph path needs {self.lds} B of LDS (> 160 KiB)"
+            raise RuntimeError(msg)
+        dev = st.device
+        tiles = (n + NC_TILE - 1) // NC_TILE
+        ints = torch.from_numpy(np.concatenate([row0, np.repeat(np.arange(h.B, dtype=np.int32), n), np.concatenate([[0], np.cumsum(tiles)]).astype(np.int32)])).to(dev)
+        self.buf = torch.empty(max(1, int(lib.dr_nc_large_scratch_floats(int(row0[-1]), h.B, n_tiles, st.n_feat))), dtype=torch.float32, device=dev)
+        self.keep = [ints, *tensors]
+        c = _lib.NcPlanC()
+        base = ints.data_ptr()
+        c.base, c.row0, c.row_slot, c.n_rows = self.buf.data_ptr(), base, base + 4 * (h.B + 1), int(row0[-1])
+        c.tile_first = base + 4 * (h.B + 1 + int(row0[-1]))
+        (c.tile_row0, c.halo_off, c.halo_ids, c.lcol_off, c.lcol, c.ltcol_off, c.ltcol) = (t.data_ptr() for t in tensors)
+        c.n_tiles, c.halo_max, c.tile_edges_max, c.tile_tedges_max = n_tiles, hmax, emax, tmax
+        self.c = c
+
+
+def _large(h, w, p):
+    """Graphs beyond one workgroup's LDS: the tile-kernel pipeline (dr_ginet_nocluster_large_pass)."""
+    plan = h._lds.get("nc_plan")  # noqa: SLF001
+    if plan is None:
+        plan = h._lds["nc_plan"] = _NcPlan(h)  # noqa: SLF001
+    rc = _lib.load().dr_ginet_nocluster_large_pass(h.store.cstruct(), h.descs.data_ptr(), h.B, plan.c, w, p, _lib.stream_ptr(h.store.device))
+    _lib.check(rc, "dr_ginet_nocluster_large_pass")
+
+
+SPEC = FusedSpec(PARAM_NAMES, _ginet.recipe, _ginet.slab_stride, _ginet.head_stride, "dr_ginet_nocluster_graph_pass", _ginet.weights_c, _lds, dropout=0.4, large=_large, layers=layered.ginet_nocluster_forward, attention=True)
 
 
 def graph_pass(h: BatchHandle, params, out_dim, flags, **kw):

@@ -314,6 +314,40 @@ int dr_ginet_nocluster_graph_pass(const dr_graph_store* store, const dr_graph_de
                                   const dr_ginet_weights* w, const dr_pass* pass, int32_t lds_bytes, void* stream);
 int64_t dr_ginet_nocluster_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_feat, int32_t out_dim);
 
+/* ginet_nocluster.GINet on graphs beyond one workgroup's LDS (atom level):
+ * the same arithmetic as a pipeline of tile kernels over the batch's rows
+ * (tiles of <= 64 consecutive rows of one graph, their halo -- out- and
+ * in-neighbours -- staged in LDS):
+ *   1. Z1 = A X, H1 = relu(Z1 [W1; W1e]^T)         (MFMA)    -> Z1, H1
+ *   2. Z2 = A H1, H2 = relu(Z2_b W2_b^T)           (MFMA)    -> Z2, relu' bits, tile column sums
+ *   3. per graph: mean, fc1/relu/dropout/fc2, loss, head backward -> dG / N
+ *   4. dZ2 = dS2 W2_b and the tile's dW2 partial  (MFMA)    -> dZ2
+ *   5. dS1 = relu'(H1) (A^T dZ2) and the tile's dW1 partial (MFMA)
+ *   6. per graph: the tiles' partials summed in tile order into the slab.
+ * Slab / head partials as dr_ginet_nocluster_graph_pass (the GINet recipe).
+ * base: dr_nc_large_scratch_floats(n_rows, B, n_tiles, F) floats.          */
+typedef struct dr_nc_plan {
+  float* base;
+  const int32_t* row0;       /* [B+1] first batch row of each slot            */
+  const int32_t* row_slot;   /* [n_rows] slot of each batch row                */
+  int64_t n_rows;
+  const int32_t* tile_row0;  /* [n_tiles+1] batch row ranges (one graph each, <= 64 rows) */
+  const int32_t* tile_first; /* [B+1] first tile of each slot                  */
+  const int32_t* halo_off;   /* [n_tiles+1] */
+  const int32_t* halo_ids;   /* per tile: local ids of its rows' out- and in-neighbours, ascending */
+  const int32_t* lcol_off;   /* [n_tiles+1] */
+  const uint16_t* lcol;      /* halo index of each of the tile's CSR edges      */
+  const int32_t* ltcol_off;  /* [n_tiles+1] */
+  const uint16_t* ltcol;     /* halo index of each of the tile's transposed edges */
+  int32_t n_tiles, halo_max, tile_edges_max, tile_tedges_max;
+} dr_nc_plan;
+int dr_ginet_nocluster_large_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                                  const dr_nc_plan* plan, const dr_ginet_weights* w, const dr_pass* pass,
+                                  void* stream);
+int64_t dr_nc_large_scratch_floats(int64_t n_rows, int32_t n_batch, int32_t n_tiles, int32_t n_feat);
+int64_t dr_nc_large_lds_bytes(int32_t n_feat, int32_t halo_max, int32_t tile_edges_max, int32_t tile_tedges_max,
+                              int32_t out_dim);
+
 /* ---- SGAT (deeprank2/neuralnets/gnn/sgat.py:13-133) -----------------------
  * Same kernel family and partial layouts as FoutNet, with dr_fout_weights
  * pointing into SGAT's parameters: wc1 = conv1.weight rows 0..F-1, wn1 = rows

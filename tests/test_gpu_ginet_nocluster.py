@@ -146,3 +146,49 @@ def test_nocluster_feature_widths_vs_oracle(f):
     ref = dict(model_o.named_parameters())
     for n, p in model.named_parameters():
         assert_grad_close(p.grad.cpu().numpy(), ref[n].grad.numpy(), err_msg=n)
+
+
+@pytest.mark.parametrize("force", [False, True])
+def test_nocluster_large_pipeline_vs_oracle(force):
+    """Graphs beyond one workgroup's LDS (or residue graphs forced through it):
+    the tile-kernel pipeline dr_ginet_nocluster_large_pass -- forward, loss with
+    a fixed dropout mask, every gradient and the Adam step vs the oracle; a
+    residue + SRV + atom mix when not forced."""
+    if force:
+        datas = _synthetic(6, seed=7)
+    else:
+        datas = _synthetic(2, seed=8, n_lo=2600, n_hi=3000, mean_degree=16.0) + _synthetic(3, seed=9) + _synthetic(2, seed=10, n_lo=26, n_hi=36, mean_degree=7.0)
+    b = len(datas)
+    torch.manual_seed(4)
+    model_o = gnn_ref.GINetNoCluster(30, 1, 3)
+    model = amd.GINet(30, 1, 3)
+    model.load_state_dict(model_o.state_dict())
+    model = model.to(DEV).train()
+    store = GraphStore(pack_graphs(records_from_batch(P.Batch.from_data_list(datas)), require_clusters=False), DEV)
+    h = BatchHandle(store, np.arange(b))
+    h.force_large = force
+    from deeprank2_amd import layered
+    from deeprank2_amd.fused import LDS_MAX, lds_for
+
+    assert not layered.needs_layers(amd.SPEC, h, 1) and (force or lds_for(amd.SPEC, h, 1) > LDS_MAX)
+    mask = (torch.rand(b, 128, generator=torch.Generator().manual_seed(5)) >= 0.4).to(torch.uint8)
+    model_o.dropout_fn = lambda x, p, training: x * mask.float() / (1 - p) if training else x
+    bat = P.Batch.from_data_list([d.clone() for d in datas])
+    out_o = model_o(bat)
+    loss_o = torch.nn.functional.mse_loss(out_o.reshape(-1), bat.y)
+    loss_o.backward()
+    step = FusedTrainStep(model)
+    before = [p.detach().clone() for p in step.params]
+    loss, out = step.step(h, mask=mask.to(DEV))
+    assert h._lds.get("nc_plan") is not None  # noqa: SLF001  (the pipeline ran)
+    np.testing.assert_allclose(out.cpu().numpy(), out_o.detach().numpy(), **TOL)
+    assert float(loss) == pytest.approx(float(loss_o.detach()), rel=1e-4)
+    grads = dict(zip(amd.PARAM_NAMES, step.grads))
+    for n, p in model_o.named_parameters():
+        assert_grad_close(grads[n].cpu().numpy(), p.grad.numpy(), ntol=1e-5, err_msg=n)
+    ref = [torch.nn.Parameter(x) for x in before]
+    for r, g in zip(ref, step.grads):
+        r.grad = g.detach().clone()
+    torch.optim.Adam(ref, lr=1e-3, weight_decay=1e-5).step()
+    for n, r, p in zip(amd.PARAM_NAMES, ref, step.params):
+        np.testing.assert_allclose(p.detach().cpu().numpy(), r.detach().cpu().numpy(), rtol=1e-5, atol=1e-7, err_msg=n)

@@ -68,7 +68,7 @@ def test_graph_beyond_lds_runs_layers_and_matches_oracle(name):
     if name == "ginet_nocluster":
         m.eval()
         model_o.eval()
-    h = _handle(datas, clusters=name != "ginet_nocluster", force=name != "ginet_nocluster")  # FoutNet / SGAT: the large kernels run such graphs unless forced
+    h = _handle(datas, clusters=name != "ginet_nocluster", force=True)  # the large-graph kernels run such graphs unless the layer path is forced
     assert layered.needs_layers(m.fused_spec, h, 1)
     out = m(SimpleNamespace(_dr_handle=h))
     out_o, loss_o, g_o = _oracle_grads(model_o, datas)
