@@ -283,6 +283,7 @@ def cpu_baseline(graphs, budget_s=15.0, max_steps=60, model_name="ginet"):
     """The CPU oracle (op-for-op restatement of the reference, torch CPU) training
     the same batch: forward, MSE, backward, Adam — on this host's cores
     (``len(os.sched_getaffinity(0))``, or the box's ``OMP_NUM_THREADS`` share)."""
+    import numpy as np  # noqa: PLC0415
     import torch  # noqa: PLC0415
 
     from oracle import data_ref, gnn_ref  # noqa: PLC0415
@@ -306,16 +307,28 @@ def cpu_baseline(graphs, budget_s=15.0, max_steps=60, model_name="ginet"):
         loss.backward()
         opt.step()
 
-    for _ in range(2):
-        one()
-    t0 = time.perf_counter()
-    n = 0
-    while n < max_steps and time.perf_counter() - t0 < budget_s:
-        one()
-        n += 1
-    dt = (time.perf_counter() - t0) / n
+    # a stable denominator: the threads pinned to `cores` fixed CPUs of the
+    # affinity set, 3 warm-up steps, then the median step time of the timed ones
+    pinned = sorted(os.sched_getaffinity(0))[:cores] if hasattr(os, "sched_getaffinity") else []
+    prev = os.sched_getaffinity(0) if pinned else None
+    if pinned:
+        os.sched_setaffinity(0, pinned)
+    try:
+        for _ in range(3):
+            one()
+        times = []
+        t0 = time.perf_counter()
+        while len(times) < max_steps and time.perf_counter() - t0 < budget_s:
+            t1 = time.perf_counter()
+            one()
+            times.append(time.perf_counter() - t1)
+    finally:
+        if prev is not None:
+            os.sched_setaffinity(0, prev)
+    dt = float(np.median(times))
+    n = len(times)
     name = ORACLE_MODELS[model_name]
-    return {"value": round(len(graphs) / dt, 2), "unit": "graphs/s", "cores": cores, "host_affinity_cores": affinity, "kind": "port", "sample": f"{n} {name}(30,1,3) train steps (fwd+MSE+bwd+Adam) on one batch of {len(graphs)} of the same synthetic graphs; oracle/gnn_ref.py on torch CPU, {cores} threads (host affinity {affinity}); {dt * 1e3:.1f} ms/step"}
+    return {"value": round(len(graphs) / dt, 2), "unit": "graphs/s", "cores": cores, "host_affinity_cores": affinity, "kind": "port", "sample": f"median of {n} {name}(30,1,3) train steps (fwd+MSE+bwd+Adam) after 3 warm-up steps, on one batch of {len(graphs)} of the same synthetic graphs; oracle/gnn_ref.py on torch CPU, {cores} threads pinned to {len(pinned) or cores} CPUs (host affinity {affinity}); {dt * 1e3:.1f} ms/step (min {min(times) * 1e3:.1f}, max {max(times) * 1e3:.1f})"}
 
 
 def parse_args(argv):
