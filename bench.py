@@ -344,6 +344,7 @@ def parse_args(argv):
     ap.add_argument("--force-large", type=int, default=0, help="GINet: run the split tile+tail path with this many nodes per tile (diagnostic)")
     ap.add_argument("--ginet-path", choices=["auto", "split", "onepass"], default="auto", help="GINet: auto = one workgroup per graph when the batch fits LDS, else the split path; split = tile kernel + tail kernel; onepass = tiles + in-launch tails (one launch)")
     ap.add_argument("--vanilla-pipeline", action="store_true", help="VanillaNetwork: the batch-wide kernel pipeline even when the per-graph kernel fits (diagnostic)")
+    ap.add_argument("--sibling-split", type=int, default=0, help="GINet per-graph kernel over K workgroups per graph (dr_ginet_sibling_pass; 0/1 off, -1 auto)")
     ap.add_argument("--mixed-dispatch", action="store_true", help="mixed batches: graphs that fit LDS on the per-graph kernel, the rest on the large path, two streams (opt-in, measured slower)")
     ap.add_argument("--one-launch", action="store_true", help="GINet, N=1: graph pass + gradient reduce + Adam in one launch (dr_ginet_train_step; opt-in, measured slower at B=64)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -432,6 +433,7 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
         h.large_onepass = args.ginet_path == "onepass"
         h.vanilla_pipeline = bool(args.vanilla_pipeline)
         h.mixed_dispatch = bool(args.mixed_dispatch)
+        h.sibling_split = None if args.sibling_split < 0 else args.sibling_split
         if os.environ.get("DR_VANILLA_TILE") is not None:  # diagnostic: rows per pipeline edge tile (0: untiled)
             h.vanilla_tile_rows = int(os.environ["DR_VANILLA_TILE"])
 

@@ -524,13 +524,27 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
 // WT: the per-graph partials are stored write-through (read back inside the
 // same launch by dr_ginet_train_step's reducers).  Returns the step counter
 // value the pass used (its dropout offset).
-template <int KPT, bool WT>
-__device__ __forceinline__ uint64_t graph_body(const GinetArgs& a) {
+// Sibling split (dr_ginet_sibling_pass): k workgroups stage the same graph,
+// each runs the front half on every k-th 16-row tile, publishes its Z rows
+// (write-through) and depth-0 keys (agent-scope 64-bit atomic max) and takes a
+// ticket; the last to arrive decodes the keys and runs the tail.  Nothing
+// waits on another workgroup.
+struct SibCtx {
+  int rk, k, b;
+  float* z;                 // [rows, XS] Z rows of the batch (dr_large_plan.z)
+  const int32_t* z_row0;    // [B+1]
+  unsigned long long* gkey; // [B, k0_max, 32], zero on entry and left zero
+  int k0_max;
+  uint32_t* arrive;         // [B], zero on entry and left zero
+};
+
+template <int KPT, bool WT, bool SIB = false>
+__device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx& sc = SibCtx{}) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int b = blockIdx.x;
+  const int b = SIB ? sc.b : (int)blockIdx.x;
   const dr_graph_store& s = a.s;
   const dr_graph_desc d = a.descs[b];  // one 64-byte scalar load
   const int g = d.gid;
@@ -660,7 +674,7 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a) {
       wa[j] = kk < F ? sW1[li * F + kk] : 0.f;
       wb[j] = kk < F ? sW1[(16 + li) * F + kk] : 0.f;
     }
-    for (int tt = wave; tt * 16 < N; tt += NW) {
+    for (int tt = SIB ? wave * sc.k + sc.rk : wave; tt * 16 < N; tt += SIB ? NW * sc.k : NW) {
       const int r0 = tt * 16;
       {  // rows r0+slot and r0+8+slot together: two independent edge chains per lane
         const int i0 = r0 + slot, i1 = r0 + 8 + slot;
@@ -733,16 +747,59 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a) {
   STAMP(2);
   __syncthreads();
   STAMP(3);
-  for (int p = tid; p < K0 * 32; p += NT) {
-    const unsigned long long key = skey[p];
-    sP1[p] = key ? __uint_as_float((uint32_t)(key >> 32)) : 0.f;
-    sA1[p] = key ? (int)(0xffffffffu - (uint32_t)key) : N;
+  typedef __attribute__((address_space(1))) unsigned long long gu64s;
+  typedef __attribute__((address_space(1))) unsigned int gu32s;
+  float* zg = SIB ? sc.z + (int64_t)sc.z_row0[b] * XS : nullptr;
+  if (SIB) {
+    // publish this sibling's Z rows (its tiles) write-through and its keys
+    gu64s* gk = (gu64s*)(sc.gkey) + (int64_t)b * sc.k0_max * 32;
+    const int ntile = (N + 15) >> 4, mine = (ntile - sc.rk + sc.k - 1) / sc.k, per = 16 * (XS >> 1);
+    for (int p = tid; p < mine * per; p += NT) {
+      const int tt = sc.rk + (p / per) * sc.k, q = p % per, i = tt * 16 + q / (XS >> 1), c2 = (q % (XS >> 1)) * 2;
+      if (i < N)
+        __hip_atomic_store((gu64s*)(zg + (int64_t)i * XS + c2),
+                           (unsigned long long)__float_as_uint(sZ[i * LDW + c2]) | ((unsigned long long)__float_as_uint(sZ[i * LDW + c2 + 1]) << 32),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    for (int p = tid; p < K0 * 32; p += NT)
+      if (skey[p]) __hip_atomic_fetch_max(gk + p, skey[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave drains its stores and atomics
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(sP1);
+    if (tid == 0) {
+      const uint32_t ticket = __hip_atomic_fetch_add((gu32s*)(sc.arrive + b), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool last = ticket == (uint32_t)sc.k - 1u;
+      if (last) __hip_atomic_store((gu32s*)(sc.arrive + b), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
+      flag[0] = last ? 1 : 0;
+    }
+    __syncthreads();
+    const bool last = flag[0] != 0;
+    __syncthreads();  // the flag read by every wave before sP1 is rewritten
+    if (!last) return drop_offset;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // the hand-off loads stay below the ticket
+    for (int p = tid; p < K0 * 32; p += NT) {
+      const unsigned long long key = __hip_atomic_load(gk + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(gk + p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // zero for the next launch
+      sP1[p] = key ? __uint_as_float((uint32_t)(key >> 32)) : 0.f;
+      sA1[p] = key ? (int)(0xffffffffu - (uint32_t)key) : N;
+    }
+  } else {
+    for (int p = tid; p < K0 * 32; p += NT) {
+      const unsigned long long key = skey[p];
+      sP1[p] = key ? __uint_as_float((uint32_t)(key >> 32)) : 0.f;
+      sA1[p] = key ? (int)(0xffffffffu - (uint32_t)key) : N;
+    }
   }
   __syncthreads();
 
   TailLds t = tail_lds(c, lds);
   t.keep = skeep;
-  auto zat = [&](int i, int kk) { return sZ[i * LDW + kk]; };
+  // Z at a pooling arg: this workgroup's LDS for its own tiles, else the
+  // sibling's write-through copy (sibling split)
+  auto zat = [&](int i, int kk) {
+    if (!SIB || ((i >> 4) % sc.k) == sc.rk) return sZ[i * LDW + kk];
+    return __uint_as_float(__hip_atomic_load((gu32s*)(zg + (int64_t)i * XS + kk), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  };
   // (dr_pass.slot: the graph's rows of the batch when it is split over launches)
   ginet_tail<decltype(zat), WT>(a, t, fc1_row, fc1_col, fc1_bias, a.p.slot ? a.p.slot[b] : b, N, K0, K1, F, OUT, y_g, drop_offset, zat);
   return drop_offset;
@@ -751,6 +808,18 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a) {
 template <int KPT>
 __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
   graph_body<KPT, false>(a);
+}
+
+// k sibling workgroups per graph: block -> (graph b, sibling rk), siblings 8
+// blocks apart (one XCD under round-robin dispatch: the hand-off stays in one
+// L2) within a window of 8k consecutive blocks
+template <int KPT>
+__global__ void __launch_bounds__(NT) ginet_sib_kernel(GinetArgs a, SibCtx sc) {
+  const int bx = blockIdx.x, hi = bx >> 3;
+  sc.rk = hi % sc.k;
+  sc.b = (hi / sc.k) * 8 + (bx & 7);
+  if (sc.b >= a.B) return;
+  graph_body<KPT, false, true>(a, sc);
 }
 
 // ---------------------------------------------------------------------------
@@ -1612,6 +1681,49 @@ extern "C" int dr_ginet_graph_pass(const dr_graph_store* store, const dr_graph_d
   } else {
     DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_graph_kernel<64>)));
     hipLaunchKernelGGL(ginet_graph_kernel<64>, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, args);
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int dr_ginet_sibling_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                                     const dr_large_plan* plan, const dr_ginet_weights* w, const dr_pass* pass,
+                                     int32_t split, int32_t lds_bytes, void* stream) {
+  if (!store || !descs || !w || !pass || !plan || n_batch < 0) return DR_E_ARG;
+  if (split < 1 || split > 8) return DR_E_ARG;
+  if (pass->out_dim < 1 || pass->out_dim > DR_MAX_OUT) return DR_E_UNSUPPORTED;
+  if (store->n_feat < 1 || 32 * store->n_feat > 2 * NT) return DR_E_UNSUPPORTED;  // F <= 64
+  if (lds_bytes > 160 * 1024) return DR_E_LDS;
+  if (pass->compute_dtype != DR_DTYPE_F32) return DR_E_UNSUPPORTED;
+  if (!plan->z || !plan->z_row0 || !plan->part_key || !plan->arrive || plan->k0_max < 1 || plan->k0_max > 64) return DR_E_ARG;
+  if ((pass->flags & DR_PASS_BACKWARD) && (!pass->slab || !pass->head)) return DR_E_ARG;
+  if ((pass->flags & DR_PASS_BACKWARD) && pass->loss_kind == DR_LOSS_NONE && !pass->dout) return DR_E_ARG;
+  if ((pass->flags & DR_PASS_FORWARD) && !pass->out) return DR_E_ARG;
+  if (pass->use_dropout == DR_DROPOUT_MASK && !pass->mask) return DR_E_ARG;
+  if (pass->use_dropout < DR_DROPOUT_OFF || pass->use_dropout > DR_DROPOUT_HASH) return DR_E_ARG;
+  if (n_batch == 0) return DR_OK;
+  if (!store->cl0) return DR_E_ARG;
+  GinetArgs args;
+  args.s = *store;
+  args.w = *w;
+  args.p = *pass;
+  args.descs = descs;
+  args.B = n_batch;
+  SibCtx sc;
+  sc.rk = 0;
+  sc.b = 0;
+  sc.k = split;
+  sc.z = plan->z;
+  sc.z_row0 = plan->z_row0;
+  sc.gkey = reinterpret_cast<unsigned long long*>(plan->part_key);
+  sc.k0_max = plan->k0_max;
+  sc.arrive = plan->arrive;
+  const dim3 grid((unsigned)(((n_batch + 7) / 8) * 8 * split));
+  if (store->n_feat <= 32) {
+    DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_sib_kernel<32>)));
+    hipLaunchKernelGGL(ginet_sib_kernel<32>, grid, dim3(NT), lds_bytes, (hipStream_t)stream, args, sc);
+  } else {
+    DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_sib_kernel<64>)));
+    hipLaunchKernelGGL(ginet_sib_kernel<64>, grid, dim3(NT), lds_bytes, (hipStream_t)stream, args, sc);
   }
   return (int)hipGetLastError();
 }

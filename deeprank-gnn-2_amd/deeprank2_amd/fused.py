@@ -45,6 +45,7 @@ class BatchHandle:
         self.vanilla_split = None  # Vanilla per-graph kernel: workgroups per graph (None: by batch size)
         self.vanilla_tile_rows = 16  # Vanilla pipeline edge kernels: rows per halo-staged tile (0: untiled gathers)
         self.fault = None  # device uint32 [2] (dr_pass.fault) of the autograd path's passes, made on first use
+        self.sibling_split = 0  # GINet per-graph kernel over k workgroups per graph (0/1: off; None: by batch size)
         self.mixed_dispatch = False  # graphs that fit LDS on the per-graph kernel, the rest on the large path (two streams; measured slower at configs[4])
 
     def lds(self, key, fn):
@@ -339,6 +340,7 @@ class FusedSpec:
     attention: bool = False  # GINetConvLayer model: batches with non-finite inputs need the layer path
     step_entry: str | None = None  # one-launch training step (graph pass + reduce + Adam), world of one
     handoffs: bool = False  # the graph pass hands rows between workgroups in-launch (dr_pass.fault can be set)
+    sibling: Callable | None = None  # (handle, weights, pass, lds, k): the per-graph kernel over k workgroups per graph
 
 
 def vanilla_fused_scratch_floats(n, e, fe):
@@ -409,6 +411,10 @@ def launch(spec: FusedSpec, h: BatchHandle, w, p):
             launch_mixed(spec, m, w, p)
             return
     if lds <= LDS_MAX and not (h.force_large and spec.large is not None):
+        k = sibling_k(spec, h)
+        if k > 1:
+            spec.sibling(h, w, p, lds, k)
+            return
         fn = getattr(_lib.load(), spec.entry)
         _lib.check(fn(h.store.cstruct(), h.descs.data_ptr(), h.B, w, p, lds, _lib.stream_ptr(h.store.device)), spec.entry)
     elif spec.large is not None:
@@ -416,6 +422,48 @@ def launch(spec: FusedSpec, h: BatchHandle, w, p):
     else:
         msg = f"largest graph of the batch needs {lds} B of LDS (> 160 KiB) and {spec.entry} has no large-graph path"
         raise RuntimeError(msg)
+
+
+def _device_cus(device):
+    try:
+        return int(torch.cuda.get_device_properties(torch.device(device)).multi_processor_count)
+    except (RuntimeError, AssertionError, ValueError):
+        return 256
+
+
+def sibling_k(spec: FusedSpec, h: BatchHandle) -> int:
+    """Workgroups per graph for the model's per-graph kernel (spec.sibling):
+    h.sibling_split, or (None) as many as keep the grid within one workgroup
+    per compute unit, at most 4."""
+    if spec.sibling is None:
+        return 1
+    k = h.sibling_split
+    if k is None:
+        k = max(1, min(4, _device_cus(h.store.device) // max(1, ((h.B + 7) // 8) * 8)))
+    return int(k) if k and k > 1 else 1
+
+
+class SiblingPlan:
+    """dr_large_plan fields dr_ginet_sibling_pass reads: Z rows, the depth-0
+    keys and the arrival tickets (both kept zero between launches)."""
+
+    def __init__(self, h: BatchHandle):
+        st = h.store
+        idx = h.gids_host.astype(np.int64)
+        n, k0 = st._sizes[0][idx], st._sizes[2][idx]  # noqa: SLF001
+        self.k0_max = max(1, int(k0.max()))
+        if self.k0_max > 64:  # noqa: PLR2004
+            msg = f"a graph of the batch has {self.k0_max} depth-0 clusters (> 64)"
+            raise RuntimeError(msg)
+        dev = st.device
+        z_row0 = np.concatenate([[0], np.cumsum(n)]).astype(np.int32)
+        self.z_row0 = torch.from_numpy(z_row0).to(dev)
+        self.z = torch.empty(max(1, int(z_row0[-1])) * st.x_stride, dtype=torch.float32, device=dev)
+        self.key = torch.zeros(h.B * self.k0_max * 32, dtype=torch.int64, device=dev)
+        self.arrive = torch.zeros(h.B, dtype=torch.int32, device=dev)
+        c = _lib.LargePlanC()
+        c.z_row0, c.z, c.part_key, c.arrive, c.k0_max = self.z_row0.data_ptr(), self.z.data_ptr(), self.key.data_ptr(), self.arrive.data_ptr(), self.k0_max
+        self.c = c
 
 
 class MixedSplit:

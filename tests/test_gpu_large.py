@@ -228,3 +228,35 @@ def test_onepass_train_step_vs_oracle_and_capture():
     torch.cuda.synchronize()
     for x, y in zip(after_replay, step.params):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("split", [2, 3, 4])
+def test_sibling_split_bit_identical_to_single_workgroup_kernel(split):
+    """dr_ginet_sibling_pass: k workgroups per graph (tiles round-robin, Z rows
+    and depth-0 keys handed over, the last to arrive runs the tail) give the
+    per-graph kernel's outputs, loss terms, slab rows and head vectors bit for
+    bit, hash dropout included; the keys and tickets are left zero; a second
+    launch repeats."""
+    datas = _datas(19, seed=23)
+    store = _store(datas)
+    torch.manual_seed(5)
+    model = amd.GINet(30, 2, 3).to(DEV)
+    params = model.ordered_params()
+    store.set_targets(np.arange(19) % 2)
+    res = []
+    for k in (1, split, split):
+        h = BatchHandle(store, np.arange(19))
+        h.sibling_split = k
+        out = torch.empty(19, 2, device=DEV)
+        slab = torch.empty(19 * amd.slab_stride(30), device=DEV)
+        head = torch.zeros(19 * amd.head_stride(2), device=DEV)
+        lpg = torch.empty(19, device=DEV)
+        amd.graph_pass(h, params, 2, 3, loss_kind=_lib.DR_LOSS_CE, loss_scale=1 / 19, dropout=Dropout(0.4, seed=9, offset=2), out=out, loss_per_graph=lpg, slab=slab, head=head)
+        torch.cuda.synchronize()
+        if k > 1:
+            plan = h._lds["sibling_plan"]  # noqa: SLF001
+            assert int(plan.key.abs().sum()) == 0 and int(plan.arrive.abs().sum()) == 0
+        res.append((out.cpu(), slab.cpu(), head.cpu(), lpg.cpu()))
+    for other in res[1:]:
+        for x, y in zip(res[0], other):
+            assert torch.equal(x, y)
