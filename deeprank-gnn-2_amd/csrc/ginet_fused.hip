@@ -749,18 +749,9 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
   STAMP(3);
   typedef __attribute__((address_space(1))) unsigned long long gu64s;
   typedef __attribute__((address_space(1))) unsigned int gu32s;
-  float* zg = SIB ? sc.z + (int64_t)sc.z_row0[b] * XS : nullptr;
   if (SIB) {
-    // publish this sibling's Z rows (its tiles) write-through and its keys
+    // publish this sibling's depth-0 keys
     gu64s* gk = (gu64s*)(sc.gkey) + (int64_t)b * sc.k0_max * 32;
-    const int ntile = (N + 15) >> 4, mine = (ntile - sc.rk + sc.k - 1) / sc.k, per = 16 * (XS >> 1);
-    for (int p = tid; p < mine * per; p += NT) {
-      const int tt = sc.rk + (p / per) * sc.k, q = p % per, i = tt * 16 + q / (XS >> 1), c2 = (q % (XS >> 1)) * 2;
-      if (i < N)
-        __hip_atomic_store((gu64s*)(zg + (int64_t)i * XS + c2),
-                           (unsigned long long)__float_as_uint(sZ[i * LDW + c2]) | ((unsigned long long)__float_as_uint(sZ[i * LDW + c2 + 1]) << 32),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
     for (int p = tid; p < K0 * 32; p += NT)
       if (skey[p]) __hip_atomic_fetch_max(gk + p, skey[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave drains its stores and atomics
@@ -783,6 +774,26 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
       sP1[p] = key ? __uint_as_float((uint32_t)(key >> 32)) : 0.f;
       sA1[p] = key ? (int)(0xffffffffu - (uint32_t)key) : N;
     }
+    __syncthreads();
+    // the Z rows of pooling args another sibling computed: gathered again from
+    // the staged graph (same CSR order, same sums; a row named by several
+    // (cluster, channel) pairs is written with the same value by each)
+    {
+      const int sub = tid & 7, nch = XS >> 2;
+      for (int p = tid >> 3; p < K0 * 32; p += NT / 8) {
+        const int i = sA1[p];
+        if (i >= N || ((i >> 4) % sc.k) == sc.rk) continue;
+        const int eb = srp[i], ee = srp[i + 1];
+        for (int ch = sub; ch < nch; ch += 8) {
+          const float4 z = drk::gather_row_chunk(scol, eb, ee, sX, XS, ch * 4);
+          float* zr = sZ + i * LDW + ch * 4;
+          zr[0] = z.x;
+          zr[1] = z.y;
+          zr[2] = z.z;
+          zr[3] = z.w;
+        }
+      }
+    }
   } else {
     for (int p = tid; p < K0 * 32; p += NT) {
       const unsigned long long key = skey[p];
@@ -794,12 +805,7 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
 
   TailLds t = tail_lds(c, lds);
   t.keep = skeep;
-  // Z at a pooling arg: this workgroup's LDS for its own tiles, else the
-  // sibling's write-through copy (sibling split)
-  auto zat = [&](int i, int kk) {
-    if (!SIB || ((i >> 4) % sc.k) == sc.rk) return sZ[i * LDW + kk];
-    return __uint_as_float(__hip_atomic_load((gu32s*)(zg + (int64_t)i * XS + kk), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  };
+  auto zat = [&](int i, int kk) { return sZ[i * LDW + kk]; };
   // (dr_pass.slot: the graph's rows of the batch when it is split over launches)
   ginet_tail<decltype(zat), WT>(a, t, fc1_row, fc1_col, fc1_bias, a.p.slot ? a.p.slot[b] : b, N, K0, K1, F, OUT, y_g, drop_offset, zat);
   return drop_offset;

@@ -10,13 +10,13 @@
 // The edge GEMM is split, We = [Wa | Wb | Wc]: B = X Wb^T is a node GEMM (MFMA),
 // A_i = Wa x_i + be is formed per CSR row inside the row pass, and
 // pre_e = A_i + B_j + Wc ea_e is rebuilt per edge, so the E x 32 messages never
-// exist.  While it sums s_i, the row pass also records, per (node i, channel c),
-//   cnt_i[c] = #{e in row i : pre_e[c] > 0}   and   eap_i[c][f] = sum of ea_e[f] over those edges,
-// and each edge's ReLU pattern (one 32-bit word, bit c = channel c active) in
-// TRANSPOSED order.  The backward then needs no pass over the CSR rows at all:
-//   D_i  = dS_i * cnt_i                  (elementwise)
-//   dWc  = sum_i dS_i * eap_i,  dbe = sum_i D_i
-//   D'_j = sum_{e=(i->j) active} dS_i     (transposed pass on the bits)
+// exist.  While it sums s_i, the row pass stores each edge's ReLU pattern (one
+// 32-bit word, bit c = channel c active) in CSR order, eight edges of a row per
+// 32-byte store.  The backward never recomputes pre_e:
+//   cnt_i[c] = #{e in row i : word_e bit c},  eap_i[c][f] = sum of ea_e[f] over those edges
+//   D_i  = dS_i * cnt_i,  dWc = sum_i dS_i * eap_i,  dbe = sum_i D_i
+//                                          (one CSR pass over words + edge attributes)
+//   D'_j = sum_{e=(i->j) active} dS_i     (transposed pass on the words, gathered through t_eid)
 //   dWa = D^T X, dWb = D'^T X, dX = [DU | D | D'] [Wn[:, :F]; Wa; Wb]   (MFMA)
 // and relu'(X2) is kept as one bit word per node, so dWn2 = dmean * (mask^T [X1|S2]).
 //
@@ -26,9 +26,9 @@
 //             U = one 16-byte record per edge {B row byte offset | transposed slot, ea[0..2]} (+ ea[3])
 //   backward: P = dS2 -> dX1 -> DU1 -> D'1,  Q = X1 -> X0,  R = D2 -> S1 -> D1,
 //             U = T (D'2 -> dS1) | ReLU words (transposed) | transposed CSR
-// Written once, read back much later by the same workgroup, and too big to
-// keep: S1, cnt, eap and the transposed ReLU words go to a per-graph global
-// scratch (L2-resident) and come back by bulk loads.  GEMM weights (the MFMA B
+// Written once, read back much later, and too big to keep: S1 and the ReLU
+// words go to a per-graph global scratch (L2-resident) and come back by bulk
+// loads (S1, own rows) and gathers (the words of the transposed slots).  GEMM weights (the MFMA B
 // operand) are loaded from global into registers once per phase and wave.
 //
 // Split (k = 2..4 workgroups per graph, so a small batch fills the chip):
@@ -99,12 +99,12 @@ __host__ __device__ inline VCarve vcarve(int N, int E, int Fe) {
   return c;
 }
 
-// per-graph global scratch (floats): S1 [32N] | cnt1 [32N] | cnt2 [32N] | eap1 [Fe][32N] | eap2 [Fe][32N] |
-// bt1 [E + 1] | bt2 [E + 1] (slot E of bt takes the padding lanes' stores) |
+// per-graph global scratch (floats): S1 [32N] | bt1 [E + 1] | bt2 [E + 1] (ReLU words, CSR order) |
 // split exchange: XA [32N] (B2, then dS1) | XB [32N] (dS2) | column sums [MAX_SPLIT][32]
 constexpr int MAXK = DR_VANILLA_MAX_SPLIT;
 __host__ __device__ inline int64_t vscratch_floats(int N, int E, int Fe) {
-  return (int64_t)(5 + 2 * Fe) * r4(32 * N) + 2LL * r4(E + 1) + 32 * MAXK;
+  (void)Fe;
+  return 3LL * r4(32 * N) + 2LL * r4(E + 1) + 32 * MAXK;
 }
 
 struct VGArgs {
@@ -204,9 +204,20 @@ __device__ __forceinline__ void gather_rows(float* slot, const float* g, int N, 
     *reinterpret_cast<float2*>(slot + i * LS + c) = make_float2(__uint_as_float((uint32_t)v), __uint_as_float((uint32_t)(v >> 32)));
   }
 }
-// ReLU words of the transposed slots [q0, q1) (stored sc1 by other siblings) -> LDS.
-__device__ __forceinline__ void gather_words(uint32_t* dst, const uint32_t* g, int q0, int q1) {
-  for (int q = q0 + (int)threadIdx.x; q < q1; q += NT) dst[q] = ld_sc1_u32(g + q);
+// ReLU words of the transposed slots [q0, q1) -> LDS: slot q is CSR edge teid[q]
+// (stored sc1, by any sibling); four slots per thread in flight.
+__device__ __forceinline__ void gather_words(uint32_t* dst, const uint32_t* g, const int* teid, int q0, int q1) {
+  for (int q = q0 + (int)threadIdx.x; q < q1; q += 4 * NT) {
+    int te[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) te[u] = teid[min(q + u * NT, q1 - 1)];
+    uint32_t v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = ld_sc1_u32(g + te[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (q + u * NT < q1) dst[q + u * NT] = v[u];
+  }
 }
 
 // Edge-balanced row bound of sibling r: the first row i with rp[i] + RW i >= r (E + RW N) / k
@@ -392,14 +403,15 @@ __device__ __forceinline__ float2 f2slot_sum(float2 v) {
 // of 2 edges, the pair's shorter row idling (masked) past its end.
 //   S_i = sum_{e in row i} relu(A_i + B_j + Wc ea_e),   A_i = Wa x_i + be
 // (A_i: each slot sums 16 of the K = 32 (padded) inputs, then the slots combine).
-// Also cnt_i / eap_i (see the header) and each edge's ReLU word at its
-// transposed slot (global bt).  Edge records: {byte offset of B row col | tpos << 16, ea0, ea1, ea2}.
+// Also each edge's ReLU word, CSR order (global bt): lane j < 8 of a row's
+// first edge slot keeps the word of the chunk's edge j and the eight go out as
+// one 32-byte store.  Edge records: {byte offset of B row col, ea0, ea1, ea2}.
 __device__ __forceinline__ float2 f2half_sum(float2 v) { return f2add(v, f2shfl_xor(v, 16)); }
 
 template <int FE>
 __device__ __forceinline__ void row_fwd(const int* rp, const uint4* rec, const float* ext, const float* X,
-                                        const float* Bs, float* S, float* S1g, float* cntg, float* eapg,
-                                        uint32_t* btg, const float* rpack, int N, int N_E, int r0, int r1) {
+                                        const float* Bs, float* S, float* S1g, uint32_t* btg, const float* rpack,
+                                        int N, int N_E, int r0, int r1) {
   constexpr int FA = FE > 0 ? FE : 1;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, cp = lane & 15, sl = lane >> 4, c0 = 2 * cp;
   const int es = sl & 1, hr = sl >> 1;
@@ -420,7 +432,7 @@ __device__ __forceinline__ void row_fwd(const int* rp, const uint4* rec, const f
   }
   const fl2 bev = rp2[20 * 64];
   const float2 be2 = make_float2(bev.x, bev.y);
-  const int n32 = 32 * N;
+  const int jme = cp & 7, sme = 16 * (2 * hr + (jme & 1));  // the word this lane keeps: edge jme of the chunk
   for (int i0 = r0 + 2 * wave; i0 < r1; i0 += 2 * NW) {
     const int i = i0 + hr;
     const bool rowok = i < r1;
@@ -438,9 +450,7 @@ __device__ __forceinline__ void row_fwd(const int* rp, const uint4* rec, const f
       }
     }
     a = f2add(f2half_sum(a), be2);
-    float2 acc = make_float2(0.f, 0.f), cnt = make_float2(0.f, 0.f), eap[FA];
-#pragma unroll
-    for (int f = 0; f < FA; ++f) eap[f] = make_float2(0.f, 0.f);
+    float2 acc = make_float2(0.f, 0.f);
     for (int off = 0; off < lmax; off += 8) {
       const int nch = len - off;
       // past this row's end (the pair's other row is longer): the zero padding records
@@ -453,6 +463,7 @@ __device__ __forceinline__ void row_fwd(const int* rp, const uint4* rec, const f
         e3[u] = FE > 3 ? ext[base + es + 2 * u] : 0.f;
       }
       float2 bj[4];
+      uint32_t mine = 0u;
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         bj[u] = *reinterpret_cast<const float2*>(reinterpret_cast<const char*>(Bs) + (r[u].x & 0xffffu) + 8 * cp);
@@ -468,76 +479,90 @@ __device__ __forceinline__ void row_fwd(const int* rp, const uint4* rec, const f
         const bool al = !(pre.x <= 0.f), ah = !(pre.y <= 0.f);  // relu keeps NaN (active)
         acc.x += al ? pre.x : 0.f;
         acc.y += ah ? pre.y : 0.f;
-        const float2 af = make_float2(al ? 1.f : 0.f, ah ? 1.f : 0.f);
-        cnt = f2add(cnt, af);
-#pragma unroll
-        for (int f = 0; f < FE; ++f) eap[f] = make_float2(fmaf(af.x, ev[f], eap[f].x), fmaf(af.y, ev[f], eap[f].y));
         const uint64_t blo = __ballot(al), bhi = __ballot(ah);
-        // lane 0 of the slot stores its edge's word (write-through: a sibling
-        // workgroup may read it); past the row end: slot E
-        if (cp == 0)
-          st_sc1_u32(btg + (ok ? (int)(r[u].x >> 16) : N_E),
-                     (uint32_t)((blo >> (16 * sl)) & 0xffffu) | ((uint32_t)((bhi >> (16 * sl)) & 0xffffu) << 16));
+        if ((jme >> 1) == u) mine = (uint32_t)((blo >> sme) & 0xffffu) | ((uint32_t)((bhi >> sme) & 0xffffu) << 16);
       }
+      // the chunk's words (write-through: a sibling workgroup may read them)
+      if (es == 0 && cp < 8 && cp < nch) st_sc1_u32(btg + eb + off + cp, mine);
     }
     acc = f2half_sum(acc);
-    cnt = f2half_sum(cnt);
-#pragma unroll
-    for (int f = 0; f < FE; ++f) eap[f] = f2half_sum(eap[f]);
     if (es == 0 && rowok) {
       *reinterpret_cast<float2*>(S + i * LS + c0) = acc;
       if (S1g) *reinterpret_cast<float2*>(S1g + i * 32 + c0) = acc;
-      *reinterpret_cast<float2*>(cntg + i * 32 + c0) = cnt;
-#pragma unroll
-      for (int f = 0; f < FE; ++f) *reinterpret_cast<float2*>(eapg + f * n32 + i * 32 + c0) = eap[f];
     }
   }
 }
 
 // D_i = dS_i * cnt_i (0 where no edge of row i is active) into D; per-wave
 // partials of dbe = sum_i D_i and dWc[c][f] = sum_i dS_i[c] eap_i[c][f] into red
-// [NW][32 * (1 + FE)].  Thread (slice sl = tid >> 5, channel c) takes rows sl, sl + 32, ...
+// [NW][32 * (1 + FE)].  cnt_i / eap_i come from one pass over row i's ReLU
+// words (global, CSR order) and edge attributes (the store), four edges per
+// lane in flight (lane layout of row_fwd).
 template <int FE>
-__device__ __forceinline__ void d_pass(const float* dS, float* D, const float* cntg, const float* eapg, float* red,
-                                       int N, int r0, int r1) {
+__device__ __forceinline__ void d_pass(const int* rp, const uint32_t* btg, const float* ea, const float* dS, float* D,
+                                       float* red, int r0, int r1) {
   constexpr int FA = FE > 0 ? FE : 1;
-  const int tid = threadIdx.x, c = tid & 31, sl = tid >> 5, wave = tid >> 6;
-  const int n32 = 32 * N;
-  float pbe = 0.f, pwc[FA];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, cp = lane & 15, c0 = 2 * cp;
+  const int es = (lane >> 4) & 1, hr = lane >> 5;
+  float2 pbe = make_float2(0.f, 0.f), pwc[FA];
 #pragma unroll
-  for (int f = 0; f < FA; ++f) pwc[f] = 0.f;
-  for (int i0 = r0 + sl; i0 < r1; i0 += 128) {  // 4 rows per step, their loads issued together
-    float cn[4], ep[4][FA];
+  for (int f = 0; f < FA; ++f) pwc[f] = make_float2(0.f, 0.f);
+  for (int i0 = r0 + 2 * wave; i0 < r1; i0 += 2 * NW) {
+    const int i = i0 + hr;
+    const bool rowok = i < r1;
+    const int ii = rowok ? i : i0;
+    const int eb = rp[ii], len = rowok ? rp[ii + 1] - eb : 0;
+    const int lmax = max(len, __shfl_xor(len, 32, 64));
+    float2 cnt = make_float2(0.f, 0.f), eap[FA];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int i = i0 + 32 * q;
-      const bool ok = i < r1;
-      const int ii = ok ? i : r0;
-      cn[q] = cntg[ii * 32 + c];
+    for (int f = 0; f < FA; ++f) eap[f] = make_float2(0.f, 0.f);
+    for (int off = 0; off < lmax; off += 8) {
+      const int nch = len - off;
+      uint32_t wd[4];
+      float ev[4][FA];
 #pragma unroll
-      for (int f = 0; f < FE; ++f) ep[q][f] = eapg[f * n32 + ii * 32 + c];
-    }
+      for (int u = 0; u < 4; ++u) {
+        const bool ok = es + 2 * u < nch;
+        const int e = ok ? eb + off + es + 2 * u : 0;  // (lmax > 0: the graph has an edge 0)
+        wd[u] = btg[e];
+        wd[u] = ok ? wd[u] : 0u;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int i = i0 + 32 * q;
-      if (i < r1) {  // (cn / ep of rows >= r1 are never used)
-        const float ds = dS[i * LS + c];
-        const float d = cn[q] != 0.f ? ds * cn[q] : 0.f;
-        D[i * LS + c] = d;
-        pbe += d;
+        for (int f = 0; f < FE; ++f) ev[u][f] = ea[(int64_t)e * FE + f];
+      }
 #pragma unroll
-        for (int f = 0; f < FE; ++f) pwc[f] += cn[q] != 0.f ? ds * ep[q][f] : 0.f;
+      for (int u = 0; u < 4; ++u) {
+        const float bl = ((wd[u] >> cp) & 1u) ? 1.f : 0.f, bh = ((wd[u] >> (16 + cp)) & 1u) ? 1.f : 0.f;
+        cnt = f2add(cnt, make_float2(bl, bh));
+#pragma unroll
+        for (int f = 0; f < FE; ++f) eap[f] = make_float2(fmaf(bl, ev[u][f], eap[f].x), fmaf(bh, ev[u][f], eap[f].y));
       }
     }
+    cnt = f2half_sum(cnt);
+#pragma unroll
+    for (int f = 0; f < FE; ++f) eap[f] = f2half_sum(eap[f]);
+    if (es == 0 && rowok) {
+      const float2 ds = *reinterpret_cast<const float2*>(dS + i * LS + c0);
+      const float2 d = make_float2(cnt.x != 0.f ? ds.x * cnt.x : 0.f, cnt.y != 0.f ? ds.y * cnt.y : 0.f);
+      *reinterpret_cast<float2*>(D + i * LS + c0) = d;
+      pbe = f2add(pbe, d);
+#pragma unroll
+      for (int f = 0; f < FE; ++f)
+        pwc[f] = f2add(pwc[f], make_float2(cnt.x != 0.f ? ds.x * eap[f].x : 0.f, cnt.y != 0.f ? ds.y * eap[f].y : 0.f));
+    }
   }
-  pbe += __shfl_xor(pbe, 32, 64);
+  // the wave's two rows (lanes cp and cp + 32, edge slot 0)
+  pbe = f2add(pbe, f2shfl_xor(pbe, 32));
 #pragma unroll
-  for (int f = 0; f < FE; ++f) pwc[f] += __shfl_xor(pwc[f], 32, 64);
+  for (int f = 0; f < FE; ++f) pwc[f] = f2add(pwc[f], f2shfl_xor(pwc[f], 32));
   constexpr int RW = 32 * (1 + FE);
-  if ((tid & 63) < 32) {
-    red[wave * RW + c] = pbe;
+  if (lane < 16) {
+    red[wave * RW + c0] = pbe.x;
+    red[wave * RW + c0 + 1] = pbe.y;
 #pragma unroll
-    for (int f = 0; f < FE; ++f) red[wave * RW + 32 + c * FE + f] = pwc[f];
+    for (int f = 0; f < FE; ++f) {
+      red[wave * RW + 32 + c0 * FE + f] = pwc[f].x;
+      red[wave * RW + 32 + (c0 + 1) * FE + f] = pwc[f].y;
+    }
   }
 }
 
@@ -646,15 +671,12 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   float* scr = a.scr + a.scr_off[b];
   const int n32 = r4(32 * N);
   float* S1g = scr;
-  float* cnt1 = S1g + n32;
-  float* cnt2 = cnt1 + n32;
-  float* eap1 = cnt2 + n32;
-  float* eap2 = eap1 + Fe * n32;
-  uint32_t* bt1g = reinterpret_cast<uint32_t*>(eap2 + Fe * n32);
+  uint32_t* bt1g = reinterpret_cast<uint32_t*>(S1g + n32);
   uint32_t* bt2g = bt1g + r4(E + 1);
   float* XA = reinterpret_cast<float*>(bt2g + r4(E + 1));  // B2, then dS1 rows (split)
   float* XB = XA + n32;                                    // dS2 rows (split)
   float* csum = XB + n32;                                  // [k][32] column sums of X2 (split)
+  const int* teid = s.t_eid + d.col0;                      // transposed slot -> CSR edge
   uint32_t* ctr = a.sync + 2 * b;
   uint32_t* tflag = a.sync + 2 * a.B;
   const bool split = k > 1;
@@ -670,19 +692,16 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   dma_words<NT>(srp, s.rowptr + d.node0 + g, N + 1);
   {
     const uint16_t* gcol = s.col + d.col0;
-    const int* teid = s.t_eid + d.col0;
-    uint16_t* r16 = reinterpret_cast<uint16_t*>(rec);
+    uint32_t* r32 = reinterpret_cast<uint32_t*>(rec);
     float* rf = reinterpret_cast<float*>(rec);
     for (int e0 = tid; e0 < E; e0 += 4 * NT) {  // 4 edges per thread and step, loads first
       uint32_t cl[4];
-      int te[4];
       float ev[4][MAXFE];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int e = e0 + u * NT;
         const int ec = e < E ? e : 0;  // E >= 1 here (the loop runs only then)
         cl[u] = gcol[ec];
-        te[u] = teid[ec];
 #pragma unroll
         for (int f = 0; f < MAXFE; ++f) ev[u][f] = f < Fe ? ea[(int64_t)ec * FeS + f] : 0.f;
       }
@@ -690,8 +709,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
       for (int u = 0; u < 4; ++u) {
         const int e = e0 + u * NT;
         if (e < E) {
-          r16[8 * e] = (uint16_t)(cl[u] * (LS * 4));  // byte offset of row col in a slot
-          r16[8 * te[u] + 1] = (uint16_t)e;  // transposed slot e holds CSR edge te[u]
+          r32[4 * e] = cl[u] * (LS * 4);  // byte offset of row col in a slot
 #pragma unroll
           for (int f = 0; f < 3; ++f) rf[4 * e + 1 + f] = ev[u][f];
           if (Fe > 3) ext[e] = ev[u][3];
@@ -721,7 +739,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
           [&](int i, int n, float v, float) { Q[i * LS + n] = v; });
   __syncthreads();
   VSTAMP(2);
-  row_fwd<FE>(srp, rec, ext, P, Q, R, S1g, cnt1, eap1, bt1g, a.wpack + ROW_BASE, N, E, r0, r1);
+  row_fwd<FE>(srp, rec, ext, P, Q, R, S1g, bt1g, a.wpack + ROW_BASE, N, E, r0, r1);
   __syncthreads();
   VSTAMP(3);
   // X1 = relu([X0 | S1] Wn1^T + bn1) -> Q (pad columns 0), own rows
@@ -743,14 +761,14 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
     __syncthreads();
   }
   VSTAMP(5);
-  row_fwd<FE>(srp, rec, ext, Q, P, R, nullptr, cnt2, eap2, bt2g, a.wpack + ROW_BASE + ROWPACK, N, E, r0, r1);
-  wait_vm();  // ReLU words, cnt, eap of both layers stored before anyone reads them back
+  row_fwd<FE>(srp, rec, ext, Q, P, R, nullptr, bt2g, a.wpack + ROW_BASE + ROWPACK, N, E, r0, r1);
+  wait_vm();  // the ReLU words of both layers stored before anyone reads them back
   __syncthreads();
   VSTAMP(6);
   // the records are dead: the backward's transposed CSR and layer-2 ReLU words
   // land in U while the forward finishes
   if (bwd) {
-    if (!split) dma_words<NT>(bt, bt2g, E);  // (split: after hand-off 2, sc1)
+    if (!split) gather_words(bt, bt2g, teid, 0, E);  // (split: after hand-off 2)
     dma_words<NT>(strp, s.t_rowptr + d.node0 + g, N + 1);
     dma_x4<NT>(stcol, s.t_col + d.col0, (E + 7) / 8);
   }
@@ -790,7 +808,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
       for (int q = 1; q < k; ++q) t += ld_sc1(csum + q * 32 + tid);
       sg[tid] = tid < F ? t / (float)N : 0.f;
     }
-    if (bwd) gather_words(bt, bt2g, strp[r0], strp[r1]);  // (strp landed: waited at the hand-off)
+    if (bwd) gather_words(bt, bt2g, teid, strp[r0], strp[r1]);  // (strp landed: waited at the hand-off)
     if (!bwd) sib_exit(ctr, k);
   }
   __syncthreads();
@@ -909,7 +927,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   }
   VSTAMP(10);
   // D2 = dS2 * cnt2 -> R (S2 is dead), dbe2 / dWc2 partials in T
-  d_pass<FE>(P, R, cnt2, eap2, T, N, r0, r1);
+  d_pass<FE>(srp, bt2g, ea, P, R, T, r0, r1);
   wait_vm();  // bt2 and the transposed CSR have landed in U
   __syncthreads();
   d_pass_sum<FE>(T, slab + LG, KE, F);
@@ -943,8 +961,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   // bulk DMA (own rows), landing while dS1 = DU1 Wn1[:, F:] -> T runs
   dma_x4<NT>(Q + r0 * XS, X0 + (int64_t)r0 * XS, nown * XS / 4);
   dma_x4<NT>(R + r0 * 32, S1g + r0 * 32, nown * 8);
-  if (split) gather_words(bt, bt1g, strp[r0], strp[r1]);
-  else dma_words<NT>(bt, bt1g, E);
+  gather_words(bt, bt1g, teid, strp[r0], strp[r1]);
   mm_w<1>(nown, [&](int i, int n) { return P[(r0 + i) * LS + n]; },
           a.wpack + op_base(OP_DS1), [&](int) -> const float* { return nullptr; },
           [&](int i, int c, float v, float) { T[(r0 + i) * LS + c] = v; });
@@ -974,7 +991,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   __syncthreads();
   VSTAMP(15);
   // D1 = dS1 * cnt1 -> R (S1 is dead), partials in P (DU1 is dead)
-  d_pass<FE>(T, R, cnt1, eap1, P, N, r0, r1);
+  d_pass<FE>(srp, bt1g, ea, T, R, P, r0, r1);
   __syncthreads();
   d_pass_sum<FE>(P, slab, KE, F);
   __syncthreads();
