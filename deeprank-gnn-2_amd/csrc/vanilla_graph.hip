@@ -68,7 +68,7 @@ struct VCarve {
 };
 
 __host__ __device__ inline int vslot(int N, int Fe) {
-  const int red = NW * 32 * (1 + Fe);  // the D pass partials live in P or T
+  const int red = NW * 32 * (1 + Fe) + 1024;  // the D pass partials + its edge buffer (>= 1024 words) live in P or T
   return imax(r4(N * LS), imax(red, 1024));
 }
 
@@ -496,65 +496,125 @@ __device__ __forceinline__ void row_fwd(const int* rp, const uint4* rec, const f
 // D_i = dS_i * cnt_i (0 where no edge of row i is active) into D; per-wave
 // partials of dbe = sum_i D_i and dWc[c][f] = sum_i dS_i[c] eap_i[c][f] into red
 // [NW][32 * (1 + FE)].  cnt_i / eap_i come from one pass over row i's ReLU
-// words (global, CSR order) and edge attributes (the store), four edges per
-// lane in flight (lane layout of row_fwd).
+// words (global, CSR order) and edge attributes (the store).  The own rows'
+// edges are contiguous, so they are copied to LDS behind red in segments of
+// whole rows that fit (one bulk copy, all loads in flight: one memory round
+// trip per segment, a single segment at k = 4), then each row is read from
+// there (lane layout of row_fwd).  A row longer than the whole buffer reads
+// global memory directly.
 template <int FE>
 __device__ __forceinline__ void d_pass(const int* rp, const uint32_t* btg, const float* ea, const float* dS, float* D,
-                                       float* red, int r0, int r1) {
-  constexpr int FA = FE > 0 ? FE : 1;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, cp = lane & 15, c0 = 2 * cp;
+                                       float* red, int N, int r0, int r1, int64_t* stp = nullptr) {
+  constexpr int FA = FE > 0 ? FE : 1, RW = 32 * (1 + FE);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, cp = lane & 15, c0 = 2 * cp;
   const int es = (lane >> 4) & 1, hr = lane >> 5;
+  constexpr int RS = FE <= 3 ? 4 : 8;  // one record per edge: {word, ea[0..FE)} (one 16-byte read for FE <= 3)
+  float* buf = red + NW * RW;
+  const int cap = (vslot(N, FE) - NW * RW) / RS;  // edges per segment
   float2 pbe = make_float2(0.f, 0.f), pwc[FA];
 #pragma unroll
   for (int f = 0; f < FA; ++f) pwc[f] = make_float2(0.f, 0.f);
-  for (int i0 = r0 + 2 * wave; i0 < r1; i0 += 2 * NW) {
-    const int i = i0 + hr;
-    const bool rowok = i < r1;
-    const int ii = rowok ? i : i0;
-    const int eb = rp[ii], len = rowok ? rp[ii + 1] - eb : 0;
-    const int lmax = max(len, __shfl_xor(len, 32, 64));
-    float2 cnt = make_float2(0.f, 0.f), eap[FA];
+  for (int s0 = r0; s0 < r1;) {
+    // the segment [s0, s1): whole rows whose edges fit the buffer (uniform)
+    int lo = s0 + 1, hi = r1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (rp[mid] - rp[s0] <= cap) lo = mid;
+      else hi = mid - 1;
+    }
+    const int s1 = lo, E0 = rp[s0], ne = rp[s1] - E0;
+    const bool inbuf = ne <= cap;
+    if (inbuf) {  // words, then attributes (AoS in HBM, as the records want them)
+      const int tot = ne * (1 + FE);
+      for (int q0 = tid; q0 < tot; q0 += 4 * NT) {
+        float v[4];
 #pragma unroll
-    for (int f = 0; f < FA; ++f) eap[f] = make_float2(0.f, 0.f);
-    for (int off = 0; off < lmax; off += 8) {
-      const int nch = len - off;
-      uint32_t wd[4];
-      float ev[4][FA];
+        for (int t = 0; t < 4; ++t) {
+          const int q = min(q0 + t * NT, tot - 1);
+          v[t] = q < ne ? __uint_as_float(btg[E0 + q]) : (FE > 0 ? ea[(int64_t)E0 * FE + q - ne] : 0.f);
+        }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const bool ok = es + 2 * u < nch;
-        const int e = ok ? eb + off + es + 2 * u : 0;  // (lmax > 0: the graph has an edge 0)
-        wd[u] = btg[e];
-        wd[u] = ok ? wd[u] : 0u;
-#pragma unroll
-        for (int f = 0; f < FE; ++f) ev[u][f] = ea[(int64_t)e * FE + f];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float bl = ((wd[u] >> cp) & 1u) ? 1.f : 0.f, bh = ((wd[u] >> (16 + cp)) & 1u) ? 1.f : 0.f;
-        cnt = f2add(cnt, make_float2(bl, bh));
-#pragma unroll
-        for (int f = 0; f < FE; ++f) eap[f] = make_float2(fmaf(bl, ev[u][f], eap[f].x), fmaf(bh, ev[u][f], eap[f].y));
+        for (int t = 0; t < 4; ++t) {
+          const int q = q0 + t * NT;
+          if (q < tot) buf[q < ne ? q * RS : ((q - ne) / FA) * RS + 1 + (q - ne) % FA] = v[t];
+        }
       }
     }
-    cnt = f2half_sum(cnt);
+    __syncthreads();
+#ifdef DR_STAMPS
+    if (stp && tid == 0 && s0 == r0) stp[23] = __builtin_amdgcn_s_memtime();
+#endif
+    // (two instantiations, so LDS and global reads stay ds_ / global_ loads)
+    auto rows = [&](auto rec) {
+      for (int i0 = s0 + 2 * wave; i0 < s1; i0 += 2 * NW) {
+        const int i = i0 + hr;
+        const bool rowok = i < s1;
+        const int ii = rowok ? i : i0;
+        const int eb = rp[ii], len = rowok ? rp[ii + 1] - eb : 0;
+        const int lmax = max(len, __shfl_xor(len, 32, 64));
+        float2 cnt = make_float2(0.f, 0.f), eap[FA];
 #pragma unroll
-    for (int f = 0; f < FE; ++f) eap[f] = f2half_sum(eap[f]);
-    if (es == 0 && rowok) {
-      const float2 ds = *reinterpret_cast<const float2*>(dS + i * LS + c0);
-      const float2 d = make_float2(cnt.x != 0.f ? ds.x * cnt.x : 0.f, cnt.y != 0.f ? ds.y * cnt.y : 0.f);
-      *reinterpret_cast<float2*>(D + i * LS + c0) = d;
-      pbe = f2add(pbe, d);
+        for (int f = 0; f < FA; ++f) eap[f] = make_float2(0.f, 0.f);
+        for (int off = 0; off < lmax; off += 8) {
+          const int nch = len - off;
+          uint32_t wd[4];
+          float ev[4][FA];
 #pragma unroll
-      for (int f = 0; f < FE; ++f)
-        pwc[f] = f2add(pwc[f], make_float2(cnt.x != 0.f ? ds.x * eap[f].x : 0.f, cnt.y != 0.f ? ds.y * eap[f].y : 0.f));
-    }
+          for (int u = 0; u < 4; ++u) {
+            const bool ok = es + 2 * u < nch;
+            const int e = ok ? eb + off + es + 2 * u : E0;  // masked: a valid edge, word forced to 0
+            rec(e, wd[u], ev[u]);
+            wd[u] = ok ? wd[u] : 0u;
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float bl = ((wd[u] >> cp) & 1u) ? 1.f : 0.f, bh = ((wd[u] >> (16 + cp)) & 1u) ? 1.f : 0.f;
+            cnt = f2add(cnt, make_float2(bl, bh));
+#pragma unroll
+            for (int f = 0; f < FE; ++f) eap[f] = make_float2(fmaf(bl, ev[u][f], eap[f].x), fmaf(bh, ev[u][f], eap[f].y));
+          }
+        }
+        cnt = f2half_sum(cnt);
+    #pragma unroll
+        for (int f = 0; f < FE; ++f) eap[f] = f2half_sum(eap[f]);
+        if (es == 0 && rowok) {
+          const float2 ds = *reinterpret_cast<const float2*>(dS + i * LS + c0);
+          const float2 d = make_float2(cnt.x != 0.f ? ds.x * cnt.x : 0.f, cnt.y != 0.f ? ds.y * cnt.y : 0.f);
+          *reinterpret_cast<float2*>(D + i * LS + c0) = d;
+          pbe = f2add(pbe, d);
+    #pragma unroll
+          for (int f = 0; f < FE; ++f)
+            pwc[f] = f2add(pwc[f], make_float2(cnt.x != 0.f ? ds.x * eap[f].x : 0.f, cnt.y != 0.f ? ds.y * eap[f].y : 0.f));
+        }
+      }
+    };
+    typedef __attribute__((address_space(1))) const uint32_t gcu32;
+    typedef __attribute__((address_space(1))) const float gcf;
+    if (inbuf)
+      rows([&](int e, uint32_t& w, float* v) {
+        const float4 r = *reinterpret_cast<const float4*>(buf + (e - E0) * RS);
+        w = __float_as_uint(r.x);
+        if (FE > 0) v[0] = r.y;
+        if (FE > 1) v[1] = r.z;
+        if (FE > 2) v[2] = r.w;
+        if (FE > 3) v[3] = buf[(e - E0) * RS + 4];
+      });
+    else
+      rows([&](int e, uint32_t& w, float* v) {
+        w = ((gcu32*)btg)[e];
+#pragma unroll
+        for (int f = 0; f < FE; ++f) v[f] = ((gcf*)ea)[(int64_t)e * FE + f];
+      });
+    __syncthreads();  // (the next segment overwrites the buffer)
+#ifdef DR_STAMPS
+    if (stp && tid == 0 && s0 == r0) stp[24] = __builtin_amdgcn_s_memtime();
+#endif
+    s0 = s1;
   }
   // the wave's two rows (lanes cp and cp + 32, edge slot 0)
   pbe = f2add(pbe, f2shfl_xor(pbe, 32));
 #pragma unroll
   for (int f = 0; f < FE; ++f) pwc[f] = f2add(pwc[f], f2shfl_xor(pwc[f], 32));
-  constexpr int RW = 32 * (1 + FE);
   if (lane < 16) {
     red[wave * RW + c0] = pbe.x;
     red[wave * RW + c0 + 1] = pbe.y;
@@ -927,7 +987,13 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   }
   VSTAMP(10);
   // D2 = dS2 * cnt2 -> R (S2 is dead), dbe2 / dWc2 partials in T
-  d_pass<FE>(srp, bt2g, ea, P, R, T, r0, r1);
+  d_pass<FE>(srp, bt2g, ea, P, R, T, N, r0, r1,
+#ifdef DR_STAMPS
+             a.p.stamps ? a.p.stamps + ((int64_t)b * a.k + rk) * 32 : nullptr
+#else
+             nullptr
+#endif
+  );
   wait_vm();  // bt2 and the transposed CSR have landed in U
   __syncthreads();
   d_pass_sum<FE>(T, slab + LG, KE, F);
@@ -991,7 +1057,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   __syncthreads();
   VSTAMP(15);
   // D1 = dS1 * cnt1 -> R (S1 is dead), partials in P (DU1 is dead)
-  d_pass<FE>(srp, bt1g, ea, T, R, P, r0, r1);
+  d_pass<FE>(srp, bt1g, ea, T, R, P, N, r0, r1);
   __syncthreads();
   d_pass_sum<FE>(P, slab, KE, F);
   __syncthreads();

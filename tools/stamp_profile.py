@@ -150,6 +150,8 @@ def vanilla(dev, B):
     if k > 1:  # hand-off waits: entry stamp (19..22) -> the next phase stamp
         for name, e, x in (("hand-off 1 (B2)", 19, 5), ("hand-off 2 (col sums)", 20, 8), ("hand-off 3 (dS2)", 21, 10), ("hand-off 4 (dS1)", 22, 14)):
             print(f"  {name:22s} {np.median(a[:, :, x] - a[:, :, e]):8.0f} cyc (wait + gather)")
+        if np.median(a[:, :, 24]) > 0:  # d_pass stamps (layer 2): copy, rows of the first segment
+            print(f"  D2 copy {np.median(a[:, :, 23] - a[:, :, 10]):8.0f}  rows {np.median(a[:, :, 24] - a[:, :, 23]):8.0f}  rest {np.median(a[:, :, 11] - a[:, :, 24]):8.0f} cyc")
         span = a[:, :, len(PHASES_V)] - a[:, :, 0]
         print(f"  workgroup span min/median/max {span.min():.0f} / {np.median(span):.0f} / {span.max():.0f} cyc")
 
