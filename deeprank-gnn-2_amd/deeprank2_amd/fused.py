@@ -102,10 +102,9 @@ class BatchHandle:
         return sc
 
     def vanilla_fused_scratch(self):
-        """Per-graph global scratch of dr_vanilla_fused_pass (S1, per-(node,
-        channel) active-edge counts and edge-attribute sums of both layers, the
-        transposed edge ReLU words, the split's exchange rows), each slot's
-        float offset into it, and the split's arrival counters."""
+        """Per-graph global scratch of dr_vanilla_fused_pass (S1, the edge ReLU
+        words of both layers in CSR order, the split's exchange rows), each
+        slot's float offset into it, and the split's arrival counters."""
         sc = self._lds.get("vanilla_fused_scratch")
         if sc is None:
             idx = self.gids_host.astype(np.int64)
@@ -345,11 +344,12 @@ class FusedSpec:
 
 def vanilla_fused_scratch_floats(n, e, fe):
     """Mirror of dr_vanilla_fused_scratch_floats (vanilla_graph.hip), vectorised
-    over graphs: S1, cnt1, cnt2 (32N each), eap1, eap2 (32N*Fe each), two ReLU
-    word arrays (E + 1 each), the split's exchange rows XA, XB (32N each) and
-    column sums (4 x 32), every part rounded up to 16 bytes."""
+    over graphs: S1 (32N), two ReLU word arrays (E + 1 each, CSR order), the
+    split's exchange rows XA, XB (32N each) and column sums (4 x 32), every part
+    rounded up to 16 bytes (fe: no per-edge-feature part since r03)."""
     r4 = lambda v: (np.asarray(v, dtype=np.int64) + 3) & ~3  # noqa: E731
-    return (5 + 2 * fe) * r4(32 * np.asarray(n, dtype=np.int64)) + 2 * r4(np.asarray(e, dtype=np.int64) + 1) + 32 * 4
+    del fe
+    return 3 * r4(32 * np.asarray(n, dtype=np.int64)) + 2 * r4(np.asarray(e, dtype=np.int64) + 1) + 32 * 4
 
 
 def make_pass(out_dim, flags, *, dropout: Dropout | None = None, dout=None, loss_kind=_lib.DR_LOSS_NONE, loss_scale=1.0, class_w=None, out=None, loss_per_graph=None, slab=None, head=None, stamps=None, step_counter=None, fault=None, spin_limit=0):
