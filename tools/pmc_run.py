@@ -1,6 +1,6 @@
 """Workload for rocprofv3 --pmc passes: eager GINet training steps (config 2).
 
-    rocprofv3 --pmc <counters> -f csv -d <dir> -- python3 tools/pmc_run.py [steps] [ginet|vanilla|foutnet|sgat]
+    rocprofv3 --pmc <counters> -f csv -d <dir> -- python3 tools/pmc_run.py [steps] [ginet|vanilla|foutnet|sgat][_atom]
 """
 
 from __future__ import annotations
@@ -26,10 +26,14 @@ def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 40
     dev = torch.device("cuda:0")
     which = sys.argv[2] if len(sys.argv) > 2 else "ginet"
-    packed = pack_graphs(records(make_dataset(64 * 16, seed=1000), 1 if which == "sgat" else 3))
+    atom = which.endswith("_atom")  # B=32 atom-level graphs (the Vanilla pipeline / large paths)
+    which = which.removesuffix("_atom")
+    B, nb = (32, 4) if atom else (64, 16)
+    fam = {"n_lo": 2700, "n_hi": 3300, "mean_degree": 16.7, "k_lo": 8, "k_hi": 32} if atom else {}
+    packed = pack_graphs(records(make_dataset(B * nb, seed=1000, **fam), 1 if which == "sgat" else 3))
     store = GraphStore(packed, dev)
     order = np.random.default_rng(0).permutation(packed.n_graphs).astype(np.int32)
-    hs = [BatchHandle(store, order[i * 64:(i + 1) * 64]) for i in range(16)]
+    hs = [BatchHandle(store, order[i * B:(i + 1) * B]) for i in range(nb)]
     torch.manual_seed(1234)
     if which in ("foutnet", "sgat"):
         from deeprank2_amd.neuralnets.gnn import foutnet, sgat  # noqa: PLC0415
@@ -39,7 +43,7 @@ def main():
         model = (VanillaNetwork if which == "vanilla" else GINet)(30, 1, 3).to(dev).train()
     step = GINetTrainStep(model)
     for i in range(steps):
-        step.step(hs[i % 16])
+        step.step(hs[i % nb])
     torch.cuda.synchronize()
     print("alg_bytes_per_launch", np.mean([__import__("bench").algorithmic_bytes(packed, h.gids_host, which) for h in hs]))
 
