@@ -321,32 +321,30 @@ __global__ void __launch_bounds__(RB) vb_edge_bwd8(VA a, int l) {
 // One workgroup per tile of consecutive rows of one graph.  The tile's halo --
 // the distinct neighbours of its rows, out- and in-edges -- is staged in LDS
 // once (B rows in the forward, dS rows in the backward: one 128-byte row each,
-// coalesced), together with the tile's edge attributes, halo-local column ids
-// and (backward) ReLU words, so the per-edge work of vb_edge_fwd8 / vb_edge_bwd8
-// reads LDS instead of gathering a 128-byte row from L2/HBM per edge.  Rows are
-// taken in the same lane layout (32 channels per row, two rows per wave) and
-// every sum runs in the same order: results are bit-identical to the untiled
-// kernels.  LDS (floats): halo rows [halo_max][32] | edge attributes
-// [edges][FeS] | words [edges] | column ids (uint16) [edges] (+ transposed).
-struct TileCarve {
-  int rows, ea, words, wt, lc, ltc, total;
+// coalesced), together with one record per edge, so the per-edge work of
+// vb_edge_fwd8 / vb_edge_bwd8 reads LDS instead of gathering a 128-byte row
+// from L2/HBM per edge, and an edge's scalars are ONE broadcast LDS read:
+//   forward CSR record   {halo-local column, ea[0..3)}      (16 bytes; Fe = 4: 32)
+//   backward CSR record  {ReLU word, ea[0..3)}              (16 bytes; Fe = 4: 32)
+//   backward transposed  {halo-local column, ReLU word}     (8 bytes)
+// Rows are taken in the same lane layout (32 channels per row, eight rows per
+// workgroup) and every sum runs in the same order: results are bit-identical
+// to the untiled kernels.  LDS (floats): halo rows [halo_max][32] | CSR
+// records [edges][RS] | (backward) transposed records [tedges][2].
+template <int FE>
+struct TileRec {
+  static constexpr int RS = FE <= 3 ? 4 : 8;  // floats per CSR record
 };
-__host__ __device__ inline TileCarve tile_carve(int hmax, int emax, int tmax, int FeS, bool bwd) {
+struct TileCarve {
+  int rows, rec, trec, total;
+};
+__host__ __device__ inline TileCarve tile_carve(int hmax, int emax, int tmax, int Fe, bool bwd) {
   TileCarve c;
-  int o = 0;
-  c.rows = o;
-  o += hmax * 32;
-  c.ea = o;
-  o += r4(emax * FeS);
-  c.words = o;  // backward: the tile's CSR-order words
-  o += bwd ? r4(emax) : 0;
-  c.wt = o;  // backward: the tile's transposed-order words
-  o += bwd ? r4(tmax) : 0;
-  c.lc = o;
-  o += bwd ? 0 : r4((emax + 1) / 2);
-  c.ltc = o;
-  o += bwd ? r4((tmax + 1) / 2) : 0;
-  c.total = o;
+  const int RS = Fe <= 3 ? 4 : 8;
+  c.rows = 0;
+  c.rec = hmax * 32;
+  c.trec = c.rec + emax * RS;
+  c.total = c.trec + (bwd ? 2 * tmax : 0);
   return c;
 }
 
@@ -356,6 +354,27 @@ __device__ __forceinline__ void stage_halo(float* dst, const float* g32, const i
     const int h = p >> 3, q = (p & 7) * 4;
     *reinterpret_cast<float4*>(dst + h * 32 + q) = *reinterpret_cast<const float4*>(g32 + (int64_t)ids[h] * 32 + q);
   }
+}
+
+// edge e's record {head, ea[0..FE)} -> LDS (RS floats); head: a column id or a word
+template <int FE>
+__device__ __forceinline__ void put_rec(float* rec, int e, uint32_t head, const float* ea_e) {
+  constexpr int RS = TileRec<FE>::RS;
+  float v[4] = {__uint_as_float(head), 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int f = 0; f < (FE < 3 ? FE : 3); ++f) v[1 + f] = ea_e[f];
+  *reinterpret_cast<float4*>(rec + e * RS) = make_float4(v[0], v[1], v[2], v[3]);
+  if (FE > 3) rec[e * RS + 4] = ea_e[3];
+}
+template <int FE>
+__device__ __forceinline__ uint32_t get_rec(const float* rec, int e, float (&ev)[FE > 0 ? FE : 1]) {
+  constexpr int RS = TileRec<FE>::RS;
+  const float4 r = *reinterpret_cast<const float4*>(rec + e * RS);
+  if (FE > 0) ev[0] = r.y;
+  if (FE > 1) ev[1 < FE ? 1 : 0] = r.z;
+  if (FE > 2) ev[2 < FE ? 2 : 0] = r.w;
+  if (FE > 3) ev[3 < FE ? 3 : 0] = rec[e * RS + 4];
+  return __float_as_uint(r.x);
 }
 
 template <int FE>
@@ -372,16 +391,14 @@ __global__ void __launch_bounds__(RB) vb_edge_fwd_tile(VA a, int l) {
   const int* rp = a.s.rowptr + d.node0 + d.gid;
   const int i0 = (int)(rt0 - g0), e0 = rp[i0], ne = rp[(int)(rt1 - g0)] - e0;
   const int h0 = a.ws.halo_off[t], H = a.ws.halo_off[t + 1] - h0;
-  const TileCarve tc = tile_carve(a.ws.halo_max, a.ws.tile_edges_max, 0, FeS, false);
+  const TileCarve tc = tile_carve(a.ws.halo_max, a.ws.tile_edges_max, 0, FE, false);
   float* sB = lds + tc.rows;
-  float* sE = lds + tc.ea;
-  uint16_t* sC = reinterpret_cast<uint16_t*>(lds + tc.lc);
+  float* sR = lds + tc.rec;
   stage_halo(sB, L.bm + g0 * 32, a.ws.halo_ids + h0, H);
   {
     const float* ea = a.s.ea + (d.col0 + e0) * FeS;
-    for (int p = tid; p < ne * FeS; p += RB) sE[p] = ea[p];
     const uint16_t* lc = a.ws.lcol + a.ws.lcol_off[t];
-    for (int p = tid; p < ne; p += RB) sC[p] = lc[p];
+    for (int p = tid; p < ne; p += RB) put_rec<FE>(sR, p, lc[p], ea + (int64_t)p * FeS);
   }
   float wcr[FA];
 #pragma unroll
@@ -397,14 +414,10 @@ __global__ void __launch_bounds__(RB) vb_edge_fwd_tile(VA a, int l) {
     int e = eb;
     auto group = [&](auto un) {
       constexpr int U = decltype(un)::value;
-      int j[U];
+      uint32_t j[U];
       float ev[U][FA], q[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) j[u] = sC[e + u];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int f = 0; f < FE; ++f) ev[u][f] = sE[(e + u) * FeS + f];
+      for (int u = 0; u < U; ++u) j[u] = get_rec<FE>(sR, e + u, ev[u]);
 #pragma unroll
       for (int u = 0; u < U; ++u) q[u] = sB[j[u] * 32 + c];
       uint32_t mine = 0u;  // lane c < U keeps word c: one contiguous store per group
@@ -444,24 +457,19 @@ __global__ void __launch_bounds__(RB) vb_edge_bwd_tile(VA a, int l) {
   const int i0 = (int)(rt0 - g0), i1 = (int)(rt1 - g0);
   const int e0 = rp[i0], ne = rp[i1] - e0, q0 = trp[i0], nq = trp[i1] - q0;
   const int h0 = a.ws.halo_off[t], H = a.ws.halo_off[t + 1] - h0;
-  const TileCarve tc = tile_carve(a.ws.halo_max, a.ws.tile_edges_max, a.ws.tile_tedges_max, FeS, true);
+  const TileCarve tc = tile_carve(a.ws.halo_max, a.ws.tile_edges_max, a.ws.tile_tedges_max, FE, true);
   float* sD = lds + tc.rows;
-  float* sE = lds + tc.ea;
-  uint32_t* sW = reinterpret_cast<uint32_t*>(lds + tc.words);
-  uint32_t* sWt = reinterpret_cast<uint32_t*>(lds + tc.wt);
-  uint16_t* sT = reinterpret_cast<uint16_t*>(lds + tc.ltc);
+  float* sR = lds + tc.rec;
+  uint2* sTR = reinterpret_cast<uint2*>(lds + tc.trec);
   const uint32_t* words = a.ws.relu_words + (int64_t)(l - 1) * a.ws.edge0[a.B] + a.ws.edge0[b];
   stage_halo(sD, DS + g0 * 32, a.ws.halo_ids + h0, H);
   {
     const float* ea = a.s.ea + (d.col0 + e0) * FeS;
-    for (int p = tid; p < ne * FeS; p += RB) sE[p] = ea[p];
-    for (int p = tid; p < ne; p += RB) sW[p] = words[e0 + p];
+    for (int p = tid; p < ne; p += RB) put_rec<FE>(sR, p, words[e0 + p], ea + (int64_t)p * FeS);
     const uint16_t* lt = a.ws.ltcol + a.ws.ltcol_off[t];
     const int* teid = a.s.t_eid + d.col0;  // transposed slot -> CSR slot
-    for (int p = tid; p < nq; p += RB) {
-      sT[p] = lt[p];
-      sWt[p] = words[teid[q0 + p]];  // gathered while staging: no dependent loads in the row loop
-    }
+    for (int p = tid; p < nq; p += RB)
+      sTR[p] = make_uint2(lt[p], words[teid[q0 + p]]);  // gathered while staging: no dependent loads in the row loop
   }
   __syncthreads();
   for (int64_t r = rt0 + (tid >> 5); r < rt1; r += RB / 32) {
@@ -477,11 +485,7 @@ __global__ void __launch_bounds__(RB) vb_edge_bwd_tile(VA a, int l) {
       uint32_t wv[8];
       float ev[8][FA];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) wv[u] = sW[e + u];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-#pragma unroll
-        for (int f = 0; f < FE; ++f) ev[u][f] = sE[(e + u) * FeS + f];
+      for (int u = 0; u < 8; ++u) wv[u] = get_rec<FE>(sR, e + u, ev[u]);
 #pragma unroll
       for (int u = 0; u < 8; ++u)
         if ((wv[u] >> c) & 1u) {
@@ -490,12 +494,15 @@ __global__ void __launch_bounds__(RB) vb_edge_bwd_tile(VA a, int l) {
           for (int f = 0; f < FE; ++f) eap[f] += ev[u][f];
         }
     }
-    for (; e < ee; ++e)
-      if ((sW[e] >> c) & 1u) {
+    for (; e < ee; ++e) {
+      float ev[FA];
+      const uint32_t wv = get_rec<FE>(sR, e, ev);
+      if ((wv >> c) & 1u) {
         ++cnt;
 #pragma unroll
-        for (int f = 0; f < FE; ++f) eap[f] += sE[e * FeS + f];
+        for (int f = 0; f < FE; ++f) eap[f] += ev[f];
       }
+    }
     D[r * 32 + c] = cnt ? dsi * (float)cnt : 0.f;
 #pragma unroll
     for (int f = 0; f < FE; ++f) EAP[(r * 32 + c) * FeS + f] = cnt ? dsi * eap[f] : 0.f;
@@ -503,22 +510,20 @@ __global__ void __launch_bounds__(RB) vb_edge_bwd_tile(VA a, int l) {
     const int qb = trp[i] - q0, qe = trp[i + 1] - q0;
     int q = qb;
     for (; q + 8 <= qe; q += 8) {
-      int src[8];
-      uint32_t wv[8];
+      uint2 tr[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        src[u] = sT[q + u];
-        wv[u] = sWt[q + u];
-      }
+      for (int u = 0; u < 8; ++u) tr[u] = sTR[q + u];
       float dv[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) dv[u] = sD[src[u] * 32 + c];
+      for (int u = 0; u < 8; ++u) dv[u] = sD[tr[u].x * 32 + c];
 #pragma unroll
       for (int u = 0; u < 8; ++u)
-        if ((wv[u] >> c) & 1u) acc += dv[u];
+        if ((tr[u].y >> c) & 1u) acc += dv[u];
     }
-    for (; q < qe; ++q)
-      if ((sWt[q] >> c) & 1u) acc += sD[sT[q] * 32 + c];
+    for (; q < qe; ++q) {
+      const uint2 tr = sTR[q];
+      if ((tr.y >> c) & 1u) acc += sD[tr.x * 32 + c];
+    }
     DP[r * 32 + c] = acc;
   }
 }

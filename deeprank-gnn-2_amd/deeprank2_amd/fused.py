@@ -173,9 +173,8 @@ def vanilla_tile_plan(h: BatchHandle, n, row0, tile_rows, n_edge_feat, lds_check
     n_tiles = len(tile_row0) - 1
     if n_tiles == 0 or hmax == 0 or hmax > 65535:  # noqa: PLR2004
         return None
-    fes = max(1, n_edge_feat)
-    r4 = lambda v: (v + 3) & ~3  # noqa: E731
-    lds = 4 * (hmax * 32 + r4(emax * fes) + r4(emax) + r4(tmax) + r4((tmax + 1) // 2))  # tile_carve (backward, the larger)
+    rs = 4 if n_edge_feat <= 3 else 8  # floats per CSR edge record
+    lds = 4 * (hmax * 32 + emax * rs + 2 * tmax)  # tile_carve (backward, the larger)
     if lds_check and lds > LDS_MAX:
         return None
     dev = h.store.device
