@@ -124,11 +124,18 @@ __device__ __forceinline__ RowGraph row_graph(const VA& a, int64_t r) {
   return g;
 }
 
-__device__ __forceinline__ float edge_const(const float* wc, const float* ea, int Fe) {
-  float v = 0.f;
+// pre_e = (A_i + be) + B_j, then + Wc ea_e by a k-ordered fmaf chain (ab =
+// A_i + be once per row; the per-graph kernel's order, vanilla_graph.hip)
+__device__ __forceinline__ float edge_pre(float ab, float q, const float* wc, const float* ea, int Fe) {
+  float v = ab + q;
   for (int f = 0; f < Fe; ++f) v = fmaf(wc[f], ea[f], v);
   return v;
 }
+
+// an edge's bit of channel c as 0 / 1 (the backward's counts and attribute
+// sums: fmaf(bit, ea, sum) adds ea exactly when the bit is set; 0 * ea for an
+// inactive edge, as in the reference's dpre^T ea product)
+__device__ __forceinline__ float edge_bit(uint32_t w, int c) { return (float)((w >> c) & 1u); }
 
 // relu'(pre) as torch's threshold_backward on relu(pre): 0 where relu(pre) <= 0
 __device__ __forceinline__ bool active(float pre) { return !(pre <= 0.f); }
@@ -152,7 +159,7 @@ __global__ void __launch_bounds__(RB) vb_edge_fwd(VA a, int l) {
   const int hs = threadIdx.x & 32;
   for (int64_t r = blockIdx.x * (RB / 32) + (threadIdx.x >> 5); r < a.ws.n_rows; r += (int64_t)gridDim.x * (RB / 32)) {
     const RowGraph g = row_graph(a, r);
-    const float ac = L.a[r * 32 + c];
+    const float ab = L.a[r * 32 + c] + bc;
     const float* Bg = L.bm + g.r0 * 32 + c;
     uint32_t* wr = words ? words + a.ws.edge0[a.ws.row_slot[r]] : nullptr;
     float acc = 0.f;
@@ -164,7 +171,7 @@ __global__ void __launch_bounds__(RB) vb_edge_fwd(VA a, int l) {
       const float* ea = g.ea + (int64_t)e * FeS;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const float pre = ac + q[u] + edge_const(wc, ea + u * FeS, Fe) + bc;
+        const float pre = edge_pre(ab, q[u], wc, ea + u * FeS, Fe);
         acc += relu_keepnan(pre);
         if (wr) {
           const uint64_t m = __ballot(active(pre));
@@ -173,7 +180,7 @@ __global__ void __launch_bounds__(RB) vb_edge_fwd(VA a, int l) {
       }
     }
     for (; e < ee; ++e) {
-      const float pre = ac + Bg[(int64_t)g.col[e] * 32] + edge_const(wc, g.ea + (int64_t)e * FeS, Fe) + bc;
+      const float pre = edge_pre(ab, Bg[(int64_t)g.col[e] * 32], wc, g.ea + (int64_t)e * FeS, Fe);
       acc += relu_keepnan(pre);
       if (wr) {
         const uint64_t m = __ballot(active(pre));
@@ -189,7 +196,7 @@ __global__ void __launch_bounds__(RB) vb_edge_fwd(VA a, int l) {
 // group are all requested before the first is used); same sums, same order.
 template <int FE, int U>
 __device__ __forceinline__ void fwd_group(const RowGraph& g, int e, const float* Bg, const float (&wcr)[FE > 0 ? FE : 1],
-                                          float ac, float bc, int FeS, int c, int hs, uint32_t* wr, float& acc) {
+                                          float ab, int FeS, int c, int hs, uint32_t* wr, float& acc) {
   constexpr int FA = FE > 0 ? FE : 1;
   int j[U];
   float ev[U][FA], q[U];
@@ -203,10 +210,9 @@ __device__ __forceinline__ void fwd_group(const RowGraph& g, int e, const float*
   for (int u = 0; u < U; ++u) q[u] = Bg[(int64_t)j[u] * 32];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    float ec = 0.f;
+    float pre = ab + q[u];
 #pragma unroll
-    for (int f = 0; f < FE; ++f) ec = fmaf(wcr[f], ev[u][f], ec);
-    const float pre = ac + q[u] + ec + bc;
+    for (int f = 0; f < FE; ++f) pre = fmaf(wcr[f], ev[u][f], pre);
     acc += relu_keepnan(pre);
     if (wr) {
       const uint64_t m = __ballot(active(pre));
@@ -229,15 +235,15 @@ __global__ void __launch_bounds__(RB) vb_edge_fwd8(VA a, int l) {
   const int hs = threadIdx.x & 32;
   for (int64_t r = blockIdx.x * (RB / 32) + (threadIdx.x >> 5); r < a.ws.n_rows; r += (int64_t)gridDim.x * (RB / 32)) {
     const RowGraph g = row_graph(a, r);
-    const float ac = L.a[r * 32 + c];
+    const float ab = L.a[r * 32 + c] + bc;
     const float* Bg = L.bm + g.r0 * 32 + c;
     uint32_t* wr = words ? words + a.ws.edge0[a.ws.row_slot[r]] : nullptr;
     float acc = 0.f;
     const int eb = g.rp[g.i], ee = g.rp[g.i + 1];
     int e = eb;
-    for (; e + 8 <= ee; e += 8) fwd_group<FE, 8>(g, e, Bg, wcr, ac, bc, FeS, c, hs, wr, acc);
-    for (; e + 4 <= ee; e += 4) fwd_group<FE, 4>(g, e, Bg, wcr, ac, bc, FeS, c, hs, wr, acc);
-    for (; e < ee; ++e) fwd_group<FE, 1>(g, e, Bg, wcr, ac, bc, FeS, c, hs, wr, acc);
+    for (; e + 8 <= ee; e += 8) fwd_group<FE, 8>(g, e, Bg, wcr, ab, FeS, c, hs, wr, acc);
+    for (; e + 4 <= ee; e += 4) fwd_group<FE, 4>(g, e, Bg, wcr, ab, FeS, c, hs, wr, acc);
+    for (; e < ee; ++e) fwd_group<FE, 1>(g, e, Bg, wcr, ab, FeS, c, hs, wr, acc);
     L.s[r * 32 + c] = acc;
   }
 }
@@ -258,7 +264,7 @@ __global__ void __launch_bounds__(RB) vb_edge_bwd8(VA a, int l) {
     const uint32_t* wr = words + a.ws.edge0[a.ws.row_slot[r]];
     const float dsi = DS[r * 32 + c];
     const float* DSg = DS + g.r0 * 32 + c;
-    int cnt = 0;
+    float cnt = 0.f;
     float eap[FA];
 #pragma unroll
     for (int f = 0; f < FA; ++f) eap[f] = 0.f;
@@ -274,22 +280,22 @@ __global__ void __launch_bounds__(RB) vb_edge_bwd8(VA a, int l) {
 #pragma unroll
         for (int f = 0; f < FE; ++f) ev[u][f] = g.ea[(int64_t)(e + u) * FeS + f];
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if ((wv[u] >> c) & 1u) {
-          ++cnt;
+      for (int u = 0; u < 8; ++u) {
+        const float bit = edge_bit(wv[u], c);
+        cnt += bit;
 #pragma unroll
-          for (int f = 0; f < FE; ++f) eap[f] += ev[u][f];
-        }
-    }
-    for (; e < ee; ++e)
-      if ((wr[e] >> c) & 1u) {
-        ++cnt;
-#pragma unroll
-        for (int f = 0; f < FE; ++f) eap[f] += g.ea[(int64_t)e * FeS + f];
+        for (int f = 0; f < FE; ++f) eap[f] = fmaf(bit, ev[u][f], eap[f]);
       }
-    D[r * 32 + c] = cnt ? dsi * (float)cnt : 0.f;
+    }
+    for (; e < ee; ++e) {
+      const float bit = edge_bit(wr[e], c);
+      cnt += bit;
 #pragma unroll
-    for (int f = 0; f < FE; ++f) EAP[(r * 32 + c) * FeS + f] = cnt ? dsi * eap[f] : 0.f;
+      for (int f = 0; f < FE; ++f) eap[f] = fmaf(bit, g.ea[(int64_t)e * FeS + f], eap[f]);
+    }
+    D[r * 32 + c] = cnt != 0.f ? dsi * cnt : 0.f;
+#pragma unroll
+    for (int f = 0; f < FE; ++f) EAP[(r * 32 + c) * FeS + f] = cnt != 0.f ? dsi * eap[f] : 0.f;
     float acc = 0.f;
     const int qb = g.trp[g.i], qe = g.trp[g.i + 1];
     int q = qb;
@@ -408,7 +414,7 @@ __global__ void __launch_bounds__(RB) vb_edge_fwd_tile(VA a, int l) {
   __syncthreads();
   for (int64_t r = rt0 + (tid >> 5); r < rt1; r += RB / 32) {
     const int i = (int)(r - g0);
-    const float ac = L.a[r * 32 + c];
+    const float ab = L.a[r * 32 + c] + bc;
     float acc = 0.f;
     const int eb = rp[i] - e0, ee = rp[i + 1] - e0;
     int e = eb;
@@ -423,10 +429,9 @@ __global__ void __launch_bounds__(RB) vb_edge_fwd_tile(VA a, int l) {
       uint32_t mine = 0u;  // lane c < U keeps word c: one contiguous store per group
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        float ec = 0.f;
+        float pre = ab + q[u];
 #pragma unroll
-        for (int f = 0; f < FE; ++f) ec = fmaf(wcr[f], ev[u][f], ec);
-        const float pre = ac + q[u] + ec + bc;
+        for (int f = 0; f < FE; ++f) pre = fmaf(wcr[f], ev[u][f], pre);
         acc += relu_keepnan(pre);
         const uint64_t m = __ballot(active(pre));
         if (c == u) mine = (uint32_t)(m >> hs);
@@ -475,7 +480,7 @@ __global__ void __launch_bounds__(RB) vb_edge_bwd_tile(VA a, int l) {
   for (int64_t r = rt0 + (tid >> 5); r < rt1; r += RB / 32) {
     const int i = (int)(r - g0);
     const float dsi = DS[r * 32 + c];
-    int cnt = 0;
+    float cnt = 0.f;
     float eap[FA];
 #pragma unroll
     for (int f = 0; f < FA; ++f) eap[f] = 0.f;
@@ -487,25 +492,23 @@ __global__ void __launch_bounds__(RB) vb_edge_bwd_tile(VA a, int l) {
 #pragma unroll
       for (int u = 0; u < 8; ++u) wv[u] = get_rec<FE>(sR, e + u, ev[u]);
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if ((wv[u] >> c) & 1u) {
-          ++cnt;
+      for (int u = 0; u < 8; ++u) {
+        const float bit = edge_bit(wv[u], c);
+        cnt += bit;
 #pragma unroll
-          for (int f = 0; f < FE; ++f) eap[f] += ev[u][f];
-        }
+        for (int f = 0; f < FE; ++f) eap[f] = fmaf(bit, ev[u][f], eap[f]);
+      }
     }
     for (; e < ee; ++e) {
       float ev[FA];
-      const uint32_t wv = get_rec<FE>(sR, e, ev);
-      if ((wv >> c) & 1u) {
-        ++cnt;
+      const float bit = edge_bit(get_rec<FE>(sR, e, ev), c);
+      cnt += bit;
 #pragma unroll
-        for (int f = 0; f < FE; ++f) eap[f] += ev[f];
-      }
+      for (int f = 0; f < FE; ++f) eap[f] = fmaf(bit, ev[f], eap[f]);
     }
-    D[r * 32 + c] = cnt ? dsi * (float)cnt : 0.f;
+    D[r * 32 + c] = cnt != 0.f ? dsi * cnt : 0.f;
 #pragma unroll
-    for (int f = 0; f < FE; ++f) EAP[(r * 32 + c) * FeS + f] = cnt ? dsi * eap[f] : 0.f;
+    for (int f = 0; f < FE; ++f) EAP[(r * 32 + c) * FeS + f] = cnt != 0.f ? dsi * eap[f] : 0.f;
     float acc = 0.f;
     const int qb = trp[i] - q0, qe = trp[i + 1] - q0;
     int q = qb;
@@ -661,39 +664,20 @@ __global__ void __launch_bounds__(RB) vb_edge_bwd(VA a, int l) {
       const uint32_t* wr = words + a.ws.edge0[a.ws.row_slot[r]];
       const float dsi = DS[r * 32 + c];
       const float* DSg = DS + g.r0 * 32 + c;
-      int cnt = 0;
+      float cnt = 0.f;
       float eap[MAXFE];
 #pragma unroll
       for (int f = 0; f < MAXFE; ++f) eap[f] = 0.f;
       const int eb = g.rp[g.i], ee = g.rp[g.i + 1];
-      int e = eb;
-      for (; e + 4 <= ee; e += 4) {
-        uint32_t wv[4];
+      for (int e = eb; e < ee; ++e) {
+        const float bit = edge_bit(wr[e], c);
+        cnt += bit;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) wv[u] = wr[e + u];
-        float ev[4][MAXFE];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-          for (int f = 0; f < MAXFE; ++f) ev[u][f] = f < Fe ? g.ea[(int64_t)(e + u) * FeS + f] : 0.f;
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if ((wv[u] >> c) & 1u) {
-            ++cnt;
-#pragma unroll
-            for (int f = 0; f < MAXFE; ++f)
-              if (f < Fe) eap[f] += ev[u][f];
-          }
+        for (int f = 0; f < MAXFE; ++f)
+          if (f < Fe) eap[f] = fmaf(bit, g.ea[(int64_t)e * FeS + f], eap[f]);
       }
-      for (; e < ee; ++e)
-        if ((wr[e] >> c) & 1u) {
-          ++cnt;
-#pragma unroll
-          for (int f = 0; f < MAXFE; ++f)
-            if (f < Fe) eap[f] += g.ea[(int64_t)e * FeS + f];
-        }
-      D[r * 32 + c] = cnt ? dsi * (float)cnt : 0.f;
-      for (int f = 0; f < Fe; ++f) EAP[(r * 32 + c) * FeS + f] = cnt ? dsi * eap[f] : 0.f;
+      D[r * 32 + c] = cnt != 0.f ? dsi * cnt : 0.f;
+      for (int f = 0; f < Fe; ++f) EAP[(r * 32 + c) * FeS + f] = cnt != 0.f ? dsi * eap[f] : 0.f;
       float acc = 0.f;  // D'_i over edges (src -> i), in transposed (original edge) order
       const int qb = g.trp[g.i], qe = g.trp[g.i + 1];
       int q = qb;
@@ -723,41 +707,25 @@ __global__ void __launch_bounds__(RB) vb_edge_bwd(VA a, int l) {
   }
   for (int64_t r = blockIdx.x * (RB / 32) + (threadIdx.x >> 5); r < a.ws.n_rows; r += (int64_t)gridDim.x * (RB / 32)) {
     const RowGraph g = row_graph(a, r);
-    const float ac = L.a[r * 32 + c], bi = L.bm[r * 32 + c], dsi = DS[r * 32 + c];
+    const float ab = L.a[r * 32 + c] + bc, bi = L.bm[r * 32 + c], dsi = DS[r * 32 + c];
     const float* Bg = L.bm + g.r0 * 32 + c;
     const float* Ag = L.a + g.r0 * 32 + c;
     const float* DSg = DS + g.r0 * 32 + c;
-    int cnt = 0;
+    float cnt = 0.f;
     float eap[MAXFE];
 #pragma unroll
     for (int f = 0; f < MAXFE; ++f) eap[f] = 0.f;
     const int eb = g.rp[g.i], ee = g.rp[g.i + 1];
-    int e = eb;
-    for (; e + 4 <= ee; e += 4) {
-      const int j0 = g.col[e], j1 = g.col[e + 1], j2 = g.col[e + 2], j3 = g.col[e + 3];
-      const float q[4] = {Bg[(int64_t)j0 * 32], Bg[(int64_t)j1 * 32], Bg[(int64_t)j2 * 32], Bg[(int64_t)j3 * 32]};
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float* ea = g.ea + (int64_t)(e + u) * FeS;
-        if (active(ac + q[u] + edge_const(wc, ea, Fe) + bc)) {
-          ++cnt;
-#pragma unroll
-          for (int f = 0; f < MAXFE; ++f)
-            if (f < Fe) eap[f] += ea[f];
-        }
-      }
-    }
-    for (; e < ee; ++e) {
+    for (int e = eb; e < ee; ++e) {
       const float* ea = g.ea + (int64_t)e * FeS;
-      if (active(ac + Bg[(int64_t)g.col[e] * 32] + edge_const(wc, ea, Fe) + bc)) {
-        ++cnt;
+      const float bit = active(edge_pre(ab, Bg[(int64_t)g.col[e] * 32], wc, ea, Fe)) ? 1.f : 0.f;
+      cnt += bit;
 #pragma unroll
-        for (int f = 0; f < MAXFE; ++f)
-          if (f < Fe) eap[f] += ea[f];
-      }
+      for (int f = 0; f < MAXFE; ++f)
+        if (f < Fe) eap[f] = fmaf(bit, ea[f], eap[f]);
     }
-    D[r * 32 + c] = cnt ? dsi * (float)cnt : 0.f;
-    for (int f = 0; f < Fe; ++f) EAP[(r * 32 + c) * FeS + f] = cnt ? dsi * eap[f] : 0.f;
+    D[r * 32 + c] = cnt != 0.f ? dsi * cnt : 0.f;
+    for (int f = 0; f < Fe; ++f) EAP[(r * 32 + c) * FeS + f] = cnt != 0.f ? dsi * eap[f] : 0.f;
     float acc = 0.f;  // D'_i over edges (src -> i): pre = A_src + B_i + Wc ea_e + be
     const int qb = g.trp[g.i], qe = g.trp[g.i + 1];
     int q = qb;
@@ -776,11 +744,11 @@ __global__ void __launch_bounds__(RB) vb_edge_bwd(VA a, int l) {
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        if (active(av[u] + bi + edge_const(wc, g.ea + (int64_t)ed[u] * FeS, Fe) + bc)) acc += dv[u];
+        if (active(edge_pre(av[u] + bc, bi, wc, g.ea + (int64_t)ed[u] * FeS, Fe))) acc += dv[u];
     }
     for (; q < qe; ++q) {
       const int src = g.tcol[q], e = g.teid[q];
-      if (active(Ag[(int64_t)src * 32] + bi + edge_const(wc, g.ea + (int64_t)e * FeS, Fe) + bc)) acc += DSg[(int64_t)src * 32];
+      if (active(edge_pre(Ag[(int64_t)src * 32] + bc, bi, wc, g.ea + (int64_t)e * FeS, Fe))) acc += DSg[(int64_t)src * 32];
     }
     DP[r * 32 + c] = acc;
   }
