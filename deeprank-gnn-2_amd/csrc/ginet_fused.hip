@@ -531,8 +531,6 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
 // waits on another workgroup.
 struct SibCtx {
   int rk, k, b;
-  float* z;                 // [rows, XS] Z rows of the batch (dr_large_plan.z)
-  const int32_t* z_row0;    // [B+1]
   unsigned long long* gkey; // [B, k0_max, 32], zero on entry and left zero
   int k0_max;
   uint32_t* arrive;         // [B], zero on entry and left zero
@@ -1700,7 +1698,7 @@ extern "C" int dr_ginet_sibling_pass(const dr_graph_store* store, const dr_graph
   if (store->n_feat < 1 || 32 * store->n_feat > 2 * NT) return DR_E_UNSUPPORTED;  // F <= 64
   if (lds_bytes > 160 * 1024) return DR_E_LDS;
   if (pass->compute_dtype != DR_DTYPE_F32) return DR_E_UNSUPPORTED;
-  if (!plan->z || !plan->z_row0 || !plan->part_key || !plan->arrive || plan->k0_max < 1 || plan->k0_max > 64) return DR_E_ARG;
+  if (!plan->part_key || !plan->arrive || plan->k0_max < 1 || plan->k0_max > 64) return DR_E_ARG;
   if ((pass->flags & DR_PASS_BACKWARD) && (!pass->slab || !pass->head)) return DR_E_ARG;
   if ((pass->flags & DR_PASS_BACKWARD) && pass->loss_kind == DR_LOSS_NONE && !pass->dout) return DR_E_ARG;
   if ((pass->flags & DR_PASS_FORWARD) && !pass->out) return DR_E_ARG;
@@ -1718,8 +1716,6 @@ extern "C" int dr_ginet_sibling_pass(const dr_graph_store* store, const dr_graph
   sc.rk = 0;
   sc.b = 0;
   sc.k = split;
-  sc.z = plan->z;
-  sc.z_row0 = plan->z_row0;
   sc.gkey = reinterpret_cast<unsigned long long*>(plan->part_key);
   sc.k0_max = plan->k0_max;
   sc.arrive = plan->arrive;

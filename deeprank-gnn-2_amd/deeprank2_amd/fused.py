@@ -443,25 +443,22 @@ def sibling_k(spec: FusedSpec, h: BatchHandle) -> int:
 
 
 class SiblingPlan:
-    """dr_large_plan fields dr_ginet_sibling_pass reads: Z rows, the depth-0
-    keys and the arrival tickets (both kept zero between launches)."""
+    """dr_large_plan fields dr_ginet_sibling_pass reads: the depth-0 keys and
+    the arrival tickets (both kept zero between launches)."""
 
     def __init__(self, h: BatchHandle):
         st = h.store
         idx = h.gids_host.astype(np.int64)
-        n, k0 = st._sizes[0][idx], st._sizes[2][idx]  # noqa: SLF001
+        k0 = st._sizes[2][idx]  # noqa: SLF001
         self.k0_max = max(1, int(k0.max()))
         if self.k0_max > 64:  # noqa: PLR2004
             msg = f"a graph of the batch has {self.k0_max} depth-0 clusters (> 64)"
             raise RuntimeError(msg)
         dev = st.device
-        z_row0 = np.concatenate([[0], np.cumsum(n)]).astype(np.int32)
-        self.z_row0 = torch.from_numpy(z_row0).to(dev)
-        self.z = torch.empty(max(1, int(z_row0[-1])) * st.x_stride, dtype=torch.float32, device=dev)
         self.key = torch.zeros(h.B * self.k0_max * 32, dtype=torch.int64, device=dev)
         self.arrive = torch.zeros(h.B, dtype=torch.int32, device=dev)
         c = _lib.LargePlanC()
-        c.z_row0, c.z, c.part_key, c.arrive, c.k0_max = self.z_row0.data_ptr(), self.z.data_ptr(), self.key.data_ptr(), self.arrive.data_ptr(), self.k0_max
+        c.part_key, c.arrive, c.k0_max = self.key.data_ptr(), self.arrive.data_ptr(), self.k0_max
         self.c = c
 
 

@@ -262,12 +262,13 @@ int dr_ginet_large_pass(const dr_graph_store* store, const dr_graph_desc* descs,
 /* Sibling split of dr_ginet_graph_pass for small batches (r03): `split` (1-8)
  * workgroups per graph each stage the graph, run the fused front half (Z = A X,
  * conv1 on MFMA, depth-0 pool keys) on every split-th 16-row tile, publish
- * their Z rows to plan->z (row stride r4(F), z_row0) write-through and their
- * keys into plan->part_key ([B, k0_max, 32], zero on entry and left zero) by
- * agent-scope 64-bit atomic max, then take a ticket on plan->arrive[b] (zero
- * on entry and left zero); the last to arrive runs the tail.  No workgroup
- * waits on another.  Bit-identical to dr_ginet_graph_pass.  Other plan fields
- * are ignored.                                                              */
+ * their keys into plan->part_key ([B, k0_max, 32], zero on entry and left
+ * zero) by agent-scope 64-bit atomic max, then take a ticket on
+ * plan->arrive[b] (zero on entry and left zero); the last to arrive regathers
+ * the Z rows at the pooling args that other workgroups computed from its own
+ * staged graph and runs the tail.  No workgroup waits on another.
+ * Bit-identical to dr_ginet_graph_pass; measured slower.
+ * Other plan fields are ignored.                                            */
 int dr_ginet_sibling_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
                           const dr_large_plan* plan, const dr_ginet_weights* w, const dr_pass* pass, int32_t split,
                           int32_t lds_bytes, void* stream);
