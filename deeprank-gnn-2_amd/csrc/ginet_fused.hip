@@ -275,20 +275,36 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
                                            int F, int OUT, float y_g, uint64_t drop_offset, ZAt zat) {
   const int tid = threadIdx.x;
   STAMP(4);
-  // ---------------- conv2 node GEMM on the pooled graph (ginet.py:101,112) --
+  // ---------------- conv2 on the pooled graph (ginet.py:101,112) ------------
+  // H2[k][o] = relu(sum over pooled row k, in edge order, of Y2[j][o]) with
+  // Y2[j][o] = P1[j] . W2[o] (16-term fmaf chain) formed per neighbour in
+  // registers: no Y2 array and no barrier between the GEMM and the sum
   for (int p = tid; p < K0 * 64; p += NT) {
     const int k = p >> 6, o = p & 63, br = o >> 5;
-    const float* wr = t.w2 + o * 16;  // rows 0..31 = W2, 32..63 = W2e
-    const float* pr = t.p1 + k * 32 + br * 16;
-    float acc = 0.f;
+    float wr[16];  // rows 0..31 = W2, 32..63 = W2e
 #pragma unroll
-    for (int j = 0; j < 16; ++j) acc = fmaf(pr[j], wr[j], acc);
-    t.y2[p] = acc;
-  }
-  __syncthreads();
-  for (int p = tid; p < K0 * 64; p += NT) {
-    const int k = p >> 6, o = p & 63;
-    t.h2[p] = relu_keepnan(pooled_row_sum(t.p1c, t.p1rp[k], t.p1rp[k + 1], t.y2, o));
+    for (int q = 0; q < 4; ++q) {
+      const float4 v = *reinterpret_cast<const float4*>(t.w2 + o * 16 + 4 * q);
+      wr[4 * q] = v.x;
+      wr[4 * q + 1] = v.y;
+      wr[4 * q + 2] = v.z;
+      wr[4 * q + 3] = v.w;
+    }
+    float acc = 0.f;
+    for (int e = t.p1rp[k]; e < t.p1rp[k + 1]; ++e) {
+      const float* pr = t.p1 + t.p1c[e] * 32 + br * 16;
+      float y = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(pr + 4 * q);
+        y = fmaf(v.x, wr[4 * q], y);
+        y = fmaf(v.y, wr[4 * q + 1], y);
+        y = fmaf(v.z, wr[4 * q + 2], y);
+        y = fmaf(v.w, wr[4 * q + 3], y);
+      }
+      acc += y;
+    }
+    t.h2[p] = relu_keepnan(acc);
   }
   __syncthreads();
 
@@ -396,21 +412,22 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
   // ---------------- depth-1 pooling + mean backward -------------------------
   // scatter_mean: grad/count; scatter_reduce amax: grad split evenly over the
   // members equal to the max ((src==max) * grad/ties, so NaN stays NaN).
-  for (int p = tid; p < K0 * 64; p += NT) {  // one (depth-0 cluster, channel) per thread
-    const int k = p >> 6, o = p & 63, mo = t.cl1[k] * 64 + o;
-    const float gm = (t.dg[o] / (float)K1) / t.nt[mo];
-    const float mx = t.p2[mo];
-    const float h = t.h2[p];
-    t.d2[p] = relu_bwd(h, (h == mx ? 1.f : 0.f) * gm);
+  // dS2[k][o] (the gradient at H2's pre-activation) is formed per neighbour
+  // inside dY2 = A1^T dS2 (pooled graph, transposed CSR, edge order): no dS2
+  // array and no barrier between the two
+  for (int p = tid; p < K0 * 64; p += NT) {
+    const int j = p >> 6, o = p & 63;
+    const float dgo = t.dg[o] / (float)K1;
+    float acc = 0.f;
+    for (int e = t.p1trp[j]; e < t.p1trp[j + 1]; ++e) {
+      const int k = t.p1tc[e], mo = t.cl1[k] * 64 + o;
+      const float h = t.h2[k * 64 + o];
+      acc += relu_bwd(h, (h == t.p2[mo] ? 1.f : 0.f) * (dgo / t.nt[mo]));
+    }
+    t.y2[p] = acc;
   }
   __syncthreads();
   STAMP(11);
-  // dY2 = A1^T dS2 (pooled graph, transposed CSR)  -> reuse t.y2
-  for (int p = tid; p < K0 * 64; p += NT) {
-    const int j = p >> 6, o = p & 63;
-    t.y2[p] = pooled_row_sum(t.p1tc, t.p1trp[j], t.p1trp[j + 1], t.d2, o);
-  }
-  __syncthreads();
   STAMP(12);
   // conv2 weight-gradient partials, and the gradient reaching each depth-0
   // arg member through relu (v = relu'(H1[arg]) * dP1); with many clusters on MFMA:
@@ -699,6 +716,7 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
       }
       // this wave's Z rows are complete in LDS before its own MFMA reads them
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (tt == 0) STAMP(20);  // (wave 0's first tile: gather done)
       const int ar = min(r0 + li, N - 1);  // rows past N compute garbage that is never pooled
       floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -712,6 +730,7 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
           acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], wb[4 * ks + u], acc1, 0, 0, 0);
         }
       }
+      if (tt == 0) STAMP(21);  // (MFMA issued)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = r0 + kq * 4 + r;
@@ -726,6 +745,10 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
             __hip_atomic_fetch_max(skey + k * 32 + 16 + li, ((unsigned long long)__float_as_uint(v1) << 32) | low,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
+      }
+      if (tt == 0) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        STAMP(22);  // (pool atomics done)
       }
     }
   }

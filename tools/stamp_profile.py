@@ -56,12 +56,13 @@ def main():
     slab = torch.empty(B * amd.slab_stride(30), device=dev)
     head = torch.empty(B * amd.head_stride(1), device=dev)
     lpg = torch.empty(B, device=dev)
-    rows = []
+    rows, rows_full = [], []
     for it in range(30):
         mod.graph_pass(h, params, 1, 3, dropout=amd.Dropout(0.4, seed=1, offset=it), loss_kind=1, loss_scale=1 / B, out=out, loss_per_graph=lpg, slab=slab, head=head, stamps=st)
         torch.cuda.synchronize()
         if it >= 5:
             rows.append(st.view(B, 32)[:, : len(phases) + 1].cpu().numpy().copy())
+            rows_full.append(st.view(B, 32).cpu().numpy().copy())
     a = np.stack(rows)  # [iters, B, 16]
     d = np.diff(a, axis=2).astype(np.float64)  # phase i = stamp[i+1]-stamp[i]
     med = np.median(d.reshape(-1, d.shape[-1]), axis=0)
@@ -70,6 +71,11 @@ def main():
     print(which)
     for name, v in zip(phases, med):
         print(f"  {name:18s} {v:8.0f} cyc  {100 * v / tot:5.1f}%")
+    if which == "ginet":  # wave 0's first tile inside the front half (stamps 20-22)
+        full = np.stack([r for r in rows_full])
+        if np.median(full[:, :, 22]) > 0:
+            g = np.median(full[:, :, 20] - full[:, :, 1]), np.median(full[:, :, 21] - full[:, :, 20]), np.median(full[:, :, 22] - full[:, :, 21])
+            print(f"  wave 0 tile 0: gather {g[0]:.0f}  MFMA {g[1]:.0f}  pool atomics {g[2]:.0f} cyc")
 
 
 PHASES_F = ["stage", "gather rowmean(X)", "gemm conv1", "pool0", "conv2 (pooled)", "pool1+mean", "head fwd", "loss", "head/pool1/conv2 bwd", "dW1"]
