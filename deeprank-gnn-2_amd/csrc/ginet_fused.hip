@@ -87,7 +87,6 @@ __host__ __device__ inline Carve carve(int N, int E, int F, int K0, int P1, int 
   TAKE(dp1, K0 * 32)
   TAKE(y2, K0 * 64)
   TAKE(h2, K0 * 64)
-  TAKE(d2, K0 * 64)
   TAKE(p1rp, K0 + 1)
   TAKE(p1c, P1)
   if (alias) {
@@ -232,7 +231,7 @@ __device__ __forceinline__ float pooled_row_sum(const int* col, int eb, int ee, 
 // the single-workgroup kernel and the large-graph tail kernel; zat(i, kk)
 // reads Z = A·X at node i (LDS or the large path's HBM workspace).
 struct TailLds {
-  float *w2, *fc2, *p1, *dp1, *y2, *h2, *d2, *p2, *nt, *dgp;
+  float *w2, *fc2, *p1, *dp1, *y2, *h2, *p2, *nt, *dgp;
   float *g, *hpre, *hh, *hd, *dh, *dg, *dout;
   int *a1, *p1rp, *p1c, *p1trp, *p1tc, *m1p, *m1i, *cl1;
   const uint8_t* keep = nullptr;  // prefetched dropout keep flags, or null (hash in the head)
@@ -248,7 +247,6 @@ __device__ __forceinline__ TailLds tail_lds(const C& c, float* lds) {
   t.dp1 = lds + c.dp1;
   t.y2 = lds + c.y2;
   t.h2 = lds + c.h2;
-  t.d2 = lds + c.d2;
   t.p1rp = reinterpret_cast<int*>(lds + c.p1rp);
   t.p1c = reinterpret_cast<int*>(lds + c.p1c);
   t.p1trp = reinterpret_cast<int*>(lds + c.p1trp);
@@ -731,11 +729,14 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
         }
       }
       if (tt == 0) STAMP(21);  // (MFMA issued)
+      // the four rows' clusters in one 16-byte read (rows past N: unused)
+      const int4 kk4 = *reinterpret_cast<const int4*>(scl0 + r0 + kq * 4);
+      const int kk[4] = {kk4.x, kk4.y, kk4.z, kk4.w};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = r0 + kq * 4 + r;
         if (row < N) {
-          const int k = scl0[row];
+          const int k = kk[r];
           const unsigned long long low = 0xffffffffull - (unsigned long long)(uint32_t)row;
           const float v0 = relu_keepnan(acc0[r]), v1 = relu_keepnan(acc1[r]);
           if (v0 == v0)
@@ -1488,7 +1489,6 @@ __host__ __device__ inline TailCarve tail_carve(int K0, int P1, int K1, int alia
   TAKE(dp1, K0 * 32)
   TAKE(y2, K0 * 64)
   TAKE(h2, K0 * 64)
-  TAKE(d2, K0 * 64)
   TAKE(p1rp, K0 + 1)
   TAKE(p1c, P1)
   if (alias) {
