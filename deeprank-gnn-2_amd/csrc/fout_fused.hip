@@ -98,7 +98,7 @@ __host__ __device__ inline Carve carve_at(int N, int E, int F, int K0, int P1, i
   TAKE(p2, K1 * 32)
   TAKE(nt, K1 * 32)
   TAKE(head, HEADW)
-  TAKE(dgp, NW * 32)
+  TAKE(dgp, NT)                        // the head backward's [NT / 32 chunks][32] partials
   TAKE(red, 2 * NT)
   if (sg) {
     TAKE(ea, E)

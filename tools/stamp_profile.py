@@ -107,13 +107,17 @@ def fout(dev, B, which):
         run_pass(spec, h, params, p)
         torch.cuda.synchronize()
         if it >= 5:
-            rows.append(st.view(B, 32)[:, : len(PHASES_F) + 1].cpu().numpy().copy())
-    d = np.diff(np.stack(rows), axis=2).astype(np.float64)
+            rows.append(st.view(B, 32).cpu().numpy().copy())
+    full = np.stack(rows)
+    d = np.diff(full[:, :, : len(PHASES_F) + 1], axis=2).astype(np.float64)
     med = np.median(d.reshape(-1, d.shape[-1]), axis=0)
     tot = med.sum()
     print(f"B={B}  median cycles per fout_graph_kernel workgroup ({which}): {tot:.0f}")
     for name, v in zip(PHASES_F, med):
         print(f"  {name:22s} {v:8.0f} cyc  {100 * v / tot:5.1f}%")
+    if np.median(full[:, :, 22]) > 0:  # wave 0's first tile inside the front half (stamps 20-22)
+        g = np.median(full[:, :, 20] - full[:, :, 1]), np.median(full[:, :, 21] - full[:, :, 20]), np.median(full[:, :, 22] - full[:, :, 21])
+        print(f"  wave 0 tile 0: gather {g[0]:.0f}  MFMA {g[1]:.0f}  pool atomics {g[2]:.0f} cyc")
 
 
 def vanilla(dev, B):
