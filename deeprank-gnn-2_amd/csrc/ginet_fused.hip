@@ -506,31 +506,35 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
   {
     const int SS = DR_SLAB_STRIDE(F);
     float* slab = a.p.slab + (int64_t)b * SS;
-    for (int p = tid; p < 32 * F; p += NT) {
-      const int ch = p / F, kk = p - ch * F;
-      float acc = 0.f;
-      int k = 0;
-      // 8 clusters at a time: the Z reads (HBM on the large path) are issued
-      // together, then accumulated in cluster order (same fmaf chain)
-      // 8 clusters at a time, the last group predicated (clusters past K0 and
-      // empty ones contribute nothing): every Z read of a group in flight
-      for (; k < K0; k += 8) {
-        float zv[8], dv[8];
-        bool ok[8];
+    // G clusters at a time, the last group predicated (clusters past K0 and
+    // empty ones contribute nothing): every Z read of a group in flight (HBM on
+    // the large path: with many clusters, groups of 16 halve the round trips),
+    // then accumulated in cluster order (same fmaf chain)
+    auto dw1 = [&](auto g_t) {
+      constexpr int G = decltype(g_t)::value;
+      for (int p = tid; p < 32 * F; p += NT) {
+        const int ch = p / F, kk = p - ch * F;
+        float acc = 0.f;
+        for (int k = 0; k < K0; k += G) {
+          float zv[G], dv[G];
+          bool ok[G];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const bool in = k + u < K0;
-          const int i = in ? t.a1[(k + u) * 32 + ch] : N;
-          ok[u] = i < N;
-          dv[u] = in ? t.dp1[(k + u) * 32 + ch] : 0.f;
-          zv[u] = zat(ok[u] ? i : 0, kk);
+          for (int u = 0; u < G; ++u) {
+            const bool in = k + u < K0;
+            const int i = in ? t.a1[(k + u) * 32 + ch] : N;
+            ok[u] = i < N;
+            dv[u] = in ? t.dp1[(k + u) * 32 + ch] : 0.f;
+            zv[u] = zat(ok[u] ? i : 0, kk);
+          }
+#pragma unroll
+          for (int u = 0; u < G; ++u)
+            if (ok[u]) acc = fmaf(dv[u], zv[u], acc);
         }
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (ok[u]) acc = fmaf(dv[u], zv[u], acc);
+        drk::st_part<WT>(slab + p, acc);
       }
-      drk::st_part<WT>(slab + p, acc);
-    }
+    };
+    if (K0 > 8) dw1(std::integral_constant<int, 16>());
+    else dw1(std::integral_constant<int, 8>());
   }
   STAMP(14);
 }

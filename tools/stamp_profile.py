@@ -41,8 +41,8 @@ def main():
         return fout(dev, B, which)
     mod, phases = (amd_nc, PHASES_NC) if which == "ginet_nocluster" else (amd, PHASES)
     large = which == "ginet_large"
-    if large:  # tail kernel of the split path on atom-level graphs (stamps 0-3: staging, tile combine)
-        phases = ["stage", "tile combine", "-", *PHASES[4:]]
+    if large:  # tail kernel of the split path on atom-level graphs (stamps 0-3: staging, tile combine; then as ginet_graph_kernel)
+        phases = ["stage", "tile combine", "-", *PHASES[3:]]
     fam = {"n_lo": 2700, "n_hi": 3300, "mean_degree": 16.7, "k_lo": 8, "k_hi": 32} if large else {}
     store = GraphStore(pack_graphs(records(make_dataset(B, seed=1000, **fam))), dev)
     h = amd.BatchHandle(store, np.arange(B))
