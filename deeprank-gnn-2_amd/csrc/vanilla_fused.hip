@@ -22,6 +22,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <type_traits>
 
 #include "graph_common.h"
@@ -477,6 +479,10 @@ __global__ void __launch_bounds__(RB) vb_edge_bwd_tile(VA a, int l) {
       sTR[p] = make_uint2(lt[p], words[teid[q0 + p]]);  // gathered while staging: no dependent loads in the row loop
   }
   __syncthreads();
+  const bool twc = a.ws.tile_wc != nullptr;  // the tile's dWc share instead of per-row eap
+  float wsum[FA];
+#pragma unroll
+  for (int f = 0; f < FA; ++f) wsum[f] = 0.f;
   for (int64_t r = rt0 + (tid >> 5); r < rt1; r += RB / 32) {
     const int i = (int)(r - g0);
     const float dsi = DS[r * 32 + c];
@@ -507,8 +513,13 @@ __global__ void __launch_bounds__(RB) vb_edge_bwd_tile(VA a, int l) {
       for (int f = 0; f < FE; ++f) eap[f] = fmaf(bit, ev[f], eap[f]);
     }
     D[r * 32 + c] = cnt != 0.f ? dsi * cnt : 0.f;
+    if (twc) {
 #pragma unroll
-    for (int f = 0; f < FE; ++f) EAP[(r * 32 + c) * FeS + f] = cnt != 0.f ? dsi * eap[f] : 0.f;
+      for (int f = 0; f < FE; ++f) wsum[f] += cnt != 0.f ? dsi * eap[f] : 0.f;
+    } else {
+#pragma unroll
+      for (int f = 0; f < FE; ++f) EAP[(r * 32 + c) * FeS + f] = cnt != 0.f ? dsi * eap[f] : 0.f;
+    }
     float acc = 0.f;
     const int qb = trp[i] - q0, qe = trp[i + 1] - q0;
     int q = qb;
@@ -528,6 +539,18 @@ __global__ void __launch_bounds__(RB) vb_edge_bwd_tile(VA a, int l) {
       if ((tr.y >> c) & 1u) acc += sD[tr.x * 32 + c];
     }
     DP[r * 32 + c] = acc;
+  }
+  if (twc && FE > 0) {  // the 8 row groups' shares, combined in group order (sD is dead)
+    __syncthreads();
+    const int rg = tid >> 5;
+#pragma unroll
+    for (int f = 0; f < FE; ++f) sD[(rg * 32 + c) * FeS + f] = wsum[f];
+    __syncthreads();
+    if (tid < 32 * FeS) {
+      float v = 0.f;
+      for (int g = 0; g < RB / 32; ++g) v += sD[g * 32 * FeS + tid];
+      a.ws.tile_wc[(int64_t)t * 32 * FeS + tid] = v;
+    }
   }
 }
 
@@ -922,7 +945,12 @@ __global__ void __launch_bounds__(RB) vb_wgrad_mfma(VA a, int l) {
   for (int p0 = threadIdx.x; p0 < 4 * (32 * Fe + 32 + F); p0 += RB) {
     const int p = p0 >> 2, qr = p0 & 3, ib = qr * (WR / 4);
     float v = 0.f;
-    if (p < 32 * Fe) {
+    if (p < 32 * Fe && a.ws.tile_wc) {  // the chunk's tiles' shares (the backward edge kernel), in tile order
+      const int c = p / Fe, f = p - c * Fe;
+      const int TR = a.ws.tile_rows, t0 = a.ws.tile_first[b] + i0 / TR, nt = (nr + TR - 1) / TR;
+      if (qr == 0)
+        for (int q = 0; q < nt; ++q) v += a.ws.tile_wc[(int64_t)(t0 + q) * 32 * FeS + c * FeS + f];
+    } else if (p < 32 * Fe) {
       const int c = p / Fe, f = p - c * Fe;
       float t[WR / 4];
 #pragma unroll
@@ -992,19 +1020,21 @@ __global__ void __launch_bounds__(RB) vb_wgrad_combine(VA a, int l) {
 }
 
 // the FE-specialised 8-in-flight edge kernels (Fe <= 4; the backward needs the
-// forward's ReLU words), tiled when the scratch carries a tile plan; false: not launched
-inline bool launch_edge8(bool fwd, const VA& a, int l, dim3 grid, hipStream_t st) {
-  if (a.Fe > 4 || (!fwd && !a.ws.relu_words)) return false;
+// forward's ReLU words), tiled when the scratch carries a tile plan.  Returns
+// 0: not launched, 1: untiled, 2: tiled (the backward then wrote tile_wc)
+inline int launch_edge8(bool fwd, const VA& a, int l, dim3 grid, hipStream_t st) {
+  if (a.Fe > 4 || (!fwd && !a.ws.relu_words)) return 0;
   if (a.ws.tile_row0 && a.ws.relu_words && a.ws.n_tiles > 0) {
     const int FeS = a.Fe > 0 ? a.Fe : 1;
-    const size_t lds = 4 * (size_t)tile_carve(a.ws.halo_max, a.ws.tile_edges_max, a.ws.tile_tedges_max, FeS, !fwd).total;
+    size_t lds = 4 * (size_t)tile_carve(a.ws.halo_max, a.ws.tile_edges_max, a.ws.tile_tedges_max, FeS, !fwd).total;
+    if (!fwd && a.ws.tile_wc) lds = std::max(lds, (size_t)4 * (RB / 32) * 32 * 4);  // the tile's dWc shares, combined in LDS
     const dim3 tg((unsigned)a.ws.n_tiles);
 #define DR_ET(FE)                                                                              \
   if (fwd) {                                                                                   \
-    if (dr_allow_big_lds(reinterpret_cast<const void*>(&vb_edge_fwd_tile<FE>))) return false;  \
+    if (dr_allow_big_lds(reinterpret_cast<const void*>(&vb_edge_fwd_tile<FE>))) return 0;      \
     hipLaunchKernelGGL(vb_edge_fwd_tile<FE>, tg, dim3(RB), lds, st, a, l);                     \
   } else {                                                                                     \
-    if (dr_allow_big_lds(reinterpret_cast<const void*>(&vb_edge_bwd_tile<FE>))) return false;  \
+    if (dr_allow_big_lds(reinterpret_cast<const void*>(&vb_edge_bwd_tile<FE>))) return 0;      \
     hipLaunchKernelGGL(vb_edge_bwd_tile<FE>, tg, dim3(RB), lds, st, a, l);                     \
   }
     switch (a.Fe) {
@@ -1015,7 +1045,7 @@ inline bool launch_edge8(bool fwd, const VA& a, int l, dim3 grid, hipStream_t st
       default: DR_ET(4) break;
     }
 #undef DR_ET
-    return true;
+    return 2;
   }
 #define DR_E8(FE)                                                                   \
   if (fwd) hipLaunchKernelGGL(vb_edge_fwd8<FE>, grid, dim3(RB), 0, st, a, l);      \
@@ -1028,7 +1058,7 @@ inline bool launch_edge8(bool fwd, const VA& a, int l, dim3 grid, hipStream_t st
     default: DR_E8(4) break;
   }
 #undef DR_E8
-  return true;
+  return 1;
 }
 
 inline int rows_grid(int64_t rows, int rows_per_block) {
@@ -1079,6 +1109,8 @@ extern "C" int dr_vanilla_graph_pass(const dr_graph_store* store, const dr_graph
         4LL * tile_carve(scratch->halo_max, scratch->tile_edges_max, scratch->tile_tedges_max, FeS, false).total > 160 * 1024)
       return DR_E_LDS;
   }
+  if (scratch->tile_wc && (!scratch->tile_row0 || !scratch->tile_first || scratch->tile_rows < 1 || WR % scratch->tile_rows))
+    return DR_E_ARG;
   if (pass->use_dropout != DR_DROPOUT_OFF) return DR_E_UNSUPPORTED;
   // no in-launch hand-offs here: the pass never faults, but it clears the
   // caller's per-launch flag like every pass that takes one (dr_pass.fault)
@@ -1112,16 +1144,21 @@ extern "C" int dr_vanilla_graph_pass(const dr_graph_store* store, const dr_graph
   if (pass->flags & DR_PASS_BACKWARD) {
     hipLaunchKernelGGL(vb_du, dim3(rows_grid(R * a.XS, RB)), dim3(RB), 0, st, a, 2);
     hipLaunchKernelGGL(vb_gemm<GM_DXS>, dim3(gg), dim3(RB), glds(GM_DXS), st, a, 2);
-    if (!launch_edge8(false, a, 2, dim3(rows_grid(R, RB / 32)), st))
-      hipLaunchKernelGGL(vb_edge_bwd, dim3(rows_grid(R, RB / 32)), dim3(RB), 0, st, a, 2);
+    // the weight-gradient chunks read tile_wc only after the tiled backward wrote it
+    VA aw = a;
+    int eb = launch_edge8(false, a, 2, dim3(rows_grid(R, RB / 32)), st);
+    if (!eb) hipLaunchKernelGGL(vb_edge_bwd, dim3(rows_grid(R, RB / 32)), dim3(RB), 0, st, a, 2);
+    if (eb != 2) aw.ws.tile_wc = nullptr;
     hipLaunchKernelGGL(vb_gemm<GM_DX1>, dim3(gg), dim3(RB), glds(GM_DX1), st, a, 2);
-    hipLaunchKernelGGL(vb_wgrad_mfma, dim3(scratch->n_chunks), dim3(RB), lds_wg, st, a, 2);
+    hipLaunchKernelGGL(vb_wgrad_mfma, dim3(scratch->n_chunks), dim3(RB), lds_wg, st, aw, 2);
     hipLaunchKernelGGL(vb_wgrad_combine, dim3(rows_grid((int64_t)n_batch * layer_grad_size(a.F, a.Fe), RB)), dim3(RB), 0, st, a, 2);
     hipLaunchKernelGGL(vb_du, dim3(rows_grid(R * a.XS, RB)), dim3(RB), 0, st, a, 1);
     hipLaunchKernelGGL(vb_gemm<GM_DXS>, dim3(gg), dim3(RB), glds(GM_DXS), st, a, 1);
-    if (!launch_edge8(false, a, 1, dim3(rows_grid(R, RB / 32)), st))
-      hipLaunchKernelGGL(vb_edge_bwd, dim3(rows_grid(R, RB / 32)), dim3(RB), 0, st, a, 1);
-    hipLaunchKernelGGL(vb_wgrad_mfma, dim3(scratch->n_chunks), dim3(RB), lds_wg, st, a, 1);
+    aw = a;
+    eb = launch_edge8(false, a, 1, dim3(rows_grid(R, RB / 32)), st);
+    if (!eb) hipLaunchKernelGGL(vb_edge_bwd, dim3(rows_grid(R, RB / 32)), dim3(RB), 0, st, a, 1);
+    if (eb != 2) aw.ws.tile_wc = nullptr;
+    hipLaunchKernelGGL(vb_wgrad_mfma, dim3(scratch->n_chunks), dim3(RB), lds_wg, st, aw, 1);
     hipLaunchKernelGGL(vb_wgrad_combine, dim3(rows_grid((int64_t)n_batch * layer_grad_size(a.F, a.Fe), RB)), dim3(RB), 0, st, a, 1);
   }
   return (int)hipGetLastError();

@@ -91,12 +91,18 @@ class BatchHandle:
             if self.vanilla_words:
                 c.edge0, c.relu_words = e0.data_ptr(), words.data_ptr()
                 if self.vanilla_tile_rows:
-                    plan = vanilla_tile_plan(self, n, row0, int(self.vanilla_tile_rows), n_edge_feat)
+                    tr = int(self.vanilla_tile_rows)
+                    plan = vanilla_tile_plan(self, n, row0, tr, n_edge_feat)
                     if plan is not None:
                         tensors, (n_tiles, hmax, emax, tmax) = plan
                         keep += tensors
                         (c.tile_row0, c.halo_off, c.halo_ids, c.lcol_off, c.lcol, c.ltcol_off, c.ltcol) = (t.data_ptr() for t in tensors)
                         c.n_tiles, c.halo_max, c.tile_edges_max, c.tile_tedges_max = n_tiles, hmax, emax, tmax
+                        if VANILLA_CHUNK % tr == 0 and 0 < n_edge_feat <= 4:  # the tiled kernels; tiles never straddle a weight-gradient chunk
+                            tfirst = torch.from_numpy(np.concatenate([[0], np.cumsum((n + tr - 1) // tr)]).astype(np.int32)).to(dev)
+                            twc = torch.empty(n_tiles * 32 * max(1, n_edge_feat), dtype=torch.float32, device=dev)
+                            keep += [tfirst, twc]
+                            c.tile_wc, c.tile_first, c.tile_rows = twc.data_ptr(), tfirst.data_ptr(), tr
             sc = (c, tuple(keep))
             self._lds[key] = sc
         return sc

@@ -446,6 +446,15 @@ typedef struct dr_vanilla_scratch {
   int32_t halo_max;           /* >= every tile's halo size (<= 65535)                        */
   int32_t tile_edges_max;     /* >= every tile's CSR edge count                               */
   int32_t tile_tedges_max;    /* >= every tile's transposed edge count                        */
+  /* Optional with the tile plan when the tile rows divide DR_VANILLA_CHUNK: the
+   * backward edge kernel then sums each tile's dWc share (sum over its rows of
+   * dS_i * eap_i, [32][Fe]) into tile_wc [n_tiles][32 * max(Fe,1)] instead of
+   * writing the per-(row, channel) eap array, and the weight-gradient chunks
+   * sum their tiles (tile_first [B+1]: first tile of each slot).           */
+  float* tile_wc;
+  const int32_t* tile_first;
+  int32_t tile_rows;
+  int32_t pad1;
 } dr_vanilla_scratch;
 #define DR_VANILLA_CHUNK 64
 

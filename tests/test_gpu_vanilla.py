@@ -171,14 +171,41 @@ def test_vanilla_captured_replay_matches_eager():
         assert torch.equal(a, b)
 
 
+def _dwc_mask(n_slab, n_graphs, fe, F=30):
+    """Slab positions of dWc (the edge-attribute columns of both layers' edge
+    MLP weight) in graph rows 0..n_graphs-1 of an n_slab-float slab: tiles that
+    divide the 64-row weight-gradient chunks sum them per tile first, another
+    fp32 order than the per-row path."""
+    KE = 2 * F + fe
+    LG = 32 * KE + 32 + F * (F + 32) + F
+    wc = np.zeros(n_slab, bool)
+    for b in range(n_graphs):
+        for lay in range(2):
+            for c in range(32):
+                o = b * 2 * LG + lay * LG + c * KE + 2 * F
+                wc[o : o + fe] = True
+    return torch.from_numpy(wc)
+
+
+def _assert_same(res, wc=None):
+    """Every tensor bit for bit, except the slab's dWc entries (wc) at 1e-5 of their scale."""
+    import itertools
+
+    for k, (a, b) in enumerate(itertools.zip_longest(*res)):
+        if k == 1 and wc is not None:
+            assert torch.equal(a[~wc], b[~wc])
+            np.testing.assert_allclose(a[wc].numpy(), b[wc].numpy(), rtol=0, atol=1e-5 * float(b[wc].abs().max()))
+        else:
+            assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("fe", [3, 6])
 def test_vanilla_pipeline_relu_words_bit_identical_to_recomputed(fe):
     """The pipeline's backward reading the forward's per-edge ReLU words
     (vb_edge_bwd8 for Fe <= 4, vb_edge_bwd for more) gives exactly the
     outputs, slabs and head vectors of the backward that recomputes every
-    activation (same decisions, same sums, same order)."""
-    import itertools
-
+    activation (same decisions, same sums, same order; the words path's
+    16-row tiles sum dWc per tile first, compared at fp32 tolerance)."""
     from deeprank2_amd import _lib
 
     datas = _datas(3, seed=46, n_lo=600, n_hi=900, mean_degree=14.0)
@@ -199,8 +226,7 @@ def test_vanilla_pipeline_relu_words_bit_identical_to_recomputed(fe):
         amd.graph_pass(m, h, m.ordered_params(), 1, _lib.DR_PASS_FORWARD | _lib.DR_PASS_BACKWARD, loss_kind=_lib.DR_LOSS_MSE, loss_scale=0.3, out=out, slab=slab, head=head)
         torch.cuda.synchronize()
         res.append((out.cpu(), slab.cpu(), head.cpu()))
-    for a, b in itertools.zip_longest(*res):
-        assert torch.equal(a, b)
+    _assert_same(res, _dwc_mask(res[0][1].numel(), len(datas), fe) if fe <= 4 else None)
 
 
 @pytest.mark.parametrize("fe,tile", [(3, 64), (1, 32), (4, 128)])
@@ -208,9 +234,8 @@ def test_vanilla_pipeline_halo_tiles_bit_identical(fe, tile):
     """The tiled edge kernels (each tile's halo rows, edge attributes, words and
     halo-local columns staged in LDS) give exactly the outputs, slabs, head
     vectors and ReLU words of the untiled 8-in-flight kernels, on atom-size
-    graphs, a small graph, a node without edges and a hub row."""
-    import itertools
-
+    graphs, a small graph, a node without edges and a hub row (tiles dividing
+    the 64-row weight-gradient chunks: dWc at fp32 tolerance, _assert_same)."""
     from deeprank2_amd import _lib
 
     datas = _datas(2, seed=47, n_lo=900, n_hi=1300, mean_degree=15.0) + _datas(1, seed=48, n_lo=20, n_hi=30)
@@ -237,5 +262,4 @@ def test_vanilla_pipeline_halo_tiles_bit_identical(fe, tile):
         c, keep = h.vanilla_scratch(30, fe)
         assert (c.n_tiles > 0) == (t > 0)
         res.append((out.cpu(), slab.cpu(), head.cpu(), keep[4].cpu()))
-    for a, b in itertools.zip_longest(*res):
-        assert torch.equal(a, b)
+    _assert_same(res, _dwc_mask(res[0][1].numel(), len(datas), fe) if 64 % tile == 0 else None)
