@@ -348,8 +348,8 @@ __device__ __forceinline__ void mm_w(int M, AF A, const float* frag, BF Bp, EF e
 
 // C[M, Nn] = sum_k A(m, k) B(k, n), both operands in LDS (weight gradients,
 // K = the graph's node count), 16x16 tiles over the waves (job j on wave
-// (start + j) % NW, so two GEMMs of a phase can share the waves).  A / B must
-// return 0 for k >= the true K (K is rounded up to 8: two accumulator chains).
+// (start + j) % NW, so two GEMMs of a phase can share the waves).  A / B are
+// called with k < K only.
 template <class AF, class BF, class EF>
 __device__ __forceinline__ void mm16(int M, int Nn, int K, int start, AF A, BF Bf, EF epi) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, kq = lane >> 4;
@@ -358,14 +358,18 @@ __device__ __forceinline__ void mm16(int M, int Nn, int K, int start, AF A, BF B
     const int m0 = (job / ntl) << 4, n0 = (job % ntl) << 4;
     const int am = min(m0 + li, M - 1), bn = min(n0 + li, Nn - 1);
     floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-    // four 8-deep k-steps per iteration, their operand reads issued together
-    // (A / B return 0 for k >= K, so the last group may run past K)
+    // four 8-deep k-steps per iteration, their operand reads issued together;
+    // past K the reads take row K-1 (so a caller's own k < K guard folds away
+    // and every read is an unconditional LDS load) and the operands are zeroed
     for (int k = 0; k < K; k += 32) {
       float av[8], bv[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        av[u] = A(am, k + 4 * u + kq);
-        bv[u] = Bf(k + 4 * u + kq, bn);
+        const int kk = k + 4 * u + kq, kc = min(kk, K - 1);
+        av[u] = A(am, kc);
+        bv[u] = Bf(kc, bn);
+        av[u] = kk < K ? av[u] : 0.f;
+        bv[u] = kk < K ? bv[u] : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < 8; u += 2) {
