@@ -32,7 +32,7 @@ struct alignas(64) ParamRec {
   float* m;
   float* v;
   int32_t numel, kind, off1, off2;
-  int32_t cols, pad0, pad1, pad2;
+  int32_t cols, mbase, pad1, pad2;  // mbase: flat index of element 0 (dr_adam.mirror_idx)
 };
 
 struct alignas(64) ReduceHdr {
@@ -50,6 +50,10 @@ struct alignas(64) ReduceHdr {
   int32_t n_params, n_blocks;
   int16_t blk0[DR_MAX_PARAMS + 1];  // first block of each parameter (prefix sums of ceil(numel / RP)), blk0[n_params] = n_blocks
   int32_t slab_rows;  // slab rows per graph (>= 1): a slab-kind gradient sums B * slab_rows rows
+  float* mirror;            // dr_adam.mirror / mirror_idx: packed copies of updated elements
+  const int4* mirror_idx;
+  uint32_t* fault_clear;    // dr_adam.fault_clear / ticket (stand-alone reduce kernel only)
+  uint32_t* ticket;
 };
 
 typedef __attribute__((address_space(1))) unsigned int gu32r;
@@ -84,7 +88,8 @@ __device__ __forceinline__ void reduce_block(const ReduceHdr& h, const ParamRec&
   const bool live = e < r.numel;
   // a graph pass whose in-launch hand-off gave up (dr_pass.fault): its
   // partials are wrong, so the step reports NaN and changes no state
-  const bool bad = !LEAN && h.fault && *h.fault != 0u;
+  const uint32_t fv = (!LEAN && h.fault) ? *h.fault : 0u;
+  const bool bad = fv != 0u;
   if (first && t < 64 && h.lpg && h.loss_out) {
     float acc = 0.f;  // lane-strided partial sums, then a fixed-order wave reduction
     for (int b = t; b < h.B; b += 64) acc += ld_part<LD>(h.lpg + b);
@@ -113,10 +118,12 @@ __device__ __forceinline__ void reduce_block(const ReduceHdr& h, const ParamRec&
   }
   const bool upd = live && ch == 0 && (LEAN || h.adam_enabled) && !bad;
   float p0 = 0.f, m0 = 0.f, v0 = 0.f, gin = 0.f;
+  int4 mi = make_int4(-1, -1, -1, -1);  // dr_adam.mirror slots of this element, loaded with the state
   if (ch == 0 && (LEAN || h.adam_enabled) && r.numel > 0) {  // numel 0: an empty record (no pointers)
     p0 = r.param[ec];
     m0 = r.m[ec];
     v0 = r.v[ec];
+    if (!LEAN && h.mirror) mi = h.mirror_idx[r.mbase + ec];
   }
   float div = 1.f;
   if (!LEAN && ch == 0 && !h.slab && r.grad) {
@@ -148,6 +155,15 @@ __device__ __forceinline__ void reduce_block(const ReduceHdr& h, const ParamRec&
   }
   __syncthreads();
   if (ch != 0 || !live) return;
+  // dr_adam.fault_clear: lane 0 of each block takes a ticket once its read of
+  // the flag has returned; the last block's lane 0 clears the flag (every
+  // block has read it by then) for the next graph pass
+  const bool tick = !LEAN && h.fault_clear && lp == 0;
+  uint32_t tk = 0u;
+  if (tick) {
+    asm volatile("" ::"v"(fv) : "memory");
+    tk = __hip_atomic_fetch_add(h.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   float gsum;
   if (LEAN || h.slab) {
     gsum = 0.f;
@@ -181,7 +197,18 @@ __device__ __forceinline__ void reduce_block(const ReduceHdr& h, const ParamRec&
     r.m[e] = mv;
     r.v[e] = vv;
     const float denom = __fadd_rn(__fdiv_rn(sqrtf(vv), bc2s), h.eps);
-    r.param[e] = fmaf(-(h.lr / bc1), __fdiv_rn(mv, denom), p0);
+    const float pn = fmaf(-(h.lr / bc1), __fdiv_rn(mv, denom), p0);
+    r.param[e] = pn;
+    if (!LEAN && h.mirror) {
+      if (mi.x >= 0) h.mirror[mi.x] = pn;
+      if (mi.y >= 0) h.mirror[mi.y] = pn;
+      if (mi.z >= 0) h.mirror[mi.z] = pn;
+      if (mi.w >= 0) h.mirror[mi.w] = pn;
+    }
+  }
+  if (tick && tk == (uint32_t)h.n_blocks - 1u) {
+    *h.fault_clear = 0u;
+    *h.ticket = 0u;
   }
 }
 
@@ -215,7 +242,14 @@ inline int build_reduce(const dr_param_table* t, const float* slab, const float*
   h.bias_c2_sqrt = adam->bias_c2_sqrt;
   h.log2_beta1 = (float)std::log2((double)adam->beta1);
   h.log2_beta2 = (float)std::log2((double)adam->beta2);
-  int blocks = 0;
+  if ((adam->mirror == nullptr) != (adam->mirror_idx == nullptr)) return DR_E_ARG;
+  if (adam->mirror_idx && (reinterpret_cast<uintptr_t>(adam->mirror_idx) & 15)) return DR_E_ARG;
+  if (adam->fault_clear && !adam->ticket) return DR_E_ARG;
+  h.mirror = adam->mirror;
+  h.mirror_idx = reinterpret_cast<const int4*>(adam->mirror_idx);
+  h.fault_clear = adam->fault_clear;
+  h.ticket = adam->ticket;
+  int blocks = 0, mbase = 0;
   for (int i = 0; i < t->n_params; ++i) {
     if (t->numel[i] < 0 || !t->param[i]) return DR_E_ARG;
     if (adam->enabled && (!t->exp_avg[i] || !t->exp_avg_sq[i])) return DR_E_ARG;
@@ -233,6 +267,8 @@ inline int build_reduce(const dr_param_table* t, const float* slab, const float*
     pr.off1 = r.off1;
     pr.off2 = r.off2;
     pr.cols = r.cols;
+    pr.mbase = mbase;
+    mbase += t->numel[i];
     h.blk0[i] = (int16_t)blocks;
     blocks += (t->numel[i] + RP - 1) / RP;
   }

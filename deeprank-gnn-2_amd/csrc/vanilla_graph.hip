@@ -1094,6 +1094,20 @@ extern "C" int64_t dr_vanilla_fused_scratch_floats(int32_t n_nodes, int32_t n_ed
 
 extern "C" int64_t dr_vanilla_wpack_floats(void) { return WPACK_FLOATS; }
 
+extern "C" int dr_vanilla_wpack(const dr_vanilla_weights* w, int32_t n_feat, int32_t n_edge_feat, float* wpack,
+                                void* stream) {
+  if (!w || !wpack) return DR_E_ARG;
+  if (n_feat < 1 || n_feat > 32 || n_edge_feat < 0 || n_edge_feat > MAXFE) return DR_E_UNSUPPORTED;
+  PackArgs pa;
+  pa.w = *w;
+  pa.out = wpack;
+  pa.fault = nullptr;
+  pa.F = n_feat;
+  pa.Fe = n_edge_feat;
+  hipLaunchKernelGGL(vanilla_pack_kernel, dim3((WPACK_FLOATS + 255) / 256), dim3(256), 0, (hipStream_t)stream, pa);
+  return (int)hipGetLastError();
+}
+
 extern "C" int dr_vanilla_fused_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
                                      const dr_vanilla_weights* w, const dr_pass* pass, float* scratch,
                                      const int64_t* scratch_off, int32_t split, uint32_t* sync, float* wpack,
@@ -1132,7 +1146,7 @@ extern "C" int dr_vanilla_fused_pass(const dr_graph_store* store, const dr_graph
   a.wpack = wpack;
   a.B = n_batch;
   a.k = split;
-  {
+  if (!(pass->flags & DR_PASS_WPACK_CURRENT)) {
     PackArgs pa;
     pa.w = *w;
     pa.out = wpack;

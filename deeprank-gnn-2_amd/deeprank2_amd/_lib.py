@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), os.environ.g
 
 DR_PASS_FORWARD = 1
 DR_PASS_BACKWARD = 2
+DR_PASS_WPACK_CURRENT = 4
 DR_LOSS_NONE = 0
 DR_LOSS_MSE = 1
 DR_LOSS_CE = 2
@@ -190,6 +191,10 @@ class AdamC(ctypes.Structure):
         ("step_counter", VP),
         ("grad_div", VP),
         ("fault", VP),
+        ("mirror", VP),
+        ("mirror_idx", VP),
+        ("fault_clear", VP),
+        ("ticket", VP),
     ]
 
 
@@ -234,6 +239,7 @@ SIGNATURES = [
     ("dr_vanilla_part_floats", ctypes.c_int64, [ctypes.c_int32] * 2),
     ("dr_vanilla_fused_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(VanillaWeightsC), ctypes.POINTER(PassC), VP, VP, ctypes.c_int32, VP, VP, ctypes.c_int32, VP]),
     ("dr_vanilla_wpack_floats", ctypes.c_int64, []),
+    ("dr_vanilla_wpack", ctypes.c_int, [ctypes.POINTER(VanillaWeightsC), ctypes.c_int32, ctypes.c_int32, VP, VP]),
     ("dr_vanilla_fused_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 3),
     ("dr_vanilla_fused_scratch_floats", ctypes.c_int64, [ctypes.c_int32] * 3),
     ("dr_fout_graph_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(FoutWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, VP]),

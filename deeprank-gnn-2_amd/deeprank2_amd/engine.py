@@ -93,6 +93,16 @@ class FusedTrainStep:
         # Off by default: measured slower at B=64 (24.7 vs 20.6 us/step)
         self.fuse_update = False
         self.sync = torch.zeros(4, dtype=torch.int32, device=dev)  # its arrival counters, left zero
+        # models whose graph pass reads its weights from a packed copy
+        # (VanillaNetwork: MFMA-fragment order): one copy per step object,
+        # rewritten by Adam as it updates the parameters (dr_adam.mirror), so
+        # the pass needs no pack launch (DR_PASS_WPACK_CURRENT); repacked when
+        # the parameters change outside the step (torch's version counters).
+        # The Adam call that follows such a pass also clears its fault flag
+        # (dr_adam.fault_clear), which the pack launch used to do.
+        self.wpack = None  # (buffer, mirror_idx, refresh), made on first use
+        self._wpack_ver = None
+        self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
         if getattr(model, "_drop_seed", 0) is None:
             model._drop_seed = int(torch.randint(0, 2**62, (1,)).item())
         self._cap = 0
@@ -147,6 +157,40 @@ class FusedTrainStep:
         self._adam_off.fault = self.fault.data_ptr()
         self._adam_div = _lib.AdamC.from_buffer_copy(a)
         self._adam_div.grad_div = self.wsum.data_ptr()
+        self._wire_packed()
+
+    def _wire_packed(self):
+        """The updating Adam calls (not the gradients-only one before an
+        all-reduce) rewrite the packed copy and clear the pass's fault flag
+        (N>1: after the flag was copied into the all-reduced buffer)."""
+        if self.wpack is None:
+            return
+        for a in (self._adam, self._adam_div):
+            a.mirror, a.mirror_idx = self.wpack[0].data_ptr(), self.wpack[1].data_ptr()
+            a.fault_clear, a.ticket = self.fault.data_ptr(), self.ticket.data_ptr()
+
+    packed_mirror = True  # False: the pass packs the weights itself every launch (A/B switch)
+
+    def _packed(self):
+        """The packed weight copy, current for the parameters as they are now
+        (None: the model has none, or ``packed_mirror`` is off)."""
+        if not self.packed_mirror or getattr(self.spec, "wpack", None) is None:
+            return None
+        ver = tuple(p._version for p in self.params)
+        if self.wpack is None:
+            self.wpack = self.spec.wpack(self.params)
+            self._wpack_ver = ver
+            self._wire_packed()
+        elif ver != self._wpack_ver:  # changed outside the step (load_state_dict, an optimizer, ...)
+            self.wpack[2]()
+            self._wpack_ver = ver
+        return self.wpack[0]
+
+    def refresh_packed(self):
+        """Repack the model's packed weight copy from the parameters now."""
+        if self.wpack is not None:
+            self.wpack[2]()
+            self._wpack_ver = tuple(p._version for p in self.params)
 
     def loss_scale(self, h: BatchHandle, global_batch):
         """Factor of the per-graph loss terms: 1/B (MSE: 1/(B*out)), or for a
@@ -207,7 +251,7 @@ class FusedTrainStep:
                 ev.append((e0, e1))
             self.step_count += 1
             return self.loss_out, self.out[: h.B]
-        launch(self.spec, h, self._w, p)
+        launch(self.spec, h, self._w, p, wpack=self._packed())
         if ev is not None:
             e1.record()
             ev.append((e0, e1))
@@ -340,7 +384,8 @@ class FusedTrainStep:
         self._build_structs()
 
     def _state_tensors(self):
-        return [*self.params, *[s for st in self.states for s in st], self.counter, self.flat, self.fault]
+        packed = [] if self.wpack is None else [self.wpack[0]]
+        return [*self.params, *[s for st in self.states for s in st], self.counter, self.flat, self.fault, *packed]
 
     def capture_sweep(self, handles, global_batch=None):
         """Capture one training step per handle, in order, into ONE HIP graph
@@ -349,6 +394,7 @@ class FusedTrainStep:
         left as before the call."""
         for h in handles:
             self._ensure(h.B)
+        self._packed()  # made before the snapshot, so the restore covers it
         snap = [t.detach().clone() for t in self._state_tensors()]
         n = self.step_count
         for h in handles:  # warm-up: LDS attributes, plans, allocator
@@ -415,9 +461,13 @@ class FusedTrainStep:
 
         Replaying it runs the same launches (plus the all-reduce for N>1) with
         no host work; the device counter advances the dropout offset and
-        Adam's step on every replay.  Capturing does not change the training
+        Adam's step on every replay.  (A model with a packed weight copy —
+        VanillaNetwork — reads it as the replays' Adam leaves it: parameters
+        changed outside the graph between replays need a ``step()`` or
+        ``refresh_packed()`` first.)  Capturing does not change the training
         state (the warm-up step it needs is rolled back)."""
         self._ensure(h.B)
+        self._packed()  # made before the snapshot, so the restore covers it
         snap = [t.detach().clone() for t in self._state_tensors()]
         n = self.step_count
         self.step(h, global_batch=global_batch, dropout=dropout)  # warm-up: LDS attribute, allocator

@@ -345,6 +345,7 @@ class FusedSpec:
     step_entry: str | None = None  # one-launch training step (graph pass + reduce + Adam), world of one
     handoffs: bool = False  # the graph pass hands rows between workgroups in-launch (dr_pass.fault can be set)
     sibling: Callable | None = None  # (handle, weights, pass, lds, k): the per-graph kernel over k workgroups per graph
+    wpack: Callable | None = None  # params -> (packed weights, dr_adam.mirror_idx, refresh()): run(..., wpack=) takes the buffer as current
 
 
 def vanilla_fused_scratch_floats(n, e, fe):
@@ -394,11 +395,15 @@ def lds_for(spec: FusedSpec, h: BatchHandle, out_dim):
     return h.lds((spec.entry, out_dim), lambda n, e, k0, p1, k1: spec.lds(n, e, k0, p1, k1, f, alias, out_dim))
 
 
-def launch(spec: FusedSpec, h: BatchHandle, w, p):
+def launch(spec: FusedSpec, h: BatchHandle, w, p, wpack=None):
     """One graph pass on the current stream: the single-workgroup kernel when
-    the batch's largest graph fits in LDS, else the model's large-graph path."""
+    the batch's largest graph fits in LDS, else the model's large-graph path.
+    wpack: the model's packed weights, already current (``FusedSpec.wpack``)."""
     if spec.run is not None:
-        spec.run(h, w, p)
+        if wpack is not None:
+            spec.run(h, w, p, wpack=wpack)
+        else:
+            spec.run(h, w, p)
         return
     if p.compute_dtype == _lib.DR_DTYPE_BF16:
         if not spec.bf16 or spec.large is None:

@@ -118,14 +118,19 @@ def make_spec(f, fe):
         (w.we1, w.be1, w.wn1, w.bn1, w.we2, w.be2, w.wn2, w.bn2, w.g1w, w.g1b, w.g2w, w.g2b) = (p.data_ptr() for p in params)
         return w
 
-    def run(h, w, p):
+    def run(h, w, p, wpack=None):
         st = h.store
         if st.n_edge_feat != fe or st.n_feat != f:
             msg = f"batch has F={st.n_feat}, Fe={st.n_edge_feat}; the model expects F={f}, Fe={fe}"
             raise ValueError(msg)
         lib = _lib.load()
         if fused_fits(h, f, fe):  # split_k(h) workgroups per graph, graph in LDS
-            buf, offs, sync, wpack = h.vanilla_fused_scratch()
+            buf, offs, sync, own = h.vanilla_fused_scratch()
+            if wpack is None:  # the pass packs the weights into the batch's own copy first
+                wpack = own
+            else:  # the caller's copy is current (FusedTrainStep: Adam keeps it so, and clears the fault flag)
+                p = _lib.PassC.from_buffer_copy(p)
+                p.flags |= _lib.DR_PASS_WPACK_CURRENT
             lds = h.lds(("vanilla_fused", fe), lambda n, e, *_: lib.dr_vanilla_fused_lds_bytes(n, e, fe))
             _lib.check(lib.dr_vanilla_fused_pass(st.cstruct(), h.descs.data_ptr(), h.B, w, p, buf.data_ptr(), offs.data_ptr(), split_k(h, f, fe), sync.data_ptr(), wpack.data_ptr(), lds, _lib.stream_ptr(st.device)), "dr_vanilla_fused_pass")
             return
@@ -147,6 +152,39 @@ def make_spec(f, fe):
             return
         _pipeline(h, w, p)
 
+    def packed(params):
+        """FusedTrainStep's packed weight copy (dr_vanilla_wpack) and its Adam
+        mirror map: packing weights that hold 1 + their flat index yields each
+        slot's source element; element i's (at most 4) slots go to
+        mirror_idx[4i .. 4i+3], -1 padded."""
+        lib = _lib.load()
+        dev = params[0].device
+        stream = _lib.stream_ptr(dev)
+        numel = [q.numel() for q in params]
+        n = int(lib.dr_vanilla_wpack_floats())
+        probe = torch.arange(1, sum(numel) + 1, dtype=torch.float32, device=dev)
+        views = [v.view_as(q) for v, q in zip(torch.split(probe, numel), params)]
+        tmp = torch.empty(n, dtype=torch.float32, device=dev)
+        _lib.check(lib.dr_vanilla_wpack(weights(views), f, fe, tmp.data_ptr(), stream), "dr_vanilla_wpack")
+        src = tmp.round().to(torch.int64) - 1
+        slot = torch.nonzero(src >= 0).flatten()
+        el = src[slot]
+        order = torch.argsort(el, stable=True)
+        el, slot = el[order], slot[order]
+        j = torch.arange(el.numel(), device=dev) - torch.searchsorted(el, el)  # rank among the element's slots
+        if el.numel() and int(j.max()) > 3:
+            msg = "a weight element appears in more than 4 packed slots"
+            raise RuntimeError(msg)
+        idx = torch.full((sum(numel), 4), -1, dtype=torch.int32, device=dev)
+        idx[el, j] = slot.to(torch.int32)
+        buf = torch.empty(n, dtype=torch.float32, device=dev)
+
+        def refresh():
+            _lib.check(lib.dr_vanilla_wpack(weights(params), f, fe, buf.data_ptr(), _lib.stream_ptr(dev)), "dr_vanilla_wpack")
+
+        refresh()
+        return buf, idx.reshape(-1), refresh
+
     def _pipeline(h, w, p):
         st = h.store
         lib = _lib.load()
@@ -154,7 +192,7 @@ def make_spec(f, fe):
         lds = int(lib.dr_vanilla_lds_bytes(f, fe, p.out_dim))
         _lib.check(lib.dr_vanilla_graph_pass(st.cstruct(), h.descs.data_ptr(), h.B, w, p, sc, lds, _lib.stream_ptr(st.device)), "dr_vanilla_graph_pass")
 
-    return FusedSpec(PARAM_NAMES, recipe, slab_stride, head_stride, "dr_vanilla_graph_pass", weights, lambda *_: 0, dropout=0.0, run=run, slab_rows=MAX_SPLIT, slab_k=lambda h: split_k(h, f, fe), handoffs=True)
+    return FusedSpec(PARAM_NAMES, recipe, slab_stride, head_stride, "dr_vanilla_graph_pass", weights, lambda *_: 0, dropout=0.0, run=run, slab_rows=MAX_SPLIT, slab_k=lambda h: split_k(h, f, fe), handoffs=True, wpack=packed)
 
 
 FUSED_MAX_FE = 4  # vanilla_graph.hip MAXFE

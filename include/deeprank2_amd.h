@@ -141,6 +141,10 @@ typedef struct dr_ginet_weights {
 
 #define DR_PASS_FORWARD 1   /* write out[B,out]                                  */
 #define DR_PASS_BACKWARD 2  /* backprop dout (given, or from the loss) to slabs   */
+#define DR_PASS_WPACK_CURRENT 4 /* dr_vanilla_fused_pass: wpack already holds these weights
+                                   (dr_vanilla_wpack, then kept current by dr_adam.mirror):
+                                   no pack launch, and pass->fault[0] must already be zero
+                                   (dr_adam.fault_clear of the previous step's update)     */
 #define DR_LOSS_NONE 0      /* dout is an input (autograd)                       */
 #define DR_LOSS_MSE 1       /* nn.MSELoss(mean) on pred.reshape(-1)               */
 #define DR_LOSS_CE 2        /* nn.CrossEntropyLoss(mean, optional class weights)  */
@@ -498,6 +502,11 @@ int dr_vanilla_fused_pass(const dr_graph_store* store, const dr_graph_desc* desc
                           const int64_t* scratch_off, int32_t split, uint32_t* sync, float* wpack,
                           int32_t lds_bytes, void* stream);
 int64_t dr_vanilla_wpack_floats(void);
+/* wpack := the weights w of a VanillaNetwork(n_feat, ., n_edge_feat) in MFMA-fragment
+ * order (the pack launch dr_vanilla_fused_pass makes unless DR_PASS_WPACK_CURRENT).
+ * Run on weights holding 1 + their flat index it yields each wpack slot's source
+ * element (0: a constant zero), from which a caller builds dr_adam.mirror_idx.   */
+int dr_vanilla_wpack(const dr_vanilla_weights* w, int32_t n_feat, int32_t n_edge_feat, float* wpack, void* stream);
 int64_t dr_vanilla_fused_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_edge_feat);
 int64_t dr_vanilla_fused_scratch_floats(int32_t n_nodes, int32_t n_edges, int32_t n_edge_feat);
 
@@ -520,6 +529,16 @@ typedef struct dr_adam {
                             partials this call reduces): when nonzero, loss_out[0] and every
                             gradient written are NaN, and Adam leaves parameters, moments
                             and the step counter unchanged                           */
+  float* mirror;         /* optional device floats: every parameter element Adam updates is
+                            also stored to mirror[mirror_idx[4 f + j]] for each j < 4 whose
+                            index is >= 0 (f = the element's flat index over the table's
+                            parameters in order): a packed copy of the weights (e.g.
+                            dr_vanilla_fused_pass's wpack) kept current with no pack launch */
+  const int32_t* mirror_idx; /* device int32 [4 * sum numel], 16-byte aligned          */
+  uint32_t* fault_clear; /* optional device flag zeroed once every block of the call has read
+                            `fault` (the next graph pass's dr_pass.fault[0] when that pass
+                            does not clear it itself, DR_PASS_WPACK_CURRENT)           */
+  uint32_t* ticket;      /* device uint32, zero, left zero: required with fault_clear  */
 } dr_adam;
 
 /* How one parameter's gradient is assembled from the per-graph partials the

@@ -234,7 +234,9 @@ def test_handoff_timeout_is_loud_and_not_sticky():
     step._pass.spin_limit = step._pass_nodrop.spin_limit = 1  # noqa: SLF001
     loss, _ = step.step(h)
     torch.cuda.synchronize()
-    assert int(step.fault[0]) == 1 and int(step.fault[1]) >= 1
+    # fault[0] was read by the update and cleared by its last block (the next
+    # pass reads the packed weights as they are and makes no pack launch)
+    assert int(step.fault[0]) == 0 and int(step.fault[1]) >= 1 and int(step.ticket[0]) == 0
     assert torch.isnan(loss).all()
     assert all(torch.isnan(g).all() for g in step.grads)
     for a, b in zip(before, step.params):
@@ -252,3 +254,44 @@ def test_handoff_timeout_is_loud_and_not_sticky():
     with pytest.raises(RuntimeError, match="gave up"):
         step.check_faults()
     step.check_faults()  # the count was reset: no error
+
+
+def test_packed_weights_kept_current_by_adam():
+    """FusedTrainStep keeps one packed weight copy that Adam rewrites as it
+    updates the parameters (dr_adam.mirror), so the pass makes no pack launch
+    (DR_PASS_WPACK_CURRENT): steps bitwise equal to packing every launch, the
+    copy equal to a fresh pack, and parameters loaded between steps repacked
+    (torch version counters)."""
+    from deeprank2_amd import _lib
+
+    datas = _datas(16, seed=95)
+    store = _store(datas)
+    torch.manual_seed(4)
+    m1 = amd.VanillaNetwork(30, 1, 3).to(DEV)
+    m2 = amd.VanillaNetwork(30, 1, 3).to(DEV)
+    m2.load_state_dict(m1.state_dict())
+    s1, s2 = FusedTrainStep(m1.train()), FusedTrainStep(m2.train())
+    s2.packed_mirror = False
+    h1, h2 = BatchHandle(store, np.arange(16)), BatchHandle(store, np.arange(16))
+    assert amd.split_k(h1, 30, 3) > 1
+
+    def same():
+        for i in range(3):
+            l1, o1 = s1.step(h1)
+            l2, o2 = s2.step(h2)
+            assert torch.equal(l1, l2) and torch.equal(o1, o2), i
+        for a, b in zip(s1.params, s2.params):
+            assert torch.equal(a, b)
+        fresh = torch.empty_like(s1.wpack[0])
+        _lib.check(_lib.load().dr_vanilla_wpack(s1._w, 30, 3, fresh.data_ptr(), _lib.stream_ptr(DEV)), "dr_vanilla_wpack")  # noqa: SLF001
+        assert torch.equal(fresh, s1.wpack[0])
+
+    same()
+    assert s2.wpack is None
+    torch.manual_seed(7)
+    state = amd.VanillaNetwork(30, 1, 3).state_dict()
+    m1.load_state_dict(state)
+    m2.load_state_dict(state)
+    same()
+    torch.cuda.synchronize()
+    assert int(s1.ticket[0]) == 0 and int(s1.fault[0]) == 0
