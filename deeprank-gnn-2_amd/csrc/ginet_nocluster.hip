@@ -694,8 +694,19 @@ __global__ void __launch_bounds__(NT) nc_l_head(NcLargeArgs a) {
   uint64_t drop_offset = a.p.drop_offset;
   if (a.p.step_counter) drop_offset = (uint64_t)a.p.step_counter[0];
   if (tid < 64) {
+    // tiles in order, 8 tiles' loads in flight (as nc_l_combine)
+    const float* part = a.pl.base + a.L.part + tid;
+    const int te = a.pl.tile_first[b + 1], NP = nc_part(F);
     float v = 0.f;
-    for (int t = a.pl.tile_first[b]; t < a.pl.tile_first[b + 1]; ++t) v += a.pl.base[a.L.part + (int64_t)t * nc_part(F) + tid];
+    int t = a.pl.tile_first[b];
+    for (; t + 8 <= te; t += 8) {
+      float u[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) u[k] = part[(int64_t)(t + k) * NP];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v += u[k];
+    }
+    for (; t < te; ++t) v += part[(int64_t)t * NP];
     hl.g[tid] = v / (float)N;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
