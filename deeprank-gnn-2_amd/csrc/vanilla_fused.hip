@@ -572,6 +572,15 @@ __global__ void __launch_bounds__(HT) vb_head(VA a) {
     if (n < F && ch < CH) {
       const int i0 = (N * ch) / CH, i1 = (N * (ch + 1)) / CH;
       int i = i0;
+      // ~100 rows per thread on an atom graph: 24 rows' loads in flight (8
+      // made the mean a chain of ~12 memory round trips), summed in row order
+      for (; i + 24 <= i1; i += 24) {
+        float v[24];
+#pragma unroll
+        for (int u = 0; u < 24; ++u) v[u] = X2[(int64_t)(i + u) * XS + n];
+#pragma unroll
+        for (int u = 0; u < 24; ++u) acc += v[u];
+      }
       for (; i + 8 <= i1; i += 8) {  // 8 rows' loads in flight, summed in row order
         float v[8];
 #pragma unroll
@@ -656,13 +665,25 @@ __global__ void __launch_bounds__(RB) vb_du(VA a, int l) {
   const float* dx1 = a.ws.base + a.L.dx1;
   float* du = a.ws.base + a.L.du;
   const int HS = DR_VANILLA_HEAD_STRIDE(F, a.p.out_dim), HD = XS + 256 + r4(a.p.out_dim);
-  const int64_t total = a.ws.n_rows * XS;
-  for (int64_t p = blockIdx.x * (int64_t)RB + threadIdx.x; p < total; p += (int64_t)gridDim.x * RB) {
-    const int64_t r = p / XS;
+  // four consecutive columns of one row per thread (XS is a multiple of 4)
+  const int64_t total4 = a.ws.n_rows * XS / 4;
+  for (int64_t p4 = blockIdx.x * (int64_t)RB + threadIdx.x; p4 < total4; p4 += (int64_t)gridDim.x * RB) {
+    const int64_t p = p4 * 4, r = p / XS;
     const int n = (int)(p - r * XS);
-    float g = 0.f;
-    if (n < F) g = (l == 2) ? a.p.head[(int64_t)(a.p.slot ? a.p.slot[a.ws.row_slot[r]] : a.ws.row_slot[r]) * HS + HD + n] : dx1[p];
-    du[p] = n < F ? relu_bwd(xo[p], g) : 0.f;
+    const float4 x4 = *reinterpret_cast<const float4*>(xo + p);
+    float4 g4;
+    if (l == 2) {
+      const float* hg = a.p.head + (int64_t)(a.p.slot ? a.p.slot[a.ws.row_slot[r]] : a.ws.row_slot[r]) * HS + HD + n;
+      g4 = make_float4(n < F ? hg[0] : 0.f, n + 1 < F ? hg[1] : 0.f, n + 2 < F ? hg[2] : 0.f, n + 3 < F ? hg[3] : 0.f);
+    } else {
+      g4 = *reinterpret_cast<const float4*>(dx1 + p);
+    }
+    float4 o;
+    o.x = n < F ? relu_bwd(x4.x, g4.x) : 0.f;
+    o.y = n + 1 < F ? relu_bwd(x4.y, g4.y) : 0.f;
+    o.z = n + 2 < F ? relu_bwd(x4.z, g4.z) : 0.f;
+    o.w = n + 3 < F ? relu_bwd(x4.w, g4.w) : 0.f;
+    *reinterpret_cast<float4*>(du + p) = o;
   }
 }
 
@@ -1013,8 +1034,20 @@ __global__ void __launch_bounds__(RB) vb_wgrad_combine(VA a, int l) {
   const int64_t work = (int64_t)a.B * total;
   for (int64_t q = blockIdx.x * (int64_t)RB + threadIdx.x; q < work; q += (int64_t)gridDim.x * RB) {
     const int b = (int)(q / total), p = (int)(q - (int64_t)b * total);
+    // chunks in order, 8 chunks' loads in flight (an atom graph has ~50: one
+    // dependent load per chunk made this a latency chain)
+    const float* part = a.ws.part + p;
+    const int ce = a.ws.chunk_first[b + 1];
     float v = 0.f;
-    for (int ch = a.ws.chunk_first[b]; ch < a.ws.chunk_first[b + 1]; ++ch) v += a.ws.part[(int64_t)ch * total + p];
+    int ch = a.ws.chunk_first[b];
+    for (; ch + 8 <= ce; ch += 8) {
+      float u[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) u[k] = part[(int64_t)(ch + k) * total];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v += u[k];
+    }
+    for (; ch < ce; ++ch) v += part[(int64_t)ch * total];
     a.p.slab[(int64_t)(a.p.slot ? a.p.slot[b] : b) * DR_VANILLA_SLAB_STRIDE(a.F, a.Fe) + (l == 2 ? total : 0) + p] = v;
   }
 }
@@ -1142,7 +1175,7 @@ extern "C" int dr_vanilla_graph_pass(const dr_graph_store* store, const dr_graph
   }
   hipLaunchKernelGGL(vb_head, dim3(n_batch), dim3(HT), 0, st, a);
   if (pass->flags & DR_PASS_BACKWARD) {
-    hipLaunchKernelGGL(vb_du, dim3(rows_grid(R * a.XS, RB)), dim3(RB), 0, st, a, 2);
+    hipLaunchKernelGGL(vb_du, dim3(rows_grid(R * a.XS / 4, RB)), dim3(RB), 0, st, a, 2);
     hipLaunchKernelGGL(vb_gemm<GM_DXS>, dim3(gg), dim3(RB), glds(GM_DXS), st, a, 2);
     // the weight-gradient chunks read tile_wc only after the tiled backward wrote it
     VA aw = a;
@@ -1152,7 +1185,7 @@ extern "C" int dr_vanilla_graph_pass(const dr_graph_store* store, const dr_graph
     hipLaunchKernelGGL(vb_gemm<GM_DX1>, dim3(gg), dim3(RB), glds(GM_DX1), st, a, 2);
     hipLaunchKernelGGL(vb_wgrad_mfma, dim3(scratch->n_chunks), dim3(RB), lds_wg, st, aw, 2);
     hipLaunchKernelGGL(vb_wgrad_combine, dim3(rows_grid((int64_t)n_batch * layer_grad_size(a.F, a.Fe), RB)), dim3(RB), 0, st, a, 2);
-    hipLaunchKernelGGL(vb_du, dim3(rows_grid(R * a.XS, RB)), dim3(RB), 0, st, a, 1);
+    hipLaunchKernelGGL(vb_du, dim3(rows_grid(R * a.XS / 4, RB)), dim3(RB), 0, st, a, 1);
     hipLaunchKernelGGL(vb_gemm<GM_DXS>, dim3(gg), dim3(RB), glds(GM_DXS), st, a, 1);
     aw = a;
     eb = launch_edge8(false, a, 1, dim3(rows_grid(R, RB / 32)), st);
