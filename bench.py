@@ -8,8 +8,12 @@ already resident in HBM (a mini-batch is a list of graph ids).
 
     python bench.py [--gpus N --steps K --warmup W]
 
-N>1: one rank per GPU over RCCL, every rank training on its own 64 graphs per
-step (weak scaling) with one gradient all-reduce per step.  Under
+N>1: one rank per GPU over RCCL, one global batch of 64*N graphs per step
+(weak scaling), the same global batch sequence on every rank (same seed), each
+rank training on its shard of it (``distributed.plan_shards``: contiguous
+shards, or edge-balanced bin packing when that split is imbalanced, as for
+config 5's mixed residue/SRV/atom batches) with one gradient all-reduce per
+step.  Under
 torch.distributed.run (WORLD_SIZE set) this process is one rank; otherwise
 ``--gpus N`` starts ``torch.distributed.run --nproc-per-node N bench.py ...`` as
 a child process before anything touches the GPU and relays its output.
@@ -351,8 +355,38 @@ def parse_args(argv):
     ap.add_argument("--no-stream-copy", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch every step from Python instead of replaying captured HIP graphs")
     ap.add_argument("--eager-ddp", action="store_true", help="N>1: launch steps from Python (default: the RCCL all-reduce is captured in the HIP graph with the kernels)")
-    ap.add_argument("--dry-run", action="store_true", help="launcher check without a GPU: each rank joins a gloo group, rank 0 prints the JSON skeleton")
+    ap.add_argument("--shard-policy", choices=["auto", "contiguous", "edges"], default="auto", help="N>1: how each global batch is split over the ranks (distributed.plan_shards)")
+    ap.add_argument("--dry-run", action="store_true", help="launcher check without a GPU: each rank joins a gloo group, builds the global batches and its shards, rank 0 prints the JSON skeleton with the per-rank edge loads")
     return ap.parse_args(argv)
+
+
+def global_batches(args, world, rank):
+    """The run's data, identical on every rank: one synthetic set of
+    B*world*batches graphs (seed 1000), one global batch of B*world graphs per
+    resident mini-batch (a seeded permutation), and this rank's shard of each
+    (``plan_shards``).  At world 1 this is the set, order and batches the
+    single-GPU bench always used.  Returns (graphs, packed, local batches,
+    plans, B)."""
+    import numpy as np  # noqa: PLC0415
+
+    from deeprank2_amd.distributed import plan_shards  # noqa: PLC0415
+    from deeprank2_amd.store import pack_graphs  # noqa: PLC0415
+
+    B = args.batch or (32 if args.graphs == "atom" else B_PER_GPU)
+    if args.graphs in ("atom", "mixed"):
+        args.batches = min(args.batches, 4)  # generation time of ~3k-node graphs
+    bg = B * world
+    graphs = make_graphs(args.graphs, bg * args.batches, seed=1000)
+    packed = pack_graphs(records(graphs, 1 if args.model == "sgat" else 3), require_clusters=args.model not in ("ginet_nocluster", "vanilla"))
+    order = np.random.default_rng(0).permutation(packed.n_graphs).astype(np.int32)
+    edges = np.diff(packed.edge_off)
+    local, plans = [], []
+    for i in range(args.batches):
+        gb = order[i * bg:(i + 1) * bg]
+        plan = plan_shards(edges[gb], world, policy=args.shard_policy)
+        plans.append(plan)
+        local.append(gb[plan.positions[rank]])
+    return graphs, packed, local, plans, B
 
 
 def dry_run(args):
@@ -369,8 +403,17 @@ def dry_run(args):
         t = torch.ones(1)
         torch.distributed.all_reduce(t)
         assert int(t.item()) == world
-    if int(os.environ.get("RANK", "0")) == 0:
-        print(json.dumps({"metric": HEADLINE_METRIC, "value": None, "unit": "graphs/s", "n_gpus": world, "world_size": world, "backend": backend, "dry_run": True, "config": {"parallelism": f"dp{world}"}}), flush=True)
+    rank = int(os.environ.get("RANK", "0"))
+    _graphs, _packed, local, plans, B = global_batches(args, world, rank)
+    mine = [int(_packed.edge_off[g + 1] - _packed.edge_off[g]) for g in local[0]]
+    if world > 1:  # every rank's own count of its first shard, checked against rank 0's plan
+        t = torch.zeros(world, dtype=torch.int64)
+        t[rank] = sum(mine)
+        torch.distributed.all_reduce(t)
+        assert t.tolist() == list(plans[0].loads), (t.tolist(), plans[0].loads)
+    if rank == 0:
+        shards = {"policy": args.shard_policy, "balanced": [p.balanced for p in plans], "rank_graphs": [p.sizes() for p in plans], "rank_edge_loads": [list(p.loads) for p in plans]}
+        print(json.dumps({"metric": HEADLINE_METRIC, "value": None, "unit": "graphs/s", "n_gpus": world, "world_size": world, "backend": backend, "dry_run": True, "config": {"graphs": args.graphs, "graphs_per_gpu": B, "global_batch": B * world, "parallelism": f"dp{world}"}, "shards": shards}), flush=True)
     if world > 1:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
@@ -387,7 +430,7 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
     from deeprank2_amd.neuralnets.gnn.ginet_nocluster import GINet as GINetNoCluster  # noqa: PLC0415
     from deeprank2_amd.neuralnets.gnn.sgat import SGAT  # noqa: PLC0415
     from deeprank2_amd.neuralnets.gnn.vanilla_gnn import VanillaNetwork  # noqa: PLC0415
-    from deeprank2_amd.store import GraphStore, pack_graphs  # noqa: PLC0415
+    from deeprank2_amd.store import GraphStore  # noqa: PLC0415
 
     models = {"ginet": GINet, "foutnet": FoutNet, "vanilla": VanillaNetwork, "sgat": SGAT, "ginet_nocluster": GINetNoCluster}
     if args.dtype == "bf16" and args.model != "ginet":
@@ -419,14 +462,12 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
         backend = torch.distributed.get_backend()
     dev = torch.device(f"cuda:{local}")
 
-    B = args.batch or (32 if args.graphs == "atom" else B_PER_GPU)
-    if args.graphs in ("atom", "mixed"):
-        args.batches = min(args.batches, 4)  # generation time of ~3k-node graphs
-    graphs = make_graphs(args.graphs, B * args.batches, seed=1000 + rank)
-    packed = pack_graphs(records(graphs, 1 if args.model == "sgat" else 3), require_clusters=args.model not in ("ginet_nocluster", "vanilla"))
+    graphs, packed, local, plans, B = global_batches(args, world, rank)
     store = GraphStore(packed, dev, dtype=args.dtype)
-    order = np.random.default_rng(rank).permutation(packed.n_graphs).astype(np.int32)
-    handles = [BatchHandle(store, order[i * B:(i + 1) * B]) for i in range(args.batches)]
+    if any(len(g) == 0 for g in local):
+        msg = f"rank {rank}: an empty shard (global batch {B * world} over {world} ranks)"
+        raise SystemExit(msg)
+    handles = [BatchHandle(store, g) for g in local]
     for h in handles:
         h.force_large = bool(args.force_large) or args.ginet_path != "auto"
         h.large_tile = args.force_large or None
@@ -617,8 +658,11 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
                 "mean_edges_per_graph": round(float(np.diff(packed.edge_off).mean()), 1),
                 "node_features": 30,
                 "edge_features": 1 if args.model == "sgat" else 3,
-                "resident_graphs_per_gpu": packed.n_graphs,
+                "resident_graphs": packed.n_graphs,
                 "parallelism": f"dp{world}",
+                "shard_policy": args.shard_policy if world > 1 else None,
+                "shards_edge_balanced": sum(p.balanced for p in plans) if world > 1 else None,
+                "rank_edge_loads_first_batch": list(plans[0].loads) if world > 1 else None,
             },
             "roofline": {
                 "kernel": kname,

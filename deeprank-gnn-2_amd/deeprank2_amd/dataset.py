@@ -162,6 +162,7 @@ class GraphDataset:
         self._stores = {}
         self._gid = None
         self._y_cache = None
+        self._e_cache = None
 
     # ------------------------------------------------------------------ files
     def _entry(self, fname, mol):
@@ -467,6 +468,23 @@ class GraphDataset:
             return None
         return self._y_cache[torch.as_tensor(indices, dtype=torch.long)]
 
+    def edge_counts(self, indices):
+        """Directed edge count of each graph at ``indices`` (``edge_index.shape[1]``
+        as ``load_one_graph`` builds it: the stored ``_index`` rows doubled),
+        from the entries' index arrays alone; what ``Trainer`` balances ranks on."""
+        if self._e_cache is None:
+            counts = []
+            for fname, mol in self.index_entries:
+                grp = self._entry(fname, mol)
+                key = f"{EDGE}/{INDEX}"
+                if key not in grp:
+                    counts.append(0)
+                    continue
+                shape = np.shape(grp[key])
+                counts.append(2 * shape[0] if len(shape) == 2 else (shape[1] if len(shape) > 1 else 0))  # noqa: PLR2004
+            self._e_cache = np.asarray(counts, dtype=np.int64)
+        return self._e_cache[np.asarray(indices, dtype=np.int64)]
+
     def graph_store(self, device):
         """All graphs of the dataset packed once into HBM (cached per device)."""
         from deeprank2_amd.store import GraphRecord, GraphStore, pack_graphs  # noqa: PLC0415
@@ -499,4 +517,5 @@ class GraphDataset:
         out.index_entries = [self.index_entries[i] for i in positions]
         out._stores = {}
         out._y_cache = None
+        out._e_cache = None
         return out

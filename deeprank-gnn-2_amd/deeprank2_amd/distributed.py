@@ -11,6 +11,9 @@ inside ``FusedTrainStep.step``.
 * ``shard_by_edges``: greedy longest-processing-time bin packing on the edge
   counts for batches of very mixed graph sizes (config 5); the returned
   permutation restores the global order of per-graph outputs.
+* ``plan_shards``: the policy ``Trainer`` (ngpu > 1) and ``bench.py --gpus N``
+  apply to each global batch — contiguous, or edge-balanced when the
+  contiguous split is imbalanced.
 
 The reference's ``nn.DataParallel`` (trainer.py:387-389) replicates the model
 per step and gathers outputs on one device; there is no counterpart here.
@@ -19,6 +22,7 @@ per step and gathers outputs on one device; there is no counterpart here.
 from __future__ import annotations
 
 import heapq
+from dataclasses import dataclass
 
 import numpy as np
 
@@ -58,3 +62,49 @@ def shard_by_edges(gids, edges, world: int):
     perm = np.empty_like(order)
     perm[order] = np.arange(order.size)
     return shards, perm
+
+
+# a contiguous split whose busiest rank carries more than this times the mean
+# edge load is re-planned by edge-balanced bin packing (mixed graph sizes)
+IMBALANCE_LIMIT = 1.25
+
+
+@dataclass(frozen=True)
+class ShardPlan:
+    """How one global batch is spread over the ranks.
+
+    ``positions[r]``: rank r's positions in the global batch (ascending);
+    ``perm``: ``np.concatenate(per_rank_rows)[perm]`` puts rows gathered rank
+    by rank back in global-batch order; ``loads[r]``: rank r's edge count;
+    ``balanced``: the plan came from ``shard_by_edges``."""
+
+    positions: tuple
+    perm: np.ndarray
+    loads: tuple
+    balanced: bool
+
+    def sizes(self):
+        return [len(p) for p in self.positions]
+
+
+def plan_shards(edges, world: int, policy: str = "auto", imbalance: float = IMBALANCE_LIMIT) -> ShardPlan:
+    """Shard a global batch whose graphs have ``edges`` directed edges each
+    (SURVEY §8(e)): ``policy`` "contiguous" (global order, sizes differ by at
+    most one), "edges" (greedy edge bin packing) or "auto" — contiguous unless
+    its heaviest rank exceeds ``imbalance`` x the mean edge load, as a batch
+    mixing residue, SRV and ~50k-edge atom graphs does (config 5).  The plan
+    is a pure function of the edge counts, so every rank computes the same one
+    without communicating."""
+    edges = np.asarray(edges, dtype=np.int64)
+    b = edges.size
+    pos = np.arange(b, dtype=np.int32)
+    if policy not in ("auto", "contiguous", "edges"):
+        msg = f"policy must be 'auto', 'contiguous' or 'edges' (got {policy!r})"
+        raise ValueError(msg)
+    contiguous = [shard_contiguous(pos, r, world) for r in range(world)]
+    c_loads = [int(edges[p].sum()) for p in contiguous]
+    use_edges = policy == "edges" or (policy == "auto" and world > 1 and b and max(c_loads) > imbalance * (sum(c_loads) / world))
+    if not use_edges:
+        return ShardPlan(tuple(contiguous), np.arange(b, dtype=np.int64), tuple(c_loads), False)
+    shards, perm = shard_by_edges(pos, edges, world)
+    return ShardPlan(tuple(shards), perm, tuple(int(edges[s].sum()) for s in shards), True)

@@ -294,7 +294,12 @@ class FusedTrainStep:
         """Raise RuntimeError if any graph pass since the last check gave up an
         in-launch hand-off (VanillaNetwork split over workgroups whose siblings
         were not co-resident): those steps reported a NaN loss and were not
-        applied.  One device read; ``Trainer`` calls it once per epoch."""
+        applied.  One device read; ``Trainer`` calls it once per epoch.
+
+        With a process group this is a collective (every rank calls it at the
+        same point): the per-rank counts are SUM-all-reduced first, so all ranks
+        raise together instead of the faulting rank alone while the others
+        block in their next collective."""
         if self.fuse_update and int(self.sync[2].item()):
             if reset:
                 self.sync[2].zero_()
@@ -302,7 +307,10 @@ class FusedTrainStep:
             raise RuntimeError(msg)
         if not self.handoffs:
             return
-        n = int(self.fault[1].item())
+        count = self.fault[1:2].clone()
+        if self.pg is not None:
+            torch.distributed.all_reduce(count, group=self.pg)
+        n = int(count.item())
         if reset:
             self.fault[1].zero_()
         if n:

@@ -96,6 +96,18 @@ def _rebuild_tensor(zf, prefix, args):
     if raw.size != numel:
         msg = f"storage {key}: {raw.size} elements, record says {numel}"
         raise CheckpointFormatError(msg)
+    # the view's geometry comes from the (untrusted) file: every element it
+    # addresses must lie inside the storage before as_strided, which checks nothing
+    if len(size) != len(stride) or offset < 0 or any(s < 0 for s in size) or any(s < 0 for s in stride):
+        msg = f"storage {key}: invalid view (offset {offset}, size {size}, stride {stride})"
+        raise CheckpointFormatError(msg)
+    n_elem = int(np.prod(size, dtype=np.int64)) if size else 1
+    last = offset + sum((n - 1) * s for n, s in zip(size, stride)) if n_elem else offset - 1
+    if last >= raw.size:
+        msg = f"storage {key}: view (offset {offset}, size {size}, stride {stride}) reaches element {last} of {raw.size}"
+        raise CheckpointFormatError(msg)
+    if not n_elem:
+        return torch.from_numpy(np.zeros(size, dtype=dt))
     arr = np.lib.stride_tricks.as_strided(raw[offset:], shape=size, strides=tuple(s * raw.itemsize for s in stride)) if size else raw[offset : offset + 1].reshape(())
     return torch.from_numpy(np.array(arr, copy=True))
 

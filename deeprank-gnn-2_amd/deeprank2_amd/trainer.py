@@ -45,7 +45,7 @@ from torch import nn
 from torch.nn.functional import softmax
 
 from deeprank2_amd.dataset import CLASSIF, REGRESS, GraphDataset
-from deeprank2_amd.distributed import shard_contiguous
+from deeprank2_amd.distributed import plan_shards
 from deeprank2_amd.engine import FusedTrainStep
 from deeprank2_amd.io.checkpoint import load_checkpoint
 from deeprank2_amd.exporters import HDF5OutputExporter, OutputExporterCollection
@@ -66,6 +66,10 @@ _LOSSES = {c.__name__: c for c in regression_losses + classification_losses + ot
 
 
 class Trainer:
+    # ngpu > 1: how a global batch is spread over the ranks (distributed.plan_shards):
+    # "auto" (contiguous unless imbalanced by edges), "contiguous" or "edges"
+    shard_policy = "auto"
+
     def __init__(  # noqa: PLR0913, PLR0912, C901
         self,
         neuralnet: type[nn.Module] | None = None,
@@ -326,11 +330,20 @@ class Trainer:
             store._dr_class_index = dict(self.classes_to_index)  # noqa: SLF001
         return store
 
-    def _local(self, idx):
+    def _shard(self, ds, idx):
+        """This rank's share of the global batch ``idx`` and the plan behind it
+        (replacing nn.DataParallel's replicate/scatter,
+        trainer.py:387-389): contiguous shards in global order, or — when that
+        split leaves one rank more than 1.25x the mean edge load, as in a batch
+        mixing residue, SRV and atom-level graphs (config 5) — greedy edge
+        bin packing; every rank derives the same plan from the edge counts.
+        Returns (local positions, plan); (idx, None) without a process group."""
         if self.process_group is None:
-            return idx
+            return np.asarray(idx), None
         pg = self.process_group  # the group's own rank / size (a subgroup need not start at global rank 0)
-        return shard_contiguous(idx, torch.distributed.get_rank(pg), torch.distributed.get_world_size(pg))
+        idx = np.asarray(idx)
+        plan = plan_shards(ds.edge_counts(idx), torch.distributed.get_world_size(pg), policy=self.shard_policy)
+        return idx[plan.positions[torch.distributed.get_rank(pg)]], plan
 
     def _format_output(self, pred, target=None):
         """trainer.py:807-835."""
@@ -415,7 +428,10 @@ class Trainer:
                     history["validation"].append(self._eval(self.valid_loader, epoch, "validation"))
                 seen = history[monitored]
                 if best_model and min(seen) == seen[-1]:
+                    # as trainer.py:628-631: the snapshot first, then the
+                    # attribute, so a checkpoint records the previous best epoch
                     kept = (self._save_model(), epoch)
+                    self.epoch_saved_model = epoch
                 if validate and stopper is not None:
                     stopper(epoch, history["validation"][-1], history["training"][-1])
                     if stopper.early_stop:
@@ -448,7 +464,7 @@ class Trainer:
         for idx in self.train_loader.batches():
             b = len(idx)
             if step is not None:
-                local = self._local(idx)
+                local, plan = self._shard(ds, idx)
                 if len(local):
                     loss, out = step.step(ds.batch_handle(local, dev), global_batch=b)
                 else:  # global batch smaller than the world
@@ -456,7 +472,7 @@ class Trainer:
                 loss_sum += loss[0].double() * b
                 pred = out.clone()
                 if self.process_group is not None:
-                    pred = _gather_rows(pred, b, self.process_group)
+                    pred = _gather_rows(pred, plan, self.process_group)
                 pred, y = self._format_output(pred, ds._targets_of(idx))  # noqa: SLF001
             elif self.process_group is not None:
                 pred, y, loss = self._generic_ddp_step(ds, idx)
@@ -493,7 +509,7 @@ class Trainer:
         takes the same optimizer step.  Returns the global predictions,
         targets and loss."""
         pg = self.process_group
-        local = self._local(idx)
+        local, plan = self._shard(ds, idx)
         self.optimizer.zero_grad()
         if len(local):
             batch = ds.batch(local).to(self.device)
@@ -508,8 +524,8 @@ class Trainer:
             cls = torch.tensor([self.classes_to_index[int(v)] for v in y_all.tolist()])
             wh = w.detach().cpu()
             total = float(wh[cls].sum())  # the weighted mean's denominator over the global batch
-            local_pos = shard_contiguous(np.arange(len(idx)), torch.distributed.get_rank(pg), torch.distributed.get_world_size(pg))
-            frac = float(wh[cls[local_pos]].sum()) / total if total else 0.0
+            local_pos = plan.positions[torch.distributed.get_rank(pg)]
+            frac = float(wh[cls[torch.as_tensor(local_pos, dtype=torch.long)]].sum()) / total if total else 0.0
         else:
             frac = len(local) / len(idx)
         if len(local):
@@ -528,7 +544,7 @@ class Trainer:
             p.grad.copy_(flat[off:off + n].view_as(p))
             off += n
         self.optimizer.step()
-        pred_all = _gather_rows(pred.detach().contiguous(), len(idx), pg)
+        pred_all = _gather_rows(pred.detach().contiguous(), plan, pg)
         pred_all, y = self._format_output(pred_all, y_all)
         return pred_all, y, flat[-1]
 
@@ -650,13 +666,20 @@ class Trainer:
         self.model.load_state_dict(self.model_load_state_dict)
 
 
-def _gather_rows(local, b, pg):
-    """All ranks' [b_r, out] predictions in global order (contiguous shards)."""
-    world = torch.distributed.get_world_size(pg)
-    sizes = [len(shard_contiguous(np.arange(b), r, world)) for r in range(world)]
-    bufs = [torch.empty(s, local.shape[1], dtype=local.dtype, device=local.device) for s in sizes]
-    torch.distributed.all_gather(bufs, local.contiguous(), group=pg)
-    return torch.cat(bufs)
+def _gather_rows(local, plan, pg):
+    """All ranks' [b_r, out] predictions, put back in global-batch order by the
+    shard plan's permutation (the exporters see the reference's row order)."""
+    sizes = plan.sizes()
+    top = max(sizes)
+    # padded to the largest shard: gloo's all_gather takes equal sizes only
+    pad = torch.zeros(top, local.shape[1], dtype=local.dtype, device=local.device)
+    pad[: local.shape[0]] = local
+    bufs = [torch.empty_like(pad) for _ in sizes]
+    torch.distributed.all_gather(bufs, pad, group=pg)
+    rows = torch.cat([buf[:s] for buf, s in zip(bufs, sizes)])
+    if plan.balanced:
+        rows = rows[torch.as_tensor(plan.perm, dtype=torch.long, device=rows.device)]
+    return rows
 
 
 def _divide_dataset(dataset, splitsize=None, process_group=None):

@@ -47,7 +47,39 @@ def _kmeans(rng, pos, k, iters=8):
     return lab.astype(np.int64)
 
 
-def make_graph(rng, n_lo=180, n_hi=220, mean_degree=15.0, k_lo=2, k_hi=6, n_feat=30, task="regress"):
+KD_MIN_NODES = 400  # contact search through a k-d tree above this many nodes (same pairs, faster)
+
+
+def _contacts(pos, n_pairs, kd_min_nodes=KD_MIN_NODES):
+    """The ``n_pairs`` closest residue pairs (i < j), in (i, j) order, and their
+    distances.  Small graphs: every pair's distance, then a partition.  Large
+    (atom-level) graphs: the pairs within a radius grown until it holds
+    ``n_pairs`` of them (scipy k-d tree), then the same partition on those —
+    the same pairs and the same float64 distances as the dense form (barring an
+    exact distance tie at the cut), ~10x faster at N = 3000."""
+    n = pos.shape[0]
+    if n < kd_min_nodes:
+        iu, ju = np.triu_indices(n, k=1)
+    else:
+        from scipy.spatial import cKDTree  # noqa: PLC0415
+
+        tree = cKDTree(pos)
+        r = 4.0
+        while True:
+            pairs = tree.query_pairs(r, output_type="ndarray")
+            if len(pairs) >= n_pairs or len(pairs) == n * (n - 1) // 2:
+                break
+            r *= 1.3
+        pairs = pairs[np.lexsort((pairs[:, 1], pairs[:, 0]))]
+        iu, ju = pairs[:, 0].astype(np.int64), pairs[:, 1].astype(np.int64)
+    d = np.linalg.norm(pos[iu] - pos[ju], axis=1)
+    n_pairs = max(1, min(n_pairs, d.size))
+    sel = np.argpartition(d, n_pairs - 1)[:n_pairs]
+    sel.sort()
+    return np.stack([iu[sel], ju[sel]], axis=1).astype(np.int64), d[sel]
+
+
+def make_graph(rng, n_lo=180, n_hi=220, mean_degree=15.0, k_lo=2, k_hi=6, n_feat=30, task="regress", kd_min_nodes=KD_MIN_NODES):
     """One synthetic graph as a dict of numpy arrays (HDF5-entry layout)."""
     n = int(rng.integers(n_lo, n_hi + 1))
     na = n // 2
@@ -57,14 +89,9 @@ def make_graph(rng, n_lo=180, n_hi=220, mean_degree=15.0, k_lo=2, k_hi=6, n_feat
     pos = np.concatenate([pos_a, pos_b]).astype(np.float64)
     chain = np.concatenate([np.zeros(na, np.int64), np.ones(nb, np.int64)])
 
-    iu, ju = np.triu_indices(n, k=1)
-    d = np.linalg.norm(pos[iu] - pos[ju], axis=1)
     n_pairs = int(round(mean_degree * n / 2 * rng.uniform(0.9, 1.1)))
-    n_pairs = max(1, min(n_pairs, d.size))
-    sel = np.argpartition(d, n_pairs - 1)[:n_pairs]
-    sel.sort()
-    index = np.stack([iu[sel], ju[sel]], axis=1).astype(np.int64)
-    dist = d[sel]
+    n_pairs = max(1, min(n_pairs, n * (n - 1) // 2))
+    index, dist = _contacts(pos, n_pairs, kd_min_nodes)
     same_chain = (chain[index[:, 0]] == chain[index[:, 1]]).astype(np.float64)
     covalent = ((dist < 2.1) & (same_chain > 0)).astype(np.float64)
 

@@ -187,11 +187,15 @@ typedef struct dr_pass {
                            step's launch arguments constant (hipGraph replay).            */
   uint32_t* fault;      /* optional device [2], passes with in-launch hand-offs between
                            workgroups (dr_vanilla_fused_pass, split > 1): fault[0] is cleared
-                           at the start of every launch and set to 1 when one of its
+                           by the pass's pack launch and set to 1 when one of its
                            hand-off waits gave up (its partials are then wrong); fault[1]
                            counts such launches and is only ever cleared by the caller.
                            Hand the same pointer to dr_adam.fault so the step's update
-                           is withheld and its loss reads NaN.                            */
+                           is withheld and its loss reads NaN.  With DR_PASS_WPACK_CURRENT
+                           there is no pack launch: the caller must clear fault[0] itself,
+                           normally through the previous update's dr_adam.fault_clear (+
+                           ticket); otherwise one give-up stays set and every later step is
+                           withheld with a NaN loss.                                      */
   int32_t spin_limit;   /* polls before a hand-off wait gives up (<= 0: 1 << 22)        */
   int32_t pad0;
   const int32_t* slot;  /* optional device [B] (GINet / FoutNet / SGAT passes): launch position b

@@ -20,7 +20,11 @@ Contents
                ``deeprank2/utils/community_pooling.py``.
 ``data_ref``   restatement of ``GraphDataset.load_one_graph`` + PyG collate over
                the ``.npz`` dump of the HDF5 fixtures.
-``synth``      seeded synthetic residue-PPI graph generator.
+``mcl_ref``    numpy restatement of networkx's adjacency + markov_clustering
+               0.0.6 ``run_mcl`` / ``get_clusters`` (``Trainer._precluster``).
+
+(The seeded synthetic graph generator of SURVEY.md §8(d) is not oracle code: it
+lives in the package, ``deeprank2_amd.utils.synthetic``.)
 
 Pinning: ``gnn_ref`` and ``pyg_ops`` are checked in ``tests/test_oracle.py``
 against golden vectors produced by importing the *reference's own*

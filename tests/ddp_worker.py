@@ -9,7 +9,11 @@ from a captured HIP graph (all-reduce included).  Writes the final parameters
 (rank 0).  DR_DDP_EMULATE=n (one process, no group): each global batch's n
 shards run one after another, their gradient buffers summed in rank order
 (what the all-reduce computes), then one Adam update; for n = 2 the same
-bits as two ranks, since a two-operand sum does not depend on the order."""
+bits as two ranks, since a two-operand sum does not depend on the order.
+DR_DDP_GRAPHS=mixed: global batches of residue, SRV and atom-level graphs
+(config 5), sharded by ``plan_shards`` (edge-balanced); rank 0 also writes the
+last step's predictions gathered back into global-batch order (the Trainer's
+``_gather_rows``)."""
 
 from __future__ import annotations
 
@@ -23,7 +27,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from deeprank2_amd.distributed import shard_contiguous  # noqa: E402
+from deeprank2_amd.distributed import plan_shards  # noqa: E402
 from deeprank2_amd.engine import FusedTrainStep  # noqa: E402
 from deeprank2_amd.fused import BatchHandle  # noqa: E402
 from deeprank2_amd.neuralnets.gnn.foutnet import FoutNet  # noqa: E402
@@ -49,8 +53,16 @@ def run(model_name, world, rank, out_path):
             dist.init_process_group("gloo", rank=rank, world_size=world)
         pg = dist.group.WORLD
     capture = os.environ.get("DR_DDP_CAPTURE") == "1"
-    datas = [data_ref.synthetic_to_data(g, f"s{i}") for i, g in enumerate(make_dataset(2 * B, seed=17, n_lo=30, n_hi=80, mean_degree=9.0))]
+    mixed = os.environ.get("DR_DDP_GRAPHS") == "mixed"
+    if mixed:  # 2 x B graphs: 12 residue, 7 SRV-like, 5 atom-level per global batch
+        fams = [{}] * 12 + [{"n_lo": 26, "n_hi": 36, "mean_degree": 7.4, "k_lo": 2, "k_hi": 3}] * 7 + [{"n_lo": 2700, "n_hi": 3300, "mean_degree": 16.7, "k_lo": 8, "k_hi": 32}] * 5
+        order = np.random.default_rng(5).permutation(2 * B)
+        graphs = [make_dataset(1, seed=100 + i, **fams[i % B])[0] for i in order]
+    else:
+        graphs = make_dataset(2 * B, seed=17, n_lo=30, n_hi=80, mean_degree=9.0)
+    datas = [data_ref.synthetic_to_data(g, f"s{i}") for i, g in enumerate(graphs)]
     store = GraphStore(pack_graphs(records_from_batch(P.Batch.from_data_list(datas))), dev)
+    edges = np.array([d.edge_index.shape[1] for d in datas])
     torch.manual_seed(42)
     model = {"ginet": lambda: GINet(30, 1, 3), "foutnet": lambda: FoutNet(30, 1), "vanilla": lambda: VanillaNetwork(30, 1, 3)}[model_name]().to(dev).train()
     step = FusedTrainStep(model, process_group=pg)
@@ -65,27 +77,38 @@ def run(model_name, world, rank, out_path):
 
         dist.all_reduce = all_reduce
         adam = step._adam_after_allreduce  # noqa: SLF001
-    losses = []
+    losses, loads = [], []
+    out_global = None
     for s in range(STEPS):
         gids = np.arange(B) + (s % 2) * B  # global batch, global order
+        plan = plan_shards(edges[gids], max(world, emulate), policy="edges" if mixed else "contiguous")
+        loads.append(plan.loads)
         if emulate:
             acc.clear()
+            out_global = np.zeros((B, 1), np.float32)
             for r in range(emulate):
                 step._adam_after_allreduce = adam if r == emulate - 1 else (lambda: None)  # noqa: SLF001
-                loss, _ = step.step(BatchHandle(store, shard_contiguous(gids, r, emulate)), global_batch=B, dropout=False)
+                loss, out = step.step(BatchHandle(store, gids[plan.positions[r]]), global_batch=B, dropout=False)
+                out_global[plan.positions[r]] = out.cpu().numpy()
             losses.append(float(loss))
             continue
-        h = BatchHandle(store, shard_contiguous(gids, rank, world))
+        h = BatchHandle(store, gids[plan.positions[rank]])
         if capture:
             g = step.capture(h, global_batch=B, dropout=False)
             g.replay()
-            loss = step.loss_out
+            loss, out = step.loss_out, step.out[: h.B]
         else:
-            loss, _ = step.step(h, global_batch=B, dropout=False)
+            loss, out = step.step(h, global_batch=B, dropout=False)
         losses.append(float(loss))
+        if pg is not None and world > 1:
+            from deeprank2_amd.trainer import _gather_rows  # noqa: PLC0415
+
+            out_global = _gather_rows(out.clone(), plan, pg).cpu().numpy()
+        else:
+            out_global = out.cpu().numpy()
     torch.cuda.synchronize()
     if rank == 0:
-        np.savez(out_path, loss=np.array(losses), grad=step.flat_grad.cpu().numpy(), **{f"p{i}": p.detach().cpu().numpy() for i, p in enumerate(step.params)})
+        np.savez(out_path, loss=np.array(losses), grad=step.flat_grad.cpu().numpy(), out=out_global, loads=np.array(loads), **{f"p{i}": p.detach().cpu().numpy() for i, p in enumerate(step.params)})
     if pg is not None:
         dist.destroy_process_group()
 

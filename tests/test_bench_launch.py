@@ -36,3 +36,18 @@ def test_gpus_2_launches_two_ranks():
 def test_gpus_1_is_one_process():
     r = _run(["--dry-run"])
     assert r["n_gpus"] == 1 and r["config"]["parallelism"] == "dp1"
+
+
+def test_gpus_2_mixed_reports_edge_balanced_shards():
+    """Config 5's launch: both ranks build the same global batches and shard
+    them by edges; the line carries every batch's per-rank edge loads (each
+    rank's own count of its first shard is checked against them in-run)."""
+    r = _run(["--gpus", "2", "--dry-run", "--graphs", "mixed", "--batches", "2"])
+    sh = r["shards"]
+    assert r["config"]["global_batch"] == 128
+    assert len(sh["rank_edge_loads"]) == 2 and all(len(x) == 2 for x in sh["rank_edge_loads"])
+    for loads, sizes in zip(sh["rank_edge_loads"], sh["rank_graphs"]):
+        assert sum(sizes) == 128
+        assert max(loads) <= 1.1 * sum(loads) / 2
+    r = _run(["--gpus", "2", "--dry-run", "--batches", "2"])  # residue graphs: contiguous halves
+    assert r["shards"]["balanced"] == [False, False] and r["shards"]["rank_graphs"] == [[64, 64], [64, 64]]

@@ -13,7 +13,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from deeprank2_amd.distributed import shard_by_edges, shard_contiguous
+from deeprank2_amd.distributed import plan_shards, shard_by_edges, shard_contiguous
 
 
 def test_shard_contiguous_covers_in_order():
@@ -43,32 +43,48 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank_main(rank, world, port, model_name, out_path):
+def _mixed_graphs():
+    """A small config-5-like global batch: residue, SRV-like and (scaled-down)
+    large graphs in a shuffled order, so contiguous shards are edge-imbalanced."""
+    from deeprank2_amd.utils.synthetic import make_dataset
+
+    fams = [{"n_lo": 20, "n_hi": 40, "mean_degree": 6.0}] * 4 + [{"n_lo": 8, "n_hi": 12, "mean_degree": 3.0, "k_lo": 2, "k_hi": 3}] * 3 + [{"n_lo": 150, "n_hi": 220, "mean_degree": 14.0, "k_lo": 4, "k_hi": 8}] * 2
+    order = [8, 0, 1, 7, 4, 2, 5, 3, 6]
+    return [make_dataset(1, seed=50 + i, **fams[i])[0] for i in order]
+
+
+def _rank_main(rank, world, port, model_name, out_path, graphs="small"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.set_num_threads(1)
+    from deeprank2_amd.trainer import _gather_rows
     from deeprank2_amd.utils.synthetic import make_dataset
     from oracle import data_ref, gnn_ref
     from oracle import pyg_ops as P
 
-    datas = [data_ref.synthetic_to_data(g, f"s{i}") for i, g in enumerate(make_dataset(6, seed=2, n_lo=20, n_hi=40, mean_degree=6.0))]
+    gs = _mixed_graphs() if graphs == "mixed" else make_dataset(6, seed=2, n_lo=20, n_hi=40, mean_degree=6.0)
+    datas = [data_ref.synthetic_to_data(g, f"s{i}") for i, g in enumerate(gs)]
+    b = len(datas)
     torch.manual_seed(0)
     model = gnn_ref.GINet(30, 1, 3) if model_name == "ginet" else gnn_ref.FoutNet(30, 1)
     model.eval()  # dropout off: the shards see the same arithmetic as the full batch
-    mine = shard_contiguous(np.arange(6), rank, world)
+    plan = plan_shards([d.edge_index.shape[1] for d in datas], world)
+    mine = plan.positions[rank]
     bat = P.Batch.from_data_list([datas[i].clone() for i in mine])
     out = model(bat)
-    loss = ((out.reshape(-1) - bat.y) ** 2).sum() / 6.0  # per-rank term of the global MSE mean
+    loss = ((out.reshape(-1) - bat.y) ** 2).sum() / b  # per-rank term of the global MSE mean
     loss.backward()
     flat = torch.cat([p.grad.reshape(-1) for p in model.parameters()] + [loss.detach().reshape(1)])
     dist.all_reduce(flat)
+    rows = _gather_rows(out.detach(), plan, dist.group.WORLD)  # the exporter's rows, global order
     if rank == 0:
         full = P.Batch.from_data_list([d.clone() for d in datas])
         model.zero_grad()
-        ref_loss = torch.nn.functional.mse_loss(model(full).reshape(-1), full.y)
+        ref_out = model(full)
+        ref_loss = torch.nn.functional.mse_loss(ref_out.reshape(-1), full.y)
         ref_loss.backward()
         ref = torch.cat([p.grad.reshape(-1) for p in model.parameters()] + [ref_loss.detach().reshape(1)])
-        np.savez(out_path, ddp=flat.numpy(), ref=ref.numpy())
+        np.savez(out_path, ddp=flat.numpy(), ref=ref.numpy(), rows=rows.numpy(), ref_rows=ref_out.detach().numpy(), balanced=plan.balanced, loads=np.array(plan.loads))
     dist.destroy_process_group()
 
 
@@ -77,7 +93,44 @@ def test_gloo_world2_allreduced_gradients_equal_global_batch(tmp_path, model_nam
     out = str(tmp_path / "g.npz")
     mp.spawn(_rank_main, args=(2, _free_port(), model_name, out), nprocs=2, join=True)
     z = np.load(out)
+    assert not z["balanced"]  # equal-sized graphs: contiguous shards
     np.testing.assert_allclose(z["ddp"], z["ref"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(z["rows"], z["ref_rows"], rtol=1e-5, atol=1e-6)
+
+
+def test_gloo_world2_mixed_batch_edge_balanced(tmp_path):
+    """Config 5 on the CPU: a mixed batch is sharded by edge bin packing
+    (contiguous shards would leave one rank with both large graphs), the
+    all-reduced gradients equal the global batch's, and the gathered
+    predictions come back in global-batch order."""
+    out = str(tmp_path / "m.npz")
+    mp.spawn(_rank_main, args=(2, _free_port(), "ginet", out, "mixed"), nprocs=2, join=True)
+    z = np.load(out)
+    assert z["balanced"]
+    assert max(z["loads"]) < 1.25 * z["loads"].mean()
+    np.testing.assert_allclose(z["ddp"], z["ref"], rtol=1e-5, atol=1e-5 * float(np.abs(z["ref"]).max()))
+    np.testing.assert_allclose(z["rows"], z["ref_rows"], rtol=1e-5, atol=1e-6)
+
+
+def test_plan_shards_policy():
+    residue = np.full(64, 3000)
+    p = plan_shards(residue, 8)
+    assert not p.balanced and p.sizes() == [8] * 8
+    np.testing.assert_array_equal(np.concatenate(p.positions), np.arange(64))
+    rng = np.random.default_rng(1)
+    mixed = np.where(rng.random(64) < 0.2, 50000, np.where(rng.random(64) < 0.4, 250, 3000))
+    c = plan_shards(mixed, 8, policy="contiguous")
+    a = plan_shards(mixed, 8)
+    assert max(c.loads) > 1.25 * np.mean(c.loads) and a.balanced
+    assert max(a.loads) < max(c.loads)
+    np.testing.assert_array_equal(np.concatenate(a.positions)[a.perm], np.arange(64))
+    for pos in a.positions:
+        assert np.all(np.diff(pos) > 0)  # global order within a rank
+    assert plan_shards(mixed, 1).sizes() == [64]
+    e = plan_shards(np.array([10, 20]), 4)  # fewer graphs than ranks: empty shards
+    assert sorted(e.sizes()) == [0, 0, 1, 1]
+    with pytest.raises(ValueError):
+        plan_shards(mixed, 2, policy="random")
 
 
 class _FakeDataset:

@@ -149,9 +149,14 @@ def test_ginet_classification_class_weights_checkpoint_and_test(files, tmp_path)
     last = [r for r in mem.records if r["phase"] == "training"][-1]
     np.testing.assert_allclose(np.array(last["output"]).sum(1), 1.0, rtol=1e-5)
     state = torch.load(path, weights_only=True)
-    # as in the reference (trainer.py:619-622) the snapshot is taken before
-    # epoch_saved_model is updated, so the file holds the previous value
+    # as in the reference (trainer.py:628-631) the snapshot is taken before
+    # epoch_saved_model is updated, so the file holds the previous best epoch
+    # (None when the kept model is the first one saved)
     assert set(state["model_state"]) == set(t.model.state_dict())
+    vl = [r["loss"] for r in mem.records if r["phase"] == "validation"][1:]
+    saves = [e for e in range(1, len(vl) + 1) if min(vl[:e]) == vl[e - 1]]
+    assert state["epoch_saved_model"] == (saves[-2] if len(saves) > 1 else None)
+    assert t.epoch_saved_model == saves[-1]
     te = GraphDataset(files[3], train_source=path, clustering_method="mcl")
     mem2 = MemoryOutputExporter()
     t2 = Trainer(GINet, dataset_test=te, pretrained_model=path, cuda=True, output_exporters=[mem2])

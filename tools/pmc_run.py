@@ -14,7 +14,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "deeprank-gnn-2_amd")]
 
-from bench import records  # noqa: E402
+from bench import make_graphs, records  # noqa: E402
 from deeprank2_amd.engine import GINetTrainStep  # noqa: E402
 from deeprank2_amd.neuralnets.gnn.ginet import BatchHandle, GINet  # noqa: E402
 from deeprank2_amd.neuralnets.gnn.vanilla_gnn import VanillaNetwork  # noqa: E402
@@ -27,10 +27,12 @@ def main():
     dev = torch.device("cuda:0")
     which = sys.argv[2] if len(sys.argv) > 2 else "ginet"
     atom = which.endswith("_atom")  # B=32 atom-level graphs (the Vanilla pipeline / large paths)
-    which = which.removesuffix("_atom")
-    B, nb = (32, 4) if atom else (64, 16)
+    mixed = which.endswith("_mixed")  # B=64 configs[4] 50/30/20 residue/SRV/atom mix (bench.py --graphs mixed)
+    which = which.removesuffix("_atom").removesuffix("_mixed")
+    B, nb = (32, 4) if atom else (64, 4) if mixed else (64, 16)
     fam = {"n_lo": 2700, "n_hi": 3300, "mean_degree": 16.7, "k_lo": 8, "k_hi": 32} if atom else {}
-    packed = pack_graphs(records(make_dataset(B * nb, seed=1000, **fam), 1 if which == "sgat" else 3))
+    graphs = make_graphs("mixed", B * nb, seed=1000) if mixed else make_dataset(B * nb, seed=1000, **fam)
+    packed = pack_graphs(records(graphs, 1 if which == "sgat" else 3), require_clusters=which not in ("ginet_nocluster", "vanilla"))
     store = GraphStore(packed, dev)
     order = np.random.default_rng(0).permutation(packed.n_graphs).astype(np.int32)
     hs = [BatchHandle(store, order[i * B:(i + 1) * B]) for i in range(nb)]
