@@ -85,9 +85,12 @@ def make_graphs(kind, n, seed):
 
     if kind != "mixed":
         return make_dataset(n, seed=seed, **FAMILIES[kind])
+    from deeprank2_amd.utils.synthetic import connect_clusters  # noqa: PLC0415
+
     rng = np.random.default_rng(seed)
     fam = rng.choice(["residue", "srv", "atom"], size=n, p=[0.5, 0.3, 0.2])
-    return [make_dataset(1, seed=int(seed * 7919 + i), **FAMILIES[f])[0] for i, f in enumerate(fam)]
+    # no pooled node without out-edges (FoutNet's NaN rows): the mix trains
+    return [connect_clusters(make_dataset(1, seed=int(seed * 7919 + i), **FAMILIES[f])[0]) for i, f in enumerate(fam)]
 
 
 def records(graphs, edge_features=3):
@@ -355,6 +358,8 @@ def parse_args(argv):
     ap.add_argument("--no-stream-copy", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch every step from Python instead of replaying captured HIP graphs")
     ap.add_argument("--eager-ddp", action="store_true", help="N>1: launch steps from Python (default: the RCCL all-reduce is captured in the HIP graph with the kernels)")
+    ap.add_argument("--trainer", action="store_true", help="diagnostic: the drop-in path, Trainer(GINet, GraphDataset(HDF5)).train(), and the GraphDataset -> GraphStore load rate (one JSON line; not the headline)")
+    ap.add_argument("--epochs", type=int, default=3, help="--trainer: timed training epochs")
     ap.add_argument("--shard-policy", choices=["auto", "contiguous", "edges"], default="auto", help="N>1: how each global batch is split over the ranks (distributed.plan_shards)")
     ap.add_argument("--dry-run", action="store_true", help="launcher check without a GPU: each rank joins a gloo group, builds the global batches and its shards, rank 0 prints the JSON skeleton with the per-rank edge loads")
     return ap.parse_args(argv)
@@ -387,6 +392,99 @@ def global_batches(args, world, rank):
         plans.append(plan)
         local.append(gb[plan.positions[rank]])
     return graphs, packed, local, plans, B
+
+
+def trainer_bench(args):
+    """The drop-in path as a user runs it (reference trainer.py:503-724 over
+    dataset.py:883-1052): configs[1]-shape graphs written as a DeepRank2 HDF5
+    file, ``GraphDataset`` on it, ``Trainer(GINet, ...)`` and ``train()``.
+    Reports (1) the load rate: HDF5 -> GraphDataset (index, features) ->
+    packed HBM ``GraphStore`` in graphs/s and per host core used, beside the
+    reference's ~400 graphs/s/core per-item HDF5 read; (2) the
+    training epochs' graphs/s and us per step through ``Trainer._epoch``
+    (device loss, one D2H per epoch), beside the captured-step number of the
+    headline line.  Prints one JSON line (diagnostic)."""
+    import tempfile  # noqa: PLC0415
+
+    import numpy as np  # noqa: PLC0415
+    import torch  # noqa: PLC0415
+
+    from deeprank2_amd.dataset import GraphDataset  # noqa: PLC0415
+    from deeprank2_amd.exporters import MemoryOutputExporter  # noqa: PLC0415
+    from deeprank2_amd.neuralnets.gnn.ginet import GINet  # noqa: PLC0415
+    from deeprank2_amd.trainer import Trainer  # noqa: PLC0415
+    from deeprank2_amd.utils import synthetic as S  # noqa: PLC0415
+
+    B = args.batch or B_PER_GPU
+    n = B * args.batches
+    graphs = make_graphs("residue", n, seed=1000)
+    dev = torch.device("cuda:0")
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "train.hdf5")
+        t0 = time.perf_counter()
+        S.write_hdf5(path, graphs)
+        t_write = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        ds = GraphDataset(path, node_features=S.SYNTH_NODE_FEATURES, edge_features=S.SYNTH_EDGE_FEATURES, target="irmsd", clustering_method="mcl")
+        t_index = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        store = ds.graph_store(dev)
+        torch.cuda.synchronize()
+        t_pack = time.perf_counter() - t0
+        cores, affinity = host_cores()
+        load = {"graphs": n, "hdf5_write_s": round(t_write, 3), "dataset_init_s": round(t_index, 3), "graph_store_s": round(t_pack, 3), "graphs_per_s": round(n / (t_index + t_pack), 1), "cores": cores, "graphs_per_s_per_core": round(n / (t_index + t_pack) / cores, 1), "reference_graphs_per_s_per_core": 400, "note": "GraphDataset(HDF5) construction (file read, index, feature checks) + graph_store (per-entry arrays, threaded C++ pack, H2D) for the whole file; the reference reads one entry per item (dataset.py:883-1052, ~2.5 ms/graph/core, SURVEY §6)"}
+        del store
+        torch.manual_seed(1234)
+        mem = MemoryOutputExporter()
+        tr = Trainer(GINet, ds, cuda=True, output_exporters=[mem], precluster=False)
+        epoch_s = []
+        orig = tr._epoch  # noqa: SLF001
+
+        def timed(*a, **k):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            r = orig(*a, **k)
+            torch.cuda.synchronize()
+            epoch_s.append(time.perf_counter() - t)
+            return r
+
+        tr._epoch = timed  # noqa: SLF001
+        tr.train(nepoch=1, batch_size=B, shuffle=True, best_model=False, filename=None)  # warm-up epoch (store, plans, the epoch's HIP graph)
+        epoch_s.clear()
+        t0 = time.perf_counter()
+        tr.train(nepoch=args.epochs, batch_size=B, shuffle=True, best_model=False, filename=None)
+        t_train = time.perf_counter() - t0
+        per_epoch = float(np.median(epoch_s))
+        captured = bool(tr._runners)  # noqa: SLF001
+        # the same epochs through the per-batch loop (descriptors + two launches per batch from Python)
+        Trainer.capture_epochs = False
+        try:
+            tr.train(nepoch=1, batch_size=B, shuffle=True, best_model=False, filename=None)
+            epoch_s.clear()
+            tr.train(nepoch=args.epochs, batch_size=B, shuffle=True, best_model=False, filename=None)
+        finally:
+            Trainer.capture_epochs = True
+        per_epoch_loop = float(np.median(epoch_s))
+    steps = int(np.ceil(len(tr.dataset_train) / B))
+    res = {
+        "metric": "graphs/sec per Trainer training epoch (drop-in path: Trainer(GINet, GraphDataset(HDF5)).train), configs[1] graphs",
+        "value": round(len(tr.dataset_train) / per_epoch, 1),
+        "unit": "graphs/s",
+        "us_per_step": round(per_epoch / steps * 1e6, 2),
+        "steps_per_epoch": steps,
+        "train_graphs": len(tr.dataset_train),
+        "batch_size": B,
+        "epochs_timed": args.epochs,
+        "fused_step": bool(tr._fused),  # noqa: SLF001
+        "captured_epochs": captured,
+        "per_batch_loop": {"graphs_per_s": round(len(tr.dataset_train) / per_epoch_loop, 1), "us_per_step": round(per_epoch_loop / steps * 1e6, 2), "note": "Trainer.capture_epochs = False: per batch, the host builds descriptors and launches the graph pass and reduce/Adam"},
+        "train_call_s": round(t_train, 3),
+        "train_call_note": "the whole train() call: epoch-0 evaluation, the timed epochs, model selection and the final state load",
+        "load": load,
+        "data": "synthetic (seeded residue graphs per SURVEY §8(d), written as a DeepRank2 HDF5 file); random-init GINet(30,1,3)",
+    }
+    print(json.dumps(res), flush=True)
+    return res
 
 
 def dry_run(args):
@@ -586,6 +684,9 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
     kernel_ms = None if layer_path else step.time_graph_pass(handles, args.steps, global_batch=B * world)
     if kernel_ms is None:  # layer path: no single graph-pass kernel; price the whole step
         kernel_ms = elapsed / args.steps * 1e3
+    # the step split (pass / reduce + Adam / the rest: launch gaps inside the
+    # replayed graphs), world of one only
+    reduce_ms = None if (layer_path or pg is not None) else step.time_reduce(handles, args.steps, global_batch=B * world)
     if pg is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -689,6 +790,7 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
                 "mfma": mfma,
                 "wallclock": {"bytes_per_step": int(alg + adam_bytes), "achieved": round(wall_gbs, 2), "frac": round(wall_gbs / HBM_PEAK_GBS, 5), "note": "B_alg(step) = sum_g B_alg(g) + 28*P (Adam fp32) over ms_per_step"},
             },
+            "step_split_us": None if reduce_ms is None else {"graph_pass": round(kernel_ms * 1e3, 2), "reduce_adam": round(reduce_ms * 1e3, 2), "other": round(ms_step * 1e3 - (kernel_ms + reduce_ms) * 1e3, 2), "note": "graph pass and dr_reduce_update each timed alone (HIP events around a HIP graph of --steps launches); other = ms_per_step minus both: the gaps between launches in the replayed step graphs"},
             "launch": ("eager" + capture_note) if captured is None else f"hipgraph-replay ({n_sweeps} x {len(handles)}-step sweep graph + " + (f"one {n_rest}-step graph" if rest is not None else f"{n_rest} per-step graphs") + f"{', RCCL all-reduce captured' if pg is not None else ''})",
             "cpu_baseline": cpu,
             "final_loss": float(loss.item()),
@@ -707,5 +809,7 @@ if __name__ == "__main__":
         sys.exit(relaunch(_args.gpus, _argv))
     if _args.dry_run:
         dry_run(_args)
+    elif _args.trainer:
+        trainer_bench(_args)
     else:
         main(_args)

@@ -1101,6 +1101,614 @@ inline int rows_grid(int64_t rows, int rows_per_block) {
   return (int)g;
 }
 
+// ---- chunk-fused pipeline: tile == weight-gradient chunk == 64 rows ---------
+// With a tile plan of DR_VANILLA_CHUNK rows (and Fe <= 4), one 1024-thread
+// workgroup per chunk runs every row-local stage of its rows around the halo
+// edge work, so the node-level intermediates between them stay in LDS:
+//   vc_fwd<l>  edge gather -> S_l (LDS), node MLP X_l = relu([X | S_l] Wn^T + bn)
+//              and, layer 1, the next layer's [A2 | B2] = X1 [Wa2; Wb2]^T
+//              (vb_edge_fwd_tile + vb_gemm<GM_NODE> + vb_gemm<GM_HALVES>);
+//   vc_nb2     DU2 = relu'(X2) dmean, [dX1 | DS2] = DU2 Wn2, dWn2 / dbn2
+//              (vb_du + vb_gemm<GM_DXS> + vb_wgrad_mfma's Wn part);
+//   vc_eb2n1   D2, D2' from the DS2 halo, dWa2 / dWb2 / dbe2 / dWc2,
+//              dX1 += [D2 | D2'] [Wa2; Wb2], DU1 = relu'(X1) dX1, DS1 = DU1 Wn1,
+//              dWn1 / dbn1 (vb_edge_bwd_tile + vb_gemm<GM_DX1> + vb_du +
+//              vb_gemm<GM_DXS> + vb_wgrad_mfma, two layers);
+//   vc_eb1     D1, D1' from the DS1 halo, dWa1 / dWb1 / dbe1 / dWc1;
+//   vc_combine every graph's chunk partials of both layers, in chunk order.
+// 8 launches per step instead of 17.  Every GEMM takes the operands and the k
+// order of the kernel it replaces, and the sums run in the same order, so the
+// outputs, slabs, head vectors and ReLU words are bit-identical to the untiled
+// pipeline; only dWc sums its rows' shares in another order (as the 16-row
+// tiles already did).
+constexpr int CT = 1024;      // threads of the chunk kernels
+constexpr int CW = CT / 64;   // waves
+constexpr int CRG = CT / 32;  // row groups (32 lanes = the 32 channels of one row)
+constexpr int NBT = 256;      // vc_nb2 threads
+
+__device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 acc) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+}
+
+// a tile's halo rows of a node-level [rows][32] array (graph block at g32) -> LDS
+template <int NT>
+__device__ __forceinline__ void stage_halo_t(float* dst, const float* g32, const int* ids, int H) {
+  for (int p = threadIdx.x; p < H * 8; p += NT) {
+    const int h = p >> 3, q = (p & 7) * 4;
+    *reinterpret_cast<float4*>(dst + h * 32 + q) = *reinterpret_cast<const float4*>(g32 + (int64_t)ids[h] * 32 + q);
+  }
+}
+
+// rows [0, WR) of a row-major [rows][W] array (W a multiple of 4) into LDS at
+// stride LD: rows < nr from src, the others zero; mask_f > 0 zeroes columns >= mask_f
+template <int NT>
+__device__ __forceinline__ void stage_rows(float* dst, int LD, const float* src, int W, int nr, int mask_f) {
+  const int CH = W / 4;
+  for (int p = threadIdx.x; p < WR * CH; p += NT) {
+    const int i = p / CH, c4 = (p - i * CH) * 4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < nr) {
+      v = *reinterpret_cast<const float4*>(src + (int64_t)i * W + c4);
+      if (mask_f > 0 && c4 + 4 > mask_f) {
+        v.x = c4 < mask_f ? v.x : 0.f;
+        v.y = c4 + 1 < mask_f ? v.y : 0.f;
+        v.z = c4 + 2 < mask_f ? v.z : 0.f;
+        v.w = c4 + 3 < mask_f ? v.w : 0.f;
+      }
+    }
+    *reinterpret_cast<float4*>(dst + i * LD + c4) = v;
+  }
+}
+
+struct FwdCarve {
+  int KP, LA, NOP, LX, a, wn, wh, x1, halo, rec, total;
+};
+__host__ __device__ inline FwdCarve fwd_carve(int F, int hmax, int emax, int Fe, bool next) {
+  FwdCarve c;
+  const int XS = r4(F);
+  c.KP = XS + 32;  // [X | S]
+  c.LA = c.KP + 4;
+  c.NOP = r16(F);
+  c.LX = XS + 4;
+  int o = 0;
+  c.a = o;    o += WR * c.LA;                 // [X | S] rows (node MLP A operand)
+  c.wn = o;   o += c.KP * c.NOP;              // Wn^T [KP][NOP]
+  c.wh = o;   o += next ? XS * 64 : 0;        // [Wa2; Wb2]^T [XS][64]
+  c.x1 = o;   o += next ? WR * c.LX : 0;      // X1 rows (halves A operand)
+  c.halo = o; o += hmax * 32;                 // B halo rows
+  c.rec = o;  o += emax * (Fe <= 3 ? 4 : 8);  // CSR records {halo column, ea}
+  c.total = o;
+  return c;
+}
+
+struct BwdCarve {
+  int LDD, LU, NOP3, d, x1, dx, w3, du, w1, sh, x0, s1, halo, rec, trec, total;
+};
+// two_layers: vc_eb2n1 (layer 2's edges + layer 1's node backward); else vc_eb1
+__host__ __device__ inline BwdCarve bwd_carve(int F, int hmax, int emax, int tmax, int Fe, bool two_layers) {
+  BwdCarve c;
+  const int XS = r4(F), FeS = Fe > 0 ? Fe : 1;
+  c.LDD = 64 + 4;  // [D | D'] rows
+  c.LU = XS + 4;
+  c.NOP3 = r16(F);
+  int o = 0;
+  c.d = o;  o += WR * c.LDD;
+  c.x1 = o; o += two_layers ? WR * XS : 0;           // X1 rows (dWa2 / dWb2 B operand, relu'(X1))
+  c.dx = o; o += two_layers ? WR * XS : 0;           // dX1 partial (DU2 Wn2[:, :F])
+  c.w3 = o; o += two_layers ? 64 * c.NOP3 : 0;        // [Wa2; Wb2] [64][NOP3]
+  c.du = o; o += two_layers ? WR * c.LU : 0;          // DU1
+  c.w1 = o; o += two_layers ? XS * 32 : 0;            // Wn1[:, F:]^T... as [XS][32]
+  c.sh = o; o += CW * 32 * FeS;                       // the waves' dWc shares
+  const int edge = hmax * 32 + emax * (Fe <= 3 ? 4 : 8) + 2 * tmax;
+  const int late = WR * XS + WR * 32;                 // X0 / S1 rows, staged after the edge phase
+  c.x0 = o;            // vc_eb1: X0 rows beside the edge region; vc_eb2n1: inside it, after the edges
+  if (!two_layers) o += WR * XS;
+  c.halo = o;
+  c.rec = c.halo + hmax * 32;
+  c.trec = c.rec + emax * (Fe <= 3 ? 4 : 8);
+  if (two_layers) {
+    c.x0 = c.halo;
+    c.s1 = c.halo + WR * XS;
+    o += edge > late ? edge : late;
+  } else {
+    c.s1 = 0;
+    o += edge;
+  }
+  c.total = o;
+  return c;
+}
+
+template <int FE, int LAYER>
+__global__ void __launch_bounds__(CT) vc_fwd(VA a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int FA = FE > 0 ? FE : 1, FeS = FA;
+  constexpr bool NEXT = LAYER == 1;
+  const Layer L = layer_of(a, LAYER);
+  const int F = a.F, KE = a.KE, KN = a.KN, XS = a.XS;
+  const int t = blockIdx.x, tid = threadIdx.x, c = tid & 31, hs = tid & 32;
+  const int64_t rt0 = a.ws.tile_row0[t], rt1 = a.ws.tile_row0[t + 1];
+  const int nr = (int)(rt1 - rt0);
+  const int b = a.ws.row_slot[rt0];
+  const dr_graph_desc& d = a.descs[b];
+  const int64_t g0 = a.ws.row0[b];
+  const int* rp = a.s.rowptr + d.node0 + d.gid;
+  const int i0 = (int)(rt0 - g0), e0 = rp[i0], ne = rp[(int)(rt1 - g0)] - e0;
+  const int h0 = a.ws.halo_off[t], H = a.ws.halo_off[t + 1] - h0;
+  const FwdCarve fc = fwd_carve(F, a.ws.halo_max, a.ws.tile_edges_max, FE, NEXT);
+  float* sA = lds + fc.a;
+  float* sWn = lds + fc.wn;
+  float* sWh = lds + fc.wh;
+  float* sX1 = lds + fc.x1;
+  float* sB = lds + fc.halo;
+  float* sR = lds + fc.rec;
+  stage_halo_t<CT>(sB, L.bm + g0 * 32, a.ws.halo_ids + h0, H);
+  {
+    const float* ea = a.s.ea + (d.col0 + e0) * FeS;
+    const uint16_t* lc = a.ws.lcol + a.ws.lcol_off[t];
+    for (int p = tid; p < ne; p += CT) put_rec<FE>(sR, p, lc[p], ea + (int64_t)p * FeS);
+  }
+  // the tile's input rows -> [X | .] (pad columns and rows past the tile zero;
+  // the S columns of rows past the tile zero too)
+  stage_rows<CT>(sA, fc.LA, LAYER == 1 ? a.s.x + (d.node0 + i0) * XS : L.xin + rt0 * XS, XS, nr, F);
+  for (int p = tid; p < (WR - nr) * 32; p += CT) sA[(nr + (p >> 5)) * fc.LA + XS + (p & 31)] = 0.f;
+  for (int p = tid; p < fc.KP * fc.NOP; p += CT) {  // vb_gemm<GM_NODE>'s W staging
+    const int k = p / fc.NOP, n = p - k * fc.NOP;
+    float v = 0.f;
+    if (n < F) v = k < F ? L.wn[n * KN + k] : (k < XS ? 0.f : L.wn[n * KN + F + k - XS]);
+    sWn[p] = v;
+  }
+  if (NEXT)
+    for (int p = tid; p < XS * 64; p += CT) {  // vb_gemm<GM_HALVES>'s W staging, layer 2's weights
+      const int k = p >> 6, n = p & 63;
+      sWh[p] = k < F ? a.w.we2[(n & 31) * KE + (n < 32 ? 0 : F) + k] : 0.f;
+    }
+  float wcr[FA];
+#pragma unroll
+  for (int f = 0; f < FE; ++f) wcr[f] = L.we[c * KE + 2 * F + f];
+  const float bc = L.be[c];
+  uint32_t* wr = a.ws.relu_words + (int64_t)(LAYER - 1) * a.ws.edge0[a.B] + a.ws.edge0[b] + e0;
+  __syncthreads();
+  for (int64_t r = rt0 + (tid >> 5); r < rt1; r += CRG) {
+    const int i = (int)(r - g0);
+    const float ab = L.a[r * 32 + c] + bc;
+    float acc = 0.f;
+    const int eb = rp[i] - e0, ee = rp[i + 1] - e0;
+    int e = eb;
+    auto group = [&](auto un) {
+      constexpr int U = decltype(un)::value;
+      uint32_t j[U];
+      float ev[U][FA], q[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) j[u] = get_rec<FE>(sR, e + u, ev[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) q[u] = sB[j[u] * 32 + c];
+      uint32_t mine = 0u;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        float pre = ab + q[u];
+#pragma unroll
+        for (int f = 0; f < FE; ++f) pre = fmaf(wcr[f], ev[u][f], pre);
+        acc += relu_keepnan(pre);
+        const uint64_t m = __ballot(active(pre));
+        if (c == u) mine = (uint32_t)(m >> hs);
+      }
+      if (c < U) wr[e + c] = mine;
+    };
+    for (; e + 8 <= ee; e += 8) group(std::integral_constant<int, 8>());
+    for (; e + 4 <= ee; e += 4) group(std::integral_constant<int, 4>());
+    for (; e < ee; ++e) group(std::integral_constant<int, 1>());
+    L.s[r * 32 + c] = acc;
+    sA[(r - rt0) * fc.LA + XS + c] = acc;
+  }
+  __syncthreads();
+  // node MLP on MFMA: vb_gemm<GM_NODE>'s operands and k order
+  const int lane = tid & 63, wave = tid >> 6, li = lane & 15, kq = lane >> 4;
+  const int nct = fc.NOP / 16;
+  for (int job = wave; job < 4 * nct; job += CW) {
+    const int ib = (job / nct) * 16, n = (job % nct) * 16 + li;
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < fc.KP; k0 += 4) acc = mfma4(sA[(ib + li) * fc.LA + k0 + kq], sWn[(k0 + kq) * fc.NOP + n], acc);
+    const float bn = n < F ? L.bn[n] : 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = ib + kq * 4 + q;
+      const float v = relu_keepnan(acc[q] + bn);
+      if (i < nr && n < F) L.xout[(rt0 + i) * XS + n] = v;
+      if (NEXT && n < XS) sX1[i * fc.LX + n] = n < F ? v : 0.f;
+    }
+  }
+  if (!NEXT) return;
+  __syncthreads();
+  // layer 2's [A | B] = X1 [Wa2; Wb2]^T: vb_gemm<GM_HALVES>'s operands and k order
+  const Layer L2 = layer_of(a, 2);
+  for (int job = wave; job < 16; job += CW) {
+    const int ib = (job >> 2) * 16, n = (job & 3) * 16 + li;
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < XS; k0 += 4) acc = mfma4(sX1[(ib + li) * fc.LX + k0 + kq], sWh[(k0 + kq) * 64 + n], acc);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = ib + kq * 4 + q;
+      if (i < nr) (n < 32 ? L2.a : L2.bm)[(rt0 + i) * 32 + (n & 31)] = acc[q];
+    }
+  }
+}
+
+// weight-gradient partial row of a layer for a chunk (both layers' rows live together)
+__device__ __forceinline__ float* part_row(const VA& a, int l, int ch) {
+  return a.ws.part + ((int64_t)(l - 1) * a.ws.n_chunks + ch) * layer_grad_size(a.F, a.Fe);
+}
+
+// dWn = DU^T [X | S] (K = the chunk's 64 rows, zero past it) and dbn = sum DU:
+// vb_wgrad_mfma's jobs and order.  DU at stride LU, X at stride XS, S at 32.
+template <int NT>
+__device__ __forceinline__ void node_wgrad(const VA& a, float* out, const float* sDU, int LU, const float* sX, const float* sS, int job0) {
+  const int F = a.F, XS = a.XS, KN = a.KN, KE = a.KE;
+  const int nwe = 32 * KE, nwn = F * KN;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, kq = lane >> 4;
+  const int KT = (F + 15) >> 4, QT = (KN + 15) >> 4;
+  for (int jj = (wave + NT / 64 - job0 % (NT / 64)) % (NT / 64); jj < KT * QT; jj += NT / 64) {
+    const int nt = jj / QT, qt = jj - nt * QT;
+    const int nn = nt * 16 + li, qc = qt * 16 + li;
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < WR; i += 4) {
+      const float av = nn < XS ? sDU[(i + kq) * LU + nn] : 0.f;
+      const float bv = qc < F ? sX[(i + kq) * XS + qc] : (qc < KN ? sS[(i + kq) * 32 + qc - F] : 0.f);
+      acc = mfma4(av, bv, acc);
+    }
+    if (qc < KN) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n = nt * 16 + kq * 4 + q;
+        if (n < F) out[nwe + 32 + n * KN + qc] = acc[q];
+      }
+    }
+  }
+  for (int p0 = threadIdx.x; p0 < 4 * F; p0 += NT) {  // dbn: four lanes of 16 rows, combined in order
+    const int p = p0 >> 2, ib = (p0 & 3) * (WR / 4);
+    float v = 0.f;
+#pragma unroll
+    for (int u = 0; u < WR / 4; ++u) v += sDU[(ib + u) * LU + p];
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    if ((p0 & 3) == 0) out[nwe + 32 + nwn + p] = v;
+  }
+}
+
+__global__ void __launch_bounds__(NBT) vc_nb2(VA a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int F = a.F, XS = a.XS, KN = a.KN;
+  const int ch = blockIdx.x, tid = threadIdx.x;
+  const int64_t rt0 = a.ws.tile_row0[ch], rt1 = a.ws.tile_row0[ch + 1];
+  const int nr = (int)(rt1 - rt0);
+  const int b = a.ws.row_slot[rt0];
+  const int LU = XS + 4, NOPD = r16(F + 32);
+  float* sDU = lds;
+  float* sX1 = sDU + WR * LU;
+  float* sS = sX1 + WR * XS;
+  float* sW = sS + WR * 32;
+  float* ws = a.ws.base;
+  const float* X2 = ws + a.L.x2 + rt0 * XS;
+  const int HD = XS + 256 + r4(a.p.out_dim);
+  const float* dmean = a.p.head + (int64_t)(a.p.slot ? a.p.slot[b] : b) * DR_VANILLA_HEAD_STRIDE(F, a.p.out_dim) + HD;
+  for (int p = tid; p < WR * XS; p += NBT) {  // vb_du (layer 2)
+    const int i = p / XS, n = p - i * XS;
+    sDU[i * LU + n] = (i < nr && n < F) ? relu_bwd(X2[(int64_t)i * XS + n], dmean[n]) : 0.f;
+  }
+  stage_rows<NBT>(sX1, XS, ws + a.L.x1 + rt0 * XS, XS, nr, 0);
+  stage_rows<NBT>(sS, 32, ws + a.L.s2 + rt0 * 32, 32, nr, 0);
+  for (int p = tid; p < XS * NOPD; p += NBT) {  // vb_gemm<GM_DXS>'s W staging (Wn2)
+    const int k = p / NOPD, n = p - k * NOPD;
+    sW[p] = (k < F && n < F + 32) ? a.w.wn2[k * KN + n] : 0.f;
+  }
+  __syncthreads();
+  const int lane = tid & 63, wave = tid >> 6, li = lane & 15, kq = lane >> 4;
+  const int nct = NOPD / 16;
+  for (int job = wave; job < 4 * nct; job += NBT / 64) {  // [dX1 | DS2] = DU2 Wn2
+    const int ib = (job / nct) * 16, n = (job % nct) * 16 + li;
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < XS; k0 += 4) acc = mfma4(sDU[(ib + li) * LU + k0 + kq], sW[(k0 + kq) * NOPD + n], acc);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = ib + kq * 4 + q;
+      if (i >= nr) continue;
+      if (n < F) ws[a.L.dx1 + (rt0 + i) * XS + n] = acc[q];
+      else if (n < F + 32) ws[a.L.ds + (rt0 + i) * 32 + n - F] = acc[q];
+    }
+  }
+  node_wgrad<NBT>(a, part_row(a, 2, ch), sDU, LU, sX1, sS, 4 * nct);
+}
+
+// a chunk's D_i = relu'-count x dS_i, D'_i (transposed), and its rows' dWc
+// shares, from the halo of dS rows (vb_edge_bwd_tile's sums and order)
+template <int FE>
+__device__ __forceinline__ void chunk_edge_bwd(const VA& a, int l, int t, const float* DS, float* sD, int LDD,
+                                               float* sDS, float* sR, uint2* sTR, float* sSh) {
+  constexpr int FA = FE > 0 ? FE : 1, FeS = FA;
+  const int tid = threadIdx.x, c = tid & 31;
+  const int64_t rt0 = a.ws.tile_row0[t], rt1 = a.ws.tile_row0[t + 1];
+  const int b = a.ws.row_slot[rt0];
+  const dr_graph_desc& d = a.descs[b];
+  const int64_t g0 = a.ws.row0[b];
+  const int* rp = a.s.rowptr + d.node0 + d.gid;
+  const int* trp = a.s.t_rowptr + d.node0 + d.gid;
+  const int i0 = (int)(rt0 - g0), i1 = (int)(rt1 - g0);
+  const int e0 = rp[i0], ne = rp[i1] - e0, q0 = trp[i0], nq = trp[i1] - q0;
+  const int h0 = a.ws.halo_off[t], H = a.ws.halo_off[t + 1] - h0;
+  const uint32_t* words = a.ws.relu_words + (int64_t)(l - 1) * a.ws.edge0[a.B] + a.ws.edge0[b];
+  stage_halo_t<CT>(sDS, DS + g0 * 32, a.ws.halo_ids + h0, H);
+  {
+    const float* ea = a.s.ea + (d.col0 + e0) * FeS;
+    for (int p = tid; p < ne; p += CT) put_rec<FE>(sR, p, words[e0 + p], ea + (int64_t)p * FeS);
+    const uint16_t* lt = a.ws.ltcol + a.ws.ltcol_off[t];
+    const int* teid = a.s.t_eid + d.col0;
+    for (int p = tid; p < nq; p += CT) sTR[p] = make_uint2(lt[p], words[teid[q0 + p]]);
+  }
+  const int nr = (int)(rt1 - rt0);
+  for (int p = tid; p < (WR - nr) * 64; p += CT) sD[(nr + (p >> 6)) * LDD + (p & 63)] = 0.f;
+  __syncthreads();
+  float wsum[FA];
+#pragma unroll
+  for (int f = 0; f < FA; ++f) wsum[f] = 0.f;
+  for (int64_t r = rt0 + (tid >> 5); r < rt1; r += CRG) {
+    const int i = (int)(r - g0);
+    const float dsi = DS[r * 32 + c];
+    float cnt = 0.f;
+    float eap[FA];
+#pragma unroll
+    for (int f = 0; f < FA; ++f) eap[f] = 0.f;
+    const int eb = rp[i] - e0, ee = rp[i + 1] - e0;
+    int e = eb;
+    for (; e + 8 <= ee; e += 8) {
+      uint32_t wv[8];
+      float ev[8][FA];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) wv[u] = get_rec<FE>(sR, e + u, ev[u]);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float bit = edge_bit(wv[u], c);
+        cnt += bit;
+#pragma unroll
+        for (int f = 0; f < FE; ++f) eap[f] = fmaf(bit, ev[u][f], eap[f]);
+      }
+    }
+    for (; e < ee; ++e) {
+      float ev[FA];
+      const float bit = edge_bit(get_rec<FE>(sR, e, ev), c);
+      cnt += bit;
+#pragma unroll
+      for (int f = 0; f < FE; ++f) eap[f] = fmaf(bit, ev[f], eap[f]);
+    }
+    const int li = (int)(r - rt0);
+    sD[li * LDD + c] = cnt != 0.f ? dsi * cnt : 0.f;
+#pragma unroll
+    for (int f = 0; f < FE; ++f) wsum[f] += cnt != 0.f ? dsi * eap[f] : 0.f;
+    float acc = 0.f;
+    const int qb = trp[i] - q0, qe = trp[i + 1] - q0;
+    int q = qb;
+    for (; q + 8 <= qe; q += 8) {
+      uint2 tr[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) tr[u] = sTR[q + u];
+      float dv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) dv[u] = sDS[tr[u].x * 32 + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if ((tr[u].y >> c) & 1u) acc += dv[u];
+    }
+    for (; q < qe; ++q) {
+      const uint2 tr = sTR[q];
+      if ((tr.y >> c) & 1u) acc += sDS[tr.x * 32 + c];
+    }
+    sD[li * LDD + 32 + c] = acc;
+  }
+  // each wave's share of dWc (its two row groups summed), combined over the
+  // waves in order by the caller
+#pragma unroll
+  for (int f = 0; f < FE; ++f) {
+    const float v = wsum[f] + __shfl_xor(wsum[f], 32, 64);
+    if (tid < 64 * CW && (tid & 63) < 32) sSh[((tid >> 6) * 32 + c) * FeS + f] = v;
+  }
+}
+
+// dWa = D^T X, dWb = D'^T X, dbe = sum D, dWc = the waves' shares in order
+// (vb_wgrad_mfma's jobs and order for the first three)
+template <int FE>
+__device__ __forceinline__ void edge_wgrad(const VA& a, float* out, const float* sD, int LDD, const float* sX, const float* sSh) {
+  constexpr int FeS = FE > 0 ? FE : 1;
+  const int F = a.F, XS = a.XS, KE = a.KE;
+  const int nwe = 32 * KE;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, kq = lane >> 4;
+  const int KT = (F + 15) >> 4, jw = 2 * 2 * KT;
+  for (int job = wave; job < jw; job += CW) {
+    const int w = job / (2 * KT), rem = job - w * 2 * KT, ct = rem / KT, kt = rem - ct * KT;
+    const int cc = ct * 16 + li, kc = kt * 16 + li;
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < WR; i += 4) acc = mfma4(sD[(i + kq) * LDD + w * 32 + cc], kc < XS ? sX[(i + kq) * XS + kc] : 0.f, acc);
+    if (kc < F) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) out[(ct * 16 + kq * 4 + q) * KE + w * F + kc] = acc[q];
+    }
+  }
+  const int tid = threadIdx.x;
+  const int p0 = tid - (CT - 4 * 32);  // the last 128 threads: dbe, four lanes of 16 rows each
+  if (p0 >= 0) {
+    const int cch = p0 >> 2, ib = (p0 & 3) * (WR / 4);
+    float v = 0.f;
+#pragma unroll
+    for (int u = 0; u < WR / 4; ++u) v += sD[(ib + u) * LDD + cch];
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    if ((p0 & 3) == 0) out[nwe + cch] = v;
+  }
+  if (tid < 32 * FE) {  // dWc [32][Fe]
+    const int cch = tid / FeS, f = tid - cch * FeS;
+    float v = 0.f;
+    for (int w = 0; w < CW; ++w) v += sSh[(w * 32 + cch) * FeS + f];
+    out[cch * KE + 2 * F + f] = v;
+  }
+}
+
+template <int FE>
+__global__ void __launch_bounds__(CT) vc_eb2n1(VA a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int F = a.F, XS = a.XS, KE = a.KE, KN = a.KN;
+  const int t = blockIdx.x, tid = threadIdx.x;
+  const int64_t rt0 = a.ws.tile_row0[t], rt1 = a.ws.tile_row0[t + 1];
+  const int nr = (int)(rt1 - rt0);
+  const int b = a.ws.row_slot[rt0];
+  const dr_graph_desc& d = a.descs[b];
+  const int64_t g0 = a.ws.row0[b];
+  const BwdCarve bc = bwd_carve(F, a.ws.halo_max, a.ws.tile_edges_max, a.ws.tile_tedges_max, FE, true);
+  float* sD = lds + bc.d;
+  float* sX1 = lds + bc.x1;
+  float* sDX = lds + bc.dx;
+  float* sW3 = lds + bc.w3;
+  float* sDU = lds + bc.du;
+  float* sW1 = lds + bc.w1;
+  float* sSh = lds + bc.sh;
+  float* ws = a.ws.base;
+  stage_rows<CT>(sX1, XS, ws + a.L.x1 + rt0 * XS, XS, nr, 0);
+  stage_rows<CT>(sDX, XS, ws + a.L.dx1 + rt0 * XS, XS, nr, 0);
+  for (int p = tid; p < 64 * bc.NOP3; p += CT) {  // vb_gemm<GM_DX1>'s W staging
+    const int k = p / bc.NOP3, n = p - k * bc.NOP3;
+    sW3[p] = n < F ? a.w.we2[(k & 31) * KE + (k < 32 ? 0 : F) + n] : 0.f;
+  }
+  for (int p = tid; p < XS * 32; p += CT) {  // vb_gemm<GM_DXS>'s W staging (Wn1), the DS columns
+    const int k = p >> 5, n = p & 31;
+    sW1[p] = k < F ? a.w.wn1[k * KN + F + n] : 0.f;
+  }
+  chunk_edge_bwd<FE>(a, 2, t, ws + a.L.ds, sD, bc.LDD, lds + bc.halo, lds + bc.rec, reinterpret_cast<uint2*>(lds + bc.trec), sSh);
+  __syncthreads();
+  // X0 / S1 rows into the dead edge region, asynchronously (needed after the next barrier)
+  float* sX0 = lds + bc.x0;
+  float* sS1 = lds + bc.s1;
+  const int i0 = (int)(rt0 - g0);
+  dma_x4<CT>(sX0, a.s.x + (d.node0 + i0) * XS, nr * XS / 4);
+  dma_x4<CT>(sS1, ws + a.L.s1 + rt0 * 32, nr * 8);
+  for (int p = tid; p < (WR - nr) * XS; p += CT) sX0[nr * XS + p] = 0.f;
+  for (int p = tid; p < (WR - nr) * 32; p += CT) sS1[nr * 32 + p] = 0.f;
+  edge_wgrad<FE>(a, part_row(a, 2, t), sD, bc.LDD, sX1, sSh);
+  // dX1 = dX1 + [D | D'] [Wa2; Wb2] (vb_gemm<GM_DX1>), then DU1 = relu'(X1) dX1 (vb_du)
+  const int lane = tid & 63, wave = tid >> 6, li = lane & 15, kq = lane >> 4;
+  const int nct = bc.NOP3 / 16;
+  for (int job = (wave + CW - 8 % CW) % CW; job < 4 * nct; job += CW) {
+    const int ib = (job / nct) * 16, n = (job % nct) * 16 + li;
+    floatx4 acc;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = n < F ? sDX[(ib + kq * 4 + q) * XS + n] : 0.f;
+    for (int k0 = 0; k0 < 64; k0 += 4) acc = mfma4(sD[(ib + li) * bc.LDD + k0 + kq], sW3[(k0 + kq) * bc.NOP3 + n], acc);
+    if (n < XS) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = ib + kq * 4 + q;
+        sDU[i * bc.LU + n] = n < F ? relu_bwd(sX1[i * XS + n], acc[q]) : 0.f;
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // DS1 = DU1 Wn1[:, F:] (vb_gemm<GM_DXS> layer 1) and layer 1's dWn / dbn
+  for (int job = wave; job < 8; job += CW) {
+    const int ib = (job >> 1) * 16, n = (job & 1) * 16 + li;
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < XS; k0 += 4) acc = mfma4(sDU[(ib + li) * bc.LU + k0 + kq], sW1[(k0 + kq) * 32 + n], acc);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = ib + kq * 4 + q;
+      if (i < nr) ws[a.L.d + (rt0 + i) * 32 + n] = acc[q];
+    }
+  }
+  node_wgrad<CT>(a, part_row(a, 1, t), sDU, bc.LU, sX0, sS1, 8);
+}
+
+template <int FE>
+__global__ void __launch_bounds__(CT) vc_eb1(VA a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int F = a.F, XS = a.XS;
+  const int t = blockIdx.x;
+  const int64_t rt0 = a.ws.tile_row0[t], rt1 = a.ws.tile_row0[t + 1];
+  const int nr = (int)(rt1 - rt0);
+  const int b = a.ws.row_slot[rt0];
+  const dr_graph_desc& d = a.descs[b];
+  const int i0 = (int)(rt0 - a.ws.row0[b]);
+  const BwdCarve bc = bwd_carve(F, a.ws.halo_max, a.ws.tile_edges_max, a.ws.tile_tedges_max, FE, false);
+  float* sD = lds + bc.d;
+  float* sX0 = lds + bc.x0;
+  stage_rows<CT>(sX0, XS, a.s.x + (d.node0 + i0) * XS, XS, nr, 0);
+  chunk_edge_bwd<FE>(a, 1, t, a.ws.base + a.L.d, sD, bc.LDD, lds + bc.halo, lds + bc.rec, reinterpret_cast<uint2*>(lds + bc.trec), lds + bc.sh);
+  __syncthreads();
+  edge_wgrad<FE>(a, part_row(a, 1, t), sD, bc.LDD, sX0, lds + bc.sh);
+}
+
+// both layers' chunk partials per graph, in chunk order (vb_wgrad_combine x 2)
+__global__ void __launch_bounds__(RB) vc_combine(VA a) {
+  const int total = layer_grad_size(a.F, a.Fe);
+  const int64_t work = (int64_t)a.B * 2 * total;
+  for (int64_t q = blockIdx.x * (int64_t)RB + threadIdx.x; q < work; q += (int64_t)gridDim.x * RB) {
+    const int b = (int)(q / (2 * total)), rem = (int)(q - (int64_t)b * 2 * total), lay = rem / total, p = rem - lay * total;
+    const float* part = a.ws.part + (int64_t)lay * a.ws.n_chunks * total + p;
+    const int ce = a.ws.chunk_first[b + 1];
+    float v = 0.f;
+    int ch = a.ws.chunk_first[b];
+    for (; ch + 8 <= ce; ch += 8) {
+      float u[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) u[k] = part[(int64_t)(ch + k) * total];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v += u[k];
+    }
+    for (; ch < ce; ++ch) v += part[(int64_t)ch * total];
+    a.p.slab[(int64_t)(a.p.slot ? a.p.slot[b] : b) * DR_VANILLA_SLAB_STRIDE(a.F, a.Fe) + (int64_t)lay * total + p] = v;
+  }
+}
+
+inline bool chunk_carves(const dr_vanilla_scratch* sc, int F, int Fe, int64_t* fwd1, int64_t* fwd2, int64_t* eb2, int64_t* eb1) {
+  *fwd1 = 4LL * fwd_carve(F, sc->halo_max, sc->tile_edges_max, Fe, true).total;
+  *fwd2 = 4LL * fwd_carve(F, sc->halo_max, sc->tile_edges_max, Fe, false).total;
+  *eb2 = 4LL * bwd_carve(F, sc->halo_max, sc->tile_edges_max, sc->tile_tedges_max, Fe, true).total;
+  *eb1 = 4LL * bwd_carve(F, sc->halo_max, sc->tile_edges_max, sc->tile_tedges_max, Fe, false).total;
+  const int64_t lim = 160 * 1024;
+  return *fwd1 <= lim && *fwd2 <= lim && *eb2 <= lim && *eb1 <= lim;
+}
+
+// the chunk-fused kernels run when the tile plan cuts graphs into the 64-row
+// weight-gradient chunks, the partial buffer holds both layers, Fe <= 4 and
+// every carve fits one workgroup's LDS
+inline bool chunk_fused(const dr_vanilla_scratch* sc, int F, int Fe) {
+  if (!sc->tile_row0 || !sc->relu_words || sc->tile_rows != WR || sc->part_layers != 2 || Fe > 4 || F > 64 ||
+      sc->n_tiles != sc->n_chunks)
+    return false;
+  int64_t f1, f2, e2, e1;
+  return chunk_carves(sc, F, Fe, &f1, &f2, &e2, &e1);
+}
+
+inline int64_t nb2_lds(int F) { return 4LL * (WR * (r4(F) + 4) + WR * r4(F) + WR * 32 + r4(F) * r16(F + 32)); }
+
+// the chunk-fused step (vb_gemm<GM_HALVES> for layer 1, then the vc_* kernels)
+template <int FE>
+int launch_chunk_fused(const VA& a, const dr_vanilla_scratch* sc, hipStream_t st, int gg, size_t glds_halves) {
+  int64_t f1, f2, e2, e1;
+  chunk_carves(sc, a.F, a.Fe, &f1, &f2, &e2, &e1);
+  const dim3 tg((unsigned)sc->n_tiles);
+  DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&vc_fwd<FE, 1>)));
+  DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&vc_fwd<FE, 2>)));
+  DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&vc_eb2n1<FE>)));
+  DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&vc_eb1<FE>)));
+  DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&vc_nb2)));
+  hipLaunchKernelGGL(vb_gemm<GM_HALVES>, dim3(gg), dim3(RB), glds_halves, st, a, 1);
+  hipLaunchKernelGGL((vc_fwd<FE, 1>), tg, dim3(CT), (size_t)f1, st, a);
+  hipLaunchKernelGGL((vc_fwd<FE, 2>), tg, dim3(CT), (size_t)f2, st, a);
+  hipLaunchKernelGGL(vb_head, dim3(a.B), dim3(HT), 0, st, a);
+  if (a.p.flags & DR_PASS_BACKWARD) {
+    hipLaunchKernelGGL(vc_nb2, tg, dim3(NBT), (size_t)nb2_lds(a.F), st, a);
+    hipLaunchKernelGGL(vc_eb2n1<FE>, tg, dim3(CT), (size_t)e2, st, a);
+    hipLaunchKernelGGL(vc_eb1<FE>, tg, dim3(CT), (size_t)e1, st, a);
+    hipLaunchKernelGGL(vc_combine, dim3(rows_grid((int64_t)a.B * 2 * layer_grad_size(a.F, a.Fe), RB)), dim3(RB), 0, st, a);
+  }
+  return (int)hipGetLastError();
+}
+
 }  // namespace
 
 extern "C" int64_t dr_vanilla_scratch_floats(int64_t n_rows, int32_t n_feat, int32_t n_edge_feat) {
@@ -1167,6 +1775,15 @@ extern "C" int dr_vanilla_graph_pass(const dr_graph_store* store, const dr_graph
   const size_t lds_wg = (size_t)dr_vanilla_lds_bytes(a.F, a.Fe, pass->out_dim);
   const int gg = rows_grid(R, GT) < 1024 ? rows_grid(R, GT) : 1024;
   auto glds = [&](int mode) { return (size_t)4 * gemm_lds_floats(mode, a.F); };
+  if (chunk_fused(scratch, a.F, a.Fe)) {
+    switch (a.Fe) {
+      case 0: return launch_chunk_fused<0>(a, scratch, st, gg, glds(GM_HALVES));
+      case 1: return launch_chunk_fused<1>(a, scratch, st, gg, glds(GM_HALVES));
+      case 2: return launch_chunk_fused<2>(a, scratch, st, gg, glds(GM_HALVES));
+      case 3: return launch_chunk_fused<3>(a, scratch, st, gg, glds(GM_HALVES));
+      default: return launch_chunk_fused<4>(a, scratch, st, gg, glds(GM_HALVES));
+    }
+  }
   for (int l = 1; l <= 2; ++l) {
     hipLaunchKernelGGL(vb_gemm<GM_HALVES>, dim3(gg), dim3(RB), glds(GM_HALVES), st, a, l);
     if (!launch_edge8(true, a, l, dim3(rows_grid(R, RB / 32)), st))

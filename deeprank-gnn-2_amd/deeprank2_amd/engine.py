@@ -464,6 +464,49 @@ class FusedTrainStep:
         self.step_count = n
         return ms
 
+    def time_reduce(self, handles, n_launches, global_batch=None):
+        """Mean duration (ms) of the step's second launch alone
+        (``dr_reduce_update``: the fixed-order gradient sums + Adam), timed like
+        :meth:`time_graph_pass` (``n_launches`` captured back to back, HIP
+        events on the launch stream).  With the graph pass's time it splits a
+        step into pass / reduce / the rest (launch gaps, host).  State is
+        restored.  None where the step has no separate reduce launch (one-launch
+        step, data-parallel step, layer-level batches)."""
+        if self.pg is not None or any(self.one_launch(h) or (self.spec.layers is not None and layered.needs_layers(self.spec, h, self.out_dim)) for h in handles):
+            return None
+        lib = _lib.load()
+        for h in handles:
+            self._ensure(h.B)
+        snap = [t.detach().clone() for t in self._state_tensors()]
+        n = self.step_count
+        for h in handles:  # one real step each, so the slabs hold a batch's partials
+            self.step(h, global_batch=global_batch)
+        torch.cuda.synchronize(self.device)
+        stream = _lib.stream_ptr(self.device)
+
+        def reduces(k):
+            for i in range(k):
+                h = handles[i % len(handles)]
+                self._table.slab_rows = slab_rows_for(self.spec, h)
+                scale = self.loss_scale(h, global_batch or h.B * self.world)
+                _lib.check(lib.dr_reduce_update(self._table, self.slab.data_ptr(), self.head.data_ptr(), h.B, self._adam, self.lpg.data_ptr(), scale, self.loss_out.data_ptr(), stream), "dr_reduce_update")
+
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            reduces(n_launches)
+        g.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize(self.device)
+        ms = e0.elapsed_time(e1) / n_launches
+        del g
+        for t, s in zip(self._state_tensors(), snap):
+            t.data.copy_(s)
+        self.step_count = n
+        return ms
+
     def capture(self, h: BatchHandle, global_batch=None, dropout=True):
         """Capture one training step on ``h`` into a HIP graph (``torch.cuda.CUDAGraph``).
 

@@ -43,7 +43,7 @@ class BatchHandle:
         self.force_layers = False  # run the layer-level path (layered.py) even when the graph pass fits (diagnostic)
         self.vanilla_words = True  # Vanilla pipeline: forward ReLU words feed the backward (False: recomputed)
         self.vanilla_split = None  # Vanilla per-graph kernel: workgroups per graph (None: by batch size)
-        self.vanilla_tile_rows = 16  # Vanilla pipeline edge kernels: rows per halo-staged tile (0: untiled gathers)
+        self.vanilla_tile_rows = VANILLA_CHUNK  # Vanilla pipeline: rows per halo-staged tile (64: the chunk-fused kernels; 16 / 32: edge kernels only; 0: untiled gathers)
         self.fault = None  # device uint32 [2] (dr_pass.fault) of the autograd path's passes, made on first use
         self.sibling_split = 0  # GINet per-graph kernel over k workgroups per graph (0/1: off; None: by batch size)
         self.mixed_dispatch = False  # graphs that fit LDS on the per-graph kernel, the rest on the large path (two streams; measured slower at configs[4])
@@ -70,7 +70,11 @@ class BatchHandle:
             chunk_slot = np.repeat(np.arange(self.B, dtype=np.int32), chunks)
             lib = _lib.load()
             floats = int(lib.dr_vanilla_scratch_floats(rows, n_feat, n_edge_feat))
-            part = int(lib.dr_vanilla_part_floats(n_feat, n_edge_feat)) * int(chunk_first[-1])
+            # the chunk-fused kernels (tiles of DR_VANILLA_CHUNK rows, Fe <= 4) keep both
+            # layers' partial rows at once (dr_vanilla_scratch.part_layers)
+            chunk_fused = self.vanilla_words and self.vanilla_tile_rows == VANILLA_CHUNK and 0 <= n_edge_feat <= 4
+            part_layers = 2 if chunk_fused else 1
+            part = int(lib.dr_vanilla_part_floats(n_feat, n_edge_feat)) * int(chunk_first[-1]) * part_layers
             dev = self.store.device
             ints = torch.from_numpy(np.concatenate([row0, slot, chunk_first, chunk_slot])).to(dev)
             c = _lib.VanillaScratchC()
@@ -82,6 +86,7 @@ class BatchHandle:
             c.chunk_slot = base + 4 * (2 * (self.B + 1) + rows)
             c.n_chunks = int(chunk_first[-1])
             c.part = pbuf.data_ptr()
+            c.part_layers = part_layers
             # per-edge ReLU words of both layers (forward -> backward);
             # vanilla_words = False: the backward recomputes them (diagnostic)
             ne = self.store._sizes[1][self.gids_host.astype(np.int64)]  # noqa: SLF001
@@ -98,7 +103,8 @@ class BatchHandle:
                         keep += tensors
                         (c.tile_row0, c.halo_off, c.halo_ids, c.lcol_off, c.lcol, c.ltcol_off, c.ltcol) = (t.data_ptr() for t in tensors)
                         c.n_tiles, c.halo_max, c.tile_edges_max, c.tile_tedges_max = n_tiles, hmax, emax, tmax
-                        if VANILLA_CHUNK % tr == 0 and 0 < n_edge_feat <= 4:  # the tiled kernels; tiles never straddle a weight-gradient chunk
+                        c.tile_rows = tr
+                        if VANILLA_CHUNK % tr == 0 and 0 < n_edge_feat <= 4 and not chunk_fused:  # the 16/32-row tiled kernels; tiles never straddle a weight-gradient chunk
                             tfirst = torch.from_numpy(np.concatenate([[0], np.cumsum((n + tr - 1) // tr)]).astype(np.int32)).to(dev)
                             twc = torch.empty(n_tiles * 32 * max(1, n_edge_feat), dtype=torch.float32, device=dev)
                             keep += [tfirst, twc]
@@ -352,10 +358,11 @@ def vanilla_fused_scratch_floats(n, e, fe):
     """Mirror of dr_vanilla_fused_scratch_floats (vanilla_graph.hip), vectorised
     over graphs: S1 (32N), two ReLU word arrays (E + 1 each, CSR order), the
     split's exchange rows XA, XB (32N each) and column sums (4 x 32), every part
-    rounded up to 16 bytes (fe: no per-edge-feature part since r03)."""
+    rounded up to 16 bytes, then the siblings' weight-gradient partial rows
+    (4 x DR_VANILLA_SLAB_STRIDE(32, fe), r04)."""
     r4 = lambda v: (np.asarray(v, dtype=np.int64) + 3) & ~3  # noqa: E731
-    del fe
-    return 3 * r4(32 * np.asarray(n, dtype=np.int64)) + 2 * r4(np.asarray(e, dtype=np.int64) + 1) + 32 * 4
+    part = 4 * 2 * (32 * (2 * 32 + fe) + 32 + 32 * (32 + 32) + 32)
+    return 3 * r4(32 * np.asarray(n, dtype=np.int64)) + 2 * r4(np.asarray(e, dtype=np.int64) + 1) + 32 * 4 + part
 
 
 def make_pass(out_dim, flags, *, dropout: Dropout | None = None, dout=None, loss_kind=_lib.DR_LOSS_NONE, loss_scale=1.0, class_w=None, out=None, loss_per_graph=None, slab=None, head=None, stamps=None, step_counter=None, fault=None, spin_limit=0):

@@ -4,8 +4,9 @@ Torch-free, like ``h5extract``, so it runs under any interpreter with h5py.
 Used to materialise synthetic datasets (``deeprank2_amd.utils.synthetic``) as
 files ``GraphDataset`` reads.
 
-Usage: ``python h5write.py IN.npz OUT.hdf5`` where IN.npz holds
-``__entries__`` and ``"<k>|<group>/<name>"`` arrays (k = entry position).
+Usage: ``python h5write.py IN.npz OUT.hdf5`` where IN.npz is an
+``h5extract`` archive (``__entries__`` = the entry names, one blob of
+``"<k>|<group>/<name>"`` arrays, k = entry position).
 """
 
 import sys
@@ -23,15 +24,14 @@ def write(path, graphs, h5py):
 
 def _main(npz, out):
     import h5py  # noqa: PLC0415
+    import h5extract  # noqa: PLC0415  (this script's directory is on sys.path)
 
     with np.load(npz, allow_pickle=False) as z:
         entries = [str(s) for s in z["__entries__"]]
         graphs = {e: {} for e in entries}
-        for key in z.files:
-            if key.startswith("__"):
-                continue
+        for key, arr in h5extract.unpack(z).items():
             k, name = key.split("|", 1)
-            graphs[entries[int(k)]][name] = z[key]
+            graphs[entries[int(k)]][name] = arr
     write(out, graphs, h5py)
 
 

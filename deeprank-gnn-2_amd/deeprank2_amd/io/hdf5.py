@@ -65,12 +65,10 @@ def _split_dump(z, n_files):
         fi, entry = str(s).split("\t", 1)
         files[int(fi)][entry] = {}
         order.append((int(fi), entry))
-    for key in z.files:
-        if key.startswith("__"):
-            continue
+    for key, arr in h5extract.unpack(z).items():
         k, name = key.split("|", 1)
         fi, entry = order[int(k)]
-        files[fi][entry][name] = z[key]
+        files[fi][entry][name] = arr
     return files
 
 
@@ -97,16 +95,11 @@ def read_files(paths) -> list:
         p = paths[i]
         try:
             if h5py is not None:
-                entries = {}
-                with h5py.File(p, "r") as f5:
-                    for entry in f5:
-                        d = {}
-                        for g in h5extract.GROUPS:
-                            if g in f5[entry]:
-                                tmp = {}
-                                h5extract._walk(f5[entry][g], g, tmp, 0)  # noqa: SLF001
-                                d.update({name.split("|", 1)[1]: v for name, v in tmp.items()})
-                        entries[entry] = d
+                ents, recs = h5extract.read_arrays([p], workers=1)  # no fork of this (torch / HIP) process
+                entries = {e.split("\t", 1)[1]: {} for e in ents}
+                names = [e.split("\t", 1)[1] for e in ents]
+                for k, name, arr in recs:
+                    entries[names[k]][name] = arr
                 res = entries
             else:
                 with tempfile.TemporaryDirectory() as td:
@@ -136,11 +129,8 @@ def write_graphs(path, graphs) -> None:
         return
     with tempfile.TemporaryDirectory() as td:
         npz = os.path.join(td, "graphs.npz")
-        arrays = {"__entries__": np.array(list(graphs), dtype=np.str_)}
-        for k, (_entry, d) in enumerate(graphs.items()):
-            for name, v in d.items():
-                arrays[f"{k}|{name}"] = np.asarray(v)
-        np.savez(npz, **arrays)
+        recs = [(k, name, np.asarray(v)) for k, d in enumerate(graphs.values()) for name, v in d.items()]
+        np.savez(npz, **h5extract.pack(list(graphs), recs, [str(path)]))
         from deeprank2_amd.io import h5write  # noqa: PLC0415
 
         r = subprocess.run([external_python(), h5write.__file__, npz, str(path)], capture_output=True, text=True, timeout=3600, check=False)

@@ -46,6 +46,7 @@ from torch.nn.functional import softmax
 
 from deeprank2_amd.dataset import CLASSIF, REGRESS, GraphDataset
 from deeprank2_amd.distributed import plan_shards
+from deeprank2_amd.epoch import runner_for
 from deeprank2_amd.engine import FusedTrainStep
 from deeprank2_amd.io.checkpoint import load_checkpoint
 from deeprank2_amd.exporters import HDF5OutputExporter, OutputExporterCollection
@@ -69,6 +70,9 @@ class Trainer:
     # ngpu > 1: how a global batch is spread over the ranks (distributed.plan_shards):
     # "auto" (contiguous unless imbalanced by edges), "contiguous" or "edges"
     shard_policy = "auto"
+    # one process, fused step, every graph on the per-graph kernel: each training
+    # epoch replays one captured HIP graph of all its steps (epoch.py)
+    capture_epochs = True
 
     def __init__(  # noqa: PLR0913, PLR0912, C901
         self,
@@ -94,6 +98,7 @@ class Trainer:
         self.data_type = self.batch_size_train = self.batch_size_test = self.shuffle = None
         self.model_load_state_dict = None
         self._fused = None
+        self._runners = {}
         if self.pretrained_model is None:
             self._setup_for_training(class_weights, precluster)
         else:
@@ -459,9 +464,13 @@ class Trainer:
         loss_sum = torch.zeros((), dtype=torch.float64, device=dev)
         count = 0
         ds = self.dataset_train
+        batches = self.train_loader.batches()
         if step is not None:
-            self._targets_for_kernel(ds, dev)
-        for idx in self.train_loader.batches():
+            store = self._targets_for_kernel(ds, dev)
+            runner = runner_for(step, store, [len(b) for b in batches], self._runners) if (self.capture_epochs and self.process_group is None) else None
+            if runner is not None:  # the whole epoch as one captured HIP graph (epoch.py)
+                return self._epoch_captured(runner, ds, batches, epoch_number, pass_name, t0)
+        for idx in batches:
             b = len(idx)
             if step is not None:
                 local, plan = self._shard(ds, idx)
@@ -495,6 +504,28 @@ class Trainer:
             step.check_faults()  # a skipped step (hand-off gave up) is an error, once per epoch
         out_l = torch.cat(outputs).cpu().numpy().tolist() if outputs else []
         tgt_l = torch.cat(targets).cpu().numpy().tolist() if targets else []
+        dt = time() - t0
+        self._output_exporters.process(pass_name, epoch_number, names, out_l, tgt_l, epoch_loss)
+        _log.info(f"{pass_name} loss {epoch_loss} | time {dt}")
+        return epoch_loss
+
+    def _epoch_captured(self, runner, ds, batches, epoch_number, pass_name, t0):
+        """The epoch's fused steps replayed from one HIP graph: the same
+        launches, losses and outputs as the per-batch loop (bit for bit), the
+        loss sum in the loop's order, one device->host copy at the end."""
+        losses, pred = runner.run(batches)
+        idx_all = np.concatenate([np.asarray(b) for b in batches])
+        pred, y = self._format_output(pred.clone(), self.dataset_train._targets_of(idx_all))  # noqa: SLF001
+        step_losses = losses.double().cpu().numpy()
+        loss_sum = 0.0
+        for lv, b in zip(step_losses, runner.sizes):
+            loss_sum += float(lv) * b
+        count = int(idx_all.size)
+        epoch_loss = loss_sum / count if count else None
+        self._fused.check_faults()
+        out_l = self._export_pred(pred).cpu().numpy().tolist()
+        tgt_l = y.detach().cpu().numpy().tolist()
+        names = [ds.index_entries[i][1] for i in idx_all]
         dt = time() - t0
         self._output_exporters.process(pass_name, epoch_number, names, out_l, tgt_l, epoch_loss)
         _log.info(f"{pass_name} loss {epoch_loss} | time {dt}")

@@ -118,6 +118,38 @@ def make_graph(rng, n_lo=180, n_hi=220, mean_degree=15.0, k_lo=2, k_hi=6, n_feat
     }
 
 
+def connect_clusters(g):
+    """Merge every depth-0 cluster that has no edge to another cluster into
+    the lowest-numbered other cluster (repeated until each cluster has one, or
+    one cluster is left — then one edge's source node becomes a cluster of its
+    own), relabelled to consecutive ids.  A cluster without a
+    cross edge becomes a pooled node without out-edges, which FoutNet turns
+    into NaN (mean(empty), foutnet.py:58): workloads meant to train keep their
+    pooled graphs free of such nodes.  A no-op on graphs that have none."""
+    c = g["cluster0"].copy()
+    ij = g["index"]
+    while True:
+        ids = np.unique(c)
+        if ids.size < 2:  # noqa: PLR2004
+            break
+        cross = c[ij[:, 0]] != c[ij[:, 1]]
+        has = np.isin(ids, np.concatenate([c[ij[cross, 0]], c[ij[cross, 1]]]))
+        if has.all():
+            break
+        lone = ids[~has][0]
+        c[c == lone] = ids[ids != lone][0]
+    if np.unique(c).size < 2 and len(ij) and g["cluster0"].max() > 0:  # noqa: PLR2004
+        c = np.ones_like(c)  # disconnected clusters merged into one: split one edge's endpoint off instead
+        c[ij[0, 0]] = 0
+    if np.array_equal(c, g["cluster0"]):
+        return g
+    _, c = np.unique(c, return_inverse=True)
+    out = dict(g)
+    out["cluster0"] = c.astype(np.int64)
+    out["cluster1"] = np.zeros(int(c.max()) + 1, dtype=np.int64)
+    return out
+
+
 def make_dataset(n_graphs, seed=0, **kw):
     rng = np.random.default_rng(seed)
     return [make_graph(rng, **kw) for _ in range(n_graphs)]

@@ -239,3 +239,54 @@ def test_foutnet_captured_replay_and_determinism():
 def test_foutnet_cpu_model_raises():
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         amd.FoutNet(30, 1)(P.Batch.from_data_list(_synthetic(1, seed=1)))
+
+
+def test_foutnet_fused_train_step_vs_oracle_config3_batch64():
+    """BASELINE configs[2] shape: 64 synthetic residue graphs (N~200, E~3k,
+    F=30, Fe=3) through FusedTrainStep — forward, MSE, backward, Adam — for
+    three consecutive steps: each step's outputs, loss and gradients against
+    the oracle (foutnet.py:48-66,99-118) run on the same weights, and the
+    fused Adam against torch.optim.Adam carrying the same state.  Pooled nodes
+    without an out-edge would give NaN rows (mean(empty), foutnet.py:58): NaN
+    positions must agree, the rest within 1e-4."""
+    from deeprank2_amd.utils.synthetic import make_dataset
+
+    datas = [data_ref.synthetic_to_data(g, f"c{i}") for i, g in enumerate(make_dataset(64, seed=0))]
+    model_o, model = _pair(30, 1, seed=31)
+    model.train()
+    store = GraphStore(pack_graphs(records_from_batch(P.Batch.from_data_list(datas))), DEV)
+    h = BatchHandle(store, np.arange(64))
+    step = FusedTrainStep(model)
+    by_name = dict(zip(amd.PARAM_NAMES, step.params))
+    adam_sd = None
+    for it in range(3):
+        with torch.no_grad():  # the oracle on the fused step's current weights
+            for n, po in model_o.named_parameters():
+                po.copy_(by_name[n].detach().cpu())
+        model_o.zero_grad()
+        bat = P.Batch.from_data_list([d.clone() for d in datas])
+        out_o = model_o(bat)
+        loss_o = torch.nn.functional.mse_loss(out_o.reshape(-1), bat.y)
+        loss_o.backward()
+        before = [p.detach().clone() for p in step.params]
+        loss, out = step.step(h)
+        o, r = out.cpu().numpy(), out_o.detach().numpy()
+        np.testing.assert_array_equal(np.isnan(o), np.isnan(r), err_msg=f"step {it}")
+        np.testing.assert_allclose(o, r, equal_nan=True, **TOL)
+        if np.isnan(r).any():
+            assert np.isnan(float(loss)) and np.isnan(float(loss_o))
+            return  # a NaN batch: the trajectory ends here on both sides
+        assert float(loss) == pytest.approx(float(loss_o.detach()), rel=1e-4)
+        grads = dict(zip(amd.PARAM_NAMES, step.grads))
+        for n, p in model_o.named_parameters():
+            assert_grad_close(grads[n].cpu().numpy(), p.grad.numpy(), err_msg=f"{n} step {it}")
+        ref = [torch.nn.Parameter(b) for b in before]
+        ref_opt = torch.optim.Adam(ref, lr=1e-3, weight_decay=1e-5)
+        if adam_sd is not None:
+            ref_opt.load_state_dict(adam_sd)
+        for rr, g in zip(ref, step.grads):
+            rr.grad = g.detach().clone()
+        ref_opt.step()
+        for n, rr, p in zip(amd.PARAM_NAMES, ref, step.params):
+            np.testing.assert_allclose(p.detach().cpu().numpy(), rr.detach().cpu().numpy(), rtol=1e-5, atol=1e-7, err_msg=f"{n} step {it}")
+        adam_sd = step.adam_state_dict()

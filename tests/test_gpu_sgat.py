@@ -137,3 +137,46 @@ def test_sgat_needs_one_edge_feature():
     la = amd.SGraphAttentionLayer(30, 16).to(DEV)
     with pytest.raises(ValueError, match="one edge feature"):
         la(datas[0].x.to(DEV), datas[0].edge_index.to(DEV), datas[0].edge_attr.to(DEV))
+
+
+def test_sgat_adam_trajectory_vs_oracle_replay():
+    """40 Adam steps of the fused SGAT step over 4 resident mini-batches of
+    residue graphs (edge weight = the distance feature, as in the bench)
+    against the oracle (sgat.py:56-133) trained by torch.optim.Adam on the
+    same batches from the same initialisation: the per-step losses and the
+    final parameters agree.  The reference itself starts from a very large
+    loss (~3e4 on the bench's batches: distance-weighted neighbour means) and
+    is still at ~30-150 after a few hundred steps (an oracle replay of the
+    bench's first 230 steps: 33461 -> 36.1), so the bench's SGAT final loss of
+    ~140 is this trajectory, not a divergence of the kernels."""
+    from deeprank2_amd.utils.synthetic import make_dataset
+
+    gs = make_dataset(64, seed=77)
+    datas = [data_ref.synthetic_to_data(g, f"t{i}") for i, g in enumerate(gs)]
+    for d in datas:
+        d.edge_attr = d.edge_attr[:, :1].contiguous()
+    batches = [list(range(k * 16, (k + 1) * 16)) for k in range(4)]
+    torch.manual_seed(12)
+    model_o = gnn_ref.SGAT(30, 1)
+    model = amd.SGAT(30, 1)
+    model.load_state_dict(model_o.state_dict())
+    model = model.to(DEV).train()
+    opt_o = torch.optim.Adam(model_o.parameters(), lr=1e-3, weight_decay=1e-5)
+    store = GraphStore(pack_graphs(records_from_batch(P.Batch.from_data_list(datas))), DEV)
+    hs = [BatchHandle(store, np.array(b)) for b in batches]
+    step = FusedTrainStep(model)
+    lo, lg = [], []
+    for s in range(40):
+        bat = P.Batch.from_data_list([datas[i].clone() for i in batches[s % 4]])
+        opt_o.zero_grad()
+        loss_o = torch.nn.functional.mse_loss(model_o(bat).reshape(-1), bat.y)
+        loss_o.backward()
+        opt_o.step()
+        lo.append(float(loss_o.detach()))
+        loss, _ = step.step(hs[s % 4])
+        lg.append(float(loss))
+    assert lo[0] > 100 * lo[-1]  # the large-initial-loss regime of the bench
+    np.testing.assert_allclose(lg, lo, rtol=2e-3)
+    ref = dict(model_o.named_parameters())
+    for n, p in zip(amd.PARAM_NAMES, step.params):
+        np.testing.assert_allclose(p.detach().cpu().numpy(), ref[n].detach().numpy(), rtol=2e-3, atol=2e-4, err_msg=n)

@@ -165,3 +165,33 @@ def test_ginet_classification_class_weights_checkpoint_and_test(files, tmp_path)
     mem.records.clear()
     t.test(batch_size=8)
     np.testing.assert_allclose(np.array(mem2.records[0]["output"]), np.array(mem.records[0]["output"]), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("model_cls", [GINet, FoutNet])
+def test_captured_epochs_bit_identical_to_per_batch_steps(files, model_cls):
+    """Trainer epochs replayed from one captured HIP graph (epoch.py) against
+    the per-batch loop: the same epoch losses, exported outputs and final
+    parameters, bit for bit (shuffled batches, a last partial batch, GINet's
+    in-kernel dropout)."""
+    from deeprank2_amd import trainer as trainer_mod
+
+    res = []
+    for captured in (True, False):
+        tr, va = _sets(files[0], files[1])
+        mem = MemoryOutputExporter()
+        torch.manual_seed(21)
+        trainer_mod.Trainer.capture_epochs = captured
+        try:
+            t = Trainer(model_cls, tr, va, cuda=True, output_exporters=[mem], precluster=False)
+            t.train(nepoch=3, batch_size=5, shuffle=True, validate=True, best_model=False, filename=None)
+        finally:
+            trainer_mod.Trainer.capture_epochs = True
+        assert t._fused  # noqa: SLF001
+        assert bool(t._runners) == captured  # noqa: SLF001  (the captured path ran)
+        res.append((mem.records, {k: v.detach().cpu() for k, v in t.model.state_dict().items()}))
+    (ra, pa), (rb, pb) = res
+    assert [r["loss"] for r in ra] == [r["loss"] for r in rb]
+    assert [r["output"] for r in ra] == [r["output"] for r in rb]
+    assert [r["entry"] for r in ra] == [r["entry"] for r in rb]
+    for k in pa:
+        assert torch.equal(pa[k], pb[k]), k

@@ -229,13 +229,15 @@ def test_vanilla_pipeline_relu_words_bit_identical_to_recomputed(fe):
     _assert_same(res, _dwc_mask(res[0][1].numel(), len(datas), fe) if fe <= 4 else None)
 
 
-@pytest.mark.parametrize("fe,tile", [(3, 64), (1, 32), (4, 128)])
+@pytest.mark.parametrize("fe,tile", [(3, 64), (1, 64), (4, 64), (3, 16), (1, 32), (4, 128)])
 def test_vanilla_pipeline_halo_tiles_bit_identical(fe, tile):
     """The tiled edge kernels (each tile's halo rows, edge attributes, words and
     halo-local columns staged in LDS) give exactly the outputs, slabs, head
     vectors and ReLU words of the untiled 8-in-flight kernels, on atom-size
     graphs, a small graph, a node without edges and a hub row (tiles dividing
-    the 64-row weight-gradient chunks: dWc at fp32 tolerance, _assert_same)."""
+    the 64-row weight-gradient chunks: dWc at fp32 tolerance, _assert_same).
+    64-row tiles run the chunk-fused kernels (vc_*: edge work, node MLPs, next
+    layer's node GEMMs, node backward and weight-gradient partials per chunk)."""
     from deeprank2_amd import _lib
 
     datas = _datas(2, seed=47, n_lo=900, n_hi=1300, mean_degree=15.0) + _datas(1, seed=48, n_lo=20, n_hi=30)

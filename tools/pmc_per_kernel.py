@@ -21,8 +21,9 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
+    name = name.replace("(anonymous namespace)::", "").replace("void ", "")
     name = re.sub(r"\(.*$", "", name)  # drop the argument list
-    return name.replace("void ", "").strip()
+    return name.strip()
 
 
 def main():
