@@ -48,3 +48,19 @@ __host__ __device__ inline float dr_uniform(uint64_t seed, uint64_t offset, uint
   z = dr_mix64(z ^ (0xD1B54A32D192ED03ULL * ((uint64_t)idx + 1)));
   return (float)(z >> 40) * (1.0f / 16777216.0f);
 }
+
+// Host-side description of an LDS carve for the carve tests
+// (tests/test_lds_carves.py): "name=value;" pairs, region offsets in 4-byte
+// words, "total" the words the carve reserves, "$name" a layout parameter.
+#include <cstdio>
+struct DrCarveDesc {
+  char* buf;
+  int len, pos;
+};
+inline void dr_carve_put(DrCarveDesc& d, const char* name, long long v) {
+  const int room = d.len - d.pos;
+  const int n = std::snprintf(d.buf + (room > 0 ? d.pos : 0), room > 0 ? room : 0, "%s=%lld;", name, v);
+  d.pos += n > 0 ? n : 0;
+}
+#define DR_DESC(d, c, f) dr_carve_put(d, #f, (long long)(c).f)
+#define DR_DESC_P(d, c, f) dr_carve_put(d, "$" #f, (long long)(c).f)

@@ -1116,3 +1116,104 @@ extern "C" int dr_sgat_large_pass(const dr_graph_store* store, const dr_graph_de
                                   int32_t z_stride, int32_t conv_lds_bytes, int32_t tail_lds_bytes, void* stream) {
   return fout_large_family(true, store, descs, n_batch, plan, w, pass, z_stride, conv_lds_bytes, tail_lds_bytes, stream);
 }
+
+// ---- carve descriptions for the host-side carve tests (tests/test_lds_carves.py)
+extern "C" int dr_debug_carve_fout(const int32_t* q, char* buf, int32_t len) {
+  const Carve c = carve(q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7], q[8] != 0, q[9]);
+  DrCarveDesc d{buf, len, 0};
+  DR_DESC_P(d, c, KP);
+  DR_DESC_P(d, c, XS);
+  DR_DESC_P(d, c, LDZ);
+  DR_DESC_P(d, c, wide);
+  DR_DESC(d, c, ea);
+  DR_DESC(d, c, c1);
+  DR_DESC(d, c, p1w);
+  DR_DESC(d, c, p1tid);
+  DR_DESC(d, c, c2);
+  DR_DESC(d, c, wc1);
+  DR_DESC(d, c, w2);
+  DR_DESC(d, c, fc1);
+  DR_DESC(d, c, fc2);
+  DR_DESC(d, c, x);
+  DR_DESC(d, c, zm);
+  DR_DESC(d, c, h1);
+  DR_DESC(d, c, rp);
+  DR_DESC(d, c, col);
+  DR_DESC(d, c, m0p);
+  DR_DESC(d, c, m0i);
+  DR_DESC(d, c, p1);
+  DR_DESC(d, c, a1);
+  DR_DESC(d, c, dp1);
+  DR_DESC(d, c, zm2);
+  DR_DESC(d, c, s2);
+  DR_DESC(d, c, h2);
+  DR_DESC(d, c, d2);
+  DR_DESC(d, c, dz2);
+  DR_DESC(d, c, p1rp);
+  DR_DESC(d, c, p1c);
+  DR_DESC(d, c, p1trp);
+  DR_DESC(d, c, p1tc);
+  DR_DESC(d, c, m1p);
+  DR_DESC(d, c, m1i);
+  DR_DESC(d, c, p2);
+  DR_DESC(d, c, nt);
+  DR_DESC(d, c, head);
+  DR_DESC(d, c, dgp);
+  DR_DESC(d, c, red);
+  DR_DESC(d, c, total);
+  return d.pos;
+}
+
+extern "C" int dr_debug_carve_fout_conv(const int32_t* q, char* buf, int32_t len) {
+  const FConvCarve c = fconv_carve(q[0], q[1], q[2], q[3], q[4], q[5] != 0);
+  DrCarveDesc d{buf, len, 0};
+  DR_DESC_P(d, c, KP);
+  DR_DESC_P(d, c, LDA);
+  DR_DESC_P(d, c, XS);
+  DR_DESC(d, c, w);
+  DR_DESC(d, c, b1);
+  DR_DESC(d, c, a);
+  DR_DESC(d, c, h);
+  DR_DESC(d, c, c1);
+  DR_DESC(d, c, m0i);
+  DR_DESC(d, c, m0p);
+  DR_DESC(d, c, xh);
+  DR_DESC(d, c, hid);
+  DR_DESC(d, c, trp);
+  DR_DESC(d, c, ew);
+  DR_DESC(d, c, lcol);
+  DR_DESC(d, c, total);
+  return d.pos;
+}
+
+extern "C" int dr_debug_carve_fout_tail(const int32_t* q, char* buf, int32_t len) {
+  const FTailCarve c = ftail_carve(q[0], q[1], q[2], q[3], q[4], q[5] != 0);
+  DrCarveDesc d{buf, len, 0};
+  DR_DESC(d, c, w2);
+  DR_DESC(d, c, fc1);
+  DR_DESC(d, c, fc2);
+  DR_DESC(d, c, p1);
+  DR_DESC(d, c, a1);
+  DR_DESC(d, c, dp1);
+  DR_DESC(d, c, zm2);
+  DR_DESC(d, c, s2);
+  DR_DESC(d, c, h2);
+  DR_DESC(d, c, d2);
+  DR_DESC(d, c, dz2);
+  DR_DESC(d, c, p1rp);
+  DR_DESC(d, c, p1c);
+  DR_DESC(d, c, p1trp);
+  DR_DESC(d, c, p1tc);
+  DR_DESC(d, c, m1p);
+  DR_DESC(d, c, m1i);
+  DR_DESC(d, c, p2);
+  DR_DESC(d, c, nt);
+  DR_DESC(d, c, head);
+  DR_DESC(d, c, dgp);
+  DR_DESC(d, c, p1w);
+  DR_DESC(d, c, p1tid);
+  DR_DESC(d, c, c2);
+  DR_DESC(d, c, total);
+  return d.pos;
+}
+

@@ -56,7 +56,7 @@ __host__ __device__ inline int r16(int v) { return (v + 15) & ~15; }
 
 struct Carve {
   int KP, LDW, XS;
-  int w1, w2, fc2, x, z, rp, col, cl0, key, p1, a1, dp1, y2, h2, d2, p1rp, p1c, p1trp, p1tc, m1p, m1i, p2, nt, cl1,
+  int w1, w2, fc2, x, z, rp, col, cl0, key, p1, a1, dp1, y2, h2, p1rp, p1c, p1trp, p1tc, m1p, m1i, p2, nt, cl1,
       head, dgp, keep, total;
 };
 
@@ -1477,7 +1477,7 @@ __global__ void __launch_bounds__(NTA) ginet_large_conv1_bf16_kernel(LargeArgs l
 }
 
 struct TailCarve {
-  int w2, fc2, p1, a1, dp1, y2, h2, d2, p1rp, p1c, p1trp, p1tc, m1p, m1i, p2, nt, cl1, head, dgp, total;
+  int w2, fc2, p1, a1, dp1, y2, h2, p1rp, p1c, p1trp, p1tc, m1p, m1i, p2, nt, cl1, head, dgp, total;
 };
 
 __host__ __device__ inline TailCarve tail_carve(int K0, int P1, int K1, int alias, int OUT) {
@@ -1880,3 +1880,106 @@ extern "C" int dr_dropout_mask(uint64_t seed, uint64_t offset, int32_t n, float 
   for (int i = 0; i < n; ++i) keep_host[i] = dr_uniform(seed, offset, (uint32_t)i) >= p ? 1 : 0;
   return DR_OK;
 }
+
+// ---- carve descriptions for the host-side carve tests (tests/test_lds_carves.py)
+extern "C" int dr_debug_carve_ginet(const int32_t* q, char* buf, int32_t len) {
+  const Carve c = carve(q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7]);
+  DrCarveDesc d{buf, len, 0};
+  DR_DESC_P(d, c, KP);
+  DR_DESC_P(d, c, LDW);
+  DR_DESC_P(d, c, XS);
+  DR_DESC(d, c, w1);
+  DR_DESC(d, c, w2);
+  DR_DESC(d, c, fc2);
+  DR_DESC(d, c, x);
+  DR_DESC(d, c, z);
+  DR_DESC(d, c, rp);
+  DR_DESC(d, c, col);
+  DR_DESC(d, c, cl0);
+  DR_DESC(d, c, key);
+  DR_DESC(d, c, p1);
+  DR_DESC(d, c, a1);
+  DR_DESC(d, c, dp1);
+  DR_DESC(d, c, y2);
+  DR_DESC(d, c, h2);
+  DR_DESC(d, c, p1rp);
+  DR_DESC(d, c, p1c);
+  DR_DESC(d, c, p1trp);
+  DR_DESC(d, c, p1tc);
+  DR_DESC(d, c, m1p);
+  DR_DESC(d, c, m1i);
+  DR_DESC(d, c, p2);
+  DR_DESC(d, c, nt);
+  DR_DESC(d, c, cl1);
+  DR_DESC(d, c, head);
+  DR_DESC(d, c, dgp);
+  DR_DESC(d, c, keep);
+  DR_DESC(d, c, total);
+  return d.pos;
+}
+
+extern "C" int dr_debug_carve_ginet_conv(const int32_t* q, char* buf, int32_t len) {
+  const ConvCarve c = conv_carve(q[0], q[1], q[2], q[3], q[4]);
+  DrCarveDesc d{buf, len, 0};
+  DR_DESC_P(d, c, KP);
+  DR_DESC_P(d, c, LDW);
+  DR_DESC_P(d, c, XS);
+  DR_DESC(d, c, w1);
+  DR_DESC(d, c, z);
+  DR_DESC(d, c, h);
+  DR_DESC(d, c, m0i);
+  DR_DESC(d, c, m0p);
+  DR_DESC(d, c, rng);
+  DR_DESC(d, c, xh);
+  DR_DESC(d, c, hid);
+  DR_DESC(d, c, lcol);
+  DR_DESC(d, c, trp);
+  DR_DESC(d, c, total);
+  return d.pos;
+}
+
+extern "C" int dr_debug_carve_ginet_conv_bf16(const int32_t* q, char* buf, int32_t len) {
+  const ConvCarveB c = conv_carve_bf16(q[0], q[1], q[2], q[3], q[4]);
+  DrCarveDesc d{buf, len, 0};
+  DR_DESC_P(d, c, KPB);
+  DR_DESC_P(d, c, ZSB);
+  DR_DESC_P(d, c, XSB);
+  DR_DESC(d, c, w1);
+  DR_DESC(d, c, z);
+  DR_DESC(d, c, h);
+  DR_DESC(d, c, m0i);
+  DR_DESC(d, c, m0p);
+  DR_DESC(d, c, rng);
+  DR_DESC(d, c, xh);
+  DR_DESC(d, c, hid);
+  DR_DESC(d, c, lcol);
+  DR_DESC(d, c, trp);
+  DR_DESC(d, c, total);
+  return d.pos;
+}
+
+extern "C" int dr_debug_carve_ginet_tail(const int32_t* q, char* buf, int32_t len) {
+  const TailCarve c = tail_carve(q[0], q[1], q[2], q[3], q[4]);
+  DrCarveDesc d{buf, len, 0};
+  DR_DESC(d, c, w2);
+  DR_DESC(d, c, fc2);
+  DR_DESC(d, c, p1);
+  DR_DESC(d, c, a1);
+  DR_DESC(d, c, dp1);
+  DR_DESC(d, c, y2);
+  DR_DESC(d, c, h2);
+  DR_DESC(d, c, p1rp);
+  DR_DESC(d, c, p1c);
+  DR_DESC(d, c, p1trp);
+  DR_DESC(d, c, p1tc);
+  DR_DESC(d, c, m1p);
+  DR_DESC(d, c, m1i);
+  DR_DESC(d, c, p2);
+  DR_DESC(d, c, nt);
+  DR_DESC(d, c, cl1);
+  DR_DESC(d, c, head);
+  DR_DESC(d, c, dgp);
+  DR_DESC(d, c, total);
+  return d.pos;
+}
+

@@ -940,3 +940,29 @@ extern "C" int dr_ginet_nocluster_large_pass(const dr_graph_store* store, const 
   }
   return (int)hipGetLastError();
 }
+
+// ---- carve descriptions for the host-side carve tests (tests/test_lds_carves.py)
+extern "C" int dr_debug_carve_nocluster(const int32_t* q, char* buf, int32_t len) {
+  const NcCarve c = nc_carve(q[0], q[1], q[2], q[3]);
+  DrCarveDesc d{buf, len, 0};
+  DR_DESC_P(d, c, KP);
+  DR_DESC_P(d, c, LDW);
+  DR_DESC_P(d, c, XS);
+  DR_DESC(d, c, w1);
+  DR_DESC(d, c, dgp);
+  DR_DESC(d, c, w2);
+  DR_DESC(d, c, fc2);
+  DR_DESC(d, c, xz2);
+  DR_DESC(d, c, z1);
+  DR_DESC(d, c, h1);
+  DR_DESC(d, c, mask);
+  DR_DESC(d, c, rp);
+  DR_DESC(d, c, trp);
+  DR_DESC(d, c, col);
+  DR_DESC(d, c, tcol);
+  DR_DESC(d, c, head);
+  DR_DESC(d, c, dgn);
+  DR_DESC(d, c, total);
+  return d.pos;
+}
+

@@ -1813,3 +1813,54 @@ extern "C" int dr_vanilla_graph_pass(const dr_graph_store* store, const dr_graph
   }
   return (int)hipGetLastError();
 }
+
+// ---- carve descriptions for the host-side carve tests (tests/test_lds_carves.py)
+extern "C" int dr_debug_carve_vanilla_tile(const int32_t* q, char* buf, int32_t len) {
+  const TileCarve c = tile_carve(q[0], q[1], q[2], q[3], q[4] != 0);
+  DrCarveDesc d{buf, len, 0};
+  DR_DESC(d, c, rows);
+  DR_DESC(d, c, rec);
+  DR_DESC(d, c, trec);
+  DR_DESC(d, c, total);
+  return d.pos;
+}
+
+extern "C" int dr_debug_carve_vanilla_chunk_fwd(const int32_t* q, char* buf, int32_t len) {
+  const FwdCarve c = fwd_carve(q[0], q[1], q[2], q[3], q[4] != 0);
+  DrCarveDesc d{buf, len, 0};
+  DR_DESC_P(d, c, KP);
+  DR_DESC_P(d, c, LA);
+  DR_DESC_P(d, c, NOP);
+  DR_DESC_P(d, c, LX);
+  DR_DESC(d, c, a);
+  DR_DESC(d, c, wn);
+  DR_DESC(d, c, wh);
+  DR_DESC(d, c, x1);
+  DR_DESC(d, c, halo);
+  DR_DESC(d, c, rec);
+  DR_DESC(d, c, total);
+  return d.pos;
+}
+
+extern "C" int dr_debug_carve_vanilla_chunk_bwd(const int32_t* q, char* buf, int32_t len) {
+  const BwdCarve c = bwd_carve(q[0], q[1], q[2], q[3], q[4], q[5] != 0);
+  DrCarveDesc d{buf, len, 0};
+  DR_DESC_P(d, c, LDD);
+  DR_DESC_P(d, c, LU);
+  DR_DESC_P(d, c, NOP3);
+  DR_DESC(d, c, d);
+  DR_DESC(d, c, x1);
+  DR_DESC(d, c, dx);
+  DR_DESC(d, c, w3);
+  DR_DESC(d, c, du);
+  DR_DESC(d, c, w1);
+  DR_DESC(d, c, sh);
+  DR_DESC(d, c, x0);
+  DR_DESC(d, c, s1);
+  DR_DESC(d, c, halo);
+  DR_DESC(d, c, rec);
+  DR_DESC(d, c, trec);
+  DR_DESC(d, c, total);
+  return d.pos;
+}
+

@@ -1206,3 +1206,24 @@ extern "C" int dr_vanilla_fused_pass(const dr_graph_store* store, const dr_graph
   }
   return (int)hipGetLastError();
 }
+
+// ---- carve descriptions for the host-side carve tests (tests/test_lds_carves.py)
+extern "C" int dr_debug_carve_vanilla_graph(const int32_t* q, char* buf, int32_t len) {
+  const VCarve c = vcarve(q[0], q[1], q[2]);
+  DrCarveDesc d{buf, len, 0};
+  DR_DESC(d, c, rp);
+  DR_DESC(d, c, xb);
+  DR_DESC(d, c, head);
+  DR_DESC(d, c, P);
+  DR_DESC(d, c, Q);
+  DR_DESC(d, c, R);
+  DR_DESC(d, c, U);
+  DR_DESC(d, c, ext);
+  DR_DESC(d, c, T);
+  DR_DESC(d, c, bt);
+  DR_DESC(d, c, trp);
+  DR_DESC(d, c, tcol);
+  DR_DESC(d, c, total);
+  return d.pos;
+}
+

@@ -100,7 +100,7 @@ def make_spec(f, fe):
     xs = _r4(f)
 
     def slab_stride(_f):
-        return MAX_SPLIT * 2 * layer  # room for one partial row per workgroup of a split graph
+        return 2 * layer  # one row per graph: a split graph's last workgroup sums the siblings' partial rows
 
     def head_stride(out):
         return 2 * xs + 256 + _r4(out)  # g | h | dh | dout | d mean

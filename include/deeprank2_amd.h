@@ -739,6 +739,28 @@ int dr_dropout_mask(uint64_t seed, uint64_t offset, int32_t n, float p, uint8_t*
 const char* dr_version(void);
 int dr_device_arch(char* buf, int32_t len); /* e.g. "gfx950"; 0 on success */
 
+/* ------------------------------------------------------------------------
+ * Debug: the LDS carve of a kernel family for given sizes, as text
+ * "name=value;..." (region offsets in 4-byte words, "total" = words reserved,
+ * "$name" = a layout parameter).  Host-only; tests/test_lds_carves.py checks
+ * alignment, overlap, the host's reservation and each region's extent.
+ * Returns the characters needed (buf may be shorter).  q = the carve's size
+ * arguments in the order of its host-side *_lds_bytes function (fout: + sgat
+ * flag + limit bytes; conv / tail variants: their own orders, see the tests).
+ * ---------------------------------------------------------------------- */
+int dr_debug_carve_ginet(const int32_t* q, char* buf, int32_t len);
+int dr_debug_carve_ginet_conv(const int32_t* q, char* buf, int32_t len);
+int dr_debug_carve_ginet_conv_bf16(const int32_t* q, char* buf, int32_t len);
+int dr_debug_carve_ginet_tail(const int32_t* q, char* buf, int32_t len);
+int dr_debug_carve_fout(const int32_t* q, char* buf, int32_t len);
+int dr_debug_carve_fout_conv(const int32_t* q, char* buf, int32_t len);
+int dr_debug_carve_fout_tail(const int32_t* q, char* buf, int32_t len);
+int dr_debug_carve_nocluster(const int32_t* q, char* buf, int32_t len);
+int dr_debug_carve_vanilla_graph(const int32_t* q, char* buf, int32_t len);
+int dr_debug_carve_vanilla_tile(const int32_t* q, char* buf, int32_t len);
+int dr_debug_carve_vanilla_chunk_fwd(const int32_t* q, char* buf, int32_t len);
+int dr_debug_carve_vanilla_chunk_bwd(const int32_t* q, char* buf, int32_t len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -2,7 +2,7 @@
 # Vanilla chunk-fused pipeline: parity tests, atom / mixed bench lines (chunk-fused vs 16-row tiles), kernel stats.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out/r04; mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests/test_gpu_vanilla.py tests/test_gpu_vanilla_fused.py tests/test_gpu_mixed.py -x -v --timeout 120 --timeout-method thread > $O/pt_vchunk.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest tests/test_gpu_vanilla.py tests/test_gpu_vanilla_fused.py tests/test_gpu_mixed.py tests/test_gpu_foutnet.py tests/test_gpu_sgat.py tests/test_gpu_trainer.py tests/test_gpu_distributed.py -x -v --timeout 120 --timeout-method thread > $O/pt_vchunk.log 2>&1; rc=$?
 echo "pytest rc=$rc"; grep -E "passed|failed|Error|error" $O/pt_vchunk.log | tail -8; [ $rc -eq 0 ] || exit $rc
 for g in atom mixed; do
   for T in 64 16; do
