@@ -555,8 +555,18 @@ struct SibCtx {
   uint32_t* arrive;         // [B], zero on entry and left zero
 };
 
-template <int KPT, bool WT, bool SIB = false>
-__device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx& sc = SibCtx{}) {
+// Reduce-at-start step (dr_ginet_ras_step, opt-in): each graph workgroup first
+// applies the PREVIOUS step's gradient reduction + Adam to its share of the
+// parameter blocks (while its graph's DMA is in flight), a grid-wide hand-off
+// publishes the new parameters, then the pass runs on them.  The kernel passes
+// the update as a hook: hook(scratch) runs it and returns the Adam step it
+// applied, or -1 when no update was pending (the first step of an epoch).
+struct NoHook {
+  __device__ int64_t operator()(float*) const { return -1; }
+};
+
+template <int KPT, bool WT, bool SIB = false, bool RAS = false, class Hook = NoHook>
+__device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx& sc = SibCtx{}, const Hook& hook = Hook{}) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -604,17 +614,26 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
   // Head weights go to registers first (their latency hides under the DMA);
   // the graph and conv1's weights are DMA'd straight into LDS.
   float fc1_row[8], fc1_col[8], fc1_bias;
-  {
+  // RAS: every weight is read after the update's hand-off, with agent-scope
+  // loads (another workgroup, maybe on another XCD, wrote it this launch)
+  auto ldw = [&](const float* p) { return RAS ? __uint_as_float(__hip_atomic_load((const __attribute__((address_space(1))) unsigned int*)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) : *p; };
+  auto load_fc1 = [&]() {
     const int r = tid >> 3, part = tid & 7;
-    const float4 u0 = *reinterpret_cast<const float4*>(a.w.fc1w + r * 64 + part * 8);
-    const float4 u1 = *reinterpret_cast<const float4*>(a.w.fc1w + r * 64 + part * 8 + 4);
-    fc1_row[0] = u0.x; fc1_row[1] = u0.y; fc1_row[2] = u0.z; fc1_row[3] = u0.w;
-    fc1_row[4] = u1.x; fc1_row[5] = u1.y; fc1_row[6] = u1.z; fc1_row[7] = u1.w;
-    fc1_bias = a.w.fc1b[r];
-    const int o = tid & 63, rc = tid >> 6;
+    if (RAS) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) fc1_col[j] = a.w.fc1w[(rc * 8 + j) * 64 + o];
-  }
+      for (int j = 0; j < 8; ++j) fc1_row[j] = ldw(a.w.fc1w + r * 64 + part * 8 + j);
+    } else {
+      const float4 u0 = *reinterpret_cast<const float4*>(a.w.fc1w + r * 64 + part * 8);
+      const float4 u1 = *reinterpret_cast<const float4*>(a.w.fc1w + r * 64 + part * 8 + 4);
+      fc1_row[0] = u0.x; fc1_row[1] = u0.y; fc1_row[2] = u0.z; fc1_row[3] = u0.w;
+      fc1_row[4] = u1.x; fc1_row[5] = u1.y; fc1_row[6] = u1.z; fc1_row[7] = u1.w;
+    }
+    fc1_bias = ldw(a.w.fc1b + r);
+    const int o = tid & 63, rcc = tid >> 6;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fc1_col[j] = ldw(a.w.fc1w + (rcc * 8 + j) * 64 + o);
+  };
+  if (!RAS) load_fc1();
   const float y_g = s.y[g];
   uint64_t drop_offset = a.p.drop_offset;
   dma_x4(sX, s.x + n0 * (int64_t)XS, N * XS / 4);
@@ -629,8 +648,10 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
   }
   dma_words(sm1p, s.m1_ptr + k10 + g, K1 + 1);
   dma_words(sm1i, s.m1_idx + k00, K0);
-  dma_words(sW1, a.w.w1, 16 * F);  // [W1; W1e] rows of F, packed
-  dma_words(sW1 + 16 * F, a.w.w1e, 16 * F);
+  if (!RAS) {
+    dma_words(sW1, a.w.w1, 16 * F);  // [W1; W1e] rows of F, packed
+    dma_words(sW1 + 16 * F, a.w.w1e, 16 * F);
+  }
   {  // zero Z's K padding (cols XS..KPT; X's own pad is zero) and the pooling keys
     const int padz = KPT - XS;
     for (int p = tid; p < N * padz; p += NT) {
@@ -640,6 +661,14 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
     for (int p = tid; p < K0 * 32; p += NT) skey[p] = 0ull;
   }
   if (a.p.step_counter) drop_offset = (uint64_t)a.p.step_counter[0];  // loaded late: no early wait
+  if (RAS) {
+    // the previous step's reduce + Adam, then the grid hand-off (scratch: the
+    // tail's dgp region, 1024 words, unused before the tail)
+    const int64_t ts = hook(lds + c.dgp);
+    if (ts >= 0) drop_offset = (uint64_t)ts;  // this pass's step: the counter value the update leaves
+    for (int p = tid; p < 32 * F; p += NT) sW1[p] = p < 16 * F ? ldw(a.w.w1 + p) : ldw(a.w.w1e + p - 16 * F);
+    load_fc1();
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // snapshot for dr_reduce_update, stored only now so that no wait for the
   // counter load sits between the descriptor and the graph DMA
@@ -653,14 +682,14 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
   // LDS read.)
   float wv2, wfc[3];
   {
-    wv2 = (tid < 512) ? a.w.w2[tid] : a.w.w2e[tid - 512];
+    wv2 = (tid < 512) ? ldw(a.w.w2 + tid) : ldw(a.w.w2e + tid - 512);
     const int nf = OUT * 128;
 #pragma unroll
     for (int u = 0; u < 3; ++u) {
       const int p = tid + u * NT;
       wfc[u] = 0.f;
-      if (p < nf) wfc[u] = a.w.fc2w[p];
-      else if (p < nf + OUT) wfc[u] = a.w.fc2b[p - nf];
+      if (p < nf) wfc[u] = ldw(a.w.fc2w + p);
+      else if (p < nf + OUT) wfc[u] = ldw(a.w.fc2b + p - nf);
     }
   }
   // ---------------- conv1 + depth-0 pooling, one 16-row tile per wave -------
@@ -973,6 +1002,91 @@ __global__ void __launch_bounds__(NT) ginet_step_kernel(GinetStepArgs a) {
     __syncthreads();  // part reused by the next pass
   }
   SSTAMP(2);
+}
+
+// ---------------------------------------------------------------------------
+// Reduce-at-start step (dr_ginet_ras_step): grid = the B graph workgroups.
+// Launch t applies step t-1's update (when sync[3] says its partials are
+// pending), then runs pass t, whose partials the next launch (or
+// dr_reduce_update, the epoch-end flush) applies.  Each workgroup reduces its
+// share of the parameter blocks with the same fixed-order arithmetic as
+// dr_reduce_update (reduce_common.h), storing the new parameters
+// write-through; every wave drains, one lane arrives on sync[0] and polls it
+// (agent-scope loads, s_sleep, bounded: a give-up sets sync[2] and the pass
+// goes on, loudly) until all B have arrived; the last workgroup past the wait
+// returns the counters to zero.  The pass then reads every weight with
+// agent-scope loads.  All B workgroups must be co-resident (B <= the CUs free
+// for a 1024-thread, ~125 KB-LDS workgroup each): the host checks B <= 256.
+// The parameters after K launches + the flush are bit-identical to K
+// two-launch steps; loss_out lags one step (launch t reports step t-1).
+// ---------------------------------------------------------------------------
+template <int KPT>
+__global__ void __launch_bounds__(NT) ginet_ras_kernel(GinetStepArgs a) {
+  const int B = a.g.B, b = blockIdx.x;
+  uint32_t* sync = a.sync;
+  const int pending = (int)sync[3];               // written by the previous launch
+  const int64_t tstep = a.g.p.step_counter[1] + 1;  // the snapshot the previous pass took, + 1
+  typedef const __attribute__((address_space(4))) drr::ParamRec ConstRec;
+  ConstRec* recs = (ConstRec*)((const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() +
+                               offsetof(GinetStepArgs, rec));
+  auto hook = [&](float* scratch) -> int64_t {
+    if (!pending) return -1;
+    const int half = threadIdx.x / drr::RT, t = threadIdx.x % drr::RT;
+    float(*part)[drr::RP] = reinterpret_cast<float(*)[drr::RP]>(scratch) + half * drr::RC;
+    const int nb = a.h.n_blocks, stride = 2 * B;
+    for (int j0 = 0; j0 < nb; j0 += stride) {
+      const int j = j0 + 2 * b + half;  // block j -> (parameter, element block)
+      int pi = 0;
+#pragma unroll
+      for (int q = 1; q <= STEP_PARAMS; ++q) pi += (a.h.blk0[q] <= j) ? 1 : 0;
+      pi = j < nb ? pi : a.h.n_params;
+      int eb = pi < a.h.n_params ? j - a.h.blk0[pi] : 0;
+      drr::ParamRec r;
+      memset(&r, 0, sizeof(r));
+      if (pi < a.h.n_params) {
+        ConstRec& q = recs[pi];
+        r.param = q.param;
+        r.grad = q.grad;
+        r.m = q.m;
+        r.v = q.v;
+        r.numel = q.numel;
+        r.kind = q.kind;
+        r.off1 = q.off1;
+        r.off2 = q.off2;
+        r.cols = q.cols;
+      } else {
+        eb = 0;
+      }
+      drr::reduce_block<0, true, true>(a.h, r, eb, j == 0, t, part, tstep);
+      __syncthreads();  // part reused by the next pass
+    }
+    if (b == 0 && threadIdx.x == 0) a.g.p.step_counter[0] = tstep;  // the LEAN reduce leaves it to the caller
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's write-through parameters drained
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      gu32* arrive = (gu32*)sync;
+      gu32* passed = (gu32*)(sync + 1);
+      __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      uint32_t polls = 0;
+      while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)B) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++polls == (1u << 22)) {  // never expected: flag it, finish the launch
+          __hip_atomic_store((gu32*)(sync + 2), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      const uint32_t d = __hip_atomic_fetch_add(passed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (d == (uint32_t)B - 1u) {  // the last past the wait: counters back to zero for the next launch
+        __hip_atomic_fetch_sub(arrive, (uint32_t)B, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(passed, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // the weight loads stay below the hand-off
+    return tstep;
+  };
+  graph_body<KPT, false, false, true>(a.g, SibCtx{}, hook);
+  if (b == 0 && threadIdx.x == 0) sync[3] = 1u;  // this pass's partials are pending
 }
 
 // =========================================================================
@@ -1801,6 +1915,51 @@ extern "C" int dr_ginet_train_step(const dr_graph_store* store, const dr_graph_d
   } else {
     DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_step_kernel<64>)));
     hipLaunchKernelGGL(ginet_step_kernel<64>, grid, dim3(NT), lds, (hipStream_t)stream, a);
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int dr_ginet_ras_step(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                                 const dr_ginet_weights* w, const dr_pass* pass, int32_t lds_bytes,
+                                 const dr_param_table* table, const dr_adam* adam, float* loss_out, uint32_t* sync,
+                                 int32_t prev_batch, float prev_loss_scale, void* stream) {
+  if (!store || !descs || !w || !pass || !table || !adam || !sync || n_batch < 0) return DR_E_ARG;
+  if (pass->out_dim < 1 || pass->out_dim > DR_MAX_OUT) return DR_E_UNSUPPORTED;
+  if (store->n_feat < 1 || 32 * store->n_feat > 2 * NT) return DR_E_UNSUPPORTED;  // F <= 64
+  if (lds_bytes > 160 * 1024) return DR_E_LDS;
+  if (n_batch > 256) return DR_E_UNSUPPORTED;  // every workgroup co-resident for the hand-off
+  if (pass->compute_dtype != DR_DTYPE_F32) return DR_E_UNSUPPORTED;
+  if (pass->flags != (DR_PASS_FORWARD | DR_PASS_BACKWARD) || pass->loss_kind == DR_LOSS_NONE) return DR_E_ARG;
+  if (!pass->out || !pass->slab || !pass->head || !pass->loss_per_graph || !pass->step_counter) return DR_E_ARG;
+  if (pass->use_dropout == DR_DROPOUT_MASK && !pass->mask) return DR_E_ARG;
+  if (pass->use_dropout < DR_DROPOUT_OFF || pass->use_dropout > DR_DROPOUT_HASH) return DR_E_ARG;
+  if (!adam->enabled || adam->step_counter != pass->step_counter || adam->grad_div || adam->fault) return DR_E_ARG;
+  if (table->n_params > STEP_PARAMS || table->slab_stride != DR_SLAB_STRIDE(store->n_feat) ||
+      table->head_stride != DR_HEAD_STRIDE(pass->out_dim))
+    return DR_E_ARG;
+  if (n_batch == 0) return DR_OK;
+  if (!store->cl0) return DR_E_ARG;
+  GinetStepArgs a;
+  std::memset(&a, 0, sizeof(a));
+  if (prev_batch < 0 || prev_batch > 256) return DR_E_ARG;
+  // the pending update is the previous pass's: its batch size and loss scale
+  const int blocks = drr::build_reduce(table, pass->slab, pass->head, prev_batch, adam, pass->loss_per_graph,
+                                       prev_loss_scale, loss_out, a.h, a.rec);
+  if (blocks < 0) return blocks;
+  a.g.s = *store;
+  a.g.w = *w;
+  a.g.p = *pass;
+  a.g.descs = descs;
+  a.g.B = n_batch;
+  a.sync = sync;
+  a.NR = 0;
+  const dim3 grid(n_batch);
+  if (store->n_feat <= 32) {
+    DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_ras_kernel<32>)));
+    hipLaunchKernelGGL(ginet_ras_kernel<32>, grid, dim3(NT), lds_bytes, (hipStream_t)stream, a);
+  } else {
+    DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_ras_kernel<64>)));
+    hipLaunchKernelGGL(ginet_ras_kernel<64>, grid, dim3(NT), lds_bytes, (hipStream_t)stream, a);
   }
   return (int)hipGetLastError();
 }

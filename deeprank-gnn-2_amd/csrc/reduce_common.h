@@ -78,7 +78,10 @@ __device__ __forceinline__ float ld_part(const float* p) {
 // issued in one straight-line group (clamped indices, zero weights past the
 // batch), so one wait covers the partials and the Adam state.  The caller
 // synchronises the workgroup between two calls that share `part`.
-template <int LD, bool LEAN = false>
+// WTP: the updated parameters are stored write-through (agent scope), for a
+// launch whose other workgroups read them after a grid-wide hand-off (the
+// reduce-at-start GINet step, ginet_fused.hip).
+template <int LD, bool LEAN = false, bool WTP = false>
 __device__ __forceinline__ void reduce_block(const ReduceHdr& h, const ParamRec& r, int elem_block, bool first, int t,
                                              float (*part)[RP], int64_t tstep) {
   // LEAN: partials always given, Adam always on (the one-launch step): the
@@ -198,7 +201,8 @@ __device__ __forceinline__ void reduce_block(const ReduceHdr& h, const ParamRec&
     r.v[e] = vv;
     const float denom = __fadd_rn(__fdiv_rn(sqrtf(vv), bc2s), h.eps);
     const float pn = fmaf(-(h.lr / bc1), __fdiv_rn(mv, denom), p0);
-    r.param[e] = pn;
+    if (WTP) __hip_atomic_store((__attribute__((address_space(1))) unsigned int*)(r.param + e), __float_as_uint(pn), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else r.param[e] = pn;
     if (!LEAN && h.mirror) {
       if (mi.x >= 0) h.mirror[mi.x] = pn;
       if (mi.y >= 0) h.mirror[mi.y] = pn;

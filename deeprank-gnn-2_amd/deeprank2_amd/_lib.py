@@ -250,6 +250,7 @@ SIGNATURES = [
     ("dr_sgat_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 8),
     ("dr_reduce_update", ctypes.c_int, [ctypes.POINTER(ParamTableC), VP, VP, ctypes.c_int32, ctypes.POINTER(AdamC), VP, ctypes.c_float, VP, VP]),
     ("dr_ginet_train_step", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, ctypes.POINTER(ParamTableC), ctypes.POINTER(AdamC), VP, VP, VP]),
+    ("dr_ginet_ras_step", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, ctypes.POINTER(ParamTableC), ctypes.POINTER(AdamC), VP, VP, ctypes.c_int32, ctypes.c_float, VP]),
     ("dr_csr_from_coo", ctypes.c_int, [VP, VP, ctypes.c_int64, ctypes.c_int32, VP, VP, VP, VP, VP]),
     ("dr_spmm_csr", ctypes.c_int, [VP, VP, VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP, VP]),
     ("dr_spmm_csr_w", ctypes.c_int, [VP, VP, VP, VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP, VP]),

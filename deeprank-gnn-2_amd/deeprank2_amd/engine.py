@@ -93,6 +93,11 @@ class FusedTrainStep:
         # Off by default: measured slower at B=64 (24.7 vs 20.6 us/step)
         self.fuse_update = False
         self.sync = torch.zeros(4, dtype=torch.int32, device=dev)  # its arrival counters, left zero
+        # reduce-at-start (GINet, world of one, opt-in; dr_ginet_ras_step): each
+        # launch applies the previous step's update, then runs its pass; loss_out
+        # lags one step and flush() applies the last update (sync[3]: pending)
+        self.ras = False
+        self._ras_last = None  # (B, loss scale) of the pending pass
         # models whose graph pass reads its weights from a packed copy
         # (VanillaNetwork: MFMA-fragment order): one copy per step object,
         # rewritten by Adam as it updates the parameters (dr_adam.mirror), so
@@ -157,6 +162,8 @@ class FusedTrainStep:
         self._adam_off.fault = self.fault.data_ptr()
         self._adam_div = _lib.AdamC.from_buffer_copy(a)
         self._adam_div.grad_div = self.wsum.data_ptr()
+        self._adam_ras = _lib.AdamC.from_buffer_copy(a)
+        self._adam_ras.fault = None
         self._wire_packed()
 
     def _wire_packed(self):
@@ -245,6 +252,13 @@ class FusedTrainStep:
         if ev is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
+        if self.pg is None and self.ras and launch_step(self.spec, h, self._w, p, self._table, self._adam_ras, self.loss_out, self.sync, entry="dr_ginet_ras_step", prev=self._ras_last):
+            if ev is not None:
+                e1.record()
+                ev.append((e0, e1))
+            self._ras_last = (h.B, scale)
+            self.step_count += 1
+            return self.loss_out, self.out[: h.B]
         if self.pg is None and self.fuse_update and launch_step(self.spec, h, self._w, p, self._table, self._adam, self.loss_out, self.sync):
             if ev is not None:
                 e1.record()
@@ -271,6 +285,19 @@ class FusedTrainStep:
                 self.fault_red.copy_(self.flat_fault)
             self._adam_after_allreduce()
         return self.loss_out, self.out[: h.B]
+
+    def flush(self):
+        """Reduce-at-start mode: apply the last launch's pending update
+        (dr_reduce_update over its partials, the arithmetic every RAS launch
+        uses) and clear the pending flag; a no-op otherwise."""
+        if self._ras_last is None or int(self.sync[3].item()) == 0:
+            self._ras_last = None
+            return
+        b, scale = self._ras_last
+        self._table.slab_rows = 1
+        _lib.check(_lib.load().dr_reduce_update(self._table, self.slab.data_ptr(), self.head.data_ptr(), b, self._adam_ras, self.lpg.data_ptr(), scale, self.loss_out.data_ptr(), _lib.stream_ptr(self.device)), "dr_reduce_update")
+        self.sync[3].zero_()
+        self._ras_last = None
 
     def step_empty(self):
         """A rank whose shard of the global batch is empty (global batch smaller
@@ -393,7 +420,7 @@ class FusedTrainStep:
 
     def _state_tensors(self):
         packed = [] if self.wpack is None else [self.wpack[0]]
-        return [*self.params, *[s for st in self.states for s in st], self.counter, self.flat, self.fault, *packed]
+        return [*self.params, *[s for st in self.states for s in st], self.counter, self.flat, self.fault, self.sync, *packed]
 
     def capture_sweep(self, handles, global_batch=None):
         """Capture one training step per handle, in order, into ONE HIP graph
@@ -421,7 +448,7 @@ class FusedTrainStep:
     def one_launch(self, h: BatchHandle) -> bool:
         """True when ``step(h)`` is a single kernel launch (``dr_ginet_train_step``)."""
         cd = _lib.DR_DTYPE_BF16 if self.compute_dtype == "bf16" else _lib.DR_DTYPE_F32
-        return self.pg is None and self.fuse_update and not h.nonfinite and step_fits(self.spec, h, cd, self.out_dim)
+        return self.pg is None and (self.fuse_update or (self.ras and h.B <= 256)) and not h.nonfinite and step_fits(self.spec, h, cd, self.out_dim)
 
     def time_graph_pass(self, handles, n_launches, global_batch=None):
         """Mean duration (ms) of the model's graph pass alone (or of the whole

@@ -540,16 +540,20 @@ def step_fits(spec: FusedSpec, h: BatchHandle, compute_dtype, out_dim) -> bool:
     return lds_for(spec, h, out_dim) <= LDS_MAX
 
 
-def launch_step(spec: FusedSpec, h: BatchHandle, w, p, table, adam, loss_out, sync) -> bool:
+def launch_step(spec: FusedSpec, h: BatchHandle, w, p, table, adam, loss_out, sync, entry=None, prev=None) -> bool:
     """The model's one-launch training step (graph pass, gradient reduction
-    and Adam; ``spec.step_entry``) when it has one and the batch runs on its
-    per-graph kernel; False (nothing launched) otherwise."""
+    and Adam; ``spec.step_entry``, or ``entry``: dr_ginet_ras_step) when it has
+    one and the batch runs on its per-graph kernel; False (nothing launched)
+    otherwise."""
     if not step_fits(spec, h, p.compute_dtype, p.out_dim):
         return False
+    if entry == "dr_ginet_ras_step" and h.B > 256:  # noqa: PLR2004  (every workgroup co-resident)
+        return False
     lds = lds_for(spec, h, p.out_dim)
-    fn = getattr(_lib.load(), spec.step_entry)
-    rc = fn(h.store.cstruct(), h.descs.data_ptr(), h.B, w, p, lds, table, adam, loss_out.data_ptr(), sync.data_ptr(), _lib.stream_ptr(h.store.device))
-    _lib.check(rc, spec.step_entry)
+    fn = getattr(_lib.load(), entry or spec.step_entry)
+    extra = () if entry != "dr_ginet_ras_step" else (prev or (h.B, p.loss_scale))  # the pending pass's batch size and loss scale
+    rc = fn(h.store.cstruct(), h.descs.data_ptr(), h.B, w, p, lds, table, adam, loss_out.data_ptr(), sync.data_ptr(), *extra, _lib.stream_ptr(h.store.device))
+    _lib.check(rc, entry or spec.step_entry)
     return True
 
 

@@ -608,6 +608,23 @@ int dr_ginet_train_step(const dr_graph_store* store, const dr_graph_desc* descs,
                         const dr_param_table* table, const dr_adam* adam, float* loss_out, uint32_t* sync,
                         void* stream);
 
+/* Reduce-at-start GINet step (opt-in; same arguments and checks as
+ * dr_ginet_train_step, B <= 256, dr_adam.fault unset): ONE launch of B graph
+ * workgroups that first applies the previous launch's gradient reduction +
+ * Adam (the same fixed-order arithmetic as dr_reduce_update) while the graph
+ * DMA is in flight, publishes the new parameters through a grid-wide hand-off
+ * (sync[0..1], bounded wait: a give-up sets sync[2]), then runs this step's
+ * graph pass.  sync[3] = 1 while a pass's partials wait for their update; the
+ * last step's update is a dr_reduce_update call (then zero sync[3]).
+ * prev_batch / prev_loss_scale: the batch size and loss scale of the pass whose
+ * update is pending.  loss_out lags one step.  Parameters after K launches +
+ * that flush are bit-identical to K dr_ginet_graph_pass + dr_reduce_update
+ * steps.                                                                     */
+int dr_ginet_ras_step(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                      const dr_ginet_weights* w, const dr_pass* pass, int32_t lds_bytes,
+                      const dr_param_table* table, const dr_adam* adam, float* loss_out, uint32_t* sync,
+                      int32_t prev_batch, float prev_loss_scale, void* stream);
+
 
 /* ---- generic layer kernels (arbitrary edge lists; GINetConvLayer API) ---- */
 

@@ -91,3 +91,47 @@ def test_one_launch_step_replays_from_hip_graph():
             two.step(h)
     torch.cuda.synchronize()
     _assert_same(one, two, "captured one-launch steps vs eager two-launch steps")
+
+
+def _ras_pair():
+    one, two = _pair()
+    one.fuse_update = False
+    one.ras = True
+    return one, two
+
+
+@pytest.mark.parametrize("sizes", [(64, 64, 64, 64), (7, 1, 130, 64, 200)])
+def test_reduce_at_start_step_bit_identical_after_flush(sizes):
+    """dr_ginet_ras_step: launch t applies step t-1's reduce + Adam to its share
+    of the parameter blocks, hands the new parameters to every workgroup
+    (grid-wide, in-launch), then runs pass t.  Every step's outputs equal the
+    two-launch step's, and after the epoch-end flush the parameters, moments,
+    gradients, loss and step counter are bit-identical; the hand-off counters
+    and the pending flag are left zero.  Batch sizes vary (the pending update
+    sums the previous pass's rows with its loss scale)."""
+    store = GraphStore(pack_graphs(_records(256, 34)), DEV)
+    one, two = _ras_pair()
+    rng = np.random.default_rng(1)
+    for i, b in enumerate(sizes):
+        h = BatchHandle(store, rng.permutation(256)[:b].astype(np.int32))
+        _l1, o1 = one.step(h)
+        _l2, o2 = two.step(h)
+        torch.cuda.synchronize()
+        assert torch.equal(o1, o2), f"outputs step {i} (B={b})"
+    one.flush()
+    torch.cuda.synchronize()
+    _assert_same(one, two, "after the flush")
+
+
+def test_reduce_at_start_steps_replay_from_hip_graph():
+    store = GraphStore(pack_graphs(_records(128, 35)), DEV)
+    one, two = _ras_pair()
+    hs = [BatchHandle(store, np.arange(k * 64, k * 64 + 64, dtype=np.int32)) for k in range(2)]
+    g = one.capture_sweep(hs)
+    for _ in range(3):
+        g.replay()
+        for h in hs:
+            two.step(h)
+    one.flush()
+    torch.cuda.synchronize()
+    _assert_same(one, two, "captured reduce-at-start steps + flush vs eager two-launch steps")
