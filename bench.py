@@ -253,6 +253,24 @@ def pmc_traffic_bytes(model="ginet"):
     return int((2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024), os.path.relpath(files[-1], ROOT)
 
 
+def pmc_traffic_step(model, graphs):
+    """HBM bytes per step of the model's graph-pass kernels from the newest
+    committed per-kernel PMC table (profiles/*/pmc_per_kernel_<model>_<graphs>.txt,
+    tools/pmc_per_kernel.py over FETCH_SIZE / WRITE_SIZE passes of
+    tools/pmc_run.py): for the multi-kernel Vanilla pipeline, whose "graph
+    pass" is a chain of launches (same gfx950 correction as pmc_traffic_bytes)."""
+    import glob  # noqa: PLC0415
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"pmc_per_kernel_{model}_{graphs}.txt")))
+    if not files:
+        return None, None
+    for line in open(files[-1]):
+        if line.startswith("per step (graph pass kernels):"):
+            mb = float(line.split(",")[1].split("MB")[0])
+            return int(mb * 1e6), os.path.relpath(files[-1], ROOT)
+    return None, None
+
+
 def stream_copy_gbs(dev, mib=1024, reps=5):
     """Achievable HBM bandwidth on this GPU: a device-to-device copy of ``mib``
     MiB timed with HIP events (bytes read + written), best of ``reps``."""
@@ -717,6 +735,8 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
     default_cfg = args.model == "ginet" and args.graphs == "residue" and B == B_PER_GPU and args.dtype == "f32"
     pmc_cfg = default_cfg or (args.model in ("foutnet", "sgat", "vanilla") and args.graphs == "residue" and B == B_PER_GPU and args.dtype == "f32")
     traffic, traffic_src = pmc_traffic_bytes(args.model) if pmc_cfg else (None, None)
+    if traffic is None and args.model == "vanilla" and args.graphs in ("atom", "mixed") and args.dtype == "f32":
+        traffic, traffic_src = pmc_traffic_step("vanilla", args.graphs)
     large = args.model == "ginet" and (bool(args.force_large) or args.ginet_path != "auto" or args.dtype == "bf16" or any(h.lds((step.spec.entry, 1), lambda *sz: 0) > 160 * 1024 for h in handles))
     copy_gbs = None if args.no_stream_copy else stream_copy_gbs(dev)
     # §8(d) FLOP side: algorithmic FLOPs per launch against the dense MFMA peak

@@ -61,6 +61,18 @@ def main():
             tot_mb += mb * calls / steps
     if steps:
         print(f"per step: {tot_us:.1f} us of kernels, {tot_mb:.2f} MB of HBM traffic")
+        # the graph pass's own kernels (model prefixes), without the optimizer and framework kernels
+        pre = ("vb_", "vc_", "vanilla_", "ginet_", "fout_", "nc_")
+        p_us = p_mb = 0.0
+        for k in per:
+            if not k.startswith(pre):
+                continue
+            f = statistics.median(per[k]["FETCH_SIZE"]) if per[k]["FETCH_SIZE"] else 0.0
+            w = statistics.median(per[k]["WRITE_SIZE"]) if per[k]["WRITE_SIZE"] else 0.0
+            us, calls = dur.get(k, (0.0, 0))
+            p_us += us * calls / steps
+            p_mb += (2 * f + w) * 1024 / 1e6 * calls / steps
+        print(f"per step (graph pass kernels): {p_us:.1f} us, {p_mb:.3f} MB of HBM traffic")
 
 
 if __name__ == "__main__":
