@@ -1126,6 +1126,21 @@ constexpr int CW = CT / 64;   // waves
 constexpr int CRG = CT / 32;  // row groups (32 lanes = the 32 channels of one row)
 constexpr int NBT = 256;      // vc_nb2 threads
 
+// diagnostic builds (-DDR_STAMPS): thread 0's s_memtime at phase i of chunk
+// kernel k (0 vc_fwd<1>, 1 vc_fwd<2>, 2 vc_nb2, 3 vc_eb2n1, 4 vc_eb1) in
+// dr_pass.stamps [5][n_tiles][16]
+#ifdef DR_STAMPS
+#define CSTAMP(k, i)                                                                                            \
+  do {                                                                                                          \
+    if (threadIdx.x == 0 && a.p.stamps)                                                                         \
+      a.p.stamps[((int64_t)(k) * gridDim.x + blockIdx.x) * 16 + (i)] = (int64_t)__builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define CSTAMP(k, i) \
+  do {               \
+  } while (0)
+#endif
+
 __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 acc) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
 }
@@ -1226,6 +1241,7 @@ __global__ void __launch_bounds__(CT) vc_fwd(VA a) {
   const Layer L = layer_of(a, LAYER);
   const int F = a.F, KE = a.KE, KN = a.KN, XS = a.XS;
   const int t = blockIdx.x, tid = threadIdx.x, c = tid & 31, hs = tid & 32;
+  CSTAMP(LAYER - 1, 0);
   const int64_t rt0 = a.ws.tile_row0[t], rt1 = a.ws.tile_row0[t + 1];
   const int nr = (int)(rt1 - rt0);
   const int b = a.ws.row_slot[rt0];
@@ -1268,6 +1284,7 @@ __global__ void __launch_bounds__(CT) vc_fwd(VA a) {
   const float bc = L.be[c];
   uint32_t* wr = a.ws.relu_words + (int64_t)(LAYER - 1) * a.ws.edge0[a.B] + a.ws.edge0[b] + e0;
   __syncthreads();
+  CSTAMP(LAYER - 1, 1);
   for (int64_t r = rt0 + (tid >> 5); r < rt1; r += CRG) {
     const int i = (int)(r - g0);
     const float ab = L.a[r * 32 + c] + bc;
@@ -1301,6 +1318,7 @@ __global__ void __launch_bounds__(CT) vc_fwd(VA a) {
     sA[(r - rt0) * fc.LA + XS + c] = acc;
   }
   __syncthreads();
+  CSTAMP(LAYER - 1, 2);
   // node MLP on MFMA: vb_gemm<GM_NODE>'s operands and k order
   const int lane = tid & 63, wave = tid >> 6, li = lane & 15, kq = lane >> 4;
   const int nct = fc.NOP / 16;
@@ -1317,6 +1335,7 @@ __global__ void __launch_bounds__(CT) vc_fwd(VA a) {
       if (NEXT && n < XS) sX1[i * fc.LX + n] = n < F ? v : 0.f;
     }
   }
+  CSTAMP(LAYER - 1, 3);
   if (!NEXT) return;
   __syncthreads();
   // layer 2's [A | B] = X1 [Wa2; Wb2]^T: vb_gemm<GM_HALVES>'s operands and k order
@@ -1331,6 +1350,7 @@ __global__ void __launch_bounds__(CT) vc_fwd(VA a) {
       if (i < nr) (n < 32 ? L2.a : L2.bm)[(rt0 + i) * 32 + (n & 31)] = acc[q];
     }
   }
+  CSTAMP(0, 4);
 }
 
 // weight-gradient partial row of a layer for a chunk (both layers' rows live together)
@@ -1378,6 +1398,7 @@ __global__ void __launch_bounds__(NBT) vc_nb2(VA a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int F = a.F, XS = a.XS, KN = a.KN;
   const int ch = blockIdx.x, tid = threadIdx.x;
+  CSTAMP(2, 0);
   const int64_t rt0 = a.ws.tile_row0[ch], rt1 = a.ws.tile_row0[ch + 1];
   const int nr = (int)(rt1 - rt0);
   const int b = a.ws.row_slot[rt0];
@@ -1401,6 +1422,7 @@ __global__ void __launch_bounds__(NBT) vc_nb2(VA a) {
     sW[p] = (k < F && n < F + 32) ? a.w.wn2[k * KN + n] : 0.f;
   }
   __syncthreads();
+  CSTAMP(2, 1);
   const int lane = tid & 63, wave = tid >> 6, li = lane & 15, kq = lane >> 4;
   const int nct = NOPD / 16;
   for (int job = wave; job < 4 * nct; job += NBT / 64) {  // [dX1 | DS2] = DU2 Wn2
@@ -1416,13 +1438,14 @@ __global__ void __launch_bounds__(NBT) vc_nb2(VA a) {
     }
   }
   node_wgrad<NBT>(a, part_row(a, 2, ch), sDU, LU, sX1, sS, 4 * nct);
+  CSTAMP(2, 2);
 }
 
 // a chunk's D_i = relu'-count x dS_i, D'_i (transposed), and its rows' dWc
 // shares, from the halo of dS rows (vb_edge_bwd_tile's sums and order)
 template <int FE>
 __device__ __forceinline__ void chunk_edge_bwd(const VA& a, int l, int t, const float* DS, float* sD, int LDD,
-                                               float* sDS, float* sR, uint2* sTR, float* sSh) {
+                                               float* sDS, float* sR, uint2* sTR, float* sSh, int sk) {
   constexpr int FA = FE > 0 ? FE : 1, FeS = FA;
   const int tid = threadIdx.x, c = tid & 31;
   const int64_t rt0 = a.ws.tile_row0[t], rt1 = a.ws.tile_row0[t + 1];
@@ -1446,6 +1469,7 @@ __device__ __forceinline__ void chunk_edge_bwd(const VA& a, int l, int t, const 
   const int nr = (int)(rt1 - rt0);
   for (int p = tid; p < (WR - nr) * 64; p += CT) sD[(nr + (p >> 6)) * LDD + (p & 63)] = 0.f;
   __syncthreads();
+  CSTAMP(sk, 1);
   float wsum[FA];
 #pragma unroll
   for (int f = 0; f < FA; ++f) wsum[f] = 0.f;
@@ -1559,6 +1583,7 @@ __global__ void __launch_bounds__(CT) vc_eb2n1(VA a) {
   const int b = a.ws.row_slot[rt0];
   const dr_graph_desc& d = a.descs[b];
   const int64_t g0 = a.ws.row0[b];
+  CSTAMP(3, 0);
   const BwdCarve bc = bwd_carve(F, a.ws.halo_max, a.ws.tile_edges_max, a.ws.tile_tedges_max, FE, true);
   float* sD = lds + bc.d;
   float* sX1 = lds + bc.x1;
@@ -1578,8 +1603,9 @@ __global__ void __launch_bounds__(CT) vc_eb2n1(VA a) {
     const int k = p >> 5, n = p & 31;
     sW1[p] = k < F ? a.w.wn1[k * KN + F + n] : 0.f;
   }
-  chunk_edge_bwd<FE>(a, 2, t, ws + a.L.ds, sD, bc.LDD, lds + bc.halo, lds + bc.rec, reinterpret_cast<uint2*>(lds + bc.trec), sSh);
+  chunk_edge_bwd<FE>(a, 2, t, ws + a.L.ds, sD, bc.LDD, lds + bc.halo, lds + bc.rec, reinterpret_cast<uint2*>(lds + bc.trec), sSh, 3);
   __syncthreads();
+  CSTAMP(3, 2);
   // X0 / S1 rows into the dead edge region, asynchronously (needed after the next barrier)
   float* sX0 = lds + bc.x0;
   float* sS1 = lds + bc.s1;
@@ -1608,6 +1634,7 @@ __global__ void __launch_bounds__(CT) vc_eb2n1(VA a) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  CSTAMP(3, 3);
   // DS1 = DU1 Wn1[:, F:] (vb_gemm<GM_DXS> layer 1) and layer 1's dWn / dbn
   for (int job = wave; job < 8; job += CW) {
     const int ib = (job >> 1) * 16, n = (job & 1) * 16 + li;
@@ -1620,6 +1647,7 @@ __global__ void __launch_bounds__(CT) vc_eb2n1(VA a) {
     }
   }
   node_wgrad<CT>(a, part_row(a, 1, t), sDU, bc.LU, sX0, sS1, 8);
+  CSTAMP(3, 4);
 }
 
 template <int FE>
@@ -1632,13 +1660,16 @@ __global__ void __launch_bounds__(CT) vc_eb1(VA a) {
   const int b = a.ws.row_slot[rt0];
   const dr_graph_desc& d = a.descs[b];
   const int i0 = (int)(rt0 - a.ws.row0[b]);
+  CSTAMP(4, 0);
   const BwdCarve bc = bwd_carve(F, a.ws.halo_max, a.ws.tile_edges_max, a.ws.tile_tedges_max, FE, false);
   float* sD = lds + bc.d;
   float* sX0 = lds + bc.x0;
   stage_rows<CT>(sX0, XS, a.s.x + (d.node0 + i0) * XS, XS, nr, 0);
-  chunk_edge_bwd<FE>(a, 1, t, a.ws.base + a.L.d, sD, bc.LDD, lds + bc.halo, lds + bc.rec, reinterpret_cast<uint2*>(lds + bc.trec), lds + bc.sh);
+  chunk_edge_bwd<FE>(a, 1, t, a.ws.base + a.L.d, sD, bc.LDD, lds + bc.halo, lds + bc.rec, reinterpret_cast<uint2*>(lds + bc.trec), lds + bc.sh, 4);
   __syncthreads();
+  CSTAMP(4, 2);
   edge_wgrad<FE>(a, part_row(a, 1, t), sD, bc.LDD, sX0, lds + bc.sh);
+  CSTAMP(4, 3);
 }
 
 // both layers' chunk partials per graph, in chunk order (vb_wgrad_combine x 2)
