@@ -102,11 +102,9 @@ __host__ __device__ inline VCarve vcarve(int N, int E, int Fe) {
 // per-graph global scratch (floats): S1 [32N] | bt1 [E + 1] | bt2 [E + 1] (ReLU words, CSR order) |
 // split exchange: XA [32N] (B2, then dS1) | XB [32N] (dS2) | column sums [MAX_SPLIT][32]
 constexpr int MAXK = DR_VANILLA_MAX_SPLIT;
-// the siblings' weight-gradient partial rows (split > 1), at most F = 32
-__host__ __device__ inline int64_t vpart_floats(int Fe) { return (int64_t)MAXK * DR_VANILLA_SLAB_STRIDE(32, Fe); }
-
 __host__ __device__ inline int64_t vscratch_floats(int N, int E, int Fe) {
-  return 3LL * r4(32 * N) + 2LL * r4(E + 1) + 32 * MAXK + vpart_floats(Fe);
+  (void)Fe;
+  return 3LL * r4(32 * N) + 2LL * r4(E + 1) + 32 * MAXK;
 }
 
 struct VGArgs {
@@ -632,26 +630,19 @@ __device__ __forceinline__ void d_pass(const int* rp, const uint32_t* btg, const
   }
 }
 
-// a weight-gradient entry: plain store, or write-through (sc1) when the graph
-// is split and the last sibling out reads the partial rows
-__device__ __forceinline__ void put_grad(float* p, float v, bool wt) {
-  if (wt) st_sc1(p, v);
-  else *p = v;
-}
-
 // dbe and dWc of one layer from the D pass partials (fixed wave order).
 template <int FE>
-__device__ __forceinline__ void d_pass_sum(const float* red, float* gw, int KE, int F, bool wt) {
+__device__ __forceinline__ void d_pass_sum(const float* red, float* gw, int KE, int F) {
   constexpr int RW = 32 * (1 + FE);
   const int tid = threadIdx.x;
   if (tid < RW) {
     float t = 0.f;
     for (int wv = 0; wv < NW; ++wv) t += red[wv * RW + tid];
-    if (tid < 32) put_grad(gw + 32 * KE + tid, t, wt);
+    if (tid < 32) gw[32 * KE + tid] = t;
     else {
       constexpr int FD = FE > 0 ? FE : 1;  // (FE == 0: this branch never runs)
       const int c = (tid - 32) / FD, f = (tid - 32) % FD;
-      put_grad(gw + c * KE + 2 * F + f, t, wt);
+      gw[c * KE + 2 * F + f] = t;
     }
   }
 }
@@ -742,7 +733,6 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   const float* X0 = s.x + d.node0 * (int64_t)XS;
   const float* ea = s.ea + d.col0 * (int64_t)FeS;
   float* scr = a.scr + a.scr_off[b];
-  const bool split = k > 1;
   const int n32 = r4(32 * N);
   float* S1g = scr;
   uint32_t* bt1g = reinterpret_cast<uint32_t*>(S1g + n32);
@@ -753,16 +743,11 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   const int* teid = s.t_eid + d.col0;                      // transposed slot -> CSR edge
   uint32_t* ctr = a.sync + 2 * b;
   uint32_t* tflag = a.sync + 2 * a.B;
+  const bool split = k > 1;
   const int spin_limit = a.p.spin_limit > 0 ? a.p.spin_limit : (1 << 22);
   const int LG = 32 * KE + 32 + F * KN + F;  // one layer's gradient entries in the slab
   const int row = p.slot ? p.slot[b] : b;  // the graph's rows of the batch (dr_pass.slot)
-  // split: each sibling's weight-gradient partials go (write-through) to its
-  // row of the graph's scratch, and the last sibling out sums the k rows in
-  // sibling order into the graph's slab row (the reduce reads B rows, not kB)
-  float* slab_row = p.slab ? p.slab + (int64_t)row * DR_VANILLA_SLAB_STRIDE(F, Fe) : nullptr;
-  float* part = scr + (3LL * r4(32 * N) + 2LL * r4(E + 1) + 32 * MAXK);  // [k][slab stride]
-  float* slab = (split && slab_row) ? part + (int64_t)rk * DR_VANILLA_SLAB_STRIDE(F, Fe) : slab_row;
-  const bool wt = split;
+  float* slab = p.slab ? p.slab + ((int64_t)row * k + rk) * DR_VANILLA_SLAB_STRIDE(F, Fe) : nullptr;
   const bool bwd = (p.flags & DR_PASS_BACKWARD) != 0;
   const bool lead = rk == 0;  // writes the graph's outputs, loss and head vectors
 
@@ -990,8 +975,8 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
            return i < nown ? (q < F ? Q[(r0 + i) * LS + q] : (q < KN ? R[(r0 + i) * LS + q - F] : 1.f)) : 0.f;
          },
          [&](int n, int q, float v) {
-           if (q < KN) put_grad(gw + 32 * KE + 32 + n * KN + q, sdm[n] * v, wt);
-           else put_grad(gw + 32 * KE + 32 + F * KN + n, sdm[n] * v, wt);
+           if (q < KN) gw[32 * KE + 32 + n * KN + q] = sdm[n] * v;
+           else gw[32 * KE + 32 + F * KN + n] = sdm[n] * v;
          });
     mm_w<1>(nown, [&](int i, int n) { return ((xb[r0 + i] >> n) & 1u) ? sdm[n] : 0.f; },
             a.wpack + op_base(OP_DS2), [&](int) -> const float* { return nullptr; },
@@ -1015,7 +1000,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   );
   wait_vm();  // bt2 and the transposed CSR have landed in U
   __syncthreads();
-  d_pass_sum<FE>(T, slab + LG, KE, F, wt);
+  d_pass_sum<FE>(T, slab + LG, KE, F);
   __syncthreads();
   VSTAMP(11);
   row_t(strp, stcol, bt, P, T, r0, r1);  // D'2 -> T
@@ -1026,10 +1011,10 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
     // dWa2 = D2^T X1,  dWb2 = D'2^T X1
     mm16(32, F, nown, 0, [&](int c, int i) { return i < nown ? R[(r0 + i) * LS + c] : 0.f; },
          [&](int i, int k) { return i < nown && k < F ? Q[(r0 + i) * LS + k] : 0.f; },
-         [&](int c, int k, float v) { put_grad(gw + c * KE + k, v, wt); });
+         [&](int c, int k, float v) { gw[c * KE + k] = v; });
     mm16(32, F, nown, 4, [&](int c, int i) { return i < nown ? T[(r0 + i) * LS + c] : 0.f; },
          [&](int i, int k) { return i < nown && k < F ? Q[(r0 + i) * LS + k] : 0.f; },
-         [&](int c, int k, float v) { put_grad(gw + c * KE + F + k, v, wt); });
+         [&](int c, int k, float v) { gw[c * KE + F + k] = v; });
     // dX1 = [DU2 | D2 | D'2] [Wn2[:, :F]; Wa2; Wb2], DU1 = relu'(X1) * dX1 -> P
     mm_w<3>(nown,
             [&](int i, int k) {
@@ -1056,6 +1041,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
     publish_rows(T, XA, r0, r1);
     VSTAMP(22);
     sib_handoff(ctr, tflag, a.p.fault, spin_limit, k);
+    sib_exit(ctr, k);
     gather_rows(T, XA, N, r0, r1);
   }
   VSTAMP(14);
@@ -1068,8 +1054,8 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
            return i < nown ? (q < F ? Q[ii * XS + q] : (q < KN ? R[ii * 32 + q - F] : 1.f)) : 0.f;
          },
          [&](int n, int q, float v) {
-           if (q < KN) put_grad(gw + 32 * KE + 32 + n * KN + q, v, wt);
-           else put_grad(gw + 32 * KE + 32 + F * KN + n, v, wt);
+           if (q < KN) gw[32 * KE + 32 + n * KN + q] = v;
+           else gw[32 * KE + 32 + F * KN + n] = v;
          });
   }
   __syncthreads();
@@ -1077,7 +1063,7 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
   // D1 = dS1 * cnt1 -> R (S1 is dead), partials in P (DU1 is dead)
   d_pass<FE>(srp, bt1g, ea, T, R, P, N, r0, r1);
   __syncthreads();
-  d_pass_sum<FE>(P, slab, KE, F, wt);
+  d_pass_sum<FE>(P, slab, KE, F);
   __syncthreads();
   VSTAMP(16);
   row_t(strp, stcol, bt, T, P, r0, r1);  // D'1 -> P
@@ -1088,38 +1074,12 @@ __global__ void __launch_bounds__(NT) vanilla_graph_kernel(VGArgs a) {
     // dWa1 = D1^T X0,  dWb1 = D'1^T X0
     mm16(32, F, nown, 0, [&](int c, int i) { return i < nown ? R[(r0 + i) * LS + c] : 0.f; },
          [&](int i, int k) { return i < nown && k < F ? Q[(r0 + i) * XS + k] : 0.f; },
-         [&](int c, int k, float v) { put_grad(gw + c * KE + k, v, wt); });
+         [&](int c, int k, float v) { gw[c * KE + k] = v; });
     mm16(32, F, nown, 4, [&](int c, int i) { return i < nown ? P[(r0 + i) * LS + c] : 0.f; },
          [&](int i, int k) { return i < nown && k < F ? Q[(r0 + i) * XS + k] : 0.f; },
-         [&](int c, int k, float v) { put_grad(gw + c * KE + F + k, v, wt); });
+         [&](int c, int k, float v) { gw[c * KE + F + k] = v; });
   }
   VSTAMP(18);
-  if (!split) return;
-  // The last sibling out (exit counter; it also resets the graph's counters for
-  // the next launch, every sibling having stopped polling) sums the k partial
-  // rows in sibling order into the graph's slab row.  Every wave drained its
-  // write-through partials before its workgroup's arrival.
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  uint32_t* lastf = reinterpret_cast<uint32_t*>(sg);
-  if (tid == 0) {
-    const uint32_t v = __hip_atomic_fetch_add((gu32*)(ctr + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool last = v == (uint32_t)k - 1u;
-    if (last) {
-      __hip_atomic_store((gu32*)ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store((gu32*)(ctr + 1), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    lastf[0] = last ? 1u : 0u;
-  }
-  __syncthreads();
-  if (!lastf[0] || !slab_row) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // the partial loads stay below the exit count
-  const int SS = DR_VANILLA_SLAB_STRIDE(F, Fe);
-  for (int q = tid; q < 2 * LG; q += NT) {
-    float v = ld_sc1(part + q);
-    for (int r = 1; r < k; ++r) v += ld_sc1(part + (int64_t)r * SS + q);
-    slab_row[q] = v;
-  }
 }
 
 }  // namespace

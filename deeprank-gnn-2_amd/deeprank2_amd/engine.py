@@ -509,9 +509,9 @@ class FusedTrainStep:
         for h in handles:  # one real step each, so the slabs hold a batch's partials
             self.step(h, global_batch=global_batch)
         torch.cuda.synchronize(self.device)
-        stream = _lib.stream_ptr(self.device)
 
         def reduces(k):
+            stream = _lib.stream_ptr(self.device)  # inside the capture: the capturing stream
             for i in range(k):
                 h = handles[i % len(handles)]
                 self._table.slab_rows = slab_rows_for(self.spec, h)

@@ -358,11 +358,10 @@ def vanilla_fused_scratch_floats(n, e, fe):
     """Mirror of dr_vanilla_fused_scratch_floats (vanilla_graph.hip), vectorised
     over graphs: S1 (32N), two ReLU word arrays (E + 1 each, CSR order), the
     split's exchange rows XA, XB (32N each) and column sums (4 x 32), every part
-    rounded up to 16 bytes, then the siblings' weight-gradient partial rows
-    (4 x DR_VANILLA_SLAB_STRIDE(32, fe), r04)."""
+    rounded up to 16 bytes (fe: no per-edge-feature part since r03)."""
     r4 = lambda v: (np.asarray(v, dtype=np.int64) + 3) & ~3  # noqa: E731
-    part = 4 * 2 * (32 * (2 * 32 + fe) + 32 + 32 * (32 + 32) + 32)
-    return 3 * r4(32 * np.asarray(n, dtype=np.int64)) + 2 * r4(np.asarray(e, dtype=np.int64) + 1) + 32 * 4 + part
+    del fe
+    return 3 * r4(32 * np.asarray(n, dtype=np.int64)) + 2 * r4(np.asarray(e, dtype=np.int64) + 1) + 32 * 4
 
 
 def make_pass(out_dim, flags, *, dropout: Dropout | None = None, dout=None, loss_kind=_lib.DR_LOSS_NONE, loss_scale=1.0, class_w=None, out=None, loss_per_graph=None, slab=None, head=None, stamps=None, step_counter=None, fault=None, spin_limit=0):

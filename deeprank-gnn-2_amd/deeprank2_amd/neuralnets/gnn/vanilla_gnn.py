@@ -100,7 +100,7 @@ def make_spec(f, fe):
     xs = _r4(f)
 
     def slab_stride(_f):
-        return 2 * layer  # one row per graph: a split graph's last workgroup sums the siblings' partial rows
+        return MAX_SPLIT * 2 * layer  # room for one partial row per workgroup of a split graph
 
     def head_stride(out):
         return 2 * xs + 256 + _r4(out)  # g | h | dh | dout | d mean
@@ -192,7 +192,7 @@ def make_spec(f, fe):
         lds = int(lib.dr_vanilla_lds_bytes(f, fe, p.out_dim))
         _lib.check(lib.dr_vanilla_graph_pass(st.cstruct(), h.descs.data_ptr(), h.B, w, p, sc, lds, _lib.stream_ptr(st.device)), "dr_vanilla_graph_pass")
 
-    return FusedSpec(PARAM_NAMES, recipe, slab_stride, head_stride, "dr_vanilla_graph_pass", weights, lambda *_: 0, dropout=0.0, run=run, handoffs=True, wpack=packed)
+    return FusedSpec(PARAM_NAMES, recipe, slab_stride, head_stride, "dr_vanilla_graph_pass", weights, lambda *_: 0, dropout=0.0, run=run, slab_rows=MAX_SPLIT, slab_k=lambda h: split_k(h, f, fe), handoffs=True, wpack=packed)
 
 
 FUSED_MAX_FE = 4  # vanilla_graph.hip MAXFE

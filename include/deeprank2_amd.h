@@ -495,11 +495,11 @@ int64_t dr_vanilla_lds_bytes(int32_t n_feat, int32_t n_edge_feat, int32_t out_di
  * fits (dr_vanilla_fused_lds_bytes(max N, max E) <= 160 KiB), F <= 32, Fe <= 4.
  * split (1..DR_VANILLA_MAX_SPLIT) workgroups per graph, each owning a
  * contiguous, edge-balanced range of CSR rows; they exchange B2 rows, the
- * mean's column sums and dS2 / dS1 rows through the scratch in-launch.  Each
- * sibling writes its weight-gradient partials to its row of the graph's
- * scratch and the last sibling out sums them in sibling order into the graph's
- * slab row, so the slab holds one row per graph whatever the split
- * (dr_param_table.slab_rows = 1), and the head vectors one row.
+ * mean's column sums and dS2 / dS1 rows through the scratch in-launch.  The
+ * slab then holds `split` partial rows per graph (slab row b*split + r; set
+ * dr_param_table.slab_rows = split), each graph's head vectors one row.
+ * (Summing the partial rows in-launch by the last sibling out was measured
+ * slower and heavier: DESIGN.md §5.)
  * Otherwise the slab/head partials of dr_vanilla_graph_pass, so
  * dr_reduce_update is shared.  scratch: device floats, slot b owns
  * dr_vanilla_fused_scratch_floats(N_b, E_b) of them from scratch_off[b]
