@@ -1124,7 +1124,6 @@ inline int rows_grid(int64_t rows, int rows_per_block) {
 constexpr int CT = 1024;      // threads of the chunk kernels
 constexpr int CW = CT / 64;   // waves
 constexpr int CRG = CT / 32;  // row groups (32 lanes = the 32 channels of one row)
-constexpr int NBT = 256;      // vc_nb2 threads
 
 // diagnostic builds (-DDR_STAMPS): thread 0's s_memtime at phase i of chunk
 // kernel k (0 vc_fwd<1>, 1 vc_fwd<2>, 2 vc_nb2, 3 vc_eb2n1, 4 vc_eb1) in
@@ -1145,39 +1144,166 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 acc) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
 }
 
-// a tile's halo rows of a node-level [rows][32] array (graph block at g32) -> LDS
-template <int NT>
-__device__ __forceinline__ void stage_halo_t(float* dst, const float* g32, const int* ids, int H) {
-  for (int p = threadIdx.x; p < H * 8; p += NT) {
-    const int h = p >> 3, q = (p & 7) * 4;
-    *reinterpret_cast<float4*>(dst + h * 32 + q) = *reinterpret_cast<const float4*>(g32 + (int64_t)ids[h] * 32 + q);
+// The chunk kernels' prologues issue every global load before the first LDS
+// store (the tile's offsets come from one dr_vanilla_tile record), so staging
+// costs about the halo's id -> row chain instead of one memory latency per
+// array and per dependent index (measured: 35-48 % of a chunk workgroup's
+// lifetime, profiles/r04/stamps_vchunk_atom.txt).  KPT items per thread go
+// through registers; anything beyond (graphs past the measured sizes) takes a
+// tail loop.
+constexpr int KPT = 2;
+
+// KPT (= 2) values per thread as two named registers: an array member indexed
+// in an unrolled loop was left in scratch memory (and its store waited for the
+// load it was meant to overlap)
+template <class T>
+struct P2 {
+  T a, b;
+  __device__ __forceinline__ T& operator[](int k) { return k ? b : a; }
+  __device__ __forceinline__ const T& operator[](int k) const { return k ? b : a; }
+};
+__device__ __forceinline__ float& f4at(float4& v, int f) { return f == 0 ? v.x : (f == 1 ? v.y : (f == 2 ? v.z : v.w)); }
+
+// A bounds-checked view of one tile's slice of an array (buffer resource,
+// built from wave-uniform values): loads past `bytes` return 0 without
+// touching memory, so the prologue's guarded loads need no branches -- the
+// compiler then issues them all before the first wait instead of waiting
+// at each branch join.
+constexpr int OOB = 0x7ffffff0;  // a byte offset past every view
+struct Buf {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ Buf(const void* base, int64_t bytes) {
+    const uint64_t p = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p), hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+    const int nb = __builtin_amdgcn_readfirstlane((int)(bytes < OOB ? bytes : OOB));
+    r = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0, nb, 0x00020000);
   }
+  __device__ __forceinline__ float f32(int off) const { return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0)); }
+  __device__ __forceinline__ uint32_t u32(int off) const { return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0); }
+  __device__ __forceinline__ uint32_t u16(int off) const { return __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0); }
+  __device__ __forceinline__ float4 f4(int off) const {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+  }
+};
+
+// a record {head, ea[0..FE)} from registers (put_rec's layout; FE <= 4)
+template <int FE>
+__device__ __forceinline__ void put_rec_v(float* rec, int e, uint32_t head, float4 ev) {
+  constexpr int RS = TileRec<FE>::RS;
+  *reinterpret_cast<float4*>(rec + e * RS) =
+      make_float4(__uint_as_float(head), FE > 0 ? ev.x : 0.f, FE > 1 ? ev.y : 0.f, FE > 2 ? ev.z : 0.f);
+  if (FE > 3) rec[e * RS + 4] = ev.w;
+}
+// edge p's FE attributes (zero past the view and past FE)
+template <int FE>
+__device__ __forceinline__ float4 ea_v(const Buf& ea, int p) {
+  constexpr int FeS = FE > 0 ? FE : 1;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int f = 0; f < FE; ++f) f4at(v, f) = ea.f32((p * FeS + f) * 4);
+  return v;
 }
 
-// rows [0, WR) of a row-major [rows][W] array (W a multiple of 4) into LDS at
-// stride LD: rows < nr from src, the others zero; mask_f > 0 zeroes columns >= mask_f
-template <int NT>
-__device__ __forceinline__ void stage_rows(float* dst, int LD, const float* src, int W, int nr, int mask_f) {
-  const int CH = W / 4;
-  for (int p = threadIdx.x; p < WR * CH; p += NT) {
-    const int i = p / CH, c4 = (p - i * CH) * 4;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (i < nr) {
-      v = *reinterpret_cast<const float4*>(src + (int64_t)i * W + c4);
-      if (mask_f > 0 && c4 + 4 > mask_f) {
-        v.x = c4 < mask_f ? v.x : 0.f;
-        v.y = c4 + 1 < mask_f ? v.y : 0.f;
-        v.z = c4 + 2 < mask_f ? v.z : 0.f;
-        v.w = c4 + 3 < mask_f ? v.w : 0.f;
-      }
-    }
-    *reinterpret_cast<float4*>(dst + i * LD + c4) = v;
+// rows [0, WR) of a row-major [rows][XS] array (XS <= 64: one float4 per
+// thread of CT), rows >= nr zero; columns >= mask_f zeroed when mask_f > 0
+struct RowsV {
+  float4 v;
+  int i, c4;
+  __device__ __forceinline__ void load(const float* src, int XS, int nr, int mask_f) {
+    const int CH = XS / 4;
+    i = threadIdx.x / CH;
+    c4 = (threadIdx.x - i * CH) * 4;
+    const Buf b(src, (int64_t)nr * XS * 4);
+    v = b.f4(i < WR ? (i * XS + c4) * 4 : OOB);
+    mf = mask_f;
   }
+  int mf;
+  // (the mask is applied here, not at the load: a branch on the loaded value
+  // there made the compiler wait for every load issued before it)
+  __device__ __forceinline__ void store(float* dst, int LD) const {
+    float4 w = v;
+    if (mf > 0) {
+      w.x = c4 < mf ? w.x : 0.f;
+      w.y = c4 + 1 < mf ? w.y : 0.f;
+      w.z = c4 + 2 < mf ? w.z : 0.f;
+      w.w = c4 + 3 < mf ? w.w : 0.f;
+    }
+    if (i < WR) *reinterpret_cast<float4*>(dst + i * LD + c4) = w;
+  }
+};
+
+// n entries of a staged weight layout: `off(p)` = the source element's float
+// offset into the weight array (or -1: zero); KPT per thread in registers,
+// the rest by a tail loop at store time
+template <class Off>
+struct MapV {
+  P2<float> v;
+  __device__ __forceinline__ void load(const Buf& w, int n, Off off) {
+#pragma unroll
+    for (int k = 0; k < KPT; ++k) {
+      const int p = threadIdx.x + k * CT;
+      const int o = p < n ? off(p) : -1;
+      v[k] = w.f32(o >= 0 ? o * 4 : OOB);
+    }
+  }
+  __device__ __forceinline__ void store(float* dst, const Buf& w, int n, Off off) const {
+#pragma unroll
+    for (int k = 0; k < KPT; ++k) {
+      const int p = threadIdx.x + k * CT;
+      if (p < n) dst[p] = v[k];
+    }
+    for (int p = threadIdx.x + KPT * CT; p < n; p += CT) {
+      const int o = off(p);
+      dst[p] = w.f32(o >= 0 ? o * 4 : OOB);
+    }
+  }
+};
+template <class Off>
+__device__ __forceinline__ MapV<Off> map_load(const Buf& w, int n, Off off) {
+  MapV<Off> m;
+  m.load(w, n, off);
+  return m;
 }
+
+// a tile's halo rows of a node-level [rows][32] array (its graph's block g32,
+// ng rows): the ids first (load_ids), the rows once they are in (load_rows),
+// then store
+struct HaloV {
+  Buf ids, rows;
+  int H;
+  P2<int> id;
+  P2<float4> v;
+  __device__ __forceinline__ HaloV(const int* ids_, int H_, const float* g32, int ng)
+      : ids(ids_, (int64_t)H_ * 4), rows(g32, (int64_t)ng * 128), H(H_) {}
+  __device__ __forceinline__ void load_ids() {
+#pragma unroll
+    for (int k = 0; k < KPT; ++k) id[k] = (int)ids.u32(((threadIdx.x + k * CT) >> 3) * 4);
+  }
+  __device__ __forceinline__ void load_rows() {
+#pragma unroll
+    for (int k = 0; k < KPT; ++k) {
+      const int p = threadIdx.x + k * CT;
+      v[k] = rows.f4(p < H * 8 ? id[k] * 128 + (p & 7) * 16 : OOB);
+    }
+  }
+  __device__ __forceinline__ void store(float* dst) const {
+#pragma unroll
+    for (int k = 0; k < KPT; ++k) {
+      const int p = threadIdx.x + k * CT;
+      if (p < H * 8) *reinterpret_cast<float4*>(dst + p * 4) = v[k];
+    }
+    for (int p = threadIdx.x + KPT * CT; p < H * 8; p += CT)
+      *reinterpret_cast<float4*>(dst + p * 4) = rows.f4((int)ids.u32((p >> 3) * 4) * 128 + (p & 7) * 16);
+  }
+};
 
 struct FwdCarve {
-  int KP, LA, NOP, LX, a, wn, wh, x1, halo, rec, total;
+  int KP, LA, NOP, LX, a, wn, bn, halo, rec, x1, wh, total;
 };
+// [X | S] rows, Wn^T, bn, then the edge phase's halo rows and CSR records;
+// once the edges are done, the same region holds X1 rows and [Wa2; Wb2]^T
+// (layer 1's next-layer GEMM)
 __host__ __device__ inline FwdCarve fwd_carve(int F, int hmax, int emax, int Fe, bool next) {
   FwdCarve c;
   const int XS = r4(F);
@@ -1186,12 +1312,16 @@ __host__ __device__ inline FwdCarve fwd_carve(int F, int hmax, int emax, int Fe,
   c.NOP = r16(F);
   c.LX = XS + 4;
   int o = 0;
-  c.a = o;    o += WR * c.LA;                 // [X | S] rows (node MLP A operand)
-  c.wn = o;   o += c.KP * c.NOP;              // Wn^T [KP][NOP]
-  c.wh = o;   o += next ? XS * 64 : 0;        // [Wa2; Wb2]^T [XS][64]
-  c.x1 = o;   o += next ? WR * c.LX : 0;      // X1 rows (halves A operand)
-  c.halo = o; o += hmax * 32;                 // B halo rows
-  c.rec = o;  o += emax * (Fe <= 3 ? 4 : 8);  // CSR records {halo column, ea}
+  c.a = o;    o += WR * c.LA;     // [X | S] rows (node MLP A operand)
+  c.wn = o;   o += c.KP * c.NOP;  // Wn^T [KP][NOP]
+  c.bn = o;   o += c.NOP;         // bn, zero past F
+  c.halo = o;                     // B halo rows
+  c.rec = o + hmax * 32;          // CSR records {halo column, ea}
+  c.x1 = o;                       // X1 rows (halves A operand), after the edges
+  c.wh = o + (next ? WR * c.LX : 0);  // [Wa2; Wb2]^T [XS][64], after the edges
+  const int edge = hmax * 32 + emax * (Fe <= 3 ? 4 : 8);
+  const int late = next ? WR * c.LX + XS * 64 : 0;
+  o += edge > late ? edge : late;
   c.total = o;
   return c;
 }
@@ -1240,57 +1370,90 @@ __global__ void __launch_bounds__(CT) vc_fwd(VA a) {
   constexpr bool NEXT = LAYER == 1;
   const Layer L = layer_of(a, LAYER);
   const int F = a.F, KE = a.KE, KN = a.KN, XS = a.XS;
-  const int t = blockIdx.x, tid = threadIdx.x, c = tid & 31, hs = tid & 32;
+  const int tid = threadIdx.x, c = tid & 31, hs = tid & 32, g = tid >> 5;
   CSTAMP(LAYER - 1, 0);
-  const int64_t rt0 = a.ws.tile_row0[t], rt1 = a.ws.tile_row0[t + 1];
-  const int nr = (int)(rt1 - rt0);
-  const int b = a.ws.row_slot[rt0];
-  const dr_graph_desc& d = a.descs[b];
-  const int64_t g0 = a.ws.row0[b];
-  const int* rp = a.s.rowptr + d.node0 + d.gid;
-  const int i0 = (int)(rt0 - g0), e0 = rp[i0], ne = rp[(int)(rt1 - g0)] - e0;
-  const int h0 = a.ws.halo_off[t], H = a.ws.halo_off[t + 1] - h0;
+  const dr_vanilla_tile m = a.ws.tile_meta[blockIdx.x];
+  const int nr = m.nr, ne = m.ne, H = m.n_halo;
+  const int64_t rt0 = m.rt0;
   const FwdCarve fc = fwd_carve(F, a.ws.halo_max, a.ws.tile_edges_max, FE, NEXT);
   float* sA = lds + fc.a;
   float* sWn = lds + fc.wn;
-  float* sWh = lds + fc.wh;
-  float* sX1 = lds + fc.x1;
+  float* sBn = lds + fc.bn;
   float* sB = lds + fc.halo;
   float* sR = lds + fc.rec;
-  stage_halo_t<CT>(sB, L.bm + g0 * 32, a.ws.halo_ids + h0, H);
-  {
-    const float* ea = a.s.ea + (d.col0 + e0) * FeS;
-    const uint16_t* lc = a.ws.lcol + a.ws.lcol_off[t];
-    for (int p = tid; p < ne; p += CT) put_rec<FE>(sR, p, lc[p], ea + (int64_t)p * FeS);
+  // ---- prologue: every global load (bounds-checked views, no branches), the
+  // halo ids first ----
+  HaloV halo(a.ws.halo_ids + m.h0, H, L.bm + m.g0 * 32, m.n_graph);
+  halo.load_ids();
+  const Buf rpv(a.s.rowptr + m.rp0 + m.i0, (int64_t)(nr + 1) * 4);  // the tile's rows' CSR bounds
+  const Buf av(L.a + rt0 * 32, (int64_t)nr * 128);
+  P2<int> rb, re;
+  P2<float> ab;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {  // CRG == 32: row group g owns tile rows g and g + 32
+    const int i = g + CRG * k;
+    rb[k] = (int)rpv.u32(i * 4);
+    re[k] = (int)rpv.u32((i + 1) * 4);
+    ab[k] = av.f32((i * 32 + c) * 4);
   }
-  // the tile's input rows -> [X | .] (pad columns and rows past the tile zero;
-  // the S columns of rows past the tile zero too)
-  stage_rows<CT>(sA, fc.LA, LAYER == 1 ? a.s.x + (d.node0 + i0) * XS : L.xin + rt0 * XS, XS, nr, F);
-  for (int p = tid; p < (WR - nr) * 32; p += CT) sA[(nr + (p >> 5)) * fc.LA + XS + (p & 31)] = 0.f;
-  for (int p = tid; p < fc.KP * fc.NOP; p += CT) {  // vb_gemm<GM_NODE>'s W staging
-    const int k = p / fc.NOP, n = p - k * fc.NOP;
-    float v = 0.f;
-    if (n < F) v = k < F ? L.wn[n * KN + k] : (k < XS ? 0.f : L.wn[n * KN + F + k - XS]);
-    sWn[p] = v;
-  }
-  if (NEXT)
-    for (int p = tid; p < XS * 64; p += CT) {  // vb_gemm<GM_HALVES>'s W staging, layer 2's weights
-      const int k = p >> 6, n = p & 63;
-      sWh[p] = k < F ? a.w.we2[(n & 31) * KE + (n < 32 ? 0 : F) + k] : 0.f;
-    }
   float wcr[FA];
 #pragma unroll
   for (int f = 0; f < FE; ++f) wcr[f] = L.we[c * KE + 2 * F + f];
   const float bc = L.be[c];
-  uint32_t* wr = a.ws.relu_words + (int64_t)(LAYER - 1) * a.ws.edge0[a.B] + a.ws.edge0[b] + e0;
+  const int n_words = a.ws.edge0[a.B];
+  const uint16_t* lc = a.ws.lcol + m.lcol_off;
+  const float* ea = a.s.ea + (m.col0 + m.e0) * FeS;
+  const Buf lcv(lc, (int64_t)ne * 2), eav(ea, (int64_t)ne * FeS * 4);
+  P2<uint32_t> rh;
+  P2<float4> rv;
+#pragma unroll
+  for (int k = 0; k < KPT; ++k) {
+    const int p = tid + k * CT;
+    rh[k] = lcv.u16(p * 2);
+    rv[k] = ea_v<FE>(eav, p);
+  }
+  RowsV xr;
+  xr.load(LAYER == 1 ? a.s.x + m.xrow * XS : L.xin + rt0 * XS, XS, nr, F);
+  const int KP = fc.KP, NOP = fc.NOP;
+  const Buf wnv(L.wn, (int64_t)F * KN * 4);
+  auto wn_off = [&](int p) -> int {  // vb_gemm<GM_NODE>'s W staging
+    const int k = p / NOP, n = p - k * NOP;
+    if (n >= F || (k >= F && k < XS)) return -1;
+    return n * KN + (k < F ? k : F + k - XS);
+  };
+  const auto wn = map_load(wnv, KP * NOP, wn_off);
+  const Buf bnb(L.bn, (int64_t)F * 4);
+  const float bnv = bnb.f32(tid < F ? tid * 4 : OOB);
+  const Buf whb(a.w.we2, (int64_t)32 * KE * 4);
+  auto wh_off = [&](int p) -> int {  // vb_gemm<GM_HALVES>'s W staging, layer 2's weights
+    const int k = p >> 6, n = p & 63;
+    return k < F ? (n & 31) * KE + (n < 32 ? 0 : F) + k : -1;
+  };
+  const auto wh = map_load(whb, NEXT ? XS * 64 : 0, wh_off);
+  halo.load_rows();
+  // ---- LDS stores, in the order of the loads (each waits only for its own) ----
+#pragma unroll
+  for (int k = 0; k < KPT; ++k) {
+    const int p = tid + k * CT;
+    if (p < ne) put_rec_v<FE>(sR, p, rh[k], rv[k]);
+  }
+  xr.store(sA, fc.LA);
+  for (int p = tid; p < (WR - nr) * 32; p += CT) sA[(nr + (p >> 5)) * fc.LA + XS + (p & 31)] = 0.f;
+  wn.store(sWn, wnv, KP * NOP, wn_off);
+  if (tid < NOP) sBn[tid] = bnv;
+  halo.store(sB);
+  for (int p = tid + KPT * CT; p < ne; p += CT) put_rec<FE>(sR, p, lc[p], ea + (int64_t)p * FeS);
+  uint32_t* wr = a.ws.relu_words + (int64_t)(LAYER - 1) * n_words + m.word0 + m.e0;
   __syncthreads();
   CSTAMP(LAYER - 1, 1);
-  for (int64_t r = rt0 + (tid >> 5); r < rt1; r += CRG) {
-    const int i = (int)(r - g0);
-    const float ab = L.a[r * 32 + c] + bc;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = g + CRG * k;
+    if (i >= nr) break;
+    const float abk = ab[k] + bc;
     float acc = 0.f;
-    const int eb = rp[i] - e0, ee = rp[i + 1] - e0;
-    int e = eb;
+    const int ee = re[k] - m.e0;
+    int e = rb[k] - m.e0;
     auto group = [&](auto un) {
       constexpr int U = decltype(un)::value;
       uint32_t j[U];
@@ -1302,31 +1465,34 @@ __global__ void __launch_bounds__(CT) vc_fwd(VA a) {
       uint32_t mine = 0u;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        float pre = ab + q[u];
+        float pre = abk + q[u];
 #pragma unroll
         for (int f = 0; f < FE; ++f) pre = fmaf(wcr[f], ev[u][f], pre);
         acc += relu_keepnan(pre);
-        const uint64_t m = __ballot(active(pre));
-        if (c == u) mine = (uint32_t)(m >> hs);
+        const uint64_t mm = __ballot(active(pre));
+        if (c == u) mine = (uint32_t)(mm >> hs);
       }
       if (c < U) wr[e + c] = mine;
     };
     for (; e + 8 <= ee; e += 8) group(std::integral_constant<int, 8>());
     for (; e + 4 <= ee; e += 4) group(std::integral_constant<int, 4>());
     for (; e < ee; ++e) group(std::integral_constant<int, 1>());
-    L.s[r * 32 + c] = acc;
-    sA[(r - rt0) * fc.LA + XS + c] = acc;
+    L.s[(rt0 + i) * 32 + c] = acc;
+    sA[i * fc.LA + XS + c] = acc;
   }
   __syncthreads();
   CSTAMP(LAYER - 1, 2);
+  float* sX1 = lds + fc.x1;
+  float* sWh = lds + fc.wh;
+  if (NEXT) wh.store(sWh, whb, XS * 64, wh_off);  // into the dead edge region
   // node MLP on MFMA: vb_gemm<GM_NODE>'s operands and k order
   const int lane = tid & 63, wave = tid >> 6, li = lane & 15, kq = lane >> 4;
-  const int nct = fc.NOP / 16;
+  const int nct = NOP / 16;
   for (int job = wave; job < 4 * nct; job += CW) {
     const int ib = (job / nct) * 16, n = (job % nct) * 16 + li;
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < fc.KP; k0 += 4) acc = mfma4(sA[(ib + li) * fc.LA + k0 + kq], sWn[(k0 + kq) * fc.NOP + n], acc);
-    const float bn = n < F ? L.bn[n] : 0.f;
+    for (int k0 = 0; k0 < KP; k0 += 4) acc = mfma4(sA[(ib + li) * fc.LA + k0 + kq], sWn[(k0 + kq) * NOP + n], acc);
+    const float bn = sBn[n];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int i = ib + kq * 4 + q;
@@ -1394,38 +1560,53 @@ __device__ __forceinline__ void node_wgrad(const VA& a, float* out, const float*
   }
 }
 
-__global__ void __launch_bounds__(NBT) vc_nb2(VA a) {
+__global__ void __launch_bounds__(CT) vc_nb2(VA a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int F = a.F, XS = a.XS, KN = a.KN;
-  const int ch = blockIdx.x, tid = threadIdx.x;
+  const int tid = threadIdx.x;
   CSTAMP(2, 0);
-  const int64_t rt0 = a.ws.tile_row0[ch], rt1 = a.ws.tile_row0[ch + 1];
-  const int nr = (int)(rt1 - rt0);
-  const int b = a.ws.row_slot[rt0];
+  const dr_vanilla_tile m = a.ws.tile_meta[blockIdx.x];
+  const int64_t rt0 = m.rt0;
+  const int nr = m.nr;
   const int LU = XS + 4, NOPD = r16(F + 32);
   float* sDU = lds;
   float* sX1 = sDU + WR * LU;
   float* sS = sX1 + WR * XS;
   float* sW = sS + WR * 32;
   float* ws = a.ws.base;
-  const float* X2 = ws + a.L.x2 + rt0 * XS;
-  const int HD = XS + 256 + r4(a.p.out_dim);
-  const float* dmean = a.p.head + (int64_t)(a.p.slot ? a.p.slot[b] : b) * DR_VANILLA_HEAD_STRIDE(F, a.p.out_dim) + HD;
-  for (int p = tid; p < WR * XS; p += NBT) {  // vb_du (layer 2)
-    const int i = p / XS, n = p - i * XS;
-    sDU[i * LU + n] = (i < nr && n < F) ? relu_bwd(X2[(int64_t)i * XS + n], dmean[n]) : 0.f;
-  }
-  stage_rows<NBT>(sX1, XS, ws + a.L.x1 + rt0 * XS, XS, nr, 0);
-  stage_rows<NBT>(sS, 32, ws + a.L.s2 + rt0 * 32, 32, nr, 0);
-  for (int p = tid; p < XS * NOPD; p += NBT) {  // vb_gemm<GM_DXS>'s W staging (Wn2)
+  const int hrow = a.p.slot ? a.p.slot[m.slot] : m.slot;
+  RowsV x2, x1, s2;
+  x2.load(ws + a.L.x2 + rt0 * XS, XS, nr, 0);
+  x1.load(ws + a.L.x1 + rt0 * XS, XS, nr, 0);
+  s2.load(ws + a.L.s2 + rt0 * 32, 32, nr, 0);
+  const Buf wb(a.w.wn2, (int64_t)F * KN * 4);
+  auto w_off = [&](int p) -> int {  // vb_gemm<GM_DXS>'s W staging (Wn2)
     const int k = p / NOPD, n = p - k * NOPD;
-    sW[p] = (k < F && n < F + 32) ? a.w.wn2[k * KN + n] : 0.f;
+    return (k < F && n < F + 32) ? k * KN + n : -1;
+  };
+  const auto w = map_load(wb, XS * NOPD, w_off);
+  const int HD = XS + 256 + r4(a.p.out_dim);
+  const Buf dmb(a.p.head + (int64_t)hrow * DR_VANILLA_HEAD_STRIDE(F, a.p.out_dim) + HD, (int64_t)F * 4);
+  float dm[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) dm[q] = dmb.f32((x2.c4 + q) * 4);
+  // DU2 = relu'(X2) dmean (vb_du, layer 2): zero past the tile's rows and past F
+  float4 du = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (x2.i < nr) {
+    du.x = x2.c4 < F ? relu_bwd(x2.v.x, dm[0]) : 0.f;
+    du.y = x2.c4 + 1 < F ? relu_bwd(x2.v.y, dm[1]) : 0.f;
+    du.z = x2.c4 + 2 < F ? relu_bwd(x2.v.z, dm[2]) : 0.f;
+    du.w = x2.c4 + 3 < F ? relu_bwd(x2.v.w, dm[3]) : 0.f;
   }
+  if (x2.i < WR) *reinterpret_cast<float4*>(sDU + x2.i * LU + x2.c4) = du;
+  x1.store(sX1, XS);
+  s2.store(sS, 32);
+  w.store(sW, wb, XS * NOPD, w_off);
   __syncthreads();
   CSTAMP(2, 1);
   const int lane = tid & 63, wave = tid >> 6, li = lane & 15, kq = lane >> 4;
   const int nct = NOPD / 16;
-  for (int job = wave; job < 4 * nct; job += NBT / 64) {  // [dX1 | DS2] = DU2 Wn2
+  for (int job = wave; job < 4 * nct; job += CW) {  // [dX1 | DS2] = DU2 Wn2
     const int ib = (job / nct) * 16, n = (job % nct) * 16 + li;
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int k0 = 0; k0 < XS; k0 += 4) acc = mfma4(sDU[(ib + li) * LU + k0 + kq], sW[(k0 + kq) * NOPD + n], acc);
@@ -1437,103 +1618,161 @@ __global__ void __launch_bounds__(NBT) vc_nb2(VA a) {
       else if (n < F + 32) ws[a.L.ds + (rt0 + i) * 32 + n - F] = acc[q];
     }
   }
-  node_wgrad<NBT>(a, part_row(a, 2, ch), sDU, LU, sX1, sS, 4 * nct);
+  node_wgrad<CT>(a, part_row(a, 2, blockIdx.x), sDU, LU, sX1, sS, 4 * nct);
   CSTAMP(2, 2);
 }
 
-// a chunk's D_i = relu'-count x dS_i, D'_i (transposed), and its rows' dWc
-// shares, from the halo of dS rows (vb_edge_bwd_tile's sums and order)
+// A chunk's D_i = relu'-count x dS_i, D'_i (transposed) and its rows' dWc
+// shares from the halo of dS rows (vb_edge_bwd_tile's sums and order).  The
+// caller interleaves: load1 (ids, records, per-row values), its own loads,
+// load2 (halo rows, transposed words), store, its own stores, a barrier, run.
 template <int FE>
-__device__ __forceinline__ void chunk_edge_bwd(const VA& a, int l, int t, const float* DS, float* sD, int LDD,
-                                               float* sDS, float* sR, uint2* sTR, float* sSh, int sk) {
-  constexpr int FA = FE > 0 ? FE : 1, FeS = FA;
-  const int tid = threadIdx.x, c = tid & 31;
-  const int64_t rt0 = a.ws.tile_row0[t], rt1 = a.ws.tile_row0[t + 1];
-  const int b = a.ws.row_slot[rt0];
-  const dr_graph_desc& d = a.descs[b];
-  const int64_t g0 = a.ws.row0[b];
-  const int* rp = a.s.rowptr + d.node0 + d.gid;
-  const int* trp = a.s.t_rowptr + d.node0 + d.gid;
-  const int i0 = (int)(rt0 - g0), i1 = (int)(rt1 - g0);
-  const int e0 = rp[i0], ne = rp[i1] - e0, q0 = trp[i0], nq = trp[i1] - q0;
-  const int h0 = a.ws.halo_off[t], H = a.ws.halo_off[t + 1] - h0;
-  const uint32_t* words = a.ws.relu_words + (int64_t)(l - 1) * a.ws.edge0[a.B] + a.ws.edge0[b];
-  stage_halo_t<CT>(sDS, DS + g0 * 32, a.ws.halo_ids + h0, H);
-  {
-    const float* ea = a.s.ea + (d.col0 + e0) * FeS;
-    for (int p = tid; p < ne; p += CT) put_rec<FE>(sR, p, words[e0 + p], ea + (int64_t)p * FeS);
-    const uint16_t* lt = a.ws.ltcol + a.ws.ltcol_off[t];
-    const int* teid = a.s.t_eid + d.col0;
-    for (int p = tid; p < nq; p += CT) sTR[p] = make_uint2(lt[p], words[teid[q0 + p]]);
+struct EdgeBwd {
+  static constexpr int FA = FE > 0 ? FE : 1, FeS = FA;
+  const dr_vanilla_tile& m;
+  const uint32_t* words;  // the graph's ReLU words of layer l
+  const float* ea;
+  const uint16_t* lt;
+  const int* teid;
+  HaloV halo;
+  Buf wv, eav, ltv, tev, wgv, rpv, trpv, dsv;
+  P2<uint32_t> rw, tc, tw;
+  P2<int> te;
+  P2<float4> rv;
+  P2<int> rb, re, qb, qe;
+  P2<float> dsi;
+
+  __device__ __forceinline__ EdgeBwd(const VA& a, const dr_vanilla_tile& mm, int l, const float* ds)
+      : m(mm),
+        words(a.ws.relu_words + (int64_t)(l - 1) * a.ws.edge0[a.B] + mm.word0),
+        ea(a.s.ea + (mm.col0 + mm.e0) * FeS),
+        lt(a.ws.ltcol + mm.ltcol_off),
+        teid(a.s.t_eid + mm.col0 + mm.q0),
+        halo(a.ws.halo_ids + mm.h0, mm.n_halo, ds + mm.g0 * 32, mm.n_graph),
+        wv(words + mm.e0, (int64_t)mm.ne * 4),
+        eav(ea, (int64_t)mm.ne * FeS * 4),
+        ltv(lt, (int64_t)mm.nq * 2),
+        tev(teid, (int64_t)mm.nq * 4),
+        wgv(words, (int64_t)mm.e_graph * 4),
+        rpv(a.s.rowptr + mm.rp0 + mm.i0, (int64_t)(mm.nr + 1) * 4),
+        trpv(a.s.t_rowptr + mm.rp0 + mm.i0, (int64_t)(mm.nr + 1) * 4),
+        dsv(ds + mm.rt0 * 32, (int64_t)mm.nr * 128) {}
+
+  __device__ __forceinline__ void load1() {
+    const int tid = threadIdx.x, c = tid & 31, g = tid >> 5;
+    halo.load_ids();
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = g + CRG * k;
+      rb[k] = (int)rpv.u32(i * 4);
+      re[k] = (int)rpv.u32((i + 1) * 4);
+      qb[k] = (int)trpv.u32(i * 4);
+      qe[k] = (int)trpv.u32((i + 1) * 4);
+      dsi[k] = dsv.f32((i * 32 + c) * 4);
+    }
+#pragma unroll
+    for (int k = 0; k < KPT; ++k) {
+      const int p = tid + k * CT;
+      rw[k] = wv.u32(p * 4);
+      rv[k] = ea_v<FE>(eav, p);
+      tc[k] = ltv.u16(p * 2);
+      te[k] = (int)tev.u32(p * 4);
+    }
   }
-  const int nr = (int)(rt1 - rt0);
-  for (int p = tid; p < (WR - nr) * 64; p += CT) sD[(nr + (p >> 6)) * LDD + (p & 63)] = 0.f;
-  __syncthreads();
-  CSTAMP(sk, 1);
-  float wsum[FA];
+  __device__ __forceinline__ void load2() {
+    halo.load_rows();
 #pragma unroll
-  for (int f = 0; f < FA; ++f) wsum[f] = 0.f;
-  for (int64_t r = rt0 + (tid >> 5); r < rt1; r += CRG) {
-    const int i = (int)(r - g0);
-    const float dsi = DS[r * 32 + c];
-    float cnt = 0.f;
-    float eap[FA];
+    for (int k = 0; k < KPT; ++k) tw[k] = wgv.u32(threadIdx.x + k * CT < m.nq ? te[k] * 4 : OOB);
+  }
+  // load1's records (store1, before the caller's own stores), then load2's
+  // halo rows and transposed records (store2, last)
+  __device__ __forceinline__ void store1(float* sR, float* sD, int LDD) const {
+    const int tid = threadIdx.x;
 #pragma unroll
-    for (int f = 0; f < FA; ++f) eap[f] = 0.f;
-    const int eb = rp[i] - e0, ee = rp[i + 1] - e0;
-    int e = eb;
-    for (; e + 8 <= ee; e += 8) {
-      uint32_t wv[8];
-      float ev[8][FA];
+    for (int k = 0; k < KPT; ++k) {
+      const int p = tid + k * CT;
+      if (p < m.ne) put_rec_v<FE>(sR, p, rw[k], rv[k]);
+    }
+    for (int p = tid; p < (WR - m.nr) * 64; p += CT) sD[(m.nr + (p >> 6)) * LDD + (p & 63)] = 0.f;
+  }
+  __device__ __forceinline__ void store2(float* sDS, float* sR, uint2* sTR) const {
+    const int tid = threadIdx.x;
+    halo.store(sDS);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) wv[u] = get_rec<FE>(sR, e + u, ev[u]);
+    for (int k = 0; k < KPT; ++k) {
+      const int p = tid + k * CT;
+      if (p < m.nq) sTR[p] = make_uint2(tc[k], tw[k]);
+    }
+    for (int p = tid + KPT * CT; p < m.ne; p += CT) put_rec<FE>(sR, p, words[m.e0 + p], ea + (int64_t)p * FeS);
+    for (int p = tid + KPT * CT; p < m.nq; p += CT) sTR[p] = make_uint2(lt[p], words[teid[p]]);
+  }
+  __device__ __forceinline__ void run(float* sD, int LDD, const float* sDS, const float* sR, const uint2* sTR, float* sSh) const {
+    const int tid = threadIdx.x, c = tid & 31, g = tid >> 5;
+    float wsum[FA];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const float bit = edge_bit(wv[u], c);
+    for (int f = 0; f < FA; ++f) wsum[f] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int li = g + CRG * k;
+      if (li >= m.nr) break;
+      float cnt = 0.f;
+      float eap[FA];
+#pragma unroll
+      for (int f = 0; f < FA; ++f) eap[f] = 0.f;
+      const int ee = re[k] - m.e0;
+      int e = rb[k] - m.e0;
+      for (; e + 8 <= ee; e += 8) {
+        uint32_t wv[8];
+        float ev[8][FA];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) wv[u] = get_rec<FE>(sR, e + u, ev[u]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const float bit = edge_bit(wv[u], c);
+          cnt += bit;
+#pragma unroll
+          for (int f = 0; f < FE; ++f) eap[f] = fmaf(bit, ev[u][f], eap[f]);
+        }
+      }
+      for (; e < ee; ++e) {
+        float ev[FA];
+        const float bit = edge_bit(get_rec<FE>(sR, e, ev), c);
         cnt += bit;
 #pragma unroll
-        for (int f = 0; f < FE; ++f) eap[f] = fmaf(bit, ev[u][f], eap[f]);
+        for (int f = 0; f < FE; ++f) eap[f] = fmaf(bit, ev[f], eap[f]);
       }
+      sD[li * LDD + c] = cnt != 0.f ? dsi[k] * cnt : 0.f;
+#pragma unroll
+      for (int f = 0; f < FE; ++f) wsum[f] += cnt != 0.f ? dsi[k] * eap[f] : 0.f;
+      float acc = 0.f;
+      const int qe_ = qe[k] - m.q0;
+      int q = qb[k] - m.q0;
+      for (; q + 8 <= qe_; q += 8) {
+        uint2 tr[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) tr[u] = sTR[q + u];
+        float dv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) dv[u] = sDS[tr[u].x * 32 + c];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if ((tr[u].y >> c) & 1u) acc += dv[u];
+      }
+      for (; q < qe_; ++q) {
+        const uint2 tr = sTR[q];
+        if ((tr.y >> c) & 1u) acc += sDS[tr.x * 32 + c];
+      }
+      sD[li * LDD + 32 + c] = acc;
     }
-    for (; e < ee; ++e) {
-      float ev[FA];
-      const float bit = edge_bit(get_rec<FE>(sR, e, ev), c);
-      cnt += bit;
+    // each wave's share of dWc (its two row groups summed), combined over the
+    // waves in order by the caller
 #pragma unroll
-      for (int f = 0; f < FE; ++f) eap[f] = fmaf(bit, ev[f], eap[f]);
+    for (int f = 0; f < FE; ++f) {
+      const float v = wsum[f] + __shfl_xor(wsum[f], 32, 64);
+      if (tid < 64 * CW && (tid & 63) < 32) sSh[((tid >> 6) * 32 + c) * FeS + f] = v;
     }
-    const int li = (int)(r - rt0);
-    sD[li * LDD + c] = cnt != 0.f ? dsi * cnt : 0.f;
-#pragma unroll
-    for (int f = 0; f < FE; ++f) wsum[f] += cnt != 0.f ? dsi * eap[f] : 0.f;
-    float acc = 0.f;
-    const int qb = trp[i] - q0, qe = trp[i + 1] - q0;
-    int q = qb;
-    for (; q + 8 <= qe; q += 8) {
-      uint2 tr[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) tr[u] = sTR[q + u];
-      float dv[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) dv[u] = sDS[tr[u].x * 32 + c];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if ((tr[u].y >> c) & 1u) acc += dv[u];
-    }
-    for (; q < qe; ++q) {
-      const uint2 tr = sTR[q];
-      if ((tr.y >> c) & 1u) acc += sDS[tr.x * 32 + c];
-    }
-    sD[li * LDD + 32 + c] = acc;
   }
-  // each wave's share of dWc (its two row groups summed), combined over the
-  // waves in order by the caller
-#pragma unroll
-  for (int f = 0; f < FE; ++f) {
-    const float v = wsum[f] + __shfl_xor(wsum[f], 32, 64);
-    if (tid < 64 * CW && (tid & 63) < 32) sSh[((tid >> 6) * 32 + c) * FeS + f] = v;
-  }
-}
+};
 
 // dWa = D^T X, dWb = D'^T X, dbe = sum D, dWc = the waves' shares in order
 // (vb_wgrad_mfma's jobs and order for the first three)
@@ -1578,12 +1817,10 @@ __global__ void __launch_bounds__(CT) vc_eb2n1(VA a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int F = a.F, XS = a.XS, KE = a.KE, KN = a.KN;
   const int t = blockIdx.x, tid = threadIdx.x;
-  const int64_t rt0 = a.ws.tile_row0[t], rt1 = a.ws.tile_row0[t + 1];
-  const int nr = (int)(rt1 - rt0);
-  const int b = a.ws.row_slot[rt0];
-  const dr_graph_desc& d = a.descs[b];
-  const int64_t g0 = a.ws.row0[b];
   CSTAMP(3, 0);
+  const dr_vanilla_tile m = a.ws.tile_meta[t];
+  const int64_t rt0 = m.rt0;
+  const int nr = m.nr;
   const BwdCarve bc = bwd_carve(F, a.ws.halo_max, a.ws.tile_edges_max, a.ws.tile_tedges_max, FE, true);
   float* sD = lds + bc.d;
   float* sX1 = lds + bc.x1;
@@ -1593,37 +1830,53 @@ __global__ void __launch_bounds__(CT) vc_eb2n1(VA a) {
   float* sW1 = lds + bc.w1;
   float* sSh = lds + bc.sh;
   float* ws = a.ws.base;
-  stage_rows<CT>(sX1, XS, ws + a.L.x1 + rt0 * XS, XS, nr, 0);
-  stage_rows<CT>(sDX, XS, ws + a.L.dx1 + rt0 * XS, XS, nr, 0);
-  for (int p = tid; p < 64 * bc.NOP3; p += CT) {  // vb_gemm<GM_DX1>'s W staging
-    const int k = p / bc.NOP3, n = p - k * bc.NOP3;
-    sW3[p] = n < F ? a.w.we2[(k & 31) * KE + (k < 32 ? 0 : F) + n] : 0.f;
-  }
-  for (int p = tid; p < XS * 32; p += CT) {  // vb_gemm<GM_DXS>'s W staging (Wn1), the DS columns
+  EdgeBwd<FE> eb(a, m, 2, ws + a.L.ds);
+  eb.load1();
+  RowsV x1, dx;
+  x1.load(ws + a.L.x1 + rt0 * XS, XS, nr, 0);
+  dx.load(ws + a.L.dx1 + rt0 * XS, XS, nr, 0);
+  const int NOP3 = bc.NOP3;
+  const Buf w3b(a.w.we2, (int64_t)32 * KE * 4);
+  auto w3_off = [&](int p) -> int {  // vb_gemm<GM_DX1>'s W staging
+    const int k = p / NOP3, n = p - k * NOP3;
+    return n < F ? (k & 31) * KE + (k < 32 ? 0 : F) + n : -1;
+  };
+  const auto w3 = map_load(w3b, 64 * NOP3, w3_off);
+  const Buf w1b(a.w.wn1, (int64_t)F * KN * 4);
+  auto w1_off = [&](int p) -> int {  // vb_gemm<GM_DXS>'s W staging (Wn1), the DS columns
     const int k = p >> 5, n = p & 31;
-    sW1[p] = k < F ? a.w.wn1[k * KN + F + n] : 0.f;
-  }
-  chunk_edge_bwd<FE>(a, 2, t, ws + a.L.ds, sD, bc.LDD, lds + bc.halo, lds + bc.rec, reinterpret_cast<uint2*>(lds + bc.trec), sSh, 3);
+    return k < F ? k * KN + F + n : -1;
+  };
+  const auto w1 = map_load(w1b, XS * 32, w1_off);
+  eb.load2();
+  eb.store1(lds + bc.rec, sD, bc.LDD);
+  x1.store(sX1, XS);
+  dx.store(sDX, XS);
+  w3.store(sW3, w3b, 64 * NOP3, w3_off);
+  w1.store(sW1, w1b, XS * 32, w1_off);
+  eb.store2(lds + bc.halo, lds + bc.rec, reinterpret_cast<uint2*>(lds + bc.trec));
+  __syncthreads();
+  CSTAMP(3, 1);
+  eb.run(sD, bc.LDD, lds + bc.halo, lds + bc.rec, reinterpret_cast<const uint2*>(lds + bc.trec), sSh);
   __syncthreads();
   CSTAMP(3, 2);
   // X0 / S1 rows into the dead edge region, asynchronously (needed after the next barrier)
   float* sX0 = lds + bc.x0;
   float* sS1 = lds + bc.s1;
-  const int i0 = (int)(rt0 - g0);
-  dma_x4<CT>(sX0, a.s.x + (d.node0 + i0) * XS, nr * XS / 4);
+  dma_x4<CT>(sX0, a.s.x + m.xrow * XS, nr * XS / 4);
   dma_x4<CT>(sS1, ws + a.L.s1 + rt0 * 32, nr * 8);
   for (int p = tid; p < (WR - nr) * XS; p += CT) sX0[nr * XS + p] = 0.f;
   for (int p = tid; p < (WR - nr) * 32; p += CT) sS1[nr * 32 + p] = 0.f;
   edge_wgrad<FE>(a, part_row(a, 2, t), sD, bc.LDD, sX1, sSh);
   // dX1 = dX1 + [D | D'] [Wa2; Wb2] (vb_gemm<GM_DX1>), then DU1 = relu'(X1) dX1 (vb_du)
   const int lane = tid & 63, wave = tid >> 6, li = lane & 15, kq = lane >> 4;
-  const int nct = bc.NOP3 / 16;
+  const int nct = NOP3 / 16;
   for (int job = (wave + CW - 8 % CW) % CW; job < 4 * nct; job += CW) {
     const int ib = (job / nct) * 16, n = (job % nct) * 16 + li;
     floatx4 acc;
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[q] = n < F ? sDX[(ib + kq * 4 + q) * XS + n] : 0.f;
-    for (int k0 = 0; k0 < 64; k0 += 4) acc = mfma4(sD[(ib + li) * bc.LDD + k0 + kq], sW3[(k0 + kq) * bc.NOP3 + n], acc);
+    for (int k0 = 0; k0 < 64; k0 += 4) acc = mfma4(sD[(ib + li) * bc.LDD + k0 + kq], sW3[(k0 + kq) * NOP3 + n], acc);
     if (n < XS) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -1655,17 +1908,22 @@ __global__ void __launch_bounds__(CT) vc_eb1(VA a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int F = a.F, XS = a.XS;
   const int t = blockIdx.x;
-  const int64_t rt0 = a.ws.tile_row0[t], rt1 = a.ws.tile_row0[t + 1];
-  const int nr = (int)(rt1 - rt0);
-  const int b = a.ws.row_slot[rt0];
-  const dr_graph_desc& d = a.descs[b];
-  const int i0 = (int)(rt0 - a.ws.row0[b]);
   CSTAMP(4, 0);
+  const dr_vanilla_tile m = a.ws.tile_meta[t];
   const BwdCarve bc = bwd_carve(F, a.ws.halo_max, a.ws.tile_edges_max, a.ws.tile_tedges_max, FE, false);
   float* sD = lds + bc.d;
   float* sX0 = lds + bc.x0;
-  stage_rows<CT>(sX0, XS, a.s.x + (d.node0 + i0) * XS, XS, nr, 0);
-  chunk_edge_bwd<FE>(a, 1, t, a.ws.base + a.L.d, sD, bc.LDD, lds + bc.halo, lds + bc.rec, reinterpret_cast<uint2*>(lds + bc.trec), lds + bc.sh, 4);
+  EdgeBwd<FE> eb(a, m, 1, a.ws.base + a.L.d);
+  eb.load1();
+  RowsV x0;
+  x0.load(a.s.x + m.xrow * XS, XS, m.nr, 0);
+  eb.load2();
+  eb.store1(lds + bc.rec, sD, bc.LDD);
+  x0.store(sX0, XS);
+  eb.store2(lds + bc.halo, lds + bc.rec, reinterpret_cast<uint2*>(lds + bc.trec));
+  __syncthreads();
+  CSTAMP(4, 1);
+  eb.run(sD, bc.LDD, lds + bc.halo, lds + bc.rec, reinterpret_cast<const uint2*>(lds + bc.trec), lds + bc.sh);
   __syncthreads();
   CSTAMP(4, 2);
   edge_wgrad<FE>(a, part_row(a, 1, t), sD, bc.LDD, sX0, lds + bc.sh);
@@ -1707,7 +1965,7 @@ inline bool chunk_carves(const dr_vanilla_scratch* sc, int F, int Fe, int64_t* f
 // weight-gradient chunks, the partial buffer holds both layers, Fe <= 4 and
 // every carve fits one workgroup's LDS
 inline bool chunk_fused(const dr_vanilla_scratch* sc, int F, int Fe) {
-  if (!sc->tile_row0 || !sc->relu_words || sc->tile_rows != WR || sc->part_layers != 2 || Fe > 4 || F > 64 ||
+  if (!sc->tile_row0 || !sc->tile_meta || !sc->relu_words || sc->tile_rows != WR || sc->part_layers != 2 || Fe > 4 || F > 64 ||
       sc->n_tiles != sc->n_chunks)
     return false;
   int64_t f1, f2, e2, e1;
@@ -1732,7 +1990,7 @@ int launch_chunk_fused(const VA& a, const dr_vanilla_scratch* sc, hipStream_t st
   hipLaunchKernelGGL((vc_fwd<FE, 2>), tg, dim3(CT), (size_t)f2, st, a);
   hipLaunchKernelGGL(vb_head, dim3(a.B), dim3(HT), 0, st, a);
   if (a.p.flags & DR_PASS_BACKWARD) {
-    hipLaunchKernelGGL(vc_nb2, tg, dim3(NBT), (size_t)nb2_lds(a.F), st, a);
+    hipLaunchKernelGGL(vc_nb2, tg, dim3(CT), (size_t)nb2_lds(a.F), st, a);
     hipLaunchKernelGGL(vc_eb2n1<FE>, tg, dim3(CT), (size_t)e2, st, a);
     hipLaunchKernelGGL(vc_eb1<FE>, tg, dim3(CT), (size_t)e1, st, a);
     hipLaunchKernelGGL(vc_combine, dim3(rows_grid((int64_t)a.B * 2 * layer_grad_size(a.F, a.Fe), RB)), dim3(RB), 0, st, a);
@@ -1865,6 +2123,7 @@ extern "C" int dr_debug_carve_vanilla_chunk_fwd(const int32_t* q, char* buf, int
   DR_DESC_P(d, c, LX);
   DR_DESC(d, c, a);
   DR_DESC(d, c, wn);
+  DR_DESC(d, c, bn);
   DR_DESC(d, c, wh);
   DR_DESC(d, c, x1);
   DR_DESC(d, c, halo);

@@ -97,13 +97,21 @@ class BatchHandle:
                 c.edge0, c.relu_words = e0.data_ptr(), words.data_ptr()
                 if self.vanilla_tile_rows:
                     tr = int(self.vanilla_tile_rows)
-                    plan = vanilla_tile_plan(self, n, row0, tr, n_edge_feat)
+                    meta = [] if chunk_fused else None
+                    plan = vanilla_tile_plan(self, n, row0, tr, n_edge_feat, meta_out=meta)
                     if plan is not None:
                         tensors, (n_tiles, hmax, emax, tmax) = plan
                         keep += tensors
                         (c.tile_row0, c.halo_off, c.halo_ids, c.lcol_off, c.lcol, c.ltcol_off, c.ltcol) = (t.data_ptr() for t in tensors)
                         c.n_tiles, c.halo_max, c.tile_edges_max, c.tile_tedges_max = n_tiles, hmax, emax, tmax
                         c.tile_rows = tr
+                        if meta:
+                            m = np.zeros(len(meta), dtype=VTILE_DTYPE)
+                            for k, name in enumerate(VTILE_DTYPE.names[:-1]):
+                                m[name] = [row[k] for row in meta]
+                            mt = torch.from_numpy(m.view(np.uint8)).to(dev)
+                            keep.append(mt)
+                            c.tile_meta = mt.data_ptr()
                         if VANILLA_CHUNK % tr == 0 and 0 < n_edge_feat <= 4 and not chunk_fused:  # the 16/32-row tiled kernels; tiles never straddle a weight-gradient chunk
                             tfirst = torch.from_numpy(np.concatenate([[0], np.cumsum((n + tr - 1) // tr)]).astype(np.int32)).to(dev)
                             twc = torch.empty(n_tiles * 32 * max(1, n_edge_feat), dtype=torch.float32, device=dev)
@@ -155,15 +163,23 @@ LDS_MAX = 160 * 1024
 VANILLA_CHUNK = 64  # DR_VANILLA_CHUNK: rows per weight-gradient partial of the Vanilla pipeline
 
 
-def vanilla_tile_plan(h: BatchHandle, n, row0, tile_rows, n_edge_feat, lds_check=True):
+# dr_vanilla_tile (include/deeprank2_amd.h): one chunk-fused tile's offsets, 128 bytes
+VTILE_DTYPE = np.dtype([(k, "<i8") for k in ("rt0", "g0", "rp0", "col0", "xrow", "word0")]
+                       + [(k, "<i4") for k in ("nr", "slot", "i0", "e0", "ne", "q0", "nq", "h0", "n_halo", "lcol_off", "ltcol_off", "n_graph", "e_graph")]
+                       + [("pad", "<i4", (7,))])  # fmt: skip
+
+
+def vanilla_tile_plan(h: BatchHandle, n, row0, tile_rows, n_edge_feat, lds_check=True, meta_out=None):
     """Edge-tile plan of the VanillaNetwork pipeline (dr_vanilla_scratch tile_*
     fields; also ginet_nocluster's large-graph pipeline, dr_nc_plan): each graph's rows cut into tiles of ``tile_rows``; per tile the
     ascending union of its rows' out- and in-neighbours (the halo staged in LDS)
     and every CSR / transposed edge's column as an index into it.  None when a
-    tile's LDS would exceed one workgroup's 160 KiB (the untiled kernels run)."""
+    tile's LDS would exceed one workgroup's 160 KiB (the untiled kernels run).
+    ``meta_out`` (a list): receives each tile's dr_vanilla_tile fields."""
     p = h.store.packed
     tile_row0, hoff, hids, loff, lcs, toff, tcs = [0], [0], [], [0], [], [0], []
     hmax = emax = tmax = 0
+    word0 = 0
     for slot, gid in enumerate(h.gids_host.astype(np.int64)):
         ng = int(n[slot])
         n0, e0, e1 = int(p.node_off[gid]), int(p.edge_off[gid]), int(p.edge_off[gid + 1])
@@ -174,6 +190,9 @@ def vanilla_tile_plan(h: BatchHandle, n, row0, tile_rows, n_edge_feat, lds_check
             r1 = min(ng, r0 + tile_rows)
             cs, ts = col[rp[r0] : rp[r1]], tcol[trp[r0] : trp[r1]]
             halo = np.union1d(cs, ts).astype(np.int32)
+            if meta_out is not None:
+                meta_out.append((int(row0[slot]) + r0, int(row0[slot]), n0 + int(gid), int(h.store.col_off_host[gid]), n0 + r0, word0,
+                                 r1 - r0, slot, r0, int(rp[r0]), cs.size, int(trp[r0]), ts.size, hoff[-1], halo.size, loff[-1], toff[-1], ng, e1 - e0))
             hids.append(halo)
             hoff.append(hoff[-1] + halo.size)
             lcs.append(np.searchsorted(halo, cs).astype(np.uint16))
@@ -182,6 +201,7 @@ def vanilla_tile_plan(h: BatchHandle, n, row0, tile_rows, n_edge_feat, lds_check
             toff.append(toff[-1] + ts.size)
             tile_row0.append(int(row0[slot]) + r1)
             hmax, emax, tmax = max(hmax, halo.size), max(emax, cs.size), max(tmax, ts.size)
+        word0 += e1 - e0
     n_tiles = len(tile_row0) - 1
     if n_tiles == 0 or hmax == 0 or hmax > 65535:  # noqa: PLR2004
         return None

@@ -470,8 +470,35 @@ typedef struct dr_vanilla_scratch {
    * partials) with the intermediates in LDS -- 8 launches per step instead of
    * 17, the same results (dWc summed in another order).  0 / 1: one layer.   */
   int32_t part_layers;
+  /* the chunk-fused kernels' per-tile records [n_tiles] (required by them):
+   * every offset a chunk workgroup needs, so its prologue is one record load
+   * instead of a chain of dependent index loads                             */
+  const struct dr_vanilla_tile* tile_meta;
 } dr_vanilla_scratch;
 #define DR_VANILLA_CHUNK 64
+
+/* One 64-row tile (chunk) of the Vanilla pipeline, 128 bytes. */
+typedef struct dr_vanilla_tile {
+  int64_t rt0;    /* batch row of the tile's first row                          */
+  int64_t g0;     /* batch row of its graph's node 0 (row0[slot])              */
+  int64_t rp0;    /* index of the graph's node 0 in rowptr / t_rowptr: node0 + gid */
+  int64_t col0;   /* the graph's first CSR slot in the store: desc.col0         */
+  int64_t xrow;   /* store x row of the tile's first row: node0 + i0            */
+  int64_t word0;  /* relu_words index of the graph's edge 0: edge0[slot]        */
+  int32_t nr;     /* rows in the tile                                          */
+  int32_t slot;   /* batch slot of the graph                                   */
+  int32_t i0;     /* graph-local index of the tile's first row                 */
+  int32_t e0;     /* graph-local CSR slot of its first edge: rowptr[i0]         */
+  int32_t ne;     /* CSR edges of its rows                                     */
+  int32_t q0;     /* graph-local transposed slot of its first in-edge: t_rowptr[i0] */
+  int32_t nq;     /* transposed edges of its rows                              */
+  int32_t h0;     /* halo_off[tile]                                            */
+  int32_t n_halo; /* halo rows                                                 */
+  int32_t lcol_off, ltcol_off;
+  int32_t n_graph; /* its graph's rows                                         */
+  int32_t e_graph; /* its graph's CSR edges                                    */
+  int32_t pad[7];
+} dr_vanilla_tile;
 
 /* slab: per layer [dWe (32 x (2F+Fe)) | dbe (32) | dWn (F x (F+32)) | dbn (F)], layer 1 then 2
  * head: g [r4(F)] | relu(fc1) [128] | its grad [128] | dout [r4(out)] | d mean [r4(F)] */

@@ -291,13 +291,17 @@ def test_vanilla_tile_and_chunk_carves(H, EM, TM, Fe):
     F = 30
     XS = r4(F)
     for nxt in (0, 1):
-        # vc_fwd: [X | S] rows at stride KP + 4 (the node MLP's A operand), Wn^T [KP][NOP],
-        # (layer 1) [Wa2; Wb2]^T [XS][64] and X1 rows at XS + 4, halo B rows, CSR records
+        # vc_fwd: [X | S] rows at stride KP + 4 (the node MLP's A operand), Wn^T [KP][NOP], bn [NOP],
+        # halo B rows and CSR records; after the edge phase the same region holds (layer 1)
+        # X1 rows at XS + 4 and [Wa2; Wb2]^T [XS][64]
         def fext(v, nxt=nxt):
             KP = XS + 32
-            return {"a": 64 * (KP + 4), "wn": KP * r16(F), "wh": XS * 64 if nxt else 0, "x1": 64 * (XS + 4) if nxt else 0, "halo": H * 32, "rec": EM * RS}
+            return {"a": 64 * (KP + 4), "wn": KP * r16(F), "bn": r16(F), "wh": XS * 64 if nxt else 0, "x1": 64 * (XS + 4) if nxt else 0, "halo": H * 32, "rec": EM * RS}
 
-        _check("vanilla_chunk_fwd", [F, H, EM, Fe, nxt], fext)
+        vals, total = _check("vanilla_chunk_fwd", [F, H, EM, Fe, nxt], fext, phases=[{"halo", "rec"}, {"x1", "wh"}])
+        assert vals["x1"] == vals["halo"]  # the late region overlays the dead edge region
+        if nxt:
+            assert vals["wh"] + XS * 64 <= total
     FeS = max(Fe, 1)
     for two in (0, 1):
         # vc_eb2n1 / vc_eb1: [D | D'] rows (LDD 68), the waves' dWc shares sSh[(wave 32 + c) FeS + f]
