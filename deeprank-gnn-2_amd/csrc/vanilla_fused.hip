@@ -1364,7 +1364,7 @@ __host__ __device__ inline BwdCarve bwd_carve(int F, int hmax, int emax, int tma
 }
 
 template <int FE, int LAYER>
-__global__ void __launch_bounds__(CT) vc_fwd(VA a) {
+__global__ void __launch_bounds__(CT, 8) vc_fwd(VA a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int FA = FE > 0 ? FE : 1, FeS = FA;
   constexpr bool NEXT = LAYER == 1;
@@ -1424,12 +1424,6 @@ __global__ void __launch_bounds__(CT) vc_fwd(VA a) {
   const auto wn = map_load(wnv, KP * NOP, wn_off);
   const Buf bnb(L.bn, (int64_t)F * 4);
   const float bnv = bnb.f32(tid < F ? tid * 4 : OOB);
-  const Buf whb(a.w.we2, (int64_t)32 * KE * 4);
-  auto wh_off = [&](int p) -> int {  // vb_gemm<GM_HALVES>'s W staging, layer 2's weights
-    const int k = p >> 6, n = p & 63;
-    return k < F ? (n & 31) * KE + (n < 32 ? 0 : F) + k : -1;
-  };
-  const auto wh = map_load(whb, NEXT ? XS * 64 : 0, wh_off);
   halo.load_rows();
   // ---- LDS stores, in the order of the loads (each waits only for its own) ----
 #pragma unroll
@@ -1474,7 +1468,10 @@ __global__ void __launch_bounds__(CT) vc_fwd(VA a) {
       }
       if (c < U) wr[e + c] = mine;
     };
-    for (; e + 8 <= ee; e += 8) group(std::integral_constant<int, 8>());
+    // (8 edges in flight for FE <= 1; 4 above, within the 64 VGPRs of two
+    // workgroups per CU)
+    if (FE <= 1)
+      for (; e + 8 <= ee; e += 8) group(std::integral_constant<int, 8>());
     for (; e + 4 <= ee; e += 4) group(std::integral_constant<int, 4>());
     for (; e < ee; ++e) group(std::integral_constant<int, 1>());
     L.s[(rt0 + i) * 32 + c] = acc;
@@ -1484,7 +1481,14 @@ __global__ void __launch_bounds__(CT) vc_fwd(VA a) {
   CSTAMP(LAYER - 1, 2);
   float* sX1 = lds + fc.x1;
   float* sWh = lds + fc.wh;
-  if (NEXT) wh.store(sWh, whb, XS * 64, wh_off);  // into the dead edge region
+  // [Wa2; Wb2]^T (layer 1): loaded now (registers stay free through the edge
+  // phase), stored into the dead edge region after the node MLP's MFMAs
+  const Buf whb(a.w.we2, (int64_t)32 * KE * 4);
+  auto wh_off = [&](int p) -> int {  // vb_gemm<GM_HALVES>'s W staging, layer 2's weights
+    const int k = p >> 6, n = p & 63;
+    return k < F ? (n & 31) * KE + (n < 32 ? 0 : F) + k : -1;
+  };
+  const auto wh = map_load(whb, NEXT ? XS * 64 : 0, wh_off);
   // node MLP on MFMA: vb_gemm<GM_NODE>'s operands and k order
   const int lane = tid & 63, wave = tid >> 6, li = lane & 15, kq = lane >> 4;
   const int nct = NOP / 16;
@@ -1503,6 +1507,7 @@ __global__ void __launch_bounds__(CT) vc_fwd(VA a) {
   }
   CSTAMP(LAYER - 1, 3);
   if (!NEXT) return;
+  wh.store(sWh, whb, XS * 64, wh_off);
   __syncthreads();
   // layer 2's [A | B] = X1 [Wa2; Wb2]^T: vb_gemm<GM_HALVES>'s operands and k order
   const Layer L2 = layer_of(a, 2);
