@@ -1298,34 +1298,6 @@ struct HaloV {
   }
 };
 
-struct FwdCarve {
-  int KP, LA, NOP, LX, a, wn, bn, halo, rec, x1, wh, total;
-};
-// [X | S] rows, Wn^T, bn, then the edge phase's halo rows and CSR records;
-// once the edges are done, the same region holds X1 rows and [Wa2; Wb2]^T
-// (layer 1's next-layer GEMM)
-__host__ __device__ inline FwdCarve fwd_carve(int F, int hmax, int emax, int Fe, bool next) {
-  FwdCarve c;
-  const int XS = r4(F);
-  c.KP = XS + 32;  // [X | S]
-  c.LA = c.KP + 4;
-  c.NOP = r16(F);
-  c.LX = XS + 4;
-  int o = 0;
-  c.a = o;    o += WR * c.LA;     // [X | S] rows (node MLP A operand)
-  c.wn = o;   o += c.KP * c.NOP;  // Wn^T [KP][NOP]
-  c.bn = o;   o += c.NOP;         // bn, zero past F
-  c.halo = o;                     // B halo rows
-  c.rec = o + hmax * 32;          // CSR records {halo column, ea}
-  c.x1 = o;                       // X1 rows (halves A operand), after the edges
-  c.wh = o + (next ? WR * c.LX : 0);  // [Wa2; Wb2]^T [XS][64], after the edges
-  const int edge = hmax * 32 + emax * (Fe <= 3 ? 4 : 8);
-  const int late = next ? WR * c.LX + XS * 64 : 0;
-  o += edge > late ? edge : late;
-  c.total = o;
-  return c;
-}
-
 struct BwdCarve {
   int LDD, LU, NOP3, d, x1, dx, w3, du, w1, sh, x0, s1, halo, rec, trec, total;
 };
@@ -1363,11 +1335,70 @@ __host__ __device__ inline BwdCarve bwd_carve(int F, int hmax, int emax, int tma
   return c;
 }
 
+struct FwdCarve {
+  int HS, KP, LA, NOP, hp, xo, wab, halo, rec, a, wn, bn, total;
+};
+// Edge phase: the halo's X rows (then, in place, their B = X Wb^T), the tile's
+// own X rows (then, in place, A = X Wa^T), [Wa; Wb]^T and the CSR records.
+// Once the edges are done the same space holds the node MLP's [X | S] rows,
+// Wn^T and bn.  Rows at stride HS = 36 (the MFMA A-operand reads of 16 rows
+// at stride 32 would hit two banks).
+__host__ __device__ inline FwdCarve fwd_carve(int F, int hmax, int emax, int Fe) {
+  FwdCarve c;
+  const int XS = r4(F);
+  c.HS = 36;
+  c.KP = XS + 32;  // [X | S]
+  c.LA = c.KP + 4;
+  c.NOP = r16(F);
+  c.hp = r16(hmax);  // halo rows rounded up to the MFMA's 16-row blocks
+  int o = 0;
+  c.xo = o;   o += WR * c.HS;       // own X rows -> A
+  c.wab = o;  o += XS * 64;         // [Wa; Wb]^T [XS][64]
+  c.halo = o; o += c.hp * c.HS;     // halo X rows -> B
+  c.rec = o;  o += emax * (Fe <= 3 ? 4 : 8);  // CSR records {halo column, ea}
+  const int edge = o;
+  c.a = 0;                          // after the edges: [X | S] rows (node MLP A operand)
+  c.wn = WR * c.LA;                 // Wn^T [KP][NOP]
+  c.bn = c.wn + c.KP * c.NOP;       // bn, zero past F
+  const int late = c.bn + c.NOP;
+  c.total = edge > late ? edge : late;
+  return c;
+}
+
+// [A | B] rows = X [Wa; Wb]^T in place over X rows at stride HS (vb_gemm<GM_HALVES>'s
+// operands and k order; half 0 = A, 1 = B): rows [0, nrows) in 16-row blocks, a
+// block's two 16-column tiles on one wave (its reads finish before its writes)
+__device__ __forceinline__ void halves_in_place(float* sX, int HS, int nrows, const float* sW, int XS, int half, int job0) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, kq = lane >> 4;
+  const int nb = (nrows + 15) >> 4;
+  for (int jb = (wave + CW - job0 % CW) % CW; jb < nb; jb += CW) {
+    const int ib = jb * 16;
+    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    const int n0 = half * 32 + li, n1 = n0 + 16;
+    for (int k0 = 0; k0 < XS; k0 += 4) {
+      const float av = sX[(ib + li) * HS + k0 + kq];
+      acc0 = mfma4(av, sW[(k0 + kq) * 64 + n0], acc0);
+      acc1 = mfma4(av, sW[(k0 + kq) * 64 + n1], acc1);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = ib + kq * 4 + q;
+      if (i < nrows) {
+        sX[i * HS + li] = acc0[q];
+        sX[i * HS + 16 + li] = acc1[q];
+      }
+    }
+  }
+}
+
+// Layer l of the chunk-fused forward: [A | B] of the tile's rows and halo
+// rows (MFMA, in LDS: the node-level A / B arrays and their GEMM launch are
+// gone), the edge gather S_i = sum_e relu(A_i + B_j + Wc ea_e + be) with the
+// ReLU words, then the node MLP X_l = relu([X | S_l] Wn^T + bn).
 template <int FE, int LAYER>
 __global__ void __launch_bounds__(CT, 8) vc_fwd(VA a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int FA = FE > 0 ? FE : 1, FeS = FA;
-  constexpr bool NEXT = LAYER == 1;
   const Layer L = layer_of(a, LAYER);
   const int F = a.F, KE = a.KE, KN = a.KN, XS = a.XS;
   const int tid = threadIdx.x, c = tid & 31, hs = tid & 32, g = tid >> 5;
@@ -1375,26 +1406,28 @@ __global__ void __launch_bounds__(CT, 8) vc_fwd(VA a) {
   const dr_vanilla_tile m = a.ws.tile_meta[blockIdx.x];
   const int nr = m.nr, ne = m.ne, H = m.n_halo;
   const int64_t rt0 = m.rt0;
-  const FwdCarve fc = fwd_carve(F, a.ws.halo_max, a.ws.tile_edges_max, FE, NEXT);
-  float* sA = lds + fc.a;
-  float* sWn = lds + fc.wn;
-  float* sBn = lds + fc.bn;
+  const FwdCarve fc = fwd_carve(F, a.ws.halo_max, a.ws.tile_edges_max, FE);
+  const int HS = fc.HS;
+  float* sXo = lds + fc.xo;
+  float* sWab = lds + fc.wab;
   float* sB = lds + fc.halo;
   float* sR = lds + fc.rec;
+  // the layer's input rows: the store's x (layer 1) or X1 (layer 2); graph block xg
+  const float* xg = LAYER == 1 ? a.s.x + (m.xrow - m.i0) * XS : L.xin + m.g0 * XS;
   // ---- prologue: every global load (bounds-checked views, no branches), the
   // halo ids first ----
-  HaloV halo(a.ws.halo_ids + m.h0, H, L.bm + m.g0 * 32, m.n_graph);
-  halo.load_ids();
+  const Buf idv(a.ws.halo_ids + m.h0, (int64_t)H * 4);
+  const Buf xgv(xg, (int64_t)m.n_graph * XS * 4);
+  P2<int> hid;
+#pragma unroll
+  for (int k = 0; k < KPT; ++k) hid[k] = (int)idv.u32(((tid + k * CT) >> 3) * 4);
   const Buf rpv(a.s.rowptr + m.rp0 + m.i0, (int64_t)(nr + 1) * 4);  // the tile's rows' CSR bounds
-  const Buf av(L.a + rt0 * 32, (int64_t)nr * 128);
   P2<int> rb, re;
-  P2<float> ab;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {  // CRG == 32: row group g owns tile rows g and g + 32
     const int i = g + CRG * k;
     rb[k] = (int)rpv.u32(i * 4);
     re[k] = (int)rpv.u32((i + 1) * 4);
-    ab[k] = av.f32((i * 32 + c) * 4);
   }
   float wcr[FA];
 #pragma unroll
@@ -1412,10 +1445,60 @@ __global__ void __launch_bounds__(CT, 8) vc_fwd(VA a) {
     rh[k] = lcv.u16(p * 2);
     rv[k] = ea_v<FE>(eav, p);
   }
-  RowsV xr;
-  xr.load(LAYER == 1 ? a.s.x + m.xrow * XS : L.xin + rt0 * XS, XS, nr, F);
-  const int KP = fc.KP, NOP = fc.NOP;
+  // own X rows: one float4 per thread (XS <= 32: WR * 8 pieces of 4 columns)
+  const int oi = tid >> 3, oc = (tid & 7) * 4;
+  const float4 xo = xgv.f4(oi < nr && oc < XS ? ((m.i0 + oi) * XS + oc) * 4 : OOB);
+  const Buf wabv(L.we, (int64_t)32 * KE * 4);
+  auto wab_off = [&](int p) -> int {  // vb_gemm<GM_HALVES>'s W staging
+    const int k = p >> 6, n = p & 63;
+    return k < F ? (n & 31) * KE + (n < 32 ? 0 : F) + k : -1;
+  };
+  const auto wab = map_load(wabv, XS * 64, wab_off);
+  // halo X rows (8 pieces of 4 columns per row; the ids are in by now)
+  P2<float4> hx;
+#pragma unroll
+  for (int k = 0; k < KPT; ++k) {
+    const int p = tid + k * CT, q4 = (p & 7) * 4;
+    hx[k] = xgv.f4(p < H * 8 && q4 < XS ? (hid[k] * XS + q4) * 4 : OOB);
+  }
+  // X rows' pad columns (>= F) read as zero (scratch rows leave them unwritten)
+  auto mask4 = [&](float4 v, int c4) {
+    if (c4 + 4 > F) {
+      v.x = c4 < F ? v.x : 0.f;
+      v.y = c4 + 1 < F ? v.y : 0.f;
+      v.z = c4 + 2 < F ? v.z : 0.f;
+      v.w = c4 + 3 < F ? v.w : 0.f;
+    }
+    return v;
+  };
+  // ---- LDS stores, in the order of the loads ----
+#pragma unroll
+  for (int k = 0; k < KPT; ++k) {
+    const int p = tid + k * CT;
+    if (p < ne) put_rec_v<FE>(sR, p, rh[k], rv[k]);
+  }
+  if (oi < WR) *reinterpret_cast<float4*>(sXo + oi * HS + oc) = mask4(xo, oc);
+  wab.store(sWab, wabv, XS * 64, wab_off);
+#pragma unroll
+  for (int k = 0; k < KPT; ++k) {
+    const int p = tid + k * CT;
+    if (p < H * 8) *reinterpret_cast<float4*>(sB + (p >> 3) * HS + (p & 7) * 4) = mask4(hx[k], (p & 7) * 4);
+  }
+  for (int p = tid + KPT * CT; p < H * 8; p += CT) {
+    const int q4 = (p & 7) * 4;
+    const float4 v = xgv.f4(q4 < XS ? ((int)idv.u32((p >> 3) * 4) * XS + q4) * 4 : OOB);
+    *reinterpret_cast<float4*>(sB + (p >> 3) * HS + q4) = mask4(v, q4);
+  }
+  for (int p = tid + KPT * CT; p < ne; p += CT) put_rec<FE>(sR, p, lc[p], ea + (int64_t)p * FeS);
+  __syncthreads();
+  CSTAMP(LAYER - 1, 1);
+  // ---- [A | B]: A of the own rows, B of the halo rows, in place ----
+  halves_in_place(sXo, HS, WR, sWab, XS, 0, 0);
+  halves_in_place(sB, HS, H, sWab, XS, 1, WR / 16);
+  // (the node MLP's operands, loaded now: they land during the edge phase)
+  const float4 xa = mask4(xo, oc);
   const Buf wnv(L.wn, (int64_t)F * KN * 4);
+  const int KP = fc.KP, NOP = fc.NOP;
   auto wn_off = [&](int p) -> int {  // vb_gemm<GM_NODE>'s W staging
     const int k = p / NOP, n = p - k * NOP;
     if (n >= F || (k >= F && k < XS)) return -1;
@@ -1424,27 +1507,16 @@ __global__ void __launch_bounds__(CT, 8) vc_fwd(VA a) {
   const auto wn = map_load(wnv, KP * NOP, wn_off);
   const Buf bnb(L.bn, (int64_t)F * 4);
   const float bnv = bnb.f32(tid < F ? tid * 4 : OOB);
-  halo.load_rows();
-  // ---- LDS stores, in the order of the loads (each waits only for its own) ----
-#pragma unroll
-  for (int k = 0; k < KPT; ++k) {
-    const int p = tid + k * CT;
-    if (p < ne) put_rec_v<FE>(sR, p, rh[k], rv[k]);
-  }
-  xr.store(sA, fc.LA);
-  for (int p = tid; p < (WR - nr) * 32; p += CT) sA[(nr + (p >> 5)) * fc.LA + XS + (p & 31)] = 0.f;
-  wn.store(sWn, wnv, KP * NOP, wn_off);
-  if (tid < NOP) sBn[tid] = bnv;
-  halo.store(sB);
-  for (int p = tid + KPT * CT; p < ne; p += CT) put_rec<FE>(sR, p, lc[p], ea + (int64_t)p * FeS);
-  uint32_t* wr = a.ws.relu_words + (int64_t)(LAYER - 1) * n_words + m.word0 + m.e0;
   __syncthreads();
-  CSTAMP(LAYER - 1, 1);
+  CSTAMP(LAYER - 1, 2);
+  // ---- edge gather ----
+  uint32_t* wr = a.ws.relu_words + (int64_t)(LAYER - 1) * n_words + m.word0 + m.e0;
+  P2<float> sacc{0.f, 0.f};
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const int i = g + CRG * k;
     if (i >= nr) break;
-    const float abk = ab[k] + bc;
+    const float abk = sXo[i * HS + c] + bc;
     float acc = 0.f;
     const int ee = re[k] - m.e0;
     int e = rb[k] - m.e0;
@@ -1455,7 +1527,7 @@ __global__ void __launch_bounds__(CT, 8) vc_fwd(VA a) {
 #pragma unroll
       for (int u = 0; u < U; ++u) j[u] = get_rec<FE>(sR, e + u, ev[u]);
 #pragma unroll
-      for (int u = 0; u < U; ++u) q[u] = sB[j[u] * 32 + c];
+      for (int u = 0; u < U; ++u) q[u] = sB[j[u] * HS + c];
       uint32_t mine = 0u;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -1475,21 +1547,21 @@ __global__ void __launch_bounds__(CT, 8) vc_fwd(VA a) {
     for (; e + 4 <= ee; e += 4) group(std::integral_constant<int, 4>());
     for (; e < ee; ++e) group(std::integral_constant<int, 1>());
     L.s[(rt0 + i) * 32 + c] = acc;
-    sA[i * fc.LA + XS + c] = acc;
+    sacc[k] = acc;
   }
   __syncthreads();
-  CSTAMP(LAYER - 1, 2);
-  float* sX1 = lds + fc.x1;
-  float* sWh = lds + fc.wh;
-  // [Wa2; Wb2]^T (layer 1): loaded now (registers stay free through the edge
-  // phase), stored into the dead edge region after the node MLP's MFMAs
-  const Buf whb(a.w.we2, (int64_t)32 * KE * 4);
-  auto wh_off = [&](int p) -> int {  // vb_gemm<GM_HALVES>'s W staging, layer 2's weights
-    const int k = p >> 6, n = p & 63;
-    return k < F ? (n & 31) * KE + (n < 32 ? 0 : F) + k : -1;
-  };
-  const auto wh = map_load(whb, NEXT ? XS * 64 : 0, wh_off);
-  // node MLP on MFMA: vb_gemm<GM_NODE>'s operands and k order
+  CSTAMP(LAYER - 1, 3);
+  // ---- node MLP: [X | S] rows, Wn^T and bn into the dead edge space ----
+  float* sA = lds + fc.a;
+  float* sWn = lds + fc.wn;
+  float* sBn = lds + fc.bn;
+  if (oi < WR && oc < XS) *reinterpret_cast<float4*>(sA + oi * fc.LA + oc) = xa;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) sA[(g + CRG * k) * fc.LA + XS + c] = g + CRG * k < nr ? sacc[k] : 0.f;
+  wn.store(sWn, wnv, KP * NOP, wn_off);
+  if (tid < NOP) sBn[tid] = bnv;
+  __syncthreads();
+  // vb_gemm<GM_NODE>'s operands and k order
   const int lane = tid & 63, wave = tid >> 6, li = lane & 15, kq = lane >> 4;
   const int nct = NOP / 16;
   for (int job = wave; job < 4 * nct; job += CW) {
@@ -1500,28 +1572,10 @@ __global__ void __launch_bounds__(CT, 8) vc_fwd(VA a) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int i = ib + kq * 4 + q;
-      const float v = relu_keepnan(acc[q] + bn);
-      if (i < nr && n < F) L.xout[(rt0 + i) * XS + n] = v;
-      if (NEXT && n < XS) sX1[i * fc.LX + n] = n < F ? v : 0.f;
+      if (i < nr && n < F) L.xout[(rt0 + i) * XS + n] = relu_keepnan(acc[q] + bn);
     }
   }
-  CSTAMP(LAYER - 1, 3);
-  if (!NEXT) return;
-  wh.store(sWh, whb, XS * 64, wh_off);
-  __syncthreads();
-  // layer 2's [A | B] = X1 [Wa2; Wb2]^T: vb_gemm<GM_HALVES>'s operands and k order
-  const Layer L2 = layer_of(a, 2);
-  for (int job = wave; job < 16; job += CW) {
-    const int ib = (job >> 2) * 16, n = (job & 3) * 16 + li;
-    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < XS; k0 += 4) acc = mfma4(sX1[(ib + li) * fc.LX + k0 + kq], sWh[(k0 + kq) * 64 + n], acc);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int i = ib + kq * 4 + q;
-      if (i < nr) (n < 32 ? L2.a : L2.bm)[(rt0 + i) * 32 + (n & 31)] = acc[q];
-    }
-  }
-  CSTAMP(0, 4);
+  CSTAMP(LAYER - 1, 4);
 }
 
 // weight-gradient partial row of a layer for a chunk (both layers' rows live together)
@@ -1958,8 +2012,7 @@ __global__ void __launch_bounds__(RB) vc_combine(VA a) {
 }
 
 inline bool chunk_carves(const dr_vanilla_scratch* sc, int F, int Fe, int64_t* fwd1, int64_t* fwd2, int64_t* eb2, int64_t* eb1) {
-  *fwd1 = 4LL * fwd_carve(F, sc->halo_max, sc->tile_edges_max, Fe, true).total;
-  *fwd2 = 4LL * fwd_carve(F, sc->halo_max, sc->tile_edges_max, Fe, false).total;
+  *fwd1 = *fwd2 = 4LL * fwd_carve(F, sc->halo_max, sc->tile_edges_max, Fe).total;
   *eb2 = 4LL * bwd_carve(F, sc->halo_max, sc->tile_edges_max, sc->tile_tedges_max, Fe, true).total;
   *eb1 = 4LL * bwd_carve(F, sc->halo_max, sc->tile_edges_max, sc->tile_tedges_max, Fe, false).total;
   const int64_t lim = 160 * 1024;
@@ -1970,7 +2023,7 @@ inline bool chunk_carves(const dr_vanilla_scratch* sc, int F, int Fe, int64_t* f
 // weight-gradient chunks, the partial buffer holds both layers, Fe <= 4 and
 // every carve fits one workgroup's LDS
 inline bool chunk_fused(const dr_vanilla_scratch* sc, int F, int Fe) {
-  if (!sc->tile_row0 || !sc->tile_meta || !sc->relu_words || sc->tile_rows != WR || sc->part_layers != 2 || Fe > 4 || F > 64 ||
+  if (!sc->tile_row0 || !sc->tile_meta || !sc->relu_words || sc->tile_rows != WR || sc->part_layers != 2 || Fe > 4 || F > 32 ||
       sc->n_tiles != sc->n_chunks)
     return false;
   int64_t f1, f2, e2, e1;
@@ -1990,7 +2043,8 @@ int launch_chunk_fused(const VA& a, const dr_vanilla_scratch* sc, hipStream_t st
   DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&vc_eb2n1<FE>)));
   DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&vc_eb1<FE>)));
   DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&vc_nb2)));
-  hipLaunchKernelGGL(vb_gemm<GM_HALVES>, dim3(gg), dim3(RB), glds_halves, st, a, 1);
+  (void)gg;
+  (void)glds_halves;
   hipLaunchKernelGGL((vc_fwd<FE, 1>), tg, dim3(CT), (size_t)f1, st, a);
   hipLaunchKernelGGL((vc_fwd<FE, 2>), tg, dim3(CT), (size_t)f2, st, a);
   hipLaunchKernelGGL(vb_head, dim3(a.B), dim3(HT), 0, st, a);
@@ -2120,19 +2174,20 @@ extern "C" int dr_debug_carve_vanilla_tile(const int32_t* q, char* buf, int32_t 
 }
 
 extern "C" int dr_debug_carve_vanilla_chunk_fwd(const int32_t* q, char* buf, int32_t len) {
-  const FwdCarve c = fwd_carve(q[0], q[1], q[2], q[3], q[4] != 0);
+  const FwdCarve c = fwd_carve(q[0], q[1], q[2], q[3]);
   DrCarveDesc d{buf, len, 0};
+  DR_DESC_P(d, c, HS);
   DR_DESC_P(d, c, KP);
   DR_DESC_P(d, c, LA);
   DR_DESC_P(d, c, NOP);
-  DR_DESC_P(d, c, LX);
+  DR_DESC_P(d, c, hp);
+  DR_DESC(d, c, xo);
+  DR_DESC(d, c, wab);
+  DR_DESC(d, c, halo);
+  DR_DESC(d, c, rec);
   DR_DESC(d, c, a);
   DR_DESC(d, c, wn);
   DR_DESC(d, c, bn);
-  DR_DESC(d, c, wh);
-  DR_DESC(d, c, x1);
-  DR_DESC(d, c, halo);
-  DR_DESC(d, c, rec);
   DR_DESC(d, c, total);
   return d.pos;
 }

@@ -290,18 +290,15 @@ def test_vanilla_tile_and_chunk_carves(H, EM, TM, Fe):
         _check("vanilla_tile", [H, EM, TM, Fe, bwd], lambda v, bwd=bwd: {"rec": EM * RS} | ({"trec": 2 * TM} if bwd else {}))
     F = 30
     XS = r4(F)
-    for nxt in (0, 1):
-        # vc_fwd: [X | S] rows at stride KP + 4 (the node MLP's A operand), Wn^T [KP][NOP], bn [NOP],
-        # halo B rows and CSR records; after the edge phase the same region holds (layer 1)
-        # X1 rows at XS + 4 and [Wa2; Wb2]^T [XS][64]
-        def fext(v, nxt=nxt):
-            KP = XS + 32
-            return {"a": 64 * (KP + 4), "wn": KP * r16(F), "bn": r16(F), "wh": XS * 64 if nxt else 0, "x1": 64 * (XS + 4) if nxt else 0, "halo": H * 32, "rec": EM * RS}
+    # vc_fwd (both layers): own X rows (-> A in place) and halo X rows (-> B in place) at
+    # stride 36 (halo rounded up to 16-row MFMA blocks), [Wa; Wb]^T [XS][64], CSR records;
+    # after the edge phase the same space holds [X | S] rows at KP + 4, Wn^T [KP][NOP], bn
+    def fext(v):
+        KP = XS + 32
+        return {"xo": 64 * 36, "wab": XS * 64, "halo": r16(H) * 36, "rec": EM * RS, "a": 64 * (KP + 4), "wn": KP * r16(F), "bn": r16(F)}
 
-        vals, total = _check("vanilla_chunk_fwd", [F, H, EM, Fe, nxt], fext, phases=[{"halo", "rec"}, {"x1", "wh"}])
-        assert vals["x1"] == vals["halo"]  # the late region overlays the dead edge region
-        if nxt:
-            assert vals["wh"] + XS * 64 <= total
+    vals, total = _check("vanilla_chunk_fwd", [F, H, EM, Fe], fext, phases=[{"xo", "wab", "halo", "rec"}, {"a", "wn", "bn"}])
+    assert vals["a"] == 0 and vals["bn"] + r16(F) <= total
     FeS = max(Fe, 1)
     for two in (0, 1):
         # vc_eb2n1 / vc_eb1: [D | D'] rows (LDD 68), the waves' dWc shares sSh[(wave 32 + c) FeS + f]

@@ -30,8 +30,8 @@ from deeprank2_amd.store import GraphStore, pack_graphs  # noqa: E402
 from deeprank2_amd.utils.synthetic import make_dataset  # noqa: E402
 
 KERNELS = [
-    ("vc_fwd<1>", ["stage", "edge gather", "node MLP", "next [A|B]"]),
-    ("vc_fwd<2>", ["stage", "edge gather", "node MLP"]),
+    ("vc_fwd<1>", ["stage", "[A|B] MFMA", "edge gather", "node MLP"]),
+    ("vc_fwd<2>", ["stage", "[A|B] MFMA", "edge gather", "node MLP"]),
     ("vc_nb2", ["stage", "GEMM dX1|DS2 + dWn2"]),
     ("vc_eb2n1", ["stage", "edge bwd", "dW edge + dX1 GEMM", "DS1 + dWn1"]),
     ("vc_eb1", ["stage", "edge bwd", "dW edge"]),
