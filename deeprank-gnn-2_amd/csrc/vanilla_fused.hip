@@ -1102,12 +1102,13 @@ inline int rows_grid(int64_t rows, int rows_per_block) {
 }
 
 // ---- chunk-fused pipeline: tile == weight-gradient chunk == 64 rows ---------
-// With a tile plan of DR_VANILLA_CHUNK rows (and Fe <= 4), one 1024-thread
-// workgroup per chunk runs every row-local stage of its rows around the halo
-// edge work, so the node-level intermediates between them stay in LDS:
-//   vc_fwd<l>  edge gather -> S_l (LDS), node MLP X_l = relu([X | S_l] Wn^T + bn)
-//              and, layer 1, the next layer's [A2 | B2] = X1 [Wa2; Wb2]^T
-//              (vb_edge_fwd_tile + vb_gemm<GM_NODE> + vb_gemm<GM_HALVES>);
+// With a tile plan of DR_VANILLA_CHUNK rows (Fe <= 4, F <= 32), one
+// 1024-thread workgroup per chunk runs every row-local stage of its rows
+// around the halo edge work, so the node-level intermediates between them
+// stay in LDS:
+//   vc_fwd<l>  [A | B] = X [Wa; Wb]^T of its own rows and of its halo rows
+//              (MFMA), edge gather -> S_l, node MLP X_l = relu([X | S_l] Wn^T
+//              + bn) (vb_gemm<GM_HALVES> + vb_edge_fwd_tile + vb_gemm<GM_NODE>);
 //   vc_nb2     DU2 = relu'(X2) dmean, [dX1 | DS2] = DU2 Wn2, dWn2 / dbn2
 //              (vb_du + vb_gemm<GM_DXS> + vb_wgrad_mfma's Wn part);
 //   vc_eb2n1   D2, D2' from the DS2 halo, dWa2 / dWb2 / dbe2 / dWc2,
@@ -1116,7 +1117,7 @@ inline int rows_grid(int64_t rows, int rows_per_block) {
 //              vb_gemm<GM_DXS> + vb_wgrad_mfma, two layers);
 //   vc_eb1     D1, D1' from the DS1 halo, dWa1 / dWb1 / dbe1 / dWc1;
 //   vc_combine every graph's chunk partials of both layers, in chunk order.
-// 8 launches per step instead of 17.  Every GEMM takes the operands and the k
+// 7 launches per step instead of 17.  Every GEMM takes the operands and the k
 // order of the kernel it replaces, and the sums run in the same order, so the
 // outputs, slabs, head vectors and ReLU words are bit-identical to the untiled
 // pipeline; only dWc sums its rows' shares in another order (as the 16-row

@@ -72,7 +72,7 @@ class BatchHandle:
             floats = int(lib.dr_vanilla_scratch_floats(rows, n_feat, n_edge_feat))
             # the chunk-fused kernels (tiles of DR_VANILLA_CHUNK rows, Fe <= 4) keep both
             # layers' partial rows at once (dr_vanilla_scratch.part_layers)
-            chunk_fused = self.vanilla_words and self.vanilla_tile_rows == VANILLA_CHUNK and 0 <= n_edge_feat <= 4
+            chunk_fused = self.vanilla_words and self.vanilla_tile_rows == VANILLA_CHUNK and 0 <= n_edge_feat <= 4 and n_feat <= 32  # noqa: PLR2004
             part_layers = 2 if chunk_fused else 1
             part = int(lib.dr_vanilla_part_floats(n_feat, n_edge_feat)) * int(chunk_first[-1]) * part_layers
             dev = self.store.device

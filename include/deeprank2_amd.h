@@ -463,12 +463,13 @@ typedef struct dr_vanilla_scratch {
   const int32_t* tile_first;
   int32_t tile_rows;
   /* 2: part holds both layers' partial rows ([2][n_chunks][part floats], layer 1
-   * first).  With tile_rows == DR_VANILLA_CHUNK, Fe <= 4 and the tile carves
-   * within 160 KiB, dr_vanilla_graph_pass then runs the chunk-fused kernels: one
-   * workgroup per 64-row chunk runs the edge work and every row-local stage
-   * around it (node MLP, next layer's node GEMMs, node backward, weight-gradient
-   * partials) with the intermediates in LDS -- 8 launches per step instead of
-   * 17, the same results (dWc summed in another order).  0 / 1: one layer.   */
+   * first).  With tile_rows == DR_VANILLA_CHUNK, tile_meta set, Fe <= 4,
+   * F <= 32 and the tile carves within 160 KiB, dr_vanilla_graph_pass then runs
+   * the chunk-fused kernels: one workgroup per 64-row chunk runs the edge work
+   * and every row-local stage around it ([A | B] of its own and halo rows, node
+   * MLP, node backward, weight-gradient partials) with the intermediates in
+   * LDS -- 7 launches per step instead of 17, the same results (dWc summed in
+   * another order).  0 / 1: one layer.                                       */
   int32_t part_layers;
   /* the chunk-fused kernels' per-tile records [n_tiles] (required by them):
    * every offset a chunk workgroup needs, so its prologue is one record load
