@@ -555,7 +555,7 @@ __global__ void __launch_bounds__(RB) vb_edge_bwd_tile(VA a, int l) {
 }
 
 // per graph: scatter_mean -> graph MLP -> loss -> head backward (one workgroup)
-constexpr int HT = 1024;  // vb_head threads: 32 row chunks per column for the mean over ~3k-node graphs
+constexpr int HT = 1024;  // vb_head threads: 32 row chunks at a time for the mean over ~3k-node graphs
 __global__ void __launch_bounds__(HT) vb_head(VA a) {
   __shared__ float sG[64], sH[128], sDh[128], sDout[16], sRed[HT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -566,37 +566,50 @@ __global__ void __launch_bounds__(HT) vb_head(VA a) {
   const float* X2 = a.ws.base + a.L.x2 + r0 * XS;
   const float y_g = a.s.y[a.descs[b].gid];
   if (a.p.step_counter && b == 0 && tid == 0) a.p.step_counter[1] = a.p.step_counter[0];
-  {  // column sums in row chunks, combined in chunk order
-    const int CH = HT / XS, n = tid % XS, ch = tid / XS;
-    float acc = 0.f;
-    if (n < F && ch < CH) {
-      const int i0 = (N * ch) / CH, i1 = (N * (ch + 1)) / CH;
-      int i = i0;
-      // ~100 rows per thread on an atom graph: 24 rows' loads in flight (8
-      // made the mean a chain of ~12 memory round trips), summed in row order
-      for (; i + 24 <= i1; i += 24) {
-        float v[24];
+  {  // the mean: column sums over the graph's DR_VANILLA_CHUNK-row chunks (rows
+     // in order within a chunk), then the chunks in order.  The chunk-fused
+     // forward leaves its tiles' sums in part_mean; otherwise summed here from X2.
+    constexpr int CR = DR_VANILLA_CHUNK;
+    const int nch = (N + CR - 1) / CR;
+    float t = 0.f;  // thread tid < F: the ordered sum over the chunks
+    if (a.ws.part_mean) {
+      if (tid < F) {
+        const float* pm = a.ws.part_mean + (int64_t)a.ws.chunk_first[b] * 32 + tid;
+        int ch = 0;
+        for (; ch + 8 <= nch; ch += 8) {  // 8 loads in flight, summed in chunk order
+          float v[8];
 #pragma unroll
-        for (int u = 0; u < 24; ++u) v[u] = X2[(int64_t)(i + u) * XS + n];
+          for (int u = 0; u < 8; ++u) v[u] = pm[(int64_t)(ch + u) * 32];
 #pragma unroll
-        for (int u = 0; u < 24; ++u) acc += v[u];
+          for (int u = 0; u < 8; ++u) t += v[u];
+        }
+        for (; ch < nch; ++ch) t += pm[(int64_t)ch * 32];
       }
-      for (; i + 8 <= i1; i += 8) {  // 8 rows' loads in flight, summed in row order
-        float v[8];
+    } else {
+      const int n = tid & 31;
+      for (int c0 = 0; c0 < nch; c0 += HT / 32) {
+        const int ch = c0 + tid / 32;
+        float acc = 0.f;
+        if (ch < nch && n < F) {
+          const int i1 = min(N, (ch + 1) * CR);
+          int i = ch * CR;
+          for (; i + 16 <= i1; i += 16) {  // 16 rows' loads in flight, summed in row order
+            float v[16];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = X2[(int64_t)(i + u) * XS + n];
+            for (int u = 0; u < 16; ++u) v[u] = X2[(int64_t)(i + u) * XS + n];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) acc += v[u];
+            for (int u = 0; u < 16; ++u) acc += v[u];
+          }
+          for (; i < i1; ++i) acc += X2[(int64_t)i * XS + n];
+        }
+        sRed[tid] = acc;
+        __syncthreads();
+        if (tid < F)
+          for (int q = 0; q < HT / 32 && c0 + q < nch; ++q) t += sRed[q * 32 + tid];
+        __syncthreads();
       }
-      for (; i < i1; ++i) acc += X2[(int64_t)i * XS + n];
     }
-    sRed[tid] = acc;
-    __syncthreads();
-    if (tid < F) {
-      float t = 0.f;
-      for (int q = 0; q < CH; ++q) t += sRed[q * XS + tid];
-      sG[tid] = t / (float)N;
-    }
+    if (tid < F) sG[tid] = t / (float)N;
   }
   __syncthreads();
   if (tid < 128) {
@@ -1337,7 +1350,7 @@ __host__ __device__ inline BwdCarve bwd_carve(int F, int hmax, int emax, int tma
 }
 
 struct FwdCarve {
-  int HS, KP, LA, NOP, hp, xo, wab, halo, rec, a, wn, bn, total;
+  int HS, KP, LA, NOP, hp, xo, wab, halo, rec, a, wn, bn, x2, total;
 };
 // Edge phase: the halo's X rows (then, in place, their B = X Wb^T), the tile's
 // own X rows (then, in place, A = X Wa^T), [Wa; Wb]^T and the CSR records.
@@ -1361,7 +1374,8 @@ __host__ __device__ inline FwdCarve fwd_carve(int F, int hmax, int emax, int Fe)
   c.a = 0;                          // after the edges: [X | S] rows (node MLP A operand)
   c.wn = WR * c.LA;                 // Wn^T [KP][NOP]
   c.bn = c.wn + c.KP * c.NOP;       // bn, zero past F
-  const int late = c.bn + c.NOP;
+  c.x2 = c.bn + c.NOP;              // layer 2: the output rows [64][33] for the tile's column sums
+  const int late = c.x2 + WR * 33;
   c.total = edge > late ? edge : late;
   return c;
 }
@@ -1573,7 +1587,17 @@ __global__ void __launch_bounds__(CT, 8) vc_fwd(VA a) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int i = ib + kq * 4 + q;
-      if (i < nr && n < F) L.xout[(rt0 + i) * XS + n] = relu_keepnan(acc[q] + bn);
+      const float v = relu_keepnan(acc[q] + bn);
+      if (i < nr && n < F) L.xout[(rt0 + i) * XS + n] = v;
+      if (LAYER == 2 && n < F) lds[fc.x2 + i * 33 + n] = v;
+    }
+  }
+  if (LAYER == 2 && a.ws.part_mean) {  // the tile's column sums for the mean (vb_head's order)
+    __syncthreads();
+    if (tid < F) {
+      float t = 0.f;
+      for (int i = 0; i < nr; ++i) t += lds[fc.x2 + i * 33 + tid];
+      a.ws.part_mean[(int64_t)blockIdx.x * 32 + tid] = t;
     }
   }
   CSTAMP(LAYER - 1, 4);
@@ -2189,6 +2213,7 @@ extern "C" int dr_debug_carve_vanilla_chunk_fwd(const int32_t* q, char* buf, int
   DR_DESC(d, c, a);
   DR_DESC(d, c, wn);
   DR_DESC(d, c, bn);
+  DR_DESC(d, c, x2);
   DR_DESC(d, c, total);
   return d.pos;
 }

@@ -119,7 +119,7 @@ class VanillaScratchC(ctypes.Structure):
     _fields_ = [("base", VP), ("row0", VP), ("row_slot", VP), ("n_rows", ctypes.c_int64), ("chunk_first", VP), ("chunk_slot", VP), ("n_chunks", ctypes.c_int32), ("pad0", ctypes.c_int32), ("part", VP), ("edge0", VP), ("relu_words", VP),
                 ("tile_row0", VP), ("halo_off", VP), ("halo_ids", VP), ("lcol_off", VP), ("lcol", VP), ("ltcol_off", VP), ("ltcol", VP),
                 ("n_tiles", ctypes.c_int32), ("halo_max", ctypes.c_int32), ("tile_edges_max", ctypes.c_int32), ("tile_tedges_max", ctypes.c_int32),
-                ("tile_wc", VP), ("tile_first", VP), ("tile_rows", ctypes.c_int32), ("part_layers", ctypes.c_int32), ("tile_meta", VP)]
+                ("tile_wc", VP), ("tile_first", VP), ("tile_rows", ctypes.c_int32), ("part_layers", ctypes.c_int32), ("tile_meta", VP), ("part_mean", VP)]
 
 
 class NcPlanC(ctypes.Structure):

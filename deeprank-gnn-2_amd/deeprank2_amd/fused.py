@@ -110,8 +110,9 @@ class BatchHandle:
                             for k, name in enumerate(VTILE_DTYPE.names[:-1]):
                                 m[name] = [row[k] for row in meta]
                             mt = torch.from_numpy(m.view(np.uint8)).to(dev)
-                            keep.append(mt)
-                            c.tile_meta = mt.data_ptr()
+                            pm = torch.empty(len(meta) * 32, dtype=torch.float32, device=dev)  # per-tile column sums of X2
+                            keep += [mt, pm]
+                            c.tile_meta, c.part_mean = mt.data_ptr(), pm.data_ptr()
                         if VANILLA_CHUNK % tr == 0 and 0 < n_edge_feat <= 4 and not chunk_fused:  # the 16/32-row tiled kernels; tiles never straddle a weight-gradient chunk
                             tfirst = torch.from_numpy(np.concatenate([[0], np.cumsum((n + tr - 1) // tr)]).astype(np.int32)).to(dev)
                             twc = torch.empty(n_tiles * 32 * max(1, n_edge_feat), dtype=torch.float32, device=dev)

@@ -475,6 +475,10 @@ typedef struct dr_vanilla_scratch {
    * every offset a chunk workgroup needs, so its prologue is one record load
    * instead of a chain of dependent index loads                             */
   const struct dr_vanilla_tile* tile_meta;
+  /* optional [n_tiles][32]: the chunk-fused forward's per-tile column sums of
+   * X2 (the mean's DR_VANILLA_CHUNK-row partials, rows in order); NULL: the
+   * head sums the same chunks from X2 itself                                 */
+  float* part_mean;
 } dr_vanilla_scratch;
 #define DR_VANILLA_CHUNK 64
 

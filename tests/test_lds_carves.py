@@ -295,10 +295,10 @@ def test_vanilla_tile_and_chunk_carves(H, EM, TM, Fe):
     # after the edge phase the same space holds [X | S] rows at KP + 4, Wn^T [KP][NOP], bn
     def fext(v):
         KP = XS + 32
-        return {"xo": 64 * 36, "wab": XS * 64, "halo": r16(H) * 36, "rec": EM * RS, "a": 64 * (KP + 4), "wn": KP * r16(F), "bn": r16(F)}
+        return {"xo": 64 * 36, "wab": XS * 64, "halo": r16(H) * 36, "rec": EM * RS, "a": 64 * (KP + 4), "wn": KP * r16(F), "bn": r16(F), "x2": 64 * 33}
 
-    vals, total = _check("vanilla_chunk_fwd", [F, H, EM, Fe], fext, phases=[{"xo", "wab", "halo", "rec"}, {"a", "wn", "bn"}])
-    assert vals["a"] == 0 and vals["bn"] + r16(F) <= total
+    vals, total = _check("vanilla_chunk_fwd", [F, H, EM, Fe], fext, phases=[{"xo", "wab", "halo", "rec"}, {"a", "wn", "bn", "x2"}])
+    assert vals["a"] == 0 and vals["x2"] + 64 * 33 <= total
     FeS = max(Fe, 1)
     for two in (0, 1):
         # vc_eb2n1 / vc_eb1: [D | D'] rows (LDD 68), the waves' dWc shares sSh[(wave 32 + c) FeS + f]
