@@ -1267,6 +1267,7 @@ struct MapV {
       const int p = threadIdx.x + k * CT;
       if (p < n) dst[p] = v[k];
     }
+    #pragma unroll 1
     for (int p = threadIdx.x + KPT * CT; p < n; p += CT) {
       const int o = off(p);
       dst[p] = w.f32(o >= 0 ? o * 4 : OOB);
@@ -1285,11 +1286,29 @@ __device__ __forceinline__ MapV<Off> map_load(const Buf& w, int n, Off off) {
 // then store
 struct HaloV {
   Buf ids, rows;
+  const float* g32;
   int H;
   P2<int> id;
   P2<float4> v;
-  __device__ __forceinline__ HaloV(const int* ids_, int H_, const float* g32, int ng)
-      : ids(ids_, (int64_t)H_ * 4), rows(g32, (int64_t)ng * 128), H(H_) {}
+  __device__ __forceinline__ HaloV(const int* ids_, int H_, const float* g32_, int ng)
+      : ids(ids_, (int64_t)H_ * 4), rows(g32_, (int64_t)ng * 128), g32(g32_), H(H_) {}
+  // the rows straight into LDS (global_load_lds: no registers; the caller
+  // waits vmcnt(0) before its barrier)
+  __device__ __forceinline__ void dma(float* dst) const {
+    const int wb = __builtin_amdgcn_readfirstlane(threadIdx.x & ~63);
+    uint4* d4 = reinterpret_cast<uint4*>(dst);
+#pragma unroll
+    for (int k = 0; k < KPT; ++k) {
+      const int p = threadIdx.x + k * CT;
+      if (p < H * 8)
+        __builtin_amdgcn_global_load_lds(DRK_AS1(g32 + (int64_t)id[k] * 32 + (p & 7) * 4), DRK_AS3(d4 + wb + k * CT), 16, 0, 0);
+    }
+    for (int base = wb + KPT * CT; base < H * 8; base += CT) {
+      const int p = base + (threadIdx.x & 63);
+      if (p < H * 8)
+        __builtin_amdgcn_global_load_lds(DRK_AS1(g32 + (int64_t)ids.u32((p >> 3) * 4) * 32 + (p & 7) * 4), DRK_AS3(d4 + base), 16, 0, 0);
+    }
+  }
   __device__ __forceinline__ void load_ids() {
 #pragma unroll
     for (int k = 0; k < KPT; ++k) id[k] = (int)ids.u32(((threadIdx.x + k * CT) >> 3) * 4);
@@ -1307,16 +1326,21 @@ struct HaloV {
       const int p = threadIdx.x + k * CT;
       if (p < H * 8) *reinterpret_cast<float4*>(dst + p * 4) = v[k];
     }
+    #pragma unroll 1
     for (int p = threadIdx.x + KPT * CT; p < H * 8; p += CT)
       *reinterpret_cast<float4*>(dst + p * 4) = rows.f4((int)ids.u32((p >> 3) * 4) * 128 + (p & 7) * 16);
   }
 };
 
 struct BwdCarve {
-  int LDD, LU, NOP3, d, x1, dx, w3, du, w1, sh, x0, s1, halo, rec, trec, total;
+  int LDD, LU, NOP3, d, w3, du, sh, halo, trec, x1, dx, x0, s1, w1, total;
 };
-// two_layers: vc_eb2n1 (layer 2's edges + layer 1's node backward); else vc_eb1
+// [D | D'] rows, (vc_eb2n1) [Wa2; Wb2] and DU1, the waves' dWc shares, then
+// the edge phase's halo dS rows and transposed records {column, word} (the
+// CSR records stay in registers).  After the edges the same space holds
+// (vc_eb2n1) X1 / dX1 / X0 / S1 rows and Wn1[:, F:]^T, (vc_eb1) X0 rows.
 __host__ __device__ inline BwdCarve bwd_carve(int F, int hmax, int emax, int tmax, int Fe, bool two_layers) {
+  (void)emax;
   BwdCarve c;
   const int XS = r4(F), FeS = Fe > 0 ? Fe : 1;
   c.LDD = 64 + 4;  // [D | D'] rows
@@ -1324,27 +1348,19 @@ __host__ __device__ inline BwdCarve bwd_carve(int F, int hmax, int emax, int tma
   c.NOP3 = r16(F);
   int o = 0;
   c.d = o;  o += WR * c.LDD;
-  c.x1 = o; o += two_layers ? WR * XS : 0;           // X1 rows (dWa2 / dWb2 B operand, relu'(X1))
-  c.dx = o; o += two_layers ? WR * XS : 0;           // dX1 partial (DU2 Wn2[:, :F])
-  c.w3 = o; o += two_layers ? 64 * c.NOP3 : 0;        // [Wa2; Wb2] [64][NOP3]
-  c.du = o; o += two_layers ? WR * c.LU : 0;          // DU1
-  c.w1 = o; o += two_layers ? XS * 32 : 0;            // Wn1[:, F:]^T... as [XS][32]
-  c.sh = o; o += CW * 32 * FeS;                       // the waves' dWc shares
-  const int edge = hmax * 32 + emax * (Fe <= 3 ? 4 : 8) + 2 * tmax;
-  const int late = WR * XS + WR * 32;                 // X0 / S1 rows, staged after the edge phase
-  c.x0 = o;            // vc_eb1: X0 rows beside the edge region; vc_eb2n1: inside it, after the edges
-  if (!two_layers) o += WR * XS;
+  c.w3 = o; o += two_layers ? 64 * c.NOP3 : 0;   // [Wa2; Wb2] [64][NOP3]
+  c.du = o; o += two_layers ? WR * c.LU : 0;     // DU1
+  c.sh = o; o += CW * 32 * FeS;                  // the waves' dWc shares
   c.halo = o;
-  c.rec = c.halo + hmax * 32;
-  c.trec = c.rec + emax * (Fe <= 3 ? 4 : 8);
-  if (two_layers) {
-    c.x0 = c.halo;
-    c.s1 = c.halo + WR * XS;
-    o += edge > late ? edge : late;
-  } else {
-    c.s1 = 0;
-    o += edge;
-  }
+  c.trec = o + hmax * 32;
+  const int edge = hmax * 32 + 2 * tmax;
+  c.x0 = o;
+  c.x1 = c.x0 + WR * XS;  // vc_eb2n1 only, as the rest (vc_eb1: empty, at the end of X0)
+  c.dx = two_layers ? c.x1 + WR * XS : c.x1;
+  c.s1 = two_layers ? c.dx + WR * XS : c.x1;
+  c.w1 = two_layers ? c.s1 + WR * 32 : c.x1;
+  const int late = two_layers ? 3 * WR * XS + WR * 32 + XS * 32 : WR * XS;
+  o += edge > late ? edge : late;
   c.total = o;
   return c;
 }
@@ -1499,11 +1515,13 @@ __global__ void __launch_bounds__(CT, 8) vc_fwd(VA a) {
     const int p = tid + k * CT;
     if (p < H * 8) *reinterpret_cast<float4*>(sB + (p >> 3) * HS + (p & 7) * 4) = mask4(hx[k], (p & 7) * 4);
   }
+  #pragma unroll 1
   for (int p = tid + KPT * CT; p < H * 8; p += CT) {
     const int q4 = (p & 7) * 4;
     const float4 v = xgv.f4(q4 < XS ? ((int)idv.u32((p >> 3) * 4) * XS + q4) * 4 : OOB);
     *reinterpret_cast<float4*>(sB + (p >> 3) * HS + q4) = mask4(v, q4);
   }
+  #pragma unroll 1
   for (int p = tid + KPT * CT; p < ne; p += CT) put_rec<FE>(sR, p, lc[p], ea + (int64_t)p * FeS);
   __syncthreads();
   CSTAMP(LAYER - 1, 1);
@@ -1707,9 +1725,12 @@ __global__ void __launch_bounds__(CT) vc_nb2(VA a) {
 }
 
 // A chunk's D_i = relu'-count x dS_i, D'_i (transposed) and its rows' dWc
-// shares from the halo of dS rows (vb_edge_bwd_tile's sums and order).  The
-// caller interleaves: load1 (ids, records, per-row values), its own loads,
-// load2 (halo rows, transposed words), store, its own stores, a barrier, run.
+// shares from the halo of dS rows (vb_edge_bwd_tile's sums and order).  A
+// row's CSR records {word, ea} go straight to registers (lane c of its row
+// group holds edge c of the row; ds_bpermute hands edge u to the group), so
+// only the halo rows and the transposed records take LDS.  The caller
+// interleaves: load1 (ids, row bounds), its own loads, load2 (halo rows,
+// records), load3 (transposed words), store, its stores, a barrier, run.
 template <int FE>
 struct EdgeBwd {
   static constexpr int FA = FE > 0 ? FE : 1, FeS = FA;
@@ -1720,11 +1741,12 @@ struct EdgeBwd {
   const int* teid;
   HaloV halo;
   Buf wv, eav, ltv, tev, wgv, rpv, trpv, dsv;
-  P2<uint32_t> rw, tc, tw;
+  P2<uint32_t> tc, tw;
   P2<int> te;
-  P2<float4> rv;
   P2<int> rb, re, qb, qe;
   P2<float> dsi;
+  P2<uint32_t> rw;  // row k's edge c (the first 32 of the row)
+  P2<float4> rv;
 
   __device__ __forceinline__ EdgeBwd(const VA& a, const dr_vanilla_tile& mm, int l, const float* ds)
       : m(mm),
@@ -1742,6 +1764,16 @@ struct EdgeBwd {
         trpv(a.s.t_rowptr + mm.rp0 + mm.i0, (int64_t)(mm.nr + 1) * 4),
         dsv(ds + mm.rt0 * 32, (int64_t)mm.nr * 128) {}
 
+  // edge p's (tile-local CSR slot) record, or zeros when !ok
+  __device__ __forceinline__ void rec_at(int p, bool ok, uint32_t& w, float4& v) const {
+    const int o = ok ? p * 4 : OOB;
+    w = wv.u32(o);
+    const int oe = ok ? p * FeS * 4 : OOB;
+    v = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int f = 0; f < FE; ++f) f4at(v, f) = eav.f32(oe + 4 * f);
+  }
+
   __device__ __forceinline__ void load1() {
     const int tid = threadIdx.x, c = tid & 31, g = tid >> 5;
     halo.load_ids();
@@ -1757,41 +1789,34 @@ struct EdgeBwd {
 #pragma unroll
     for (int k = 0; k < KPT; ++k) {
       const int p = tid + k * CT;
-      rw[k] = wv.u32(p * 4);
-      rv[k] = ea_v<FE>(eav, p);
       tc[k] = ltv.u16(p * 2);
       te[k] = (int)tev.u32(p * 4);
     }
   }
-  __device__ __forceinline__ void load2() {
-    halo.load_rows();
+  __device__ __forceinline__ void load2(float* sDS) {
+    const int c = threadIdx.x & 31;
+    halo.dma(sDS);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) rec_at(rb[k] - m.e0 + c, c < re[k] - rb[k], rw[k], rv[k]);
+  }
+  __device__ __forceinline__ void load3() {
 #pragma unroll
     for (int k = 0; k < KPT; ++k) tw[k] = wgv.u32(threadIdx.x + k * CT < m.nq ? te[k] * 4 : OOB);
   }
-  // load1's records (store1, before the caller's own stores), then load2's
-  // halo rows and transposed records (store2, last)
-  __device__ __forceinline__ void store1(float* sR, float* sD, int LDD) const {
+  __device__ __forceinline__ void store(uint2* sTR, float* sD, int LDD) const {
     const int tid = threadIdx.x;
-#pragma unroll
-    for (int k = 0; k < KPT; ++k) {
-      const int p = tid + k * CT;
-      if (p < m.ne) put_rec_v<FE>(sR, p, rw[k], rv[k]);
-    }
+    #pragma unroll 1
     for (int p = tid; p < (WR - m.nr) * 64; p += CT) sD[(m.nr + (p >> 6)) * LDD + (p & 63)] = 0.f;
-  }
-  __device__ __forceinline__ void store2(float* sDS, float* sR, uint2* sTR) const {
-    const int tid = threadIdx.x;
-    halo.store(sDS);
 #pragma unroll
     for (int k = 0; k < KPT; ++k) {
       const int p = tid + k * CT;
       if (p < m.nq) sTR[p] = make_uint2(tc[k], tw[k]);
     }
-    for (int p = tid + KPT * CT; p < m.ne; p += CT) put_rec<FE>(sR, p, words[m.e0 + p], ea + (int64_t)p * FeS);
+    #pragma unroll 1
     for (int p = tid + KPT * CT; p < m.nq; p += CT) sTR[p] = make_uint2(lt[p], words[teid[p]]);
   }
-  __device__ __forceinline__ void run(float* sD, int LDD, const float* sDS, const float* sR, const uint2* sTR, float* sSh) const {
-    const int tid = threadIdx.x, c = tid & 31, g = tid >> 5;
+  __device__ __forceinline__ void run(float* sD, int LDD, const float* sDS, const uint2* sTR, float* sSh) const {
+    const int tid = threadIdx.x, c = tid & 31, g = tid >> 5, hs = tid & 32;
     float wsum[FA];
 #pragma unroll
     for (int f = 0; f < FA; ++f) wsum[f] = 0.f;
@@ -1803,27 +1828,25 @@ struct EdgeBwd {
       float eap[FA];
 #pragma unroll
       for (int f = 0; f < FA; ++f) eap[f] = 0.f;
-      const int ee = re[k] - m.e0;
-      int e = rb[k] - m.e0;
-      for (; e + 8 <= ee; e += 8) {
-        uint32_t wv[8];
-        float ev[8][FA];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) wv[u] = get_rec<FE>(sR, e + u, ev[u]);
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const float bit = edge_bit(wv[u], c);
-          cnt += bit;
-#pragma unroll
-          for (int f = 0; f < FE; ++f) eap[f] = fmaf(bit, ev[u][f], eap[f]);
-        }
-      }
-      for (; e < ee; ++e) {
+      const int deg = re[k] - rb[k];
+      uint32_t w_r = rw[k];
+      float4 v_r = rv[k];
+      // the row's edges in order, 32 at a time from the lanes of the row group
+      auto edge = [&](int u) {
+        const int src = (hs + u) << 2;
+        const uint32_t w = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)w_r);
         float ev[FA];
-        const float bit = edge_bit(get_rec<FE>(sR, e, ev), c);
+#pragma unroll
+        for (int f = 0; f < FE; ++f) ev[f] = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(f4at(v_r, f))));
+        const float bit = edge_bit(w, c);
         cnt += bit;
 #pragma unroll
         for (int f = 0; f < FE; ++f) eap[f] = fmaf(bit, ev[f], eap[f]);
+      };
+      for (int base = 0; base < deg; base += 32) {
+        if (base > 0) rec_at(rb[k] - m.e0 + base + c, base + c < deg, w_r, v_r);  // degree > 32
+        const int n = min(32, deg - base);
+        for (int u = 0; u < n; ++u) edge(u);
       }
       sD[li * LDD + c] = cnt != 0.f ? dsi[k] * cnt : 0.f;
 #pragma unroll
@@ -1831,15 +1854,15 @@ struct EdgeBwd {
       float acc = 0.f;
       const int qe_ = qe[k] - m.q0;
       int q = qb[k] - m.q0;
-      for (; q + 8 <= qe_; q += 8) {
-        uint2 tr[8];
+      for (; q + 4 <= qe_; q += 4) {
+        uint2 tr[4];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) tr[u] = sTR[q + u];
-        float dv[8];
+        for (int u = 0; u < 4; ++u) tr[u] = sTR[q + u];
+        float dv[4];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) dv[u] = sDS[tr[u].x * 32 + c];
+        for (int u = 0; u < 4; ++u) dv[u] = sDS[tr[u].x * 32 + c];
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
+        for (int u = 0; u < 4; ++u)
           if ((tr[u].y >> c) & 1u) acc += dv[u];
       }
       for (; q < qe_; ++q) {
@@ -1897,7 +1920,7 @@ __device__ __forceinline__ void edge_wgrad(const VA& a, float* out, const float*
 }
 
 template <int FE>
-__global__ void __launch_bounds__(CT) vc_eb2n1(VA a) {
+__global__ void __launch_bounds__(CT, 8) vc_eb2n1(VA a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int F = a.F, XS = a.XS, KE = a.KE, KN = a.KN;
   const int t = blockIdx.x, tid = threadIdx.x;
@@ -1907,18 +1930,12 @@ __global__ void __launch_bounds__(CT) vc_eb2n1(VA a) {
   const int nr = m.nr;
   const BwdCarve bc = bwd_carve(F, a.ws.halo_max, a.ws.tile_edges_max, a.ws.tile_tedges_max, FE, true);
   float* sD = lds + bc.d;
-  float* sX1 = lds + bc.x1;
-  float* sDX = lds + bc.dx;
   float* sW3 = lds + bc.w3;
   float* sDU = lds + bc.du;
-  float* sW1 = lds + bc.w1;
   float* sSh = lds + bc.sh;
   float* ws = a.ws.base;
   EdgeBwd<FE> eb(a, m, 2, ws + a.L.ds);
   eb.load1();
-  RowsV x1, dx;
-  x1.load(ws + a.L.x1 + rt0 * XS, XS, nr, 0);
-  dx.load(ws + a.L.dx1 + rt0 * XS, XS, nr, 0);
   const int NOP3 = bc.NOP3;
   const Buf w3b(a.w.we2, (int64_t)32 * KE * 4);
   auto w3_off = [&](int p) -> int {  // vb_gemm<GM_DX1>'s W staging
@@ -1926,31 +1943,44 @@ __global__ void __launch_bounds__(CT) vc_eb2n1(VA a) {
     return n < F ? (k & 31) * KE + (k < 32 ? 0 : F) + n : -1;
   };
   const auto w3 = map_load(w3b, 64 * NOP3, w3_off);
+  eb.load2(lds + bc.halo);
+  eb.load3();
+  w3.store(sW3, w3b, 64 * NOP3, w3_off);
+  eb.store(reinterpret_cast<uint2*>(lds + bc.trec), sD, bc.LDD);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the halo DMA
+  __syncthreads();
+  CSTAMP(3, 1);
+  eb.run(sD, bc.LDD, lds + bc.halo, reinterpret_cast<const uint2*>(lds + bc.trec), sSh);
+  __syncthreads();
+  CSTAMP(3, 2);
+  // X1 / dX1 / X0 / S1 rows (DMA) and Wn1's DS columns into the dead edge space
+  float* sX1 = lds + bc.x1;
+  float* sDX = lds + bc.dx;
+  float* sX0 = lds + bc.x0;
+  float* sS1 = lds + bc.s1;
+  float* sW1 = lds + bc.w1;
+  dma_x4<CT>(sX1, ws + a.L.x1 + rt0 * XS, nr * XS / 4);
+  dma_x4<CT>(sDX, ws + a.L.dx1 + rt0 * XS, nr * XS / 4);
+  dma_x4<CT>(sX0, a.s.x + m.xrow * XS, nr * XS / 4);
+  dma_x4<CT>(sS1, ws + a.L.s1 + rt0 * 32, nr * 8);
   const Buf w1b(a.w.wn1, (int64_t)F * KN * 4);
   auto w1_off = [&](int p) -> int {  // vb_gemm<GM_DXS>'s W staging (Wn1), the DS columns
     const int k = p >> 5, n = p & 31;
     return k < F ? k * KN + F + n : -1;
   };
   const auto w1 = map_load(w1b, XS * 32, w1_off);
-  eb.load2();
-  eb.store1(lds + bc.rec, sD, bc.LDD);
-  x1.store(sX1, XS);
-  dx.store(sDX, XS);
-  w3.store(sW3, w3b, 64 * NOP3, w3_off);
-  w1.store(sW1, w1b, XS * 32, w1_off);
-  eb.store2(lds + bc.halo, lds + bc.rec, reinterpret_cast<uint2*>(lds + bc.trec));
-  __syncthreads();
-  CSTAMP(3, 1);
-  eb.run(sD, bc.LDD, lds + bc.halo, lds + bc.rec, reinterpret_cast<const uint2*>(lds + bc.trec), sSh);
-  __syncthreads();
-  CSTAMP(3, 2);
-  // X0 / S1 rows into the dead edge region, asynchronously (needed after the next barrier)
-  float* sX0 = lds + bc.x0;
-  float* sS1 = lds + bc.s1;
-  dma_x4<CT>(sX0, a.s.x + m.xrow * XS, nr * XS / 4);
-  dma_x4<CT>(sS1, ws + a.L.s1 + rt0 * 32, nr * 8);
-  for (int p = tid; p < (WR - nr) * XS; p += CT) sX0[nr * XS + p] = 0.f;
+  #pragma unroll 1
+  for (int p = tid; p < (WR - nr) * XS; p += CT) {
+    sX1[nr * XS + p] = 0.f;
+    sDX[nr * XS + p] = 0.f;
+    sX0[nr * XS + p] = 0.f;
+  }
+  #pragma unroll 1
   for (int p = tid; p < (WR - nr) * 32; p += CT) sS1[nr * 32 + p] = 0.f;
+  w1.store(sW1, w1b, XS * 32, w1_off);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  CSTAMP(3, 3);
   edge_wgrad<FE>(a, part_row(a, 2, t), sD, bc.LDD, sX1, sSh);
   // dX1 = dX1 + [D | D'] [Wa2; Wb2] (vb_gemm<GM_DX1>), then DU1 = relu'(X1) dX1 (vb_du)
   const int lane = tid & 63, wave = tid >> 6, li = lane & 15, kq = lane >> 4;
@@ -1969,9 +1999,8 @@ __global__ void __launch_bounds__(CT) vc_eb2n1(VA a) {
       }
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  CSTAMP(3, 3);
+  CSTAMP(3, 4);
   // DS1 = DU1 Wn1[:, F:] (vb_gemm<GM_DXS> layer 1) and layer 1's dWn / dbn
   for (int job = wave; job < 8; job += CW) {
     const int ib = (job >> 1) * 16, n = (job & 1) * 16 + li;
@@ -1984,32 +2013,36 @@ __global__ void __launch_bounds__(CT) vc_eb2n1(VA a) {
     }
   }
   node_wgrad<CT>(a, part_row(a, 1, t), sDU, bc.LU, sX0, sS1, 8);
-  CSTAMP(3, 4);
+  CSTAMP(3, 5);
 }
 
 template <int FE>
-__global__ void __launch_bounds__(CT) vc_eb1(VA a) {
+__global__ void __launch_bounds__(CT, 8) vc_eb1(VA a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int F = a.F, XS = a.XS;
-  const int t = blockIdx.x;
+  const int t = blockIdx.x, tid = threadIdx.x;
   CSTAMP(4, 0);
   const dr_vanilla_tile m = a.ws.tile_meta[t];
+  const int nr = m.nr;
   const BwdCarve bc = bwd_carve(F, a.ws.halo_max, a.ws.tile_edges_max, a.ws.tile_tedges_max, FE, false);
   float* sD = lds + bc.d;
-  float* sX0 = lds + bc.x0;
   EdgeBwd<FE> eb(a, m, 1, a.ws.base + a.L.d);
   eb.load1();
-  RowsV x0;
-  x0.load(a.s.x + m.xrow * XS, XS, m.nr, 0);
-  eb.load2();
-  eb.store1(lds + bc.rec, sD, bc.LDD);
-  x0.store(sX0, XS);
-  eb.store2(lds + bc.halo, lds + bc.rec, reinterpret_cast<uint2*>(lds + bc.trec));
+  eb.load2(lds + bc.halo);
+  eb.load3();
+  eb.store(reinterpret_cast<uint2*>(lds + bc.trec), sD, bc.LDD);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the halo DMA
   __syncthreads();
   CSTAMP(4, 1);
-  eb.run(sD, bc.LDD, lds + bc.halo, lds + bc.rec, reinterpret_cast<const uint2*>(lds + bc.trec), lds + bc.sh);
+  eb.run(sD, bc.LDD, lds + bc.halo, reinterpret_cast<const uint2*>(lds + bc.trec), lds + bc.sh);
   __syncthreads();
   CSTAMP(4, 2);
+  float* sX0 = lds + bc.x0;  // X0 rows into the dead edge space
+  dma_x4<CT>(sX0, a.s.x + m.xrow * XS, nr * XS / 4);
+  #pragma unroll 1
+  for (int p = tid; p < (WR - nr) * XS; p += CT) sX0[nr * XS + p] = 0.f;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   edge_wgrad<FE>(a, part_row(a, 1, t), sD, bc.LDD, sX0, lds + bc.sh);
   CSTAMP(4, 3);
 }
@@ -2148,6 +2181,7 @@ extern "C" int dr_vanilla_graph_pass(const dr_graph_store* store, const dr_graph
   const size_t lds_wg = (size_t)dr_vanilla_lds_bytes(a.F, a.Fe, pass->out_dim);
   const int gg = rows_grid(R, GT) < 1024 ? rows_grid(R, GT) : 1024;
   auto glds = [&](int mode) { return (size_t)4 * gemm_lds_floats(mode, a.F); };
+  if (!chunk_fused(scratch, a.F, a.Fe)) a.ws.part_mean = nullptr;  // (only the chunk-fused forward writes it)
   if (chunk_fused(scratch, a.F, a.Fe)) {
     switch (a.Fe) {
       case 0: return launch_chunk_fused<0>(a, scratch, st, gg, glds(GM_HALVES));
@@ -2225,17 +2259,16 @@ extern "C" int dr_debug_carve_vanilla_chunk_bwd(const int32_t* q, char* buf, int
   DR_DESC_P(d, c, LU);
   DR_DESC_P(d, c, NOP3);
   DR_DESC(d, c, d);
-  DR_DESC(d, c, x1);
-  DR_DESC(d, c, dx);
   DR_DESC(d, c, w3);
   DR_DESC(d, c, du);
-  DR_DESC(d, c, w1);
   DR_DESC(d, c, sh);
-  DR_DESC(d, c, x0);
-  DR_DESC(d, c, s1);
   DR_DESC(d, c, halo);
-  DR_DESC(d, c, rec);
   DR_DESC(d, c, trec);
+  DR_DESC(d, c, x0);
+  DR_DESC(d, c, x1);
+  DR_DESC(d, c, dx);
+  DR_DESC(d, c, s1);
+  DR_DESC(d, c, w1);
   DR_DESC(d, c, total);
   return d.pos;
 }

@@ -301,20 +301,18 @@ def test_vanilla_tile_and_chunk_carves(H, EM, TM, Fe):
     assert vals["a"] == 0 and vals["x2"] + 64 * 33 <= total
     FeS = max(Fe, 1)
     for two in (0, 1):
-        # vc_eb2n1 / vc_eb1: [D | D'] rows (LDD 68), the waves' dWc shares sSh[(wave 32 + c) FeS + f]
-        # (chunk_edge_bwd), halo dS rows, CSR {word, ea} and transposed {col, word} records; vc_eb2n1
-        # also X1 / dX1 rows, [Wa2; Wb2] [64][NOP3], DU1 at XS + 4, Wn1 [XS][32], and X0 / S1 rows
-        # placed in the edge region once the edges are done
+        # vc_eb2n1 / vc_eb1: [D | D'] rows (LDD 68), (vc_eb2n1) [Wa2; Wb2] [64][NOP3] and DU1 at
+        # XS + 4, the waves' dWc shares sSh[(wave 32 + c) FeS + f], halo dS rows and transposed
+        # {col, word} records (the CSR records stay in registers); after the edge phase the same
+        # space holds X0 rows and (vc_eb2n1) X1 / dX1 / S1 rows and Wn1[:, F:]^T [XS][32]
         def bext(v, two=two):
-            e = {"d": 64 * 68, "sh": 16 * 32 * FeS, "halo": H * 32, "rec": EM * RS, "trec": 2 * TM}
+            e = {"d": 64 * 68, "sh": 16 * 32 * FeS, "halo": H * 32, "trec": 2 * TM, "x0": 64 * XS}
             if two:
-                e |= {"x1": 64 * XS, "dx": 64 * XS, "w3": 64 * r16(F), "du": 64 * (XS + 4), "w1": XS * 32}
-                e |= {"x0": 64 * XS, "s1": 64 * 32}
-            else:
-                e |= {"x0": 64 * XS}
+                e |= {"w3": 64 * r16(F), "du": 64 * (XS + 4), "x1": 64 * XS, "dx": 64 * XS, "s1": 64 * 32, "w1": XS * 32}
             return e
 
-        vals, total = _check("vanilla_chunk_bwd", [F, H, EM, TM, Fe, two], bext, phases=[{"halo", "rec", "trec"}, {"x0", "s1"}] if two else ())
-        if two:  # X0 and S1 live in the edge region after the edge phase, inside the carve
-            assert vals["x0"] == vals["halo"] and vals["s1"] == vals["x0"] + 64 * XS
-            assert vals["s1"] + 64 * 32 <= total
+        late = {"x0", "x1", "dx", "s1", "w1"}  # (vc_eb1: x1 .. w1 empty)
+        vals, total = _check("vanilla_chunk_bwd", [F, H, EM, TM, Fe, two], bext, phases=[{"halo", "trec"}, late])
+        assert vals["x0"] == vals["halo"]  # the late rows overlay the dead edge space
+        if two:
+            assert vals["w1"] + XS * 32 <= total

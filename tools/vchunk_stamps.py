@@ -33,8 +33,8 @@ KERNELS = [
     ("vc_fwd<1>", ["stage", "[A|B] MFMA", "edge gather", "node MLP"]),
     ("vc_fwd<2>", ["stage", "[A|B] MFMA", "edge gather", "node MLP"]),
     ("vc_nb2", ["stage", "GEMM dX1|DS2 + dWn2"]),
-    ("vc_eb2n1", ["stage", "edge bwd", "dW edge + dX1 GEMM", "DS1 + dWn1"]),
-    ("vc_eb1", ["stage", "edge bwd", "dW edge"]),
+    ("vc_eb2n1", ["stage", "edge bwd", "late rows (DMA)", "dW edge + dX1 GEMM", "DS1 + dWn1"]),
+    ("vc_eb1", ["stage", "edge bwd", "X0 (DMA) + dW edge"]),
 ]
 
 
