@@ -558,9 +558,25 @@ __global__ void __launch_bounds__(RB) vb_edge_bwd_tile(VA a, int l) {
 constexpr int HT = 1024;  // vb_head threads: 32 row chunks at a time for the mean over ~3k-node graphs
 __global__ void __launch_bounds__(HT) vb_head(VA a) {
   __shared__ float sG[64], sH[128], sDh[128], sDout[16], sRed[HT];
+  __shared__ float sW1[128 * 65];  // fc1.weight [128][F] at row stride F + 1 (conflict-free both ways)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.x;
   const int F = a.F, XS = a.XS, OUT = a.p.out_dim;
+  const int LW = F + 1;
+  {  // fc1.weight into LDS first: its loads overlap the mean's (the MLP and its
+     // backward then read LDS instead of 128-long chains of global loads)
+    float w[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int p = tid + u * HT;
+      w[u] = p < 128 * F ? a.w.g1w[p] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int p = tid + u * HT;
+      if (p < 128 * F) sW1[(p / F) * LW + p % F] = w[u];
+    }
+  }
   const int64_t r0 = a.ws.row0[b];
   const int N = a.ws.row0[b + 1] - (int)r0;
   const float* X2 = a.ws.base + a.L.x2 + r0 * XS;
@@ -614,7 +630,7 @@ __global__ void __launch_bounds__(HT) vb_head(VA a) {
   __syncthreads();
   if (tid < 128) {
     float acc = 0.f;
-    for (int n = 0; n < F; ++n) acc = fmaf(sG[n], a.w.g1w[tid * F + n], acc);
+    for (int n = 0; n < F; ++n) acc = fmaf(sG[n], sW1[tid * LW + n], acc);
     sH[tid] = relu_keepnan(acc + a.w.g1b[tid]);
   }
   __syncthreads();
@@ -658,7 +674,7 @@ __global__ void __launch_bounds__(HT) vb_head(VA a) {
   const int HD = XS + 256 + r4(OUT);  // d mean, consumed by vb_du2
   if (tid < F) {
     float acc = 0.f;
-    for (int r = 0; r < 128; ++r) acc = fmaf(a.w.g1w[r * F + tid], sDh[r], acc);
+    for (int r = 0; r < 128; ++r) acc = fmaf(sW1[r * LW + tid], sDh[r], acc);
     hg[HD + tid] = acc / (float)N;  // scatter_mean backward: grad / count
   }
   if (tid < XS) hg[tid] = tid < F ? sG[tid] : 0.f;
