@@ -1639,7 +1639,7 @@ __global__ void __launch_bounds__(CT, 8) vc_fwd(VA a) {
 
 // weight-gradient partial row of a layer for a chunk (both layers' rows live together)
 __device__ __forceinline__ float* part_row(const VA& a, int l, int ch) {
-  return a.ws.part + ((int64_t)(l - 1) * a.ws.n_chunks + ch) * layer_grad_size(a.F, a.Fe);
+  return a.ws.part + ((int64_t)(l - 1) * a.ws.n_chunks + ch) * r4(layer_grad_size(a.F, a.Fe));  // rows at 16 bytes (vc_combine)
 }
 
 // dWn = DU^T [X | S] (K = the chunk's 64 rows, zero past it) and dbn = sum DU:
@@ -2063,25 +2063,31 @@ __global__ void __launch_bounds__(CT, 8) vc_eb1(VA a) {
   CSTAMP(4, 3);
 }
 
-// both layers' chunk partials per graph, in chunk order (vb_wgrad_combine x 2)
+// both layers' chunk partials per graph, in chunk order (vb_wgrad_combine x 2):
+// four consecutive entries per thread (16-byte loads; part rows at stride
+// r4(total)), 8 chunks' loads in flight
 __global__ void __launch_bounds__(RB) vc_combine(VA a) {
-  const int total = layer_grad_size(a.F, a.Fe);
-  const int64_t work = (int64_t)a.B * 2 * total;
+  const int total = layer_grad_size(a.F, a.Fe), PS = r4(total), P4 = PS / 4;
+  const int64_t work = (int64_t)a.B * 2 * P4;
   for (int64_t q = blockIdx.x * (int64_t)RB + threadIdx.x; q < work; q += (int64_t)gridDim.x * RB) {
-    const int b = (int)(q / (2 * total)), rem = (int)(q - (int64_t)b * 2 * total), lay = rem / total, p = rem - lay * total;
-    const float* part = a.ws.part + (int64_t)lay * a.ws.n_chunks * total + p;
+    const int b = (int)(q / (2 * P4)), rem = (int)(q - (int64_t)b * 2 * P4), lay = rem / P4, p = (rem - lay * P4) * 4;
+    const float* part = a.ws.part + (int64_t)lay * a.ws.n_chunks * PS + p;
     const int ce = a.ws.chunk_first[b + 1];
-    float v = 0.f;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     int ch = a.ws.chunk_first[b];
     for (; ch + 8 <= ce; ch += 8) {
-      float u[8];
+      float4 u[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) u[k] = part[(int64_t)(ch + k) * total];
+      for (int k = 0; k < 8; ++k) u[k] = *reinterpret_cast<const float4*>(part + (int64_t)(ch + k) * PS);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v += u[k];
+      for (int k = 0; k < 8; ++k) v = f4add(v, u[k]);
     }
-    for (; ch < ce; ++ch) v += part[(int64_t)ch * total];
-    a.p.slab[(int64_t)(a.p.slot ? a.p.slot[b] : b) * DR_VANILLA_SLAB_STRIDE(a.F, a.Fe) + (int64_t)lay * total + p] = v;
+    for (; ch < ce; ++ch) v = f4add(v, *reinterpret_cast<const float4*>(part + (int64_t)ch * PS));
+    float* dst = a.p.slab + (int64_t)(a.p.slot ? a.p.slot[b] : b) * DR_VANILLA_SLAB_STRIDE(a.F, a.Fe) + (int64_t)lay * total + p;
+    if (p < total) dst[0] = v.x;
+    if (p + 1 < total) dst[1] = v.y;
+    if (p + 2 < total) dst[2] = v.z;
+    if (p + 3 < total) dst[3] = v.w;
   }
 }
 
@@ -2126,7 +2132,7 @@ int launch_chunk_fused(const VA& a, const dr_vanilla_scratch* sc, hipStream_t st
     hipLaunchKernelGGL(vc_nb2, tg, dim3(CT), (size_t)nb2_lds(a.F), st, a);
     hipLaunchKernelGGL(vc_eb2n1<FE>, tg, dim3(CT), (size_t)e2, st, a);
     hipLaunchKernelGGL(vc_eb1<FE>, tg, dim3(CT), (size_t)e1, st, a);
-    hipLaunchKernelGGL(vc_combine, dim3(rows_grid((int64_t)a.B * 2 * layer_grad_size(a.F, a.Fe), RB)), dim3(RB), 0, st, a);
+    hipLaunchKernelGGL(vc_combine, dim3(rows_grid((int64_t)a.B * 2 * (r4(layer_grad_size(a.F, a.Fe)) / 4), RB)), dim3(RB), 0, st, a);
   }
   return (int)hipGetLastError();
 }
@@ -2145,7 +2151,7 @@ extern "C" int64_t dr_vanilla_lds_bytes(int32_t n_feat, int32_t n_edge_feat, int
 }
 
 extern "C" int64_t dr_vanilla_part_floats(int32_t n_feat, int32_t n_edge_feat) {
-  return layer_grad_size(n_feat, n_edge_feat);
+  return r4(layer_grad_size(n_feat, n_edge_feat));  // (the chunk-fused rows are 16-byte aligned)
 }
 
 extern "C" int dr_vanilla_graph_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,

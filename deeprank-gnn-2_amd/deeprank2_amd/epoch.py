@@ -11,9 +11,9 @@ epoch loop:
   store; an epoch's batches are one pinned host->device copy of the epoch's
   graph order and one gather (``index_select``) into a fixed descriptor
   buffer that the handles of the epoch's batches view;
-* the steps of one epoch (graph pass + reduce/Adam per batch, plus the copy of
-  each batch's predictions and loss into epoch buffers) are captured once into
-  a HIP graph and replayed every epoch: one graph launch per epoch;
+* the steps of one epoch (graph pass + reduce/Adam per batch, each writing its
+  predictions and loss straight into epoch buffers) are captured once into a
+  HIP graph and replayed every epoch: one graph launch per epoch;
 * the dropout offset and Adam's step live in FusedTrainStep's device counter,
   so replays advance them exactly as eager steps do.
 
@@ -97,11 +97,22 @@ class EpochRunner:
         step._ensure(max(self.sizes))  # noqa: SLF001  (buffers sized before the capture)
 
     def _steps(self):
+        """The epoch's steps, each writing its predictions and loss straight
+        into the epoch buffers (the graph pass's ``dr_pass.out`` and the
+        reduce's loss pointer redirected per step: no copy launches)."""
         s = self.step
-        for k, (h, o, b) in enumerate(zip(self.handles, self.offs[:-1], self.sizes)):
-            loss, out = s.step(h, global_batch=b)
-            self.out[o : o + b].copy_(out)
-            self.loss[k : k + 1].copy_(loss)
+        passes = (s._pass, s._pass_nodrop)  # noqa: SLF001
+        saved = [p.out for p in passes], s.loss_out
+        try:
+            for k, (h, o, b) in enumerate(zip(self.handles, self.offs[:-1], self.sizes)):
+                for p in passes:
+                    p.out = self.out[o : o + b].data_ptr()
+                s.loss_out = self.loss[k : k + 1]
+                s.step(h, global_batch=b)
+        finally:
+            for p, v in zip(passes, saved[0]):
+                p.out = v
+            s.loss_out = saved[1]
 
     def _load(self, order):
         self.pin.copy_(torch.from_numpy(np.asarray(order, dtype=np.int64)))

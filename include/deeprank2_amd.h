@@ -519,7 +519,7 @@ int dr_vanilla_graph_pass(const dr_graph_store* store, const dr_graph_desc* desc
                           const dr_vanilla_weights* w, const dr_pass* pass, const dr_vanilla_scratch* scratch,
                           int32_t lds_bytes, void* stream);
 int64_t dr_vanilla_scratch_floats(int64_t n_rows, int32_t n_feat, int32_t n_edge_feat);
-int64_t dr_vanilla_part_floats(int32_t n_feat, int32_t n_edge_feat); /* one layer's gradient entries */
+int64_t dr_vanilla_part_floats(int32_t n_feat, int32_t n_edge_feat); /* one layer's gradient entries, rounded up to 4 (a 16-byte row) */
 int64_t dr_vanilla_lds_bytes(int32_t n_feat, int32_t n_edge_feat, int32_t out_dim);
 
 /* The same VanillaNetwork training pass (vanilla_gnn.py:26-65 + trainer.py:686-689)
