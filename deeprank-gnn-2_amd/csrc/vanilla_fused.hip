@@ -1266,13 +1266,13 @@ struct RowsV {
 // n entries of a staged weight layout: `off(p)` = the source element's float
 // offset into the weight array (or -1: zero); KPT per thread in registers,
 // the rest by a tail loop at store time
-template <class Off>
+template <class Off, int NT = CT>
 struct MapV {
   P2<float> v;
   __device__ __forceinline__ void load(const Buf& w, int n, Off off) {
 #pragma unroll
     for (int k = 0; k < KPT; ++k) {
-      const int p = threadIdx.x + k * CT;
+      const int p = threadIdx.x + k * NT;
       const int o = p < n ? off(p) : -1;
       v[k] = w.f32(o >= 0 ? o * 4 : OOB);
     }
@@ -1280,19 +1280,19 @@ struct MapV {
   __device__ __forceinline__ void store(float* dst, const Buf& w, int n, Off off) const {
 #pragma unroll
     for (int k = 0; k < KPT; ++k) {
-      const int p = threadIdx.x + k * CT;
+      const int p = threadIdx.x + k * NT;
       if (p < n) dst[p] = v[k];
     }
     #pragma unroll 1
-    for (int p = threadIdx.x + KPT * CT; p < n; p += CT) {
+    for (int p = threadIdx.x + KPT * NT; p < n; p += NT) {
       const int o = off(p);
       dst[p] = w.f32(o >= 0 ? o * 4 : OOB);
     }
   }
 };
-template <class Off>
-__device__ __forceinline__ MapV<Off> map_load(const Buf& w, int n, Off off) {
-  MapV<Off> m;
+template <int NT = CT, class Off>
+__device__ __forceinline__ MapV<Off, NT> map_load(const Buf& w, int n, Off off) {
+  MapV<Off, NT> m;
   m.load(w, n, off);
   return m;
 }
@@ -1678,7 +1678,9 @@ __device__ __forceinline__ void node_wgrad(const VA& a, float* out, const float*
   }
 }
 
-__global__ void __launch_bounds__(CT) vc_nb2(VA a) {
+constexpr int NB2 = 512;  // vc_nb2 threads: 4 workgroups per CU
+
+__global__ void __launch_bounds__(NB2, 8) vc_nb2(VA a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int F = a.F, XS = a.XS, KN = a.KN;
   const int tid = threadIdx.x;
@@ -1702,7 +1704,10 @@ __global__ void __launch_bounds__(CT) vc_nb2(VA a) {
     const int k = p / NOPD, n = p - k * NOPD;
     return (k < F && n < F + 32) ? k * KN + n : -1;
   };
-  const auto w = map_load(wb, XS * NOPD, w_off);
+  // XS * NOPD <= 2048 weights (F <= 32): two register batches of 2 x NB2
+  const auto w = map_load<NB2>(wb, XS * NOPD, w_off);
+  auto w_off2 = [&](int p) -> int { return w_off(p + 2 * NB2); };
+  const auto w2 = map_load<NB2>(wb, XS * NOPD - 2 * NB2, w_off2);
   const int HD = XS + 256 + r4(a.p.out_dim);
   const Buf dmb(a.p.head + (int64_t)hrow * DR_VANILLA_HEAD_STRIDE(F, a.p.out_dim) + HD, (int64_t)F * 4);
   float dm[4];
@@ -1719,12 +1724,13 @@ __global__ void __launch_bounds__(CT) vc_nb2(VA a) {
   if (x2.i < WR) *reinterpret_cast<float4*>(sDU + x2.i * LU + x2.c4) = du;
   x1.store(sX1, XS);
   s2.store(sS, 32);
-  w.store(sW, wb, XS * NOPD, w_off);
+  w.store(sW, wb, min(XS * NOPD, 2 * NB2), w_off);
+  w2.store(sW + 2 * NB2, wb, XS * NOPD - 2 * NB2, w_off2);
   __syncthreads();
   CSTAMP(2, 1);
   const int lane = tid & 63, wave = tid >> 6, li = lane & 15, kq = lane >> 4;
   const int nct = NOPD / 16;
-  for (int job = wave; job < 4 * nct; job += CW) {  // [dX1 | DS2] = DU2 Wn2
+  for (int job = wave; job < 4 * nct; job += NB2 / 64) {  // [dX1 | DS2] = DU2 Wn2
     const int ib = (job / nct) * 16, n = (job % nct) * 16 + li;
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int k0 = 0; k0 < XS; k0 += 4) acc = mfma4(sDU[(ib + li) * LU + k0 + kq], sW[(k0 + kq) * NOPD + n], acc);
@@ -1736,7 +1742,7 @@ __global__ void __launch_bounds__(CT) vc_nb2(VA a) {
       else if (n < F + 32) ws[a.L.ds + (rt0 + i) * 32 + n - F] = acc[q];
     }
   }
-  node_wgrad<CT>(a, part_row(a, 2, blockIdx.x), sDU, LU, sX1, sS, 4 * nct);
+  node_wgrad<NB2>(a, part_row(a, 2, blockIdx.x), sDU, LU, sX1, sS, 4 * nct);
   CSTAMP(2, 2);
 }
 
@@ -2129,7 +2135,7 @@ int launch_chunk_fused(const VA& a, const dr_vanilla_scratch* sc, hipStream_t st
   hipLaunchKernelGGL((vc_fwd<FE, 2>), tg, dim3(CT), (size_t)f2, st, a);
   hipLaunchKernelGGL(vb_head, dim3(a.B), dim3(HT), 0, st, a);
   if (a.p.flags & DR_PASS_BACKWARD) {
-    hipLaunchKernelGGL(vc_nb2, tg, dim3(CT), (size_t)nb2_lds(a.F), st, a);
+    hipLaunchKernelGGL(vc_nb2, tg, dim3(NB2), (size_t)nb2_lds(a.F), st, a);
     hipLaunchKernelGGL(vc_eb2n1<FE>, tg, dim3(CT), (size_t)e2, st, a);
     hipLaunchKernelGGL(vc_eb1<FE>, tg, dim3(CT), (size_t)e1, st, a);
     hipLaunchKernelGGL(vc_combine, dim3(rows_grid((int64_t)a.B * 2 * (r4(layer_grad_size(a.F, a.Fe)) / 4), RB)), dim3(RB), 0, st, a);
