@@ -1522,7 +1522,7 @@ __global__ void __launch_bounds__(CT, 8) vc_fwd(VA a) {
 #pragma unroll
   for (int k = 0; k < KPT; ++k) {
     const int p = tid + k * CT;
-    if (p < ne) put_rec_v<FE>(sR, p, rh[k], rv[k]);
+    if (p < ne) put_rec_v<FE>(sR, p, rh[k] * (HS * 4), rv[k]);  // the halo row's byte offset
   }
   if (oi < WR) *reinterpret_cast<float4*>(sXo + oi * HS + oc) = mask4(xo, oc);
   wab.store(sWab, wabv, XS * 64, wab_off);
@@ -1538,7 +1538,7 @@ __global__ void __launch_bounds__(CT, 8) vc_fwd(VA a) {
     *reinterpret_cast<float4*>(sB + (p >> 3) * HS + q4) = mask4(v, q4);
   }
   #pragma unroll 1
-  for (int p = tid + KPT * CT; p < ne; p += CT) put_rec<FE>(sR, p, lc[p], ea + (int64_t)p * FeS);
+  for (int p = tid + KPT * CT; p < ne; p += CT) put_rec<FE>(sR, p, lc[p] * (HS * 4), ea + (int64_t)p * FeS);
   __syncthreads();
   CSTAMP(LAYER - 1, 1);
   // ---- [A | B]: A of the own rows, B of the halo rows, in place ----
@@ -1561,6 +1561,7 @@ __global__ void __launch_bounds__(CT, 8) vc_fwd(VA a) {
   // ---- edge gather ----
   uint32_t* wr = a.ws.relu_words + (int64_t)(LAYER - 1) * n_words + m.word0 + m.e0;
   P2<float> sacc{0.f, 0.f};
+  const char* sBc = reinterpret_cast<const char*>(sB + c);  // + a record's byte offset = B[j][c]
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const int i = g + CRG * k;
@@ -1576,7 +1577,7 @@ __global__ void __launch_bounds__(CT, 8) vc_fwd(VA a) {
 #pragma unroll
       for (int u = 0; u < U; ++u) j[u] = get_rec<FE>(sR, e + u, ev[u]);
 #pragma unroll
-      for (int u = 0; u < U; ++u) q[u] = sB[j[u] * HS + c];
+      for (int u = 0; u < U; ++u) q[u] = *reinterpret_cast<const float*>(sBc + j[u]);
       uint32_t mine = 0u;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -1832,10 +1833,10 @@ struct EdgeBwd {
 #pragma unroll
     for (int k = 0; k < KPT; ++k) {
       const int p = tid + k * CT;
-      if (p < m.nq) sTR[p] = make_uint2(tc[k], tw[k]);
+      if (p < m.nq) sTR[p] = make_uint2(tc[k] * 128, tw[k]);  // the halo row's byte offset
     }
     #pragma unroll 1
-    for (int p = tid + KPT * CT; p < m.nq; p += CT) sTR[p] = make_uint2(lt[p], words[teid[p]]);
+    for (int p = tid + KPT * CT; p < m.nq; p += CT) sTR[p] = make_uint2(lt[p] * 128u, words[teid[p]]);
   }
   __device__ __forceinline__ void run(float* sD, int LDD, const float* sDS, const uint2* sTR, float* sSh) const {
     const int tid = threadIdx.x, c = tid & 31, g = tid >> 5, hs = tid & 32;
@@ -1874,6 +1875,7 @@ struct EdgeBwd {
 #pragma unroll
       for (int f = 0; f < FE; ++f) wsum[f] += cnt != 0.f ? dsi[k] * eap[f] : 0.f;
       float acc = 0.f;
+      const char* sDSc = reinterpret_cast<const char*>(sDS + c);  // + a record's byte offset = dS[j][c]
       const int qe_ = qe[k] - m.q0;
       int q = qb[k] - m.q0;
       for (; q + 4 <= qe_; q += 4) {
@@ -1882,14 +1884,14 @@ struct EdgeBwd {
         for (int u = 0; u < 4; ++u) tr[u] = sTR[q + u];
         float dv[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) dv[u] = sDS[tr[u].x * 32 + c];
+        for (int u = 0; u < 4; ++u) dv[u] = *reinterpret_cast<const float*>(sDSc + tr[u].x);
 #pragma unroll
         for (int u = 0; u < 4; ++u)
           if ((tr[u].y >> c) & 1u) acc += dv[u];
       }
       for (; q < qe_; ++q) {
         const uint2 tr = sTR[q];
-        if ((tr.y >> c) & 1u) acc += sDS[tr.x * 32 + c];
+        if ((tr.y >> c) & 1u) acc += *reinterpret_cast<const float*>(sDSc + tr.x);
       }
       sD[li * LDD + 32 + c] = acc;
     }
