@@ -15,19 +15,23 @@ Layout read (writer: reference ``deeprank2/utils/graph.py:210-264``; reader:
     <entry>/clustering/<method>/depth_{0,1}
 
 Reading goes through h5py's low-level API (``h5o.visit`` for an entry's
-datasets, ``h5d.read`` into preallocated arrays): ~80 us per dataset here
-against ~250 us through ``Group.__getitem__`` / ``Dataset.__getitem__``, and
-the entries are split over worker processes (each opens the file read-only).
-The reference instead reopens the file and reads every feature per item
-(``dataset.py:893-1052``, ~2.5 ms per graph on one core).
+datasets), split over worker processes (each opens the file read-only).  A
+contiguous dataset (DeepRank2 writes no chunked or compressed ones) is not
+read through HDF5 at all: the workers report its file offset, dtype and shape
+(``h5d.get_offset``), and the reader takes its bytes from ONE sequential read
+of the whole file (``np.fromfile``); anything else is read by ``h5d.read``
+into the archive's blob.  The reference instead reopens the file and reads
+every feature per item (``dataset.py:893-1052``, ~2.5 ms per graph on one
+core).
 
 Archive layout (a handful of arrays whatever the number of datasets, so the
-archive loads in one read): ``__entries__`` ("<file-index>\\t<entry>"),
+archive loads in one read): ``__entries__`` ("<file-index>\t<entry>"),
 ``__files__`` (paths), ``__names__`` ("<k>|<group>/<name>", k = the entry's
 position in ``__entries__``), ``__dtypes__``, ``__shapes__`` (flattened) with
-``__ndim__``, ``__offsets__`` (byte offsets into ``__blob__``, one more than
-datasets) and ``__blob__`` (every dataset's bytes, C order).  String datasets
-(``_name``, ``_chain_id``) are skipped.
+``__ndim__``, ``__src__`` (-1: the bytes are in ``__blob__``; f >= 0: in file
+f at the offset), ``__offsets__`` (byte offsets into ``__blob__`` or the
+file) and ``__blob__``.  String datasets (``_name``, ``_chain_id``) are
+skipped.
 
 Usage: ``python h5extract.py OUT.npz FILE.hdf5 [FILE.hdf5 ...]``
 """
@@ -41,10 +45,12 @@ GROUPS = ("node_features", "edge_features", "target_values", "clustering")
 
 
 def _read_entries(args):
-    """Worker: (path, [(k, entry)]) -> [(k, "group/name", array)] (low-level h5py)."""
+    """Worker: (file index, path, [(k, entry)]) -> [(k, "group/name", src)] with
+    src = (dtype str, shape, file index, byte offset) for a contiguous dataset,
+    else the array (low-level h5py)."""
     import h5py  # noqa: PLC0415
 
-    path, todo = args
+    fi, path, todo = args
     out = []
     fid = h5py.h5f.open(os.fsencode(path), h5py.h5f.ACC_RDONLY)
     try:
@@ -62,9 +68,16 @@ def _read_entries(args):
                 dt = dsid.dtype
                 if dt.kind in ("S", "O", "U", "V"):
                     continue
-                arr = np.empty(dsid.shape, dtype=dt)
-                dsid.read(h5py.h5s.ALL, h5py.h5s.ALL, arr)
-                out.append((k, name.decode(), arr))
+                shape = dsid.shape
+                off = dsid.get_offset()
+                nbytes = int(np.prod(shape, dtype=np.int64)) * dt.itemsize
+                if off is not None and dsid.get_storage_size() == nbytes and nbytes > 0:
+                    out.append((k, name.decode(), (dt.str, tuple(shape), fi, int(off))))
+                else:
+                    arr = np.empty(shape, dtype=dt)
+                    if nbytes:
+                        dsid.read(h5py.h5s.ALL, h5py.h5s.ALL, arr)
+                    out.append((k, name.decode(), arr))
     finally:
         fid.close()
     return out
@@ -81,9 +94,9 @@ def _workers(n_entries):
     return max(1, min(cores, 16, n_entries // 64))
 
 
-def read_arrays(paths, workers=None):
-    """Every entry of every file: (entries ["<file-index>\\t<entry>"], records
-    [(k, "group/name", array)] in entry order)."""
+def read_index(paths, workers=None):
+    """Every entry of every file: (entries ["<file-index>\t<entry>"], records
+    [(k, "group/name", src)] in entry order; src as in _read_entries)."""
     import h5py  # noqa: PLC0415
 
     entries, jobs = [], []
@@ -96,7 +109,7 @@ def read_arrays(paths, workers=None):
             entries.append(f"{fi}\t{entry}")
         n = workers or _workers(len(todo))
         step = -(-len(todo) // n) if todo else 1
-        jobs += [(str(p), todo[i : i + step]) for i in range(0, len(todo), step)]
+        jobs += [(fi, str(p), todo[i : i + step]) for i in range(0, len(todo), step)]
     if len(jobs) > 1:
         import multiprocessing as mp  # noqa: PLC0415
 
@@ -107,42 +120,92 @@ def read_arrays(paths, workers=None):
     return entries, [r for part in parts for r in part]
 
 
+def read_arrays(paths, workers=None):
+    """As read_index, with every record's array (file-offset records as views
+    into one read of their file)."""
+    entries, records = read_index(paths, workers)
+    bufs = {}
+    out = []
+    for k, name, src in records:
+        if isinstance(src, tuple):
+            dt, shape, fi, off = src
+            if fi not in bufs:
+                bufs[fi] = np.fromfile(paths[fi], dtype=np.uint8)
+            dtype = np.dtype(dt)
+            src = np.frombuffer(bufs[fi], dtype=dtype, count=int(np.prod(shape, dtype=np.int64)), offset=off).reshape(shape)
+        out.append((k, name, src))
+    return entries, out
+
+
 def pack(entries, records, paths):
-    """The archive's arrays (see the module docstring) from (k, name, array) records."""
-    sizes = [a.nbytes for _, _, a in records]
-    offsets = np.zeros(len(records) + 1, dtype=np.int64)
-    offsets[1:] = np.cumsum(sizes)
-    blob = np.empty(int(offsets[-1]), dtype=np.uint8)
-    for (_, _, a), o in zip(records, offsets[:-1]):
-        blob[o : o + a.nbytes] = np.ascontiguousarray(a).reshape(-1).view(np.uint8)
+    """The archive's arrays (see the module docstring) from (k, name, src) records."""
+    n = len(records)
+    src = np.full(n, -1, dtype=np.int64)
+    offsets = np.zeros(n + 1, dtype=np.int64)
+    dts, shapes, ndims = [], [], np.zeros(n, dtype=np.int64)
+    pos = 0
+    blobs = []
+    for i, (_, _, r) in enumerate(records):
+        if isinstance(r, tuple):
+            dt, shape, fi, off = r
+            src[i], offsets[i] = fi, off
+        else:
+            a = np.asarray(r)
+            dt, shape = a.dtype.str, a.shape  # (before ascontiguousarray, which makes 0-d arrays 1-d)
+            a = np.ascontiguousarray(a)
+            offsets[i] = pos
+            blobs.append(a.reshape(-1).view(np.uint8))
+            pos += a.nbytes
+        dts.append(dt)
+        shapes.extend(shape)
+        ndims[i] = len(shape)
+    offsets[n] = pos
+    blob = np.concatenate(blobs) if blobs else np.zeros(0, dtype=np.uint8)
     return {
         "__entries__": np.array(entries, dtype=np.str_),
         "__files__": np.array([str(p) for p in paths], dtype=np.str_),
-        "__names__": np.array([f"{k}|{n}" for k, n, _ in records], dtype=np.str_),
-        "__dtypes__": np.array([a.dtype.str for _, _, a in records], dtype=np.str_),
-        "__ndim__": np.array([a.ndim for _, _, a in records], dtype=np.int64),
-        "__shapes__": np.array([s for _, _, a in records for s in a.shape], dtype=np.int64),
+        "__names__": np.array([f"{k}|{nm}" for k, nm, _ in records], dtype=np.str_),
+        "__dtypes__": np.array(dts, dtype=np.str_),
+        "__ndim__": ndims,
+        "__shapes__": np.array(shapes, dtype=np.int64),
+        "__src__": src,
         "__offsets__": offsets,
         "__blob__": blob,
     }
 
 
 def unpack(z):
-    """Inverse of :func:`pack`: {"<k>|<group>/<name>": array} (views into the blob)."""
+    """Inverse of :func:`pack`: {"<k>|<group>/<name>": array} (views into the
+    blob, or into one read of each source file)."""
     blob, offsets, ndim, shapes = z["__blob__"], z["__offsets__"], z["__ndim__"], z["__shapes__"]
-    out, s = {}, 0
-    for i, (name, dt) in enumerate(zip(z["__names__"], z["__dtypes__"])):
+    src = z["__src__"] if "__src__" in z else np.full(ndim.size, -1, dtype=np.int64)
+    files = [str(f) for f in z["__files__"]]
+    ends = np.cumsum(ndim)
+    bufs = {}
+    dtypes = {}
+    out = {}
+    for i, (name, dt) in enumerate(zip(z["__names__"].tolist(), z["__dtypes__"].tolist())):
         nd = int(ndim[i])
-        shape = tuple(int(v) for v in shapes[s : s + nd])
-        s += nd
-        dtype = np.dtype(str(dt))
-        count = int(np.prod(shape, dtype=np.int64)) if nd else 1
-        out[str(name)] = np.frombuffer(blob, dtype=dtype, count=count, offset=int(offsets[i])).reshape(shape) if count else np.empty(shape, dtype=dtype)
+        shape = tuple(shapes[ends[i] - nd : ends[i]].tolist())
+        dtype = dtypes.get(dt)
+        if dtype is None:
+            dtype = dtypes[dt] = np.dtype(dt)
+        count = 1
+        for v in shape:
+            count *= v
+        f = int(src[i])
+        if f < 0:
+            buf = blob
+        else:
+            buf = bufs.get(f)
+            if buf is None:
+                buf = bufs[f] = np.fromfile(files[f], dtype=np.uint8)
+        out[name] = np.frombuffer(buf, dtype=dtype, count=count, offset=int(offsets[i])).reshape(shape) if count else np.empty(shape, dtype=dtype)
     return out
 
 
 def extract(out_path, paths):
-    entries, records = read_arrays(paths)
+    entries, records = read_index(paths)
     np.savez(out_path, **pack(entries, records, paths))
 
 
