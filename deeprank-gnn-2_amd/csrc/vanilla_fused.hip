@@ -583,47 +583,52 @@ __global__ void __launch_bounds__(HT) vb_head(VA a) {
   const float y_g = a.s.y[a.descs[b].gid];
   if (a.p.step_counter && b == 0 && tid == 0) a.p.step_counter[1] = a.p.step_counter[0];
   {  // the mean: column sums over the graph's DR_VANILLA_CHUNK-row chunks (rows
-     // in order within a chunk), then the chunks in order.  The chunk-fused
-     // forward leaves its tiles' sums in part_mean; otherwise summed here from X2.
-    constexpr int CR = DR_VANILLA_CHUNK;
+     // in order within a chunk), the chunks summed in groups of 8 (in order),
+     // then the groups in order.  The chunk-fused forward leaves its tiles'
+     // sums in part_mean; otherwise they are summed here from X2.  (Groups, not
+     // one running sum: a group's 8 loads are in flight together.)
+    constexpr int CR = DR_VANILLA_CHUNK, GS = 8, NG = HT / 32;  // NG groups of GS chunks per round
     const int nch = (N + CR - 1) / CR;
-    float t = 0.f;  // thread tid < F: the ordered sum over the chunks
-    if (a.ws.part_mean) {
-      if (tid < F) {
-        const float* pm = a.ws.part_mean + (int64_t)a.ws.chunk_first[b] * 32 + tid;
-        int ch = 0;
-        for (; ch + 8 <= nch; ch += 8) {  // 8 loads in flight, summed in chunk order
-          float v[8];
+    const int n = tid & 31, gq = tid >> 5;
+    float t = 0.f;  // thread n < F: the ordered sum over the groups
+    for (int g0 = 0; g0 * GS < nch; g0 += NG) {
+      const int c0 = (g0 + gq) * GS;
+      float gs = 0.f;
+      if (n < F && c0 < nch) {
+        const int c1 = min(nch, c0 + GS);
+        float v[GS];
+        if (a.ws.part_mean) {
+          const float* pm = a.ws.part_mean + ((int64_t)a.ws.chunk_first[b] + c0) * 32 + n;
 #pragma unroll
-          for (int u = 0; u < 8; ++u) v[u] = pm[(int64_t)(ch + u) * 32];
+          for (int u = 0; u < GS; ++u) v[u] = c0 + u < c1 ? pm[(int64_t)u * 32] : 0.f;
+        } else {
+#pragma unroll 1
+          for (int u = 0; u < GS; ++u) {  // the chunk's rows in order
+            float acc = 0.f;
+            if (c0 + u < c1) {
+              const int i1 = min(N, (c0 + u + 1) * CR);
+              int i = (c0 + u) * CR;
+              for (; i + 16 <= i1; i += 16) {  // 16 rows' loads in flight, summed in row order
+                float w[16];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) t += v[u];
-        }
-        for (; ch < nch; ++ch) t += pm[(int64_t)ch * 32];
-      }
-    } else {
-      const int n = tid & 31;
-      for (int c0 = 0; c0 < nch; c0 += HT / 32) {
-        const int ch = c0 + tid / 32;
-        float acc = 0.f;
-        if (ch < nch && n < F) {
-          const int i1 = min(N, (ch + 1) * CR);
-          int i = ch * CR;
-          for (; i + 16 <= i1; i += 16) {  // 16 rows' loads in flight, summed in row order
-            float v[16];
+                for (int q = 0; q < 16; ++q) w[q] = X2[(int64_t)(i + q) * XS + n];
 #pragma unroll
-            for (int u = 0; u < 16; ++u) v[u] = X2[(int64_t)(i + u) * XS + n];
-#pragma unroll
-            for (int u = 0; u < 16; ++u) acc += v[u];
+                for (int q = 0; q < 16; ++q) acc += w[q];
+              }
+              for (; i < i1; ++i) acc += X2[(int64_t)i * XS + n];
+            }
+            v[u] = acc;
           }
-          for (; i < i1; ++i) acc += X2[(int64_t)i * XS + n];
         }
-        sRed[tid] = acc;
-        __syncthreads();
-        if (tid < F)
-          for (int q = 0; q < HT / 32 && c0 + q < nch; ++q) t += sRed[q * 32 + tid];
-        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < GS; ++u)
+          if (c0 + u < c1) gs += v[u];
       }
+      sRed[tid] = gs;
+      __syncthreads();
+      if (tid < F)
+        for (int q = 0; q < NG && (g0 + q) * GS < nch; ++q) t += sRed[q * 32 + tid];
+      __syncthreads();
     }
     if (tid < F) sG[tid] = t / (float)N;
   }
@@ -2073,7 +2078,7 @@ __global__ void __launch_bounds__(CT, 8) vc_eb1(VA a) {
 
 // both layers' chunk partials per graph, in chunk order (vb_wgrad_combine x 2):
 // four consecutive entries per thread (16-byte loads; part rows at stride
-// r4(total)), 8 chunks' loads in flight
+// r4(total)), 16 chunks' loads in flight
 __global__ void __launch_bounds__(RB) vc_combine(VA a) {
   const int total = layer_grad_size(a.F, a.Fe), PS = r4(total), P4 = PS / 4;
   const int64_t work = (int64_t)a.B * 2 * P4;
@@ -2083,12 +2088,19 @@ __global__ void __launch_bounds__(RB) vc_combine(VA a) {
     const int ce = a.ws.chunk_first[b + 1];
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     int ch = a.ws.chunk_first[b];
-    for (; ch + 8 <= ce; ch += 8) {
-      float4 u[8];
+    for (; ch + 16 <= ce; ch += 16) {
+      float4 u[16];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) u[k] = *reinterpret_cast<const float4*>(part + (int64_t)(ch + k) * PS);
+      for (int k = 0; k < 16; ++k) u[k] = *reinterpret_cast<const float4*>(part + (int64_t)(ch + k) * PS);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v = f4add(v, u[k]);
+      for (int k = 0; k < 16; ++k) v = f4add(v, u[k]);
+    }
+    for (; ch + 4 <= ce; ch += 4) {
+      float4 u[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) u[k] = *reinterpret_cast<const float4*>(part + (int64_t)(ch + k) * PS);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v = f4add(v, u[k]);
     }
     for (; ch < ce; ++ch) v = f4add(v, *reinterpret_cast<const float4*>(part + (int64_t)ch * PS));
     float* dst = a.p.slab + (int64_t)(a.p.slot ? a.p.slot[b] : b) * DR_VANILLA_SLAB_STRIDE(a.F, a.Fe) + (int64_t)lay * total + p;
