@@ -809,6 +809,7 @@ int dr_debug_carve_vanilla_graph(const int32_t* q, char* buf, int32_t len);
 int dr_debug_carve_vanilla_tile(const int32_t* q, char* buf, int32_t len);
 int dr_debug_carve_vanilla_chunk_fwd(const int32_t* q, char* buf, int32_t len);
 int dr_debug_carve_vanilla_chunk_bwd(const int32_t* q, char* buf, int32_t len);
+int dr_debug_carve_vanilla_chunk_eb2(const int32_t* q, char* buf, int32_t len);
 
 #ifdef __cplusplus
 }
