@@ -1143,15 +1143,16 @@ inline int rows_grid(int64_t rows, int rows_per_block) {
 //   vc_fwd<l>  [A | B] = X [Wa; Wb]^T of its own rows and of its halo rows
 //              (MFMA), edge gather -> S_l, node MLP X_l = relu([X | S_l] Wn^T
 //              + bn) (vb_gemm<GM_HALVES> + vb_edge_fwd_tile + vb_gemm<GM_NODE>);
-//   vc_nb2     DU2 = relu'(X2) dmean, [dX1 | DS2] = DU2 Wn2, dWn2 / dbn2
-//              (vb_du + vb_gemm<GM_DXS> + vb_wgrad_mfma's Wn part);
-//   vc_eb2n1   D2, D2' from the DS2 halo, dWa2 / dWb2 / dbe2 / dWc2,
-//              dX1 += [D2 | D2'] [Wa2; Wb2], DU1 = relu'(X1) dX1, DS1 = DU1 Wn1,
-//              dWn1 / dbn1 (vb_edge_bwd_tile + vb_gemm<GM_DX1> + vb_du +
+//   vb_head    the mean (from the tiles' column sums), graph MLP, loss, head bwd;
+//   vc_eb2     DU2 = relu'(X2) dmean, [dX1 | DS2] = DU2 Wn2 of its own rows and
+//              DS2 of its halo rows (MFMA), dWn2 / dbn2, then D2, D2' from the
+//              DS2 halo, dWa2 / dWb2 / dbe2 / dWc2, dX1 += [D2 | D2'] [Wa2; Wb2],
+//              DU1 = relu'(X1) dX1, DS1 = DU1 Wn1, dWn1 / dbn1 (vb_du +
+//              vb_gemm<GM_DXS> + vb_edge_bwd_tile + vb_gemm<GM_DX1> + vb_du +
 //              vb_gemm<GM_DXS> + vb_wgrad_mfma, two layers);
 //   vc_eb1     D1, D1' from the DS1 halo, dWa1 / dWb1 / dbe1 / dWc1;
 //   vc_combine every graph's chunk partials of both layers, in chunk order.
-// 7 launches per step instead of 17.  Every GEMM takes the operands and the k
+// 6 launches per step instead of 17.  Every GEMM takes the operands and the k
 // order of the kernel it replaces, and the sums run in the same order, so the
 // outputs, slabs, head vectors and ReLU words are bit-identical to the untiled
 // pipeline; only dWc sums its rows' shares in another order (as the 16-row
