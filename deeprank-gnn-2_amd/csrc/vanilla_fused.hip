@@ -1143,16 +1143,15 @@ inline int rows_grid(int64_t rows, int rows_per_block) {
 //   vc_fwd<l>  [A | B] = X [Wa; Wb]^T of its own rows and of its halo rows
 //              (MFMA), edge gather -> S_l, node MLP X_l = relu([X | S_l] Wn^T
 //              + bn) (vb_gemm<GM_HALVES> + vb_edge_fwd_tile + vb_gemm<GM_NODE>);
-//   vb_head    the mean (from the tiles' column sums), graph MLP, loss, head bwd;
-//   vc_eb2     DU2 = relu'(X2) dmean, [dX1 | DS2] = DU2 Wn2 of its own rows and
-//              DS2 of its halo rows (MFMA), dWn2 / dbn2, then D2, D2' from the
-//              DS2 halo, dWa2 / dWb2 / dbe2 / dWc2, dX1 += [D2 | D2'] [Wa2; Wb2],
-//              DU1 = relu'(X1) dX1, DS1 = DU1 Wn1, dWn1 / dbn1 (vb_du +
-//              vb_gemm<GM_DXS> + vb_edge_bwd_tile + vb_gemm<GM_DX1> + vb_du +
+//   vc_nb2     DU2 = relu'(X2) dmean, [dX1 | DS2] = DU2 Wn2, dWn2 / dbn2
+//              (vb_du + vb_gemm<GM_DXS> + vb_wgrad_mfma's Wn part);
+//   vc_eb2n1   D2, D2' from the DS2 halo, dWa2 / dWb2 / dbe2 / dWc2,
+//              dX1 += [D2 | D2'] [Wa2; Wb2], DU1 = relu'(X1) dX1, DS1 = DU1 Wn1,
+//              dWn1 / dbn1 (vb_edge_bwd_tile + vb_gemm<GM_DX1> + vb_du +
 //              vb_gemm<GM_DXS> + vb_wgrad_mfma, two layers);
 //   vc_eb1     D1, D1' from the DS1 halo, dWa1 / dWb1 / dbe1 / dWc1;
 //   vc_combine every graph's chunk partials of both layers, in chunk order.
-// 6 launches per step instead of 17.  Every GEMM takes the operands and the k
+// 7 launches per step instead of 17.  Every GEMM takes the operands and the k
 // order of the kernel it replaces, and the sums run in the same order, so the
 // outputs, slabs, head vectors and ReLU words are bit-identical to the untiled
 // pipeline; only dWc sums its rows' shares in another order (as the 16-row
@@ -1776,19 +1775,14 @@ struct EdgeBwd {
   P2<float> dsi;
   P2<uint32_t> rw;  // row k's edge c (the first 32 of the row)
   P2<float4> rv;
-  const bool own_ds;  // ds given: the halo's and the rows' dS come from it (else the caller's LDS)
-  const int hb;       // bytes per halo row in LDS
 
-  // ds: the layer's dS array (halo rows DMA'd, the rows' dS loaded), or
-  // nullptr: the caller stages the halo (rows of hb bytes) and passes the
-  // rows' dS to run()
-  __device__ __forceinline__ EdgeBwd(const VA& a, const dr_vanilla_tile& mm, int l, const float* ds, int hrow_bytes = 128)
+  __device__ __forceinline__ EdgeBwd(const VA& a, const dr_vanilla_tile& mm, int l, const float* ds)
       : m(mm),
         words(a.ws.relu_words + (int64_t)(l - 1) * a.ws.edge0[a.B] + mm.word0),
         ea(a.s.ea + (mm.col0 + mm.e0) * FeS),
         lt(a.ws.ltcol + mm.ltcol_off),
         teid(a.s.t_eid + mm.col0 + mm.q0),
-        halo(a.ws.halo_ids + mm.h0, ds ? mm.n_halo : 0, ds ? ds + mm.g0 * 32 : a.ws.base, mm.n_graph),
+        halo(a.ws.halo_ids + mm.h0, mm.n_halo, ds + mm.g0 * 32, mm.n_graph),
         wv(words + mm.e0, (int64_t)mm.ne * 4),
         eav(ea, (int64_t)mm.ne * FeS * 4),
         ltv(lt, (int64_t)mm.nq * 2),
@@ -1796,9 +1790,7 @@ struct EdgeBwd {
         wgv(words, (int64_t)mm.e_graph * 4),
         rpv(a.s.rowptr + mm.rp0 + mm.i0, (int64_t)(mm.nr + 1) * 4),
         trpv(a.s.t_rowptr + mm.rp0 + mm.i0, (int64_t)(mm.nr + 1) * 4),
-        dsv(ds ? ds + mm.rt0 * 32 : a.ws.base, ds ? (int64_t)mm.nr * 128 : 0),
-        own_ds(ds != nullptr),
-        hb(hrow_bytes) {}
+        dsv(ds + mm.rt0 * 32, (int64_t)mm.nr * 128) {}
 
   // edge p's (tile-local CSR slot) record, or zeros when !ok
   __device__ __forceinline__ void rec_at(int p, bool ok, uint32_t& w, float4& v) const {
@@ -1825,7 +1817,7 @@ struct EdgeBwd {
 #pragma unroll
     for (int k = 0; k < KPT; ++k) {
       const int p = tid + k * CT;
-      tc[k] = ltv.u16(p * 2) * (uint32_t)hb;  // the halo row's byte offset
+      tc[k] = ltv.u16(p * 2);
       te[k] = (int)tev.u32(p * 4);
     }
   }
@@ -1846,14 +1838,12 @@ struct EdgeBwd {
 #pragma unroll
     for (int k = 0; k < KPT; ++k) {
       const int p = tid + k * CT;
-      if (p < m.nq) sTR[p] = make_uint2(tc[k], tw[k]);
+      if (p < m.nq) sTR[p] = make_uint2(tc[k] * 128, tw[k]);  // the halo row's byte offset
     }
     #pragma unroll 1
-    for (int p = tid + KPT * CT; p < m.nq; p += CT) sTR[p] = make_uint2(lt[p] * (uint32_t)hb, words[teid[p]]);
+    for (int p = tid + KPT * CT; p < m.nq; p += CT) sTR[p] = make_uint2(lt[p] * 128u, words[teid[p]]);
   }
-  // sDSo: the rows' dS [64][32] in LDS when the caller computed them
-  __device__ __forceinline__ void run(float* sD, int LDD, const float* sDS, const uint2* sTR, float* sSh,
-                                      const float* sDSo = nullptr) const {
+  __device__ __forceinline__ void run(float* sD, int LDD, const float* sDS, const uint2* sTR, float* sSh) const {
     const int tid = threadIdx.x, c = tid & 31, g = tid >> 5, hs = tid & 32;
     float wsum[FA];
 #pragma unroll
@@ -1886,10 +1876,9 @@ struct EdgeBwd {
         const int n = min(32, deg - base);
         for (int u = 0; u < n; ++u) edge(u);
       }
-      const float ds_i = sDSo ? sDSo[li * 32 + c] : dsi[k];
-      sD[li * LDD + c] = cnt != 0.f ? ds_i * cnt : 0.f;
+      sD[li * LDD + c] = cnt != 0.f ? dsi[k] * cnt : 0.f;
 #pragma unroll
-      for (int f = 0; f < FE; ++f) wsum[f] += cnt != 0.f ? ds_i * eap[f] : 0.f;
+      for (int f = 0; f < FE; ++f) wsum[f] += cnt != 0.f ? dsi[k] * eap[f] : 0.f;
       float acc = 0.f;
       const char* sDSc = reinterpret_cast<const char*>(sDS + c);  // + a record's byte offset = dS[j][c]
       const int qe_ = qe[k] - m.q0;
@@ -2056,238 +2045,6 @@ __global__ void __launch_bounds__(CT, 8) vc_eb2n1(VA a) {
   CSTAMP(3, 5);
 }
 
-struct Eb2Carve {
-  int LDD, LU, NOP3, NOPD, HS, hp, d, sh, du, x1, dx, ds2, s2, wn2, halo, trec, w3, w1, x0, s1, total;
-};
-// vc_eb2: [D | D'] rows, the waves' dWc shares, DU2 of the own rows (later
-// DU1), X1 / dX1 / DS2 / S2 of the own rows, Wn2, then the edge phase's halo
-// rows (X2 -> DU2 -> DS2 in place, stride HS) and transposed records; after
-// the edges the same space holds [Wa2; Wb2], Wn1's DS columns, X0 and S1.
-__host__ __device__ inline Eb2Carve eb2_carve(int F, int hmax, int tmax, int Fe) {
-  Eb2Carve c;
-  const int XS = r4(F), FeS = Fe > 0 ? Fe : 1;
-  c.LDD = 64 + 4;
-  c.LU = XS + 4;
-  c.NOP3 = r16(F);
-  c.NOPD = r16(F + 32);
-  c.HS = 36;
-  c.hp = r16(hmax);
-  int o = 0;
-  c.d = o;   o += WR * c.LDD;
-  c.sh = o;  o += CW * 32 * FeS;
-  c.du = o;  o += WR * c.LU;   // DU2 of the own rows, then DU1
-  c.x1 = o;  o += WR * XS;
-  c.dx = o;  o += WR * XS;     // dX1 = DU2 Wn2[:, :F], then + [D | D'] [Wa2; Wb2]
-  c.ds2 = o; o += WR * 32;     // DS2 of the own rows
-  c.s2 = o;  o += WR * 32;
-  c.wn2 = o; o += XS * c.NOPD;
-  c.halo = o;
-  c.trec = o + c.hp * c.HS;
-  const int edge = c.hp * c.HS + 2 * tmax;
-  c.w3 = o;
-  c.w1 = c.w3 + 64 * c.NOP3;
-  c.x0 = c.w1 + XS * 32;
-  c.s1 = c.x0 + WR * XS;
-  const int late = 64 * c.NOP3 + XS * 32 + WR * XS + WR * 32;
-  o += edge > late ? edge : late;
-  c.total = o;
-  return c;
-}
-
-// Layer 2's node backward fused into its edge backward (r04: was vc_nb2 +
-// vc_eb2n1).  DU2 = relu'(X2) dmean and [dX1 | DS2] = DU2 Wn2 of the tile's
-// own rows, DS2 of its halo rows (from their X2 rows, MFMA, in LDS: the DS2
-// and dX1 arrays and their launch are gone) and the dWn2 / dbn2 partials;
-// then D2, D2' and the edge weight gradients, dX1 += [D2 | D2'] [Wa2; Wb2],
-// DU1 = relu'(X1) dX1, DS1 = DU1 Wn1[:, F:] and layer 1's dWn / dbn.  Every
-// GEMM keeps vc_nb2's / vb_gemm's operands and k order: bit-identical.
-template <int FE>
-__global__ void __launch_bounds__(CT) vc_eb2(VA a) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int F = a.F, XS = a.XS, KE = a.KE, KN = a.KN;
-  const int t = blockIdx.x, tid = threadIdx.x;
-  CSTAMP(3, 0);
-  const dr_vanilla_tile m = a.ws.tile_meta[t];
-  const int64_t rt0 = m.rt0;
-  const int nr = m.nr, H = m.n_halo;
-  const Eb2Carve c = eb2_carve(F, a.ws.halo_max, a.ws.tile_tedges_max, FE);
-  const int HS = c.HS, LU = c.LU, NOPD = c.NOPD, NOP3 = c.NOP3;
-  float* sD = lds + c.d;
-  float* sSh = lds + c.sh;
-  float* sDU = lds + c.du;
-  float* sX1 = lds + c.x1;
-  float* sDX = lds + c.dx;
-  float* sDS2 = lds + c.ds2;
-  float* sS2 = lds + c.s2;
-  float* sWn2 = lds + c.wn2;
-  float* sXh = lds + c.halo;
-  float* ws = a.ws.base;
-  // ---- prologue: every global load, the halo ids and the head row first ----
-  const float* X2g = ws + a.L.x2 + m.g0 * XS;  // the graph's X2 rows
-  const Buf idv(a.ws.halo_ids + m.h0, (int64_t)H * 4);
-  const Buf x2v(X2g, (int64_t)m.n_graph * XS * 4);
-  P2<int> hid;
-#pragma unroll
-  for (int k = 0; k < KPT; ++k) hid[k] = (int)idv.u32(((tid + k * CT) >> 3) * 4);
-  const int hrow = a.p.slot ? a.p.slot[m.slot] : m.slot;
-  EdgeBwd<FE> eb(a, m, 2, nullptr, HS * 4);
-  eb.load1();
-  const int oi = tid >> 3, oc = (tid & 7) * 4;  // own rows: one float4 per thread (XS <= 32)
-  const float4 xo = x2v.f4(oi < nr && oc < XS ? ((m.i0 + oi) * XS + oc) * 4 : OOB);
-  RowsV x1, s2;
-  x1.load(ws + a.L.x1 + rt0 * XS, XS, nr, 0);
-  s2.load(ws + a.L.s2 + rt0 * 32, 32, nr, 0);
-  const Buf wb(a.w.wn2, (int64_t)F * KN * 4);
-  auto w_off = [&](int p) -> int {  // vb_gemm<GM_DXS>'s W staging (Wn2)
-    const int k = p / NOPD, n = p - k * NOPD;
-    return (k < F && n < F + 32) ? k * KN + n : -1;
-  };
-  const auto wn2 = map_load(wb, XS * NOPD, w_off);
-  const int HD = XS + 256 + r4(a.p.out_dim);
-  const Buf dmb(a.p.head + (int64_t)hrow * DR_VANILLA_HEAD_STRIDE(F, a.p.out_dim) + HD, (int64_t)F * 4);
-  float dm[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) dm[q] = dmb.f32((oc + q) * 4);  // (a thread's halo pieces have the same columns)
-  P2<float4> hx;
-#pragma unroll
-  for (int k = 0; k < KPT; ++k) {
-    const int p = tid + k * CT;
-    hx[k] = x2v.f4(p < H * 8 && oc < XS ? (hid[k] * XS + oc) * 4 : OOB);
-  }
-  eb.load2(nullptr);
-  eb.load3();
-  // DU2 = relu'(X2) dmean, zero past F (vb_du, layer 2)
-  auto du4 = [&](float4 x) {
-    float4 o;
-    o.x = oc < F ? relu_bwd(x.x, dm[0]) : 0.f;
-    o.y = oc + 1 < F ? relu_bwd(x.y, dm[1]) : 0.f;
-    o.z = oc + 2 < F ? relu_bwd(x.z, dm[2]) : 0.f;
-    o.w = oc + 3 < F ? relu_bwd(x.w, dm[3]) : 0.f;
-    return o;
-  };
-  // ---- LDS stores ----
-  eb.store(reinterpret_cast<uint2*>(lds + c.trec), sD, c.LDD);
-  if (oi < WR && oc < XS) *reinterpret_cast<float4*>(sDU + oi * LU + oc) = du4(xo);  // rows >= nr: X2 = 0 -> 0
-  x1.store(sX1, XS);
-  s2.store(sS2, 32);
-  wn2.store(sWn2, wb, XS * NOPD, w_off);
-#pragma unroll
-  for (int k = 0; k < KPT; ++k) {
-    const int p = tid + k * CT;
-    if (p < H * 8 && oc < XS) *reinterpret_cast<float4*>(sXh + (p >> 3) * HS + oc) = du4(hx[k]);
-  }
-#pragma unroll 1
-  for (int p = tid + KPT * CT; p < H * 8; p += CT) {
-    if (oc >= XS) continue;
-    const float4 v = x2v.f4(((int)idv.u32((p >> 3) * 4) * XS + oc) * 4);
-    *reinterpret_cast<float4*>(sXh + (p >> 3) * HS + oc) = du4(v);
-  }
-  __syncthreads();
-  CSTAMP(3, 1);
-  // ---- [dX1 | DS2] = DU2 Wn2 of the own rows, DS2 of the halo rows (in
-  // place), dWn2 / dbn2 partials: vc_nb2's operands and k order ----
-  const int lane = tid & 63, wave = tid >> 6, li = lane & 15, kq = lane >> 4;
-  const int nct = NOPD / 16;
-  for (int job = wave; job < 4 * nct; job += CW) {
-    const int ib = (job / nct) * 16, n = (job % nct) * 16 + li;
-    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < XS; k0 += 4) acc = mfma4(sDU[(ib + li) * LU + k0 + kq], sWn2[(k0 + kq) * NOPD + n], acc);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int i = ib + kq * 4 + q;
-      if (n < F) sDX[i * XS + n] = acc[q];
-      else if (n < F + 32) sDS2[i * 32 + n - F] = acc[q];
-    }
-  }
-  {
-    const int nb = (H + 15) >> 4;  // halo blocks, both 16-column tiles of DS2 on one wave
-    for (int jb = (wave + CW - (4 * nct) % CW) % CW; jb < nb; jb += CW) {
-      const int ib = jb * 16;
-      floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-      for (int k0 = 0; k0 < XS; k0 += 4) {
-        const float av = sXh[(ib + li) * HS + k0 + kq];
-        acc0 = mfma4(av, sWn2[(k0 + kq) * NOPD + F + li], acc0);
-        acc1 = mfma4(av, sWn2[(k0 + kq) * NOPD + F + 16 + li], acc1);
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int i = ib + kq * 4 + q;
-        if (i < H) {
-          sXh[i * HS + li] = acc0[q];
-          sXh[i * HS + 16 + li] = acc1[q];
-        }
-      }
-    }
-  }
-  node_wgrad<CT>(a, part_row(a, 2, t), sDU, LU, sX1, sS2, 4 * nct + ((H + 15) >> 4));
-  __syncthreads();
-  CSTAMP(3, 2);
-  // ---- D2, D2' and the dWc shares ----
-  eb.run(sD, c.LDD, sXh, reinterpret_cast<const uint2*>(lds + c.trec), sSh, sDS2);
-  __syncthreads();
-  CSTAMP(3, 3);
-  // [Wa2; Wb2], Wn1's DS columns, X0 / S1 rows into the dead edge space
-  float* sW3 = lds + c.w3;
-  float* sW1 = lds + c.w1;
-  float* sX0 = lds + c.x0;
-  float* sS1 = lds + c.s1;
-  dma_x4<CT>(sX0, a.s.x + m.xrow * XS, nr * XS / 4);
-  dma_x4<CT>(sS1, ws + a.L.s1 + rt0 * 32, nr * 8);
-  const Buf w3b(a.w.we2, (int64_t)32 * KE * 4);
-  auto w3_off = [&](int p) -> int {  // vb_gemm<GM_DX1>'s W staging
-    const int k = p / NOP3, n = p - k * NOP3;
-    return n < F ? (k & 31) * KE + (k < 32 ? 0 : F) + n : -1;
-  };
-  const auto w3 = map_load(w3b, 64 * NOP3, w3_off);
-  const Buf w1b(a.w.wn1, (int64_t)F * KN * 4);
-  auto w1_off = [&](int p) -> int {  // vb_gemm<GM_DXS>'s W staging (Wn1), the DS columns
-    const int k = p >> 5, n = p & 31;
-    return k < F ? k * KN + F + n : -1;
-  };
-  const auto w1 = map_load(w1b, XS * 32, w1_off);
-#pragma unroll 1
-  for (int p = tid; p < (WR - nr) * XS; p += CT) sX0[nr * XS + p] = 0.f;
-#pragma unroll 1
-  for (int p = tid; p < (WR - nr) * 32; p += CT) sS1[nr * 32 + p] = 0.f;
-  w3.store(sW3, w3b, 64 * NOP3, w3_off);
-  w1.store(sW1, w1b, XS * 32, w1_off);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  CSTAMP(3, 4);
-  edge_wgrad<FE>(a, part_row(a, 2, t), sD, c.LDD, sX1, sSh);
-  // dX1 += [D | D'] [Wa2; Wb2] (vb_gemm<GM_DX1>), then DU1 = relu'(X1) dX1 (vb_du)
-  const int nc3 = NOP3 / 16;
-  for (int job = (wave + CW - 8 % CW) % CW; job < 4 * nc3; job += CW) {
-    const int ib = (job / nc3) * 16, n = (job % nc3) * 16 + li;
-    floatx4 acc;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] = n < F ? sDX[(ib + kq * 4 + q) * XS + n] : 0.f;
-    for (int k0 = 0; k0 < 64; k0 += 4) acc = mfma4(sD[(ib + li) * c.LDD + k0 + kq], sW3[(k0 + kq) * NOP3 + n], acc);
-    if (n < XS) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int i = ib + kq * 4 + q;
-        sDU[i * LU + n] = n < F ? relu_bwd(sX1[i * XS + n], acc[q]) : 0.f;
-      }
-    }
-  }
-  __syncthreads();
-  CSTAMP(3, 5);
-  // DS1 = DU1 Wn1[:, F:] (vb_gemm<GM_DXS> layer 1) and layer 1's dWn / dbn
-  for (int job = wave; job < 8; job += CW) {
-    const int ib = (job >> 1) * 16, n = (job & 1) * 16 + li;
-    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < XS; k0 += 4) acc = mfma4(sDU[(ib + li) * LU + k0 + kq], sW1[(k0 + kq) * 32 + n], acc);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int i = ib + kq * 4 + q;
-      if (i < nr) ws[a.L.d + (rt0 + i) * 32 + n] = acc[q];
-    }
-  }
-  node_wgrad<CT>(a, part_row(a, 1, t), sDU, LU, sX0, sS1, 8);
-  CSTAMP(3, 6);
-}
-
 template <int FE>
 __global__ void __launch_bounds__(CT, 8) vc_eb1(VA a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -2356,7 +2113,7 @@ __global__ void __launch_bounds__(RB) vc_combine(VA a) {
 
 inline bool chunk_carves(const dr_vanilla_scratch* sc, int F, int Fe, int64_t* fwd1, int64_t* fwd2, int64_t* eb2, int64_t* eb1) {
   *fwd1 = *fwd2 = 4LL * fwd_carve(F, sc->halo_max, sc->tile_edges_max, Fe).total;
-  *eb2 = 4LL * eb2_carve(F, sc->halo_max, sc->tile_tedges_max, Fe).total;
+  *eb2 = 4LL * bwd_carve(F, sc->halo_max, sc->tile_edges_max, sc->tile_tedges_max, Fe, true).total;
   *eb1 = 4LL * bwd_carve(F, sc->halo_max, sc->tile_edges_max, sc->tile_tedges_max, Fe, false).total;
   const int64_t lim = 160 * 1024;
   return *fwd1 <= lim && *fwd2 <= lim && *eb2 <= lim && *eb1 <= lim;
@@ -2383,15 +2140,17 @@ int launch_chunk_fused(const VA& a, const dr_vanilla_scratch* sc, hipStream_t st
   const dim3 tg((unsigned)sc->n_tiles);
   DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&vc_fwd<FE, 1>)));
   DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&vc_fwd<FE, 2>)));
-  DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&vc_eb2<FE>)));
+  DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&vc_eb2n1<FE>)));
   DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&vc_eb1<FE>)));
+  DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&vc_nb2)));
   (void)gg;
   (void)glds_halves;
   hipLaunchKernelGGL((vc_fwd<FE, 1>), tg, dim3(CT), (size_t)f1, st, a);
   hipLaunchKernelGGL((vc_fwd<FE, 2>), tg, dim3(CT), (size_t)f2, st, a);
   hipLaunchKernelGGL(vb_head, dim3(a.B), dim3(HT), 0, st, a);
   if (a.p.flags & DR_PASS_BACKWARD) {
-    hipLaunchKernelGGL(vc_eb2<FE>, tg, dim3(CT), (size_t)e2, st, a);
+    hipLaunchKernelGGL(vc_nb2, tg, dim3(NB2), (size_t)nb2_lds(a.F), st, a);
+    hipLaunchKernelGGL(vc_eb2n1<FE>, tg, dim3(CT), (size_t)e2, st, a);
     hipLaunchKernelGGL(vc_eb1<FE>, tg, dim3(CT), (size_t)e1, st, a);
     hipLaunchKernelGGL(vc_combine, dim3(rows_grid((int64_t)a.B * 2 * (r4(layer_grad_size(a.F, a.Fe)) / 4), RB)), dim3(RB), 0, st, a);
   }
@@ -2531,33 +2290,6 @@ extern "C" int dr_debug_carve_vanilla_chunk_fwd(const int32_t* q, char* buf, int
   DR_DESC(d, c, wn);
   DR_DESC(d, c, bn);
   DR_DESC(d, c, x2);
-  DR_DESC(d, c, total);
-  return d.pos;
-}
-
-extern "C" int dr_debug_carve_vanilla_chunk_eb2(const int32_t* q, char* buf, int32_t len) {
-  const Eb2Carve c = eb2_carve(q[0], q[1], q[2], q[3]);
-  DrCarveDesc d{buf, len, 0};
-  DR_DESC_P(d, c, LDD);
-  DR_DESC_P(d, c, LU);
-  DR_DESC_P(d, c, NOP3);
-  DR_DESC_P(d, c, NOPD);
-  DR_DESC_P(d, c, HS);
-  DR_DESC_P(d, c, hp);
-  DR_DESC(d, c, d);
-  DR_DESC(d, c, sh);
-  DR_DESC(d, c, du);
-  DR_DESC(d, c, x1);
-  DR_DESC(d, c, dx);
-  DR_DESC(d, c, ds2);
-  DR_DESC(d, c, s2);
-  DR_DESC(d, c, wn2);
-  DR_DESC(d, c, halo);
-  DR_DESC(d, c, trec);
-  DR_DESC(d, c, w3);
-  DR_DESC(d, c, w1);
-  DR_DESC(d, c, x0);
-  DR_DESC(d, c, s1);
   DR_DESC(d, c, total);
   return d.pos;
 }

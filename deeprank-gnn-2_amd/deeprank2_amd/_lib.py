@@ -268,7 +268,7 @@ SIGNATURES = [
     ("dr_mcl", ctypes.c_int, [ctypes.POINTER(MclGraphsC), ctypes.c_int32, ctypes.c_int32, ctypes.c_double, VP]),
     ("dr_mcl_assign", ctypes.c_int, [VP, VP, VP, ctypes.c_int32, VP, VP]),
     ("dr_dropout_mask", ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int32, ctypes.c_float, VP]),
-    *[(f"dr_debug_carve_{k}", ctypes.c_int, [VP, ctypes.c_char_p, ctypes.c_int32]) for k in ("ginet", "ginet_conv", "ginet_conv_bf16", "ginet_tail", "fout", "fout_conv", "fout_tail", "nocluster", "vanilla_graph", "vanilla_tile", "vanilla_chunk_fwd", "vanilla_chunk_bwd", "vanilla_chunk_eb2")],
+    *[(f"dr_debug_carve_{k}", ctypes.c_int, [VP, ctypes.c_char_p, ctypes.c_int32]) for k in ("ginet", "ginet_conv", "ginet_conv_bf16", "ginet_tail", "fout", "fout_conv", "fout_tail", "nocluster", "vanilla_graph", "vanilla_tile", "vanilla_chunk_fwd", "vanilla_chunk_bwd")],
     ("dr_version", ctypes.c_char_p, []),
     ("dr_device_arch", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32]),
 ]

@@ -468,7 +468,7 @@ typedef struct dr_vanilla_scratch {
    * the chunk-fused kernels: one workgroup per 64-row chunk runs the edge work
    * and every row-local stage around it ([A | B] of its own and halo rows, node
    * MLP, node backward, weight-gradient partials) with the intermediates in
-   * LDS -- 6 launches per step instead of 17, the same results (dWc summed in
+   * LDS -- 7 launches per step instead of 17, the same results (dWc summed in
    * another order).  0 / 1: one layer.                                       */
   int32_t part_layers;
   /* the chunk-fused kernels' per-tile records [n_tiles] (required by them):
@@ -809,7 +809,6 @@ int dr_debug_carve_vanilla_graph(const int32_t* q, char* buf, int32_t len);
 int dr_debug_carve_vanilla_tile(const int32_t* q, char* buf, int32_t len);
 int dr_debug_carve_vanilla_chunk_fwd(const int32_t* q, char* buf, int32_t len);
 int dr_debug_carve_vanilla_chunk_bwd(const int32_t* q, char* buf, int32_t len);
-int dr_debug_carve_vanilla_chunk_eb2(const int32_t* q, char* buf, int32_t len);
 
 #ifdef __cplusplus
 }

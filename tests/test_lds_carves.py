@@ -316,12 +316,3 @@ def test_vanilla_tile_and_chunk_carves(H, EM, TM, Fe):
         assert vals["x0"] == vals["halo"]  # the late rows overlay the dead edge space
         if two:
             assert vals["w1"] + XS * 32 <= total
-    # vc_eb2 (layer 2's node + edge backward): [D | D'], the dWc shares, DU2 then DU1 at XS + 4,
-    # own X1 / dX1 / DS2 / S2 rows, Wn2 [XS][NOPD], halo rows at stride 36 (16-row blocks) and
-    # transposed records; after the edges [Wa2; Wb2] [64][NOP3], Wn1 DS columns, X0, S1
-    def e2ext(v):
-        return {"d": 64 * 68, "sh": 16 * 32 * FeS, "du": 64 * (XS + 4), "x1": 64 * XS, "dx": 64 * XS, "ds2": 64 * 32, "s2": 64 * 32,
-                "wn2": XS * r16(F + 32), "halo": r16(H) * 36, "trec": 2 * TM, "w3": 64 * r16(F), "w1": XS * 32, "x0": 64 * XS, "s1": 64 * 32}
-
-    vals, total = _check("vanilla_chunk_eb2", [F, H, TM, Fe], e2ext, phases=[{"halo", "trec"}, {"w3", "w1", "x0", "s1"}])
-    assert vals["w3"] == vals["halo"] and vals["s1"] + 64 * 32 <= total

@@ -32,8 +32,8 @@ from deeprank2_amd.utils.synthetic import make_dataset  # noqa: E402
 KERNELS = [
     ("vc_fwd<1>", ["stage", "[A|B] MFMA", "edge gather", "node MLP"]),
     ("vc_fwd<2>", ["stage", "[A|B] MFMA", "edge gather", "node MLP"]),
-    ("(vc_nb2: fused into vc_eb2)", ["-"]),
-    ("vc_eb2", ["stage", "DU2/DS2 GEMMs + dWn2", "edge bwd", "late rows (DMA)", "dW edge + dX1 GEMM", "DS1 + dWn1"]),
+    ("vc_nb2", ["stage", "GEMM dX1|DS2 + dWn2"]),
+    ("vc_eb2n1", ["stage", "edge bwd", "late rows (DMA)", "dW edge + dX1 GEMM", "DS1 + dWn1"]),
     ("vc_eb1", ["stage", "edge bwd", "X0 (DMA) + dW edge"]),
 ]
 
