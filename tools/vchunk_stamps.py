@@ -5,8 +5,9 @@ of the atom-level (B=32) or mixed (B=64) workload.
     DR_LIB_NAME=libdeeprank2_amd_stamps.so python tools/vchunk_stamps.py [atom|mixed]
 
 Per kernel: the median workgroup lifetime and phase split (thread 0's
-s_memtime after each phase barrier), the kernel's span (first start to last
-end) and the mean number of workgroups in flight (sum of lifetimes / span).
+s_memtime after each phase barrier).  Only differences of one workgroup's own
+stamps are read: s_memtime counters of different CUs / XCDs are not aligned
+(spans across workgroups came out as ~1e8 ticks).
 The stamps build is never used for timing claims: read the shares.
 """
 
@@ -62,7 +63,6 @@ def main():
     torch.cuda.synchronize()
     a = st.view(5, n_tiles, 16).cpu().numpy().astype(np.int64)
     print(f"workload {which}: B={B} chunks={n_tiles} (stamp ticks; shares matter, not absolute length)")
-    t0 = a[0, :, 0][a[0, :, 0] > 0].min()
     for k, (name, phases) in enumerate(KERNELS):
         s = a[k]
         if not (s[:, 0] > 0).all():
@@ -71,12 +71,10 @@ def main():
         np_ = len(phases)
         end = s[:, np_]
         life = end - s[:, 0]
-        span = end.max() - s[:, 0].min()
         d = np.diff(s[:, : np_ + 1], axis=1)
         med = np.median(d, axis=0)
         parts = ", ".join(f"{ph} {m:.0f} ({100 * m / med.sum():.0f}%)" for ph, m in zip(phases, med))
-        print(f"{name}: start +{s[:, 0].min() - t0}, span {span}, WG lifetime median {np.median(life):.0f} p90 {np.percentile(life, 90):.0f}, "
-              f"in flight {life.sum() / span:.1f}; phases: {parts}")
+        print(f"{name}: WG lifetime median {np.median(life):.0f} p90 {np.percentile(life, 90):.0f}; phases: {parts}")
 
 
 if __name__ == "__main__":
