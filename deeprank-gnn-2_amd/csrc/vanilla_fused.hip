@@ -1762,6 +1762,7 @@ __global__ void __launch_bounds__(NB2, 8) vc_nb2(VA a) {
 template <int FE>
 struct EdgeBwd {
   static constexpr int FA = FE > 0 ? FE : 1, FeS = FA;
+  static constexpr bool MF = FE <= 3;  // cnt / eap on MFMA (part1_mfma); FE = 4: the VALU pass
   const dr_vanilla_tile& m;
   const uint32_t* words;  // the graph's ReLU words of layer l
   const float* ea;
@@ -1824,8 +1825,75 @@ struct EdgeBwd {
   __device__ __forceinline__ void load2(float* sDS) {
     const int c = threadIdx.x & 31;
     halo.dma(sDS);
+    if constexpr (!MF) {
 #pragma unroll
-    for (int k = 0; k < 2; ++k) rec_at(rb[k] - m.e0 + c, c < re[k] - rb[k], rw[k], rv[k]);
+      for (int k = 0; k < 2; ++k) rec_at(rb[k] - m.e0 + c, c < re[k] - rb[k], rw[k], rv[k]);
+    }
+  }
+  // cnt_i and eap_i of the wave's four rows (2w, 2w + 1, 2w + 32, 2w + 33) on
+  // MFMA: C[c][4r + s] = sum over row r's edges e of bit_c(w_e) * [ea_e | 1][s]
+  // (A = the edges' ReLU bits, 16 channels x 4 edges per step; B = each
+  // edge's attributes and a one in its row's four columns), so a step takes 4
+  // edges for all 32 channels instead of one edge per row group.  The counts
+  // are exact (sums of ones); D_i = dS_i cnt_i as in the VALU pass, and the
+  // dWc share sum_i dS_i eap_i in another order (fp32 tolerance, like the
+  // tiles' dWc).  Then D rows into sD and the wave's dWc share into sSh.
+  __device__ __forceinline__ void part1_mfma(float* sD, int LDD, float* sSh) const {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, chl = lane & 15, kq = lane >> 4;
+    const int sn = lane & 3, rn = (lane >> 2) & 3;  // this lane's B / C column: row rn, slot sn (3: the count)
+    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int rowA = 2 * wave + CRG * kk;
+      if (rowA >= m.nr) break;
+      // rows A = rowA and rowA + 1 are consecutive CSR rows: [sA, mA), [mA, eB)
+      const int sA = __builtin_amdgcn_readlane(rb[kk], 0), mA = __builtin_amdgcn_readlane(re[kk], 0);
+      const int eB = rowA + 1 < m.nr ? __builtin_amdgcn_readlane(re[kk], 32) : mA;
+      // two steps (8 edges) per iteration, their loads issued together; a
+      // step past the rows reads zeros and adds nothing
+      for (int j0 = sA; j0 < eB; j0 += 8) {
+        uint32_t w[2];
+        float ev[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int jj = j0 + 4 * u + kq, p = jj - m.e0;
+          const bool ok = jj < eB;
+          w[u] = wv.u32(ok ? p * 4 : OOB);
+          ev[u] = eav.f32(ok && sn < FE ? (p * FeS + sn) * 4 : OOB);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int jj = j0 + 4 * u + kq;
+          const int r = 2 * kk + (jj < mA ? 0 : 1);
+          const float bv = (jj < eB && r == rn) ? (sn == 3 ? 1.f : ev[u]) : 0.f;
+          acc0 = mfma4(edge_bit(w[u], chl), bv, acc0);
+          acc1 = mfma4(edge_bit(w[u], chl + 16), bv, acc1);
+        }
+      }
+    }
+    // lane: C[channel kq * 4 + q (+ 16)][row rn, slot sn]
+    const int li = 2 * wave + (rn & 1) + CRG * (rn >> 1);  // the tile row of column group rn
+    float ds[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ds[h][q] = dsv.f32(li < m.nr ? (li * 32 + kq * 4 + q + 16 * h) * 4 : OOB);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int ch = kq * 4 + q + 16 * h;
+        const float v = h ? acc1[q] : acc0[q];
+        // the row's count, from the quad's slot-3 lane
+        const float cnt = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xFF, 0xF, 0xF, false));
+        if (sn == 3) sD[li * LDD + ch] = cnt != 0.f ? ds[h][q] * cnt : 0.f;
+        if constexpr (FE > 0) {
+          float sh = (sn < FE && cnt != 0.f) ? ds[h][q] * v : 0.f;
+          sh += __shfl_xor(sh, 4, 64);  // the wave's four rows
+          sh += __shfl_xor(sh, 8, 64);
+          if (rn == 0 && sn < FE) sSh[(wave * 32 + ch) * FeS + sn] = sh;
+        }
+      }
   }
   __device__ __forceinline__ void load3() {
 #pragma unroll
@@ -1845,6 +1913,7 @@ struct EdgeBwd {
   }
   __device__ __forceinline__ void run(float* sD, int LDD, const float* sDS, const uint2* sTR, float* sSh) const {
     const int tid = threadIdx.x, c = tid & 31, g = tid >> 5, hs = tid & 32;
+    if constexpr (MF) part1_mfma(sD, LDD, sSh);
     float wsum[FA];
 #pragma unroll
     for (int f = 0; f < FA; ++f) wsum[f] = 0.f;
@@ -1852,6 +1921,7 @@ struct EdgeBwd {
     for (int k = 0; k < 2; ++k) {
       const int li = g + CRG * k;
       if (li >= m.nr) break;
+      if constexpr (!MF) {
       float cnt = 0.f;
       float eap[FA];
 #pragma unroll
@@ -1879,6 +1949,7 @@ struct EdgeBwd {
       sD[li * LDD + c] = cnt != 0.f ? dsi[k] * cnt : 0.f;
 #pragma unroll
       for (int f = 0; f < FE; ++f) wsum[f] += cnt != 0.f ? dsi[k] * eap[f] : 0.f;
+      }
       float acc = 0.f;
       const char* sDSc = reinterpret_cast<const char*>(sDS + c);  // + a record's byte offset = dS[j][c]
       const int qe_ = qe[k] - m.q0;
@@ -1902,6 +1973,7 @@ struct EdgeBwd {
     }
     // each wave's share of dWc (its two row groups summed), combined over the
     // waves in order by the caller
+    if constexpr (!MF)
 #pragma unroll
     for (int f = 0; f < FE; ++f) {
       const float v = wsum[f] + __shfl_xor(wsum[f], 32, 64);
