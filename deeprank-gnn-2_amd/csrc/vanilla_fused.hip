@@ -1911,9 +1911,12 @@ struct EdgeBwd {
     #pragma unroll 1
     for (int p = tid + KPT * CT; p < m.nq; p += CT) sTR[p] = make_uint2(lt[p] * 128u, words[teid[p]]);
   }
-  __device__ __forceinline__ void run(float* sD, int LDD, const float* sDS, const uint2* sTR, float* sSh) const {
+  __device__ __forceinline__ void run(const VA& a, int sk, float* sD, int LDD, const float* sDS, const uint2* sTR, float* sSh) const {
+    (void)a;
+    (void)sk;
     const int tid = threadIdx.x, c = tid & 31, g = tid >> 5, hs = tid & 32;
     if constexpr (MF) part1_mfma(sD, LDD, sSh);
+    CSTAMP(sk, 8);  // (stamps build: the end of the counts pass)
     float wsum[FA];
 #pragma unroll
     for (int f = 0; f < FA; ++f) wsum[f] = 0.f;
@@ -2051,7 +2054,7 @@ __global__ void __launch_bounds__(CT, 8) vc_eb2n1(VA a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the halo DMA
   __syncthreads();
   CSTAMP(3, 1);
-  eb.run(sD, bc.LDD, lds + bc.halo, reinterpret_cast<const uint2*>(lds + bc.trec), sSh);
+  eb.run(a, 3, sD, bc.LDD, lds + bc.halo, reinterpret_cast<const uint2*>(lds + bc.trec), sSh);
   __syncthreads();
   CSTAMP(3, 2);
   // X1 / dX1 / X0 / S1 rows (DMA) and Wn1's DS columns into the dead edge space
@@ -2135,7 +2138,7 @@ __global__ void __launch_bounds__(CT, 8) vc_eb1(VA a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the halo DMA
   __syncthreads();
   CSTAMP(4, 1);
-  eb.run(sD, bc.LDD, lds + bc.halo, reinterpret_cast<const uint2*>(lds + bc.trec), lds + bc.sh);
+  eb.run(a, 4, sD, bc.LDD, lds + bc.halo, reinterpret_cast<const uint2*>(lds + bc.trec), lds + bc.sh);
   __syncthreads();
   CSTAMP(4, 2);
   float* sX0 = lds + bc.x0;  // X0 rows into the dead edge space

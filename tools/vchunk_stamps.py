@@ -75,6 +75,8 @@ def main():
         med = np.median(d, axis=0)
         parts = ", ".join(f"{ph} {m:.0f} ({100 * m / med.sum():.0f}%)" for ph, m in zip(phases, med))
         print(f"{name}: WG lifetime median {np.median(life):.0f} p90 {np.percentile(life, 90):.0f}; phases: {parts}")
+        if name.startswith("vc_eb") and (s[:, 8] > 0).all():  # the edge backward's counts pass (stamp 8) / transposed pass
+            print(f"  edge bwd split: counts {np.median(s[:, 8] - s[:, 1]):.0f}, transposed {np.median(s[:, 2] - s[:, 8]):.0f}")
 
 
 if __name__ == "__main__":
