@@ -1762,7 +1762,11 @@ __global__ void __launch_bounds__(NB2, 8) vc_nb2(VA a) {
 template <int FE>
 struct EdgeBwd {
   static constexpr int FA = FE > 0 ? FE : 1, FeS = FA;
-  static constexpr bool MF = FE <= 3;  // cnt / eap on MFMA (part1_mfma); FE = 4: the VALU pass
+  static constexpr bool MF = FE <= 3;  // cnt / eap on MFMA (part1_mfma) in half the waves; FE = 4: the VALU pass
+  // The MFMA pass is bound by the fp32 MFMA pipe and the VALU pass by VALU /
+  // LDS issue, so the waves split: on every SIMD (waves w, w + 4, w + 8,
+  // w + 12) two take each pass, and the two pipes work side by side
+  __device__ __forceinline__ static bool mf_wave() { return MF && ((threadIdx.x >> 8) & 1); }
   const dr_vanilla_tile& m;
   const uint32_t* words;  // the graph's ReLU words of layer l
   const float* ea;
@@ -1825,7 +1829,7 @@ struct EdgeBwd {
   __device__ __forceinline__ void load2(float* sDS) {
     const int c = threadIdx.x & 31;
     halo.dma(sDS);
-    if constexpr (!MF) {
+    if (!mf_wave()) {
 #pragma unroll
       for (int k = 0; k < 2; ++k) rec_at(rb[k] - m.e0 + c, c < re[k] - rb[k], rw[k], rv[k]);
     }
@@ -1915,7 +1919,8 @@ struct EdgeBwd {
     (void)a;
     (void)sk;
     const int tid = threadIdx.x, c = tid & 31, g = tid >> 5, hs = tid & 32;
-    if constexpr (MF) part1_mfma(sD, LDD, sSh);
+    const bool mfw = mf_wave();
+    if (mfw) part1_mfma(sD, LDD, sSh);
     CSTAMP(sk, 8);  // (stamps build: the end of the counts pass)
     float wsum[FA];
 #pragma unroll
@@ -1924,7 +1929,7 @@ struct EdgeBwd {
     for (int k = 0; k < 2; ++k) {
       const int li = g + CRG * k;
       if (li >= m.nr) break;
-      if constexpr (!MF) {
+      if (!mfw) {
       float cnt = 0.f;
       float eap[FA];
 #pragma unroll
@@ -1976,7 +1981,7 @@ struct EdgeBwd {
     }
     // each wave's share of dWc (its two row groups summed), combined over the
     // waves in order by the caller
-    if constexpr (!MF)
+    if (!mfw)
 #pragma unroll
     for (int f = 0; f < FE; ++f) {
       const float v = wsum[f] + __shfl_xor(wsum[f], 32, 64);
