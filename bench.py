@@ -35,6 +35,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "deeprank-gnn-2_amd")]
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 B_PER_GPU = 64
+B_PER_GPU_FOR = {"residue": 64, "mixed": 64, "atom": 32}  # the default per-GPU batch of each workload (pmc_run.py's)
 MODEL_NAMES = ("foutnet", "ginet", "ginet_nocluster", "sgat", "vanilla")
 ORACLE_MODELS = {"ginet": "GINet", "foutnet": "FoutNet", "vanilla": "VanillaNetwork", "sgat": "SGAT", "ginet_nocluster": "GINetNoCluster"}
 # graph families of SURVEY §8(d): residue-PPI (configs 2/3), atom-level (config 4), SRV-like
@@ -253,21 +254,41 @@ def pmc_traffic_bytes(model="ginet"):
     return int((2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024), os.path.relpath(files[-1], ROOT)
 
 
-def pmc_traffic_step(model, graphs):
-    """HBM bytes per step of the model's graph-pass kernels from the newest
-    committed per-kernel PMC table (profiles/*/pmc_per_kernel_<model>_<graphs>.txt,
-    tools/pmc_per_kernel.py over FETCH_SIZE / WRITE_SIZE passes of
-    tools/pmc_run.py): for the multi-kernel Vanilla pipeline, whose "graph
-    pass" is a chain of launches (same gfx950 correction as pmc_traffic_bytes)."""
+def newest_profile(stem):
+    """Newest committed ``profiles/r<NN>/<stem>[_final<k>].txt``: the highest
+    round first, then the highest ``_final`` suffix (r04 committed its HEAD
+    tables as ``_final2``); ``_baseline`` / ``_not_kept`` files never match."""
     import glob  # noqa: PLC0415
+    import re  # noqa: PLC0415
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"pmc_per_kernel_{model}_{graphs}.txt")))
-    if not files:
+    pat = re.compile(re.escape(stem) + r"(?:_final(\d*))?\.txt")
+    best = None
+    for path in glob.glob(os.path.join(ROOT, "profiles", "r*", f"{stem}*.txt")):
+        m = pat.fullmatch(os.path.basename(path))
+        if not m:
+            continue
+        # the canonical name is a round's own HEAD table; among _final<k>, the highest k
+        rank = 1000 if m.group(1) is None and not os.path.basename(path).endswith("_final.txt") else int(m.group(1) or 0)
+        key = (os.path.basename(os.path.dirname(path)), rank)
+        if best is None or key > best[0]:
+            best = (key, path)
+    return None if best is None else best[1]
+
+
+def pmc_traffic_step(model, graphs, dtype="f32"):
+    """HBM bytes per step of the model's graph-pass kernels from the newest
+    committed per-kernel PMC table (profiles/*/pmc_per_kernel_<model>_<graphs>[_bf16].txt,
+    tools/pmc_per_kernel.py over FETCH_SIZE / WRITE_SIZE passes of
+    tools/pmc_run.py): for the multi-kernel paths (the Vanilla pipeline, the
+    GINet tile + tail kernels), whose "graph pass" is a chain of launches
+    (same gfx950 correction as pmc_traffic_bytes)."""
+    path = newest_profile(f"pmc_per_kernel_{model}_{graphs}" + ("_bf16" if dtype == "bf16" else ""))
+    if path is None:
         return None, None
-    for line in open(files[-1]):
+    for line in open(path):
         if line.startswith("per step (graph pass kernels):"):
             mb = float(line.split(",")[1].split("MB")[0])
-            return int(mb * 1e6), os.path.relpath(files[-1], ROOT)
+            return int(mb * 1e6), os.path.relpath(path, ROOT)
     return None, None
 
 
@@ -379,6 +400,7 @@ def parse_args(argv):
     ap.add_argument("--eager-ddp", action="store_true", help="N>1: launch steps from Python (default: the RCCL all-reduce is captured in the HIP graph with the kernels)")
     ap.add_argument("--trainer", action="store_true", help="diagnostic: the drop-in path, Trainer(GINet, GraphDataset(HDF5)).train(), and the GraphDataset -> GraphStore load rate (one JSON line; not the headline)")
     ap.add_argument("--epochs", type=int, default=3, help="--trainer: timed training epochs")
+    ap.add_argument("--validate", action="store_true", help="--trainer: train(validate=True), timing each validation pass")
     ap.add_argument("--shard-policy", choices=["auto", "contiguous", "edges"], default="auto", help="N>1: how each global batch is split over the ranks (distributed.plan_shards)")
     ap.add_argument("--dry-run", action="store_true", help="launcher check without a GPU: each rank joins a gloo group, builds the global batches and its shards, rank 0 prints the JSON skeleton with the per-rank edge loads")
     return ap.parse_args(argv)
@@ -438,6 +460,13 @@ def trainer_bench(args):
     n = B * args.batches
     graphs = make_graphs("residue", n, seed=1000)
     dev = torch.device("cuda:0")
+    # DR_BENCH_PG=1: Trainer(ngpu=2) on a one-rank RCCL group, the data-parallel
+    # code path (shards, the all-reduce captured in the epoch graph, the epoch's
+    # loss all-reduce and prediction gather) rehearsed on one GPU
+    ddp = os.environ.get("DR_BENCH_PG") == "1"
+    if ddp:
+        torch.cuda.set_device(dev)
+        torch.distributed.init_process_group("nccl", device_id=dev, init_method=f"tcp://127.0.0.1:{_free_port()}", world_size=1, rank=0)
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "train.hdf5")
         t0 = time.perf_counter()
@@ -455,36 +484,48 @@ def trainer_bench(args):
         del store
         torch.manual_seed(1234)
         mem = MemoryOutputExporter()
-        tr = Trainer(GINet, ds, cuda=True, output_exporters=[mem], precluster=False)
-        epoch_s = []
-        orig = tr._epoch  # noqa: SLF001
+        tr = Trainer(GINet, ds, cuda=True, output_exporters=[mem], precluster=False, ngpu=2 if ddp else 0)
+        epoch_s, eval_s = [], []
 
-        def timed(*a, **k):
-            torch.cuda.synchronize()
-            t = time.perf_counter()
-            r = orig(*a, **k)
-            torch.cuda.synchronize()
-            epoch_s.append(time.perf_counter() - t)
-            return r
+        def timer(orig, sink):
+            def timed(*a, **k):
+                torch.cuda.synchronize()
+                t = time.perf_counter()
+                r = orig(*a, **k)
+                torch.cuda.synchronize()
+                sink.append(time.perf_counter() - t)
+                return r
 
-        tr._epoch = timed  # noqa: SLF001
-        tr.train(nepoch=1, batch_size=B, shuffle=True, best_model=False, filename=None)  # warm-up epoch (store, plans, the epoch's HIP graph)
+            return timed
+
+        tr._epoch = timer(tr._epoch, epoch_s)  # noqa: SLF001
+        tr._eval = timer(tr._eval, eval_s)  # noqa: SLF001
+        val = bool(args.validate)
+        tr.train(nepoch=1, batch_size=B, shuffle=True, best_model=False, filename=None, validate=val)  # warm-up epoch (store, plans, the epoch's HIP graphs)
         epoch_s.clear()
+        eval_s.clear()
         t0 = time.perf_counter()
-        tr.train(nepoch=args.epochs, batch_size=B, shuffle=True, best_model=False, filename=None)
+        tr.train(nepoch=args.epochs, batch_size=B, shuffle=True, best_model=False, filename=None, validate=val)
         t_train = time.perf_counter() - t0
         per_epoch = float(np.median(epoch_s))
-        captured = bool(tr._runners)  # noqa: SLF001
+        # evaluations: the epoch-0 pass over the training set, then one validation per epoch
+        val_evals = eval_s[2:] if val else []
+        per_eval = float(np.median(val_evals)) if val_evals else None
+        captured = any(not (isinstance(k, tuple) and k and k[0] == "eval") for k in tr._runners)  # noqa: SLF001
+        eval_captured = any(isinstance(k, tuple) and k and k[0] == "eval" for k in tr._runners)  # noqa: SLF001
         # the same epochs through the per-batch loop (descriptors + two launches per batch from Python)
         Trainer.capture_epochs = False
         try:
-            tr.train(nepoch=1, batch_size=B, shuffle=True, best_model=False, filename=None)
+            tr.train(nepoch=1, batch_size=B, shuffle=True, best_model=False, filename=None, validate=val)
             epoch_s.clear()
-            tr.train(nepoch=args.epochs, batch_size=B, shuffle=True, best_model=False, filename=None)
+            eval_s.clear()
+            tr.train(nepoch=args.epochs, batch_size=B, shuffle=True, best_model=False, filename=None, validate=val)
         finally:
             Trainer.capture_epochs = True
         per_epoch_loop = float(np.median(epoch_s))
+        per_eval_loop = float(np.median(eval_s[2:])) if val and len(eval_s) > 2 else None
     steps = int(np.ceil(len(tr.dataset_train) / B))
+    val_batches = int(np.ceil(len(tr.dataset_val) / B)) if tr.dataset_val is not None else 0
     res = {
         "metric": "graphs/sec per Trainer training epoch (drop-in path: Trainer(GINet, GraphDataset(HDF5)).train), configs[1] graphs",
         "value": round(len(tr.dataset_train) / per_epoch, 1),
@@ -497,12 +538,20 @@ def trainer_bench(args):
         "fused_step": bool(tr._fused),  # noqa: SLF001
         "captured_epochs": captured,
         "per_batch_loop": {"graphs_per_s": round(len(tr.dataset_train) / per_epoch_loop, 1), "us_per_step": round(per_epoch_loop / steps * 1e6, 2), "note": "Trainer.capture_epochs = False: per batch, the host builds descriptors and launches the graph pass and reduce/Adam"},
+        "data_parallel": {"process_group": "nccl, world 1 (DR_BENCH_PG=1: Trainer(ngpu=2) code path on one GPU)", "world": 1} if ddp else None,
+        "validation": None if per_eval is None else {
+            "graphs": len(tr.dataset_val), "batches": val_batches, "captured": eval_captured,
+            "us_per_eval": round(per_eval * 1e6, 1), "us_per_batch": round(per_eval / max(val_batches, 1) * 1e6, 2),
+            "per_batch_loop_us_per_batch": None if per_eval_loop is None else round(per_eval_loop / max(val_batches, 1) * 1e6, 2),
+            "note": "Trainer._eval on the validation loader (forward passes, per-batch loss on the device, exporters, one D2H): captured = the evaluation's passes as one HIP graph (epoch.EvalRunner)"},
         "train_call_s": round(t_train, 3),
         "train_call_note": "the whole train() call: epoch-0 evaluation, the timed epochs, model selection and the final state load",
         "load": load,
         "data": "synthetic (seeded residue graphs per SURVEY §8(d), written as a DeepRank2 HDF5 file); random-init GINet(30,1,3)",
     }
     print(json.dumps(res), flush=True)
+    if ddp:
+        torch.distributed.destroy_process_group()
     return res
 
 
@@ -735,9 +784,13 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
     default_cfg = args.model == "ginet" and args.graphs == "residue" and B == B_PER_GPU and args.dtype == "f32"
     pmc_cfg = default_cfg or (args.model in ("foutnet", "sgat", "vanilla") and args.graphs == "residue" and B == B_PER_GPU and args.dtype == "f32")
     traffic, traffic_src = pmc_traffic_bytes(args.model) if pmc_cfg else (None, None)
-    if traffic is None and args.model == "vanilla" and args.graphs in ("atom", "mixed") and args.dtype == "f32":
-        traffic, traffic_src = pmc_traffic_step("vanilla", args.graphs)
     large = args.model == "ginet" and (bool(args.force_large) or args.ginet_path != "auto" or args.dtype == "bf16" or any(h.lds((step.spec.entry, 1), lambda *sz: 0) > 160 * 1024 for h in handles))
+    # multi-kernel graph passes (Vanilla pipeline, GINet tile + tail kernels):
+    # the per-kernel PMC table of the same workload (tools/pmc_run.py <model>_<graphs>[_bf16])
+    if traffic is None and B == B_PER_GPU_FOR.get(args.graphs) and not args.force_large and args.ginet_path == "auto" and (
+        (args.model == "vanilla" and args.graphs in ("atom", "mixed")) or (args.model == "ginet" and args.graphs in ("atom", "mixed"))
+    ):
+        traffic, traffic_src = pmc_traffic_step(args.model, args.graphs, args.dtype)
     copy_gbs = None if args.no_stream_copy else stream_copy_gbs(dev)
     # §8(d) FLOP side: algorithmic FLOPs per launch against the dense MFMA peak
     # of the compute dtype, and MFMA utilisation from the committed PMC pass

@@ -18,6 +18,40 @@ __device__ __forceinline__ float dr_wave_sum(float v) {
   return v;
 }
 
+// Lane permutations on the DPP path (a VALU operand modifier, no LDS round
+// trip as ds_bpermute has): CTRL is the gfx9 dpp_ctrl (0xB1 quad_perm
+// [1,0,3,2] = lane^1, 0x4E quad_perm [2,3,0,1] = lane^2, 0x141
+// row_half_mirror = 7-i within 8 lanes, 0x140 row_mirror = 15-i within 16).
+template <int CTRL>
+__device__ __forceinline__ float dr_dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// Sum over each aligned group of 8 lanes, in every lane of the group: the
+// same pairs, in the same order, as the __shfl_xor 1, 2, 4 butterfly (after
+// the quad steps all four lanes of a quad hold its sum, so the mirrored lane
+// of the other quad holds the other quad's), bit for bit.
+__device__ __forceinline__ float dr_sum8(float v) {
+  v += dr_dpp<0xB1>(v);
+  v += dr_dpp<0x4E>(v);
+  v += dr_dpp<0x141>(v);
+  return v;
+}
+
+// Sum over the 64 lanes, wave-uniform result: 8-lane groups and rows by DPP,
+// then the four row sums by readlane ((r0 + r1) + (r2 + r3)).  A different
+// association than dr_wave_sum's butterfly; a few tens of cycles instead of
+// six dependent LDS round trips.
+__device__ __forceinline__ float dr_wave_sum_dpp(float v) {
+  v = dr_sum8(v);
+  v += dr_dpp<0x140>(v);
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return (r0 + r1) + (r2 + r3);
+}
+
 // Allow up to the full 160 KiB of LDS for a kernel; done once per kernel
 // (hipFuncSetAttribute is not a stream operation, so it stays out of capture).
 inline int dr_allow_big_lds(const void* fn) {

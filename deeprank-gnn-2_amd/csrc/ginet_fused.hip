@@ -313,9 +313,16 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
   // max (NaN-propagating) and its count of members equal to it, combined per
   // pair (max is order-free here: H2 >= +0 or NaN).  Also record each
   // depth-0 cluster's depth-1 cluster for the backward.
-  for (int q = tid; q < K0; q += NT) {
+  // (by the last wave, idle here unless K1 >= 15: the pooling pairs start at
+  // wave 0; m counts the member offsets at or below q, all reads in flight)
+  for (int q = tid - (NT - 64); q >= 0 && q < K0; q += 64) {
     int m = 0;
-    while (q >= t.m1p[m + 1]) ++m;
+    if (K1 <= 16) {
+#pragma unroll
+      for (int j = 1; j < 16; ++j) m += (j < K1 && t.m1p[j < K1 ? j : 0] <= q) ? 1 : 0;
+    } else {
+      while (q >= t.m1p[m + 1]) ++m;
+    }
     t.cl1[t.m1i[q]] = m;
   }
   if (K0 < 16) {  // few members per pair: one pass
@@ -565,6 +572,41 @@ struct NoHook {
   __device__ int64_t operator()(float*) const { return -1; }
 };
 
+// Next-step prefetch (dr_pass.prefetch_descs): one 4-byte LDS-DMA load per
+// 64-byte line of the next batch's graph b, from the waves the front half
+// leaves idle, so its lines sit in this XCD's L2 when the next launch's
+// workgroup b (dispatched to the same XCD) stages them.  The DMA lands in a
+// 256-byte scratch per wave (the tail's dgp region, unused until the tail):
+// nothing consumes the data, so every load is issued back to back and the
+// wave drains them once before the front half's barrier.  A compact loop: this
+// kernel runs each instruction once per launch from a cold instruction cache.
+__device__ __forceinline__ void pf_range(const void* p, int64_t bytes, int gl, int nl, float* scratch) {
+  if (bytes <= 0) return;
+  const uintptr_t lo = reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)63;
+  const int lines = (int)((reinterpret_cast<uintptr_t>(p) + bytes - 1 - lo) >> 6) + 1;
+  for (int k = gl; k < lines; k += nl)
+    __builtin_amdgcn_global_load_lds(AS1(lo + ((uintptr_t)k << 6)), AS3(scratch), 4, 0, 0);
+}
+
+__device__ __forceinline__ void prefetch_next_graph(const dr_graph_store& s, const dr_graph_desc* next, int gl, int nl, float* scratch) {
+  const dr_graph_desc d = *next;
+  const int XS = (s.n_feat + 3) & ~3;
+  pf_range(s.x + d.node0 * (int64_t)XS, (int64_t)d.n_nodes * XS * 4, gl, nl, scratch);
+  pf_range(s.col + d.col0, (int64_t)d.n_edges * 2, gl, nl, scratch);
+  pf_range(s.rowptr + d.node0 + d.gid, (int64_t)(d.n_nodes + 1) * 4, gl, nl, scratch);
+  pf_range(s.cl0 + d.node0, (int64_t)d.n_nodes * 4, gl, nl, scratch);
+  pf_range(s.p1_rowptr + d.k0 + d.gid, (int64_t)(d.n_k0 + 1) * 4, gl, nl, scratch);
+  pf_range(s.p1_col + d.p1, (int64_t)d.n_p1 * 4, gl, nl, scratch);
+  if (!s.transpose_aliased) {
+    pf_range(s.p1t_rowptr + d.k0 + d.gid, (int64_t)(d.n_k0 + 1) * 4, gl, nl, scratch);
+    pf_range(s.p1t_col + d.p1, (int64_t)d.n_p1 * 4, gl, nl, scratch);
+  }
+  pf_range(s.m1_ptr + d.k1 + d.gid, (int64_t)(d.n_k1 + 1) * 4, gl, nl, scratch);
+  pf_range(s.m1_idx + d.k0, (int64_t)d.n_k0 * 4, gl, nl, scratch);
+  pf_range(s.y + d.gid, 4, gl, nl, scratch);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 template <int KPT, bool WT, bool SIB = false, bool RAS = false, class Hook = NoHook>
 __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx& sc = SibCtx{}, const Hook& hook = Hook{}) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -611,8 +653,10 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
 
   STAMP(0);
   // ---------------- stage the graph into LDS --------------------------------
-  // Head weights go to registers first (their latency hides under the DMA);
-  // the graph and conv1's weights are DMA'd straight into LDS.
+  // Only the graph and conv1's weights are staged (DMA'd straight into LDS):
+  // one CU pulls ~11-30 B/cycle, so the staging time is its bytes, and the
+  // head's 64 KB of fc1 registers (row and column layouts) are loaded after
+  // the staging barrier instead, under the LDS-bound front half.
   float fc1_row[8], fc1_col[8], fc1_bias;
   // RAS: every weight is read after the update's hand-off, with agent-scope
   // loads (another workgroup, maybe on another XCD, wrote it this launch)
@@ -633,7 +677,9 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
 #pragma unroll
     for (int j = 0; j < 8; ++j) fc1_col[j] = ldw(a.w.fc1w + (rcc * 8 + j) * 64 + o);
   };
+#ifdef DR_FC1_EARLY  // A/B diagnostic: the r04 order (fc1 before the graph DMA)
   if (!RAS) load_fc1();
+#endif
   const float y_g = s.y[g];
   uint64_t drop_offset = a.p.drop_offset;
   dma_x4(sX, s.x + n0 * (int64_t)XS, N * XS / 4);
@@ -692,6 +738,11 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
       else if (p < nf + OUT) wfc[u] = ldw(a.w.fc2b + p - nf);
     }
   }
+  // fc1 last: the wait for W2 / fc2 before their LDS stores (end of the
+  // front half) then leaves these 11 loads in flight (vmcnt counts in order)
+#ifndef DR_FC1_EARLY
+  if (!RAS) load_fc1();
+#endif
   // ---------------- conv1 + depth-0 pooling, one 16-row tile per wave -------
   // Each wave runs its rows through the whole front half with no workgroup
   // barrier in between:
@@ -786,6 +837,14 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
       }
     }
   }
+#ifdef DR_PREFETCH
+  // the next step's graph b into this XCD's L2, by the waves with no tile
+  // (N <= 240: at least one); a hint, the results do not depend on it
+  if (!SIB && a.p.prefetch_descs && b < a.p.prefetch_n) {
+    const int w0 = (N + 15) >> 4;
+    if (wave >= w0) prefetch_next_graph(s, a.p.prefetch_descs + b, (wave - w0) * 64 + lane, (NW - w0) * 64, lds + c.dgp + (wave - w0) * 64);
+  }
+#endif
   // the head's dropout keep flags, by the last two waves (idle in the front
   // half up to N = 224): off the tail's critical path
   if (tid >= NT - 128) {
@@ -1086,7 +1145,17 @@ __global__ void __launch_bounds__(NT) ginet_ras_kernel(GinetStepArgs a) {
     return tstep;
   };
   graph_body<KPT, false, false, true>(a.g, SibCtx{}, hook);
-  if (b == 0 && threadIdx.x == 0) sync[3] = 1u;  // this pass's partials are pending
+  // this pass's partials are pending for the next launch: flagged by the LAST
+  // workgroup to finish (sync[4] counts them), so no workgroup of this launch
+  // can still read the flag at its entry and take the partials being written
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t d = __hip_atomic_fetch_add((gu32*)(sync + 4), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == (uint32_t)B - 1u) {
+      __hip_atomic_store((gu32*)(sync + 4), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store((gu32*)(sync + 3), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 // =========================================================================

@@ -68,9 +68,13 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
     float acc = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc = fmaf(t.g[part * 8 + j], fc1_row[j], acc);
+#ifdef DR_HEAD_SHFL
     acc += __shfl_xor(acc, 1, 64);
     acc += __shfl_xor(acc, 2, 64);
     acc += __shfl_xor(acc, 4, 64);
+#else
+    acc = dr_sum8(acc);  // the same sums as the xor-1,2,4 shuffles, on the DPP path
+#endif
     if (part == 0) {
       acc += fc1_bias;
       t.hpre[r] = acc;
@@ -85,13 +89,20 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
   for (int q = wave; q < OUT; q += NW) {
     const float* wr = t.fc2 + q * 128;
     float v = fmaf(t.hd[lane], wr[lane], t.hd[lane + 64] * wr[lane + 64]);
+#ifdef DR_HEAD_SHFL
     v = dr_wave_sum(v);
+#else
+    v = dr_wave_sum_dpp(v);
+#endif
     if (lane == 0) t.dout[q] = v + t.fc2[OUT * 128 + q];  // logits parked in t.dout
   }
   __syncthreads();
   if ((p.flags & DR_PASS_FORWARD) && tid < OUT) p.out[(int64_t)b * OUT + tid] = t.dout[tid];
   if (!(p.flags & DR_PASS_BACKWARD)) return false;
-  __syncthreads();
+  // (the loss below is taken by thread 0, which read its logits above in
+  // program order; the other logits' readers are lanes of the same wave 0
+  // while OUT <= 64: no barrier needed between the output stores and the loss)
+  if (OUT > 64) __syncthreads();
   head_stamp(srow, stamp0);
 
   // ---------------- loss gradient (trainer.py:688-689) ----------------------
@@ -100,6 +111,7 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
       const float d = t.dout[0] - y_g;
       if (p.loss_per_graph) st_part<WT>(p.loss_per_graph + b, d * d);
       t.dout[0] = 2.f * d * p.loss_scale;
+      for (int q = 1; q < OUT; ++q) t.dout[q] = 0.f;  // the loss reads column 0 only (engine's layer path alike)
     } else if (p.loss_kind == DR_LOSS_CE) {
       const int yi = (int)y_g;
       float mx = t.dout[0];

@@ -173,8 +173,9 @@ class PassC(ctypes.Structure):
         ("step_counter", VP),
         ("fault", VP),
         ("spin_limit", ctypes.c_int32),
-        ("pad0", ctypes.c_int32),
+        ("prefetch_n", ctypes.c_int32),
         ("slot", VP),
+        ("prefetch_descs", VP),
     ]
 
 

@@ -92,7 +92,8 @@ class FusedTrainStep:
         # has it (GINet: dr_ginet_train_step; bit-identical to the two launches).
         # Off by default: measured slower at B=64 (24.7 vs 20.6 us/step)
         self.fuse_update = False
-        self.sync = torch.zeros(4, dtype=torch.int32, device=dev)  # its arrival counters, left zero
+        # its arrival counters (left zero); RAS: [2] timeout flag, [3] update pending, [4] finished workgroups
+        self.sync = torch.zeros(8, dtype=torch.int32, device=dev)
         # reduce-at-start (GINet, world of one, opt-in; dr_ginet_ras_step): each
         # launch applies the previous step's update, then runs its pass; loss_out
         # lags one step and flush() applies the last update (sync[3]: pending)
@@ -111,6 +112,12 @@ class FusedTrainStep:
         if getattr(model, "_drop_seed", 0) is None:
             model._drop_seed = int(torch.randint(0, 2**62, (1,)).item())
         self._cap = 0
+        # the batch the NEXT step trains on, when the caller knows it (captured
+        # sweeps and epochs): the GINet graph pass then reads those graphs into
+        # L2 from its idle waves (dr_pass.prefetch_descs; a hint, the results
+        # are the same without it).  Consumed by the next step().
+        self.prefetch_next = None
+        self.prefetch = True
         self._ensure(max_batch)
 
     # ---- persistent C structs (built once; a step makes two ctypes calls) ----
@@ -232,6 +239,11 @@ class FusedTrainStep:
         Dropout (ginet.py:122): ``mask`` (uint8 [B,128]) if given, else the
         in-kernel hash RNG (offset = the device step counter) when ``dropout``
         and the model's p > 0."""
+        if self._ras_last is not None and (h.B > self._cap or not (self.pg is None and self.ras and self.one_launch(h) and not (self.spec.layers is not None and layered.needs_layers(self.spec, h, self.out_dim)))):
+            # reduce-at-start: this step takes another path (or regrows the
+            # partial buffers), so the pending update is applied first (the
+            # other paths overwrite the partials)
+            self.flush()
         self._ensure(h.B)
         if global_batch is None:
             global_batch = h.B * self.world
@@ -248,6 +260,11 @@ class FusedTrainStep:
         else:
             p = self._pass if (dropout and self.spec.dropout > 0 and self.model.dropout > 0) else self._pass_nodrop
         p.loss_scale = scale
+        nxt, self.prefetch_next = self.prefetch_next, None
+        if nxt is not None and self.prefetch and nxt.descs is not None:
+            p.prefetch_descs, p.prefetch_n = nxt.descs.data_ptr(), nxt.B
+        else:
+            p.prefetch_descs, p.prefetch_n = None, 0
         ev = self.kernel_events
         if ev is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -327,10 +344,11 @@ class FusedTrainStep:
         same point): the per-rank counts are SUM-all-reduced first, so all ranks
         raise together instead of the faulting rank alone while the others
         block in their next collective."""
-        if self.fuse_update and int(self.sync[2].item()):
+        if (self.fuse_update or self.ras) and int(self.sync[2].item()):
             if reset:
                 self.sync[2].zero_()
-            msg = "a one-launch training step's reducer gave up waiting for the graph workgroups: that step's update was skipped"
+            msg = ("a reduce-at-start step's grid hand-off gave up waiting (some workgroups ran their pass on a mix of old and new parameters)"
+                   if self.ras else "a one-launch training step's reducer gave up waiting for the graph workgroups: that step's update was skipped")
             raise RuntimeError(msg)
         if not self.handoffs:
             return
@@ -384,6 +402,7 @@ class FusedTrainStep:
     def adam_state_dict(self):
         """The fused optimizer state as ``torch.optim.Adam(model.parameters()).state_dict()``
         would hold it (parameter order = the model's ``parameters()`` order)."""
+        self.flush()
         opt = torch.optim.Adam(self.params, lr=self.lr, betas=self.betas, eps=self.eps, weight_decay=self.weight_decay)
         t = int(self.counter[0].item())
         if t > 0:
@@ -427,6 +446,7 @@ class FusedTrainStep:
         (a sweep over the resident mini-batches): replaying it runs
         len(handles) steps with a single graph launch.  Training state is
         left as before the call."""
+        self.flush()  # a pending reduce-at-start update is applied before the snapshot (the slabs are not in it)
         for h in handles:
             self._ensure(h.B)
         self._packed()  # made before the snapshot, so the restore covers it
@@ -437,7 +457,9 @@ class FusedTrainStep:
         torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            for h in handles:
+            for i, h in enumerate(handles):
+                # replays run back to back: after the last step comes the first
+                self.prefetch_next = handles[(i + 1) % len(handles)]
                 self.step(h, global_batch=global_batch)
         torch.cuda.synchronize(self.device)
         for t, s in zip(self._state_tensors(), snap):
@@ -457,6 +479,7 @@ class FusedTrainStep:
         graph, replayed between two HIP events on the launch stream.  Used for
         ``roofline.achieved``; no host launch overhead enters the number (the
         rocprofv3 kernel average is the cross-check).  State is restored."""
+        self.flush()
         for h in handles:
             self._ensure(h.B)
         snap = [t.detach().clone() for t in self._state_tensors()]
@@ -471,7 +494,11 @@ class FusedTrainStep:
                     self.step(h, global_batch=global_batch)
                     continue
                 p.loss_scale = self.loss_scale(h, global_batch or h.B * self.world)
+                nxt = handles[(i + 1) % len(handles)]  # as in a captured sweep
+                if self.prefetch and nxt.descs is not None:
+                    p.prefetch_descs, p.prefetch_n = nxt.descs.data_ptr(), nxt.B
                 launch(self.spec, h, self._w, p)
+                p.prefetch_descs, p.prefetch_n = None, 0
 
         passes(len(handles))  # warm-up: LDS attributes, plans
         torch.cuda.synchronize(self.device)
@@ -502,6 +529,7 @@ class FusedTrainStep:
         if self.pg is not None or any(self.one_launch(h) or (self.spec.layers is not None and layered.needs_layers(self.spec, h, self.out_dim)) for h in handles):
             return None
         lib = _lib.load()
+        self.flush()
         for h in handles:
             self._ensure(h.B)
         snap = [t.detach().clone() for t in self._state_tensors()]
@@ -544,6 +572,7 @@ class FusedTrainStep:
         changed outside the graph between replays need a ``step()`` or
         ``refresh_packed()`` first.)  Capturing does not change the training
         state (the warm-up step it needs is rolled back)."""
+        self.flush()  # a pending reduce-at-start update is applied before the snapshot (the slabs are not in it)
         self._ensure(h.B)
         self._packed()  # made before the snapshot, so the restore covers it
         snap = [t.detach().clone() for t in self._state_tensors()]

@@ -18,8 +18,10 @@ Reading goes through h5py's low-level API (``h5o.visit`` for an entry's
 datasets), split over worker processes (each opens the file read-only).  A
 contiguous dataset (DeepRank2 writes no chunked or compressed ones) is not
 read through HDF5 at all: the workers report its file offset, dtype and shape
-(``h5d.get_offset``), and the reader takes its bytes from ONE sequential read
-of the whole file (``np.fromfile``); anything else is read by ``h5d.read``
+(``h5d.get_offset``), and the reader takes its bytes from a read-only memory
+map of the file (``np.memmap``: only the pages of the extracted datasets are
+read and stay resident, not the file's names, metadata and free space);
+anything else is read by ``h5d.read``
 into the archive's blob.  The reference instead reopens the file and reads
 every feature per item (``dataset.py:893-1052``, ~2.5 ms per graph on one
 core).
@@ -130,7 +132,7 @@ def read_arrays(paths, workers=None):
         if isinstance(src, tuple):
             dt, shape, fi, off = src
             if fi not in bufs:
-                bufs[fi] = np.fromfile(paths[fi], dtype=np.uint8)
+                bufs[fi] = np.memmap(paths[fi], dtype=np.uint8, mode="r")  # pages read as touched: only the extracted bytes stay resident
             dtype = np.dtype(dt)
             src = np.frombuffer(bufs[fi], dtype=dtype, count=int(np.prod(shape, dtype=np.int64)), offset=off).reshape(shape)
         out.append((k, name, src))
@@ -199,7 +201,7 @@ def unpack(z):
         else:
             buf = bufs.get(f)
             if buf is None:
-                buf = bufs[f] = np.fromfile(files[f], dtype=np.uint8)
+                buf = bufs[f] = np.memmap(files[f], dtype=np.uint8, mode="r")  # pages read as touched, not the whole file pinned
         out[name] = np.frombuffer(buf, dtype=dtype, count=count, offset=int(offsets[i])).reshape(shape) if count else np.empty(shape, dtype=dtype)
     return out
 

@@ -197,13 +197,19 @@ typedef struct dr_pass {
                            ticket); otherwise one give-up stays set and every later step is
                            withheld with a NaN loss.                                      */
   int32_t spin_limit;   /* polls before a hand-off wait gives up (<= 0: 1 << 22)        */
-  int32_t pad0;
+  int32_t prefetch_n;   /* entries of prefetch_descs (0: no prefetch)                    */
   const int32_t* slot;  /* optional device [B] (GINet / FoutNet / SGAT passes): launch position b
                            writes row slot[b] of out, loss_per_graph, slab, head and reads row
                            slot[b] of dout / mask, and draws dropout unit slot[b] -- a batch run
                            as several launches (graphs that fit one workgroup's LDS on the
                            per-graph kernel, the others on the large-graph path) fills the rows
                            one launch over the whole batch would                          */
+  const struct dr_graph_desc* prefetch_descs;
+                        /* optional device [prefetch_n] (dr_ginet_graph_pass): the NEXT step's
+                           batch.  Workgroup b's idle waves read graph b of it into their XCD's
+                           L2 during the front half (the same block index lands on the same
+                           XCD next launch), so the next pass stages from L2.  A hint: the
+                           results do not depend on it.                                    */
 } dr_pass;
 
 /* One workgroup per graph: conv1 -> depth-0 community pooling -> conv2 ->
@@ -646,8 +652,10 @@ int dr_ginet_train_step(const dr_graph_store* store, const dr_graph_desc* descs,
  * Adam (the same fixed-order arithmetic as dr_reduce_update) while the graph
  * DMA is in flight, publishes the new parameters through a grid-wide hand-off
  * (sync[0..1], bounded wait: a give-up sets sync[2]), then runs this step's
- * graph pass.  sync[3] = 1 while a pass's partials wait for their update; the
- * last step's update is a dr_reduce_update call (then zero sync[3]).
+ * graph pass.  sync[3] = 1 while a pass's partials wait for their update (set
+ * by the launch's last workgroup to finish, counted in sync[4]: sync holds 5
+ * uint32, zero before the first call); the last step's update is a
+ * dr_reduce_update call (then zero sync[3]).
  * prev_batch / prev_loss_scale: the batch size and loss scale of the pass whose
  * update is pending.  loss_out lags one step.  Parameters after K launches +
  * that flush are bit-identical to K dr_ginet_graph_pass + dr_reduce_update

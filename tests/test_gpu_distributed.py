@@ -101,3 +101,31 @@ def test_two_ranks_mixed_batch_edge_balanced_bit_identical(tmp_path, model_name)
     assert (loads.max(1) < 1.25 * loads.mean(1)).all()
     for k in a.files:
         np.testing.assert_array_equal(b[k], a[k], err_msg=k)
+
+
+def test_trainer_ddp_captured_epochs_bit_identical(tmp_path):
+    """``Trainer(ngpu=2)`` on a one-rank RCCL group: each training epoch
+    replayed from one captured HIP graph (graph pass, gradient reduce, the
+    RCCL all-reduce and Adam per step; the epoch's losses all-reduced and its
+    predictions gathered once) and each validation's forward passes from
+    another (epoch.EvalRunner) give the same losses, exported predictions and
+    final parameters, bit for bit, as the per-batch loop."""
+    from deeprank2_amd.utils import synthetic as S
+
+    tr, va = str(tmp_path / "train.hdf5"), str(tmp_path / "valid.hdf5")
+    S.write_hdf5(tr, S.make_dataset(23, seed=41, n_lo=25, n_hi=60, mean_degree=8.0), prefix="tr")
+    S.write_hdf5(va, S.make_dataset(9, seed=42, n_lo=25, n_hi=60, mean_degree=8.0), prefix="va")
+    res = {}
+    for cap in ("1", "0"):
+        out = str(tmp_path / f"cap{cap}.npz")
+        env = dict(os.environ, DR_TRAINER_CAPTURE=cap, OMP_NUM_THREADS="2")
+        p = subprocess.run([sys.executable, os.path.join(HERE, "trainer_ddp_worker.py"), tr, va, out], env=env, timeout=240, check=False)
+        assert p.returncode == 0, p.returncode
+        res[cap] = np.load(out)
+    a, b = res["1"], res["0"]
+    assert bool(a["captured_train"]) and bool(a["captured_eval"])
+    assert not bool(b["captured_train"]) and not bool(b["captured_eval"])
+    assert set(a.files) - {"captured_train", "captured_eval"} == set(b.files) - {"captured_train", "captured_eval"}
+    for k in a.files:
+        if not k.startswith("captured"):
+            np.testing.assert_array_equal(a[k], b[k], err_msg=k)

@@ -272,10 +272,11 @@ def test_foutnet_fused_train_step_vs_oracle_config3_batch64():
         loss, out = step.step(h)
         o, r = out.cpu().numpy(), out_o.detach().numpy()
         np.testing.assert_array_equal(np.isnan(o), np.isnan(r), err_msg=f"step {it}")
-        np.testing.assert_allclose(o, r, equal_nan=True, **TOL)
-        if np.isnan(r).any():
-            assert np.isnan(float(loss)) and np.isnan(float(loss_o))
-            return  # a NaN batch: the trajectory ends here on both sides
+        # this seeded batch has no pooled node without out-edges, so every step
+        # is finite and checked in full (a NaN batch would end the trajectory
+        # and shrink the test to a NaN-position check: fail loudly instead)
+        assert np.isfinite(r).all() and np.isfinite(o).all(), f"step {it}: the configs[2] batch must stay finite"
+        np.testing.assert_allclose(o, r, **TOL)
         assert float(loss) == pytest.approx(float(loss_o.detach()), rel=1e-4)
         grads = dict(zip(amd.PARAM_NAMES, step.grads))
         for n, p in model_o.named_parameters():

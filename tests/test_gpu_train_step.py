@@ -48,7 +48,7 @@ def _assert_same(one, two, what):
         if not torch.equal(a, b):
             bad.append((k, a.numel(), int((a != b).sum()), float((a.double() - b.double()).abs().max())))
     assert not bad, f"{what}: (tensor, numel, n_diff, max|diff|) {bad}; sync {one.sync.tolist()}"
-    assert one.sync.tolist() == [0, 0, 0, 0], "arrival counters must be left zero"
+    assert not any(one.sync.tolist()), "arrival counters and flags must be left zero"
 
 
 @pytest.mark.parametrize("sizes", [(64, 64, 64), (7, 1, 130, 64, 200)])
@@ -135,3 +135,25 @@ def test_reduce_at_start_steps_replay_from_hip_graph():
     one.flush()
     torch.cuda.synchronize()
     _assert_same(one, two, "captured reduce-at-start steps + flush vs eager two-launch steps")
+
+
+def test_reduce_at_start_pending_update_flushed_before_other_paths():
+    """A batch the reduce-at-start launch cannot take (B > 256: the regular
+    two-launch step) applies the pending update first, and reading the
+    optimizer state flushes it too: the state stays bit-identical to the
+    two-launch steps (without the flush the regular step's reduce
+    overwrote the pending partials, and the next RAS launch re-applied them)."""
+    store = GraphStore(pack_graphs(_records(320, 36)), DEV)
+    one, two = _ras_pair()
+    rng = np.random.default_rng(2)
+    for i, b in enumerate((64, 300, 64, 257, 32)):
+        h = BatchHandle(store, rng.permutation(320)[:b].astype(np.int32))
+        _l1, o1 = one.step(h)
+        _l2, o2 = two.step(h)
+        torch.cuda.synchronize()
+        assert torch.equal(o1, o2), f"outputs step {i} (B={b})"
+    sd1, sd2 = one.adam_state_dict(), two.adam_state_dict()  # flushes the pending update
+    for k in sd2["state"]:
+        for name in ("exp_avg", "exp_avg_sq"):
+            assert torch.equal(sd1["state"][k][name], sd2["state"][k][name]), (k, name)
+    _assert_same(one, two, "after B > 256 steps and the optimizer-state flush")

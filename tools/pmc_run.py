@@ -26,6 +26,8 @@ def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 40
     dev = torch.device("cuda:0")
     which = sys.argv[2] if len(sys.argv) > 2 else "ginet"
+    bf16 = which.endswith("_bf16")  # GINet bf16 compute (BASELINE configs[3]): the tile kernels for every graph
+    which = which.removesuffix("_bf16")
     atom = which.endswith("_atom")  # B=32 atom-level graphs (the Vanilla pipeline / large paths)
     mixed = which.endswith("_mixed")  # B=64 configs[4] 50/30/20 residue/SRV/atom mix (bench.py --graphs mixed)
     which = which.removesuffix("_atom").removesuffix("_mixed")
@@ -33,7 +35,7 @@ def main():
     fam = {"n_lo": 2700, "n_hi": 3300, "mean_degree": 16.7, "k_lo": 8, "k_hi": 32} if atom else {}
     graphs = make_graphs("mixed", B * nb, seed=1000) if mixed else make_dataset(B * nb, seed=1000, **fam)
     packed = pack_graphs(records(graphs, 1 if which == "sgat" else 3), require_clusters=which not in ("ginet_nocluster", "vanilla"))
-    store = GraphStore(packed, dev)
+    store = GraphStore(packed, dev, dtype="bf16" if bf16 else "f32")
     order = np.random.default_rng(0).permutation(packed.n_graphs).astype(np.int32)
     hs = [BatchHandle(store, order[i * B:(i + 1) * B]) for i in range(nb)]
     torch.manual_seed(1234)
@@ -43,11 +45,11 @@ def main():
         model = (sgat.SGAT(30, 1, 1) if which == "sgat" else foutnet.FoutNet(30, 1, 3)).to(dev).train()
     else:
         model = (VanillaNetwork if which == "vanilla" else GINet)(30, 1, 3).to(dev).train()
-    step = GINetTrainStep(model)
+    step = GINetTrainStep(model, compute_dtype="bf16" if bf16 else "f32")
     for i in range(steps):
         step.step(hs[i % nb])
     torch.cuda.synchronize()
-    print("alg_bytes_per_launch", np.mean([__import__("bench").algorithmic_bytes(packed, h.gids_host, which) for h in hs]))
+    print("alg_bytes_per_launch", np.mean([__import__("bench").algorithmic_bytes(packed, h.gids_host, which, 2 if bf16 else 4) for h in hs]))
 
 
 if __name__ == "__main__":
