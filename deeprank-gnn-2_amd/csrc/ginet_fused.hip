@@ -202,7 +202,17 @@ __device__ __forceinline__ void gather_rows(const int* rp, const uint16_t* col, 
     if (tid == 0 && ga.p.stamps) ga.p.stamps[(int64_t)b * 32 + (i)] = __builtin_amdgcn_s_memtime(); \
     __builtin_amdgcn_sched_barrier(0);                                                              \
   } while (0)
+// cross-workgroup timeline (s_memrealtime: one 100 MHz clock for the whole chip)
+#define RSTAMP(row, i)                                                                                  \
+  do {                                                                                                  \
+    __builtin_amdgcn_sched_barrier(0);                                                                  \
+    if (threadIdx.x == 0 && a.g.p.stamps) a.g.p.stamps[(int64_t)(row) * 32 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    __builtin_amdgcn_sched_barrier(0);                                                                  \
+  } while (0)
 #else
+#define RSTAMP(row, i) \
+  do {                 \
+  } while (0)
 #define STAMP(i) \
   do {           \
   } while (0)
@@ -270,7 +280,8 @@ __device__ __forceinline__ TailLds tail_lds(const C& c, float* lds) {
 template <class ZAt, bool WT = false>
 __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t, const float (&fc1_row)[8],
                                            const float (&fc1_col)[8], float fc1_bias, int b, int N, int K0, int K1,
-                                           int F, int OUT, float y_g, uint64_t drop_offset, ZAt zat) {
+                                           int F, int OUT, float y_g, uint64_t drop_offset, ZAt zat, int pb = -1) {
+  if (pb < 0) pb = b;  // the partials' row (slab, head vectors, loss term)
   const int tid = threadIdx.x;
   STAMP(4);
   // ---------------- conv2 on the pooled graph (ginet.py:101,112) ------------
@@ -410,7 +421,7 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
     hl.dout = t.dout;
     hl.dgp = t.dgp;
     hl.keep = t.keep;
-    if (!drk::ginet_head<NT, WT>(a.p, hl, fc1_row, fc1_col, fc1_bias, b, OUT, y_g, drop_offset, 8)) return;
+    if (!drk::ginet_head<NT, WT>(a.p, hl, fc1_row, fc1_col, fc1_bias, b, OUT, y_g, drop_offset, 8, pb)) return;
   }  // stamps 8 (forward head done) and 9 (loss gradient done) are taken inside
 
   STAMP(10);
@@ -439,7 +450,7 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
   // dW2 = dY2^T P1 per branch (4 tiles of 16 x 16, K = K0) and
   // dP1 = dY2 W2 per branch (ceil(K0/16) row tiles, K = 32); one wave per tile
   if (K0 < 12) {  // few clusters: direct loops
-    float* slab = a.p.slab + (int64_t)b * DR_SLAB_STRIDE(F) + 32 * F;
+    float* slab = a.p.slab + (int64_t)pb * DR_SLAB_STRIDE(F) + 32 * F;
     for (int p = tid; p < 1024; p += NT) {
       const int br = p >> 9, o = ((p >> 4) & 31) + br * 32, j = p & 15;
       float acc = 0.f;
@@ -469,7 +480,7 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
   } else
   {
     const int lane = tid & 63, wave = tid >> 6, li = lane & 15, kq = lane >> 4;
-    float* slab = a.p.slab + (int64_t)b * DR_SLAB_STRIDE(F) + 32 * F;
+    float* slab = a.p.slab + (int64_t)pb * DR_SLAB_STRIDE(F) + 32 * F;
     const int nrt = (K0 + 15) >> 4;
     for (int job = wave; job < 4 + 2 * nrt; job += NW) {
       if (job < 4) {
@@ -512,7 +523,7 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
   // K0 rows of Z per channel instead of a backward gather over all edges.)
   {
     const int SS = DR_SLAB_STRIDE(F);
-    float* slab = a.p.slab + (int64_t)b * SS;
+    float* slab = a.p.slab + (int64_t)pb * SS;
     // G clusters at a time, the last group predicated (clusters past K0 and
     // empty ones contribute nothing): every Z read of a group in flight (HBM on
     // the large path: with many clusters, groups of 16 halve the round trips),
@@ -572,43 +583,54 @@ struct NoHook {
   __device__ int64_t operator()(float*) const { return -1; }
 };
 
-// Next-step prefetch (dr_pass.prefetch_descs): one 4-byte LDS-DMA load per
-// 64-byte line of the next batch's graph b, from the waves the front half
-// leaves idle, so its lines sit in this XCD's L2 when the next launch's
-// workgroup b (dispatched to the same XCD) stages them.  The DMA lands in a
-// 256-byte scratch per wave (the tail's dgp region, unused until the tail):
-// nothing consumes the data, so every load is issued back to back and the
-// wave drains them once before the front half's barrier.  A compact loop: this
-// kernel runs each instruction once per launch from a cold instruction cache.
-__device__ __forceinline__ void pf_range(const void* p, int64_t bytes, int gl, int nl, float* scratch) {
-  if (bytes <= 0) return;
-  const uintptr_t lo = reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)63;
-  const int lines = (int)((reinterpret_cast<uintptr_t>(p) + bytes - 1 - lo) >> 6) + 1;
-  for (int k = gl; k < lines; k += nl)
-    __builtin_amdgcn_global_load_lds(AS1(lo + ((uintptr_t)k << 6)), AS3(scratch), 4, 0, 0);
-}
+// Pipelined step (dr_ginet_piped_step): this launch's pass blocks follow NR
+// reducer blocks that apply the PREVIOUS pass's update.  A pass block stages
+// its graph and gathers its first tile while they run, and only then waits
+// (each wave for itself, polling the update counter) before it reads any
+// weight, with agent-scope loads.  Its partials go to the half of the double
+// buffer the step's parity selects, the previous pass's half being the one the
+// reducers read.
+struct PipeCtx {
+  int NR = 0;                  // reducer blocks ahead of the pass blocks
+  bool pending = false;        // reducers of this launch apply an update: wait for it
+  uint32_t want = 0;           // the update counter value that means "applied"
+  const uint32_t* ver = nullptr;
+  uint32_t* fault = nullptr;   // set when a wait gives up (bounded spin)
+  int spin = 0;
+  int prow = 0;                // first partials row of this pass's buffer half
+};
 
-__device__ __forceinline__ void prefetch_next_graph(const dr_graph_store& s, const dr_graph_desc* next, int gl, int nl, float* scratch) {
-  const dr_graph_desc d = *next;
-  const int XS = (s.n_feat + 3) & ~3;
-  pf_range(s.x + d.node0 * (int64_t)XS, (int64_t)d.n_nodes * XS * 4, gl, nl, scratch);
-  pf_range(s.col + d.col0, (int64_t)d.n_edges * 2, gl, nl, scratch);
-  pf_range(s.rowptr + d.node0 + d.gid, (int64_t)(d.n_nodes + 1) * 4, gl, nl, scratch);
-  pf_range(s.cl0 + d.node0, (int64_t)d.n_nodes * 4, gl, nl, scratch);
-  pf_range(s.p1_rowptr + d.k0 + d.gid, (int64_t)(d.n_k0 + 1) * 4, gl, nl, scratch);
-  pf_range(s.p1_col + d.p1, (int64_t)d.n_p1 * 4, gl, nl, scratch);
-  if (!s.transpose_aliased) {
-    pf_range(s.p1t_rowptr + d.k0 + d.gid, (int64_t)(d.n_k0 + 1) * 4, gl, nl, scratch);
-    pf_range(s.p1t_col + d.p1, (int64_t)d.n_p1 * 4, gl, nl, scratch);
+// One wave per workgroup polls the update counter (the first to arrive claims
+// the job through an LDS word); it then sets an LDS flag that the workgroup's
+// other waves poll (MI355X_MICROARCH.md, inter-workgroup visibility: the other
+// waves load after an LDS word the polling wave sets).  lf: [0] flag, [1] claim,
+// both zeroed before the staging barrier.
+__device__ __forceinline__ void pipe_wait(const PipeCtx& pc, uint32_t* lf) {
+  if (!pc.pending) return;
+  if ((threadIdx.x & 63) == 0) {
+    typedef const __attribute__((address_space(1))) unsigned int gcu32;
+    uint32_t polls = 0;
+    if (__hip_atomic_fetch_add(lf + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
+      while (__hip_atomic_load((gcu32*)pc.ver, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < pc.want) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++polls == (uint32_t)pc.spin) {  // never expected: flag it and go on (loudly)
+          __hip_atomic_store((__attribute__((address_space(1))) unsigned int*)pc.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      __hip_atomic_store(lf, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+      while (__hip_atomic_load(lf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++polls == 4u * (uint32_t)pc.spin) break;  // the poller gives up first
+      }
+    }
   }
-  pf_range(s.m1_ptr + d.k1 + d.gid, (int64_t)(d.n_k1 + 1) * 4, gl, nl, scratch);
-  pf_range(s.m1_idx + d.k0, (int64_t)d.n_k0 * 4, gl, nl, scratch);
-  pf_range(s.y + d.gid, 4, gl, nl, scratch);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // the weight loads stay below the poll
 }
 
-template <int KPT, bool WT, bool SIB = false, bool RAS = false, class Hook = NoHook>
-__device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx& sc = SibCtx{}, const Hook& hook = Hook{}) {
+template <int KPT, bool WT, bool SIB = false, bool RAS = false, class Hook = NoHook, bool PIPED = false>
+__device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx& sc = SibCtx{}, const Hook& hook = Hook{}, const PipeCtx& pc = PipeCtx{}) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -660,10 +682,11 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
   float fc1_row[8], fc1_col[8], fc1_bias;
   // RAS: every weight is read after the update's hand-off, with agent-scope
   // loads (another workgroup, maybe on another XCD, wrote it this launch)
-  auto ldw = [&](const float* p) { return RAS ? __uint_as_float(__hip_atomic_load((const __attribute__((address_space(1))) unsigned int*)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) : *p; };
+  // (PIPED: the same, after the wave's wait for the update of this launch's reducers)
+  auto ldw = [&](const float* p) { return (RAS || PIPED) ? __uint_as_float(__hip_atomic_load((const __attribute__((address_space(1))) unsigned int*)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) : *p; };
   auto load_fc1 = [&]() {
     const int r = tid >> 3, part = tid & 7;
-    if (RAS) {
+    if (RAS || PIPED) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) fc1_row[j] = ldw(a.w.fc1w + r * 64 + part * 8 + j);
     } else {
@@ -694,7 +717,7 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
   }
   dma_words(sm1p, s.m1_ptr + k10 + g, K1 + 1);
   dma_words(sm1i, s.m1_idx + k00, K0);
-  if (!RAS) {
+  if (!RAS && !PIPED) {
     dma_words(sW1, a.w.w1, 16 * F);  // [W1; W1e] rows of F, packed
     dma_words(sW1 + 16 * F, a.w.w1e, 16 * F);
   }
@@ -705,6 +728,7 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
       sZ[i * LDW + XS + (p - i * padz)] = 0.f;
     }
     for (int p = tid; p < K0 * 32; p += NT) skey[p] = 0ull;
+    if (PIPED && tid < 2) reinterpret_cast<uint32_t*>(lds + c.dgp)[tid] = 0u;  // pipe_wait's flag and claim
   }
   if (a.p.step_counter) drop_offset = (uint64_t)a.p.step_counter[0];  // loaded late: no early wait
   if (RAS) {
@@ -727,7 +751,7 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
   // overlaps it.  (An LDS DMA here would make hipcc wait for it before every
   // LDS read.)
   float wv2, wfc[3];
-  {
+  auto load_head_weights = [&]() {
     wv2 = (tid < 512) ? ldw(a.w.w2 + tid) : ldw(a.w.w2e + tid - 512);
     const int nf = OUT * 128;
 #pragma unroll
@@ -737,12 +761,13 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
       if (p < nf) wfc[u] = ldw(a.w.fc2w + p);
       else if (p < nf + OUT) wfc[u] = ldw(a.w.fc2b + p - nf);
     }
-  }
-  // fc1 last: the wait for W2 / fc2 before their LDS stores (end of the
-  // front half) then leaves these 11 loads in flight (vmcnt counts in order)
-#ifndef DR_FC1_EARLY
-  if (!RAS) load_fc1();
+    // (fc1 is loaded after the front half, below: its 17 registers would
+    // otherwise be held through the gather loop)
+#ifdef DR_FC1_EARLY
+    if (PIPED) load_fc1();
 #endif
+  };
+  if (!PIPED) load_head_weights();
   // ---------------- conv1 + depth-0 pooling, one 16-row tile per wave -------
   // Each wave runs its rows through the whole front half with no workgroup
   // barrier in between:
@@ -765,12 +790,23 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
     // W[li][k + 4u + kq] (wa: conv1 rows, wb: conv1_ext rows), zero past F
     constexpr int NKV = KPT / 4;
     float wa[NKV], wb[NKV];
+    // PIPED: W1 straight from global memory after the wave's wait (the
+    // first tile's gather runs before it, under this launch's reducers)
+    bool have_w = !PIPED;
+    auto load_w1 = [&]() {
 #pragma unroll
-    for (int j = 0; j < NKV; ++j) {
-      const int kk = 16 * (j >> 2) + 4 * (j & 3) + kq;
-      wa[j] = kk < F ? sW1[li * F + kk] : 0.f;
-      wb[j] = kk < F ? sW1[(16 + li) * F + kk] : 0.f;
-    }
+      for (int j = 0; j < NKV; ++j) {
+        const int kk = 16 * (j >> 2) + 4 * (j & 3) + kq;
+        if (PIPED) {
+          wa[j] = kk < F ? ldw(a.w.w1 + li * F + kk) : 0.f;
+          wb[j] = kk < F ? ldw(a.w.w1e + li * F + kk) : 0.f;
+        } else {
+          wa[j] = kk < F ? sW1[li * F + kk] : 0.f;
+          wb[j] = kk < F ? sW1[(16 + li) * F + kk] : 0.f;
+        }
+      }
+    };
+    if (!PIPED) load_w1();
     for (int tt = SIB ? wave * sc.k + sc.rk : wave; tt * 16 < N; tt += SIB ? NW * sc.k : NW) {
       const int r0 = tt * 16;
       {  // rows r0+slot and r0+8+slot together: two independent edge chains per lane
@@ -779,7 +815,11 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
         const int eb1 = i1 < N ? srp[i1] : 0, ee1 = i1 < N ? srp[i1 + 1] : 0;
         for (int ch = sub; ch < nch; ch += 8) {
           float4 z0, z1;
+#ifdef DR_GATHER_PIPE
+          drk::gather_two_row_chunks_pipe(scol, eb0, ee0, eb1, ee1, sX, XS, ch * 4, z0, z1);
+#else
           drk::gather_two_row_chunks(scol, eb0, ee0, eb1, ee1, sX, XS, ch * 4, z0, z1);
+#endif
           if (i0 < N) {
             float* zr = sZ + i0 * LDW + ch * 4;
             zr[0] = z0.x;
@@ -799,6 +839,18 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
       // this wave's Z rows are complete in LDS before its own MFMA reads them
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (tt == 0) STAMP(20);  // (wave 0's first tile: gather done)
+      if (PIPED && !have_w) {
+#ifdef DR_STAMPS
+        if (tt == 0 && lane == 0 && a.p.stamps) a.p.stamps[(int64_t)b * 32 + 28] = __builtin_amdgcn_s_memrealtime();
+#endif
+        pipe_wait(pc, reinterpret_cast<uint32_t*>(lds + c.dgp));
+#ifdef DR_STAMPS
+        if (tt == 0 && lane == 0 && a.p.stamps) a.p.stamps[(int64_t)b * 32 + 29] = __builtin_amdgcn_s_memrealtime();
+#endif
+        load_w1();
+        load_head_weights();
+        have_w = true;
+      }
       const int ar = min(r0 + li, N - 1);  // rows past N compute garbage that is never pooled
       floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -836,15 +888,11 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
         STAMP(22);  // (pool atomics done)
       }
     }
+    if (PIPED && !have_w) {  // a wave with no tile: wait now, then its share of the head weights
+      pipe_wait(pc, reinterpret_cast<uint32_t*>(lds + c.dgp));
+      load_head_weights();
+    }
   }
-#ifdef DR_PREFETCH
-  // the next step's graph b into this XCD's L2, by the waves with no tile
-  // (N <= 240: at least one); a hint, the results do not depend on it
-  if (!SIB && a.p.prefetch_descs && b < a.p.prefetch_n) {
-    const int w0 = (N + 15) >> 4;
-    if (wave >= w0) prefetch_next_graph(s, a.p.prefetch_descs + b, (wave - w0) * 64 + lane, (NW - w0) * 64, lds + c.dgp + (wave - w0) * 64);
-  }
-#endif
   // the head's dropout keep flags, by the last two waves (idle in the front
   // half up to N = 224): off the tail's critical path
   if (tid >= NT - 128) {
@@ -861,6 +909,11 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
   STAMP(2);
   __syncthreads();
   STAMP(3);
+#ifndef DR_FC1_EARLY
+  // the head's fc1 registers: issued now, first read by the head ~4 K cycles
+  // later (conv2, the depth-1 pool and the mean run in between)
+  if (!RAS) load_fc1();
+#endif
   typedef __attribute__((address_space(1))) unsigned long long gu64s;
   typedef __attribute__((address_space(1))) unsigned int gu32s;
   if (SIB) {
@@ -921,7 +974,8 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
   t.keep = skeep;
   auto zat = [&](int i, int kk) { return sZ[i * LDW + kk]; };
   // (dr_pass.slot: the graph's rows of the batch when it is split over launches)
-  ginet_tail<decltype(zat), WT>(a, t, fc1_row, fc1_col, fc1_bias, a.p.slot ? a.p.slot[b] : b, N, K0, K1, F, OUT, y_g, drop_offset, zat);
+  const int orow = a.p.slot ? a.p.slot[b] : b;
+  ginet_tail<decltype(zat), WT>(a, t, fc1_row, fc1_col, fc1_bias, orow, N, K0, K1, F, OUT, y_g, drop_offset, zat, PIPED ? pc.prow + orow : orow);
   return drop_offset;
 }
 
@@ -970,6 +1024,8 @@ struct GinetStepArgs {
   uint32_t* sync;  // [4]: arrivals, reducers past the poll, timeout flag, spare
   int32_t NR;      // reducer workgroups (blockIdx B .. B+NR-1)
   int32_t diag;    // DR_STEP_DIAG=1: reducers skip the reduction (times the pass + hand-off alone)
+  int32_t alt_rows;  // dr_ginet_piped_step: rows per half of the partials' double buffer
+  int32_t spin;      // dr_ginet_piped_step: polls before a wait gives up
 };
 
 template <int KPT>
@@ -1154,6 +1210,109 @@ __global__ void __launch_bounds__(NT) ginet_ras_kernel(GinetStepArgs a) {
     if (d == (uint32_t)B - 1u) {
       __hip_atomic_store((gu32*)(sync + 4), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store((gu32*)(sync + 3), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Pipelined step (dr_ginet_piped_step): launch s = pass s by B graph blocks
+// (blockIdx < B, dispatched first) + the update of pass s-1 by NR reducer
+// blocks behind them.  The reducers read the previous launch's partials (rows
+// of the buffer half (s-1) & 1) with the fixed-order arithmetic of
+// dr_reduce_update (reduce_common.h) and store the new parameters
+// write-through; every wave drains, and the last reducer to take a ticket
+// (sync[6]) publishes the update counter sync[5] = s.  The pass blocks never
+// wait for the reducers before their staging and their first tile's gather:
+// a wave waits (pipe_wait: one poller per workgroup, the others on an LDS
+// flag) only right before it reads a weight, so the update runs under the
+// staging instead of as a launch of its own.  Nothing ever waits for a pass
+// block and the reducers never wait, so the waits need only that NR + B
+// one-per-CU workgroups be co-resident (the host checks NR + B <= 224).
+// s = counter[0] at launch; the last block of the launch to finish (sync[4])
+// sets counter[0] = s + 1 and the pending flag sync[3] (with no pass blocks,
+// n_batch 0: the flush of the last update, counter[0] unchanged, sync[3] and
+// sync[5] cleared).  The parameters, moments, gradients and loss terms are
+// bit-identical to dr_ginet_graph_pass + dr_reduce_update steps; loss_out
+// lags one launch.
+// ---------------------------------------------------------------------------
+template <int KPT>
+__global__ void __launch_bounds__(NT) ginet_piped_kernel(GinetStepArgs a) {
+  uint32_t* sync = a.sync;
+  const int NR = a.NR;
+  const bool pending = sync[3] != 0u;                  // written by the previous launch
+  const int64_t s_step = a.g.p.step_counter[0];        // passes done before this launch
+  const int B = a.g.B;
+  RSTAMP(blockIdx.x, 24);
+  if ((int)blockIdx.x >= B) {  // the reducers follow the pass blocks (those start first)
+    const int rb = (int)blockIdx.x - B;
+    if (pending && !(a.diag & 2)) {  // DR_STEP_DIAG bit 1 (diagnostic, wrong results): no update
+      typedef const __attribute__((address_space(4))) drr::ParamRec ConstRec;
+      ConstRec* recs = (ConstRec*)((const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() +
+                                   offsetof(GinetStepArgs, rec));
+      extern __shared__ __attribute__((aligned(16))) float lds[];
+      const int half = threadIdx.x / drr::RT, t = threadIdx.x % drr::RT;
+      float(*part)[drr::RP] = reinterpret_cast<float(*)[drr::RP]>(lds) + half * drr::RC;
+      const int nb = a.h.n_blocks;
+      const int64_t row_off = ((s_step - 1) & 1) * (int64_t)a.alt_rows;
+      for (int j0 = 0; j0 < nb; j0 += 2 * NR) {
+        const int j = j0 + 2 * rb + half;  // block j -> (parameter, element block)
+        int pi = 0;
+#pragma unroll
+        for (int q = 1; q <= STEP_PARAMS; ++q) pi += (a.h.blk0[q] <= j) ? 1 : 0;
+        pi = j < nb ? pi : a.h.n_params;
+        int eb = pi < a.h.n_params ? j - a.h.blk0[pi] : 0;
+        drr::ParamRec r;
+        memset(&r, 0, sizeof(r));
+        if (pi < a.h.n_params) {
+          ConstRec& q = recs[pi];
+          r.param = q.param;
+          r.grad = q.grad;
+          r.m = q.m;
+          r.v = q.v;
+          r.numel = q.numel;
+          r.kind = q.kind;
+          r.off1 = q.off1;
+          r.off2 = q.off2;
+          r.cols = q.cols;
+        } else {
+          eb = 0;
+        }
+        drr::reduce_block<0, true, true>(a.h, r, eb, j == 0, t, part, s_step, row_off);
+        __syncthreads();  // part reused by the next round
+      }
+      RSTAMP(blockIdx.x, 25);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's write-through parameters drained
+      __syncthreads();
+      RSTAMP(blockIdx.x, 26);
+      if (threadIdx.x == 0) {
+        const uint32_t k = __hip_atomic_fetch_add((gu32*)(sync + 6), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == (uint32_t)NR - 1u) {  // the last reducer: every update is out
+          __hip_atomic_store((gu32*)(sync + 6), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store((gu32*)(sync + 5), (uint32_t)s_step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+  } else {
+    PipeCtx pc;
+    pc.NR = NR;
+    pc.pending = pending && !(a.diag & 1);  // DR_STEP_DIAG bit 0 (diagnostic, wrong results): no waits
+    pc.want = (uint32_t)s_step;
+    pc.ver = sync + 5;
+    pc.fault = sync + 2;
+    pc.spin = a.spin;
+    pc.prow = (int)((s_step & 1) * a.alt_rows);
+    graph_body<KPT, false, false, false, NoHook, true>(a.g, SibCtx{}, NoHook{}, pc);
+  }
+  // the last block of the launch to finish: the step counter and the pending flag
+  __syncthreads();
+  RSTAMP(blockIdx.x, 27);
+  if (threadIdx.x == 0) {
+    const uint32_t d = __hip_atomic_fetch_add((gu32*)(sync + 4), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == gridDim.x - 1u) {
+      __hip_atomic_store((gu32*)(sync + 4), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (a.g.B > 0) a.g.p.step_counter[0] = s_step + 1;
+      else __hip_atomic_store((gu32*)(sync + 5), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // flushed: counters back to zero
+      __hip_atomic_store((gu32*)(sync + 3), a.g.B > 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -1984,6 +2143,63 @@ extern "C" int dr_ginet_train_step(const dr_graph_store* store, const dr_graph_d
   } else {
     DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_step_kernel<64>)));
     hipLaunchKernelGGL(ginet_step_kernel<64>, grid, dim3(NT), lds, (hipStream_t)stream, a);
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int dr_ginet_piped_step(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                                   const dr_ginet_weights* w, const dr_pass* pass, int32_t lds_bytes,
+                                   const dr_param_table* table, const dr_adam* adam, float* loss_out, uint32_t* sync,
+                                   int32_t prev_batch, float prev_loss_scale, int32_t alt_rows, void* stream) {
+  if (!store || !w || !pass || !table || !adam || !sync || n_batch < 0 || alt_rows < 1) return DR_E_ARG;
+  if (n_batch > 0 && !descs) return DR_E_ARG;
+  if (pass->out_dim < 1 || pass->out_dim > DR_MAX_OUT) return DR_E_UNSUPPORTED;
+  if (store->n_feat < 1 || 32 * store->n_feat > 2 * NT) return DR_E_UNSUPPORTED;  // F <= 64
+  if (lds_bytes > 160 * 1024) return DR_E_LDS;
+  if (n_batch > alt_rows || prev_batch < 0 || prev_batch > alt_rows) return DR_E_ARG;
+  if (pass->compute_dtype != DR_DTYPE_F32 || pass->slot) return DR_E_UNSUPPORTED;
+  if (pass->flags != (DR_PASS_FORWARD | DR_PASS_BACKWARD) || pass->loss_kind == DR_LOSS_NONE) return DR_E_ARG;
+  if (!pass->out || !pass->slab || !pass->head || !pass->loss_per_graph || !pass->step_counter) return DR_E_ARG;
+  if (pass->use_dropout == DR_DROPOUT_MASK && !pass->mask) return DR_E_ARG;
+  if (pass->use_dropout < DR_DROPOUT_OFF || pass->use_dropout > DR_DROPOUT_HASH) return DR_E_ARG;
+  if (!adam->enabled || adam->step_counter != pass->step_counter || adam->grad_div || adam->fault) return DR_E_ARG;
+  if (table->n_params > STEP_PARAMS || table->slab_stride != DR_SLAB_STRIDE(store->n_feat) ||
+      table->head_stride != DR_HEAD_STRIDE(pass->out_dim))
+    return DR_E_ARG;
+  if (!store->cl0) return DR_E_ARG;
+  GinetStepArgs a;
+  std::memset(&a, 0, sizeof(a));
+  // the pending update is the previous pass's: its batch size and loss scale
+  const int blocks = drr::build_reduce(table, pass->slab, pass->head, prev_batch, adam, pass->loss_per_graph,
+                                       prev_loss_scale, loss_out, a.h, a.rec);
+  if (blocks < 0) return blocks;
+  a.g.s = *store;
+  a.g.w = *w;
+  a.g.p = *pass;
+  a.g.descs = descs;
+  a.g.B = n_batch;
+  a.sync = sync;
+  {
+    static const char* env = std::getenv("DR_PIPED_NR");  // reducer workgroups (tuning; default 32)
+    const int want = env ? std::atoi(env) : 32;
+    a.NR = (blocks + 1) / 2 < want ? (blocks + 1) / 2 : (want > 0 ? want : 1);
+  }
+  a.alt_rows = alt_rows;
+  a.spin = pass->spin_limit > 0 ? pass->spin_limit : (1 << 22);
+  {
+    static const char* env = std::getenv("DR_STEP_DIAG");  // diagnostic timing switches (wrong results)
+    a.diag = env ? std::atoi(env) : 0;
+  }
+  if (a.NR < 1 || a.NR + n_batch > 224) return DR_E_UNSUPPORTED;  // one workgroup per CU, all co-resident
+  // the reducers' LDS scratch (2 x RC x RP floats) fits any pass carve
+  const int lds = lds_bytes > 2 * drr::RC * drr::RP * 4 ? lds_bytes : 2 * drr::RC * drr::RP * 4;
+  const dim3 grid(a.NR + n_batch);
+  if (store->n_feat <= 32) {
+    DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_piped_kernel<32>)));
+    hipLaunchKernelGGL(ginet_piped_kernel<32>, grid, dim3(NT), lds, (hipStream_t)stream, a);
+  } else {
+    DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_piped_kernel<64>)));
+    hipLaunchKernelGGL(ginet_piped_kernel<64>, grid, dim3(NT), lds, (hipStream_t)stream, a);
   }
   return (int)hipGetLastError();
 }

@@ -56,7 +56,10 @@ __device__ __forceinline__ void st_part(float* p, float v) {
 template <int NT, bool WT = false>
 __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds& t, const float (&fc1_row)[8],
                                            const float (&fc1_col)[8], float fc1_bias, int b, int OUT, float y_g,
-                                           uint64_t drop_offset, int stamp0 = -1) {
+                                           uint64_t drop_offset, int stamp0 = -1, int pb = -1) {
+  // pb: the row of the per-graph partials (loss term, head vectors) when it
+  // differs from the output row b (dr_ginet_piped_step's double buffer)
+  if (pb < 0) pb = b;
   int64_t* srow = (stamp0 >= 0 && p.stamps) ? p.stamps + (int64_t)b * 32 : nullptr;
   constexpr int NW = NT / 64;
   const int tid = threadIdx.x;
@@ -109,7 +112,7 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
   if (tid == 0) {
     if (p.loss_kind == DR_LOSS_MSE) {
       const float d = t.dout[0] - y_g;
-      if (p.loss_per_graph) st_part<WT>(p.loss_per_graph + b, d * d);
+      if (p.loss_per_graph) st_part<WT>(p.loss_per_graph + pb, d * d);
       t.dout[0] = 2.f * d * p.loss_scale;
       for (int q = 1; q < OUT; ++q) t.dout[q] = 0.f;  // the loss reads column 0 only (engine's layer path alike)
     } else if (p.loss_kind == DR_LOSS_CE) {
@@ -120,7 +123,7 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
       for (int q = 0; q < OUT; ++q) se += expf(t.dout[q] - mx);
       const float lse = mx + logf(se);
       const float wy = p.class_w ? p.class_w[yi] : 1.f;
-      if (p.loss_per_graph) st_part<WT>(p.loss_per_graph + b, wy * (lse - t.dout[yi]));
+      if (p.loss_per_graph) st_part<WT>(p.loss_per_graph + pb, wy * (lse - t.dout[yi]));
       for (int q = 0; q < OUT; ++q) t.dout[q] = wy * (expf(t.dout[q] - lse) - (q == yi ? 1.f : 0.f)) * p.loss_scale;
     } else {
       for (int q = 0; q < OUT; ++q) t.dout[q] = p.dout[(int64_t)b * OUT + q];
@@ -152,7 +155,7 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
   }
   {
     const int HS = DR_HEAD_STRIDE(OUT);
-    float* hg = p.head + (int64_t)b * HS;
+    float* hg = p.head + (int64_t)pb * HS;
     if (tid < 64) st_part<WT>(hg + tid, t.g[tid]);
     if (tid < 128) {
       st_part<WT>(hg + 64 + tid, t.hd[tid]);

@@ -81,9 +81,11 @@ __device__ __forceinline__ float ld_part(const float* p) {
 // WTP: the updated parameters are stored write-through (agent scope), for a
 // launch whose other workgroups read them after a grid-wide hand-off (the
 // reduce-at-start GINet step, ginet_fused.hip).
+// row_off: the partials of graph b sit at row row_off + b (slab: (row_off + b)
+// * slab_rows): the half of the pipelined step's double buffer.
 template <int LD, bool LEAN = false, bool WTP = false>
 __device__ __forceinline__ void reduce_block(const ReduceHdr& h, const ParamRec& r, int elem_block, bool first, int t,
-                                             float (*part)[RP], int64_t tstep) {
+                                             float (*part)[RP], int64_t tstep, int64_t row_off = 0) {
   // LEAN: partials always given, Adam always on (the one-launch step): the
   // gradients-supplied path is compiled out (less code to fetch cold)
   const int lp = t % RP, ch = t / RP;
@@ -95,7 +97,7 @@ __device__ __forceinline__ void reduce_block(const ReduceHdr& h, const ParamRec&
   const bool bad = fv != 0u;
   if (first && t < 64 && h.lpg && h.loss_out) {
     float acc = 0.f;  // lane-strided partial sums, then a fixed-order wave reduction
-    for (int b = t; b < h.B; b += 64) acc += ld_part<LD>(h.lpg + b);
+    for (int b = t; b < h.B; b += 64) acc += ld_part<LD>(h.lpg + row_off + b);
     acc = dr_wave_sum(acc);
     if (t == 0) h.loss_out[0] = bad ? __builtin_nanf("") : acc * h.loss_scale;
   } else if (bad && first && t == 0 && h.loss_out) {
@@ -104,8 +106,8 @@ __device__ __forceinline__ void reduce_block(const ReduceHdr& h, const ParamRec&
   const int ec = live ? e : 0;
   const bool slab_kind = r.kind == DR_GRAD_SLAB, outer = r.kind == DR_GRAD_OUTER;
   const bool has_src = h.slab && (slab_kind || outer || r.kind == DR_GRAD_HEAD);
-  const float* base = slab_kind ? h.slab : h.head;
   const int64_t st = slab_kind ? h.slab_stride : h.head_stride;
+  const float* base = (slab_kind ? h.slab : h.head) + row_off * (slab_kind ? h.slab_rows : 1) * st;
   const int col1 = outer ? r.off1 + ec / r.cols : r.off1 + ec;
   const int col2 = outer ? r.off2 + ec % r.cols : 0;
   const int nb = slab_kind ? h.B * h.slab_rows : h.B;  // rows of this gradient's partials

@@ -173,9 +173,8 @@ class PassC(ctypes.Structure):
         ("step_counter", VP),
         ("fault", VP),
         ("spin_limit", ctypes.c_int32),
-        ("prefetch_n", ctypes.c_int32),
+        ("pad0", ctypes.c_int32),
         ("slot", VP),
-        ("prefetch_descs", VP),
     ]
 
 
@@ -252,6 +251,7 @@ SIGNATURES = [
     ("dr_reduce_update", ctypes.c_int, [ctypes.POINTER(ParamTableC), VP, VP, ctypes.c_int32, ctypes.POINTER(AdamC), VP, ctypes.c_float, VP, VP]),
     ("dr_ginet_train_step", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, ctypes.POINTER(ParamTableC), ctypes.POINTER(AdamC), VP, VP, VP]),
     ("dr_ginet_ras_step", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, ctypes.POINTER(ParamTableC), ctypes.POINTER(AdamC), VP, VP, ctypes.c_int32, ctypes.c_float, VP]),
+    ("dr_ginet_piped_step", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, ctypes.POINTER(ParamTableC), ctypes.POINTER(AdamC), VP, VP, ctypes.c_int32, ctypes.c_float, ctypes.c_int32, VP]),
     ("dr_csr_from_coo", ctypes.c_int, [VP, VP, ctypes.c_int64, ctypes.c_int32, VP, VP, VP, VP, VP]),
     ("dr_spmm_csr", ctypes.c_int, [VP, VP, VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP, VP]),
     ("dr_spmm_csr_w", ctypes.c_int, [VP, VP, VP, VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP, VP]),

@@ -99,6 +99,15 @@ class FusedTrainStep:
         # lags one step and flush() applies the last update (sync[3]: pending)
         self.ras = False
         self._ras_last = None  # (B, loss scale) of the pending pass
+        # pipelined step (GINet, world of one; dr_ginet_piped_step): launch s =
+        # the update of pass s-1 (its own reducer workgroups) beside pass s,
+        # whose workgroups wait for that update only right before they read a
+        # weight; one launch per step, partials double-buffered, loss_out lags
+        # one step, flush() applies the last update.  Captured sweeps and
+        # epochs (bench.py, epoch.EpochRunner) turn it on for their steps.
+        self.piped = False
+        self._piped_last = None  # (B, loss scale) of the pending pass
+        self._piped_store = None
         # models whose graph pass reads its weights from a packed copy
         # (VanillaNetwork: MFMA-fragment order): one copy per step object,
         # rewritten by Adam as it updates the parameters (dr_adam.mirror), so
@@ -112,12 +121,6 @@ class FusedTrainStep:
         if getattr(model, "_drop_seed", 0) is None:
             model._drop_seed = int(torch.randint(0, 2**62, (1,)).item())
         self._cap = 0
-        # the batch the NEXT step trains on, when the caller knows it (captured
-        # sweeps and epochs): the GINet graph pass then reads those graphs into
-        # L2 from its idle waves (dr_pass.prefetch_descs; a hint, the results
-        # are the same without it).  Consumed by the next step().
-        self.prefetch_next = None
-        self.prefetch = True
         self._ensure(max_batch)
 
     # ---- persistent C structs (built once; a step makes two ctypes calls) ----
@@ -126,9 +129,11 @@ class FusedTrainStep:
             return
         f = self.model.input_shape
         dev = self.device
-        self.slab = torch.empty(b * self.spec.slab_stride(f), dtype=torch.float32, device=dev)
-        self.head = torch.zeros(b * self.spec.head_stride(self.out_dim), dtype=torch.float32, device=dev)
-        self.lpg = torch.empty(b, dtype=torch.float32, device=dev)
+        # two halves of b rows each: the pipelined step's double buffer (the
+        # other paths use the first half)
+        self.slab = torch.empty(2 * b * self.spec.slab_stride(f), dtype=torch.float32, device=dev)
+        self.head = torch.zeros(2 * b * self.spec.head_stride(self.out_dim), dtype=torch.float32, device=dev)
+        self.lpg = torch.empty(2 * b, dtype=torch.float32, device=dev)
         self.out = torch.empty(b, self.out_dim, dtype=torch.float32, device=dev)
         self._cap = b
         self._build_structs()
@@ -239,6 +244,8 @@ class FusedTrainStep:
         Dropout (ginet.py:122): ``mask`` (uint8 [B,128]) if given, else the
         in-kernel hash RNG (offset = the device step counter) when ``dropout``
         and the model's p > 0."""
+        if self._piped_last is not None and (h.B > self._cap or not self._piped_fits(h)):
+            self.flush()  # the pipelined step's pending update first: the other paths reuse the partials
         if self._ras_last is not None and (h.B > self._cap or not (self.pg is None and self.ras and self.one_launch(h) and not (self.spec.layers is not None and layered.needs_layers(self.spec, h, self.out_dim)))):
             # reduce-at-start: this step takes another path (or regrows the
             # partial buffers), so the pending update is applied first (the
@@ -260,15 +267,18 @@ class FusedTrainStep:
         else:
             p = self._pass if (dropout and self.spec.dropout > 0 and self.model.dropout > 0) else self._pass_nodrop
         p.loss_scale = scale
-        nxt, self.prefetch_next = self.prefetch_next, None
-        if nxt is not None and self.prefetch and nxt.descs is not None:
-            p.prefetch_descs, p.prefetch_n = nxt.descs.data_ptr(), nxt.B
-        else:
-            p.prefetch_descs, p.prefetch_n = None, 0
         ev = self.kernel_events
         if ev is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
+        if self._piped_fits(h):
+            self._launch_piped(h, p, scale)
+            if ev is not None:
+                e1.record()
+                ev.append((e0, e1))
+            self._piped_last = (h.B, scale)
+            self.step_count += 1
+            return self.loss_out, self.out[: h.B]
         if self.pg is None and self.ras and launch_step(self.spec, h, self._w, p, self._table, self._adam_ras, self.loss_out, self.sync, entry="dr_ginet_ras_step", prev=self._ras_last):
             if ev is not None:
                 e1.record()
@@ -303,10 +313,47 @@ class FusedTrainStep:
             self._adam_after_allreduce()
         return self.loss_out, self.out[: h.B]
 
+    def _piped_fits(self, h: BatchHandle) -> bool:
+        """The pipelined step takes this batch: GINet's per-graph kernel, one
+        process, fp32, reducers + graph workgroups co-resident."""
+        if not self.piped or self.pg is not None or self.spec.entry != "dr_ginet_graph_pass" or self.compute_dtype != "f32" or self.fuse_update or self.ras:
+            return False
+        if h.nonfinite or h.B > self._cap or h.B + self._reduce_nr() > 224:  # noqa: PLR2004
+            return False
+        return step_fits(self.spec, h, _lib.DR_DTYPE_F32, self.out_dim) and not (self.spec.layers is not None and layered.needs_layers(self.spec, h, self.out_dim))
+
+    def _reduce_nr(self):
+        """Reducer workgroups of the pipelined step (two reduce blocks of 64
+        parameter elements each, at most DR_PIPED_NR = 32 workgroups)."""
+        import os  # noqa: PLC0415
+
+        blocks = sum((p.numel() + 63) // 64 for p in self.params)
+        want = int(os.environ.get("DR_PIPED_NR", "32"))
+        return min((blocks + 1) // 2, max(want, 1))
+
+    def _launch_piped(self, h, p, scale, flush=False):
+        from deeprank2_amd.fused import lds_for  # noqa: PLC0415
+
+        prev = self._piped_last or (0, 1.0)
+        self._table.slab_rows = 1
+        lds = lds_for(self.spec, h, p.out_dim) if h is not None else 0
+        rc = _lib.load().dr_ginet_piped_step(
+            (h.store.cstruct() if h is not None else self._piped_store), None if h is None else h.descs.data_ptr(), 0 if h is None else h.B, self._w, p, lds,
+            self._table, self._adam_ras, self.loss_out.data_ptr(), self.sync.data_ptr(), prev[0], prev[1], self._cap, _lib.stream_ptr(self.device))
+        _lib.check(rc, "dr_ginet_piped_step")
+        if h is not None:
+            self._piped_store = h.store.cstruct()
+
     def flush(self):
-        """Reduce-at-start mode: apply the last launch's pending update
-        (dr_reduce_update over its partials, the arithmetic every RAS launch
-        uses) and clear the pending flag; a no-op otherwise."""
+        """Reduce-at-start / pipelined mode: apply the last launch's pending
+        update (the arithmetic every such launch uses) and clear the pending
+        flag; a no-op otherwise.  (Pipelined: one launch of the reducers alone,
+        no host synchronisation; capturable.)"""
+        if self._piped_last is not None:
+            p = self._pass_nodrop
+            p.loss_scale = self._piped_last[1]
+            self._launch_piped(None, p, self._piped_last[1], flush=True)
+            self._piped_last = None
         if self._ras_last is None or int(self.sync[3].item()) == 0:
             self._ras_last = None
             return
@@ -344,11 +391,11 @@ class FusedTrainStep:
         same point): the per-rank counts are SUM-all-reduced first, so all ranks
         raise together instead of the faulting rank alone while the others
         block in their next collective."""
-        if (self.fuse_update or self.ras) and int(self.sync[2].item()):
+        if (self.fuse_update or self.ras or self.piped) and int(self.sync[2].item()):
             if reset:
                 self.sync[2].zero_()
-            msg = ("a reduce-at-start step's grid hand-off gave up waiting (some workgroups ran their pass on a mix of old and new parameters)"
-                   if self.ras else "a one-launch training step's reducer gave up waiting for the graph workgroups: that step's update was skipped")
+            msg = ("a reduce-at-start / pipelined step's hand-off gave up waiting (some workgroups ran their pass on a mix of old and new parameters)"
+                   if (self.ras or self.piped) else "a one-launch training step's reducer gave up waiting for the graph workgroups: that step's update was skipped")
             raise RuntimeError(msg)
         if not self.handoffs:
             return
@@ -457,9 +504,7 @@ class FusedTrainStep:
         torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            for i, h in enumerate(handles):
-                # replays run back to back: after the last step comes the first
-                self.prefetch_next = handles[(i + 1) % len(handles)]
+            for h in handles:
                 self.step(h, global_batch=global_batch)
         torch.cuda.synchronize(self.device)
         for t, s in zip(self._state_tensors(), snap):
@@ -470,6 +515,8 @@ class FusedTrainStep:
     def one_launch(self, h: BatchHandle) -> bool:
         """True when ``step(h)`` is a single kernel launch (``dr_ginet_train_step``)."""
         cd = _lib.DR_DTYPE_BF16 if self.compute_dtype == "bf16" else _lib.DR_DTYPE_F32
+        if self._piped_fits(h):
+            return True
         return self.pg is None and (self.fuse_update or (self.ras and h.B <= 256)) and not h.nonfinite and step_fits(self.spec, h, cd, self.out_dim)
 
     def time_graph_pass(self, handles, n_launches, global_batch=None):
@@ -494,11 +541,7 @@ class FusedTrainStep:
                     self.step(h, global_batch=global_batch)
                     continue
                 p.loss_scale = self.loss_scale(h, global_batch or h.B * self.world)
-                nxt = handles[(i + 1) % len(handles)]  # as in a captured sweep
-                if self.prefetch and nxt.descs is not None:
-                    p.prefetch_descs, p.prefetch_n = nxt.descs.data_ptr(), nxt.B
                 launch(self.spec, h, self._w, p)
-                p.prefetch_descs, p.prefetch_n = None, 0
 
         passes(len(handles))  # warm-up: LDS attributes, plans
         torch.cuda.synchronize(self.device)

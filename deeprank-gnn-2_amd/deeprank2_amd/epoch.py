@@ -96,6 +96,12 @@ def eligible(step, store) -> bool:
 class EpochRunner:
     """The fused steps of one epoch's batches (sizes ``sizes``, in order) as one HIP graph."""
 
+    # GINet in a world of one: the epoch's steps as pipelined launches
+    # (FusedTrainStep.piped, dr_ginet_piped_step: each launch runs the previous
+    # step's update beside its pass; the epoch ends with the last update).
+    # Measured slower (DESIGN §5): off.
+    piped = False
+
     def __init__(self, step, store, sizes, global_sizes=None):
         self.step, self.store = step, store
         self.sizes = [int(s) for s in sizes]
@@ -120,18 +126,25 @@ class EpochRunner:
         reduce's loss pointer redirected per step: no copy launches)."""
         s = self.step
         passes = (s._pass, s._pass_nodrop)  # noqa: SLF001
-        saved = [p.out for p in passes], s.loss_out
+        saved = [p.out for p in passes], s.loss_out, s.piped
+        s.piped = self.piped and s.pg is None
         try:
             for k, (h, o, b) in enumerate(zip(self.handles, self.offs[:-1], self.sizes)):
                 for p in passes:
                     p.out = self.out[o : o + b].data_ptr()
-                s.loss_out = self.loss[k : k + 1]
-                s.prefetch_next = self.handles[k + 1] if k + 1 < len(self.handles) else None
+                # a pipelined launch reports the PREVIOUS step's loss (its
+                # reducers apply that step's update)
+                lag = s._piped_fits(h)  # noqa: SLF001
+                s.loss_out = self.loss[k - 1 : k] if (lag and k > 0) else self.loss[k : k + 1]
                 s.step(h, global_batch=self.global_sizes[k])
+            if s._piped_last is not None:  # noqa: SLF001  (the epoch's last update, and its loss)
+                s.loss_out = self.loss[len(self.sizes) - 1 :]
+                s.flush()
         finally:
             for p, v in zip(passes, saved[0]):
                 p.out = v
             s.loss_out = saved[1]
+            s.piped = saved[2]
 
     def _load(self, order):
         self.pin.copy_(torch.from_numpy(np.asarray(order, dtype=np.int64)))

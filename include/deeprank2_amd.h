@@ -197,19 +197,13 @@ typedef struct dr_pass {
                            ticket); otherwise one give-up stays set and every later step is
                            withheld with a NaN loss.                                      */
   int32_t spin_limit;   /* polls before a hand-off wait gives up (<= 0: 1 << 22)        */
-  int32_t prefetch_n;   /* entries of prefetch_descs (0: no prefetch)                    */
+  int32_t pad0;
   const int32_t* slot;  /* optional device [B] (GINet / FoutNet / SGAT passes): launch position b
                            writes row slot[b] of out, loss_per_graph, slab, head and reads row
                            slot[b] of dout / mask, and draws dropout unit slot[b] -- a batch run
                            as several launches (graphs that fit one workgroup's LDS on the
                            per-graph kernel, the others on the large-graph path) fills the rows
                            one launch over the whole batch would                          */
-  const struct dr_graph_desc* prefetch_descs;
-                        /* optional device [prefetch_n] (dr_ginet_graph_pass): the NEXT step's
-                           batch.  Workgroup b's idle waves read graph b of it into their XCD's
-                           L2 during the front half (the same block index lands on the same
-                           XCD next launch), so the next pass stages from L2.  A hint: the
-                           results do not depend on it.                                    */
 } dr_pass;
 
 /* One workgroup per graph: conv1 -> depth-0 community pooling -> conv2 ->
@@ -660,6 +654,27 @@ int dr_ginet_train_step(const dr_graph_store* store, const dr_graph_desc* descs,
  * update is pending.  loss_out lags one step.  Parameters after K launches +
  * that flush are bit-identical to K dr_ginet_graph_pass + dr_reduce_update
  * steps.                                                                     */
+/* Pipelined GINet step (world of one; replaces trainer.py:686-690 for one
+ * mini-batch like dr_ginet_graph_pass + dr_reduce_update, one launch per step):
+ * launch s runs the Adam update of pass s-1 (NR reducer workgroups, the
+ * fixed-order arithmetic of dr_reduce_update, parameters stored write-through)
+ * beside pass s (n_batch graph workgroups).  A pass workgroup stages its graph
+ * and gathers its first tile while the reducers run, and each wave waits for
+ * the published update (sync[5], bounded: a give-up sets sync[2]) only right
+ * before it reads a weight.  The partials are double-buffered: slab, head and
+ * loss_per_graph hold 2 x alt_rows rows; pass s writes half s & 1, its update
+ * reads it in the next launch.  sync: device uint32 [8], zero when allocated
+ * ([3] pending, [4] finished workgroups, [5] updates applied, [6] reducer
+ * tickets).  prev_batch / prev_loss_scale: the pending update's pass.
+ * n_batch 0: the update alone (the flush after the last pass).  loss_out lags
+ * one launch.  Needs NR + n_batch <= 224 (NR = half the reduce blocks) and no
+ * dr_pass.slot / dr_adam.fault; parameters, moments, gradients and loss terms
+ * are bit-identical to the two-launch steps.                                  */
+int dr_ginet_piped_step(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                        const dr_ginet_weights* w, const dr_pass* pass, int32_t lds_bytes,
+                        const dr_param_table* table, const dr_adam* adam, float* loss_out, uint32_t* sync,
+                        int32_t prev_batch, float prev_loss_scale, int32_t alt_rows, void* stream);
+
 int dr_ginet_ras_step(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
                       const dr_ginet_weights* w, const dr_pass* pass, int32_t lds_bytes,
                       const dr_param_table* table, const dr_adam* adam, float* loss_out, uint32_t* sync,

@@ -42,7 +42,7 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_lib.GinetWeightsC) == 8 * 8
     assert ctypes.sizeof(_lib.FoutWeightsC) == 10 * 8
     assert ctypes.sizeof(_lib.LargePlanC) == 3 * 8 + 16 + 3 * 8 + 7 * 8 + 8  # ... part_key, arrive
-    assert ctypes.sizeof(_lib.PassC) == 16 + 8 + 16 + 8 + 9 * 8 + 8 + 8 + 8 + 8  # + fault, spin_limit/prefetch_n, slot, prefetch_descs
+    assert ctypes.sizeof(_lib.PassC) == 16 + 8 + 16 + 8 + 9 * 8 + 8 + 8 + 8  # + fault, spin_limit, slot
     assert ctypes.sizeof(_lib.AdamC) == 32 + 8 + 8 + 8 + 4 * 8  # + grad_div, fault, mirror, mirror_idx, fault_clear, ticket
     assert ctypes.sizeof(_lib.MclGraphsC) == 10 * 8
     assert ctypes.sizeof(_lib.VanillaScratchC) == 6 * 8 + 8 + 3 * 8 + 7 * 8 + 16 + 2 * 8 + 8 + 8 + 8  # ... tile plan, tile_wc, tile_first, tile_meta, part_mean

@@ -157,3 +157,50 @@ def test_reduce_at_start_pending_update_flushed_before_other_paths():
         for name in ("exp_avg", "exp_avg_sq"):
             assert torch.equal(sd1["state"][k][name], sd2["state"][k][name]), (k, name)
     _assert_same(one, two, "after B > 256 steps and the optimizer-state flush")
+
+
+def _piped_pair():
+    one, two = _pair()
+    one.fuse_update = False
+    one.piped = True
+    return one, two
+
+
+@pytest.mark.parametrize("sizes", [(64, 64, 64, 64, 64), (7, 1, 130, 64, 200, 33)])
+def test_piped_step_bit_identical_after_flush(sizes):
+    """dr_ginet_piped_step: launch t runs step t-1's reduce + Adam on its own
+    reducer workgroups beside pass t, whose waves wait for that update only
+    right before reading a weight; partials double-buffered.  Every step's
+    outputs equal the two-launch step's and after the flush the parameters,
+    moments, gradients, loss and step counter are bit-identical; a batch the
+    pipelined launch cannot take (B = 200: reducers + graph workgroups over
+    224) runs the regular step after flushing the pending update."""
+    store = GraphStore(pack_graphs(_records(256, 37)), DEV)
+    one, two = _piped_pair()
+    rng = np.random.default_rng(3)
+    for i, b in enumerate(sizes):
+        h = BatchHandle(store, rng.permutation(256)[:b].astype(np.int32))
+        _l1, o1 = one.step(h)
+        _l2, o2 = two.step(h)
+        torch.cuda.synchronize()
+        assert torch.equal(o1, o2), f"outputs step {i} (B={b})"
+    one.flush()
+    torch.cuda.synchronize()
+    _assert_same(one, two, "pipelined steps after the flush")
+
+
+def test_piped_steps_replay_from_hip_graph():
+    """Captured sweeps of pipelined steps replayed back to back (the update of
+    each sweep's last pass runs in the next replay's first launch), flushed at
+    the end: bit-identical to eager two-launch steps."""
+    store = GraphStore(pack_graphs(_records(192, 38)), DEV)
+    one, two = _piped_pair()
+    hs = [BatchHandle(store, np.arange(k * 64, k * 64 + 64, dtype=np.int32)) for k in range(3)]
+    g = one.capture_sweep(hs)
+    for _ in range(3):
+        g.replay()
+        for h in hs:
+            two.step(h)
+    one.flush()
+    torch.cuda.synchronize()
+    _assert_same(one, two, "captured pipelined steps + flush vs eager two-launch steps")
