@@ -482,6 +482,16 @@ def trainer_bench(args):
         t_pack = time.perf_counter() - t0
         cores, affinity = host_cores()
         load = {"graphs": n, "hdf5_write_s": round(t_write, 3), "dataset_init_s": round(t_index, 3), "graph_store_s": round(t_pack, 3), "graphs_per_s": round(n / (t_index + t_pack), 1), "cores": cores, "graphs_per_s_per_core": round(n / (t_index + t_pack) / cores, 1), "reference_graphs_per_s_per_core": 400, "note": "GraphDataset(HDF5) construction (file read, index, feature checks) + graph_store (per-entry arrays, threaded C++ pack, H2D) for the whole file; the reference reads one entry per item (dataset.py:883-1052, ~2.5 ms/graph/core, SURVEY §6)"}
+        # the same host-side load on ONE core (a child pinned to one CPU,
+        # OMP_NUM_THREADS=1: one HDF5 worker, one packer thread, no upload)
+        try:
+            cpu = sorted(os.sched_getaffinity(0))[0]
+            env = dict(os.environ, OMP_NUM_THREADS="1")
+            r = subprocess.run([sys.executable, "-c", f"import os, runpy, sys; os.sched_setaffinity(0, {{{cpu}}}); sys.argv = ['load_one_core.py', {path!r}]; runpy.run_path({os.path.join(ROOT, 'tools', 'load_one_core.py')!r}, run_name='__main__')"], capture_output=True, text=True, env=env, timeout=600, check=False)
+            one = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+            load["one_core"] = {**one, "note": "GraphDataset + per-entry arrays + C++ pack on one pinned CPU (tools/load_one_core.py): graphs/s on one core, the reference's per-core unit"}
+        except Exception as e:  # noqa: BLE001  (diagnostic only)
+            load["one_core"] = {"error": str(e)[:200]}
         del store
         torch.manual_seed(1234)
         mem = MemoryOutputExporter()

@@ -700,9 +700,6 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
 #pragma unroll
     for (int j = 0; j < 8; ++j) fc1_col[j] = ldw(a.w.fc1w + (rcc * 8 + j) * 64 + o);
   };
-#ifdef DR_FC1_EARLY  // A/B diagnostic: the r04 order (fc1 before the graph DMA)
-  if (!RAS) load_fc1();
-#endif
   const float y_g = s.y[g];
   uint64_t drop_offset = a.p.drop_offset;
   dma_x4(sX, s.x + n0 * (int64_t)XS, N * XS / 4);
@@ -761,11 +758,9 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
       if (p < nf) wfc[u] = ldw(a.w.fc2w + p);
       else if (p < nf + OUT) wfc[u] = ldw(a.w.fc2b + p - nf);
     }
-    // (fc1 is loaded after the front half, below: its 17 registers would
-    // otherwise be held through the gather loop)
-#ifdef DR_FC1_EARLY
-    if (PIPED) load_fc1();
-#endif
+    // fc1 last: the wait for W2 / fc2 before their LDS stores (end of the
+    // front half) then leaves these 11 loads in flight (vmcnt counts in order)
+    if (!RAS) load_fc1();
   };
   if (!PIPED) load_head_weights();
   // ---------------- conv1 + depth-0 pooling, one 16-row tile per wave -------
@@ -815,11 +810,7 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
         const int eb1 = i1 < N ? srp[i1] : 0, ee1 = i1 < N ? srp[i1 + 1] : 0;
         for (int ch = sub; ch < nch; ch += 8) {
           float4 z0, z1;
-#ifdef DR_GATHER_PIPE
-          drk::gather_two_row_chunks_pipe(scol, eb0, ee0, eb1, ee1, sX, XS, ch * 4, z0, z1);
-#else
           drk::gather_two_row_chunks(scol, eb0, ee0, eb1, ee1, sX, XS, ch * 4, z0, z1);
-#endif
           if (i0 < N) {
             float* zr = sZ + i0 * LDW + ch * 4;
             zr[0] = z0.x;
@@ -909,11 +900,6 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
   STAMP(2);
   __syncthreads();
   STAMP(3);
-#ifndef DR_FC1_EARLY
-  // the head's fc1 registers: issued now, first read by the head ~4 K cycles
-  // later (conv2, the depth-1 pool and the mean run in between)
-  if (!RAS) load_fc1();
-#endif
   typedef __attribute__((address_space(1))) unsigned long long gu64s;
   typedef __attribute__((address_space(1))) unsigned int gu32s;
   if (SIB) {

@@ -124,69 +124,6 @@ __device__ __forceinline__ void gather_two_row_chunks(const uint16_t* col, int e
   out1 = a1;
 }
 
-// gather_two_row_chunks with the joint loop software-pipelined: the next
-// step's eight column ids are read while this step's eight rows are in
-// flight, so a step costs one LDS round trip instead of two (index, then
-// rows).  Same edges, same order, same sums.
-__device__ __forceinline__ void gather_two_row_chunks_pipe(const uint16_t* col, int eb0, int ee0, int eb1, int ee1,
-                                                           const float* X, int XS, int c4, float4& out0, float4& out1) {
-  float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
-  int e0 = eb0, e1 = eb1;
-  const int q0 = (ee0 - eb0) >> 2, q1 = (ee1 - eb1) >> 2;
-  const int n = q0 < q1 ? q0 : q1;  // joint steps of four edges per row
-  if (n > 0) {
-    int f1 = e0 + 1, f2 = e0 + 2, f3 = e0 + 3, g1 = e1 + 1, g2 = e1 + 2, g3 = e1 + 3;
-    asm volatile("" : "+v"(f1), "+v"(f2), "+v"(f3), "+v"(g1), "+v"(g2), "+v"(g3));
-    int j0 = col[e0], j1 = col[f1], j2 = col[f2], j3 = col[f3];
-    int k0 = col[e1], k1 = col[g1], k2 = col[g2], k3 = col[g3];
-    for (int it = 0; it < n; ++it) {
-      const float4 v0 = *reinterpret_cast<const float4*>(&X[__umul24(j0, XS) + c4]);
-      const float4 v1 = *reinterpret_cast<const float4*>(&X[__umul24(j1, XS) + c4]);
-      const float4 v2 = *reinterpret_cast<const float4*>(&X[__umul24(j2, XS) + c4]);
-      const float4 v3 = *reinterpret_cast<const float4*>(&X[__umul24(j3, XS) + c4]);
-      const float4 w0 = *reinterpret_cast<const float4*>(&X[__umul24(k0, XS) + c4]);
-      const float4 w1 = *reinterpret_cast<const float4*>(&X[__umul24(k1, XS) + c4]);
-      const float4 w2 = *reinterpret_cast<const float4*>(&X[__umul24(k2, XS) + c4]);
-      const float4 w3 = *reinterpret_cast<const float4*>(&X[__umul24(k3, XS) + c4]);
-      e0 += 4;
-      e1 += 4;
-      if (it + 1 < n) {  // the next step's ids, in flight under this step's rows
-        int h1 = e0 + 1, h2 = e0 + 2, h3 = e0 + 3, i1 = e1 + 1, i2 = e1 + 2, i3 = e1 + 3;
-        asm volatile("" : "+v"(h1), "+v"(h2), "+v"(h3), "+v"(i1), "+v"(i2), "+v"(i3));
-        j0 = col[e0], j1 = col[h1], j2 = col[h2], j3 = col[h3];
-        k0 = col[e1], k1 = col[i1], k2 = col[i2], k3 = col[i3];
-      }
-      a0 = f4add(f4add(f4add(f4add(a0, v0), v1), v2), v3);
-      a1 = f4add(f4add(f4add(f4add(a1, w0), w1), w2), w3);
-    }
-  }
-  // the rest of each row on its own (4 edges in flight, then singles)
-  for (; e0 + 4 <= ee0; e0 += 4) {
-    int f1 = e0 + 1, f2 = e0 + 2, f3 = e0 + 3;
-    asm volatile("" : "+v"(f1), "+v"(f2), "+v"(f3));
-    const int j0 = col[e0], j1 = col[f1], j2 = col[f2], j3 = col[f3];
-    const float4 v0 = *reinterpret_cast<const float4*>(&X[__umul24(j0, XS) + c4]);
-    const float4 v1 = *reinterpret_cast<const float4*>(&X[__umul24(j1, XS) + c4]);
-    const float4 v2 = *reinterpret_cast<const float4*>(&X[__umul24(j2, XS) + c4]);
-    const float4 v3 = *reinterpret_cast<const float4*>(&X[__umul24(j3, XS) + c4]);
-    a0 = f4add(f4add(f4add(f4add(a0, v0), v1), v2), v3);
-  }
-  for (; e1 + 4 <= ee1; e1 += 4) {
-    int g1 = e1 + 1, g2 = e1 + 2, g3 = e1 + 3;
-    asm volatile("" : "+v"(g1), "+v"(g2), "+v"(g3));
-    const int k0 = col[e1], k1 = col[g1], k2 = col[g2], k3 = col[g3];
-    const float4 w0 = *reinterpret_cast<const float4*>(&X[__umul24(k0, XS) + c4]);
-    const float4 w1 = *reinterpret_cast<const float4*>(&X[__umul24(k1, XS) + c4]);
-    const float4 w2 = *reinterpret_cast<const float4*>(&X[__umul24(k2, XS) + c4]);
-    const float4 w3 = *reinterpret_cast<const float4*>(&X[__umul24(k3, XS) + c4]);
-    a1 = f4add(f4add(f4add(f4add(a1, w0), w1), w2), w3);
-  }
-  for (; e0 < ee0; ++e0) a0 = f4add(a0, *reinterpret_cast<const float4*>(&X[__umul24((int)col[e0], XS) + c4]));
-  for (; e1 < ee1; ++e1) a1 = f4add(a1, *reinterpret_cast<const float4*>(&X[__umul24((int)col[e1], XS) + c4]));
-  out0 = a0;
-  out1 = a1;
-}
-
 // As gather_two_row_chunks with the column ids pre-scaled to byte offsets of
 // X rows (col[e] = j * XS * 4, so rows up to 64 KiB into X): one add per edge
 // and lane forms the address (same sums, same order).

@@ -223,7 +223,7 @@ def nonfinite_graphs(x, node_off, edge_attr=None, edge_off=None) -> np.ndarray:
     G = node_off.size - 1
     bad = np.zeros(G, bool)
     for a, off in ((x, node_off), (edge_attr, edge_off)):
-        if a is None or a.size == 0:
+        if a is None or a.size == 0 or np.isfinite(a).all():  # (one flat pass: the common, finite case)
             continue
         rows = np.flatnonzero(~np.isfinite(a.reshape(a.shape[0], -1)).all(axis=1))
         if rows.size:
