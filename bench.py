@@ -394,6 +394,7 @@ def parse_args(argv):
     ap.add_argument("--mixed-dispatch", action="store_true", help="mixed batches: graphs that fit LDS on the per-graph kernel, the rest on the large path, two streams (opt-in, measured slower)")
     ap.add_argument("--one-launch", action="store_true", help="GINet, N=1: graph pass + gradient reduce + Adam in one launch (dr_ginet_train_step; opt-in, measured slower at B=64)")
     ap.add_argument("--piped", action="store_true", help="GINet, N=1: pipelined step (dr_ginet_piped_step: each launch runs the previous pass's update on its own workgroups beside this pass, which waits for it only before reading a weight)")
+    ap.add_argument("--acc", choices=["auto", "on", "off"], default="auto", help="GINet fp32: accumulating pass (dr_ginet_acc_pass: each workgroup sums every R-th graph's gradients on chip, one partial row per workgroup); auto = batches past the CU count")
     ap.add_argument("--ras", action="store_true", help="GINet, N=1: reduce-at-start step (dr_ginet_ras_step: each launch applies the previous update, then runs its pass; opt-in experiment)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stream-copy", action="store_true")
@@ -665,6 +666,7 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
     step.fuse_update = bool(args.one_launch)
     step.ras = bool(args.ras) and pg is None
     step.piped = bool(args.piped) and pg is None
+    step.acc = {"auto": None, "on": True, "off": False}[args.acc]
 
     def run_eager(i):
         return step.step(handles[i % len(handles)], global_batch=B * world)
@@ -821,7 +823,7 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(graphs[:B], model_name=args.model)
         workload = WORKLOADS.get((args.model, args.graphs), f"{args.model} on {args.graphs} graphs (diagnostic)")
-        kname = "layer-level path (FoutLayer/SGAT/GINetConvLayer + pooling kernels, torch autograd): whole-step wall clock" if layer_path else {"ginet": ("ginet_onepass_kernel (dr_ginet_large_pass, one launch)" if args.ginet_path == "onepass" else "ginet_large_conv1_kernel + ginet_large_tail_kernel (dr_ginet_large_pass)") if large else (("ginet_piped_kernel (dr_ginet_piped_step: the previous pass's gradient reduce + Adam on its own workgroups beside this pass's fwd+loss+bwd, 1 workgroup/graph, which waits for the update only before reading a weight)" if args.piped else "ginet_ras_kernel (dr_ginet_ras_step: the previous step's gradient reduce + Adam, a grid hand-off, then fwd+loss+bwd, 1 workgroup/graph)" if args.ras else "ginet_step_kernel (dr_ginet_train_step: fwd+loss+bwd, 1 workgroup/graph, then gradient reduce + Adam by the last 64 workgroups)") if one else "ginet_graph_kernel (dr_ginet_graph_pass, fwd+loss+bwd, 1 workgroup/graph)"), "foutnet": "fout_graph_kernel<false> (dr_fout_graph_pass)", "vanilla": "vanilla_graph_kernel (dr_vanilla_fused_pass) / vanilla pipeline (dr_vanilla_graph_pass)", "sgat": "fout_graph_kernel<true> (dr_sgat_graph_pass)", "ginet_nocluster": "ginet_nocluster_kernel (dr_ginet_nocluster_graph_pass)"}[args.model]
+        kname = "layer-level path (FoutLayer/SGAT/GINetConvLayer + pooling kernels, torch autograd): whole-step wall clock" if layer_path else {"ginet": ("ginet_onepass_kernel (dr_ginet_large_pass, one launch)" if args.ginet_path == "onepass" else "ginet_large_conv1_kernel + ginet_large_tail_kernel (dr_ginet_large_pass)") if large else (("ginet_piped_kernel (dr_ginet_piped_step: the previous pass's gradient reduce + Adam on its own workgroups beside this pass's fwd+loss+bwd, 1 workgroup/graph, which waits for the update only before reading a weight)" if args.piped else "ginet_ras_kernel (dr_ginet_ras_step: the previous step's gradient reduce + Adam, a grid hand-off, then fwd+loss+bwd, 1 workgroup/graph)" if args.ras else "ginet_step_kernel (dr_ginet_train_step: fwd+loss+bwd, 1 workgroup/graph, then gradient reduce + Adam by the last 64 workgroups)") if one else (f"ginet_acc_kernel (dr_ginet_acc_pass: {step._acc_rows(handles[0])} workgroups, each runs every R-th graph's fwd+loss+bwd and sums its gradients on chip; one partial row per workgroup)" if step._acc_rows(handles[0]) else "ginet_graph_kernel (dr_ginet_graph_pass, fwd+loss+bwd, 1 workgroup/graph)")), "foutnet": "fout_graph_kernel<false> (dr_fout_graph_pass)", "vanilla": "vanilla_graph_kernel (dr_vanilla_fused_pass) / vanilla pipeline (dr_vanilla_graph_pass)", "sgat": "fout_graph_kernel<true> (dr_sgat_graph_pass)", "ginet_nocluster": "ginet_nocluster_kernel (dr_ginet_nocluster_graph_pass)"}[args.model]
         result = {
             "metric": HEADLINE_METRIC if default_cfg else f"graphs/sec per training step, {workload} (fwd+MSE+bwd+Adam)",
             "value": round(graphs_total / elapsed, 1),

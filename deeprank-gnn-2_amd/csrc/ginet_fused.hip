@@ -129,8 +129,8 @@ __device__ __forceinline__ float relu_bwd(float out, float g) { return (out <= 0
 // Asynchronous global->LDS copy of n 4-byte words (global_load_lds_dword: one
 // wave instruction moves 256 contiguous bytes, no VGPR round trip).  The LDS
 // base handed to the instruction (M0) is wave-uniform; lane l lands at base+4l.
-__device__ __forceinline__ void dma_words(void* lds_dst, const void* gsrc, int n) {
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+__device__ __forceinline__ void dma_words(void* lds_dst, const void* gsrc, int n, int tid = threadIdx.x) {
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t* src = reinterpret_cast<const uint32_t*>(gsrc);
   uint32_t* dst = reinterpret_cast<uint32_t*>(lds_dst);
   for (int base = wave * 64; base < n; base += NT)
@@ -139,8 +139,8 @@ __device__ __forceinline__ void dma_words(void* lds_dst, const void* gsrc, int n
 
 // Same with 16-byte lanes (global_load_lds_dwordx4, 1 KiB per wave
 // instruction).  Source and destination 16-byte aligned; n4 = 16-byte units.
-__device__ __forceinline__ void dma_x4(void* lds_dst, const void* gsrc, int n4) {
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+__device__ __forceinline__ void dma_x4(void* lds_dst, const void* gsrc, int n4, int tid = threadIdx.x) {
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint4* src = reinterpret_cast<const uint4*>(gsrc);
   uint4* dst = reinterpret_cast<uint4*>(lds_dst);
   for (int base = wave * 64; base < n4; base += NT)
@@ -157,10 +157,10 @@ __device__ __forceinline__ float4 f4add(float4 a, float4 v) {
 // 4); edges unrolled by 4 so 4 index reads and then their row reads are in
 // flight together.  Z rows have the stride ldz of the MFMA operand layout.
 __device__ __forceinline__ void gather_rows(const int* rp, const uint16_t* col, const float* X, int XS, float* Z,
-                                            int ldz, int n) {
+                                            int ldz, int n, int tid = threadIdx.x) {
   const int nch = XS >> 2;
-  const int sub = threadIdx.x & 7;
-  for (int i = threadIdx.x >> 3; i < n; i += NT / 8) {
+  const int sub = tid & 7;
+  for (int i = tid >> 3; i < n; i += NT / 8) {
     const int eb = rp[i], ee = rp[i + 1];
     for (int ch = sub; ch < nch; ch += 8) {
       const int c4 = ch * 4;
@@ -245,6 +245,10 @@ struct TailLds {
   float *g, *hpre, *hh, *hd, *dh, *dg, *dout;
   int *a1, *p1rp, *p1c, *p1trp, *p1tc, *m1p, *m1i, *cl1;
   const uint8_t* keep = nullptr;  // prefetched dropout keep flags, or null (hash in the head)
+  // accumulating pass (dr_ginet_acc_pass): the workgroup's running sums
+  // [dW1cat 32F | dW2cat 1024 | the head's, GinetHeadLds::acc], or null
+  float* acc = nullptr;
+  float* accf = nullptr;  // GinetHeadLds::accf
 };
 
 template <class C>
@@ -277,12 +281,12 @@ __device__ __forceinline__ TailLds tail_lds(const C& c, float* lds) {
   return t;
 }
 
-template <class ZAt, bool WT = false>
+template <class ZAt, bool WT = false, bool ACC = false>
 __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t, const float (&fc1_row)[8],
                                            const float (&fc1_col)[8], float fc1_bias, int b, int N, int K0, int K1,
-                                           int F, int OUT, float y_g, uint64_t drop_offset, ZAt zat, int pb = -1) {
+                                           int F, int OUT, float y_g, uint64_t drop_offset, ZAt zat, int pb) {
   if (pb < 0) pb = b;  // the partials' row (slab, head vectors, loss term)
-  const int tid = threadIdx.x;
+  const int tid = dr_tid<ACC>();
   STAMP(4);
   // ---------------- conv2 on the pooled graph (ginet.py:101,112) ------------
   // H2[k][o] = relu(sum over pooled row k, in edge order, of Y2[j][o]) with
@@ -421,7 +425,9 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
     hl.dout = t.dout;
     hl.dgp = t.dgp;
     hl.keep = t.keep;
-    if (!drk::ginet_head<NT, WT>(a.p, hl, fc1_row, fc1_col, fc1_bias, b, OUT, y_g, drop_offset, 8, pb)) return;
+    hl.acc = ACC ? t.acc + 32 * F + 1024 : nullptr;
+    hl.accf = ACC ? t.accf : nullptr;
+    if (!drk::ginet_head<NT, WT, ACC>(a.p, hl, fc1_row, fc1_col, fc1_bias, b, OUT, y_g, drop_offset, 8, pb)) return;
   }  // stamps 8 (forward head done) and 9 (loss gradient done) are taken inside
 
   STAMP(10);
@@ -466,7 +472,8 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
         for (int u = 0; u < 4; ++u) acc = fmaf(yv[u], pv[u], acc);
       }
       for (; k < K0; ++k) acc = fmaf(t.y2[k * 64 + o], t.p1[k * 32 + br * 16 + j], acc);
-      drk::st_part<WT>(slab + p, acc);
+      if (ACC) t.acc[32 * F + p] += acc;
+      else drk::st_part<WT>(slab + p, acc);
     }
     for (int p = tid; p < K0 * 32; p += NT) {
       const int k = p >> 5, ch = p & 31, br = ch >> 4, j = ch & 15;
@@ -479,7 +486,7 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
     }
   } else
   {
-    const int lane = tid & 63, wave = tid >> 6, li = lane & 15, kq = lane >> 4;
+    const int lane = tid & 63, wave = dr_wave<ACC>(tid), li = lane & 15, kq = lane >> 4;
     float* slab = a.p.slab + (int64_t)pb * DR_SLAB_STRIDE(F) + 32 * F;
     const int nrt = (K0 + 15) >> 4;
     for (int job = wave; job < 4 + 2 * nrt; job += NW) {
@@ -492,8 +499,16 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
           const float bv = k < K0 ? t.p1[k * 32 + br * 16 + li] : 0.f;
           acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
         }
+        if (ACC) {  // the four sums read first, then written (no read-after-write chain)
+          float o[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) drk::st_part<WT>(slab + br * 512 + (ot * 16 + kq * 4 + r) * 16 + li, acc[r]);
+          for (int r = 0; r < 4; ++r) o[r] = t.acc[32 * F + br * 512 + (ot * 16 + kq * 4 + r) * 16 + li];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) t.acc[32 * F + br * 512 + (ot * 16 + kq * 4 + r) * 16 + li] = o[r] + acc[r];
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) drk::st_part<WT>(slab + br * 512 + (ot * 16 + kq * 4 + r) * 16 + li, acc[r]);
+        }
       } else {
         const int q = job - 4, br = q & 1, r0 = (q >> 1) * 16;
         const int kr = min(r0 + li, K0 - 1);
@@ -548,7 +563,8 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
           for (int u = 0; u < G; ++u)
             if (ok[u]) acc = fmaf(dv[u], zv[u], acc);
         }
-        drk::st_part<WT>(slab + p, acc);
+        if (ACC) t.acc[p] += acc;
+        else drk::st_part<WT>(slab + p, acc);
       }
     };
     if (K0 > 8) dw1(std::integral_constant<int, 16>());
@@ -629,13 +645,26 @@ __device__ __forceinline__ void pipe_wait(const PipeCtx& pc, uint32_t* lf) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // the weight loads stay below the poll
 }
 
-template <int KPT, bool WT, bool SIB = false, bool RAS = false, class Hook = NoHook, bool PIPED = false>
-__device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx& sc = SibCtx{}, const Hook& hook = Hook{}, const PipeCtx& pc = PipeCtx{}) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int tid = threadIdx.x;
+// Accumulating pass (dr_ginet_acc_pass): a workgroup runs graphs gi, gi + R,
+// ... one after another and adds each graph's gradients to running sums (LDS
+// region acc at the front of its LDS, fc1.weight's in the caller's registers)
+// instead of writing per-graph partials; the graph carve starts acc_words in.
+struct AccCtx {
+  int gi = -1;           // the graph (batch position) this call runs
+  float* acc = nullptr;  // the row (acc_row_floats) + the loss
+  float* accf = nullptr;  // fc1.weight's sums in the kernel's registers (null: in acc)
+  int acc_words = 0;
+};
+
+template <int KPT, bool WT, bool SIB = false, bool RAS = false, class Hook = NoHook, bool PIPED = false, bool ACC = false>
+__device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx& sc, const Hook& hook, const PipeCtx& pc,
+                                               const AccCtx& ac) {
+  extern __shared__ __attribute__((aligned(16))) float lds_raw[];
+  float* lds = lds_raw + (ACC ? ac.acc_words : 0);
+  const int tid = dr_tid<ACC>();
   const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int b = SIB ? sc.b : (int)blockIdx.x;
+  const int wave = dr_wave<ACC>(tid);
+  const int b = SIB ? sc.b : ACC ? ac.gi : (int)blockIdx.x;
   const dr_graph_store& s = a.s;
   const dr_graph_desc d = a.descs[b];  // one 64-byte scalar load
   const int g = d.gid;
@@ -696,27 +725,27 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
       fc1_row[4] = u1.x; fc1_row[5] = u1.y; fc1_row[6] = u1.z; fc1_row[7] = u1.w;
     }
     fc1_bias = ldw(a.w.fc1b + r);
-    const int o = tid & 63, rcc = tid >> 6;
+    const int o = tid & 63, rcc = dr_wave<ACC>(tid);
 #pragma unroll
     for (int j = 0; j < 8; ++j) fc1_col[j] = ldw(a.w.fc1w + (rcc * 8 + j) * 64 + o);
   };
   const float y_g = s.y[g];
   uint64_t drop_offset = a.p.drop_offset;
-  dma_x4(sX, s.x + n0 * (int64_t)XS, N * XS / 4);
-  dma_x4(scol, s.col + ec0, (E + 7) / 8);
-  dma_words(srp, s.rowptr + n0 + g, N + 1);
-  dma_words(scl0, s.cl0 + n0, N);
-  dma_words(sp1rp, s.p1_rowptr + k00 + g, K0 + 1);
-  dma_words(sp1c, s.p1_col + q0, P1);
+  dma_x4(sX, s.x + n0 * (int64_t)XS, N * XS / 4, tid);
+  dma_x4(scol, s.col + ec0, (E + 7) / 8, tid);
+  dma_words(srp, s.rowptr + n0 + g, N + 1, tid);
+  dma_words(scl0, s.cl0 + n0, N, tid);
+  dma_words(sp1rp, s.p1_rowptr + k00 + g, K0 + 1, tid);
+  dma_words(sp1c, s.p1_col + q0, P1, tid);
   if (!alias) {
-    dma_words(sp1trp, s.p1t_rowptr + k00 + g, K0 + 1);
-    dma_words(sp1tc, s.p1t_col + q0, P1);
+    dma_words(sp1trp, s.p1t_rowptr + k00 + g, K0 + 1, tid);
+    dma_words(sp1tc, s.p1t_col + q0, P1, tid);
   }
-  dma_words(sm1p, s.m1_ptr + k10 + g, K1 + 1);
-  dma_words(sm1i, s.m1_idx + k00, K0);
+  dma_words(sm1p, s.m1_ptr + k10 + g, K1 + 1, tid);
+  dma_words(sm1i, s.m1_idx + k00, K0, tid);
   if (!RAS && !PIPED) {
-    dma_words(sW1, a.w.w1, 16 * F);  // [W1; W1e] rows of F, packed
-    dma_words(sW1 + 16 * F, a.w.w1e, 16 * F);
+    dma_words(sW1, a.w.w1, 16 * F, tid);  // [W1; W1e] rows of F, packed
+    dma_words(sW1 + 16 * F, a.w.w1e, 16 * F, tid);
   }
   {  // zero Z's K padding (cols XS..KPT; X's own pad is zero) and the pooling keys
     const int padz = KPT - XS;
@@ -958,16 +987,80 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
 
   TailLds t = tail_lds(c, lds);
   t.keep = skeep;
+  t.acc = ACC ? ac.acc : nullptr;
+  t.accf = ACC ? ac.accf : nullptr;
   auto zat = [&](int i, int kk) { return sZ[i * LDW + kk]; };
   // (dr_pass.slot: the graph's rows of the batch when it is split over launches)
   const int orow = a.p.slot ? a.p.slot[b] : b;
-  ginet_tail<decltype(zat), WT>(a, t, fc1_row, fc1_col, fc1_bias, orow, N, K0, K1, F, OUT, y_g, drop_offset, zat, PIPED ? pc.prow + orow : orow);
+  ginet_tail<decltype(zat), WT, ACC>(a, t, fc1_row, fc1_col, fc1_bias, orow, N, K0, K1, F, OUT, y_g, drop_offset, zat, PIPED ? pc.prow + orow : orow);
   return drop_offset;
 }
 
 template <int KPT>
 __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
-  graph_body<KPT, false>(a);
+  graph_body<KPT, false>(a, SibCtx{}, NoHook{}, PipeCtx{}, AccCtx{});
+}
+
+// ---------------------------------------------------------------------------
+// Accumulating pass (dr_ginet_acc_pass; batches past the CU count): R
+// workgroups, workgroup w runs graphs w, w + R, w + 2R, ... in that order and
+// sums their gradients on chip — the conv weights' and the head's in an LDS
+// region ahead of the graph carve, fc1.weight's (dh (x) g, 128 x 64) in
+// registers — then writes ONE row [dW1cat | dW2cat | fc1.weight | fc1.bias |
+// fc2.weight | fc2.bias] (dr_ginet_acc_row_floats) and its loss sum to
+// loss_per_graph[w].  The reduce then sums R rows instead of B per-graph
+// partials (and no outer products): the per-graph slab, B x (32F + 1024 +
+// 320) floats written and read back per step, becomes R x ~10 K.  The graph
+// -> workgroup map and each workgroup's order are fixed, so the sums are
+// deterministic (another fp32 association than the per-graph partials: the
+// tests compare the two at fp32 tolerance).
+// ---------------------------------------------------------------------------
+// the accumulators' LDS words = the row: [dW1cat 32F | dW2cat 1024 | fc1.weight
+// 128 x 64 | fc1.bias 128 | fc2.weight OUT x 128 | fc2.bias OUT], then the loss
+__host__ __device__ inline int acc_row_floats(int F, int OUT) { return r4(32 * F + 1024 + 128 * 64 + 128 + 128 * OUT + OUT); }
+__host__ __device__ inline int acc_words(int F, int OUT) { return r4(32 * F + 1024 + 128 * 64 + 128 + 128 * OUT + OUT + 1); }
+
+template <int KPT>
+__global__ void __launch_bounds__(NT) ginet_acc_kernel(GinetArgs a, const int32_t* plan) {
+  extern __shared__ __attribute__((aligned(16))) float lds_raw[];
+  const int F = a.s.n_feat, OUT = a.p.out_dim, tid = threadIdx.x;
+  AccCtx ac;
+  ac.acc = lds_raw;
+  ac.acc_words = acc_words(F, OUT);
+  // fc1.weight's sums in registers where the kernel has them to spare (F <= 32)
+  float accf[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  ac.accf = KPT == 32 ? accf : nullptr;
+  for (int p = tid; p < ac.acc_words; p += NT) lds_raw[p] = 0.f;
+  __syncthreads();
+  // plan: [R + 1 starts | the batch positions, workgroup by workgroup], or
+  // null: every R-th position from blockIdx.x
+  const int R = gridDim.x, w = blockIdx.x;
+  const int k0 = plan ? plan[w] : 0, k1 = plan ? plan[w + 1] : (a.B - w + R - 1) / R;
+  for (int k = k0; k < k1; ++k) {
+    ac.gi = plan ? plan[R + 1 + k] : w + k * R;
+    // the body reads the arguments from the kernarg segment through a pointer
+    // the optimiser cannot follow across iterations: each graph reloads what it
+    // uses (scalar loads) instead of every argument being held in SGPRs over the
+    // whole loop (spilled to VGPR lanes: ~650 readlane/writelane)
+    typedef const __attribute__((address_space(4))) GinetArgs* KArgs;
+    KArgs ka = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("; dr_kargs" : "+s"(ka));
+    graph_body<KPT, false, false, false, NoHook, false, true>(*(const GinetArgs*)ka, SibCtx{}, NoHook{}, PipeCtx{}, ac);
+    __syncthreads();  // the graph carve is restaged by the next graph
+  }
+  const int c0 = 32 * F + 1024;
+  if (KPT == 32) {
+    float4* d = reinterpret_cast<float4*>(lds_raw + c0 + tid * 8);
+    d[0] = make_float4(accf[0], accf[1], accf[2], accf[3]);
+    d[1] = make_float4(accf[4], accf[5], accf[6], accf[7]);
+    __syncthreads();
+  }
+  // the workgroup's row, then its loss sum
+  const int RS = acc_row_floats(F, OUT);
+  float4* row = reinterpret_cast<float4*>(a.p.slab + (int64_t)blockIdx.x * RS);
+  const float4* src = reinterpret_cast<const float4*>(lds_raw);
+  for (int p = tid; p < RS / 4; p += NT) row[p] = src[p];
+  if (tid == 0) a.p.loss_per_graph[blockIdx.x] = lds_raw[c0 + 128 * 64 + 128 + 128 * OUT + OUT];
 }
 
 // k sibling workgroups per graph: block -> (graph b, sibling rk), siblings 8
@@ -979,7 +1072,7 @@ __global__ void __launch_bounds__(NT) ginet_sib_kernel(GinetArgs a, SibCtx sc) {
   sc.rk = hi % sc.k;
   sc.b = (hi / sc.k) * 8 + (bx & 7);
   if (sc.b >= a.B) return;
-  graph_body<KPT, false, true>(a, sc);
+  graph_body<KPT, false, true>(a, sc, NoHook{}, PipeCtx{}, AccCtx{});
 }
 
 // ---------------------------------------------------------------------------
@@ -1021,7 +1114,7 @@ __global__ void __launch_bounds__(NT) ginet_step_kernel(GinetStepArgs a) {
   gu32* passed = (gu32*)(a.sync + 1);
   const int B = a.g.B;
   if ((int)blockIdx.x < B) {
-    graph_body<KPT, true>(a.g);
+    graph_body<KPT, true>(a.g, SibCtx{}, NoHook{}, PipeCtx{}, AccCtx{});
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave drains its write-through partials
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1186,7 +1279,7 @@ __global__ void __launch_bounds__(NT) ginet_ras_kernel(GinetStepArgs a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // the weight loads stay below the hand-off
     return tstep;
   };
-  graph_body<KPT, false, false, true>(a.g, SibCtx{}, hook);
+  graph_body<KPT, false, false, true>(a.g, SibCtx{}, hook, PipeCtx{}, AccCtx{});
   // this pass's partials are pending for the next launch: flagged by the LAST
   // workgroup to finish (sync[4] counts them), so no workgroup of this launch
   // can still read the flag at its entry and take the partials being written
@@ -1287,7 +1380,7 @@ __global__ void __launch_bounds__(NT) ginet_piped_kernel(GinetStepArgs a) {
     pc.fault = sync + 2;
     pc.spin = a.spin;
     pc.prow = (int)((s_step & 1) * a.alt_rows);
-    graph_body<KPT, false, false, false, NoHook, true>(a.g, SibCtx{}, NoHook{}, pc);
+    graph_body<KPT, false, false, false, NoHook, true>(a.g, SibCtx{}, NoHook{}, pc, AccCtx{});
   }
   // the last block of the launch to finish: the step counter and the pending flag
   __syncthreads();
@@ -1950,20 +2043,20 @@ __device__ __forceinline__ void tail_body(const LargeArgs& la, int b, float* lds
         const int64_t o = (int64_t)i * XSB + kk;  // the 4-byte word holding the bf16 value
         const uint32_t w = load_sc1_u32(zb + (o & ~(int64_t)1));
         return __uint_as_float((o & 1) ? (w & 0xffff0000u) : (w << 16));
-      });
+      }, -1);
     else
       ginet_tail(a, t, fc1_row, fc1_col, fc1_bias, row, N, K0, K1, F, OUT, y_g, drop_offset,
-                 [&](int i, int kk) { return bf2f(zb[(int64_t)i * XSB + kk]); });
+                 [&](int i, int kk) { return bf2f(zb[(int64_t)i * XSB + kk]); }, -1);
     return;
   }
   const float* z = pl.z + (int64_t)pl.z_row0[b] * r4(F);
   const int XS = r4(F);
   if (INL)
     ginet_tail(a, t, fc1_row, fc1_col, fc1_bias, row, N, K0, K1, F, OUT, y_g, drop_offset,
-               [&](int i, int kk) { return __uint_as_float(load_sc1_u32(z + (int64_t)i * XS + kk)); });
+               [&](int i, int kk) { return __uint_as_float(load_sc1_u32(z + (int64_t)i * XS + kk)); }, -1);
   else
     ginet_tail(a, t, fc1_row, fc1_col, fc1_bias, row, N, K0, K1, F, OUT, y_g, drop_offset,
-               [&](int i, int kk) { return z[(int64_t)i * XS + kk]; });
+               [&](int i, int kk) { return z[(int64_t)i * XS + kk]; }, -1);
 }
 
 __global__ void __launch_bounds__(NT) ginet_large_tail_kernel(LargeArgs la) {
@@ -2040,6 +2133,46 @@ extern "C" int dr_ginet_graph_pass(const dr_graph_store* store, const dr_graph_d
   } else {
     DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_graph_kernel<64>)));
     hipLaunchKernelGGL(ginet_graph_kernel<64>, dim3(n_batch), dim3(NT), lds_bytes, (hipStream_t)stream, args);
+  }
+  return (int)hipGetLastError();
+}
+
+// Accumulating pass: n_groups workgroups, graph gi on workgroup gi % n_groups
+// (or as plan lists them); each writes one row of dr_ginet_acc_row_floats floats to pass->slab and its
+// loss sum to pass->loss_per_graph[w].  lds_bytes is the graph carve (as for
+// dr_ginet_graph_pass); the accumulators' words are added here.
+extern "C" int32_t dr_ginet_acc_row_floats(int32_t n_feat, int32_t out_dim) { return acc_row_floats(n_feat, out_dim); }
+
+extern "C" int dr_ginet_acc_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                                 const dr_ginet_weights* w, const dr_pass* pass, int32_t lds_bytes, int32_t n_groups,
+                                 const int32_t* plan, void* stream) {
+  if (!store || !descs || !w || !pass || n_batch < 0 || n_groups < 1) return DR_E_ARG;
+  if (pass->out_dim < 1 || pass->out_dim > DR_MAX_OUT) return DR_E_UNSUPPORTED;
+  if (store->n_feat < 1 || 32 * store->n_feat > 2 * NT) return DR_E_UNSUPPORTED;  // F <= 64
+  if (pass->compute_dtype != DR_DTYPE_F32) return DR_E_UNSUPPORTED;
+  // training passes only (the sums are gradients), with the fused loss
+  if (!(pass->flags & DR_PASS_BACKWARD) || !pass->slab || !pass->loss_per_graph) return DR_E_ARG;
+  if (pass->loss_kind == DR_LOSS_NONE || pass->slot) return DR_E_UNSUPPORTED;
+  if ((pass->flags & DR_PASS_FORWARD) && !pass->out) return DR_E_ARG;
+  if (pass->use_dropout == DR_DROPOUT_MASK && !pass->mask) return DR_E_ARG;
+  if (pass->use_dropout < DR_DROPOUT_OFF || pass->use_dropout > DR_DROPOUT_HASH) return DR_E_ARG;
+  const int64_t lds = (int64_t)lds_bytes + 4LL * acc_words(store->n_feat, pass->out_dim);
+  if (lds > 160 * 1024) return DR_E_LDS;
+  if (n_batch == 0) return DR_OK;
+  if (!store->cl0) return DR_E_ARG;
+  if (n_groups > n_batch && !plan) n_groups = n_batch;
+  GinetArgs args;
+  args.s = *store;
+  args.w = *w;
+  args.p = *pass;
+  args.descs = descs;
+  args.B = n_batch;
+  if (store->n_feat <= 32) {
+    DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_acc_kernel<32>)));
+    hipLaunchKernelGGL(ginet_acc_kernel<32>, dim3(n_groups), dim3(NT), (int)lds, (hipStream_t)stream, args, plan);
+  } else {
+    DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_acc_kernel<64>)));
+    hipLaunchKernelGGL(ginet_acc_kernel<64>, dim3(n_groups), dim3(NT), (int)lds, (hipStream_t)stream, args, plan);
   }
   return (int)hipGetLastError();
 }

@@ -18,6 +18,12 @@ __device__ __forceinline__ bool keep_unit(const dr_pass& p, uint64_t offset, int
 struct GinetHeadLds {
   float *fc2, *g, *hpre, *hh, *hd, *dh, *dg, *dout, *dgp;
   const uint8_t* keep = nullptr;  // optional [128] dropout keep flags computed ahead (head_keep_prefetch)
+  // accumulating pass (dr_ginet_acc_pass): the workgroup's running sums of the
+  // head gradients over its graphs, [fc1.weight 128 x 64 | fc1.bias 128 |
+  // fc2.weight OUT x 128 | fc2.bias OUT | loss 1], instead of per-graph head
+  // vectors (16-byte aligned)
+  float* acc = nullptr;
+  float* accf = nullptr;  // or: fc1.weight's sums of this thread (row tid/8, columns 8 (tid%8) ..) in registers
 };
 
 // The fc1-output dropout keep flags of graph b, written to LDS by the first
@@ -53,7 +59,7 @@ __device__ __forceinline__ void st_part(float* p, float v) {
     *p = v;
 }
 
-template <int NT, bool WT = false>
+template <int NT, bool WT = false, bool ACC = false>
 __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds& t, const float (&fc1_row)[8],
                                            const float (&fc1_col)[8], float fc1_bias, int b, int OUT, float y_g,
                                            uint64_t drop_offset, int stamp0 = -1, int pb = -1) {
@@ -62,9 +68,9 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
   if (pb < 0) pb = b;
   int64_t* srow = (stamp0 >= 0 && p.stamps) ? p.stamps + (int64_t)b * 32 : nullptr;
   constexpr int NW = NT / 64;
-  const int tid = threadIdx.x;
+  const int tid = dr_tid<ACC>();
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = dr_wave<ACC>(tid);
   // ---------------- head: fc1 -> relu -> dropout -> fc2 (ginet.py:120-123) --
   {
     const int r = tid >> 3, part = tid & 7;  // 8 lanes per fc1 row
@@ -112,7 +118,8 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
   if (tid == 0) {
     if (p.loss_kind == DR_LOSS_MSE) {
       const float d = t.dout[0] - y_g;
-      if (p.loss_per_graph) st_part<WT>(p.loss_per_graph + pb, d * d);
+      if (ACC) t.acc[8192 + 128 + 128 * OUT + OUT] += d * d;
+      else if (p.loss_per_graph) st_part<WT>(p.loss_per_graph + pb, d * d);
       t.dout[0] = 2.f * d * p.loss_scale;
       for (int q = 1; q < OUT; ++q) t.dout[q] = 0.f;  // the loss reads column 0 only (engine's layer path alike)
     } else if (p.loss_kind == DR_LOSS_CE) {
@@ -123,7 +130,8 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
       for (int q = 0; q < OUT; ++q) se += expf(t.dout[q] - mx);
       const float lse = mx + logf(se);
       const float wy = p.class_w ? p.class_w[yi] : 1.f;
-      if (p.loss_per_graph) st_part<WT>(p.loss_per_graph + pb, wy * (lse - t.dout[yi]));
+      if (ACC) t.acc[8192 + 128 + 128 * OUT + OUT] += wy * (lse - t.dout[yi]);
+      else if (p.loss_per_graph) st_part<WT>(p.loss_per_graph + pb, wy * (lse - t.dout[yi]));
       for (int q = 0; q < OUT; ++q) t.dout[q] = wy * (expf(t.dout[q] - lse) - (q == yi ? 1.f : 0.f)) * p.loss_scale;
     } else {
       for (int q = 0; q < OUT; ++q) t.dout[q] = p.dout[(int64_t)b * OUT + q];
@@ -141,7 +149,7 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
   }
   __syncthreads();
   {
-    const int o = tid & 63, rc = tid >> 6;  // 16 chunks of 8 fc1 rows
+    const int o = tid & 63, rc = dr_wave<ACC>(tid);  // 16 chunks of 8 fc1 rows
     float acc = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc = fmaf(fc1_col[j], t.dh[rc * 8 + j], acc);
@@ -153,7 +161,33 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
     for (int rc = 0; rc < NW; ++rc) acc += t.dgp[rc * 64 + tid];
     t.dg[tid] = acc;
   }
-  {
+  if (ACC) {
+    // this graph's head gradients added to the workgroup's sums: fc1.weight
+    // += dh (x) g (thread (r, part): row r, columns 8 part ..), fc1.bias +=
+    // dh, fc2.weight += dout (x) hd, fc2.bias += dout
+    const int r = tid >> 3, part = tid & 7;
+    const float dhr = t.dh[r];
+    const float4* gv = reinterpret_cast<const float4*>(t.g + part * 8);
+    const float4 x0 = gv[0], x1 = gv[1];
+    if (t.accf) {  // in the caller's registers
+      float* f = t.accf;
+      f[0] = fmaf(dhr, x0.x, f[0]); f[1] = fmaf(dhr, x0.y, f[1]); f[2] = fmaf(dhr, x0.z, f[2]); f[3] = fmaf(dhr, x0.w, f[3]);
+      f[4] = fmaf(dhr, x1.x, f[4]); f[5] = fmaf(dhr, x1.y, f[5]); f[6] = fmaf(dhr, x1.z, f[6]); f[7] = fmaf(dhr, x1.w, f[7]);
+    } else {  // in LDS (the row's fc1.weight block)
+      float4* w = reinterpret_cast<float4*>(t.acc + r * 64 + part * 8);
+      float4 v0 = w[0], v1 = w[1];
+      v0.x = fmaf(dhr, x0.x, v0.x); v0.y = fmaf(dhr, x0.y, v0.y); v0.z = fmaf(dhr, x0.z, v0.z); v0.w = fmaf(dhr, x0.w, v0.w);
+      v1.x = fmaf(dhr, x1.x, v1.x); v1.y = fmaf(dhr, x1.y, v1.y); v1.z = fmaf(dhr, x1.z, v1.z); v1.w = fmaf(dhr, x1.w, v1.w);
+      w[0] = v0;
+      w[1] = v1;
+    }
+    float* hacc = t.acc + 128 * 64;
+    if (tid < 128) {
+      hacc[tid] += t.dh[tid];
+      for (int q = 0; q < OUT; ++q) hacc[128 + q * 128 + tid] = fmaf(t.dout[q], t.hd[tid], hacc[128 + q * 128 + tid]);
+    }
+    if (tid < OUT) hacc[128 + 128 * OUT + tid] += t.dout[tid];
+  } else {
     const int HS = DR_HEAD_STRIDE(OUT);
     float* hg = p.head + (int64_t)pb * HS;
     if (tid < 64) st_part<WT>(hg + tid, t.g[tid]);

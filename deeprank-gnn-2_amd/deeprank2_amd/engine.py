@@ -34,6 +34,33 @@ from deeprank2_amd import _lib, layered
 from deeprank2_amd.fused import BatchHandle, launch, launch_step, param_table, slab_rows_for, step_fits
 
 
+def acc_plan(h: BatchHandle, r: int) -> torch.Tensor:
+    """The accumulating pass's work plan for ``r`` workgroups (cached on the
+    handle): graphs by descending cost N + E/4 dealt to the workgroups in
+    snake order (0..r-1, r-1..0, ...), so every workgroup gets B/r graphs
+    of about the same total size; [r + 1 starts | positions].  Depends only on
+    the batch, so the sums' order — and the result — is deterministic."""
+    import numpy as np  # noqa: PLC0415
+
+    key = ("acc_plan", r)
+    plan = h._lds.get(key)  # noqa: SLF001
+    if plan is not None:
+        return plan
+    idx = h.gids_host.astype(np.int64)
+    n, e = (h.store._sizes[0][idx].astype(np.int64), h.store._sizes[1][idx].astype(np.int64))  # noqa: SLF001
+    order = np.argsort(-(4 * n + e), kind="stable")
+    i = np.arange(h.B)
+    rnd, j = i // r, i % r
+    wg = np.where(rnd % 2 == 0, j, r - 1 - j)
+    by_wg = np.argsort(wg, kind="stable")
+    starts = np.zeros(r + 1, dtype=np.int32)
+    starts[1:] = np.cumsum(np.bincount(wg, minlength=r))
+    host = np.concatenate([starts, order[by_wg].astype(np.int32)])
+    plan = torch.from_numpy(host).to(h.store.device)
+    h._lds[key] = plan  # noqa: SLF001
+    return plan
+
+
 class FusedTrainStep:
     def __init__(self, model, lr=1e-3, weight_decay=1e-5, betas=(0.9, 0.999), eps=1e-8, loss="mse", class_weights=None, process_group=None, max_batch=64, compute_dtype="f32"):
         self.model = model
@@ -108,6 +135,17 @@ class FusedTrainStep:
         self.piped = False
         self._piped_last = None  # (B, loss scale) of the pending pass
         self._piped_store = None
+        # accumulating pass (GINet fp32, batches past the CU count;
+        # dr_ginet_acc_pass): acc_groups workgroups each run every
+        # acc_groups-th graph and sum the gradients on chip, one row each,
+        # so the reduce reads acc_groups rows instead of B per-graph partials.
+        # None = auto (B > the device's CU count), False = off, True = on
+        # wherever the batch allows it.  Another fp32 association than the
+        # per-graph partials (deterministic).
+        self.acc = None
+        self.acc_groups = None  # workgroups (None: the CU count)
+        self._acc_slab = None
+        self._table_acc = None
         # models whose graph pass reads its weights from a packed copy
         # (VanillaNetwork: MFMA-fragment order): one copy per step object,
         # rewritten by Adam as it updates the parameters (dr_adam.mirror), so
@@ -176,6 +214,7 @@ class FusedTrainStep:
         self._adam_div.grad_div = self.wsum.data_ptr()
         self._adam_ras = _lib.AdamC.from_buffer_copy(a)
         self._adam_ras.fault = None
+        self._table_acc = None  # rebuilt on first use (parameters / grads may have moved)
         self._wire_packed()
 
     def _wire_packed(self):
@@ -292,17 +331,17 @@ class FusedTrainStep:
                 ev.append((e0, e1))
             self.step_count += 1
             return self.loss_out, self.out[: h.B]
-        launch(self.spec, h, self._w, p, wpack=self._packed())
+        rows = self._launch_pass(h, p)
         if ev is not None:
             e1.record()
             ev.append((e0, e1))
         self.step_count += 1
-        slab, head, lpg, lout = self.slab.data_ptr(), self.head.data_ptr(), self.lpg.data_ptr(), self.loss_out.data_ptr()
-        self._table.slab_rows = slab_rows_for(self.spec, h)
+        table, slab, n_rows = self._reduce_args(h, rows)
+        head, lpg, lout = self.head.data_ptr(), self.lpg.data_ptr(), self.loss_out.data_ptr()
         if self.pg is None:
-            _lib.check(lib.dr_reduce_update(self._table, slab, head, h.B, self._adam, lpg, scale, lout, stream), "dr_reduce_update")
+            _lib.check(lib.dr_reduce_update(table, slab, head, n_rows, self._adam, lpg, scale, lout, stream), "dr_reduce_update")
         else:
-            _lib.check(lib.dr_reduce_update(self._table, slab, head, h.B, self._adam_off, lpg, scale, lout, stream), "dr_reduce_update")
+            _lib.check(lib.dr_reduce_update(table, slab, head, n_rows, self._adam_off, lpg, scale, lout, stream), "dr_reduce_update")
             if self.device_div:
                 self._local_wsum(h)
             if self.handoffs:
@@ -312,6 +351,71 @@ class FusedTrainStep:
                 self.fault_red.copy_(self.flat_fault)
             self._adam_after_allreduce()
         return self.loss_out, self.out[: h.B]
+
+    def _acc_rows(self, h: BatchHandle) -> int:
+        """Workgroups (= partial rows) of the accumulating pass for this
+        batch, or 0 when the batch takes the per-graph partials."""
+        from deeprank2_amd.fused import _device_cus, lds_for  # noqa: PLC0415
+
+        if self.acc is False or self.spec.entry != "dr_ginet_graph_pass" or self.compute_dtype != "f32":
+            return 0
+        if h.nonfinite or h.force_large or self.spec.layers is not None and layered.needs_layers(self.spec, h, self.out_dim):
+            return 0
+        r = int(self.acc_groups or _device_cus(self.device))
+        if self.acc is None and h.B <= r:
+            return 0
+        f = self.model.input_shape
+        lib = _lib.load()
+        words = (32 * f + 1024 + 128 + 128 * self.out_dim + self.out_dim + 1 + 3) & ~3
+        if lds_for(self.spec, h, self.out_dim) + 4 * words > 160 * 1024:  # noqa: PLR2004
+            return 0
+        r = min(r, h.B)
+        rs = int(lib.dr_ginet_acc_row_floats(f, self.out_dim))
+        if self._acc_slab is None or self._acc_slab.numel() < r * rs:
+            self._acc_slab = torch.empty(r * rs, dtype=torch.float32, device=self.device)
+        if self._table_acc is None:
+            from deeprank2_amd.fused import param_table  # noqa: PLC0415
+
+            self._table_acc = param_table(self.spec, self.params, self.grads, self.states, f, self.out_dim)
+            slab, z = _lib.DR_GRAD_SLAB, (_lib.DR_GRAD_ZERO, 0, 0, 0)
+            c0 = 32 * f + 1024
+            rec = [
+                (slab, 0, 0, 0), z, z, (slab, 32 * f, 0, 0), z, z,
+                (slab, 16 * f, 0, 0), z, z, (slab, 32 * f + 512, 0, 0), z, z,
+                (slab, c0, 0, 0), (slab, c0 + 8192, 0, 0), (slab, c0 + 8320, 0, 0), (slab, c0 + 8320 + 128 * self.out_dim, 0, 0),
+            ]  # fmt: skip
+            for i, (kind, o1, o2, cols) in enumerate(rec):
+                t = self._table_acc.recipe[i]
+                t.kind, t.off1, t.off2, t.cols = kind, o1, o2, cols
+            self._table_acc.slab_stride = rs
+            self._table_acc.slab_rows = 1
+        return r
+
+    def _launch_pass(self, h: BatchHandle, p) -> int:
+        """The graph pass of a two-launch step: the accumulating pass (returns
+        its row count) or the model's per-graph pass (returns 0)."""
+        from deeprank2_amd.fused import lds_for  # noqa: PLC0415
+
+        r = self._acc_rows(h)
+        if r == 0:
+            launch(self.spec, h, self._w, p, wpack=self._packed())
+            return 0
+        p.slab = self._acc_slab.data_ptr()
+        plan = acc_plan(h, r)
+        try:
+            rc = _lib.load().dr_ginet_acc_pass(h.store.cstruct(), h.descs.data_ptr(), h.B, self._w, p, lds_for(self.spec, h, self.out_dim), r, plan.data_ptr(), _lib.stream_ptr(self.device))
+        finally:
+            p.slab = self.slab.data_ptr()
+        _lib.check(rc, "dr_ginet_acc_pass")
+        return r
+
+    def _reduce_args(self, h: BatchHandle, acc_rows: int):
+        """(table, slab pointer, rows) of the reduce after a pass that
+        returned ``acc_rows`` from :meth:`_launch_pass`."""
+        if acc_rows:
+            return self._table_acc, self._acc_slab.data_ptr(), acc_rows
+        self._table.slab_rows = slab_rows_for(self.spec, h)
+        return self._table, self.slab.data_ptr(), h.B
 
     def _piped_fits(self, h: BatchHandle) -> bool:
         """The pipelined step takes this batch: GINet's per-graph kernel, one
@@ -541,7 +645,7 @@ class FusedTrainStep:
                     self.step(h, global_batch=global_batch)
                     continue
                 p.loss_scale = self.loss_scale(h, global_batch or h.B * self.world)
-                launch(self.spec, h, self._w, p)
+                self._launch_pass(h, p)
 
         passes(len(handles))  # warm-up: LDS attributes, plans
         torch.cuda.synchronize(self.device)
@@ -585,9 +689,9 @@ class FusedTrainStep:
             stream = _lib.stream_ptr(self.device)  # inside the capture: the capturing stream
             for i in range(k):
                 h = handles[i % len(handles)]
-                self._table.slab_rows = slab_rows_for(self.spec, h)
+                table, slab, n_rows = self._reduce_args(h, self._acc_rows(h))
                 scale = self.loss_scale(h, global_batch or h.B * self.world)
-                _lib.check(lib.dr_reduce_update(self._table, self.slab.data_ptr(), self.head.data_ptr(), h.B, self._adam, self.lpg.data_ptr(), scale, self.loss_out.data_ptr(), stream), "dr_reduce_update")
+                _lib.check(lib.dr_reduce_update(table, slab, self.head.data_ptr(), n_rows, self._adam, self.lpg.data_ptr(), scale, self.loss_out.data_ptr(), stream), "dr_reduce_update")
 
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):

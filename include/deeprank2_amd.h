@@ -219,6 +219,29 @@ int dr_ginet_graph_pass(const dr_graph_store* store, const dr_graph_desc* descs,
 int64_t dr_ginet_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_feat, int32_t k0,
                            int32_t p1_edges, int32_t k1, int32_t transpose_aliased, int32_t out_dim);
 
+/* Accumulating training pass for batches larger than the CU count (r05):
+ * the loss + backward of GINet.forward over the batch (ginet.py:90-125 under
+ * trainer.py:_train_epoch's loss.backward) like dr_ginet_graph_pass, but
+ * n_groups workgroups each run graphs w, w + n_groups, ... in that order and
+ * keep the sums of their gradients on chip, then write ONE row per workgroup:
+ * pass->slab[w * dr_ginet_acc_row_floats(F, OUT) ...] = [dW1cat 32F | dW2cat
+ * 1024 | fc1.weight 128x64 | fc1.bias 128 | fc2.weight OUTx128 | fc2.bias OUT]
+ * and pass->loss_per_graph[w] = the workgroup's loss sum.  pass->out gets
+ * every graph's output as usual; pass->head is unused.  The reduce sums the
+ * n_groups rows (dr_reduce_update with an all-slab table).  Deterministic
+ * (fixed graph -> workgroup map and order); a different fp32 association
+ * than the per-graph partials.  Needs BACKWARD, a fused loss, no slot; F32.
+ * lds_bytes: the graph carve as for dr_ginet_graph_pass (the accumulators'
+ * words are added inside; the total must fit 160 KB).  plan (optional,
+ * device int32 [n_groups + 1 + n_batch]): workgroup w runs the batch
+ * positions plan[n_groups + 1 + k] for k in [plan[w], plan[w + 1]) in that
+ * order (every position exactly once: the caller balances the work, e.g. by
+ * graph size); NULL: positions w, w + n_groups, ...                         */
+int dr_ginet_acc_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
+                      const dr_ginet_weights* w, const dr_pass* pass, int32_t lds_bytes, int32_t n_groups,
+                      const int32_t* plan, void* stream);
+int32_t dr_ginet_acc_row_floats(int32_t n_feat, int32_t out_dim);
+
 /* ---- GINet on graphs larger than one workgroup's LDS (atom-level graphs) ----
  * Two launches with the same result as dr_ginet_graph_pass:
  *   1. one workgroup per tile of plan->tile_rows nodes: Z = A X for its rows
