@@ -42,6 +42,9 @@
 
 namespace {
 
+#ifndef DR_DMA_ROT
+#define DR_DMA_ROT 1
+#endif
 constexpr int NT = 1024;     // 16 waves
 constexpr int NW = NT / 64;
 constexpr int HEADW = 672;   // G64 hpre128 hh128 hd128 dh128 dG64 dout16 spare16
@@ -109,6 +112,81 @@ __host__ __device__ inline Carve carve(int N, int E, int F, int K0, int P1, int 
   return c;
 }
 
+// The accumulating pass's prefetch layout (dr_ginet_acc_pass with the batch's
+// maximum sizes): the weights stay put across a workgroup's graphs, and the
+// inputs of graph k+1 are DMA'd while graph k's tail runs, so they need
+// regions graph k's tail does not touch:
+//   [W1 | W2 | fc2] [front inputs: x rp col cl0 — dead once the front half is
+//   done] [tail inputs, two buffers by graph parity: p1rp p1c p1trp p1tc m1p
+//   m1i] [scratch: z key p1 a1 dp1 y2 h2 p2 nt cl1 head dgp keep]
+// (word offsets from the carve base; each region sized for the batch maxima).
+struct AccLayout {
+  int fin, tin0, tin1, scr, total;
+};
+
+__host__ __device__ inline Carve carve_acc(int N, int E, int F, int K0, int P1, int K1, int alias, int OUT,
+                                           const AccLayout& L, int par) {
+  Carve c;
+  c.KP = r16(F);
+  c.LDW = c.KP + 2;
+  c.XS = r4(F);
+  int o = 0;
+#define TAKE(field, words) \
+  c.field = o;             \
+  o += r4(words);
+  TAKE(w1, 32 * F)
+  TAKE(w2, 1024)
+  TAKE(fc2, OUT * 128 + OUT)
+  o = L.fin;
+  TAKE(x, N * c.XS)
+  TAKE(rp, N + 1)
+  TAKE(col, (E + 1) / 2)
+  TAKE(cl0, N)
+  o = par ? L.tin1 : L.tin0;
+  TAKE(p1rp, K0 + 1)
+  TAKE(p1c, P1)
+  if (alias) {
+    c.p1trp = c.p1rp;
+    c.p1tc = c.p1c;
+  } else {
+    TAKE(p1trp, K0 + 1)
+    TAKE(p1tc, P1)
+  }
+  TAKE(m1p, K1 + 1)
+  TAKE(m1i, K0)
+  o = L.scr;
+  TAKE(z, N * c.LDW)
+  TAKE(key, 2 * K0 * 32)
+  TAKE(p1, K0 * 32)
+  TAKE(a1, K0 * 32)
+  TAKE(dp1, K0 * 32)
+  TAKE(y2, K0 * 64)
+  TAKE(h2, K0 * 64)
+  TAKE(p2, K1 * 64)
+  TAKE(nt, K1 * 64)
+  TAKE(cl1, K0)
+  TAKE(head, HEADW)
+  TAKE(dgp, NW * 64)
+  TAKE(keep, 32)
+#undef TAKE
+  c.total = o;
+  return c;
+}
+
+// the layout for the batch maxima (every graph's carve_acc fits inside it)
+__host__ __device__ inline AccLayout acc_layout(int Nm, int Em, int F, int K0m, int P1m, int K1m, int alias, int OUT) {
+  AccLayout L;
+  L.fin = r4(32 * F) + 1024 + r4(OUT * 128 + OUT);
+  const int XS = r4(F), LDW = r16(F) + 2;
+  L.tin0 = L.fin + r4(Nm * XS) + r4(Nm + 1) + r4((Em + 1) / 2) + r4(Nm);
+  const int tin = r4(K0m + 1) + r4(P1m) + (alias ? 0 : r4(K0m + 1) + r4(P1m)) + r4(K1m + 1) + r4(K0m);
+  L.tin1 = L.tin0 + tin;
+  L.scr = L.tin1 + tin;
+  L.total = L.scr + r4(Nm * LDW) + r4(2 * K0m * 32) + 3 * r4(K0m * 32) + 2 * r4(K0m * 64) + 2 * r4(K1m * 64) + r4(K0m) +
+            r4(HEADW) + r4(NW * 64) + r4(32);
+  return L;
+}
+
 struct GinetArgs {
   dr_graph_store s;
   dr_ginet_weights w;
@@ -129,8 +207,11 @@ __device__ __forceinline__ float relu_bwd(float out, float g) { return (out <= 0
 // Asynchronous global->LDS copy of n 4-byte words (global_load_lds_dword: one
 // wave instruction moves 256 contiguous bytes, no VGPR round trip).  The LDS
 // base handed to the instruction (M0) is wave-uniform; lane l lands at base+4l.
-__device__ __forceinline__ void dma_words(void* lds_dst, const void* gsrc, int n, int tid = threadIdx.x) {
-  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+// w0: the wave that takes the first 64 lanes (the copies of a staging
+// sequence start on different waves, so the short ones do not all queue on
+// wave 0: an LDS DMA instruction holds its wave ~a few hundred cycles at issue)
+__device__ __forceinline__ void dma_words(void* lds_dst, const void* gsrc, int n, int tid = threadIdx.x, int w0 = 0) {
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(((tid >> 6) - w0) & (NW - 1));
   const uint32_t* src = reinterpret_cast<const uint32_t*>(gsrc);
   uint32_t* dst = reinterpret_cast<uint32_t*>(lds_dst);
   for (int base = wave * 64; base < n; base += NT)
@@ -139,12 +220,41 @@ __device__ __forceinline__ void dma_words(void* lds_dst, const void* gsrc, int n
 
 // Same with 16-byte lanes (global_load_lds_dwordx4, 1 KiB per wave
 // instruction).  Source and destination 16-byte aligned; n4 = 16-byte units.
-__device__ __forceinline__ void dma_x4(void* lds_dst, const void* gsrc, int n4, int tid = threadIdx.x) {
-  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+__device__ __forceinline__ void dma_x4(void* lds_dst, const void* gsrc, int n4, int tid = threadIdx.x, int w0 = 0) {
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(((tid >> 6) - w0) & (NW - 1));
   const uint4* src = reinterpret_cast<const uint4*>(gsrc);
   uint4* dst = reinterpret_cast<uint4*>(lds_dst);
   for (int base = wave * 64; base < n4; base += NT)
     if (base + lane < n4) __builtin_amdgcn_global_load_lds(AS1(src + base + lane), AS3(dst + base), 16, 0, 0);
+}
+
+// The same copies issued from inline asm: the compiler does not know they
+// write LDS, so it inserts no wait for them before later LDS reads (with the
+// builtin it waits for the DMA before the next LDS access), and (no memory
+// clobber) reloads nothing around them.  For copies into
+// LDS no one reads until an explicit s_waitcnt vmcnt(0) + barrier: the
+// accumulating pass's prefetch of the next graph's inputs under this graph's
+// tail.
+__device__ __forceinline__ void dma_words_async(void* lds_dst, const void* gsrc, int n, int tid, int w0 = 0) {
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(((tid >> 6) - w0) & (NW - 1));
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(gsrc);
+  const uint32_t dst = (uint32_t)(size_t)AS3(lds_dst);
+  for (int base = wave * 64; base < n; base += NT)
+    if (base + lane < n)
+      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" ::"s"(__builtin_amdgcn_readfirstlane(dst + 4 * base)),
+                   "v"(src + base + lane)
+                   : "m0");
+}
+
+__device__ __forceinline__ void dma_x4_async(void* lds_dst, const void* gsrc, int n4, int tid, int w0 = 0) {
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(((tid >> 6) - w0) & (NW - 1));
+  const uint4* src = reinterpret_cast<const uint4*>(gsrc);
+  const uint32_t dst = (uint32_t)(size_t)AS3(lds_dst);
+  for (int base = wave * 64; base < n4; base += NT)
+    if (base + lane < n4)
+      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(__builtin_amdgcn_readfirstlane(dst + 16 * base)),
+                   "v"(src + base + lane)
+                   : "m0");
 }
 
 __device__ __forceinline__ float4 f4add(float4 a, float4 v) {
@@ -651,12 +761,19 @@ __device__ __forceinline__ void pipe_wait(const PipeCtx& pc, uint32_t* lf) {
 // instead of writing per-graph partials; the graph carve starts acc_words in.
 struct AccCtx {
   int gi = -1;           // the graph (batch position) this call runs
-  float* acc = nullptr;  // the row (acc_row_floats) + the loss
+  float* acc = nullptr;  // [dW1cat 32F | dW2cat 1024 | GinetHeadLds::acc's block]
   float* accf = nullptr;  // fc1.weight's sums in the kernel's registers (null: in acc)
   int acc_words = 0;
+  // prefetch layout (graph_body<..., PF = true>): this graph's tail-input
+  // buffer (parity), whether its inputs and W1 still need staging (the
+  // workgroup's first graph), and the next graph's batch position (-1: none)
+  AccLayout lay;
+  int par = 0, next = -1;
+  bool first = true;
 };
 
-template <int KPT, bool WT, bool SIB = false, bool RAS = false, class Hook = NoHook, bool PIPED = false, bool ACC = false>
+template <int KPT, bool WT, bool SIB = false, bool RAS = false, class Hook = NoHook, bool PIPED = false, bool ACC = false,
+          bool PF = false>
 __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx& sc, const Hook& hook, const PipeCtx& pc,
                                                const AccCtx& ac) {
   extern __shared__ __attribute__((aligned(16))) float lds_raw[];
@@ -667,6 +784,8 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
   const int b = SIB ? sc.b : ACC ? ac.gi : (int)blockIdx.x;
   const dr_graph_store& s = a.s;
   const dr_graph_desc d = a.descs[b];  // one 64-byte scalar load
+  // PF: the next graph's descriptor, read now so its latency hides under the front half
+  const dr_graph_desc dnext = (PF && ac.next >= 0) ? a.descs[ac.next] : d;
   const int g = d.gid;
   const int64_t n0 = d.node0, ec0 = d.col0, k00 = d.k0, q0 = d.p1, k10 = d.k1;
   const int N = d.n_nodes, E = d.n_edges, K0 = d.n_k0, P1 = d.n_p1, K1 = d.n_k1;
@@ -680,7 +799,7 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
                "s"(s.p1t_rowptr), "s"(s.p1t_col), "s"(s.m1_ptr), "s"(s.m1_idx), "s"(s.y), "s"(F), "s"(alias),
                "s"(OUT), "s"(n0), "s"(ec0), "s"(k00), "s"(q0), "s"(k10), "s"(N), "s"(E), "s"(K0), "s"(P1), "s"(K1),
                "s"(g));
-  const Carve c = carve(N, E, F, K0, P1, K1, alias, OUT);
+  const Carve c = PF ? carve_acc(N, E, F, K0, P1, K1, alias, OUT, ac.lay, ac.par) : carve(N, E, F, K0, P1, K1, alias, OUT);
   const int LDW = c.LDW, XS = c.XS;
 
   float* sW1 = lds + c.w1;
@@ -731,21 +850,43 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
   };
   const float y_g = s.y[g];
   uint64_t drop_offset = a.p.drop_offset;
-  dma_x4(sX, s.x + n0 * (int64_t)XS, N * XS / 4, tid);
-  dma_x4(scol, s.col + ec0, (E + 7) / 8, tid);
-  dma_words(srp, s.rowptr + n0 + g, N + 1, tid);
-  dma_words(scl0, s.cl0 + n0, N, tid);
-  dma_words(sp1rp, s.p1_rowptr + k00 + g, K0 + 1, tid);
-  dma_words(sp1c, s.p1_col + q0, P1, tid);
-  if (!alias) {
-    dma_words(sp1trp, s.p1t_rowptr + k00 + g, K0 + 1, tid);
-    dma_words(sp1tc, s.p1t_col + q0, P1, tid);
+  // the graph's inputs (PF: graph k+1's are DMA'd during graph k's tail)
+  // (asm-issued: waited for by the s_waitcnt vmcnt(0) before the staging barrier)
+  auto stage_inputs = [&](const dr_graph_desc& dd, const Carve& cc) {
+    const int64_t dn0 = dd.node0, dk00 = dd.k0;
+    const int dg = dd.gid, dN = dd.n_nodes, dK0 = dd.n_k0;
+    dma_x4_async(lds + cc.x, s.x + dn0 * (int64_t)XS, dN * XS / 4, tid);
+    dma_x4_async(lds + cc.col, s.col + dd.col0, (dd.n_edges + 7) / 8, tid, 7);
+    dma_words_async(lds + cc.rp, s.rowptr + dn0 + dg, dN + 1, tid, 13);
+    dma_words_async(lds + cc.cl0, s.cl0 + dn0, dN, tid, 3);
+    dma_words_async(lds + cc.p1rp, s.p1_rowptr + dk00 + dg, dK0 + 1, tid, 10);
+    dma_words_async(lds + cc.p1c, s.p1_col + dd.p1, dd.n_p1, tid, 11);
+    if (!alias) {
+      dma_words_async(lds + cc.p1trp, s.p1t_rowptr + dk00 + dg, dK0 + 1, tid, 12);
+      dma_words_async(lds + cc.p1tc, s.p1t_col + dd.p1, dd.n_p1, tid, 9);
+    }
+    dma_words_async(lds + cc.m1p, s.m1_ptr + dd.k1 + dg, dd.n_k1 + 1, tid, 8);
+    dma_words_async(lds + cc.m1i, s.m1_idx + dk00, dK0, tid, 1);
+  };
+  if (!PF) {  // (DR_DMA_ROT: starting waves spread over the copies, A/B)
+    dma_x4(sX, s.x + n0 * (int64_t)XS, N * XS / 4, tid);
+    dma_x4(scol, s.col + ec0, (E + 7) / 8, tid, DR_DMA_ROT * 7);
+    dma_words(srp, s.rowptr + n0 + g, N + 1, tid, DR_DMA_ROT * 13);
+    dma_words(scl0, s.cl0 + n0, N, tid, DR_DMA_ROT * 3);
+    dma_words(sp1rp, s.p1_rowptr + k00 + g, K0 + 1, tid, DR_DMA_ROT * 10);
+    dma_words(sp1c, s.p1_col + q0, P1, tid, DR_DMA_ROT * 11);
+    if (!alias) {
+      dma_words(sp1trp, s.p1t_rowptr + k00 + g, K0 + 1, tid, DR_DMA_ROT * 12);
+      dma_words(sp1tc, s.p1t_col + q0, P1, tid, DR_DMA_ROT * 9);
+    }
+    dma_words(sm1p, s.m1_ptr + k10 + g, K1 + 1, tid, DR_DMA_ROT * 8);
+    dma_words(sm1i, s.m1_idx + k00, K0, tid, DR_DMA_ROT * 1);
+  } else if (ac.first) {
+    stage_inputs(d, c);
   }
-  dma_words(sm1p, s.m1_ptr + k10 + g, K1 + 1, tid);
-  dma_words(sm1i, s.m1_idx + k00, K0, tid);
-  if (!RAS && !PIPED) {
-    dma_words(sW1, a.w.w1, 16 * F, tid);  // [W1; W1e] rows of F, packed
-    dma_words(sW1 + 16 * F, a.w.w1e, 16 * F, tid);
+  if (!RAS && !PIPED && (!PF || ac.first)) {
+    dma_words(sW1, a.w.w1, 16 * F, tid, DR_DMA_ROT * 5);  // [W1; W1e] rows of F, packed
+    dma_words(sW1 + 16 * F, a.w.w1e, 16 * F, tid, DR_DMA_ROT * 14);
   }
   {  // zero Z's K padding (cols XS..KPT; X's own pad is zero) and the pooling keys
     const int padz = KPT - XS;
@@ -985,6 +1126,14 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
   }
   __syncthreads();
 
+  if (PF && ac.next >= 0) {  // the next graph's inputs, under this graph's tail
+    STAMP(16);
+    const dr_graph_desc dn = dnext;
+    const Carve cn = carve_acc(dn.n_nodes, dn.n_edges, F, dn.n_k0, dn.n_p1, dn.n_k1, alias, OUT, ac.lay, ac.par ^ 1);
+    STAMP(17);
+    stage_inputs(dn, cn);
+    STAMP(18);
+  }
   TailLds t = tail_lds(c, lds);
   t.keep = skeep;
   t.acc = ACC ? ac.acc : nullptr;
@@ -1015,21 +1164,27 @@ __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
 // deterministic (another fp32 association than the per-graph partials: the
 // tests compare the two at fp32 tolerance).
 // ---------------------------------------------------------------------------
-// the accumulators' LDS words = the row: [dW1cat 32F | dW2cat 1024 | fc1.weight
-// 128 x 64 | fc1.bias 128 | fc2.weight OUT x 128 | fc2.bias OUT], then the loss
+// The accumulators (LDS, ahead of the graph carve): [dW1cat 32F | dW2cat 1024
+// | fc1.bias 128 | fc2.weight OUT x 128 | fc2.bias OUT | loss | pad | fc1.weight
+// 128 x 64 unless it is summed in registers (F <= 32)].  The row written per
+// workgroup: [dW1cat | dW2cat | fc1.weight | fc1.bias | fc2.weight | fc2.bias].
 __host__ __device__ inline int acc_row_floats(int F, int OUT) { return r4(32 * F + 1024 + 128 * 64 + 128 + 128 * OUT + OUT); }
-__host__ __device__ inline int acc_words(int F, int OUT) { return r4(32 * F + 1024 + 128 * 64 + 128 + 128 * OUT + OUT + 1); }
+__host__ __device__ inline int acc_head_words(int OUT) { return r4(128 + 128 * OUT + OUT + 1); }
+__host__ __device__ inline int acc_words(int F, int OUT, bool fc1_in_lds) {
+  return 32 * F + 1024 + acc_head_words(OUT) + (fc1_in_lds ? 128 * 64 : 0);
+}
 
-template <int KPT>
-__global__ void __launch_bounds__(NT) ginet_acc_kernel(GinetArgs a, const int32_t* plan) {
+template <int KPT, bool PF>
+__global__ void __launch_bounds__(NT) ginet_acc_kernel(GinetArgs a, const int32_t* plan, AccLayout lay) {
   extern __shared__ __attribute__((aligned(16))) float lds_raw[];
   const int F = a.s.n_feat, OUT = a.p.out_dim, tid = threadIdx.x;
+  constexpr bool REG = KPT == 32;  // fc1.weight's sums in registers where the kernel has them to spare
   AccCtx ac;
   ac.acc = lds_raw;
-  ac.acc_words = acc_words(F, OUT);
-  // fc1.weight's sums in registers where the kernel has them to spare (F <= 32)
+  ac.acc_words = acc_words(F, OUT, !REG);
+  ac.lay = lay;
   float accf[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  ac.accf = KPT == 32 ? accf : nullptr;
+  ac.accf = REG ? accf : nullptr;
   for (int p = tid; p < ac.acc_words; p += NT) lds_raw[p] = 0.f;
   __syncthreads();
   // plan: [R + 1 starts | the batch positions, workgroup by workgroup], or
@@ -1038,6 +1193,9 @@ __global__ void __launch_bounds__(NT) ginet_acc_kernel(GinetArgs a, const int32_
   const int k0 = plan ? plan[w] : 0, k1 = plan ? plan[w + 1] : (a.B - w + R - 1) / R;
   for (int k = k0; k < k1; ++k) {
     ac.gi = plan ? plan[R + 1 + k] : w + k * R;
+    ac.first = k == k0;
+    ac.par = (k - k0) & 1;
+    ac.next = k + 1 < k1 ? (plan ? plan[R + 2 + k] : w + (k + 1) * R) : -1;
     // the body reads the arguments from the kernarg segment through a pointer
     // the optimiser cannot follow across iterations: each graph reloads what it
     // uses (scalar loads) instead of every argument being held in SGPRs over the
@@ -1045,22 +1203,24 @@ __global__ void __launch_bounds__(NT) ginet_acc_kernel(GinetArgs a, const int32_
     typedef const __attribute__((address_space(4))) GinetArgs* KArgs;
     KArgs ka = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile("; dr_kargs" : "+s"(ka));
-    graph_body<KPT, false, false, false, NoHook, false, true>(*(const GinetArgs*)ka, SibCtx{}, NoHook{}, PipeCtx{}, ac);
+    graph_body<KPT, false, false, false, NoHook, false, true, PF>(*(const GinetArgs*)ka, SibCtx{}, NoHook{}, PipeCtx{}, ac);
     __syncthreads();  // the graph carve is restaged by the next graph
   }
-  const int c0 = 32 * F + 1024;
-  if (KPT == 32) {
-    float4* d = reinterpret_cast<float4*>(lds_raw + c0 + tid * 8);
-    d[0] = make_float4(accf[0], accf[1], accf[2], accf[3]);
-    d[1] = make_float4(accf[4], accf[5], accf[6], accf[7]);
-    __syncthreads();
-  }
   // the workgroup's row, then its loss sum
-  const int RS = acc_row_floats(F, OUT);
-  float4* row = reinterpret_cast<float4*>(a.p.slab + (int64_t)blockIdx.x * RS);
-  const float4* src = reinterpret_cast<const float4*>(lds_raw);
-  for (int p = tid; p < RS / 4; p += NT) row[p] = src[p];
-  if (tid == 0) a.p.loss_per_graph[blockIdx.x] = lds_raw[c0 + 128 * 64 + 128 + 128 * OUT + OUT];
+  const int c0 = 32 * F + 1024, HW = 128 + 128 * OUT + OUT;
+  float* row = a.p.slab + (int64_t)blockIdx.x * acc_row_floats(F, OUT);
+  for (int p = tid; p < c0 / 4; p += NT) reinterpret_cast<float4*>(row)[p] = reinterpret_cast<const float4*>(lds_raw)[p];
+  float4* rw = reinterpret_cast<float4*>(row + c0 + tid * 8);
+  if (REG) {
+    rw[0] = make_float4(accf[0], accf[1], accf[2], accf[3]);
+    rw[1] = make_float4(accf[4], accf[5], accf[6], accf[7]);
+  } else {
+    const float4* src = reinterpret_cast<const float4*>(lds_raw + c0 + acc_head_words(OUT) + tid * 8);
+    rw[0] = src[0];
+    rw[1] = src[1];
+  }
+  for (int p = tid; p < HW; p += NT) row[c0 + 128 * 64 + p] = lds_raw[c0 + p];
+  if (tid == 0) a.p.loss_per_graph[blockIdx.x] = lds_raw[c0 + HW];
 }
 
 // k sibling workgroups per graph: block -> (graph b, sibling rk), siblings 8
@@ -2138,14 +2298,23 @@ extern "C" int dr_ginet_graph_pass(const dr_graph_store* store, const dr_graph_d
 }
 
 // Accumulating pass: n_groups workgroups, graph gi on workgroup gi % n_groups
-// (or as plan lists them); each writes one row of dr_ginet_acc_row_floats floats to pass->slab and its
-// loss sum to pass->loss_per_graph[w].  lds_bytes is the graph carve (as for
-// dr_ginet_graph_pass); the accumulators' words are added here.
+// (or as plan lists them); each writes one row of dr_ginet_acc_row_floats
+// floats to pass->slab and its loss sum to pass->loss_per_graph[w].
+// max_sizes (host, optional): the batch's largest N, E, K0, P1, K1 — the
+// prefetch layout when it fits, else lds_bytes (the largest graph's carve, as
+// for dr_ginet_graph_pass) plus the accumulators.
 extern "C" int32_t dr_ginet_acc_row_floats(int32_t n_feat, int32_t out_dim) { return acc_row_floats(n_feat, out_dim); }
+
+extern "C" int64_t dr_ginet_acc_lds_bytes(const int32_t* max_sizes, int32_t n_feat, int32_t transpose_aliased, int32_t out_dim) {
+  if (!max_sizes) return -1;
+  const AccLayout L = acc_layout(max_sizes[0], max_sizes[1], n_feat, max_sizes[2], max_sizes[3], max_sizes[4],
+                                 transpose_aliased, out_dim);
+  return 4LL * (acc_words(n_feat, out_dim, n_feat > 32) + L.total);
+}
 
 extern "C" int dr_ginet_acc_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
                                  const dr_ginet_weights* w, const dr_pass* pass, int32_t lds_bytes, int32_t n_groups,
-                                 const int32_t* plan, void* stream) {
+                                 const int32_t* plan, const int32_t* max_sizes, void* stream) {
   if (!store || !descs || !w || !pass || n_batch < 0 || n_groups < 1) return DR_E_ARG;
   if (pass->out_dim < 1 || pass->out_dim > DR_MAX_OUT) return DR_E_UNSUPPORTED;
   if (store->n_feat < 1 || 32 * store->n_feat > 2 * NT) return DR_E_UNSUPPORTED;  // F <= 64
@@ -2156,8 +2325,16 @@ extern "C" int dr_ginet_acc_pass(const dr_graph_store* store, const dr_graph_des
   if ((pass->flags & DR_PASS_FORWARD) && !pass->out) return DR_E_ARG;
   if (pass->use_dropout == DR_DROPOUT_MASK && !pass->mask) return DR_E_ARG;
   if (pass->use_dropout < DR_DROPOUT_OFF || pass->use_dropout > DR_DROPOUT_HASH) return DR_E_ARG;
-  const int64_t lds = (int64_t)lds_bytes + 4LL * acc_words(store->n_feat, pass->out_dim);
-  if (lds > 160 * 1024) return DR_E_LDS;
+  const int F = store->n_feat, OUT = pass->out_dim;
+  const int64_t lds = (int64_t)lds_bytes + 4LL * acc_words(F, OUT, F > 32);
+  AccLayout L{};
+  int64_t lds_pf = -1;
+  if (max_sizes) {
+    L = acc_layout(max_sizes[0], max_sizes[1], F, max_sizes[2], max_sizes[3], max_sizes[4], store->transpose_aliased, OUT);
+    lds_pf = dr_ginet_acc_lds_bytes(max_sizes, F, store->transpose_aliased, OUT);
+  }
+  const bool pf = lds_pf > 0 && lds_pf <= 160 * 1024;
+  if (!pf && lds > 160 * 1024) return DR_E_LDS;
   if (n_batch == 0) return DR_OK;
   if (!store->cl0) return DR_E_ARG;
   if (n_groups > n_batch && !plan) n_groups = n_batch;
@@ -2167,13 +2344,20 @@ extern "C" int dr_ginet_acc_pass(const dr_graph_store* store, const dr_graph_des
   args.p = *pass;
   args.descs = descs;
   args.B = n_batch;
-  if (store->n_feat <= 32) {
-    DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_acc_kernel<32>)));
-    hipLaunchKernelGGL(ginet_acc_kernel<32>, dim3(n_groups), dim3(NT), (int)lds, (hipStream_t)stream, args, plan);
+  const hipStream_t st = (hipStream_t)stream;
+#define DR_ACC_LAUNCH(KPT, PF, BYTES)                                                                   \
+  do {                                                                                                \
+    DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_acc_kernel<KPT, PF>)));            \
+    hipLaunchKernelGGL((ginet_acc_kernel<KPT, PF>), dim3(n_groups), dim3(NT), (int)(BYTES), st, args, plan, L); \
+  } while (0)
+  if (F <= 32) {
+    if (pf) DR_ACC_LAUNCH(32, true, lds_pf);
+    else DR_ACC_LAUNCH(32, false, lds);
   } else {
-    DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_acc_kernel<64>)));
-    hipLaunchKernelGGL(ginet_acc_kernel<64>, dim3(n_groups), dim3(NT), (int)lds, (hipStream_t)stream, args, plan);
+    if (pf) DR_ACC_LAUNCH(64, true, lds_pf);
+    else DR_ACC_LAUNCH(64, false, lds);
   }
+#undef DR_ACC_LAUNCH
   return (int)hipGetLastError();
 }
 

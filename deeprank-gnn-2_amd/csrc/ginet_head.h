@@ -19,9 +19,9 @@ struct GinetHeadLds {
   float *fc2, *g, *hpre, *hh, *hd, *dh, *dg, *dout, *dgp;
   const uint8_t* keep = nullptr;  // optional [128] dropout keep flags computed ahead (head_keep_prefetch)
   // accumulating pass (dr_ginet_acc_pass): the workgroup's running sums of the
-  // head gradients over its graphs, [fc1.weight 128 x 64 | fc1.bias 128 |
-  // fc2.weight OUT x 128 | fc2.bias OUT | loss 1], instead of per-graph head
-  // vectors (16-byte aligned)
+  // head gradients over its graphs, [fc1.bias 128 | fc2.weight OUT x 128 |
+  // fc2.bias OUT | loss 1 | pad to 16 B | fc1.weight 128 x 64 unless accf],
+  // instead of per-graph head vectors (16-byte aligned)
   float* acc = nullptr;
   float* accf = nullptr;  // or: fc1.weight's sums of this thread (row tid/8, columns 8 (tid%8) ..) in registers
 };
@@ -118,7 +118,7 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
   if (tid == 0) {
     if (p.loss_kind == DR_LOSS_MSE) {
       const float d = t.dout[0] - y_g;
-      if (ACC) t.acc[8192 + 128 + 128 * OUT + OUT] += d * d;
+      if (ACC) t.acc[128 + 128 * OUT + OUT] += d * d;
       else if (p.loss_per_graph) st_part<WT>(p.loss_per_graph + pb, d * d);
       t.dout[0] = 2.f * d * p.loss_scale;
       for (int q = 1; q < OUT; ++q) t.dout[q] = 0.f;  // the loss reads column 0 only (engine's layer path alike)
@@ -130,7 +130,7 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
       for (int q = 0; q < OUT; ++q) se += expf(t.dout[q] - mx);
       const float lse = mx + logf(se);
       const float wy = p.class_w ? p.class_w[yi] : 1.f;
-      if (ACC) t.acc[8192 + 128 + 128 * OUT + OUT] += wy * (lse - t.dout[yi]);
+      if (ACC) t.acc[128 + 128 * OUT + OUT] += wy * (lse - t.dout[yi]);
       else if (p.loss_per_graph) st_part<WT>(p.loss_per_graph + pb, wy * (lse - t.dout[yi]));
       for (int q = 0; q < OUT; ++q) t.dout[q] = wy * (expf(t.dout[q] - lse) - (q == yi ? 1.f : 0.f)) * p.loss_scale;
     } else {
@@ -174,14 +174,14 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
       f[0] = fmaf(dhr, x0.x, f[0]); f[1] = fmaf(dhr, x0.y, f[1]); f[2] = fmaf(dhr, x0.z, f[2]); f[3] = fmaf(dhr, x0.w, f[3]);
       f[4] = fmaf(dhr, x1.x, f[4]); f[5] = fmaf(dhr, x1.y, f[5]); f[6] = fmaf(dhr, x1.z, f[6]); f[7] = fmaf(dhr, x1.w, f[7]);
     } else {  // in LDS (the row's fc1.weight block)
-      float4* w = reinterpret_cast<float4*>(t.acc + r * 64 + part * 8);
+      float4* w = reinterpret_cast<float4*>(t.acc + ((128 + 128 * OUT + OUT + 1 + 3) & ~3) + r * 64 + part * 8);
       float4 v0 = w[0], v1 = w[1];
       v0.x = fmaf(dhr, x0.x, v0.x); v0.y = fmaf(dhr, x0.y, v0.y); v0.z = fmaf(dhr, x0.z, v0.z); v0.w = fmaf(dhr, x0.w, v0.w);
       v1.x = fmaf(dhr, x1.x, v1.x); v1.y = fmaf(dhr, x1.y, v1.y); v1.z = fmaf(dhr, x1.z, v1.z); v1.w = fmaf(dhr, x1.w, v1.w);
       w[0] = v0;
       w[1] = v1;
     }
-    float* hacc = t.acc + 128 * 64;
+    float* hacc = t.acc;
     if (tid < 128) {
       hacc[tid] += t.dh[tid];
       for (int q = 0; q < OUT; ++q) hacc[128 + q * 128 + tid] = fmaf(t.dout[q], t.hd[tid], hacc[128 + q * 128 + tid]);

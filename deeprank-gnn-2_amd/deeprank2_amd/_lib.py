@@ -221,8 +221,9 @@ class ParamTableC(ctypes.Structure):
 SIGNATURES = [
     ("dr_ginet_graph_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, VP]),
     ("dr_ginet_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 8),
-    ("dr_ginet_acc_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, ctypes.c_int32, VP, VP]),
+    ("dr_ginet_acc_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, ctypes.c_int32, VP, _c_i32, VP]),
     ("dr_ginet_acc_row_floats", ctypes.c_int32, [ctypes.c_int32] * 2),
+    ("dr_ginet_acc_lds_bytes", ctypes.c_int64, [_c_i32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
     ("dr_ginet_large_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(LargePlanC), ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, ctypes.c_int32, VP]),
     ("dr_ginet_sibling_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(LargePlanC), ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, ctypes.c_int32, VP]),
     ("dr_ginet_large_conv_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 5),

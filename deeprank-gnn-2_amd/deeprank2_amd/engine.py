@@ -28,6 +28,8 @@ reduced gradients.  That is the only collective (``distributed.py`` shards).
 
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from deeprank2_amd import _lib, layered
@@ -366,8 +368,7 @@ class FusedTrainStep:
             return 0
         f = self.model.input_shape
         lib = _lib.load()
-        words = (32 * f + 1024 + 128 + 128 * self.out_dim + self.out_dim + 1 + 3) & ~3
-        if lds_for(self.spec, h, self.out_dim) + 4 * words > 160 * 1024:  # noqa: PLR2004
+        if self.acc_lds(h) > 160 * 1024:  # noqa: PLR2004
             return 0
         r = min(r, h.B)
         rs = int(lib.dr_ginet_acc_row_floats(f, self.out_dim))
@@ -391,6 +392,34 @@ class FusedTrainStep:
             self._table_acc.slab_rows = 1
         return r
 
+    # the accumulating pass's prefetch layout where it fits (opt-in: measured
+    # slower, DESIGN §5 — the LDS DMA instructions hold their waves at issue)
+    acc_prefetch = False
+
+    def _acc_max_sizes(self, h: BatchHandle):
+        if not self.acc_prefetch:
+            return None
+        key = "acc_max_sizes"
+        m = h._lds.get(key)  # noqa: SLF001
+        if m is None:
+            m = h._lds[key] = (ctypes.c_int32 * 5)(*h.max_sizes)  # noqa: SLF001
+        return m
+
+    def acc_lds(self, h: BatchHandle) -> int:
+        """Dynamic LDS bytes the accumulating pass takes for this batch: the
+        prefetch layout when it fits, else the largest graph's carve plus the
+        accumulators."""
+        from deeprank2_amd.fused import lds_for  # noqa: PLC0415
+
+        f, out = self.model.input_shape, self.out_dim
+        m = self._acc_max_sizes(h)
+        if m is not None:
+            pf = int(_lib.load().dr_ginet_acc_lds_bytes(m, f, int(h.store.packed.transpose_aliased), out))
+            if 0 < pf <= 160 * 1024:  # noqa: PLR2004
+                return pf
+        words = 32 * f + 1024 + ((128 + 128 * out + out + 1 + 3) & ~3) + (8192 if f > 32 else 0)  # noqa: PLR2004
+        return lds_for(self.spec, h, out) + 4 * words
+
     def _launch_pass(self, h: BatchHandle, p) -> int:
         """The graph pass of a two-launch step: the accumulating pass (returns
         its row count) or the model's per-graph pass (returns 0)."""
@@ -403,7 +432,7 @@ class FusedTrainStep:
         p.slab = self._acc_slab.data_ptr()
         plan = acc_plan(h, r)
         try:
-            rc = _lib.load().dr_ginet_acc_pass(h.store.cstruct(), h.descs.data_ptr(), h.B, self._w, p, lds_for(self.spec, h, self.out_dim), r, plan.data_ptr(), _lib.stream_ptr(self.device))
+            rc = _lib.load().dr_ginet_acc_pass(h.store.cstruct(), h.descs.data_ptr(), h.B, self._w, p, lds_for(self.spec, h, self.out_dim), r, plan.data_ptr(), self._acc_max_sizes(h), _lib.stream_ptr(self.device))
         finally:
             p.slab = self.slab.data_ptr()
         _lib.check(rc, "dr_ginet_acc_pass")

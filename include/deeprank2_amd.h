@@ -236,11 +236,19 @@ int64_t dr_ginet_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_feat, int
  * device int32 [n_groups + 1 + n_batch]): workgroup w runs the batch
  * positions plan[n_groups + 1 + k] for k in [plan[w], plan[w + 1]) in that
  * order (every position exactly once: the caller balances the work, e.g. by
- * graph size); NULL: positions w, w + n_groups, ...                         */
+ * graph size); NULL: positions w, w + n_groups, ...
+ * max_sizes (optional, host int32 [5]): the batch's largest n_nodes, n_edges,
+ * n_k0, n_p1, n_k1.  When given and dr_ginet_acc_lds_bytes(max_sizes, ...)
+ * fits 160 KB, the prefetch layout runs: the weights stay in LDS across a
+ * workgroup's graphs and graph k+1's inputs are DMA'd while graph k's tail
+ * runs; otherwise lds_bytes applies.  Same results either way.             */
 int dr_ginet_acc_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
                       const dr_ginet_weights* w, const dr_pass* pass, int32_t lds_bytes, int32_t n_groups,
-                      const int32_t* plan, void* stream);
+                      const int32_t* plan, const int32_t* max_sizes, void* stream);
 int32_t dr_ginet_acc_row_floats(int32_t n_feat, int32_t out_dim);
+/* Dynamic LDS bytes of dr_ginet_acc_pass's prefetch layout for these batch
+ * maxima (host int32 [5] as above), or -1 for NULL.                          */
+int64_t dr_ginet_acc_lds_bytes(const int32_t* max_sizes, int32_t n_feat, int32_t transpose_aliased, int32_t out_dim);
 
 /* ---- GINet on graphs larger than one workgroup's LDS (atom-level graphs) ----
  * Two launches with the same result as dr_ginet_graph_pass:

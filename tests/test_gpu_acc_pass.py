@@ -80,6 +80,26 @@ def test_acc_pass_matches_per_graph_partials(n, groups):
     _assert_close_grads(acc, per, f"B={n} groups={groups}")
 
 
+@pytest.mark.parametrize("n", [300, 1000])
+def test_acc_prefetch_layout_bit_identical(n):
+    """The prefetch layout (weights kept in LDS across a workgroup's graphs,
+    graph k+1's inputs DMA'd under graph k's tail) moves data, not
+    arithmetic: bit-identical to the accumulating pass without it."""
+    store = GraphStore(pack_graphs(_records(n, 44)), DEV)
+    one, _ = _pair()
+    two, _ = _pair()
+    one.acc_prefetch, two.acc_prefetch = True, False
+    h = BatchHandle(store, np.arange(n, dtype=np.int32))
+    assert one.acc_lds(h) != two.acc_lds(h), "the prefetch layout must be the one taken"
+    for _ in range(2):
+        l1, o1 = one.step(h)
+        l2, o2 = two.step(h)
+        torch.cuda.synchronize()
+        assert torch.equal(o1, o2) and torch.equal(l1, l2)
+    for k, (a, b) in enumerate(zip(one._state_tensors(), two._state_tensors())):  # noqa: SLF001
+        assert torch.equal(a, b), f"state tensor {k}"
+
+
 def test_acc_pass_cross_entropy_ragged_several_steps():
     """CE with 3 classes over batches of varying size (one of them below the
     CU count: auto mode takes the per-graph partials there), 3 steps; the

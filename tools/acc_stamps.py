@@ -76,6 +76,12 @@ def main():
         for k in range(1, len(g)):
             gaps.append(a[:, g[k], 0] - a[:, g[k - 1], n])
     gaps = np.concatenate(gaps)
+    pf = a[:, :, 16] > 0
+    if pf.any():
+        d1 = (a[:, :, 17] - a[:, :, 16])[pf]
+        d2 = (a[:, :, 18] - a[:, :, 17])[pf]
+        d3 = (a[:, :, 4] - a[:, :, 18])[pf]
+        print(f"  acc prefetch (wave 0): next descriptor {np.median(d1):.0f} cyc, DMA issue {np.median(d2):.0f} cyc, issue -> tail start {np.median(d3):.0f} cyc")
     print(f"  acc: gap between a workgroup's consecutive graphs: median {np.median(gaps):.0f} cyc, p90 {np.percentile(gaps, 90):.0f}")
     # per-graph kernel: the spread of graph spans (longest / median)
     span = a[:, :, n] - a[:, :, 0]
