@@ -755,6 +755,19 @@ __device__ __forceinline__ void pipe_wait(const PipeCtx& pc, uint32_t* lf) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // the weight loads stay below the poll
 }
 
+// A graph descriptor by one s_load_dwordx16 (the pointer is wave-uniform)
+__device__ __forceinline__ dr_graph_desc desc_scalar(const dr_graph_desc* p) {
+  typedef int v16i __attribute__((ext_vector_type(16)));
+  const uint64_t u = reinterpret_cast<uint64_t>(p);
+  const uint64_t su = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(u >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)u);
+  v16i r;
+  asm volatile("s_load_dwordx16 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(su));
+  dr_graph_desc d;
+  __builtin_memcpy(&d, &r, sizeof(d));
+  return d;
+}
+
 // Accumulating pass (dr_ginet_acc_pass): a workgroup runs graphs gi, gi + R,
 // ... one after another and adds each graph's gradients to running sums (LDS
 // region acc at the front of its LDS, fc1.weight's in the caller's registers)
@@ -783,9 +796,12 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
   const int wave = dr_wave<ACC>(tid);
   const int b = SIB ? sc.b : ACC ? ac.gi : (int)blockIdx.x;
   const dr_graph_store& s = a.s;
-  const dr_graph_desc d = a.descs[b];  // one 64-byte scalar load
+  // one 64-byte scalar load (ACC: spelled out — in the accumulating kernel's
+  // loop hipcc cannot prove the descriptors unwritten and reads them with
+  // vector loads and readfirstlanes, ~1 K cycles)
+  const dr_graph_desc d = ACC ? desc_scalar(a.descs + b) : a.descs[b];
   // PF: the next graph's descriptor, read now so its latency hides under the front half
-  const dr_graph_desc dnext = (PF && ac.next >= 0) ? a.descs[ac.next] : d;
+  const dr_graph_desc dnext = (PF && ac.next >= 0) ? desc_scalar(a.descs + ac.next) : d;
   const int g = d.gid;
   const int64_t n0 = d.node0, ec0 = d.col0, k00 = d.k0, q0 = d.p1, k10 = d.k1;
   const int N = d.n_nodes, E = d.n_edges, K0 = d.n_k0, P1 = d.n_p1, K1 = d.n_k1;
@@ -1190,12 +1206,14 @@ __global__ void __launch_bounds__(NT) ginet_acc_kernel(GinetArgs a, const int32_
   // plan: [R + 1 starts | the batch positions, workgroup by workgroup], or
   // null: every R-th position from blockIdx.x
   const int R = gridDim.x, w = blockIdx.x;
-  const int k0 = plan ? plan[w] : 0, k1 = plan ? plan[w + 1] : (a.B - w + R - 1) / R;
+  typedef const __attribute__((address_space(4))) int32_t* CPlan;  // scalar loads (read-only for the launch)
+  const CPlan cp = (CPlan)plan;
+  const int k0 = plan ? cp[w] : 0, k1 = plan ? cp[w + 1] : (a.B - w + R - 1) / R;
   for (int k = k0; k < k1; ++k) {
-    ac.gi = plan ? plan[R + 1 + k] : w + k * R;
+    ac.gi = plan ? cp[R + 1 + k] : w + k * R;
     ac.first = k == k0;
     ac.par = (k - k0) & 1;
-    ac.next = k + 1 < k1 ? (plan ? plan[R + 2 + k] : w + (k + 1) * R) : -1;
+    ac.next = k + 1 < k1 ? (plan ? cp[R + 2 + k] : w + (k + 1) * R) : -1;
     // the body reads the arguments from the kernarg segment through a pointer
     // the optimiser cannot follow across iterations: each graph reloads what it
     // uses (scalar loads) instead of every argument being held in SGPRs over the

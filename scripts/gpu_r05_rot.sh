@@ -7,3 +7,6 @@ for v in stamps0 stamps; do
   echo "== $v"; grep -v amdgpu.ids $O/stamps_$v.txt | head -8
 done
 bash scripts/gpu_ab.sh r05rot/ab "rot0 -" "--model ginet" 3 "acc or train_step or test_gpu_ginet"
+timeout -k 10 300 python tools/acc_stamps.py 4096 > $O/acc_stamps.txt 2>&1 || exit 1
+grep -v amdgpu.ids $O/acc_stamps.txt
+bash scripts/gpu_r05_acc2.sh
