@@ -43,7 +43,7 @@
 namespace {
 
 #ifndef DR_DMA_ROT
-#define DR_DMA_ROT 1
+#define DR_DMA_ROT 0  // 1: spread starting waves (measured 0.1 us slower per pass, r05)
 #endif
 constexpr int NT = 1024;     // 16 waves
 constexpr int NW = NT / 64;
@@ -114,14 +114,14 @@ __host__ __device__ inline Carve carve(int N, int E, int F, int K0, int P1, int 
 
 // The accumulating pass's prefetch layout (dr_ginet_acc_pass with the batch's
 // maximum sizes): the weights stay put across a workgroup's graphs, and the
-// inputs of graph k+1 are DMA'd while graph k's tail runs, so they need
-// regions graph k's tail does not touch:
-//   [W1 | W2 | fc2] [front inputs: x rp col cl0 — dead once the front half is
-//   done] [tail inputs, two buffers by graph parity: p1rp p1c p1trp p1tc m1p
-//   m1i] [scratch: z key p1 a1 dp1 y2 h2 p2 nt cl1 head dgp keep]
+// inputs of graph k+1 are DMA'd by the waves that have no tile in graph k's
+// front half (N <= 240), into the other of two input buffers:
+//   [W1 | W2 | fc2] [inputs, parity 0: x rp col cl0 p1rp p1c p1trp p1tc m1p
+//   m1i] [inputs, parity 1] [scratch: z key p1 a1 dp1 y2 h2 p2 nt cl1 head
+//   dgp keep]
 // (word offsets from the carve base; each region sized for the batch maxima).
 struct AccLayout {
-  int fin, tin0, tin1, scr, total;
+  int in0, in1, scr, total;
 };
 
 __host__ __device__ inline Carve carve_acc(int N, int E, int F, int K0, int P1, int K1, int alias, int OUT,
@@ -137,12 +137,11 @@ __host__ __device__ inline Carve carve_acc(int N, int E, int F, int K0, int P1, 
   TAKE(w1, 32 * F)
   TAKE(w2, 1024)
   TAKE(fc2, OUT * 128 + OUT)
-  o = L.fin;
+  o = par ? L.in1 : L.in0;
   TAKE(x, N * c.XS)
   TAKE(rp, N + 1)
   TAKE(col, (E + 1) / 2)
   TAKE(cl0, N)
-  o = par ? L.tin1 : L.tin0;
   TAKE(p1rp, K0 + 1)
   TAKE(p1c, P1)
   if (alias) {
@@ -176,12 +175,12 @@ __host__ __device__ inline Carve carve_acc(int N, int E, int F, int K0, int P1, 
 // the layout for the batch maxima (every graph's carve_acc fits inside it)
 __host__ __device__ inline AccLayout acc_layout(int Nm, int Em, int F, int K0m, int P1m, int K1m, int alias, int OUT) {
   AccLayout L;
-  L.fin = r4(32 * F) + 1024 + r4(OUT * 128 + OUT);
+  L.in0 = r4(32 * F) + 1024 + r4(OUT * 128 + OUT);
   const int XS = r4(F), LDW = r16(F) + 2;
-  L.tin0 = L.fin + r4(Nm * XS) + r4(Nm + 1) + r4((Em + 1) / 2) + r4(Nm);
-  const int tin = r4(K0m + 1) + r4(P1m) + (alias ? 0 : r4(K0m + 1) + r4(P1m)) + r4(K1m + 1) + r4(K0m);
-  L.tin1 = L.tin0 + tin;
-  L.scr = L.tin1 + tin;
+  const int in = r4(Nm * XS) + r4(Nm + 1) + r4((Em + 1) / 2) + r4(Nm) + r4(K0m + 1) + r4(P1m) +
+                 (alias ? 0 : r4(K0m + 1) + r4(P1m)) + r4(K1m + 1) + r4(K0m);
+  L.in1 = L.in0 + in;
+  L.scr = L.in1 + in;
   L.total = L.scr + r4(Nm * LDW) + r4(2 * K0m * 32) + 3 * r4(K0m * 32) + 2 * r4(K0m * 64) + 2 * r4(K1m * 64) + r4(K0m) +
             r4(HEADW) + r4(NW * 64) + r4(32);
   return L;
@@ -242,6 +241,30 @@ __device__ __forceinline__ void dma_words_async(void* lds_dst, const void* gsrc,
   for (int base = wave * 64; base < n; base += NT)
     if (base + lane < n)
       asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" ::"s"(__builtin_amdgcn_readfirstlane(dst + 4 * base)),
+                   "v"(src + base + lane)
+                   : "m0");
+}
+
+// the same over waves [wf, wf + nw) only (the others skip)
+__device__ __forceinline__ void dma_words_async_sub(void* lds_dst, const void* gsrc, int n, int tid, int wf, int nw) {
+  const int lane = tid & 63, rw = __builtin_amdgcn_readfirstlane((tid >> 6) - wf);
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(gsrc);
+  const uint32_t dst = (uint32_t)(size_t)AS3(lds_dst);
+  if (rw < 0) return;
+  for (int base = rw * 64; base < n; base += nw * 64)
+    if (base + lane < n)
+      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" ::"s"(__builtin_amdgcn_readfirstlane(dst + 4 * base)),
+                   "v"(src + base + lane)
+                   : "m0");
+}
+__device__ __forceinline__ void dma_x4_async_sub(void* lds_dst, const void* gsrc, int n4, int tid, int wf, int nw) {
+  const int lane = tid & 63, rw = __builtin_amdgcn_readfirstlane((tid >> 6) - wf);
+  const uint4* src = reinterpret_cast<const uint4*>(gsrc);
+  const uint32_t dst = (uint32_t)(size_t)AS3(lds_dst);
+  if (rw < 0) return;
+  for (int base = rw * 64; base < n4; base += nw * 64)
+    if (base + lane < n4)
+      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(__builtin_amdgcn_readfirstlane(dst + 16 * base)),
                    "v"(src + base + lane)
                    : "m0");
 }
@@ -755,14 +778,24 @@ __device__ __forceinline__ void pipe_wait(const PipeCtx& pc, uint32_t* lf) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // the weight loads stay below the poll
 }
 
-// A graph descriptor by one s_load_dwordx16 (the pointer is wave-uniform)
-__device__ __forceinline__ dr_graph_desc desc_scalar(const dr_graph_desc* p) {
-  typedef int v16i __attribute__((ext_vector_type(16)));
+// A graph descriptor by one s_load_dwordx16 (the pointer is wave-uniform);
+// `touch` (optional): one dword of another descriptor loaded beside it and
+// dropped, so that line is in the scalar cache when its graph starts
+__device__ __forceinline__ uint64_t uniform_ptr(const void* p) {
   const uint64_t u = reinterpret_cast<uint64_t>(p);
-  const uint64_t su = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(u >> 32)) << 32) |
-                      (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)u);
+  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(u >> 32)) << 32) | (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)u);
+}
+__device__ __forceinline__ dr_graph_desc desc_scalar(const dr_graph_desc* p, const dr_graph_desc* touch = nullptr) {
+  typedef int v16i __attribute__((ext_vector_type(16)));
   v16i r;
-  asm volatile("s_load_dwordx16 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(su));
+  if (touch) {
+    int dropped;
+    asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dword %1, %3, 0x0\n\ts_waitcnt lgkmcnt(0)"
+                 : "=s"(r), "=s"(dropped)
+                 : "s"(uniform_ptr(p)), "s"(uniform_ptr(touch)));
+  } else {
+    asm volatile("s_load_dwordx16 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(uniform_ptr(p)));
+  }
   dr_graph_desc d;
   __builtin_memcpy(&d, &r, sizeof(d));
   return d;
@@ -783,6 +816,9 @@ struct AccCtx {
   AccLayout lay;
   int par = 0, next = -1;
   bool first = true;
+  // PF: LDS word set to 1 by the graph whose idle waves staged the next
+  // graph's inputs (read by that next graph before its staging)
+  uint32_t* staged = nullptr;
 };
 
 template <int KPT, bool WT, bool SIB = false, bool RAS = false, class Hook = NoHook, bool PIPED = false, bool ACC = false,
@@ -799,9 +835,7 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
   // one 64-byte scalar load (ACC: spelled out — in the accumulating kernel's
   // loop hipcc cannot prove the descriptors unwritten and reads them with
   // vector loads and readfirstlanes, ~1 K cycles)
-  const dr_graph_desc d = ACC ? desc_scalar(a.descs + b) : a.descs[b];
-  // PF: the next graph's descriptor, read now so its latency hides under the front half
-  const dr_graph_desc dnext = (PF && ac.next >= 0) ? desc_scalar(a.descs + ac.next) : d;
+  const dr_graph_desc d = ACC ? desc_scalar(a.descs + b, ac.next >= 0 ? a.descs + ac.next : nullptr) : a.descs[b];
   const int g = d.gid;
   const int64_t n0 = d.node0, ec0 = d.col0, k00 = d.k0, q0 = d.p1, k10 = d.k1;
   const int N = d.n_nodes, E = d.n_edges, K0 = d.n_k0, P1 = d.n_p1, K1 = d.n_k1;
@@ -884,7 +918,7 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
     dma_words_async(lds + cc.m1p, s.m1_ptr + dd.k1 + dg, dd.n_k1 + 1, tid, 8);
     dma_words_async(lds + cc.m1i, s.m1_idx + dk00, dK0, tid, 1);
   };
-  if (!PF) {  // (DR_DMA_ROT: starting waves spread over the copies, A/B)
+  if (!PF) {  // (DR_DMA_ROT = 1: starting waves spread over the copies; measured slower)
     dma_x4(sX, s.x + n0 * (int64_t)XS, N * XS / 4, tid);
     dma_x4(scol, s.col + ec0, (E + 7) / 8, tid, DR_DMA_ROT * 7);
     dma_words(srp, s.rowptr + n0 + g, N + 1, tid, DR_DMA_ROT * 13);
@@ -897,7 +931,7 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
     }
     dma_words(sm1p, s.m1_ptr + k10 + g, K1 + 1, tid, DR_DMA_ROT * 8);
     dma_words(sm1i, s.m1_idx + k00, K0, tid, DR_DMA_ROT * 1);
-  } else if (ac.first) {
+  } else if (ac.first || *ac.staged == 0u) {
     stage_inputs(d, c);
   }
   if (!RAS && !PIPED && (!PF || ac.first)) {
@@ -988,6 +1022,29 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
       }
     };
     if (!PIPED) load_w1();
+    if (PF) {  // the waves with no tile stage the next graph's inputs into the other buffer
+      const int busy = (N + 15) >> 4;
+      if (ac.next >= 0 && busy < NW && wave >= busy) {
+        const dr_graph_desc dn = desc_scalar(a.descs + ac.next);
+        const Carve cn = carve_acc(dn.n_nodes, dn.n_edges, F, dn.n_k0, dn.n_p1, dn.n_k1, alias, OUT, ac.lay, ac.par ^ 1);
+        const int nw = NW - busy;
+        const int64_t dn0 = dn.node0, dk00 = dn.k0;
+        const int dg = dn.gid, dN = dn.n_nodes, dK0 = dn.n_k0;
+        dma_x4_async_sub(lds + cn.x, s.x + dn0 * (int64_t)XS, dN * XS / 4, tid, busy, nw);
+        dma_x4_async_sub(lds + cn.col, s.col + dn.col0, (dn.n_edges + 7) / 8, tid, busy, nw);
+        dma_words_async_sub(lds + cn.rp, s.rowptr + dn0 + dg, dN + 1, tid, busy, nw);
+        dma_words_async_sub(lds + cn.cl0, s.cl0 + dn0, dN, tid, busy, nw);
+        dma_words_async_sub(lds + cn.p1rp, s.p1_rowptr + dk00 + dg, dK0 + 1, tid, busy, nw);
+        dma_words_async_sub(lds + cn.p1c, s.p1_col + dn.p1, dn.n_p1, tid, busy, nw);
+        if (!alias) {
+          dma_words_async_sub(lds + cn.p1trp, s.p1t_rowptr + dk00 + dg, dK0 + 1, tid, busy, nw);
+          dma_words_async_sub(lds + cn.p1tc, s.p1t_col + dn.p1, dn.n_p1, tid, busy, nw);
+        }
+        dma_words_async_sub(lds + cn.m1p, s.m1_ptr + dn.k1 + dg, dn.n_k1 + 1, tid, busy, nw);
+        dma_words_async_sub(lds + cn.m1i, s.m1_idx + dk00, dK0, tid, busy, nw);
+      }
+      if (tid == 0) *ac.staged = (ac.next >= 0 && busy < NW) ? 1u : 0u;
+    }
     for (int tt = SIB ? wave * sc.k + sc.rk : wave; tt * 16 < N; tt += SIB ? NW * sc.k : NW) {
       const int r0 = tt * 16;
       {  // rows r0+slot and r0+8+slot together: two independent edge chains per lane
@@ -1142,14 +1199,6 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
   }
   __syncthreads();
 
-  if (PF && ac.next >= 0) {  // the next graph's inputs, under this graph's tail
-    STAMP(16);
-    const dr_graph_desc dn = dnext;
-    const Carve cn = carve_acc(dn.n_nodes, dn.n_edges, F, dn.n_k0, dn.n_p1, dn.n_k1, alias, OUT, ac.lay, ac.par ^ 1);
-    STAMP(17);
-    stage_inputs(dn, cn);
-    STAMP(18);
-  }
   TailLds t = tail_lds(c, lds);
   t.keep = skeep;
   t.acc = ACC ? ac.acc : nullptr;
@@ -1197,7 +1246,8 @@ __global__ void __launch_bounds__(NT) ginet_acc_kernel(GinetArgs a, const int32_
   constexpr bool REG = KPT == 32;  // fc1.weight's sums in registers where the kernel has them to spare
   AccCtx ac;
   ac.acc = lds_raw;
-  ac.acc_words = acc_words(F, OUT, !REG);
+  ac.acc_words = acc_words(F, OUT, !REG) + 4;  // + the staged flag (16 bytes)
+  ac.staged = reinterpret_cast<uint32_t*>(lds_raw + ac.acc_words - 4);
   ac.lay = lay;
   float accf[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   ac.accf = REG ? accf : nullptr;
@@ -2327,7 +2377,7 @@ extern "C" int64_t dr_ginet_acc_lds_bytes(const int32_t* max_sizes, int32_t n_fe
   if (!max_sizes) return -1;
   const AccLayout L = acc_layout(max_sizes[0], max_sizes[1], n_feat, max_sizes[2], max_sizes[3], max_sizes[4],
                                  transpose_aliased, out_dim);
-  return 4LL * (acc_words(n_feat, out_dim, n_feat > 32) + L.total);
+  return 4LL * (acc_words(n_feat, out_dim, n_feat > 32) + 4 + L.total);
 }
 
 extern "C" int dr_ginet_acc_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
@@ -2344,7 +2394,7 @@ extern "C" int dr_ginet_acc_pass(const dr_graph_store* store, const dr_graph_des
   if (pass->use_dropout == DR_DROPOUT_MASK && !pass->mask) return DR_E_ARG;
   if (pass->use_dropout < DR_DROPOUT_OFF || pass->use_dropout > DR_DROPOUT_HASH) return DR_E_ARG;
   const int F = store->n_feat, OUT = pass->out_dim;
-  const int64_t lds = (int64_t)lds_bytes + 4LL * acc_words(F, OUT, F > 32);
+  const int64_t lds = (int64_t)lds_bytes + 4LL * (acc_words(F, OUT, F > 32) + 4);
   AccLayout L{};
   int64_t lds_pf = -1;
   if (max_sizes) {

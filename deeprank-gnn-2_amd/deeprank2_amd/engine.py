@@ -417,7 +417,7 @@ class FusedTrainStep:
             pf = int(_lib.load().dr_ginet_acc_lds_bytes(m, f, int(h.store.packed.transpose_aliased), out))
             if 0 < pf <= 160 * 1024:  # noqa: PLR2004
                 return pf
-        words = 32 * f + 1024 + ((128 + 128 * out + out + 1 + 3) & ~3) + (8192 if f > 32 else 0)  # noqa: PLR2004
+        words = 32 * f + 1024 + ((128 + 128 * out + out + 1 + 3) & ~3) + (8192 if f > 32 else 0) + 4  # noqa: PLR2004
         return lds_for(self.spec, h, out) + 4 * words
 
     def _launch_pass(self, h: BatchHandle, p) -> int:

@@ -57,6 +57,7 @@ def main():
         torch.manual_seed(1234)
         step = FusedTrainStep(GINet(30, 1, 3).to(dev).train(), max_batch=B)
         step.acc = mode == "acc"
+        step.acc_prefetch = os.environ.get("DR_ACC_PREFETCH") == "1"
         res[mode] = run(step, h, stamps)
     n = len(PHASES)
     print(f"B={B}  median cycles per graph (s_memtime)")
