@@ -395,7 +395,7 @@ def parse_args(argv):
     ap.add_argument("--one-launch", action="store_true", help="GINet, N=1: graph pass + gradient reduce + Adam in one launch (dr_ginet_train_step; opt-in, measured slower at B=64)")
     ap.add_argument("--piped", action="store_true", help="GINet, N=1: pipelined step (dr_ginet_piped_step: each launch runs the previous pass's update on its own workgroups beside this pass, which waits for it only before reading a weight)")
     ap.add_argument("--acc", choices=["auto", "on", "off"], default="auto", help="GINet fp32: accumulating pass (dr_ginet_acc_pass: each workgroup sums every R-th graph's gradients on chip, one partial row per workgroup); auto = batches past the CU count")
-    ap.add_argument("--acc-prefetch", action="store_true", help="with the accumulating pass: the prefetch layout (the next graph's inputs staged by the waves idle in the front half)")
+    ap.add_argument("--no-acc-prefetch", action="store_true", help="accumulating pass without the prefetch layout (A/B: each graph stages its own inputs)")
     ap.add_argument("--ras", action="store_true", help="GINet, N=1: reduce-at-start step (dr_ginet_ras_step: each launch applies the previous update, then runs its pass; opt-in experiment)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stream-copy", action="store_true")
@@ -668,7 +668,7 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
     step.ras = bool(args.ras) and pg is None
     step.piped = bool(args.piped) and pg is None
     step.acc = {"auto": None, "on": True, "off": False}[args.acc]
-    step.acc_prefetch = bool(args.acc_prefetch)
+    step.acc_prefetch = not args.no_acc_prefetch
 
     def run_eager(i):
         return step.step(handles[i % len(handles)], global_batch=B * world)

@@ -1,6 +1,6 @@
 """Workload for rocprofv3 --pmc passes: eager GINet training steps (config 2).
 
-    rocprofv3 --pmc <counters> -f csv -d <dir> -- python3 tools/pmc_run.py [steps] [ginet|vanilla|foutnet|sgat][_atom]
+    rocprofv3 --pmc <counters> -f csv -d <dir> -- python3 tools/pmc_run.py [steps] [ginet|vanilla|foutnet|sgat][_atom|_mixed|_b<B>][_bf16]
 """
 
 from __future__ import annotations
@@ -32,6 +32,9 @@ def main():
     mixed = which.endswith("_mixed")  # B=64 configs[4] 50/30/20 residue/SRV/atom mix (bench.py --graphs mixed)
     which = which.removesuffix("_atom").removesuffix("_mixed")
     B, nb = (32, 4) if atom else (64, 4) if mixed else (64, 16)
+    if "_b" in which:  # e.g. ginet_b4096: B residue graphs per step, two batches (the accumulating pass past the CU count)
+        which, b = which.split("_b")
+        B, nb = int(b), 2
     fam = {"n_lo": 2700, "n_hi": 3300, "mean_degree": 16.7, "k_lo": 8, "k_hi": 32} if atom else {}
     graphs = make_graphs("mixed", B * nb, seed=1000) if mixed else make_dataset(B * nb, seed=1000, **fam)
     packed = pack_graphs(records(graphs, 1 if which == "sgat" else 3), require_clusters=which not in ("ginet_nocluster", "vanilla"))
