@@ -289,8 +289,14 @@ def load():
         msg = f"{LIB_PATH} is missing: build it with `make -C deeprank-gnn-2_amd/csrc` (or __graft_entry__.build()). There is no CPU fallback."
         raise RuntimeError(msg)
     lib = ctypes.CDLL(LIB_PATH)
+    variant = "DR_LIB_NAME" in os.environ  # an A/B build of an older HEAD may lack newer entries
     for name, res, args in SIGNATURES:
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            if variant:
+                continue
+            raise
         fn.restype = res
         fn.argtypes = args
     _LIB = lib

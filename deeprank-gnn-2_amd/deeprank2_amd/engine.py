@@ -148,6 +148,7 @@ class FusedTrainStep:
         self.acc_groups = None  # workgroups (None: the CU count)
         self._acc_slab = None
         self._table_acc = None
+        self._cus = None  # the device's CU count (queried once)
         # models whose graph pass reads its weights from a packed copy
         # (VanillaNetwork: MFMA-fragment order): one copy per step object,
         # rewritten by Adam as it updates the parameters (dr_adam.mirror), so
@@ -363,7 +364,9 @@ class FusedTrainStep:
             return 0
         if h.nonfinite or h.force_large or self.spec.layers is not None and layered.needs_layers(self.spec, h, self.out_dim):
             return 0
-        r = int(self.acc_groups or _device_cus(self.device))
+        if self._cus is None:
+            self._cus = _device_cus(self.device)
+        r = int(self.acc_groups or self._cus)
         if self.acc is None and h.B <= r:
             return 0
         f = self.model.input_shape
