@@ -32,20 +32,20 @@ GRAD_TOL = 1e-5  # x max |grad| of the parameter
 LOSS_TOL = 1e-6  # relative
 
 
-def _records(n, seed, classes=0):
+def _records(n, seed, classes=0, n_feat=30):
     from bench import records
 
-    recs = records(make_dataset(n, seed=seed))
+    recs = records(make_dataset(n, seed=seed, n_feat=n_feat))
     if classes:
         for i, r in enumerate(recs):
             r.y = float(i % classes)
     return recs
 
 
-def _pair(loss="mse", out=1, groups=None):
+def _pair(loss="mse", out=1, groups=None, f=30):
     torch.manual_seed(5)
-    m1 = amd.GINet(30, out, 3).to(DEV).train()
-    m2 = amd.GINet(30, out, 3).to(DEV).train()
+    m1 = amd.GINet(f, out, 3).to(DEV).train()
+    m2 = amd.GINet(f, out, 3).to(DEV).train()
     m2.load_state_dict(m1.state_dict())
     m2._drop_seed = m1._drop_seed = 777  # noqa: SLF001
     acc = FusedTrainStep(m1, loss=loss, max_batch=64)
@@ -65,10 +65,11 @@ def _assert_close_grads(acc, per, what):
         assert err <= GRAD_TOL * scale, f"{what}: {name} max|diff| {err:.3g} vs max|grad| {scale:.3g}"
 
 
-@pytest.mark.parametrize(("n", "groups"), [(300, None), (1000, None), (64, 7), (40, 1)])
-def test_acc_pass_matches_per_graph_partials(n, groups):
-    store = GraphStore(pack_graphs(_records(max(n, 64), 41)), DEV)
-    acc, per = _pair(groups=groups)
+@pytest.mark.parametrize(("n", "groups", "f"), [(300, None, 30), (1000, None, 30), (64, 7, 30), (40, 1, 30), (300, None, 40)])
+def test_acc_pass_matches_per_graph_partials(n, groups, f):
+    """(F = 40: the F > 32 kernel, fc1.weight's sums in LDS instead of registers.)"""
+    store = GraphStore(pack_graphs(_records(max(n, 64), 41, n_feat=f)), DEV)
+    acc, per = _pair(groups=groups, f=f)
     rng = np.random.default_rng(4)
     h = BatchHandle(store, rng.permutation(max(n, 64))[:n].astype(np.int32))
     assert acc._acc_rows(h) > 0 and per._acc_rows(h) == 0  # noqa: SLF001
@@ -80,14 +81,14 @@ def test_acc_pass_matches_per_graph_partials(n, groups):
     _assert_close_grads(acc, per, f"B={n} groups={groups}")
 
 
-@pytest.mark.parametrize("n", [300, 1000])
-def test_acc_prefetch_layout_bit_identical(n):
+@pytest.mark.parametrize(("n", "f"), [(300, 30), (1000, 30)])
+def test_acc_prefetch_layout_bit_identical(n, f):
     """The prefetch layout (weights kept in LDS across a workgroup's graphs,
     graph k+1's inputs DMA'd under graph k's tail) moves data, not
     arithmetic: bit-identical to the accumulating pass without it."""
-    store = GraphStore(pack_graphs(_records(n, 44)), DEV)
-    one, _ = _pair()
-    two, _ = _pair()
+    store = GraphStore(pack_graphs(_records(n, 44, n_feat=f)), DEV)
+    one, _ = _pair(f=f)
+    two, _ = _pair(f=f)
     one.acc_prefetch, two.acc_prefetch = True, False
     h = BatchHandle(store, np.arange(n, dtype=np.int32))
     assert one.acc_lds(h) != two.acc_lds(h), "the prefetch layout must be the one taken"
