@@ -36,34 +36,13 @@ from deeprank2_amd import _lib, layered
 from deeprank2_amd.fused import BatchHandle, launch, launch_step, param_table, slab_rows_for, step_fits
 
 
-def acc_plan(h: BatchHandle, r: int) -> torch.Tensor:
-    """The accumulating pass's work plan for ``r`` workgroups (cached on the
-    handle): graphs by descending cost N + E/4 dealt to the workgroups in
-    snake order (0..r-1, r-1..0, ...), so every workgroup gets B/r graphs
-    of about the same total size; [r + 1 starts | positions].  Depends only on
-    the batch, so the sums' order — and the result — is deterministic."""
-    import numpy as np  # noqa: PLC0415
-
-    key = ("acc_plan", r)
-    plan = h._lds.get(key)  # noqa: SLF001
-    if plan is not None:
-        return plan
-    idx = h.gids_host.astype(np.int64)
-    n, e = (h.store._sizes[0][idx].astype(np.int64), h.store._sizes[1][idx].astype(np.int64))  # noqa: SLF001
-    order = np.argsort(-(4 * n + e), kind="stable")
-    i = np.arange(h.B)
-    rnd, j = i // r, i % r
-    wg = np.where(rnd % 2 == 0, j, r - 1 - j)
-    by_wg = np.argsort(wg, kind="stable")
-    starts = np.zeros(r + 1, dtype=np.int32)
-    starts[1:] = np.cumsum(np.bincount(wg, minlength=r))
-    host = np.concatenate([starts, order[by_wg].astype(np.int32)])
-    plan = torch.from_numpy(host).to(h.store.device)
-    h._lds[key] = plan  # noqa: SLF001
-    return plan
-
-
 class FusedTrainStep:
+    # the accumulating pass's defaults for new step objects (instance
+    # attributes acc / acc_groups override them; tests set these to drive the
+    # Trainer's own steps)
+    acc_default = None
+    acc_groups_default = None
+
     def __init__(self, model, lr=1e-3, weight_decay=1e-5, betas=(0.9, 0.999), eps=1e-8, loss="mse", class_weights=None, process_group=None, max_batch=64, compute_dtype="f32"):
         self.model = model
         if compute_dtype not in ("f32", "bf16"):
@@ -144,8 +123,8 @@ class FusedTrainStep:
         # None = auto (B > the device's CU count), False = off, True = on
         # wherever the batch allows it.  Another fp32 association than the
         # per-graph partials (deterministic).
-        self.acc = None
-        self.acc_groups = None  # workgroups (None: the CU count)
+        self.acc = self.acc_default
+        self.acc_groups = self.acc_groups_default  # workgroups (None: the CU count)
         self._acc_slab = None
         self._table_acc = None
         self._cus = None  # the device's CU count (queried once)
@@ -434,9 +413,8 @@ class FusedTrainStep:
             launch(self.spec, h, self._w, p, wpack=self._packed())
             return 0
         p.slab = self._acc_slab.data_ptr()
-        plan = acc_plan(h, r)
-        try:
-            rc = _lib.load().dr_ginet_acc_pass(h.store.cstruct(), h.descs.data_ptr(), h.B, self._w, p, lds_for(self.spec, h, self.out_dim), r, plan.data_ptr(), self._acc_max_sizes(h), _lib.stream_ptr(self.device))
+        try:  # (no plan: workgroup w runs positions w, w + r, ... — the same order eager and captured)
+            rc = _lib.load().dr_ginet_acc_pass(h.store.cstruct(), h.descs.data_ptr(), h.B, self._w, p, lds_for(self.spec, h, self.out_dim), r, None, self._acc_max_sizes(h), _lib.stream_ptr(self.device))
         finally:
             p.slab = self.slab.data_ptr()
         _lib.check(rc, "dr_ginet_acc_pass")

@@ -169,13 +169,15 @@ def test_ginet_classification_class_weights_checkpoint_and_test(files, tmp_path)
     np.testing.assert_allclose(np.array(mem2.records[0]["output"]), np.array(mem.records[0]["output"]), rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("model_cls", [GINet, FoutNet, SGAT, GINetNoCluster])
-def test_captured_epochs_bit_identical_to_per_batch_steps(files, model_cls):
+@pytest.mark.parametrize(("model_cls", "acc"), [(GINet, False), (FoutNet, False), (SGAT, False), (GINetNoCluster, False), (GINet, True)])
+def test_captured_epochs_bit_identical_to_per_batch_steps(files, model_cls, acc):
     """Trainer epochs replayed from one captured HIP graph (epoch.py) against
     the per-batch loop: the same epoch losses, exported outputs and final
     parameters, bit for bit (shuffled batches, a last partial batch, GINet's
-    in-kernel dropout)."""
+    in-kernel dropout).  acc: every step on the accumulating pass over 2
+    workgroups (what batches past the CU count take), prefetch layout on."""
     from deeprank2_amd import trainer as trainer_mod
+    from deeprank2_amd.engine import FusedTrainStep
 
     res = []
     for captured in (True, False):
@@ -184,13 +186,17 @@ def test_captured_epochs_bit_identical_to_per_batch_steps(files, model_cls):
         mem = MemoryOutputExporter()
         torch.manual_seed(21)
         trainer_mod.Trainer.capture_epochs = captured
+        if acc:
+            FusedTrainStep.acc_default, FusedTrainStep.acc_groups_default = True, 2
         try:
             t = Trainer(model_cls, tr, va, cuda=True, output_exporters=[mem], precluster=False)
             t.train(nepoch=3, batch_size=5, shuffle=True, validate=True, best_model=False, filename=None)
         finally:
             trainer_mod.Trainer.capture_epochs = True
+            FusedTrainStep.acc_default = FusedTrainStep.acc_groups_default = None
         assert t._fused  # noqa: SLF001
         assert bool(t._runners) == captured  # noqa: SLF001  (the captured path ran)
+        assert (t._fused._acc_slab is not None) == acc  # noqa: SLF001  (the accumulating pass ran)
         res.append((mem.records, {k: v.detach().cpu() for k, v in t.model.state_dict().items()}))
     (ra, pa), (rb, pb) = res
     assert [r["loss"] for r in ra] == [r["loss"] for r in rb]
