@@ -227,6 +227,22 @@ __device__ __forceinline__ void dma_x4(void* lds_dst, const void* gsrc, int n4, 
     if (base + lane < n4) __builtin_amdgcn_global_load_lds(AS1(src + base + lane), AS3(dst + base), 16, 0, 0);
 }
 
+// One LDS-DMA instruction from inline asm (M0 = the wave's LDS destination,
+// saved and restored around it: M0 is a reserved register the compiler may be
+// using)
+__device__ __forceinline__ void lds_dma_dword(uint32_t m0, const void* src) {
+  uint32_t saved;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %2, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(saved)
+               : "s"(m0), "v"(src));
+}
+__device__ __forceinline__ void lds_dma_x4(uint32_t m0, const void* src) {
+  uint32_t saved;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(saved)
+               : "s"(m0), "v"(src));
+}
+
 // The same copies issued from inline asm: the compiler does not know they
 // write LDS, so it inserts no wait for them before later LDS reads (with the
 // builtin it waits for the DMA before the next LDS access), and (no memory
@@ -240,9 +256,7 @@ __device__ __forceinline__ void dma_words_async(void* lds_dst, const void* gsrc,
   const uint32_t dst = (uint32_t)(size_t)AS3(lds_dst);
   for (int base = wave * 64; base < n; base += NT)
     if (base + lane < n)
-      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" ::"s"(__builtin_amdgcn_readfirstlane(dst + 4 * base)),
-                   "v"(src + base + lane)
-                   : "m0");
+      lds_dma_dword(__builtin_amdgcn_readfirstlane(dst + 4 * base), src + base + lane);
 }
 
 // the same over waves [wf, wf + nw) only (the others skip)
@@ -253,9 +267,7 @@ __device__ __forceinline__ void dma_words_async_sub(void* lds_dst, const void* g
   if (rw < 0) return;
   for (int base = rw * 64; base < n; base += nw * 64)
     if (base + lane < n)
-      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" ::"s"(__builtin_amdgcn_readfirstlane(dst + 4 * base)),
-                   "v"(src + base + lane)
-                   : "m0");
+      lds_dma_dword(__builtin_amdgcn_readfirstlane(dst + 4 * base), src + base + lane);
 }
 __device__ __forceinline__ void dma_x4_async_sub(void* lds_dst, const void* gsrc, int n4, int tid, int wf, int nw) {
   const int lane = tid & 63, rw = __builtin_amdgcn_readfirstlane((tid >> 6) - wf);
@@ -264,9 +276,7 @@ __device__ __forceinline__ void dma_x4_async_sub(void* lds_dst, const void* gsrc
   if (rw < 0) return;
   for (int base = rw * 64; base < n4; base += nw * 64)
     if (base + lane < n4)
-      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(__builtin_amdgcn_readfirstlane(dst + 16 * base)),
-                   "v"(src + base + lane)
-                   : "m0");
+      lds_dma_x4(__builtin_amdgcn_readfirstlane(dst + 16 * base), src + base + lane);
 }
 
 __device__ __forceinline__ void dma_x4_async(void* lds_dst, const void* gsrc, int n4, int tid, int w0 = 0) {
@@ -275,9 +285,7 @@ __device__ __forceinline__ void dma_x4_async(void* lds_dst, const void* gsrc, in
   const uint32_t dst = (uint32_t)(size_t)AS3(lds_dst);
   for (int base = wave * 64; base < n4; base += NT)
     if (base + lane < n4)
-      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(__builtin_amdgcn_readfirstlane(dst + 16 * base)),
-                   "v"(src + base + lane)
-                   : "m0");
+      lds_dma_x4(__builtin_amdgcn_readfirstlane(dst + 16 * base), src + base + lane);
 }
 
 __device__ __forceinline__ float4 f4add(float4 a, float4 v) {
@@ -816,6 +824,7 @@ struct AccCtx {
   AccLayout lay;
   int par = 0, next = -1;
   bool first = true;
+  int64_t step = 0;  // dr_pass.step_counter[0] (constant for the launch)
   // PF: LDS word set to 1 by the graph whose idle waves staged the next
   // graph's inputs (read by that next graph before its staging)
   uint32_t* staged = nullptr;
@@ -898,7 +907,11 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
 #pragma unroll
     for (int j = 0; j < 8; ++j) fc1_col[j] = ldw(a.w.fc1w + (rcc * 8 + j) * 64 + o);
   };
-  const float y_g = s.y[g];
+  // (ACC: scalar loads through the constant address space — read-only for the
+  // launch; hipcc cannot prove that in the accumulating loop and would use a
+  // vector load, waited for by the staging's vmcnt(0))
+  typedef const __attribute__((address_space(4))) float* CF32;
+  const float y_g = ACC ? *(CF32)(s.y + g) : s.y[g];
   uint64_t drop_offset = a.p.drop_offset;
   // the graph's inputs (PF: graph k+1's are DMA'd during graph k's tail)
   // (asm-issued: waited for by the s_waitcnt vmcnt(0) before the staging barrier)
@@ -947,7 +960,8 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
     for (int p = tid; p < K0 * 32; p += NT) skey[p] = 0ull;
     if (PIPED && tid < 2) reinterpret_cast<uint32_t*>(lds + c.dgp)[tid] = 0u;  // pipe_wait's flag and claim
   }
-  if (a.p.step_counter) drop_offset = (uint64_t)a.p.step_counter[0];  // loaded late: no early wait
+  // loaded late: no early wait (ACC: read once per launch by the kernel)
+  if (a.p.step_counter) drop_offset = ACC ? (uint64_t)ac.step : (uint64_t)a.p.step_counter[0];
   if (RAS) {
     // the previous step's reduce + Adam, then the grid hand-off (scratch: the
     // tail's dgp region, 1024 words, unused before the tail)
@@ -1249,6 +1263,8 @@ __global__ void __launch_bounds__(NT) ginet_acc_kernel(GinetArgs a, const int32_
   ac.acc_words = acc_words(F, OUT, !REG) + 4;  // + the staged flag (16 bytes)
   ac.staged = reinterpret_cast<uint32_t*>(lds_raw + ac.acc_words - 4);
   ac.lay = lay;
+  typedef const __attribute__((address_space(4))) int64_t* CI64K;
+  ac.step = a.p.step_counter ? *(CI64K)a.p.step_counter : 0;
   float accf[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   ac.accf = REG ? accf : nullptr;
   for (int p = tid; p < ac.acc_words; p += NT) lds_raw[p] = 0.f;
