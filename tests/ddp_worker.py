@@ -13,7 +13,7 @@ bits as two ranks, since a two-operand sum does not depend on the order.
 DR_DDP_GRAPHS=mixed: global batches of residue, SRV and atom-level graphs
 (config 5), sharded by ``plan_shards`` (edge-balanced); rank 0 also writes the
 last step's predictions gathered back into global-batch order (the Trainer's
-``_gather_rows``)."""
+``_gather_rows``).  DR_DDP_ACC=1: GINet's accumulating pass (3 workgroups)."""
 
 from __future__ import annotations
 
@@ -65,6 +65,8 @@ def run(model_name, world, rank, out_path):
     edges = np.array([d.edge_index.shape[1] for d in datas])
     torch.manual_seed(42)
     model = {"ginet": lambda: GINet(30, 1, 3), "foutnet": lambda: FoutNet(30, 1), "vanilla": lambda: VanillaNetwork(30, 1, 3)}[model_name]().to(dev).train()
+    if os.environ.get("DR_DDP_ACC") == "1":  # the accumulating pass on 3 workgroups per shard
+        FusedTrainStep.acc_default, FusedTrainStep.acc_groups_default = True, 3
     step = FusedTrainStep(model, process_group=pg)
     emulate = int(os.environ.get("DR_DDP_EMULATE", "0"))
     if emulate:

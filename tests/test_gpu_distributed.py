@@ -55,16 +55,18 @@ def test_two_ranks_match_single_process(tmp_path, model_name):
             assert np.mean(np.abs(b[k] - a[k]) < 1e-6) > 0.95, k
 
 
-@pytest.mark.parametrize("model_name", ["ginet", "vanilla"])
-def test_two_ranks_bit_identical_to_summed_shards(tmp_path, model_name):
+@pytest.mark.parametrize(("model_name", "acc"), [("ginet", "0"), ("vanilla", "0"), ("ginet", "1")])
+def test_two_ranks_bit_identical_to_summed_shards(tmp_path, model_name, acc):
     """Two gloo ranks against one process that runs the same two shards one
     after another and sums their gradient buffers (the all-reduce's sum of two
     operands, order-free) before one Adam update: losses, all-reduced gradients
     and parameters after 3 steps agree bit for bit.  VanillaNetwork runs its
-    shards of 12 graphs on 4 workgroups per graph (split partial rows)."""
+    shards of 12 graphs on 4 workgroups per graph (split partial rows).
+    acc: GINet's accumulating pass (3 workgroups per shard, one row each)
+    under the same all-reduce."""
     emu, two = str(tmp_path / "emu.npz"), str(tmp_path / "w2.npz")
-    _launch(model_name, 1, emu, DR_DDP_EMULATE="2")
-    _launch(model_name, 2, two)
+    _launch(model_name, 1, emu, DR_DDP_EMULATE="2", DR_DDP_ACC=acc)
+    _launch(model_name, 2, two, DR_DDP_ACC=acc)
     a, b = np.load(emu), np.load(two)
     for k in a.files:
         np.testing.assert_array_equal(b[k], a[k], err_msg=k)
