@@ -18,10 +18,6 @@ __device__ __forceinline__ float dr_wave_sum(float v) {
   return v;
 }
 
-// Lane permutations on the DPP path (a VALU operand modifier, no LDS round
-// trip as ds_bpermute has): CTRL is the gfx9 dpp_ctrl (0xB1 quad_perm
-// [1,0,3,2] = lane^1, 0x4E quad_perm [2,3,0,1] = lane^2, 0x141
-// row_half_mirror = 7-i within 8 lanes, 0x140 row_mirror = 15-i within 16).
 // threadIdx.x, opaque to the optimiser when OPAQUE: a kernel that loops a
 // body over several work items (ginet_acc_kernel) would otherwise get the
 // body's thread-index arithmetic hoisted out of the loop and kept live across
@@ -43,6 +39,10 @@ __device__ __forceinline__ int dr_wave(int tid) {
   return OPAQUE ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
 }
 
+// Lane permutations on the DPP path (a VALU operand modifier, no LDS round
+// trip as ds_bpermute has): CTRL is the gfx9 dpp_ctrl (0xB1 quad_perm
+// [1,0,3,2] = lane^1, 0x4E quad_perm [2,3,0,1] = lane^2, 0x141
+// row_half_mirror = 7-i within 8 lanes, 0x140 row_mirror = 15-i within 16).
 template <int CTRL>
 __device__ __forceinline__ float dr_dpp(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));

@@ -503,6 +503,7 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
         if (mb + u < me) ties += (v[u] == mx) ? 1.f : 0.f;
       t.p2[p] = mx;
       t.nt[p] = ties;
+      if (K1 == 1) t.g[o] = (0.f + mx) / (float)K1;  // the mean below, for one cluster (same ops)
     }
   } else {
     const int pairs = K1 * 64;
@@ -546,12 +547,15 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
 
   STAMP(6);
   // ---------------- per-graph mean (scatter_mean, ginet.py:117-118) ----------
-  if (tid < 64) {
-    float acc = 0.f;
-    for (int m = 0; m < K1; ++m) acc += t.p2[m * 64 + tid];
-    t.g[tid] = acc / (float)K1;
+  // (K1 = 1 with K0 < 16: written by the pooling above)
+  if (!(K1 == 1 && K0 < 16)) {
+    if (tid < 64) {
+      float acc = 0.f;
+      for (int m = 0; m < K1; ++m) acc += t.p2[m * 64 + tid];
+      t.g[tid] = acc / (float)K1;
+    }
+    __syncthreads();
   }
-  __syncthreads();
 
   STAMP(7);
   {
