@@ -95,57 +95,85 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
     }
   }
   __syncthreads();
-  for (int q = wave; q < OUT; q += NW) {
-    const float* wr = t.fc2 + q * 128;
-    float v = fmaf(t.hd[lane], wr[lane], t.hd[lane + 64] * wr[lane + 64]);
+  if (OUT == 1 && p.loss_kind == DR_LOSS_MSE && (p.flags & DR_PASS_BACKWARD)) {
+    // one MSE logit (the headline): waves 0 and 1 each form the logit (the
+    // same sums), the loss gradient and their 64 rows of dh, so the logit,
+    // loss and dh steps need no workgroup barrier between them
+    if (tid < 128) {
+      float v = fmaf(t.hd[lane], t.fc2[lane], t.hd[lane + 64] * t.fc2[lane + 64]);
 #ifdef DR_HEAD_SHFL
-    v = dr_wave_sum(v);
+      v = dr_wave_sum(v);
 #else
-    v = dr_wave_sum_dpp(v);
+      v = dr_wave_sum_dpp(v);
 #endif
-    if (lane == 0) t.dout[q] = v + t.fc2[OUT * 128 + q];  // logits parked in t.dout
-  }
-  __syncthreads();
-  if ((p.flags & DR_PASS_FORWARD) && tid < OUT) p.out[(int64_t)b * OUT + tid] = t.dout[tid];
-  if (!(p.flags & DR_PASS_BACKWARD)) return false;
-  // (the loss below is taken by thread 0, which read its logits above in
-  // program order; the other logits' readers are lanes of the same wave 0
-  // while OUT <= 64: no barrier needed between the output stores and the loss)
-  if (OUT > 64) __syncthreads();
-  head_stamp(srow, stamp0);
-
-  // ---------------- loss gradient (trainer.py:688-689) ----------------------
-  if (tid == 0) {
-    if (p.loss_kind == DR_LOSS_MSE) {
-      const float d = t.dout[0] - y_g;
-      if (ACC) t.acc[128 + 128 * OUT + OUT] += d * d;
-      else if (p.loss_per_graph) st_part<WT>(p.loss_per_graph + pb, d * d);
-      t.dout[0] = 2.f * d * p.loss_scale;
-      for (int q = 1; q < OUT; ++q) t.dout[q] = 0.f;  // the loss reads column 0 only (engine's layer path alike)
-    } else if (p.loss_kind == DR_LOSS_CE) {
-      const int yi = (int)y_g;
-      float mx = t.dout[0];
-      for (int q = 1; q < OUT; ++q) mx = fmaxf(mx, t.dout[q]);
-      float se = 0.f;
-      for (int q = 0; q < OUT; ++q) se += expf(t.dout[q] - mx);
-      const float lse = mx + logf(se);
-      const float wy = p.class_w ? p.class_w[yi] : 1.f;
-      if (ACC) t.acc[128 + 128 * OUT + OUT] += wy * (lse - t.dout[yi]);
-      else if (p.loss_per_graph) st_part<WT>(p.loss_per_graph + pb, wy * (lse - t.dout[yi]));
-      for (int q = 0; q < OUT; ++q) t.dout[q] = wy * (expf(t.dout[q] - lse) - (q == yi ? 1.f : 0.f)) * p.loss_scale;
-    } else {
-      for (int q = 0; q < OUT; ++q) t.dout[q] = p.dout[(int64_t)b * OUT + q];
+      const float logit = v + t.fc2[128];
+      const float d = logit - y_g;
+      const float dout0 = 2.f * d * p.loss_scale;
+      if (tid == 0) {
+        if (p.flags & DR_PASS_FORWARD) p.out[b] = logit;
+        if (ACC) t.acc[128 + 128 + 1] += d * d;
+        else if (p.loss_per_graph) st_part<WT>(p.loss_per_graph + pb, d * d);
+        t.dout[0] = dout0;
+      }
+      head_stamp(srow, stamp0);
+      head_stamp(srow, stamp0 + 1);
+      float acc = fmaf(t.fc2[tid], dout0, 0.f);
+      if (p.use_dropout) acc = ((t.keep ? t.keep[tid] != 0 : keep_unit(p, drop_offset, b, tid)) ? acc : 0.f) * p.drop_scale;
+      t.dh[tid] = relu_bwd(t.hh[tid], acc);
     }
-  }
-  __syncthreads();
+  } else {
+    for (int q = wave; q < OUT; q += NW) {
+      const float* wr = t.fc2 + q * 128;
+      float v = fmaf(t.hd[lane], wr[lane], t.hd[lane + 64] * wr[lane + 64]);
+#ifdef DR_HEAD_SHFL
+      v = dr_wave_sum(v);
+#else
+      v = dr_wave_sum_dpp(v);
+#endif
+      if (lane == 0) t.dout[q] = v + t.fc2[OUT * 128 + q];  // logits parked in t.dout
+    }
+    __syncthreads();
+    if ((p.flags & DR_PASS_FORWARD) && tid < OUT) p.out[(int64_t)b * OUT + tid] = t.dout[tid];
+    if (!(p.flags & DR_PASS_BACKWARD)) return false;
+    // (the loss below is taken by thread 0, which read its logits above in
+    // program order; the other logits' readers are lanes of the same wave 0
+    // while OUT <= 64: no barrier needed between the output stores and the loss)
+    if (OUT > 64) __syncthreads();
+    head_stamp(srow, stamp0);
 
-  head_stamp(srow, stamp0 + 1);
-  // ---------------- head backward -------------------------------------------
-  if (tid < 128) {
-    float acc = 0.f;
-    for (int q = 0; q < OUT; ++q) acc = fmaf(t.fc2[q * 128 + tid], t.dout[q], acc);
-    if (p.use_dropout) acc = ((t.keep ? t.keep[tid] != 0 : keep_unit(p, drop_offset, b, tid)) ? acc : 0.f) * p.drop_scale;
-    t.dh[tid] = relu_bwd(t.hh[tid], acc);
+    // ---------------- loss gradient (trainer.py:688-689) ----------------------
+    if (tid == 0) {
+      if (p.loss_kind == DR_LOSS_MSE) {
+        const float d = t.dout[0] - y_g;
+        if (ACC) t.acc[128 + 128 * OUT + OUT] += d * d;
+        else if (p.loss_per_graph) st_part<WT>(p.loss_per_graph + pb, d * d);
+        t.dout[0] = 2.f * d * p.loss_scale;
+        for (int q = 1; q < OUT; ++q) t.dout[q] = 0.f;  // the loss reads column 0 only (engine's layer path alike)
+      } else if (p.loss_kind == DR_LOSS_CE) {
+        const int yi = (int)y_g;
+        float mx = t.dout[0];
+        for (int q = 1; q < OUT; ++q) mx = fmaxf(mx, t.dout[q]);
+        float se = 0.f;
+        for (int q = 0; q < OUT; ++q) se += expf(t.dout[q] - mx);
+        const float lse = mx + logf(se);
+        const float wy = p.class_w ? p.class_w[yi] : 1.f;
+        if (ACC) t.acc[128 + 128 * OUT + OUT] += wy * (lse - t.dout[yi]);
+        else if (p.loss_per_graph) st_part<WT>(p.loss_per_graph + pb, wy * (lse - t.dout[yi]));
+        for (int q = 0; q < OUT; ++q) t.dout[q] = wy * (expf(t.dout[q] - lse) - (q == yi ? 1.f : 0.f)) * p.loss_scale;
+      } else {
+        for (int q = 0; q < OUT; ++q) t.dout[q] = p.dout[(int64_t)b * OUT + q];
+      }
+    }
+    __syncthreads();
+
+    head_stamp(srow, stamp0 + 1);
+    // ---------------- head backward -------------------------------------------
+    if (tid < 128) {
+      float acc = 0.f;
+      for (int q = 0; q < OUT; ++q) acc = fmaf(t.fc2[q * 128 + tid], t.dout[q], acc);
+      if (p.use_dropout) acc = ((t.keep ? t.keep[tid] != 0 : keep_unit(p, drop_offset, b, tid)) ? acc : 0.f) * p.drop_scale;
+      t.dh[tid] = relu_bwd(t.hh[tid], acc);
+    }
   }
   __syncthreads();
   {
