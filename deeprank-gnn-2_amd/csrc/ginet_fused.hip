@@ -572,6 +572,7 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
     hl.keep = t.keep;
     hl.acc = ACC ? t.acc + 32 * F + 1024 : nullptr;
     hl.accf = ACC ? t.accf : nullptr;
+    hl.dg_deferred = true;  // summed from dgp by the pooling backward below
     if (!drk::ginet_head<NT, WT, ACC>(a.p, hl, fc1_row, fc1_col, fc1_bias, b, OUT, y_g, drop_offset, 8, pb)) return;
   }  // stamps 8 (forward head done) and 9 (loss gradient done) are taken inside
 
@@ -584,7 +585,10 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
   // array and no barrier between the two
   for (int p = tid; p < K0 * 64; p += NT) {
     const int j = p >> 6, o = p & 63;
-    const float dgo = t.dg[o] / (float)K1;
+    float dgs = 0.f;  // dG[o]: the head's 16 per-wave partials in order (ginet_head, dg_deferred)
+#pragma unroll
+    for (int rc = 0; rc < NW; ++rc) dgs += t.dgp[rc * 64 + o];
+    const float dgo = dgs / (float)K1;
     float acc = 0.f;
     for (int e = t.p1trp[j]; e < t.p1trp[j + 1]; ++e) {
       const int k = t.p1tc[e], mo = t.cl1[k] * 64 + o;

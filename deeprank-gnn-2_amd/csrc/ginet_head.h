@@ -24,6 +24,9 @@ struct GinetHeadLds {
   // instead of per-graph head vectors (16-byte aligned)
   float* acc = nullptr;
   float* accf = nullptr;  // or: fc1.weight's sums of this thread (row tid/8, columns 8 (tid%8) ..) in registers
+  // the caller sums dG from the 16 per-wave partials (dgp) itself, in the
+  // same order, where it first needs it: no dG step and no closing barrier
+  bool dg_deferred = false;
 };
 
 // The fc1-output dropout keep flags of graph b, written to LDS by the first
@@ -184,7 +187,7 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
     t.dgp[rc * 64 + o] = acc;
   }
   __syncthreads();
-  if (tid < 64) {
+  if (!t.dg_deferred && tid < 64) {
     float acc = 0.f;
     for (int rc = 0; rc < NW; ++rc) acc += t.dgp[rc * 64 + tid];
     t.dg[tid] = acc;
@@ -225,7 +228,7 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
     }
     if (tid < OUT) st_part<WT>(hg + 320 + tid, t.dout[tid]);
   }
-  __syncthreads();
+  if (!t.dg_deferred) __syncthreads();
 
   return true;
 }
