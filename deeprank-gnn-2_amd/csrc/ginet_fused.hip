@@ -42,6 +42,9 @@
 
 namespace {
 
+#ifndef DR_CONV2_KEYS
+#define DR_CONV2_KEYS 1  // conv2 reads the pooled rows from the depth-0 keys (no barrier after their decode)
+#endif
 #ifndef DR_DMA_ROT
 #define DR_DMA_ROT 0  // 1: spread starting waves (measured 0.1 us slower per pass, r05)
 #endif
@@ -390,6 +393,9 @@ struct TailLds {
   // [dW1cat 32F | dW2cat 1024 | the head's, GinetHeadLds::acc], or null
   float* acc = nullptr;
   float* accf = nullptr;  // GinetHeadLds::accf
+  // or null: the depth-0 pooling keys, P1 not yet decoded (conv2 decodes the
+  // rows it reads; the decode runs beside it in the same step)
+  const unsigned long long* key = nullptr;
 };
 
 template <class C>
@@ -446,15 +452,27 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
     }
     float acc = 0.f;
     for (int e = t.p1rp[k]; e < t.p1rp[k + 1]; ++e) {
-      const float* pr = t.p1 + t.p1c[e] * 32 + br * 16;
       float y = 0.f;
+      if (t.key) {  // P1 = the key's value half, 0 for an empty (cluster, channel)
+        const unsigned long long* kr = t.key + t.p1c[e] * 32 + br * 16;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 v = *reinterpret_cast<const float4*>(pr + 4 * q);
-        y = fmaf(v.x, wr[4 * q], y);
-        y = fmaf(v.y, wr[4 * q + 1], y);
-        y = fmaf(v.z, wr[4 * q + 2], y);
-        y = fmaf(v.w, wr[4 * q + 3], y);
+        for (int q = 0; q < 8; ++q) {
+          const ulonglong2 kv = *reinterpret_cast<const ulonglong2*>(kr + 2 * q);
+          const float v0 = kv.x ? __uint_as_float((uint32_t)(kv.x >> 32)) : 0.f;
+          const float v1 = kv.y ? __uint_as_float((uint32_t)(kv.y >> 32)) : 0.f;
+          y = fmaf(v0, wr[2 * q], y);
+          y = fmaf(v1, wr[2 * q + 1], y);
+        }
+      } else {
+        const float* pr = t.p1 + t.p1c[e] * 32 + br * 16;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 v = *reinterpret_cast<const float4*>(pr + 4 * q);
+          y = fmaf(v.x, wr[4 * q], y);
+          y = fmaf(v.y, wr[4 * q + 1], y);
+          y = fmaf(v.z, wr[4 * q + 2], y);
+          y = fmaf(v.w, wr[4 * q + 3], y);
+        }
       }
       acc += y;
     }
@@ -960,7 +978,10 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
     dma_words(sW1 + 16 * F, a.w.w1e, 16 * F, tid, DR_DMA_ROT * 14);
   }
   {  // zero Z's K padding (cols XS..KPT; X's own pad is zero) and the pooling keys
-    const int padz = KPT - XS;
+    // (to the row's own padded width KP = r16(F): with KPT = 64 and F <= 48
+    // the row stride LDW = KP + 2 is shorter than KPT, and zeroing to KPT ran
+    // 14 words past Z into the row pointers being DMA'd beside it)
+    const int padz = c.KP - XS;
     for (int p = tid; p < N * padz; p += NT) {
       const int i = p / padz;
       sZ[i * LDW + XS + (p - i * padz)] = 0.f;
@@ -1110,6 +1131,8 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
       const int ar = min(r0 + li, N - 1);  // rows past N compute garbage that is never pooled
       floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
+      // (k steps past the row's KP read the next row's finite values against
+      // W's zero padding: no contribution)
       for (int ks = 0; ks < KPT / 16; ++ks) {
         float av[4];
 #pragma unroll
@@ -1213,15 +1236,18 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
       }
     }
   } else {
+    // (no barrier after the decode: conv2, the tail's first step, reads the
+    // pooled rows from the keys themselves — TailLds::key)
     for (int p = tid; p < K0 * 32; p += NT) {
       const unsigned long long key = skey[p];
       sP1[p] = key ? __uint_as_float((uint32_t)(key >> 32)) : 0.f;
       sA1[p] = key ? (int)(0xffffffffu - (uint32_t)key) : N;
     }
   }
-  __syncthreads();
+  if (SIB || !DR_CONV2_KEYS) __syncthreads();
 
   TailLds t = tail_lds(c, lds);
+  t.key = (SIB || !DR_CONV2_KEYS) ? nullptr : skey;
   t.keep = skeep;
   t.acc = ACC ? ac.acc : nullptr;
   t.accf = ACC ? ac.accf : nullptr;

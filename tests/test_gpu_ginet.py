@@ -136,6 +136,30 @@ def test_fused_train_step_vs_oracle_config2_batch64():
         np.testing.assert_allclose(p.detach().cpu().numpy(), r.detach().cpu().numpy(), rtol=1e-5, atol=1e-7, err_msg=n)
 
 
+@pytest.mark.parametrize("f", [12, 40])
+def test_fused_train_step_vs_oracle_other_feature_counts(f):
+    """F = 12 (K padded to 16 under the 32-wide kernel) and F = 40 (48 under
+    the 64-wide kernel): the per-graph kernel's Z rows are shorter than the
+    kernel's K there.  (Before r05 the Z padding was zeroed to the kernel's
+    K, 14 words past Z into the row pointers DMA'd beside it: wrong outputs
+    whenever the zeroing landed after the DMA.)  Five launches, each against
+    the oracle."""
+    torch.manual_seed(1234)
+    datas = _synthetic(16, seed=5, n_feat=f)
+    model_o = gnn_ref.GINet(f, 1, 3)
+    mask = (torch.rand(16, 128, generator=torch.Generator().manual_seed(3)) >= 0.4).float()
+    out_o, loss_o = _oracle_step(model_o, [d.clone() for d in datas], mask)
+    store = GraphStore(pack_graphs(records_from_batch(P.Batch.from_data_list(datas))), DEV)
+    h = amd.BatchHandle(store, np.arange(16))
+    for _ in range(5):
+        model = amd.GINet(f, 1, 3)
+        model.load_state_dict(model_o.state_dict())
+        step = GINetTrainStep(model.to(DEV).train())
+        loss, out = step.step(h, mask=mask.to(torch.uint8).to(DEV))
+        np.testing.assert_allclose(out.cpu().numpy(), out_o, **TOL)
+        assert float(loss) == pytest.approx(loss_o, rel=1e-4)
+
+
 def test_module_autograd_vs_oracle_single_cluster_graphs():
     """test.hdf5-like batches: one depth-0 cluster per graph -> conv2 sees no
     edges; also a graph with several depth-1 clusters."""
