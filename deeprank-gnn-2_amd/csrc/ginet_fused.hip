@@ -43,7 +43,7 @@
 namespace {
 
 #ifndef DR_CONV2_KEYS
-#define DR_CONV2_KEYS 1  // conv2 reads the pooled rows from the depth-0 keys (no barrier after their decode)
+#define DR_CONV2_KEYS 0  // 1: conv2 reads the pooled rows from the depth-0 keys, no barrier after their decode (measured 0.1 us slower, r05)
 #endif
 #ifndef DR_DMA_ROT
 #define DR_DMA_ROT 0  // 1: spread starting waves (measured 0.1 us slower per pass, r05)
@@ -72,7 +72,12 @@ struct Carve {
 // free.
 __host__ __device__ inline Carve carve(int N, int E, int F, int K0, int P1, int K1, int alias, int OUT) {
   Carve c;
-  c.KP = r16(F);      // K padded for the 16x16x4 MFMA steps (zeros)
+  // K padded to the kernel's KPT (32 for F <= 32, else 64: the MFMA steps it
+  // runs; zeros past F).  (Until r05 KP was r16(F), shorter than KPT for F <= 16
+  // and 33..48: the padding zeroed to KPT then ran 14 words past Z into the
+  // row pointers being DMA'd beside it, and the last k steps read other
+  // waves' rows.)
+  c.KP = F <= 32 ? 32 : 64;
   c.LDW = c.KP + 2;   // rows 2 words apart: lanes (row li, k+kq) hit 32 distinct banks
   c.XS = r4(F);
   int o = 0;
@@ -130,7 +135,7 @@ struct AccLayout {
 __host__ __device__ inline Carve carve_acc(int N, int E, int F, int K0, int P1, int K1, int alias, int OUT,
                                            const AccLayout& L, int par) {
   Carve c;
-  c.KP = r16(F);
+  c.KP = F <= 32 ? 32 : 64;  // as carve()
   c.LDW = c.KP + 2;
   c.XS = r4(F);
   int o = 0;
@@ -179,7 +184,7 @@ __host__ __device__ inline Carve carve_acc(int N, int E, int F, int K0, int P1, 
 __host__ __device__ inline AccLayout acc_layout(int Nm, int Em, int F, int K0m, int P1m, int K1m, int alias, int OUT) {
   AccLayout L;
   L.in0 = r4(32 * F) + 1024 + r4(OUT * 128 + OUT);
-  const int XS = r4(F), LDW = r16(F) + 2;
+  const int XS = r4(F), LDW = (F <= 32 ? 32 : 64) + 2;
   const int in = r4(Nm * XS) + r4(Nm + 1) + r4((Em + 1) / 2) + r4(Nm) + r4(K0m + 1) + r4(P1m) +
                  (alias ? 0 : r4(K0m + 1) + r4(P1m)) + r4(K1m + 1) + r4(K0m);
   L.in1 = L.in0 + in;
@@ -978,10 +983,7 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
     dma_words(sW1 + 16 * F, a.w.w1e, 16 * F, tid, DR_DMA_ROT * 14);
   }
   {  // zero Z's K padding (cols XS..KPT; X's own pad is zero) and the pooling keys
-    // (to the row's own padded width KP = r16(F): with KPT = 64 and F <= 48
-    // the row stride LDW = KP + 2 is shorter than KPT, and zeroing to KPT ran
-    // 14 words past Z into the row pointers being DMA'd beside it)
-    const int padz = c.KP - XS;
+    const int padz = KPT - XS;  // (rows are KP = KPT wide, carve)
     for (int p = tid; p < N * padz; p += NT) {
       const int i = p / padz;
       sZ[i * LDW + XS + (p - i * padz)] = 0.f;
@@ -1131,8 +1133,6 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
       const int ar = min(r0 + li, N - 1);  // rows past N compute garbage that is never pooled
       floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      // (k steps past the row's KP read the next row's finite values against
-      // W's zero padding: no contribution)
       for (int ks = 0; ks < KPT / 16; ++ks) {
         float av[4];
 #pragma unroll

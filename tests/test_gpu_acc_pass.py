@@ -35,7 +35,10 @@ LOSS_TOL = 1e-6  # relative
 def _records(n, seed, classes=0, n_feat=30):
     from bench import records
 
-    recs = records(make_dataset(n, seed=seed, n_feat=n_feat))
+    # (F > 32: graphs of <= 150 nodes, so the carve with 64-wide Z rows plus
+    # the LDS fc1.weight block fits one workgroup)
+    kw = {"n_lo": 110, "n_hi": 150} if n_feat > 32 else {}
+    recs = records(make_dataset(n, seed=seed, n_feat=n_feat, **kw))
     if classes:
         for i, r in enumerate(recs):
             r.y = float(i % classes)

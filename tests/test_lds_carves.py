@@ -92,7 +92,8 @@ def _check(kind, q, extents, aliases=(), host_bytes=None, phases=()):
 # ---- GINet per-graph kernel (ginet_fused.hip:67-109; graph_body :560-838) ----
 def _ginet_ext(N, E, F, K0, P1, K1, alias, OUT):
     def ext(v):
-        XS, KP, LDW = r4(F), r16(F), r16(F) + 2
+        KP = 32 if F <= 32 else 64  # the kernel's KPT: rows as wide as its MFMA steps (r05)
+        XS, LDW = r4(F), KP + 2
         assert (v["$XS"], v["$KP"], v["$LDW"]) == (XS, KP, LDW)
         e = {
             "w1": 32 * F,  # dma_words(sW1, w1, 16F) + (sW1 + 16F, w1e, 16F) (:632-633)
