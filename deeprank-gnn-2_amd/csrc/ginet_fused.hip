@@ -401,6 +401,10 @@ struct TailLds {
   // or null: the depth-0 pooling keys, P1 not yet decoded (conv2 decodes the
   // rows it reads; the decode runs beside it in the same step)
   const unsigned long long* key = nullptr;
+  // p2's first row zeroed by the caller before its last barrier: with one
+  // depth-1 cluster (K1 = 1, K0 < 16) conv2 folds the depth-1 max into it by
+  // LDS atomic max, and the pooling and mean steps go
+  bool p2_zeroed = false;
 };
 
 template <class C>
@@ -440,6 +444,11 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
   if (pb < 0) pb = b;  // the partials' row (slab, head vectors, loss term)
   const int tid = dr_tid<ACC>();
   STAMP(4);
+  // one depth-1 cluster: its max over the K0 pooled rows per channel by LDS
+  // atomic max on the bits as conv2 produces the rows (H2 >= +0 or NaN, so
+  // the unsigned order of the bits is the value order; NaN wins, as the
+  // reference's NaN-propagating amax), the tie counts in the pooling backward
+  const bool one_cl = t.p2_zeroed && K1 == 1 && K0 < 16;
   // ---------------- conv2 on the pooled graph (ginet.py:101,112) ------------
   // H2[k][o] = relu(sum over pooled row k, in edge order, of Y2[j][o]) with
   // Y2[j][o] = P1[j] . W2[o] (16-term fmaf chain) formed per neighbour in
@@ -481,110 +490,117 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
       }
       acc += y;
     }
-    t.h2[p] = relu_keepnan(acc);
+    const float h2v = relu_keepnan(acc);
+    t.h2[p] = h2v;
+    if (one_cl) __hip_atomic_fetch_max(reinterpret_cast<uint32_t*>(t.p2) + o, __float_as_uint(h2v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   __syncthreads();
 
-  STAMP(5);
-  // ---------------- depth-1 max_pool_x: scatter_reduce amax (ginet.py:103) --
-  // NaN propagates; remember the tie count for the even-split backward.
-  // Members are split into S slices per (cluster, channel): each slice's
-  // max (NaN-propagating) and its count of members equal to it, combined per
-  // pair (max is order-free here: H2 >= +0 or NaN).  Also record each
-  // depth-0 cluster's depth-1 cluster for the backward.
-  // (by the last wave, idle here unless K1 >= 15: the pooling pairs start at
-  // wave 0; m counts the member offsets at or below q, all reads in flight)
-  for (int q = tid - (NT - 64); q >= 0 && q < K0; q += 64) {
-    int m = 0;
-    if (K1 <= 16) {
-#pragma unroll
-      for (int j = 1; j < 16; ++j) m += (j < K1 && t.m1p[j < K1 ? j : 0] <= q) ? 1 : 0;
-    } else {
-      while (q >= t.m1p[m + 1]) ++m;
-    }
-    t.cl1[t.m1i[q]] = m;
-  }
-  if (K0 < 16) {  // few members per pair: one pass
-    for (int p = tid; p < K1 * 64; p += NT) {
-      const int m = p >> 6, o = p & 63;
-      const int mb = t.m1p[m], me = t.m1p[m + 1];
-      // members' values gathered once (<= 15): all index reads, then all
-      // value reads in flight (predicated); max and tie count are order-free
-      float v[16];
-      int q[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) q[u] = t.m1i[(mb + u < me) ? mb + u : mb];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = t.h2[q[u] * 64 + o];
-      float mx = v[0];
-#pragma unroll
-      for (int u = 1; u < 16; ++u)
-        if (mb + u < me) mx = (mx != mx || v[u] != v[u]) ? __int_as_float(0x7fc00000) : fmaxf(mx, v[u]);
-      float ties = 0.f;
-#pragma unroll
-      for (int u = 0; u < 16; ++u)
-        if (mb + u < me) ties += (v[u] == mx) ? 1.f : 0.f;
-      t.p2[p] = mx;
-      t.nt[p] = ties;
-      if (K1 == 1) t.g[o] = (0.f + mx) / (float)K1;  // the mean below, for one cluster (same ops)
-    }
+  if (one_cl) {
+    STAMP(5);  // (no pooling or mean step: stamps 5, 6 mark the same point)
+    STAMP(6);
   } else {
-    const int pairs = K1 * 64;
-    const int LS = pairs <= 32 ? 4 : pairs <= 64 ? 3 : pairs <= 128 ? 2 : pairs <= 256 ? 1 : 0;  // pairs*S <= 512
-    const int S = 1 << LS;
-    float* smx = t.dgp;            // [pairs*S] (dgp is free until the head)
-    float* scnt = t.dgp + 512;
-    const float NEG = -__builtin_inff();
-    for (int p = tid; p < pairs * S; p += NT) {
-      const int sl = p & (S - 1), pr = p >> LS, m = pr >> 6, o = pr & 63;
-      const int mb = t.m1p[m], cnt = t.m1p[m + 1] - mb;
-      const int qb = mb + ((cnt * sl) >> LS), qe = mb + ((cnt * (sl + 1)) >> LS);
-      float mx = NEG;
-      for (int q = qb; q < qe; ++q) {
-        const float v = t.h2[t.m1i[q] * 64 + o];
-        mx = (mx != mx || v != v) ? __int_as_float(0x7fc00000) : fmaxf(mx, v);
+    STAMP(5);
+    // ---------------- depth-1 max_pool_x: scatter_reduce amax (ginet.py:103) --
+    // NaN propagates; remember the tie count for the even-split backward.
+    // Members are split into S slices per (cluster, channel): each slice's
+    // max (NaN-propagating) and its count of members equal to it, combined per
+    // pair (max is order-free here: H2 >= +0 or NaN).  Also record each
+    // depth-0 cluster's depth-1 cluster for the backward.
+    // (by the last wave, idle here unless K1 >= 15: the pooling pairs start at
+    // wave 0; m counts the member offsets at or below q, all reads in flight)
+    for (int q = tid - (NT - 64); q >= 0 && q < K0; q += 64) {
+      int m = 0;
+      if (K1 <= 16) {
+#pragma unroll
+        for (int j = 1; j < 16; ++j) m += (j < K1 && t.m1p[j < K1 ? j : 0] <= q) ? 1 : 0;
+      } else {
+        while (q >= t.m1p[m + 1]) ++m;
       }
-      float ties = 0.f;
-      for (int q = qb; q < qe; ++q) ties += (t.h2[t.m1i[q] * 64 + o] == mx) ? 1.f : 0.f;
-      smx[p] = mx;
-      scnt[p] = ties;
+      t.cl1[t.m1i[q]] = m;
+    }
+    if (K0 < 16) {  // few members per pair: one pass
+      for (int p = tid; p < K1 * 64; p += NT) {
+        const int m = p >> 6, o = p & 63;
+        const int mb = t.m1p[m], me = t.m1p[m + 1];
+        // members' values gathered once (<= 15): all index reads, then all
+        // value reads in flight (predicated); max and tie count are order-free
+        float v[16];
+        int q[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) q[u] = t.m1i[(mb + u < me) ? mb + u : mb];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = t.h2[q[u] * 64 + o];
+        float mx = v[0];
+#pragma unroll
+        for (int u = 1; u < 16; ++u)
+          if (mb + u < me) mx = (mx != mx || v[u] != v[u]) ? __int_as_float(0x7fc00000) : fmaxf(mx, v[u]);
+        float ties = 0.f;
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (mb + u < me) ties += (v[u] == mx) ? 1.f : 0.f;
+        t.p2[p] = mx;
+        t.nt[p] = ties;
+        if (K1 == 1) t.g[o] = (0.f + mx) / (float)K1;  // the mean below, for one cluster (same ops)
+      }
+    } else {
+      const int pairs = K1 * 64;
+      const int LS = pairs <= 32 ? 4 : pairs <= 64 ? 3 : pairs <= 128 ? 2 : pairs <= 256 ? 1 : 0;  // pairs*S <= 512
+      const int S = 1 << LS;
+      float* smx = t.dgp;            // [pairs*S] (dgp is free until the head)
+      float* scnt = t.dgp + 512;
+      const float NEG = -__builtin_inff();
+      for (int p = tid; p < pairs * S; p += NT) {
+        const int sl = p & (S - 1), pr = p >> LS, m = pr >> 6, o = pr & 63;
+        const int mb = t.m1p[m], cnt = t.m1p[m + 1] - mb;
+        const int qb = mb + ((cnt * sl) >> LS), qe = mb + ((cnt * (sl + 1)) >> LS);
+        float mx = NEG;
+        for (int q = qb; q < qe; ++q) {
+          const float v = t.h2[t.m1i[q] * 64 + o];
+          mx = (mx != mx || v != v) ? __int_as_float(0x7fc00000) : fmaxf(mx, v);
+        }
+        float ties = 0.f;
+        for (int q = qb; q < qe; ++q) ties += (t.h2[t.m1i[q] * 64 + o] == mx) ? 1.f : 0.f;
+        smx[p] = mx;
+        scnt[p] = ties;
+      }
+      __syncthreads();
+      for (int p = tid; p < pairs; p += NT) {
+        float mx = NEG;
+        bool nan = false;
+        for (int sl = 0; sl < S; ++sl) {
+          const float v = smx[(p << LS) + sl];
+          if (v != v) nan = true;
+          else mx = fmaxf(mx, v);
+        }
+        float ties = 0.f;
+        if (nan) mx = __int_as_float(0x7fc00000);
+        else
+          for (int sl = 0; sl < S; ++sl) ties += (smx[(p << LS) + sl] == mx) ? scnt[(p << LS) + sl] : 0.f;
+        t.p2[p] = mx;
+        t.nt[p] = ties;
+      }
     }
     __syncthreads();
-    for (int p = tid; p < pairs; p += NT) {
-      float mx = NEG;
-      bool nan = false;
-      for (int sl = 0; sl < S; ++sl) {
-        const float v = smx[(p << LS) + sl];
-        if (v != v) nan = true;
-        else mx = fmaxf(mx, v);
-      }
-      float ties = 0.f;
-      if (nan) mx = __int_as_float(0x7fc00000);
-      else
-        for (int sl = 0; sl < S; ++sl) ties += (smx[(p << LS) + sl] == mx) ? scnt[(p << LS) + sl] : 0.f;
-      t.p2[p] = mx;
-      t.nt[p] = ties;
-    }
-  }
-  __syncthreads();
 
-  STAMP(6);
-  // ---------------- per-graph mean (scatter_mean, ginet.py:117-118) ----------
-  // (K1 = 1 with K0 < 16: written by the pooling above)
-  if (!(K1 == 1 && K0 < 16)) {
-    if (tid < 64) {
-      float acc = 0.f;
-      for (int m = 0; m < K1; ++m) acc += t.p2[m * 64 + tid];
-      t.g[tid] = acc / (float)K1;
+    STAMP(6);
+    // ---------------- per-graph mean (scatter_mean, ginet.py:117-118) ----------
+    // (K1 = 1 with K0 < 16: written by the pooling above)
+    if (!(K1 == 1 && K0 < 16)) {
+      if (tid < 64) {
+        float acc = 0.f;
+        for (int m = 0; m < K1; ++m) acc += t.p2[m * 64 + tid];
+        t.g[tid] = acc / (float)K1;
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
 
   STAMP(7);
   {
     drk::GinetHeadLds hl;
     hl.fc2 = t.fc2;
-    hl.g = t.g;
+    hl.g = one_cl ? t.p2 : t.g;  // (one cluster: the mean (0 + max) / 1 is the max itself)
     hl.hpre = t.hpre;
     hl.hh = t.hh;
     hl.hd = t.hd;
@@ -613,10 +629,20 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
     for (int rc = 0; rc < NW; ++rc) dgs += t.dgp[rc * 64 + o];
     const float dgo = dgs / (float)K1;
     float acc = 0.f;
-    for (int e = t.p1trp[j]; e < t.p1trp[j + 1]; ++e) {
-      const int k = t.p1tc[e], mo = t.cl1[k] * 64 + o;
-      const float h = t.h2[k * 64 + o];
-      acc += relu_bwd(h, (h == t.p2[mo] ? 1.f : 0.f) * (dgo / t.nt[mo]));
+    if (one_cl) {  // the one cluster's tie count per channel, here instead of in the pooling step
+      const float mx = t.p2[o];
+      float ties = 0.f;
+      for (int q = 0; q < K0; ++q) ties += (t.h2[q * 64 + o] == mx) ? 1.f : 0.f;
+      for (int e = t.p1trp[j]; e < t.p1trp[j + 1]; ++e) {
+        const float h = t.h2[t.p1tc[e] * 64 + o];
+        acc += relu_bwd(h, (h == mx ? 1.f : 0.f) * (dgo / ties));
+      }
+    } else {
+      for (int e = t.p1trp[j]; e < t.p1trp[j + 1]; ++e) {
+        const int k = t.p1tc[e], mo = t.cl1[k] * 64 + o;
+        const float h = t.h2[k * 64 + o];
+        acc += relu_bwd(h, (h == t.p2[mo] ? 1.f : 0.f) * (dgo / t.nt[mo]));
+      }
     }
     t.y2[p] = acc;
   }
@@ -989,6 +1015,7 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
       sZ[i * LDW + XS + (p - i * padz)] = 0.f;
     }
     for (int p = tid; p < K0 * 32; p += NT) skey[p] = 0ull;
+    if (tid < 64) lds[c.p2 + tid] = 0.f;  // (TailLds::p2_zeroed)
     if (PIPED && tid < 2) reinterpret_cast<uint32_t*>(lds + c.dgp)[tid] = 0u;  // pipe_wait's flag and claim
   }
   // loaded late: no early wait (ACC: read once per launch by the kernel)
@@ -1248,6 +1275,7 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
 
   TailLds t = tail_lds(c, lds);
   t.key = (SIB || !DR_CONV2_KEYS) ? nullptr : skey;
+  t.p2_zeroed = true;
   t.keep = skeep;
   t.acc = ACC ? ac.acc : nullptr;
   t.accf = ACC ? ac.accf : nullptr;
