@@ -70,7 +70,16 @@ __device__ __forceinline__ float4 gather_row_chunk(const uint16_t* col, int eb, 
     const float4 v3 = *reinterpret_cast<const float4*>(&X[__umul24(j3, XS) + c4]);
     acc = f4add(f4add(f4add(f4add(acc, v0), v1), v2), v3);
   }
-  for (; e < ee; ++e) acc = f4add(acc, *reinterpret_cast<const float4*>(&X[__umul24((int)col[e], XS) + c4]));
+  if (e < ee) {  // the last 1-3 edges: their index and row reads in flight together, adds predicated
+    const int l = ee - 1;
+    const int j0 = col[e], j1 = col[min(e + 1, l)], j2 = col[min(e + 2, l)];
+    const float4 v0 = *reinterpret_cast<const float4*>(&X[__umul24(j0, XS) + c4]);
+    const float4 v1 = *reinterpret_cast<const float4*>(&X[__umul24(j1, XS) + c4]);
+    const float4 v2 = *reinterpret_cast<const float4*>(&X[__umul24(j2, XS) + c4]);
+    acc = f4add(acc, v0);
+    acc = e + 1 < ee ? f4add(acc, v1) : acc;
+    acc = e + 2 < ee ? f4add(acc, v2) : acc;
+  }
   return acc;
 }
 

@@ -1,0 +1,9 @@
+#!/bin/bash
+# r05: predicated quad tails in the CSR row gathers — suite, stamps, A/B vs HEAD (GINet, FoutNet, GINet atom).
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+O=gpurun_out/r05r; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
+echo "pytest rc=$rc"; tail -2 $O/pytest_gpu.log; [ $rc -eq 0 ] || { grep -E "^E |FAILED" $O/pytest_gpu.log | head -20; exit $rc; }
+DR_LIB_NAME=libdeeprank2_amd_stamps.so timeout -k 10 200 python tools/stamp_profile.py 64 > $O/stamps.txt 2>&1 || exit 1
+grep -v amdgpu.ids $O/stamps.txt
+bash scripts/gpu_ab.sh r05r/ab "base -" "--model ginet;--model foutnet;--model ginet --graphs atom" 3
