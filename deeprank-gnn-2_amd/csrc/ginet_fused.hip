@@ -42,6 +42,9 @@
 
 namespace {
 
+#ifndef DR_GATHER_ROW2
+#define DR_GATHER_ROW2 1  // GINet gather: one row, two chunks per lane (0: two rows, one chunk)
+#endif
 #ifndef DR_CONV2_KEYS
 #define DR_CONV2_KEYS 0  // 1: conv2 reads the pooled rows from the depth-0 keys, no barrier after their decode (measured 0.1 us slower, r05)
 #endif
@@ -1126,6 +1129,31 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
     }
     for (int tt = SIB ? wave * sc.k + sc.rk : wave; tt * 16 < N; tt += SIB ? NW * sc.k : NW) {
       const int r0 = tt * 16;
+#if DR_GATHER_ROW2
+      if (nch <= 8) {  // one row per lane (r0 + lane/4), chunks q and q ^ 4 (q = lane%4, or +4 on odd rows)
+        const int i = r0 + (lane >> 2);
+        const int ca = (lane & 3) | ((lane & 4)), cb = ca ^ 4;
+        const int eb = i < N ? srp[i] : 0, ee = i < N ? srp[i + 1] : 0;
+        float4 za, zb;
+        drk::gather_row_two_chunks(scol, eb, ee, sX, XS, ca * 4, cb * 4, za, zb);
+        if (i < N) {
+          if (ca < nch) {
+            float* zr = sZ + i * LDW + ca * 4;
+            zr[0] = za.x;
+            zr[1] = za.y;
+            zr[2] = za.z;
+            zr[3] = za.w;
+          }
+          if (cb < nch) {
+            float* zr = sZ + i * LDW + cb * 4;
+            zr[0] = zb.x;
+            zr[1] = zb.y;
+            zr[2] = zb.z;
+            zr[3] = zb.w;
+          }
+        }
+      } else
+#endif
       {  // rows r0+slot and r0+8+slot together: two independent edge chains per lane
         const int i0 = r0 + slot, i1 = r0 + 8 + slot;
         const int eb0 = i0 < N ? srp[i0] : 0, ee0 = i0 < N ? srp[i0 + 1] : 0;

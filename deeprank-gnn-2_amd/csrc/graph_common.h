@@ -83,6 +83,38 @@ __device__ __forceinline__ float4 gather_row_chunk(const uint16_t* col, int eb, 
   return acc;
 }
 
+// One CSR row's sums of two 16-byte X chunks (c4a, c4b) at once: one index
+// read per edge feeds both chunks' row reads, four edges per step; each chunk
+// summed in edge order (same sums as gather_row_chunk)
+__device__ __forceinline__ void gather_row_two_chunks(const uint16_t* col, int eb, int ee, const float* X, int XS,
+                                                      int c4a, int c4b, float4& outa, float4& outb) {
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+  int e = eb;
+  for (; e + 4 <= ee; e += 4) {
+    int e1 = e + 1, e2 = e + 2, e3 = e + 3;
+    asm volatile("" : "+v"(e1), "+v"(e2), "+v"(e3));
+    const int r0 = __umul24((int)col[e], XS), r1 = __umul24((int)col[e1], XS);
+    const int r2 = __umul24((int)col[e2], XS), r3 = __umul24((int)col[e3], XS);
+    const float4 v0 = *reinterpret_cast<const float4*>(&X[r0 + c4a]);
+    const float4 v1 = *reinterpret_cast<const float4*>(&X[r1 + c4a]);
+    const float4 v2 = *reinterpret_cast<const float4*>(&X[r2 + c4a]);
+    const float4 v3 = *reinterpret_cast<const float4*>(&X[r3 + c4a]);
+    const float4 w0 = *reinterpret_cast<const float4*>(&X[r0 + c4b]);
+    const float4 w1 = *reinterpret_cast<const float4*>(&X[r1 + c4b]);
+    const float4 w2 = *reinterpret_cast<const float4*>(&X[r2 + c4b]);
+    const float4 w3 = *reinterpret_cast<const float4*>(&X[r3 + c4b]);
+    a = f4add(f4add(f4add(f4add(a, v0), v1), v2), v3);
+    b = f4add(f4add(f4add(f4add(b, w0), w1), w2), w3);
+  }
+  for (; e < ee; ++e) {
+    const int r = __umul24((int)col[e], XS);
+    a = f4add(a, *reinterpret_cast<const float4*>(&X[r + c4a]));
+    b = f4add(b, *reinterpret_cast<const float4*>(&X[r + c4b]));
+  }
+  outa = a;
+  outb = b;
+}
+
 // Two CSR rows' sums of X chunks at once (one lane, two rows): each row in
 // its own edge order (same sums as gather_row_chunk), four edges of each row
 // per step, so eight index reads and then eight row reads are in flight.
