@@ -1137,19 +1137,16 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
         float4 za, zb;
         drk::gather_row_two_chunks(scol, eb, ee, sX, XS, ca * 4, cb * 4, za, zb);
         if (i < N) {
+          // (rows LDW = KP + 2 words apart: 8-byte aligned, two 64-bit stores per chunk)
           if (ca < nch) {
-            float* zr = sZ + i * LDW + ca * 4;
-            zr[0] = za.x;
-            zr[1] = za.y;
-            zr[2] = za.z;
-            zr[3] = za.w;
+            float2* zr = reinterpret_cast<float2*>(sZ + i * LDW + ca * 4);
+            zr[0] = make_float2(za.x, za.y);
+            zr[1] = make_float2(za.z, za.w);
           }
           if (cb < nch) {
-            float* zr = sZ + i * LDW + cb * 4;
-            zr[0] = zb.x;
-            zr[1] = zb.y;
-            zr[2] = zb.z;
-            zr[3] = zb.w;
+            float2* zr = reinterpret_cast<float2*>(sZ + i * LDW + cb * 4);
+            zr[0] = make_float2(zb.x, zb.y);
+            zr[1] = make_float2(zb.z, zb.w);
           }
         }
       } else
