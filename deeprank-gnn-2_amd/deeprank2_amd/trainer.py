@@ -472,7 +472,13 @@ class Trainer:
                 runner = runner_for(step, store, [len(b) for b in batches], self._runners)
             else:  # this rank's shards of the epoch's global batches (every rank plans the same)
                 plans = [self._shard(ds, idx) for idx in batches]
-                runner = runner_for(step, store, [len(lo) for lo, _ in plans], self._runners, global_sizes=[len(b) for b in batches])
+                # eligibility from the plans, which every rank computes alike: a
+                # global batch leaving ANY rank an empty shard sends every rank
+                # to the loop, so the ranks' collective sequences stay matched
+                if all(min(pl.sizes()) >= 1 for _, pl in plans):
+                    runner = runner_for(step, store, [len(lo) for lo, _ in plans], self._runners, global_sizes=[len(b) for b in batches])
+                else:
+                    runner = None
             if runner is not None:  # the whole epoch as one captured HIP graph (epoch.py)
                 return self._epoch_captured(runner, ds, batches, epoch_number, pass_name, t0, plans)
         for idx in batches:
@@ -532,7 +538,9 @@ class Trainer:
         pred, y = self._format_output(pred.clone(), self.dataset_train._targets_of(idx_all))  # noqa: SLF001
         step_losses = losses.double().cpu().numpy()
         loss_sum = 0.0
-        for lv, b in zip(step_losses, runner.sizes):
+        # each (rank-summed) step loss is the GLOBAL batch's mean: weight it by
+        # the global batch size, as the loop weights loss[0] by len(idx)
+        for lv, b in zip(step_losses, runner.global_sizes):
             loss_sum += float(lv) * b
         count = int(idx_all.size)
         epoch_loss = loss_sum / count if count else None

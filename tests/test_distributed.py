@@ -185,3 +185,128 @@ def test_gloo_world2_trainer_split_and_epoch_order_from_rank0(tmp_path):
         visited = [i for b0, b1 in zip(e0, e1) for i in b0 + b1]
         assert sorted(visited) == list(range(len(r0["main"])))  # every graph once per epoch
     assert r0["epochs"][0] != r0["epochs"][1]  # reshuffled per epoch
+
+
+class _EpochDS:
+    """A dataset stand-in for Trainer._epoch: graph g has loss term g, one edge."""
+
+    def __init__(self, n):
+        self.index_entries = [("f", f"g{i}") for i in range(n)]
+
+    def __len__(self):
+        return len(self.index_entries)
+
+    def edge_counts(self, idx):
+        return np.ones(len(idx), dtype=np.int64)
+
+    def _targets_of(self, idx):
+        return torch.zeros(len(idx))
+
+    def batch_handle(self, local, dev):
+        return np.asarray(local)
+
+
+class _StubStep:
+    """FusedTrainStep stand-in: a step's loss slot is this rank's share of the
+    global batch mean (sum of its graphs' terms / global batch), as the fused
+    step's 1/B_global loss scale gives; the all-reduce is a gloo SUM."""
+
+    def __init__(self, pg):
+        self.pg = pg
+
+    def step(self, local, global_batch):
+        t = torch.tensor([float(np.sum(local)) / global_batch])
+        torch.distributed.all_reduce(t, group=self.pg)
+        return t, torch.as_tensor(np.asarray(local, dtype=np.float32)).reshape(-1, 1)
+
+    def step_empty(self):
+        t = torch.zeros(1)
+        torch.distributed.all_reduce(t, group=self.pg)
+        return t, torch.zeros(0, 1)
+
+    def check_faults(self):
+        pass
+
+
+class _StubRunner:
+    """EpochRunner stand-in: per-step local loss terms into the epoch's vector."""
+
+    def __init__(self, sizes, global_sizes):
+        self.sizes, self.global_sizes = sizes, global_sizes
+
+    def run(self, local_batches):
+        losses = torch.tensor([float(np.sum(lo)) / g for lo, g in zip(local_batches, self.global_sizes)])
+        pred = torch.as_tensor(np.concatenate([np.asarray(lo, dtype=np.float32) for lo in local_batches])).reshape(-1, 1)
+        return losses, pred
+
+
+def _captured_epoch_rank_main(rank, world, port, out_path):
+    """Trainer._epoch on one rank of a world-2 gloo group with stub step/runner
+    (ADVICE r05): the captured epoch's loss weights each rank-summed step loss
+    by the GLOBAL batch size, and a global batch that leaves some rank an
+    empty shard sends EVERY rank to the per-batch loop."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import deeprank2_amd.trainer as T
+
+    pg = dist.group.WORLD
+    calls = []
+
+    def fake_runner_for(step, store, sizes, cache, global_sizes=None):
+        calls.append(list(sizes))
+        return _StubRunner(list(sizes), list(global_sizes))
+
+    T.runner_for = fake_runner_for
+
+    class _Exp:
+        def process(self, *a):
+            self.last = a
+
+    class _Fake:
+        _epoch = T.Trainer._epoch
+        _epoch_captured = T.Trainer._epoch_captured
+        _shard = T.Trainer._shard
+        _format_output = T.Trainer._format_output
+        _export_pred = T.Trainer._export_pred
+
+    res = {}
+    for name, batches in (("captured", [[0, 1, 2, 3, 4], [5, 6, 7]]), ("trailing1", [[0, 1, 2, 3, 4], [5, 6, 7], [8]])):
+        f = _Fake()
+        f.device, f.task, f.process_group, f.shard_policy = torch.device("cpu"), T.REGRESS, pg, "contiguous"
+        f.capture_epochs, f._runners = True, {}
+        f.dataset_train = _EpochDS(9)
+        f.train_loader = type("L", (), {"batches": staticmethod(lambda b=batches: b)})()
+        step = _StubStep(pg)
+        f._fused_step = lambda s=step: s
+        f._fused = step
+        f._targets_for_kernel = lambda ds, dev: None
+        f._output_exporters = _Exp()
+        calls.clear()
+        loss = f._epoch(1, "training")
+        res[name] = {"loss": loss, "runner_calls": len(calls), "preds": f._output_exporters.last[3]}
+    box = [None] * world
+    dist.all_gather_object(box, res)
+    if rank == 0:
+        import json
+
+        with open(out_path, "w") as fh:
+            json.dump(box, fh)
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_captured_epoch_loss_and_eligibility(tmp_path):
+    import json
+
+    out = str(tmp_path / "e.json")
+    mp.spawn(_captured_epoch_rank_main, args=(2, _free_port(), out), nprocs=2, join=True)
+    r0, r1 = json.load(open(out))
+    # unequal shards (3/2 and 2/1): the epoch loss is the mean of the 8 graphs' terms on both ranks
+    for r in (r0, r1):
+        assert r["captured"]["runner_calls"] == 1
+        assert r["captured"]["loss"] == pytest.approx(np.mean(np.arange(8)), rel=1e-6)
+        assert r["captured"]["preds"] == [float(i) for i in range(8)]
+    # a trailing batch of 1 at world 2: no rank captures; the loop gives the same loss on both
+    for r in (r0, r1):
+        assert r["trailing1"]["runner_calls"] == 0
+        assert r["trailing1"]["loss"] == pytest.approx(np.mean(np.arange(9)), rel=1e-6)
+        assert r["trailing1"]["preds"] == [float(i) for i in range(9)]
