@@ -134,7 +134,9 @@ def read_arrays(paths, workers=None):
             if fi not in bufs:
                 bufs[fi] = np.memmap(paths[fi], dtype=np.uint8, mode="r")  # pages read as touched: only the extracted bytes stay resident
             dtype = np.dtype(dt)
-            src = np.frombuffer(bufs[fi], dtype=dtype, count=int(np.prod(shape, dtype=np.int64)), offset=off).reshape(shape)
+            # a private copy: the caller caches these, and a view would see (or
+            # SIGBUS on) an HDF5 file rewritten in place while it is alive
+            src = np.frombuffer(bufs[fi], dtype=dtype, count=int(np.prod(shape, dtype=np.int64)), offset=off).reshape(shape).copy()
         out.append((k, name, src))
     return entries, out
 
@@ -202,7 +204,10 @@ def unpack(z):
             buf = bufs.get(f)
             if buf is None:
                 buf = bufs[f] = np.memmap(files[f], dtype=np.uint8, mode="r")  # pages read as touched, not the whole file pinned
-        out[name] = np.frombuffer(buf, dtype=dtype, count=count, offset=int(offsets[i])).reshape(shape) if count else np.empty(shape, dtype=dtype)
+        a = np.frombuffer(buf, dtype=dtype, count=count, offset=int(offsets[i])).reshape(shape) if count else np.empty(shape, dtype=dtype)
+        # file-backed arrays are copied out of the map (writable, and immune to
+        # the user's HDF5 file being rewritten while the dataset is alive)
+        out[name] = a.copy() if (f >= 0 and count) else a
     return out
 
 
