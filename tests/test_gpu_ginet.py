@@ -292,3 +292,38 @@ def test_captured_sweep_matches_eager():
     for a, b in zip(s1.params, s2.params):
         assert torch.equal(a, b)
     assert int(s2.counter[0]) == 6
+
+
+def test_accumulating_pass_vs_oracle_batch300():
+    """a batch past the CU count (B = 300) takes the
+    accumulating pass by default (``FusedTrainStep.acc = None``:
+    ``dr_ginet_acc_pass``, each workgroup summing its graphs' gradients on
+    chip).  Outputs, loss and every gradient against the oracle
+    (``ginet.py:90-125`` under ``trainer.py:686-690``), then one fused Adam
+    step against torch.optim.Adam, as the B = 64 test above."""
+    torch.manual_seed(4321)
+    datas = _synthetic(300, seed=21)
+    model_o = gnn_ref.GINet(30, 1, 3)
+    model = amd.GINet(30, 1, 3)
+    model.load_state_dict(model_o.state_dict())
+    model = model.to(DEV).train()
+    mask = (torch.rand(300, 128, generator=torch.Generator().manual_seed(8)) >= 0.4).float()
+    out_o, loss_o = _oracle_step(model_o, [d.clone() for d in datas], mask)
+
+    store = GraphStore(pack_graphs(records_from_batch(P.Batch.from_data_list(datas))), DEV)
+    h = amd.BatchHandle(store, np.arange(300))
+    step = GINetTrainStep(model)
+    assert step.acc is None and step._acc_rows(h) > 0  # noqa: SLF001  (the default path is the accumulating pass)
+    before = [p.detach().clone() for p in step.params]
+    loss, out = step.step(h, mask=mask.to(torch.uint8).to(DEV))
+    np.testing.assert_allclose(out.cpu().numpy(), out_o, **TOL)
+    assert float(loss) == pytest.approx(loss_o, rel=1e-4)
+    grads = dict(zip(amd.PARAM_NAMES, step.grads))
+    for n, p in model_o.named_parameters():
+        assert_grad_close(grads[n].cpu().numpy(), p.grad.numpy(), err_msg=n)
+    ref = [torch.nn.Parameter(b) for b in before]
+    for r, g in zip(ref, step.grads):
+        r.grad = g.detach().clone()
+    torch.optim.Adam(ref, lr=1e-3, weight_decay=1e-5).step()
+    for n, r, p in zip(amd.PARAM_NAMES, ref, step.params):
+        np.testing.assert_allclose(p.detach().cpu().numpy(), r.detach().cpu().numpy(), rtol=1e-5, atol=1e-7, err_msg=n)
