@@ -186,7 +186,7 @@ def algorithmic_flops(packed, gids, model="ginet"):
 
 def pmc_mfma(model, kernel_ms, n_wg):
     """MFMA utilisation of the dominant kernel from the newest committed PMC pass
-    (profiles/*/pmc_mfma_<model>.txt, scripts/gpu_pmc_mfma.sh: one rocprofv3
+    (profiles/*/pmc_mfma_<model>.txt, scripts/gpu.sh pmc: one rocprofv3
     --pmc run of SQ_VALU_MFMA_BUSY_CYCLES, SQ_INSTS_MFMA, SQ_BUSY_CU_CYCLES,
     GRBM_GUI_ACTIVE, median over dispatches).
     * executed MFMA FLOPs = SQ_INSTS_MFMA x 2048 (16x16x4 f32), priced against
@@ -230,13 +230,13 @@ def pmc_mfma(model, kernel_ms, n_wg):
     }
 
 
-PMC_FILES = {"ginet": "pmc_ginet_graph_kernel.txt", "foutnet": "pmc_foutnet_graph_kernel.txt", "sgat": "pmc_sgat_graph_kernel.txt", "vanilla": "pmc_vanilla_graph_kernel.txt"}
+PMC_FILES = {"ginet": "pmc_ginet_graph_kernel.txt", "foutnet": "pmc_foutnet_graph_kernel.txt", "sgat": "pmc_sgat_graph_kernel.txt", "vanilla": "pmc_vanilla_graph_kernel.txt", "ginet_nocluster": "pmc_ginet_nocluster_graph_kernel.txt"}
 
 
 def pmc_traffic_bytes(model="ginet"):
     """HBM bytes per graph-kernel launch from the newest committed PMC pass
-    (profiles/*/pmc_<model>_graph_kernel.txt, collected by scripts/gpu_pmc.sh /
-    scripts/gpu_pmc_traffic.sh with FETCH_SIZE and WRITE_SIZE in separate passes).  gfx950 correction
+    (profiles/*/pmc_<model>_graph_kernel.txt, collected by scripts/gpu.sh's pmc
+    section with FETCH_SIZE and WRITE_SIZE in separate passes).  gfx950 correction
     (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts half the bytes of wide
     coalesced reads, so bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024."""
     import glob  # noqa: PLC0415
@@ -388,15 +388,10 @@ def parse_args(argv):
     ap.add_argument("--graphs", choices=["residue", "atom", "mixed", "srv"], default="residue")
     ap.add_argument("--dtype", choices=["f32", "bf16"], default="f32", help="compute dtype of the node GEMMs (bf16: GINet only; fp32 accumulate, fp32 master weights and Adam)")
     ap.add_argument("--force-large", type=int, default=0, help="GINet: run the split tile+tail path with this many nodes per tile (diagnostic)")
-    ap.add_argument("--ginet-path", choices=["auto", "split", "onepass"], default="auto", help="GINet: auto = one workgroup per graph when the batch fits LDS, else the split path; split = tile kernel + tail kernel; onepass = tiles + in-launch tails (one launch)")
+    ap.add_argument("--ginet-path", choices=["auto", "split"], default="auto", help="GINet: auto = one workgroup per graph when the batch fits LDS, else the split path; split = tile kernel + tail kernel")
     ap.add_argument("--vanilla-pipeline", action="store_true", help="VanillaNetwork: the batch-wide kernel pipeline even when the per-graph kernel fits (diagnostic)")
-    ap.add_argument("--sibling-split", type=int, default=0, help="GINet per-graph kernel over K workgroups per graph (dr_ginet_sibling_pass; 0/1 off, -1 auto)")
-    ap.add_argument("--mixed-dispatch", action="store_true", help="mixed batches: graphs that fit LDS on the per-graph kernel, the rest on the large path, two streams (opt-in, measured slower)")
-    ap.add_argument("--one-launch", action="store_true", help="GINet, N=1: graph pass + gradient reduce + Adam in one launch (dr_ginet_train_step; opt-in, measured slower at B=64)")
-    ap.add_argument("--piped", action="store_true", help="GINet, N=1: pipelined step (dr_ginet_piped_step: each launch runs the previous pass's update on its own workgroups beside this pass, which waits for it only before reading a weight)")
     ap.add_argument("--acc", choices=["auto", "on", "off"], default="auto", help="GINet fp32: accumulating pass (dr_ginet_acc_pass: each workgroup sums every R-th graph's gradients on chip, one partial row per workgroup); auto = batches past the CU count")
     ap.add_argument("--no-acc-prefetch", action="store_true", help="accumulating pass without the prefetch layout (A/B: each graph stages its own inputs)")
-    ap.add_argument("--ras", action="store_true", help="GINet, N=1: reduce-at-start step (dr_ginet_ras_step: each launch applies the previous update, then runs its pass; opt-in experiment)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stream-copy", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch every step from Python instead of replaying captured HIP graphs")
@@ -650,10 +645,7 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
     for h in handles:
         h.force_large = bool(args.force_large) or args.ginet_path != "auto"
         h.large_tile = args.force_large or None
-        h.large_onepass = args.ginet_path == "onepass"
         h.vanilla_pipeline = bool(args.vanilla_pipeline)
-        h.mixed_dispatch = bool(args.mixed_dispatch)
-        h.sibling_split = None if args.sibling_split < 0 else args.sibling_split
         if os.environ.get("DR_VANILLA_TILE") is not None:  # diagnostic: rows per pipeline edge tile (0: untiled)
             h.vanilla_tile_rows = int(os.environ["DR_VANILLA_TILE"])
 
@@ -664,9 +656,6 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
             torch.distributed.broadcast(p.data, 0)
     step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5, loss="mse", process_group=pg, compute_dtype=args.dtype)
     model._drop_seed = 77 + rank  # training-mode dropout drawn in-kernel (counter hash)
-    step.fuse_update = bool(args.one_launch)
-    step.ras = bool(args.ras) and pg is None
-    step.piped = bool(args.piped) and pg is None
     step.acc = {"auto": None, "on": True, "off": False}[args.acc]
     step.acc_prefetch = not args.no_acc_prefetch
 
@@ -761,7 +750,6 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
         torch.distributed.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    step.flush()  # reduce-at-start: the last launch's update (outside the timed region, as the first timed launch applied the warm-up's)
 
     # Dominant-kernel duration: the graph pass alone, args.steps launches over
     # the resident mini-batches captured back to back in one HIP graph and
@@ -788,17 +776,16 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
         torch.distributed.all_reduce(et)
     edges_total = float(et.item())
     s = 2 if args.dtype == "bf16" else 4
-    one = all(step.one_launch(h) for h in handles)  # graph pass + reduce + Adam in one kernel
     alg = float(np.mean([algorithmic_bytes(packed, h.gids_host, args.model, s) for h in handles]))
     design = float(np.mean([design_bytes(packed, h.gids_host, args.model) for h in handles]))
     n_params = sum(p.numel() for p in model.parameters())
     adam_bytes = 28 * n_params  # Adam fp32: read param, grad, m, v; write param, m, v (§8(d))
-    kernel_alg = alg + (adam_bytes if one else 0)
+    kernel_alg = alg
     achieved = kernel_alg / (kernel_ms * 1e-3) / 1e9
     ms_step = elapsed / args.steps * 1e3
     wall_gbs = (alg + adam_bytes) / (ms_step * 1e-3) / 1e9
     default_cfg = args.model == "ginet" and args.graphs == "residue" and B == B_PER_GPU and args.dtype == "f32"
-    pmc_cfg = default_cfg or (args.model in ("foutnet", "sgat", "vanilla") and args.graphs == "residue" and B == B_PER_GPU and args.dtype == "f32")
+    pmc_cfg = default_cfg or (args.model in ("foutnet", "sgat", "vanilla", "ginet_nocluster") and args.graphs == "residue" and B == B_PER_GPU and args.dtype == "f32")
     traffic, traffic_src = pmc_traffic_bytes(args.model) if pmc_cfg else (None, None)
     large = args.model == "ginet" and (bool(args.force_large) or args.ginet_path != "auto" or args.dtype == "bf16" or any(h.lds((step.spec.entry, 1), lambda *sz: 0) > 160 * 1024 for h in handles))
     # multi-kernel graph passes (Vanilla pipeline, GINet tile + tail kernels):
@@ -825,7 +812,7 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(graphs[:B], model_name=args.model)
         workload = WORKLOADS.get((args.model, args.graphs), f"{args.model} on {args.graphs} graphs (diagnostic)")
-        kname = "layer-level path (FoutLayer/SGAT/GINetConvLayer + pooling kernels, torch autograd): whole-step wall clock" if layer_path else {"ginet": ("ginet_onepass_kernel (dr_ginet_large_pass, one launch)" if args.ginet_path == "onepass" else "ginet_large_conv1_kernel + ginet_large_tail_kernel (dr_ginet_large_pass)") if large else (("ginet_piped_kernel (dr_ginet_piped_step: the previous pass's gradient reduce + Adam on its own workgroups beside this pass's fwd+loss+bwd, 1 workgroup/graph, which waits for the update only before reading a weight)" if args.piped else "ginet_ras_kernel (dr_ginet_ras_step: the previous step's gradient reduce + Adam, a grid hand-off, then fwd+loss+bwd, 1 workgroup/graph)" if args.ras else "ginet_step_kernel (dr_ginet_train_step: fwd+loss+bwd, 1 workgroup/graph, then gradient reduce + Adam by the last 64 workgroups)") if one else (f"ginet_acc_kernel (dr_ginet_acc_pass: {step._acc_rows(handles[0])} workgroups, each runs every R-th graph's fwd+loss+bwd and sums its gradients on chip; one partial row per workgroup)" if step._acc_rows(handles[0]) else "ginet_graph_kernel (dr_ginet_graph_pass, fwd+loss+bwd, 1 workgroup/graph)")), "foutnet": "fout_graph_kernel<false> (dr_fout_graph_pass)", "vanilla": "vanilla_graph_kernel (dr_vanilla_fused_pass) / vanilla pipeline (dr_vanilla_graph_pass)", "sgat": "fout_graph_kernel<true> (dr_sgat_graph_pass)", "ginet_nocluster": "ginet_nocluster_kernel (dr_ginet_nocluster_graph_pass)"}[args.model]
+        kname = "layer-level path (FoutLayer/SGAT/GINetConvLayer + pooling kernels, torch autograd): whole-step wall clock" if layer_path else {"ginet": "ginet_large_conv1_kernel + ginet_large_tail_kernel (dr_ginet_large_pass)" if large else ((f"ginet_acc_kernel (dr_ginet_acc_pass: {step._acc_rows(handles[0])} workgroups, each runs every R-th graph's fwd+loss+bwd and sums its gradients on chip; one partial row per workgroup)" if step._acc_rows(handles[0]) else "ginet_graph_kernel (dr_ginet_graph_pass, fwd+loss+bwd, 1 workgroup/graph)")), "foutnet": "fout_graph_kernel<false> (dr_fout_graph_pass)", "vanilla": "vanilla_graph_kernel (dr_vanilla_fused_pass) / vanilla pipeline (dr_vanilla_graph_pass)", "sgat": "fout_graph_kernel<true> (dr_sgat_graph_pass)", "ginet_nocluster": "ginet_nocluster_kernel (dr_ginet_nocluster_graph_pass)"}[args.model]
         result = {
             "metric": HEADLINE_METRIC if default_cfg else f"graphs/sec per training step, {workload} (fwd+MSE+bwd+Adam)",
             "value": round(graphs_total / elapsed, 1),
@@ -867,11 +854,11 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": int(kernel_alg),
-                "algorithmic_definition": "SURVEY §8(d) B_alg: s*N*F + 4E + 4(N+1) + 4N + 4K0 + 4 per graph (s=2 bf16, 4 fp32; +s*E*Fe Vanilla, no clusters for Vanilla/ginet_nocluster)" + (" + 28*P Adam bytes (the kernel runs the optimizer step)" if one else ""),
+                "algorithmic_definition": "SURVEY §8(d) B_alg: s*N*F + 4E + 4(N+1) + 4N + 4K0 + 4 per graph (s=2 bf16, 4 fp32; +s*E*Fe Vanilla, no clusters for Vanilla/ginet_nocluster)",
                 "design_bytes_per_launch": int(design),
                 "design_definition": "per-graph gradient slab + head vectors (written, then read by the reduce) and the precomputed pooling structures: intermediates of this design, not compulsory",
                 "kernel_ms_avg": round(kernel_ms, 5),
-                "kernel_timing": "wall clock per eager step (layer-level path)" if layer_path else f"HIP events around one HIP graph of {args.steps} back-to-back {('dr_ginet_train_step' if one else step.spec.entry) if not large else 'dr_ginet_large_pass'} launches on the launch stream, divided by {args.steps}",
+                "kernel_timing": "wall clock per eager step (layer-level path)" if layer_path else f"HIP events around one HIP graph of {args.steps} back-to-back {step.spec.entry if not large else 'dr_ginet_large_pass'} launches on the launch stream, divided by {args.steps}",
                 "stream_copy_GBs": None if copy_gbs is None else round(copy_gbs, 1),
                 "frac_of_stream_copy": None if copy_gbs is None else round(achieved / copy_gbs, 5),
                 "flops_per_launch": int(flops),

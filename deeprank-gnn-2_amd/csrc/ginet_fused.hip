@@ -38,7 +38,6 @@
 #include "dr_common.h"
 #include "graph_common.h"
 #include "ginet_head.h"
-#include "reduce_common.h"
 
 namespace {
 
@@ -774,78 +773,6 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
   STAMP(14);
 }
 
-// KPT: conv1's K (F) padded to whole 16-deep MFMA steps, 32 (F <= 32) or 64.
-// WT: the per-graph partials are stored write-through (read back inside the
-// same launch by dr_ginet_train_step's reducers).  Returns the step counter
-// value the pass used (its dropout offset).
-// Sibling split (dr_ginet_sibling_pass): k workgroups stage the same graph,
-// each runs the front half on every k-th 16-row tile, publishes its Z rows
-// (write-through) and depth-0 keys (agent-scope 64-bit atomic max) and takes a
-// ticket; the last to arrive decodes the keys and runs the tail.  Nothing
-// waits on another workgroup.
-struct SibCtx {
-  int rk, k, b;
-  unsigned long long* gkey; // [B, k0_max, 32], zero on entry and left zero
-  int k0_max;
-  uint32_t* arrive;         // [B], zero on entry and left zero
-};
-
-// Reduce-at-start step (dr_ginet_ras_step, opt-in): each graph workgroup first
-// applies the PREVIOUS step's gradient reduction + Adam to its share of the
-// parameter blocks (while its graph's DMA is in flight), a grid-wide hand-off
-// publishes the new parameters, then the pass runs on them.  The kernel passes
-// the update as a hook: hook(scratch) runs it and returns the Adam step it
-// applied, or -1 when no update was pending (the first step of an epoch).
-struct NoHook {
-  __device__ int64_t operator()(float*) const { return -1; }
-};
-
-// Pipelined step (dr_ginet_piped_step): this launch's pass blocks follow NR
-// reducer blocks that apply the PREVIOUS pass's update.  A pass block stages
-// its graph and gathers its first tile while they run, and only then waits
-// (each wave for itself, polling the update counter) before it reads any
-// weight, with agent-scope loads.  Its partials go to the half of the double
-// buffer the step's parity selects, the previous pass's half being the one the
-// reducers read.
-struct PipeCtx {
-  int NR = 0;                  // reducer blocks ahead of the pass blocks
-  bool pending = false;        // reducers of this launch apply an update: wait for it
-  uint32_t want = 0;           // the update counter value that means "applied"
-  const uint32_t* ver = nullptr;
-  uint32_t* fault = nullptr;   // set when a wait gives up (bounded spin)
-  int spin = 0;
-  int prow = 0;                // first partials row of this pass's buffer half
-};
-
-// One wave per workgroup polls the update counter (the first to arrive claims
-// the job through an LDS word); it then sets an LDS flag that the workgroup's
-// other waves poll (MI355X_MICROARCH.md, inter-workgroup visibility: the other
-// waves load after an LDS word the polling wave sets).  lf: [0] flag, [1] claim,
-// both zeroed before the staging barrier.
-__device__ __forceinline__ void pipe_wait(const PipeCtx& pc, uint32_t* lf) {
-  if (!pc.pending) return;
-  if ((threadIdx.x & 63) == 0) {
-    typedef const __attribute__((address_space(1))) unsigned int gcu32;
-    uint32_t polls = 0;
-    if (__hip_atomic_fetch_add(lf + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
-      while (__hip_atomic_load((gcu32*)pc.ver, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < pc.want) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++polls == (uint32_t)pc.spin) {  // never expected: flag it and go on (loudly)
-          __hip_atomic_store((__attribute__((address_space(1))) unsigned int*)pc.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-      __hip_atomic_store(lf, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    } else {
-      while (__hip_atomic_load(lf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++polls == 4u * (uint32_t)pc.spin) break;  // the poller gives up first
-      }
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // the weight loads stay below the poll
-}
-
 // A graph descriptor by one s_load_dwordx16 (the pointer is wave-uniform);
 // `touch` (optional): one dword of another descriptor loaded beside it and
 // dropped, so that line is in the scalar cache when its graph starts
@@ -890,16 +817,17 @@ struct AccCtx {
   uint32_t* staged = nullptr;
 };
 
-template <int KPT, bool WT, bool SIB = false, bool RAS = false, class Hook = NoHook, bool PIPED = false, bool ACC = false,
-          bool PF = false>
-__device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx& sc, const Hook& hook, const PipeCtx& pc,
-                                               const AccCtx& ac) {
+// KPT: conv1's K (F) padded to whole 16-deep MFMA steps, 32 (F <= 32) or 64.
+// ACC / PF: the accumulating pass (AccCtx) and its prefetch layout.  Returns
+// the step counter value the pass used (its dropout offset).
+template <int KPT, bool ACC = false, bool PF = false>
+__device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const AccCtx& ac) {
   extern __shared__ __attribute__((aligned(16))) float lds_raw[];
   float* lds = lds_raw + (ACC ? ac.acc_words : 0);
   const int tid = dr_tid<ACC>();
   const int lane = tid & 63;
   const int wave = dr_wave<ACC>(tid);
-  const int b = SIB ? sc.b : ACC ? ac.gi : (int)blockIdx.x;
+  const int b = ACC ? ac.gi : (int)blockIdx.x;
   const dr_graph_store& s = a.s;
   // one 64-byte scalar load (ACC: spelled out — in the accumulating kernel's
   // loop hipcc cannot prove the descriptors unwritten and reads them with
@@ -947,25 +875,16 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
   // head's 64 KB of fc1 registers (row and column layouts) are loaded after
   // the staging barrier instead, under the LDS-bound front half.
   float fc1_row[8], fc1_col[8], fc1_bias;
-  // RAS: every weight is read after the update's hand-off, with agent-scope
-  // loads (another workgroup, maybe on another XCD, wrote it this launch)
-  // (PIPED: the same, after the wave's wait for the update of this launch's reducers)
-  auto ldw = [&](const float* p) { return (RAS || PIPED) ? __uint_as_float(__hip_atomic_load((const __attribute__((address_space(1))) unsigned int*)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) : *p; };
   auto load_fc1 = [&]() {
     const int r = tid >> 3, part = tid & 7;
-    if (RAS || PIPED) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) fc1_row[j] = ldw(a.w.fc1w + r * 64 + part * 8 + j);
-    } else {
-      const float4 u0 = *reinterpret_cast<const float4*>(a.w.fc1w + r * 64 + part * 8);
-      const float4 u1 = *reinterpret_cast<const float4*>(a.w.fc1w + r * 64 + part * 8 + 4);
-      fc1_row[0] = u0.x; fc1_row[1] = u0.y; fc1_row[2] = u0.z; fc1_row[3] = u0.w;
-      fc1_row[4] = u1.x; fc1_row[5] = u1.y; fc1_row[6] = u1.z; fc1_row[7] = u1.w;
-    }
-    fc1_bias = ldw(a.w.fc1b + r);
+    const float4 u0 = *reinterpret_cast<const float4*>(a.w.fc1w + r * 64 + part * 8);
+    const float4 u1 = *reinterpret_cast<const float4*>(a.w.fc1w + r * 64 + part * 8 + 4);
+    fc1_row[0] = u0.x; fc1_row[1] = u0.y; fc1_row[2] = u0.z; fc1_row[3] = u0.w;
+    fc1_row[4] = u1.x; fc1_row[5] = u1.y; fc1_row[6] = u1.z; fc1_row[7] = u1.w;
+    fc1_bias = a.w.fc1b[r];
     const int o = tid & 63, rcc = dr_wave<ACC>(tid);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) fc1_col[j] = ldw(a.w.fc1w + (rcc * 8 + j) * 64 + o);
+    for (int j = 0; j < 8; ++j) fc1_col[j] = a.w.fc1w[(rcc * 8 + j) * 64 + o];
   };
   // (ACC: scalar loads through the constant address space — read-only for the
   // launch; hipcc cannot prove that in the accumulating loop and would use a
@@ -1007,7 +926,7 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
   } else if (ac.first || *ac.staged == 0u) {
     stage_inputs(d, c);
   }
-  if (!RAS && !PIPED && (!PF || ac.first)) {
+  if (!PF || ac.first) {
     dma_words(sW1, a.w.w1, 16 * F, tid, DR_DMA_ROT * 5);  // [W1; W1e] rows of F, packed
     dma_words(sW1 + 16 * F, a.w.w1e, 16 * F, tid, DR_DMA_ROT * 14);
   }
@@ -1019,18 +938,9 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
     }
     for (int p = tid; p < K0 * 32; p += NT) skey[p] = 0ull;
     if (tid < 64) lds[c.p2 + tid] = 0.f;  // (TailLds::p2_zeroed)
-    if (PIPED && tid < 2) reinterpret_cast<uint32_t*>(lds + c.dgp)[tid] = 0u;  // pipe_wait's flag and claim
   }
   // loaded late: no early wait (ACC: read once per launch by the kernel)
   if (a.p.step_counter) drop_offset = ACC ? (uint64_t)ac.step : (uint64_t)a.p.step_counter[0];
-  if (RAS) {
-    // the previous step's reduce + Adam, then the grid hand-off (scratch: the
-    // tail's dgp region, 1024 words, unused before the tail)
-    const int64_t ts = hook(lds + c.dgp);
-    if (ts >= 0) drop_offset = (uint64_t)ts;  // this pass's step: the counter value the update leaves
-    for (int p = tid; p < 32 * F; p += NT) sW1[p] = p < 16 * F ? ldw(a.w.w1 + p) : ldw(a.w.w1e + p - 16 * F);
-    load_fc1();
-  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // snapshot for dr_reduce_update, stored only now so that no wait for the
   // counter load sits between the descriptor and the graph DMA
@@ -1044,20 +954,20 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
   // LDS read.)
   float wv2, wfc[3];
   auto load_head_weights = [&]() {
-    wv2 = (tid < 512) ? ldw(a.w.w2 + tid) : ldw(a.w.w2e + tid - 512);
+    wv2 = (tid < 512) ? a.w.w2[tid] : a.w.w2e[tid - 512];
     const int nf = OUT * 128;
 #pragma unroll
     for (int u = 0; u < 3; ++u) {
       const int p = tid + u * NT;
       wfc[u] = 0.f;
-      if (p < nf) wfc[u] = ldw(a.w.fc2w + p);
-      else if (p < nf + OUT) wfc[u] = ldw(a.w.fc2b + p - nf);
+      if (p < nf) wfc[u] = a.w.fc2w[p];
+      else if (p < nf + OUT) wfc[u] = a.w.fc2b[p - nf];
     }
     // fc1 last: the wait for W2 / fc2 before their LDS stores (end of the
     // front half) then leaves these 11 loads in flight (vmcnt counts in order)
-    if (!RAS) load_fc1();
+    load_fc1();
   };
-  if (!PIPED) load_head_weights();
+  load_head_weights();
   // ---------------- conv1 + depth-0 pooling, one 16-row tile per wave -------
   // Each wave runs its rows through the whole front half with no workgroup
   // barrier in between:
@@ -1087,23 +997,12 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
     // W[li][k + 4u + kq] (wa: conv1 rows, wb: conv1_ext rows), zero past F
     constexpr int NKV = KPT / 4;
     float wa[NKV], wb[NKV];
-    // PIPED: W1 straight from global memory after the wave's wait (the
-    // first tile's gather runs before it, under this launch's reducers)
-    bool have_w = !PIPED;
-    auto load_w1 = [&]() {
 #pragma unroll
-      for (int j = 0; j < NKV; ++j) {
-        const int kk = 16 * (j >> 2) + 4 * (j & 3) + kq;
-        if (PIPED) {
-          wa[j] = kk < F ? ldw(a.w.w1 + li * F + kk) : 0.f;
-          wb[j] = kk < F ? ldw(a.w.w1e + li * F + kk) : 0.f;
-        } else {
-          wa[j] = kk < F ? sW1[li * F + kk] : 0.f;
-          wb[j] = kk < F ? sW1[(16 + li) * F + kk] : 0.f;
-        }
-      }
-    };
-    if (!PIPED) load_w1();
+    for (int j = 0; j < NKV; ++j) {
+      const int kk = 16 * (j >> 2) + 4 * (j & 3) + kq;
+      wa[j] = kk < F ? sW1[li * F + kk] : 0.f;
+      wb[j] = kk < F ? sW1[(16 + li) * F + kk] : 0.f;
+    }
     if (PF) {  // the waves with no tile stage the next graph's inputs into the other buffer
       const int busy = (N + 15) >> 4;
       if (ac.next >= 0 && busy < NW && wave >= busy) {
@@ -1127,7 +1026,7 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
       }
       if (tid == 0) *ac.staged = (ac.next >= 0 && busy < NW) ? 1u : 0u;
     }
-    for (int tt = SIB ? wave * sc.k + sc.rk : wave; tt * 16 < N; tt += SIB ? NW * sc.k : NW) {
+    for (int tt = wave; tt * 16 < N; tt += NW) {
       const int r0 = tt * 16;
 #if DR_GATHER_ROW2
       if (nch <= 8) {  // one row per lane (r0 + lane/4), chunks q and q ^ 4 (q = lane%4, or +4 on odd rows)
@@ -1177,18 +1076,6 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
       // this wave's Z rows are complete in LDS before its own MFMA reads them
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (tt == 0) STAMP(20);  // (wave 0's first tile: gather done)
-      if (PIPED && !have_w) {
-#ifdef DR_STAMPS
-        if (tt == 0 && lane == 0 && a.p.stamps) a.p.stamps[(int64_t)b * 32 + 28] = __builtin_amdgcn_s_memrealtime();
-#endif
-        pipe_wait(pc, reinterpret_cast<uint32_t*>(lds + c.dgp));
-#ifdef DR_STAMPS
-        if (tt == 0 && lane == 0 && a.p.stamps) a.p.stamps[(int64_t)b * 32 + 29] = __builtin_amdgcn_s_memrealtime();
-#endif
-        load_w1();
-        load_head_weights();
-        have_w = true;
-      }
       const int ar = min(r0 + li, N - 1);  // rows past N compute garbage that is never pooled
       floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -1226,10 +1113,6 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
         STAMP(22);  // (pool atomics done)
       }
     }
-    if (PIPED && !have_w) {  // a wave with no tile: wait now, then its share of the head weights
-      pipe_wait(pc, reinterpret_cast<uint32_t*>(lds + c.dgp));
-      load_head_weights();
-    }
   }
   // the head's dropout keep flags, by the last two waves (idle in the front
   // half up to N = 224): off the tail's critical path
@@ -1247,66 +1130,17 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
   STAMP(2);
   __syncthreads();
   STAMP(3);
-  typedef __attribute__((address_space(1))) unsigned long long gu64s;
-  typedef __attribute__((address_space(1))) unsigned int gu32s;
-  if (SIB) {
-    // publish this sibling's depth-0 keys
-    gu64s* gk = (gu64s*)(sc.gkey) + (int64_t)b * sc.k0_max * 32;
-    for (int p = tid; p < K0 * 32; p += NT)
-      if (skey[p]) __hip_atomic_fetch_max(gk + p, skey[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave drains its stores and atomics
-    __syncthreads();
-    int* flag = reinterpret_cast<int*>(sP1);
-    if (tid == 0) {
-      const uint32_t ticket = __hip_atomic_fetch_add((gu32s*)(sc.arrive + b), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const bool last = ticket == (uint32_t)sc.k - 1u;
-      if (last) __hip_atomic_store((gu32s*)(sc.arrive + b), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
-      flag[0] = last ? 1 : 0;
-    }
-    __syncthreads();
-    const bool last = flag[0] != 0;
-    __syncthreads();  // the flag read by every wave before sP1 is rewritten
-    if (!last) return drop_offset;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // the hand-off loads stay below the ticket
-    for (int p = tid; p < K0 * 32; p += NT) {
-      const unsigned long long key = __hip_atomic_load(gk + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(gk + p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // zero for the next launch
-      sP1[p] = key ? __uint_as_float((uint32_t)(key >> 32)) : 0.f;
-      sA1[p] = key ? (int)(0xffffffffu - (uint32_t)key) : N;
-    }
-    __syncthreads();
-    // the Z rows of pooling args another sibling computed: gathered again from
-    // the staged graph (same CSR order, same sums; a row named by several
-    // (cluster, channel) pairs is written with the same value by each)
-    {
-      const int sub = tid & 7, nch = XS >> 2;
-      for (int p = tid >> 3; p < K0 * 32; p += NT / 8) {
-        const int i = sA1[p];
-        if (i >= N || ((i >> 4) % sc.k) == sc.rk) continue;
-        const int eb = srp[i], ee = srp[i + 1];
-        for (int ch = sub; ch < nch; ch += 8) {
-          const float4 z = drk::gather_row_chunk(scol, eb, ee, sX, XS, ch * 4);
-          float* zr = sZ + i * LDW + ch * 4;
-          zr[0] = z.x;
-          zr[1] = z.y;
-          zr[2] = z.z;
-          zr[3] = z.w;
-        }
-      }
-    }
-  } else {
-    // (no barrier after the decode: conv2, the tail's first step, reads the
-    // pooled rows from the keys themselves — TailLds::key)
-    for (int p = tid; p < K0 * 32; p += NT) {
-      const unsigned long long key = skey[p];
-      sP1[p] = key ? __uint_as_float((uint32_t)(key >> 32)) : 0.f;
-      sA1[p] = key ? (int)(0xffffffffu - (uint32_t)key) : N;
-    }
+  // (no barrier after the decode: conv2, the tail's first step, reads the
+  // pooled rows from the keys themselves — TailLds::key)
+  for (int p = tid; p < K0 * 32; p += NT) {
+    const unsigned long long key = skey[p];
+    sP1[p] = key ? __uint_as_float((uint32_t)(key >> 32)) : 0.f;
+    sA1[p] = key ? (int)(0xffffffffu - (uint32_t)key) : N;
   }
-  if (SIB || !DR_CONV2_KEYS) __syncthreads();
+  if (!DR_CONV2_KEYS) __syncthreads();
 
   TailLds t = tail_lds(c, lds);
-  t.key = (SIB || !DR_CONV2_KEYS) ? nullptr : skey;
+  t.key = !DR_CONV2_KEYS ? nullptr : skey;
   t.p2_zeroed = true;
   t.keep = skeep;
   t.acc = ACC ? ac.acc : nullptr;
@@ -1314,13 +1148,13 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const SibCtx&
   auto zat = [&](int i, int kk) { return sZ[i * LDW + kk]; };
   // (dr_pass.slot: the graph's rows of the batch when it is split over launches)
   const int orow = a.p.slot ? a.p.slot[b] : b;
-  ginet_tail<decltype(zat), WT, ACC>(a, t, fc1_row, fc1_col, fc1_bias, orow, N, K0, K1, F, OUT, y_g, drop_offset, zat, PIPED ? pc.prow + orow : orow);
+  ginet_tail<decltype(zat), false, ACC>(a, t, fc1_row, fc1_col, fc1_bias, orow, N, K0, K1, F, OUT, y_g, drop_offset, zat, orow);
   return drop_offset;
 }
 
 template <int KPT>
 __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
-  graph_body<KPT, false>(a, SibCtx{}, NoHook{}, PipeCtx{}, AccCtx{});
+  graph_body<KPT>(a, AccCtx{});
 }
 
 // ---------------------------------------------------------------------------
@@ -1381,7 +1215,7 @@ __global__ void __launch_bounds__(NT) ginet_acc_kernel(GinetArgs a, const int32_
     typedef const __attribute__((address_space(4))) GinetArgs* KArgs;
     KArgs ka = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile("; dr_kargs" : "+s"(ka));
-    graph_body<KPT, false, false, false, NoHook, false, true, PF>(*(const GinetArgs*)ka, SibCtx{}, NoHook{}, PipeCtx{}, ac);
+    graph_body<KPT, true, PF>(*(const GinetArgs*)ka, ac);
     __syncthreads();  // the graph carve is restaged by the next graph
   }
   // the workgroup's row, then its loss sum
@@ -1399,339 +1233,6 @@ __global__ void __launch_bounds__(NT) ginet_acc_kernel(GinetArgs a, const int32_
   }
   for (int p = tid; p < HW; p += NT) row[c0 + 128 * 64 + p] = lds_raw[c0 + p];
   if (tid == 0) a.p.loss_per_graph[blockIdx.x] = lds_raw[c0 + HW];
-}
-
-// k sibling workgroups per graph: block -> (graph b, sibling rk), siblings 8
-// blocks apart (one XCD under round-robin dispatch: the hand-off stays in one
-// L2) within a window of 8k consecutive blocks
-template <int KPT>
-__global__ void __launch_bounds__(NT) ginet_sib_kernel(GinetArgs a, SibCtx sc) {
-  const int bx = blockIdx.x, hi = bx >> 3;
-  sc.rk = hi % sc.k;
-  sc.b = (hi / sc.k) * 8 + (bx & 7);
-  if (sc.b >= a.B) return;
-  graph_body<KPT, false, true>(a, sc, NoHook{}, PipeCtx{}, AccCtx{});
-}
-
-// ---------------------------------------------------------------------------
-// One-launch training step (dr_ginet_train_step): B graph workgroups run the
-// graph pass; NR more workgroups of the same grid (blockIdx >= B) are the
-// reducers: they wait for the B arrivals, then sum the partials over the batch
-// and apply Adam (reduce_common.h: the same fixed-order arithmetic as
-// dr_reduce_update, so parameters are bit-identical to the two-launch step).
-//
-// Hand-off (MI355X_MICROARCH.md §inter-workgroup visibility, table row 1):
-// every graph workgroup stores its partials (slab, head vectors, loss term)
-// write-through (sc1), every wave drains them (s_waitcnt vmcnt(0)), and after
-// a workgroup barrier one lane adds to the arrival counter (agent atomic).  A
-// reducer polls the counter (sc1 loads, s_sleep, bounded) until all B have
-// arrived; its waves then read the partials with sc1 loads only.  Graph
-// workgroups never wait, and at most NR <= 128 reducers (of 256 CUs) ever do,
-// so any dispatch order completes.  Each reducer reads the step counter before
-// it counts itself past the poll; the last one past it writes the new step
-// and returns the counters to zero for the next launch.
-// ---------------------------------------------------------------------------
-constexpr int STEP_PARAMS = 16;
-constexpr int STEP_NR_MAX = 128;
-
-struct GinetStepArgs {
-  GinetArgs g;
-  drr::ReduceHdr h;
-  drr::ParamRec rec[STEP_PARAMS];
-  uint32_t* sync;  // [4]: arrivals, reducers past the poll, timeout flag, spare
-  int32_t NR;      // reducer workgroups (blockIdx B .. B+NR-1)
-  int32_t diag;    // DR_STEP_DIAG=1: reducers skip the reduction (times the pass + hand-off alone)
-  int32_t alt_rows;  // dr_ginet_piped_step: rows per half of the partials' double buffer
-  int32_t spin;      // dr_ginet_piped_step: polls before a wait gives up
-};
-
-template <int KPT>
-__global__ void __launch_bounds__(NT) ginet_step_kernel(GinetStepArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  gu32* arrive = (gu32*)(a.sync);
-  gu32* passed = (gu32*)(a.sync + 1);
-  const int B = a.g.B;
-  if ((int)blockIdx.x < B) {
-    graph_body<KPT, true>(a.g, SibCtx{}, NoHook{}, PipeCtx{}, AccCtx{});
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave drains its write-through partials
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  const int role = blockIdx.x - B;
-  const int tid = threadIdx.x, b = blockIdx.x;
-  const GinetArgs& ga = a.g;
-  (void)tid;
-  (void)b;
-  (void)ga;
-  SSTAMP(0);
-  int64_t* sw = reinterpret_cast<int64_t*>(lds);
-  if (threadIdx.x == 0) {
-    // Adam's step: the counter every graph workgroup read (nothing writes it
-    // before every reducer is past the poll)
-    const int64_t t = (int64_t)__hip_atomic_load((__attribute__((address_space(1))) unsigned long long*)(a.g.p.step_counter),
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-    uint32_t polls = 0;
-    int ok = 1;
-    while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)B) {
-      __builtin_amdgcn_s_sleep(20);  // ~1.3 K cycles between polls: little traffic beside the graph pass
-      if (++polls == (1u << 22)) {  // seconds: never expected; flag it and finish the launch
-        __hip_atomic_store((gu32*)(a.sync + 2), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = 0;
-        break;
-      }
-    }
-    const uint32_t d = __hip_atomic_fetch_add(passed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (d == (uint32_t)a.NR - 1) {  // the last reducer past the poll: new step, counters back to zero
-      a.g.p.step_counter[0] = t;
-      // minus B, not := 0: after a give-up, graph workgroups still arriving in
-      // this launch bring it back to exactly 0 by the launch's end
-      __hip_atomic_fetch_sub(arrive, (uint32_t)B, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(passed, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    sw[0] = ok && !a.diag ? t : -1;
-  }
-  __syncthreads();
-  SSTAMP(1);
-  const int64_t tstep = sw[0];
-  if (tstep < 0) return;
-  // reduce blocks: two per workgroup pass (2 x 512 threads), slot = 2 role +
-  // half, blocks slot, slot + 2 NR, ...; every thread runs the same number of
-  // calls (reduce_block holds a workgroup barrier), past the end on an empty
-  // record
-  const int half = threadIdx.x / drr::RT, t = threadIdx.x % drr::RT;
-  float(*part)[drr::RP] = reinterpret_cast<float(*)[drr::RP]>(lds + 64) + half * drr::RC;
-  const int nb = a.h.n_blocks, stride = 2 * a.NR;
-  // the records, read in place from the kernel-argument segment (a dynamic
-  // index into the by-value argument would copy it to scratch)
-  typedef const __attribute__((address_space(4))) drr::ParamRec ConstRec;
-  ConstRec* recs = (ConstRec*)((const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() +
-                               offsetof(GinetStepArgs, rec));
-  for (int j0 = 0; j0 < nb; j0 += stride) {
-    const int j = j0 + 2 * role + half;  // block j -> (parameter, element block): no dependent loads
-    int pi = 0;
-#pragma unroll
-    for (int q = 1; q <= STEP_PARAMS; ++q) pi += (a.h.blk0[q] <= j) ? 1 : 0;
-    pi = j < nb ? pi : a.h.n_params;
-    int eb = pi < a.h.n_params ? j - a.h.blk0[pi] : 0;
-    drr::ParamRec r;
-    memset(&r, 0, sizeof(r));
-    if (pi < a.h.n_params) {  // field by field: scalar loads from the argument segment
-      ConstRec& q = recs[pi];
-      r.param = q.param;
-      r.grad = q.grad;
-      r.m = q.m;
-      r.v = q.v;
-      r.numel = q.numel;
-      r.kind = q.kind;
-      r.off1 = q.off1;
-      r.off2 = q.off2;
-      r.cols = q.cols;
-    } else {
-      eb = 0;
-    }
-    drr::reduce_block<1, true>(a.h, r, eb, j == 0, t, part, tstep);
-    __syncthreads();  // part reused by the next pass
-  }
-  SSTAMP(2);
-}
-
-// ---------------------------------------------------------------------------
-// Reduce-at-start step (dr_ginet_ras_step): grid = the B graph workgroups.
-// Launch t applies step t-1's update (when sync[3] says its partials are
-// pending), then runs pass t, whose partials the next launch (or
-// dr_reduce_update, the epoch-end flush) applies.  Each workgroup reduces its
-// share of the parameter blocks with the same fixed-order arithmetic as
-// dr_reduce_update (reduce_common.h), storing the new parameters
-// write-through; every wave drains, one lane arrives on sync[0] and polls it
-// (agent-scope loads, s_sleep, bounded: a give-up sets sync[2] and the pass
-// goes on, loudly) until all B have arrived; the last workgroup past the wait
-// returns the counters to zero.  The pass then reads every weight with
-// agent-scope loads.  All B workgroups must be co-resident (B <= the CUs free
-// for a 1024-thread, ~125 KB-LDS workgroup each): the host checks B <= 256.
-// The parameters after K launches + the flush are bit-identical to K
-// two-launch steps; loss_out lags one step (launch t reports step t-1).
-// ---------------------------------------------------------------------------
-template <int KPT>
-__global__ void __launch_bounds__(NT) ginet_ras_kernel(GinetStepArgs a) {
-  const int B = a.g.B, b = blockIdx.x;
-  uint32_t* sync = a.sync;
-  const int pending = (int)sync[3];               // written by the previous launch
-  const int64_t tstep = a.g.p.step_counter[1] + 1;  // the snapshot the previous pass took, + 1
-  typedef const __attribute__((address_space(4))) drr::ParamRec ConstRec;
-  ConstRec* recs = (ConstRec*)((const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() +
-                               offsetof(GinetStepArgs, rec));
-  auto hook = [&](float* scratch) -> int64_t {
-    if (!pending) return -1;
-    const int half = threadIdx.x / drr::RT, t = threadIdx.x % drr::RT;
-    float(*part)[drr::RP] = reinterpret_cast<float(*)[drr::RP]>(scratch) + half * drr::RC;
-    const int nb = a.h.n_blocks, stride = 2 * B;
-    for (int j0 = 0; j0 < nb; j0 += stride) {
-      const int j = j0 + 2 * b + half;  // block j -> (parameter, element block)
-      int pi = 0;
-#pragma unroll
-      for (int q = 1; q <= STEP_PARAMS; ++q) pi += (a.h.blk0[q] <= j) ? 1 : 0;
-      pi = j < nb ? pi : a.h.n_params;
-      int eb = pi < a.h.n_params ? j - a.h.blk0[pi] : 0;
-      drr::ParamRec r;
-      memset(&r, 0, sizeof(r));
-      if (pi < a.h.n_params) {
-        ConstRec& q = recs[pi];
-        r.param = q.param;
-        r.grad = q.grad;
-        r.m = q.m;
-        r.v = q.v;
-        r.numel = q.numel;
-        r.kind = q.kind;
-        r.off1 = q.off1;
-        r.off2 = q.off2;
-        r.cols = q.cols;
-      } else {
-        eb = 0;
-      }
-      drr::reduce_block<0, true, true>(a.h, r, eb, j == 0, t, part, tstep);
-      __syncthreads();  // part reused by the next pass
-    }
-    if (b == 0 && threadIdx.x == 0) a.g.p.step_counter[0] = tstep;  // the LEAN reduce leaves it to the caller
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's write-through parameters drained
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      gu32* arrive = (gu32*)sync;
-      gu32* passed = (gu32*)(sync + 1);
-      __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      uint32_t polls = 0;
-      while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)B) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++polls == (1u << 22)) {  // never expected: flag it, finish the launch
-          __hip_atomic_store((gu32*)(sync + 2), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-      const uint32_t d = __hip_atomic_fetch_add(passed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (d == (uint32_t)B - 1u) {  // the last past the wait: counters back to zero for the next launch
-        __hip_atomic_fetch_sub(arrive, (uint32_t)B, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(passed, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // the weight loads stay below the hand-off
-    return tstep;
-  };
-  graph_body<KPT, false, false, true>(a.g, SibCtx{}, hook, PipeCtx{}, AccCtx{});
-  // this pass's partials are pending for the next launch: flagged by the LAST
-  // workgroup to finish (sync[4] counts them), so no workgroup of this launch
-  // can still read the flag at its entry and take the partials being written
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t d = __hip_atomic_fetch_add((gu32*)(sync + 4), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (d == (uint32_t)B - 1u) {
-      __hip_atomic_store((gu32*)(sync + 4), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store((gu32*)(sync + 3), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Pipelined step (dr_ginet_piped_step): launch s = pass s by B graph blocks
-// (blockIdx < B, dispatched first) + the update of pass s-1 by NR reducer
-// blocks behind them.  The reducers read the previous launch's partials (rows
-// of the buffer half (s-1) & 1) with the fixed-order arithmetic of
-// dr_reduce_update (reduce_common.h) and store the new parameters
-// write-through; every wave drains, and the last reducer to take a ticket
-// (sync[6]) publishes the update counter sync[5] = s.  The pass blocks never
-// wait for the reducers before their staging and their first tile's gather:
-// a wave waits (pipe_wait: one poller per workgroup, the others on an LDS
-// flag) only right before it reads a weight, so the update runs under the
-// staging instead of as a launch of its own.  Nothing ever waits for a pass
-// block and the reducers never wait, so the waits need only that NR + B
-// one-per-CU workgroups be co-resident (the host checks NR + B <= 224).
-// s = counter[0] at launch; the last block of the launch to finish (sync[4])
-// sets counter[0] = s + 1 and the pending flag sync[3] (with no pass blocks,
-// n_batch 0: the flush of the last update, counter[0] unchanged, sync[3] and
-// sync[5] cleared).  The parameters, moments, gradients and loss terms are
-// bit-identical to dr_ginet_graph_pass + dr_reduce_update steps; loss_out
-// lags one launch.
-// ---------------------------------------------------------------------------
-template <int KPT>
-__global__ void __launch_bounds__(NT) ginet_piped_kernel(GinetStepArgs a) {
-  uint32_t* sync = a.sync;
-  const int NR = a.NR;
-  const bool pending = sync[3] != 0u;                  // written by the previous launch
-  const int64_t s_step = a.g.p.step_counter[0];        // passes done before this launch
-  const int B = a.g.B;
-  RSTAMP(blockIdx.x, 24);
-  if ((int)blockIdx.x >= B) {  // the reducers follow the pass blocks (those start first)
-    const int rb = (int)blockIdx.x - B;
-    if (pending && !(a.diag & 2)) {  // DR_STEP_DIAG bit 1 (diagnostic, wrong results): no update
-      typedef const __attribute__((address_space(4))) drr::ParamRec ConstRec;
-      ConstRec* recs = (ConstRec*)((const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() +
-                                   offsetof(GinetStepArgs, rec));
-      extern __shared__ __attribute__((aligned(16))) float lds[];
-      const int half = threadIdx.x / drr::RT, t = threadIdx.x % drr::RT;
-      float(*part)[drr::RP] = reinterpret_cast<float(*)[drr::RP]>(lds) + half * drr::RC;
-      const int nb = a.h.n_blocks;
-      const int64_t row_off = ((s_step - 1) & 1) * (int64_t)a.alt_rows;
-      for (int j0 = 0; j0 < nb; j0 += 2 * NR) {
-        const int j = j0 + 2 * rb + half;  // block j -> (parameter, element block)
-        int pi = 0;
-#pragma unroll
-        for (int q = 1; q <= STEP_PARAMS; ++q) pi += (a.h.blk0[q] <= j) ? 1 : 0;
-        pi = j < nb ? pi : a.h.n_params;
-        int eb = pi < a.h.n_params ? j - a.h.blk0[pi] : 0;
-        drr::ParamRec r;
-        memset(&r, 0, sizeof(r));
-        if (pi < a.h.n_params) {
-          ConstRec& q = recs[pi];
-          r.param = q.param;
-          r.grad = q.grad;
-          r.m = q.m;
-          r.v = q.v;
-          r.numel = q.numel;
-          r.kind = q.kind;
-          r.off1 = q.off1;
-          r.off2 = q.off2;
-          r.cols = q.cols;
-        } else {
-          eb = 0;
-        }
-        drr::reduce_block<0, true, true>(a.h, r, eb, j == 0, t, part, s_step, row_off);
-        __syncthreads();  // part reused by the next round
-      }
-      RSTAMP(blockIdx.x, 25);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's write-through parameters drained
-      __syncthreads();
-      RSTAMP(blockIdx.x, 26);
-      if (threadIdx.x == 0) {
-        const uint32_t k = __hip_atomic_fetch_add((gu32*)(sync + 6), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (k == (uint32_t)NR - 1u) {  // the last reducer: every update is out
-          __hip_atomic_store((gu32*)(sync + 6), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store((gu32*)(sync + 5), (uint32_t)s_step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-    }
-  } else {
-    PipeCtx pc;
-    pc.NR = NR;
-    pc.pending = pending && !(a.diag & 1);  // DR_STEP_DIAG bit 0 (diagnostic, wrong results): no waits
-    pc.want = (uint32_t)s_step;
-    pc.ver = sync + 5;
-    pc.fault = sync + 2;
-    pc.spin = a.spin;
-    pc.prow = (int)((s_step & 1) * a.alt_rows);
-    graph_body<KPT, false, false, false, NoHook, true>(a.g, SibCtx{}, NoHook{}, pc, AccCtx{});
-  }
-  // the last block of the launch to finish: the step counter and the pending flag
-  __syncthreads();
-  RSTAMP(blockIdx.x, 27);
-  if (threadIdx.x == 0) {
-    const uint32_t d = __hip_atomic_fetch_add((gu32*)(sync + 4), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (d == gridDim.x - 1u) {
-      __hip_atomic_store((gu32*)(sync + 4), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (a.g.B > 0) a.g.p.step_counter[0] = s_step + 1;
-      else __hip_atomic_store((gu32*)(sync + 5), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // flushed: counters back to zero
-      __hip_atomic_store((gu32*)(sync + 3), a.g.B > 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
 }
 
 // =========================================================================
@@ -2402,41 +1903,6 @@ __global__ void __launch_bounds__(NT) ginet_large_tail_kernel(LargeArgs la) {
   tail_body<false>(la, blockIdx.x, lds);
 }
 
-// One launch for the whole pass (dr_large_plan.arrive set): every workgroup
-// runs one tile (conv_tile_*), publishes its Z rows (sc1 stores) and its
-// partial maxima (agent-scope atomic max), drains them, and takes a ticket on
-// its graph's arrival counter; the workgroup that draws the last ticket runs
-// the graph's tail (tail_body<true>) right away — no second launch, and a
-// graph's tail starts as soon as its own tiles are done.  Nothing waits on
-// another workgroup, so any dispatch order or placement completes.
-template <bool BF16>
-__global__ void __launch_bounds__(NT) ginet_onepass_kernel(LargeArgs la) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const dr_large_plan& pl = la.plan;
-  if (BF16)
-    conv_tile_bf16<NT, true>(la, lds);
-  else
-    conv_tile_f32<NT, true>(la, lds);
-  const int tile = blockIdx.x, b = pl.tile_slot[tile];
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave drains its Z stores and key atomics
-  __syncthreads();
-  int* flag = reinterpret_cast<int*>(lds);
-  if (threadIdx.x == 0) {
-    const uint32_t tiles = (uint32_t)(pl.tile_first[b + 1] - pl.tile_first[b]);
-    gu32* cnt = (gu32*)(pl.arrive + b);
-    const uint32_t ticket = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool last = ticket == tiles - 1;
-    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next pass
-    flag[0] = last ? 1 : 0;
-  }
-  __syncthreads();
-  const bool last = flag[0] != 0;
-  __syncthreads();  // flag read by every wave before the tail reuses the LDS
-  if (!last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the hand-off loads below the ticket
-  tail_body<true>(la, b, lds);
-}
-
 }  // namespace
 
 extern "C" int64_t dr_ginet_lds_bytes(int32_t n_nodes, int32_t n_edges, int32_t n_feat, int32_t k0, int32_t p1_edges,
@@ -2539,197 +2005,6 @@ extern "C" int dr_ginet_acc_pass(const dr_graph_store* store, const dr_graph_des
   return (int)hipGetLastError();
 }
 
-extern "C" int dr_ginet_sibling_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
-                                     const dr_large_plan* plan, const dr_ginet_weights* w, const dr_pass* pass,
-                                     int32_t split, int32_t lds_bytes, void* stream) {
-  if (!store || !descs || !w || !pass || !plan || n_batch < 0) return DR_E_ARG;
-  if (split < 1 || split > 8) return DR_E_ARG;
-  if (pass->out_dim < 1 || pass->out_dim > DR_MAX_OUT) return DR_E_UNSUPPORTED;
-  if (store->n_feat < 1 || 32 * store->n_feat > 2 * NT) return DR_E_UNSUPPORTED;  // F <= 64
-  if (lds_bytes > 160 * 1024) return DR_E_LDS;
-  if (pass->compute_dtype != DR_DTYPE_F32) return DR_E_UNSUPPORTED;
-  if (!plan->part_key || !plan->arrive || plan->k0_max < 1 || plan->k0_max > 64) return DR_E_ARG;
-  if ((pass->flags & DR_PASS_BACKWARD) && (!pass->slab || !pass->head)) return DR_E_ARG;
-  if ((pass->flags & DR_PASS_BACKWARD) && pass->loss_kind == DR_LOSS_NONE && !pass->dout) return DR_E_ARG;
-  if ((pass->flags & DR_PASS_FORWARD) && !pass->out) return DR_E_ARG;
-  if (pass->use_dropout == DR_DROPOUT_MASK && !pass->mask) return DR_E_ARG;
-  if (pass->use_dropout < DR_DROPOUT_OFF || pass->use_dropout > DR_DROPOUT_HASH) return DR_E_ARG;
-  if (n_batch == 0) return DR_OK;
-  if (!store->cl0) return DR_E_ARG;
-  GinetArgs args;
-  args.s = *store;
-  args.w = *w;
-  args.p = *pass;
-  args.descs = descs;
-  args.B = n_batch;
-  SibCtx sc;
-  sc.rk = 0;
-  sc.b = 0;
-  sc.k = split;
-  sc.gkey = reinterpret_cast<unsigned long long*>(plan->part_key);
-  sc.k0_max = plan->k0_max;
-  sc.arrive = plan->arrive;
-  const dim3 grid((unsigned)(((n_batch + 7) / 8) * 8 * split));
-  if (store->n_feat <= 32) {
-    DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_sib_kernel<32>)));
-    hipLaunchKernelGGL(ginet_sib_kernel<32>, grid, dim3(NT), lds_bytes, (hipStream_t)stream, args, sc);
-  } else {
-    DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_sib_kernel<64>)));
-    hipLaunchKernelGGL(ginet_sib_kernel<64>, grid, dim3(NT), lds_bytes, (hipStream_t)stream, args, sc);
-  }
-  return (int)hipGetLastError();
-}
-
-extern "C" int dr_ginet_train_step(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
-                                   const dr_ginet_weights* w, const dr_pass* pass, int32_t lds_bytes,
-                                   const dr_param_table* table, const dr_adam* adam, float* loss_out, uint32_t* sync,
-                                   void* stream) {
-  if (!store || !descs || !w || !pass || !table || !adam || !sync || n_batch < 0) return DR_E_ARG;
-  if (pass->out_dim < 1 || pass->out_dim > DR_MAX_OUT) return DR_E_UNSUPPORTED;
-  if (store->n_feat < 1 || 32 * store->n_feat > 2 * NT) return DR_E_UNSUPPORTED;  // F <= 64
-  if (lds_bytes > 160 * 1024) return DR_E_LDS;
-  if (pass->compute_dtype != DR_DTYPE_F32) return DR_E_UNSUPPORTED;
-  if (pass->flags != (DR_PASS_FORWARD | DR_PASS_BACKWARD) || pass->loss_kind == DR_LOSS_NONE) return DR_E_ARG;
-  if (!pass->out || !pass->slab || !pass->head || !pass->loss_per_graph || !pass->step_counter) return DR_E_ARG;
-  if (pass->use_dropout == DR_DROPOUT_MASK && !pass->mask) return DR_E_ARG;
-  if (pass->use_dropout < DR_DROPOUT_OFF || pass->use_dropout > DR_DROPOUT_HASH) return DR_E_ARG;
-  if (!adam->enabled || adam->step_counter != pass->step_counter || adam->grad_div) return DR_E_ARG;
-  if (table->n_params > STEP_PARAMS || table->slab_stride != DR_SLAB_STRIDE(store->n_feat) ||
-      table->head_stride != DR_HEAD_STRIDE(pass->out_dim))
-    return DR_E_ARG;
-  if (n_batch == 0) return DR_OK;
-  if (!store->cl0) return DR_E_ARG;
-  GinetStepArgs a;
-  std::memset(&a, 0, sizeof(a));
-  const int blocks = drr::build_reduce(table, pass->slab, pass->head, n_batch, adam, pass->loss_per_graph,
-                                       pass->loss_scale, loss_out, a.h, a.rec);
-  if (blocks < 0) return blocks;
-  a.g.s = *store;
-  a.g.w = *w;
-  a.g.p = *pass;
-  a.g.descs = descs;
-  a.g.B = n_batch;
-  a.sync = sync;
-  a.NR = (blocks + 1) / 2 < STEP_NR_MAX ? (blocks + 1) / 2 : STEP_NR_MAX;
-  if (a.NR < 1) return DR_E_ARG;
-  {
-    static const char* env = std::getenv("DR_STEP_DIAG");  // diagnostic: skip the reduction
-    a.diag = env ? std::atoi(env) : 0;
-  }
-  const int lds = lds_bytes > (64 + 2 * drr::RT) * 4 ? lds_bytes : (64 + 2 * drr::RT) * 4;
-  const dim3 grid(n_batch + a.NR);
-  if (store->n_feat <= 32) {
-    DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_step_kernel<32>)));
-    hipLaunchKernelGGL(ginet_step_kernel<32>, grid, dim3(NT), lds, (hipStream_t)stream, a);
-  } else {
-    DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_step_kernel<64>)));
-    hipLaunchKernelGGL(ginet_step_kernel<64>, grid, dim3(NT), lds, (hipStream_t)stream, a);
-  }
-  return (int)hipGetLastError();
-}
-
-extern "C" int dr_ginet_piped_step(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
-                                   const dr_ginet_weights* w, const dr_pass* pass, int32_t lds_bytes,
-                                   const dr_param_table* table, const dr_adam* adam, float* loss_out, uint32_t* sync,
-                                   int32_t prev_batch, float prev_loss_scale, int32_t alt_rows, void* stream) {
-  if (!store || !w || !pass || !table || !adam || !sync || n_batch < 0 || alt_rows < 1) return DR_E_ARG;
-  if (n_batch > 0 && !descs) return DR_E_ARG;
-  if (pass->out_dim < 1 || pass->out_dim > DR_MAX_OUT) return DR_E_UNSUPPORTED;
-  if (store->n_feat < 1 || 32 * store->n_feat > 2 * NT) return DR_E_UNSUPPORTED;  // F <= 64
-  if (lds_bytes > 160 * 1024) return DR_E_LDS;
-  if (n_batch > alt_rows || prev_batch < 0 || prev_batch > alt_rows) return DR_E_ARG;
-  if (pass->compute_dtype != DR_DTYPE_F32 || pass->slot) return DR_E_UNSUPPORTED;
-  if (pass->flags != (DR_PASS_FORWARD | DR_PASS_BACKWARD) || pass->loss_kind == DR_LOSS_NONE) return DR_E_ARG;
-  if (!pass->out || !pass->slab || !pass->head || !pass->loss_per_graph || !pass->step_counter) return DR_E_ARG;
-  if (pass->use_dropout == DR_DROPOUT_MASK && !pass->mask) return DR_E_ARG;
-  if (pass->use_dropout < DR_DROPOUT_OFF || pass->use_dropout > DR_DROPOUT_HASH) return DR_E_ARG;
-  if (!adam->enabled || adam->step_counter != pass->step_counter || adam->grad_div || adam->fault) return DR_E_ARG;
-  if (table->n_params > STEP_PARAMS || table->slab_stride != DR_SLAB_STRIDE(store->n_feat) ||
-      table->head_stride != DR_HEAD_STRIDE(pass->out_dim))
-    return DR_E_ARG;
-  if (!store->cl0) return DR_E_ARG;
-  GinetStepArgs a;
-  std::memset(&a, 0, sizeof(a));
-  // the pending update is the previous pass's: its batch size and loss scale
-  const int blocks = drr::build_reduce(table, pass->slab, pass->head, prev_batch, adam, pass->loss_per_graph,
-                                       prev_loss_scale, loss_out, a.h, a.rec);
-  if (blocks < 0) return blocks;
-  a.g.s = *store;
-  a.g.w = *w;
-  a.g.p = *pass;
-  a.g.descs = descs;
-  a.g.B = n_batch;
-  a.sync = sync;
-  {
-    static const char* env = std::getenv("DR_PIPED_NR");  // reducer workgroups (tuning; default 32)
-    const int want = env ? std::atoi(env) : 32;
-    a.NR = (blocks + 1) / 2 < want ? (blocks + 1) / 2 : (want > 0 ? want : 1);
-  }
-  a.alt_rows = alt_rows;
-  a.spin = pass->spin_limit > 0 ? pass->spin_limit : (1 << 22);
-  {
-    static const char* env = std::getenv("DR_STEP_DIAG");  // diagnostic timing switches (wrong results)
-    a.diag = env ? std::atoi(env) : 0;
-  }
-  if (a.NR < 1 || a.NR + n_batch > 224) return DR_E_UNSUPPORTED;  // one workgroup per CU, all co-resident
-  // the reducers' LDS scratch (2 x RC x RP floats) fits any pass carve
-  const int lds = lds_bytes > 2 * drr::RC * drr::RP * 4 ? lds_bytes : 2 * drr::RC * drr::RP * 4;
-  const dim3 grid(a.NR + n_batch);
-  if (store->n_feat <= 32) {
-    DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_piped_kernel<32>)));
-    hipLaunchKernelGGL(ginet_piped_kernel<32>, grid, dim3(NT), lds, (hipStream_t)stream, a);
-  } else {
-    DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_piped_kernel<64>)));
-    hipLaunchKernelGGL(ginet_piped_kernel<64>, grid, dim3(NT), lds, (hipStream_t)stream, a);
-  }
-  return (int)hipGetLastError();
-}
-
-extern "C" int dr_ginet_ras_step(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
-                                 const dr_ginet_weights* w, const dr_pass* pass, int32_t lds_bytes,
-                                 const dr_param_table* table, const dr_adam* adam, float* loss_out, uint32_t* sync,
-                                 int32_t prev_batch, float prev_loss_scale, void* stream) {
-  if (!store || !descs || !w || !pass || !table || !adam || !sync || n_batch < 0) return DR_E_ARG;
-  if (pass->out_dim < 1 || pass->out_dim > DR_MAX_OUT) return DR_E_UNSUPPORTED;
-  if (store->n_feat < 1 || 32 * store->n_feat > 2 * NT) return DR_E_UNSUPPORTED;  // F <= 64
-  if (lds_bytes > 160 * 1024) return DR_E_LDS;
-  if (n_batch > 256) return DR_E_UNSUPPORTED;  // every workgroup co-resident for the hand-off
-  if (pass->compute_dtype != DR_DTYPE_F32) return DR_E_UNSUPPORTED;
-  if (pass->flags != (DR_PASS_FORWARD | DR_PASS_BACKWARD) || pass->loss_kind == DR_LOSS_NONE) return DR_E_ARG;
-  if (!pass->out || !pass->slab || !pass->head || !pass->loss_per_graph || !pass->step_counter) return DR_E_ARG;
-  if (pass->use_dropout == DR_DROPOUT_MASK && !pass->mask) return DR_E_ARG;
-  if (pass->use_dropout < DR_DROPOUT_OFF || pass->use_dropout > DR_DROPOUT_HASH) return DR_E_ARG;
-  if (!adam->enabled || adam->step_counter != pass->step_counter || adam->grad_div || adam->fault) return DR_E_ARG;
-  if (table->n_params > STEP_PARAMS || table->slab_stride != DR_SLAB_STRIDE(store->n_feat) ||
-      table->head_stride != DR_HEAD_STRIDE(pass->out_dim))
-    return DR_E_ARG;
-  if (n_batch == 0) return DR_OK;
-  if (!store->cl0) return DR_E_ARG;
-  GinetStepArgs a;
-  std::memset(&a, 0, sizeof(a));
-  if (prev_batch < 0 || prev_batch > 256) return DR_E_ARG;
-  // the pending update is the previous pass's: its batch size and loss scale
-  const int blocks = drr::build_reduce(table, pass->slab, pass->head, prev_batch, adam, pass->loss_per_graph,
-                                       prev_loss_scale, loss_out, a.h, a.rec);
-  if (blocks < 0) return blocks;
-  a.g.s = *store;
-  a.g.w = *w;
-  a.g.p = *pass;
-  a.g.descs = descs;
-  a.g.B = n_batch;
-  a.sync = sync;
-  a.NR = 0;
-  const dim3 grid(n_batch);
-  if (store->n_feat <= 32) {
-    DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_ras_kernel<32>)));
-    hipLaunchKernelGGL(ginet_ras_kernel<32>, grid, dim3(NT), lds_bytes, (hipStream_t)stream, a);
-  } else {
-    DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_ras_kernel<64>)));
-    hipLaunchKernelGGL(ginet_ras_kernel<64>, grid, dim3(NT), lds_bytes, (hipStream_t)stream, a);
-  }
-  return (int)hipGetLastError();
-}
-
 extern "C" int64_t dr_ginet_large_conv_lds_bytes(int32_t n_nodes, int32_t n_feat, int32_t k0, int32_t halo_max,
                                                  int32_t tile_edges_max) {
   return 4LL * conv_carve(n_nodes, n_feat, k0, halo_max, tile_edges_max).total;
@@ -2760,7 +2035,7 @@ extern "C" int dr_ginet_large_pass(const dr_graph_store* store, const dr_graph_d
                          !plan->lcol || !plan->tile_members || !plan->tile_mptr))
     return DR_E_ARG;
   if (!plan->halo_ids && plan->halo_max) return DR_E_ARG;
-  if (plan->arrive && !plan->part_key) return DR_E_ARG;  // the one-launch form combines tiles by atomic max
+  if (plan->arrive) return DR_E_ARG;  // (the one-launch form was removed in r06)
   if ((pass->flags & DR_PASS_BACKWARD) && (!pass->slab || !pass->head)) return DR_E_ARG;
   if ((pass->flags & DR_PASS_BACKWARD) && pass->loss_kind == DR_LOSS_NONE && !pass->dout) return DR_E_ARG;
   if ((pass->flags & DR_PASS_FORWARD) && !pass->out) return DR_E_ARG;
@@ -2781,17 +2056,6 @@ extern "C" int dr_ginet_large_pass(const dr_graph_store* store, const dr_graph_d
   la.g.B = n_batch;
   la.plan = *plan;
   hipStream_t st = (hipStream_t)stream;
-  if (plan->arrive) {  // one launch: tiles + in-launch tail by each graph's last-arriving tile
-    const int lds = conv_lds_bytes > tail_lds_bytes ? conv_lds_bytes : tail_lds_bytes;
-    if (bf16) {
-      DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_onepass_kernel<true>)));
-      hipLaunchKernelGGL(ginet_onepass_kernel<true>, dim3(plan->n_tiles), dim3(NT), lds, st, la);
-    } else {
-      DR_CHECK(dr_allow_big_lds(reinterpret_cast<const void*>(&ginet_onepass_kernel<false>)));
-      hipLaunchKernelGGL(ginet_onepass_kernel<false>, dim3(plan->n_tiles), dim3(NT), lds, st, la);
-    }
-    return (int)hipGetLastError();
-  }
   if (bf16)
     hipLaunchKernelGGL(ginet_large_conv1_bf16_kernel, dim3(plan->n_tiles), dim3(NTA), conv_lds_bytes, st, la);
   else

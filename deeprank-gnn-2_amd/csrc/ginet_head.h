@@ -80,13 +80,7 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
     float acc = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc = fmaf(t.g[part * 8 + j], fc1_row[j], acc);
-#ifdef DR_HEAD_SHFL
-    acc += __shfl_xor(acc, 1, 64);
-    acc += __shfl_xor(acc, 2, 64);
-    acc += __shfl_xor(acc, 4, 64);
-#else
-    acc = dr_sum8(acc);  // the same sums as the xor-1,2,4 shuffles, on the DPP path
-#endif
+    acc = dr_sum8(acc);  // the xor-1,2,4 butterfly sums, on the DPP path
     if (part == 0) {
       acc += fc1_bias;
       t.hpre[r] = acc;
@@ -104,11 +98,7 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
     // loss and dh steps need no workgroup barrier between them
     if (tid < 128) {
       float v = fmaf(t.hd[lane], t.fc2[lane], t.hd[lane + 64] * t.fc2[lane + 64]);
-#ifdef DR_HEAD_SHFL
-      v = dr_wave_sum(v);
-#else
       v = dr_wave_sum_dpp(v);
-#endif
       const float logit = v + t.fc2[128];
       const float d = logit - y_g;
       const float dout0 = 2.f * d * p.loss_scale;
@@ -128,11 +118,7 @@ __device__ __forceinline__ bool ginet_head(const dr_pass& p, const GinetHeadLds&
     for (int q = wave; q < OUT; q += NW) {
       const float* wr = t.fc2 + q * 128;
       float v = fmaf(t.hd[lane], wr[lane], t.hd[lane + 64] * wr[lane + 64]);
-#ifdef DR_HEAD_SHFL
-      v = dr_wave_sum(v);
-#else
       v = dr_wave_sum_dpp(v);
-#endif
       if (lane == 0) t.dout[q] = v + t.fc2[OUT * 128 + q];  // logits parked in t.dout
     }
     __syncthreads();

@@ -225,7 +225,6 @@ SIGNATURES = [
     ("dr_ginet_acc_row_floats", ctypes.c_int32, [ctypes.c_int32] * 2),
     ("dr_ginet_acc_lds_bytes", ctypes.c_int64, [_c_i32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
     ("dr_ginet_large_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(LargePlanC), ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, ctypes.c_int32, VP]),
-    ("dr_ginet_sibling_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(LargePlanC), ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, ctypes.c_int32, VP]),
     ("dr_ginet_large_conv_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 5),
     ("dr_ginet_nocluster_large_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(NcPlanC), ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), VP]),
     ("dr_nc_large_scratch_floats", ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
@@ -252,9 +251,6 @@ SIGNATURES = [
     ("dr_sgat_graph_pass", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(FoutWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, VP]),
     ("dr_sgat_lds_bytes", ctypes.c_int64, [ctypes.c_int32] * 8),
     ("dr_reduce_update", ctypes.c_int, [ctypes.POINTER(ParamTableC), VP, VP, ctypes.c_int32, ctypes.POINTER(AdamC), VP, ctypes.c_float, VP, VP]),
-    ("dr_ginet_train_step", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, ctypes.POINTER(ParamTableC), ctypes.POINTER(AdamC), VP, VP, VP]),
-    ("dr_ginet_ras_step", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, ctypes.POINTER(ParamTableC), ctypes.POINTER(AdamC), VP, VP, ctypes.c_int32, ctypes.c_float, VP]),
-    ("dr_ginet_piped_step", ctypes.c_int, [ctypes.POINTER(GraphStoreC), VP, ctypes.c_int32, ctypes.POINTER(GinetWeightsC), ctypes.POINTER(PassC), ctypes.c_int32, ctypes.POINTER(ParamTableC), ctypes.POINTER(AdamC), VP, VP, ctypes.c_int32, ctypes.c_float, ctypes.c_int32, VP]),
     ("dr_csr_from_coo", ctypes.c_int, [VP, VP, ctypes.c_int64, ctypes.c_int32, VP, VP, VP, VP, VP]),
     ("dr_spmm_csr", ctypes.c_int, [VP, VP, VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP, VP]),
     ("dr_spmm_csr_w", ctypes.c_int, [VP, VP, VP, VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, VP, VP]),

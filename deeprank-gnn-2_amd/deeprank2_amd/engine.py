@@ -2,10 +2,6 @@
 (reference ``deeprank2/trainer.py:682-690``) in two launches per mini-batch,
 for any model with a ``fused_spec`` (GINet, FoutNet).
 
-(GINet in a world of one, opt-in ``fuse_update``: both in ONE launch,
-``dr_ginet_train_step`` — extra reducer workgroups of the same grid wait for
-the graph workgroups, then reduce the partials and run Adam.)
-
 1. the model's graph pass (``dr_ginet_graph_pass`` / ``dr_fout_graph_pass``;
    FORWARD|BACKWARD, loss in-kernel): one workgroup per graph computes the
    prediction, the loss term and the whole backward of its graph, writing
@@ -33,7 +29,7 @@ import ctypes
 import torch
 
 from deeprank2_amd import _lib, layered
-from deeprank2_amd.fused import BatchHandle, launch, launch_step, param_table, slab_rows_for, step_fits
+from deeprank2_amd.fused import BatchHandle, launch, param_table, slab_rows_for
 
 
 class FusedTrainStep:
@@ -96,26 +92,9 @@ class FusedTrainStep:
         # by the all-reduced weight sum (dr_adam.grad_div)
         self.device_div = self.loss == "ce" and self.class_weights is not None and self.world > 1
         self.kernel_events = None  # list -> (start, end) HIP events around each graph pass
-        # world of one: graph pass + reduce + Adam in ONE launch where the model
-        # has it (GINet: dr_ginet_train_step; bit-identical to the two launches).
-        # Off by default: measured slower at B=64 (24.7 vs 20.6 us/step)
-        self.fuse_update = False
-        # its arrival counters (left zero); RAS: [2] timeout flag, [3] update pending, [4] finished workgroups
-        self.sync = torch.zeros(8, dtype=torch.int32, device=dev)
-        # reduce-at-start (GINet, world of one, opt-in; dr_ginet_ras_step): each
-        # launch applies the previous step's update, then runs its pass; loss_out
-        # lags one step and flush() applies the last update (sync[3]: pending)
-        self.ras = False
-        self._ras_last = None  # (B, loss scale) of the pending pass
-        # pipelined step (GINet, world of one; dr_ginet_piped_step): launch s =
-        # the update of pass s-1 (its own reducer workgroups) beside pass s,
-        # whose workgroups wait for that update only right before they read a
-        # weight; one launch per step, partials double-buffered, loss_out lags
-        # one step, flush() applies the last update.  Captured sweeps and
-        # epochs (bench.py, epoch.EpochRunner) turn it on for their steps.
-        self.piped = False
-        self._piped_last = None  # (B, loss scale) of the pending pass
-        self._piped_store = None
+        # (r03-r05 also shipped one-launch, reduce-at-start and pipelined GINet
+        # steps and a sibling split of the per-graph kernel; all measured slower
+        # than these two launches and removed in r06)
         # accumulating pass (GINet fp32, batches past the CU count;
         # dr_ginet_acc_pass): acc_groups workgroups each run every
         # acc_groups-th graph and sum the gradients on chip, one row each,
@@ -149,11 +128,9 @@ class FusedTrainStep:
             return
         f = self.model.input_shape
         dev = self.device
-        # two halves of b rows each: the pipelined step's double buffer (the
-        # other paths use the first half)
-        self.slab = torch.empty(2 * b * self.spec.slab_stride(f), dtype=torch.float32, device=dev)
-        self.head = torch.zeros(2 * b * self.spec.head_stride(self.out_dim), dtype=torch.float32, device=dev)
-        self.lpg = torch.empty(2 * b, dtype=torch.float32, device=dev)
+        self.slab = torch.empty(b * self.spec.slab_stride(f), dtype=torch.float32, device=dev)
+        self.head = torch.zeros(b * self.spec.head_stride(self.out_dim), dtype=torch.float32, device=dev)
+        self.lpg = torch.empty(b, dtype=torch.float32, device=dev)
         self.out = torch.empty(b, self.out_dim, dtype=torch.float32, device=dev)
         self._cap = b
         self._build_structs()
@@ -194,8 +171,6 @@ class FusedTrainStep:
         self._adam_off.fault = self.fault.data_ptr()
         self._adam_div = _lib.AdamC.from_buffer_copy(a)
         self._adam_div.grad_div = self.wsum.data_ptr()
-        self._adam_ras = _lib.AdamC.from_buffer_copy(a)
-        self._adam_ras.fault = None
         self._table_acc = None  # rebuilt on first use (parameters / grads may have moved)
         self._wire_packed()
 
@@ -265,13 +240,6 @@ class FusedTrainStep:
         Dropout (ginet.py:122): ``mask`` (uint8 [B,128]) if given, else the
         in-kernel hash RNG (offset = the device step counter) when ``dropout``
         and the model's p > 0."""
-        if self._piped_last is not None and (h.B > self._cap or not self._piped_fits(h)):
-            self.flush()  # the pipelined step's pending update first: the other paths reuse the partials
-        if self._ras_last is not None and (h.B > self._cap or not (self.pg is None and self.ras and self.one_launch(h) and not (self.spec.layers is not None and layered.needs_layers(self.spec, h, self.out_dim)))):
-            # reduce-at-start: this step takes another path (or regrows the
-            # partial buffers), so the pending update is applied first (the
-            # other paths overwrite the partials)
-            self.flush()
         self._ensure(h.B)
         if global_batch is None:
             global_batch = h.B * self.world
@@ -292,27 +260,6 @@ class FusedTrainStep:
         if ev is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        if self._piped_fits(h):
-            self._launch_piped(h, p, scale)
-            if ev is not None:
-                e1.record()
-                ev.append((e0, e1))
-            self._piped_last = (h.B, scale)
-            self.step_count += 1
-            return self.loss_out, self.out[: h.B]
-        if self.pg is None and self.ras and launch_step(self.spec, h, self._w, p, self._table, self._adam_ras, self.loss_out, self.sync, entry="dr_ginet_ras_step", prev=self._ras_last):
-            if ev is not None:
-                e1.record()
-                ev.append((e0, e1))
-            self._ras_last = (h.B, scale)
-            self.step_count += 1
-            return self.loss_out, self.out[: h.B]
-        if self.pg is None and self.fuse_update and launch_step(self.spec, h, self._w, p, self._table, self._adam, self.loss_out, self.sync):
-            if ev is not None:
-                e1.record()
-                ev.append((e0, e1))
-            self.step_count += 1
-            return self.loss_out, self.out[: h.B]
         rows = self._launch_pass(h, p)
         if ev is not None:
             e1.record()
@@ -428,56 +375,6 @@ class FusedTrainStep:
         self._table.slab_rows = slab_rows_for(self.spec, h)
         return self._table, self.slab.data_ptr(), h.B
 
-    def _piped_fits(self, h: BatchHandle) -> bool:
-        """The pipelined step takes this batch: GINet's per-graph kernel, one
-        process, fp32, reducers + graph workgroups co-resident."""
-        if not self.piped or self.pg is not None or self.spec.entry != "dr_ginet_graph_pass" or self.compute_dtype != "f32" or self.fuse_update or self.ras:
-            return False
-        if h.nonfinite or h.B > self._cap or h.B + self._reduce_nr() > 224:  # noqa: PLR2004
-            return False
-        return step_fits(self.spec, h, _lib.DR_DTYPE_F32, self.out_dim) and not (self.spec.layers is not None and layered.needs_layers(self.spec, h, self.out_dim))
-
-    def _reduce_nr(self):
-        """Reducer workgroups of the pipelined step (two reduce blocks of 64
-        parameter elements each, at most DR_PIPED_NR = 32 workgroups)."""
-        import os  # noqa: PLC0415
-
-        blocks = sum((p.numel() + 63) // 64 for p in self.params)
-        want = int(os.environ.get("DR_PIPED_NR", "32"))
-        return min((blocks + 1) // 2, max(want, 1))
-
-    def _launch_piped(self, h, p, scale, flush=False):
-        from deeprank2_amd.fused import lds_for  # noqa: PLC0415
-
-        prev = self._piped_last or (0, 1.0)
-        self._table.slab_rows = 1
-        lds = lds_for(self.spec, h, p.out_dim) if h is not None else 0
-        rc = _lib.load().dr_ginet_piped_step(
-            (h.store.cstruct() if h is not None else self._piped_store), None if h is None else h.descs.data_ptr(), 0 if h is None else h.B, self._w, p, lds,
-            self._table, self._adam_ras, self.loss_out.data_ptr(), self.sync.data_ptr(), prev[0], prev[1], self._cap, _lib.stream_ptr(self.device))
-        _lib.check(rc, "dr_ginet_piped_step")
-        if h is not None:
-            self._piped_store = h.store.cstruct()
-
-    def flush(self):
-        """Reduce-at-start / pipelined mode: apply the last launch's pending
-        update (the arithmetic every such launch uses) and clear the pending
-        flag; a no-op otherwise.  (Pipelined: one launch of the reducers alone,
-        no host synchronisation; capturable.)"""
-        if self._piped_last is not None:
-            p = self._pass_nodrop
-            p.loss_scale = self._piped_last[1]
-            self._launch_piped(None, p, self._piped_last[1], flush=True)
-            self._piped_last = None
-        if self._ras_last is None or int(self.sync[3].item()) == 0:
-            self._ras_last = None
-            return
-        b, scale = self._ras_last
-        self._table.slab_rows = 1
-        _lib.check(_lib.load().dr_reduce_update(self._table, self.slab.data_ptr(), self.head.data_ptr(), b, self._adam_ras, self.lpg.data_ptr(), scale, self.loss_out.data_ptr(), _lib.stream_ptr(self.device)), "dr_reduce_update")
-        self.sync[3].zero_()
-        self._ras_last = None
-
     def step_empty(self):
         """A rank whose shard of the global batch is empty (global batch smaller
         than the world): zero gradients and loss into the all-reduce, then the
@@ -506,12 +403,6 @@ class FusedTrainStep:
         same point): the per-rank counts are SUM-all-reduced first, so all ranks
         raise together instead of the faulting rank alone while the others
         block in their next collective."""
-        if (self.fuse_update or self.ras or self.piped) and int(self.sync[2].item()):
-            if reset:
-                self.sync[2].zero_()
-            msg = ("a reduce-at-start / pipelined step's hand-off gave up waiting (some workgroups ran their pass on a mix of old and new parameters)"
-                   if (self.ras or self.piped) else "a one-launch training step's reducer gave up waiting for the graph workgroups: that step's update was skipped")
-            raise RuntimeError(msg)
         if not self.handoffs:
             return
         count = self.fault[1:2].clone()
@@ -564,7 +455,6 @@ class FusedTrainStep:
     def adam_state_dict(self):
         """The fused optimizer state as ``torch.optim.Adam(model.parameters()).state_dict()``
         would hold it (parameter order = the model's ``parameters()`` order)."""
-        self.flush()
         opt = torch.optim.Adam(self.params, lr=self.lr, betas=self.betas, eps=self.eps, weight_decay=self.weight_decay)
         t = int(self.counter[0].item())
         if t > 0:
@@ -601,14 +491,13 @@ class FusedTrainStep:
 
     def _state_tensors(self):
         packed = [] if self.wpack is None else [self.wpack[0]]
-        return [*self.params, *[s for st in self.states for s in st], self.counter, self.flat, self.fault, self.sync, *packed]
+        return [*self.params, *[s for st in self.states for s in st], self.counter, self.flat, self.fault, *packed]
 
     def capture_sweep(self, handles, global_batch=None):
         """Capture one training step per handle, in order, into ONE HIP graph
         (a sweep over the resident mini-batches): replaying it runs
         len(handles) steps with a single graph launch.  Training state is
         left as before the call."""
-        self.flush()  # a pending reduce-at-start update is applied before the snapshot (the slabs are not in it)
         for h in handles:
             self._ensure(h.B)
         self._packed()  # made before the snapshot, so the restore covers it
@@ -627,34 +516,21 @@ class FusedTrainStep:
         self.step_count = n
         return g
 
-    def one_launch(self, h: BatchHandle) -> bool:
-        """True when ``step(h)`` is a single kernel launch (``dr_ginet_train_step``)."""
-        cd = _lib.DR_DTYPE_BF16 if self.compute_dtype == "bf16" else _lib.DR_DTYPE_F32
-        if self._piped_fits(h):
-            return True
-        return self.pg is None and (self.fuse_update or (self.ras and h.B <= 256)) and not h.nonfinite and step_fits(self.spec, h, cd, self.out_dim)
-
     def time_graph_pass(self, handles, n_launches, global_batch=None):
-        """Mean duration (ms) of the model's graph pass alone (or of the whole
-        step where ``one_launch``: graph pass + reduce + Adam): ``n_launches``
+        """Mean duration (ms) of the model's graph pass alone: ``n_launches``
         passes over ``handles`` (cycled) captured back to back into one HIP
         graph, replayed between two HIP events on the launch stream.  Used for
         ``roofline.achieved``; no host launch overhead enters the number (the
         rocprofv3 kernel average is the cross-check).  State is restored."""
-        self.flush()
         for h in handles:
             self._ensure(h.B)
         snap = [t.detach().clone() for t in self._state_tensors()]
         n = self.step_count
         p = self._pass if (self.spec.dropout > 0 and self.model.dropout > 0) else self._pass_nodrop
-        one = all(self.one_launch(h) for h in handles)
 
         def passes(k):
             for i in range(k):
                 h = handles[i % len(handles)]
-                if one:  # the step IS one kernel: time it whole (reduce + Adam included)
-                    self.step(h, global_batch=global_batch)
-                    continue
                 p.loss_scale = self.loss_scale(h, global_batch or h.B * self.world)
                 self._launch_pass(h, p)
 
@@ -682,12 +558,11 @@ class FusedTrainStep:
         :meth:`time_graph_pass` (``n_launches`` captured back to back, HIP
         events on the launch stream).  With the graph pass's time it splits a
         step into pass / reduce / the rest (launch gaps, host).  State is
-        restored.  None where the step has no separate reduce launch (one-launch
-        step, data-parallel step, layer-level batches)."""
-        if self.pg is not None or any(self.one_launch(h) or (self.spec.layers is not None and layered.needs_layers(self.spec, h, self.out_dim)) for h in handles):
+        restored.  None where the step has no separate reduce launch
+        (data-parallel step, layer-level batches)."""
+        if self.pg is not None or any(self.spec.layers is not None and layered.needs_layers(self.spec, h, self.out_dim) for h in handles):
             return None
         lib = _lib.load()
-        self.flush()
         for h in handles:
             self._ensure(h.B)
         snap = [t.detach().clone() for t in self._state_tensors()]
@@ -730,7 +605,6 @@ class FusedTrainStep:
         changed outside the graph between replays need a ``step()`` or
         ``refresh_packed()`` first.)  Capturing does not change the training
         state (the warm-up step it needs is rolled back)."""
-        self.flush()  # a pending reduce-at-start update is applied before the snapshot (the slabs are not in it)
         self._ensure(h.B)
         self._packed()  # made before the snapshot, so the restore covers it
         snap = [t.detach().clone() for t in self._state_tensors()]

@@ -46,7 +46,7 @@ import numpy as np
 import torch
 
 from deeprank2_amd import _lib
-from deeprank2_amd.fused import LDS_MAX, BatchHandle, lds_for, sibling_k
+from deeprank2_amd.fused import LDS_MAX, BatchHandle, lds_for
 
 
 def _static_handle(store, descs, b, max_sizes):
@@ -61,11 +61,10 @@ def _static_handle(store, descs, b, max_sizes):
     h.max_sizes = max_sizes
     h.nonfinite = False
     h._lds = {}  # noqa: SLF001
-    h.force_large = h.force_layers = h.large_onepass = h.mixed_dispatch = False
+    h.force_large = h.force_layers = False
     h.large_tile = h.vanilla_split = h.fault = None
     h.large_halos = h.large_atomic_max = h.vanilla_words = True
     h.vanilla_tile_rows = 0
-    h.sibling_split = 0
     return h
 
 
@@ -80,7 +79,7 @@ def descriptor_table(store):
 
 def eligible(step, store) -> bool:
     spec = step.spec
-    if step.compute_dtype != "f32" or spec.run is not None or step.fuse_update or step.ras:
+    if step.compute_dtype != "f32" or spec.run is not None:
         return False
     if step.pg is not None and (torch.distributed.get_backend(step.pg) != "nccl" or step.device_div):
         return False
@@ -90,17 +89,11 @@ def eligible(step, store) -> bool:
     if nf is not None and bool(np.asarray(nf).any()):
         return False
     probe = _static_handle(store, None, 1, store.max_sizes(np.arange(store.packed.n_graphs)))
-    return lds_for(spec, probe, step.out_dim) <= LDS_MAX and sibling_k(spec, probe) == 1
+    return lds_for(spec, probe, step.out_dim) <= LDS_MAX
 
 
 class EpochRunner:
     """The fused steps of one epoch's batches (sizes ``sizes``, in order) as one HIP graph."""
-
-    # GINet in a world of one: the epoch's steps as pipelined launches
-    # (FusedTrainStep.piped, dr_ginet_piped_step: each launch runs the previous
-    # step's update beside its pass; the epoch ends with the last update).
-    # Measured slower (DESIGN §5): off.
-    piped = False
 
     def __init__(self, step, store, sizes, global_sizes=None):
         self.step, self.store = step, store
@@ -126,25 +119,17 @@ class EpochRunner:
         reduce's loss pointer redirected per step: no copy launches)."""
         s = self.step
         passes = (s._pass, s._pass_nodrop)  # noqa: SLF001
-        saved = [p.out for p in passes], s.loss_out, s.piped
-        s.piped = self.piped and s.pg is None
+        saved = [p.out for p in passes], s.loss_out
         try:
             for k, (h, o, b) in enumerate(zip(self.handles, self.offs[:-1], self.sizes)):
                 for p in passes:
                     p.out = self.out[o : o + b].data_ptr()
-                # a pipelined launch reports the PREVIOUS step's loss (its
-                # reducers apply that step's update)
-                lag = s._piped_fits(h)  # noqa: SLF001
-                s.loss_out = self.loss[k - 1 : k] if (lag and k > 0) else self.loss[k : k + 1]
+                s.loss_out = self.loss[k : k + 1]
                 s.step(h, global_batch=self.global_sizes[k])
-            if s._piped_last is not None:  # noqa: SLF001  (the epoch's last update, and its loss)
-                s.loss_out = self.loss[len(self.sizes) - 1 :]
-                s.flush()
         finally:
             for p, v in zip(passes, saved[0]):
                 p.out = v
             s.loss_out = saved[1]
-            s.piped = saved[2]
 
     def _load(self, order):
         self.pin.copy_(torch.from_numpy(np.asarray(order, dtype=np.int64)))
@@ -257,7 +242,7 @@ def eval_eligible(model, store) -> bool:
     if nf is not None and bool(np.asarray(nf).any()):
         return False
     probe = _static_handle(store, None, 1, store.max_sizes(np.arange(store.packed.n_graphs)))
-    return lds_for(spec, probe, model.output_shape) <= LDS_MAX and sibling_k(spec, probe) == 1
+    return lds_for(spec, probe, model.output_shape) <= LDS_MAX
 
 
 def eval_runner_for(model, store, sizes, cache: dict):

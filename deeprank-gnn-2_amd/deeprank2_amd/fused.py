@@ -39,14 +39,11 @@ class BatchHandle:
         self.large_tile = None  # nodes per tile of the split path (default 128)
         self.large_halos = True  # stage each tile's neighbour rows in LDS (False: per-edge HBM gather)
         self.large_atomic_max = True  # depth-0 max over tiles by 64-bit atomic max (False: per-tile partials)
-        self.large_onepass = False  # split path in ONE launch: each graph's last-arriving tile runs its tail (dr_large_plan.arrive)
         self.force_layers = False  # run the layer-level path (layered.py) even when the graph pass fits (diagnostic)
         self.vanilla_words = True  # Vanilla pipeline: forward ReLU words feed the backward (False: recomputed)
         self.vanilla_split = None  # Vanilla per-graph kernel: workgroups per graph (None: by batch size)
         self.vanilla_tile_rows = VANILLA_CHUNK  # Vanilla pipeline: rows per halo-staged tile (64: the chunk-fused kernels; 16 / 32: edge kernels only; 0: untiled gathers)
         self.fault = None  # device uint32 [2] (dr_pass.fault) of the autograd path's passes, made on first use
-        self.sibling_split = 0  # GINet per-graph kernel over k workgroups per graph (0/1: off; None: by batch size)
-        self.mixed_dispatch = False  # graphs that fit LDS on the per-graph kernel, the rest on the large path (two streams; measured slower at configs[4])
 
     def lds(self, key, fn):
         """Dynamic LDS bytes for the largest graph of the batch (cached per model kind)."""
@@ -153,7 +150,7 @@ class BatchHandle:
         plan = self._lds.get(("large", out_dim, bf16, kind))
         if plan is None:
             if kind == "ginet":
-                plan = LargePlan(self, out_dim, use_halos=self.large_halos, use_atomic_max=self.large_atomic_max or self.large_onepass, bf16=bf16, onepass=self.large_onepass)
+                plan = LargePlan(self, out_dim, use_halos=self.large_halos, use_atomic_max=self.large_atomic_max, bf16=bf16)
             else:
                 plan = LargePlan(self, out_dim, use_halos=self.large_halos, use_atomic_max=True, kind=kind)
             self._lds[("large", out_dim, bf16, kind)] = plan
@@ -222,7 +219,7 @@ class LargePlan:
 
     TILE = 64  # measured best for atom-level graphs with tile halos (tools/large_tiles.py)
 
-    def __init__(self, h: BatchHandle, out_dim, tile_rows=None, use_halos=True, use_atomic_max=True, bf16=False, onepass=False, kind="ginet"):
+    def __init__(self, h: BatchHandle, out_dim, tile_rows=None, use_halos=True, use_atomic_max=True, bf16=False, kind="ginet"):
         st = h.store
         self.kind = kind
         self.TILE = int(tile_rows or h.large_tile or self.TILE)
@@ -232,8 +229,6 @@ class LargePlan:
             msg = f"a graph of the batch has {self.k0_max} depth-0 clusters (> 64): not supported by the large-graph path"
             raise RuntimeError(msg)
         tiles = (n + self.TILE - 1) // self.TILE
-        if onepass:  # every graph needs a tile workgroup to run its tail (an empty graph gets an empty tile)
-            tiles = np.maximum(tiles, 1)
         tile_first = np.concatenate([[0], np.cumsum(tiles)]).astype(np.int32)
         z_row0 = np.concatenate([[0], np.cumsum(n)]).astype(np.int32)
         tile_slot = np.repeat(np.arange(h.B, dtype=np.int32), tiles)
@@ -276,8 +271,7 @@ class LargePlan:
         c.part_arg = self.part_arg.data_ptr()
         c.halo_max = hmax
         c.part_key = self.part_key.data_ptr() if use_atomic_max else None
-        self.arrive = torch.zeros(h.B, dtype=torch.int32, device=dev) if onepass else None  # kept zero between passes
-        c.arrive = None if self.arrive is None else self.arrive.data_ptr()
+        c.arrive = None
         self.halo_tensors = None
         if halo is not None:
             _, _, hoff, hids, loff, lcol, tmem, tmptr = halo
@@ -369,9 +363,7 @@ class FusedSpec:
     layers: Callable | None = None  # (model, batch tensors, training) -> out: layer-level path (layered.py) for batches beyond LDS
     bf16: bool = False  # dr_pass.compute_dtype = DR_DTYPE_BF16 supported (runs on the large-graph path)
     attention: bool = False  # GINetConvLayer model: batches with non-finite inputs need the layer path
-    step_entry: str | None = None  # one-launch training step (graph pass + reduce + Adam), world of one
     handoffs: bool = False  # the graph pass hands rows between workgroups in-launch (dr_pass.fault can be set)
-    sibling: Callable | None = None  # (handle, weights, pass, lds, k): the per-graph kernel over k workgroups per graph
     wpack: Callable | None = None  # params -> (packed weights, dr_adam.mirror_idx, refresh()): run(..., wpack=) takes the buffer as current
 
 
@@ -442,16 +434,7 @@ def launch(spec: FusedSpec, h: BatchHandle, w, p, wpack=None):
         spec.large(h, w, p)  # the tile kernel holds the bf16 node GEMM, for every graph size
         return
     lds = lds_for(spec, h, p.out_dim)
-    if lds > LDS_MAX and spec.large is not None and not h.force_large and h.mixed_dispatch:
-        m = mixed_split(spec, h, p.out_dim)
-        if m is not None:
-            launch_mixed(spec, m, w, p)
-            return
     if lds <= LDS_MAX and not (h.force_large and spec.large is not None):
-        k = sibling_k(spec, h)
-        if k > 1:
-            spec.sibling(h, w, p, lds, k)
-            return
         fn = getattr(_lib.load(), spec.entry)
         _lib.check(fn(h.store.cstruct(), h.descs.data_ptr(), h.B, w, p, lds, _lib.stream_ptr(h.store.device)), spec.entry)
     elif spec.large is not None:
@@ -466,115 +449,6 @@ def _device_cus(device):
         return int(torch.cuda.get_device_properties(torch.device(device)).multi_processor_count)
     except (RuntimeError, AssertionError, ValueError):
         return 256
-
-
-def sibling_k(spec: FusedSpec, h: BatchHandle) -> int:
-    """Workgroups per graph for the model's per-graph kernel (spec.sibling):
-    h.sibling_split, or (None) as many as keep the grid within one workgroup
-    per compute unit, at most 4."""
-    if spec.sibling is None:
-        return 1
-    k = h.sibling_split
-    if k is None:
-        k = max(1, min(4, _device_cus(h.store.device) // max(1, ((h.B + 7) // 8) * 8)))
-    return int(k) if k and k > 1 else 1
-
-
-class SiblingPlan:
-    """dr_large_plan fields dr_ginet_sibling_pass reads: the depth-0 keys and
-    the arrival tickets (both kept zero between launches)."""
-
-    def __init__(self, h: BatchHandle):
-        st = h.store
-        idx = h.gids_host.astype(np.int64)
-        k0 = st._sizes[2][idx]  # noqa: SLF001
-        self.k0_max = max(1, int(k0.max()))
-        if self.k0_max > 64:  # noqa: PLR2004
-            msg = f"a graph of the batch has {self.k0_max} depth-0 clusters (> 64)"
-            raise RuntimeError(msg)
-        dev = st.device
-        self.key = torch.zeros(h.B * self.k0_max * 32, dtype=torch.int64, device=dev)
-        self.arrive = torch.zeros(h.B, dtype=torch.int32, device=dev)
-        c = _lib.LargePlanC()
-        c.part_key, c.arrive, c.k0_max = self.key.data_ptr(), self.arrive.data_ptr(), self.k0_max
-        self.c = c
-
-
-class MixedSplit:
-    """A batch whose graphs do not all fit one workgroup's LDS (BASELINE configs[4]:
-    residue / SRV / atom graphs together), run as two launches: the graphs that
-    fit on the model's per-graph kernel, the others on its large-graph path, on
-    two HIP streams so they overlap.  ``dr_pass.slot`` sends every graph's
-    outputs, loss term and partials to its row of the whole batch, so the
-    reduction, outputs and dropout units are those of one launch over it."""
-
-    def __init__(self, spec: FusedSpec, h: BatchHandle, out_dim, fits=None):
-        st = h.store
-        if fits is None:  # per graph: does the model's per-graph kernel hold it
-            f, alias = st.n_feat, int(st.packed.transpose_aliased)
-            idx = h.gids_host.astype(np.int64)
-            sizes = [a[idx] for a in st._sizes]  # noqa: SLF001
-            fits = np.array([spec.lds(*(int(a[i]) for a in sizes), f, alias, out_dim) <= LDS_MAX for i in range(h.B)])
-        self.valid = bool(fits.any() and not fits.all())
-        if not self.valid:
-            return
-        dev = st.device
-        self.hs, self.hl = BatchHandle(st, h.gids_host[fits]), BatchHandle(st, h.gids_host[~fits])
-        for sub in (self.hs, self.hl):
-            sub.large_tile, sub.large_halos, sub.large_atomic_max = h.large_tile, h.large_halos, h.large_atomic_max
-        self.slot_s = torch.from_numpy(np.nonzero(fits)[0].astype(np.int32)).to(dev)
-        self.slot_l = torch.from_numpy(np.nonzero(~fits)[0].astype(np.int32)).to(dev)
-        self.side = torch.cuda.Stream(device=dev)
-        self.out_dim = out_dim
-
-
-def mixed_split(spec: FusedSpec, h: BatchHandle, out_dim):
-    key = ("mixed", spec.entry, out_dim)
-    m = h._lds.get(key)  # noqa: SLF001
-    if m is None:
-        m = MixedSplit(spec, h, out_dim)
-        h._lds[key] = m  # noqa: SLF001
-    return m if m.valid else None
-
-
-def launch_mixed(spec: FusedSpec, m: MixedSplit, w, p):
-    ps, pl = _lib.PassC.from_buffer_copy(p), _lib.PassC.from_buffer_copy(p)
-    ps.slot, pl.slot = m.slot_s.data_ptr(), m.slot_l.data_ptr()
-    dev = m.hs.store.device
-    cur = torch.cuda.current_stream(dev)
-    fork, join = torch.cuda.Event(), torch.cuda.Event()
-    fork.record(cur)
-    m.side.wait_event(fork)
-    with torch.cuda.stream(m.side):  # the large graphs (tile kernel + tail)
-        spec.large(m.hl, w, pl)
-        join.record(m.side)
-    fn = getattr(_lib.load(), spec.entry)  # the graphs that fit, on the per-graph kernel
-    _lib.check(fn(m.hs.store.cstruct(), m.hs.descs.data_ptr(), m.hs.B, w, ps, lds_for(spec, m.hs, p.out_dim), _lib.stream_ptr(dev)), spec.entry)
-    cur.wait_event(join)
-
-
-def step_fits(spec: FusedSpec, h: BatchHandle, compute_dtype, out_dim) -> bool:
-    """True when ``launch_step`` runs this batch in one launch."""
-    if spec.step_entry is None or spec.run is not None or compute_dtype != _lib.DR_DTYPE_F32 or h.force_large:
-        return False
-    return lds_for(spec, h, out_dim) <= LDS_MAX
-
-
-def launch_step(spec: FusedSpec, h: BatchHandle, w, p, table, adam, loss_out, sync, entry=None, prev=None) -> bool:
-    """The model's one-launch training step (graph pass, gradient reduction
-    and Adam; ``spec.step_entry``, or ``entry``: dr_ginet_ras_step) when it has
-    one and the batch runs on its per-graph kernel; False (nothing launched)
-    otherwise."""
-    if not step_fits(spec, h, p.compute_dtype, p.out_dim):
-        return False
-    if entry == "dr_ginet_ras_step" and h.B > 256:  # noqa: PLR2004  (every workgroup co-resident)
-        return False
-    lds = lds_for(spec, h, p.out_dim)
-    fn = getattr(_lib.load(), entry or spec.step_entry)
-    extra = () if entry != "dr_ginet_ras_step" else (prev or (h.B, p.loss_scale))  # the pending pass's batch size and loss scale
-    rc = fn(h.store.cstruct(), h.descs.data_ptr(), h.B, w, p, lds, table, adam, loss_out.data_ptr(), sync.data_ptr(), *extra, _lib.stream_ptr(h.store.device))
-    _lib.check(rc, entry or spec.step_entry)
-    return True
 
 
 def run_pass(spec: FusedSpec, h: BatchHandle, params, p, w=None):

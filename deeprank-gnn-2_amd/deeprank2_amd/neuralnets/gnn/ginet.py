@@ -38,7 +38,7 @@ import torch
 from torch import nn
 
 from deeprank2_amd import _lib, layered, ops
-from deeprank2_amd.fused import BatchHandle, Dropout, FusedFn, FusedSpec, SiblingPlan, make_pass, resolve_batch, run_pass  # noqa: F401
+from deeprank2_amd.fused import BatchHandle, Dropout, FusedFn, FusedSpec, make_pass, resolve_batch, run_pass  # noqa: F401
 
 
 def _uniform(size, t):
@@ -187,16 +187,7 @@ def _large(h, w, p):
     _lib.check(rc, "dr_ginet_large_pass")
 
 
-def _sibling(h, w, p, lds, k):
-    """The per-graph kernel over k workgroups per graph (dr_ginet_sibling_pass)."""
-    plan = h._lds.get("sibling_plan")  # noqa: SLF001
-    if plan is None:
-        plan = h._lds["sibling_plan"] = SiblingPlan(h)  # noqa: SLF001
-    rc = _lib.load().dr_ginet_sibling_pass(h.store.cstruct(), h.descs.data_ptr(), h.B, plan.c, w, p, k, lds, _lib.stream_ptr(h.store.device))
-    _lib.check(rc, "dr_ginet_sibling_pass")
-
-
-SPEC = FusedSpec(PARAM_NAMES, recipe, slab_stride, head_stride, "dr_ginet_graph_pass", weights_c, _lds, dropout=0.4, large=_large, bf16=True, layers=layered.ginet_forward, attention=True, step_entry="dr_ginet_train_step", sibling=_sibling)
+SPEC = FusedSpec(PARAM_NAMES, recipe, slab_stride, head_stride, "dr_ginet_graph_pass", weights_c, _lds, dropout=0.4, large=_large, bf16=True, layers=layered.ginet_forward, attention=True)
 
 
 def graph_pass(h: BatchHandle, params, out_dim, flags, **kw):

@@ -20,7 +20,7 @@ import torch
 from torch import nn
 
 from deeprank2_amd import _lib, ops
-from deeprank2_amd.fused import LDS_MAX, BatchHandle, FusedFn, FusedSpec, MixedSplit, make_pass, resolve_batch, run_pass
+from deeprank2_amd.fused import LDS_MAX, BatchHandle, FusedFn, FusedSpec, make_pass, resolve_batch, run_pass
 
 MESSAGE = 32
 
@@ -134,22 +134,6 @@ def make_spec(f, fe):
             lds = h.lds(("vanilla_fused", fe), lambda n, e, *_: lib.dr_vanilla_fused_lds_bytes(n, e, fe))
             _lib.check(lib.dr_vanilla_fused_pass(st.cstruct(), h.descs.data_ptr(), h.B, w, p, buf.data_ptr(), offs.data_ptr(), split_k(h, f, fe), sync.data_ptr(), wpack.data_ptr(), lds, _lib.stream_ptr(st.device)), "dr_vanilla_fused_pass")
             return
-        m = _mixed_split(h, f, fe, p.out_dim) if h.mixed_dispatch and not getattr(h, "vanilla_pipeline", False) else None
-        if m is not None:  # the graphs that fit on the per-graph kernel (1 workgroup each: no hand-offs), the others on the pipeline, two streams
-            ps, pl = _lib.PassC.from_buffer_copy(p), _lib.PassC.from_buffer_copy(p)
-            ps.slot, pl.slot = m.slot_s.data_ptr(), m.slot_l.data_ptr()
-            cur = torch.cuda.current_stream(st.device)
-            fork, join = torch.cuda.Event(), torch.cuda.Event()
-            fork.record(cur)
-            m.side.wait_event(fork)
-            with torch.cuda.stream(m.side):
-                _pipeline(m.hl, w, pl)
-                join.record(m.side)
-            buf, offs, sync, wpack = m.hs.vanilla_fused_scratch()
-            lds = m.hs.lds(("vanilla_fused", fe), lambda n, e, *_: lib.dr_vanilla_fused_lds_bytes(n, e, fe))
-            _lib.check(lib.dr_vanilla_fused_pass(st.cstruct(), m.hs.descs.data_ptr(), m.hs.B, w, ps, buf.data_ptr(), offs.data_ptr(), 1, sync.data_ptr(), wpack.data_ptr(), lds, _lib.stream_ptr(st.device)), "dr_vanilla_fused_pass")
-            cur.wait_event(join)
-            return
         _pipeline(h, w, p)
 
     def packed(params):
@@ -236,23 +220,6 @@ def fused_fits(h: BatchHandle, f, fe):
         return False
     lib = _lib.load()
     return h.lds(("vanilla_fused", fe), lambda n, e, *_: lib.dr_vanilla_fused_lds_bytes(n, e, fe)) <= LDS_MAX
-
-
-def _mixed_split(h: BatchHandle, f, fe, out_dim):
-    """A batch beyond the per-graph kernel (some graph exceeds its LDS) that also
-    holds graphs it fits: those run on it, the others on the pipeline."""
-    key = ("vanilla_mixed", fe, out_dim)
-    m = h._lds.get(key)  # noqa: SLF001
-    if m is None:
-        lib = _lib.load()
-        idx = h.gids_host.astype(np.int64)
-        n, e = h.store._sizes[0][idx], h.store._sizes[1][idx]  # noqa: SLF001
-        fits = np.array([f <= 32 and fe <= FUSED_MAX_FE and lib.dr_vanilla_fused_lds_bytes(int(a), int(b), fe) <= LDS_MAX for a, b in zip(n, e)])  # noqa: PLR2004
-        m = MixedSplit(None, h, out_dim, fits=fits)
-        if m.valid:
-            m.hs.vanilla_split = 1
-        h._lds[key] = m  # noqa: SLF001
-    return m if m.valid else None
 
 
 def graph_pass(model, h: BatchHandle, params, out_dim, flags, **kw):

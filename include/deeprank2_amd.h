@@ -288,29 +288,13 @@ typedef struct dr_large_plan {
                                   max over tiles by 64-bit atomic max of (H bits << 32 | ~node), i.e.
                                   the largest value and, among equal values, the first node (H >= +0
                                   after relu, NaN never enters); replaces part_val/part_arg */
-  uint32_t* arrive;            /* optional [B], zero on entry and left zero: one launch instead of
-                                  two — each tile workgroup publishes its Z rows and partial maxima
-                                  (agent-scope stores / atomics), takes a ticket here, and the
-                                  graph's last-arriving tile runs its tail; needs part_key    */
+  uint32_t* arrive;            /* must be NULL (the one-launch form of r03-r05 was measured
+                                  slower and removed in r06; the field keeps the layout)    */
 } dr_large_plan;
 
 int dr_ginet_large_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
                         const dr_large_plan* plan, const dr_ginet_weights* w, const dr_pass* pass,
                         int32_t conv_lds_bytes, int32_t tail_lds_bytes, void* stream);
-
-/* Sibling split of dr_ginet_graph_pass for small batches (r03): `split` (1-8)
- * workgroups per graph each stage the graph, run the fused front half (Z = A X,
- * conv1 on MFMA, depth-0 pool keys) on every split-th 16-row tile, publish
- * their keys into plan->part_key ([B, k0_max, 32], zero on entry and left
- * zero) by agent-scope 64-bit atomic max, then take a ticket on
- * plan->arrive[b] (zero on entry and left zero); the last to arrive regathers
- * the Z rows at the pooling args that other workgroups computed from its own
- * staged graph and runs the tail.  No workgroup waits on another.
- * Bit-identical to dr_ginet_graph_pass; measured slower.
- * Other plan fields are ignored.                                            */
-int dr_ginet_sibling_pass(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
-                          const dr_large_plan* plan, const dr_ginet_weights* w, const dr_pass* pass, int32_t split,
-                          int32_t lds_bytes, void* stream);
 
 /* Dynamic LDS of the two launches of dr_ginet_large_pass (largest graph).  */
 int64_t dr_ginet_large_conv_lds_bytes(int32_t n_nodes, int32_t n_feat, int32_t k0, int32_t halo_max,
@@ -653,64 +637,6 @@ typedef struct dr_param_table {
 int dr_reduce_update(const dr_param_table* t, const float* slab, const float* head, int32_t n_batch,
                      const dr_adam* adam, const float* loss_per_graph, float loss_scale, float* loss_out,
                      void* stream);
-
-/* One-launch GINet training step (data-parallel world of one): the graph pass
- * above (FORWARD|BACKWARD with the fused loss), then the gradient reduction
- * over the batch and Adam, by the last min(B, 64) workgroups to finish their
- * graph inside the same launch.  Replaces the forward, loss.backward() and
- * optimizer.step() of one Trainer._epoch iteration (deeprank2/trainer.py:686-690;
- * Adam as configured at trainer.py:419) -- what dr_ginet_graph_pass followed by
- * dr_reduce_update does in two launches, with bit-identical results.
- * table / adam / loss_out: as for dr_reduce_update (adam->enabled, no grad_div,
- * adam->step_counter == pass->step_counter, at most 16 parameters, GINet's
- * slab/head strides).  sync: device uint32 [4], zero before the first call and
- * left zero by every call; sync[2] is set to 1 if a reducer ever gave up
- * waiting (never expected; the step's update is then incomplete).  */
-int dr_ginet_train_step(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
-                        const dr_ginet_weights* w, const dr_pass* pass, int32_t lds_bytes,
-                        const dr_param_table* table, const dr_adam* adam, float* loss_out, uint32_t* sync,
-                        void* stream);
-
-/* Reduce-at-start GINet step (opt-in; same arguments and checks as
- * dr_ginet_train_step, B <= 256, dr_adam.fault unset): ONE launch of B graph
- * workgroups that first applies the previous launch's gradient reduction +
- * Adam (the same fixed-order arithmetic as dr_reduce_update) while the graph
- * DMA is in flight, publishes the new parameters through a grid-wide hand-off
- * (sync[0..1], bounded wait: a give-up sets sync[2]), then runs this step's
- * graph pass.  sync[3] = 1 while a pass's partials wait for their update (set
- * by the launch's last workgroup to finish, counted in sync[4]: sync holds 5
- * uint32, zero before the first call); the last step's update is a
- * dr_reduce_update call (then zero sync[3]).
- * prev_batch / prev_loss_scale: the batch size and loss scale of the pass whose
- * update is pending.  loss_out lags one step.  Parameters after K launches +
- * that flush are bit-identical to K dr_ginet_graph_pass + dr_reduce_update
- * steps.                                                                     */
-/* Pipelined GINet step (world of one; replaces trainer.py:686-690 for one
- * mini-batch like dr_ginet_graph_pass + dr_reduce_update, one launch per step):
- * launch s runs the Adam update of pass s-1 (NR reducer workgroups, the
- * fixed-order arithmetic of dr_reduce_update, parameters stored write-through)
- * beside pass s (n_batch graph workgroups).  A pass workgroup stages its graph
- * and gathers its first tile while the reducers run, and each wave waits for
- * the published update (sync[5], bounded: a give-up sets sync[2]) only right
- * before it reads a weight.  The partials are double-buffered: slab, head and
- * loss_per_graph hold 2 x alt_rows rows; pass s writes half s & 1, its update
- * reads it in the next launch.  sync: device uint32 [8], zero when allocated
- * ([3] pending, [4] finished workgroups, [5] updates applied, [6] reducer
- * tickets).  prev_batch / prev_loss_scale: the pending update's pass.
- * n_batch 0: the update alone (the flush after the last pass).  loss_out lags
- * one launch.  Needs NR + n_batch <= 224 (NR = half the reduce blocks) and no
- * dr_pass.slot / dr_adam.fault; parameters, moments, gradients and loss terms
- * are bit-identical to the two-launch steps.                                  */
-int dr_ginet_piped_step(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
-                        const dr_ginet_weights* w, const dr_pass* pass, int32_t lds_bytes,
-                        const dr_param_table* table, const dr_adam* adam, float* loss_out, uint32_t* sync,
-                        int32_t prev_batch, float prev_loss_scale, int32_t alt_rows, void* stream);
-
-int dr_ginet_ras_step(const dr_graph_store* store, const dr_graph_desc* descs, int32_t n_batch,
-                      const dr_ginet_weights* w, const dr_pass* pass, int32_t lds_bytes,
-                      const dr_param_table* table, const dr_adam* adam, float* loss_out, uint32_t* sync,
-                      int32_t prev_batch, float prev_loss_scale, void* stream);
-
 
 /* ---- generic layer kernels (arbitrary edge lists; GINetConvLayer API) ---- */
 

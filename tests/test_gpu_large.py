@@ -137,126 +137,3 @@ def test_atom_graphs_fused_train_step_vs_oracle():
     grads = dict(zip(amd.PARAM_NAMES, step.grads))
     for n, p in model_o.named_parameters():
         assert_grad_close(grads[n].cpu().numpy(), p.grad.numpy(), err_msg=n)
-
-
-def _pass_results(store, b, out_dim, *, onepass, bf16=False, seed=3, reps=1):
-    torch.manual_seed(seed)
-    model = amd.GINet(30, out_dim, 3).to(DEV)
-    params = model.ordered_params()
-    res = []
-    for _ in range(reps):  # repeated passes: the arrival counters and keys are left zero
-        h = BatchHandle(store, np.arange(b))
-        h.large_onepass = onepass
-        out = torch.empty(b, out_dim, device=DEV)
-        slab = torch.empty(b * amd.slab_stride(30), device=DEV)
-        head = torch.zeros(b * amd.head_stride(out_dim), device=DEV)
-        lpg = torch.empty(b, device=DEV)
-        p = fused_make_pass(out_dim, bf16, loss_kind=_lib.DR_LOSS_CE if out_dim > 1 else _lib.DR_LOSS_MSE, loss_scale=1 / b, dropout=Dropout(0.4, seed=7, offset=3), out=out, loss_per_graph=lpg, slab=slab, head=head)
-        amd.SPEC.large(h, amd.weights_c(params), p)
-        torch.cuda.synchronize()
-        res.append((out.cpu(), slab.cpu(), head.cpu(), lpg.cpu()))
-    return res
-
-
-def fused_make_pass(out_dim, bf16, **kw):
-    from deeprank2_amd.fused import make_pass
-
-    p = make_pass(out_dim, _lib.DR_PASS_FORWARD | _lib.DR_PASS_BACKWARD, **kw)
-    p.compute_dtype = _lib.DR_DTYPE_BF16 if bf16 else _lib.DR_DTYPE_F32
-    return p
-
-
-@pytest.mark.parametrize("family", ["residue", "atom", "mixed"])
-@pytest.mark.parametrize("bf16", [False, True])
-def test_onepass_bit_identical_to_two_launch_split_path(family, bf16):
-    """The one-launch form (tiles hand their Z rows and partial maxima to the
-    graph's last-arriving tile, which runs the tail) gives the same bits as
-    the tile kernel + tail kernel launches, on every graph family, also when
-    run repeatedly (counters and keys left zero)."""
-    if family == "residue":
-        datas = _datas(24, seed=81)
-    elif family == "atom":
-        datas = _atoms(3, seed=82)
-    else:
-        datas = _datas(5, seed=83) + _atoms(2, seed=84) + _datas(4, seed=85, n_lo=26, n_hi=36, mean_degree=7.4, k_lo=2, k_hi=3)
-    b = len(datas)
-    store = GraphStore(pack_graphs(records_from_batch(P.Batch.from_data_list(datas))), DEV, dtype="bf16" if bf16 else "f32")
-    store.set_targets(np.arange(b) % 2)
-    two = _pass_results(store, b, 2, onepass=False, bf16=bf16)
-    one = _pass_results(store, b, 2, onepass=True, bf16=bf16, reps=3)
-    for r in one:
-        for x, y in zip(two[0], r):
-            assert torch.equal(x, y)
-
-
-def test_onepass_train_step_vs_oracle_and_capture():
-    datas = _datas(6, seed=86) + _atoms(2, seed=87)
-    torch.manual_seed(11)
-    model_o = gnn_ref.GINet(30, 1, 3)
-    model = amd.GINet(30, 1, 3)
-    model.load_state_dict(model_o.state_dict())
-    model = model.to(DEV).train()
-    mask = (torch.rand(len(datas), 128, generator=torch.Generator().manual_seed(3)) >= 0.4).float()
-    model_o.train()
-    from _util import fixed_dropout
-
-    model_o.dropout_fn = fixed_dropout(mask)
-    bat = P.Batch.from_data_list([d.clone() for d in datas])
-    out_o = model_o(bat)
-    loss_o = torch.nn.functional.mse_loss(out_o.reshape(-1), bat.y)
-    loss_o.backward()
-    h = BatchHandle(_store(datas), np.arange(len(datas)))
-    h.large_onepass = True
-    step = FusedTrainStep(model)
-    loss, out = step.step(h, mask=mask.to(torch.uint8).to(DEV))
-    np.testing.assert_allclose(out.cpu().numpy(), out_o.detach().numpy(), **TOL)
-    assert float(loss) == pytest.approx(float(loss_o.detach()), rel=1e-4)
-    grads = dict(zip(amd.PARAM_NAMES, step.grads))
-    for n, p in model_o.named_parameters():
-        assert_grad_close(grads[n].cpu().numpy(), p.grad.numpy(), err_msg=n)
-    # captured replay == eager steps
-    g = step.capture(h)
-    snap = [t.detach().clone() for t in step._state_tensors()]  # noqa: SLF001
-    g.replay()
-    g.replay()
-    torch.cuda.synchronize()
-    after_replay = [p.detach().clone() for p in step.params]
-    for t, s_ in zip(step._state_tensors(), snap):  # noqa: SLF001
-        t.data.copy_(s_)
-    step.step(h)
-    step.step(h)
-    torch.cuda.synchronize()
-    for x, y in zip(after_replay, step.params):
-        assert torch.equal(x, y)
-
-
-@pytest.mark.parametrize("split", [2, 3, 4])
-def test_sibling_split_bit_identical_to_single_workgroup_kernel(split):
-    """dr_ginet_sibling_pass: k workgroups per graph (tiles round-robin, Z rows
-    and depth-0 keys handed over, the last to arrive runs the tail) give the
-    per-graph kernel's outputs, loss terms, slab rows and head vectors bit for
-    bit, hash dropout included; the keys and tickets are left zero; a second
-    launch repeats."""
-    datas = _datas(19, seed=23)
-    store = _store(datas)
-    torch.manual_seed(5)
-    model = amd.GINet(30, 2, 3).to(DEV)
-    params = model.ordered_params()
-    store.set_targets(np.arange(19) % 2)
-    res = []
-    for k in (1, split, split):
-        h = BatchHandle(store, np.arange(19))
-        h.sibling_split = k
-        out = torch.empty(19, 2, device=DEV)
-        slab = torch.empty(19 * amd.slab_stride(30), device=DEV)
-        head = torch.zeros(19 * amd.head_stride(2), device=DEV)
-        lpg = torch.empty(19, device=DEV)
-        amd.graph_pass(h, params, 2, 3, loss_kind=_lib.DR_LOSS_CE, loss_scale=1 / 19, dropout=Dropout(0.4, seed=9, offset=2), out=out, loss_per_graph=lpg, slab=slab, head=head)
-        torch.cuda.synchronize()
-        if k > 1:
-            plan = h._lds["sibling_plan"]  # noqa: SLF001
-            assert int(plan.key.abs().sum()) == 0 and int(plan.arrive.abs().sum()) == 0
-        res.append((out.cpu(), slab.cpu(), head.cpu(), lpg.cpu()))
-    for other in res[1:]:
-        for x, y in zip(res[0], other):
-            assert torch.equal(x, y)

@@ -114,63 +114,6 @@ def test_ginet_mixed_batch_train_step_vs_oracle():
     _check_step(ginet_amd.PARAM_NAMES, step, model, model_o, out, loss, out_o, loss_o)
 
 
-@pytest.mark.parametrize("name", ["ginet", "foutnet", "sgat"])
-def test_mixed_dispatch_rows_bit_identical(name):
-    """A mixed batch runs its residue / SRV graphs on the per-graph kernel and
-    its atom graphs on the large-graph path, on two streams, each writing its
-    batch rows (dr_pass.slot): outputs, loss terms, slab rows and head vectors
-    are bit-identical to the whole batch on the large path (dispatch off; the
-    large path equals the per-graph kernel bit for bit), to the residue / SRV
-    graphs alone and to the atom graphs alone; GINet with hash dropout too
-    (units follow the batch row)."""
-    from deeprank2_amd.fused import Dropout, mixed_split
-    from deeprank2_amd.neuralnets.gnn import sgat as sgat_amd
-
-    fam_datas = _mixed({"residue": 4, "srv": 4, "atom": 2}, seed=43)
-    datas = [d for _, d in fam_datas]
-    if name == "sgat":
-        for d in datas:
-            d.edge_attr = d.edge_attr[:, :1].contiguous()
-    small = [i for i, (f, _) in enumerate(fam_datas) if f != "atom"]
-    atoms = [i for i, (f, _) in enumerate(fam_datas) if f == "atom"]
-    store = _store(datas)
-    torch.manual_seed(13)
-    mod = {"ginet": ginet_amd, "foutnet": fout_amd, "sgat": sgat_amd}[name]
-    model = {"ginet": lambda: ginet_amd.GINet(30, 2, 3), "foutnet": lambda: fout_amd.FoutNet(30, 2), "sgat": lambda: sgat_amd.SGAT(30, 2, 1)}[name]()
-    params = model.to(DEV).ordered_params()
-    ss, hs = (ginet_amd.slab_stride, ginet_amd.head_stride) if name == "ginet" else (fout_amd.slab_stride, fout_amd.head_stride)
-    store.set_targets(np.arange(len(datas)) % 2)
-
-    def run(gids, mixed=True, dropout=None):
-        h = BatchHandle(store, np.asarray(gids))
-        h.mixed_dispatch = mixed
-        b = len(gids)
-        out = torch.empty(b, 2, device=DEV)
-        lpg = torch.empty(b, device=DEV)
-        slab = torch.empty(b * ss(30), device=DEV)
-        head = torch.zeros(b * hs(2), device=DEV)
-        mod.graph_pass(h, params, 2, 3, loss_kind=_lib.DR_LOSS_CE, loss_scale=0.1, out=out, loss_per_graph=lpg, slab=slab, head=head, dropout=dropout)
-        torch.cuda.synchronize()
-        return (out.cpu(), lpg.cpu(), slab.cpu().view(b, -1), head.cpu().view(b, -1)), h
-
-    every = list(range(len(datas)))
-    on, h_on = run(every)
-    assert mixed_split(mod.SPEC, h_on, 2) is not None
-    off, _ = run(every, mixed=False)
-    for x, y in zip(on, off):
-        assert torch.equal(x, y)
-    for part in (small, atoms):
-        alone, _ = run(part)
-        for x, y in zip(on, alone):
-            assert torch.equal(x[part], y)
-    if name == "ginet":
-        drop = Dropout(0.4, seed=7, offset=3)
-        on_d, _ = run(every, dropout=drop)
-        off_d, _ = run(every, mixed=False, dropout=drop)
-        for x, y in zip(on_d, off_d):
-            assert torch.equal(x, y)
-
-
 def _vanilla_datas(counts, seed):
     out = []
     for f, d in _mixed(counts, seed):
@@ -179,10 +122,10 @@ def _vanilla_datas(counts, seed):
     return out
 
 
-@pytest.mark.parametrize("with_atoms,dispatch", [(True, False), (True, True), (False, False)])
-def test_vanilla_mixed_batch_train_step_vs_oracle(with_atoms, dispatch):
-    """dispatch: the residue / SRV graphs on the per-graph kernel, the atom
-    graphs on the pipeline, two streams, rows by dr_pass.slot."""
+@pytest.mark.parametrize("with_atoms", [True, False])
+def test_vanilla_mixed_batch_train_step_vs_oracle(with_atoms):
+    """A mixed batch with atom graphs runs on the pipeline; without, on the
+    per-graph kernel."""
     counts = {"residue": 5, "srv": 3, "atom": 2} if with_atoms else {"residue": 6, "srv": 4}
     datas = [d for _, d in _vanilla_datas(counts, seed=47)]
     torch.manual_seed(21)
@@ -195,9 +138,7 @@ def test_vanilla_mixed_batch_train_step_vs_oracle(with_atoms, dispatch):
     model.load_state_dict(model_o.state_dict())
     model = model.to(DEV).train()
     h = BatchHandle(_store(datas, clusters=False), np.arange(len(datas)))
-    h.mixed_dispatch = dispatch
     assert van_amd.fused_fits(h, 30, 3) == (not with_atoms)  # per-graph kernel only without atom graphs
-    assert (van_amd._mixed_split(h, 30, 3, 1) is not None) == with_atoms  # noqa: SLF001
     step = FusedTrainStep(model)
     loss, out = step.step(h)
     torch.cuda.synchronize()

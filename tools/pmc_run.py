@@ -1,6 +1,6 @@
 """Workload for rocprofv3 --pmc passes: eager GINet training steps (config 2).
 
-    rocprofv3 --pmc <counters> -f csv -d <dir> -- python3 tools/pmc_run.py [steps] [ginet|vanilla|foutnet|sgat][_atom|_mixed|_b<B>][_bf16]
+    rocprofv3 --pmc <counters> -f csv -d <dir> -- python3 tools/pmc_run.py [steps] [ginet|vanilla|foutnet|sgat|ginet_nocluster][_atom|_mixed|_b<B>][_bf16]
 """
 
 from __future__ import annotations
@@ -46,6 +46,10 @@ def main():
         from deeprank2_amd.neuralnets.gnn import foutnet, sgat  # noqa: PLC0415
 
         model = (sgat.SGAT(30, 1, 1) if which == "sgat" else foutnet.FoutNet(30, 1, 3)).to(dev).train()
+    elif which == "ginet_nocluster":
+        from deeprank2_amd.neuralnets.gnn import ginet_nocluster  # noqa: PLC0415
+
+        model = ginet_nocluster.GINet(30, 1, 3).to(dev).train()
     else:
         model = (VanillaNetwork if which == "vanilla" else GINet)(30, 1, 3).to(dev).train()
     step = GINetTrainStep(model, compute_dtype="bf16" if bf16 else "f32")
