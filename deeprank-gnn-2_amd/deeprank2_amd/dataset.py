@@ -163,6 +163,7 @@ class GraphDataset:
         self._gid = None
         self._y_cache = None
         self._e_cache = None
+        self._names_cache = None
 
     # ------------------------------------------------------------------ files
     def _entry(self, fname, mol):
@@ -468,6 +469,19 @@ class GraphDataset:
             return None
         return self._y_cache[torch.as_tensor(indices, dtype=torch.long)]
 
+    def targets_host(self):
+        """Every entry's target as a float32 numpy array (None without targets):
+        the host copy the trainer's exporters index, built once."""
+        if self._y_cache is None:
+            self._targets_of([])
+        return None if self._y_cache is None else self._y_cache.numpy()
+
+    def entry_names(self, indices):
+        """The entry names (``index_entries[i][1]``) at ``indices``, as a list."""
+        if self._names_cache is None:
+            self._names_cache = np.array([e[1] for e in self.index_entries], dtype=object)
+        return self._names_cache[np.asarray(indices, dtype=np.int64)].tolist()
+
     def edge_counts(self, indices):
         """Directed edge count of each graph at ``indices`` (``edge_index.shape[1]``
         as ``load_one_graph`` builds it: the stored ``_index`` rows doubled),
@@ -518,4 +532,5 @@ class GraphDataset:
         out._stores = {}
         out._y_cache = None
         out._e_cache = None
+        out._names_cache = None
         return out

@@ -108,3 +108,40 @@ def plan_shards(edges, world: int, policy: str = "auto", imbalance: float = IMBA
         return ShardPlan(tuple(contiguous), np.arange(b, dtype=np.int64), tuple(c_loads), False)
     shards, perm = shard_by_edges(pos, edges, world)
     return ShardPlan(tuple(shards), perm, tuple(int(edges[s].sum()) for s in shards), True)
+
+
+def plan_epoch(edges, sizes, world: int, policy: str = "auto", imbalance: float = IMBALANCE_LIMIT) -> list:
+    """``plan_shards`` for every global batch of an epoch at once: ``edges``
+    holds the epoch's graphs' edge counts batch after batch, ``sizes`` the
+    batch sizes.  The same plans as one ``plan_shards`` call per batch; the
+    contiguous splits and their loads are computed for all batches together
+    (one segmented sum), so only batches that need edge bin packing cost a
+    Python-level plan."""
+    edges = np.asarray(edges, dtype=np.int64)
+    sizes = np.asarray(sizes, dtype=np.int64)
+    if policy not in ("auto", "contiguous", "edges"):
+        msg = f"policy must be 'auto', 'contiguous' or 'edges' (got {policy!r})"
+        raise ValueError(msg)
+    starts = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    # contiguous cut r of batch k: rows [lo_kr, hi_kr) with lo = (b r) // world
+    cuts = (sizes[:, None] * np.arange(world + 1)[None, :]) // world  # [nb, world+1]
+    csum = np.concatenate([[0], np.cumsum(edges)])
+    loads = csum[starts[:-1, None] + cuts[:, 1:]] - csum[starts[:-1, None] + cuts[:, :-1]]  # [nb, world]
+    if policy == "edges":
+        bal = np.ones(sizes.size, bool)
+    elif policy == "contiguous" or world == 1:
+        bal = np.zeros(sizes.size, bool)
+    else:
+        bal = (sizes > 0) & (loads.max(1) > imbalance * (loads.sum(1) / world))
+    cache = {}
+    plans = []
+    for k, b in enumerate(sizes.tolist()):
+        if bal[k]:
+            plans.append(plan_shards(edges[starts[k] : starts[k + 1]], world, policy="edges"))
+            continue
+        pos = cache.get(b)
+        if pos is None:
+            ar = np.arange(b, dtype=np.int32)
+            pos = cache[b] = (tuple(shard_contiguous(ar, r, world) for r in range(world)), np.arange(b, dtype=np.int64))
+        plans.append(ShardPlan(pos[0], pos[1], tuple(int(v) for v in loads[k]), False))
+    return plans

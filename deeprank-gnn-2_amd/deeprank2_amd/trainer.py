@@ -45,7 +45,7 @@ from torch import nn
 from torch.nn.functional import softmax
 
 from deeprank2_amd.dataset import CLASSIF, REGRESS, GraphDataset
-from deeprank2_amd.distributed import plan_shards
+from deeprank2_amd.distributed import plan_epoch, plan_shards
 from deeprank2_amd.epoch import eval_runner_for, runner_for
 from deeprank2_amd.engine import FusedTrainStep
 from deeprank2_amd.io.checkpoint import load_checkpoint
@@ -350,6 +350,15 @@ class Trainer:
         plan = plan_shards(ds.edge_counts(idx), torch.distributed.get_world_size(pg), policy=self.shard_policy)
         return idx[plan.positions[torch.distributed.get_rank(pg)]], plan
 
+    def _shard_epoch(self, ds, batches):
+        """``_shard`` for every global batch of an epoch (``plan_epoch``: the
+        same plans, computed together): [(local positions, plan)]."""
+        pg = self.process_group
+        idx_all = np.concatenate([np.asarray(b) for b in batches]) if batches else np.zeros(0, np.int64)
+        plans = plan_epoch(ds.edge_counts(idx_all), [len(b) for b in batches], torch.distributed.get_world_size(pg), policy=self.shard_policy)
+        rank = torch.distributed.get_rank(pg)
+        return [(np.asarray(idx)[pl.positions[rank]], pl) for idx, pl in zip(batches, plans)]
+
     def _format_output(self, pred, target=None):
         """trainer.py:807-835."""
         if self.task == CLASSIF and target is not None:
@@ -471,7 +480,7 @@ class Trainer:
             if self.process_group is None:
                 runner = runner_for(step, store, [len(b) for b in batches], self._runners)
             else:  # this rank's shards of the epoch's global batches (every rank plans the same)
-                plans = [self._shard(ds, idx) for idx in batches]
+                plans = self._shard_epoch(ds, batches)
                 # eligibility from the plans, which every rank computes alike: a
                 # global batch leaving ANY rank an empty shard sends every rank
                 # to the loop, so the ranks' collective sequences stay matched
@@ -523,10 +532,15 @@ class Trainer:
     def _epoch_captured(self, runner, ds, batches, epoch_number, pass_name, t0, plans=None):
         """The epoch's fused steps replayed from one HIP graph: the same
         launches, losses and outputs as the per-batch loop (bit for bit), the
-        loss sum in the loop's order, one device->host copy at the end.
-        Data parallel (``plans``: this rank's shard of each global batch): the
-        per-step loss terms are summed over the ranks and the predictions
-        gathered back into global batch order, once per epoch."""
+        loss sum in the loop's order.  Data parallel (``plans``: this rank's
+        shard of each global batch): the per-step loss terms are summed over
+        the ranks and the predictions gathered back into global batch order,
+        once per epoch.
+
+        Host work overlaps the replay: the device work is queued first (the
+        replay, then the exported predictions and the loss terms into one
+        buffer), the exporters' names and targets are built from host copies
+        while it runs, and ONE device->host copy ends the epoch."""
         if plans is None:
             losses, pred = runner.run(batches)
         else:
@@ -534,9 +548,15 @@ class Trainer:
             losses = losses.clone()
             torch.distributed.all_reduce(losses, group=self.process_group)
             pred = _gather_epoch_rows(pred, [pl for _, pl in plans], self.process_group)
+        nb = len(runner.sizes)
+        exp = self._export_pred(self._format_output(pred)[0])
+        both = torch.cat([losses.reshape(-1), exp.reshape(-1)])
+        # (while the GPU runs the epoch)
         idx_all = np.concatenate([np.asarray(b) for b in batches])
-        pred, y = self._format_output(pred.clone(), self.dataset_train._targets_of(idx_all))  # noqa: SLF001
-        step_losses = losses.double().cpu().numpy()
+        names = ds.entry_names(idx_all)
+        tgt_l = self._host_targets(ds, idx_all).tolist()
+        host = both.cpu()
+        step_losses = host[:nb].double().numpy()
         loss_sum = 0.0
         # each (rank-summed) step loss is the GLOBAL batch's mean: weight it by
         # the global batch size, as the loop weights loss[0] by len(idx)
@@ -545,13 +565,51 @@ class Trainer:
         count = int(idx_all.size)
         epoch_loss = loss_sum / count if count else None
         self._fused.check_faults()
-        out_l = self._export_pred(pred).cpu().numpy().tolist()
-        tgt_l = y.detach().cpu().numpy().tolist()
-        names = [ds.index_entries[i][1] for i in idx_all]
+        out_l = host[nb:].view(exp.shape).numpy().tolist()
         dt = time() - t0
         self._output_exporters.process(pass_name, epoch_number, names, out_l, tgt_l, epoch_loss)
         _log.info(f"{pass_name} loss {epoch_loss} | time {dt}")
         return epoch_loss
+
+    def _host_targets(self, ds, idx):
+        """The targets of dataset positions ``idx`` as ``_format_output`` gives
+        them (regression: the float values; classification: class indices),
+        from a host array built once per dataset; None without targets."""
+        y = ds.targets_host()
+        if y is None:
+            return None
+        if self.task != CLASSIF:
+            return y[np.asarray(idx, dtype=np.int64)]
+        cached = getattr(ds, "_dr_class_targets", None)
+        if cached is None or cached[0] != self.classes_to_index:
+            cached = (dict(self.classes_to_index), np.array([self.classes_to_index[int(v)] for v in y.tolist()], dtype=np.int64))
+            ds._dr_class_targets = cached  # noqa: SLF001
+        return cached[1][np.asarray(idx, dtype=np.int64)]
+
+    def _eval_losses(self, pred, y, sizes):
+        """Per-batch losses of an evaluation (trainer.py:760-763:
+        ``lossfunction(pred, y)`` per mini-batch) from all its predictions at
+        once: MSELoss and CrossEntropyLoss (mean, optional class weights) in
+        float64 on host copies, with one device->host copy for the whole
+        evaluation; any other loss per batch on the device.  Returns the float
+        loss of each batch."""
+        lf = self.lossfunction
+        offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+        if isinstance(lf, nn.MSELoss) and lf.reduction == "mean" and self.task != CLASSIF:
+            p = pred.reshape(-1).astype(np.float64)
+            sq = (p - y.astype(np.float64)) ** 2
+            return [float(sq[a:b].mean()) for a, b in zip(offs[:-1], offs[1:])]
+        if isinstance(lf, nn.CrossEntropyLoss) and lf.reduction == "mean" and lf.label_smoothing == 0.0 and self.task == CLASSIF and not (y == lf.ignore_index).any():
+            z = pred.astype(np.float64)
+            m = z.max(1, keepdims=True)
+            lse = (m[:, 0] + np.log(np.exp(z - m).sum(1)))
+            nll = lse - z[np.arange(z.shape[0]), y]
+            w = np.ones(z.shape[0]) if lf.weight is None else lf.weight.detach().cpu().double().numpy()[y]
+            return [float((nll[a:b] * w[a:b]).sum() / w[a:b].sum()) for a, b in zip(offs[:-1], offs[1:])]
+        dev = self.device
+        pt = torch.as_tensor(pred, device=dev)
+        yt = torch.as_tensor(y, device=dev)
+        return [float(lf(pt[a:b].reshape(-1) if self.task != CLASSIF else pt[a:b], yt[a:b])) for a, b in zip(offs[:-1], offs[1:])]
 
     def _generic_ddp_step(self, ds, idx):
         """Any optimizer / loss outside the fused step, one process per GPU:
@@ -602,43 +660,50 @@ class Trainer:
         return pred_all, y, flat[-1]
 
     def _eval(self, loader: DataLoader, epoch_number: int, pass_name: str):
-        """trainer.py:726-795: forward passes, loss per batch on the device."""
+        """trainer.py:726-795: forward passes, then the per-batch losses and
+        the exporters.  The forward passes are one captured HIP graph where the
+        model allows it (epoch.EvalRunner), else one launch per batch; either
+        way the predictions of the whole evaluation come back in one
+        device->host copy and the per-batch losses are computed from them
+        (``_eval_losses``), while names and targets come from host arrays."""
         self.model.eval()
         dev = self.device
-        outputs, targets, names = [], [], []
-        loss_sum = torch.zeros((), dtype=torch.float64, device=dev)
-        count = 0
-        has_target = True
         t0 = time()
         batches = loader.batches()
+        ds = loader.dataset
         runner = None
         if self.capture_epochs and getattr(self.model, "fused_spec", None) is not None and self.cuda:
             # the evaluation's forward passes as one captured HIP graph (epoch.EvalRunner)
-            runner = eval_runner_for(self.model, self._targets_for_kernel(loader.dataset, dev), [len(b) for b in batches], self._runners)
-        pred_all = runner.run(batches) if runner is not None else None
-        o = 0
+            runner = eval_runner_for(self.model, self._targets_for_kernel(ds, dev), [len(b) for b in batches], self._runners)
+        sizes = [len(b) for b in batches]
         with torch.no_grad():
-            for idx in batches:
-                if pred_all is not None:
-                    pred = pred_all[o : o + len(idx)]
-                    o += len(idx)
-                    pred, y = self._format_output(pred, loader.dataset._targets_of(idx))  # noqa: SLF001
-                else:
-                    batch = loader.dataset.batch(idx).to(dev)
-                    pred = self.model(batch)
-                    pred, y = self._format_output(pred, batch.y)
-                if y is not None:
-                    loss = self.lossfunction(pred, y)
-                    loss_sum += loss.double() * pred.shape[0]
-                    count += pred.shape[0]
-                    targets.append(y)
-                else:
-                    has_target = False
-                outputs.append(self._export_pred(pred))
-                names += [loader.dataset.index_entries[i][1] for i in idx]
-        eval_loss = float(loss_sum.item()) / count if count else None
-        out_l = torch.cat(outputs).cpu().numpy().tolist() if outputs else []
-        tgt_l = torch.cat(targets).cpu().numpy().tolist() if (targets and has_target) else [None] * len(out_l)
+            if runner is not None:
+                pred_all = runner.run(batches)
+            elif batches:
+                pred_all = torch.cat([self.model(ds.batch(idx).to(dev)) for idx in batches])
+            else:
+                pred_all = torch.zeros((0, self.output_shape), dtype=torch.float32, device=dev)
+            exp = self._export_pred(self._format_output(pred_all)[0])
+            both = torch.cat([pred_all.reshape(-1), exp.reshape(-1)])
+        # (while the GPU runs the passes)
+        idx_all = np.concatenate([np.asarray(b) for b in batches]) if batches else np.zeros(0, np.int64)
+        names = ds.entry_names(idx_all)
+        y = self._host_targets(ds, idx_all)
+        if self.task == CLASSIF and y is not None:
+            self._format_output(pred_all[:0], torch.zeros(0))  # the reference's loss-type checks
+        host = both.cpu().numpy()
+        n_pred = pred_all.numel()
+        out_l = host[n_pred:].reshape(exp.shape).tolist()
+        if y is not None and len(idx_all):
+            loss_sum, count = 0.0, 0
+            for lb, n in zip(self._eval_losses(host[:n_pred].reshape(pred_all.shape), y, sizes), sizes):
+                loss_sum += lb * n
+                count += n
+            eval_loss = loss_sum / count
+            tgt_l = y.tolist()
+        else:
+            eval_loss = None
+            tgt_l = [None] * len(out_l)
         dt = time() - t0
         self._output_exporters.process(pass_name, epoch_number, names, out_l, tgt_l, eval_loss)
         _log.info(f"{pass_name} loss {eval_loss} | time {dt}")
@@ -761,11 +826,18 @@ def _gather_epoch_rows(local, plans, pg):
     bufs = [torch.empty_like(pad) for _ in range(world)]
     torch.distributed.all_gather(bufs, pad, group=pg)
     rows = torch.cat(bufs)
-    index = []
+    # segments batch-major, rank-minor: batch k's rows from rank r start at
+    # r * pad + offs[k, r]; balanced batches then take their plan's permutation
+    lens = per_rank.reshape(-1)
+    base = (np.arange(world, dtype=np.int64)[None, :] * pad.shape[0] + offs[:-1]).reshape(-1)
+    seg0 = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    index = np.repeat(base - seg0, lens) + np.arange(int(lens.sum()), dtype=np.int64)
+    b0 = 0
     for k, pl in enumerate(plans):
-        cat = np.concatenate([r * pad.shape[0] + offs[k, r] + np.arange(per_rank[k, r]) for r in range(world)])
-        index.append(cat[pl.perm] if pl.balanced else cat)
-    index = np.concatenate(index) if index else np.zeros(0, np.int64)
+        b1 = b0 + int(per_rank[k].sum())
+        if pl.balanced:
+            index[b0:b1] = index[b0:b1][pl.perm]
+        b0 = b1
     return rows[torch.as_tensor(index, dtype=torch.long, device=rows.device)]
 
 

@@ -202,6 +202,12 @@ class _EpochDS:
     def _targets_of(self, idx):
         return torch.zeros(len(idx))
 
+    def targets_host(self):
+        return np.zeros(len(self), dtype=np.float32)
+
+    def entry_names(self, idx):
+        return [self.index_entries[i][1] for i in idx]
+
     def batch_handle(self, local, dev):
         return np.asarray(local)
 
@@ -268,6 +274,8 @@ def _captured_epoch_rank_main(rank, world, port, out_path):
         _shard = T.Trainer._shard
         _format_output = T.Trainer._format_output
         _export_pred = T.Trainer._export_pred
+        _host_targets = T.Trainer._host_targets
+        _shard_epoch = T.Trainer._shard_epoch
 
     res = {}
     for name, batches in (("captured", [[0, 1, 2, 3, 4], [5, 6, 7]]), ("trailing1", [[0, 1, 2, 3, 4], [5, 6, 7], [8]])):
