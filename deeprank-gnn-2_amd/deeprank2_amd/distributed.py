@@ -135,13 +135,15 @@ def plan_epoch(edges, sizes, world: int, policy: str = "auto", imbalance: float 
         bal = (sizes > 0) & (loads.max(1) > imbalance * (loads.sum(1) / world))
     cache = {}
     plans = []
+    loads_l = loads.tolist()
+    bal_l = bal.tolist()
     for k, b in enumerate(sizes.tolist()):
-        if bal[k]:
+        if bal_l[k]:
             plans.append(plan_shards(edges[starts[k] : starts[k + 1]], world, policy="edges"))
             continue
         pos = cache.get(b)
         if pos is None:
             ar = np.arange(b, dtype=np.int32)
             pos = cache[b] = (tuple(shard_contiguous(ar, r, world) for r in range(world)), np.arange(b, dtype=np.int64))
-        plans.append(ShardPlan(pos[0], pos[1], tuple(int(v) for v in loads[k]), False))
+        plans.append(ShardPlan(pos[0], pos[1], tuple(loads_l[k]), False))
     return plans

@@ -357,7 +357,15 @@ class Trainer:
         idx_all = np.concatenate([np.asarray(b) for b in batches]) if batches else np.zeros(0, np.int64)
         plans = plan_epoch(ds.edge_counts(idx_all), [len(b) for b in batches], torch.distributed.get_world_size(pg), policy=self.shard_policy)
         rank = torch.distributed.get_rank(pg)
-        return [(np.asarray(idx)[pl.positions[rank]], pl) for idx, pl in zip(batches, plans)]
+        out = []
+        for idx, pl in zip(batches, plans):
+            pos = pl.positions[rank]
+            if pl.balanced:
+                out.append((np.asarray(idx)[pos], pl))
+            else:  # contiguous: a slice
+                lo = int(pos[0]) if len(pos) else 0
+                out.append((np.asarray(idx)[lo : lo + len(pos)], pl))
+        return out
 
     def _format_output(self, pred, target=None):
         """trainer.py:807-835."""
@@ -436,7 +444,7 @@ class Trainer:
                 self._eval(self.valid_loader, 0, "validation")
             while epoch < nepoch:
                 epoch += 1
-                self.model.train()
+                self._set_mode(True)
                 history["training"].append(self._epoch(epoch, "training"))
                 if validate:
                     history["validation"].append(self._eval(self.valid_loader, epoch, "validation"))
@@ -544,10 +552,10 @@ class Trainer:
         if plans is None:
             losses, pred = runner.run(batches)
         else:
+            # one collective per epoch: every rank's loss terms travel with its
+            # predictions, and the ranks' terms are summed in rank order
             losses, pred = runner.run([lo for lo, _ in plans])
-            losses = losses.clone()
-            torch.distributed.all_reduce(losses, group=self.process_group)
-            pred = _gather_epoch_rows(pred, [pl for _, pl in plans], self.process_group)
+            pred, losses = _gather_epoch_rows(pred, [pl for _, pl in plans], self.process_group, extra=losses)
         nb = len(runner.sizes)
         exp = self._export_pred(self._format_output(pred)[0])
         both = torch.cat([losses.reshape(-1), exp.reshape(-1)])
@@ -570,6 +578,20 @@ class Trainer:
         self._output_exporters.process(pass_name, epoch_number, names, out_l, tgt_l, epoch_loss)
         _log.info(f"{pass_name} loss {epoch_loss} | time {dt}")
         return epoch_loss
+
+    def _set_mode(self, training: bool):
+        """``model.train(training)`` (trainer.py:667 / :735 switch it per epoch
+        and evaluation): the ``training`` flag of every submodule, set directly
+        on a module list built once per model (nn.Module.train walks the tree
+        through __setattr__, ~40 us per switch for GINet)."""
+        mods = getattr(self, "_mode_modules", None)
+        if mods is None or mods[0] is not self.model:
+            mods = self._mode_modules = (self.model, list(self.model.modules()))
+        if type(self.model).train is not nn.Module.train:  # a model with its own train(): keep its semantics
+            self.model.train(training)
+            return
+        for m in mods[1]:
+            object.__setattr__(m, "training", training)
 
     def _host_targets(self, ds, idx):
         """The targets of dataset positions ``idx`` as ``_format_output`` gives
@@ -595,17 +617,18 @@ class Trainer:
         loss of each batch."""
         lf = self.lossfunction
         offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+        sizes_a = np.asarray(sizes, dtype=np.float64)
         if isinstance(lf, nn.MSELoss) and lf.reduction == "mean" and self.task != CLASSIF:
             p = pred.reshape(-1).astype(np.float64)
             sq = (p - y.astype(np.float64)) ** 2
-            return [float(sq[a:b].mean()) for a, b in zip(offs[:-1], offs[1:])]
+            return (np.add.reduceat(sq, offs[:-1]) / sizes_a).tolist() if sq.size else []
         if isinstance(lf, nn.CrossEntropyLoss) and lf.reduction == "mean" and lf.label_smoothing == 0.0 and self.task == CLASSIF and not (y == lf.ignore_index).any():
             z = pred.astype(np.float64)
             m = z.max(1, keepdims=True)
             lse = (m[:, 0] + np.log(np.exp(z - m).sum(1)))
             nll = lse - z[np.arange(z.shape[0]), y]
             w = np.ones(z.shape[0]) if lf.weight is None else lf.weight.detach().cpu().double().numpy()[y]
-            return [float((nll[a:b] * w[a:b]).sum() / w[a:b].sum()) for a, b in zip(offs[:-1], offs[1:])]
+            return (np.add.reduceat(nll * w, offs[:-1]) / np.add.reduceat(w, offs[:-1])).tolist() if nll.size else []
         dev = self.device
         pt = torch.as_tensor(pred, device=dev)
         yt = torch.as_tensor(y, device=dev)
@@ -666,7 +689,7 @@ class Trainer:
         way the predictions of the whole evaluation come back in one
         device->host copy and the per-batch losses are computed from them
         (``_eval_losses``), while names and targets come from host arrays."""
-        self.model.eval()
+        self._set_mode(False)
         dev = self.device
         t0 = time()
         batches = loader.batches()
@@ -707,7 +730,7 @@ class Trainer:
         dt = time() - t0
         self._output_exporters.process(pass_name, epoch_number, names, out_l, tgt_l, eval_loss)
         _log.info(f"{pass_name} loss {eval_loss} | time {dt}")
-        self.model.train()
+        self._set_mode(True)
         return eval_loss
 
     def test(self, batch_size: int = 32, num_workers: int = 0):
@@ -812,24 +835,23 @@ def _gather_rows(local, plan, pg):
     return rows
 
 
-def _gather_epoch_rows(local, plans, pg):
+def _gather_epoch_rows(local, plans, pg, extra=None):
     """``_gather_rows`` for a whole epoch at once: ``local`` holds this rank's
     rows of every batch, batch after batch; one all-gather (padded to the
     largest rank) and one index gather put every batch's rows back in its
-    global order, batch after batch."""
+    global order, batch after batch.  ``extra`` (optional, [n] floats: the
+    epoch's per-step loss terms) travels in the same all-gather and comes back
+    summed over the ranks in rank order: returns (rows, summed extra).  No
+    host synchronisation (the index goes up from pinned memory)."""
     world = torch.distributed.get_world_size(pg)
     per_rank = np.array([pl.sizes() for pl in plans], dtype=np.int64).reshape(len(plans), world)  # [batch, rank]
     offs = np.concatenate([np.zeros((1, world), np.int64), np.cumsum(per_rank, 0)])  # each rank's row offset of each batch
     top = int(offs[-1].max()) if len(plans) else 0
-    pad = torch.zeros(max(top, 1), local.shape[1], dtype=local.dtype, device=local.device)
-    pad[: local.shape[0]] = local
-    bufs = [torch.empty_like(pad) for _ in range(world)]
-    torch.distributed.all_gather(bufs, pad, group=pg)
-    rows = torch.cat(bufs)
+    rows_n = max(top, 1)
     # segments batch-major, rank-minor: batch k's rows from rank r start at
-    # r * pad + offs[k, r]; balanced batches then take their plan's permutation
+    # r * rows_n + offs[k, r]; balanced batches then take their plan's permutation
     lens = per_rank.reshape(-1)
-    base = (np.arange(world, dtype=np.int64)[None, :] * pad.shape[0] + offs[:-1]).reshape(-1)
+    base = (np.arange(world, dtype=np.int64)[None, :] * rows_n + offs[:-1]).reshape(-1)
     seg0 = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
     index = np.repeat(base - seg0, lens) + np.arange(int(lens.sum()), dtype=np.int64)
     b0 = 0
@@ -838,7 +860,25 @@ def _gather_epoch_rows(local, plans, pg):
         if pl.balanced:
             index[b0:b1] = index[b0:b1][pl.perm]
         b0 = b1
-    return rows[torch.as_tensor(index, dtype=torch.long, device=rows.device)]
+    index_t = torch.from_numpy(index)
+    if local.is_cuda:
+        index_t = index_t.pin_memory().to(local.device, non_blocking=True)
+    c = local.shape[1]
+    nx = 0 if extra is None else int(extra.numel())
+    flat = torch.zeros(rows_n * c + nx, dtype=local.dtype, device=local.device)
+    flat[: local.numel()] = local.reshape(-1)
+    if nx:
+        flat[rows_n * c :] = extra.reshape(-1)
+    bufs = [torch.empty_like(flat) for _ in range(world)]
+    torch.distributed.all_gather(bufs, flat, group=pg)
+    summed = None
+    if nx:
+        summed = bufs[0][rows_n * c :].clone()
+        for r in range(1, world):
+            summed += bufs[r][rows_n * c :]
+    rows = torch.cat([bf[: rows_n * c].view(rows_n, c) for bf in bufs])
+    out = rows[index_t]
+    return out if extra is None else (out, summed)
 
 
 def _divide_dataset(dataset, splitsize=None, process_group=None):
