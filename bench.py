@@ -883,7 +883,7 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
                 "mfma": mfma,
                 "wallclock": {"bytes_per_step": int(alg + adam_bytes), "achieved": round(wall_gbs, 2), "frac": round(wall_gbs / HBM_PEAK_GBS, 5), "note": "B_alg(step) = sum_g B_alg(g) + 28*P (Adam fp32) over ms_per_step"},
             },
-            "step_split_us": None if reduce_ms is None else {"graph_pass": round(kernel_ms * 1e3, 2), "reduce_adam": round(reduce_ms * 1e3, 2), "other": round(ms_step * 1e3 - (kernel_ms + reduce_ms) * 1e3, 2), "note": "graph pass and dr_reduce_update each timed alone (HIP events around a HIP graph of --steps launches); other = ms_per_step minus both: the gaps between launches in the replayed step graphs"},
+            "step_split_us": None if reduce_ms is None else {"graph_pass": round(kernel_ms * 1e3, 2), "reduce_adam": round(reduce_ms * 1e3, 2), "other": round(ms_step * 1e3 - (kernel_ms + reduce_ms) * 1e3, 2), "note": "graph pass and dr_reduce_update each timed alone (HIP events around a HIP graph of max(--steps, 200) launches); other = ms_per_step minus both: the gaps between launches in the replayed step graphs"},
             "launch": ("eager" + capture_note) if captured is None else f"hipgraph-replay ({n_sweeps} x {len(handles)}-step sweep graph + " + (f"one {n_rest}-step graph" if rest is not None else f"{n_rest} per-step graphs") + f"{', RCCL all-reduce captured' if pg is not None else ''})",
             "cpu_baseline": cpu,
             "final_loss": float(loss.item()),
