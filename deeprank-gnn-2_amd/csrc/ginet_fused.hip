@@ -1154,7 +1154,13 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const AccCtx&
 
 template <int KPT>
 __global__ void __launch_bounds__(NT) ginet_graph_kernel(GinetArgs a) {
+#ifdef DR_STAMPS  // cross-kernel timeline (s_memrealtime, 100 MHz chip clock): slots 30 / 31 = entry / exit
+  if (threadIdx.x == 0 && a.p.stamps) a.p.stamps[(int64_t)blockIdx.x * 32 + 30] = __builtin_amdgcn_s_memrealtime();
+#endif
   graph_body<KPT>(a, AccCtx{});
+#ifdef DR_STAMPS
+  if (threadIdx.x == 0 && a.p.stamps) a.p.stamps[(int64_t)blockIdx.x * 32 + 31] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 // ---------------------------------------------------------------------------
