@@ -25,11 +25,10 @@ constexpr int RC = 8;   // batch chunks per element
 constexpr int RU = 8;   // batch rows per chunk issued together (predicated)
 constexpr int RU2 = 24; // then the rest of a chunk, this many at a time
 constexpr int RT = RP * RC;  // threads per block
-// Outer-product blocks (DR_GRAD_OUTER, e.g. fc1.weight = sum_b dh_b g_b^T):
-// R = RT / cols rows of the parameter per block, the batch's two head-vector
-// slices staged once in LDS ([B][R] and [B][cols]) instead of every element
-// loading its own 2 x B partials (at B = 64: 1 M dword loads -> 74 K for
-// GINet's fc1.weight; those loads were the reduce's critical path, 1.5 us of
+// Outer-product blocks (DR_GRAD_OUTER, e.g. fc1.weight = sum_b dh_b g_b^T)
+// stage the head slices they read in LDS first (reduce_outer_block): at B =
+// 64 GINet's fc1.weight took 1 M dword loads from 128 blocks (16 K
+// wave-level loads, 128 per CU: the reduce's critical path, ~1.5 us of
 // address processing, tools/step_timeline.py).  Up to this many LDS floats:
 constexpr int OUTER_LDS_FLOATS = 12288;
 constexpr uint8_t BLK_OUTER = 0x80;  // blk_param flag: the block is an outer-product block
@@ -255,53 +254,70 @@ __device__ __forceinline__ void reduce_block(const ReduceHdr& h, const ParamRec&
   RDSTAMP(4);
 }
 
-// One outer-product block: rows [i0, i0 + R) of a DR_GRAD_OUTER parameter
-// (grad[i][j] = sum_b head[b][off1 + i] head[b][off2 + j], R = RT / cols),
-// one element per thread; the block first stages U = head[:, off1 + i0 ..]
-// ([B][R]) and W = head[:, off2 ..] ([B][cols]) in LDS (sm), then sums in the
-// fixed order of reduce_block (RC chunks of rows, each from zero, fmaf(u, w),
-// then the chunks in order), so the gradients are the same bits as there.
-// Needs partials (h.slab set) and B * (R + cols) <= OUTER_LDS_FLOATS.
+// One outer-product block: RP consecutive elements from e0 of a
+// DR_GRAD_OUTER parameter (grad[i][j] = sum_b head[b][off1 + i] head[b][off2 + j]),
+// RC batch chunks per element as in reduce_block.  The block first stages the
+// head slices its elements read — U = head[:, off1 + rows of the block]
+// ([rows][B]) and W = head[:, off2 + columns of the block] ([B][cols]),
+// 16-byte loads where aligned — in LDS (sm) with a few loads per thread,
+// instead of every thread loading 2 x B/RC scattered partials: the same
+// products, sums and order as reduce_block, so the same bits.  Needs partials
+// (h.slab set) and B * (columns + rows) <= OUTER_LDS_FLOATS - RC * RP.
 __device__ __forceinline__ void reduce_outer_block(const ReduceHdr& h, const ParamRec& r, int e0, bool first, int t,
                                                    float* sm, int64_t tstep) {
-  const int cols = r.cols, R = RT / cols;
-  const int i0 = e0 / cols, nrow = min(R, r.numel / cols - i0);
-  const int li = t / cols, j = t - li * cols;
-  const bool live = li < nrow;
-  const int e = e0 + t;
+  const int lp = t % RP, ch = t / RP;
+  const int cols = r.cols, e = e0 + lp;
+  const int elast = min(e0 + RP, r.numel) - 1;
+  const bool live = e < r.numel;
   const uint32_t fv = h.fault ? *h.fault : 0u;
   const bool bad = fv != 0u;
-  const ElemState s = load_state(h, r, live ? e : e0, live);
+  const ElemState s = load_state(h, r, live ? e : e0, ch == 0 && live);
   reduce_loss(h, first, t, bad);
-  const int nb = h.B;
+  const int ir0 = e0 / cols, ir1 = elast / cols;  // the block's rows
+  const int jlo = ir0 == ir1 ? e0 - ir0 * cols : 0, jn = ir0 == ir1 ? elast - e0 + 1 : cols;  // its columns
+  const int nr = ir1 - ir0 + 1, nb = h.B;
   const int64_t st = h.head_stride;
-  float* sU = sm;
-  float* sW = sm + nb * R;
-  for (int p = t; p < nb * R; p += RT) {
-    const int b = p / R, ii = p - b * R;
-    sU[p] = ii < nrow ? h.head[b * st + r.off1 + i0 + ii] : 0.f;
+  float* part = sm;                  // [RC][RP]
+  float* sU = sm + RC * RP;          // [nr][nb]
+  float* sW = sU + nr * nb;          // [nb][jn]
+  const float* wsrc = h.head + r.off2 + jlo;
+  if (((r.off2 + jlo) & 3) == 0 && (jn & 3) == 0 && (st & 3) == 0) {
+    const int q = jn >> 2;
+    for (int p = t; p < nb * q; p += RT) {
+      const int b = p / q, c4 = p - b * q;
+      *reinterpret_cast<float4*>(sW + b * jn + 4 * c4) = *reinterpret_cast<const float4*>(wsrc + b * st + 4 * c4);
+    }
+  } else {
+    for (int p = t; p < nb * jn; p += RT) {
+      const int b = p / jn, jj = p - b * jn;
+      sW[p] = wsrc[b * st + jj];
+    }
   }
-  for (int p = t; p < nb * cols; p += RT) {
-    const int b = p / cols, jj = p - b * cols;
-    sW[p] = h.head[b * st + r.off2 + jj];
+  for (int p = t; p < nr * nb; p += RT) {
+    const int ii = p / nb, b = p - ii * nb;
+    sU[p] = h.head[b * st + r.off1 + ir0 + ii];
+  }
+  __syncthreads();
+  {
+    const int ec = live ? e : e0;
+    const int ii = ec / cols - ir0, jj = ec % cols - jlo;
+    const int b0 = (nb * ch) / RC, b1 = (nb * (ch + 1)) / RC;
+    float acc = 0.f;
+    for (int b = b0; b < b1; ++b) acc = fmaf(sU[ii * nb + b], sW[b * jn + jj], acc);
+    part[ch * RP + lp] = acc;
   }
   RDSTAMP(1);
   __syncthreads();
   RDSTAMP(2);
-  if (!live) return;
-  const uint32_t tk = take_ticket(h, t == 0, fv);
+  if (ch != 0 || !live) return;
+  const uint32_t tk = take_ticket(h, lp == 0, fv);
   float gsum = 0.f;
 #pragma unroll
-  for (int ch = 0; ch < RC; ++ch) {
-    const int b0 = (nb * ch) / RC, b1 = (nb * (ch + 1)) / RC;
-    float acc = 0.f;
-    for (int b = b0; b < b1; ++b) acc = fmaf(sU[b * R + li], sW[b * cols + j], acc);
-    gsum += acc;
-  }
+  for (int k = 0; k < RC; ++k) gsum += part[k * RP + lp];
   if (bad) gsum = __builtin_nanf("");
   if (r.grad) r.grad[e] = gsum;
-  adam_element(h, r, e, gsum, s, h.adam_enabled && !bad, first && t == 0, tstep);
-  last_ticket(h, t == 0, tk);
+  adam_element(h, r, e, gsum, s, h.adam_enabled && !bad, first && lp == 0, tstep);
+  last_ticket(h, lp == 0, tk);
   RDSTAMP(3);
 #ifdef DR_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -312,8 +328,10 @@ __device__ __forceinline__ void reduce_outer_block(const ReduceHdr& h, const Par
 // Host: whether parameter i of the table reduces in outer-product blocks
 inline bool outer_blocks(const dr_param_table* t, int i, const float* slab, int32_t n_batch) {
   const dr_grad_recipe r = t->recipe[i];
-  if (r.kind != DR_GRAD_OUTER || !slab || r.cols <= 0 || r.cols > RT || t->numel[i] % r.cols) return false;
-  return (int64_t)n_batch * (RT / r.cols + r.cols) <= OUTER_LDS_FLOATS;
+  if (r.kind != DR_GRAD_OUTER || !slab || r.cols <= 0) return false;
+  // the widest block: RP columns of one row, or every column of RP / cols + 2 rows
+  const int64_t cols = r.cols >= RP ? RP : r.cols, rows = r.cols >= RP ? 2 : RP / r.cols + 2;
+  return (int64_t)n_batch * (cols + rows) <= OUTER_LDS_FLOATS - RC * RP;
 }
 
 // Host: header + records from the C-ABI table and Adam settings; the block
@@ -377,8 +395,7 @@ inline int build_reduce(const dr_param_table* t, const float* slab, const float*
     mbase += t->numel[i];
     h.blk0[i] = (int16_t)blocks;
     const bool ob = outer_blocks(t, i, slab, n_batch);
-    const int step = ob ? (RT / r.cols) * r.cols : RP;  // elements per block
-    for (int e0 = 0; e0 < t->numel[i]; e0 += step, ++blocks) {
+    for (int e0 = 0; e0 < t->numel[i]; e0 += RP, ++blocks) {
       if (blocks >= max_blocks) return DR_E_UNSUPPORTED;
       blk_param[blocks] = (uint8_t)(i | (ob ? BLK_OUTER : 0));
       blk_elem[blocks] = (uint16_t)e0;
