@@ -16,25 +16,24 @@ namespace {
 
 using drr::RP;
 using drr::RT;
-#define DR_REDUCE_MAX_BLOCKS 512  // 32 K parameter elements in row-partial blocks (GINet at F=64: ~11.5 K)
+#define DR_REDUCE_MAX_BLOCKS 512  // 32 K parameter elements (GINet at F=64: ~11.5 K)
 
 struct alignas(64) ReduceArgs {
   drr::ReduceHdr h;
   drr::ParamRec rec[DR_MAX_PARAMS];
-  // 1-D grid: block -> (parameter | BLK_OUTER, first element); blocks never straddle two parameters
+  // 1-D grid: block -> (parameter, first element); blocks never straddle two parameters
   uint8_t blk_param[DR_REDUCE_MAX_BLOCKS];
-  uint16_t blk_elem[DR_REDUCE_MAX_BLOCKS];
+  uint16_t blk_elem[DR_REDUCE_MAX_BLOCKS];  // first element / RP
 };
 
-// 1-D grid: block j reduces a run of parameter blk_param[j]'s elements from
-// blk_elem[j]: RP of them in row-partial blocks, or whole rows of an
-// outer-product parameter (BLK_OUTER).  Its record and the header are scalar
-// loads from the kernel arguments.
+// 1-D grid over sum_p ceil(numel_p / RP) blocks: block j reduces RP
+// consecutive elements of parameter blk_param[j].  Its record and the header
+// are scalar loads from the kernel arguments.
 __global__ void __launch_bounds__(RT) reduce_adam_kernel(ReduceArgs a) {
-  __shared__ __attribute__((aligned(16))) float sm[drr::OUTER_LDS_FLOATS];
+  __shared__ float part[drr::RC][RP];
   RDSTAMP(0);
-  const int bp = a.blk_param[blockIdx.x];
-  const drr::ParamRec r = a.rec[bp & 0x7f];
+  const int pi = a.blk_param[blockIdx.x];
+  const drr::ParamRec r = a.rec[pi];
   // Pull every kernel-argument line this block uses in one scalar round trip
   // (hipcc would otherwise issue them lazily, one wait each).
   {
@@ -45,11 +44,7 @@ __global__ void __launch_bounds__(RT) reduce_adam_kernel(ReduceArgs a) {
   }
   RDSTAMP(5);  // (stamps build: the block's kernel-argument record is in)
   const int64_t tstep = (a.h.step_counter && a.h.adam_enabled) ? a.h.step_counter[1] + 1 : 0;
-  const int e0 = a.blk_elem[blockIdx.x];
-  if (bp & drr::BLK_OUTER)
-    drr::reduce_outer_block(a.h, r, e0, blockIdx.x == 0, threadIdx.x, sm, tstep);
-  else
-    drr::reduce_block(a.h, r, e0 / RP, blockIdx.x == 0, threadIdx.x, reinterpret_cast<float(*)[RP]>(sm), tstep);
+  drr::reduce_block<0>(a.h, r, a.blk_elem[blockIdx.x], blockIdx.x == 0, threadIdx.x, part, tstep);
 }
 
 }  // namespace
@@ -59,9 +54,15 @@ extern "C" int dr_reduce_update(const dr_param_table* t, const float* slab, cons
                                 void* stream) {
   ReduceArgs a;
   std::memset(&a, 0, sizeof(a));
-  const int blocks = drr::build_reduce(t, slab, head, n_batch, adam, loss_per_graph, loss_scale, loss_out, a.h, a.rec,
-                                       a.blk_param, a.blk_elem, DR_REDUCE_MAX_BLOCKS);
+  const int blocks = drr::build_reduce(t, slab, head, n_batch, adam, loss_per_graph, loss_scale, loss_out, a.h, a.rec);
   if (blocks < 0) return blocks;
+  if (blocks > DR_REDUCE_MAX_BLOCKS) return DR_E_UNSUPPORTED;
+  int j = 0;
+  for (int i = 0; i < t->n_params; ++i)
+    for (int x = 0; x * RP < t->numel[i]; ++x, ++j) {
+      a.blk_param[j] = (uint8_t)i;
+      a.blk_elem[j] = (uint16_t)x;
+    }
   if (blocks == 0) return DR_OK;
   hipLaunchKernelGGL(reduce_adam_kernel, dim3(blocks), dim3(RT), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();

@@ -1,13 +1,13 @@
 // Gradient reduction over the batch + Adam for one block of parameter
-// elements (the stand-alone reduce kernel, reduce_adam.hip).
+// elements (the stand-alone reduce kernel, reduce_adam.hip; the r03-r05
+// one-launch GINet steps that also ran it are gone).  r06 measured and did
+// not keep blocks that stage their partials in LDS first (outer products and
+// row sums): 3.9 vs 3.5 us per launch, the load -> LDS -> barrier -> sum
+// chain is longer than the direct loads (profiles/r06/not_kept/).
 //
 // Replaces loss_.backward()'s accumulation over the batch and
 // optimizer.step() of Trainer._epoch (deeprank2/trainer.py:689-690; Adam
-// configured at trainer.py:419).  Every gradient element is a sum over the
-// per-graph partials in a fixed order — RC chunks of consecutive batch rows,
-// each summed in row order from zero, then the chunks in order — so the
-// result is deterministic (no float atomics) and the same whichever block
-// form below computes it.
+// configured at trainer.py:419).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -20,18 +20,11 @@
 
 namespace drr {
 
-constexpr int RP = 64;  // parameter elements per block (row-partial blocks)
-constexpr int RC = 8;   // batch chunks per element
+constexpr int RP = 64;  // parameter elements per block
+constexpr int RC = 8;   // batch chunks per block
 constexpr int RU = 8;   // batch rows per chunk issued together (predicated)
 constexpr int RU2 = 24; // then the rest of a chunk, this many at a time
 constexpr int RT = RP * RC;  // threads per block
-// Outer-product blocks (DR_GRAD_OUTER, e.g. fc1.weight = sum_b dh_b g_b^T)
-// stage the head slices they read in LDS first (reduce_outer_block): at B =
-// 64 GINet's fc1.weight took 1 M dword loads from 128 blocks (16 K
-// wave-level loads, 128 per CU: the reduce's critical path, ~1.5 us of
-// address processing, tools/step_timeline.py).  Up to this many LDS floats:
-constexpr int OUTER_LDS_FLOATS = 12288;
-constexpr uint8_t BLK_OUTER = 0x80;  // blk_param flag: the block is an outer-product block
 
 // One 64-byte kernel-argument line per parameter: a block fetches everything
 // it needs about its parameter with one scalar load.
@@ -57,13 +50,15 @@ struct alignas(64) ReduceHdr {
   float lr, beta1, beta2, eps, weight_decay, bias_c1, bias_c2_sqrt, pad1;
   float log2_beta1, log2_beta2;  // beta^t = exp2(t log2 beta): one v_exp_f32, not powf
   int32_t n_params, n_blocks;
-  int16_t blk0[DR_MAX_PARAMS + 1];  // first block of each parameter, blk0[n_params] = n_blocks
+  int16_t blk0[DR_MAX_PARAMS + 1];  // first block of each parameter (prefix sums of ceil(numel / RP)), blk0[n_params] = n_blocks
   int32_t slab_rows;  // slab rows per graph (>= 1): a slab-kind gradient sums B * slab_rows rows
   float* mirror;            // dr_adam.mirror / mirror_idx: packed copies of updated elements
   const int4* mirror_idx;
-  uint32_t* fault_clear;    // dr_adam.fault_clear / ticket
+  uint32_t* fault_clear;    // dr_adam.fault_clear / ticket (stand-alone reduce kernel only)
   uint32_t* ticket;
 };
+
+typedef __attribute__((address_space(1))) unsigned int gu32r;
 
 // Diagnostic timeline (stamps build only, dr_debug_reduce_stamps): thread 0
 // of block j writes s_memrealtime (100 MHz chip clock) at point i to
@@ -83,81 +78,16 @@ __device__ int64_t g_reduce_stamps[4096 * 8];
   } while (0)
 #endif
 
-// The loss: loss_out[0] = loss_scale * sum(loss_per_graph) (lane-strided
-// partial sums, then a fixed-order wave reduction), by the first 64 threads
-// of block 0; NaN after a faulted pass.
-__device__ __forceinline__ void reduce_loss(const ReduceHdr& h, bool first, int t, bool bad) {
-  if (first && t < 64 && h.lpg && h.loss_out) {
-    float acc = 0.f;
-    for (int b = t; b < h.B; b += 64) acc += h.lpg[b];
-    acc = dr_wave_sum(acc);
-    if (t == 0) h.loss_out[0] = bad ? __builtin_nanf("") : acc * h.loss_scale;
-  } else if (bad && first && t == 0 && h.loss_out) {
-    h.loss_out[0] = __builtin_nanf("");
-  }
-}
-
-// Element e's Adam state (and its dr_adam.mirror slots), loaded up front so
-// the loads leave ahead of the partials'
-struct ElemState {
-  float p0 = 0.f, m0 = 0.f, v0 = 0.f;
-  int4 mi = make_int4(-1, -1, -1, -1);
-};
-__device__ __forceinline__ ElemState load_state(const ReduceHdr& h, const ParamRec& r, int ec, bool want) {
-  ElemState s;
-  if (want && h.adam_enabled && r.numel > 0) {  // numel 0: an empty record (no pointers)
-    s.p0 = r.param[ec];
-    s.m0 = r.m[ec];
-    s.v0 = r.v[ec];
-    if (h.mirror) s.mi = h.mirror_idx[r.mbase + ec];
-  }
-  return s;
-}
-
-// Element e with its gradient gsum (from the partials): the gradient store,
-// then torch.optim.Adam's update
-__device__ __forceinline__ void adam_element(const ReduceHdr& h, const ParamRec& r, int e, float gsum, const ElemState& s,
-                                             bool upd, bool counter_lane, int64_t tstep) {
-  if (!upd) return;
-  float bc1 = h.bias_c1, bc2s = h.bias_c2_sqrt;
-  if (h.step_counter) {  // step and bias corrections from the device counter
-    bc1 = 1.f - exp2f((float)tstep * h.log2_beta1);
-    bc2s = sqrtf(1.f - exp2f((float)tstep * h.log2_beta2));
-    if (counter_lane) h.step_counter[0] = tstep;
-  }
-  float gr = gsum;
-  if (h.weight_decay != 0.f) gr = fmaf(h.weight_decay, s.p0, gr);
-  // torch.optim.Adam: exp_avg.lerp_(g, 1-b1); exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
-  // every product-sum spelled out (fmaf / __fmul_rn / __fadd_rn): contraction
-  // is then the same in every block form that inlines this
-  const float mv = fmaf(1.f - h.beta1, __fsub_rn(gr, s.m0), s.m0);
-  const float vv = fmaf(__fmul_rn(1.f - h.beta2, gr), gr, __fmul_rn(s.v0, h.beta2));
-  r.m[e] = mv;
-  r.v[e] = vv;
-  const float denom = __fadd_rn(__fdiv_rn(sqrtf(vv), bc2s), h.eps);
-  const float pn = fmaf(-(h.lr / bc1), __fdiv_rn(mv, denom), s.p0);
-  r.param[e] = pn;
-  if (h.mirror) {
-    if (s.mi.x >= 0) h.mirror[s.mi.x] = pn;
-    if (s.mi.y >= 0) h.mirror[s.mi.y] = pn;
-    if (s.mi.z >= 0) h.mirror[s.mi.z] = pn;
-    if (s.mi.w >= 0) h.mirror[s.mi.w] = pn;
-  }
-}
-
-// dr_adam.fault_clear: one lane of each block takes a ticket once its read of
-// the flag has returned; the last block's lane clears the flag (every block
-// has read it by then) for the next graph pass
-__device__ __forceinline__ uint32_t take_ticket(const ReduceHdr& h, bool lane, uint32_t fv) {
-  if (!(lane && h.fault_clear)) return 0u;
-  asm volatile("" ::"v"(fv) : "memory");
-  return __hip_atomic_fetch_add(h.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void last_ticket(const ReduceHdr& h, bool lane, uint32_t tk) {
-  if (lane && h.fault_clear && tk == (uint32_t)h.n_blocks - 1u) {
-    *h.fault_clear = 0u;
-    *h.ticket = 0u;
-  }
+// LD: how the partials are read.  0: plain loads (written by an earlier
+// launch).  1: agent-scope relaxed atomic loads (sc1: past this CU's L1) and
+// 2: system-scope ones, for partials published inside the same launch by
+// write-through stores of other workgroups (MI355X_MICROARCH.md
+// §inter-workgroup visibility).
+template <int LD>
+__device__ __forceinline__ float ld_part(const float* p) {
+  if (LD == 1) return __uint_as_float(__hip_atomic_load((const gu32r*)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (LD == 2) return __uint_as_float(__hip_atomic_load((const gu32r*)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+  return *p;
 }
 
 // One block = RP consecutive elements (from elem_block * RP) of parameter r,
@@ -166,28 +96,38 @@ __device__ __forceinline__ void last_ticket(const ReduceHdr& h, bool lane, uint3
 // also sums the loss and advances the step counter.  tstep: the Adam step
 // (counter[1] + 1) when h.step_counter is set.  Every load of the block is
 // issued in one straight-line group (clamped indices, zero weights past the
-// batch), the Adam state first, so one wait covers them.
+// batch), so one wait covers the partials and the Adam state.  The caller
+// synchronises the workgroup between two calls that share `part`.
+// WTP: the updated parameters are stored write-through (agent scope), for a
+// launch whose other workgroups read them after a grid-wide hand-off (the
+// reduce-at-start GINet step, ginet_fused.hip).
+// row_off: the partials of graph b sit at row row_off + b (slab: (row_off + b)
+// * slab_rows): the half of the pipelined step's double buffer.
+template <int LD, bool LEAN = false, bool WTP = false>
 __device__ __forceinline__ void reduce_block(const ReduceHdr& h, const ParamRec& r, int elem_block, bool first, int t,
-                                             float (*part)[RP], int64_t tstep) {
+                                             float (*part)[RP], int64_t tstep, int64_t row_off = 0) {
+  // LEAN: partials always given, Adam always on (the one-launch step): the
+  // gradients-supplied path is compiled out (less code to fetch cold)
   const int lp = t % RP, ch = t / RP;
   const int e = elem_block * RP + lp;
   const bool live = e < r.numel;
   // a graph pass whose in-launch hand-off gave up (dr_pass.fault): its
   // partials are wrong, so the step reports NaN and changes no state
-  const uint32_t fv = h.fault ? *h.fault : 0u;
+  const uint32_t fv = (!LEAN && h.fault) ? *h.fault : 0u;
   const bool bad = fv != 0u;
-  const int ec = live ? e : 0;
-  const ElemState s = load_state(h, r, ec, ch == 0);
-  float gin = 0.f, div = 1.f;
-  if (ch == 0 && !h.slab && r.grad) {
-    gin = r.grad[ec];
-    if (h.grad_div) div = *h.grad_div;
+  if (first && t < 64 && h.lpg && h.loss_out) {
+    float acc = 0.f;  // lane-strided partial sums, then a fixed-order wave reduction
+    for (int b = t; b < h.B; b += 64) acc += ld_part<LD>(h.lpg + row_off + b);
+    acc = dr_wave_sum(acc);
+    if (t == 0) h.loss_out[0] = bad ? __builtin_nanf("") : acc * h.loss_scale;
+  } else if (bad && first && t == 0 && h.loss_out) {
+    h.loss_out[0] = __builtin_nanf("");
   }
-  reduce_loss(h, first, t, bad);
+  const int ec = live ? e : 0;
   const bool slab_kind = r.kind == DR_GRAD_SLAB, outer = r.kind == DR_GRAD_OUTER;
   const bool has_src = h.slab && (slab_kind || outer || r.kind == DR_GRAD_HEAD);
   const int64_t st = slab_kind ? h.slab_stride : h.head_stride;
-  const float* base = slab_kind ? h.slab : h.head;
+  const float* base = (slab_kind ? h.slab : h.head) + row_off * (slab_kind ? h.slab_rows : 1) * st;
   const int col1 = outer ? r.off1 + ec / r.cols : r.off1 + ec;
   const int col2 = outer ? r.off2 + ec % r.cols : 0;
   const int nb = slab_kind ? h.B * h.slab_rows : h.B;  // rows of this gradient's partials
@@ -197,9 +137,23 @@ __device__ __forceinline__ void reduce_block(const ReduceHdr& h, const ParamRec&
 #pragma unroll
     for (int k = 0; k < RU; ++k) {
       const int64_t row = min(b0 + k, b1 - 1);
-      u[k] = base[row * st + col1];
-      w[k] = outer ? base[row * st + col2] : 1.f;
+      u[k] = ld_part<LD>(base + row * st + col1);
+      w[k] = outer ? ld_part<LD>(base + row * st + col2) : 1.f;
     }
+  }
+  const bool upd = live && ch == 0 && (LEAN || h.adam_enabled) && !bad;
+  float p0 = 0.f, m0 = 0.f, v0 = 0.f, gin = 0.f;
+  int4 mi = make_int4(-1, -1, -1, -1);  // dr_adam.mirror slots of this element, loaded with the state
+  if (ch == 0 && (LEAN || h.adam_enabled) && r.numel > 0) {  // numel 0: an empty record (no pointers)
+    p0 = r.param[ec];
+    m0 = r.m[ec];
+    v0 = r.v[ec];
+    if (!LEAN && h.mirror) mi = h.mirror_idx[r.mbase + ec];
+  }
+  float div = 1.f;
+  if (!LEAN && ch == 0 && !h.slab && r.grad) {
+    gin = r.grad[ec];
+    if (h.grad_div) div = *h.grad_div;
   }
   if (h.slab) {
     float acc = 0.f;
@@ -214,8 +168,8 @@ __device__ __forceinline__ void reduce_block(const ReduceHdr& h, const ParamRec&
 #pragma unroll
         for (int k = 0; k < RU2; ++k) {
           const int64_t row = min(bb + k, b1 - 1);
-          u2[k] = base[row * st + col1];
-          w2[k] = outer ? base[row * st + col2] : 1.f;
+          u2[k] = ld_part<LD>(base + row * st + col1);
+          w2[k] = outer ? ld_part<LD>(base + row * st + col2) : 1.f;
         }
 #pragma unroll
         for (int k = 0; k < RU2; ++k)
@@ -228,9 +182,17 @@ __device__ __forceinline__ void reduce_block(const ReduceHdr& h, const ParamRec&
   __syncthreads();
   RDSTAMP(2);
   if (ch != 0 || !live) return;
-  const uint32_t tk = take_ticket(h, lp == 0, fv);
+  // dr_adam.fault_clear: lane 0 of each block takes a ticket once its read of
+  // the flag has returned; the last block's lane 0 clears the flag (every
+  // block has read it by then) for the next graph pass
+  const bool tick = !LEAN && h.fault_clear && lp == 0;
+  uint32_t tk = 0u;
+  if (tick) {
+    asm volatile("" ::"v"(fv) : "memory");
+    tk = __hip_atomic_fetch_add(h.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   float gsum;
-  if (h.slab) {
+  if (LEAN || h.slab) {
     gsum = 0.f;
 #pragma unroll
     for (int k = 0; k < RC; ++k) gsum += part[k][lp];
@@ -245,8 +207,37 @@ __device__ __forceinline__ void reduce_block(const ReduceHdr& h, const ParamRec&
     }
     if (bad) r.grad[e] = __builtin_nanf("");
   }
-  adam_element(h, r, e, gsum, s, h.adam_enabled && !bad, first && lp == 0, tstep);
-  last_ticket(h, lp == 0, tk);
+  if (upd) {
+    float bc1 = h.bias_c1, bc2s = h.bias_c2_sqrt;
+    if (h.step_counter) {  // step and bias corrections from the device counter
+      bc1 = 1.f - exp2f((float)tstep * h.log2_beta1);
+      bc2s = sqrtf(1.f - exp2f((float)tstep * h.log2_beta2));
+      if (!LEAN && first && lp == 0) h.step_counter[0] = tstep;  // LEAN: the caller advances it
+    }
+    float gr = gsum;
+    if (h.weight_decay != 0.f) gr = fmaf(h.weight_decay, p0, gr);
+    // torch.optim.Adam: exp_avg.lerp_(g, 1-b1); exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
+    // every product-sum spelled out (fmaf / __fmul_rn / __fadd_rn): contraction
+    // is then the same in every kernel that inlines this block
+    const float mv = fmaf(1.f - h.beta1, __fsub_rn(gr, m0), m0);
+    const float vv = fmaf(__fmul_rn(1.f - h.beta2, gr), gr, __fmul_rn(v0, h.beta2));
+    r.m[e] = mv;
+    r.v[e] = vv;
+    const float denom = __fadd_rn(__fdiv_rn(sqrtf(vv), bc2s), h.eps);
+    const float pn = fmaf(-(h.lr / bc1), __fdiv_rn(mv, denom), p0);
+    if (WTP) __hip_atomic_store((__attribute__((address_space(1))) unsigned int*)(r.param + e), __float_as_uint(pn), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else r.param[e] = pn;
+    if (!LEAN && h.mirror) {
+      if (mi.x >= 0) h.mirror[mi.x] = pn;
+      if (mi.y >= 0) h.mirror[mi.y] = pn;
+      if (mi.z >= 0) h.mirror[mi.z] = pn;
+      if (mi.w >= 0) h.mirror[mi.w] = pn;
+    }
+  }
+  if (tick && tk == (uint32_t)h.n_blocks - 1u) {
+    *h.fault_clear = 0u;
+    *h.ticket = 0u;
+  }
   RDSTAMP(3);
 #ifdef DR_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -254,93 +245,11 @@ __device__ __forceinline__ void reduce_block(const ReduceHdr& h, const ParamRec&
   RDSTAMP(4);
 }
 
-// One outer-product block: RP consecutive elements from e0 of a
-// DR_GRAD_OUTER parameter (grad[i][j] = sum_b head[b][off1 + i] head[b][off2 + j]),
-// RC batch chunks per element as in reduce_block.  The block first stages the
-// head slices its elements read — U = head[:, off1 + rows of the block]
-// ([rows][B]) and W = head[:, off2 + columns of the block] ([B][cols]),
-// 16-byte loads where aligned — in LDS (sm) with a few loads per thread,
-// instead of every thread loading 2 x B/RC scattered partials: the same
-// products, sums and order as reduce_block, so the same bits.  Needs partials
-// (h.slab set) and B * (columns + rows) <= OUTER_LDS_FLOATS - RC * RP.
-__device__ __forceinline__ void reduce_outer_block(const ReduceHdr& h, const ParamRec& r, int e0, bool first, int t,
-                                                   float* sm, int64_t tstep) {
-  const int lp = t % RP, ch = t / RP;
-  const int cols = r.cols, e = e0 + lp;
-  const int elast = min(e0 + RP, r.numel) - 1;
-  const bool live = e < r.numel;
-  const uint32_t fv = h.fault ? *h.fault : 0u;
-  const bool bad = fv != 0u;
-  const ElemState s = load_state(h, r, live ? e : e0, ch == 0 && live);
-  reduce_loss(h, first, t, bad);
-  const int ir0 = e0 / cols, ir1 = elast / cols;  // the block's rows
-  const int jlo = ir0 == ir1 ? e0 - ir0 * cols : 0, jn = ir0 == ir1 ? elast - e0 + 1 : cols;  // its columns
-  const int nr = ir1 - ir0 + 1, nb = h.B;
-  const int64_t st = h.head_stride;
-  float* part = sm;                  // [RC][RP]
-  float* sU = sm + RC * RP;          // [nr][nb]
-  float* sW = sU + nr * nb;          // [nb][jn]
-  const float* wsrc = h.head + r.off2 + jlo;
-  if (((r.off2 + jlo) & 3) == 0 && (jn & 3) == 0 && (st & 3) == 0) {
-    const int q = jn >> 2;
-    for (int p = t; p < nb * q; p += RT) {
-      const int b = p / q, c4 = p - b * q;
-      *reinterpret_cast<float4*>(sW + b * jn + 4 * c4) = *reinterpret_cast<const float4*>(wsrc + b * st + 4 * c4);
-    }
-  } else {
-    for (int p = t; p < nb * jn; p += RT) {
-      const int b = p / jn, jj = p - b * jn;
-      sW[p] = wsrc[b * st + jj];
-    }
-  }
-  for (int p = t; p < nr * nb; p += RT) {
-    const int ii = p / nb, b = p - ii * nb;
-    sU[p] = h.head[b * st + r.off1 + ir0 + ii];
-  }
-  __syncthreads();
-  {
-    const int ec = live ? e : e0;
-    const int ii = ec / cols - ir0, jj = ec % cols - jlo;
-    const int b0 = (nb * ch) / RC, b1 = (nb * (ch + 1)) / RC;
-    float acc = 0.f;
-    for (int b = b0; b < b1; ++b) acc = fmaf(sU[ii * nb + b], sW[b * jn + jj], acc);
-    part[ch * RP + lp] = acc;
-  }
-  RDSTAMP(1);
-  __syncthreads();
-  RDSTAMP(2);
-  if (ch != 0 || !live) return;
-  const uint32_t tk = take_ticket(h, lp == 0, fv);
-  float gsum = 0.f;
-#pragma unroll
-  for (int k = 0; k < RC; ++k) gsum += part[k * RP + lp];
-  if (bad) gsum = __builtin_nanf("");
-  if (r.grad) r.grad[e] = gsum;
-  adam_element(h, r, e, gsum, s, h.adam_enabled && !bad, first && lp == 0, tstep);
-  last_ticket(h, lp == 0, tk);
-  RDSTAMP(3);
-#ifdef DR_STAMPS
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-  RDSTAMP(4);
-}
-
-// Host: whether parameter i of the table reduces in outer-product blocks
-inline bool outer_blocks(const dr_param_table* t, int i, const float* slab, int32_t n_batch) {
-  const dr_grad_recipe r = t->recipe[i];
-  if (r.kind != DR_GRAD_OUTER || !slab || r.cols <= 0) return false;
-  // the widest block: RP columns of one row, or every column of RP / cols + 2 rows
-  const int64_t cols = r.cols >= RP ? RP : r.cols, rows = r.cols >= RP ? 2 : RP / r.cols + 2;
-  return (int64_t)n_batch * (cols + rows) <= OUTER_LDS_FLOATS - RC * RP;
-}
-
-// Host: header + records from the C-ABI table and Adam settings; the block
-// list goes to blk_param / blk_elem (each block's parameter, BLK_OUTER for an
-// outer-product block, and its first element); returns the number of blocks,
-// or a negative DR_E_* code.
+// Host: header + records from the C-ABI table and Adam settings; returns the
+// number of RP-element blocks, or a negative DR_E_* code.
 inline int build_reduce(const dr_param_table* t, const float* slab, const float* head, int32_t n_batch,
                         const dr_adam* adam, const float* loss_per_graph, float loss_scale, float* loss_out,
-                        ReduceHdr& h, ParamRec* rec, uint8_t* blk_param, uint16_t* blk_elem, int max_blocks) {
+                        ReduceHdr& h, ParamRec* rec) {
   if (!t || !adam || n_batch < 0) return DR_E_ARG;
   if ((slab == nullptr) != (head == nullptr)) return DR_E_ARG;
   if (t->n_params < 1 || t->n_params > DR_MAX_PARAMS) return DR_E_ARG;
@@ -375,7 +284,7 @@ inline int build_reduce(const dr_param_table* t, const float* slab, const float*
   h.ticket = adam->ticket;
   int blocks = 0, mbase = 0;
   for (int i = 0; i < t->n_params; ++i) {
-    if (t->numel[i] < 0 || t->numel[i] > 65535 || !t->param[i]) return t->numel[i] > 65535 ? DR_E_UNSUPPORTED : DR_E_ARG;
+    if (t->numel[i] < 0 || !t->param[i]) return DR_E_ARG;
     if (adam->enabled && (!t->exp_avg[i] || !t->exp_avg_sq[i])) return DR_E_ARG;
     if (!slab && !t->grad[i]) return DR_E_ARG;
     const dr_grad_recipe r = t->recipe[i];
@@ -394,13 +303,9 @@ inline int build_reduce(const dr_param_table* t, const float* slab, const float*
     pr.mbase = mbase;
     mbase += t->numel[i];
     h.blk0[i] = (int16_t)blocks;
-    const bool ob = outer_blocks(t, i, slab, n_batch);
-    for (int e0 = 0; e0 < t->numel[i]; e0 += RP, ++blocks) {
-      if (blocks >= max_blocks) return DR_E_UNSUPPORTED;
-      blk_param[blocks] = (uint8_t)(i | (ob ? BLK_OUTER : 0));
-      blk_elem[blocks] = (uint16_t)e0;
-    }
+    blocks += (t->numel[i] + RP - 1) / RP;
   }
+  if (blocks > 32767) return DR_E_UNSUPPORTED;
   for (int i = t->n_params; i <= DR_MAX_PARAMS; ++i) h.blk0[i] = (int16_t)blocks;
   h.n_params = t->n_params;
   h.n_blocks = blocks;

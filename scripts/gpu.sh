@@ -23,6 +23,8 @@
 #   sweep       the GINet batch sweep (per-graph vs accumulating pass)
 #   trainer     bench.py --trainer --validate (captured epochs / eval, load rate)
 #   ddp1        the same on a one-rank RCCL group (Trainer(ngpu=2) code path)
+#   ab:<v>,<w>  the headline bench per A/B library (tools/build_variant.sh), ABBA
+#   timeline    one GINet step's cross-kernel timeline (stamps build, tools/step_timeline.py)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 R=$(pwd); O=$R/gpurun_out/${1:?out-subdir}; shift; mkdir -p $O
 export TMPDIR=/tmp
@@ -103,6 +105,17 @@ for S in "$@"; do
     ddp1)
       DR_BENCH_PG=1 timeout -k 10 500 python bench.py --trainer --validate --batches 64 > $O/bench_trainer_b64_validate_ddp1.json 2> $O/bench_trainer_ddp1.err || { tail $O/bench_trainer_ddp1.err; fail ddp1; }
       cut -c1-600 $O/bench_trainer_b64_validate_ddp1.json ;;
+    ab:*)  # ab:<variant>,<variant>,... : the headline bench per library (DR_LIB_NAME; "main" = the shipped one), twice in ABBA order
+      IFS=, read -ra V <<< "${S#ab:}"; order=("${V[@]}"); for ((k=${#V[@]}-1; k>=0; k--)); do order+=("${V[k]}"); done
+      : > $O/ab.txt
+      for v in "${order[@]}"; do
+        lib=libdeeprank2_amd.so; [ "$v" = main ] || lib=libdeeprank2_amd_$v.so
+        DR_LIB_NAME=$lib timeout -k 10 300 python bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-stream-copy > $O/ab_$v.json 2> $O/ab_$v.err || { tail -5 $O/ab_$v.err; fail "ab $v"; }
+        echo "$v | $(js $O/ab_$v.json)" | tee -a $O/ab.txt
+      done ;;
+    timeline)
+      DR_LIB_NAME=libdeeprank2_amd_stamps.so timeout -k 10 200 python tools/step_timeline.py 64 20 > $O/timeline.txt 2>&1 || fail timeline
+      grep -v amdgpu.ids $O/timeline.txt ;;
     *) fail "unknown section $S" ;;
   esac
 done
