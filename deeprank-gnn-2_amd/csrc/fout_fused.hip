@@ -33,6 +33,10 @@
 
 #include "graph_common.h"
 
+#ifndef DR_TILE_STORE_WAIT
+#define DR_TILE_STORE_WAIT 0  // 1: the tile kernel waits for its Zm stores before the MFMA phase (r05 form, A/B)
+#endif
+
 namespace {
 
 using namespace drk;
@@ -798,7 +802,8 @@ __global__ void __launch_bounds__(NTA) fout_large_conv1_kernel(FoutLargeArgs la)
   } else {  // per-edge gather of X rows from HBM / L2
     gather_rows(s.col + ec0, SG ? s.ea + ec0 : nullptr, X, s.rowptr + n0 + g + r0, 0);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // (no wait for the Zm stores: the MFMA reads LDS; the tail reads Zm next launch)
+  if (DR_TILE_STORE_WAIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   // conv1 on MFMA: H1 = relu([c1 x | Zm] [Wc; Wn] + b) -- fout_graph_kernel's operand order
   {

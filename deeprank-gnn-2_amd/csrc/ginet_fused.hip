@@ -47,6 +47,9 @@ namespace {
 #ifndef DR_CONV2_KEYS
 #define DR_CONV2_KEYS 0  // 1: conv2 reads the pooled rows from the depth-0 keys, no barrier after their decode (measured 0.1 us slower, r05)
 #endif
+#ifndef DR_TILE_STORE_WAIT
+#define DR_TILE_STORE_WAIT 0  // 1: the tile kernels wait for their Z stores before the MFMA phase (r05 form, A/B)
+#endif
 #ifndef DR_DMA_ROT
 #define DR_DMA_ROT 0  // 1: spread starting waves (measured 0.1 us slower per pass, r05)
 #endif
@@ -1487,7 +1490,10 @@ __device__ __forceinline__ void conv_tile_f32(const LargeArgs& la, float* lds) {
     }
   }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // (no s_waitcnt vmcnt(0) here: the MFMA phase reads Z from LDS, and the Z
+  // stores to global memory need not land before it -- the tail reads them in
+  // the next launch.  DR_TILE_STORE_WAIT = 1 restores the wait, A/B)
+  if (DR_TILE_STORE_WAIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   // H = relu(Z [W1; W1e]^T), one 16-row MFMA tile per wave
   {
@@ -1707,7 +1713,7 @@ __device__ __forceinline__ void conv_tile_bf16(const LargeArgs& la, float* lds) 
       }
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (DR_TILE_STORE_WAIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (as in conv_tile_f32)
   __syncthreads();
   // H = relu(Z [W1; W1e]^T): lane l holds Z[row l&15][k 8(l>>4)..+7] and
   // W[col l&15][same k] (16-byte LDS reads); C row (l>>4)*4+r, col l&15.

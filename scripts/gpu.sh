@@ -24,6 +24,7 @@
 #   trainer     bench.py --trainer --validate (captured epochs / eval, load rate)
 #   ddp1        the same on a one-rank RCCL group (Trainer(ngpu=2) code path)
 #   ab:<v>,<w>  the headline bench per A/B library (tools/build_variant.sh), ABBA
+#               (AB_ARGS: other bench.py arguments, e.g. "--model ginet --graphs atom"; AB_STEPS)
 #   timeline    one GINet step's cross-kernel timeline (stamps build, tools/step_timeline.py)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 R=$(pwd); O=$R/gpurun_out/${1:?out-subdir}; shift; mkdir -p $O
@@ -110,7 +111,7 @@ for S in "$@"; do
       : > $O/ab.txt
       for v in "${order[@]}"; do
         lib=libdeeprank2_amd.so; [ "$v" = main ] || lib=libdeeprank2_amd_$v.so
-        DR_LIB_NAME=$lib timeout -k 10 300 python bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-stream-copy > $O/ab_$v.json 2> $O/ab_$v.err || { tail -5 $O/ab_$v.err; fail "ab $v"; }
+        DR_LIB_NAME=$lib timeout -k 10 300 python bench.py --steps ${AB_STEPS:-200} --warmup 20 --no-cpu-baseline --no-stream-copy $AB_ARGS > $O/ab_$v.json 2> $O/ab_$v.err || { tail -5 $O/ab_$v.err; fail "ab $v"; }
         echo "$v | $(js $O/ab_$v.json)" | tee -a $O/ab.txt
       done ;;
     timeline)
