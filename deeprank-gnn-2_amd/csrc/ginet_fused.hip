@@ -1044,14 +1044,18 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const AccCtx&
     // (at most one per slot), and the slot holding the next part adds it after
     // a barrier, slot by slot (fixed order: deterministic).  Rows inside one
     // slot sum exactly as the row gather did; split rows sum as (first part +
-    // part 2) + part 3.  Scratch: the head (slot start rows) and the tail's dG
-    // partials (continuations), both unused before the tail.  Then each wave
-    // runs the MFMA and the pooling of its tiles on the complete Z.
-    const bool bal = DR_GATHER_BAL && !ACC && nch <= 8;
+    // part 2) + part 3.  Scratch:
+    // the head region (slot start rows, unused before the tail) and X's space
+    // (the continuations, after the gather).  Then each wave runs the MFMA
+    // and the pooling of its tiles on the complete Z.
+    // (the continuations go to X's space once every gather is done: graphs
+    // with N * XS >= 32 S words, e.g. every residue graph; smaller ones keep
+    // the tile gather)
+    const bool bal = DR_GATHER_BAL && !ACC && nch <= 8 && N * XS >= 32 * (NT / 8);
     if (bal) {
       constexpr int S = NT / 8;
       int* sfirst = reinterpret_cast<int*>(lds + c.head);
-      float* scont = lds + c.dgp;
+      float* scont = sX;
       for (int i = tid; i < N; i += NT) {  // the slots whose first edge lies in row i (an empty row: Z = 0)
         const int a0 = srp[i], a1 = srp[i + 1];
         if (a1 > a0) {
@@ -1066,6 +1070,8 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const AccCtx&
       const int sl = tid >> 3, cc = tid & 7;
       const int eb = (E * sl) / S, ee = (E * (sl + 1)) / S;
       int spill = -1;  // this slot's last row, when it began here and runs on past the slot
+      bool has_cont = false;  // this slot began inside a row: its part of that row
+      float4 contv = make_float4(0.f, 0.f, 0.f, 0.f);
       if (eb < ee && cc < nch) {
         int i = sfirst[sl];
         int e = eb;
@@ -1078,7 +1084,8 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const AccCtx&
             zr[1] = make_float2(z.z, z.w);
             if (r1i > ee) spill = i;
           } else {  // a continuation of a row begun in an earlier slot
-            *reinterpret_cast<float4*>(scont + sl * 32 + cc * 4) = z;
+            contv = z;
+            has_cont = true;
           }
           e = stop;
           if (e >= ee) break;
@@ -1087,6 +1094,8 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const AccCtx&
           } while (srp[i + 1] == e);  // (rows without edges: zeroed above)
         }
       }
+      __syncthreads();  // every gather done: X is dead
+      if (has_cont) *reinterpret_cast<float4*>(scont + sl * 32 + cc * 4) = contv;
       __syncthreads();
       // a row split over slots: its first part's slot adds the later slots'
       // parts in slot order (every non-empty slot starting inside the row)
