@@ -41,14 +41,14 @@
 
 namespace {
 
+#ifndef DR_GATHER_IMM
+#define DR_GATHER_IMM 1  // the row gather's index reads as one base + immediate offsets (0: compiler-formed addresses)
+#endif
 #ifndef DR_GATHER_ROW2
 #define DR_GATHER_ROW2 1  // GINet gather: one row, two chunks per lane (0: two rows, one chunk)
 #endif
 #ifndef DR_CONV2_KEYS
 #define DR_CONV2_KEYS 0  // 1: conv2 reads the pooled rows from the depth-0 keys, no barrier after their decode (measured 0.1 us slower, r05)
-#endif
-#ifndef DR_GATHER_BAL
-#define DR_GATHER_BAL 1  // the per-graph kernel's edge-balanced gather (0: one 16-row tile per wave, r05)
 #endif
 #ifndef DR_TILE_STORE_WAIT
 #define DR_TILE_STORE_WAIT 0  // 1: the tile kernels wait for their Z stores before the MFMA phase (r05 form, A/B)
@@ -1032,96 +1032,19 @@ __device__ __forceinline__ uint64_t graph_body(const GinetArgs& a, const AccCtx&
       }
       if (tid == 0) *ac.staged = (ac.next >= 0 && busy < NW) ? 1u : 0u;
     }
-    // Edge-balanced gather (r06, the per-graph kernel, F <= 32): Z = A X by
-    // all 16 waves over equal slices of the graph's CSR edges instead of one
-    // 16-row tile per wave, whose time was set by its highest-degree row (the
-    // tiles' max / mean degree 1.28, and the heaviest tile 1.46x the mean
-    // tile: waves idled on the slowest lane and then at the barrier).  Slot s
-    // (8 lanes, one 16-byte chunk each) sums edges [E s / S, E (s+1) / S) row
-    // segment by row segment (gather_row_chunk: each segment in CSR order from
-    // zero).  A row's segment that starts in its slot is the row's first part
-    // and goes to Z; a row begun in an earlier slot leaves its part in cont[s]
-    // (at most one per slot), and the slot holding the next part adds it after
-    // a barrier, slot by slot (fixed order: deterministic).  Rows inside one
-    // slot sum exactly as the row gather did; split rows sum as (first part +
-    // part 2) + part 3.  Scratch:
-    // the head region (slot start rows, unused before the tail) and X's space
-    // (the continuations, after the gather).  Then each wave runs the MFMA
-    // and the pooling of its tiles on the complete Z.
-    // (the continuations go to X's space once every gather is done: graphs
-    // with N * XS >= 32 S words, e.g. every residue graph; smaller ones keep
-    // the tile gather)
-    const bool bal = DR_GATHER_BAL && !ACC && nch <= 8 && N * XS >= 32 * (NT / 8);
-    if (bal) {
-      constexpr int S = NT / 8;
-      int* sfirst = reinterpret_cast<int*>(lds + c.head);
-      float* scont = sX;
-      for (int i = tid; i < N; i += NT) {  // the slots whose first edge lies in row i (an empty row: Z = 0)
-        const int a0 = srp[i], a1 = srp[i + 1];
-        if (a1 > a0) {
-          const int s1 = min((a1 * S + E - 1) / E, S);
-          for (int q = (a0 * S + E - 1) / E; q < s1; ++q) sfirst[q] = i;
-        } else {
-          float2* zr = reinterpret_cast<float2*>(sZ + i * LDW);
-          for (int q = 0; q < XS / 2; ++q) zr[q] = make_float2(0.f, 0.f);
-        }
-      }
-      __syncthreads();
-      const int sl = tid >> 3, cc = tid & 7;
-      const int eb = (E * sl) / S, ee = (E * (sl + 1)) / S;
-      int spill = -1;  // this slot's last row, when it began here and runs on past the slot
-      bool has_cont = false;  // this slot began inside a row: its part of that row
-      float4 contv = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (eb < ee && cc < nch) {
-        int i = sfirst[sl];
-        int e = eb;
-        while (true) {
-          const int r0i = srp[i], r1i = srp[i + 1], stop = min(r1i, ee);
-          const float4 z = drk::gather_row_chunk(scol, e, stop, sX, XS, cc * 4);
-          if (r0i >= eb) {  // the row's first part
-            float2* zr = reinterpret_cast<float2*>(sZ + i * LDW + cc * 4);
-            zr[0] = make_float2(z.x, z.y);
-            zr[1] = make_float2(z.z, z.w);
-            if (r1i > ee) spill = i;
-          } else {  // a continuation of a row begun in an earlier slot
-            contv = z;
-            has_cont = true;
-          }
-          e = stop;
-          if (e >= ee) break;
-          do {
-            ++i;
-          } while (srp[i + 1] == e);  // (rows without edges: zeroed above)
-        }
-      }
-      __syncthreads();  // every gather done: X is dead
-      if (has_cont) *reinterpret_cast<float4*>(scont + sl * 32 + cc * 4) = contv;
-      __syncthreads();
-      // a row split over slots: its first part's slot adds the later slots'
-      // parts in slot order (every non-empty slot starting inside the row)
-      if (spill >= 0) {
-        float2* zr = reinterpret_cast<float2*>(sZ + spill * LDW + cc * 4);
-        float4 z = make_float4(zr[0].x, zr[0].y, zr[1].x, zr[1].y);
-        const int rend = srp[spill + 1];
-        for (int q = sl + 1; q < S && (E * q) / S < rend; ++q)
-          if ((E * q) / S < (E * (q + 1)) / S) z = f4add(z, *reinterpret_cast<const float4*>(scont + q * 32 + cc * 4));
-        zr[0] = make_float2(z.x, z.y);
-        zr[1] = make_float2(z.z, z.w);
-      }
-      __syncthreads();
-      if (wave == 0) STAMP(20);  // (the balanced gather done)
-    }
     for (int tt = wave; tt * 16 < N; tt += NW) {
       const int r0 = tt * 16;
-      if (bal) {
-      } else
 #if DR_GATHER_ROW2
       if (nch <= 8) {  // one row per lane (r0 + lane/4), chunks q and q ^ 4 (q = lane%4, or +4 on odd rows)
         const int i = r0 + (lane >> 2);
         const int ca = (lane & 3) | ((lane & 4)), cb = ca ^ 4;
         const int eb = i < N ? srp[i] : 0, ee = i < N ? srp[i + 1] : 0;
         float4 za, zb;
+#if DR_GATHER_IMM
+        drk::gather_row_two_chunks_imm(scol, eb, ee, reinterpret_cast<const char*>(sX + ca * 4), (cb - ca) * 16, XS * 4, za, zb);
+#else
         drk::gather_row_two_chunks(scol, eb, ee, sX, XS, ca * 4, cb * 4, za, zb);
+#endif
         if (i < N) {
           // (rows LDW = KP + 2 words apart: 8-byte aligned, two 64-bit stores per chunk)
           if (ca < nch) {

@@ -115,6 +115,50 @@ __device__ __forceinline__ void gather_row_two_chunks(const uint16_t* col, int e
   outb = b;
 }
 
+// gather_row_two_chunks with fewer VALU instructions per edge, for the
+// per-graph kernels, whose gathers run 16 waves on 4 SIMDs and are VALU-issue
+// bound (a wave64 VALU op holds its SIMD 4 cycles): the four index reads of
+// a step are one base address and immediate offsets (inline asm, waited for
+// inside the same statement -- the compiler does not track them), and each
+// edge's two 16-byte reads are one v_mad_u32_u24 (row base) and a lane
+// constant byte delta.  xa: LDS byte pointer of this lane's first chunk in
+// row 0; db: the second chunk's byte distance from the first; rb: bytes per X
+// row.  Same sums, same edge order as gather_row_chunk.
+__device__ __forceinline__ void gather_row_two_chunks_imm(const uint16_t* col, int eb, int ee, const char* xa, int db,
+                                                          int rb, float4& outa, float4& outb) {
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+  int e = eb;
+  for (; e + 4 <= ee; e += 4) {
+    const uint32_t ad = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) uint16_t*)(col + e));
+    int j0, j1, j2, j3;
+    asm volatile(
+        "ds_read_u16 %0, %4\n\t"
+        "ds_read_u16 %1, %4 offset:2\n\t"
+        "ds_read_u16 %2, %4 offset:4\n\t"
+        "ds_read_u16 %3, %4 offset:6\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(j0), "=&v"(j1), "=&v"(j2), "=&v"(j3)
+        : "v"(ad));
+    const char* p0 = xa + __umul24(j0, rb);
+    const char* p1 = xa + __umul24(j1, rb);
+    const char* p2 = xa + __umul24(j2, rb);
+    const char* p3 = xa + __umul24(j3, rb);
+    const float4 v0 = *reinterpret_cast<const float4*>(p0), w0 = *reinterpret_cast<const float4*>(p0 + db);
+    const float4 v1 = *reinterpret_cast<const float4*>(p1), w1 = *reinterpret_cast<const float4*>(p1 + db);
+    const float4 v2 = *reinterpret_cast<const float4*>(p2), w2 = *reinterpret_cast<const float4*>(p2 + db);
+    const float4 v3 = *reinterpret_cast<const float4*>(p3), w3 = *reinterpret_cast<const float4*>(p3 + db);
+    a = f4add(f4add(f4add(f4add(a, v0), v1), v2), v3);
+    b = f4add(f4add(f4add(f4add(b, w0), w1), w2), w3);
+  }
+  for (; e < ee; ++e) {
+    const char* p = xa + __umul24((int)col[e], rb);
+    a = f4add(a, *reinterpret_cast<const float4*>(p));
+    b = f4add(b, *reinterpret_cast<const float4*>(p + db));
+  }
+  outa = a;
+  outb = b;
+}
+
 // Two CSR rows' sums of X chunks at once (one lane, two rows): each row in
 // its own edge order (same sums as gather_row_chunk), four edges of each row
 // per step, so eight index reads and then eight row reads are in flight.
