@@ -535,7 +535,8 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
       for (int ch = sub; ch < nch; ch += 8) {
         const int c4 = ch * 4;
         float sw;
-        const float4 acc = SG ? gather_row_chunk_w(scol, sEa, eb, ee, sX, XS, c4, sw) : gather_row_chunk(scol, eb, ee, sX, XS, c4);
+        const float4 acc = SG ? gather_row_chunk_w(scol, sEa, eb, ee, sX, XS, c4, sw)
+                              : gather_row_chunk_lds(scol, eb, ee, sX, XS, c4);
         if (SG && ch == 0) sC1[i] = sw / deg;
         // Rows are 8-byte aligned (LDZ even): two 64-bit stores per chunk; the
         // pad columns F..XS-1 they also fill are never read.

@@ -41,9 +41,6 @@
 
 namespace {
 
-#ifndef DR_GATHER_IMM
-#define DR_GATHER_IMM 1  // the row gather's index reads as one base + immediate offsets (0: compiler-formed addresses)
-#endif
 #ifndef DR_GATHER_ROW2
 #define DR_GATHER_ROW2 1  // GINet gather: one row, two chunks per lane (0: two rows, one chunk)
 #endif
@@ -1454,7 +1451,7 @@ __device__ __forceinline__ void conv_tile_f32(const LargeArgs& la, float* lds) {
       const int eb = strp[r] - ebase, ee = strp[r + 1] - ebase;
       for (int ch = sub; ch < nch; ch += 8) {
         const int c4 = ch * 4;
-        const float4 acc = drk::gather_row_chunk(slcol, eb, ee, sXh, XS, c4);
+        const float4 acc = drk::gather_row_chunk(slcol, eb, ee, sXh, XS, c4);  // (the _imm form measured +0.4 us here)
         float* zr = sZ + r * LDW + c4;
         zr[0] = acc.x;
         zr[1] = acc.y;

@@ -88,7 +88,7 @@ __device__ __forceinline__ void gather_rows(const int* rp, const uint16_t* col, 
     const int eb = rp[i], ee = rp[i + 1];
     for (int ch = sub; ch < nch; ch += 8) {
       const int c4 = ch * 4;
-      const float4 acc = gather_row_chunk(col, eb, ee, Y, ys, c4);
+      const float4 acc = gather_row_chunk_lds(col, eb, ee, Y, ys, c4);
       float* o = out + i * ldo + c4;
       o[0] = acc.x;
       o[1] = acc.y;
@@ -378,7 +378,7 @@ __global__ void __launch_bounds__(NT) ginet_nocluster_kernel(NcArgs a) {
     for (int jn = tid >> 3; jn < N; jn += NT / 8) {
       const int eb = strp[jn], ee = strp[jn + 1];
       const int c4 = sub * 4;
-      const float4 acc = gather_row_chunk(stcol, eb, ee, sZ2, LZ, c4);
+      const float4 acc = gather_row_chunk_lds(stcol, eb, ee, sZ2, LZ, c4);
       float* h = sH1 + jn * 32 + c4;
       h[0] = relu_bwd(h[0], acc.x);
       h[1] = relu_bwd(h[1], acc.y);
@@ -539,7 +539,7 @@ __global__ void __launch_bounds__(TB) nc_l_conv1(NcLargeArgs a) {
       const int eb = q.rp[q.i0 + r] - e0, ee = q.rp[q.i0 + r + 1] - e0;
       for (int ch = sub; ch < nch; ch += 8) {
         const int c4 = ch * 4;
-        const float4 acc = gather_row_chunk(sLc, eb, ee, sXh, XS, c4);
+        const float4 acc = gather_row_chunk_lds(sLc, eb, ee, sXh, XS, c4);
         float* zr = sZ + r * LDW + c4;
         zr[0] = acc.x;
         zr[1] = acc.y;
@@ -604,7 +604,7 @@ __global__ void __launch_bounds__(TB) nc_l_conv2(NcLargeArgs a) {
     for (int r = tid >> 3; r < q.nrows; r += TB / 8) {
       const int eb = q.rp[q.i0 + r] - e0, ee = q.rp[q.i0 + r + 1] - e0;
       const int c4 = sub * 4;
-      const float4 acc = gather_row_chunk(sLc, eb, ee, sHh, 32, c4);
+      const float4 acc = gather_row_chunk_lds(sLc, eb, ee, sHh, 32, c4);
       float* zr = sZ2 + r * LZ + c4;
       zr[0] = acc.x;
       zr[1] = acc.y;
@@ -803,7 +803,7 @@ __global__ void __launch_bounds__(TB) nc_l_bwd1(NcLargeArgs a) {
     const int sub = tid & 7, c4 = sub * 4;
     for (int r = tid >> 3; r < q.nrows; r += TB / 8) {
       const int eb = q.trp[q.i0 + r] - q0, ee = q.trp[q.i0 + r + 1] - q0;
-      const float4 acc = gather_row_chunk(sLt, eb, ee, sDh, 32, c4);
+      const float4 acc = gather_row_chunk_lds(sLt, eb, ee, sDh, 32, c4);
       float* h = sS1 + r * LZ + c4;
       h[0] = relu_bwd(h[0], acc.x);
       h[1] = relu_bwd(h[1], acc.y);

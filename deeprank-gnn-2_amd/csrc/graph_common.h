@@ -6,6 +6,10 @@
 #include "../../include/deeprank2_amd.h"
 #include "dr_common.h"
 
+#ifndef DR_GATHER_IMM
+#define DR_GATHER_IMM 1  // per-graph gathers: index reads as one base + immediate offsets (0: compiler-formed addresses)
+#endif
+
 namespace drk {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
@@ -115,6 +119,60 @@ __device__ __forceinline__ void gather_row_two_chunks(const uint16_t* col, int e
   outb = b;
 }
 
+// The four index reads of a gather step from an LDS column array: one base
+// address and immediate offsets, waited for inside the statement (the
+// compiler does not track inline-asm LDS reads).  col must point into LDS.
+__device__ __forceinline__ void lds_index4(const uint16_t* col, int& j0, int& j1, int& j2, int& j3) {
+  const uint32_t ad = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) uint16_t*)col);
+  asm volatile(
+      "ds_read_u16 %0, %4\n\t"
+      "ds_read_u16 %1, %4 offset:2\n\t"
+      "ds_read_u16 %2, %4 offset:4\n\t"
+      "ds_read_u16 %3, %4 offset:6\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(j0), "=&v"(j1), "=&v"(j2), "=&v"(j3)
+      : "v"(ad));
+}
+
+// gather_row_chunk for an LDS column array, with the index reads of
+// lds_index4 and each row read addressed by one v_mad_u32_u24 (xc: LDS byte
+// pointer of this lane's chunk in row 0; rb: bytes per X row).  Same sums,
+// same edge order.
+__device__ __forceinline__ float4 gather_row_chunk_imm(const uint16_t* col, int eb, int ee, const char* xc, int rb) {
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  int e = eb;
+  for (; e + 4 <= ee; e += 4) {
+    int j0, j1, j2, j3;
+    lds_index4(col + e, j0, j1, j2, j3);
+    const float4 v0 = *reinterpret_cast<const float4*>(xc + __umul24(j0, rb));
+    const float4 v1 = *reinterpret_cast<const float4*>(xc + __umul24(j1, rb));
+    const float4 v2 = *reinterpret_cast<const float4*>(xc + __umul24(j2, rb));
+    const float4 v3 = *reinterpret_cast<const float4*>(xc + __umul24(j3, rb));
+    acc = f4add(f4add(f4add(f4add(acc, v0), v1), v2), v3);
+  }
+  if (e < ee) {  // the last 1-3 edges: their index and row reads in flight together, adds predicated
+    const int l = ee - 1;
+    const int j0 = col[e], j1 = col[min(e + 1, l)], j2 = col[min(e + 2, l)];
+    const float4 v0 = *reinterpret_cast<const float4*>(xc + __umul24(j0, rb));
+    const float4 v1 = *reinterpret_cast<const float4*>(xc + __umul24(j1, rb));
+    const float4 v2 = *reinterpret_cast<const float4*>(xc + __umul24(j2, rb));
+    acc = f4add(acc, v0);
+    acc = e + 1 < ee ? f4add(acc, v1) : acc;
+    acc = e + 2 < ee ? f4add(acc, v2) : acc;
+  }
+  return acc;
+}
+
+// gather_row_chunk for LDS column arrays: the _imm form unless built with
+// DR_GATHER_IMM=0 (A/B)
+__device__ __forceinline__ float4 gather_row_chunk_lds(const uint16_t* col, int eb, int ee, const float* X, int XS, int c4) {
+#if DR_GATHER_IMM
+  return gather_row_chunk_imm(col, eb, ee, reinterpret_cast<const char*>(X + c4), XS * 4);
+#else
+  return gather_row_chunk(col, eb, ee, X, XS, c4);
+#endif
+}
+
 // gather_row_two_chunks with fewer VALU instructions per edge, for the
 // per-graph kernels, whose gathers run 16 waves on 4 SIMDs and are VALU-issue
 // bound (a wave64 VALU op holds its SIMD 4 cycles): the four index reads of
@@ -129,16 +187,8 @@ __device__ __forceinline__ void gather_row_two_chunks_imm(const uint16_t* col, i
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
   int e = eb;
   for (; e + 4 <= ee; e += 4) {
-    const uint32_t ad = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) uint16_t*)(col + e));
     int j0, j1, j2, j3;
-    asm volatile(
-        "ds_read_u16 %0, %4\n\t"
-        "ds_read_u16 %1, %4 offset:2\n\t"
-        "ds_read_u16 %2, %4 offset:4\n\t"
-        "ds_read_u16 %3, %4 offset:6\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(j0), "=&v"(j1), "=&v"(j2), "=&v"(j3)
-        : "v"(ad));
+    lds_index4(col + e, j0, j1, j2, j3);
     const char* p0 = xa + __umul24(j0, rb);
     const char* p1 = xa + __umul24(j1, rb);
     const char* p2 = xa + __umul24(j2, rb);
