@@ -155,6 +155,46 @@ __device__ __forceinline__ float4 gather_row_chunk_w(const uint16_t* col, const 
   return acc;
 }
 
+// gather_row_chunk_w for LDS col / w (the per-graph kernel): four edges per
+// step, their index reads as lds_index4 and their row reads in flight
+// together; the fmaf chain and the weight sum in edge order as above
+__device__ __forceinline__ float4 gather_row_chunk_w_lds(const uint16_t* col, const float* w, int eb, int ee,
+                                                         const float* X, int XS, int c4, float& sw) {
+#if DR_GATHER_IMM
+  const char* xc = reinterpret_cast<const char*>(X + c4);
+  const int rb = XS * 4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  float s = 0.f;
+  int e = eb;
+  for (; e + 4 <= ee; e += 4) {
+    int j[4];
+    lds_index4(col + e, j[0], j[1], j[2], j[3]);
+    float we[4];
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      we[u] = w[e + u];
+      v[u] = *reinterpret_cast<const float4*>(xc + __umul24(j[u], rb));
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      s += we[u];
+      acc = make_float4(fmaf(we[u], v[u].x, acc.x), fmaf(we[u], v[u].y, acc.y), fmaf(we[u], v[u].z, acc.z), fmaf(we[u], v[u].w, acc.w));
+    }
+  }
+  for (; e < ee; ++e) {
+    const float we = w[e];
+    s += we;
+    const float4 v = *reinterpret_cast<const float4*>(xc + __umul24((int)col[e], rb));
+    acc = make_float4(fmaf(we, v.x, acc.x), fmaf(we, v.y, acc.y), fmaf(we, v.z, acc.z), fmaf(we, v.w, acc.w));
+  }
+  sw = s;
+  return acc;
+#else
+  return gather_row_chunk_w(col, w, eb, ee, X, XS, c4, sw);
+#endif
+}
+
 // The per-graph tail shared by fout_graph_kernel and the large-graph tail
 // kernel: conv2 on the pooled graph, depth-1 max pool, mean, head, loss and
 // the whole backward down to the conv1 weight partials.  Needs the depth-0
@@ -535,7 +575,7 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
       for (int ch = sub; ch < nch; ch += 8) {
         const int c4 = ch * 4;
         float sw;
-        const float4 acc = SG ? gather_row_chunk_w(scol, sEa, eb, ee, sX, XS, c4, sw)
+        const float4 acc = SG ? gather_row_chunk_w_lds(scol, sEa, eb, ee, sX, XS, c4, sw)
                               : gather_row_chunk_lds(scol, eb, ee, sX, XS, c4);
         if (SG && ch == 0) sC1[i] = sw / deg;
         // Rows are 8-byte aligned (LDZ even): two 64-bit stores per chunk; the
