@@ -754,8 +754,16 @@ def main(args):  # noqa: PLR0915, PLR0912, C901
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    if os.environ.get("DR_BENCH_EVT"):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
     loss = run_steps(args.warmup, args.steps)
+    if os.environ.get("DR_BENCH_EVT"):
+        t_issue = time.perf_counter() - t0
+        e1.record()
     torch.cuda.synchronize()
+    if os.environ.get("DR_BENCH_EVT"):
+        print(f"[bench] timed region: wall {1e6 * (time.perf_counter() - t0):.1f} us, events {1e3 * e0.elapsed_time(e1):.1f} us, host issue {1e6 * t_issue:.1f} us", file=sys.stderr)
     if pg is not None:
         torch.distributed.barrier()
     torch.cuda.synchronize()
