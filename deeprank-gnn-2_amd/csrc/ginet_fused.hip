@@ -770,7 +770,7 @@ __device__ __forceinline__ void ginet_tail(const GinetArgs& a, const TailLds& t,
         else drk::st_part<WT>(slab + p, acc);
       }
     };
-    if (K0 > 8) dw1(std::integral_constant<int, 16>());
+    if (K0 > 8) dw1(std::integral_constant<int, 16>());  // (all of K0 <= 32 in flight at once: +0.6 us atom, not kept)
     else dw1(std::integral_constant<int, 8>());
   }
   STAMP(14);

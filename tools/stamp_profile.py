@@ -76,9 +76,6 @@ def main():
         if np.median(full[:, :, 22]) > 0:
             g = np.median(full[:, :, 20] - full[:, :, 1]), np.median(full[:, :, 21] - full[:, :, 20]), np.median(full[:, :, 22] - full[:, :, 21])
             print(f"  wave 0 tile 0: gather {g[0]:.0f}  MFMA {g[1]:.0f}  pool atomics {g[2]:.0f} cyc")
-        if np.median(full[:, :, 24]) > 0:  # the edge-balanced gather: slot setup, wave 0's slots, hand-over
-            g = np.median(full[:, :, 23] - full[:, :, 1]), np.median(full[:, :, 24] - full[:, :, 23]), np.median(full[:, :, 20] - full[:, :, 24])
-            print(f"  balanced gather: to slot setup {g[0]:.0f}  wave 0 slots {g[1]:.0f}  barriers + continuations {g[2]:.0f} cyc")
 
 
 PHASES_F = ["stage", "gather rowmean(X)", "gemm conv1", "pool0", "conv2 (pooled)", "pool1+mean", "head fwd", "loss", "head/pool1/conv2 bwd", "dW1"]
