@@ -1157,6 +1157,21 @@ inline int rows_grid(int64_t rows, int rows_per_block) {
 // pipeline; only dWc sums its rows' shares in another order (as the 16-row
 // tiles already did).
 constexpr int CT = 1024;      // threads of the chunk kernels
+#ifndef DR_VC_XCD
+#define DR_VC_XCD 1  // chunk kernels: consecutive tiles on one XCD (0: tile = blockIdx.x)
+#endif
+// The tile a chunk-kernel workgroup runs.  Workgroups are dispatched to the 8
+// XCDs round-robin (block b to XCD group b % 8), so with tile = blockIdx.x a
+// graph's consecutive tiles land on 8 different L2s and each fetches the
+// graph's halo rows itself.  The bijective remap gives XCD group x the
+// contiguous tiles [x*per + min(x, rem), ...) (cdna_hip_programming.md T1).
+__device__ __forceinline__ int vc_tile() {
+  const int b = blockIdx.x;
+  if (!DR_VC_XCD) return b;
+  const int n = gridDim.x, x = b & 7, q = b >> 3, per = n >> 3, rem = n & 7;
+  return x * per + min(x, rem) + q;
+}
+
 constexpr int CW = CT / 64;   // waves
 constexpr int CRG = CT / 32;  // row groups (32 lanes = the 32 channels of one row)
 
@@ -1455,7 +1470,8 @@ __global__ void __launch_bounds__(CT, 8) vc_fwd(VA a) {
   const int F = a.F, KE = a.KE, KN = a.KN, XS = a.XS;
   const int tid = threadIdx.x, c = tid & 31, hs = tid & 32, g = tid >> 5;
   CSTAMP(LAYER - 1, 0);
-  const dr_vanilla_tile m = a.ws.tile_meta[blockIdx.x];
+  const int tile = vc_tile();
+  const dr_vanilla_tile m = a.ws.tile_meta[tile];
   const int nr = m.nr, ne = m.ne, H = m.n_halo;
   const int64_t rt0 = m.rt0;
   const FwdCarve fc = fwd_carve(F, a.ws.halo_max, a.ws.tile_edges_max, FE);
@@ -1637,7 +1653,7 @@ __global__ void __launch_bounds__(CT, 8) vc_fwd(VA a) {
     if (tid < F) {
       float t = 0.f;
       for (int i = 0; i < nr; ++i) t += lds[fc.x2 + i * 33 + tid];
-      a.ws.part_mean[(int64_t)blockIdx.x * 32 + tid] = t;
+      a.ws.part_mean[(int64_t)tile * 32 + tid] = t;
     }
   }
   CSTAMP(LAYER - 1, 4);
@@ -1691,7 +1707,8 @@ __global__ void __launch_bounds__(NB2, 8) vc_nb2(VA a) {
   const int F = a.F, XS = a.XS, KN = a.KN;
   const int tid = threadIdx.x;
   CSTAMP(2, 0);
-  const dr_vanilla_tile m = a.ws.tile_meta[blockIdx.x];
+  const int tile = vc_tile();
+  const dr_vanilla_tile m = a.ws.tile_meta[tile];
   const int64_t rt0 = m.rt0;
   const int nr = m.nr;
   const int LU = XS + 4, NOPD = r16(F + 32);
@@ -1748,7 +1765,7 @@ __global__ void __launch_bounds__(NB2, 8) vc_nb2(VA a) {
       else if (n < F + 32) ws[a.L.ds + (rt0 + i) * 32 + n - F] = acc[q];
     }
   }
-  node_wgrad<NB2>(a, part_row(a, 2, blockIdx.x), sDU, LU, sX1, sS, 4 * nct);
+  node_wgrad<NB2>(a, part_row(a, 2, tile), sDU, LU, sX1, sS, 4 * nct);
   CSTAMP(2, 2);
 }
 
@@ -2032,7 +2049,7 @@ template <int FE>
 __global__ void __launch_bounds__(CT, 8) vc_eb2n1(VA a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int F = a.F, XS = a.XS, KE = a.KE, KN = a.KN;
-  const int t = blockIdx.x, tid = threadIdx.x;
+  const int t = vc_tile(), tid = threadIdx.x;
   CSTAMP(3, 0);
   const dr_vanilla_tile m = a.ws.tile_meta[t];
   const int64_t rt0 = m.rt0;
@@ -2129,7 +2146,7 @@ template <int FE>
 __global__ void __launch_bounds__(CT, 8) vc_eb1(VA a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int F = a.F, XS = a.XS;
-  const int t = blockIdx.x, tid = threadIdx.x;
+  const int t = vc_tile(), tid = threadIdx.x;
   CSTAMP(4, 0);
   const dr_vanilla_tile m = a.ws.tile_meta[t];
   const int nr = m.nr;
