@@ -750,7 +750,7 @@ __global__ void __launch_bounds__(NTA) fout_large_conv1_kernel(FoutLargeArgs la)
   const FoutArgs& a = la.f;
   const dr_large_plan& pl = la.plan;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tile = blockIdx.x;
+  const int tile = xcd_tile();
   const int b = pl.tile_slot[tile];
   const int t = tile - pl.tile_first[b];
   const dr_graph_desc d = a.descs[b];

@@ -1381,7 +1381,7 @@ __device__ __forceinline__ void conv_tile_f32(const LargeArgs& la, float* lds) {
   const GinetArgs& a = la.g;
   const dr_large_plan& pl = la.plan;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tile = blockIdx.x;
+  const int tile = drk::xcd_tile();
   const int b = pl.tile_slot[tile];
   const int t = tile - pl.tile_first[b];
   const dr_graph_desc d = a.descs[b];
@@ -1604,7 +1604,7 @@ __device__ __forceinline__ void conv_tile_bf16(const LargeArgs& la, float* lds) 
   const GinetArgs& a = la.g;
   const dr_large_plan& pl = la.plan;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tile = blockIdx.x;
+  const int tile = drk::xcd_tile();
   const int b = pl.tile_slot[tile];
   const int t = tile - pl.tile_first[b];
   const dr_graph_desc d = a.descs[b];

@@ -483,7 +483,7 @@ struct NcTile {
 };
 __device__ __forceinline__ NcTile nc_tile(const NcLargeArgs& a) {
   NcTile q;
-  q.t = blockIdx.x;
+  q.t = xcd_tile();
   q.r0 = a.pl.tile_row0[q.t];
   q.nrows = (int)(a.pl.tile_row0[q.t + 1] - q.r0);
   q.b = a.pl.row_slot[q.r0];

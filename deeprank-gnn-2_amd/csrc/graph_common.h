@@ -10,6 +10,10 @@
 #define DR_GATHER_IMM 1  // per-graph gathers: index reads as one base + immediate offsets (0: compiler-formed addresses)
 #endif
 
+#ifndef DR_TILE_XCD
+#define DR_TILE_XCD 1  // tile kernels: consecutive tiles on one XCD (0: tile = blockIdx.x)
+#endif
+
 namespace drk {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
@@ -49,6 +53,18 @@ __device__ __forceinline__ void dma_x4(void* lds_dst, const void* gsrc, int n4) 
   uint4* dst = reinterpret_cast<uint4*>(lds_dst);
   for (int base = wave * 64; base < n4; base += NT)
     if (base + lane < n4) __builtin_amdgcn_global_load_lds(DRK_AS1(src + base + lane), DRK_AS3(dst + base), 16, 0, 0);
+}
+
+// The tile a tile-kernel workgroup runs.  Workgroups are dispatched to the 8
+// XCDs round-robin (block b to XCD group b % 8), so with tile = blockIdx.x a
+// graph's consecutive tiles land on 8 different L2s and each fetches the
+// graph's halo rows itself.  The bijective remap gives XCD group x the
+// contiguous tiles [x*per + min(x, rem), ...) (cdna_hip_programming.md T1).
+__device__ __forceinline__ int xcd_tile() {
+  const int b = blockIdx.x;
+  if (!DR_TILE_XCD) return b;
+  const int n = gridDim.x, x = b & 7, q = b >> 3, per = n >> 3, rem = n & 7;
+  return x * per + min(x, rem) + q;
 }
 
 __device__ __forceinline__ float4 f4add(float4 a, float4 v) {

@@ -1157,20 +1157,7 @@ inline int rows_grid(int64_t rows, int rows_per_block) {
 // pipeline; only dWc sums its rows' shares in another order (as the 16-row
 // tiles already did).
 constexpr int CT = 1024;      // threads of the chunk kernels
-#ifndef DR_VC_XCD
-#define DR_VC_XCD 1  // chunk kernels: consecutive tiles on one XCD (0: tile = blockIdx.x)
-#endif
-// The tile a chunk-kernel workgroup runs.  Workgroups are dispatched to the 8
-// XCDs round-robin (block b to XCD group b % 8), so with tile = blockIdx.x a
-// graph's consecutive tiles land on 8 different L2s and each fetches the
-// graph's halo rows itself.  The bijective remap gives XCD group x the
-// contiguous tiles [x*per + min(x, rem), ...) (cdna_hip_programming.md T1).
-__device__ __forceinline__ int vc_tile() {
-  const int b = blockIdx.x;
-  if (!DR_VC_XCD) return b;
-  const int n = gridDim.x, x = b & 7, q = b >> 3, per = n >> 3, rem = n & 7;
-  return x * per + min(x, rem) + q;
-}
+__device__ __forceinline__ int vc_tile() { return xcd_tile(); }  // (graph_common.h)
 
 constexpr int CW = CT / 64;   // waves
 constexpr int CRG = CT / 32;  // row groups (32 lanes = the 32 channels of one row)
