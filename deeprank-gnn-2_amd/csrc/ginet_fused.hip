@@ -41,6 +41,9 @@
 
 namespace {
 
+#ifndef DR_Z_ARGS
+#define DR_Z_ARGS 1  // large-path fp32 tile kernel: Z rows stored only at the tile's pooling arg candidates (0: every row)
+#endif
 #ifndef DR_GATHER_ROW2
 #define DR_GATHER_ROW2 1  // GINet gather: one row, two chunks per lane (0: two rows, one chunk)
 #endif
@@ -1261,7 +1264,7 @@ struct LargeArgs {
 };
 
 struct ConvCarve {
-  int KP, LDW, XS, w1, z, h, m0i, m0p, rng, xh, hid, lcol, trp, total;
+  int KP, LDW, XS, w1, z, h, m0i, m0p, rng, flg, xh, hid, lcol, trp, total;
 };
 
 // HM / EM: halo rows and edges of the largest tile (0: no halo staging)
@@ -1285,6 +1288,8 @@ __host__ __device__ inline ConvCarve conv_carve(int N, int F, int K0, int HM, in
   o += r4(K0 + 1);
   c.rng = o;
   o += r4(2 * K0);
+  c.flg = o;  // per tile row: a depth-0 pooling arg candidate (its Z row is stored)
+  o += r4(TR);
   c.xh = o;  // halo X rows (XS stride, 16-byte rows), then H
   o += HM ? r4(drk::imax(HM * c.XS, TR * 32)) : 0;
   if (HM) c.h = c.xh;
@@ -1340,7 +1345,7 @@ __device__ __forceinline__ uint32_t load_sc1_u32(const void* p) {
 template <int NTT, bool INL>
 __device__ __forceinline__ void tile_partial_max(const dr_large_plan& pl, const float* sH, const int* sm0i,
                                                  const int* sm0p, int* srng, bool compact, int tile, int b, int K0,
-                                                 int N, int r0, int nrows) {
+                                                 int N, int r0, int nrows, int* sflag = nullptr) {
   const int tid = threadIdx.x;
   // each cluster's members inside this tile: a sub-run of its ascending list
   for (int k = tid; k < K0; k += NTT) {
@@ -1361,6 +1366,7 @@ __device__ __forceinline__ void tile_partial_max(const dr_large_plan& pl, const 
         arg = i;
       }
     }
+    if (sflag && arg < N) sflag[arg - r0] = 1;  // (benign race: every writer stores 1)
     if (pl.part_key) {  // order-free combine over the graph's tiles (see dr_large_plan.part_key)
       if (best > LOWEST)
         __hip_atomic_fetch_max((gu64*)(pl.part_key) + ((int64_t)b * pl.k0_max + k) * 32 + ch,
@@ -1418,6 +1424,12 @@ __device__ __forceinline__ void conv_tile_f32(const LargeArgs& la, float* lds) {
     const int r = p / (KP - XS);
     sZ[r * LDW + XS + (p - r * (KP - XS))] = 0.f;
   }
+  // Z rows go to global memory only at the tile's depth-0 pooling arg
+  // candidates (the tail reads Z at the final args, which are tile args)
+  constexpr bool ZARGS = DR_Z_ARGS && !INL;
+  int* sflag = reinterpret_cast<int*>(lds + c.flg);
+  if (ZARGS)
+    for (int p = tid; p < TRr; p += NTT) sflag[p] = 0;
   if (pl.halo_ids) {
     // Halo path: stage the tile's rowptr slice, its halo ids, then the halo X
     // rows and the tile's edges (as halo indices) into LDS; gather from LDS.
@@ -1457,7 +1469,7 @@ __device__ __forceinline__ void conv_tile_f32(const LargeArgs& la, float* lds) {
         zr[1] = acc.y;
         zr[2] = acc.z;
         zr[3] = acc.w;
-        store_z4<INL>(zg + (int64_t)(r0 + r) * XS + c4, acc);
+        if (!ZARGS) store_z4<INL>(zg + (int64_t)(r0 + r) * XS + c4, acc);
       }
     }
   } else {
@@ -1489,7 +1501,7 @@ __device__ __forceinline__ void conv_tile_f32(const LargeArgs& la, float* lds) {
         zr[1] = acc.y;
         zr[2] = acc.z;
         zr[3] = acc.w;
-        store_z4<INL>(zg + (int64_t)i * XS + c4, acc);
+        if (!ZARGS) store_z4<INL>(zg + (int64_t)i * XS + c4, acc);
       }
     }
   }
@@ -1531,7 +1543,20 @@ __device__ __forceinline__ void conv_tile_f32(const LargeArgs& la, float* lds) {
       }
     }
   }
-  tile_partial_max<NTT, INL>(pl, sH, sm0i, sm0p, srng, compact, tile, b, K0, N, r0, nrows);
+  tile_partial_max<NTT, INL>(pl, sH, sm0i, sm0p, srng, compact, tile, b, K0, N, r0, nrows, ZARGS ? sflag : nullptr);
+  if (ZARGS) {
+    __syncthreads();
+    float* zg = pl.z + (int64_t)pl.z_row0[b] * XS;
+    const int nch = XS >> 2;
+    for (int p = tid; p < nrows * nch; p += NTT) {
+      const int r = p / nch, c4 = (p - r * nch) * 4;
+      if (sflag[r]) {
+        const float2* zr = reinterpret_cast<const float2*>(sZ + r * LDW + c4);  // (rows 8-byte aligned)
+        const float2 lo = zr[0], hi = zr[1];
+        *reinterpret_cast<float4*>(zg + (int64_t)(r0 + r) * XS + c4) = make_float4(lo.x, lo.y, hi.x, hi.y);
+      }
+    }
+  }
 }
 
 __global__ void __launch_bounds__(NTA) ginet_large_conv1_kernel(LargeArgs la) {
@@ -1566,7 +1591,7 @@ __device__ __forceinline__ float4 unpack4bf(uint2 v) {
 }
 
 struct ConvCarveB {  // offsets in 4-byte words; bf16 row strides in bf16 elements
-  int KPB, ZSB, XSB, w1, z, h, m0i, m0p, rng, xh, hid, lcol, trp, total;
+  int KPB, ZSB, XSB, w1, z, h, m0i, m0p, rng, flg, xh, hid, lcol, trp, total;
 };
 
 __host__ __device__ inline ConvCarveB conv_carve_bf16(int N, int F, int K0, int HM, int EM) {
@@ -1587,6 +1612,8 @@ __host__ __device__ inline ConvCarveB conv_carve_bf16(int N, int F, int K0, int 
   o += r4(K0 + 1);
   c.rng = o;
   o += r4(2 * K0);
+  c.flg = o;  // per tile row: a depth-0 pooling arg candidate (as conv_carve)
+  o += r4(TR);
   c.xh = o;  // halo X rows, bf16, XSB stride
   o += HM ? r4(HM * c.XSB / 2) : 0;
   c.hid = o;
@@ -1643,6 +1670,10 @@ __device__ __forceinline__ void conv_tile_bf16(const LargeArgs& la, float* lds) 
     const int r = p / (KPB - XSB);
     sZ[r * ZSB + XSB + (p - r * (KPB - XSB))] = 0;
   }
+  constexpr bool ZARGS = DR_Z_ARGS && !INL;  // (as conv_tile_f32)
+  int* sflag = reinterpret_cast<int*>(lds + c.flg);
+  if (ZARGS)
+    for (int p = tid; p < TRr; p += NTT) sflag[p] = 0;
   // Z = A X for the tile's rows: 8 lanes per row, 4 bf16 (8 bytes) per lane
   // and edge, summed in fp32 in CSR order; rounded to bf16 once per row.
   const int nch = XSB >> 2, sub = tid & 7;
@@ -1689,7 +1720,7 @@ __device__ __forceinline__ void conv_tile_bf16(const LargeArgs& la, float* lds) 
         for (; e < ee; ++e) acc = f4add(acc, unpack4bf(*reinterpret_cast<const uint2*>(&sXh[__umul24((int)slcol[e], XSB) + c4])));
         const uint2 zb = pack4bf(acc.x, acc.y, acc.z, acc.w);
         *reinterpret_cast<uint2*>(&sZ[r * ZSB + c4]) = zb;
-        store_u64<INL>(zg + (int64_t)(r0 + r) * XSB + c4, (uint64_t)zb.x | ((uint64_t)zb.y << 32));
+        if (!ZARGS) store_u64<INL>(zg + (int64_t)(r0 + r) * XSB + c4, (uint64_t)zb.x | ((uint64_t)zb.y << 32));
       }
     }
   } else {
@@ -1713,7 +1744,7 @@ __device__ __forceinline__ void conv_tile_bf16(const LargeArgs& la, float* lds) 
         for (; e < ee; ++e) acc = f4add(acc, unpack4bf(*reinterpret_cast<const uint2*>(X + (int64_t)col[e] * XSB + c4)));
         const uint2 zb = pack4bf(acc.x, acc.y, acc.z, acc.w);
         *reinterpret_cast<uint2*>(&sZ[r * ZSB + c4]) = zb;
-        store_u64<INL>(zg + (int64_t)i * XSB + c4, (uint64_t)zb.x | ((uint64_t)zb.y << 32));
+        if (!ZARGS) store_u64<INL>(zg + (int64_t)i * XSB + c4, (uint64_t)zb.x | ((uint64_t)zb.y << 32));
       }
     }
   }
@@ -1744,7 +1775,15 @@ __device__ __forceinline__ void conv_tile_bf16(const LargeArgs& la, float* lds) 
       }
     }
   }
-  tile_partial_max<NTT, INL>(pl, sH, sm0i, sm0p, srng, compact, tile, b, K0, N, r0, nrows);
+  tile_partial_max<NTT, INL>(pl, sH, sm0i, sm0p, srng, compact, tile, b, K0, N, r0, nrows, ZARGS ? sflag : nullptr);
+  if (ZARGS) {
+    __syncthreads();
+    const int nch = XSB >> 2;
+    for (int p = tid; p < nrows * nch; p += NTT) {
+      const int r = p / nch, c4 = (p - r * nch) * 4;
+      if (sflag[r]) *reinterpret_cast<uint2*>(zg + (int64_t)(r0 + r) * XSB + c4) = *reinterpret_cast<const uint2*>(&sZ[r * ZSB + c4]);
+    }
+  }
 }
 
 __global__ void __launch_bounds__(NTA) ginet_large_conv1_bf16_kernel(LargeArgs la) {
@@ -2135,6 +2174,7 @@ extern "C" int dr_debug_carve_ginet_conv(const int32_t* q, char* buf, int32_t le
   DR_DESC(d, c, m0i);
   DR_DESC(d, c, m0p);
   DR_DESC(d, c, rng);
+  DR_DESC(d, c, flg);
   DR_DESC(d, c, xh);
   DR_DESC(d, c, hid);
   DR_DESC(d, c, lcol);
@@ -2155,6 +2195,7 @@ extern "C" int dr_debug_carve_ginet_conv_bf16(const int32_t* q, char* buf, int32
   DR_DESC(d, c, m0i);
   DR_DESC(d, c, m0p);
   DR_DESC(d, c, rng);
+  DR_DESC(d, c, flg);
   DR_DESC(d, c, xh);
   DR_DESC(d, c, hid);
   DR_DESC(d, c, lcol);

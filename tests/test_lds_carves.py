@@ -143,7 +143,8 @@ TR = 128  # DR_LARGE_TILE
 def test_ginet_large_conv_carves(N, F, K0, HM, EM):
     def ext(v):
         XS, LDW = r4(F), r16(F) + 2
-        e = {"w1": 32 * LDW, "z": TR * LDW, "m0i": TR if HM else N, "m0p": K0 + 1, "rng": 2 * K0, "hid": HM}
+        # flg: one word per tile row, the pooling-arg flags of conv_tile_f32 (r06)
+        e = {"w1": 32 * LDW, "z": TR * LDW, "m0i": TR if HM else N, "m0p": K0 + 1, "rng": 2 * K0, "flg": TR, "hid": HM}
         if HM:
             e |= {"xh": max(HM * XS, TR * 32), "trp": TR + 1, "lcol": (EM + 8) // 2}
         else:
@@ -156,7 +157,7 @@ def test_ginet_large_conv_carves(N, F, K0, HM, EM):
     def ext_b(v):
         KPB = (F + 31) & ~31
         ZSB, XSB = KPB + 8, (F + 7) & ~7
-        e = {"w1": 32 * ZSB // 2, "z": TR * ZSB // 2, "h": TR * 32, "m0i": TR if HM else N, "m0p": K0 + 1, "rng": 2 * K0, "hid": HM}
+        e = {"w1": 32 * ZSB // 2, "z": TR * ZSB // 2, "h": TR * 32, "m0i": TR if HM else N, "m0p": K0 + 1, "rng": 2 * K0, "flg": TR, "hid": HM}
         if HM:
             e |= {"xh": HM * XSB // 2, "trp": TR + 1, "lcol": (EM + 8) // 2}
         return e
