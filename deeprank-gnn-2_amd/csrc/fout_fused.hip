@@ -713,7 +713,7 @@ struct FoutLargeArgs {
 };
 
 struct FConvCarve {
-  int KP, LDA, XS, w, b1, a, h, c1, m0i, m0p, xh, hid, trp, ew, lcol, total;
+  int KP, LDA, XS, w, b1, a, h, c1, m0i, m0p, flg, xh, hid, trp, ew, lcol, total;
 };
 __host__ __device__ inline FConvCarve fconv_carve(int N, int F, int K0, int HM, int EM, bool sg) {
   FConvCarve c;
@@ -731,6 +731,7 @@ __host__ __device__ inline FConvCarve fconv_carve(int N, int F, int K0, int HM, 
   TAKE(c1, sg ? TRF : 0)
   TAKE(m0i, HM ? TRF : N)
   TAKE(m0p, K0 + 1)
+  TAKE(flg, TRF)  // per tile row: a depth-0 pooling arg candidate (its Zm row is stored)
   TAKE(xh, HM * c.XS)
   TAKE(hid, HM)
   TAKE(trp, HM ? TRF + 1 : 0)
@@ -769,6 +770,12 @@ __global__ void __launch_bounds__(NTA) fout_large_conv1_kernel(FoutLargeArgs la)
   float* sC1 = lds + c.c1;
   int* sm0i = reinterpret_cast<int*>(lds + c.m0i);
   int* sm0p = reinterpret_cast<int*>(lds + c.m0p);
+  // Zm (and SGAT's c1) go to global memory only at the tile's depth-0 pooling
+  // arg candidates: the tail reads them only at the final args, tile args
+  constexpr bool ZARGS = DR_Z_ARGS;
+  int* sflag = reinterpret_cast<int*>(lds + c.flg);
+  if (ZARGS)
+    for (int p = tid; p < TRr; p += NTA) sflag[p] = 0;
   const bool compact = pl.tile_members != nullptr;
   if (compact) {  // this tile's members by cluster (host-built), runs from tile_mptr
     dma_words<NTA>(sm0i, pl.tile_members + (int64_t)tile * TRr, nrows);
@@ -805,10 +812,10 @@ __global__ void __launch_bounds__(NTA) fout_large_conv1_kernel(FoutLargeArgs la)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           if (c4 + q < F) sA[r * LDA + F + c4 + q] = zv[q];
-        *reinterpret_cast<float4*>(zg + (int64_t)(r0 + r) * ZS + c4) = zm;
+        if (!ZARGS) *reinterpret_cast<float4*>(zg + (int64_t)(r0 + r) * ZS + c4) = zm;
         if (SG && ch == 0) {
           sC1[r] = sw / deg;
-          zg[(int64_t)(r0 + r) * ZS + XS] = sw / deg;
+          if (!ZARGS) zg[(int64_t)(r0 + r) * ZS + XS] = sw / deg;
         }
       }
     }
@@ -903,10 +910,24 @@ __global__ void __launch_bounds__(NTA) fout_large_conv1_kernel(FoutLargeArgs la)
         arg = i;
       }
     }
+    if (ZARGS && arg < N) sflag[arg - r0] = 1;  // (benign race: every writer stores 1)
     if (best > LOWEST)
       __hip_atomic_fetch_max((__attribute__((address_space(1))) unsigned long long*)(pl.part_key) + ((int64_t)b * pl.k0_max + k) * 32 + ch,
                              ((unsigned long long)__float_as_uint(best) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)arg),
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (ZARGS) {  // the flagged rows' Zm (from the A tile's columns F..2F-1) and c1
+    __syncthreads();
+    const int nch = XS >> 2;
+    for (int p = tid; p < nrows * nch; p += NTA) {
+      const int r = p / nch, c4 = (p - r * nch) * 4;
+      if (sflag[r]) {
+        const float* zr = sA + r * LDA + F + c4;
+        *reinterpret_cast<float4*>(zg + (int64_t)(r0 + r) * ZS + c4) =
+            make_float4(zr[0], c4 + 1 < F ? zr[1] : 0.f, c4 + 2 < F ? zr[2] : 0.f, c4 + 3 < F ? zr[3] : 0.f);
+        if (SG && c4 == 0) zg[(int64_t)(r0 + r) * ZS + XS] = sC1[r];
+      }
+    }
   }
 }
 
@@ -1223,6 +1244,7 @@ extern "C" int dr_debug_carve_fout_conv(const int32_t* q, char* buf, int32_t len
   DR_DESC(d, c, c1);
   DR_DESC(d, c, m0i);
   DR_DESC(d, c, m0p);
+  DR_DESC(d, c, flg);
   DR_DESC(d, c, xh);
   DR_DESC(d, c, hid);
   DR_DESC(d, c, trp);

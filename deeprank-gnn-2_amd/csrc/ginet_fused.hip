@@ -41,9 +41,6 @@
 
 namespace {
 
-#ifndef DR_Z_ARGS
-#define DR_Z_ARGS 1  // large-path fp32 tile kernel: Z rows stored only at the tile's pooling arg candidates (0: every row)
-#endif
 #ifndef DR_GATHER_ROW2
 #define DR_GATHER_ROW2 1  // GINet gather: one row, two chunks per lane (0: two rows, one chunk)
 #endif

@@ -10,6 +10,9 @@
 #define DR_GATHER_IMM 1  // per-graph gathers: index reads as one base + immediate offsets (0: compiler-formed addresses)
 #endif
 
+#ifndef DR_Z_ARGS
+#define DR_Z_ARGS 1  // large-graph tile kernels: Z rows stored only at the tile's depth-0 pooling arg candidates (0: every row)
+#endif
 #ifndef DR_TILE_XCD
 #define DR_TILE_XCD 1  // tile kernels: consecutive tiles on one XCD (0: tile = blockIdx.x)
 #endif

@@ -19,6 +19,7 @@
 #   lds         LDS bank-conflict counters of ginet_graph_kernel
 #   large       per-kernel HBM tables: GINet atom f32 / bf16 / mixed
 #   vanilla     per-kernel HBM tables: Vanilla chunk pipeline atom / mixed
+#   kernels:<w>,<w>  per-kernel HBM tables of any tools/pmc_run.py workloads (e.g. foutnet_atom)
 #   configs     every BASELINE config line (+ the model variants), with CPU baselines
 #   sweep       the GINet batch sweep (per-graph vs accumulating pass)
 #   trainer     bench.py --trainer --validate (captured epochs / eval, load rate)
@@ -86,6 +87,8 @@ for S in "$@"; do
       for W in ginet_atom ginet_atom_bf16 ginet_mixed; do per_kernel $W 20; done ;;
     vanilla)
       for W in vanilla_atom vanilla_mixed; do per_kernel $W 20; done ;;
+    kernels:*)  # kernels:<workload>,... : per-kernel HBM tables of any tools/pmc_run.py workloads
+      IFS=, read -ra WS <<< "${S#kernels:}"; for W in "${WS[@]}"; do per_kernel $W 20; done ;;
     configs)
       : > $O/bench_configs.jsonl
       for cfg in "--model foutnet --graphs residue" "--model ginet --graphs atom" "--model ginet --graphs atom --dtype bf16" "--model ginet --graphs mixed" "--model vanilla --graphs mixed" "--model vanilla --graphs atom" "--model vanilla --graphs residue" "--model sgat --graphs residue" "--model ginet_nocluster --graphs residue"; do

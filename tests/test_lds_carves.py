@@ -238,7 +238,7 @@ def test_fout_large_carves(N, F, K0, HM, EM, sg):
 
     def ext(v):
         KP = r16(2 * F)
-        e = {"w": KP * 16, "b1": 16, "a": TRF * (KP + 4), "h": TRF * 16, "c1": TRF if sg else 0, "m0i": TRF if HM else N, "m0p": K0 + 1, "xh": HM * r4(F), "hid": HM, "trp": TRF + 1 if HM else 0, "lcol": (EM + 8) // 2 if HM else 0}
+        e = {"w": KP * 16, "b1": 16, "a": TRF * (KP + 4), "h": TRF * 16, "c1": TRF if sg else 0, "m0i": TRF if HM else N, "m0p": K0 + 1, "flg": TRF, "xh": HM * r4(F), "hid": HM, "trp": TRF + 1 if HM else 0, "lcol": (EM + 8) // 2 if HM else 0}
         return e
 
     q = [N, F, K0, HM, EM, sg]
