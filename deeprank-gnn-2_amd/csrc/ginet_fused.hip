@@ -2159,6 +2159,12 @@ extern "C" int dr_debug_carve_ginet(const int32_t* q, char* buf, int32_t len) {
   return d.pos;
 }
 
+extern "C" int dr_debug_xcd_tile(int32_t n_blocks, int32_t* tiles) {
+  if (n_blocks < 0 || (n_blocks > 0 && !tiles)) return DR_E_ARG;
+  for (int b = 0; b < n_blocks; ++b) tiles[b] = drk::xcd_tile_of(b, n_blocks);
+  return DR_OK;
+}
+
 extern "C" int dr_debug_carve_ginet_conv(const int32_t* q, char* buf, int32_t len) {
   const ConvCarve c = conv_carve(q[0], q[1], q[2], q[3], q[4]);
   DrCarveDesc d{buf, len, 0};

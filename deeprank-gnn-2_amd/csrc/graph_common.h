@@ -63,12 +63,12 @@ __device__ __forceinline__ void dma_x4(void* lds_dst, const void* gsrc, int n4) 
 // graph's consecutive tiles land on 8 different L2s and each fetches the
 // graph's halo rows itself.  The bijective remap gives XCD group x the
 // contiguous tiles [x*per + min(x, rem), ...) (cdna_hip_programming.md T1).
-__device__ __forceinline__ int xcd_tile() {
-  const int b = blockIdx.x;
+__host__ __device__ inline int xcd_tile_of(int b, int n) {
   if (!DR_TILE_XCD) return b;
-  const int n = gridDim.x, x = b & 7, q = b >> 3, per = n >> 3, rem = n & 7;
-  return x * per + min(x, rem) + q;
+  const int x = b & 7, q = b >> 3, per = n >> 3, rem = n & 7;
+  return x * per + (x < rem ? x : rem) + q;
 }
+__device__ __forceinline__ int xcd_tile() { return xcd_tile_of(blockIdx.x, gridDim.x); }
 
 __device__ __forceinline__ float4 f4add(float4 a, float4 v) {
   return make_float4(a.x + v.x, a.y + v.y, a.z + v.z, a.w + v.w);

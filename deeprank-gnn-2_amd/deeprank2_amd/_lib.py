@@ -269,6 +269,7 @@ SIGNATURES = [
     ("dr_mcl_assign", ctypes.c_int, [VP, VP, VP, ctypes.c_int32, VP, VP]),
     ("dr_dropout_mask", ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int32, ctypes.c_float, VP]),
     *[(f"dr_debug_carve_{k}", ctypes.c_int, [VP, ctypes.c_char_p, ctypes.c_int32]) for k in ("ginet", "ginet_conv", "ginet_conv_bf16", "ginet_tail", "fout", "fout_conv", "fout_tail", "nocluster", "vanilla_graph", "vanilla_tile", "vanilla_chunk_fwd", "vanilla_chunk_bwd")],
+    ("dr_debug_xcd_tile", ctypes.c_int, [ctypes.c_int32, VP]),
     ("dr_version", ctypes.c_char_p, []),
     ("dr_device_arch", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32]),
 ]

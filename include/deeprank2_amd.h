@@ -790,6 +790,13 @@ int dr_debug_carve_vanilla_tile(const int32_t* q, char* buf, int32_t len);
 int dr_debug_carve_vanilla_chunk_fwd(const int32_t* q, char* buf, int32_t len);
 int dr_debug_carve_vanilla_chunk_bwd(const int32_t* q, char* buf, int32_t len);
 
+/* Debug: the tile each of n_blocks workgroups runs in the tile kernels
+ * (large-graph GINet / FoutNet / SGAT / ginet_nocluster tiles, the Vanilla
+ * chunk kernels): the XCD-contiguous order of graph_common.h xcd_tile_of.
+ * Host-only; tests/test_lds_carves.py checks it is a permutation giving each
+ * XCD group (block % 8) one contiguous range of tiles. */
+int dr_debug_xcd_tile(int32_t n_blocks, int32_t* tiles);
+
 #ifdef __cplusplus
 }
 #endif

@@ -318,3 +318,16 @@ def test_vanilla_tile_and_chunk_carves(H, EM, TM, Fe):
         assert vals["x0"] == vals["halo"]  # the late rows overlay the dead edge space
         if two:
             assert vals["w1"] + XS * 32 <= total
+
+
+# ---- tile order of the tile kernels (graph_common.h xcd_tile_of, r06) ----
+@pytest.mark.parametrize("n", [1, 7, 8, 9, 64, 255, 642, 1528, 3001])
+def test_xcd_tile_order_is_a_contiguous_permutation(n):
+    lib = _lib.load()
+    out = (ctypes.c_int32 * n)()
+    assert lib.dr_debug_xcd_tile(n, out) == 0
+    tiles = list(out)
+    assert sorted(tiles) == list(range(n))  # every tile run exactly once
+    for x in range(8):  # blocks b, b + 8, ... (one XCD under round-robin dispatch) take consecutive tiles
+        mine = tiles[x::8]
+        assert mine == list(range(mine[0], mine[0] + len(mine))) if mine else True
