@@ -33,6 +33,9 @@
 
 #include "graph_common.h"
 
+#ifndef DR_FOUT_FRONT
+#define DR_FOUT_FRONT 1  // FoutNet per-graph kernel: Zm, conv1 and depth-0 pooling fused per wave (0: three barrier phases)
+#endif
 #ifndef DR_TILE_STORE_WAIT
 #define DR_TILE_STORE_WAIT 0  // 1: the tile kernel waits for its Zm stores before the MFMA phase (r05 form, A/B)
 #endif
@@ -535,6 +538,22 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
     dma_words<NT>(sP1w, s.p1_ea + q0, P1);
     dma_words<NT>(sP1tid, s.p1t_pid + q0, P1);
   }
+  // The fused front (FoutNet, F <= 32, K0 <= 64): each wave gathers its 16-row
+  // tile's Zm, runs conv1 on it and pools it by 64-bit LDS atomic max keys
+  // (ginet_fused.hip's front half), so conv1's weights and the node clusters
+  // are staged here, the keys live in the reduction scratch and the H1 rows
+  // are never formed (the tail reads P1 / A1 and [x | Zm] at the args only).
+  const bool FRONT = !SG && DR_FOUT_FRONT && XS <= 32 && K0 * 32 <= 2 * NT;
+  int* scl0 = reinterpret_cast<int*>(sH1);
+  unsigned long long* skey = reinterpret_cast<unsigned long long*>(sRed);
+  if (FRONT) {
+    dma_words<NT>(scl0, s.cl0 + n0, N);
+    dma_words<NT>(sWc1, a.w.wc1, F * 16);  // [Wc; Wn] k-major, as the weight image below
+    dma_words<NT>(sWc1 + F * 16, a.w.wn1, F * 16);
+    dma_words<NT>(sB1, a.w.b1, 16);
+    for (int p = 2 * F * 16 + tid; p < KP * 16; p += NT) sWc1[p] = 0.f;  // K padding rows
+    for (int p = tid; p < K0 * 16; p += NT) skey[p] = 0ull;
+  }
   const int64_t counter0 = (a.p.step_counter && b == 0) ? a.p.step_counter[0] : 0;  // loaded late: no early wait
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (a.p.step_counter && b == 0 && tid == 0) a.p.step_counter[1] = counter0;
@@ -564,6 +583,91 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
     }
     wr[u] = v;
   }
+  if (FRONT) {
+    // ------ fused front: Zm rows, conv1, depth-0 pooling keys, per wave ------
+    // Zm = D^-1 A X (foutnet.py:55-58; 0/0 = NaN on empty rows): one row per
+    // four lanes, 16-byte chunks q and q ^ 4 (same sums and order as the
+    // 8-lanes-per-row gather); H1 = relu([X | Zm] [Wc; Wn] + b) on MFMA; the
+    // max per (cluster, channel) as (H bits << 32 | ~node): H >= +0 or NaN
+    // (never pooled), the first max in node order wins (scatter_max).
+    const int li = lane & 15, kq = lane >> 4, nch = XS >> 2;
+    const int ca = (lane & 3) | (lane & 4), cb = ca ^ 4;
+    for (int tt = wave; tt * 16 < N; tt += NW) {
+      const int r0 = tt * 16, i = r0 + (lane >> 2);
+      const int eb = i < N ? srp[i] : 0, ee = i < N ? srp[i + 1] : 0;
+      const float deg = (float)(ee - eb);
+      float4 za, zb;
+      gather_row_two_chunks_imm(scol, eb, ee, reinterpret_cast<const char*>(sX + ca * 4), (cb - ca) * 16, XS * 4, za, zb);
+      if (i < N) {
+        if (ca < nch) {
+          if (WIDE) {
+            const float4 xv = *reinterpret_cast<const float4*>(sX + i * XS + ca * 4);
+            float2* xr = reinterpret_cast<float2*>(sZm + i * LDZ + ca * 4);
+            xr[0] = make_float2(xv.x, xv.y);
+            xr[1] = make_float2(xv.z, xv.w);
+          }
+          float2* zr = reinterpret_cast<float2*>(sZm + i * LDZ + ZO + ca * 4);
+          zr[0] = make_float2(za.x / deg, za.y / deg);
+          zr[1] = make_float2(za.z / deg, za.w / deg);
+        }
+        if (cb < nch) {
+          if (WIDE) {
+            const float4 xv = *reinterpret_cast<const float4*>(sX + i * XS + cb * 4);
+            float2* xr = reinterpret_cast<float2*>(sZm + i * LDZ + cb * 4);
+            xr[0] = make_float2(xv.x, xv.y);
+            xr[1] = make_float2(xv.z, xv.w);
+          }
+          float2* zr = reinterpret_cast<float2*>(sZm + i * LDZ + ZO + cb * 4);
+          zr[0] = make_float2(zb.x / deg, zb.y / deg);
+          zr[1] = make_float2(zb.z / deg, zb.w / deg);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's Zm rows are in LDS before its MFMA reads them
+      const int ar = min(r0 + li, N - 1);
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < KP; k += 16) {  // (B from LDS: a register-resident B measured +1.2 us per pass)
+        float av[4], bv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int kk = k + 4 * u + kq;
+          av[u] = kk < F ? (WIDE ? sZm[ar * LDZ + kk] : sX[ar * XS + kk]) : (kk < 2 * F ? sZm[ar * LDZ + ZO + kk - F] : 0.f);
+          bv[u] = sWc1[kk * 16 + li];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
+      }
+      const float b1 = sB1[li];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = r0 + kq * 4 + r;
+        if (row < N) {
+          const float v = relu_keepnan(acc[r] + b1);
+          if (v == v)
+            __hip_atomic_fetch_max(skey + scl0[row] * 16 + li,
+                                   ((unsigned long long)__float_as_uint(v) << 32) | (0xffffffffull - (unsigned long long)(uint32_t)row),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < WREG; ++u) {  // the other weights ([Wc; Wn] and b1 were staged)
+      const int p = tid + u * NT;
+      if (p < nw1) continue;
+      if (p < nw1 + nw2) {
+        if (p - nw1 < 1056) sWc2[p - nw1] = wr[u];
+      } else if (p < nw1 + nw2 + nf1) sFc1[p - nw1 - nw2] = wr[u];
+      else if (p < ntot) sFc2[p - nw1 - nw2 - nf1] = wr[u];
+    }
+    __syncthreads();
+    DRK_STAMP(2);
+    DRK_STAMP(3);
+    for (int p = tid; p < K0 * 16; p += NT) {  // the keys decoded: P1 = H1[arg] exactly; empty: 0, arg N
+      const unsigned long long key = skey[p];
+      sP1[p] = key ? __uint_as_float((uint32_t)(key >> 32)) : 0.f;
+      sA1[p] = key ? (int)(0xffffffffu - (uint32_t)key) : N;
+    }
+    __syncthreads();
+  } else {
   // ---------------- Zm = D^-1 A X (foutnet.py:55-58; NaN on empty rows) ----
   // SGAT: Zw = D^-1 A_w X and c = D^-1 A_w 1 with D clamped to 1 (sgat.py:74-76)
   {
@@ -676,6 +780,7 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
     }
   }
   __syncthreads();
+  }
 
   FoutTail t;
   t.P1 = sP1; t.A1 = sA1; t.dP1 = sdP1; t.Zm2 = sZm2; t.S2 = sS2; t.H2 = sH2; t.D2 = sD2; t.Dz2 = sDz2;
