@@ -198,6 +198,46 @@ __device__ __forceinline__ float4 gather_row_chunk_w_lds(const uint16_t* col, co
 #endif
 }
 
+// gather_row_chunk_w_lds for two 16-byte chunks of a row at once (the fused
+// front's lane layout): one index and one weight read per edge feed both
+// chunks; each chunk's fmaf chain and the weight sum in edge order, as above
+__device__ __forceinline__ void gather_row_two_chunks_w_lds(const uint16_t* col, const float* w, int eb, int ee, const char* xa,
+                                                            int db, int rb, float4& outa, float4& outb, float& sw) {
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+  float s = 0.f;
+  int e = eb;
+  for (; e + 4 <= ee; e += 4) {
+    int j[4];
+    lds_index4(col + e, j[0], j[1], j[2], j[3]);
+    float we[4];
+    float4 v[4], x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      we[u] = w[e + u];
+      const char* pr = xa + __umul24(j[u], rb);
+      v[u] = *reinterpret_cast<const float4*>(pr);
+      x[u] = *reinterpret_cast<const float4*>(pr + db);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      s += we[u];
+      a = make_float4(fmaf(we[u], v[u].x, a.x), fmaf(we[u], v[u].y, a.y), fmaf(we[u], v[u].z, a.z), fmaf(we[u], v[u].w, a.w));
+      b = make_float4(fmaf(we[u], x[u].x, b.x), fmaf(we[u], x[u].y, b.y), fmaf(we[u], x[u].z, b.z), fmaf(we[u], x[u].w, b.w));
+    }
+  }
+  for (; e < ee; ++e) {
+    const float we = w[e];
+    s += we;
+    const char* pr = xa + __umul24((int)col[e], rb);
+    const float4 v = *reinterpret_cast<const float4*>(pr), x = *reinterpret_cast<const float4*>(pr + db);
+    a = make_float4(fmaf(we, v.x, a.x), fmaf(we, v.y, a.y), fmaf(we, v.z, a.z), fmaf(we, v.w, a.w));
+    b = make_float4(fmaf(we, x.x, b.x), fmaf(we, x.y, b.y), fmaf(we, x.z, b.z), fmaf(we, x.w, b.w));
+  }
+  outa = a;
+  outb = b;
+  sw = s;
+}
+
 // The per-graph tail shared by fout_graph_kernel and the large-graph tail
 // kernel: conv2 on the pooled graph, depth-1 max pool, mean, head, loss and
 // the whole backward down to the conv1 weight partials.  Needs the depth-0
@@ -543,7 +583,7 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
   // (ginet_fused.hip's front half), so conv1's weights and the node clusters
   // are staged here, the keys live in the reduction scratch and the H1 rows
   // are never formed (the tail reads P1 / A1 and [x | Zm] at the args only).
-  const bool FRONT = !SG && DR_FOUT_FRONT && XS <= 32 && K0 * 32 <= 2 * NT;
+  const bool FRONT = DR_FOUT_FRONT && XS <= 32 && K0 * 32 <= 2 * NT;
   int* scl0 = reinterpret_cast<int*>(sH1);
   unsigned long long* skey = reinterpret_cast<unsigned long long*>(sRed);
   if (FRONT) {
@@ -595,9 +635,15 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
     for (int tt = wave; tt * 16 < N; tt += NW) {
       const int r0 = tt * 16, i = r0 + (lane >> 2);
       const int eb = i < N ? srp[i] : 0, ee = i < N ? srp[i + 1] : 0;
-      const float deg = (float)(ee - eb);
+      const float deg = SG ? (float)imax(ee - eb, 1) : (float)(ee - eb);
       float4 za, zb;
-      gather_row_two_chunks_imm(scol, eb, ee, reinterpret_cast<const char*>(sX + ca * 4), (cb - ca) * 16, XS * 4, za, zb);
+      if (SG) {  // SGAT: Zw = D^-1 A_w X, c1 = D^-1 A_w 1 (D clamped to 1, sgat.py:74-76)
+        float sw;
+        gather_row_two_chunks_w_lds(scol, sEa, eb, ee, reinterpret_cast<const char*>(sX + ca * 4), (cb - ca) * 16, XS * 4, za, zb, sw);
+        if (i < N && (lane & 3) == 0) sC1[i] = sw / deg;
+      } else {
+        gather_row_two_chunks_imm(scol, eb, ee, reinterpret_cast<const char*>(sX + ca * 4), (cb - ca) * 16, XS * 4, za, zb);
+      }
       if (i < N) {
         if (ca < nch) {
           if (WIDE) {
@@ -624,13 +670,14 @@ __global__ void __launch_bounds__(NT) fout_graph_kernel(FoutArgs a) {
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's Zm rows are in LDS before its MFMA reads them
       const int ar = min(r0 + li, N - 1);
+      const float cx = SG ? sC1[ar] : 1.f;
       floatx4 acc = {0.f, 0.f, 0.f, 0.f};
       for (int k = 0; k < KP; k += 16) {  // (B from LDS: a register-resident B measured +1.2 us per pass)
         float av[4], bv[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int kk = k + 4 * u + kq;
-          av[u] = kk < F ? (WIDE ? sZm[ar * LDZ + kk] : sX[ar * XS + kk]) : (kk < 2 * F ? sZm[ar * LDZ + ZO + kk - F] : 0.f);
+          av[u] = kk < F ? cx * (WIDE ? sZm[ar * LDZ + kk] : sX[ar * XS + kk]) : (kk < 2 * F ? sZm[ar * LDZ + ZO + kk - F] : 0.f);
           bv[u] = sWc1[kk * 16 + li];
         }
 #pragma unroll
