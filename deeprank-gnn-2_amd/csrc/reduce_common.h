@@ -20,8 +20,14 @@
 
 namespace drr {
 
-constexpr int RP = 64;  // parameter elements per block
-constexpr int RC = 8;   // batch chunks per block
+#ifndef DR_RP
+#define DR_RP 64
+#endif
+#ifndef DR_RC
+#define DR_RC 8
+#endif
+constexpr int RP = DR_RP;  // parameter elements per block
+constexpr int RC = DR_RC;  // batch chunks per block
 constexpr int RU = 8;   // batch rows per chunk issued together (predicated)
 constexpr int RU2 = 24; // then the rest of a chunk, this many at a time
 constexpr int RT = RP * RC;  // threads per block
