@@ -36,6 +36,9 @@
 #ifndef DR_FOUT_FRONT
 #define DR_FOUT_FRONT 1  // FoutNet per-graph kernel: Zm, conv1 and depth-0 pooling fused per wave (0: three barrier phases)
 #endif
+#ifndef DR_FOUT_MSE_HEAD
+#define DR_FOUT_MSE_HEAD 1  // FoutNet tail: one MSE logit's logit / loss / dh on wave 0 without barriers (0: the general head)
+#endif
 #ifndef DR_TILE_STORE_WAIT
 #define DR_TILE_STORE_WAIT 0  // 1: the tile kernel waits for its Zm stores before the MFMA phase (r05 form, A/B)
 #endif
@@ -342,6 +345,25 @@ __device__ __forceinline__ void fout_tail(const dr_pass& p, const FoutTail t, in
     }
   }
   __syncthreads();
+  if (DR_FOUT_MSE_HEAD && OUT == 1 && p.loss_kind == DR_LOSS_MSE && (p.flags & DR_PASS_BACKWARD)) {
+    // one MSE logit (configs[2]): wave 0 forms the logit (the same wave sum),
+    // the loss gradient and dh for the 64 hidden units, with no workgroup
+    // barrier between them (as ginet_head.h's MSE path)
+    if (wave == 0) {
+      const float v = dr_wave_sum(t.Hh[lane] * t.Fc2[lane]);
+      const float logit = v + t.Fc2[64];
+      const float dlt = logit - y_g;
+      const float dout0 = 2.f * dlt * p.loss_scale;
+      if (lane == 0) {
+        if (p.flags & DR_PASS_FORWARD) p.out[b] = logit;
+        if (p.loss_per_graph) p.loss_per_graph[b] = dlt * dlt;
+        t.Dout[0] = dout0;
+      }
+      t.Dh[lane] = relu_bwd(t.Hh[lane], fmaf(t.Fc2[lane], dout0, 0.f));
+    }
+    FT_STAMP(7);
+    __syncthreads();
+  } else {
   for (int q = wave; q < OUT; q += NW) {
     float v = t.Hh[lane] * t.Fc2[q * 64 + lane];
     v = dr_wave_sum(v);
@@ -382,6 +404,7 @@ __device__ __forceinline__ void fout_tail(const dr_pass& p, const FoutTail t, in
     t.Dh[tid] = relu_bwd(t.Hh[tid], acc);
   }
   __syncthreads();
+  }
   {
     const int o = tid & 31, rc = tid >> 5;  // 32 chunks of 2 fc1 rows
     float acc = fmaf(t.Fc1[(rc * 2) * 32 + o], t.Dh[rc * 2], t.Fc1[(rc * 2 + 1) * 32 + o] * t.Dh[rc * 2 + 1]);
